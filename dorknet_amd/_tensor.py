@@ -1,0 +1,77 @@
+"""Device-tensor plumbing shared by the layers.
+
+Activations keep the reference's logical NCHW shape (layers/convolution.py:86 already
+returns an NCHW *view* of an NHWC buffer) and use channels_last strides, i.e. NHWC
+bytes in HBM, which is what every kernel in libdorknet_hip.so reads and writes.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from ._hip import lib, stream_handle
+
+F32 = torch.float32
+
+
+def device() -> torch.device:
+    return torch.device("cuda", torch.cuda.current_device())
+
+
+def as_device(x, dtype=F32) -> torch.Tensor:
+    """numpy / torch (any device) -> torch tensor on the current HIP device (the
+    cp.asarray of the reference's training loop, examples/...depsep.py:219-221)."""
+    if isinstance(x, torch.Tensor):
+        if x.device.type != "cuda" or x.dtype != dtype:
+            x = x.to(device=device(), dtype=dtype)
+        return x
+    return torch.as_tensor(np.asarray(x), dtype=dtype, device=device())
+
+
+def empty_nhwc(n: int, c: int, h: int, w: int) -> torch.Tensor:
+    return torch.empty((n, c, h, w), dtype=F32, device=device(), memory_format=torch.channels_last)
+
+
+def is_nhwc(x: torch.Tensor) -> bool:
+    return x.is_contiguous(memory_format=torch.channels_last)
+
+
+def to_nhwc(x, cpad: int = 1) -> torch.Tensor:
+    """Return a channels_last fp32 device tensor whose channel count is padded (with
+    zeros) up to a multiple of `cpad`.  No copy when `x` already qualifies."""
+    x = as_device(x)
+    if x.dim() != 4:
+        raise ValueError(f"expected a 4-D (N, C, H, W) tensor, got shape {tuple(x.shape)}")
+    n, c, h, w = x.shape
+    cp = -(-c // cpad) * cpad
+    if cp == c and is_nhwc(x):
+        return x
+    if cp == c and x.is_contiguous():
+        src = x
+    else:
+        src = x.contiguous()
+    out = empty_nhwc(n, cp, h, w)
+    lib.dk_nchw_to_nhwc_f32(src.data_ptr(), n, c, h, w, cp, out.data_ptr(), stream_handle())
+    return out
+
+
+def rows(x: torch.Tensor) -> torch.Tensor:
+    """A row-major 2-D fp32 device tensor (dense-layer activations)."""
+    x = as_device(x)
+    return x if x.is_contiguous() else x.contiguous()
+
+
+def ptr(t) -> int:
+    return 0 if t is None else t.data_ptr()
+
+
+def to_param(v) -> torch.Tensor:
+    """Reference parameters start as numpy arrays (layers/layer.py:18-34 moves them with
+    cp.asarray); here to_gpu() makes them fp32 device tensors."""
+    if isinstance(v, torch.Tensor):
+        return v.to(device=device(), dtype=F32).contiguous()
+    return torch.as_tensor(np.ascontiguousarray(v, dtype=np.float32), device=device())
+
+
+def scalar_zero() -> torch.Tensor:
+    return torch.zeros((), dtype=F32, device=device())

@@ -1,0 +1,51 @@
+// Shared helpers for the dorknet_amd HIP library (gfx950 / CDNA4 only).
+//
+// Conventions of every extern "C" entry point (see include/dorknet_hip.h):
+//   * all tensor pointers are device pointers owned by the caller;
+//   * activations are NHWC (channels innermost), fp32;
+//   * kernels never allocate: scratch comes from a caller-provided workspace
+//     whose size is reported by a matching *_workspace_bytes() query;
+//   * work is stream-ordered on the caller's stream (a hipStream_t passed as void*);
+//   * the return value is a hipError_t cast to int (0 == success).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#include "../../include/dorknet_hip.h"
+
+#define DK_API extern "C" __attribute__((visibility("default")))
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+namespace dk {
+
+static inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+static inline int launch_status() { return static_cast<int>(hipGetLastError()); }
+
+static inline int cdiv(int a, int b) { return (a + b - 1) / b; }
+static inline long long cdivll(long long a, long long b) { return (a + b - 1) / b; }
+
+__device__ __forceinline__ f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
+__device__ __forceinline__ void st4(float* p, f32x4 v) { *reinterpret_cast<f32x4*>(p) = v; }
+
+// Wave-level (64 lanes) sum.
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// Error codes returned for argument errors detected on the host side.  They
+// live above the hipError_t range used by the runtime so callers can tell
+// "bad call" from "device fault".
+enum : int { DK_ERR_ARGS = 10001, DK_ERR_WORKSPACE = 10002 };
+
+}  // namespace dk

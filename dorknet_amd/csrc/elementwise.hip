@@ -1,0 +1,308 @@
+// Elementwise / small-reduction kernels around the convolution hot path, gfx950.
+//   ReLU fwd/bwd ............ layers/activations.py:14-47 (mask kept as uint8, not fp32)
+//   residual add (+ReLU) ..... layers/residual_block.py:65-97
+//   global average pool ...... layers/pooling.py:23-36
+//   softmax + cross-entropy .. layers/losses.py:13-34 (no max shift, as the reference)
+//   SGD momentum (multi-tensor, one launch) ... optimisers/SGDMomentum.py:31-39
+//   l2 loss term ............. regularisers/l2.py:12-14
+//   bias gradients (column sums), NCHW -> NHWC(+channel pad) layout conversion
+#include "dk_common.h"
+
+namespace dk {
+
+__global__ void relu_fwd_kernel(const float* __restrict__ x, long long n, float* __restrict__ y,
+                                uint8_t* __restrict__ mask) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float v = x[i];
+  const bool pos = v > 0.f;
+  y[i] = pos ? v : 0.f;
+  if (mask) mask[i] = pos;
+}
+
+__global__ void relu_bwd_kernel(const float* __restrict__ dy, const uint8_t* __restrict__ mask, long long n,
+                                float* __restrict__ dx) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  dx[i] = mask[i] ? dy[i] : 0.f;
+}
+
+__global__ void mask_to_f32_kernel(const uint8_t* __restrict__ mask, long long n, float* __restrict__ out) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = mask[i] ? 1.f : 0.f;
+}
+
+// y = a + b, optionally ReLU'd with mask.
+__global__ void add_kernel(const float* __restrict__ a, const float* __restrict__ b, long long n, int relu,
+                           float* __restrict__ y, uint8_t* __restrict__ mask) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float v = a[i] + b[i];
+  if (relu) {
+    const bool pos = v > 0.f;
+    v = pos ? v : 0.f;
+    if (mask) mask[i] = pos;
+  }
+  y[i] = v;
+}
+
+// out[n][c] = mean_{hw} x[n][hw][c]
+__global__ void gap_fwd_kernel(const float* __restrict__ x, int N, int HW, int C, float* __restrict__ out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= N * C) return;
+  const int n = i / C, c = i - n * C;
+  const float* p = x + (size_t)n * HW * C + c;
+  float s = 0.f;
+  for (int k = 0; k < HW; ++k) s += p[(size_t)k * C];
+  out[i] = s / (float)HW;
+}
+
+// dx[n][hw][c] = (1/HW) * dy[n][c]
+__global__ void gap_bwd_kernel(const float* __restrict__ dy, int N, int HW, int C, float* __restrict__ dx) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long total = (long long)N * HW * C;
+  if (i >= total) return;
+  const int c = (int)(i % C);
+  const int n = (int)(i / ((long long)HW * C));
+  dx[i] = (1.0f / (float)HW) * dy[(size_t)n * C + c];
+}
+
+// p = e^x / sum e^x per row (no max subtraction, losses.py:15-16);
+// loss = mean_b -log(sum_j p[b][j] * y[b][j])  (losses.py:23-26).  One block.
+__global__ __launch_bounds__(256) void softmax_xent_fwd_kernel(const float* __restrict__ x,
+                                                               const float* __restrict__ y, int B, int K,
+                                                               float* __restrict__ p, float* __restrict__ loss) {
+  __shared__ double red[256];
+  double acc = 0.0;
+  for (int b = threadIdx.x; b < B; b += 256) {
+    const float* xr = x + (size_t)b * K;
+    float* pr = p + (size_t)b * K;
+    float s = 0.f;
+    for (int j = 0; j < K; ++j) {
+      const float e = expf(xr[j]);
+      pr[j] = e;
+      s += e;
+    }
+    const float inv = 1.0f / s;
+    float dot = 0.f;
+    for (int j = 0; j < K; ++j) {
+      const float v = inv * pr[j];
+      pr[j] = v;
+      if (y) dot += v * y[(size_t)b * K + j];
+    }
+    if (y) acc += (double)(-logf(dot));
+  }
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0 && loss) *loss = (float)((1.0 / (double)B) * red[0]);
+}
+
+// dx = (1/B) * (p - y)   (losses.py:29-34)
+__global__ void softmax_xent_bwd_kernel(const float* __restrict__ p, const float* __restrict__ y, int B, int K,
+                                        float* __restrict__ dx) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= B * K) return;
+  dx[i] = (1.0f / (float)B) * (p[i] - y[i]);
+}
+
+// Multi-tensor SGD momentum: for every listed tensor t and element i
+//   d = (-lr) * g + mom * v;  w += d;  v = d      (SGDMomentum.py:33-39, same op order)
+struct SgdEntry {
+  float* w;
+  const float* g;
+  float* v;
+  long long n;
+  long long block0;  // first block index owned by this tensor
+};
+
+__global__ __launch_bounds__(256) void sgd_momentum_multi_kernel(const SgdEntry* __restrict__ tab, int ntens,
+                                                                 float lr, float mom, float gscale) {
+  // find the tensor owning this block (ntens ~ 100: linear scan of a cached table)
+  int t = 0;
+  const long long b = blockIdx.x;
+  while (t + 1 < ntens && tab[t + 1].block0 <= b) ++t;
+  const SgdEntry e = tab[t];
+  const long long i = (b - e.block0) * 256 + threadIdx.x;
+  if (i >= e.n) return;
+  const float g = gscale == 1.0f ? e.g[i] : __fmul_rn(gscale, e.g[i]);
+  const float d = __fadd_rn(__fmul_rn(-lr, g), __fmul_rn(mom, e.v[i]));
+  e.w[i] = __fadd_rn(e.w[i], d);
+  e.v[i] = d;
+}
+
+// out[0] = 0.5 * strength * sum w^2 (one block, fp64 accumulate).  With accumulate != 0,
+// adds into out[0] instead of overwriting.
+__global__ __launch_bounds__(256) void l2_loss_kernel(const float* __restrict__ w, long long n, float strength,
+                                                      int accumulate, float* __restrict__ out) {
+  __shared__ double red[256];
+  double s = 0.0;
+  for (long long i = threadIdx.x; i < n; i += 256) {
+    const double v = w[i];
+    s += v * v;
+  }
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const float v = (float)(0.5 * (double)strength * red[0]);
+    out[0] = accumulate ? out[0] + v : v;
+  }
+}
+
+// Column sums of an [M][N] matrix, stage 1: ws[chunk][n] = sum of rows in the chunk.
+__global__ void colsum_partial_kernel(const float* __restrict__ in, int M, int N, int rpc, double* __restrict__ ws) {
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= N) return;
+  const int r0 = blockIdx.y * rpc, r1 = min(M, r0 + rpc);
+  double s = 0.0;
+  for (int r = r0; r < r1; ++r) s += (double)in[(size_t)r * N + n];
+  ws[(size_t)blockIdx.y * N + n] = s;
+}
+
+__global__ void colsum_final_kernel(const double* __restrict__ ws, int chunks, int N, float* __restrict__ out) {
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= N) return;
+  double s = 0.0;
+  for (int k = 0; k < chunks; ++k) s += ws[(size_t)k * N + n];
+  out[n] = (float)s;
+}
+
+// NCHW -> NHWC with channel padding to Cp (zeros).
+__global__ void nchw_to_nhwc_kernel(const float* __restrict__ x, int N, int C, int H, int W, int Cp,
+                                    float* __restrict__ y) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long total = (long long)N * H * W * Cp;
+  if (i >= total) return;
+  const int c = (int)(i % Cp);
+  long long t = i / Cp;
+  const int w = (int)(t % W);
+  t /= W;
+  const int h = (int)(t % H);
+  const int n = (int)(t / H);
+  y[i] = c < C ? x[(((size_t)n * C + c) * H + h) * W + w] : 0.f;
+}
+
+// NHWC with padded channels (Cp) -> NHWC with C channels (drop the pad).
+__global__ void nhwc_unpad_kernel(const float* __restrict__ x, long long P, int Cp, int C, float* __restrict__ y) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= P * C) return;
+  const long long p = i / C;
+  const int c = (int)(i - p * C);
+  y[i] = x[p * Cp + c];
+}
+
+__global__ void scale_kernel(const float* __restrict__ x, long long n, float s, float* __restrict__ y) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) y[i] = s * x[i];
+}
+
+static int colsum_chunks(int M) {
+  int chunks = cdiv(M, 2048);
+  if (chunks > 512) chunks = 512;
+  if (chunks < 1) chunks = 1;
+  return chunks;
+}
+
+static inline dim3 grid1(long long n) { return dim3((unsigned)cdivll(n, 256)); }
+
+}  // namespace dk
+
+using namespace dk;
+
+DK_API int dk_relu_fwd_f32(const float* x, long long n, float* y, uint8_t* mask, void* stream) {
+  hipLaunchKernelGGL(relu_fwd_kernel, grid1(n), dim3(256), 0, as_stream(stream), x, n, y, mask);
+  return launch_status();
+}
+
+DK_API int dk_relu_bwd_f32(const float* dy, const uint8_t* mask, long long n, float* dx, void* stream) {
+  hipLaunchKernelGGL(relu_bwd_kernel, grid1(n), dim3(256), 0, as_stream(stream), dy, mask, n, dx);
+  return launch_status();
+}
+
+DK_API int dk_mask_to_f32(const uint8_t* mask, long long n, float* out, void* stream) {
+  hipLaunchKernelGGL(mask_to_f32_kernel, grid1(n), dim3(256), 0, as_stream(stream), mask, n, out);
+  return launch_status();
+}
+
+DK_API int dk_add_f32(const float* a, const float* b, long long n, int relu, float* y, uint8_t* mask, void* stream) {
+  hipLaunchKernelGGL(add_kernel, grid1(n), dim3(256), 0, as_stream(stream), a, b, n, relu, y, mask);
+  return launch_status();
+}
+
+DK_API int dk_gap_fwd_f32(const float* x, int N, int HW, int C, float* out, void* stream) {
+  hipLaunchKernelGGL(gap_fwd_kernel, grid1((long long)N * C), dim3(256), 0, as_stream(stream), x, N, HW, C, out);
+  return launch_status();
+}
+
+DK_API int dk_gap_bwd_f32(const float* dy, int N, int HW, int C, float* dx, void* stream) {
+  hipLaunchKernelGGL(gap_bwd_kernel, grid1((long long)N * HW * C), dim3(256), 0, as_stream(stream), dy, N, HW, C, dx);
+  return launch_status();
+}
+
+DK_API int dk_softmax_xent_fwd_f32(const float* x, const float* y_onehot, int B, int K, float* p, float* loss,
+                                   void* stream) {
+  hipLaunchKernelGGL(softmax_xent_fwd_kernel, dim3(1), dim3(256), 0, as_stream(stream), x, y_onehot, B, K, p, loss);
+  return launch_status();
+}
+
+DK_API int dk_softmax_xent_bwd_f32(const float* p, const float* y_onehot, int B, int K, float* dx, void* stream) {
+  hipLaunchKernelGGL(softmax_xent_bwd_kernel, grid1((long long)B * K), dim3(256), 0, as_stream(stream), p, y_onehot, B,
+                     K, dx);
+  return launch_status();
+}
+
+// table: device array of ntens SgdEntry records (40 bytes each, see include/dorknet_hip.h),
+// total_blocks = sum over tensors of ceil(n / 256) (== block0 of a virtual entry ntens).
+DK_API int dk_sgd_momentum_multi_f32(const void* table, int ntens, long long total_blocks, float lr, float momentum,
+                                     float grad_scale, void* stream) {
+  if (ntens <= 0) return 0;
+  hipLaunchKernelGGL(sgd_momentum_multi_kernel, dim3((unsigned)total_blocks), dim3(256), 0, as_stream(stream),
+                     static_cast<const SgdEntry*>(table), ntens, lr, momentum, grad_scale);
+  return launch_status();
+}
+
+DK_API int dk_l2_loss_f32(const float* w, long long n, float strength, int accumulate, float* out, void* stream) {
+  hipLaunchKernelGGL(l2_loss_kernel, dim3(1), dim3(256), 0, as_stream(stream), w, n, strength, accumulate, out);
+  return launch_status();
+}
+
+DK_API size_t dk_colsum_workspace_bytes(int M, int N) { return (size_t)colsum_chunks(M) * N * sizeof(double); }
+
+DK_API int dk_colsum_f32(const float* in, int M, int N, float* out, void* ws, size_t ws_bytes, void* stream) {
+  if (ws_bytes < dk_colsum_workspace_bytes(M, N)) return DK_ERR_WORKSPACE;
+  const int chunks = colsum_chunks(M);
+  const int rpc = cdiv(M, chunks);
+  hipLaunchKernelGGL(colsum_partial_kernel, dim3(cdiv(N, 256), chunks), dim3(256), 0, as_stream(stream), in, M, N, rpc,
+                     static_cast<double*>(ws));
+  int rc = launch_status();
+  if (rc) return rc;
+  hipLaunchKernelGGL(colsum_final_kernel, dim3(cdiv(N, 256)), dim3(256), 0, as_stream(stream),
+                     static_cast<const double*>(ws), chunks, N, out);
+  return launch_status();
+}
+
+DK_API int dk_nchw_to_nhwc_f32(const float* x, int N, int C, int H, int W, int Cp, float* y, void* stream) {
+  hipLaunchKernelGGL(nchw_to_nhwc_kernel, grid1((long long)N * H * W * Cp), dim3(256), 0, as_stream(stream), x, N, C, H,
+                     W, Cp, y);
+  return launch_status();
+}
+
+DK_API int dk_nhwc_unpad_f32(const float* x, long long P, int Cp, int C, float* y, void* stream) {
+  hipLaunchKernelGGL(nhwc_unpad_kernel, grid1(P * C), dim3(256), 0, as_stream(stream), x, P, Cp, C, y);
+  return launch_status();
+}
+
+// y = s * x (l2 backward, regularisers/l2.py:16-17; gradient averaging in data parallel)
+DK_API int dk_scale_f32(const float* x, long long n, float s, float* y, void* stream) {
+  hipLaunchKernelGGL(scale_kernel, grid1(n), dim3(256), 0, as_stream(stream), x, n, s, y);
+  return launch_status();
+}
+
+DK_API int dk_abi_version(void) { return 1; }

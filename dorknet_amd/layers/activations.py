@@ -1,0 +1,107 @@
+"""ReLU (reference: layers/activations.py).
+
+``out = max(0, X)``; the backward mask is ``out > 0`` (gradient 0 at 0, :41).  The mask
+is kept as uint8 (the reference stores an fp32 copy, :42); ``positive_locs`` still
+returns the fp32 mask on request.  When the layer directly follows a BatchNormLayer in a
+network or residual chain, the two run fused (BatchNormLayer.forward_bn_relu) and this
+layer only records its output.
+"""
+from __future__ import annotations
+
+import torch
+
+from .._hip import lib, stream_handle
+from .._tensor import as_device, empty_nhwc, rows, to_nhwc
+from .layer import Layer
+
+
+def _same_layout(X):
+    X = as_device(X)
+    return to_nhwc(X) if X.dim() == 4 else rows(X)
+
+
+class ReLu(Layer):
+
+    def __init__(self, layer_name):
+        super().__init__(layer_name)
+        self._mask = None
+        self._fused_out = None
+
+    def __repr__(self):
+        return "ReLu({})".format(self.layer_name)
+
+    def _empty_like(self, x):
+        return empty_nhwc(*x.shape) if x.dim() == 4 else torch.empty_like(x)
+
+    def forward(self, X, test_mode=False):
+        self._require_on_gpu()
+        st = stream_handle()
+        x = _same_layout(X)
+        y = self._empty_like(x)
+        mask = None
+        if not test_mode:
+            mask = torch.empty(x.shape, dtype=torch.uint8, device=x.device,
+                               memory_format=torch.channels_last if x.dim() == 4 else torch.contiguous_format)
+        lib.dk_relu_fwd_f32(x.data_ptr(), x.numel(), y.data_ptr(), 0 if mask is None else mask.data_ptr(), st)
+        if not test_mode:
+            self._mask, self._fused_out = mask, None
+        return y
+
+    def forward_add(self, A, B, test_mode=False):
+        """ReLU(A + B) in one pass -- the residual join (residual_block.py:75)."""
+        self._require_on_gpu()
+        st = stream_handle()
+        a, b = _same_layout(A), _same_layout(B)
+        if a.shape != b.shape:
+            raise ValueError("residual join shape mismatch: {} vs {}".format(tuple(a.shape), tuple(b.shape)))
+        y = self._empty_like(a)
+        mask = None
+        if not test_mode:
+            mask = torch.empty(a.shape, dtype=torch.uint8, device=a.device,
+                               memory_format=torch.channels_last if a.dim() == 4 else torch.contiguous_format)
+        lib.dk_add_f32(a.data_ptr(), b.data_ptr(), a.numel(), 1, y.data_ptr(),
+                       0 if mask is None else mask.data_ptr(), st)
+        if not test_mode:
+            self._mask, self._fused_out = mask, None
+        return y
+
+    def _attach_fused(self, y, test_mode):
+        if not test_mode:
+            self._mask, self._fused_out = None, y
+
+    @property
+    def positive_locs(self):
+        """fp32 mask (out > 0), as the reference's attribute (activations.py:42)."""
+        if self._mask is not None:
+            out = torch.empty(self._mask.shape, dtype=torch.float32, device=self._mask.device,
+                              memory_format=torch.channels_last if self._mask.dim() == 4 else torch.contiguous_format)
+            lib.dk_mask_to_f32(self._mask.data_ptr(), self._mask.numel(), out.data_ptr(), stream_handle())
+            return out
+        if self._fused_out is not None:
+            y = self._fused_out
+            mask = torch.empty(y.shape, dtype=torch.uint8, device=y.device,
+                               memory_format=torch.channels_last if y.dim() == 4 else torch.contiguous_format)
+            tmp = self._empty_like(y)
+            lib.dk_relu_fwd_f32(y.data_ptr(), y.numel(), tmp.data_ptr(), mask.data_ptr(), stream_handle())
+            out = self._empty_like(y)
+            lib.dk_mask_to_f32(mask.data_ptr(), mask.numel(), out.data_ptr(), stream_handle())
+            return out
+        return None
+
+    def backward(self, upstream_dx):
+        self._require_on_gpu()
+        if self._mask is None:
+            raise RuntimeError("ReLu {}: backward without a training-mode forward (or the layer ran fused with "
+                               "the preceding BatchNormLayer; its backward is BatchNormLayer.backward_bn_relu)"
+                               .format(self.layer_name))
+        dy = _same_layout(upstream_dx)
+        dx = self._empty_like(dy)
+        lib.dk_relu_bwd_f32(dy.data_ptr(), self._mask.data_ptr(), dy.numel(), dx.data_ptr(), stream_handle())
+        return dx
+
+    def save_to_h5(self, open_f, save_grads=True):
+        from ..network.checkpoint import save_layer
+        save_layer(self, open_f, save_grads)
+
+    def load_from_h5(self, open_f, load_grads=True):
+        pass

@@ -1,0 +1,204 @@
+"""Batch normalisation (reference: layers/batch_norm.py).
+
+Training mode normalises with the batch statistics (population variance, eps = 1e-5),
+keeps running **mean and std** (not var) with momentum ``run_momentum`` and first-batch
+initialisation (batch_norm.py:76-89), and test mode uses the running statistics
+(:101-115).  Backward follows the explicit formula of :125-174.
+
+Implementation (dk_bn_* in libdorknet_hip.so): one fp64 statistics pass over X, a
+finalize, an apply pass; backward = one reduce pass + one apply pass.  Only X and the
+per-channel (mean, invstd) are kept for backward (the reference stores X_demean and
+X_hat).  When a network/residual chain puts a plain ReLu right after this layer, the
+pair runs fused (``forward_bn_relu`` / ``backward_bn_relu``): the ReLU is applied in the
+same pass and its backward mask is recomputed from X.
+
+With ``sync_group`` set (data-parallel SyncBN, see dorknet_amd.parallel), the per-channel
+sums are all-reduced between the partial and finalize stages so every rank normalises
+with full-batch statistics.
+"""
+from __future__ import annotations
+
+import torch
+
+from .._hip import lib, stream_handle, workspace
+from .._tensor import as_device, empty_nhwc, rows, to_nhwc
+from ._common import grad_buffer
+from .layer import Layer
+
+
+class BatchNormLayer(Layer):
+    """
+    https://arxiv.org/pdf/1502.03167.pdf
+    """
+
+    def __init__(self, layer_name, input_dimension=4,
+                 incoming_chans=None, run_momentum=0.95, is_on_gpu=True):
+        super().__init__(layer_name)
+        import numpy as np
+        self.eps = 1e-5
+        self.input_dimension = input_dimension
+        self.non_learned_params = {"running_mean": None, "running_std": None}
+        self.run_momentum = run_momentum
+        if self.input_dimension not in {2, 4}:
+            raise ValueError("BatchNorm input_dimension should have length 2 or 4...")
+        if self.input_dimension == 4:
+            self.av_axis = (0, 2, 3)
+        elif self.input_dimension == 2:
+            self.av_axis = 0
+        self.incoming_chans = incoming_chans
+        self.sync_group = None
+        if incoming_chans is not None:
+            gamma = np.ones(incoming_chans, dtype=np.float32)
+            beta = np.zeros(incoming_chans, dtype=np.float32)
+            if self.input_dimension == 4:
+                gamma = gamma[np.newaxis, :, np.newaxis, np.newaxis]
+                beta = beta[np.newaxis, :, np.newaxis, np.newaxis]
+            self.learned_params = {"gamma": gamma, "beta": beta}
+            self.grads = {"gamma": np.zeros_like(gamma), "beta": np.zeros_like(beta)}
+        else:
+            self.learned_params = {}
+            self.grads = {}
+
+    def __repr__(self):
+        return "BatchNormLayer({}, input_dimension={}, incoming_chans={}, run_momentum={})".format(
+            self.layer_name, self.input_dimension, self.incoming_chans, self.run_momentum)
+
+    # -- helpers -------------------------------------------------------------------------
+
+    def _param_shape(self, C):
+        return (1, C, 1, 1) if self.input_dimension == 4 else (C,)
+
+    def _prep_input(self, X):
+        if X.dim() == 4:
+            x = to_nhwc(X)
+            N, C, H, W = x.shape
+            return x, N * H * W, C
+        x = rows(X)
+        return x, x.shape[0], x.shape[1]
+
+    def _out_like(self, x):
+        if x.dim() == 4:
+            return empty_nhwc(*x.shape)
+        return torch.empty_like(x)
+
+    def _world(self):
+        import torch.distributed as dist
+        return dist.get_world_size(self.sync_group)
+
+    def _stats(self, x, P, C, st):
+        dev = x.device
+        mean = torch.empty(C, dtype=torch.float32, device=dev)
+        std = torch.empty(C, dtype=torch.float32, device=dev)
+        invstd = torch.empty(C, dtype=torch.float32, device=dev)
+        nlp = self.non_learned_params
+        first = nlp["running_mean"] is None
+        if first:
+            nlp["running_mean"] = torch.empty(self._param_shape(C), dtype=torch.float32, device=dev)
+            nlp["running_std"] = torch.empty(self._param_shape(C), dtype=torch.float32, device=dev)
+        rm, rs = as_device(nlp["running_mean"]), as_device(nlp["running_std"])
+        nlp["running_mean"], nlp["running_std"] = rm, rs
+        nb = lib.dk_bn_workspace_bytes(P, C)
+        ws = workspace.get(nb)
+        if self.sync_group is None:
+            lib.dk_bn_stats_f32(x.data_ptr(), P, C, float(self.eps), float(self.run_momentum), int(first),
+                                mean.data_ptr(), std.data_ptr(), invstd.data_ptr(), rm.data_ptr(), rs.data_ptr(),
+                                ws, nb, st)
+        else:
+            import torch.distributed as dist
+            lib.dk_bn_stats_partial_f64(x.data_ptr(), P, C, ws, nb, st)
+            sums = torch.empty(2 * C, dtype=torch.float64, device=dev)
+            lib.dk_bn_collapse_f64(ws, lib.dk_bn_partial_blocks(P, C), C, sums.data_ptr(), st)
+            dist.all_reduce(sums, group=self.sync_group)
+            count = float(P) * self._world()
+            lib.dk_bn_stats_finalize_f32(sums.data_ptr(), 1, C, count, float(self.eps), float(self.run_momentum),
+                                         int(first), mean.data_ptr(), std.data_ptr(), invstd.data_ptr(),
+                                         rm.data_ptr(), rs.data_ptr(), st)
+        return mean, std, invstd
+
+    # -- forward -------------------------------------------------------------------------
+
+    def _forward(self, X, test_mode, relu):
+        self._require_on_gpu()
+        st = stream_handle()
+        x, P, C = self._prep_input(as_device(X))
+        self.input_shape = tuple(x.shape)
+        gamma, beta = self.learned_params["gamma"], self.learned_params["beta"]
+        y = self._out_like(x)
+        if not test_mode:
+            mean, std, invstd = self._stats(x, P, C, st)
+            self.X = x
+            self._mean, self._invstd = mean, invstd
+            self.std = std.view(self._param_shape(C))
+        else:
+            rm = as_device(self.non_learned_params["running_mean"])
+            rs = as_device(self.non_learned_params["running_std"]).contiguous()
+            mean = rm.contiguous()
+            invstd = torch.empty(C, dtype=torch.float32, device=x.device)
+            lib.dk_bn_infer_params_f32(rs.data_ptr(), C, invstd.data_ptr(), st)
+        lib.dk_bn_apply_f32(x.data_ptr(), x.numel(), C, mean.data_ptr(), invstd.data_ptr(), gamma.data_ptr(),
+                            beta.data_ptr(), int(relu), y.data_ptr(), 0, st)
+        return y
+
+    def forward(self, X, test_mode=False, use_express=False):
+        """X.shape = (batch_size, channel, height, width) or (batch_size, features)."""
+        return self._forward(X, test_mode, relu=False)
+
+    def forward_bn_relu(self, X, relu_layer, test_mode=False):
+        """BN followed by ReLU in one pass (activations.py:37-42 fused into the apply)."""
+        y = self._forward(X, test_mode, relu=True)
+        relu_layer._attach_fused(y, test_mode)
+        return y
+
+    # -- backward ------------------------------------------------------------------------
+
+    def _backward(self, upstream_dx, relu):
+        self._require_on_gpu()
+        st = stream_handle()
+        x = self.X
+        dy = to_nhwc(upstream_dx) if x.dim() == 4 else rows(upstream_dx)
+        C = x.shape[1]
+        P = x.numel() // C
+        gamma, beta = self.learned_params["gamma"], self.learned_params["beta"]
+        dgamma = grad_buffer(self, "gamma", gamma.shape)
+        dbeta = grad_buffer(self, "beta", beta.shape)
+        dx = self._out_like(x)
+        if self.sync_group is None:
+            nb = lib.dk_bn_bwd_workspace_bytes(P, C)
+            lib.dk_bn_bwd_f32(x.data_ptr(), dy.data_ptr(), P, C, self._mean.data_ptr(), self._invstd.data_ptr(),
+                              gamma.data_ptr(), beta.data_ptr(), int(relu), dgamma.data_ptr(), dbeta.data_ptr(),
+                              dx.data_ptr(), workspace.get(nb), nb, st)
+        else:
+            import torch.distributed as dist
+            nb = lib.dk_bn_workspace_bytes(P, C)
+            ws = workspace.get(nb)
+            lib.dk_bn_bwd_partial_f64(x.data_ptr(), dy.data_ptr(), P, C, self._mean.data_ptr(),
+                                      self._invstd.data_ptr(), gamma.data_ptr(), beta.data_ptr(), int(relu), ws, nb,
+                                      st)
+            nblk = lib.dk_bn_partial_blocks(P, C)
+            local = torch.empty(2 * C, dtype=torch.float64, device=x.device)
+            glob = torch.empty(2 * C, dtype=torch.float64, device=x.device)
+            lib.dk_bn_collapse_f64(ws, nblk, C, local.data_ptr(), st)
+            lib.dk_bn_collapse_f64(ws, nblk, C, glob.data_ptr(), st)
+            dist.all_reduce(glob, group=self.sync_group)
+            k12 = torch.empty(2 * C, dtype=torch.float32, device=x.device)
+            lib.dk_bn_bwd_finalize_f32(local.data_ptr(), 1, glob.data_ptr(), 1, C, float(P) * self._world(),
+                                       dgamma.data_ptr(), dbeta.data_ptr(), k12.data_ptr(), st)
+            lib.dk_bn_bwd_apply_f32(x.data_ptr(), dy.data_ptr(), x.numel(), C, self._mean.data_ptr(),
+                                    self._invstd.data_ptr(), gamma.data_ptr(), beta.data_ptr(), int(relu),
+                                    k12.data_ptr(), dx.data_ptr(), st)
+        return dx
+
+    def backward(self, upstream_dx):
+        return self._backward(upstream_dx, relu=False)
+
+    def backward_bn_relu(self, upstream_dx, relu_layer):
+        """Backward of the fused BN+ReLU pair; upstream_dx is the gradient w.r.t. the ReLU output."""
+        return self._backward(upstream_dx, relu=True)
+
+    def save_to_h5(self, open_f, save_grads=True):
+        from ..network.checkpoint import save_layer
+        save_layer(self, open_f, save_grads)
+
+    def load_from_h5(self, open_f, load_grads=True):
+        from ..network.checkpoint import load_layer
+        load_layer(self, open_f, load_grads)

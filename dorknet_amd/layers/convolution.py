@@ -1,0 +1,135 @@
+"""Dense 2-D convolution (reference: layers/convolution.py).
+
+The reference lowers the convolution to im2col + cuBLAS SGEMM: it zero-fills and
+materialises a [N*OH*OW, C*R*S] patch matrix (convolution.py:69-74), multiplies it by
+the flattened filters (:75), and in backward multiplies again and scatters the result
+back with atomics (:101-111).  Here the same contraction runs as an implicit GEMM on the
+fp32 MFMA units: patches are gathered straight from the NHWC activation into LDS tiles
+and never exist in HBM (dk_conv2d_fwd_f32 / _dgrad_f32 / _wgrad_f32).
+
+Public surface identical to the reference: constructor signature and defaults
+(:13-14), ``learned_params`` / ``grads`` keys and shapes (weights (K, C, R, S), bias (K,)),
+``forward(X, test_mode=False)`` -> (N, K, OH, OW), ``backward(upstream_dx)`` -> dx with
+the input's shape, ``__repr__`` text (:40-51), and the float-then-int output-size
+arithmetic (:67-68, :105-106).
+"""
+from __future__ import annotations
+
+import torch
+
+from .._hip import lib, stream_handle, workspace
+from .._tensor import empty_nhwc, ptr, to_nhwc
+from ._common import add_regulariser_grad, grad_buffer, init_weights, l2_strength
+from .layer import Layer
+
+
+class ConvLayer(Layer):
+    def __init__(self, layer_name, filter_block_shape=None, stride=1, padding=1,
+                 with_bias=True, weight_regulariser=None, weight_initialiser="normal"):
+        super().__init__(layer_name)
+        self.stride = stride
+        self.padding = padding
+        self.patches = None
+        self.weight_regulariser = weight_regulariser
+        self.weight_initialiser = weight_initialiser
+        self.with_bias = with_bias
+        if filter_block_shape:
+            self.num_filters, self.filter_chans, self.f_rows, self.f_cols = filter_block_shape
+            weights = init_weights(tuple(filter_block_shape), weight_initialiser,
+                                   self.filter_chans + self.num_filters)
+            self.learned_params = {"weights": weights}
+            self.grads = {"weights": weights * 0}
+            if with_bias:
+                bias = (weights[:, 0, 0, 0] * 0).copy()
+                self.learned_params["bias"] = bias
+                self.grads["bias"] = bias * 0
+        else:
+            self.num_filters = None
+            self.learned_params = {}
+            self.grads = {}
+
+    def __repr__(self):
+        out = "ConvLayer({}, ".format(self.layer_name)
+        if self.num_filters is not None:
+            out += "filter_block_shape=({},{},{},{}), ".format(self.num_filters, self.filter_chans,
+                                                               self.f_rows, self.f_rows)
+        out += "stride={}, padding={}, with_bias={}, weight_regulariser={})".format(
+            self.stride, self.padding, self.with_bias, self.weight_regulariser)
+        return out
+
+    # -- helpers -------------------------------------------------------------------------
+
+    def _out_size(self, H, W):
+        # float arithmetic on the padded size, as convolution.py:67-68
+        self.num_row_patches = ((H + 2 * self.padding - self.f_rows) / self.stride) + 1
+        self.num_col_patches = ((W + 2 * self.padding - self.f_cols) / self.stride) + 1
+        return int(self.num_row_patches), int(self.num_col_patches)
+
+    # -- forward / backward --------------------------------------------------------------
+
+    def forward(self, X, test_mode=False):
+        self._require_on_gpu()
+        st = stream_handle()
+        self.input_shape = tuple(X.shape)
+        x = to_nhwc(X, cpad=4)
+        N, Cp, H, W = x.shape
+        K, C, R, S = self.num_filters, self.filter_chans, self.f_rows, self.f_cols
+        OH, OW = self._out_size(H, W)
+        w = self.learned_params["weights"]
+        w_krsc = torch.empty((K, R, S, Cp), dtype=torch.float32, device=x.device)
+        lib.dk_conv_weight_krsc_f32(w.data_ptr(), K, C, R, S, Cp, w_krsc.data_ptr(), st)
+        y = empty_nhwc(N, K, OH, OW)
+        bias = self.learned_params["bias"] if self.with_bias else None
+        lib.dk_conv2d_fwd_f32(x.data_ptr(), N, H, W, Cp, w_krsc.data_ptr(), K, R, S, self.stride, self.padding,
+                              ptr(bias), y.data_ptr(), OH, OW, st)
+        # The reference caches the patch matrix (convolution.py:69-74); the implicit GEMM
+        # only needs the (NHWC) input itself.
+        self.X = x
+        return y
+
+    def backward(self, upstream_dx):
+        self._require_on_gpu()
+        st = stream_handle()
+        dy = to_nhwc(upstream_dx)
+        x = self.X
+        N, Cp, H, W = x.shape
+        K, C, R, S = self.num_filters, self.filter_chans, self.f_rows, self.f_cols
+        OH, OW = int(self.num_row_patches), int(self.num_col_patches)
+        w = self.learned_params["weights"]
+        P = N * OH * OW
+        if self.with_bias:
+            gb = grad_buffer(self, "bias", (K,))
+            nb = lib.dk_colsum_workspace_bytes(P, K)
+            lib.dk_colsum_f32(dy.data_ptr(), P, K, gb.data_ptr(), workspace.get(nb), nb, st)
+        # weight gradient (+ l2 folded in, convolution.py:93-100)
+        gw = grad_buffer(self, "weights", (K, C, R, S))
+        s = l2_strength(self.weight_regulariser)
+        nb = lib.dk_conv2d_wgrad_workspace_bytes(N, OH, OW, K, Cp, R, S)
+        lib.dk_conv2d_wgrad_f32(dy.data_ptr(), x.data_ptr(), N, H, W, Cp, C, K, R, S, self.stride, self.padding,
+                                OH, OW, w.data_ptr() if s else 0, s or 0.0, gw.data_ptr(), workspace.get(nb), nb,
+                                st)
+        if s is None:
+            add_regulariser_grad(gw, w, self.weight_regulariser)
+        # input gradient (convolution.py:101-117); shape = the forward input's shape
+        Hin, Win = self.input_shape[2], self.input_shape[3]
+        dx = empty_nhwc(N, C, Hin, Win)
+        if self.stride == 1 and K % 4 == 0:
+            w_crsk = torch.empty((C, R, S, K), dtype=torch.float32, device=x.device)
+            lib.dk_conv_weight_crsk_f32(w.data_ptr(), K, C, R, S, w_crsk.data_ptr(), st)
+            lib.dk_conv2d_dgrad_f32(dy.data_ptr(), N, OH, OW, K, w_crsk.data_ptr(), C, R, S, self.padding,
+                                    dx.data_ptr(), Hin, Win, st)
+        else:
+            nb = lib.dk_conv2d_dgrad_cols_workspace_bytes(N, OH, OW, C, R, S)
+            lib.dk_conv2d_dgrad_strided_f32(dy.data_ptr(), N, OH, OW, K, w.data_ptr(), C, R, S, self.stride,
+                                            self.padding, dx.data_ptr(), Hin, Win, workspace.get(nb), nb, st)
+        return dx
+
+    # -- checkpoint hooks (h5py is not available in this image; kept for API parity) ------
+
+    def save_to_h5(self, open_f, save_grads=True):
+        from ..network.checkpoint import save_layer
+        save_layer(self, open_f, save_grads)
+
+    def load_from_h5(self, open_f, load_grads=True):
+        from ..network.checkpoint import load_layer
+        load_layer(self, open_f, load_grads)

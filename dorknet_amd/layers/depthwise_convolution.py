@@ -1,0 +1,114 @@
+"""Depthwise (per-channel) convolution (reference: layers/depthwise_convolution.py).
+
+The reference GPU path (forward_cp :85-102, backward_cp :198-221) pads the input into a
+copy, runs one thread per output with nine global read-modify-writes, and in backward
+funnels N*OH*OW atomicAdds into each weight.  Here: direct NHWC kernels with register
+accumulation, bounds checks instead of a padded copy, and a two-stage deterministic
+weight-gradient reduction (dk_dwconv_fwd_f32 / _dgrad_f32 / _wgrad_f32).
+
+Public surface identical to the reference: constructor (:11-13), weights (C, R, S),
+bias (C,), ``forward`` / ``backward`` / ``__repr__`` (:41-51).
+"""
+from __future__ import annotations
+
+import torch
+
+from .._hip import lib, stream_handle, workspace
+from .._tensor import empty_nhwc, ptr, to_nhwc
+from ._common import add_regulariser_grad, grad_buffer, init_weights, l2_strength
+from .layer import Layer
+
+
+class DepthwiseConvLayer(Layer):
+    def __init__(self, layer_name, filter_block_shape=None,
+                 stride=1, padding=1, with_bias=True,
+                 weight_regulariser=None, weight_initialiser="normal"):
+        """
+        filter_block_shape = (num_incoming_channels, num_filter_rows, num_filter_cols)
+        """
+        super().__init__(layer_name)
+        self.stride = stride
+        self.padding = padding
+        self.with_bias = with_bias
+        self.weight_regulariser = weight_regulariser
+        self.weight_initialiser = weight_initialiser
+        if filter_block_shape is not None:
+            self.num_filters, self.f_rows, self.f_cols = filter_block_shape
+            weights = init_weights(tuple(filter_block_shape), weight_initialiser, 2 * self.num_filters)
+            self.learned_params = {"weights": weights}
+            self.grads = {"weights": weights * 0}
+            if with_bias:
+                bias = (weights[:, 0, 0] * 0).copy()
+                self.learned_params["bias"] = bias
+                self.grads["bias"] = bias * 0
+        else:
+            self.num_filters = None
+            self.learned_params = {}
+            self.grads = {}
+
+    def __repr__(self):
+        out = "DepthwiseConvLayer({}, ".format(self.layer_name)
+        if self.num_filters is not None:
+            out += "filter_block_shape=({}, {}, {}), ".format(self.num_filters, self.f_rows, self.f_cols)
+        out += "stride={}, padding={}, with_bias={}, weight_regulariser={})".format(
+            self.stride, self.padding, self.with_bias, repr(self.weight_regulariser))
+        return out
+
+    def _w_rsc(self, st):
+        w = self.learned_params["weights"]
+        C, R, S = w.shape
+        w_rsc = torch.empty((R, S, C), dtype=torch.float32, device=w.device)
+        lib.dk_dw_weight_rsc_f32(w.data_ptr(), C, R, S, w_rsc.data_ptr(), st)
+        return w_rsc
+
+    def forward(self, X, test_mode=False):
+        self._require_on_gpu()
+        st = stream_handle()
+        x = to_nhwc(X)
+        N, C, H, W = x.shape
+        R, S = self.f_rows, self.f_cols
+        # float-then-int output size (depthwise_convolution.py:89-90)
+        self.num_row_patches = ((H + 2 * self.padding - R) / self.stride) + 1
+        self.num_col_patches = ((W + 2 * self.padding - S) / self.stride) + 1
+        OH, OW = int(self.num_row_patches), int(self.num_col_patches)
+        y = empty_nhwc(N, C, OH, OW)
+        bias = self.learned_params["bias"] if self.with_bias else None
+        lib.dk_dwconv_fwd_f32(x.data_ptr(), N, H, W, C, self._w_rsc(st).data_ptr(), R, S, self.stride,
+                              self.padding, ptr(bias), y.data_ptr(), OH, OW, st)
+        if not test_mode:
+            self.X = x  # the reference keeps the *padded* input (:87-88); padding is implicit here
+        return y
+
+    def backward(self, upstream_dx):
+        self._require_on_gpu()
+        st = stream_handle()
+        dy = to_nhwc(upstream_dx)
+        x = self.X
+        N, C, H, W = x.shape
+        R, S = self.f_rows, self.f_cols
+        OH, OW = int(self.num_row_patches), int(self.num_col_patches)
+        P = N * OH * OW
+        w = self.learned_params["weights"]
+        if self.with_bias:
+            gb = grad_buffer(self, "bias", (C,))
+            nb = lib.dk_colsum_workspace_bytes(P, C)
+            lib.dk_colsum_f32(dy.data_ptr(), P, C, gb.data_ptr(), workspace.get(nb), nb, st)
+        gw = grad_buffer(self, "weights", (C, R, S))
+        s = l2_strength(self.weight_regulariser)
+        nb = lib.dk_dwconv_wgrad_workspace_bytes(N, OH, OW, C, R, S)
+        lib.dk_dwconv_wgrad_f32(dy.data_ptr(), x.data_ptr(), N, H, W, C, R, S, self.stride, self.padding, OH, OW,
+                                w.data_ptr() if s else 0, s or 0.0, gw.data_ptr(), workspace.get(nb), nb, st)
+        if s is None:
+            add_regulariser_grad(gw, w, self.weight_regulariser)
+        dx = empty_nhwc(N, C, H, W)
+        lib.dk_dwconv_dgrad_f32(dy.data_ptr(), N, OH, OW, C, self._w_rsc(st).data_ptr(), R, S, self.stride,
+                                self.padding, dx.data_ptr(), H, W, st)
+        return dx
+
+    def save_to_h5(self, open_f, save_grads=True):
+        from ..network.checkpoint import save_layer
+        save_layer(self, open_f, save_grads)
+
+    def load_from_h5(self, open_f, load_grads=True):
+        from ..network.checkpoint import load_layer
+        load_layer(self, open_f, load_grads)

@@ -1,0 +1,105 @@
+"""1x1 (pointwise) convolution (reference: layers/pointwise_convolution.py).
+
+The reference subsamples with a strided view (:48-49), copies the input into an NHWC
+row matrix (:50), runs cuBLAS SGEMM (:51), and in backward widens the stride-s gradient
+into a freshly zeroed buffer (:68-72).  Here the activations are already NHWC, so the
+layer is the R = S = 1 case of the implicit-GEMM MFMA engine: subsampling is a strided
+gather in the A-tile loader and the widen is fused into the dgrad epilogue.
+
+Public surface identical to the reference: constructor (:7-8, note ``stride`` is the
+second positional argument), weights (K, C), bias (K,), ``__repr__`` (:35-44), the
+output spatial size ceil(H/s), and the backward output size (s*OH, s*OW).
+"""
+from __future__ import annotations
+
+from .._hip import lib, stream_handle, workspace
+from .._tensor import empty_nhwc, ptr, to_nhwc
+from ._common import add_regulariser_grad, grad_buffer, init_weights, l2_strength
+from .layer import Layer
+
+
+class PointwiseConvLayer(Layer):
+    def __init__(self, layer_name, stride=1, filter_block_shape=None, with_bias=True,
+                 weight_regulariser=None, weight_initialiser="normal"):
+        """
+        filter_block_shape = (num_filters, num_incoming_channels)
+        """
+        super().__init__(layer_name)
+        self.stride = stride
+        self.with_bias = with_bias
+        self.weight_regulariser = weight_regulariser
+        self.weight_initialiser = weight_initialiser
+        if filter_block_shape is not None:
+            self.num_filters, self.num_channels = filter_block_shape
+            weights = init_weights(tuple(filter_block_shape), weight_initialiser,
+                                   self.num_channels + self.num_filters)
+            self.learned_params = {"weights": weights}
+            self.grads = {"weights": weights * 0}
+            if with_bias:
+                bias = (weights[:, 0] * 0).copy()
+                self.learned_params["bias"] = bias
+                self.grads["bias"] = bias * 0
+        else:
+            self.num_filters = None
+            self.learned_params = {}
+            self.grads = {}
+
+    def __repr__(self):
+        out = "PointwiseConvLayer({}, ".format(self.layer_name)
+        if self.num_filters is not None:
+            out += "filter_block_shape=({}, {}), ".format(self.num_filters, self.num_channels)
+        out += "stride={}, with_bias={}, weight_regulariser={}, is_on_gpu={})".format(
+            self.stride, self.with_bias, repr(self.weight_regulariser), self.is_on_gpu)
+        return out
+
+    def forward(self, X, test_mode=False):
+        self._require_on_gpu()
+        st = stream_handle()
+        x = to_nhwc(X, cpad=4)
+        N, Cp, H, W = x.shape
+        K = self.num_filters
+        s = self.stride
+        OH, OW = -(-H // s), -(-W // s)  # len(range(0, H, s)), as X[:, :, ::s, ::s]
+        y = empty_nhwc(N, K, OH, OW)
+        w = self.learned_params["weights"]
+        if Cp != self.num_channels:
+            raise ValueError("PointwiseConvLayer {}: input has {} channels, weights expect {} (a multiple of 4 "
+                             "is required)".format(self.layer_name, X.shape[1], self.num_channels))
+        bias = self.learned_params["bias"] if self.with_bias else None
+        lib.dk_pwconv_fwd_f32(x.data_ptr(), N, H, W, Cp, w.data_ptr(), K, s, ptr(bias), y.data_ptr(), OH, OW, st)
+        self.X = x  # the reference keeps the NHWC row copy as self.patches (:50)
+        self.out_hw = (OH, OW)
+        return y
+
+    def backward(self, upstream_dx):
+        self._require_on_gpu()
+        st = stream_handle()
+        dy = to_nhwc(upstream_dx)
+        x = self.X
+        N, C, H, W = x.shape
+        K, s = self.num_filters, self.stride
+        OH, OW = self.out_hw
+        P = N * OH * OW
+        w = self.learned_params["weights"]
+        if self.with_bias:
+            gb = grad_buffer(self, "bias", (K,))
+            nb = lib.dk_colsum_workspace_bytes(P, K)
+            lib.dk_colsum_f32(dy.data_ptr(), P, K, gb.data_ptr(), workspace.get(nb), nb, st)
+        gw = grad_buffer(self, "weights", (K, C))
+        l2s = l2_strength(self.weight_regulariser)
+        nb = lib.dk_pwconv_wgrad_workspace_bytes(N, OH, OW, K, C)
+        lib.dk_pwconv_wgrad_f32(dy.data_ptr(), x.data_ptr(), N, H, W, C, K, s, OH, OW, w.data_ptr() if l2s else 0,
+                                l2s or 0.0, gw.data_ptr(), workspace.get(nb), nb, st)
+        if l2s is None:
+            add_regulariser_grad(gw, w, self.weight_regulariser)
+        dx = empty_nhwc(N, C, OH * s, OW * s)  # widened shape, pointwise_convolution.py:68-72
+        lib.dk_pwconv_dgrad_f32(dy.data_ptr(), N, OH, OW, K, w.data_ptr(), C, s, dx.data_ptr(), st)
+        return dx
+
+    def save_to_h5(self, open_f, save_grads=True):
+        from ..network.checkpoint import save_layer
+        save_layer(self, open_f, save_grads)
+
+    def load_from_h5(self, open_f, load_grads=True):
+        from ..network.checkpoint import load_layer
+        load_layer(self, open_f, load_grads)

@@ -1,0 +1,100 @@
+"""Residual block (reference: layers/residual_block.py).
+
+``forward``: post_skip_activation(layer_list(X) + skip_projection(X)) -- the join and a
+ReLU post-activation run as one pass (ReLu.forward_add); BN+ReLU pairs inside the chain
+run fused.  ``backward``: the activation's backward, the chain in reverse, plus the skip
+branch (or identity), summed (:86-97).  ``regulariser_forward`` sums the chain's terms
+only -- the skip projection's l2 is *not* in the loss (:78-84), while its gradient still
+gets the l2 term in its own backward; and SGDMomentum never updates the skip projection
+(optimisers/SGDMomentum.py:7-14).  Both quirks are kept.
+"""
+from __future__ import annotations
+
+from .._hip import lib, stream_handle
+from .._tensor import empty_nhwc, to_nhwc
+from ._chain import chain_backward, chain_forward
+from .activations import ReLu
+from .batch_norm import BatchNormLayer
+from .convolution import ConvLayer
+from .depthwise_convolution import DepthwiseConvLayer
+from .layer import Layer
+from .pointwise_convolution import PointwiseConvLayer
+
+
+def _add(a, b):
+    a, b = to_nhwc(a), to_nhwc(b)
+    if a.shape != b.shape:
+        raise ValueError("residual backward shape mismatch: {} vs {}".format(tuple(a.shape), tuple(b.shape)))
+    out = empty_nhwc(*a.shape)
+    lib.dk_add_f32(a.data_ptr(), b.data_ptr(), a.numel(), 0, out.data_ptr(), 0, stream_handle())
+    return out
+
+
+class ResidualBlock(Layer):
+    """
+    A block with a skip connection around the provided layer_list.  The output of
+    layer_list[-1] must have the same shape as skip_projection(X) because they are joined
+    by addition - skip_projection=None means an identity projection.  The nonlinear
+    activation (if not None) is applied after the join.
+    """
+
+    def __init__(self, layer_name, layer_list=None, skip_projection=None, post_skip_activation=None):
+        super().__init__(layer_name)
+        self.layer_list = layer_list
+        self.skip_projection = skip_projection
+        self.post_skip_activation = post_skip_activation
+        if layer_list is None:
+            self.layer_list = []
+        self._steps = None
+
+    def __repr__(self):
+        return "ResidualBlock({}, layer_list={}, skip_projection={}, post_skip_activation={})".format(
+            self.layer_name, self.layer_list, self.skip_projection, self.post_skip_activation)
+
+    def to_gpu(self):
+        if self.is_on_gpu:
+            print("Layer already on GPU, ignoring request")
+            return
+        for layer in self.layer_list:
+            layer.to_gpu()
+        if self.skip_projection is not None:
+            self.skip_projection.to_gpu()
+        if self.post_skip_activation is not None:
+            self.post_skip_activation.to_gpu()
+        self.is_on_gpu = True
+
+    def forward(self, X, test_mode=False):
+        X_tmp, self._steps = chain_forward(self.layer_list, X, test_mode=test_mode)
+        if self.skip_projection is not None:
+            skippee = self.skip_projection.forward(X, test_mode=test_mode)
+        else:
+            skippee = X
+        post = self.post_skip_activation
+        if type(post) is ReLu:
+            return post.forward_add(X_tmp, skippee, test_mode=test_mode)
+        return post.forward(_add(X_tmp, skippee), test_mode=test_mode)
+
+    def regulariser_forward(self):
+        regularisation = 0
+        for l in self.layer_list:
+            if hasattr(l, "regulariser_forward"):
+                regularisation += l.regulariser_forward()
+        return regularisation
+
+    def backward(self, upstream_dx):
+        joined_dx = self.post_skip_activation.backward(upstream_dx)
+        dx = chain_backward(self._steps, joined_dx)
+        if self.skip_projection is not None:
+            return _add(dx, self.skip_projection.backward(joined_dx))
+        return _add(dx, joined_dx)
+
+    def save_to_h5(self, open_f, save_grads=True):
+        from ..network.checkpoint import save_layer
+        save_layer(self, open_f, save_grads)
+
+    def load_from_h5(self, open_f, load_grads=True):
+        from ..network.checkpoint import load_layer
+        load_layer(self, open_f, load_grads)
+
+
+__all__ = ["ResidualBlock", "ConvLayer", "DepthwiseConvLayer", "PointwiseConvLayer", "ReLu", "BatchNormLayer"]

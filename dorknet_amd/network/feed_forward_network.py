@@ -1,0 +1,130 @@
+"""Sequential network container (reference: network/feed_forward_network.py).
+
+Same API: ``add_layer``, ``set_loss_layer``, ``to_gpu``, ``forward(X, y_one_hot,
+test_mode=False, terminal_layer_name=None) -> (loss, X)``, ``backward()``, ``test``,
+``save_weights_to_h5``, ``save_layer_structure_to_json``,
+``load_network_from_json_and_h5``.  The forward pass runs (BatchNormLayer, ReLu) pairs
+fused (layers/_chain.py) and remembers the steps it took for ``backward``.
+"""
+from __future__ import annotations
+
+import json
+
+import numpy as np
+
+from ..layers._chain import chain_backward, fusable_pair, fusion_enabled
+from ..layers.activations import ReLu  # noqa: F401  (re-exported names used by loaders)
+from ..layers.batch_norm import BatchNormLayer  # noqa: F401
+from ..layers.convolution import ConvLayer  # noqa: F401
+from ..layers.dense_layer import DenseLayer  # noqa: F401
+from ..layers.depthwise_convolution import DepthwiseConvLayer  # noqa: F401
+from ..layers.losses import SoftmaxWithCrossEntropy  # noqa: F401
+from ..layers.pointwise_convolution import PointwiseConvLayer  # noqa: F401
+from ..layers.pooling import GlobalAveragePoolingLayer  # noqa: F401
+from ..layers.residual_block import ResidualBlock  # noqa: F401
+from .._tensor import as_device
+
+
+class FeedForwardNetwork:
+    def __init__(self, name):
+        self.name = name
+        self.is_on_gpu = False
+        self.layers = []
+        self.loss_layer = None
+        self._steps = None
+
+    def __repr__(self):
+        out = "{}: \n".format(self.name)
+        for l in self.layers:
+            out += "\t" + l.__repr__() + "\n"
+        return out
+
+    def add_layer(self, layer):
+        self.layers.append(layer)
+
+    def set_loss_layer(self, loss_layer):
+        self.loss_layer = loss_layer
+
+    def to_gpu(self):
+        if self.is_on_gpu:
+            print("Model already on GPU, ignoring request")
+            return
+        layer = None
+        try:
+            for layer in self.layers:
+                layer.to_gpu()
+            if self.loss_layer is not None:
+                self.loss_layer.is_on_gpu = True
+            self.is_on_gpu = True
+        except Exception as e:
+            print("Error putting layer {} on GPU, error was: {}".format(layer, e))
+            raise e
+
+    def forward(self, X, y_one_hot, test_mode=False, terminal_layer_name=None):
+        loss = 0
+        regularisation_terms = []
+        steps = []
+        self._steps = steps
+        fuse = fusion_enabled()
+        layers = self.layers
+        i = 0
+        while i < len(layers):
+            layer = layers[i]
+            nxt = layers[i + 1] if i + 1 < len(layers) else None
+            if fuse and nxt is not None and fusable_pair(layer, nxt) and layer.layer_name != terminal_layer_name:
+                X = layer.forward_bn_relu(X, nxt, test_mode=test_mode)
+                group = (layer, nxt)
+                i += 2
+            else:
+                X = layer.forward(X, test_mode=test_mode)
+                group = (layer,)
+                i += 1
+            steps.append(group)
+            for l in group:
+                if l.layer_name == terminal_layer_name:
+                    return loss, X
+                if not test_mode and hasattr(l, "regulariser_forward"):
+                    regularisation_terms.append(l.regulariser_forward())
+        if self.loss_layer is not None:
+            this_loss, X = self.loss_layer.forward(X, y_one_hot, test_mode=test_mode)
+            loss += this_loss
+            loss += sum(regularisation_terms)
+        return loss, X  # NB if test_mode=True, you get softmax scores ("logits")
+
+    def backward(self):
+        if self.loss_layer is not None:
+            upstream_dx = self.loss_layer.backward()
+        else:
+            raise ValueError("Network doesn't have a loss, can't run backward pass.")
+        chain_backward(self._steps, upstream_dx)
+
+    def test(self, data_loader, batch_size, test_set_size):
+        from tqdm import tqdm
+        test_correct_total = 0
+        for X_test_batch, y_test_batch, _ in tqdm(data_loader, total=test_set_size / batch_size):
+            X_test_batch = as_device(X_test_batch)
+            _, batch_scores = self.forward(X_test_batch, y_one_hot=None, test_mode=True)
+            test_correct_total += np.sum(np.asarray(y_test_batch) ==
+                                         np.argmax(batch_scores.cpu().numpy(), axis=1))
+        return float(test_correct_total) / test_set_size
+
+    def save_weights_to_h5(self, fname):
+        from .checkpoint import open_h5
+        with open_h5(fname, "w") as f:
+            for layer in self.layers:
+                layer.save_to_h5(f)
+            if self.loss_layer is not None:
+                self.loss_layer.save_to_h5(f)
+
+    def save_layer_structure_to_json(self, fname):
+        structure_dict = {"name": self.name}
+        for layer in self.layers:
+            structure_dict[layer.layer_name] = repr(layer)
+        if self.loss_layer is not None:
+            structure_dict[self.loss_layer.layer_name] = repr(self.loss_layer)
+        with open(fname, "w") as f:
+            json.dump(structure_dict, f, indent=4)
+
+    def load_network_from_json_and_h5(self, json_fname, h5_fname):
+        from .checkpoint import load_network
+        load_network(self, json_fname, h5_fname)

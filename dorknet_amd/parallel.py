@@ -1,0 +1,158 @@
+"""Data parallelism over RCCL (one process per GPU, torch.distributed backend "nccl").
+
+The reference is single-process.  Here each rank runs the same network
+on its slice of the global batch; the only exchange is an all-reduce (average) of the
+weight gradients, grouped into ~`bucket_bytes` buckets in reverse layer order and issued
+asynchronously as soon as the backward pass has produced a bucket, so communication
+overlaps the remaining backward work.  All gradient tensors are re-pointed into one flat
+buffer so the kernels write straight into the buckets (no packing copies).
+
+Batch norm: "local" (per-rank statistics, standard DDP semantics, the default for
+throughput) or "sync" (SyncBN: per-channel sums all-reduced in forward and backward, so
+the result equals single-process training on the concatenated batch).
+
+Averaging: the reference's loss gradient is already divided by the local batch
+(layers/losses.py:34), so the mean over ranks equals the full-batch gradient, and the
+per-layer `+ strength * W` l2 term stays correct (a sum would scale it by world size).
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+from .layers._chain import chain_backward
+
+
+def _all_layers(layers):
+    """Every layer (depth-first, forward order), including ResidualBlock children and
+    skip projections."""
+    out = []
+    for l in layers:
+        out.append(l)
+        if hasattr(l, "layer_list"):
+            out.extend(_all_layers(l.layer_list))
+            if getattr(l, "skip_projection", None) is not None:
+                out.append(l.skip_projection)
+    return out
+
+
+def grad_slots(network):
+    """[(top_level_index, layer, key, shape)] for every gradient, in forward order."""
+    slots = []
+    for ti, top in enumerate(network.layers):
+        for l in _all_layers([top]):
+            if not l.grads:
+                continue
+            for k, g in l.grads.items():
+                slots.append((ti, l, k, tuple(g.shape)))
+    return slots
+
+
+def plan_buckets(slot_numels, slot_owner, bucket_bytes):
+    """Group slots (given in forward order) into buckets in *reverse* order.
+    Returns a list of buckets; each is (list_of_slot_indices, last_top_level_index) where
+    the bucket is complete once backward has finished top-level layer `last...` (the
+    smallest top-level index in it, since backward runs in reverse)."""
+    buckets, cur, cur_bytes = [], [], 0
+    for si in reversed(range(len(slot_numels))):
+        cur.append(si)
+        cur_bytes += 4 * slot_numels[si]
+        if cur_bytes >= bucket_bytes:
+            buckets.append(cur)
+            cur, cur_bytes = [], 0
+    if cur:
+        buckets.append(cur)
+    return [(b, min(slot_owner[s] for s in b)) for b in buckets]
+
+
+class DataParallel:
+    def __init__(self, network, group=None, batch_norm="local", bucket_bytes=2 << 20, device=None):
+        if batch_norm not in ("local", "sync"):
+            raise ValueError("batch_norm must be 'local' or 'sync'")
+        self.network = network
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.batch_norm = batch_norm
+        slots = grad_slots(network)
+        numels = [int(torch.Size(s[3]).numel()) for s in slots]
+        self.total = sum(numels)
+        dev = device if device is not None else (torch.device("cuda", torch.cuda.current_device())
+                                                 if torch.cuda.is_available() else torch.device("cpu"))
+        self.flat = torch.zeros(self.total, dtype=torch.float32, device=dev)
+        # offsets laid out in reverse order so each bucket is one contiguous range
+        order = list(reversed(range(len(slots))))
+        offs, off = {}, 0
+        for si in order:
+            offs[si] = off
+            off += numels[si]
+        for si, (_, layer, key, shape) in enumerate(slots):
+            view = self.flat[offs[si]:offs[si] + numels[si]].view(shape)
+            old = layer.grads[key]
+            if isinstance(old, torch.Tensor):
+                view.copy_(old.to(view.device))
+            layer.grads[key] = view
+        self.buckets = []
+        for idxs, ready_after in plan_buckets(numels, [s[0] for s in slots], bucket_bytes):
+            lo = min(offs[i] for i in idxs)
+            hi = max(offs[i] + numels[i] for i in idxs)
+            self.buckets.append((lo, hi, ready_after))
+        if batch_norm == "sync":
+            from .layers.batch_norm import BatchNormLayer
+            for l in _all_layers(network.layers):
+                if isinstance(l, BatchNormLayer):
+                    l.sync_group = group if group is not None else dist.group.WORLD
+        self._works = []
+
+    def _launch(self, lo, hi):
+        view = self.flat[lo:hi]
+        if view.is_cuda:
+            work = dist.all_reduce(view, op=dist.ReduceOp.AVG, group=self.group, async_op=True)
+        else:  # gloo (CPU tests): no AVG; sum then scale after wait
+            work = dist.all_reduce(view, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+        self._works.append((work, view))
+
+    def backward(self):
+        """network.backward() with gradient all-reduce overlapped per bucket."""
+        net = self.network
+        dy = net.loss_layer.backward()
+        steps = net._steps
+        top_index = {id(l): i for i, l in enumerate(net.layers)}
+        pending = list(self.buckets)
+        self._works = []
+        for step in reversed(steps):
+            dy = chain_backward([step], dy)
+            done_idx = min(top_index[id(l)] for l in step)
+            still = []
+            for lo, hi, ready_after in pending:
+                if done_idx <= ready_after:
+                    self._launch(lo, hi)
+                else:
+                    still.append((lo, hi, ready_after))
+            pending = still
+        for lo, hi, _ in pending:
+            self._launch(lo, hi)
+        self.finish()
+
+    def allreduce_grads(self):
+        """All-reduce every bucket now (for callers that ran network.backward() themselves)."""
+        self._works = []
+        for lo, hi, _ in self.buckets:
+            self._launch(lo, hi)
+        self.finish()
+
+    def finish(self):
+        for work, view in self._works:
+            work.wait()
+            if not view.is_cuda:
+                view.div_(self.world)
+        self._works = []
+
+    def broadcast_parameters(self, src=0):
+        """Make every rank start from rank `src`'s parameters and running statistics."""
+        for l in _all_layers(self.network.layers):
+            for d in (l.learned_params, l.non_learned_params):
+                if not d:
+                    continue
+                for v in d.values():
+                    if isinstance(v, torch.Tensor):
+                        dist.broadcast(v, src, group=self.group)

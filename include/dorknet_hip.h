@@ -1,0 +1,145 @@
+/*
+ * dorknet_hip.h -- C ABI of libdorknet_hip.so, the MI355X (gfx950) implementation of
+ * Dorknet's convolution training hot path (reference: WJGiles/Dorknet).
+ *
+ * Conventions (every entry point):
+ *   - pointers are DEVICE pointers owned by the caller; nothing here allocates;
+ *   - activations are NHWC fp32 ([P][C] with P = N*H*W pixels, channels innermost);
+ *   - scratch memory comes from a caller-provided workspace (ws, ws_bytes); each user of
+ *     one has a matching *_workspace_bytes() query with the same shape arguments;
+ *   - `stream` is a hipStream_t passed as void*; all work is stream-ordered on it;
+ *   - the int return value is a hipError_t (0 = success); 10001 = bad arguments,
+ *     10002 = workspace too small.  Nothing is checked on the device.
+ *   - reentrant: no global mutable state.
+ *
+ * Each block cites the reference interface it replaces (file:line under the reference
+ * repository).  In the reference these are CuPy RawKernel launches (NVRTC CUDA strings),
+ * cuBLAS SGEMM through cp.dot, and CuPy elementwise / reduction kernels, called from the
+ * Layer classes; here the Layer classes (dorknet_amd/layers/) call these entry points
+ * through ctypes (dorknet_amd/_hip.py).  Parsed by dorknet_amd/_hip.py to declare the
+ * ctypes prototypes: keep one declaration per statement, `int|size_t name(args);`.
+ */
+#ifndef DORKNET_HIP_H
+#define DORKNET_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+int dk_abi_version(void);
+
+/* ---------------------------------------------------------------------------------------
+ * Dense convolution, implicit GEMM on fp32 MFMA.
+ * Replaces ConvLayer.forward GPU branch (layers/convolution.py:58-87: pad_input :144-151,
+ * CUDA im2col :187-203, cp.dot :75) and ConvLayer.backward (:90-117: wgrad cp.dot :96,
+ * l2 :99-100, dgrad cp.dot :104, CUDA row2im :205-222).
+ * Weights stay in the reference layout W[K][C][R][S]; the *_krsc / *_crsk helpers produce
+ * the GEMM-friendly copies (C padded to Cp, a multiple of 4, with zeros).
+ * OH/OW are passed in: the caller computes them with the reference formula
+ * int((H + 2*pad - R)/stride + 1) (convolution.py:67-68).
+ * ------------------------------------------------------------------------------------- */
+int dk_conv_weight_krsc_f32(const float* w_kcrs, int K, int C, int R, int S, int Cp, float* w_krsc, void* stream);
+int dk_conv_weight_crsk_f32(const float* w_kcrs, int K, int C, int R, int S, float* w_crsk, void* stream);
+int dk_conv2d_fwd_f32(const float* x, int N, int H, int W, int C, const float* w_krsc, int K, int R, int S, int stride, int pad, const float* bias, float* y, int OH, int OW, void* stream);
+int dk_conv2d_dgrad_f32(const float* dy, int N, int OH, int OW, int K, const float* w_crsk, int C, int R, int S, int pad, float* dx, int H, int W, void* stream);
+size_t dk_conv2d_dgrad_cols_workspace_bytes(int N, int OH, int OW, int C, int R, int S);
+int dk_conv2d_dgrad_strided_f32(const float* dy, int N, int OH, int OW, int K, const float* w_kcrs, int C, int R, int S, int stride, int pad, float* dx, int H, int W, void* ws, size_t ws_bytes, void* stream);
+size_t dk_conv2d_wgrad_workspace_bytes(int N, int OH, int OW, int K, int Cp, int R, int S);
+int dk_conv2d_wgrad_f32(const float* dy, const float* x, int N, int H, int W, int Cp, int C, int K, int R, int S, int stride, int pad, int OH, int OW, const float* w_kcrs, float l2, float* dw_kcrs, void* ws, size_t ws_bytes, void* stream);
+
+/* ---------------------------------------------------------------------------------------
+ * Pointwise (1x1) convolution = the R=S=1 case of the GEMM engine.
+ * Replaces PointwiseConvLayer.forward/backward (layers/pointwise_convolution.py:46-75):
+ * the X[:, :, ::s, ::s] subsample (:48-49) is a strided gather, the NHWC transpose copy
+ * (:50) disappears, and the stride-s backward widen (:68-72) is fused into dgrad.
+ * Weights W[K][C] as in the reference.
+ * ------------------------------------------------------------------------------------- */
+int dk_pwconv_fwd_f32(const float* x, int N, int H, int W, int C, const float* w_kc, int K, int stride, const float* bias, float* y, int OH, int OW, void* stream);
+int dk_pwconv_dgrad_f32(const float* dy, int N, int OH, int OW, int K, const float* w_kc, int C, int stride, float* dx, void* stream);
+size_t dk_pwconv_wgrad_workspace_bytes(int N, int OH, int OW, int K, int C);
+int dk_pwconv_wgrad_f32(const float* dy, const float* x, int N, int H, int W, int C, int K, int stride, int OH, int OW, const float* w_kc, float l2, float* dw_kc, void* ws, size_t ws_bytes, void* stream);
+
+/* ---------------------------------------------------------------------------------------
+ * Depthwise convolution, direct (no MFMA).
+ * Replaces DepthwiseConvLayer.forward_cp (layers/depthwise_convolution.py:85-102, CUDA
+ * forward_conv :105-121) and backward_cp (:198-221, CUDA backward_conv :122-140).
+ * Weights W[C][R][S] as in the reference; dk_dw_weight_rsc_f32 makes the [R][S][C] copy
+ * the kernels read.  R x S in {1x1, 3x3, 5x5}.
+ * ------------------------------------------------------------------------------------- */
+int dk_dw_weight_rsc_f32(const float* w_crs, int C, int R, int S, float* w_rsc, void* stream);
+int dk_dwconv_fwd_f32(const float* x, int N, int H, int W, int C, const float* w_rsc, int R, int S, int stride, int pad, const float* bias, float* y, int OH, int OW, void* stream);
+int dk_dwconv_dgrad_f32(const float* dy, int N, int OH, int OW, int C, const float* w_rsc, int R, int S, int stride, int pad, float* dx, int H, int W, void* stream);
+size_t dk_dwconv_wgrad_workspace_bytes(int N, int OH, int OW, int C, int R, int S);
+int dk_dwconv_wgrad_f32(const float* dy, const float* x, int N, int H, int W, int C, int R, int S, int stride, int pad, int OH, int OW, const float* w_crs, float l2, float* dw_crs, void* ws, size_t ws_bytes, void* stream);
+
+/* ---------------------------------------------------------------------------------------
+ * Dense layer (layers/dense_layer.py:46-67; W stored (in, out) as the reference).
+ * ------------------------------------------------------------------------------------- */
+int dk_dense_fwd_f32(const float* x, int B, int IN, const float* w_io, int OUT, const float* bias, float* y, void* stream);
+int dk_dense_dgrad_f32(const float* dy, int B, int OUT, const float* w_io, int IN, float* dx, void* stream);
+size_t dk_dense_wgrad_workspace_bytes(int B, int IN, int OUT);
+int dk_dense_wgrad_f32(const float* x, const float* dy, int B, int IN, int OUT, const float* w_io, float l2, float* dw_io, void* ws, size_t ws_bytes, void* stream);
+
+/* ---------------------------------------------------------------------------------------
+ * Batch norm, training mode with batch statistics (layers/batch_norm.py:54-174).
+ * Forward: partial sums -> (optional SyncBN all-reduce of the collapsed [2][C] sums) ->
+ * finalize (mean, std, invstd, running mean/std as batch_norm.py:76-89) -> apply
+ * (gamma*x_hat + beta, optionally fused with the following ReLU, activations.py:37-42).
+ * Backward: partials of (sum dy, sum dy*x_hat) -> finalize (dgamma, dbeta from the local
+ * sums, the dx coefficients k12 = [k1[C], k2[C]] from the global sums) -> apply.
+ * Partial buffers are fp64 [nblk][2][C], nblk = dk_bn_partial_blocks(P, C).
+ * ------------------------------------------------------------------------------------- */
+int dk_bn_partial_blocks(int P, int C);
+size_t dk_bn_workspace_bytes(int P, int C);
+size_t dk_bn_bwd_workspace_bytes(int P, int C);
+int dk_bn_stats_partial_f64(const float* x, int P, int C, void* ws, size_t ws_bytes, void* stream);
+int dk_bn_collapse_f64(const void* part, int nblk, int C, void* out, void* stream);
+int dk_bn_stats_finalize_f32(const void* part, int nblk, int C, double count, float eps, float momentum, int first, float* mean, float* std_, float* invstd, float* run_mean, float* run_std, void* stream);
+int dk_bn_stats_f32(const float* x, int P, int C, float eps, float momentum, int first, float* mean, float* std_, float* invstd, float* run_mean, float* run_std, void* ws, size_t ws_bytes, void* stream);
+int dk_bn_infer_params_f32(const float* run_std, int C, float* invstd, void* stream);
+int dk_bn_apply_f32(const float* x, long long numel, int C, const float* mean, const float* invstd, const float* gamma, const float* beta, int relu, float* y, uint8_t* mask, void* stream);
+int dk_bn_bwd_partial_f64(const float* x, const float* dy, int P, int C, const float* mean, const float* invstd, const float* gamma, const float* beta, int relu, void* ws, size_t ws_bytes, void* stream);
+int dk_bn_bwd_finalize_f32(const void* part_local, int nblk_local, const void* part_global, int nblk_global, int C, double count, float* dgamma, float* dbeta, float* k12, void* stream);
+int dk_bn_bwd_apply_f32(const float* x, const float* dy, long long numel, int C, const float* mean, const float* invstd, const float* gamma, const float* beta, int relu, const float* k12, float* dx, void* stream);
+int dk_bn_bwd_f32(const float* x, const float* dy, int P, int C, const float* mean, const float* invstd, const float* gamma, const float* beta, int relu, float* dgamma, float* dbeta, float* dx, void* ws, size_t ws_bytes, void* stream);
+
+/* ---------------------------------------------------------------------------------------
+ * Activation, residual join, pooling head, loss.
+ *   ReLU: layers/activations.py:14-47 (mask is uint8 here, fp32 in the reference).
+ *   add (+ReLU): ResidualBlock.forward/backward joins (layers/residual_block.py:75, :94-97).
+ *   GAP: layers/pooling.py:23-36.   softmax + CE: layers/losses.py:13-34.
+ * ------------------------------------------------------------------------------------- */
+int dk_relu_fwd_f32(const float* x, long long n, float* y, uint8_t* mask, void* stream);
+int dk_relu_bwd_f32(const float* dy, const uint8_t* mask, long long n, float* dx, void* stream);
+int dk_mask_to_f32(const uint8_t* mask, long long n, float* out, void* stream);
+int dk_add_f32(const float* a, const float* b, long long n, int relu, float* y, uint8_t* mask, void* stream);
+int dk_gap_fwd_f32(const float* x, int N, int HW, int C, float* out, void* stream);
+int dk_gap_bwd_f32(const float* dy, int N, int HW, int C, float* dx, void* stream);
+int dk_softmax_xent_fwd_f32(const float* x, const float* y_onehot, int B, int K, float* p, float* loss, void* stream);
+int dk_softmax_xent_bwd_f32(const float* p, const float* y_onehot, int B, int K, float* dx, void* stream);
+
+/* ---------------------------------------------------------------------------------------
+ * Optimiser / regulariser / utilities.
+ *   SGD momentum over a table of tensors in ONE launch (optimisers/SGDMomentum.py:31-39;
+ *   the reference issues ~4 CuPy kernels per tensor).  Table entry (40 bytes):
+ *   { float* w; const float* g; float* v; int64 n; int64 first_block }, first_block =
+ *   sum of ceil(n/256) over the preceding entries; total_blocks = that sum over all.
+ *   l2 loss term: regularisers/l2.py:12-14; scale: l2.py:16-17 and DP averaging.
+ *   colsum: bias gradients, np.sum(upstream_dx, axis=(0,2,3)) (convolution.py:91-92 etc.).
+ * ------------------------------------------------------------------------------------- */
+int dk_sgd_momentum_multi_f32(const void* table, int ntens, long long total_blocks, float lr, float momentum, float grad_scale, void* stream);
+int dk_l2_loss_f32(const float* w, long long n, float strength, int accumulate, float* out, void* stream);
+int dk_scale_f32(const float* x, long long n, float s, float* y, void* stream);
+size_t dk_colsum_workspace_bytes(int M, int N);
+int dk_colsum_f32(const float* in, int M, int N, float* out, void* ws, size_t ws_bytes, void* stream);
+int dk_nchw_to_nhwc_f32(const float* x, int N, int C, int H, int W, int Cp, float* y, void* stream);
+int dk_nhwc_unpad_f32(const float* x, long long P, int Cp, int C, float* y, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* DORKNET_HIP_H */

@@ -1,0 +1,155 @@
+"""Whole training steps on the HIP path vs the oracle (fp64), plus full-size properties."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import net as O
+from tests._convert import all_layers, network_to_oracle, rel_err
+
+pytestmark = pytest.mark.gpu
+
+
+def dev(a):
+    return torch.as_tensor(np.ascontiguousarray(a, dtype=np.float32), device="cuda")
+
+
+def host(t):
+    return t.detach().float().cpu().numpy()
+
+
+def _compare_step(net, onet, X, onehot, lr, steps=2, tol=1e-4):
+    from dorknet_amd.optimisers.SGDMomentum import SGDMomentum
+    sgd = SGDMomentum(net, lr, 0.9)
+    osgd = O.OSGDMomentum(onet, lr, 0.9)
+    for step in range(steps):
+        loss, P = net.forward(dev(X), dev(onehot))
+        oloss, oP = onet.forward(X.astype(np.float64), onehot.astype(np.float64))
+        assert abs(float(loss) - oloss) <= tol * abs(oloss), (step, float(loss), oloss)
+        assert rel_err(host(P), oP) <= tol
+        net.backward()
+        onet.backward()
+        worst = []
+        for l, ol in zip(all_layers(net.layers), all_layers(onet.layers)):
+            for k in (ol.grads or {}):
+                worst.append((rel_err(host(l.grads[k]), ol.grads[k]), l.layer_name, k))
+        worst.sort(reverse=True)
+        assert worst[0][0] <= tol, worst[:5]
+        sgd.update_weights()
+        osgd.update_weights()
+    for l, ol in zip(all_layers(net.layers), all_layers(onet.layers)):
+        for k in (ol.learned_params or {}):
+            assert rel_err(host(l.learned_params[k]), ol.learned_params[k]) <= tol, (l.layer_name, k)
+        nlp = getattr(ol, "non_learned_params", None)
+        if nlp and nlp.get("running_mean") is not None:
+            assert rel_err(host(l.non_learned_params["running_std"]), nlp["running_std"]) <= tol
+
+
+def test_resnet18_depsep_training_steps():
+    """BASELINE config 3's model at batch 2: forward (loss, probabilities), every gradient
+    and the SGD-momentum update, two steps, vs the oracle."""
+    from examples.resnet18_depsep import ResNet18, synthetic_batch
+    np.random.seed(0)
+    net = ResNet18("r18")
+    onet = network_to_oracle(net)
+    net.to_gpu()
+    X, _, onehot = synthetic_batch(2, seed=1)
+    _compare_step(net, onet, X, onehot, lr=0.05 * 2 / 200.0)
+
+
+def test_mnist_training_steps():
+    """BASELINE config 1's model (MNISTNet, C=1 input, 4x4 stride-2 convs) on the GPU."""
+    from examples.mnist_convnet import MNISTNet
+    np.random.seed(1)
+    net = MNISTNet("mnist")
+    onet = network_to_oracle(net)
+    net.to_gpu()
+    rng = np.random.default_rng(2)
+    X = rng.uniform(0, 1, size=(8, 1, 28, 28)).astype(np.float32)
+    onehot = np.eye(10, dtype=np.float32)[rng.integers(0, 10, 8)]
+    _compare_step(net, onet, X, onehot, lr=0.01)
+
+
+def test_fused_and_unfused_paths_are_bitwise_equal(monkeypatch):
+    from examples.resnet18_depsep import ResNet18, synthetic_batch
+    X, _, onehot = synthetic_batch(2, seed=3)
+    outs = []
+    for fuse in ("1", "0"):
+        monkeypatch.setenv("DORKNET_FUSE", fuse)
+        np.random.seed(5)
+        net = ResNet18("r18")
+        net.to_gpu()
+        loss, P = net.forward(dev(X), dev(onehot))
+        net.backward()
+        outs.append((host(P), [host(l.grads[k]) for l in all_layers(net.layers) for k in (l.grads or {})]))
+    assert np.array_equal(outs[0][0], outs[1][0])
+    for a, b in zip(outs[0][1], outs[1][1]):
+        assert np.array_equal(a, b)
+
+
+def test_inference_and_terminal_layer():
+    from examples.resnet18_depsep import ResNet18, synthetic_batch
+    np.random.seed(6)
+    net = ResNet18("r18")
+    onet = network_to_oracle(net)
+    net.to_gpu()
+    X, _, onehot = synthetic_batch(2, seed=4)
+    net.forward(dev(X), dev(onehot))       # sets running statistics
+    onet.forward(X.astype(np.float64), onehot.astype(np.float64))
+    _, P = net.forward(dev(X), None, test_mode=True)
+    _, oP = onet.forward(X.astype(np.float64), None, test_mode=True)
+    assert rel_err(host(P), oP) <= 1e-4
+    loss, feat = net.forward(dev(X), None, test_mode=True, terminal_layer_name="res8")
+    assert tuple(feat.shape) == (2, 512, 7, 7) and loss == 0
+
+
+# ---------------------------------------------------------------------------------------
+# BASELINE config 2 at full size: 256 x 64 x 56 x 56, 3x3 conv, fwd + dgrad + wgrad
+# ---------------------------------------------------------------------------------------
+
+def test_config2_full_size_conv():
+    """Per-image outputs (forward, dgrad) are checked on two images of the full batch
+    against the oracle; the batch-reduced weight gradient against torch CPU conv2d autograd."""
+    from dorknet_amd.layers.convolution import ConvLayer
+    from oracle import ref
+    np.random.seed(0)
+    layer = ConvLayer("c", (64, 64, 3, 3), stride=1, padding=1, with_bias=False)
+    W = layer.learned_params["weights"].copy()
+    layer.to_gpu()
+    g = torch.Generator(device="cuda").manual_seed(0)
+    X = torch.randn(256, 64, 56, 56, device="cuda", generator=g)
+    dY = torch.randn(256, 64, 56, 56, device="cuda", generator=g)
+    Y = layer.forward(X)
+    dX = layer.backward(dY)
+    torch.cuda.synchronize()
+    idx = [0, 255]
+    Xs = host(X[idx]).astype(np.float64)
+    dYs = host(dY[idx]).astype(np.float64)
+    Yo, cache = ref.conv_forward(Xs, W.astype(np.float64), None, 1, 1)
+    dXo, _, _ = ref.conv_backward(dYs, W.astype(np.float64), cache, 1, 1, False)
+    assert rel_err(host(Y[idx]), Yo) <= 1e-4
+    assert rel_err(host(dX[idx]), dXo) <= 1e-4
+    Xc = X.cpu()
+    Wt = torch.from_numpy(W).requires_grad_(True)
+    out = torch.nn.functional.conv2d(Xc, Wt, padding=1)   # torch CPU as an independent checker
+    out.backward(dY.cpu())
+    assert rel_err(host(layer.grads["weights"]), Wt.grad.numpy()) <= 1e-4
+
+
+def test_batchnorm_full_size_statistics():
+    """conv0_bn's full shape (256 x 64 x 112 x 112): batch statistics and running buffers
+    vs fp64 torch reductions, output normalisation property."""
+    from dorknet_amd.layers.batch_norm import BatchNormLayer
+    layer = BatchNormLayer("bn", incoming_chans=64)
+    layer.to_gpu()
+    g = torch.Generator(device="cuda").manual_seed(1)
+    X = (5.0 + 3.0 * torch.randn(256, 64, 112, 112, device="cuda", generator=g)).contiguous(
+        memory_format=torch.channels_last)
+    Y = layer.forward(X)
+    Xd = X.double()
+    mean = Xd.mean(dim=(0, 2, 3))
+    std = torch.sqrt(Xd.var(dim=(0, 2, 3), unbiased=False) + 1e-5)
+    assert rel_err(host(layer.non_learned_params["running_mean"]).ravel(), mean.cpu().numpy()) <= 1e-6
+    assert rel_err(host(layer.std).ravel(), std.cpu().numpy()) <= 1e-6
+    Yd = Y.double()
+    assert float(Yd.mean(dim=(0, 2, 3)).abs().max()) < 1e-4
+    assert float((Yd.var(dim=(0, 2, 3), unbiased=False) - 1).abs().max()) < 1e-3
