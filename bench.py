@@ -1,0 +1,253 @@
+"""Benchmark: ResNet-18-depsep 225x225 training step (BASELINE config 3; config 4 with --gpus N).
+
+One step = forward (loss) + backward + SGD-momentum update of the whole network on one
+synthetic batch of 256 images per GPU (fp32), inputs resident in HBM before timing.
+Multi-GPU: one process per GPU (torchrun), data parallel over RCCL, per-rank batch fixed
+(weak scaling); gradients are averaged with bucketed all-reduces overlapped with backward.
+
+Prints ONE JSON line (rank 0).  Besides the driver's contract fields it carries
+  roofline      -- the dominant kernel (largest share of the step, measured with HIP events
+                   around every call of that C-ABI entry point during the timed region):
+                   algorithmic work per call / average call duration vs the MI355X peak;
+  cpu_baseline  -- the reference's CPU path restated (oracle/cpu_path.py: C/OpenMP versions
+                   of its Cython kernels + numpy BLAS), timed on this host at N=1 on a small
+                   sample of the same workload;
+  breakdown     -- per entry point: ms per step and roofline fraction (one instrumented step).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "images/sec training step, ResNet-18-depsep 225x225 bs=256, 1/2/4/8 MI355X"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=256, help="images per GPU")
+    ap.add_argument("--bn", choices=["local", "sync"], default="local")
+    ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--cpu-sample", type=int, default=16, help="images in the CPU-baseline sample (0 = skip)")
+    return ap.parse_args()
+
+
+class Instrument:
+    """Wraps C-ABI entry points so every call is bracketed by HIP events on the current
+    stream (the stream the kernels are launched on)."""
+
+    def __init__(self, names):
+        from dorknet_amd._hip import lib
+        self.lib = lib
+        self.names = list(names)
+        self.calls = {n: [] for n in self.names}
+        self.orig = {}
+
+    def __enter__(self):
+        import torch
+        for n in self.names:
+            orig = getattr(self.lib, n)
+            self.orig[n] = orig
+            calls = self.calls[n]
+
+            def wrapped(*args, _orig=orig, _calls=calls):
+                e0 = torch.cuda.Event(enable_timing=True)
+                e1 = torch.cuda.Event(enable_timing=True)
+                e0.record()
+                r = _orig(*args)
+                e1.record()
+                _calls.append((e0, e1, args))
+                return r
+            setattr(self.lib, n, wrapped)
+        return self
+
+    def __exit__(self, *exc):
+        for n, f in self.orig.items():
+            setattr(self.lib, n, f)
+
+    def summary(self):
+        import torch
+        from dorknet_amd import perfmodel
+        torch.cuda.synchronize()
+        out = {}
+        for n, calls in self.calls.items():
+            if not calls:
+                continue
+            ms = [a.elapsed_time(b) for a, b, _ in calls]
+            fl, by = 0, 0
+            bound = 0.0
+            for _, _, args in calls:
+                f, b = perfmodel.work(n, args)
+                fl += f
+                by += b
+                bound += perfmodel.bound_time_s(f, b)
+            out[n] = dict(calls=len(calls), ms=sum(ms), flops=fl, bytes=by, bound_ms=1e3 * bound)
+        return out
+
+
+def roofline_entry(name, s, steps):
+    from dorknet_amd import perfmodel
+    t = s["ms"] / 1e3 / s["calls"]
+    flops = s["flops"] / s["calls"]
+    nbytes = s["bytes"] / s["calls"]
+    mfma = flops / (perfmodel.PEAK_F32_TFLOPS * 1e12) > nbytes / (perfmodel.PEAK_HBM_GBS * 1e9)
+    if mfma:
+        achieved, peak, unit = flops / t / 1e12, perfmodel.PEAK_F32_TFLOPS, "TFLOP/s"
+    else:
+        achieved, peak, unit = nbytes / t / 1e9, perfmodel.PEAK_HBM_GBS, "GB/s"
+    return {"kernel": name, "bound": "mfma" if mfma else "hbm", "achieved": round(achieved, 2), "peak": peak,
+            "unit": unit, "frac": round(achieved / peak, 4), "traffic": None,
+            "calls_per_step": s["calls"] // max(steps, 1), "avg_call_us": round(1e6 * t, 2),
+            "algorithmic_per_call": {"flops": int(flops), "bytes": int(nbytes)}}
+
+
+def cpu_baseline(batch):
+    """Reference CPU path (restated) on `batch` images: 1 warm-up + 1 timed step."""
+    import numpy as np
+    try:
+        cores = min(16, len(os.sched_getaffinity(0)))
+    except AttributeError:
+        cores = min(16, os.cpu_count() or 1)
+    os.environ.setdefault("OMP_NUM_THREADS", str(cores))
+    cores = int(os.environ["OMP_NUM_THREADS"])
+    from threadpoolctl import threadpool_limits
+    from oracle import models
+    from oracle.net import OSGDMomentum
+    from examples.resnet18_depsep import synthetic_batch
+    with threadpool_limits(limits=cores):
+        net = models.resnet18_depsep(backend="cy", rng=np.random.RandomState(0))
+        sgd = OSGDMomentum(net, 0.05 * batch / 200.0, 0.9)
+        X, _, onehot = synthetic_batch(batch, seed=0)
+        net.forward(X, onehot)
+        net.backward()
+        sgd.update_weights()
+        t0 = time.perf_counter()
+        net.forward(X, onehot)
+        net.backward()
+        sgd.update_weights()
+        dt = time.perf_counter() - t0
+    return {"value": round(batch / dt, 3), "unit": "images/s", "cores": cores, "kind": "port",
+            "sample": "{} images x 1 training step (fwd+bwd+SGD) of ResNet-18-depsep 225x225 fp32 on the "
+                      "reference CPU path restated (C/OpenMP Cython kernels + numpy BLAS), {:.1f} s".format(batch, dt)}
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit("--gpus {} but WORLD_SIZE={} (launch N>1 with torch.distributed.run)".format(args.gpus, world))
+    torch.cuda.set_device(local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    from examples.resnet18_depsep import ResNet18, synthetic_batch
+    from dorknet_amd._tensor import as_device
+    from dorknet_amd.optimisers.SGDMomentum import SGDMomentum
+    from dorknet_amd import perfmodel
+
+    np.random.seed(0)  # identical initial weights on every rank
+    net = ResNet18("DogsImageNet225ResNet18DepSep")
+    net.to_gpu()
+    dp = None
+    if world > 1:
+        from dorknet_amd.parallel import DataParallel
+        dp = DataParallel(net, batch_norm=args.bn)
+    sgd = SGDMomentum(net, 0.05 * args.batch / 200.0, 0.9)
+    X, _, onehot = synthetic_batch(args.batch, seed=1000 + rank)
+    X, onehot = as_device(X), as_device(onehot)
+
+    def step():
+        net.forward(X, onehot)
+        if dp is None:
+            net.backward()
+        else:
+            dp.backward()
+        sgd.update_weights()
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        step()
+    barrier()
+
+    breakdown, dominant = None, None
+    if not args.no_roofline:
+        with Instrument(perfmodel.MODEL.keys()) as ins:
+            step()
+        summ = ins.summary()
+        dominant = max(summ, key=lambda n: summ[n]["ms"])
+        tot = sum(s["ms"] for s in summ.values())
+        breakdown = {n: {"ms": round(s["ms"], 3), "calls": s["calls"],
+                         "frac_of_roofline": round(s["bound_ms"] / s["ms"], 3) if s["ms"] else None}
+                     for n, s in sorted(summ.items(), key=lambda kv: -kv[1]["ms"])}
+        step_bound = sum(s["bound_ms"] for s in summ.values())
+        breakdown["_total_instrumented_ms"] = round(tot, 3)
+        breakdown["_step_roofline_bound_ms"] = round(step_bound, 3)
+        barrier()
+
+    ins = Instrument([dominant]) if dominant else None
+    barrier()
+    t0 = time.perf_counter()
+    if ins:
+        ins.__enter__()
+    try:
+        for _ in range(args.steps):
+            step()
+        barrier()
+    finally:
+        if ins:
+            ins.__exit__(None, None, None)
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    roof = None
+    if ins:
+        s = ins.summary()[dominant]
+        roof = roofline_entry(dominant, s, args.steps)
+    value = world * args.batch * args.steps / elapsed
+    ms_per_step = 1e3 * elapsed / args.steps
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_sample > 0:
+        cpu = cpu_baseline(args.cpu_sample)
+    if rank == 0:
+        out = {"metric": METRIC, "value": round(value, 2), "unit": "images/s", "n_gpus": world,
+               "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
+               "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+               "data": "synthetic (X ~ U[-128,128) 3x225x225, random one-hot labels over 120 classes; "
+                       "random-init weights, seed 0)",
+               "config": {"workload": "ResNet-18-depsep 225x225 training step (fwd+loss+bwd+SGD-momentum), "
+                                      "BASELINE config {}".format(3 if world == 1 else 4),
+                          "global_batch": world * args.batch, "per_gpu_batch": args.batch,
+                          "parallelism": "dp{}".format(world), "batch_norm": args.bn if world > 1 else "local"},
+               "roofline": roof, "cpu_baseline": cpu}
+        if breakdown is not None:
+            out["breakdown"] = breakdown
+            if breakdown["_total_instrumented_ms"]:
+                out["step_roofline_frac"] = round(breakdown["_step_roofline_bound_ms"] / ms_per_step, 4)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,154 @@
+"""Algorithmic work (flops, compulsory HBM bytes) per C-ABI call, for roofline reporting.
+
+Formulas follow SURVEY.md 8(d): a conv/pw pass moves its input, output and weights once
+(e = 4 bytes, fp32) and does 2*N*K*OH*OW*C*R*S flops; depthwise 2*N*C*OH*OW*R*S flops;
+BN forward apply reads + writes each element, the BN reduce passes read it once; etc.
+Only the *compulsory* bytes count (a stride-s pointwise layer reads N*OH*OW*C input
+values, not N*H*W*C), so `achieved` is never inflated by bytes the algorithm does not need.
+
+Each entry maps the positional arguments of the C function (include/dorknet_hip.h) to
+(flops, bytes).  Unlisted entry points are treated as (0, 0).
+"""
+from __future__ import annotations
+
+E = 4  # fp32
+
+PEAK_F32_TFLOPS = 157.3   # MI355X fp32 MFMA / vector, dense (MI355X_MICROARCH.md)
+PEAK_HBM_GBS = 8000.0     # MI355X HBM3E spec
+
+
+def _conv_fwd(x, N, H, W, C, w, K, R, S, stride, pad, bias, y, OH, OW, st):
+    return 2 * N * OH * OW * K * C * R * S, E * (N * H * W * C + N * OH * OW * K + K * R * S * C)
+
+
+def _conv_dgrad(dy, N, OH, OW, K, w, C, R, S, pad, dx, H, W, st):
+    return 2 * N * OH * OW * K * C * R * S, E * (N * OH * OW * K + N * H * W * C + K * R * S * C)
+
+
+def _conv_dgrad_strided(dy, N, OH, OW, K, w, C, R, S, stride, pad, dx, H, W, ws, nb, st):
+    return 2 * N * OH * OW * K * C * R * S, E * (N * OH * OW * K + N * H * W * C + K * R * S * C)
+
+
+def _conv_wgrad(dy, x, N, H, W, Cp, C, K, R, S, stride, pad, OH, OW, w, l2, dw, ws, nb, st):
+    return 2 * N * OH * OW * K * C * R * S, E * (N * OH * OW * K + N * H * W * C + K * R * S * C)
+
+
+def _pw_fwd(x, N, H, W, C, w, K, stride, bias, y, OH, OW, st):
+    return 2 * N * OH * OW * K * C, E * (N * OH * OW * C + N * OH * OW * K + K * C)
+
+
+def _pw_dgrad(dy, N, OH, OW, K, w, C, stride, dx, st):
+    return 2 * N * OH * OW * K * C, E * (N * OH * OW * K + N * OH * OW * stride * stride * C + K * C)
+
+
+def _pw_wgrad(dy, x, N, H, W, C, K, stride, OH, OW, w, l2, dw, ws, nb, st):
+    return 2 * N * OH * OW * K * C, E * (N * OH * OW * K + N * OH * OW * C + K * C)
+
+
+def _dw_fwd(x, N, H, W, C, w, R, S, stride, pad, bias, y, OH, OW, st):
+    return 2 * N * C * OH * OW * R * S, E * (N * H * W * C + N * OH * OW * C + C * R * S)
+
+
+def _dw_dgrad(dy, N, OH, OW, C, w, R, S, stride, pad, dx, H, W, st):
+    return 2 * N * C * OH * OW * R * S, E * (N * OH * OW * C + N * H * W * C + C * R * S)
+
+
+def _dw_wgrad(dy, x, N, H, W, C, R, S, stride, pad, OH, OW, w, l2, dw, ws, nb, st):
+    return 2 * N * C * OH * OW * R * S, E * (N * OH * OW * C + N * H * W * C + C * R * S)
+
+
+def _dense_fwd(x, B, IN, w, OUT, bias, y, st):
+    return 2 * B * IN * OUT, E * (B * IN + B * OUT + IN * OUT)
+
+
+def _dense_dgrad(dy, B, OUT, w, IN, dx, st):
+    return 2 * B * IN * OUT, E * (B * IN + B * OUT + IN * OUT)
+
+
+def _dense_wgrad(x, dy, B, IN, OUT, w, l2, dw, ws, nb, st):
+    return 2 * B * IN * OUT, E * (B * IN + B * OUT + IN * OUT)
+
+
+def _bn_stats(x, P, C, *rest):
+    return 3 * P * C, E * P * C
+
+
+def _bn_apply(x, numel, C, *rest):
+    return 4 * numel, E * 2 * numel
+
+
+def _bn_bwd(x, dy, P, C, *rest):
+    return 12 * P * C, E * 5 * P * C   # reduce pass reads x, dy; apply pass reads x, dy, writes dx
+
+
+def _relu_fwd(x, n, y, mask, st):
+    return n, E * 2 * n + (n if mask else 0)
+
+
+def _relu_bwd(dy, mask, n, dx, st):
+    return n, E * 2 * n + n
+
+
+def _add(a, b, n, relu, y, mask, st):
+    return n, E * 3 * n + (n if mask else 0)
+
+
+def _gap_fwd(x, N, HW, C, out, st):
+    return N * HW * C, E * (N * HW * C + N * C)
+
+
+def _gap_bwd(dy, N, HW, C, dx, st):
+    return N * HW * C, E * (N * HW * C + N * C)
+
+
+def _sgd(table, ntens, total_blocks, *rest):
+    n = total_blocks * 256
+    return 4 * n, 5 * E * n
+
+
+def _colsum(x, M, N, *rest):
+    return M * N, E * M * N
+
+
+def _nchw_to_nhwc(x, N, C, H, W, Cp, y, st):
+    return 0, E * (N * C * H * W + N * Cp * H * W)
+
+
+MODEL = {
+    "dk_conv2d_fwd_f32": _conv_fwd,
+    "dk_conv2d_dgrad_f32": _conv_dgrad,
+    "dk_conv2d_dgrad_strided_f32": _conv_dgrad_strided,
+    "dk_conv2d_wgrad_f32": _conv_wgrad,
+    "dk_pwconv_fwd_f32": _pw_fwd,
+    "dk_pwconv_dgrad_f32": _pw_dgrad,
+    "dk_pwconv_wgrad_f32": _pw_wgrad,
+    "dk_dwconv_fwd_f32": _dw_fwd,
+    "dk_dwconv_dgrad_f32": _dw_dgrad,
+    "dk_dwconv_wgrad_f32": _dw_wgrad,
+    "dk_dense_fwd_f32": _dense_fwd,
+    "dk_dense_dgrad_f32": _dense_dgrad,
+    "dk_dense_wgrad_f32": _dense_wgrad,
+    "dk_bn_stats_f32": _bn_stats,
+    "dk_bn_apply_f32": _bn_apply,
+    "dk_bn_bwd_f32": _bn_bwd,
+    "dk_relu_fwd_f32": _relu_fwd,
+    "dk_relu_bwd_f32": _relu_bwd,
+    "dk_add_f32": _add,
+    "dk_gap_fwd_f32": _gap_fwd,
+    "dk_gap_bwd_f32": _gap_bwd,
+    "dk_sgd_momentum_multi_f32": _sgd,
+    "dk_colsum_f32": _colsum,
+    "dk_nchw_to_nhwc_f32": _nchw_to_nhwc,
+}
+
+
+def work(name: str, args) -> tuple[int, int]:
+    f = MODEL.get(name)
+    if f is None:
+        return 0, 0
+    return f(*args)
+
+
+def bound_time_s(flops: float, nbytes: float) -> float:
+    """Roofline lower bound on time for one call: max(flops / peak, bytes / BW)."""
+    return max(flops / (PEAK_F32_TFLOPS * 1e12), nbytes / (PEAK_HBM_GBS * 1e9))

@@ -1,0 +1,22 @@
+#!/bin/bash
+# One GPU-box session: parity tests, a 1-GPU bench line, a rocprofv3 kernel-stats profile.
+# Usage (from the repo root, via gpurun): bash scripts/gpu_session.sh [tag]
+# Each GPU step has its own time limit; a crash / timeout (rc > 1) ends the session.
+set -u
+TAG=${1:-r01}
+ROOT=$(pwd)
+OUT=$ROOT/gpurun_out
+mkdir -p "$OUT"
+step() { echo "== $1 rc=$2"; if [ "$2" -gt 1 ]; then echo "stopping after rc=$2"; exit "$2"; fi; }
+
+timeout -k 10 900 python -m pytest tests -m gpu -q -p no:cacheprovider > "$OUT/tests_$TAG.log" 2>&1
+rc=$?; tail -15 "$OUT/tests_$TAG.log"; step tests $rc
+
+timeout -k 10 600 python bench.py --steps 10 --warmup 3 > "$OUT/bench_$TAG.json" 2> "$OUT/bench_$TAG.err"
+rc=$?; cat "$OUT/bench_$TAG.json"; tail -5 "$OUT/bench_$TAG.err"; step bench $rc
+
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$TAG" -o bench -- \
+    python "$ROOT/bench.py" --steps 5 --warmup 2 --cpu-sample 0 > "$OUT/prof_bench_$TAG.json" 2> "$OUT/prof_$TAG.err"
+rc=$?; step rocprof $rc
+find "$OUT/prof_$TAG" -name "*kernel_stats.csv" | head -3

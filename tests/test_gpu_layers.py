@@ -23,28 +23,37 @@ def host(t):
     return t.detach().float().cpu().numpy()
 
 
-def check(name, got, want, tol=TOL):
+def check(name, got, want, tol=TOL, want32=None):
+    """||got - want|| <= max(tol * ||want||, 10 * ||want32 - want||): within 1e-4 of the
+    fp64 restatement, or (for quantities that are ~0 in exact arithmetic, e.g. the shift
+    gradient of a BN followed by another BN) no worse than 10x the reference's own fp32
+    pipeline error."""
     got = host(got) if isinstance(got, torch.Tensor) else np.asarray(got)
-    want = np.asarray(want)
+    want = np.asarray(want, dtype=np.float64)
     assert got.shape == want.shape, f"{name}: shape {got.shape} != {want.shape}"
-    e = rel_err(got, want)
-    assert e <= tol, f"{name}: normwise rel err {e:.3e} > {tol:.0e}"
+    err = np.linalg.norm((got.astype(np.float64) - want).ravel())
+    bound = tol * np.linalg.norm(want.ravel())
+    if want32 is not None:
+        bound = max(bound, 10 * np.linalg.norm((np.asarray(want32, dtype=np.float64) - want).ravel()))
+    assert err <= bound or err == 0, f"{name}: err {err:.3e} > bound {bound:.3e} (rel {rel_err(got, want):.3e})"
 
 
 def run_layer(layer, X, dY=None, rng=None, test_mode=False):
-    """Forward (+ backward) through a dorknet_amd layer and its oracle twin (fp64)."""
+    """Forward (+ backward) through a dorknet_amd layer and its oracle twins (fp64 and the
+    reference-faithful fp32)."""
     olayer = layer_to_oracle(layer)  # before to_gpu: same numpy weights
+    o32 = layer_to_oracle(layer, np.float32)
     layer.to_gpu()
     Y = layer.forward(dev(X), test_mode=test_mode)
     Yo = olayer.forward(X.astype(np.float64), test_mode)
-    check(f"{layer.layer_name} forward", Y, Yo)
+    check(f"{layer.layer_name} forward", Y, Yo, want32=o32.forward(X, test_mode))
     if dY is None:
         return layer, olayer
     dX = layer.backward(dev(dY))
     dXo = olayer.backward(dY.astype(np.float64))
-    check(f"{layer.layer_name} dX", dX, dXo)
+    check(f"{layer.layer_name} dX", dX, dXo, want32=o32.backward(dY))
     for k in olayer.grads:
-        check(f"{layer.layer_name} d{k}", layer.grads[k], olayer.grads[k])
+        check(f"{layer.layer_name} d{k}", layer.grads[k], olayer.grads[k], want32=o32.grads[k])
     return layer, olayer
 
 
@@ -238,18 +247,19 @@ def test_residual_block_and_sgd():
     block = shell.layers[0]
     assert isinstance(block, ResidualBlock)
     oblock = layer_to_oracle(block)
+    o32 = layer_to_oracle(block, np.float32)
     net = FeedForwardNetwork("n")
     net.add_layer(block)
     net.to_gpu()
     rng = np.random.RandomState(13)
     X = rng.randn(2, 16, 10, 10).astype(np.float32)
     dY = rng.randn(2, 32, 5, 5).astype(np.float32)
-    check("resblock fwd", block.forward(dev(X)), oblock.forward(X.astype(np.float64)))
-    check("resblock dX", block.backward(dev(dY)), oblock.backward(dY.astype(np.float64)))
+    check("resblock fwd", block.forward(dev(X)), oblock.forward(X.astype(np.float64)), want32=o32.forward(X))
+    check("resblock dX", block.backward(dev(dY)), oblock.backward(dY.astype(np.float64)), want32=o32.backward(dY))
     from tests._convert import all_layers
-    for l, ol in zip(all_layers([block]), all_layers([oblock])):
+    for l, ol, o3 in zip(all_layers([block]), all_layers([oblock]), all_layers([o32])):
         for k in (ol.grads or {}):
-            check(f"{l.layer_name} d{k}", l.grads[k], ol.grads[k])
+            check(f"{l.layer_name} d{k}", l.grads[k], ol.grads[k], want32=o3.grads[k])
     sgd = SGDMomentum(net, 0.1, 0.9)
     osgd = O.OSGDMomentum(O.ONetwork([oblock], None), 0.1, 0.9)
     for _ in range(2):
