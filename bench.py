@@ -36,7 +36,8 @@ def parse():
     ap.add_argument("--batch", type=int, default=256, help="images per GPU")
     ap.add_argument("--bn", choices=["local", "sync"], default="local")
     ap.add_argument("--no-roofline", action="store_true")
-    ap.add_argument("--cpu-sample", type=int, default=16, help="images in the CPU-baseline sample (0 = skip)")
+    ap.add_argument("--cpu-sample", type=int, default=64, help="images in the CPU-baseline sample (0 = skip)")
+    ap.add_argument("--cpu-steps", type=int, default=3, help="timed CPU-baseline steps (after one warm-up)")
     return ap.parse_args()
 
 
@@ -109,8 +110,8 @@ def roofline_entry(name, s, steps):
             "algorithmic_per_call": {"flops": int(flops), "bytes": int(nbytes)}}
 
 
-def cpu_baseline(batch):
-    """Reference CPU path (restated) on `batch` images: 1 warm-up + 1 timed step."""
+def cpu_baseline(batch, steps=3):
+    """Reference CPU path (restated) on `batch` images: 1 warm-up + `steps` timed steps."""
     import numpy as np
     try:
         cores = min(16, len(os.sched_getaffinity(0)))
@@ -130,13 +131,15 @@ def cpu_baseline(batch):
         net.backward()
         sgd.update_weights()
         t0 = time.perf_counter()
-        net.forward(X, onehot)
-        net.backward()
-        sgd.update_weights()
+        for _ in range(steps):
+            net.forward(X, onehot)
+            net.backward()
+            sgd.update_weights()
         dt = time.perf_counter() - t0
-    return {"value": round(batch / dt, 3), "unit": "images/s", "cores": cores, "kind": "port",
-            "sample": "{} images x 1 training step (fwd+bwd+SGD) of ResNet-18-depsep 225x225 fp32 on the "
-                      "reference CPU path restated (C/OpenMP Cython kernels + numpy BLAS), {:.1f} s".format(batch, dt)}
+    return {"value": round(steps * batch / dt, 3), "unit": "images/s", "cores": cores, "kind": "port",
+            "sample": "{} timed training steps (fwd+bwd+SGD, after 1 warm-up) on a {}-image batch of "
+                      "ResNet-18-depsep 225x225 fp32, reference CPU path restated (C/OpenMP versions of its "
+                      "Cython kernels + numpy BLAS), {:.1f} s".format(steps, batch, dt)}
 
 
 def main():
@@ -228,7 +231,7 @@ def main():
     ms_per_step = 1e3 * elapsed / args.steps
     cpu = None
     if rank == 0 and world == 1 and args.cpu_sample > 0:
-        cpu = cpu_baseline(args.cpu_sample)
+        cpu = cpu_baseline(args.cpu_sample, args.cpu_steps)
     if rank == 0:
         out = {"metric": METRIC, "value": round(value, 2), "unit": "images/s", "n_gpus": world,
                "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),

@@ -8,10 +8,13 @@
 //   * nothing but X and the per-channel (mean, std) is kept for backward: X_demean and
 //     X_hat are recomputed on the fly (batch_norm.py:72-73 stores both);
 //   * the optional ReLU that follows BN (activations.py:37-42) is fused into the
-//     apply pass, and its backward mask is recomputed from X in the backward reduce;
+//     apply pass, and its backward mask is recomputed from X in the backward passes;
 //   * backward is one reduce pass (sum dy, sum dy*x_hat) and one apply pass.
 //
-// Per-channel parameter vectors (mean, std, invstd, gamma, beta, ...) are fp32 [C].
+// Layout of the streaming kernels ("row loop"): a block owns a contiguous range of
+// rows (pixels); thread (cg, pl) owns channel group cg (V = 4 channels, one float4) and
+// walks rows pl, pl + PL, ... with four rows of loads in flight.  Per-channel
+// parameters live in registers, so there is no per-element index arithmetic.
 #include "dk_common.h"
 
 namespace dk {
@@ -23,36 +26,80 @@ __device__ __forceinline__ float bn_out(float x, float mean, float invstd, float
   return gamma * xh + beta;
 }
 
-// Stats partials.  Thread (cg, pl) owns channel group cg (V channels) and pixel lane pl.
-// part[blk][0][c] = sum x, part[blk][1][c] = sum x^2 (fp64).
+template <int V>
+struct VecT;
+template <>
+struct VecT<4> {
+  using T = f32x4;
+  __device__ static T load(const float* p) { return ld4(p); }
+  __device__ static void store(float* p, T v) { st4(p, v); }
+};
+template <>
+struct VecT<1> {
+  using T = float;
+  __device__ static T load(const float* p) { return *p; }
+  __device__ static void store(float* p, T v) { *p = v; }
+};
+
+__device__ __forceinline__ float el(const f32x4& v, int e) { return v[e]; }
+__device__ __forceinline__ float el(const float& v, int) { return v; }
+__device__ __forceinline__ void set_el(f32x4& v, int e, float x) { v[e] = x; }
+__device__ __forceinline__ void set_el(float& v, int, float x) { v = x; }
+
+// Geometry of the row loop, shared by host and device.
+struct RowGeom {
+  int CG;   // channel groups = C / V
+  int cgt;  // channel groups per block (<= 256)
+  int PL;   // pixel lanes = 256 / cgt
+};
+
+__host__ __device__ inline RowGeom row_geom(int C, int V) {
+  RowGeom g;
+  g.CG = C / V;
+  g.cgt = g.CG < 256 ? g.CG : 256;
+  g.PL = 256 / g.cgt;
+  return g;
+}
+
+// ---------------------------------------------------------------------------------------
+// forward statistics: part[blk][0][c] = sum x, part[blk][1][c] = sum x^2 (fp64)
+// ---------------------------------------------------------------------------------------
 template <int V>
 __global__ __launch_bounds__(256) void bn_stats_partial_kernel(const float* __restrict__ x, int P, int C, int ppb,
                                                                double* __restrict__ part) {
+  using VT = VecT<V>;
   __shared__ double red[2][256][V];
-  const int CG = C / V;
-  const int cgt = CG < 256 ? CG : 256;
-  const int PL = 256 / cgt;
+  const RowGeom g = row_geom(C, V);
   const int tid = threadIdx.x;
-  const int cg = blockIdx.y * cgt + tid % cgt;
-  const int pl = tid / cgt;
-  const bool active = pl < PL && cg < CG;
+  const int cg = blockIdx.y * g.cgt + tid % g.cgt;
+  const int pl = tid / g.cgt;
+  const bool active = pl < g.PL && cg < g.CG;
   const int p0 = blockIdx.x * ppb, p1 = min(P, p0 + ppb);
   double s[V], q[V];
 #pragma unroll
   for (int e = 0; e < V; ++e) s[e] = q[e] = 0.0;
   if (active) {
-    for (int p = p0 + pl; p < p1; p += PL) {
-      const float* src = x + (size_t)p * C + cg * V;
-      float v[V];
-      if constexpr (V == 4) {
-        const f32x4 t = ld4(src);
-        v[0] = t[0]; v[1] = t[1]; v[2] = t[2]; v[3] = t[3];
-      } else {
-        v[0] = src[0];
-      }
+    const float* base = x + cg * V;
+    const int PL = g.PL;
+    int p = p0 + pl;
+    for (; p + 3 * PL < p1; p += 4 * PL) {
+      typename VT::T v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = VT::load(base + (size_t)(p + u * PL) * C);
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int e = 0; e < V; ++e) {
+          const double d = (double)el(v[u], e);
+          s[e] += d;
+          q[e] += d * d;
+        }
+    }
+    for (; p < p1; p += PL) {
+      const typename VT::T v = VT::load(base + (size_t)p * C);
 #pragma unroll
       for (int e = 0; e < V; ++e) {
-        const double d = (double)v[e];
+        const double d = (double)el(v, e);
         s[e] += d;
         q[e] += d * d;
       }
@@ -64,32 +111,55 @@ __global__ __launch_bounds__(256) void bn_stats_partial_kernel(const float* __re
     red[1][tid][e] = q[e];
   }
   __syncthreads();
-  const int items = 2 * cgt * V;
+  const int items = 2 * g.cgt * V;
   for (int it = tid; it < items; it += 256) {
     const int e = it % V;
-    const int g = (it / V) % cgt;
-    const int which = it / (V * cgt);
-    const int cgg = blockIdx.y * cgt + g;
-    if (cgg >= CG) continue;
+    const int gg = (it / V) % g.cgt;
+    const int which = it / (V * g.cgt);
+    const int cgg = blockIdx.y * g.cgt + gg;
+    if (cgg >= g.CG) continue;
     double acc = 0.0;
-    for (int qq = 0; qq < PL; ++qq) acc += red[which][qq * cgt + g][e];
+    for (int qq = 0; qq < g.PL; ++qq) acc += red[which][qq * g.cgt + gg][e];
     part[((size_t)blockIdx.x * 2 + which) * C + cgg * V + e] = acc;
   }
 }
 
-// Finalize: mean, population var, std = sqrt(var + eps); running mean/std update
-// (batch_norm.py:76-89: first call copies, later calls blend with `momentum`).
-__global__ void bn_stats_finalize_kernel(const double* __restrict__ part, int nblk, int C, double count, float eps,
-                                         float momentum, int first, float* __restrict__ mean_out,
-                                         float* __restrict__ std_out, float* __restrict__ invstd_out,
-                                         float* __restrict__ run_mean, float* __restrict__ run_std) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
+// Fixed-order block sum of part[b][which][c] over b (one block per channel).
+__device__ __forceinline__ void block_sum2(const double* __restrict__ part, int nblk, int C, int c, double* out_s,
+                                           double* out_q) {
+  __shared__ double rs[256], rq[256];
   double s = 0.0, q = 0.0;
-  for (int b = 0; b < nblk; ++b) {
+  for (int b = threadIdx.x; b < nblk; b += 256) {
     s += part[((size_t)b * 2 + 0) * C + c];
     q += part[((size_t)b * 2 + 1) * C + c];
   }
+  rs[threadIdx.x] = s;
+  rq[threadIdx.x] = q;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o) {
+      rs[threadIdx.x] += rs[threadIdx.x + o];
+      rq[threadIdx.x] += rq[threadIdx.x + o];
+    }
+    __syncthreads();
+  }
+  *out_s = rs[0];
+  *out_q = rq[0];
+}
+
+// Finalize (one block per channel): mean, population var, std = sqrt(var + eps);
+// running mean/std update (batch_norm.py:76-89: first call copies, later calls blend).
+__global__ __launch_bounds__(256) void bn_stats_finalize_kernel(const double* __restrict__ part, int nblk, int C,
+                                                                double count, float eps, float momentum, int first,
+                                                                float* __restrict__ mean_out,
+                                                                float* __restrict__ std_out,
+                                                                float* __restrict__ invstd_out,
+                                                                float* __restrict__ run_mean,
+                                                                float* __restrict__ run_std) {
+  const int c = blockIdx.x;
+  double s, q;
+  block_sum2(part, nblk, C, c, &s, &q);
+  if (threadIdx.x != 0) return;
   const double mean = s / count;
   double var = q / count - mean * mean;
   if (var < 0.0) var = 0.0;
@@ -109,32 +179,81 @@ __global__ void bn_stats_finalize_kernel(const double* __restrict__ part, int nb
   }
 }
 
-// y = gamma * (x - mean) * invstd + beta, optionally ReLU'd (mask = y > 0 as uint8).
+// out[w][c] = sum_b part[b][w][c] (one block per channel) -- the per-rank vector SyncBN all-reduces.
+__global__ __launch_bounds__(256) void bn_collapse_kernel(const double* __restrict__ part, int nblk, int C,
+                                                          double* __restrict__ out) {
+  const int c = blockIdx.x;
+  double s, q;
+  block_sum2(part, nblk, C, c, &s, &q);
+  if (threadIdx.x == 0) {
+    out[c] = s;
+    out[C + c] = q;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// forward apply: y = gamma * (x - mean) * invstd + beta  [+ ReLU, optional uint8 mask]
+// ---------------------------------------------------------------------------------------
 template <int V>
-__global__ __launch_bounds__(256) void bn_apply_kernel(const float* __restrict__ x, long long nvec, int C,
+__global__ __launch_bounds__(256) void bn_apply_kernel(const float* __restrict__ x, int P, int C, int ppb,
                                                        const float* __restrict__ mean,
                                                        const float* __restrict__ invstd,
                                                        const float* __restrict__ gamma,
                                                        const float* __restrict__ beta, int relu,
                                                        float* __restrict__ y, uint8_t* __restrict__ mask) {
-  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= nvec) return;
-  const int c0 = (int)((i * V) % C);
+  using VT = VecT<V>;
+  const RowGeom g = row_geom(C, V);
+  const int tid = threadIdx.x;
+  const int cg = blockIdx.y * g.cgt + tid % g.cgt;
+  const int pl = tid / g.cgt;
+  if (pl >= g.PL || cg >= g.CG) return;
+  const int c0 = cg * V;
+  float mu[V], is[V], ga[V], be[V];
 #pragma unroll
   for (int e = 0; e < V; ++e) {
-    const int c = c0 + e;
-    float o = bn_out(x[i * V + e], mean[c], invstd[c], gamma[c], beta[c]);
-    if (relu) {
-      const bool pos = o > 0.f;
-      o = pos ? o : 0.f;
-      if (mask) mask[i * V + e] = pos;
-    }
-    y[i * V + e] = o;
+    mu[e] = mean[c0 + e];
+    is[e] = invstd[c0 + e];
+    ga[e] = gamma[c0 + e];
+    be[e] = beta[c0 + e];
   }
+  const int p0 = blockIdx.x * ppb, p1 = min(P, p0 + ppb);
+  const int PL = g.PL;
+  auto one = [&](typename VT::T v, size_t off) {
+    typename VT::T o;
+    uint32_t mbits = 0;
+#pragma unroll
+    for (int e = 0; e < V; ++e) {
+      float r = bn_out(el(v, e), mu[e], is[e], ga[e], be[e]);
+      if (relu) {
+        const bool pos = r > 0.f;
+        r = pos ? r : 0.f;
+        mbits |= (uint32_t)pos << (8 * e);
+      }
+      set_el(o, e, r);
+    }
+    VT::store(y + off, o);
+    if (mask) {
+      if constexpr (V == 4)
+        *reinterpret_cast<uint32_t*>(mask + off) = mbits;
+      else
+        mask[off] = (uint8_t)mbits;
+    }
+  };
+  int p = p0 + pl;
+  for (; p + 3 * PL < p1; p += 4 * PL) {
+    typename VT::T v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = VT::load(x + (size_t)(p + u * PL) * C + c0);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) one(v[u], (size_t)(p + u * PL) * C + c0);
+  }
+  for (; p < p1; p += PL) one(VT::load(x + (size_t)p * C + c0), (size_t)p * C + c0);
 }
 
-// Backward reduce partials: sum dy_e and sum dy_e * x_hat, where dy_e = dy, or with
-// relu: dy * (bn_out(x) > 0) -- the fused ReLU backward (activations.py:44-47).
+// ---------------------------------------------------------------------------------------
+// backward reduce: sum dy_e and sum dy_e * x_hat, where dy_e = dy, or with relu:
+// dy * (bn_out(x) > 0) -- the fused ReLU backward (activations.py:44-47).
+// ---------------------------------------------------------------------------------------
 template <int V>
 __global__ __launch_bounds__(256) void bn_bwd_partial_kernel(const float* __restrict__ x,
                                                              const float* __restrict__ dy, int P, int C, int ppb,
@@ -143,38 +262,53 @@ __global__ __launch_bounds__(256) void bn_bwd_partial_kernel(const float* __rest
                                                              const float* __restrict__ gamma,
                                                              const float* __restrict__ beta, int relu,
                                                              double* __restrict__ part) {
+  using VT = VecT<V>;
   __shared__ double red[2][256][V];
-  const int CG = C / V;
-  const int cgt = CG < 256 ? CG : 256;
-  const int PL = 256 / cgt;
+  const RowGeom g = row_geom(C, V);
   const int tid = threadIdx.x;
-  const int cg = blockIdx.y * cgt + tid % cgt;
-  const int pl = tid / cgt;
-  const bool active = pl < PL && cg < CG;
+  const int cg = blockIdx.y * g.cgt + tid % g.cgt;
+  const int pl = tid / g.cgt;
+  const bool active = pl < g.PL && cg < g.CG;
   const int p0 = blockIdx.x * ppb, p1 = min(P, p0 + ppb);
   double s[V], q[V];
   float mu[V], is[V], ga[V], be[V];
+  const int c0 = active ? cg * V : 0;
 #pragma unroll
   for (int e = 0; e < V; ++e) {
     s[e] = q[e] = 0.0;
-    const int c = active ? cg * V + e : 0;
-    mu[e] = mean[c];
-    is[e] = invstd[c];
-    ga[e] = gamma[c];
-    be[e] = beta[c];
+    mu[e] = mean[c0 + e];
+    is[e] = invstd[c0 + e];
+    ga[e] = gamma[c0 + e];
+    be[e] = beta[c0 + e];
   }
-  if (active) {
-    for (int p = p0 + pl; p < p1; p += PL) {
-      const size_t off = (size_t)p * C + cg * V;
+  auto acc = [&](typename VT::T xv, typename VT::T gv) {
 #pragma unroll
-      for (int e = 0; e < V; ++e) {
-        const float xv = x[off + e];
-        float g = dy[off + e];
-        const float xh = (xv - mu[e]) * is[e];
-        if (relu && !(bn_out(xv, mu[e], is[e], ga[e], be[e]) > 0.f)) g = 0.f;
-        s[e] += (double)g;
-        q[e] += (double)g * (double)xh;
+    for (int e = 0; e < V; ++e) {
+      const float xe = el(xv, e);
+      float ge = el(gv, e);
+      const float xh = (xe - mu[e]) * is[e];
+      if (relu && !(bn_out(xe, mu[e], is[e], ga[e], be[e]) > 0.f)) ge = 0.f;
+      s[e] += (double)ge;
+      q[e] += (double)ge * (double)xh;
+    }
+  };
+  if (active) {
+    const int PL = g.PL;
+    int p = p0 + pl;
+    for (; p + 3 * PL < p1; p += 4 * PL) {
+      typename VT::T xv[4], gv[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const size_t off = (size_t)(p + u * PL) * C + c0;
+        xv[u] = VT::load(x + off);
+        gv[u] = VT::load(dy + off);
       }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) acc(xv[u], gv[u]);
+    }
+    for (; p < p1; p += PL) {
+      const size_t off = (size_t)p * C + c0;
+      acc(VT::load(x + off), VT::load(dy + off));
     }
   }
 #pragma unroll
@@ -183,76 +317,99 @@ __global__ __launch_bounds__(256) void bn_bwd_partial_kernel(const float* __rest
     red[1][tid][e] = q[e];
   }
   __syncthreads();
-  const int items = 2 * cgt * V;
+  const int items = 2 * g.cgt * V;
   for (int it = tid; it < items; it += 256) {
     const int e = it % V;
-    const int g = (it / V) % cgt;
-    const int which = it / (V * cgt);
-    const int cgg = blockIdx.y * cgt + g;
-    if (cgg >= CG) continue;
-    double acc = 0.0;
-    for (int qq = 0; qq < PL; ++qq) acc += red[which][qq * cgt + g][e];
-    part[((size_t)blockIdx.x * 2 + which) * C + cgg * V + e] = acc;
+    const int gg = (it / V) % g.cgt;
+    const int which = it / (V * g.cgt);
+    const int cgg = blockIdx.y * g.cgt + gg;
+    if (cgg >= g.CG) continue;
+    double a = 0.0;
+    for (int qq = 0; qq < g.PL; ++qq) a += red[which][qq * g.cgt + gg][e];
+    part[((size_t)blockIdx.x * 2 + which) * C + cgg * V + e] = a;
   }
 }
 
 // dgamma = sum dy_e * x_hat, dbeta = sum dy_e (batch_norm.py:159-174) from the *local*
 // partials; k1 = mean(dy_e), k2 = sum(dy_e * x_hat) / count from the (possibly
 // all-reduced, SyncBN) *global* partials.  Without SyncBN both are the same buffer.
-__global__ void bn_bwd_finalize_kernel(const double* __restrict__ part_l, int nblk_l,
-                                       const double* __restrict__ part_g, int nblk_g, int C, double count,
-                                       float* __restrict__ dgamma, float* __restrict__ dbeta,
-                                       float* __restrict__ k12) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  double s = 0.0, q = 0.0;
-  for (int b = 0; b < nblk_l; ++b) {
-    s += part_l[((size_t)b * 2 + 0) * C + c];
-    q += part_l[((size_t)b * 2 + 1) * C + c];
+__global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const double* __restrict__ part_l, int nblk_l,
+                                                              const double* __restrict__ part_g, int nblk_g, int C,
+                                                              double count, float* __restrict__ dgamma,
+                                                              float* __restrict__ dbeta, float* __restrict__ k12) {
+  const int c = blockIdx.x;
+  double s, q;
+  block_sum2(part_l, nblk_l, C, c, &s, &q);
+  if (threadIdx.x == 0) {
+    dgamma[c] = (float)q;
+    dbeta[c] = (float)s;
   }
-  dgamma[c] = (float)q;
-  dbeta[c] = (float)s;
   if (part_g != part_l || nblk_g != nblk_l) {
-    s = q = 0.0;
-    for (int b = 0; b < nblk_g; ++b) {
-      s += part_g[((size_t)b * 2 + 0) * C + c];
-      q += part_g[((size_t)b * 2 + 1) * C + c];
-    }
+    __syncthreads();
+    block_sum2(part_g, nblk_g, C, c, &s, &q);
   }
-  k12[c] = (float)(s / count);
-  k12[C + c] = (float)(q / count);
-}
-
-// out[w][c] = sum_b part[b][w][c]   (fixed order) -- the per-rank vector SyncBN all-reduces
-__global__ void bn_collapse_kernel(const double* __restrict__ part, int nblk, int C, double* __restrict__ out) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= 2 * C) return;
-  double s = 0.0;
-  for (int b = 0; b < nblk; ++b) s += part[(size_t)b * 2 * C + i];
-  out[i] = s;
+  if (threadIdx.x == 0) {
+    k12[c] = (float)(s / count);
+    k12[C + c] = (float)(q / count);
+  }
 }
 
 // dx = gamma * invstd * (dy_e - k1 - x_hat * k2)   (batch_norm.py:125-156, rearranged:
 // (1/M) * X_demean / std^2 * sum(dy * X_demean) == x_hat * sum(dy * x_hat) / M)
 template <int V>
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const float* __restrict__ x, const float* __restrict__ dy,
-                                                           long long nvec, int C, const float* __restrict__ mean,
+                                                           int P, int C, int ppb, const float* __restrict__ mean,
                                                            const float* __restrict__ invstd,
                                                            const float* __restrict__ gamma,
                                                            const float* __restrict__ beta, int relu,
                                                            const float* __restrict__ k12, float* __restrict__ dx) {
-  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= nvec) return;
-  const int c0 = (int)((i * V) % C);
+  using VT = VecT<V>;
+  const RowGeom g = row_geom(C, V);
+  const int tid = threadIdx.x;
+  const int cg = blockIdx.y * g.cgt + tid % g.cgt;
+  const int pl = tid / g.cgt;
+  if (pl >= g.PL || cg >= g.CG) return;
+  const int c0 = cg * V;
+  float mu[V], is[V], ga[V], be[V], k1[V], k2[V], f[V];
 #pragma unroll
   for (int e = 0; e < V; ++e) {
-    const int c = c0 + e;
-    const float xv = x[i * V + e];
-    float g = dy[i * V + e];
-    const float mu = mean[c], is = invstd[c], ga = gamma[c];
-    if (relu && !(bn_out(xv, mu, is, ga, beta[c]) > 0.f)) g = 0.f;
-    const float xh = (xv - mu) * is;
-    dx[i * V + e] = (ga * is) * (g - k12[c] - xh * k12[C + c]);
+    mu[e] = mean[c0 + e];
+    is[e] = invstd[c0 + e];
+    ga[e] = gamma[c0 + e];
+    be[e] = beta[c0 + e];
+    k1[e] = k12[c0 + e];
+    k2[e] = k12[C + c0 + e];
+    f[e] = ga[e] * is[e];
+  }
+  auto one = [&](typename VT::T xv, typename VT::T gv, size_t off) {
+    typename VT::T o;
+#pragma unroll
+    for (int e = 0; e < V; ++e) {
+      const float xe = el(xv, e);
+      float ge = el(gv, e);
+      if (relu && !(bn_out(xe, mu[e], is[e], ga[e], be[e]) > 0.f)) ge = 0.f;
+      const float xh = (xe - mu[e]) * is[e];
+      set_el(o, e, f[e] * (ge - k1[e] - xh * k2[e]));
+    }
+    VT::store(dx + off, o);
+  };
+  const int p0 = blockIdx.x * ppb, p1 = min(P, p0 + ppb);
+  const int PL = g.PL;
+  int p = p0 + pl;
+  for (; p + 3 * PL < p1; p += 4 * PL) {
+    typename VT::T xv[4], gv[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const size_t off = (size_t)(p + u * PL) * C + c0;
+      xv[u] = VT::load(x + off);
+      gv[u] = VT::load(dy + off);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) one(xv[u], gv[u], (size_t)(p + u * PL) * C + c0);
+  }
+  for (; p < p1; p += PL) {
+    const size_t off = (size_t)p * C + c0;
+    one(VT::load(x + off), VT::load(dy + off), off);
   }
 }
 
@@ -263,14 +420,26 @@ __global__ void bn_infer_params_kernel(const float* __restrict__ run_std, int C,
   if (c < C) invstd[c] = 1.0f / run_std[c];
 }
 
+// Blocks for the reduce passes: ~32 row iterations per pixel lane, <= 1024 partials.
 static int bn_blocks(int P, int C) {
-  // ~64 rows per pixel lane keeps fp64 accumulation short and gives >= 4 blocks per CU.
-  int nblk = cdiv(P, 1024);
+  const int V = (C % 4 == 0) ? 4 : 1;
+  const RowGeom g = row_geom(C, V);
+  int nblk = cdiv(P, g.PL * 32);
   if (nblk > 1024) nblk = 1024;
   if (nblk < 1) nblk = 1;
-  (void)C;
   return nblk;
 }
+
+// Blocks for the streaming apply passes (no partials to keep small): up to 4096.
+static int bn_apply_blocks(int P, int C, int V) {
+  const RowGeom g = row_geom(C, V);
+  int nblk = cdiv(P, g.PL * 16);
+  if (nblk > 4096) nblk = 4096;
+  if (nblk < 1) nblk = 1;
+  return nblk;
+}
+
+static inline bool vec_ok(const void* p, int C) { return (C % 4 == 0) && ((reinterpret_cast<uintptr_t>(p) & 15) == 0); }
 
 }  // namespace dk
 
@@ -280,22 +449,15 @@ DK_API int dk_bn_partial_blocks(int P, int C) { return bn_blocks(P, C); }
 
 DK_API size_t dk_bn_workspace_bytes(int P, int C) { return (size_t)bn_blocks(P, C) * 2 * C * sizeof(double); }
 
-static int bn_grid(const float* x, int C, int nblk, dim3* grid) {
-  const bool vec = (C % 4 == 0) && ((reinterpret_cast<uintptr_t>(x) & 15) == 0);
-  const int V = vec ? 4 : 1;
-  const int CG = C / V;
-  const int cgt = CG < 256 ? CG : 256;
-  *grid = dim3(nblk, cdiv(CG, cgt));
-  return vec;
-}
-
 // Stage 1 of forward statistics: part[nblk][2][C] (fp64 sum x, sum x^2) over x[P][C].
 DK_API int dk_bn_stats_partial_f64(const float* x, int P, int C, void* ws, size_t ws_bytes, void* stream) {
   if (ws_bytes < dk_bn_workspace_bytes(P, C)) return DK_ERR_WORKSPACE;
   const int nblk = bn_blocks(P, C);
   const int ppb = cdiv(P, nblk);
-  dim3 grid;
-  if (bn_grid(x, C, nblk, &grid))
+  const bool vec = vec_ok(x, C);
+  const RowGeom g = row_geom(C, vec ? 4 : 1);
+  const dim3 grid(nblk, cdiv(g.CG, g.cgt));
+  if (vec)
     hipLaunchKernelGGL(bn_stats_partial_kernel<4>, grid, dim3(256), 0, as_stream(stream), x, P, C, ppb,
                        static_cast<double*>(ws));
   else
@@ -306,8 +468,8 @@ DK_API int dk_bn_stats_partial_f64(const float* x, int P, int C, void* ws, size_
 
 // out[2][C] = fixed-order sum of part[nblk][2][C].
 DK_API int dk_bn_collapse_f64(const void* part, int nblk, int C, void* out, void* stream) {
-  hipLaunchKernelGGL(bn_collapse_kernel, dim3(cdiv(2 * C, 256)), dim3(256), 0, as_stream(stream),
-                     static_cast<const double*>(part), nblk, C, static_cast<double*>(out));
+  hipLaunchKernelGGL(bn_collapse_kernel, dim3(C), dim3(256), 0, as_stream(stream), static_cast<const double*>(part),
+                     nblk, C, static_cast<double*>(out));
   return launch_status();
 }
 
@@ -315,7 +477,7 @@ DK_API int dk_bn_collapse_f64(const void* part, int nblk, int C, void* out, void
 DK_API int dk_bn_stats_finalize_f32(const void* part, int nblk, int C, double count, float eps, float momentum,
                                     int first, float* mean, float* std_, float* invstd, float* run_mean,
                                     float* run_std, void* stream) {
-  hipLaunchKernelGGL(bn_stats_finalize_kernel, dim3(cdiv(C, 256)), dim3(256), 0, as_stream(stream),
+  hipLaunchKernelGGL(bn_stats_finalize_kernel, dim3(C), dim3(256), 0, as_stream(stream),
                      static_cast<const double*>(part), nblk, C, count, eps, momentum, first, mean, std_, invstd,
                      run_mean, run_std);
   return launch_status();
@@ -339,15 +501,19 @@ DK_API int dk_bn_infer_params_f32(const float* run_std, int C, float* invstd, vo
 // y = gamma * (x - mean) * invstd + beta  [+ ReLU; mask (uint8) may be null]
 DK_API int dk_bn_apply_f32(const float* x, long long numel, int C, const float* mean, const float* invstd,
                            const float* gamma, const float* beta, int relu, float* y, uint8_t* mask, void* stream) {
-  const bool vec = (C % 4 == 0) && (numel % 4 == 0);
-  if (vec) {
-    const long long nvec = numel / 4;
-    hipLaunchKernelGGL(bn_apply_kernel<4>, dim3((unsigned)cdivll(nvec, 256)), dim3(256), 0, as_stream(stream), x,
-                       nvec, C, mean, invstd, gamma, beta, relu, y, mask);
-  } else {
-    hipLaunchKernelGGL(bn_apply_kernel<1>, dim3((unsigned)cdivll(numel, 256)), dim3(256), 0, as_stream(stream), x,
-                       numel, C, mean, invstd, gamma, beta, relu, y, mask);
-  }
+  const int P = (int)(numel / C);
+  const bool vec = vec_ok(x, C) && vec_ok(y, C);
+  const int V = vec ? 4 : 1;
+  const RowGeom g = row_geom(C, V);
+  const int nblk = bn_apply_blocks(P, C, V);
+  const dim3 grid(nblk, cdiv(g.CG, g.cgt));
+  const int ppb = cdiv(P, nblk);
+  if (vec)
+    hipLaunchKernelGGL(bn_apply_kernel<4>, grid, dim3(256), 0, as_stream(stream), x, P, C, ppb, mean, invstd, gamma,
+                       beta, relu, y, mask);
+  else
+    hipLaunchKernelGGL(bn_apply_kernel<1>, grid, dim3(256), 0, as_stream(stream), x, P, C, ppb, mean, invstd, gamma,
+                       beta, relu, y, mask);
   return launch_status();
 }
 
@@ -359,8 +525,10 @@ DK_API int dk_bn_bwd_partial_f64(const float* x, const float* dy, int P, int C, 
   if (ws_bytes < dk_bn_workspace_bytes(P, C)) return DK_ERR_WORKSPACE;
   const int nblk = bn_blocks(P, C);
   const int ppb = cdiv(P, nblk);
-  dim3 grid;
-  if (bn_grid(x, C, nblk, &grid))
+  const bool vec = vec_ok(x, C) && vec_ok(dy, C);
+  const RowGeom g = row_geom(C, vec ? 4 : 1);
+  const dim3 grid(nblk, cdiv(g.CG, g.cgt));
+  if (vec)
     hipLaunchKernelGGL(bn_bwd_partial_kernel<4>, grid, dim3(256), 0, as_stream(stream), x, dy, P, C, ppb, mean,
                        invstd, gamma, beta, relu, static_cast<double*>(ws));
   else
@@ -372,7 +540,7 @@ DK_API int dk_bn_bwd_partial_f64(const float* x, const float* dy, int P, int C, 
 // Backward stage 2: dgamma/dbeta from the local partials, k12 = [k1[C], k2[C]] from the global ones.
 DK_API int dk_bn_bwd_finalize_f32(const void* part_local, int nblk_local, const void* part_global, int nblk_global,
                                   int C, double count, float* dgamma, float* dbeta, float* k12, void* stream) {
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(cdiv(C, 256)), dim3(256), 0, as_stream(stream),
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C), dim3(256), 0, as_stream(stream),
                      static_cast<const double*>(part_local), nblk_local, static_cast<const double*>(part_global),
                      nblk_global, C, count, dgamma, dbeta, k12);
   return launch_status();
@@ -382,15 +550,19 @@ DK_API int dk_bn_bwd_finalize_f32(const void* part_local, int nblk_local, const 
 DK_API int dk_bn_bwd_apply_f32(const float* x, const float* dy, long long numel, int C, const float* mean,
                                const float* invstd, const float* gamma, const float* beta, int relu,
                                const float* k12, float* dx, void* stream) {
-  const bool vec = (C % 4 == 0) && (numel % 4 == 0);
-  if (vec) {
-    const long long nvec = numel / 4;
-    hipLaunchKernelGGL(bn_bwd_apply_kernel<4>, dim3((unsigned)cdivll(nvec, 256)), dim3(256), 0, as_stream(stream), x,
-                       dy, nvec, C, mean, invstd, gamma, beta, relu, k12, dx);
-  } else {
-    hipLaunchKernelGGL(bn_bwd_apply_kernel<1>, dim3((unsigned)cdivll(numel, 256)), dim3(256), 0, as_stream(stream),
-                       x, dy, numel, C, mean, invstd, gamma, beta, relu, k12, dx);
-  }
+  const int P = (int)(numel / C);
+  const bool vec = vec_ok(x, C) && vec_ok(dy, C) && vec_ok(dx, C);
+  const int V = vec ? 4 : 1;
+  const RowGeom g = row_geom(C, V);
+  const int nblk = bn_apply_blocks(P, C, V);
+  const dim3 grid(nblk, cdiv(g.CG, g.cgt));
+  const int ppb = cdiv(P, nblk);
+  if (vec)
+    hipLaunchKernelGGL(bn_bwd_apply_kernel<4>, grid, dim3(256), 0, as_stream(stream), x, dy, P, C, ppb, mean, invstd,
+                       gamma, beta, relu, k12, dx);
+  else
+    hipLaunchKernelGGL(bn_bwd_apply_kernel<1>, grid, dim3(256), 0, as_stream(stream), x, dy, P, C, ppb, mean, invstd,
+                       gamma, beta, relu, k12, dx);
   return launch_status();
 }
 

@@ -48,4 +48,9 @@ __device__ __forceinline__ double wave_sum(double v) {
 // "bad call" from "device fault".
 enum : int { DK_ERR_ARGS = 10001, DK_ERR_WORKSPACE = 10002 };
 
+// Split-K second stage (reduce.hip): out = sum_s ws[s][M][N] (+ l2 * w), fixed order.
+//   mode 0: out[m][n];  mode 1: columns (r, s, c) with c padded to Cp -> out KCRS.
+int splitk_reduce(const float* ws, int splits, int M, int N, float* out, const float* w, float l2, int mode, int C,
+                  int Cp, int R, int S, hipStream_t st);
+
 }  // namespace dk

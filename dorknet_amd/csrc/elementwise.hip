@@ -10,21 +10,44 @@
 
 namespace dk {
 
-__global__ void relu_fwd_kernel(const float* __restrict__ x, long long n, float* __restrict__ y,
-                                uint8_t* __restrict__ mask) {
-  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const float v = x[i];
-  const bool pos = v > 0.f;
-  y[i] = pos ? v : 0.f;
-  if (mask) mask[i] = pos;
+// Vectorised elementwise kernels: each thread handles float4 chunks (grid-stride), the
+// uint8 masks as one 32-bit word per chunk; a scalar tail handles n % 4.
+__global__ __launch_bounds__(256) void relu_fwd_kernel(const float* __restrict__ x, long long n, float* __restrict__ y,
+                                                       uint8_t* __restrict__ mask, int vec) {
+  const long long nv = vec ? (n >> 2) : 0;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += stride) {
+    f32x4 v = ld4(x + 4 * i);
+    uint32_t m = 0;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const bool pos = v[e] > 0.f;
+      v[e] = pos ? v[e] : 0.f;
+      m |= (uint32_t)pos << (8 * e);
+    }
+    st4(y + 4 * i, v);
+    if (mask) reinterpret_cast<uint32_t*>(mask)[i] = m;
+  }
+  for (long long i = 4 * nv + (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const bool pos = x[i] > 0.f;
+    y[i] = pos ? x[i] : 0.f;
+    if (mask) mask[i] = pos;
+  }
 }
 
-__global__ void relu_bwd_kernel(const float* __restrict__ dy, const uint8_t* __restrict__ mask, long long n,
-                                float* __restrict__ dx) {
-  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  dx[i] = mask[i] ? dy[i] : 0.f;
+__global__ __launch_bounds__(256) void relu_bwd_kernel(const float* __restrict__ dy, const uint8_t* __restrict__ mask,
+                                                       long long n, float* __restrict__ dx, int vec) {
+  const long long nv = vec ? (n >> 2) : 0;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += stride) {
+    f32x4 g = ld4(dy + 4 * i);
+    const uint32_t m = reinterpret_cast<const uint32_t*>(mask)[i];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) g[e] = ((m >> (8 * e)) & 0xff) ? g[e] : 0.f;
+    st4(dx + 4 * i, g);
+  }
+  for (long long i = 4 * nv + (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+    dx[i] = mask[i] ? dy[i] : 0.f;
 }
 
 __global__ void mask_to_f32_kernel(const uint8_t* __restrict__ mask, long long n, float* __restrict__ out) {
@@ -33,17 +56,34 @@ __global__ void mask_to_f32_kernel(const uint8_t* __restrict__ mask, long long n
 }
 
 // y = a + b, optionally ReLU'd with mask.
-__global__ void add_kernel(const float* __restrict__ a, const float* __restrict__ b, long long n, int relu,
-                           float* __restrict__ y, uint8_t* __restrict__ mask) {
-  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  float v = a[i] + b[i];
-  if (relu) {
-    const bool pos = v > 0.f;
-    v = pos ? v : 0.f;
-    if (mask) mask[i] = pos;
+__global__ __launch_bounds__(256) void add_kernel(const float* __restrict__ a, const float* __restrict__ b,
+                                                  long long n, int relu, float* __restrict__ y,
+                                                  uint8_t* __restrict__ mask, int vec) {
+  const long long nv = vec ? (n >> 2) : 0;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += stride) {
+    f32x4 v = ld4(a + 4 * i) + ld4(b + 4 * i);
+    if (relu) {
+      uint32_t m = 0;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const bool pos = v[e] > 0.f;
+        v[e] = pos ? v[e] : 0.f;
+        m |= (uint32_t)pos << (8 * e);
+      }
+      if (mask) reinterpret_cast<uint32_t*>(mask)[i] = m;
+    }
+    st4(y + 4 * i, v);
   }
-  y[i] = v;
+  for (long long i = 4 * nv + (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    float v = a[i] + b[i];
+    if (relu) {
+      const bool pos = v > 0.f;
+      v = pos ? v : 0.f;
+      if (mask) mask[i] = pos;
+    }
+    y[i] = v;
+  }
 }
 
 // out[n][c] = mean_{hw} x[n][hw][c]
@@ -156,6 +196,60 @@ __global__ __launch_bounds__(256) void l2_loss_kernel(const float* __restrict__ 
   }
 }
 
+// Multi-tensor l2 loss term, stage 1: block b (owning a 2048-element chunk of tensor t)
+// writes part[b] = 0.5 * strength_t * sum(w^2) over its chunk (fp64).
+struct L2Entry {
+  const float* w;
+  long long n;
+  long long block0;
+  float strength;
+  float pad_;
+};
+
+constexpr int kL2Chunk = 2048;
+
+__global__ __launch_bounds__(256) void l2_multi_partial_kernel(const L2Entry* __restrict__ tab, int ntens,
+                                                               double* __restrict__ part) {
+  __shared__ double red[256];
+  int t = 0;
+  const long long b = blockIdx.x;
+  while (t + 1 < ntens && tab[t + 1].block0 <= b) ++t;
+  const L2Entry e = tab[t];
+  const long long i0 = (b - e.block0) * kL2Chunk;
+  double s = 0.0;
+#pragma unroll
+  for (int k = 0; k < kL2Chunk / 256; ++k) {
+    const long long i = i0 + k * 256 + threadIdx.x;
+    if (i < e.n) {
+      const double v = e.w[i];
+      s += v * v;
+    }
+  }
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) part[b] = 0.5 * (double)e.strength * red[0];
+}
+
+// Stage 2 (one block): out[0] = (add_to ? add_to[0] : 0) + sum_b part[b], fixed order.
+__global__ __launch_bounds__(256) void l2_multi_final_kernel(const double* __restrict__ part, long long nparts,
+                                                             const float* __restrict__ add_to,
+                                                             float* __restrict__ out) {
+  __shared__ double red[256];
+  double s = 0.0;
+  for (long long i = threadIdx.x; i < nparts; i += 256) s += part[i];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[0] = (float)((add_to ? (double)add_to[0] : 0.0) + red[0]);
+}
+
 // Column sums of an [M][N] matrix, stage 1: ws[chunk][n] = sum of rows in the chunk.
 __global__ void colsum_partial_kernel(const float* __restrict__ in, int M, int N, int rpc, double* __restrict__ ws) {
   const int n = blockIdx.x * blockDim.x + threadIdx.x;
@@ -198,9 +292,13 @@ __global__ void nhwc_unpad_kernel(const float* __restrict__ x, long long P, int 
   y[i] = x[p * Cp + c];
 }
 
-__global__ void scale_kernel(const float* __restrict__ x, long long n, float s, float* __restrict__ y) {
-  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) y[i] = s * x[i];
+__global__ __launch_bounds__(256) void scale_kernel(const float* __restrict__ x, long long n, float s,
+                                                    float* __restrict__ y, int vec) {
+  const long long nv = vec ? (n >> 2) : 0;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += stride)
+    st4(y + 4 * i, s * ld4(x + 4 * i));
+  for (long long i = 4 * nv + (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) y[i] = s * x[i];
 }
 
 static int colsum_chunks(int M) {
@@ -210,19 +308,32 @@ static int colsum_chunks(int M) {
   return chunks;
 }
 
+static inline bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+static inline bool al4(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 3) == 0; }
+
 static inline dim3 grid1(long long n) { return dim3((unsigned)cdivll(n, 256)); }
+
+// Grid for the float4 grid-stride kernels: one float4 per thread, capped at 16k blocks.
+static inline dim3 grid4(long long n) {
+  long long b = cdivll((n + 3) / 4, 256);
+  if (b > 16384) b = 16384;
+  if (b < 1) b = 1;
+  return dim3((unsigned)b);
+}
 
 }  // namespace dk
 
 using namespace dk;
 
 DK_API int dk_relu_fwd_f32(const float* x, long long n, float* y, uint8_t* mask, void* stream) {
-  hipLaunchKernelGGL(relu_fwd_kernel, grid1(n), dim3(256), 0, as_stream(stream), x, n, y, mask);
+  hipLaunchKernelGGL(relu_fwd_kernel, grid4(n), dim3(256), 0, as_stream(stream), x, n, y, mask,
+                     (int)(al16(x) && al16(y) && al4(mask)));
   return launch_status();
 }
 
 DK_API int dk_relu_bwd_f32(const float* dy, const uint8_t* mask, long long n, float* dx, void* stream) {
-  hipLaunchKernelGGL(relu_bwd_kernel, grid1(n), dim3(256), 0, as_stream(stream), dy, mask, n, dx);
+  hipLaunchKernelGGL(relu_bwd_kernel, grid4(n), dim3(256), 0, as_stream(stream), dy, mask, n, dx,
+                     (int)(al16(dy) && al16(dx) && al4(mask)));
   return launch_status();
 }
 
@@ -232,7 +343,8 @@ DK_API int dk_mask_to_f32(const uint8_t* mask, long long n, float* out, void* st
 }
 
 DK_API int dk_add_f32(const float* a, const float* b, long long n, int relu, float* y, uint8_t* mask, void* stream) {
-  hipLaunchKernelGGL(add_kernel, grid1(n), dim3(256), 0, as_stream(stream), a, b, n, relu, y, mask);
+  hipLaunchKernelGGL(add_kernel, grid4(n), dim3(256), 0, as_stream(stream), a, b, n, relu, y, mask,
+                     (int)(al16(a) && al16(b) && al16(y) && al4(mask)));
   return launch_status();
 }
 
@@ -273,6 +385,25 @@ DK_API int dk_l2_loss_f32(const float* w, long long n, float strength, int accum
   return launch_status();
 }
 
+// All l2 loss terms of a network in two launches.  table: ntens L2Entry records (32 bytes:
+// { const float* w; int64 n; int64 first_block; float strength; float pad }), first_block =
+// sum of ceil(n / 2048) over the preceding entries, total_blocks = that sum over all.
+// out[0] = add_to[0] (may be null) + sum_t 0.5 * strength_t * sum(w_t^2).
+DK_API size_t dk_l2_multi_workspace_bytes(long long total_blocks) { return (size_t)total_blocks * sizeof(double); }
+
+DK_API int dk_l2_loss_multi_f32(const void* table, int ntens, long long total_blocks, const float* add_to,
+                                float* out, void* ws, size_t ws_bytes, void* stream) {
+  if (ntens <= 0 || total_blocks <= 0) return DK_ERR_ARGS;
+  if (ws_bytes < dk_l2_multi_workspace_bytes(total_blocks)) return DK_ERR_WORKSPACE;
+  hipLaunchKernelGGL(l2_multi_partial_kernel, dim3((unsigned)total_blocks), dim3(256), 0, as_stream(stream),
+                     static_cast<const L2Entry*>(table), ntens, static_cast<double*>(ws));
+  int rc = launch_status();
+  if (rc) return rc;
+  hipLaunchKernelGGL(l2_multi_final_kernel, dim3(1), dim3(256), 0, as_stream(stream), static_cast<const double*>(ws),
+                     total_blocks, add_to, out);
+  return launch_status();
+}
+
 DK_API size_t dk_colsum_workspace_bytes(int M, int N) { return (size_t)colsum_chunks(M) * N * sizeof(double); }
 
 DK_API int dk_colsum_f32(const float* in, int M, int N, float* out, void* ws, size_t ws_bytes, void* stream) {
@@ -301,7 +432,7 @@ DK_API int dk_nhwc_unpad_f32(const float* x, long long P, int Cp, int C, float* 
 
 // y = s * x (l2 backward, regularisers/l2.py:16-17; gradient averaging in data parallel)
 DK_API int dk_scale_f32(const float* x, long long n, float s, float* y, void* stream) {
-  hipLaunchKernelGGL(scale_kernel, grid1(n), dim3(256), 0, as_stream(stream), x, n, s, y);
+  hipLaunchKernelGGL(scale_kernel, grid4(n), dim3(256), 0, as_stream(stream), x, n, s, y, (int)(al16(x) && al16(y)));
   return launch_status();
 }
 

@@ -455,40 +455,9 @@ static size_t splitk_ws_bytes(int M, int N, int Kred) {
   return (size_t)wgrad_splits(M, N, Kred, BM, BN) * (size_t)M * (size_t)N * sizeof(float);
 }
 
-// Second stage of split-K: fixed-order sum over the partial slabs (fp64 accumulate),
-// + l2 * W (regularisers/l2.py:16-17 folded in, as convolution.py:99-100 does),
-// and a scatter into the caller's weight layout.
-//   mode 0: out[m][n]
-//   mode 1: columns are (r, s, c) with c padded to Cp; out is KCRS (convolution.py weight layout)
-__global__ void splitk_reduce_kernel(const float* __restrict__ ws, int splits, int M, int N, float* __restrict__ out,
-                                     const float* __restrict__ w, float l2, int mode, int C, int Cp, int R, int S) {
-  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= M * N) return;
-  const int m = idx / N, n = idx - m * N;
-  double acc = 0.0;
-  for (int s = 0; s < splits; ++s) acc += (double)ws[(size_t)s * M * N + idx];
-  size_t o;
-  if (mode == 0) {
-    o = (size_t)m * N + n;
-  } else {
-    const int tap = n / Cp;
-    const int c = n - tap * Cp;
-    if (c >= C) return;
-    const int r = tap / S, s = tap - r * S;
-    o = (((size_t)m * C + c) * R + r) * S + s;
-  }
-  float v = (float)acc;
-  if (w) v = v + l2 * w[o];
-  out[o] = v;
-}
-
-static int splitk_reduce(const float* ws, int splits, int M, int N, float* out, const float* w, float l2, int mode,
-                         int C, int Cp, int R, int S, hipStream_t st) {
-  const int total = M * N;
-  hipLaunchKernelGGL(splitk_reduce_kernel, dim3(cdiv(total, 256)), dim3(256), 0, st, ws, splits, M, N, out, w, l2,
-                     mode, C, Cp, R, S);
-  return launch_status();
-}
+// Second stage of split-K (reduce.hip): fixed-order sum over the partial slabs,
+// + l2 * W (regularisers/l2.py:16-17 folded in, as convolution.py:99-100 does), and a
+// scatter into the caller's weight layout (mode 0: out[m][n]; mode 1: KCRS from (r,s,c)).
 
 // Weight re-layouts (tiny; run once per call on the caller's stream).
 __global__ void w_kcrs_to_krsc_kernel(const float* __restrict__ w, int K, int C, int R, int S, int Cp,

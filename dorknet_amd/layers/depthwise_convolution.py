@@ -101,8 +101,9 @@ class DepthwiseConvLayer(Layer):
         if s is None:
             add_regulariser_grad(gw, w, self.weight_regulariser)
         dx = empty_nhwc(N, C, H, W)
-        lib.dk_dwconv_dgrad_f32(dy.data_ptr(), N, OH, OW, C, self._w_rsc(st).data_ptr(), R, S, self.stride,
-                                self.padding, dx.data_ptr(), H, W, st)
+        nb = lib.dk_dwconv_dgrad_workspace_bytes(C, R, S)
+        lib.dk_dwconv_dgrad_f32(dy.data_ptr(), N, OH, OW, C, w.data_ptr(), R, S, self.stride, self.padding,
+                                dx.data_ptr(), H, W, workspace.get(nb), nb, st)
         return dx
 
     def save_to_h5(self, open_f, save_grads=True):

@@ -60,12 +60,71 @@ class FeedForwardNetwork:
             print("Error putting layer {} on GPU, error was: {}".format(layer, e))
             raise e
 
+    def _l2_plan(self):
+        """If every regularisation term the forward pass would add is a plain l2 on a
+        layer's weights, return the (weights, strength) list (in the order
+        feed_forward_network.py:55-60 and residual_block.py:78-84 visit them) so all terms
+        are computed in one multi-tensor launch; None otherwise (per-layer fallback)."""
+        from ..layers.layer import Layer
+        from ..layers.residual_block import ResidualBlock
+        from ..layers._common import l2_strength
+        plan = []
+
+        def visit(layer):
+            rf = type(layer).regulariser_forward
+            if rf is ResidualBlock.regulariser_forward:
+                for l in layer.layer_list:
+                    if hasattr(l, "regulariser_forward") and not visit(l):
+                        return False
+                return True
+            if rf is not Layer.regulariser_forward:
+                return False
+            reg = layer.weight_regulariser
+            if not reg:
+                return True
+            s = l2_strength(reg)
+            w = layer.learned_params["weights"] if layer.learned_params else None
+            if s is None or not (hasattr(w, "is_cuda") and w.is_cuda and w.is_contiguous()):
+                return False
+            plan.append((w, s))
+            return True
+
+        for layer in self.layers:
+            if hasattr(layer, "regulariser_forward") and not visit(layer):
+                return None
+        return plan
+
+    def _l2_total(self, plan, loss_tensor):
+        """loss_tensor + sum of 0.5*s*sum(W^2) over `plan` (dk_l2_loss_multi_f32)."""
+        import torch
+        from .._hip import lib, stream_handle, workspace
+        sig = tuple((w.data_ptr(), w.numel(), s) for w, s in plan)
+        if getattr(self, "_l2_sig", None) != sig:
+            rows, block0 = [], 0
+            for w, s in plan:
+                f = np.array([s, 0.0], dtype=np.float32).view(np.int64)[0]
+                rows.append((w.data_ptr(), w.numel(), block0, int(f)))
+                block0 += -(-w.numel() // 2048)
+            self._l2_table = torch.as_tensor(np.array(rows, dtype=np.int64).reshape(-1, 4), device="cuda")
+            self._l2_blocks = block0
+            self._l2_sig = sig
+        out = torch.empty((), dtype=torch.float32, device=loss_tensor.device)
+        nb = lib.dk_l2_multi_workspace_bytes(self._l2_blocks)
+        lib.dk_l2_loss_multi_f32(self._l2_table.data_ptr(), len(plan), self._l2_blocks, loss_tensor.data_ptr(),
+                                 out.data_ptr(), workspace.get(nb), nb, stream_handle())
+        return out
+
     def forward(self, X, y_one_hot, test_mode=False, terminal_layer_name=None):
         loss = 0
         regularisation_terms = []
         steps = []
         self._steps = steps
         fuse = fusion_enabled()
+        plan = None
+        if not test_mode and self.loss_layer is not None and terminal_layer_name is None:
+            plan = self._l2_plan()
+            if plan is not None and not plan:
+                plan = None
         layers = self.layers
         i = 0
         while i < len(layers):
@@ -83,10 +142,12 @@ class FeedForwardNetwork:
             for l in group:
                 if l.layer_name == terminal_layer_name:
                     return loss, X
-                if not test_mode and hasattr(l, "regulariser_forward"):
+                if not test_mode and plan is None and hasattr(l, "regulariser_forward"):
                     regularisation_terms.append(l.regulariser_forward())
         if self.loss_layer is not None:
             this_loss, X = self.loss_layer.forward(X, y_one_hot, test_mode=test_mode)
+            if plan is not None:
+                return self._l2_total(plan, this_loss), X
             loss += this_loss
             loss += sum(regularisation_terms)
         return loss, X  # NB if test_mode=True, you get softmax scores ("logits")

@@ -49,7 +49,7 @@ def _dw_fwd(x, N, H, W, C, w, R, S, stride, pad, bias, y, OH, OW, st):
     return 2 * N * C * OH * OW * R * S, E * (N * H * W * C + N * OH * OW * C + C * R * S)
 
 
-def _dw_dgrad(dy, N, OH, OW, C, w, R, S, stride, pad, dx, H, W, st):
+def _dw_dgrad(dy, N, OH, OW, C, w, R, S, stride, pad, dx, H, W, ws, nb, st):
     return 2 * N * C * OH * OW * R * S, E * (N * OH * OW * C + N * H * W * C + C * R * S)
 
 
@@ -106,6 +106,11 @@ def _sgd(table, ntens, total_blocks, *rest):
     return 4 * n, 5 * E * n
 
 
+def _l2_multi(table, ntens, total_blocks, *rest):
+    n = total_blocks * 2048
+    return 2 * n, E * n
+
+
 def _colsum(x, M, N, *rest):
     return M * N, E * M * N
 
@@ -138,6 +143,7 @@ MODEL = {
     "dk_gap_bwd_f32": _gap_bwd,
     "dk_sgd_momentum_multi_f32": _sgd,
     "dk_colsum_f32": _colsum,
+    "dk_l2_loss_multi_f32": _l2_multi,
     "dk_nchw_to_nhwc_f32": _nchw_to_nhwc,
 }
 

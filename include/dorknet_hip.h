@@ -67,11 +67,13 @@ int dk_pwconv_wgrad_f32(const float* dy, const float* x, int N, int H, int W, in
  * Replaces DepthwiseConvLayer.forward_cp (layers/depthwise_convolution.py:85-102, CUDA
  * forward_conv :105-121) and backward_cp (:198-221, CUDA backward_conv :122-140).
  * Weights W[C][R][S] as in the reference; dk_dw_weight_rsc_f32 makes the [R][S][C] copy
- * the kernels read.  R x S in {1x1, 3x3, 5x5}.
+ * the forward kernel reads (dgrad takes W[C][R][S] and re-lays it out in its workspace).
+ * R x S in {1x1, 3x3, 5x5}; stride 1 or 2 for forward / wgrad.
  * ------------------------------------------------------------------------------------- */
 int dk_dw_weight_rsc_f32(const float* w_crs, int C, int R, int S, float* w_rsc, void* stream);
 int dk_dwconv_fwd_f32(const float* x, int N, int H, int W, int C, const float* w_rsc, int R, int S, int stride, int pad, const float* bias, float* y, int OH, int OW, void* stream);
-int dk_dwconv_dgrad_f32(const float* dy, int N, int OH, int OW, int C, const float* w_rsc, int R, int S, int stride, int pad, float* dx, int H, int W, void* stream);
+size_t dk_dwconv_dgrad_workspace_bytes(int C, int R, int S);
+int dk_dwconv_dgrad_f32(const float* dy, int N, int OH, int OW, int C, const float* w_crs, int R, int S, int stride, int pad, float* dx, int H, int W, void* ws, size_t ws_bytes, void* stream);
 size_t dk_dwconv_wgrad_workspace_bytes(int N, int OH, int OW, int C, int R, int S);
 int dk_dwconv_wgrad_f32(const float* dy, const float* x, int N, int H, int W, int C, int R, int S, int stride, int pad, int OH, int OW, const float* w_crs, float l2, float* dw_crs, void* ws, size_t ws_bytes, void* stream);
 
@@ -132,6 +134,8 @@ int dk_softmax_xent_bwd_f32(const float* p, const float* y_onehot, int B, int K,
  * ------------------------------------------------------------------------------------- */
 int dk_sgd_momentum_multi_f32(const void* table, int ntens, long long total_blocks, float lr, float momentum, float grad_scale, void* stream);
 int dk_l2_loss_f32(const float* w, long long n, float strength, int accumulate, float* out, void* stream);
+size_t dk_l2_multi_workspace_bytes(long long total_blocks);
+int dk_l2_loss_multi_f32(const void* table, int ntens, long long total_blocks, const float* add_to, float* out, void* ws, size_t ws_bytes, void* stream);
 int dk_scale_f32(const float* x, long long n, float s, float* y, void* stream);
 size_t dk_colsum_workspace_bytes(int M, int N);
 int dk_colsum_f32(const float* in, int M, int N, float* out, void* ws, size_t ws_bytes, void* stream);

@@ -262,12 +262,15 @@ def test_residual_block_and_sgd():
             check(f"{l.layer_name} d{k}", l.grads[k], ol.grads[k], want32=o3.grads[k])
     sgd = SGDMomentum(net, 0.1, 0.9)
     osgd = O.OSGDMomentum(O.ONetwork([oblock], None), 0.1, 0.9)
+    osgd32 = O.OSGDMomentum(O.ONetwork([o32], None), 0.1, 0.9)
     for _ in range(2):
         sgd.update_weights()
         osgd.update_weights()
-    for l, ol in zip(all_layers([block]), all_layers([oblock])):
+        osgd32.update_weights()
+    for l, ol, o3 in zip(all_layers([block]), all_layers([oblock]), all_layers([o32])):
         for k in (ol.learned_params or {}):
-            check(f"{l.layer_name} {k} after sgd", l.learned_params[k], ol.learned_params[k])
+            check(f"{l.layer_name} {k} after sgd", l.learned_params[k], ol.learned_params[k],
+                  want32=o3.learned_params[k])
     # the skip projection is not updated (SGDMomentum.py:7-14)
     assert sgd.learnable_layers and block.skip_projection not in sgd.learnable_layers
 
@@ -277,5 +280,6 @@ def test_l2_regulariser():
     rng = np.random.RandomState(14)
     W = rng.randn(64, 3, 5, 5).astype(np.float32)
     r = l2(1e-4)
-    assert abs(float(r.forward(dev(W))) - ref.l2_forward(W.astype(np.float64), 1e-4)) < 1e-9
+    want = ref.l2_forward(W.astype(np.float64), 1e-4)
+    assert abs(float(r.forward(dev(W))) - want) <= 1e-6 * want
     check("l2 bwd", r.backward(dev(W)), ref.l2_backward(W.astype(np.float64), 1e-4), 1e-7)

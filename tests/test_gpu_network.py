@@ -175,3 +175,18 @@ def test_batchnorm_full_size_statistics():
     Yd = Y.double()
     assert float(Yd.mean(dim=(0, 2, 3)).abs().max()) < 1e-4
     assert float((Yd.var(dim=(0, 2, 3), unbiased=False) - 1).abs().max()) < 1e-3
+
+
+def test_regularisation_fast_path_matches_per_layer_terms():
+    """The network's one-launch l2 total equals loss + sum(layer.regulariser_forward())
+    (feed_forward_network.py:55-60; ResidualBlock counts only its layer_list)."""
+    from examples.resnet18_depsep import ResNet18, synthetic_batch
+    np.random.seed(7)
+    net = ResNet18("r18")
+    net.to_gpu()
+    X, _, onehot = synthetic_batch(2, seed=5)
+    assert net._l2_plan() is not None
+    fast, _ = net.forward(dev(X), dev(onehot))
+    net._l2_plan = lambda: None          # force the per-layer reference path
+    slow, _ = net.forward(dev(X), dev(onehot))
+    assert abs(float(fast) - float(slow)) <= 1e-6 * abs(float(slow))
