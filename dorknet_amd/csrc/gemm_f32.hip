@@ -16,23 +16,45 @@
 //       is fused into the epilogue
 //   * dense fwd/dgrad/wgrad (layers/dense_layer.py:46-67)
 //
-// Tiles are staged global -> registers -> LDS with one tile of register prefetch
-// and two LDS buffers (one barrier per K-tile).  In LDS every operand tile is
-// stored k-major ([BK][rows], rows contiguous), so an MFMA operand fetch is one
-// conflict-free ds_read_b32 per lane: lanes 0-31 read k, lanes 32-63 read k+1.
+// Data movement: operand tiles go global -> registers (one K-tile of prefetch) -> LDS
+// (two buffers, one barrier per K-tile).  Global reads are buffer loads whose
+// out-of-range offsets return 0 in hardware, so padding, ragged tiles and the K tail need
+// no branches.  An operand whose source is K-contiguous (activation rows, weight rows)
+// is kept K-contiguous in LDS ([rows][BK+4]) and read with one conflict-free
+// ds_read_b128 per lane that feeds four MFMAs; an operand whose source is
+// row-contiguous (wgrad operands) is kept [BK][rows] and read with ds_read_b32.  Because
+// the MFMA sums over k in any order, the four MFMAs of a q-block use k = 8q + 4h + t
+// (h = lane half, t = 0..3) on both operands.
 #include "dk_common.h"
 
 namespace dk {
 
 // ----------------------------------------------------------------------------
+// Buffer loads (OOB -> 0)
+// ----------------------------------------------------------------------------
+
+constexpr uint32_t kOOB = 0x80000000u;  // an offset past any buffer we build (tensors < 2 GiB)
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const float* p, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p), (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ f32x4 bload4(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0));
+}
+__device__ __forceinline__ float bload1(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, 0));
+}
+
+// ----------------------------------------------------------------------------
 // Operand descriptors
 // ----------------------------------------------------------------------------
 
-// Implicit-im2col view of an NHWC tensor x[n][ih][iw][c] (C % 4 == 0).
+// Implicit-im2col view of an NHWC tensor x[n][ih][iw][c] (C % 4 == 0, < 2 GiB).
 // Row/pixel index m -> (n, oh, ow) over an OH x OW grid; tap (r,s) reads
 // (ih, iw) = (oh*sa + dr*r + off, ow*sa + dr*s + off), zero outside [0,H)x[0,W).
 struct ImgDesc {
   const float* x;
+  uint32_t bytes;
   int H, W, C;
   int OH, OW;
   int R, S;
@@ -43,22 +65,43 @@ struct ImgDesc {
 // Row-major matrix p[row][ld]; `ext` bounds the non-reduction index.
 struct MatDesc {
   const float* p;
+  uint32_t bytes;
   int ld;
   int ext;
-  int vec;  // 1 when float4 loads are legal (ld, ext/Ktot and base 16B aligned)
 };
 
 // ----------------------------------------------------------------------------
-// Loaders: each fills an LDS tile T[BK][S] (S >= ROWS, row = k).
+// Loaders.  K-contiguous ("KC") loaders fill T[ROWS][BK+4]; row-contiguous ("IC")
+// loaders fill T[BK][ROWS].  frag(T, row, q, h) returns the four k values
+// 8q + 4h + {0,1,2,3} of `row` for the MFMA loop.
 // ----------------------------------------------------------------------------
 
-// Source is k-contiguous (rows = i): im2col rows of an NHWC image.
+template <int ROWS, int BK>
+struct KCLayout {
+  static constexpr int SK = BK + 4;  // row stride in floats: (BK+4)/4 odd -> conflict-free b128 reads
+  static constexpr int BUF = ROWS * SK;
+  __device__ static __forceinline__ f32x4 frag(const float* T, int row, int q, int h) {
+    return ld4(T + row * SK + 8 * q + 4 * h);
+  }
+};
+
+template <int ROWS, int BK>
+struct ICLayout {
+  static constexpr int S = ROWS;
+  static constexpr int BUF = BK * ROWS;
+  __device__ static __forceinline__ f32x4 frag(const float* T, int row, int q, int h) {
+    const float* p = T + (8 * q + 4 * h) * S + row;
+    return f32x4{p[0], p[S], p[2 * S], p[3 * S]};
+  }
+};
+
+// Implicit-im2col rows of an NHWC image (K-contiguous).
 template <int ROWS, int BK, int NT>
-struct LdImgKC {
+struct LdImgKC : KCLayout<ROWS, BK> {
+  using L = KCLayout<ROWS, BK>;
   static constexpr int KQ = BK / 4;
   static constexpr int RSTEP = NT / KQ;
   static constexpr int NR = ROWS >= RSTEP ? ROWS / RSTEP : 1;
-  static constexpr int S = ROWS + 2;  // S % 32 == 2: conflict-free transposing writes
   int kq, rb;
   bool active;
   int base[NR], ih0[NR], iw0[NR];
@@ -88,6 +131,7 @@ struct LdImgKC {
   }
 
   __device__ __forceinline__ void load(const ImgDesc& d, int k0, int Ktot) {
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc(d.x, d.bytes);
     const int k = k0 + 4 * kq;
     const bool kv = k < Ktot;
     const int tap = k / d.C;
@@ -100,33 +144,31 @@ struct LdImgKC {
     for (int j = 0; j < NR; ++j) {
       const int ih = ih0[j] + dri, iw = iw0[j] + dsi;
       const bool ok = kv && (unsigned)ih < (unsigned)d.H && (unsigned)iw < (unsigned)d.W;
-      v[j] = ok ? ld4(d.x + (size_t)(base[j] + doff) * d.C + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+      const uint32_t off = ok ? (uint32_t)((base[j] + doff) * d.C + c) * 4u : kOOB;
+      v[j] = bload4(rs, off);
     }
   }
 
-  __device__ __forceinline__ void store(float* t) const {
+  __device__ __forceinline__ void store(float* T) const {
     if (!active) return;
 #pragma unroll
-    for (int j = 0; j < NR; ++j) {
-      const int row = rb + j * RSTEP;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) t[(4 * kq + e) * S + row] = v[j][e];
-    }
+    for (int j = 0; j < NR; ++j) st4(T + (rb + j * RSTEP) * L::SK + 4 * kq, v[j]);
   }
 };
 
-// Source is k-contiguous row-major matrix p[i][ld] (k along the row).
-template <int ROWS, int BK, int NT>
-struct LdMatKC {
+// Row-major matrix p[i][ld], k along the row (K-contiguous).  VEC: float4 loads
+// (ld % 4 == 0, Ktot % 4 == 0); otherwise four scalar loads.
+template <int ROWS, int BK, int NT, bool VEC>
+struct LdMatKCT : KCLayout<ROWS, BK> {
+  using L = KCLayout<ROWS, BK>;
   static constexpr int KQ = BK / 4;
   static constexpr int RSTEP = NT / KQ;
   static constexpr int NR = ROWS >= RSTEP ? ROWS / RSTEP : 1;
-  static constexpr int S = ROWS + 2;
   int kq, rb, row0;
   bool active;
   f32x4 v[NR];
 
-  __device__ __forceinline__ void init(const MatDesc& d, int row0_, int tid) {
+  __device__ __forceinline__ void init(const MatDesc&, int row0_, int tid) {
     kq = tid % KQ;
     rb = tid / KQ;
     row0 = row0_;
@@ -134,43 +176,45 @@ struct LdMatKC {
   }
 
   __device__ __forceinline__ void load(const MatDesc& d, int k0, int Ktot) {
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc(d.p, d.bytes);
     const int k = k0 + 4 * kq;
 #pragma unroll
     for (int j = 0; j < NR; ++j) {
       const int i = row0 + rb + j * RSTEP;
       const bool iv = active && i < d.ext;
-      if (d.vec) {
-        v[j] = (iv && k < Ktot) ? ld4(d.p + (size_t)i * d.ld + k) : f32x4{0.f, 0.f, 0.f, 0.f};
+      const uint32_t base = (uint32_t)(i * d.ld + k) * 4u;
+      if constexpr (VEC) {
+        v[j] = bload4(rs, (iv && k < Ktot) ? base : kOOB);
       } else {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) v[j][e] = (iv && k + e < Ktot) ? d.p[(size_t)i * d.ld + k + e] : 0.f;
+        for (int e = 0; e < 4; ++e) v[j][e] = bload1(rs, (iv && k + e < Ktot) ? base + 4u * e : kOOB);
       }
     }
   }
 
-  __device__ __forceinline__ void store(float* t) const {
+  __device__ __forceinline__ void store(float* T) const {
     if (!active) return;
 #pragma unroll
-    for (int j = 0; j < NR; ++j) {
-      const int row = rb + j * RSTEP;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) t[(4 * kq + e) * S + row] = v[j][e];
-    }
+    for (int j = 0; j < NR; ++j) st4(T + (rb + j * RSTEP) * L::SK + 4 * kq, v[j]);
   }
 };
-
-// Source is i-contiguous row-major matrix p[k][ld] (i along the row).
 template <int ROWS, int BK, int NT>
-struct LdMatIC {
+using LdMatKC = LdMatKCT<ROWS, BK, NT, true>;
+template <int ROWS, int BK, int NT>
+using LdMatKC1 = LdMatKCT<ROWS, BK, NT, false>;
+
+// Row-major matrix p[k][ld], i along the row (row-contiguous).
+template <int ROWS, int BK, int NT, bool VEC>
+struct LdMatICT : ICLayout<ROWS, BK> {
+  using L = ICLayout<ROWS, BK>;
   static constexpr int IQ = ROWS / 4;
   static constexpr int KSTEP = NT / IQ;
   static constexpr int NK = BK >= KSTEP ? BK / KSTEP : 1;
-  static constexpr int S = ROWS;
   int iq, kb, i0;
   bool active;
   f32x4 v[NK];
 
-  __device__ __forceinline__ void init(const MatDesc& d, int row0, int tid) {
+  __device__ __forceinline__ void init(const MatDesc&, int row0, int tid) {
     iq = tid % IQ;
     kb = tid / IQ;
     i0 = row0 + 4 * iq;
@@ -178,34 +222,40 @@ struct LdMatIC {
   }
 
   __device__ __forceinline__ void load(const MatDesc& d, int k0, int Ktot) {
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc(d.p, d.bytes);
 #pragma unroll
     for (int j = 0; j < NK; ++j) {
       const int k = k0 + kb + j * KSTEP;
       const bool kv = active && k < Ktot;
-      if (d.vec) {
-        v[j] = (kv && i0 < d.ext) ? ld4(d.p + (size_t)k * d.ld + i0) : f32x4{0.f, 0.f, 0.f, 0.f};
+      const uint32_t base = (uint32_t)(k * d.ld + i0) * 4u;
+      if constexpr (VEC) {
+        v[j] = bload4(rs, (kv && i0 < d.ext) ? base : kOOB);
       } else {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) v[j][e] = (kv && i0 + e < d.ext) ? d.p[(size_t)k * d.ld + i0 + e] : 0.f;
+        for (int e = 0; e < 4; ++e) v[j][e] = bload1(rs, (kv && i0 + e < d.ext) ? base + 4u * e : kOOB);
       }
     }
   }
 
-  __device__ __forceinline__ void store(float* t) const {
+  __device__ __forceinline__ void store(float* T) const {
     if (!active) return;
 #pragma unroll
-    for (int j = 0; j < NK; ++j) st4(t + (kb + j * KSTEP) * S + 4 * iq, v[j]);
+    for (int j = 0; j < NK; ++j) st4(T + (kb + j * KSTEP) * L::S + 4 * iq, v[j]);
   }
 };
+template <int ROWS, int BK, int NT>
+using LdMatIC = LdMatICT<ROWS, BK, NT, true>;
+template <int ROWS, int BK, int NT>
+using LdMatIC1 = LdMatICT<ROWS, BK, NT, false>;
 
-// Source is an implicit-im2col image, i = (r,s,c) (c innermost), k = pixel.
+// Implicit-im2col image with i = (r,s,c) (c innermost) and k = pixel (row-contiguous).
 // Used by wgrad: B(i=(r,s,c), k=m) = x[pixel(m) shifted by tap (r,s)][c].
 template <int ROWS, int BK, int NT>
-struct LdImgIC {
+struct LdImgIC : ICLayout<ROWS, BK> {
+  using L = ICLayout<ROWS, BK>;
   static constexpr int IQ = ROWS / 4;
   static constexpr int KSTEP = NT / IQ;
   static constexpr int NK = BK >= KSTEP ? BK / KSTEP : 1;
-  static constexpr int S = ROWS;
   int iq, kb;
   bool active, colv;
   int c, dri, dsi;
@@ -216,7 +266,7 @@ struct LdImgIC {
     kb = tid / IQ;
     active = kb < BK;
     const int j = row0 + 4 * iq;
-    colv = j < d.R * d.S * d.C;
+    colv = active && j < d.R * d.S * d.C;
     const int tap = j / d.C;
     c = j - tap * d.C;
     const int r = tap / d.S;
@@ -226,28 +276,25 @@ struct LdImgIC {
   }
 
   __device__ __forceinline__ void load(const ImgDesc& d, int k0, int Ktot) {
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc(d.x, d.bytes);
 #pragma unroll
     for (int jj = 0; jj < NK; ++jj) {
       const int m = k0 + kb + jj * KSTEP;
-      bool ok = active && colv && m < d.M;
-      int ih = 0, iw = 0, n = 0;
-      if (ok) {
-        const int ow = m % d.OW;
-        const int t = m / d.OW;
-        const int oh = t % d.OH;
-        n = t / d.OH;
-        ih = oh * d.sa + dri + d.off;
-        iw = ow * d.sa + dsi + d.off;
-        ok = (unsigned)ih < (unsigned)d.H && (unsigned)iw < (unsigned)d.W;
-      }
-      v[jj] = ok ? ld4(d.x + ((size_t)(n * d.H + ih) * d.W + iw) * d.C + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+      const int ow = m % d.OW;
+      const int t = m / d.OW;
+      const int oh = t % d.OH;
+      const int n = t / d.OH;
+      const int ih = oh * d.sa + dri + d.off;
+      const int iw = ow * d.sa + dsi + d.off;
+      const bool ok = colv && m < d.M && (unsigned)ih < (unsigned)d.H && (unsigned)iw < (unsigned)d.W;
+      v[jj] = bload4(rs, ok ? (uint32_t)(((n * d.H + ih) * d.W + iw) * d.C + c) * 4u : kOOB);
     }
   }
 
-  __device__ __forceinline__ void store(float* t) const {
+  __device__ __forceinline__ void store(float* T) const {
     if (!active) return;
 #pragma unroll
-    for (int j = 0; j < NK; ++j) st4(t + (kb + j * KSTEP) * S + 4 * iq, v[j]);
+    for (int j = 0; j < NK; ++j) st4(T + (kb + j * KSTEP) * L::S + 4 * iq, v[j]);
   }
 };
 
@@ -255,30 +302,33 @@ struct LdImgIC {
 // Epilogues
 // ----------------------------------------------------------------------------
 
-// out[row(m)][n] = acc (+ bias[n]).  With st > 1 the GEMM row m = (b, oh, ow) of
-// an OH x OW grid lands at (b, oh*st, ow*st) of an (OH*st) x (OW*st) grid and
-// the other st*st-1 positions of that cell are written as zeros: this is the
-// pointwise stride-s backward "widen" (pointwise_convolution.py:68-72) fused.
+// out[m][n] = acc (+ bias[n]).
 struct EpStore {
   float* out;
   int ldo;
   const float* bias;
-  int OH, OW, st;
   __device__ __forceinline__ void put(int m, int n, float v, int) const {
     if (bias) v += bias[n];
-    if (st == 1) {
-      out[(size_t)m * ldo + n] = v;
-    } else {
-      const int ow = m % OW;
-      const int t = m / OW;
-      const int oh = t % OH;
-      const int b = t / OH;
-      const int OW2 = OW * st, OH2 = OH * st;
-      const size_t cell = (size_t)(b * OH2 + oh * st) * OW2 + (size_t)ow * st;
-      for (int dy = 0; dy < st; ++dy)
-        for (int dx = 0; dx < st; ++dx)
-          out[(cell + (size_t)dy * OW2 + dx) * ldo + n] = (dy | dx) ? 0.f : v;
-    }
+    out[(size_t)m * ldo + n] = v;
+  }
+};
+
+// Pointwise stride-st backward "widen" (pointwise_convolution.py:68-72) fused: the GEMM
+// row m = (b, oh, ow) of an OH x OW grid lands at (b, oh*st, ow*st) of an
+// (OH*st) x (OW*st) grid and the other st*st-1 positions of that cell are zero.
+struct EpWiden {
+  float* out;
+  int ldo;
+  int OH, OW, st;
+  __device__ __forceinline__ void put(int m, int n, float v, int) const {
+    const int ow = m % OW;
+    const int t = m / OW;
+    const int oh = t % OH;
+    const int b = t / OH;
+    const int OW2 = OW * st, OH2 = OH * st;
+    const size_t cell = (size_t)(b * OH2 + oh * st) * OW2 + (size_t)ow * st;
+    for (int dy = 0; dy < st; ++dy)
+      for (int dx = 0; dx < st; ++dx) out[(cell + (size_t)dy * OW2 + dx) * ldo + n] = (dy | dx) ? 0.f : v;
   }
 };
 
@@ -301,9 +351,8 @@ __global__ __launch_bounds__(64 * WM * WN) void igemm_f32(DA da, DB db, EP ep, i
   constexpr int TM = BM / (32 * WM);
   constexpr int TN = BN / (32 * WN);
   static_assert(TM >= 1 && TN >= 1 && BM == 32 * WM * TM && BN == 32 * WN * TN, "tile");
-  static_assert(BK % 4 == 0, "BK");
-  constexpr int SA = LA::S, SB = LB::S;
-  constexpr int ABUF = BK * SA, BBUF = BK * SB;
+  static_assert(BK % 8 == 0, "BK");
+  constexpr int ABUF = LA::BUF, BBUF = LB::BUF;
   __shared__ float smem[2 * (ABUF + BBUF)];
   float* const As = smem;
   float* const Bs = smem + 2 * ABUF;
@@ -340,26 +389,30 @@ __global__ __launch_bounds__(64 * WM * WN) void igemm_f32(DA da, DB db, EP ep, i
     lb.store(Bs);
     __syncthreads();
     int cur = 0;
+    const int arow = wm * 32 * TM + l32;
+    const int brow = wn * 32 * TN + l32;
     for (int kt = kt0; kt < kt1; ++kt) {
       const bool more = kt + 1 < kt1;
       if (more) {
         la.load(da, (kt + 1) * BK, Ktot);
         lb.load(db, (kt + 1) * BK, Ktot);
       }
-      const float* a_t = As + cur * ABUF + h * SA + wm * 32 * TM + l32;
-      const float* b_t = Bs + cur * BBUF + h * SB + wn * 32 * TN + l32;
+      const float* A_t = As + cur * ABUF;
+      const float* B_t = Bs + cur * BBUF;
 #pragma unroll
-      for (int kk = 0; kk < BK / 2; ++kk) {
-        float a[TM], b[TN];
+      for (int q = 0; q < BK / 8; ++q) {
+        f32x4 af[TM], bf[TN];
 #pragma unroll
-        for (int t = 0; t < TM; ++t) a[t] = a_t[2 * kk * SA + 32 * t];
+        for (int t = 0; t < TM; ++t) af[t] = LA::frag(A_t, arow + 32 * t, q, h);
 #pragma unroll
-        for (int u = 0; u < TN; ++u) b[u] = b_t[2 * kk * SB + 32 * u];
+        for (int u = 0; u < TN; ++u) bf[u] = LB::frag(B_t, brow + 32 * u, q, h);
 #pragma unroll
-        for (int t = 0; t < TM; ++t)
+        for (int e = 0; e < 4; ++e)
 #pragma unroll
-          for (int u = 0; u < TN; ++u)
-            acc[t][u] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[t], b[u], acc[t][u], 0, 0, 0);
+          for (int t = 0; t < TM; ++t)
+#pragma unroll
+            for (int u = 0; u < TN; ++u)
+              acc[t][u] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[t][e], bf[u][e], acc[t][u], 0, 0, 0);
       }
       if (more) {
         la.store(As + (cur ^ 1) * ABUF);
@@ -387,39 +440,98 @@ __global__ __launch_bounds__(64 * WM * WN) void igemm_f32(DA da, DB db, EP ep, i
 // Host-side launch helpers and tile selection
 // ----------------------------------------------------------------------------
 
-constexpr int kBK = 16;
+// Tile configurations.  Row problems (forward / dgrad: output-stationary, one pass over
+// K) and split-K problems (wgrad: K = pixels, split over blocks) have separate tables.
+// The heuristics below pick one per shape; dk_debug_set_gemm_config() overrides the
+// choice for tuning runs (scripts/gemm_tune.py).
+//                 id  BM   BN  BK  WM WN
+#define DK_ROW_CONFIGS(X) \
+  X(0, 256, 64, 16, 4, 1)  \
+  X(1, 128, 64, 16, 2, 1)  \
+  X(2, 128, 64, 32, 2, 1)  \
+  X(3, 256, 64, 32, 4, 1)  \
+  X(4, 128, 128, 16, 2, 2) \
+  X(5, 128, 128, 32, 2, 2) \
+  X(6, 64, 64, 16, 2, 2)   \
+  X(7, 128, 32, 16, 4, 1)  \
+  X(8, 64, 64, 32, 2, 2)   \
+  X(9, 256, 128, 16, 4, 2) \
+  X(10, 64, 64, 64, 2, 2)  \
+  X(11, 128, 64, 64, 2, 1)
+#define DK_SPLITK_CONFIGS(X) \
+  X(0, 64, 64, 16, 2, 2)     \
+  X(1, 64, 64, 32, 2, 2)     \
+  X(2, 64, 64, 64, 2, 2)     \
+  X(3, 128, 128, 16, 2, 2)   \
+  X(4, 128, 128, 32, 2, 2)   \
+  X(5, 128, 64, 32, 2, 2)    \
+  X(6, 64, 128, 32, 2, 2)
 
-template <int BM, int BN, int WM, int WN, template <int, int, int> class LA, class DA,
+struct TileCfg {
+  int BM, BN, BK;
+};
+#define DK_CFG_ENTRY(id, bm, bn, bk, wm, wn) {bm, bn, bk},
+static const TileCfg kRowCfg[] = {DK_ROW_CONFIGS(DK_CFG_ENTRY)};
+static const TileCfg kSplitCfg[] = {DK_SPLITK_CONFIGS(DK_CFG_ENTRY)};
+#undef DK_CFG_ENTRY
+static const int kNumRowCfg = sizeof(kRowCfg) / sizeof(kRowCfg[0]);
+static const int kNumSplitCfg = sizeof(kSplitCfg) / sizeof(kSplitCfg[0]);
+
+static int g_cfg_override[2] = {-1, -1};  // tuning knob only (see header)
+
+template <int BM, int BN, int BK, int WM, int WN, template <int, int, int> class LA, class DA,
           template <int, int, int> class LB, class DB, class EP>
 static int launch_igemm(const DA& da, const DB& db, const EP& ep, int M, int N, int Ktot, int splits,
                         hipStream_t st) {
   constexpr int NT = 64 * WM * WN;
-  using A = LA<BM, kBK, NT>;
-  using B = LB<BN, kBK, NT>;
+  using A = LA<BM, BK, NT>;
+  using B = LB<BN, BK, NT>;
   const int tiles = cdiv(M, BM) * cdiv(N, BN);
-  const int KT = cdiv(Ktot, kBK);
+  const int KT = cdiv(Ktot, BK);
   if (splits < 1) splits = 1;
   if (splits > KT) splits = KT > 0 ? KT : 1;
   const int kps = KT > 0 ? cdiv(KT, splits) : 1;
   splits = KT > 0 ? cdiv(KT, kps) : 1;
-  hipLaunchKernelGGL((igemm_f32<BM, BN, kBK, WM, WN, A, DA, B, DB, EP>), dim3(tiles, splits), dim3(NT), 0, st,
-                     da, db, ep, M, N, Ktot, kps);
+  hipLaunchKernelGGL((igemm_f32<BM, BN, BK, WM, WN, A, DA, B, DB, EP>), dim3(tiles, splits), dim3(NT), 0, st, da,
+                     db, ep, M, N, Ktot, kps);
   return launch_status();
 }
 
-// Output-stationary problems (fwd / dgrad): tile by the N extent.
+static int row_config(int M, int N, int K) {
+  if (g_cfg_override[0] >= 0) return g_cfg_override[0];
+  (void)M;
+  (void)N;
+  // Measured on MI355X (scripts/gemm_tune.py, profiles/r01c_gemm_tune.md): 64x64 tiles win on
+  // every ResNet shape; a deeper k-tile pays once the reduction is longer than ~100.
+  return K <= 96 ? 6 : 8;
+}
+
+// Output-stationary problems (fwd / dgrad).
 template <template <int, int, int> class LA, class DA, template <int, int, int> class LB, class DB, class EP>
 static int igemm_rows(const DA& da, const DB& db, const EP& ep, int M, int N, int Ktot, hipStream_t st) {
-  if (N <= 32) return launch_igemm<128, 32, 4, 1, LA, DA, LB, DB, EP>(da, db, ep, M, N, Ktot, 1, st);
-  if (N <= 64) return launch_igemm<256, 64, 4, 1, LA, DA, LB, DB, EP>(da, db, ep, M, N, Ktot, 1, st);
-  if (M <= 4096) return launch_igemm<64, 64, 2, 2, LA, DA, LB, DB, EP>(da, db, ep, M, N, Ktot, 1, st);
-  return launch_igemm<128, 128, 2, 2, LA, DA, LB, DB, EP>(da, db, ep, M, N, Ktot, 1, st);
+  switch (row_config(M, N, Ktot)) {
+#define DK_CASE(id, bm, bn, bk, wm, wn) \
+  case id:                              \
+    return launch_igemm<bm, bn, bk, wm, wn, LA, DA, LB, DB, EP>(da, db, ep, M, N, Ktot, 1, st);
+    DK_ROW_CONFIGS(DK_CASE)
+#undef DK_CASE
+    default:
+      return DK_ERR_ARGS;
+  }
 }
 
 // Reduction-heavy problems (wgrad): split K over enough blocks to fill the chip.
-static int wgrad_splits(int M, int N, int Kred, int BM, int BN) {
-  const int tiles = cdiv(M, BM) * cdiv(N, BN);
-  const int KT = cdiv(Kred, kBK);
+static int splitk_config(int M, int N, int Kred) {
+  if (g_cfg_override[1] >= 0) return g_cfg_override[1];
+  (void)M;
+  (void)N;
+  (void)Kred;
+  return 1;  // 64x64x32: best or within 3% of best on every measured wgrad shape
+}
+
+static int wgrad_splits(int M, int N, int Kred, const TileCfg& c) {
+  const int tiles = cdiv(M, c.BM) * cdiv(N, c.BN);
+  const int KT = cdiv(Kred, c.BK);
   int splits = cdiv(1024, tiles);
   if (splits > KT) splits = KT;
   if (splits < 1) splits = 1;
@@ -427,37 +539,30 @@ static int wgrad_splits(int M, int N, int Kred, int BM, int BN) {
   return cdiv(KT, kps);
 }
 
-static void wgrad_tile(int M, int N, int* BM, int* BN) {
-  if (M >= 128 && N >= 128) {
-    *BM = 128;
-    *BN = 128;
-  } else {
-    *BM = 64;
-    *BN = 64;
-  }
-}
-
 template <template <int, int, int> class LA, class DA, template <int, int, int> class LB, class DB>
 static int igemm_splitk(const DA& da, const DB& db, float* ws, int M, int N, int Kred, hipStream_t st,
                         int* splits_out) {
-  int BM, BN;
-  wgrad_tile(M, N, &BM, &BN);
-  const int splits = wgrad_splits(M, N, Kred, BM, BN);
+  const int id = splitk_config(M, N, Kred);
+  if (id < 0 || id >= kNumSplitCfg) return DK_ERR_ARGS;
+  const int splits = wgrad_splits(M, N, Kred, kSplitCfg[id]);
   *splits_out = splits;
   EpPartial ep{ws, M, N};
-  if (BM == 128) return launch_igemm<128, 128, 2, 2, LA, DA, LB, DB, EpPartial>(da, db, ep, M, N, Kred, splits, st);
-  return launch_igemm<64, 64, 2, 2, LA, DA, LB, DB, EpPartial>(da, db, ep, M, N, Kred, splits, st);
+  switch (id) {
+#define DK_CASE(cid, bm, bn, bk, wm, wn) \
+  case cid:                              \
+    return launch_igemm<bm, bn, bk, wm, wn, LA, DA, LB, DB, EpPartial>(da, db, ep, M, N, Kred, splits, st);
+    DK_SPLITK_CONFIGS(DK_CASE)
+#undef DK_CASE
+    default:
+      return DK_ERR_ARGS;
+  }
 }
 
 static size_t splitk_ws_bytes(int M, int N, int Kred) {
-  int BM, BN;
-  wgrad_tile(M, N, &BM, &BN);
-  return (size_t)wgrad_splits(M, N, Kred, BM, BN) * (size_t)M * (size_t)N * sizeof(float);
+  int id = splitk_config(M, N, Kred);
+  if (id < 0 || id >= kNumSplitCfg) id = 0;
+  return (size_t)wgrad_splits(M, N, Kred, kSplitCfg[id]) * (size_t)M * (size_t)N * sizeof(float);
 }
-
-// Second stage of split-K (reduce.hip): fixed-order sum over the partial slabs,
-// + l2 * W (regularisers/l2.py:16-17 folded in, as convolution.py:99-100 does), and a
-// scatter into the caller's weight layout (mode 0: out[m][n]; mode 1: KCRS from (r,s,c)).
 
 // Weight re-layouts (tiny; run once per call on the caller's stream).
 __global__ void w_kcrs_to_krsc_kernel(const float* __restrict__ w, int K, int C, int R, int S, int Cp,
@@ -522,10 +627,21 @@ __global__ void col2im_kernel(const float* __restrict__ cols, int N, int C, int 
 
 static inline int aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
-static inline MatDesc mat(const float* p, int ld, int ext, int kext) {
-  MatDesc d{p, ld, ext, 0};
-  d.vec = (ld % 4 == 0) && (ext % 4 == 0) && (kext % 4 == 0) && aligned16(p);
-  return d;
+// Buffer resources address < 2 GiB (32-bit offsets with kOOB as the out-of-range marker).
+static inline bool fits(size_t bytes) { return bytes < ((size_t)1 << 31); }
+
+// rows x ld matrix; ext = extent of the non-reduction index (rows for a K-contiguous
+// operand, valid columns for a row-contiguous one).
+static inline MatDesc mat(const float* p, int rows, int ld, int ext) {
+  return MatDesc{p, (uint32_t)((size_t)rows * ld * sizeof(float)), ld, ext};
+}
+static inline bool vec_ok(const MatDesc& d, int kext, int iext) {
+  return d.ld % 4 == 0 && kext % 4 == 0 && iext % 4 == 0 && aligned16(d.p);
+}
+
+static inline ImgDesc img(const float* x, int N, int H, int W, int C, int OH, int OW, int R, int S, int sa, int dr,
+                          int off, int M) {
+  return ImgDesc{x, (uint32_t)((size_t)N * H * W * C * sizeof(float)), H, W, C, OH, OW, R, S, sa, dr, off, M};
 }
 
 }  // namespace dk
@@ -535,6 +651,14 @@ using namespace dk;
 // ============================================================================
 // C ABI
 // ============================================================================
+
+// Tuning knob: kind 0 = row problems (fwd/dgrad), 1 = split-K (wgrad); cfg -1 = heuristic.
+// Returns the number of configurations of that kind.  Not thread-safe; for tuning runs.
+DK_API int dk_debug_set_gemm_config(int kind, int cfg) {
+  if (kind < 0 || kind > 1) return -1;
+  g_cfg_override[kind] = cfg;
+  return kind == 0 ? kNumRowCfg : kNumSplitCfg;
+}
 
 DK_API int dk_conv_weight_krsc_f32(const float* w_kcrs, int K, int C, int R, int S, int Cp, float* w_krsc,
                                    void* stream) {
@@ -554,22 +678,22 @@ DK_API int dk_conv_weight_crsk_f32(const float* w_kcrs, int K, int C, int R, int
 // y[n,oh,ow,k] = sum_{r,s,c} x[n, oh*stride + r - pad, ow*stride + s - pad, c] * w[k][r][s][c] (+ bias[k])
 DK_API int dk_conv2d_fwd_f32(const float* x, int N, int H, int W, int C, const float* w_krsc, int K, int R, int S,
                              int stride, int pad, const float* bias, float* y, int OH, int OW, void* stream) {
-  if (C % 4 || !aligned16(x)) return DK_ERR_ARGS;
-  ImgDesc a{x, H, W, C, OH, OW, R, S, stride, 1, -pad, N * OH * OW};
+  if (C % 4 || !aligned16(x) || !aligned16(w_krsc) || !fits((size_t)N * H * W * C * 4)) return DK_ERR_ARGS;
+  ImgDesc a = img(x, N, H, W, C, OH, OW, R, S, stride, 1, -pad, N * OH * OW);
   const int Ktot = R * S * C;
-  MatDesc b = mat(w_krsc, Ktot, K, Ktot);
-  EpStore ep{y, K, bias, OH, OW, 1};
+  MatDesc b = mat(w_krsc, K, Ktot, K);
+  EpStore ep{y, K, bias};
   return igemm_rows<LdImgKC, ImgDesc, LdMatKC, MatDesc, EpStore>(a, b, ep, N * OH * OW, K, Ktot, as_stream(stream));
 }
 
 // Stride-1 dgrad as an implicit GEMM: dx[n,h,w,c] = sum_{r,s,k} dy[n, h+pad-r, w+pad-s, k] * w[k][c][r][s]
 DK_API int dk_conv2d_dgrad_f32(const float* dy, int N, int OH, int OW, int K, const float* w_crsk, int C, int R,
                                int S, int pad, float* dx, int H, int W, void* stream) {
-  if (K % 4 || !aligned16(dy)) return DK_ERR_ARGS;
-  ImgDesc a{dy, OH, OW, K, H, W, R, S, 1, -1, pad, N * H * W};
+  if (K % 4 || !aligned16(dy) || !aligned16(w_crsk) || !fits((size_t)N * OH * OW * K * 4)) return DK_ERR_ARGS;
+  ImgDesc a = img(dy, N, OH, OW, K, H, W, R, S, 1, -1, pad, N * H * W);
   const int Ktot = R * S * K;
-  MatDesc b = mat(w_crsk, Ktot, C, Ktot);
-  EpStore ep{dx, C, nullptr, H, W, 1};
+  MatDesc b = mat(w_crsk, C, Ktot, C);
+  EpStore ep{dx, C, nullptr};
   return igemm_rows<LdImgKC, ImgDesc, LdMatKC, MatDesc, EpStore>(a, b, ep, N * H * W, C, Ktot, as_stream(stream));
 }
 
@@ -584,15 +708,24 @@ DK_API int dk_conv2d_dgrad_strided_f32(const float* dy, int N, int OH, int OW, i
   const int M = N * OH * OW;
   const int CRS = C * R * S;
   if (ws_bytes < dk_conv2d_dgrad_cols_workspace_bytes(N, OH, OW, C, R, S)) return DK_ERR_WORKSPACE;
+  if (!fits((size_t)M * K * 4) || !fits((size_t)M * CRS * 4)) return DK_ERR_ARGS;
   float* cols = static_cast<float*>(ws);
-  MatDesc a = mat(dy, K, M, K);
-  MatDesc b = mat(w_kcrs, CRS, CRS, K);
-  EpStore ep{cols, CRS, nullptr, OH, OW, 1};
-  int rc = igemm_rows<LdMatKC, MatDesc, LdMatIC, MatDesc, EpStore>(a, b, ep, M, CRS, K, as_stream(stream));
+  MatDesc a = mat(dy, M, K, M);
+  MatDesc b = mat(w_kcrs, K, CRS, CRS);
+  EpStore ep{cols, CRS, nullptr};
+  const hipStream_t st = as_stream(stream);
+  int rc;
+  const bool va = vec_ok(a, K, 4), vb = vec_ok(b, 4, CRS);
+  if (va && vb)
+    rc = igemm_rows<LdMatKC, MatDesc, LdMatIC, MatDesc, EpStore>(a, b, ep, M, CRS, K, st);
+  else if (va)
+    rc = igemm_rows<LdMatKC, MatDesc, LdMatIC1, MatDesc, EpStore>(a, b, ep, M, CRS, K, st);
+  else
+    rc = igemm_rows<LdMatKC1, MatDesc, LdMatIC1, MatDesc, EpStore>(a, b, ep, M, CRS, K, st);
   if (rc) return rc;
   const long long total = (long long)N * H * W * C;
-  hipLaunchKernelGGL(col2im_kernel, dim3((unsigned)cdivll(total, 256)), dim3(256), 0, as_stream(stream), cols, N, C,
-                     H, W, OH, OW, R, S, stride, pad, dx);
+  hipLaunchKernelGGL(col2im_kernel, dim3((unsigned)cdivll(total, 256)), dim3(256), 0, st, cols, N, C, H, W, OH, OW, R,
+                     S, stride, pad, dx);
   return launch_status();
 }
 
@@ -606,12 +739,16 @@ DK_API int dk_conv2d_wgrad_f32(const float* dy, const float* x, int N, int H, in
                                float* dw_kcrs, void* ws, size_t ws_bytes, void* stream) {
   if (Cp % 4 || !aligned16(x)) return DK_ERR_ARGS;
   const int M = K, Ncol = R * S * Cp, Kred = N * OH * OW;
+  if (!fits((size_t)Kred * K * 4) || !fits((size_t)N * H * W * Cp * 4)) return DK_ERR_ARGS;
   if (ws_bytes < splitk_ws_bytes(M, Ncol, Kred)) return DK_ERR_WORKSPACE;
-  MatDesc a = mat(dy, K, K, Kred);
-  ImgDesc b{x, H, W, Cp, OH, OW, R, S, stride, 1, -pad, Kred};
+  MatDesc a = mat(dy, Kred, K, K);
+  ImgDesc b = img(x, N, H, W, Cp, OH, OW, R, S, stride, 1, -pad, Kred);
   int splits = 1;
-  int rc = igemm_splitk<LdMatIC, MatDesc, LdImgIC, ImgDesc>(a, b, static_cast<float*>(ws), M, Ncol, Kred,
-                                                              as_stream(stream), &splits);
+  float* part = static_cast<float*>(ws);
+  int rc = vec_ok(a, 4, K)
+               ? igemm_splitk<LdMatIC, MatDesc, LdImgIC, ImgDesc>(a, b, part, M, Ncol, Kred, as_stream(stream), &splits)
+               : igemm_splitk<LdMatIC1, MatDesc, LdImgIC, ImgDesc>(a, b, part, M, Ncol, Kred, as_stream(stream),
+                                                                   &splits);
   if (rc) return rc;
   return splitk_reduce(static_cast<float*>(ws), splits, M, Ncol, dw_kcrs, w_kcrs, l2, 1, C, Cp, R, S,
                        as_stream(stream));
@@ -621,10 +758,16 @@ DK_API int dk_conv2d_wgrad_f32(const float* dy, const float* x, int N, int H, in
 // y[n,oh,ow,k] = sum_c x[n, oh*s, ow*s, c] * w[k][c] (+ bias)
 DK_API int dk_pwconv_fwd_f32(const float* x, int N, int H, int W, int C, const float* w_kc, int K, int stride,
                              const float* bias, float* y, int OH, int OW, void* stream) {
-  if (C % 4 || !aligned16(x)) return DK_ERR_ARGS;
-  ImgDesc a{x, H, W, C, OH, OW, 1, 1, stride, 1, 0, N * OH * OW};
-  MatDesc b = mat(w_kc, C, K, C);
-  EpStore ep{y, K, bias, OH, OW, 1};
+  if (!fits((size_t)N * H * W * C * 4)) return DK_ERR_ARGS;
+  MatDesc b = mat(w_kc, K, C, K);
+  EpStore ep{y, K, bias};
+  if (C % 4 || !aligned16(x) || !aligned16(w_kc)) {
+    // Unaligned channel count: scalar loads, stride 1 only (the rows are then a plain matrix).
+    if (stride != 1) return DK_ERR_ARGS;
+    MatDesc a = mat(x, N * H * W, C, N * H * W);
+    return igemm_rows<LdMatKC1, MatDesc, LdMatKC1, MatDesc, EpStore>(a, b, ep, N * H * W, K, C, as_stream(stream));
+  }
+  ImgDesc a = img(x, N, H, W, C, OH, OW, 1, 1, stride, 1, 0, N * OH * OW);
   return igemm_rows<LdImgKC, ImgDesc, LdMatKC, MatDesc, EpStore>(a, b, ep, N * OH * OW, K, C, as_stream(stream));
 }
 
@@ -632,11 +775,20 @@ DK_API int dk_pwconv_fwd_f32(const float* x, int N, int H, int W, int C, const f
 // result is widened to (OH*s, OW*s) with zeros off the sampling lattice.
 DK_API int dk_pwconv_dgrad_f32(const float* dy, int N, int OH, int OW, int K, const float* w_kc, int C, int stride,
                                float* dx, void* stream) {
-  if (K % 4 || !aligned16(dy)) return DK_ERR_ARGS;
-  ImgDesc a{dy, OH, OW, K, OH, OW, 1, 1, 1, 1, 0, N * OH * OW};
-  MatDesc b = mat(w_kc, C, C, K);
-  EpStore ep{dx, C, nullptr, OH, OW, stride};
-  return igemm_rows<LdImgKC, ImgDesc, LdMatIC, MatDesc, EpStore>(a, b, ep, N * OH * OW, C, K, as_stream(stream));
+  const int M = N * OH * OW;
+  if (!fits((size_t)M * K * 4)) return DK_ERR_ARGS;
+  MatDesc a = mat(dy, M, K, M);
+  MatDesc b = mat(w_kc, K, C, C);
+  const hipStream_t st = as_stream(stream);
+  const bool vec = vec_ok(a, K, 4) && vec_ok(b, 4, C);
+  if (stride == 1) {
+    EpStore ep{dx, C, nullptr};
+    if (vec) return igemm_rows<LdMatKC, MatDesc, LdMatIC, MatDesc, EpStore>(a, b, ep, M, C, K, st);
+    return igemm_rows<LdMatKC1, MatDesc, LdMatIC1, MatDesc, EpStore>(a, b, ep, M, C, K, st);
+  }
+  EpWiden ep{dx, C, OH, OW, stride};
+  if (vec) return igemm_rows<LdMatKC, MatDesc, LdMatIC, MatDesc, EpWiden>(a, b, ep, M, C, K, st);
+  return igemm_rows<LdMatKC1, MatDesc, LdMatIC1, MatDesc, EpWiden>(a, b, ep, M, C, K, st);
 }
 
 DK_API size_t dk_pwconv_wgrad_workspace_bytes(int N, int OH, int OW, int K, int C) {
@@ -649,12 +801,15 @@ DK_API int dk_pwconv_wgrad_f32(const float* dy, const float* x, int N, int H, in
                                void* stream) {
   if (C % 4 || !aligned16(x)) return DK_ERR_ARGS;
   const int Kred = N * OH * OW;
+  if (!fits((size_t)Kred * K * 4) || !fits((size_t)N * H * W * C * 4)) return DK_ERR_ARGS;
   if (ws_bytes < splitk_ws_bytes(K, C, Kred)) return DK_ERR_WORKSPACE;
-  MatDesc a = mat(dy, K, K, Kred);
-  ImgDesc b{x, H, W, C, OH, OW, 1, 1, stride, 1, 0, Kred};
+  MatDesc a = mat(dy, Kred, K, K);
+  ImgDesc b = img(x, N, H, W, C, OH, OW, 1, 1, stride, 1, 0, Kred);
   int splits = 1;
-  int rc = igemm_splitk<LdMatIC, MatDesc, LdImgIC, ImgDesc>(a, b, static_cast<float*>(ws), K, C, Kred,
-                                                              as_stream(stream), &splits);
+  float* part = static_cast<float*>(ws);
+  int rc = vec_ok(a, 4, K)
+               ? igemm_splitk<LdMatIC, MatDesc, LdImgIC, ImgDesc>(a, b, part, K, C, Kred, as_stream(stream), &splits)
+               : igemm_splitk<LdMatIC1, MatDesc, LdImgIC, ImgDesc>(a, b, part, K, C, Kred, as_stream(stream), &splits);
   if (rc) return rc;
   return splitk_reduce(static_cast<float*>(ws), splits, K, C, dw_kc, w_kc, l2, 0, C, C, 1, 1, as_stream(stream));
 }
@@ -662,18 +817,24 @@ DK_API int dk_pwconv_wgrad_f32(const float* dy, const float* x, int N, int H, in
 // Dense (dense_layer.py:46-55): y[b][o] = sum_i x[b][i] * w[i][o] (+ bias[o]);  w stored (in, out).
 DK_API int dk_dense_fwd_f32(const float* x, int B, int IN, const float* w_io, int OUT, const float* bias, float* y,
                             void* stream) {
-  MatDesc a = mat(x, IN, B, IN);
-  MatDesc b = mat(w_io, OUT, OUT, IN);
-  EpStore ep{y, OUT, bias, 1, 1, 1};
-  return igemm_rows<LdMatKC, MatDesc, LdMatIC, MatDesc, EpStore>(a, b, ep, B, OUT, IN, as_stream(stream));
+  MatDesc a = mat(x, B, IN, B);
+  MatDesc b = mat(w_io, IN, OUT, OUT);
+  EpStore ep{y, OUT, bias};
+  const hipStream_t st = as_stream(stream);
+  const bool va = vec_ok(a, IN, 4), vb = vec_ok(b, 4, OUT);
+  if (va && vb) return igemm_rows<LdMatKC, MatDesc, LdMatIC, MatDesc, EpStore>(a, b, ep, B, OUT, IN, st);
+  return igemm_rows<LdMatKC1, MatDesc, LdMatIC1, MatDesc, EpStore>(a, b, ep, B, OUT, IN, st);
 }
 
 // dx[b][i] = sum_o dy[b][o] * w[i][o]   (dense_layer.py:67)
 DK_API int dk_dense_dgrad_f32(const float* dy, int B, int OUT, const float* w_io, int IN, float* dx, void* stream) {
-  MatDesc a = mat(dy, OUT, B, OUT);
-  MatDesc b = mat(w_io, OUT, IN, OUT);
-  EpStore ep{dx, IN, nullptr, 1, 1, 1};
-  return igemm_rows<LdMatKC, MatDesc, LdMatKC, MatDesc, EpStore>(a, b, ep, B, IN, OUT, as_stream(stream));
+  MatDesc a = mat(dy, B, OUT, B);
+  MatDesc b = mat(w_io, IN, OUT, IN);
+  EpStore ep{dx, IN, nullptr};
+  const hipStream_t st = as_stream(stream);
+  if (vec_ok(a, OUT, 4) && vec_ok(b, OUT, 4))
+    return igemm_rows<LdMatKC, MatDesc, LdMatKC, MatDesc, EpStore>(a, b, ep, B, IN, OUT, st);
+  return igemm_rows<LdMatKC1, MatDesc, LdMatKC1, MatDesc, EpStore>(a, b, ep, B, IN, OUT, st);
 }
 
 DK_API size_t dk_dense_wgrad_workspace_bytes(int B, int IN, int OUT) { return splitk_ws_bytes(IN, OUT, B); }
@@ -682,12 +843,15 @@ DK_API size_t dk_dense_wgrad_workspace_bytes(int B, int IN, int OUT) { return sp
 DK_API int dk_dense_wgrad_f32(const float* x, const float* dy, int B, int IN, int OUT, const float* w_io, float l2,
                               float* dw_io, void* ws, size_t ws_bytes, void* stream) {
   if (ws_bytes < splitk_ws_bytes(IN, OUT, B)) return DK_ERR_WORKSPACE;
-  MatDesc a = mat(x, IN, IN, B);
-  MatDesc b = mat(dy, OUT, OUT, B);
+  MatDesc a = mat(x, B, IN, IN);
+  MatDesc b = mat(dy, B, OUT, OUT);
   int splits = 1;
-  int rc = igemm_splitk<LdMatIC, MatDesc, LdMatIC, MatDesc>(a, b, static_cast<float*>(ws), IN, OUT, B,
-                                                              as_stream(stream), &splits);
+  const hipStream_t st = as_stream(stream);
+  int rc;
+  if (vec_ok(a, 4, IN) && vec_ok(b, 4, OUT))
+    rc = igemm_splitk<LdMatIC, MatDesc, LdMatIC, MatDesc>(a, b, static_cast<float*>(ws), IN, OUT, B, st, &splits);
+  else
+    rc = igemm_splitk<LdMatIC1, MatDesc, LdMatIC1, MatDesc>(a, b, static_cast<float*>(ws), IN, OUT, B, st, &splits);
   if (rc) return rc;
-  return splitk_reduce(static_cast<float*>(ws), splits, IN, OUT, dw_io, w_io, l2, 0, OUT, OUT, 1, 1,
-                       as_stream(stream));
+  return splitk_reduce(static_cast<float*>(ws), splits, IN, OUT, dw_io, w_io, l2, 0, OUT, OUT, 1, 1, st);
 }

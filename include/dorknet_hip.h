@@ -31,6 +31,11 @@ extern "C" {
 
 int dk_abi_version(void);
 
+/* Tuning knob (not for production use; not thread-safe): force GEMM tile configuration
+ * `cfg` for kind 0 = forward/dgrad problems or 1 = split-K weight-gradient problems;
+ * cfg = -1 restores the built-in heuristic.  Returns the number of configurations. */
+int dk_debug_set_gemm_config(int kind, int cfg);
+
 /* ---------------------------------------------------------------------------------------
  * Dense convolution, implicit GEMM on fp32 MFMA.
  * Replaces ConvLayer.forward GPU branch (layers/convolution.py:58-87: pad_input :144-151,

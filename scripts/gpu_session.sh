@@ -16,7 +16,7 @@ timeout -k 10 600 python bench.py --steps 10 --warmup 3 > "$OUT/bench_$TAG.json"
 rc=$?; cat "$OUT/bench_$TAG.json"; tail -5 "$OUT/bench_$TAG.err"; step bench $rc
 
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$TAG" -o bench -- \
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/prof_$TAG" -o bench -- \
     python "$ROOT/bench.py" --steps 5 --warmup 2 --cpu-sample 0 > "$OUT/prof_bench_$TAG.json" 2> "$OUT/prof_$TAG.err"
 rc=$?; step rocprof $rc
-find "$OUT/prof_$TAG" -name "*kernel_stats.csv" | head -3
+find "$OUT/prof_$TAG" -name "*kernel_stats.csv"
