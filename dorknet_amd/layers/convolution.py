@@ -118,6 +118,11 @@ class ConvLayer(Layer):
             lib.dk_conv_weight_crsk_f32(w.data_ptr(), K, C, R, S, w_crsk.data_ptr(), st)
             lib.dk_conv2d_dgrad_f32(dy.data_ptr(), N, OH, OW, K, w_crsk.data_ptr(), C, R, S, self.padding,
                                     dx.data_ptr(), Hin, Win, st)
+        elif lib.dk_conv2d_dgrad_subpixel_workspace_bytes(K, C, R, S, self.stride, self.padding):
+            # strided, narrow input (the stem): sub-pixel gather, no column matrix
+            nb = lib.dk_conv2d_dgrad_subpixel_workspace_bytes(K, C, R, S, self.stride, self.padding)
+            lib.dk_conv2d_dgrad_subpixel_f32(dy.data_ptr(), N, OH, OW, K, w.data_ptr(), C, R, S, self.stride,
+                                             self.padding, dx.data_ptr(), Hin, Win, workspace.get(nb), nb, st)
         else:
             nb = lib.dk_conv2d_dgrad_cols_workspace_bytes(N, OH, OW, C, R, S)
             lib.dk_conv2d_dgrad_strided_f32(dy.data_ptr(), N, OH, OW, K, w.data_ptr(), C, R, S, self.stride,

@@ -123,6 +123,7 @@ MODEL = {
     "dk_conv2d_fwd_f32": _conv_fwd,
     "dk_conv2d_dgrad_f32": _conv_dgrad,
     "dk_conv2d_dgrad_strided_f32": _conv_dgrad_strided,
+    "dk_conv2d_dgrad_subpixel_f32": _conv_dgrad_strided,
     "dk_conv2d_wgrad_f32": _conv_wgrad,
     "dk_pwconv_fwd_f32": _pw_fwd,
     "dk_pwconv_dgrad_f32": _pw_dgrad,

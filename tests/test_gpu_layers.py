@@ -66,6 +66,9 @@ CONV_CASES = [
     (40, 12, 3, 3, 1, 0, 2, 10, 10, True, 0.0),     # K not a multiple of 32, no padding
     (32, 1, 3, 3, 1, 1, 2, 28, 28, False, 1e-4),    # MNIST conv_1 (C=1)
     (130, 68, 3, 3, 1, 1, 1, 6, 5, False, 1e-4),    # K > 128 tile, ragged M
+    (70, 5, 3, 3, 2, 1, 2, 33, 150, False, 0.0),    # sub-pixel dgrad: K % 4 != 0, 2 channel groups, 2 column tiles
+    (8, 3, 7, 7, 2, 3, 1, 20, 19, True, 0.0),       # sub-pixel dgrad, 7x7 stem geometry
+    (6, 20, 3, 3, 2, 1, 2, 9, 9, False, 0.0),       # strided, C > 16: column-matrix dgrad path
 ]
 
 
