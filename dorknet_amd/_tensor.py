@@ -21,6 +21,8 @@ def device() -> torch.device:
 def as_device(x, dtype=F32) -> torch.Tensor:
     """numpy / torch (any device) -> torch tensor on the current HIP device (the
     cp.asarray of the reference's training loop, examples/...depsep.py:219-221)."""
+    if hasattr(x, "materialize"):  # a BatchNorm output not yet written (layers/_bn_input.BNOut)
+        x = x.materialize()
     if isinstance(x, torch.Tensor):
         if x.device.type != "cuda" or x.dtype != dtype:
             x = x.to(device=device(), dtype=dtype)

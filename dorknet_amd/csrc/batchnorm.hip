@@ -19,12 +19,6 @@
 
 namespace dk {
 
-// The BN output for one element.  Forward apply and the backward ReLU-mask
-// recompute call this same function so the mask is bit-identical to forward.
-__device__ __forceinline__ float bn_out(float x, float mean, float invstd, float gamma, float beta) {
-  const float xh = (x - mean) * invstd;
-  return gamma * xh + beta;
-}
 
 template <int V>
 struct VecT;

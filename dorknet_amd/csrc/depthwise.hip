@@ -16,7 +16,6 @@
 
 namespace dk {
 
-constexpr int kTW = 8;  // outputs per thread along W
 
 // w[c][r][s] -> wt[r][s][c] (flip != 0: wt[r][s][c] = w[c][R-1-r][S-1-s]) so one float4
 // load fetches a tap for 4 channels.
@@ -33,14 +32,62 @@ __global__ void dw_weight_rsc_kernel(const float* __restrict__ w, int C, int R, 
   wt[idx] = w[((size_t)c * R + r) * S + s];
 }
 
+// Buffer loads: out-of-range offsets (kOOB) return 0 in hardware, so the padding needs no
+// branches and every load of a thread can be in flight at once.
+constexpr uint32_t kOOB = 0x80000000u;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const float* p, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p), (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ f32x4 bload4(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0));
+}
+
+// Outputs per thread along W: the input strip R x ((TW-1)*ST + S) float4s is loaded at once.
+template <int ST>
+struct DwTile {
+  static constexpr int TW = ST == 1 ? 8 : 4;
+};
+
+// Loads the R x NC input strip whose top-left tap is (ih0, iw0); with BN, every in-image
+// element is replaced by bn(x) (+ReLU) -- padding stays 0.
+template <int R, int NC, bool BN>
+__device__ __forceinline__ void load_strip(f32x4 (&strip)[R][NC], __amdgpu_buffer_rsrc_t rs, int n, int ih0, int iw0,
+                                           int H, int W, int C, int c, const BnIn& bn) {
+  bool ok[R][NC];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int ih = ih0 + r;
+#pragma unroll
+    for (int q = 0; q < NC; ++q) {
+      const int iw = iw0 + q;
+      ok[r][q] = (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
+      strip[r][q] = bload4(rs, ok[r][q] ? (uint32_t)(((n * H + ih) * W + iw) * C + c) * 4u : kOOB);
+    }
+  }
+  if constexpr (BN) {
+    const f32x4 m = ld4(bn.mean + c), is = ld4(bn.invstd + c), g = ld4(bn.gamma + c), b = ld4(bn.beta + c);
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+      for (int q = 0; q < NC; ++q) {
+        const f32x4 t = bn_in4(strip[r][q], m, is, g, b, bn.relu);
+        strip[r][q] = ok[r][q] ? t : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+  }
+}
+
 // y[n,oh,ow,c] = sum_{r,s} w[r][s][c] * x[n, oh*ST + r - pad, ow*ST + s - pad, c] (+ bias[c])
-// Thread = (n, oh, TW-wide chunk of ow, 4 channels).
-template <int R, int S, int ST>
-__global__ __launch_bounds__(256) void dw_fwd_kernel(const float* __restrict__ x, const float* __restrict__ wt,
-                                                     const float* __restrict__ bias, float* __restrict__ y, int N,
-                                                     int H, int W, int C, int OH, int OW, int pad) {
+// Thread = (n, oh, TW-wide chunk of ow, 4 channels); consecutive threads take consecutive
+// channel groups, so a wave reads whole pixel rows.
+template <int R, int S, int ST, bool BN>
+__global__ __launch_bounds__(256) void dw_fwd_kernel(const float* __restrict__ x, uint32_t xbytes,
+                                                     const float* __restrict__ wt, const float* __restrict__ bias,
+                                                     float* __restrict__ y, int N, int H, int W, int C, int OH, int OW,
+                                                     int pad, BnIn bn) {
+  constexpr int TW = DwTile<ST>::TW;
+  constexpr int NC = (TW - 1) * ST + S;
   const int C4 = C >> 2;
-  const int nwc = (OW + kTW - 1) / kTW;
+  const int nwc = (OW + TW - 1) / TW;
   const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const long long total = (long long)N * OH * nwc * C4;
   if (idx >= total) return;
@@ -51,55 +98,24 @@ __global__ __launch_bounds__(256) void dw_fwd_kernel(const float* __restrict__ x
   const int oh = (int)(t % OH);
   const int n = (int)(t / OH);
   const int c = cq * 4;
+  const int ow0 = wc * TW;
+  f32x4 strip[R][NC];
+  load_strip<R, NC, BN>(strip, make_rsrc(x, xbytes), n, oh * ST - pad, ow0 * ST - pad, H, W, C, c, bn);
   f32x4 wv[R][S];
 #pragma unroll
   for (int r = 0; r < R; ++r)
 #pragma unroll
     for (int s = 0; s < S; ++s) wv[r][s] = ld4(wt + (r * S + s) * C + c);
   const f32x4 b0 = bias ? ld4(bias + c) : f32x4{0.f, 0.f, 0.f, 0.f};
-  const int ow0 = wc * kTW;
-  const int ih0 = oh * ST - pad;
-  const int iw0 = ow0 * ST - pad;
-  bool rv[R];
-  const float* rowp[R];
-#pragma unroll
-  for (int r = 0; r < R; ++r) {
-    const int ih = ih0 + r;
-    rv[r] = (unsigned)ih < (unsigned)H;
-    rowp[r] = x + ((size_t)(n * H + (rv[r] ? ih : 0)) * W) * C + c;
-  }
-  auto load_col = [&](int r, int iw) -> f32x4 {
-    return (rv[r] && (unsigned)iw < (unsigned)W) ? ld4(rowp[r] + (size_t)iw * C) : f32x4{0.f, 0.f, 0.f, 0.f};
-  };
-  f32x4 win[R][S];
-#pragma unroll
-  for (int r = 0; r < R; ++r)
-#pragma unroll
-    for (int s = 0; s < S; ++s) win[r][s] = load_col(r, iw0 + s);
   float* yrow = y + ((size_t)(n * OH + oh) * OW) * C + c;
 #pragma unroll
-  for (int j = 0; j < kTW; ++j) {
-    if (j > 0) {
+  for (int j = 0; j < TW; ++j) {
+    f32x4 acc = b0;
 #pragma unroll
-      for (int r = 0; r < R; ++r) {
+    for (int r = 0; r < R; ++r)
 #pragma unroll
-        for (int s = 0; s < S; ++s) {
-          if (s + ST < S)
-            win[r][s] = win[r][s + ST];
-          else
-            win[r][s] = load_col(r, iw0 + j * ST + s);
-        }
-      }
-    }
-    const int ow = ow0 + j;
-    if (ow < OW) {
-      f32x4 acc = b0;
-#pragma unroll
-      for (int r = 0; r < R; ++r)
-#pragma unroll
-        for (int s = 0; s < S; ++s) acc += win[r][s] * wv[r][s];
-      st4(yrow + (size_t)ow * C, acc);
-    }
+      for (int s = 0; s < S; ++s) acc += strip[r][j * ST + s] * wv[r][s];
+    if (ow0 + j < OW) st4(yrow + (size_t)(ow0 + j) * C, acc);
   }
 }
 
@@ -142,13 +158,20 @@ __global__ __launch_bounds__(256) void dw_dgrad_gather_kernel(const float* __res
 
 // wgrad partials: part[blk][c][r*S+s] = sum over the block's (n, oh, ow-chunk) items of
 // dy[n,oh,ow,c] * x[n, oh*ST + r - pad, ow*ST + s - pad, c].  Thread (cq, pl): channel group
-// cq, walks items pl, pl + PL, ... with the same sliding window as the forward kernel.
-template <int R, int S, int ST>
-__global__ __launch_bounds__(256) void dw_wgrad_partial_kernel(const float* __restrict__ dy,
-                                                               const float* __restrict__ x,
+// cq, walks items pl, pl + PL, ...; per item it loads the input strip and TW dy values at once.
+template <int ST>
+struct DwWgTile {
+  static constexpr int TW = ST == 1 ? 4 : 2;
+};
+
+template <int R, int S, int ST, bool BN>
+__global__ __launch_bounds__(256) void dw_wgrad_partial_kernel(const float* __restrict__ dy, uint32_t dybytes,
+                                                               const float* __restrict__ x, uint32_t xbytes,
                                                                float* __restrict__ part, int N, int H, int W,
-                                                               int C, int OH, int OW, int pad, int ipb) {
+                                                               int C, int OH, int OW, int pad, int ipb, BnIn bn) {
   constexpr int RS = R * S;
+  constexpr int TW = DwWgTile<ST>::TW;
+  constexpr int NC = (TW - 1) * ST + S;
   extern __shared__ float red[];  // [256][RS][4]
   const int C4 = C >> 2;
   const int cgt = C4 < 256 ? C4 : 256;
@@ -158,9 +181,10 @@ __global__ __launch_bounds__(256) void dw_wgrad_partial_kernel(const float* __re
   const int pl = tid / cgt;
   const bool active = pl < PL && cq < C4;
   const int c = cq * 4;
-  const int nwc = (OW + kTW - 1) / kTW;
+  const int nwc = (OW + TW - 1) / TW;
   const int items = N * OH * nwc;
   const int i0 = blockIdx.x * ipb, i1 = min(items, i0 + ipb);
+  const __amdgpu_buffer_rsrc_t rx = make_rsrc(x, xbytes), rg = make_rsrc(dy, dybytes);
   f32x4 acc[R][S];
 #pragma unroll
   for (int r = 0; r < R; ++r)
@@ -172,49 +196,19 @@ __global__ __launch_bounds__(256) void dw_wgrad_partial_kernel(const float* __re
       const int t = it / nwc;
       const int oh = t % OH;
       const int n = t / OH;
-      const int ow0 = wc * kTW;
-      const int ih0 = oh * ST - pad;
-      const int iw0 = ow0 * ST - pad;
-      bool rv[R];
-      const float* rowp[R];
+      const int ow0 = wc * TW;
+      f32x4 g[TW];
 #pragma unroll
-      for (int r = 0; r < R; ++r) {
-        const int ih = ih0 + r;
-        rv[r] = (unsigned)ih < (unsigned)H;
-        rowp[r] = x + ((size_t)(n * H + (rv[r] ? ih : 0)) * W) * C + c;
-      }
-      auto load_col = [&](int r, int iw) -> f32x4 {
-        return (rv[r] && (unsigned)iw < (unsigned)W) ? ld4(rowp[r] + (size_t)iw * C)
-                                                     : f32x4{0.f, 0.f, 0.f, 0.f};
-      };
-      f32x4 win[R][S];
+      for (int j = 0; j < TW; ++j)
+        g[j] = bload4(rg, ow0 + j < OW ? (uint32_t)(((n * OH + oh) * OW + ow0 + j) * C + c) * 4u : kOOB);
+      f32x4 strip[R][NC];
+      load_strip<R, NC, BN>(strip, rx, n, oh * ST - pad, ow0 * ST - pad, H, W, C, c, bn);
 #pragma unroll
-      for (int r = 0; r < R; ++r)
+      for (int j = 0; j < TW; ++j)
 #pragma unroll
-        for (int s = 0; s < S; ++s) win[r][s] = load_col(r, iw0 + s);
-      const float* grow = dy + ((size_t)(n * OH + oh) * OW) * C + c;
+        for (int r = 0; r < R; ++r)
 #pragma unroll
-      for (int j = 0; j < kTW; ++j) {
-        if (j > 0) {
-#pragma unroll
-          for (int r = 0; r < R; ++r)
-#pragma unroll
-            for (int s = 0; s < S; ++s) {
-              if (s + ST < S)
-                win[r][s] = win[r][s + ST];
-              else
-                win[r][s] = load_col(r, iw0 + j * ST + s);
-            }
-        }
-        const int ow = ow0 + j;
-        if (ow < OW) {
-          const f32x4 g = ld4(grow + (size_t)ow * C);
-#pragma unroll
-          for (int r = 0; r < R; ++r)
-#pragma unroll
-            for (int s = 0; s < S; ++s) acc[r][s] += g * win[r][s];
-        }
-      }
+          for (int s = 0; s < S; ++s) acc[r][s] += g[j] * strip[r][j * ST + s];
     }
   }
 #pragma unroll
@@ -227,25 +221,68 @@ __global__ __launch_bounds__(256) void dw_wgrad_partial_kernel(const float* __re
   for (int k = tid; k < nitems; k += 256) {
     const int e = k % 4;
     const int tap = (k / 4) % RS;
-    const int g = k / (4 * RS);
-    if (blockIdx.y * cgt + g >= C4) continue;
+    const int gq = k / (4 * RS);
+    if (blockIdx.y * cgt + gq >= C4) continue;
     float sum = 0.f;
-    for (int q = 0; q < PL; ++q) sum += red[((q * cgt + g) * RS + tap) * 4 + e];
-    const int cc = (blockIdx.y * cgt + g) * 4 + e;
+    for (int q = 0; q < PL; ++q) sum += red[((q * cgt + gq) * RS + tap) * 4 + e];
+    const int cc = (blockIdx.y * cgt + gq) * 4 + e;
     part[((size_t)blockIdx.x * C + cc) * RS + tap] = sum;
   }
 }
 
 static int dw_wgrad_blocks(int N, int OH, int OW, int C) {
-  const int items = N * OH * ((OW + kTW - 1) / kTW);
   const int C4 = C / 4;
   const int cgt = C4 < 256 ? C4 : 256;
   const int PL = 256 / cgt;
-  int nblk = cdiv(items, PL * 4);  // ~4 items (32 outputs) per thread
+  int nblk = (int)cdivll((long long)N * OH * OW, (long long)PL * 16);  // ~16 outputs per thread
   if (nblk > 1024) nblk = 1024;
   if (nblk < 1) nblk = 1;
   return nblk;
 }
+
+static inline bool fits(size_t bytes) { return bytes < ((size_t)1 << 31); }
+static inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+static inline bool bn_ok(const BnIn& bn) {
+  return !bn.mean || (bn.invstd && bn.gamma && bn.beta && aligned16(bn.mean) && aligned16(bn.invstd) &&
+                      aligned16(bn.gamma) && aligned16(bn.beta));
+}
+
+template <int R, int S, int ST>
+static void launch_dw_fwd(const float* x, const float* wt, const float* bias, float* y, int N, int H, int W, int C,
+                          int OH, int OW, int pad, const BnIn& bn, hipStream_t st) {
+  constexpr int TW = DwTile<ST>::TW;
+  const long long total = (long long)N * OH * ((OW + TW - 1) / TW) * (C / 4);
+  const uint32_t xb = (uint32_t)((size_t)N * H * W * C * sizeof(float));
+  const dim3 grid((unsigned)cdivll(total, 256));
+  if (bn.mean)
+    hipLaunchKernelGGL((dw_fwd_kernel<R, S, ST, true>), grid, dim3(256), 0, st, x, xb, wt, bias, y, N, H, W, C, OH, OW,
+                       pad, bn);
+  else
+    hipLaunchKernelGGL((dw_fwd_kernel<R, S, ST, false>), grid, dim3(256), 0, st, x, xb, wt, bias, y, N, H, W, C, OH,
+                       OW, pad, bn);
+}
+
+static int dw_fwd_dispatch(const float* x, const float* wt, const float* bias, float* y, int N, int H, int W, int C,
+                           int R, int S, int stride, int OH, int OW, int pad, const BnIn& bn, hipStream_t st) {
+  if (C % 4 || !aligned16(x) || !aligned16(wt) || !fits((size_t)N * H * W * C * 4) || !bn_ok(bn)) return DK_ERR_ARGS;
+#define DW_CASE(RR, SS, STR)                                                      \
+  if (R == RR && S == SS && stride == STR) {                                      \
+    launch_dw_fwd<RR, SS, STR>(x, wt, bias, y, N, H, W, C, OH, OW, pad, bn, st);  \
+    return launch_status();                                                       \
+  }
+  DW_CASE(3, 3, 1)
+  DW_CASE(3, 3, 2)
+  DW_CASE(5, 5, 1)
+  DW_CASE(5, 5, 2)
+  DW_CASE(1, 1, 1)
+  DW_CASE(1, 1, 2)
+#undef DW_CASE
+  return DK_ERR_ARGS;
+}
+
+static int dw_wgrad(const float* dy, const float* x, int N, int H, int W, int C, int R, int S, int stride, int pad,
+                    int OH, int OW, const float* w_crs, float l2, float* dw_crs, void* ws, size_t ws_bytes,
+                    const BnIn& bn, hipStream_t st);
 
 }  // namespace dk
 
@@ -258,35 +295,18 @@ DK_API int dk_dw_weight_rsc_f32(const float* w_crs, int C, int R, int S, float* 
   return launch_status();
 }
 
-template <int R, int S, int ST>
-static void launch_dw_fwd(const float* x, const float* wt, const float* bias, float* y, int N, int H, int W, int C,
-                          int OH, int OW, int pad, hipStream_t st) {
-  const long long total = (long long)N * OH * ((OW + kTW - 1) / kTW) * (C / 4);
-  hipLaunchKernelGGL((dw_fwd_kernel<R, S, ST>), dim3((unsigned)cdivll(total, 256)), dim3(256), 0, st, x, wt, bias, y,
-                     N, H, W, C, OH, OW, pad);
-}
-
-static int dw_fwd_dispatch(const float* x, const float* wt, const float* bias, float* y, int N, int H, int W, int C,
-                           int R, int S, int stride, int OH, int OW, int pad, hipStream_t st) {
-#define DW_CASE(RR, SS, STR)                                                   \
-  if (R == RR && S == SS && stride == STR) {                                   \
-    launch_dw_fwd<RR, SS, STR>(x, wt, bias, y, N, H, W, C, OH, OW, pad, st);   \
-    return launch_status();                                                    \
-  }
-  DW_CASE(3, 3, 1)
-  DW_CASE(3, 3, 2)
-  DW_CASE(5, 5, 1)
-  DW_CASE(5, 5, 2)
-  DW_CASE(1, 1, 1)
-  DW_CASE(1, 1, 2)
-#undef DW_CASE
-  return DK_ERR_ARGS;
-}
-
 DK_API int dk_dwconv_fwd_f32(const float* x, int N, int H, int W, int C, const float* w_rsc, int R, int S, int stride,
                              int pad, const float* bias, float* y, int OH, int OW, void* stream) {
-  if (C % 4) return DK_ERR_ARGS;
-  return dw_fwd_dispatch(x, w_rsc, bias, y, N, H, W, C, R, S, stride, OH, OW, pad, as_stream(stream));
+  return dw_fwd_dispatch(x, w_rsc, bias, y, N, H, W, C, R, S, stride, OH, OW, pad, BnIn{}, as_stream(stream));
+}
+
+DK_API int dk_dwconv_fwd_bnx_f32(const float* x, int N, int H, int W, int C, const float* w_rsc, int R, int S,
+                                 int stride, int pad, const float* bias, float* y, int OH, int OW,
+                                 const float* bn_mean, const float* bn_invstd, const float* bn_gamma,
+                                 const float* bn_beta, int bn_relu, void* stream) {
+  if (!bn_mean) return DK_ERR_ARGS;
+  return dw_fwd_dispatch(x, w_rsc, bias, y, N, H, W, C, R, S, stride, OH, OW, pad,
+                         BnIn{bn_mean, bn_invstd, bn_gamma, bn_beta, bn_relu}, as_stream(stream));
 }
 
 // w_rsc is the (unflipped) [R][S][C] copy; stride-1 dgrad flips it internally into ws.
@@ -304,7 +324,7 @@ DK_API int dk_dwconv_dgrad_f32(const float* dy, int N, int OH, int OW, int C, co
     hipLaunchKernelGGL(dw_weight_rsc_kernel, dim3(cdiv(C * R * S, 256)), dim3(256), 0, st, w_crs, C, R, S, 1, wt);
     int rc = launch_status();
     if (rc) return rc;
-    return dw_fwd_dispatch(dy, wt, nullptr, dx, N, OH, OW, C, R, S, 1, H, W, R - 1 - pad, st);
+    return dw_fwd_dispatch(dy, wt, nullptr, dx, N, OH, OW, C, R, S, 1, H, W, R - 1 - pad, BnIn{}, st);
   }
   hipLaunchKernelGGL(dw_weight_rsc_kernel, dim3(cdiv(C * R * S, 256)), dim3(256), 0, st, w_crs, C, R, S, 0, wt);
   int rc = launch_status();
@@ -329,28 +349,36 @@ DK_API size_t dk_dwconv_wgrad_workspace_bytes(int N, int OH, int OW, int C, int 
   return (size_t)dw_wgrad_blocks(N, OH, OW, C) * C * R * S * sizeof(float);
 }
 
-// dw[c][r][s] = sum_{n,oh,ow} dy[n,oh,ow,c] * x[n, oh*st + r - pad, ow*st + s - pad, c] (+ l2 * w)
-DK_API int dk_dwconv_wgrad_f32(const float* dy, const float* x, int N, int H, int W, int C, int R, int S, int stride,
-                               int pad, int OH, int OW, const float* w_crs, float l2, float* dw_crs, void* ws,
-                               size_t ws_bytes, void* stream) {
-  if (C % 4) return DK_ERR_ARGS;
+namespace dk {
+static int dw_wgrad(const float* dy, const float* x, int N, int H, int W, int C, int R, int S, int stride, int pad,
+                    int OH, int OW, const float* w_crs, float l2, float* dw_crs, void* ws, size_t ws_bytes,
+                    const BnIn& bn, hipStream_t st) {
+  if (C % 4 || !aligned16(x) || !aligned16(dy) || !bn_ok(bn)) return DK_ERR_ARGS;
+  if (!fits((size_t)N * H * W * C * 4) || !fits((size_t)N * OH * OW * C * 4)) return DK_ERR_ARGS;
   if (ws_bytes < dk_dwconv_wgrad_workspace_bytes(N, OH, OW, C, R, S)) return DK_ERR_WORKSPACE;
   const int nblk = dw_wgrad_blocks(N, OH, OW, C);
-  const int items = N * OH * ((OW + kTW - 1) / kTW);
-  const int ipb = cdiv(items, nblk);
   const int C4 = C / 4;
   const int cgt = C4 < 256 ? C4 : 256;
   const dim3 grid(nblk, cdiv(C4, cgt));
   float* part = static_cast<float*>(ws);
   const size_t shm = (size_t)256 * R * S * 4 * sizeof(float);
-  const hipStream_t st = as_stream(stream);
-#define DW_WG(RR, SS, STR)                                                                                          \
-  if (R == RR && S == SS && stride == STR) {                                                                        \
-    if (shm > 65536)                                                                                                \
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&dw_wgrad_partial_kernel<RR, SS, STR>),               \
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);                              \
-    hipLaunchKernelGGL((dw_wgrad_partial_kernel<RR, SS, STR>), grid, dim3(256), shm, st, dy, x, part, N, H, W, C, OH, \
-                       OW, pad, ipb);                                                                               \
+  const uint32_t xb = (uint32_t)((size_t)N * H * W * C * 4), gb = (uint32_t)((size_t)N * OH * OW * C * 4);
+#define DW_WG_LAUNCH(RR, SS, STR, B)                                                                                 \
+  {                                                                                                                  \
+    const int items = N * OH * ((OW + DwWgTile<STR>::TW - 1) / DwWgTile<STR>::TW);                                   \
+    const int ipb = cdiv(items, nblk);                                                                               \
+    if (shm > 65536)                                                                                                 \
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&dw_wgrad_partial_kernel<RR, SS, STR, B>),             \
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);                               \
+    hipLaunchKernelGGL((dw_wgrad_partial_kernel<RR, SS, STR, B>), grid, dim3(256), shm, st, dy, gb, x, xb, part, N,  \
+                       H, W, C, OH, OW, pad, ipb, bn);                                                               \
+  }
+#define DW_WG(RR, SS, STR)                 \
+  if (R == RR && S == SS && stride == STR) { \
+    if (bn.mean)                           \
+      DW_WG_LAUNCH(RR, SS, STR, true)      \
+    else                                   \
+      DW_WG_LAUNCH(RR, SS, STR, false)     \
   } else
   DW_WG(3, 3, 1)
   DW_WG(3, 3, 2)
@@ -359,7 +387,26 @@ DK_API int dk_dwconv_wgrad_f32(const float* dy, const float* x, int N, int H, in
   DW_WG(1, 1, 1)
   DW_WG(1, 1, 2) { return DK_ERR_ARGS; }
 #undef DW_WG
+#undef DW_WG_LAUNCH
   int rc = launch_status();
   if (rc) return rc;
   return splitk_reduce(part, nblk, 1, C * R * S, dw_crs, w_crs, l2, 0, C, C, 1, 1, st);
+}
+}  // namespace dk
+
+// dw[c][r][s] = sum_{n,oh,ow} dy[n,oh,ow,c] * x[n, oh*st + r - pad, ow*st + s - pad, c] (+ l2 * w)
+DK_API int dk_dwconv_wgrad_f32(const float* dy, const float* x, int N, int H, int W, int C, int R, int S, int stride,
+                               int pad, int OH, int OW, const float* w_crs, float l2, float* dw_crs, void* ws,
+                               size_t ws_bytes, void* stream) {
+  return dw_wgrad(dy, x, N, H, W, C, R, S, stride, pad, OH, OW, w_crs, l2, dw_crs, ws, ws_bytes, BnIn{},
+                  as_stream(stream));
+}
+
+DK_API int dk_dwconv_wgrad_bnx_f32(const float* dy, const float* x, int N, int H, int W, int C, int R, int S,
+                                   int stride, int pad, int OH, int OW, const float* w_crs, float l2, float* dw_crs,
+                                   void* ws, size_t ws_bytes, const float* bn_mean, const float* bn_invstd,
+                                   const float* bn_gamma, const float* bn_beta, int bn_relu, void* stream) {
+  if (!bn_mean) return DK_ERR_ARGS;
+  return dw_wgrad(dy, x, N, H, W, C, R, S, stride, pad, OH, OW, w_crs, l2, dw_crs, ws, ws_bytes,
+                  BnIn{bn_mean, bn_invstd, bn_gamma, bn_beta, bn_relu}, as_stream(stream));
 }

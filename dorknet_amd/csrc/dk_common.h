@@ -43,6 +43,35 @@ __device__ __forceinline__ double wave_sum(double v) {
   return v;
 }
 
+// The BN output for one element (layers/batch_norm.py:91-96).  The standalone apply, the
+// backward ReLU-mask recompute and every consumer that applies a BN on load call this
+// same function, so all of them see bit-identical values.
+__device__ __forceinline__ float bn_out(float x, float mean, float invstd, float gamma, float beta) {
+  const float xh = (x - mean) * invstd;
+  return gamma * xh + beta;
+}
+__device__ __forceinline__ float bn_relu_out(float x, float mean, float invstd, float gamma, float beta, int relu) {
+  const float r = bn_out(x, mean, invstd, gamma, beta);
+  return (relu && !(r > 0.f)) ? 0.f : r;
+}
+
+// A BatchNorm (+ ReLU) applied to an operand as it is loaded: the producer's raw output x
+// plus per-channel statistics and affine parameters.  mean == nullptr: no transform.
+struct BnIn {
+  const float* mean;
+  const float* invstd;
+  const float* gamma;
+  const float* beta;
+  int relu;
+};
+
+__device__ __forceinline__ f32x4 bn_in4(f32x4 v, f32x4 m, f32x4 is, f32x4 g, f32x4 b, int relu) {
+  f32x4 o;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) o[e] = bn_relu_out(v[e], m[e], is[e], g[e], b[e], relu);
+  return o;
+}
+
 // Error codes returned for argument errors detected on the host side.  They
 // live above the hipError_t range used by the runtime so callers can tell
 // "bad call" from "device fault".

@@ -86,6 +86,36 @@ __global__ __launch_bounds__(256) void add_kernel(const float* __restrict__ a, c
   }
 }
 
+// Residual join with the BatchNorm(s) of its inputs applied on load:
+// y = [ReLU](bnA(a) + bnB(b)), bnX = identity when its mean is null.  Element i has channel
+// i % C (NHWC rows).  Bit-identical to dk_bn_apply_f32 on each input followed by dk_add_f32.
+__device__ __forceinline__ f32x4 bn_in4_at(f32x4 v, const BnIn& bn, int c) {
+  if (!bn.mean) return v;
+  return bn_in4(v, ld4(bn.mean + c), ld4(bn.invstd + c), ld4(bn.gamma + c), ld4(bn.beta + c), bn.relu);
+}
+
+__global__ __launch_bounds__(256) void bn_add_kernel(const float* __restrict__ a, BnIn ba, const float* __restrict__ b,
+                                                     BnIn bb, long long n, int C, int relu, float* __restrict__ y,
+                                                     uint8_t* __restrict__ mask) {
+  const long long nv = n >> 2;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += stride) {
+    const int c = (int)((uint32_t)(4 * i) % (uint32_t)C);
+    f32x4 v = bn_in4_at(ld4(a + 4 * i), ba, c) + bn_in4_at(ld4(b + 4 * i), bb, c);
+    if (relu) {
+      uint32_t m = 0;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const bool pos = v[e] > 0.f;
+        v[e] = pos ? v[e] : 0.f;
+        m |= (uint32_t)pos << (8 * e);
+      }
+      if (mask) reinterpret_cast<uint32_t*>(mask)[i] = m;
+    }
+    st4(y + 4 * i, v);
+  }
+}
+
 // out[n][c] = mean_{hw} x[n][hw][c]
 __global__ void gap_fwd_kernel(const float* __restrict__ x, int N, int HW, int C, float* __restrict__ out) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -345,6 +375,21 @@ DK_API int dk_mask_to_f32(const uint8_t* mask, long long n, float* out, void* st
 DK_API int dk_add_f32(const float* a, const float* b, long long n, int relu, float* y, uint8_t* mask, void* stream) {
   hipLaunchKernelGGL(add_kernel, grid4(n), dim3(256), 0, as_stream(stream), a, b, n, relu, y, mask,
                      (int)(al16(a) && al16(b) && al16(y) && al4(mask)));
+  return launch_status();
+}
+
+DK_API int dk_bn_add_f32(const float* a, const float* a_mean, const float* a_invstd, const float* a_gamma,
+                         const float* a_beta, int a_relu, const float* b, const float* b_mean, const float* b_invstd,
+                         const float* b_gamma, const float* b_beta, int b_relu, long long n, int C, int relu, float* y,
+                         uint8_t* mask, void* stream) {
+  const BnIn ba{a_mean, a_invstd, a_gamma, a_beta, a_relu}, bb{b_mean, b_invstd, b_gamma, b_beta, b_relu};
+  auto params_ok = [](const BnIn& p) {
+    return !p.mean || (p.invstd && p.gamma && p.beta && al16(p.mean) && al16(p.invstd) && al16(p.gamma) &&
+                       al16(p.beta));
+  };
+  if (C < 4 || C % 4 || n % C || n >= (1ll << 31) || !al16(a) || !al16(b) || !al16(y) || !al4(mask) || !params_ok(ba) || !params_ok(bb))
+    return DK_ERR_ARGS;
+  hipLaunchKernelGGL(bn_add_kernel, grid4(n), dim3(256), 0, as_stream(stream), a, ba, b, bb, n, C, relu, y, mask);
   return launch_status();
 }
 

@@ -53,6 +53,7 @@ __device__ __forceinline__ float bload1(__amdgpu_buffer_rsrc_t r, uint32_t off) 
 // Row/pixel index m -> (n, oh, ow) over an OH x OW grid; tap (r,s) reads
 // (ih, iw) = (oh*sa + dr*r + off, ow*sa + dr*s + off), zero outside [0,H)x[0,W).
 struct ImgDesc {
+  static constexpr bool kBnIn = false;
   const float* x;
   uint32_t bytes;
   int H, W, C;
@@ -60,6 +61,14 @@ struct ImgDesc {
   int R, S;
   int sa, dr, off;
   int M;  // N * OH * OW
+};
+
+// The same view of bn(x) (+ReLU): the loaders apply the BatchNorm of the layer that
+// produced x to every in-image element (padding stays exactly 0, as in the reference,
+// which pads the BN output).
+struct ImgBnDesc : ImgDesc {
+  static constexpr bool kBnIn = true;
+  BnIn bn;
 };
 
 // Row-major matrix p[row][ld]; `ext` bounds the non-reduction index.
@@ -106,8 +115,13 @@ struct LdImgKC : KCLayout<ROWS, BK> {
   bool active;
   int base[NR], ih0[NR], iw0[NR];
   f32x4 v[NR];
+  // input BatchNorm (ImgBnDesc): parameters of this thread's 4 channels, in-image rows
+  f32x4 bm, bi, bg, bb;
+  uint32_t okm;
+  int relu;
 
-  __device__ __forceinline__ void init(const ImgDesc& d, int row0, int tid) {
+  template <class D>
+  __device__ __forceinline__ void init(const D& d, int row0, int tid) {
     kq = tid % KQ;
     rb = tid / KQ;
     active = rb < ROWS;
@@ -128,9 +142,11 @@ struct LdImgKC : KCLayout<ROWS, BK> {
         base[j] = 0;
       }
     }
+    if constexpr (D::kBnIn) relu = d.bn.relu;
   }
 
-  __device__ __forceinline__ void load(const ImgDesc& d, int k0, int Ktot) {
+  template <class D>
+  __device__ __forceinline__ void load(const D& d, int k0, int Ktot) {
     const __amdgpu_buffer_rsrc_t rs = make_rsrc(d.x, d.bytes);
     const int k = k0 + 4 * kq;
     const bool kv = k < Ktot;
@@ -140,19 +156,36 @@ struct LdImgKC : KCLayout<ROWS, BK> {
     const int s = tap - r * d.S;
     const int dri = d.dr * r, dsi = d.dr * s;
     const int doff = dri * d.W + dsi;
+    uint32_t om = 0;
 #pragma unroll
     for (int j = 0; j < NR; ++j) {
       const int ih = ih0[j] + dri, iw = iw0[j] + dsi;
       const bool ok = kv && (unsigned)ih < (unsigned)d.H && (unsigned)iw < (unsigned)d.W;
       const uint32_t off = ok ? (uint32_t)((base[j] + doff) * d.C + c) * 4u : kOOB;
       v[j] = bload4(rs, off);
+      om |= (uint32_t)ok << j;
+    }
+    if constexpr (D::kBnIn) {
+      const int cc = kv ? c : 0;
+      bm = ld4(d.bn.mean + cc);
+      bi = ld4(d.bn.invstd + cc);
+      bg = ld4(d.bn.gamma + cc);
+      bb = ld4(d.bn.beta + cc);
+      okm = om;
     }
   }
 
+  template <class D>
   __device__ __forceinline__ void store(float* T) const {
     if (!active) return;
 #pragma unroll
-    for (int j = 0; j < NR; ++j) st4(T + (rb + j * RSTEP) * L::SK + 4 * kq, v[j]);
+    for (int j = 0; j < NR; ++j) {
+      f32x4 o = v[j];
+      if constexpr (D::kBnIn) {
+        if ((okm >> j) & 1u) o = bn_in4(o, bm, bi, bg, bb, relu);
+      }
+      st4(T + (rb + j * RSTEP) * L::SK + 4 * kq, o);
+    }
   }
 };
 
@@ -192,6 +225,7 @@ struct LdMatKCT : KCLayout<ROWS, BK> {
     }
   }
 
+  template <class>
   __device__ __forceinline__ void store(float* T) const {
     if (!active) return;
 #pragma unroll
@@ -237,6 +271,7 @@ struct LdMatICT : ICLayout<ROWS, BK> {
     }
   }
 
+  template <class>
   __device__ __forceinline__ void store(float* T) const {
     if (!active) return;
 #pragma unroll
@@ -260,8 +295,12 @@ struct LdImgIC : ICLayout<ROWS, BK> {
   bool active, colv;
   int c, dri, dsi;
   f32x4 v[NK];
+  f32x4 bm, bi, bg, bb;  // input BatchNorm of this thread's (fixed) 4 channels
+  uint32_t okm;
+  int relu;
 
-  __device__ __forceinline__ void init(const ImgDesc& d, int row0, int tid) {
+  template <class D>
+  __device__ __forceinline__ void init(const D& d, int row0, int tid) {
     iq = tid % IQ;
     kb = tid / IQ;
     active = kb < BK;
@@ -273,10 +312,20 @@ struct LdImgIC : ICLayout<ROWS, BK> {
     const int s = tap - r * d.S;
     dri = d.dr * r;
     dsi = d.dr * s;
+    if constexpr (D::kBnIn) {
+      const int cc = colv ? c : 0;
+      bm = ld4(d.bn.mean + cc);
+      bi = ld4(d.bn.invstd + cc);
+      bg = ld4(d.bn.gamma + cc);
+      bb = ld4(d.bn.beta + cc);
+      relu = d.bn.relu;
+    }
   }
 
-  __device__ __forceinline__ void load(const ImgDesc& d, int k0, int Ktot) {
+  template <class D>
+  __device__ __forceinline__ void load(const D& d, int k0, int Ktot) {
     const __amdgpu_buffer_rsrc_t rs = make_rsrc(d.x, d.bytes);
+    uint32_t om = 0;
 #pragma unroll
     for (int jj = 0; jj < NK; ++jj) {
       const int m = k0 + kb + jj * KSTEP;
@@ -288,13 +337,22 @@ struct LdImgIC : ICLayout<ROWS, BK> {
       const int iw = ow * d.sa + dsi + d.off;
       const bool ok = colv && m < d.M && (unsigned)ih < (unsigned)d.H && (unsigned)iw < (unsigned)d.W;
       v[jj] = bload4(rs, ok ? (uint32_t)(((n * d.H + ih) * d.W + iw) * d.C + c) * 4u : kOOB);
+      om |= (uint32_t)ok << jj;
     }
+    if constexpr (D::kBnIn) okm = om;
   }
 
+  template <class D>
   __device__ __forceinline__ void store(float* T) const {
     if (!active) return;
 #pragma unroll
-    for (int j = 0; j < NK; ++j) st4(T + (kb + j * KSTEP) * L::S + 4 * iq, v[j]);
+    for (int j = 0; j < NK; ++j) {
+      f32x4 o = v[j];
+      if constexpr (D::kBnIn) {
+        if ((okm >> j) & 1u) o = bn_in4(o, bm, bi, bg, bb, relu);
+      }
+      st4(T + (kb + j * KSTEP) * L::S + 4 * iq, o);
+    }
   }
 };
 
@@ -385,8 +443,8 @@ __global__ __launch_bounds__(64 * WM * WN) void igemm_f32(DA da, DB db, EP ep, i
     lb.init(db, n0, tid);
     la.load(da, kt0 * BK, Ktot);
     lb.load(db, kt0 * BK, Ktot);
-    la.store(As);
-    lb.store(Bs);
+    la.template store<DA>(As);
+    lb.template store<DB>(Bs);
     __syncthreads();
     int cur = 0;
     const int arow = wm * 32 * TM + l32;
@@ -415,8 +473,8 @@ __global__ __launch_bounds__(64 * WM * WN) void igemm_f32(DA da, DB db, EP ep, i
               acc[t][u] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[t][e], bf[u][e], acc[t][u], 0, 0, 0);
       }
       if (more) {
-        la.store(As + (cur ^ 1) * ABUF);
-        lb.store(Bs + (cur ^ 1) * BBUF);
+        la.template store<DA>(As + (cur ^ 1) * ABUF);
+        lb.template store<DB>(Bs + (cur ^ 1) * BBUF);
       }
       __syncthreads();
       cur ^= 1;
@@ -676,14 +734,41 @@ DK_API int dk_conv_weight_crsk_f32(const float* w_kcrs, int K, int C, int R, int
 }
 
 // y[n,oh,ow,k] = sum_{r,s,c} x[n, oh*stride + r - pad, ow*stride + s - pad, c] * w[k][r][s][c] (+ bias[k])
+template <class D>
+static int conv_fwd(const D& a, const float* w_krsc, int K, int Ktot, const float* bias, float* y, void* stream) {
+  MatDesc b = mat(w_krsc, K, Ktot, K);
+  EpStore ep{y, K, bias};
+  return igemm_rows<LdImgKC, D, LdMatKC, MatDesc, EpStore>(a, b, ep, a.M, K, Ktot, as_stream(stream));
+}
+
+static inline ImgBnDesc with_bn(const ImgDesc& d, const float* mean, const float* invstd, const float* gamma,
+                                const float* beta, int relu) {
+  ImgBnDesc o;
+  static_cast<ImgDesc&>(o) = d;
+  o.bn = BnIn{mean, invstd, gamma, beta, relu};
+  return o;
+}
+static inline bool bn_ok(const float* mean, const float* invstd, const float* gamma, const float* beta) {
+  return mean && invstd && gamma && beta && aligned16(mean) && aligned16(invstd) && aligned16(gamma) &&
+         aligned16(beta);
+}
+
 DK_API int dk_conv2d_fwd_f32(const float* x, int N, int H, int W, int C, const float* w_krsc, int K, int R, int S,
                              int stride, int pad, const float* bias, float* y, int OH, int OW, void* stream) {
   if (C % 4 || !aligned16(x) || !aligned16(w_krsc) || !fits((size_t)N * H * W * C * 4)) return DK_ERR_ARGS;
-  ImgDesc a = img(x, N, H, W, C, OH, OW, R, S, stride, 1, -pad, N * OH * OW);
-  const int Ktot = R * S * C;
-  MatDesc b = mat(w_krsc, K, Ktot, K);
-  EpStore ep{y, K, bias};
-  return igemm_rows<LdImgKC, ImgDesc, LdMatKC, MatDesc, EpStore>(a, b, ep, N * OH * OW, K, Ktot, as_stream(stream));
+  return conv_fwd(img(x, N, H, W, C, OH, OW, R, S, stride, 1, -pad, N * OH * OW), w_krsc, K, R * S * C, bias, y,
+                  stream);
+}
+
+DK_API int dk_conv2d_fwd_bnx_f32(const float* x, int N, int H, int W, int C, const float* w_krsc, int K, int R, int S,
+                                 int stride, int pad, const float* bias, float* y, int OH, int OW,
+                                 const float* bn_mean, const float* bn_invstd, const float* bn_gamma,
+                                 const float* bn_beta, int bn_relu, void* stream) {
+  if (C % 4 || !aligned16(x) || !aligned16(w_krsc) || !fits((size_t)N * H * W * C * 4)) return DK_ERR_ARGS;
+  if (!bn_ok(bn_mean, bn_invstd, bn_gamma, bn_beta)) return DK_ERR_ARGS;
+  return conv_fwd(with_bn(img(x, N, H, W, C, OH, OW, R, S, stride, 1, -pad, N * OH * OW), bn_mean, bn_invstd,
+                          bn_gamma, bn_beta, bn_relu),
+                  w_krsc, K, R * S * C, bias, y, stream);
 }
 
 // Stride-1 dgrad as an implicit GEMM: dx[n,h,w,c] = sum_{r,s,k} dy[n, h+pad-r, w+pad-s, k] * w[k][c][r][s]
@@ -734,24 +819,43 @@ DK_API size_t dk_conv2d_wgrad_workspace_bytes(int N, int OH, int OW, int K, int 
 }
 
 // dw[k][c][r][s] = sum_{n,oh,ow} dy[n,oh,ow,k] * x[n, oh*stride + r - pad, ow*stride + s - pad, c]  (+ l2 * w)
+// Weight gradient through the split-K engine: part = dy^T . im2col(x) then the fixed-order
+// reduce (+ l2 * w) into the KCRS (mode 1) or [K][C] (mode 0) layout.
+template <class D>
+static int wgrad(const float* dy, const D& b, int K, int Ncol, const float* w, float l2, float* dw, int mode, int C,
+                 int Cp, int R, int S, void* ws, size_t ws_bytes, void* stream) {
+  const int Kred = b.M;
+  if (!fits((size_t)Kred * K * 4)) return DK_ERR_ARGS;
+  if (ws_bytes < splitk_ws_bytes(K, Ncol, Kred)) return DK_ERR_WORKSPACE;
+  MatDesc a = mat(dy, Kred, K, K);
+  int splits = 1;
+  float* part = static_cast<float*>(ws);
+  const hipStream_t st = as_stream(stream);
+  int rc = vec_ok(a, 4, K) ? igemm_splitk<LdMatIC, MatDesc, LdImgIC, D>(a, b, part, K, Ncol, Kred, st, &splits)
+                           : igemm_splitk<LdMatIC1, MatDesc, LdImgIC, D>(a, b, part, K, Ncol, Kred, st, &splits);
+  if (rc) return rc;
+  return splitk_reduce(part, splits, K, Ncol, dw, w, l2, mode, C, Cp, R, S, st);
+}
+
 DK_API int dk_conv2d_wgrad_f32(const float* dy, const float* x, int N, int H, int W, int Cp, int C, int K, int R,
                                int S, int stride, int pad, int OH, int OW, const float* w_kcrs, float l2,
                                float* dw_kcrs, void* ws, size_t ws_bytes, void* stream) {
-  if (Cp % 4 || !aligned16(x)) return DK_ERR_ARGS;
-  const int M = K, Ncol = R * S * Cp, Kred = N * OH * OW;
-  if (!fits((size_t)Kred * K * 4) || !fits((size_t)N * H * W * Cp * 4)) return DK_ERR_ARGS;
-  if (ws_bytes < splitk_ws_bytes(M, Ncol, Kred)) return DK_ERR_WORKSPACE;
-  MatDesc a = mat(dy, Kred, K, K);
-  ImgDesc b = img(x, N, H, W, Cp, OH, OW, R, S, stride, 1, -pad, Kred);
-  int splits = 1;
-  float* part = static_cast<float*>(ws);
-  int rc = vec_ok(a, 4, K)
-               ? igemm_splitk<LdMatIC, MatDesc, LdImgIC, ImgDesc>(a, b, part, M, Ncol, Kred, as_stream(stream), &splits)
-               : igemm_splitk<LdMatIC1, MatDesc, LdImgIC, ImgDesc>(a, b, part, M, Ncol, Kred, as_stream(stream),
-                                                                   &splits);
-  if (rc) return rc;
-  return splitk_reduce(static_cast<float*>(ws), splits, M, Ncol, dw_kcrs, w_kcrs, l2, 1, C, Cp, R, S,
-                       as_stream(stream));
+  if (Cp % 4 || !aligned16(x) || !fits((size_t)N * H * W * Cp * 4)) return DK_ERR_ARGS;
+  return wgrad(dy, img(x, N, H, W, Cp, OH, OW, R, S, stride, 1, -pad, N * OH * OW), K, R * S * Cp, w_kcrs, l2,
+               dw_kcrs, 1, C, Cp, R, S, ws, ws_bytes, stream);
+}
+
+DK_API int dk_conv2d_wgrad_bnx_f32(const float* dy, const float* x, int N, int H, int W, int Cp, int C, int K, int R,
+                                   int S, int stride, int pad, int OH, int OW, const float* w_kcrs, float l2,
+                                   float* dw_kcrs, void* ws, size_t ws_bytes, const float* bn_mean,
+                                   const float* bn_invstd, const float* bn_gamma, const float* bn_beta, int bn_relu,
+                                   void* stream) {
+  if (Cp % 4 || !aligned16(x) || !fits((size_t)N * H * W * Cp * 4)) return DK_ERR_ARGS;
+  if (!bn_ok(bn_mean, bn_invstd, bn_gamma, bn_beta)) return DK_ERR_ARGS;
+  return wgrad(dy,
+               with_bn(img(x, N, H, W, Cp, OH, OW, R, S, stride, 1, -pad, N * OH * OW), bn_mean, bn_invstd, bn_gamma,
+                       bn_beta, bn_relu),
+               K, R * S * Cp, w_kcrs, l2, dw_kcrs, 1, C, Cp, R, S, ws, ws_bytes, stream);
 }
 
 // Pointwise (1x1) forward with optional stride-s subsampling (pointwise_convolution.py:46-55):
@@ -767,8 +871,19 @@ DK_API int dk_pwconv_fwd_f32(const float* x, int N, int H, int W, int C, const f
     MatDesc a = mat(x, N * H * W, C, N * H * W);
     return igemm_rows<LdMatKC1, MatDesc, LdMatKC1, MatDesc, EpStore>(a, b, ep, N * H * W, K, C, as_stream(stream));
   }
-  ImgDesc a = img(x, N, H, W, C, OH, OW, 1, 1, stride, 1, 0, N * OH * OW);
-  return igemm_rows<LdImgKC, ImgDesc, LdMatKC, MatDesc, EpStore>(a, b, ep, N * OH * OW, K, C, as_stream(stream));
+  return conv_fwd(img(x, N, H, W, C, OH, OW, 1, 1, stride, 1, 0, N * OH * OW), w_kc, K, C, bias, y, stream);
+}
+
+// The same with x = the raw output of the previous layer and y = pw(bn(x)) (+ReLU inside).
+DK_API int dk_pwconv_fwd_bnx_f32(const float* x, int N, int H, int W, int C, const float* w_kc, int K, int stride,
+                                 const float* bias, float* y, int OH, int OW, const float* bn_mean,
+                                 const float* bn_invstd, const float* bn_gamma, const float* bn_beta, int bn_relu,
+                                 void* stream) {
+  if (C % 4 || !aligned16(x) || !aligned16(w_kc) || !fits((size_t)N * H * W * C * 4)) return DK_ERR_ARGS;
+  if (!bn_ok(bn_mean, bn_invstd, bn_gamma, bn_beta)) return DK_ERR_ARGS;
+  return conv_fwd(with_bn(img(x, N, H, W, C, OH, OW, 1, 1, stride, 1, 0, N * OH * OW), bn_mean, bn_invstd, bn_gamma,
+                          bn_beta, bn_relu),
+                  w_kc, K, C, bias, y, stream);
 }
 
 // Pointwise dgrad (pointwise_convolution.py:65-72): dx_rows = dy_rows . W; for stride > 1 the
@@ -799,19 +914,21 @@ DK_API size_t dk_pwconv_wgrad_workspace_bytes(int N, int OH, int OW, int K, int 
 DK_API int dk_pwconv_wgrad_f32(const float* dy, const float* x, int N, int H, int W, int C, int K, int stride,
                                int OH, int OW, const float* w_kc, float l2, float* dw_kc, void* ws, size_t ws_bytes,
                                void* stream) {
-  if (C % 4 || !aligned16(x)) return DK_ERR_ARGS;
-  const int Kred = N * OH * OW;
-  if (!fits((size_t)Kred * K * 4) || !fits((size_t)N * H * W * C * 4)) return DK_ERR_ARGS;
-  if (ws_bytes < splitk_ws_bytes(K, C, Kred)) return DK_ERR_WORKSPACE;
-  MatDesc a = mat(dy, Kred, K, K);
-  ImgDesc b = img(x, N, H, W, C, OH, OW, 1, 1, stride, 1, 0, Kred);
-  int splits = 1;
-  float* part = static_cast<float*>(ws);
-  int rc = vec_ok(a, 4, K)
-               ? igemm_splitk<LdMatIC, MatDesc, LdImgIC, ImgDesc>(a, b, part, K, C, Kred, as_stream(stream), &splits)
-               : igemm_splitk<LdMatIC1, MatDesc, LdImgIC, ImgDesc>(a, b, part, K, C, Kred, as_stream(stream), &splits);
-  if (rc) return rc;
-  return splitk_reduce(static_cast<float*>(ws), splits, K, C, dw_kc, w_kc, l2, 0, C, C, 1, 1, as_stream(stream));
+  if (C % 4 || !aligned16(x) || !fits((size_t)N * H * W * C * 4)) return DK_ERR_ARGS;
+  return wgrad(dy, img(x, N, H, W, C, OH, OW, 1, 1, stride, 1, 0, N * OH * OW), K, C, w_kc, l2, dw_kc, 0, C, C, 1, 1,
+               ws, ws_bytes, stream);
+}
+
+DK_API int dk_pwconv_wgrad_bnx_f32(const float* dy, const float* x, int N, int H, int W, int C, int K, int stride,
+                                   int OH, int OW, const float* w_kc, float l2, float* dw_kc, void* ws,
+                                   size_t ws_bytes, const float* bn_mean, const float* bn_invstd,
+                                   const float* bn_gamma, const float* bn_beta, int bn_relu, void* stream) {
+  if (C % 4 || !aligned16(x) || !fits((size_t)N * H * W * C * 4)) return DK_ERR_ARGS;
+  if (!bn_ok(bn_mean, bn_invstd, bn_gamma, bn_beta)) return DK_ERR_ARGS;
+  return wgrad(dy,
+               with_bn(img(x, N, H, W, C, OH, OW, 1, 1, stride, 1, 0, N * OH * OW), bn_mean, bn_invstd, bn_gamma,
+                       bn_beta, bn_relu),
+               K, C, w_kc, l2, dw_kc, 0, C, C, 1, 1, ws, ws_bytes, stream);
 }
 
 // Dense (dense_layer.py:46-55): y[b][o] = sum_i x[b][i] * w[i][o] (+ bias[o]);  w stored (in, out).

@@ -1,0 +1,71 @@
+"""BatchNorm output that is applied by its consumer ("BN on load").
+
+In the reference a BatchNormLayer writes its normalised output (layers/batch_norm.py:91-96),
+an optional ReLu writes another copy (activations.py:37-42), and the next layer reads it.
+Here, when the next layer can take it, the pair hands over a ``BNOut`` instead: the raw
+input x (which BatchNormLayer keeps for its backward anyway) plus the per-channel mean,
+1/std, gamma, beta and the ReLU flag.  Consumers apply ``bn_out`` as they load each tile
+(the dk_*_bnx_f32 entry points), with the same arithmetic as dk_bn_apply_f32, so their
+results are bit-identical to running the layers one by one -- the normalised activation
+just never exists in HBM (forward and weight-gradient passes recompute it on load).
+
+Anything that cannot consume it calls ``materialize()`` (one dk_bn_apply_f32 pass).
+"""
+from __future__ import annotations
+
+import torch
+
+from .._hip import lib, stream_handle
+from .._tensor import empty_nhwc
+
+
+class BNOut:
+    __slots__ = ("x", "mean", "invstd", "gamma", "beta", "relu", "_y")
+
+    def __init__(self, x, mean, invstd, gamma, beta, relu):
+        self.x = x            # raw input of the BatchNormLayer (NHWC storage, logical NCHW)
+        self.mean = mean      # (C,) fp32 device tensors
+        self.invstd = invstd
+        self.gamma = gamma
+        self.beta = beta
+        self.relu = bool(relu)
+        self._y = None
+
+    @property
+    def shape(self):
+        return self.x.shape
+
+    def dim(self):
+        return self.x.dim()
+
+    @property
+    def device(self):
+        return self.x.device
+
+    @property
+    def dtype(self):
+        return self.x.dtype
+
+    def bn_args(self):
+        """(mean, invstd, gamma, beta, relu) for a dk_*_bnx_f32 call."""
+        return (self.mean.data_ptr(), self.invstd.data_ptr(), self.gamma.data_ptr(), self.beta.data_ptr(),
+                int(self.relu))
+
+    def materialize(self):
+        """The normalised tensor itself (computed once)."""
+        if self._y is None:
+            x = self.x
+            y = empty_nhwc(*x.shape) if x.dim() == 4 else torch.empty_like(x)
+            lib.dk_bn_apply_f32(x.data_ptr(), x.numel(), x.shape[1], self.mean.data_ptr(), self.invstd.data_ptr(),
+                                self.gamma.data_ptr(), self.beta.data_ptr(), int(self.relu), y.data_ptr(), 0,
+                                stream_handle())
+            self._y = y
+        return self._y
+
+
+def materialize(X):
+    return X.materialize() if isinstance(X, BNOut) else X
+
+
+def accepts_bn_input(layer) -> bool:
+    return bool(getattr(layer, "accepts_bn_input", False))

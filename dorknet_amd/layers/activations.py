@@ -11,7 +11,8 @@ from __future__ import annotations
 import torch
 
 from .._hip import lib, stream_handle
-from .._tensor import as_device, empty_nhwc, rows, to_nhwc
+from .._tensor import as_device, empty_nhwc, is_nhwc as is_nhwc_t, rows, to_nhwc
+from ._bn_input import BNOut
 from .layer import Layer
 
 
@@ -48,9 +49,14 @@ class ReLu(Layer):
         return y
 
     def forward_add(self, A, B, test_mode=False):
-        """ReLU(A + B) in one pass -- the residual join (residual_block.py:75)."""
+        """ReLU(A + B) in one pass -- the residual join (residual_block.py:75).  A and/or B may
+        be a BatchNorm output not yet written (BNOut): the normalisation is applied on load."""
         self._require_on_gpu()
         st = stream_handle()
+        if isinstance(A, BNOut) or isinstance(B, BNOut):
+            y = self._bn_add(A, B, test_mode, st)
+            if y is not None:
+                return y
         a, b = _same_layout(A), _same_layout(B)
         if a.shape != b.shape:
             raise ValueError("residual join shape mismatch: {} vs {}".format(tuple(a.shape), tuple(b.shape)))
@@ -61,6 +67,26 @@ class ReLu(Layer):
                                memory_format=torch.channels_last if a.dim() == 4 else torch.contiguous_format)
         lib.dk_add_f32(a.data_ptr(), b.data_ptr(), a.numel(), 1, y.data_ptr(),
                        0 if mask is None else mask.data_ptr(), st)
+        if not test_mode:
+            self._mask, self._fused_out = mask, None
+        return y
+
+    def _bn_add(self, A, B, test_mode, st):
+        def parts(T):
+            if isinstance(T, BNOut):
+                return T.x, T.bn_args()
+            return to_nhwc(T), (0, 0, 0, 0, 0)
+        if A.dim() != 4 or tuple(A.shape) != tuple(B.shape) or A.shape[1] % 4:
+            return None
+        (a, pa), (b, pb) = parts(A), parts(B)
+        if not (is_nhwc_t(a) and is_nhwc_t(b)):
+            return None
+        y = empty_nhwc(*a.shape)
+        mask = None
+        if not test_mode:
+            mask = torch.empty(a.shape, dtype=torch.uint8, device=a.device, memory_format=torch.channels_last)
+        lib.dk_bn_add_f32(a.data_ptr(), *pa, b.data_ptr(), *pb, a.numel(), a.shape[1], 1, y.data_ptr(),
+                          0 if mask is None else mask.data_ptr(), st)
         if not test_mode:
             self._mask, self._fused_out = mask, None
         return y
@@ -78,7 +104,7 @@ class ReLu(Layer):
             lib.dk_mask_to_f32(self._mask.data_ptr(), self._mask.numel(), out.data_ptr(), stream_handle())
             return out
         if self._fused_out is not None:
-            y = self._fused_out
+            y = as_device(self._fused_out)  # a BNOut is materialised here
             mask = torch.empty(y.shape, dtype=torch.uint8, device=y.device,
                                memory_format=torch.channels_last if y.dim() == 4 else torch.contiguous_format)
             tmp = self._empty_like(y)

@@ -117,13 +117,13 @@ class BatchNormLayer(Layer):
 
     # -- forward -------------------------------------------------------------------------
 
-    def _forward(self, X, test_mode, relu):
+    def _normalisation(self, X, test_mode):
+        """(x, mean, invstd): batch statistics in training mode (kept for backward), the
+        running statistics in test mode (batch_norm.py:76-115)."""
         self._require_on_gpu()
         st = stream_handle()
         x, P, C = self._prep_input(as_device(X))
         self.input_shape = tuple(x.shape)
-        gamma, beta = self.learned_params["gamma"], self.learned_params["beta"]
-        y = self._out_like(x)
         if not test_mode:
             mean, std, invstd = self._stats(x, P, C, st)
             self.X = x
@@ -135,9 +135,26 @@ class BatchNormLayer(Layer):
             mean = rm.contiguous()
             invstd = torch.empty(C, dtype=torch.float32, device=x.device)
             lib.dk_bn_infer_params_f32(rs.data_ptr(), C, invstd.data_ptr(), st)
-        lib.dk_bn_apply_f32(x.data_ptr(), x.numel(), C, mean.data_ptr(), invstd.data_ptr(), gamma.data_ptr(),
-                            beta.data_ptr(), int(relu), y.data_ptr(), 0, st)
+        return x, mean, invstd
+
+    def _forward(self, X, test_mode, relu):
+        x, mean, invstd = self._normalisation(X, test_mode)
+        gamma, beta = self.learned_params["gamma"], self.learned_params["beta"]
+        y = self._out_like(x)
+        lib.dk_bn_apply_f32(x.data_ptr(), x.numel(), x.shape[1], mean.data_ptr(), invstd.data_ptr(),
+                            gamma.data_ptr(), beta.data_ptr(), int(relu), y.data_ptr(), 0, stream_handle())
         return y
+
+    def forward_deferred(self, X, relu_layer=None, test_mode=False):
+        """Statistics only; the normalisation (and the following ReLu, if given) is applied
+        by the consumer as it loads its input (layers/_bn_input.py)."""
+        from ._bn_input import BNOut
+        x, mean, invstd = self._normalisation(X, test_mode)
+        out = BNOut(x, mean, invstd, self.learned_params["gamma"], self.learned_params["beta"],
+                    relu_layer is not None)
+        if relu_layer is not None:
+            relu_layer._attach_fused(out, test_mode)
+        return out
 
     def forward(self, X, test_mode=False, use_express=False):
         """X.shape = (batch_size, channel, height, width) or (batch_size, features)."""

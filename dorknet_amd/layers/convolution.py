@@ -19,6 +19,7 @@ import torch
 
 from .._hip import lib, stream_handle, workspace
 from .._tensor import empty_nhwc, ptr, to_nhwc
+from ._bn_input import BNOut
 from ._common import add_regulariser_grad, grad_buffer, init_weights, l2_strength
 from .layer import Layer
 
@@ -67,11 +68,14 @@ class ConvLayer(Layer):
 
     # -- forward / backward --------------------------------------------------------------
 
+    accepts_bn_input = True  # forward(BNOut): the preceding BatchNorm is applied on load
+
     def forward(self, X, test_mode=False):
         self._require_on_gpu()
         st = stream_handle()
         self.input_shape = tuple(X.shape)
-        x = to_nhwc(X, cpad=4)
+        bn = X if isinstance(X, BNOut) and X.dim() == 4 and X.shape[1] % 4 == 0 else None
+        x = bn.x if bn is not None else to_nhwc(X, cpad=4)
         N, Cp, H, W = x.shape
         K, C, R, S = self.num_filters, self.filter_chans, self.f_rows, self.f_cols
         OH, OW = self._out_size(H, W)
@@ -80,11 +84,16 @@ class ConvLayer(Layer):
         lib.dk_conv_weight_krsc_f32(w.data_ptr(), K, C, R, S, Cp, w_krsc.data_ptr(), st)
         y = empty_nhwc(N, K, OH, OW)
         bias = self.learned_params["bias"] if self.with_bias else None
-        lib.dk_conv2d_fwd_f32(x.data_ptr(), N, H, W, Cp, w_krsc.data_ptr(), K, R, S, self.stride, self.padding,
-                              ptr(bias), y.data_ptr(), OH, OW, st)
+        if bn is not None:
+            lib.dk_conv2d_fwd_bnx_f32(x.data_ptr(), N, H, W, Cp, w_krsc.data_ptr(), K, R, S, self.stride,
+                                      self.padding, ptr(bias), y.data_ptr(), OH, OW, *bn.bn_args(), st)
+        else:
+            lib.dk_conv2d_fwd_f32(x.data_ptr(), N, H, W, Cp, w_krsc.data_ptr(), K, R, S, self.stride, self.padding,
+                                  ptr(bias), y.data_ptr(), OH, OW, st)
         # The reference caches the patch matrix (convolution.py:69-74); the implicit GEMM
-        # only needs the (NHWC) input itself.
+        # only needs the (NHWC) input itself (for a BNOut: the BatchNorm's raw input).
         self.X = x
+        self._bn_in = bn
         return y
 
     def backward(self, upstream_dx):
@@ -105,9 +114,14 @@ class ConvLayer(Layer):
         gw = grad_buffer(self, "weights", (K, C, R, S))
         s = l2_strength(self.weight_regulariser)
         nb = lib.dk_conv2d_wgrad_workspace_bytes(N, OH, OW, K, Cp, R, S)
-        lib.dk_conv2d_wgrad_f32(dy.data_ptr(), x.data_ptr(), N, H, W, Cp, C, K, R, S, self.stride, self.padding,
-                                OH, OW, w.data_ptr() if s else 0, s or 0.0, gw.data_ptr(), workspace.get(nb), nb,
-                                st)
+        if self._bn_in is not None:
+            lib.dk_conv2d_wgrad_bnx_f32(dy.data_ptr(), x.data_ptr(), N, H, W, Cp, C, K, R, S, self.stride,
+                                        self.padding, OH, OW, w.data_ptr() if s else 0, s or 0.0, gw.data_ptr(),
+                                        workspace.get(nb), nb, *self._bn_in.bn_args(), st)
+        else:
+            lib.dk_conv2d_wgrad_f32(dy.data_ptr(), x.data_ptr(), N, H, W, Cp, C, K, R, S, self.stride, self.padding,
+                                    OH, OW, w.data_ptr() if s else 0, s or 0.0, gw.data_ptr(), workspace.get(nb), nb,
+                                    st)
         if s is None:
             add_regulariser_grad(gw, w, self.weight_regulariser)
         # input gradient (convolution.py:101-117); shape = the forward input's shape

@@ -15,6 +15,7 @@ import torch
 
 from .._hip import lib, stream_handle, workspace
 from .._tensor import empty_nhwc, ptr, to_nhwc
+from ._bn_input import BNOut
 from ._common import add_regulariser_grad, grad_buffer, init_weights, l2_strength
 from .layer import Layer
 
@@ -61,10 +62,13 @@ class DepthwiseConvLayer(Layer):
         lib.dk_dw_weight_rsc_f32(w.data_ptr(), C, R, S, w_rsc.data_ptr(), st)
         return w_rsc
 
+    accepts_bn_input = True  # forward(BNOut): the preceding BatchNorm is applied on load
+
     def forward(self, X, test_mode=False):
         self._require_on_gpu()
         st = stream_handle()
-        x = to_nhwc(X)
+        bn = X if isinstance(X, BNOut) and X.dim() == 4 and X.shape[1] % 4 == 0 else None
+        x = bn.x if bn is not None else to_nhwc(X)
         N, C, H, W = x.shape
         R, S = self.f_rows, self.f_cols
         # float-then-int output size (depthwise_convolution.py:89-90)
@@ -73,10 +77,17 @@ class DepthwiseConvLayer(Layer):
         OH, OW = int(self.num_row_patches), int(self.num_col_patches)
         y = empty_nhwc(N, C, OH, OW)
         bias = self.learned_params["bias"] if self.with_bias else None
-        lib.dk_dwconv_fwd_f32(x.data_ptr(), N, H, W, C, self._w_rsc(st).data_ptr(), R, S, self.stride,
-                              self.padding, ptr(bias), y.data_ptr(), OH, OW, st)
+        if bn is not None:
+            lib.dk_dwconv_fwd_bnx_f32(x.data_ptr(), N, H, W, C, self._w_rsc(st).data_ptr(), R, S, self.stride,
+                                      self.padding, ptr(bias), y.data_ptr(), OH, OW, *bn.bn_args(), st)
+        else:
+            lib.dk_dwconv_fwd_f32(x.data_ptr(), N, H, W, C, self._w_rsc(st).data_ptr(), R, S, self.stride,
+                                  self.padding, ptr(bias), y.data_ptr(), OH, OW, st)
         if not test_mode:
-            self.X = x  # the reference keeps the *padded* input (:87-88); padding is implicit here
+            # the reference keeps the *padded* input (:87-88); padding is implicit here, and
+            # a BNOut input is kept as the BatchNorm's raw input + parameters
+            self.X = x
+            self._bn_in = bn
         return y
 
     def backward(self, upstream_dx):
@@ -96,8 +107,13 @@ class DepthwiseConvLayer(Layer):
         gw = grad_buffer(self, "weights", (C, R, S))
         s = l2_strength(self.weight_regulariser)
         nb = lib.dk_dwconv_wgrad_workspace_bytes(N, OH, OW, C, R, S)
-        lib.dk_dwconv_wgrad_f32(dy.data_ptr(), x.data_ptr(), N, H, W, C, R, S, self.stride, self.padding, OH, OW,
-                                w.data_ptr() if s else 0, s or 0.0, gw.data_ptr(), workspace.get(nb), nb, st)
+        if self._bn_in is not None:
+            lib.dk_dwconv_wgrad_bnx_f32(dy.data_ptr(), x.data_ptr(), N, H, W, C, R, S, self.stride, self.padding,
+                                        OH, OW, w.data_ptr() if s else 0, s or 0.0, gw.data_ptr(), workspace.get(nb),
+                                        nb, *self._bn_in.bn_args(), st)
+        else:
+            lib.dk_dwconv_wgrad_f32(dy.data_ptr(), x.data_ptr(), N, H, W, C, R, S, self.stride, self.padding, OH, OW,
+                                    w.data_ptr() if s else 0, s or 0.0, gw.data_ptr(), workspace.get(nb), nb, st)
         if s is None:
             add_regulariser_grad(gw, w, self.weight_regulariser)
         dx = empty_nhwc(N, C, H, W)

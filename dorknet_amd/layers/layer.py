@@ -21,6 +21,7 @@ class Layer:
         self.non_learned_params = None
         self.grads = None
         self.weight_regulariser = None
+        self._bn_in = None  # BNOut consumed by forward (layers/_bn_input.py), if any
 
     def __repr__(self):
         return "Layer of type {} didn't implement __repr__".format(self.__class__.__name__)

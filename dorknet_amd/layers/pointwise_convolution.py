@@ -14,6 +14,7 @@ from __future__ import annotations
 
 from .._hip import lib, stream_handle, workspace
 from .._tensor import empty_nhwc, ptr, to_nhwc
+from ._bn_input import BNOut
 from ._common import add_regulariser_grad, grad_buffer, init_weights, l2_strength
 from .layer import Layer
 
@@ -52,10 +53,13 @@ class PointwiseConvLayer(Layer):
             self.stride, self.with_bias, repr(self.weight_regulariser), self.is_on_gpu)
         return out
 
+    accepts_bn_input = True  # forward(BNOut): the preceding BatchNorm is applied on load
+
     def forward(self, X, test_mode=False):
         self._require_on_gpu()
         st = stream_handle()
-        x = to_nhwc(X, cpad=4)
+        bn = X if isinstance(X, BNOut) and X.dim() == 4 and X.shape[1] % 4 == 0 else None
+        x = bn.x if bn is not None else to_nhwc(X, cpad=4)
         N, Cp, H, W = x.shape
         K = self.num_filters
         s = self.stride
@@ -66,8 +70,15 @@ class PointwiseConvLayer(Layer):
             raise ValueError("PointwiseConvLayer {}: input has {} channels, weights expect {} (a multiple of 4 "
                              "is required)".format(self.layer_name, X.shape[1], self.num_channels))
         bias = self.learned_params["bias"] if self.with_bias else None
-        lib.dk_pwconv_fwd_f32(x.data_ptr(), N, H, W, Cp, w.data_ptr(), K, s, ptr(bias), y.data_ptr(), OH, OW, st)
-        self.X = x  # the reference keeps the NHWC row copy as self.patches (:50)
+        if bn is not None:
+            lib.dk_pwconv_fwd_bnx_f32(x.data_ptr(), N, H, W, Cp, w.data_ptr(), K, s, ptr(bias), y.data_ptr(), OH, OW,
+                                      *bn.bn_args(), st)
+        else:
+            lib.dk_pwconv_fwd_f32(x.data_ptr(), N, H, W, Cp, w.data_ptr(), K, s, ptr(bias), y.data_ptr(), OH, OW, st)
+        # the reference keeps the NHWC row copy as self.patches (:50); here the input itself
+        # (or, for a BNOut, the BatchNorm's raw input + parameters)
+        self.X = x
+        self._bn_in = bn
         self.out_hw = (OH, OW)
         return y
 
@@ -88,8 +99,13 @@ class PointwiseConvLayer(Layer):
         gw = grad_buffer(self, "weights", (K, C))
         l2s = l2_strength(self.weight_regulariser)
         nb = lib.dk_pwconv_wgrad_workspace_bytes(N, OH, OW, K, C)
-        lib.dk_pwconv_wgrad_f32(dy.data_ptr(), x.data_ptr(), N, H, W, C, K, s, OH, OW, w.data_ptr() if l2s else 0,
-                                l2s or 0.0, gw.data_ptr(), workspace.get(nb), nb, st)
+        if self._bn_in is not None:
+            lib.dk_pwconv_wgrad_bnx_f32(dy.data_ptr(), x.data_ptr(), N, H, W, C, K, s, OH, OW,
+                                        w.data_ptr() if l2s else 0, l2s or 0.0, gw.data_ptr(), workspace.get(nb), nb,
+                                        *self._bn_in.bn_args(), st)
+        else:
+            lib.dk_pwconv_wgrad_f32(dy.data_ptr(), x.data_ptr(), N, H, W, C, K, s, OH, OW, w.data_ptr() if l2s else 0,
+                                    l2s or 0.0, gw.data_ptr(), workspace.get(nb), nb, st)
         if l2s is None:
             add_regulariser_grad(gw, w, self.weight_regulariser)
         dx = empty_nhwc(N, C, OH * s, OW * s)  # widened shape, pointwise_convolution.py:68-72

@@ -12,6 +12,7 @@ from __future__ import annotations
 
 from .._hip import lib, stream_handle
 from .._tensor import empty_nhwc, to_nhwc
+from ._bn_input import accepts_bn_input, materialize
 from ._chain import chain_backward, chain_forward
 from .activations import ReLu
 from .batch_norm import BatchNormLayer
@@ -63,16 +64,22 @@ class ResidualBlock(Layer):
             self.post_skip_activation.to_gpu()
         self.is_on_gpu = True
 
+    # X may be a BNOut (the block input's BatchNorm applied on load by the chain's first layer,
+    # the skip projection and the join); the chain's last BatchNorm is applied by the join.
+    accepts_bn_input = True
+
     def forward(self, X, test_mode=False):
-        X_tmp, self._steps = chain_forward(self.layer_list, X, test_mode=test_mode)
+        post = self.post_skip_activation
+        join_fused = type(post) is ReLu
+        X_tmp, self._steps = chain_forward(self.layer_list, X, test_mode=test_mode, out_accepts=join_fused)
         if self.skip_projection is not None:
-            skippee = self.skip_projection.forward(X, test_mode=test_mode)
+            skippee = self.skip_projection.forward(X if accepts_bn_input(self.skip_projection) else materialize(X),
+                                                   test_mode=test_mode)
         else:
             skippee = X
-        post = self.post_skip_activation
-        if type(post) is ReLu:
+        if join_fused:
             return post.forward_add(X_tmp, skippee, test_mode=test_mode)
-        return post.forward(_add(X_tmp, skippee), test_mode=test_mode)
+        return post.forward(_add(materialize(X_tmp), materialize(skippee)), test_mode=test_mode)
 
     def regulariser_forward(self):
         regularisation = 0

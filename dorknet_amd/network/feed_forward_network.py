@@ -12,7 +12,8 @@ import json
 
 import numpy as np
 
-from ..layers._chain import chain_backward, fusable_pair, fusion_enabled
+from ..layers._bn_input import materialize
+from ..layers._chain import chain_backward, fusion_enabled, plan_group, run_group
 from ..layers.activations import ReLu  # noqa: F401  (re-exported names used by loaders)
 from ..layers.batch_norm import BatchNormLayer  # noqa: F401
 from ..layers.convolution import ConvLayer  # noqa: F401
@@ -126,22 +127,18 @@ class FeedForwardNetwork:
             if plan is not None and not plan:
                 plan = None
         layers = self.layers
+        keep = () if terminal_layer_name is None else (terminal_layer_name,)
         i = 0
         while i < len(layers):
-            layer = layers[i]
-            nxt = layers[i + 1] if i + 1 < len(layers) else None
-            if fuse and nxt is not None and fusable_pair(layer, nxt) and layer.layer_name != terminal_layer_name:
-                X = layer.forward_bn_relu(X, nxt, test_mode=test_mode)
-                group = (layer, nxt)
-                i += 2
-            else:
-                X = layer.forward(X, test_mode=test_mode)
-                group = (layer,)
-                i += 1
+            group, mode = plan_group(layers, i, fuse, keep=keep)
+            if mode == "pair" and group[0].layer_name in keep:
+                group, mode = group[:1], "single"  # the terminal BN's own output is requested
+            X = run_group(group, mode, X, test_mode)
+            i += len(group)
             steps.append(group)
             for l in group:
                 if l.layer_name == terminal_layer_name:
-                    return loss, X
+                    return loss, materialize(X)
                 if not test_mode and plan is None and hasattr(l, "regulariser_forward"):
                     regularisation_terms.append(l.regulariser_forward())
         if self.loss_layer is not None:

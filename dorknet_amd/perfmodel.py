@@ -119,6 +119,16 @@ def _nchw_to_nhwc(x, N, C, H, W, Cp, y, st):
     return 0, E * (N * C * H * W + N * Cp * H * W)
 
 
+def _bnx(f):
+    """A *_bnx_* entry = the plain entry with 5 BatchNorm arguments before the stream; the
+    compulsory bytes are the same (the BN output it replaces is never written or read)."""
+    return lambda *a: f(*(a[:-6] + a[-1:]))
+
+
+def _bn_add(a, am, ai, ag, ab, ar, b, bm, bi, bg, bb, br, n, C, relu, y, mask, st):
+    return n * (1 + 4 * (bool(am) + bool(bm))), E * 3 * n + (n if mask else 0)
+
+
 MODEL = {
     "dk_conv2d_fwd_f32": _conv_fwd,
     "dk_conv2d_dgrad_f32": _conv_dgrad,
@@ -146,6 +156,13 @@ MODEL = {
     "dk_colsum_f32": _colsum,
     "dk_l2_loss_multi_f32": _l2_multi,
     "dk_nchw_to_nhwc_f32": _nchw_to_nhwc,
+    "dk_conv2d_fwd_bnx_f32": _bnx(_conv_fwd),
+    "dk_conv2d_wgrad_bnx_f32": _bnx(_conv_wgrad),
+    "dk_pwconv_fwd_bnx_f32": _bnx(_pw_fwd),
+    "dk_pwconv_wgrad_bnx_f32": _bnx(_pw_wgrad),
+    "dk_dwconv_fwd_bnx_f32": _bnx(_dw_fwd),
+    "dk_dwconv_wgrad_bnx_f32": _bnx(_dw_wgrad),
+    "dk_bn_add_f32": _bn_add,
 }
 
 

@@ -75,6 +75,20 @@ size_t dk_pwconv_wgrad_workspace_bytes(int N, int OH, int OW, int K, int C);
 int dk_pwconv_wgrad_f32(const float* dy, const float* x, int N, int H, int W, int C, int K, int stride, int OH, int OW, const float* w_kc, float l2, float* dw_kc, void* ws, size_t ws_bytes, void* stream);
 
 /* ---------------------------------------------------------------------------------------
+ * "BN on load" variants (*_bnx_*): the input operand is bn(x) (+ReLU if bn_relu), computed
+ * from the raw x of the layer before the BatchNormLayer as each tile is loaded, so the BN
+ * output is never written to HBM.  Replaces the pair BatchNormLayer.forward (apply,
+ * layers/batch_norm.py:91-96) [+ ReLu.forward, activations.py:37-42] -> consumer forward /
+ * weight gradient; the values the consumer sees are bit-identical to dk_bn_apply_f32's
+ * output (same bn_out arithmetic), and padding stays exactly 0.
+ * bn_*: per-channel mean, 1/std, gamma, beta (C floats each, 16-byte aligned).
+ * ------------------------------------------------------------------------------------- */
+int dk_conv2d_fwd_bnx_f32(const float* x, int N, int H, int W, int C, const float* w_krsc, int K, int R, int S, int stride, int pad, const float* bias, float* y, int OH, int OW, const float* bn_mean, const float* bn_invstd, const float* bn_gamma, const float* bn_beta, int bn_relu, void* stream);
+int dk_conv2d_wgrad_bnx_f32(const float* dy, const float* x, int N, int H, int W, int Cp, int C, int K, int R, int S, int stride, int pad, int OH, int OW, const float* w_kcrs, float l2, float* dw_kcrs, void* ws, size_t ws_bytes, const float* bn_mean, const float* bn_invstd, const float* bn_gamma, const float* bn_beta, int bn_relu, void* stream);
+int dk_pwconv_fwd_bnx_f32(const float* x, int N, int H, int W, int C, const float* w_kc, int K, int stride, const float* bias, float* y, int OH, int OW, const float* bn_mean, const float* bn_invstd, const float* bn_gamma, const float* bn_beta, int bn_relu, void* stream);
+int dk_pwconv_wgrad_bnx_f32(const float* dy, const float* x, int N, int H, int W, int C, int K, int stride, int OH, int OW, const float* w_kc, float l2, float* dw_kc, void* ws, size_t ws_bytes, const float* bn_mean, const float* bn_invstd, const float* bn_gamma, const float* bn_beta, int bn_relu, void* stream);
+
+/* ---------------------------------------------------------------------------------------
  * Depthwise convolution, direct (no MFMA).
  * Replaces DepthwiseConvLayer.forward_cp (layers/depthwise_convolution.py:85-102, CUDA
  * forward_conv :105-121) and backward_cp (:198-221, CUDA backward_conv :122-140).
@@ -88,6 +102,9 @@ size_t dk_dwconv_dgrad_workspace_bytes(int C, int R, int S);
 int dk_dwconv_dgrad_f32(const float* dy, int N, int OH, int OW, int C, const float* w_crs, int R, int S, int stride, int pad, float* dx, int H, int W, void* ws, size_t ws_bytes, void* stream);
 size_t dk_dwconv_wgrad_workspace_bytes(int N, int OH, int OW, int C, int R, int S);
 int dk_dwconv_wgrad_f32(const float* dy, const float* x, int N, int H, int W, int C, int R, int S, int stride, int pad, int OH, int OW, const float* w_crs, float l2, float* dw_crs, void* ws, size_t ws_bytes, void* stream);
+/* BN-on-load variants (see the *_bnx_* note after the pointwise block). */
+int dk_dwconv_fwd_bnx_f32(const float* x, int N, int H, int W, int C, const float* w_rsc, int R, int S, int stride, int pad, const float* bias, float* y, int OH, int OW, const float* bn_mean, const float* bn_invstd, const float* bn_gamma, const float* bn_beta, int bn_relu, void* stream);
+int dk_dwconv_wgrad_bnx_f32(const float* dy, const float* x, int N, int H, int W, int C, int R, int S, int stride, int pad, int OH, int OW, const float* w_crs, float l2, float* dw_crs, void* ws, size_t ws_bytes, const float* bn_mean, const float* bn_invstd, const float* bn_gamma, const float* bn_beta, int bn_relu, void* stream);
 
 /* ---------------------------------------------------------------------------------------
  * Dense layer (layers/dense_layer.py:46-67; W stored (in, out) as the reference).
@@ -130,6 +147,10 @@ int dk_relu_fwd_f32(const float* x, long long n, float* y, uint8_t* mask, void* 
 int dk_relu_bwd_f32(const float* dy, const uint8_t* mask, long long n, float* dx, void* stream);
 int dk_mask_to_f32(const uint8_t* mask, long long n, float* out, void* stream);
 int dk_add_f32(const float* a, const float* b, long long n, int relu, float* y, uint8_t* mask, void* stream);
+/* Residual join with BN on load (see *_bnx_*): y = [ReLU](bnA(a) + bnB(b)) over NHWC rows of C
+ * channels; a_mean (b_mean) == NULL: that input is used as is.  Replaces BatchNormLayer
+ * apply + ResidualBlock join + post-activation (residual_block.py:65-75). */
+int dk_bn_add_f32(const float* a, const float* a_mean, const float* a_invstd, const float* a_gamma, const float* a_beta, int a_relu, const float* b, const float* b_mean, const float* b_invstd, const float* b_gamma, const float* b_beta, int b_relu, long long n, int C, int relu, float* y, uint8_t* mask, void* stream);
 int dk_gap_fwd_f32(const float* x, int N, int HW, int C, float* out, void* stream);
 int dk_gap_bwd_f32(const float* dy, int N, int HW, int C, float* dx, void* stream);
 int dk_softmax_xent_fwd_f32(const float* x, const float* y_onehot, int B, int K, float* p, float* loss, void* stream);

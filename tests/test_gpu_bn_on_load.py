@@ -1,0 +1,150 @@
+"""BN on load (dk_*_bnx_f32, dk_bn_add_f32): a consumer that applies the preceding
+BatchNorm (+ReLU) as it loads its input must produce exactly -- bitwise -- what the
+unfused sequence dk_bn_apply_f32 -> consumer produces (same bn_out arithmetic, padding 0).
+Parity of the unfused sequence itself with the oracle is covered in test_gpu_layers.py."""
+import numpy as np
+import pytest
+import torch
+
+from dorknet_amd._hip import lib, stream_handle, workspace
+
+pytestmark = pytest.mark.gpu
+
+
+def nhwc(a):
+    t = torch.as_tensor(np.ascontiguousarray(a, dtype=np.float32), device="cuda")
+    return t.contiguous(memory_format=torch.channels_last) if t.dim() == 4 else t
+
+
+def bn_params(C, rng):
+    mean = torch.as_tensor(rng.randn(C).astype(np.float32), device="cuda")
+    invstd = torch.as_tensor((0.5 + rng.rand(C)).astype(np.float32), device="cuda")
+    gamma = torch.as_tensor(rng.randn(C).astype(np.float32), device="cuda")
+    beta = torch.as_tensor(rng.randn(C).astype(np.float32), device="cuda")
+    return mean, invstd, gamma, beta
+
+
+def args(p, relu):
+    return (p[0].data_ptr(), p[1].data_ptr(), p[2].data_ptr(), p[3].data_ptr(), int(relu))
+
+
+def apply(x, p, relu):
+    y = torch.empty_like(x)
+    lib.dk_bn_apply_f32(x.data_ptr(), x.numel(), x.shape[1], p[0].data_ptr(), p[1].data_ptr(), p[2].data_ptr(),
+                        p[3].data_ptr(), int(relu), y.data_ptr(), 0, stream_handle())
+    return y
+
+
+def same(a, b):
+    torch.cuda.synchronize()
+    assert torch.equal(a, b), float((a - b).abs().max())
+
+
+@pytest.mark.parametrize("stride,relu", [(1, 0), (1, 1), (2, 1), (2, 0)])
+def test_pointwise_bnx_bitwise(stride, relu):
+    rng = np.random.RandomState(stride * 10 + relu)
+    N, C, H, W, K = 3, 24, 13, 11, 40
+    x = nhwc(rng.randn(N, C, H, W))
+    w = torch.as_tensor(rng.randn(K, C).astype(np.float32), device="cuda")
+    p = bn_params(C, rng)
+    OH, OW = -(-H // stride), -(-W // stride)
+    st = stream_handle()
+    y0 = torch.empty((N, K, OH, OW), device="cuda").contiguous(memory_format=torch.channels_last)
+    y1 = torch.empty_like(y0)
+    xa = apply(x, p, relu)
+    lib.dk_pwconv_fwd_f32(xa.data_ptr(), N, H, W, C, w.data_ptr(), K, stride, 0, y0.data_ptr(), OH, OW, st)
+    lib.dk_pwconv_fwd_bnx_f32(x.data_ptr(), N, H, W, C, w.data_ptr(), K, stride, 0, y1.data_ptr(), OH, OW,
+                              *args(p, relu), st)
+    same(y0, y1)
+    dy = nhwc(rng.randn(N, K, OH, OW))
+    nb = lib.dk_pwconv_wgrad_workspace_bytes(N, OH, OW, K, C)
+    g0 = torch.empty((K, C), device="cuda")
+    g1 = torch.empty_like(g0)
+    lib.dk_pwconv_wgrad_f32(dy.data_ptr(), xa.data_ptr(), N, H, W, C, K, stride, OH, OW, 0, 0.0, g0.data_ptr(),
+                            workspace.get(nb), nb, st)
+    lib.dk_pwconv_wgrad_bnx_f32(dy.data_ptr(), x.data_ptr(), N, H, W, C, K, stride, OH, OW, 0, 0.0, g1.data_ptr(),
+                                workspace.get(nb), nb, *args(p, relu), st)
+    same(g0, g1)
+
+
+@pytest.mark.parametrize("stride,relu", [(1, 1), (2, 1), (1, 0)])
+def test_depthwise_bnx_bitwise(stride, relu):
+    rng = np.random.RandomState(7 + stride + relu)
+    N, C, H, W, R = 2, 36, 15, 14, 3
+    pad = 1
+    x = nhwc(rng.randn(N, C, H, W))
+    w = torch.as_tensor(rng.randn(C, R, R).astype(np.float32), device="cuda")
+    p = bn_params(C, rng)
+    OH, OW = (H + 2 * pad - R) // stride + 1, (W + 2 * pad - R) // stride + 1
+    st = stream_handle()
+    w_rsc = torch.empty((R, R, C), device="cuda")
+    lib.dk_dw_weight_rsc_f32(w.data_ptr(), C, R, R, w_rsc.data_ptr(), st)
+    y0 = torch.empty((N, C, OH, OW), device="cuda").contiguous(memory_format=torch.channels_last)
+    y1 = torch.empty_like(y0)
+    xa = apply(x, p, relu)
+    lib.dk_dwconv_fwd_f32(xa.data_ptr(), N, H, W, C, w_rsc.data_ptr(), R, R, stride, pad, 0, y0.data_ptr(), OH, OW,
+                          st)
+    lib.dk_dwconv_fwd_bnx_f32(x.data_ptr(), N, H, W, C, w_rsc.data_ptr(), R, R, stride, pad, 0, y1.data_ptr(), OH, OW,
+                              *args(p, relu), st)
+    same(y0, y1)
+    dy = nhwc(rng.randn(N, C, OH, OW))
+    nb = lib.dk_dwconv_wgrad_workspace_bytes(N, OH, OW, C, R, R)
+    g0 = torch.empty((C, R, R), device="cuda")
+    g1 = torch.empty_like(g0)
+    lib.dk_dwconv_wgrad_f32(dy.data_ptr(), xa.data_ptr(), N, H, W, C, R, R, stride, pad, OH, OW, 0, 0.0,
+                            g0.data_ptr(), workspace.get(nb), nb, st)
+    lib.dk_dwconv_wgrad_bnx_f32(dy.data_ptr(), x.data_ptr(), N, H, W, C, R, R, stride, pad, OH, OW, 0, 0.0,
+                                g1.data_ptr(), workspace.get(nb), nb, *args(p, relu), st)
+    same(g0, g1)
+
+
+def test_conv_bnx_bitwise():
+    rng = np.random.RandomState(3)
+    N, C, H, W, K, R, pad, stride = 2, 12, 10, 9, 20, 3, 1, 1
+    x = nhwc(rng.randn(N, C, H, W))
+    w = torch.as_tensor(rng.randn(K, C, R, R).astype(np.float32), device="cuda")
+    p = bn_params(C, rng)
+    OH, OW = H, W
+    st = stream_handle()
+    w_krsc = torch.empty((K, R, R, C), device="cuda")
+    lib.dk_conv_weight_krsc_f32(w.data_ptr(), K, C, R, R, C, w_krsc.data_ptr(), st)
+    y0 = torch.empty((N, K, OH, OW), device="cuda").contiguous(memory_format=torch.channels_last)
+    y1 = torch.empty_like(y0)
+    xa = apply(x, p, 1)
+    lib.dk_conv2d_fwd_f32(xa.data_ptr(), N, H, W, C, w_krsc.data_ptr(), K, R, R, stride, pad, 0, y0.data_ptr(), OH,
+                          OW, st)
+    lib.dk_conv2d_fwd_bnx_f32(x.data_ptr(), N, H, W, C, w_krsc.data_ptr(), K, R, R, stride, pad, 0, y1.data_ptr(),
+                              OH, OW, *args(p, 1), st)
+    same(y0, y1)
+    dy = nhwc(rng.randn(N, K, OH, OW))
+    nb = lib.dk_conv2d_wgrad_workspace_bytes(N, OH, OW, K, C, R, R)
+    g0 = torch.empty((K, C, R, R), device="cuda")
+    g1 = torch.empty_like(g0)
+    lib.dk_conv2d_wgrad_f32(dy.data_ptr(), xa.data_ptr(), N, H, W, C, C, K, R, R, stride, pad, OH, OW, 0, 0.0,
+                            g0.data_ptr(), workspace.get(nb), nb, st)
+    lib.dk_conv2d_wgrad_bnx_f32(dy.data_ptr(), x.data_ptr(), N, H, W, C, C, K, R, R, stride, pad, OH, OW, 0, 0.0,
+                                g1.data_ptr(), workspace.get(nb), nb, *args(p, 1), st)
+    same(g0, g1)
+
+
+@pytest.mark.parametrize("bn_a,bn_b", [(True, False), (True, True), (False, True)])
+def test_bn_add_bitwise(bn_a, bn_b):
+    rng = np.random.RandomState(int(bn_a) * 2 + int(bn_b))
+    N, C, H, W = 2, 20, 7, 9
+    a = nhwc(rng.randn(N, C, H, W))
+    b = nhwc(rng.randn(N, C, H, W))
+    pa, pb = bn_params(C, rng), bn_params(C, rng)
+    st = stream_handle()
+    a0 = apply(a, pa, 0) if bn_a else a
+    b0 = apply(b, pb, 1) if bn_b else b
+    n = a.numel()
+    y0 = torch.empty_like(a)
+    m0 = torch.empty(a.shape, dtype=torch.uint8, device="cuda").contiguous(memory_format=torch.channels_last)
+    lib.dk_add_f32(a0.data_ptr(), b0.data_ptr(), n, 1, y0.data_ptr(), m0.data_ptr(), st)
+    y1 = torch.empty_like(a)
+    m1 = torch.empty_like(m0)
+    none = (0, 0, 0, 0, 0)
+    lib.dk_bn_add_f32(a.data_ptr(), *(args(pa, 0) if bn_a else none), b.data_ptr(), *(args(pb, 1) if bn_b else none),
+                      n, C, 1, y1.data_ptr(), m1.data_ptr(), st)
+    same(y0, y1)
+    same(m0, m1)

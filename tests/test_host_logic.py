@@ -131,3 +131,52 @@ def test_perf_model_config2():
     f, b = perfmodel.work("dk_conv2d_fwd_f32", (0, 256, 56, 56, 64, 0, 64, 3, 3, 1, 1, 0, 0, 56, 56, 0))
     assert f == 2 * 256 * 56 * 56 * 64 * 64 * 9            # 59.19 GFLOP
     assert b == 4 * (2 * 256 * 56 * 56 * 64 + 64 * 64 * 9)
+
+
+def test_perf_model_covers_header_signatures():
+    """Every modelled entry point is declared in include/dorknet_hip.h and its formula takes
+    exactly the declared arguments (the bench's roofline accounting cannot drift)."""
+    from dorknet_amd import perfmodel
+    from dorknet_amd._hip import parse_header
+    decls = parse_header()
+    for name in perfmodel.MODEL:
+        assert name in decls, name
+        args = tuple(1 for _ in decls[name][1])
+        f, b = perfmodel.work(name, args)
+        assert f >= 0 and b >= 0, name
+
+
+def test_bn_fusion_plan_resnet():
+    """The executor's plan for ResNet-18-depsep: every BatchNorm is applied by its consumer
+    (pointwise / depthwise convolutions, residual blocks and joins) -- none is written."""
+    from dorknet_amd.layers._chain import plan_group
+    from dorknet_amd.layers.batch_norm import BatchNormLayer
+    from dorknet_amd.layers.residual_block import ResidualBlock
+    from examples.resnet18_depsep import ResNet18
+    net = ResNet18("r18")
+    modes = []
+    i = 0
+    while i < len(net.layers):
+        group, mode = plan_group(net.layers, i, True)
+        modes.append((group[0].layer_name, mode))
+        i += len(group)
+    assert ("conv0_bn", "defer") in modes and ("pw0_bn", "defer") in modes
+    for layer in net.layers:
+        if isinstance(layer, ResidualBlock):
+            ll, j, inner = layer.layer_list, 0, []
+            while j < len(ll):
+                group, mode = plan_group(ll, j, True, out_accepts=True)
+                if isinstance(group[0], BatchNormLayer):
+                    inner.append(mode)
+                j += len(group)
+            assert inner == ["defer"] * 4, (layer.layer_name, inner)
+
+
+def test_bn_fusion_plan_keeps_terminal_output():
+    from dorknet_amd.layers._chain import plan_group
+    from examples.resnet18_depsep import ResNet18
+    net = ResNet18("r18")
+    group, mode = plan_group(net.layers, 1, True, keep=("conv0_relu",))
+    assert mode == "pair"
+    group, mode = plan_group(net.layers, 1, False)
+    assert mode == "single"
