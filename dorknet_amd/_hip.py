@@ -89,7 +89,7 @@ class _Lib:
             fn = getattr(lib, name)
             fn.restype = ctypes.c_size_t if ret == "size_t" else ctypes.c_int
             fn.argtypes = [_argtype(t) for t, _ in params]
-            if ret == "int" and not name.endswith(("_blocks", "_version")) and not name.startswith("dk_debug"):
+            if ret == "int" and not name.endswith(("_blocks", "_version", "_rows")) and not name.startswith("dk_debug"):
                 fn.errcheck = _errcheck
         self._decls = decls
         self._lib = lib

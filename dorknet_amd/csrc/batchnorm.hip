@@ -185,6 +185,32 @@ __global__ __launch_bounds__(256) void bn_collapse_kernel(const double* __restri
   }
 }
 
+// Coalesced fixed-order row reduction of partials: out[blockIdx.x][w][c] =
+// sum_{b in the block's kRowsPerBlock rows} part[b][w][c].  Block = 64 channels x 4 row lanes.
+constexpr int kRowsPerBlock = 64;
+__global__ __launch_bounds__(256) void bn_rows_reduce_kernel(const double* __restrict__ part, int nblk, int C,
+                                                             double* __restrict__ out) {
+  __shared__ double red[4][64][2];
+  const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
+  const int c = blockIdx.y * 64 + cl;
+  const int b0 = blockIdx.x * kRowsPerBlock;
+  const int b1 = min(nblk, b0 + kRowsPerBlock);
+  double s = 0.0, q = 0.0;
+  if (c < C) {
+    for (int b = b0 + rl; b < b1; b += 4) {
+      s += part[((size_t)b * 2 + 0) * C + c];
+      q += part[((size_t)b * 2 + 1) * C + c];
+    }
+  }
+  red[rl][cl][0] = s;
+  red[rl][cl][1] = q;
+  __syncthreads();
+  if (rl == 0 && c < C) {
+    out[((size_t)blockIdx.x * 2 + 0) * C + c] = red[0][cl][0] + red[1][cl][0] + red[2][cl][0] + red[3][cl][0];
+    out[((size_t)blockIdx.x * 2 + 1) * C + c] = red[0][cl][1] + red[1][cl][1] + red[2][cl][1] + red[3][cl][1];
+  }
+}
+
 // ---------------------------------------------------------------------------------------
 // forward apply: y = gamma * (x - mean) * invstd + beta  [+ ReLU, optional uint8 mask]
 // ---------------------------------------------------------------------------------------
@@ -485,6 +511,42 @@ DK_API int dk_bn_stats_f32(const float* x, int P, int C, float eps, float moment
   if (rc) return rc;
   return dk_bn_stats_finalize_f32(ws, bn_blocks(P, C), C, (double)P, eps, momentum, first, mean, std_, invstd,
                                   run_mean, run_std, stream);
+}
+
+// Statistics from partial sums written by a producer's epilogue (*_fwd_ex_f32): part[nblk][2][C].
+DK_API size_t dk_bn_partials_workspace_bytes(int nblk, int C) {
+  return (size_t)cdiv(nblk, kRowsPerBlock) * 2 * C * sizeof(double);
+}
+
+// Fold part[nblk][2][C] to <= kRowsPerBlock rows in ws (fixed order); returns the row count.
+static int fold_partials(const double* part, int nblk, int C, double* ws, hipStream_t st, const double** out) {
+  *out = part;
+  if (nblk <= kRowsPerBlock) return nblk;
+  const int n2 = cdiv(nblk, kRowsPerBlock);
+  hipLaunchKernelGGL(bn_rows_reduce_kernel, dim3(n2, cdiv(C, 64)), dim3(256), 0, st, part, nblk, C, ws);
+  *out = ws;
+  return n2;
+}
+
+DK_API int dk_bn_stats_from_partials_f32(const void* part, int nblk, int C, double count, float eps, float momentum,
+                                         int first, float* mean, float* std_, float* invstd, float* run_mean,
+                                         float* run_std, void* ws, size_t ws_bytes, void* stream) {
+  if (ws_bytes < dk_bn_partials_workspace_bytes(nblk, C)) return DK_ERR_WORKSPACE;
+  const double* p;
+  const int n = fold_partials(static_cast<const double*>(part), nblk, C, static_cast<double*>(ws),
+                              as_stream(stream), &p);
+  return dk_bn_stats_finalize_f32(p, n, C, count, eps, momentum, first, mean, std_, invstd, run_mean, run_std,
+                                  stream);
+}
+
+// out[2][C] = the column sums of part[nblk][2][C] (SyncBN: the vector each rank all-reduces).
+DK_API int dk_bn_reduce_partials_f64(const void* part, int nblk, int C, void* out, void* ws, size_t ws_bytes,
+                                     void* stream) {
+  if (ws_bytes < dk_bn_partials_workspace_bytes(nblk, C)) return DK_ERR_WORKSPACE;
+  const double* p;
+  const int n = fold_partials(static_cast<const double*>(part), nblk, C, static_cast<double*>(ws),
+                              as_stream(stream), &p);
+  return dk_bn_collapse_f64(p, n, C, out, stream);
 }
 
 DK_API int dk_bn_infer_params_f32(const float* run_std, int C, float* invstd, void* stream) {

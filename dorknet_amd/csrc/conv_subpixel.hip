@@ -21,22 +21,6 @@
 namespace dk {
 namespace {
 
-template <int R, int ST, int PAD>
-struct SubPix {
-  static constexpr int phase(int r) { return ((r - PAD) % ST + ST) % ST; }
-  static constexpr int nb(int r) { return (phase(r) + PAD - r) / ST; }
-  static constexpr int dmin() {
-    int m = 1 << 20;
-    for (int r = 0; r < R; ++r) m = nb(r) < m ? nb(r) : m;
-    return m;
-  }
-  static constexpr int dmax() {
-    int m = -(1 << 20);
-    for (int r = 0; r < R; ++r) m = nb(r) > m ? nb(r) : m;
-    return m;
-  }
-};
-
 constexpr int kTI = 4;          // quad rows per block (one wave each)
 constexpr int kTJ = 64;         // quad columns per block (one lane each)
 constexpr int kKC = 16;         // dy channels staged per pass

@@ -79,47 +79,148 @@ __device__ __forceinline__ void load_strip(f32x4 (&strip)[R][NC], __amdgpu_buffe
 // y[n,oh,ow,c] = sum_{r,s} w[r][s][c] * x[n, oh*ST + r - pad, ow*ST + s - pad, c] (+ bias[c])
 // Thread = (n, oh, TW-wide chunk of ow, 4 channels); consecutive threads take consecutive
 // channel groups, so a wave reads whole pixel rows.
-template <int R, int S, int ST, bool BN>
+// STATS: also the BatchNorm statistics of y (fp64 sum, sum of squares per channel) of this
+// block's outputs -> part[block][2][C]; needs 256 % (C/4) == 0 so that a block covers every
+// channel (thread tid always has channel group tid % (C/4)).
+template <int R, int S, int ST, bool BN, bool STATS>
 __global__ __launch_bounds__(256) void dw_fwd_kernel(const float* __restrict__ x, uint32_t xbytes,
                                                      const float* __restrict__ wt, const float* __restrict__ bias,
                                                      float* __restrict__ y, int N, int H, int W, int C, int OH, int OW,
-                                                     int pad, BnIn bn) {
+                                                     int pad, BnIn bn, double* __restrict__ part) {
   constexpr int TW = DwTile<ST>::TW;
   constexpr int NC = (TW - 1) * ST + S;
   const int C4 = C >> 2;
   const int nwc = (OW + TW - 1) / TW;
   const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const long long total = (long long)N * OH * nwc * C4;
-  if (idx >= total) return;
+  const bool live = idx < total;
+  if (!STATS && !live) return;
+  const int cq = (int)(idx % C4);
+  const int c = cq * 4;
+  double s1[4] = {0.0, 0.0, 0.0, 0.0}, s2[4] = {0.0, 0.0, 0.0, 0.0};
+  if (live) {
+    long long t = idx / C4;
+    const int wc = (int)(t % nwc);
+    t /= nwc;
+    const int oh = (int)(t % OH);
+    const int n = (int)(t / OH);
+    const int ow0 = wc * TW;
+    f32x4 strip[R][NC];
+    load_strip<R, NC, BN>(strip, make_rsrc(x, xbytes), n, oh * ST - pad, ow0 * ST - pad, H, W, C, c, bn);
+    f32x4 wv[R][S];
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+      for (int s = 0; s < S; ++s) wv[r][s] = ld4(wt + (r * S + s) * C + c);
+    const f32x4 b0 = bias ? ld4(bias + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+    float* yrow = y + ((size_t)(n * OH + oh) * OW) * C + c;
+#pragma unroll
+    for (int j = 0; j < TW; ++j) {
+      f32x4 acc = b0;
+#pragma unroll
+      for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int s = 0; s < S; ++s) acc += strip[r][j * ST + s] * wv[r][s];
+      if (ow0 + j < OW) {
+        st4(yrow + (size_t)(ow0 + j) * C, acc);
+        if constexpr (STATS) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const double v = (double)acc[e];
+            s1[e] += v;
+            s2[e] += v * v;
+          }
+        }
+      }
+    }
+  }
+  if constexpr (STATS) {
+    // fixed-order block reduction over the 256 / C4 threads of each channel group
+    __shared__ double red[256][8];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      red[threadIdx.x][e] = s1[e];
+      red[threadIdx.x][4 + e] = s2[e];
+    }
+    __syncthreads();
+    const int per = 256 / C4;
+    for (int i = threadIdx.x; i < C4 * 8; i += 256) {
+      const int g = i >> 3, e = i & 7;
+      double a = 0.0;
+      for (int k = 0; k < per; ++k) a += red[k * C4 + g][e];
+      part[((size_t)blockIdx.x * 2 + (e >> 2)) * C + g * 4 + (e & 3)] = a;
+    }
+  }
+}
+
+// Stride > 1 dgrad by sub-pixel decomposition (see SubPix): thread = 4 channels of TWQ
+// consecutive ST x ST quads of dx; the dy neighbourhood columns are shared by adjacent quads.
+template <int R, int S, int ST, int PAD>
+__global__ __launch_bounds__(256) void dw_dgrad_subpixel_kernel(const float* __restrict__ dy, uint32_t dybytes,
+                                                                const float* __restrict__ wt, float* __restrict__ dx,
+                                                                int N, int H, int W, int C, int OH, int OW) {
+  using RP = SubPix<R, ST, PAD>;
+  using SP = SubPix<S, ST, PAD>;
+  constexpr int DR0 = RP::dmin(), NR = RP::dmax() - RP::dmin() + 1;
+  constexpr int DS0 = SP::dmin(), NS = SP::dmax() - SP::dmin() + 1;
+  constexpr int TWQ = 4;
+  constexpr int NCOL = TWQ + NS - 1;
+  const int C4 = C >> 2;
+  const int QH = (H + ST - 1) / ST, QW = (W + ST - 1) / ST;
+  const int nqc = (QW + TWQ - 1) / TWQ;
+  const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (long long)N * QH * nqc * C4) return;
   const int cq = (int)(idx % C4);
   long long t = idx / C4;
-  const int wc = (int)(t % nwc);
-  t /= nwc;
-  const int oh = (int)(t % OH);
-  const int n = (int)(t / OH);
+  const int qc = (int)(t % nqc);
+  t /= nqc;
+  const int qi = (int)(t % QH);
+  const int n = (int)(t / QH);
   const int c = cq * 4;
-  const int ow0 = wc * TW;
-  f32x4 strip[R][NC];
-  load_strip<R, NC, BN>(strip, make_rsrc(x, xbytes), n, oh * ST - pad, ow0 * ST - pad, H, W, C, c, bn);
+  const int j0 = qc * TWQ;
+  const __amdgpu_buffer_rsrc_t rs = make_rsrc(dy, dybytes);
+  f32x4 d[NR][NCOL];
+#pragma unroll
+  for (int a = 0; a < NR; ++a) {
+    const int oh = qi + DR0 + a;
+#pragma unroll
+    for (int b = 0; b < NCOL; ++b) {
+      const int ow = j0 + DS0 + b;
+      const bool ok = (unsigned)oh < (unsigned)OH && (unsigned)ow < (unsigned)OW;
+      d[a][b] = bload4(rs, ok ? (uint32_t)(((n * OH + oh) * OW + ow) * C + c) * 4u : kOOB);
+    }
+  }
   f32x4 wv[R][S];
 #pragma unroll
   for (int r = 0; r < R; ++r)
 #pragma unroll
     for (int s = 0; s < S; ++s) wv[r][s] = ld4(wt + (r * S + s) * C + c);
-  const f32x4 b0 = bias ? ld4(bias + c) : f32x4{0.f, 0.f, 0.f, 0.f};
-  float* yrow = y + ((size_t)(n * OH + oh) * OW) * C + c;
 #pragma unroll
-  for (int j = 0; j < TW; ++j) {
-    f32x4 acc = b0;
+  for (int q = 0; q < TWQ; ++q) {
+    f32x4 acc[ST][ST];
+#pragma unroll
+    for (int a = 0; a < ST; ++a)
+#pragma unroll
+      for (int b = 0; b < ST; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int r = 0; r < R; ++r)
 #pragma unroll
-      for (int s = 0; s < S; ++s) acc += strip[r][j * ST + s] * wv[r][s];
-    if (ow0 + j < OW) st4(yrow + (size_t)(ow0 + j) * C, acc);
+      for (int s = 0; s < S; ++s)
+        acc[RP::phase(r)][SP::phase(s)] += d[RP::nb(r) - DR0][q + SP::nb(s) - DS0] * wv[r][s];
+    const int j = j0 + q;
+#pragma unroll
+    for (int a = 0; a < ST; ++a) {
+      const int h = qi * ST + a;
+#pragma unroll
+      for (int b = 0; b < ST; ++b) {
+        const int w = j * ST + b;
+        if (j < QW && h < H && w < W) st4(dx + (((size_t)n * H + h) * W + w) * C + c, acc[a][b]);
+      }
+    }
   }
 }
 
-// General-stride dgrad gather (used for stride > 1):
+// General-stride dgrad gather (used for stride > 1 geometries without a sub-pixel kernel):
 // dx[n,h,w,c] = sum_{r,s : h + pad - r = oh*st, w + pad - s = ow*st} w[r][s][c] * dy[n,oh,ow,c]
 template <int R, int S>
 __global__ __launch_bounds__(256) void dw_dgrad_gather_kernel(const float* __restrict__ dy,
@@ -247,28 +348,43 @@ static inline bool bn_ok(const BnIn& bn) {
                       aligned16(bn.gamma) && aligned16(bn.beta));
 }
 
+template <int ST>
+static long long dw_fwd_threads(int N, int OH, int OW, int C) {
+  constexpr int TW = DwTile<ST>::TW;
+  return (long long)N * OH * ((OW + TW - 1) / TW) * (C / 4);
+}
+
 template <int R, int S, int ST>
 static void launch_dw_fwd(const float* x, const float* wt, const float* bias, float* y, int N, int H, int W, int C,
-                          int OH, int OW, int pad, const BnIn& bn, hipStream_t st) {
-  constexpr int TW = DwTile<ST>::TW;
-  const long long total = (long long)N * OH * ((OW + TW - 1) / TW) * (C / 4);
+                          int OH, int OW, int pad, const BnIn& bn, double* part, hipStream_t st) {
   const uint32_t xb = (uint32_t)((size_t)N * H * W * C * sizeof(float));
-  const dim3 grid((unsigned)cdivll(total, 256));
-  if (bn.mean)
-    hipLaunchKernelGGL((dw_fwd_kernel<R, S, ST, true>), grid, dim3(256), 0, st, x, xb, wt, bias, y, N, H, W, C, OH, OW,
-                       pad, bn);
-  else
-    hipLaunchKernelGGL((dw_fwd_kernel<R, S, ST, false>), grid, dim3(256), 0, st, x, xb, wt, bias, y, N, H, W, C, OH,
-                       OW, pad, bn);
+  const dim3 grid((unsigned)cdivll(dw_fwd_threads<ST>(N, OH, OW, C), 256));
+#define DW_LAUNCH(B, ST_)                                                                                            \
+  hipLaunchKernelGGL((dw_fwd_kernel<R, S, ST, B, ST_>), grid, dim3(256), 0, st, x, xb, wt, bias, y, N, H, W, C, OH, \
+                     OW, pad, bn, part)
+  if (bn.mean) {
+    if (part)
+      DW_LAUNCH(true, true);
+    else
+      DW_LAUNCH(true, false);
+  } else {
+    if (part)
+      DW_LAUNCH(false, true);
+    else
+      DW_LAUNCH(false, false);
+  }
+#undef DW_LAUNCH
 }
 
 static int dw_fwd_dispatch(const float* x, const float* wt, const float* bias, float* y, int N, int H, int W, int C,
-                           int R, int S, int stride, int OH, int OW, int pad, const BnIn& bn, hipStream_t st) {
+                           int R, int S, int stride, int OH, int OW, int pad, const BnIn& bn, hipStream_t st,
+                           double* part = nullptr) {
   if (C % 4 || !aligned16(x) || !aligned16(wt) || !fits((size_t)N * H * W * C * 4) || !bn_ok(bn)) return DK_ERR_ARGS;
-#define DW_CASE(RR, SS, STR)                                                      \
-  if (R == RR && S == SS && stride == STR) {                                      \
-    launch_dw_fwd<RR, SS, STR>(x, wt, bias, y, N, H, W, C, OH, OW, pad, bn, st);  \
-    return launch_status();                                                       \
+  if (part && (C / 4 > 256 || 256 % (C / 4))) return DK_ERR_ARGS;
+#define DW_CASE(RR, SS, STR)                                                            \
+  if (R == RR && S == SS && stride == STR) {                                            \
+    launch_dw_fwd<RR, SS, STR>(x, wt, bias, y, N, H, W, C, OH, OW, pad, bn, part, st);  \
+    return launch_status();                                                             \
   }
   DW_CASE(3, 3, 1)
   DW_CASE(3, 3, 2)
@@ -309,6 +425,23 @@ DK_API int dk_dwconv_fwd_bnx_f32(const float* x, int N, int H, int W, int C, con
                          BnIn{bn_mean, bn_invstd, bn_gamma, bn_beta, bn_relu}, as_stream(stream));
 }
 
+// Rows of BatchNorm partial statistics dk_dwconv_fwd_ex_f32 writes; 0 = statistics not
+// supported for this channel count (C/4 must divide 256).
+DK_API int dk_dwconv_fwd_stats_rows(int N, int OH, int OW, int C, int stride) {
+  if (C % 4 || C / 4 > 256 || 256 % (C / 4)) return 0;
+  const long long thr = stride == 1 ? dw_fwd_threads<1>(N, OH, OW, C) : dw_fwd_threads<2>(N, OH, OW, C);
+  return (int)cdivll(thr, 256);
+}
+
+DK_API int dk_dwconv_fwd_ex_f32(const float* x, int N, int H, int W, int C, const float* w_rsc, int R, int S,
+                                int stride, int pad, const float* bias, float* y, int OH, int OW,
+                                const float* bn_mean, const float* bn_invstd, const float* bn_gamma,
+                                const float* bn_beta, int bn_relu, double* stats, void* stream) {
+  if (stride != 1 && stride != 2) return DK_ERR_ARGS;
+  return dw_fwd_dispatch(x, w_rsc, bias, y, N, H, W, C, R, S, stride, OH, OW, pad,
+                         BnIn{bn_mean, bn_invstd, bn_gamma, bn_beta, bn_relu}, as_stream(stream), stats);
+}
+
 // w_rsc is the (unflipped) [R][S][C] copy; stride-1 dgrad flips it internally into ws.
 DK_API size_t dk_dwconv_dgrad_workspace_bytes(int C, int R, int S) { return (size_t)C * R * S * sizeof(float); }
 
@@ -329,6 +462,19 @@ DK_API int dk_dwconv_dgrad_f32(const float* dy, int N, int OH, int OW, int C, co
   hipLaunchKernelGGL(dw_weight_rsc_kernel, dim3(cdiv(C * R * S, 256)), dim3(256), 0, st, w_crs, C, R, S, 0, wt);
   int rc = launch_status();
   if (rc) return rc;
+  if (!fits((size_t)N * OH * OW * C * 4) || !aligned16(dy) || !aligned16(dx)) return DK_ERR_ARGS;
+  const uint32_t gb = (uint32_t)((size_t)N * OH * OW * C * 4);
+#define DW_SUBPIX(RR, SS, STR, PD)                                                                                   \
+  if (R == RR && S == SS && stride == STR && pad == PD) {                                                            \
+    const long long items = (long long)N * cdiv(H, STR) * cdiv(cdiv(W, STR), 4) * (C / 4);                         \
+    hipLaunchKernelGGL((dw_dgrad_subpixel_kernel<RR, SS, STR, PD>), dim3((unsigned)cdivll(items, 256)), dim3(256), 0, \
+                       st, dy, gb, wt, dx, N, H, W, C, OH, OW);                                                      \
+    return launch_status();                                                                                          \
+  }
+  DW_SUBPIX(3, 3, 2, 1)
+  DW_SUBPIX(5, 5, 2, 2)
+  DW_SUBPIX(1, 1, 2, 0)
+#undef DW_SUBPIX
   const long long total = (long long)N * H * W * (C / 4);
   const dim3 grid((unsigned)cdivll(total, 256));
   if (R == 3 && S == 3)

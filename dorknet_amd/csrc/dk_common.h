@@ -72,6 +72,25 @@ __device__ __forceinline__ f32x4 bn_in4(f32x4 v, f32x4 m, f32x4 is, f32x4 g, f32
   return o;
 }
 
+// Sub-pixel decomposition of a stride-ST correlation's input gradient (conv_subpixel.hip,
+// depthwise.hip): with h = ST*i + a, tap r reaches dx row h iff a == phase(r), and then
+// reads dy row i + nb(r).  dmin/dmax bound the dy neighbourhood of one ST x ST "quad".
+template <int R, int ST, int PAD>
+struct SubPix {
+  static constexpr int phase(int r) { return ((r - PAD) % ST + ST) % ST; }
+  static constexpr int nb(int r) { return (phase(r) + PAD - r) / ST; }
+  static constexpr int dmin() {
+    int m = 1 << 20;
+    for (int r = 0; r < R; ++r) m = nb(r) < m ? nb(r) : m;
+    return m;
+  }
+  static constexpr int dmax() {
+    int m = -(1 << 20);
+    for (int r = 0; r < R; ++r) m = nb(r) > m ? nb(r) : m;
+    return m;
+  }
+};
+
 // Error codes returned for argument errors detected on the host side.  They
 // live above the hipError_t range used by the runtime so callers can tell
 // "bad call" from "device fault".

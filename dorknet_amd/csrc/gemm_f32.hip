@@ -73,6 +73,7 @@ struct ImgBnDesc : ImgDesc {
 
 // Row-major matrix p[row][ld]; `ext` bounds the non-reduction index.
 struct MatDesc {
+  static constexpr bool kBnIn = false;
   const float* p;
   uint32_t bytes;
   int ld;
@@ -107,6 +108,7 @@ struct ICLayout {
 // Implicit-im2col rows of an NHWC image (K-contiguous).
 template <int ROWS, int BK, int NT>
 struct LdImgKC : KCLayout<ROWS, BK> {
+  static constexpr bool kTable = true;  // reads the BN table from LDS (see igemm_f32)
   using L = KCLayout<ROWS, BK>;
   static constexpr int KQ = BK / 4;
   static constexpr int RSTEP = NT / KQ;
@@ -115,8 +117,10 @@ struct LdImgKC : KCLayout<ROWS, BK> {
   bool active;
   int base[NR], ih0[NR], iw0[NR];
   f32x4 v[NR];
-  // input BatchNorm (ImgBnDesc): parameters of this thread's 4 channels, in-image rows
-  f32x4 bm, bi, bg, bb;
+  // input BatchNorm (ImgBnDesc): per-channel {mean, invstd, gamma, beta} table in LDS
+  // (filled by the kernel prologue), this k-tile's channel, in-image rows
+  const f32x4* tab;
+  int cch;
   uint32_t okm;
   int relu;
 
@@ -166,11 +170,7 @@ struct LdImgKC : KCLayout<ROWS, BK> {
       om |= (uint32_t)ok << j;
     }
     if constexpr (D::kBnIn) {
-      const int cc = kv ? c : 0;
-      bm = ld4(d.bn.mean + cc);
-      bi = ld4(d.bn.invstd + cc);
-      bg = ld4(d.bn.gamma + cc);
-      bb = ld4(d.bn.beta + cc);
+      cch = kv ? c : 0;
       okm = om;
     }
   }
@@ -182,7 +182,10 @@ struct LdImgKC : KCLayout<ROWS, BK> {
     for (int j = 0; j < NR; ++j) {
       f32x4 o = v[j];
       if constexpr (D::kBnIn) {
-        if ((okm >> j) & 1u) o = bn_in4(o, bm, bi, bg, bb, relu);
+        const f32x4 p0 = tab[cch], p1 = tab[cch + 1], p2 = tab[cch + 2], p3 = tab[cch + 3];
+        const f32x4 t = bn_in4(o, f32x4{p0[0], p1[0], p2[0], p3[0]}, f32x4{p0[1], p1[1], p2[1], p3[1]},
+                               f32x4{p0[2], p1[2], p2[2], p3[2]}, f32x4{p0[3], p1[3], p2[3], p3[3]}, relu);
+        if ((okm >> j) & 1u) o = t;
       }
       st4(T + (rb + j * RSTEP) * L::SK + 4 * kq, o);
     }
@@ -193,6 +196,7 @@ struct LdImgKC : KCLayout<ROWS, BK> {
 // (ld % 4 == 0, Ktot % 4 == 0); otherwise four scalar loads.
 template <int ROWS, int BK, int NT, bool VEC>
 struct LdMatKCT : KCLayout<ROWS, BK> {
+  static constexpr bool kTable = false;  // reads the BN table from LDS (see igemm_f32)
   using L = KCLayout<ROWS, BK>;
   static constexpr int KQ = BK / 4;
   static constexpr int RSTEP = NT / KQ;
@@ -240,6 +244,7 @@ using LdMatKC1 = LdMatKCT<ROWS, BK, NT, false>;
 // Row-major matrix p[k][ld], i along the row (row-contiguous).
 template <int ROWS, int BK, int NT, bool VEC>
 struct LdMatICT : ICLayout<ROWS, BK> {
+  static constexpr bool kTable = false;  // reads the BN table from LDS (see igemm_f32)
   using L = ICLayout<ROWS, BK>;
   static constexpr int IQ = ROWS / 4;
   static constexpr int KSTEP = NT / IQ;
@@ -287,6 +292,7 @@ using LdMatIC1 = LdMatICT<ROWS, BK, NT, false>;
 // Used by wgrad: B(i=(r,s,c), k=m) = x[pixel(m) shifted by tap (r,s)][c].
 template <int ROWS, int BK, int NT>
 struct LdImgIC : ICLayout<ROWS, BK> {
+  static constexpr bool kTable = false;  // reads the BN table from LDS (see igemm_f32)
   using L = ICLayout<ROWS, BK>;
   static constexpr int IQ = ROWS / 4;
   static constexpr int KSTEP = NT / IQ;
@@ -362,19 +368,28 @@ struct LdImgIC : ICLayout<ROWS, BK> {
 
 // out[m][n] = acc (+ bias[n]).
 struct EpStore {
+  static constexpr bool kColStats = false;
   float* out;
   int ldo;
   const float* bias;
-  __device__ __forceinline__ void put(int m, int n, float v, int) const {
-    if (bias) v += bias[n];
-    out[(size_t)m * ldo + n] = v;
-  }
+  __device__ __forceinline__ float value(int n, float v) const { return bias ? v + bias[n] : v; }
+  __device__ __forceinline__ void put(int m, int n, float v, int) const { out[(size_t)m * ldo + n] = value(n, v); }
+};
+
+// EpStore + the BatchNorm statistics of the stored output (layers/batch_norm.py:76-80's
+// mean/var, as fp64 sum / sum of squares per column): part[m_tile][2][N], one row per
+// BM-row tile, reduced in a fixed order by dk_bn_stats_from_partials_f32.  Saves the
+// separate statistics pass over y.
+struct EpStoreStats : EpStore {
+  static constexpr bool kColStats = true;
+  double* part;
 };
 
 // Pointwise stride-st backward "widen" (pointwise_convolution.py:68-72) fused: the GEMM
 // row m = (b, oh, ow) of an OH x OW grid lands at (b, oh*st, ow*st) of an
 // (OH*st) x (OW*st) grid and the other st*st-1 positions of that cell are zero.
 struct EpWiden {
+  static constexpr bool kColStats = false;
   float* out;
   int ldo;
   int OH, OW, st;
@@ -392,6 +407,7 @@ struct EpWiden {
 
 // Split-K partial tile: ws[split][M][N].
 struct EpPartial {
+  static constexpr bool kColStats = false;
   float* ws;
   int M, N;
   __device__ __forceinline__ void put(int m, int n, float v, int split) const {
@@ -441,6 +457,14 @@ __global__ __launch_bounds__(64 * WM * WN) void igemm_f32(DA da, DB db, EP ep, i
     LB lb;
     la.init(da, m0, tid);
     lb.init(db, n0, tid);
+    if constexpr (DA::kBnIn && LA::kTable) {
+      // BN-on-load parameter table for the A operand: {mean, invstd, gamma, beta} per channel
+      extern __shared__ f32x4 bn_tab[];
+      for (int c = tid; c < da.C; c += 64 * WM * WN)
+        bn_tab[c] = f32x4{da.bn.mean[c], da.bn.invstd[c], da.bn.gamma[c], da.bn.beta[c]};
+      la.tab = bn_tab;
+      __syncthreads();
+    }
     la.load(da, kt0 * BK, Ktot);
     lb.load(db, kt0 * BK, Ktot);
     la.template store<DA>(As);
@@ -492,6 +516,52 @@ __global__ __launch_bounds__(64 * WM * WN) void igemm_f32(DA da, DB db, EP ep, i
         if (row < M && col < N) ep.put(row, col, acc[t][u][r], blockIdx.y);
       }
     }
+
+  if constexpr (EP::kColStats) {
+    static_assert(WM * BN * 4 <= 2 * (ABUF + BBUF), "stats scratch fits the operand LDS");
+    // Column sums of the stored values over this tile's valid rows, fp64, fixed order:
+    // lane's 16*TM rows -> lane halves (h) -> waves along M (wm) -> part[m_tile][.][col].
+    __syncthreads();  // the MFMA loop's last LDS reads are done; reuse smem
+    double* red = reinterpret_cast<double*>(smem);  // [WM][BN][2]
+#pragma unroll
+    for (int u = 0; u < TN; ++u) {
+      const int lcol = wn * 32 * TN + u * 32 + l32;
+      const int col = n0 + lcol;
+      double s1 = 0.0, s2 = 0.0;
+      if (col < N) {
+#pragma unroll
+        for (int t = 0; t < TM; ++t)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int row = m0 + wm * 32 * TM + t * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+            if (row < M) {
+              const double v = (double)ep.value(col, acc[t][u][r]);
+              s1 += v;
+              s2 += v * v;
+            }
+          }
+      }
+      const double o1 = __shfl_xor(s1, 32, 64), o2 = __shfl_xor(s2, 32, 64);
+      if (h == 0) {
+        red[(wm * BN + lcol) * 2 + 0] = s1 + o1;
+        red[(wm * BN + lcol) * 2 + 1] = s2 + o2;
+      }
+    }
+    __syncthreads();
+    const int mt = blockIdx.x / tiles_n;
+    for (int i = tid; i < BN; i += 64 * WM * WN) {
+      const int col = n0 + i;
+      if (col >= N) continue;
+      double s1 = 0.0, s2 = 0.0;
+#pragma unroll
+      for (int w = 0; w < WM; ++w) {
+        s1 += red[(w * BN + i) * 2 + 0];
+        s2 += red[(w * BN + i) * 2 + 1];
+      }
+      ep.part[((size_t)mt * 2 + 0) * N + col] = s1;
+      ep.part[((size_t)mt * 2 + 1) * N + col] = s2;
+    }
+  }
 }
 
 // ----------------------------------------------------------------------------
@@ -550,7 +620,13 @@ static int launch_igemm(const DA& da, const DB& db, const EP& ep, int M, int N, 
   if (splits > KT) splits = KT > 0 ? KT : 1;
   const int kps = KT > 0 ? cdiv(KT, splits) : 1;
   splits = KT > 0 ? cdiv(KT, kps) : 1;
-  hipLaunchKernelGGL((igemm_f32<BM, BN, BK, WM, WN, A, DA, B, DB, EP>), dim3(tiles, splits), dim3(NT), 0, st, da,
+  size_t dyn = 0;
+  if constexpr (DA::kBnIn && A::kTable) {
+    dyn = (size_t)da.C * sizeof(f32x4);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&igemm_f32<BM, BN, BK, WM, WN, A, DA, B, DB, EP>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn);
+  }
+  hipLaunchKernelGGL((igemm_f32<BM, BN, BK, WM, WN, A, DA, B, DB, EP>), dim3(tiles, splits), dim3(NT), dyn, st, da,
                      db, ep, M, N, Ktot, kps);
   return launch_status();
 }
@@ -734,13 +810,6 @@ DK_API int dk_conv_weight_crsk_f32(const float* w_kcrs, int K, int C, int R, int
 }
 
 // y[n,oh,ow,k] = sum_{r,s,c} x[n, oh*stride + r - pad, ow*stride + s - pad, c] * w[k][r][s][c] (+ bias[k])
-template <class D>
-static int conv_fwd(const D& a, const float* w_krsc, int K, int Ktot, const float* bias, float* y, void* stream) {
-  MatDesc b = mat(w_krsc, K, Ktot, K);
-  EpStore ep{y, K, bias};
-  return igemm_rows<LdImgKC, D, LdMatKC, MatDesc, EpStore>(a, b, ep, a.M, K, Ktot, as_stream(stream));
-}
-
 static inline ImgBnDesc with_bn(const ImgDesc& d, const float* mean, const float* invstd, const float* gamma,
                                 const float* beta, int relu) {
   ImgBnDesc o;
@@ -751,6 +820,40 @@ static inline ImgBnDesc with_bn(const ImgDesc& d, const float* mean, const float
 static inline bool bn_ok(const float* mean, const float* invstd, const float* gamma, const float* beta) {
   return mean && invstd && gamma && beta && aligned16(mean) && aligned16(invstd) && aligned16(gamma) &&
          aligned16(beta);
+}
+
+template <class D>
+static int conv_fwd(const D& a, const float* w_krsc, int K, int Ktot, const float* bias, float* y, void* stream,
+                    double* stats = nullptr) {
+  if constexpr (D::kBnIn) {
+    if (a.C > 2048) return DK_ERR_ARGS;  // the LDS parameter table holds <= 2048 channels (32 KB)
+  }
+  MatDesc b = mat(w_krsc, K, Ktot, K);
+  if (stats) {
+    EpStoreStats ep;
+    ep.out = y;
+    ep.ldo = K;
+    ep.bias = bias;
+    ep.part = stats;
+    return igemm_rows<LdImgKC, D, LdMatKC, MatDesc, EpStoreStats>(a, b, ep, a.M, K, Ktot, as_stream(stream));
+  }
+  EpStore ep{y, K, bias};
+  return igemm_rows<LdImgKC, D, LdMatKC, MatDesc, EpStore>(a, b, ep, a.M, K, Ktot, as_stream(stream));
+}
+
+// Rows of BatchNorm partial statistics a *_fwd_ex_f32 call writes (one per output tile row).
+static int stats_rows(int M, int N, int Ktot) { return cdiv(M, kRowCfg[row_config(M, N, Ktot)].BM); }
+
+// Forward with an optional input BatchNorm (bn_mean != NULL, see *_bnx_*) and optional output
+// statistics (stats != NULL: stats_rows x 2 x K doubles).
+static int conv_fwd_ex(const ImgDesc& base, const float* w, int K, int Ktot, const float* bias, float* y,
+                       const float* bn_mean, const float* bn_invstd, const float* bn_gamma, const float* bn_beta,
+                       int bn_relu, double* stats, void* stream) {
+  if (bn_mean) {
+    if (!bn_ok(bn_mean, bn_invstd, bn_gamma, bn_beta)) return DK_ERR_ARGS;
+    return conv_fwd(with_bn(base, bn_mean, bn_invstd, bn_gamma, bn_beta, bn_relu), w, K, Ktot, bias, y, stream, stats);
+  }
+  return conv_fwd(base, w, K, Ktot, bias, y, stream, stats);
 }
 
 DK_API int dk_conv2d_fwd_f32(const float* x, int N, int H, int W, int C, const float* w_krsc, int K, int R, int S,
@@ -769,6 +872,21 @@ DK_API int dk_conv2d_fwd_bnx_f32(const float* x, int N, int H, int W, int C, con
   return conv_fwd(with_bn(img(x, N, H, W, C, OH, OW, R, S, stride, 1, -pad, N * OH * OW), bn_mean, bn_invstd,
                           bn_gamma, bn_beta, bn_relu),
                   w_krsc, K, R * S * C, bias, y, stream);
+}
+
+DK_API int dk_conv2d_fwd_stats_rows(int N, int OH, int OW, int K, int C, int R, int S) {
+  return stats_rows(N * OH * OW, K, R * S * C);
+}
+
+// Forward with optional BN on load (bn_mean != NULL) and optional output statistics
+// (stats != NULL: dk_conv2d_fwd_stats_rows() x 2 x K doubles, for dk_bn_stats_from_partials_f32).
+DK_API int dk_conv2d_fwd_ex_f32(const float* x, int N, int H, int W, int C, const float* w_krsc, int K, int R, int S,
+                                int stride, int pad, const float* bias, float* y, int OH, int OW,
+                                const float* bn_mean, const float* bn_invstd, const float* bn_gamma,
+                                const float* bn_beta, int bn_relu, double* stats, void* stream) {
+  if (C % 4 || !aligned16(x) || !aligned16(w_krsc) || !fits((size_t)N * H * W * C * 4)) return DK_ERR_ARGS;
+  return conv_fwd_ex(img(x, N, H, W, C, OH, OW, R, S, stride, 1, -pad, N * OH * OW), w_krsc, K, R * S * C, bias, y,
+                     bn_mean, bn_invstd, bn_gamma, bn_beta, bn_relu, stats, stream);
 }
 
 // Stride-1 dgrad as an implicit GEMM: dx[n,h,w,c] = sum_{r,s,k} dy[n, h+pad-r, w+pad-s, k] * w[k][c][r][s]
@@ -884,6 +1002,17 @@ DK_API int dk_pwconv_fwd_bnx_f32(const float* x, int N, int H, int W, int C, con
   return conv_fwd(with_bn(img(x, N, H, W, C, OH, OW, 1, 1, stride, 1, 0, N * OH * OW), bn_mean, bn_invstd, bn_gamma,
                           bn_beta, bn_relu),
                   w_kc, K, C, bias, y, stream);
+}
+
+DK_API int dk_pwconv_fwd_stats_rows(int N, int OH, int OW, int K, int C) { return stats_rows(N * OH * OW, K, C); }
+
+DK_API int dk_pwconv_fwd_ex_f32(const float* x, int N, int H, int W, int C, const float* w_kc, int K, int stride,
+                                const float* bias, float* y, int OH, int OW, const float* bn_mean,
+                                const float* bn_invstd, const float* bn_gamma, const float* bn_beta, int bn_relu,
+                                double* stats, void* stream) {
+  if (C % 4 || !aligned16(x) || !aligned16(w_kc) || !fits((size_t)N * H * W * C * 4)) return DK_ERR_ARGS;
+  return conv_fwd_ex(img(x, N, H, W, C, OH, OW, 1, 1, stride, 1, 0, N * OH * OW), w_kc, K, C, bias, y, bn_mean,
+                     bn_invstd, bn_gamma, bn_beta, bn_relu, stats, stream);
 }
 
 // Pointwise dgrad (pointwise_convolution.py:65-72): dx_rows = dy_rows . W; for stride > 1 the

@@ -46,30 +46,65 @@ def plan_group(layers, i, fuse, out_accepts=False, keep=()):
         consumer_ok = accepts_bn_input(layers[j]) if j < len(layers) else out_accepts
         if consumer_ok and not any(l.layer_name in keep for l in group):
             return group, "defer"
-        if relu is not None:
+        if relu is not None and layer.layer_name not in keep:
             return group, "pair"
     return (layer,), "single"
 
 
-def run_group(group, mode, X, test_mode=False):
+class StatsRequest:
+    """Asks a producer layer (``produces_bn_stats``) to emit, with its forward output, the
+    BatchNorm partial statistics of that output (the *_fwd_ex_f32 entry points); the
+    BatchNormLayer that follows then skips its own statistics pass."""
+    __slots__ = ("part", "rows")
+
+    def __init__(self):
+        self.part = None   # fp64 device tensor [rows, 2, C], set by the producer
+        self.rows = 0
+
+
+def run_group(group, mode, X, test_mode=False, stats_req=None, bn_stats=None):
+    from .batch_norm import BatchNormLayer
     if mode == "defer":
-        return group[0].forward_deferred(X, group[1] if len(group) == 2 else None, test_mode=test_mode)
+        return group[0].forward_deferred(X, group[1] if len(group) == 2 else None, test_mode=test_mode,
+                                         stats=bn_stats)
     if mode == "pair":
-        return group[0].forward_bn_relu(X, group[1], test_mode=test_mode)
+        return group[0].forward_bn_relu(X, group[1], test_mode=test_mode, stats=bn_stats)
+    if bn_stats is not None and type(group[0]) is BatchNormLayer:
+        return group[0].forward(X, test_mode=test_mode, stats=bn_stats)
+    if stats_req is not None:
+        return group[0].forward(X, test_mode=test_mode, bn_stats=stats_req)
     return group[0].forward(X, test_mode=test_mode)
+
+
+def execute(layers, X, test_mode=False, out_accepts=False, keep=(), visit=None):
+    """Run `layers` in order with the fusions above; also lets a producer hand the next
+    BatchNormLayer its output statistics.  `visit(group, X)` is called after each group and
+    may return True to stop early.  Returns (X, steps, stopped)."""
+    from .batch_norm import BatchNormLayer
+    steps = []
+    fuse = fusion_enabled()
+    pending = None
+    i = 0
+    while i < len(layers):
+        group, mode = plan_group(layers, i, fuse, out_accepts, keep)
+        nxt = i + len(group)
+        req = None
+        if (fuse and not test_mode and mode == "single" and getattr(group[0], "produces_bn_stats", False)
+                and nxt < len(layers) and type(layers[nxt]) is BatchNormLayer):
+            req = StatsRequest()
+        X = run_group(group, mode, X, test_mode, stats_req=req, bn_stats=pending)
+        pending = req if req is not None and req.part is not None else None
+        steps.append(group)
+        i = nxt
+        if visit is not None and visit(group, X):
+            return X, steps, True
+    return X, steps, False
 
 
 def chain_forward(layers, X, test_mode=False, out_accepts=False):
     """Run `layers` in order; returns (output, steps).  The output is a BNOut when the list
     ends in a BatchNormLayer [+ ReLu] and `out_accepts`."""
-    steps = []
-    fuse = fusion_enabled()
-    i = 0
-    while i < len(layers):
-        group, mode = plan_group(layers, i, fuse, out_accepts)
-        X = run_group(group, mode, X, test_mode)
-        steps.append(group)
-        i += len(group)
+    X, steps, _ = execute(layers, X, test_mode, out_accepts)
     return X, steps
 
 

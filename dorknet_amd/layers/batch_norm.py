@@ -85,7 +85,7 @@ class BatchNormLayer(Layer):
         import torch.distributed as dist
         return dist.get_world_size(self.sync_group)
 
-    def _stats(self, x, P, C, st):
+    def _stats(self, x, P, C, st, partials=None):
         dev = x.device
         mean = torch.empty(C, dtype=torch.float32, device=dev)
         std = torch.empty(C, dtype=torch.float32, device=dev)
@@ -97,17 +97,33 @@ class BatchNormLayer(Layer):
             nlp["running_std"] = torch.empty(self._param_shape(C), dtype=torch.float32, device=dev)
         rm, rs = as_device(nlp["running_mean"]), as_device(nlp["running_std"])
         nlp["running_mean"], nlp["running_std"] = rm, rs
-        nb = lib.dk_bn_workspace_bytes(P, C)
-        ws = workspace.get(nb)
+        if partials is not None and partials.part.shape[-1] != C:
+            partials = None
+        if partials is not None:
+            nb = lib.dk_bn_partials_workspace_bytes(partials.rows, C)
+            ws = workspace.get(nb)
+        else:
+            nb = lib.dk_bn_workspace_bytes(P, C)
+            ws = workspace.get(nb)
         if self.sync_group is None:
-            lib.dk_bn_stats_f32(x.data_ptr(), P, C, float(self.eps), float(self.run_momentum), int(first),
-                                mean.data_ptr(), std.data_ptr(), invstd.data_ptr(), rm.data_ptr(), rs.data_ptr(),
-                                ws, nb, st)
+            if partials is not None:
+                lib.dk_bn_stats_from_partials_f32(partials.part.data_ptr(), partials.rows, C, float(P),
+                                                  float(self.eps), float(self.run_momentum), int(first),
+                                                  mean.data_ptr(), std.data_ptr(), invstd.data_ptr(), rm.data_ptr(),
+                                                  rs.data_ptr(), ws, nb, st)
+            else:
+                lib.dk_bn_stats_f32(x.data_ptr(), P, C, float(self.eps), float(self.run_momentum), int(first),
+                                    mean.data_ptr(), std.data_ptr(), invstd.data_ptr(), rm.data_ptr(),
+                                    rs.data_ptr(), ws, nb, st)
         else:
             import torch.distributed as dist
-            lib.dk_bn_stats_partial_f64(x.data_ptr(), P, C, ws, nb, st)
             sums = torch.empty(2 * C, dtype=torch.float64, device=dev)
-            lib.dk_bn_collapse_f64(ws, lib.dk_bn_partial_blocks(P, C), C, sums.data_ptr(), st)
+            if partials is not None:
+                lib.dk_bn_reduce_partials_f64(partials.part.data_ptr(), partials.rows, C, sums.data_ptr(), ws, nb,
+                                              st)
+            else:
+                lib.dk_bn_stats_partial_f64(x.data_ptr(), P, C, ws, nb, st)
+                lib.dk_bn_collapse_f64(ws, lib.dk_bn_partial_blocks(P, C), C, sums.data_ptr(), st)
             dist.all_reduce(sums, group=self.sync_group)
             count = float(P) * self._world()
             lib.dk_bn_stats_finalize_f32(sums.data_ptr(), 1, C, count, float(self.eps), float(self.run_momentum),
@@ -117,15 +133,16 @@ class BatchNormLayer(Layer):
 
     # -- forward -------------------------------------------------------------------------
 
-    def _normalisation(self, X, test_mode):
+    def _normalisation(self, X, test_mode, stats=None):
         """(x, mean, invstd): batch statistics in training mode (kept for backward), the
-        running statistics in test mode (batch_norm.py:76-115)."""
+        running statistics in test mode (batch_norm.py:76-115).  `stats`: partial sums of X
+        already computed by the layer that produced it (layers/_chain.StatsRequest)."""
         self._require_on_gpu()
         st = stream_handle()
         x, P, C = self._prep_input(as_device(X))
         self.input_shape = tuple(x.shape)
         if not test_mode:
-            mean, std, invstd = self._stats(x, P, C, st)
+            mean, std, invstd = self._stats(x, P, C, st, stats)
             self.X = x
             self._mean, self._invstd = mean, invstd
             self.std = std.view(self._param_shape(C))
@@ -137,32 +154,32 @@ class BatchNormLayer(Layer):
             lib.dk_bn_infer_params_f32(rs.data_ptr(), C, invstd.data_ptr(), st)
         return x, mean, invstd
 
-    def _forward(self, X, test_mode, relu):
-        x, mean, invstd = self._normalisation(X, test_mode)
+    def _forward(self, X, test_mode, relu, stats=None):
+        x, mean, invstd = self._normalisation(X, test_mode, stats)
         gamma, beta = self.learned_params["gamma"], self.learned_params["beta"]
         y = self._out_like(x)
         lib.dk_bn_apply_f32(x.data_ptr(), x.numel(), x.shape[1], mean.data_ptr(), invstd.data_ptr(),
                             gamma.data_ptr(), beta.data_ptr(), int(relu), y.data_ptr(), 0, stream_handle())
         return y
 
-    def forward_deferred(self, X, relu_layer=None, test_mode=False):
+    def forward_deferred(self, X, relu_layer=None, test_mode=False, stats=None):
         """Statistics only; the normalisation (and the following ReLu, if given) is applied
         by the consumer as it loads its input (layers/_bn_input.py)."""
         from ._bn_input import BNOut
-        x, mean, invstd = self._normalisation(X, test_mode)
+        x, mean, invstd = self._normalisation(X, test_mode, stats)
         out = BNOut(x, mean, invstd, self.learned_params["gamma"], self.learned_params["beta"],
                     relu_layer is not None)
         if relu_layer is not None:
             relu_layer._attach_fused(out, test_mode)
         return out
 
-    def forward(self, X, test_mode=False, use_express=False):
+    def forward(self, X, test_mode=False, use_express=False, stats=None):
         """X.shape = (batch_size, channel, height, width) or (batch_size, features)."""
-        return self._forward(X, test_mode, relu=False)
+        return self._forward(X, test_mode, relu=False, stats=stats)
 
-    def forward_bn_relu(self, X, relu_layer, test_mode=False):
+    def forward_bn_relu(self, X, relu_layer, test_mode=False, stats=None):
         """BN followed by ReLU in one pass (activations.py:37-42 fused into the apply)."""
-        y = self._forward(X, test_mode, relu=True)
+        y = self._forward(X, test_mode, relu=True, stats=stats)
         relu_layer._attach_fused(y, test_mode)
         return y
 

@@ -68,9 +68,10 @@ class ConvLayer(Layer):
 
     # -- forward / backward --------------------------------------------------------------
 
-    accepts_bn_input = True  # forward(BNOut): the preceding BatchNorm is applied on load
+    accepts_bn_input = True   # forward(BNOut): the preceding BatchNorm is applied on load
+    produces_bn_stats = True  # forward(..., bn_stats=StatsRequest): emits the next BN's statistics
 
-    def forward(self, X, test_mode=False):
+    def forward(self, X, test_mode=False, bn_stats=None):
         self._require_on_gpu()
         st = stream_handle()
         self.input_shape = tuple(X.shape)
@@ -84,9 +85,16 @@ class ConvLayer(Layer):
         lib.dk_conv_weight_krsc_f32(w.data_ptr(), K, C, R, S, Cp, w_krsc.data_ptr(), st)
         y = empty_nhwc(N, K, OH, OW)
         bias = self.learned_params["bias"] if self.with_bias else None
-        if bn is not None:
-            lib.dk_conv2d_fwd_bnx_f32(x.data_ptr(), N, H, W, Cp, w_krsc.data_ptr(), K, R, S, self.stride,
-                                      self.padding, ptr(bias), y.data_ptr(), OH, OW, *bn.bn_args(), st)
+        stats = None
+        if bn_stats is not None and not test_mode:
+            rows = lib.dk_conv2d_fwd_stats_rows(N, OH, OW, K, Cp, R, S)
+            stats = torch.empty((rows, 2, K), dtype=torch.float64, device=x.device)
+        if bn is not None or stats is not None:
+            lib.dk_conv2d_fwd_ex_f32(x.data_ptr(), N, H, W, Cp, w_krsc.data_ptr(), K, R, S, self.stride,
+                                     self.padding, ptr(bias), y.data_ptr(), OH, OW,
+                                     *(bn.bn_args() if bn is not None else (0, 0, 0, 0, 0)), ptr(stats), st)
+            if stats is not None:
+                bn_stats.part, bn_stats.rows = stats, stats.shape[0]
         else:
             lib.dk_conv2d_fwd_f32(x.data_ptr(), N, H, W, Cp, w_krsc.data_ptr(), K, R, S, self.stride, self.padding,
                                   ptr(bias), y.data_ptr(), OH, OW, st)

@@ -62,9 +62,10 @@ class DepthwiseConvLayer(Layer):
         lib.dk_dw_weight_rsc_f32(w.data_ptr(), C, R, S, w_rsc.data_ptr(), st)
         return w_rsc
 
-    accepts_bn_input = True  # forward(BNOut): the preceding BatchNorm is applied on load
+    accepts_bn_input = True   # forward(BNOut): the preceding BatchNorm is applied on load
+    produces_bn_stats = True  # forward(..., bn_stats=StatsRequest): emits the next BN's statistics
 
-    def forward(self, X, test_mode=False):
+    def forward(self, X, test_mode=False, bn_stats=None):
         self._require_on_gpu()
         st = stream_handle()
         bn = X if isinstance(X, BNOut) and X.dim() == 4 and X.shape[1] % 4 == 0 else None
@@ -77,9 +78,17 @@ class DepthwiseConvLayer(Layer):
         OH, OW = int(self.num_row_patches), int(self.num_col_patches)
         y = empty_nhwc(N, C, OH, OW)
         bias = self.learned_params["bias"] if self.with_bias else None
-        if bn is not None:
-            lib.dk_dwconv_fwd_bnx_f32(x.data_ptr(), N, H, W, C, self._w_rsc(st).data_ptr(), R, S, self.stride,
-                                      self.padding, ptr(bias), y.data_ptr(), OH, OW, *bn.bn_args(), st)
+        stats = None
+        if bn_stats is not None and not test_mode and self.stride in (1, 2):
+            rows = lib.dk_dwconv_fwd_stats_rows(N, OH, OW, C, self.stride)
+            if rows:
+                stats = torch.empty((rows, 2, C), dtype=torch.float64, device=x.device)
+        if bn is not None or stats is not None:
+            lib.dk_dwconv_fwd_ex_f32(x.data_ptr(), N, H, W, C, self._w_rsc(st).data_ptr(), R, S, self.stride,
+                                     self.padding, ptr(bias), y.data_ptr(), OH, OW,
+                                     *(bn.bn_args() if bn is not None else (0, 0, 0, 0, 0)), ptr(stats), st)
+            if stats is not None:
+                bn_stats.part, bn_stats.rows = stats, stats.shape[0]
         else:
             lib.dk_dwconv_fwd_f32(x.data_ptr(), N, H, W, C, self._w_rsc(st).data_ptr(), R, S, self.stride,
                                   self.padding, ptr(bias), y.data_ptr(), OH, OW, st)

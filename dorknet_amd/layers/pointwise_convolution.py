@@ -12,6 +12,8 @@ output spatial size ceil(H/s), and the backward output size (s*OH, s*OW).
 """
 from __future__ import annotations
 
+import torch
+
 from .._hip import lib, stream_handle, workspace
 from .._tensor import empty_nhwc, ptr, to_nhwc
 from ._bn_input import BNOut
@@ -53,9 +55,10 @@ class PointwiseConvLayer(Layer):
             self.stride, self.with_bias, repr(self.weight_regulariser), self.is_on_gpu)
         return out
 
-    accepts_bn_input = True  # forward(BNOut): the preceding BatchNorm is applied on load
+    accepts_bn_input = True   # forward(BNOut): the preceding BatchNorm is applied on load
+    produces_bn_stats = True  # forward(..., bn_stats=StatsRequest): emits the next BN's statistics
 
-    def forward(self, X, test_mode=False):
+    def forward(self, X, test_mode=False, bn_stats=None):
         self._require_on_gpu()
         st = stream_handle()
         bn = X if isinstance(X, BNOut) and X.dim() == 4 and X.shape[1] % 4 == 0 else None
@@ -70,9 +73,15 @@ class PointwiseConvLayer(Layer):
             raise ValueError("PointwiseConvLayer {}: input has {} channels, weights expect {} (a multiple of 4 "
                              "is required)".format(self.layer_name, X.shape[1], self.num_channels))
         bias = self.learned_params["bias"] if self.with_bias else None
-        if bn is not None:
-            lib.dk_pwconv_fwd_bnx_f32(x.data_ptr(), N, H, W, Cp, w.data_ptr(), K, s, ptr(bias), y.data_ptr(), OH, OW,
-                                      *bn.bn_args(), st)
+        stats = None
+        if bn_stats is not None and not test_mode:
+            rows = lib.dk_pwconv_fwd_stats_rows(N, OH, OW, K, Cp)
+            stats = torch.empty((rows, 2, K), dtype=torch.float64, device=x.device)
+        if bn is not None or stats is not None:
+            lib.dk_pwconv_fwd_ex_f32(x.data_ptr(), N, H, W, Cp, w.data_ptr(), K, s, ptr(bias), y.data_ptr(), OH, OW,
+                                     *(bn.bn_args() if bn is not None else (0, 0, 0, 0, 0)), ptr(stats), st)
+            if stats is not None:
+                bn_stats.part, bn_stats.rows = stats, stats.shape[0]
         else:
             lib.dk_pwconv_fwd_f32(x.data_ptr(), N, H, W, Cp, w.data_ptr(), K, s, ptr(bias), y.data_ptr(), OH, OW, st)
         # the reference keeps the NHWC row copy as self.patches (:50); here the input itself

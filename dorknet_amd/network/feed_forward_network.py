@@ -13,7 +13,7 @@ import json
 import numpy as np
 
 from ..layers._bn_input import materialize
-from ..layers._chain import chain_backward, fusion_enabled, plan_group, run_group
+from ..layers._chain import chain_backward, execute
 from ..layers.activations import ReLu  # noqa: F401  (re-exported names used by loaders)
 from ..layers.batch_norm import BatchNormLayer  # noqa: F401
 from ..layers.convolution import ConvLayer  # noqa: F401
@@ -120,27 +120,25 @@ class FeedForwardNetwork:
         regularisation_terms = []
         steps = []
         self._steps = steps
-        fuse = fusion_enabled()
         plan = None
         if not test_mode and self.loss_layer is not None and terminal_layer_name is None:
             plan = self._l2_plan()
             if plan is not None and not plan:
                 plan = None
-        layers = self.layers
         keep = () if terminal_layer_name is None else (terminal_layer_name,)
-        i = 0
-        while i < len(layers):
-            group, mode = plan_group(layers, i, fuse, keep=keep)
-            if mode == "pair" and group[0].layer_name in keep:
-                group, mode = group[:1], "single"  # the terminal BN's own output is requested
-            X = run_group(group, mode, X, test_mode)
-            i += len(group)
-            steps.append(group)
+
+        def visit(group, X):
             for l in group:
                 if l.layer_name == terminal_layer_name:
-                    return loss, materialize(X)
+                    return True
                 if not test_mode and plan is None and hasattr(l, "regulariser_forward"):
                     regularisation_terms.append(l.regulariser_forward())
+            return False
+
+        X, steps, stopped = execute(self.layers, X, test_mode, keep=keep, visit=visit)
+        self._steps = steps
+        if stopped:
+            return loss, materialize(X)
         if self.loss_layer is not None:
             this_loss, X = self.loss_layer.forward(X, y_one_hot, test_mode=test_mode)
             if plan is not None:

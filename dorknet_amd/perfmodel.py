@@ -125,6 +125,13 @@ def _bnx(f):
     return lambda *a: f(*(a[:-6] + a[-1:]))
 
 
+def _ex(f):
+    """A *_fwd_ex_f32 entry: the plain arguments, 5 BatchNorm arguments, the statistics
+    pointer, the stream.  The statistics are computed in the epilogue (no extra traffic
+    beyond the partial sums, ignored here)."""
+    return lambda *a: f(*(a[:-7] + a[-1:]))
+
+
 def _bn_add(a, am, ai, ag, ab, ar, b, bm, bi, bg, bb, br, n, C, relu, y, mask, st):
     return n * (1 + 4 * (bool(am) + bool(bm))), E * 3 * n + (n if mask else 0)
 
@@ -163,6 +170,9 @@ MODEL = {
     "dk_dwconv_fwd_bnx_f32": _bnx(_dw_fwd),
     "dk_dwconv_wgrad_bnx_f32": _bnx(_dw_wgrad),
     "dk_bn_add_f32": _bn_add,
+    "dk_conv2d_fwd_ex_f32": _ex(_conv_fwd),
+    "dk_pwconv_fwd_ex_f32": _ex(_pw_fwd),
+    "dk_dwconv_fwd_ex_f32": _ex(_dw_fwd),
 }
 
 

@@ -9,8 +9,9 @@
  *     one has a matching *_workspace_bytes() query with the same shape arguments;
  *   - `stream` is a hipStream_t passed as void*; all work is stream-ordered on it;
  *   - the int return value is a hipError_t (0 = success); 10001 = bad arguments,
- *     10002 = workspace too small.  Nothing is checked on the device.
- *   - reentrant: no global mutable state.
+ *     10002 = workspace too small.  Nothing is checked on the device.  Exceptions: the
+ *     count queries (*_blocks, *_rows, dk_abi_version, dk_debug_*) return a count;
+ *   - reentrant: no global mutable state (except the dk_debug_* tuning knob).
  *
  * Each block cites the reference interface it replaces (file:line under the reference
  * repository).  In the reference these are CuPy RawKernel launches (NVRTC CUDA strings),
@@ -87,6 +88,18 @@ int dk_conv2d_fwd_bnx_f32(const float* x, int N, int H, int W, int C, const floa
 int dk_conv2d_wgrad_bnx_f32(const float* dy, const float* x, int N, int H, int W, int Cp, int C, int K, int R, int S, int stride, int pad, int OH, int OW, const float* w_kcrs, float l2, float* dw_kcrs, void* ws, size_t ws_bytes, const float* bn_mean, const float* bn_invstd, const float* bn_gamma, const float* bn_beta, int bn_relu, void* stream);
 int dk_pwconv_fwd_bnx_f32(const float* x, int N, int H, int W, int C, const float* w_kc, int K, int stride, const float* bias, float* y, int OH, int OW, const float* bn_mean, const float* bn_invstd, const float* bn_gamma, const float* bn_beta, int bn_relu, void* stream);
 int dk_pwconv_wgrad_bnx_f32(const float* dy, const float* x, int N, int H, int W, int C, int K, int stride, int OH, int OW, const float* w_kc, float l2, float* dw_kc, void* ws, size_t ws_bytes, const float* bn_mean, const float* bn_invstd, const float* bn_gamma, const float* bn_beta, int bn_relu, void* stream);
+/* Producer side of the same fusion: *_fwd_ex_f32 = forward with an optional input BN
+ * (bn_mean == NULL: raw input) and, when stats != NULL, the BatchNorm statistics of the
+ * output y (fp64 sum and sum of squares per output channel, per tile: stats[rows][2][K],
+ * rows = the matching *_fwd_stats_rows()).  dk_bn_stats_from_partials_f32 turns them into
+ * mean/std -- the separate statistics pass over y (batch_norm.py:76-80) disappears.
+ * dk_dwconv_fwd_stats_rows returns 0 when C/4 does not divide 256 (no statistics variant). */
+int dk_conv2d_fwd_stats_rows(int N, int OH, int OW, int K, int C, int R, int S);
+int dk_conv2d_fwd_ex_f32(const float* x, int N, int H, int W, int C, const float* w_krsc, int K, int R, int S, int stride, int pad, const float* bias, float* y, int OH, int OW, const float* bn_mean, const float* bn_invstd, const float* bn_gamma, const float* bn_beta, int bn_relu, double* stats, void* stream);
+int dk_pwconv_fwd_stats_rows(int N, int OH, int OW, int K, int C);
+int dk_pwconv_fwd_ex_f32(const float* x, int N, int H, int W, int C, const float* w_kc, int K, int stride, const float* bias, float* y, int OH, int OW, const float* bn_mean, const float* bn_invstd, const float* bn_gamma, const float* bn_beta, int bn_relu, double* stats, void* stream);
+int dk_dwconv_fwd_stats_rows(int N, int OH, int OW, int C, int stride);
+int dk_dwconv_fwd_ex_f32(const float* x, int N, int H, int W, int C, const float* w_rsc, int R, int S, int stride, int pad, const float* bias, float* y, int OH, int OW, const float* bn_mean, const float* bn_invstd, const float* bn_gamma, const float* bn_beta, int bn_relu, double* stats, void* stream);
 
 /* ---------------------------------------------------------------------------------------
  * Depthwise convolution, direct (no MFMA).
@@ -130,6 +143,12 @@ int dk_bn_stats_partial_f64(const float* x, int P, int C, void* ws, size_t ws_by
 int dk_bn_collapse_f64(const void* part, int nblk, int C, void* out, void* stream);
 int dk_bn_stats_finalize_f32(const void* part, int nblk, int C, double count, float eps, float momentum, int first, float* mean, float* std_, float* invstd, float* run_mean, float* run_std, void* stream);
 int dk_bn_stats_f32(const float* x, int P, int C, float eps, float momentum, int first, float* mean, float* std_, float* invstd, float* run_mean, float* run_std, void* ws, size_t ws_bytes, void* stream);
+/* Statistics from a producer's partial sums (stats of *_fwd_ex_f32): fixed-order fold of
+ * part[nblk][2][C] (workspace: dk_bn_partials_workspace_bytes) then the finalize above;
+ * dk_bn_reduce_partials_f64 gives the [2][C] sums a SyncBN rank all-reduces. */
+size_t dk_bn_partials_workspace_bytes(int nblk, int C);
+int dk_bn_stats_from_partials_f32(const void* part, int nblk, int C, double count, float eps, float momentum, int first, float* mean, float* std_, float* invstd, float* run_mean, float* run_std, void* ws, size_t ws_bytes, void* stream);
+int dk_bn_reduce_partials_f64(const void* part, int nblk, int C, void* out, void* ws, size_t ws_bytes, void* stream);
 int dk_bn_infer_params_f32(const float* run_std, int C, float* invstd, void* stream);
 int dk_bn_apply_f32(const float* x, long long numel, int C, const float* mean, const float* invstd, const float* gamma, const float* beta, int relu, float* y, uint8_t* mask, void* stream);
 int dk_bn_bwd_partial_f64(const float* x, const float* dy, int P, int C, const float* mean, const float* invstd, const float* gamma, const float* beta, int relu, void* ws, size_t ws_bytes, void* stream);

@@ -148,3 +148,71 @@ def test_bn_add_bitwise(bn_a, bn_b):
                       n, C, 1, y1.data_ptr(), m1.data_ptr(), st)
     same(y0, y1)
     same(m0, m1)
+
+
+def _stats_pair(y, part, rows, C):
+    """(mean, std) from the producer's partials and from a separate pass over y."""
+    st = stream_handle()
+    P = y.numel() // C
+    out = []
+    for use_part in (True, False):
+        mean, std, invstd, rm, rs = [torch.empty(C, device="cuda") for _ in range(5)]
+        if use_part:
+            nb = lib.dk_bn_partials_workspace_bytes(rows, C)
+            lib.dk_bn_stats_from_partials_f32(part.data_ptr(), rows, C, float(P), 1e-5, 0.95, 1, mean.data_ptr(),
+                                              std.data_ptr(), invstd.data_ptr(), rm.data_ptr(), rs.data_ptr(),
+                                              workspace.get(nb), nb, st)
+        else:
+            nb = lib.dk_bn_workspace_bytes(P, C)
+            lib.dk_bn_stats_f32(y.data_ptr(), P, C, 1e-5, 0.95, 1, mean.data_ptr(), std.data_ptr(),
+                                invstd.data_ptr(), rm.data_ptr(), rs.data_ptr(), workspace.get(nb), nb, st)
+        out.append((mean, std))
+    torch.cuda.synchronize()
+    return out
+
+
+@pytest.mark.parametrize("kind,bn_in", [("pw", False), ("pw", True), ("conv", True), ("dw", False), ("dw", True)])
+def test_producer_statistics(kind, bn_in):
+    """*_fwd_ex_f32 with stats: y bit-identical to the plain forward, and mean/std from the
+    epilogue partial sums equal to a separate statistics pass over y (to fp32 rounding)."""
+    rng = np.random.RandomState(11)
+    N, C, H, W = 3, 16, 37, 29   # ragged tiles: M = 3*37*29 is not a multiple of any tile
+    K = 48
+    x = nhwc(rng.randn(N, C, H, W) + 0.5)
+    p = bn_params(C, rng)
+    bargs = args(p, 1) if bn_in else (0, 0, 0, 0, 0)
+    st = stream_handle()
+    if kind == "pw":
+        w = torch.as_tensor(rng.randn(K, C).astype(np.float32), device="cuda")
+        OH, OW = H, W
+        rows = lib.dk_pwconv_fwd_stats_rows(N, OH, OW, K, C)
+        Cout = K
+        run = lambda yy, part: lib.dk_pwconv_fwd_ex_f32(x.data_ptr(), N, H, W, C, w.data_ptr(), K, 1, 0,  # noqa
+                                                        yy.data_ptr(), OH, OW, *bargs, part, st)
+    elif kind == "conv":
+        w = torch.as_tensor(rng.randn(K, C, 3, 3).astype(np.float32), device="cuda")
+        wk = torch.empty((K, 3, 3, C), device="cuda")
+        lib.dk_conv_weight_krsc_f32(w.data_ptr(), K, C, 3, 3, C, wk.data_ptr(), st)
+        OH, OW = H, W
+        rows = lib.dk_conv2d_fwd_stats_rows(N, OH, OW, K, C, 3, 3)
+        Cout = K
+        run = lambda yy, part: lib.dk_conv2d_fwd_ex_f32(x.data_ptr(), N, H, W, C, wk.data_ptr(), K, 3, 3, 1, 1,  # noqa
+                                                        0, yy.data_ptr(), OH, OW, *bargs, part, st)
+    else:
+        w = torch.as_tensor(rng.randn(C, 3, 3).astype(np.float32), device="cuda")
+        wr = torch.empty((3, 3, C), device="cuda")
+        lib.dk_dw_weight_rsc_f32(w.data_ptr(), C, 3, 3, wr.data_ptr(), st)
+        OH, OW = H, W
+        rows = lib.dk_dwconv_fwd_stats_rows(N, OH, OW, C, 1)
+        Cout = C
+        run = lambda yy, part: lib.dk_dwconv_fwd_ex_f32(x.data_ptr(), N, H, W, C, wr.data_ptr(), 3, 3, 1, 1, 0,  # noqa
+                                                        yy.data_ptr(), OH, OW, *bargs, part, st)
+    assert rows > 0
+    y0 = torch.empty((N, Cout, OH, OW), device="cuda").contiguous(memory_format=torch.channels_last)
+    y1 = torch.empty_like(y0)
+    part = torch.empty((rows, 2, Cout), dtype=torch.float64, device="cuda")
+    run(y0, 0)
+    run(y1, part.data_ptr())
+    same(y0, y1)
+    (m1, s1), (m0, s0) = _stats_pair(y1, part, rows, Cout)
+    assert torch.allclose(m1, m0, rtol=1e-6, atol=1e-6) and torch.allclose(s1, s0, rtol=1e-6, atol=0)

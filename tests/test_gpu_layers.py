@@ -98,6 +98,9 @@ DW_CASES = [
     (64, 3, 3, 1, 1, 3, 8, 8, False),
     (12, 5, 5, 1, 2, 2, 11, 11, True),
     (512, 3, 3, 1, 1, 2, 7, 7, False),    # res8 shape
+    (8, 5, 5, 2, 2, 2, 13, 12, False),    # 5x5 stride-2 sub-pixel dgrad
+    (4, 1, 1, 2, 0, 2, 9, 8, True),       # 1x1 stride-2
+    (24, 3, 3, 2, 0, 1, 10, 11, False),   # stride 2 without a sub-pixel kernel (gather path)
 ]
 
 

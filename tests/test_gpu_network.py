@@ -91,7 +91,11 @@ def test_mnist_training_steps():
     _compare_step(net, onet, o32, X, onehot, lr=0.01)
 
 
-def test_fused_and_unfused_paths_are_bitwise_equal(monkeypatch):
+def test_fused_and_unfused_paths_agree(monkeypatch):
+    """DORKNET_FUSE=1 (BN on load, producer-side BN statistics, fused joins) vs every layer
+    on its own.  The values a consumer sees are bit-identical (test_gpu_bn_on_load.py); the
+    statistics are fp64 sums taken in a different order, so the two runs agree to fp32
+    rounding rather than bitwise."""
     from examples.resnet18_depsep import ResNet18, synthetic_batch
     X, _, onehot = synthetic_batch(2, seed=3)
     outs = []
@@ -103,9 +107,9 @@ def test_fused_and_unfused_paths_are_bitwise_equal(monkeypatch):
         loss, P = net.forward(dev(X), dev(onehot))
         net.backward()
         outs.append((host(P), [host(l.grads[k]) for l in all_layers(net.layers) for k in (l.grads or {})]))
-    assert np.array_equal(outs[0][0], outs[1][0])
+    assert rel_err(outs[0][0], outs[1][0]) <= 1e-5
     for a, b in zip(outs[0][1], outs[1][1]):
-        assert np.array_equal(a, b)
+        assert np.linalg.norm(a - b) <= 1e-4 * np.linalg.norm(b) + 1e-6
 
 
 def test_inference_and_terminal_layer():
