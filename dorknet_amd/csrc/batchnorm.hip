@@ -274,14 +274,19 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const float* __restrict__
 // backward reduce: sum dy_e and sum dy_e * x_hat, where dy_e = dy, or with relu:
 // dy * (bn_out(x) > 0) -- the fused ReLU backward (activations.py:44-47).
 // ---------------------------------------------------------------------------------------
-template <int V>
+// MASKED: dy is the upstream gradient of a ReLU that follows (the post-residual join's,
+// residual_block.py:86): g = mask ? dy : 0 is written to gout and reduced -- the ReLU
+// backward and this BN's backward reduction in one pass.
+template <int V, bool MASKED = false>
 __global__ __launch_bounds__(256) void bn_bwd_partial_kernel(const float* __restrict__ x,
                                                              const float* __restrict__ dy, int P, int C, int ppb,
                                                              const float* __restrict__ mean,
                                                              const float* __restrict__ invstd,
                                                              const float* __restrict__ gamma,
                                                              const float* __restrict__ beta, int relu,
-                                                             double* __restrict__ part) {
+                                                             double* __restrict__ part,
+                                                             const uint8_t* __restrict__ mask = nullptr,
+                                                             float* __restrict__ gout = nullptr) {
   using VT = VecT<V>;
   __shared__ double red[2][256][V];
   const RowGeom g = row_geom(C, V);
@@ -314,6 +319,16 @@ __global__ __launch_bounds__(256) void bn_bwd_partial_kernel(const float* __rest
   };
   if (active) {
     const int PL = g.PL;
+    auto grad = [&](size_t off) -> typename VT::T {
+      typename VT::T gv = VT::load(dy + off);
+      if constexpr (MASKED) {
+#pragma unroll
+        for (int e = 0; e < V; ++e)
+          if (!mask[off + e]) set_el(gv, e, 0.f);
+        VT::store(gout + off, gv);
+      }
+      return gv;
+    };
     int p = p0 + pl;
     for (; p + 3 * PL < p1; p += 4 * PL) {
       typename VT::T xv[4], gv[4];
@@ -321,14 +336,14 @@ __global__ __launch_bounds__(256) void bn_bwd_partial_kernel(const float* __rest
       for (int u = 0; u < 4; ++u) {
         const size_t off = (size_t)(p + u * PL) * C + c0;
         xv[u] = VT::load(x + off);
-        gv[u] = VT::load(dy + off);
+        gv[u] = grad(off);
       }
 #pragma unroll
       for (int u = 0; u < 4; ++u) acc(xv[u], gv[u]);
     }
     for (; p < p1; p += PL) {
       const size_t off = (size_t)p * C + c0;
-      acc(VT::load(x + off), VT::load(dy + off));
+      acc(VT::load(x + off), grad(off));
     }
   }
 #pragma unroll
@@ -591,6 +606,37 @@ DK_API int dk_bn_bwd_partial_f64(const float* x, const float* dy, int P, int C, 
     hipLaunchKernelGGL(bn_bwd_partial_kernel<1>, grid, dim3(256), 0, as_stream(stream), x, dy, P, C, ppb, mean,
                        invstd, gamma, beta, relu, static_cast<double*>(ws));
   return launch_status();
+}
+
+// ReLU backward (mask from the forward join) fused with stage 1 of the backward of the BN
+// that produced the join's input: dx = mask ? dy : 0 and part[nblk][2][C] over dx.
+DK_API int dk_relu_bwd_bn_partial_f64(const float* dy, const uint8_t* mask, const float* x, int P, int C,
+                                      const float* mean, const float* invstd, const float* gamma, const float* beta,
+                                      int relu, float* dx, void* part, size_t part_bytes, void* stream) {
+  if (part_bytes < dk_bn_workspace_bytes(P, C)) return DK_ERR_WORKSPACE;
+  const int nblk = bn_blocks(P, C);
+  const int ppb = cdiv(P, nblk);
+  const bool vec = vec_ok(x, C) && vec_ok(dy, C) && vec_ok(dx, C);
+  const RowGeom g = row_geom(C, vec ? 4 : 1);
+  const dim3 grid(nblk, cdiv(g.CG, g.cgt));
+  if (vec)
+    hipLaunchKernelGGL((bn_bwd_partial_kernel<4, true>), grid, dim3(256), 0, as_stream(stream), x, dy, P, C, ppb,
+                       mean, invstd, gamma, beta, relu, static_cast<double*>(part), mask, dx);
+  else
+    hipLaunchKernelGGL((bn_bwd_partial_kernel<1, true>), grid, dim3(256), 0, as_stream(stream), x, dy, P, C, ppb,
+                       mean, invstd, gamma, beta, relu, static_cast<double*>(part), mask, dx);
+  return launch_status();
+}
+
+// Backward stage 2 from partials of any origin (dk_bn_bwd_partial_f64, a consumer's
+// dgrad_ex epilogue, dk_relu_bwd_bn_partial_f64): fixed-order fold, then the finalize.
+DK_API int dk_bn_bwd_from_partials_f32(const void* part, int nblk, int C, double count, float* dgamma, float* dbeta,
+                                       float* k12, void* ws, size_t ws_bytes, void* stream) {
+  if (ws_bytes < dk_bn_partials_workspace_bytes(nblk, C)) return DK_ERR_WORKSPACE;
+  const double* p;
+  const int n = fold_partials(static_cast<const double*>(part), nblk, C, static_cast<double*>(ws),
+                              as_stream(stream), &p);
+  return dk_bn_bwd_finalize_f32(p, n, p, n, C, count, dgamma, dbeta, k12, stream);
 }
 
 // Backward stage 2: dgamma/dbeta from the local partials, k12 = [k1[C], k2[C]] from the global ones.

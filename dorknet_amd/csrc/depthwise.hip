@@ -79,14 +79,18 @@ __device__ __forceinline__ void load_strip(f32x4 (&strip)[R][NC], __amdgpu_buffe
 // y[n,oh,ow,c] = sum_{r,s} w[r][s][c] * x[n, oh*ST + r - pad, ow*ST + s - pad, c] (+ bias[c])
 // Thread = (n, oh, TW-wide chunk of ow, 4 channels); consecutive threads take consecutive
 // channel groups, so a wave reads whole pixel rows.
-// STATS: also the BatchNorm statistics of y (fp64 sum, sum of squares per channel) of this
-// block's outputs -> part[block][2][C]; needs 256 % (C/4) == 0 so that a block covers every
-// channel (thread tid always has channel group tid % (C/4)).
-template <int R, int S, int ST, bool BN, bool STATS>
+// STATS: also a per-channel reduction of this block's outputs -> part[block][2][C]; needs
+// 256 % (C/4) == 0 so that a block covers every channel (thread tid always has channel group
+// tid % (C/4)).  STATS == 1: BatchNorm statistics of y (fp64 sum, sum of squares);
+// STATS == 2 (this kernel computing a stride-1 dgrad): the BN-backward sums of the BatchNorm
+// whose output the layer consumed -- sum(g), sum(g * x_hat) with g = y masked by that BN's
+// fused ReLU (batch_norm.py:125-174, dk_bn_bwd_partial_f64); xo is that BN's raw input.
+template <int R, int S, int ST, bool BN, int STATS>
 __global__ __launch_bounds__(256) void dw_fwd_kernel(const float* __restrict__ x, uint32_t xbytes,
                                                      const float* __restrict__ wt, const float* __restrict__ bias,
                                                      float* __restrict__ y, int N, int H, int W, int C, int OH, int OW,
-                                                     int pad, BnIn bn, double* __restrict__ part) {
+                                                     int pad, BnIn bn, double* __restrict__ part,
+                                                     const float* __restrict__ xo, BnIn obn) {
   constexpr int TW = DwTile<ST>::TW;
   constexpr int NC = (TW - 1) * ST + S;
   const int C4 = C >> 2;
@@ -94,7 +98,7 @@ __global__ __launch_bounds__(256) void dw_fwd_kernel(const float* __restrict__ x
   const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const long long total = (long long)N * OH * nwc * C4;
   const bool live = idx < total;
-  if (!STATS && !live) return;
+  if (STATS == 0 && !live) return;
   const int cq = (int)(idx % C4);
   const int c = cq * 4;
   double s1[4] = {0.0, 0.0, 0.0, 0.0}, s2[4] = {0.0, 0.0, 0.0, 0.0};
@@ -114,6 +118,13 @@ __global__ __launch_bounds__(256) void dw_fwd_kernel(const float* __restrict__ x
       for (int s = 0; s < S; ++s) wv[r][s] = ld4(wt + (r * S + s) * C + c);
     const f32x4 b0 = bias ? ld4(bias + c) : f32x4{0.f, 0.f, 0.f, 0.f};
     float* yrow = y + ((size_t)(n * OH + oh) * OW) * C + c;
+    f32x4 om, oi, og, ob;
+    if constexpr (STATS == 2) {
+      om = ld4(obn.mean + c);
+      oi = ld4(obn.invstd + c);
+      og = ld4(obn.gamma + c);
+      ob = ld4(obn.beta + c);
+    }
 #pragma unroll
     for (int j = 0; j < TW; ++j) {
       f32x4 acc = b0;
@@ -123,18 +134,28 @@ __global__ __launch_bounds__(256) void dw_fwd_kernel(const float* __restrict__ x
         for (int s = 0; s < S; ++s) acc += strip[r][j * ST + s] * wv[r][s];
       if (ow0 + j < OW) {
         st4(yrow + (size_t)(ow0 + j) * C, acc);
-        if constexpr (STATS) {
+        if constexpr (STATS == 1) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             const double v = (double)acc[e];
             s1[e] += v;
             s2[e] += v * v;
           }
+        } else if constexpr (STATS == 2) {
+          const f32x4 xv = ld4(xo + ((size_t)(n * OH + oh) * OW + ow0 + j) * C + c);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            float g = acc[e];
+            const float xh = (xv[e] - om[e]) * oi[e];
+            if (obn.relu && !(bn_out(xv[e], om[e], oi[e], og[e], ob[e]) > 0.f)) g = 0.f;
+            s1[e] += (double)g;
+            s2[e] += (double)g * (double)xh;
+          }
         }
       }
     }
   }
-  if constexpr (STATS) {
+  if constexpr (STATS != 0) {
     // fixed-order block reduction over the 256 / C4 threads of each channel group
     __shared__ double red[256][8];
 #pragma unroll
@@ -354,37 +375,43 @@ static long long dw_fwd_threads(int N, int OH, int OW, int C) {
   return (long long)N * OH * ((OW + TW - 1) / TW) * (C / 4);
 }
 
+// part: per-block sums (mode 1: output statistics; mode 2 with xo/obn: BN-backward sums).
 template <int R, int S, int ST>
 static void launch_dw_fwd(const float* x, const float* wt, const float* bias, float* y, int N, int H, int W, int C,
-                          int OH, int OW, int pad, const BnIn& bn, double* part, hipStream_t st) {
+                          int OH, int OW, int pad, const BnIn& bn, double* part, const float* xo, const BnIn& obn,
+                          hipStream_t st) {
   const uint32_t xb = (uint32_t)((size_t)N * H * W * C * sizeof(float));
   const dim3 grid((unsigned)cdivll(dw_fwd_threads<ST>(N, OH, OW, C), 256));
 #define DW_LAUNCH(B, ST_)                                                                                            \
   hipLaunchKernelGGL((dw_fwd_kernel<R, S, ST, B, ST_>), grid, dim3(256), 0, st, x, xb, wt, bias, y, N, H, W, C, OH, \
-                     OW, pad, bn, part)
+                     OW, pad, bn, part, xo, obn)
+  const int mode = part ? (xo ? 2 : 1) : 0;
   if (bn.mean) {
-    if (part)
-      DW_LAUNCH(true, true);
-    else
-      DW_LAUNCH(true, false);
+    if (mode == 1)
+      DW_LAUNCH(true, 1);
+    else if (mode == 0)
+      DW_LAUNCH(true, 0);
   } else {
-    if (part)
-      DW_LAUNCH(false, true);
+    if (mode == 2)
+      DW_LAUNCH(false, 2);
+    else if (mode == 1)
+      DW_LAUNCH(false, 1);
     else
-      DW_LAUNCH(false, false);
+      DW_LAUNCH(false, 0);
   }
 #undef DW_LAUNCH
 }
 
 static int dw_fwd_dispatch(const float* x, const float* wt, const float* bias, float* y, int N, int H, int W, int C,
                            int R, int S, int stride, int OH, int OW, int pad, const BnIn& bn, hipStream_t st,
-                           double* part = nullptr) {
+                           double* part = nullptr, const float* xo = nullptr, const BnIn& obn = BnIn{}) {
   if (C % 4 || !aligned16(x) || !aligned16(wt) || !fits((size_t)N * H * W * C * 4) || !bn_ok(bn)) return DK_ERR_ARGS;
   if (part && (C / 4 > 256 || 256 % (C / 4))) return DK_ERR_ARGS;
-#define DW_CASE(RR, SS, STR)                                                            \
-  if (R == RR && S == SS && stride == STR) {                                            \
-    launch_dw_fwd<RR, SS, STR>(x, wt, bias, y, N, H, W, C, OH, OW, pad, bn, part, st);  \
-    return launch_status();                                                             \
+  if (xo && (bn.mean || !obn.mean || !aligned16(xo) || !bn_ok(obn))) return DK_ERR_ARGS;
+#define DW_CASE(RR, SS, STR)                                                                     \
+  if (R == RR && S == SS && stride == STR) {                                                     \
+    launch_dw_fwd<RR, SS, STR>(x, wt, bias, y, N, H, W, C, OH, OW, pad, bn, part, xo, obn, st);  \
+    return launch_status();                                                                      \
   }
   DW_CASE(3, 3, 1)
   DW_CASE(3, 3, 2)
@@ -489,6 +516,33 @@ DK_API int dk_dwconv_dgrad_f32(const float* dy, int N, int OH, int OW, int C, co
   else
     return DK_ERR_ARGS;
   return launch_status();
+}
+
+// Stride-1 dgrad + the BN-backward partial sums of the BatchNorm whose output the layer
+// consumed (bn_x = its raw input, same shape as dx).  Returns DK_ERR_ARGS for geometries this
+// fusion does not cover (stride != 1, or dk_dwconv_dgrad_stats_rows() == 0).
+DK_API int dk_dwconv_dgrad_stats_rows(int N, int H, int W, int C, int stride) {
+  if (stride != 1) return 0;
+  return dk_dwconv_fwd_stats_rows(N, H, W, C, 1);
+}
+
+DK_API int dk_dwconv_dgrad_ex_f32(const float* dy, int N, int OH, int OW, int C, const float* w_crs, int R, int S,
+                                  int stride, int pad, float* dx, int H, int W, void* ws, size_t ws_bytes,
+                                  const float* bn_x, const float* bn_mean, const float* bn_invstd,
+                                  const float* bn_gamma, const float* bn_beta, int bn_relu, double* part,
+                                  void* stream) {
+  if (C % 4) return DK_ERR_ARGS;
+  if (ws_bytes < dk_dwconv_dgrad_workspace_bytes(C, R, S)) return DK_ERR_WORKSPACE;
+  if (!(stride == 1 && pad <= R - 1 && pad <= S - 1 && R == S) || !part || !bn_x ||
+      dk_dwconv_dgrad_stats_rows(N, H, W, C, 1) == 0)
+    return DK_ERR_ARGS;
+  float* wt = static_cast<float*>(ws);
+  const hipStream_t st = as_stream(stream);
+  hipLaunchKernelGGL(dw_weight_rsc_kernel, dim3(cdiv(C * R * S, 256)), dim3(256), 0, st, w_crs, C, R, S, 1, wt);
+  int rc = launch_status();
+  if (rc) return rc;
+  return dw_fwd_dispatch(dy, wt, nullptr, dx, N, OH, OW, C, R, S, 1, H, W, R - 1 - pad, BnIn{}, st, part, bn_x,
+                         BnIn{bn_mean, bn_invstd, bn_gamma, bn_beta, bn_relu});
 }
 
 DK_API size_t dk_dwconv_wgrad_workspace_bytes(int N, int OH, int OW, int C, int R, int S) {

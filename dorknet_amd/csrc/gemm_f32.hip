@@ -383,6 +383,32 @@ struct EpStore {
 struct EpStoreStats : EpStore {
   static constexpr bool kColStats = true;
   double* part;
+  __device__ __forceinline__ void contrib(int, int n, float v, double& a, double& b) const {
+    a = (double)value(n, v);
+    b = a * a;
+  }
+};
+
+// The BatchNorm-backward reduction of the layer whose input gradient this GEMM produces
+// (batch_norm.py:125-174's sum(dy) and sum(dy * x_hat), with the fused ReLU's mask
+// recomputed from the BN's raw input x as in dk_bn_bwd_partial_f64): part[m_tile][2][N].
+// `pix(m)` maps the GEMM row to the pixel of x (identity, or the widened lattice point).
+__device__ __forceinline__ void bn_bwd_contrib(float g, float x, const BnIn& bn, int n, double& a, double& b) {
+  const float mu = bn.mean[n], is = bn.invstd[n];
+  const float xh = (x - mu) * is;
+  if (bn.relu && !(bn_out(x, mu, is, bn.gamma[n], bn.beta[n]) > 0.f)) g = 0.f;
+  a = (double)g;
+  b = (double)g * (double)xh;
+}
+
+struct EpStoreBnBwd : EpStore {
+  static constexpr bool kColStats = true;
+  double* part;
+  const float* xbn;  // [M][ldo], the BN's raw input
+  BnIn bn;
+  __device__ __forceinline__ void contrib(int m, int n, float v, double& a, double& b) const {
+    bn_bwd_contrib(v, xbn[(size_t)m * ldo + n], bn, n, a, b);
+  }
 };
 
 // Pointwise stride-st backward "widen" (pointwise_convolution.py:68-72) fused: the GEMM
@@ -402,6 +428,23 @@ struct EpWiden {
     const size_t cell = (size_t)(b * OH2 + oh * st) * OW2 + (size_t)ow * st;
     for (int dy = 0; dy < st; ++dy)
       for (int dx = 0; dx < st; ++dx) out[(cell + (size_t)dy * OW2 + dx) * ldo + n] = (dy | dx) ? 0.f : v;
+  }
+};
+
+// EpWiden + the BN-backward reduction over the written (lattice) points; the zeros off the
+// lattice contribute nothing.
+struct EpWidenBnBwd : EpWiden {
+  static constexpr bool kColStats = true;
+  double* part;
+  const float* xbn;  // the BN's raw input on the widened grid
+  BnIn bn;
+  __device__ __forceinline__ void contrib(int m, int n, float v, double& a, double& b) const {
+    const int ow = m % OW;
+    const int t = m / OW;
+    const int oh = t % OH;
+    const int bb = t / OH;
+    const size_t px = (size_t)(bb * OH * st + oh * st) * (OW * st) + (size_t)ow * st;
+    bn_bwd_contrib(v, xbn[px * ldo + n], bn, n, a, b);
   }
 };
 
@@ -519,7 +562,8 @@ __global__ __launch_bounds__(64 * WM * WN) void igemm_f32(DA da, DB db, EP ep, i
 
   if constexpr (EP::kColStats) {
     static_assert(WM * BN * 4 <= 2 * (ABUF + BBUF), "stats scratch fits the operand LDS");
-    // Column sums of the stored values over this tile's valid rows, fp64, fixed order:
+    // Column sums of ep.contrib (the stored values and their squares, or the BN-backward
+    // terms) over this tile's valid rows, fp64, fixed order:
     // lane's 16*TM rows -> lane halves (h) -> waves along M (wm) -> part[m_tile][.][col].
     __syncthreads();  // the MFMA loop's last LDS reads are done; reuse smem
     double* red = reinterpret_cast<double*>(smem);  // [WM][BN][2]
@@ -535,9 +579,10 @@ __global__ __launch_bounds__(64 * WM * WN) void igemm_f32(DA da, DB db, EP ep, i
           for (int r = 0; r < 16; ++r) {
             const int row = m0 + wm * 32 * TM + t * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
             if (row < M) {
-              const double v = (double)ep.value(col, acc[t][u][r]);
-              s1 += v;
-              s2 += v * v;
+              double a, b;
+              ep.contrib(row, col, acc[t][u][r], a, b);
+              s1 += a;
+              s2 += b;
             }
           }
       }
@@ -1033,6 +1078,46 @@ DK_API int dk_pwconv_dgrad_f32(const float* dy, int N, int OH, int OW, int K, co
   EpWiden ep{dx, C, OH, OW, stride};
   if (vec) return igemm_rows<LdMatKC, MatDesc, LdMatIC, MatDesc, EpWiden>(a, b, ep, M, C, K, st);
   return igemm_rows<LdMatKC1, MatDesc, LdMatIC1, MatDesc, EpWiden>(a, b, ep, M, C, K, st);
+}
+
+DK_API int dk_pwconv_dgrad_stats_rows(int N, int OH, int OW, int K, int C) { return stats_rows(N * OH * OW, C, K); }
+
+// dgrad + the BN-backward partial sums of the BatchNorm whose output this layer consumed
+// (bn_x = that BN's raw input, on the dx grid; part: dk_pwconv_dgrad_stats_rows() x 2 x C).
+DK_API int dk_pwconv_dgrad_ex_f32(const float* dy, int N, int OH, int OW, int K, const float* w_kc, int C, int stride,
+                                  float* dx, const float* bn_x, const float* bn_mean, const float* bn_invstd,
+                                  const float* bn_gamma, const float* bn_beta, int bn_relu, double* part,
+                                  void* stream) {
+  const int M = N * OH * OW;
+  if (!fits((size_t)M * K * 4) || !bn_x || !part || !bn_mean || !bn_invstd || !bn_gamma || !bn_beta)
+    return DK_ERR_ARGS;
+  MatDesc a = mat(dy, M, K, M);
+  MatDesc b = mat(w_kc, K, C, C);
+  const hipStream_t st = as_stream(stream);
+  const bool vec = vec_ok(a, K, 4) && vec_ok(b, 4, C);
+  const BnIn bn{bn_mean, bn_invstd, bn_gamma, bn_beta, bn_relu};
+  if (stride == 1) {
+    EpStoreBnBwd ep;
+    ep.out = dx;
+    ep.ldo = C;
+    ep.bias = nullptr;
+    ep.part = part;
+    ep.xbn = bn_x;
+    ep.bn = bn;
+    if (vec) return igemm_rows<LdMatKC, MatDesc, LdMatIC, MatDesc, EpStoreBnBwd>(a, b, ep, M, C, K, st);
+    return igemm_rows<LdMatKC1, MatDesc, LdMatIC1, MatDesc, EpStoreBnBwd>(a, b, ep, M, C, K, st);
+  }
+  EpWidenBnBwd ep;
+  ep.out = dx;
+  ep.ldo = C;
+  ep.OH = OH;
+  ep.OW = OW;
+  ep.st = stride;
+  ep.part = part;
+  ep.xbn = bn_x;
+  ep.bn = bn;
+  if (vec) return igemm_rows<LdMatKC, MatDesc, LdMatIC, MatDesc, EpWidenBnBwd>(a, b, ep, M, C, K, st);
+  return igemm_rows<LdMatKC1, MatDesc, LdMatIC1, MatDesc, EpWidenBnBwd>(a, b, ep, M, C, K, st);
 }
 
 DK_API size_t dk_pwconv_wgrad_workspace_bytes(int N, int OH, int OW, int K, int C) {

@@ -20,15 +20,16 @@ from .._tensor import empty_nhwc
 
 
 class BNOut:
-    __slots__ = ("x", "mean", "invstd", "gamma", "beta", "relu", "_y")
+    __slots__ = ("x", "mean", "invstd", "gamma", "beta", "relu", "owner", "_y")
 
-    def __init__(self, x, mean, invstd, gamma, beta, relu):
+    def __init__(self, x, mean, invstd, gamma, beta, relu, owner=None):
         self.x = x            # raw input of the BatchNormLayer (NHWC storage, logical NCHW)
         self.mean = mean      # (C,) fp32 device tensors
         self.invstd = invstd
         self.gamma = gamma
         self.beta = beta
         self.relu = bool(relu)
+        self.owner = owner    # the BatchNormLayer (its backward can take partial sums, see below)
         self._y = None
 
     @property
@@ -50,6 +51,12 @@ class BNOut:
         """(mean, invstd, gamma, beta, relu) for a dk_*_bnx_f32 call."""
         return (self.mean.data_ptr(), self.invstd.data_ptr(), self.gamma.data_ptr(), self.beta.data_ptr(),
                 int(self.relu))
+
+    def hand_backward_partials(self, dx, part):
+        """A consumer's backward computed stage 1 of this BatchNorm's backward (the
+        *_dgrad_ex_f32 epilogue) while producing `dx`, the gradient w.r.t. this BNOut."""
+        if self.owner is not None:
+            self.owner._pending_bwd = (dx, part)
 
     def materialize(self):
         """The normalised tensor itself (computed once)."""

@@ -27,6 +27,7 @@ class ReLu(Layer):
         super().__init__(layer_name)
         self._mask = None
         self._fused_out = None
+        self._join_bn = None
 
     def __repr__(self):
         return "ReLu({})".format(self.layer_name)
@@ -45,7 +46,7 @@ class ReLu(Layer):
                                memory_format=torch.channels_last if x.dim() == 4 else torch.contiguous_format)
         lib.dk_relu_fwd_f32(x.data_ptr(), x.numel(), y.data_ptr(), 0 if mask is None else mask.data_ptr(), st)
         if not test_mode:
-            self._mask, self._fused_out = mask, None
+            self._mask, self._fused_out, self._join_bn = mask, None, None
         return y
 
     def forward_add(self, A, B, test_mode=False):
@@ -68,7 +69,7 @@ class ReLu(Layer):
         lib.dk_add_f32(a.data_ptr(), b.data_ptr(), a.numel(), 1, y.data_ptr(),
                        0 if mask is None else mask.data_ptr(), st)
         if not test_mode:
-            self._mask, self._fused_out = mask, None
+            self._mask, self._fused_out, self._join_bn = mask, None, None
         return y
 
     def _bn_add(self, A, B, test_mode, st):
@@ -89,11 +90,12 @@ class ReLu(Layer):
                           0 if mask is None else mask.data_ptr(), st)
         if not test_mode:
             self._mask, self._fused_out = mask, None
+            self._join_bn = A if isinstance(A, BNOut) else None
         return y
 
     def _attach_fused(self, y, test_mode):
         if not test_mode:
-            self._mask, self._fused_out = None, y
+            self._mask, self._fused_out, self._join_bn = None, y, None
 
     @property
     def positive_locs(self):
@@ -122,6 +124,17 @@ class ReLu(Layer):
                                .format(self.layer_name))
         dy = _same_layout(upstream_dx)
         dx = self._empty_like(dy)
+        bn = getattr(self, "_join_bn", None)
+        if bn is not None and tuple(bn.x.shape) == tuple(dy.shape) and is_nhwc_t(dy):
+            # the join's BN input: its backward stage 1 rides on this pass (residual_block.py:85-86)
+            C = dy.shape[1]
+            P = dy.numel() // C
+            nb = lib.dk_bn_workspace_bytes(P, C)
+            part = torch.empty((lib.dk_bn_partial_blocks(P, C), 2, C), dtype=torch.float64, device=dy.device)
+            lib.dk_relu_bwd_bn_partial_f64(dy.data_ptr(), self._mask.data_ptr(), bn.x.data_ptr(), P, C,
+                                           *bn.bn_args(), dx.data_ptr(), part.data_ptr(), nb, stream_handle())
+            bn.hand_backward_partials(dx, part)
+            return dx
         lib.dk_relu_bwd_f32(dy.data_ptr(), self._mask.data_ptr(), dy.numel(), dx.data_ptr(), stream_handle())
         return dx
 

@@ -141,6 +141,7 @@ class BatchNormLayer(Layer):
         st = stream_handle()
         x, P, C = self._prep_input(as_device(X))
         self.input_shape = tuple(x.shape)
+        self._pending_bwd = None
         if not test_mode:
             mean, std, invstd = self._stats(x, P, C, st, stats)
             self.X = x
@@ -168,7 +169,7 @@ class BatchNormLayer(Layer):
         from ._bn_input import BNOut
         x, mean, invstd = self._normalisation(X, test_mode, stats)
         out = BNOut(x, mean, invstd, self.learned_params["gamma"], self.learned_params["beta"],
-                    relu_layer is not None)
+                    relu_layer is not None, owner=self)
         if relu_layer is not None:
             relu_layer._attach_fused(out, test_mode)
         return out
@@ -196,7 +197,29 @@ class BatchNormLayer(Layer):
         dgamma = grad_buffer(self, "gamma", gamma.shape)
         dbeta = grad_buffer(self, "beta", beta.shape)
         dx = self._out_like(x)
-        if self.sync_group is None:
+        pending, self._pending_bwd = getattr(self, "_pending_bwd", None), None
+        if pending is not None and pending[0].data_ptr() == dy.data_ptr() and pending[0].shape == dy.shape:
+            # stage 1 was computed by the consumer's dgrad epilogue (layers/_bn_input.py)
+            part = pending[1]
+            nrows = part.shape[0]
+            k12 = torch.empty(2 * C, dtype=torch.float32, device=x.device)
+            nb = lib.dk_bn_partials_workspace_bytes(nrows, C)
+            ws = workspace.get(nb)
+            if self.sync_group is None:
+                lib.dk_bn_bwd_from_partials_f32(part.data_ptr(), nrows, C, float(P), dgamma.data_ptr(),
+                                                dbeta.data_ptr(), k12.data_ptr(), ws, nb, st)
+            else:
+                import torch.distributed as dist
+                local = torch.empty(2 * C, dtype=torch.float64, device=x.device)
+                lib.dk_bn_reduce_partials_f64(part.data_ptr(), nrows, C, local.data_ptr(), ws, nb, st)
+                glob = local.clone()
+                dist.all_reduce(glob, group=self.sync_group)
+                lib.dk_bn_bwd_finalize_f32(local.data_ptr(), 1, glob.data_ptr(), 1, C, float(P) * self._world(),
+                                           dgamma.data_ptr(), dbeta.data_ptr(), k12.data_ptr(), st)
+            lib.dk_bn_bwd_apply_f32(x.data_ptr(), dy.data_ptr(), x.numel(), C, self._mean.data_ptr(),
+                                    self._invstd.data_ptr(), gamma.data_ptr(), beta.data_ptr(), int(relu),
+                                    k12.data_ptr(), dx.data_ptr(), st)
+        elif self.sync_group is None:
             nb = lib.dk_bn_bwd_workspace_bytes(P, C)
             lib.dk_bn_bwd_f32(x.data_ptr(), dy.data_ptr(), P, C, self._mean.data_ptr(), self._invstd.data_ptr(),
                               gamma.data_ptr(), beta.data_ptr(), int(relu), dgamma.data_ptr(), dbeta.data_ptr(),

@@ -127,8 +127,18 @@ class DepthwiseConvLayer(Layer):
             add_regulariser_grad(gw, w, self.weight_regulariser)
         dx = empty_nhwc(N, C, H, W)
         nb = lib.dk_dwconv_dgrad_workspace_bytes(C, R, S)
-        lib.dk_dwconv_dgrad_f32(dy.data_ptr(), N, OH, OW, C, w.data_ptr(), R, S, self.stride, self.padding,
-                                dx.data_ptr(), H, W, workspace.get(nb), nb, st)
+        bn = self._bn_in
+        rows = lib.dk_dwconv_dgrad_stats_rows(N, H, W, C, self.stride) if bn is not None and R == S else 0
+        if rows and self.padding <= R - 1:
+            # + stage 1 of the input BatchNorm's backward, in the dgrad epilogue
+            part = torch.empty((rows, 2, C), dtype=torch.float64, device=dx.device)
+            lib.dk_dwconv_dgrad_ex_f32(dy.data_ptr(), N, OH, OW, C, w.data_ptr(), R, S, self.stride, self.padding,
+                                       dx.data_ptr(), H, W, workspace.get(nb), nb, bn.x.data_ptr(), *bn.bn_args(),
+                                       part.data_ptr(), st)
+            bn.hand_backward_partials(dx, part)
+        else:
+            lib.dk_dwconv_dgrad_f32(dy.data_ptr(), N, OH, OW, C, w.data_ptr(), R, S, self.stride, self.padding,
+                                    dx.data_ptr(), H, W, workspace.get(nb), nb, st)
         return dx
 
     def save_to_h5(self, open_f, save_grads=True):

@@ -118,7 +118,16 @@ class PointwiseConvLayer(Layer):
         if l2s is None:
             add_regulariser_grad(gw, w, self.weight_regulariser)
         dx = empty_nhwc(N, C, OH * s, OW * s)  # widened shape, pointwise_convolution.py:68-72
-        lib.dk_pwconv_dgrad_f32(dy.data_ptr(), N, OH, OW, K, w.data_ptr(), C, s, dx.data_ptr(), st)
+        bn = self._bn_in
+        if bn is not None and (OH * s, OW * s) == (H, W):
+            # + stage 1 of the input BatchNorm's backward, in the dgrad epilogue
+            rows = lib.dk_pwconv_dgrad_stats_rows(N, OH, OW, K, C)
+            part = torch.empty((rows, 2, C), dtype=torch.float64, device=dx.device)
+            lib.dk_pwconv_dgrad_ex_f32(dy.data_ptr(), N, OH, OW, K, w.data_ptr(), C, s, dx.data_ptr(),
+                                       bn.x.data_ptr(), *bn.bn_args(), part.data_ptr(), st)
+            bn.hand_backward_partials(dx, part)
+        else:
+            lib.dk_pwconv_dgrad_f32(dy.data_ptr(), N, OH, OW, K, w.data_ptr(), C, s, dx.data_ptr(), st)
         return dx
 
     def save_to_h5(self, open_f, save_grads=True):

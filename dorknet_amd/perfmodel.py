@@ -173,6 +173,15 @@ MODEL = {
     "dk_conv2d_fwd_ex_f32": _ex(_conv_fwd),
     "dk_pwconv_fwd_ex_f32": _ex(_pw_fwd),
     "dk_dwconv_fwd_ex_f32": _ex(_dw_fwd),
+    # dgrad + BN-backward partials: also reads the BN's raw input (same size as dx)
+    "dk_pwconv_dgrad_ex_f32": lambda dy, N, OH, OW, K, w, C, s, dx, bx, m, i, g, b, r, part, st: (
+        _pw_dgrad(dy, N, OH, OW, K, w, C, s, dx, st)[0],
+        _pw_dgrad(dy, N, OH, OW, K, w, C, s, dx, st)[1] + E * N * OH * OW * C),
+    "dk_dwconv_dgrad_ex_f32": lambda dy, N, OH, OW, C, w, R, S, s, p, dx, H, W, ws, nb, bx, m, i, g, b, r, part, st: (
+        _dw_dgrad(dy, N, OH, OW, C, w, R, S, s, p, dx, H, W, ws, nb, st)[0],
+        _dw_dgrad(dy, N, OH, OW, C, w, R, S, s, p, dx, H, W, ws, nb, st)[1] + E * N * H * W * C),
+    "dk_relu_bwd_bn_partial_f64": lambda dy, mask, x, P, C, *rest: (4 * P * C, E * 3 * P * C + P * C),
+    "dk_bn_bwd_apply_f32": lambda x, dy, n, C, *rest: (6 * n, E * 3 * n),
 }
 
 

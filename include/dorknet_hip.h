@@ -100,6 +100,17 @@ int dk_pwconv_fwd_stats_rows(int N, int OH, int OW, int K, int C);
 int dk_pwconv_fwd_ex_f32(const float* x, int N, int H, int W, int C, const float* w_kc, int K, int stride, const float* bias, float* y, int OH, int OW, const float* bn_mean, const float* bn_invstd, const float* bn_gamma, const float* bn_beta, int bn_relu, double* stats, void* stream);
 int dk_dwconv_fwd_stats_rows(int N, int OH, int OW, int C, int stride);
 int dk_dwconv_fwd_ex_f32(const float* x, int N, int H, int W, int C, const float* w_rsc, int R, int S, int stride, int pad, const float* bias, float* y, int OH, int OW, const float* bn_mean, const float* bn_invstd, const float* bn_gamma, const float* bn_beta, int bn_relu, double* stats, void* stream);
+/* Backward side: *_dgrad_ex_f32 = the input gradient plus stage 1 of the backward of the
+ * BatchNorm whose output this layer consumed (the BN-on-load input of its forward): with
+ * g = dx masked by that BN's fused ReLU (recomputed from bn_x, the BN's raw input, laid out
+ * like dx), part[rows][2][C] = per-tile (sum g, sum g * x_hat) -- what dk_bn_bwd_partial_f64
+ * computes in a separate pass over x and dx (batch_norm.py:125-174).  Consume with
+ * dk_bn_bwd_from_partials_f32.  dk_dwconv_dgrad_stats_rows returns 0 (no fused variant)
+ * unless stride == 1 and C/4 divides 256. */
+int dk_pwconv_dgrad_stats_rows(int N, int OH, int OW, int K, int C);
+int dk_pwconv_dgrad_ex_f32(const float* dy, int N, int OH, int OW, int K, const float* w_kc, int C, int stride, float* dx, const float* bn_x, const float* bn_mean, const float* bn_invstd, const float* bn_gamma, const float* bn_beta, int bn_relu, double* part, void* stream);
+int dk_dwconv_dgrad_stats_rows(int N, int H, int W, int C, int stride);
+int dk_dwconv_dgrad_ex_f32(const float* dy, int N, int OH, int OW, int C, const float* w_crs, int R, int S, int stride, int pad, float* dx, int H, int W, void* ws, size_t ws_bytes, const float* bn_x, const float* bn_mean, const float* bn_invstd, const float* bn_gamma, const float* bn_beta, int bn_relu, double* part, void* stream);
 
 /* ---------------------------------------------------------------------------------------
  * Depthwise convolution, direct (no MFMA).
@@ -149,6 +160,13 @@ int dk_bn_stats_f32(const float* x, int P, int C, float eps, float momentum, int
 size_t dk_bn_partials_workspace_bytes(int nblk, int C);
 int dk_bn_stats_from_partials_f32(const void* part, int nblk, int C, double count, float eps, float momentum, int first, float* mean, float* std_, float* invstd, float* run_mean, float* run_std, void* ws, size_t ws_bytes, void* stream);
 int dk_bn_reduce_partials_f64(const void* part, int nblk, int C, void* out, void* ws, size_t ws_bytes, void* stream);
+/* Backward stage 2 from partials of any origin ([nblk][2][C]: dk_bn_bwd_partial_f64, a
+ * consumer's *_dgrad_ex_f32, dk_relu_bwd_bn_partial_f64): dgamma, dbeta and k12 for
+ * dk_bn_bwd_apply_f32.  The fused post-residual ReLU backward (residual_block.py:85-86) +
+ * stage 1 of the backward of the BN feeding the join: dx = mask ? dy : 0 and part (sized
+ * dk_bn_workspace_bytes(P, C), dk_bn_partial_blocks(P, C) rows). */
+int dk_bn_bwd_from_partials_f32(const void* part, int nblk, int C, double count, float* dgamma, float* dbeta, float* k12, void* ws, size_t ws_bytes, void* stream);
+int dk_relu_bwd_bn_partial_f64(const float* dy, const uint8_t* mask, const float* x, int P, int C, const float* mean, const float* invstd, const float* gamma, const float* beta, int relu, float* dx, void* part, size_t part_bytes, void* stream);
 int dk_bn_infer_params_f32(const float* run_std, int C, float* invstd, void* stream);
 int dk_bn_apply_f32(const float* x, long long numel, int C, const float* mean, const float* invstd, const float* gamma, const float* beta, int relu, float* y, uint8_t* mask, void* stream);
 int dk_bn_bwd_partial_f64(const float* x, const float* dy, int P, int C, const float* mean, const float* invstd, const float* gamma, const float* beta, int relu, void* ws, size_t ws_bytes, void* stream);

@@ -216,3 +216,95 @@ def test_producer_statistics(kind, bn_in):
     same(y0, y1)
     (m1, s1), (m0, s0) = _stats_pair(y1, part, rows, Cout)
     assert torch.allclose(m1, m0, rtol=1e-6, atol=1e-6) and torch.allclose(s1, s0, rtol=1e-6, atol=0)
+
+
+def _bwd_finalize(part, rows, C, P):
+    st = stream_handle()
+    dg, db, k12 = torch.empty(C, device="cuda"), torch.empty(C, device="cuda"), torch.empty(2 * C, device="cuda")
+    nb = lib.dk_bn_partials_workspace_bytes(rows, C)
+    lib.dk_bn_bwd_from_partials_f32(part.data_ptr(), rows, C, float(P), dg.data_ptr(), db.data_ptr(), k12.data_ptr(),
+                                    workspace.get(nb), nb, st)
+    return dg, db, k12
+
+
+def _bwd_reference(xbn, g, p, relu):
+    """Stage 1 + 2 by the standalone passes (dk_bn_bwd_partial_f64 over xbn, g)."""
+    st = stream_handle()
+    C = xbn.shape[1]
+    P = xbn.numel() // C
+    nb = lib.dk_bn_workspace_bytes(P, C)
+    part = torch.empty(nb // 8, dtype=torch.float64, device="cuda")
+    lib.dk_bn_bwd_partial_f64(xbn.data_ptr(), g.data_ptr(), P, C, *args(p, relu)[:4], relu, part.data_ptr(), nb, st)
+    return _bwd_finalize(part, lib.dk_bn_partial_blocks(P, C), C, P)
+
+
+def _close(a, b):
+    torch.cuda.synchronize()
+    for u, v in zip(a, b):
+        assert torch.allclose(u, v, rtol=1e-5, atol=1e-6 * float(v.abs().max()) + 1e-12), float((u - v).abs().max())
+
+
+@pytest.mark.parametrize("stride,relu", [(1, 0), (2, 1)])
+def test_pointwise_dgrad_bn_partials(stride, relu):
+    """dgrad_ex: dx bit-identical to the plain dgrad, and the BN-backward sums of its
+    epilogue equal the standalone reduction over (bn_x, dx)."""
+    rng = np.random.RandomState(21 + stride)
+    N, C, K, OH, OW = 3, 24, 40, 9, 7
+    H, W = OH * stride, OW * stride
+    dy = nhwc(rng.randn(N, K, OH, OW))
+    w = torch.as_tensor(rng.randn(K, C).astype(np.float32), device="cuda")
+    xbn = nhwc(rng.randn(N, C, H, W))
+    p = bn_params(C, rng)
+    st = stream_handle()
+    dx0 = torch.empty((N, C, H, W), device="cuda").contiguous(memory_format=torch.channels_last)
+    dx1 = torch.empty_like(dx0)
+    lib.dk_pwconv_dgrad_f32(dy.data_ptr(), N, OH, OW, K, w.data_ptr(), C, stride, dx0.data_ptr(), st)
+    rows = lib.dk_pwconv_dgrad_stats_rows(N, OH, OW, K, C)
+    part = torch.empty((rows, 2, C), dtype=torch.float64, device="cuda")
+    lib.dk_pwconv_dgrad_ex_f32(dy.data_ptr(), N, OH, OW, K, w.data_ptr(), C, stride, dx1.data_ptr(), xbn.data_ptr(),
+                               *args(p, relu), part.data_ptr(), st)
+    same(dx0, dx1)
+    _close(_bwd_finalize(part, rows, C, N * H * W), _bwd_reference(xbn, dx0, p, relu))
+
+
+def test_depthwise_dgrad_bn_partials():
+    rng = np.random.RandomState(31)
+    N, C, H, W = 2, 32, 11, 13
+    dy = nhwc(rng.randn(N, C, H, W))
+    w = torch.as_tensor(rng.randn(C, 3, 3).astype(np.float32), device="cuda")
+    xbn = nhwc(rng.randn(N, C, H, W))
+    p = bn_params(C, rng)
+    st = stream_handle()
+    nb = lib.dk_dwconv_dgrad_workspace_bytes(C, 3, 3)
+    dx0 = torch.empty_like(dy)
+    dx1 = torch.empty_like(dy)
+    lib.dk_dwconv_dgrad_f32(dy.data_ptr(), N, H, W, C, w.data_ptr(), 3, 3, 1, 1, dx0.data_ptr(), H, W,
+                            workspace.get(nb), nb, st)
+    rows = lib.dk_dwconv_dgrad_stats_rows(N, H, W, C, 1)
+    part = torch.empty((rows, 2, C), dtype=torch.float64, device="cuda")
+    lib.dk_dwconv_dgrad_ex_f32(dy.data_ptr(), N, H, W, C, w.data_ptr(), 3, 3, 1, 1, dx1.data_ptr(), H, W,
+                               workspace.get(nb), nb, xbn.data_ptr(), *args(p, 1), part.data_ptr(), st)
+    same(dx0, dx1)
+    _close(_bwd_finalize(part, rows, C, N * H * W), _bwd_reference(xbn, dx0, p, 1))
+
+
+def test_relu_bwd_bn_partials():
+    rng = np.random.RandomState(41)
+    N, C, H, W = 2, 48, 9, 10
+    dy = nhwc(rng.randn(N, C, H, W))
+    xbn = nhwc(rng.randn(N, C, H, W))
+    mask = torch.as_tensor((rng.rand(N, C, H, W) > 0.4).astype(np.uint8), device="cuda").contiguous(
+        memory_format=torch.channels_last)
+    p = bn_params(C, rng)
+    st = stream_handle()
+    n = dy.numel()
+    P = n // C
+    dx0 = torch.empty_like(dy)
+    dx1 = torch.empty_like(dy)
+    lib.dk_relu_bwd_f32(dy.data_ptr(), mask.data_ptr(), n, dx0.data_ptr(), st)
+    nb = lib.dk_bn_workspace_bytes(P, C)
+    part = torch.empty(nb // 8, dtype=torch.float64, device="cuda")
+    lib.dk_relu_bwd_bn_partial_f64(dy.data_ptr(), mask.data_ptr(), xbn.data_ptr(), P, C, *args(p, 0),
+                                   dx1.data_ptr(), part.data_ptr(), nb, st)
+    same(dx0, dx1)
+    _close(_bwd_finalize(part, lib.dk_bn_partial_blocks(P, C), C, P), _bwd_reference(xbn, dx0, p, 0))
