@@ -38,6 +38,9 @@ def parse():
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=64, help="images in the CPU-baseline sample (0 = skip)")
     ap.add_argument("--cpu-steps", type=int, default=3, help="timed CPU-baseline steps (after one warm-up)")
+    ap.add_argument("--pmc", default=None,
+                    help="per-kernel HBM traffic from rocprofv3 FETCH_SIZE/WRITE_SIZE passes of this same command "
+                         "(scripts/pmc_summary.py output; default: the newest profiles/*_pmc.json)")
     return ap.parse_args()
 
 
@@ -108,6 +111,39 @@ def roofline_entry(name, s, steps):
             "unit": unit, "frac": round(achieved / peak, 4), "traffic": None,
             "calls_per_step": s["calls"] // max(steps, 1), "avg_call_us": round(1e6 * t, 2),
             "algorithmic_per_call": {"flops": int(flops), "bytes": int(nbytes)}}
+
+
+# The kernel each single-kernel entry point launches (for the PMC traffic lookup).
+ENTRY_KERNEL = {
+    "dk_bn_bwd_apply_f32": "dk::bn_bwd_apply_kernel",
+    "dk_bn_apply_f32": "dk::bn_apply_kernel",
+    "dk_add_f32": "dk::add_kernel",
+    "dk_bn_add_f32": "dk::bn_add_kernel",
+    "dk_relu_bwd_f32": "dk::relu_bwd_kernel",
+    "dk_relu_bwd_bn_partial_f64": "dk::bn_bwd_partial_kernel",
+}
+
+
+def pmc_traffic(entry, path):
+    """Average HBM bytes per dispatch of `entry`'s kernel from a committed PMC summary, or
+    (None, None) when there is none for it."""
+    import glob
+    if path is None:
+        cands = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")))
+        path = cands[-1] if cands else None
+    kern = ENTRY_KERNEL.get(entry)
+    if not path or not kern or not os.path.exists(path):
+        return None, None
+    with open(path) as f:
+        d = json.load(f)
+    n = t = 0
+    for name, v in d.get("kernels", {}).items():
+        if name.startswith(kern + "<") or name == kern:
+            n += v["dispatches"]
+            t += v["traffic_bytes"] * v["dispatches"]
+    if n == 0:
+        return None, None
+    return t / n, os.path.relpath(path, ROOT)
 
 
 def cpu_baseline(batch, steps=3):
@@ -227,6 +263,11 @@ def main():
     if ins:
         s = ins.summary()[dominant]
         roof = roofline_entry(dominant, s, args.steps)
+        traffic, src = pmc_traffic(dominant, args.pmc)
+        if traffic is not None:
+            roof["traffic"] = round(traffic / 1e6, 2)
+            roof["traffic_unit"] = "MB per launch (HBM, rocprofv3 2*FETCH_SIZE + WRITE_SIZE)"
+            roof["traffic_source"] = src
     value = world * args.batch * args.steps / elapsed
     ms_per_step = 1e3 * elapsed / args.steps
     cpu = None

@@ -185,29 +185,92 @@ __global__ __launch_bounds__(256) void bn_collapse_kernel(const double* __restri
   }
 }
 
-// Coalesced fixed-order row reduction of partials: out[blockIdx.x][w][c] =
-// sum_{b in the block's kRowsPerBlock rows} part[b][w][c].  Block = 64 channels x 4 row lanes.
-constexpr int kRowsPerBlock = 64;
-__global__ __launch_bounds__(256) void bn_rows_reduce_kernel(const double* __restrict__ part, int nblk, int C,
-                                                             double* __restrict__ out) {
-  __shared__ double red[4][64][2];
+// Fixed-order reduction of partial rows part[nblk][2][C] (fp64) with the stage-2 maths fused
+// in: block = 64 channels x 16 row lanes, each lane holding 16 rows (all loads in flight at
+// once), up to kFoldRows rows per block.  With one block along x the block finishes the job
+// (FINAL): mode 0 statistics (batch_norm.py:76-89), 1 backward coefficients (:125-174),
+// 2 plain sums.  Otherwise it writes one folded row per block and runs again on those.
+constexpr int kFoldLanes = 16, kFoldPerLane = 16, kFoldRows = kFoldLanes * kFoldPerLane;
+
+struct FoldOut {
+  int mode;
+  double count;
+  float eps, momentum;
+  int first;
+  float *mean, *std_, *invstd, *run_mean, *run_std;  // mode 0
+  float *dgamma, *dbeta, *k12;                        // mode 1
+  double* sums;                                       // mode 2: [2][C]
+};
+
+__device__ __forceinline__ void bn_finalize_channel(int c, int C, double s, double q, const FoldOut& o) {
+  if (o.mode == 0) {
+    const double mean = s / o.count;
+    double var = q / o.count - mean * mean;
+    if (var < 0.0) var = 0.0;
+    const float meanf = (float)mean;
+    const float stdf = sqrtf((float)var + o.eps);
+    o.mean[c] = meanf;
+    o.std_[c] = stdf;
+    o.invstd[c] = 1.0f / stdf;
+    if (o.run_mean) {
+      if (o.first) {
+        o.run_mean[c] = meanf;
+        o.run_std[c] = stdf;
+      } else {
+        o.run_mean[c] = o.momentum * o.run_mean[c] + (1.0f - o.momentum) * meanf;
+        o.run_std[c] = o.momentum * o.run_std[c] + (1.0f - o.momentum) * stdf;
+      }
+    }
+  } else if (o.mode == 1) {
+    o.dgamma[c] = (float)q;
+    o.dbeta[c] = (float)s;
+    o.k12[c] = (float)(s / o.count);
+    o.k12[C + c] = (float)(q / o.count);
+  } else {
+    o.sums[c] = s;
+    o.sums[C + c] = q;
+  }
+}
+
+template <bool FINAL>
+__global__ __launch_bounds__(1024) void bn_fold_kernel(const double* __restrict__ part, int nblk, int C,
+                                                       double* __restrict__ out, FoldOut o) {
+  __shared__ double red[kFoldLanes][64][2];
   const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
   const int c = blockIdx.y * 64 + cl;
-  const int b0 = blockIdx.x * kRowsPerBlock;
-  const int b1 = min(nblk, b0 + kRowsPerBlock);
+  const int b0 = blockIdx.x * kFoldRows + rl;
   double s = 0.0, q = 0.0;
   if (c < C) {
-    for (int b = b0 + rl; b < b1; b += 4) {
-      s += part[((size_t)b * 2 + 0) * C + c];
-      q += part[((size_t)b * 2 + 1) * C + c];
+    double vs[kFoldPerLane], vq[kFoldPerLane];
+#pragma unroll
+    for (int k = 0; k < kFoldPerLane; ++k) {
+      const int b = b0 + k * kFoldLanes;
+      const int bb = b < nblk ? b : nblk - 1;  // clamp, load unconditionally, mask after
+      vs[k] = part[((size_t)bb * 2 + 0) * C + c];
+      vq[k] = part[((size_t)bb * 2 + 1) * C + c];
+    }
+#pragma unroll
+    for (int k = 0; k < kFoldPerLane; ++k) {
+      const bool in = b0 + k * kFoldLanes < nblk;
+      s += in ? vs[k] : 0.0;
+      q += in ? vq[k] : 0.0;
     }
   }
   red[rl][cl][0] = s;
   red[rl][cl][1] = q;
   __syncthreads();
-  if (rl == 0 && c < C) {
-    out[((size_t)blockIdx.x * 2 + 0) * C + c] = red[0][cl][0] + red[1][cl][0] + red[2][cl][0] + red[3][cl][0];
-    out[((size_t)blockIdx.x * 2 + 1) * C + c] = red[0][cl][1] + red[1][cl][1] + red[2][cl][1] + red[3][cl][1];
+  if (rl != 0 || c >= C) return;
+  double S = 0.0, Q = 0.0;
+#pragma unroll
+  for (int l = 0; l < kFoldLanes; ++l) {
+    S += red[l][cl][0];
+    Q += red[l][cl][1];
+  }
+  if constexpr (FINAL) {
+    bn_finalize_channel(c, C, S, Q, o);
+  } else {
+    out[((size_t)blockIdx.x * 2 + 0) * C + c] = S;
+    out[((size_t)blockIdx.x * 2 + 1) * C + c] = Q;
   }
 }
 
@@ -483,6 +546,7 @@ using namespace dk;
 DK_API int dk_bn_partial_blocks(int P, int C) { return bn_blocks(P, C); }
 
 DK_API size_t dk_bn_workspace_bytes(int P, int C) { return (size_t)bn_blocks(P, C) * 2 * C * sizeof(double); }
+static size_t bn_fold_offset(int P, int C) { return (size_t)bn_blocks(P, C) * 2 * C * sizeof(double); }
 
 // Stage 1 of forward statistics: part[nblk][2][C] (fp64 sum x, sum x^2) over x[P][C].
 DK_API int dk_bn_stats_partial_f64(const float* x, int P, int C, void* ws, size_t ws_bytes, void* stream) {
@@ -522,46 +586,68 @@ DK_API int dk_bn_stats_finalize_f32(const void* part, int nblk, int C, double co
 DK_API int dk_bn_stats_f32(const float* x, int P, int C, float eps, float momentum, int first, float* mean,
                            float* std_, float* invstd, float* run_mean, float* run_std, void* ws, size_t ws_bytes,
                            void* stream) {
+  const int nblk = bn_blocks(P, C);
+  if (ws_bytes < bn_fold_offset(P, C) + dk_bn_partials_workspace_bytes(nblk, C)) return DK_ERR_WORKSPACE;
   int rc = dk_bn_stats_partial_f64(x, P, C, ws, ws_bytes, stream);
   if (rc) return rc;
-  return dk_bn_stats_finalize_f32(ws, bn_blocks(P, C), C, (double)P, eps, momentum, first, mean, std_, invstd,
-                                  run_mean, run_std, stream);
+  return dk_bn_stats_from_partials_f32(ws, nblk, C, (double)P, eps, momentum, first, mean, std_, invstd, run_mean,
+                                       run_std, static_cast<char*>(ws) + bn_fold_offset(P, C),
+                                       ws_bytes - bn_fold_offset(P, C), stream);
+}
+
+// Workspace of dk_bn_stats_f32: the partials plus their fold rows.
+DK_API size_t dk_bn_stats_workspace_bytes(int P, int C) {
+  return bn_fold_offset(P, C) + dk_bn_partials_workspace_bytes(bn_blocks(P, C), C);
 }
 
 // Statistics from partial sums written by a producer's epilogue (*_fwd_ex_f32): part[nblk][2][C].
 DK_API size_t dk_bn_partials_workspace_bytes(int nblk, int C) {
-  return (size_t)cdiv(nblk, kRowsPerBlock) * 2 * C * sizeof(double);
+  // fold levels: ceil(n / 256) rows each, until one block finishes
+  size_t rows = 0;
+  for (int n = nblk; n > kFoldRows; n = cdiv(n, kFoldRows)) rows += (size_t)cdiv(n, kFoldRows);
+  return (rows > 0 ? rows : 1) * 2 * C * sizeof(double);
 }
 
-// Fold part[nblk][2][C] to <= kRowsPerBlock rows in ws (fixed order); returns the row count.
-static int fold_partials(const double* part, int nblk, int C, double* ws, hipStream_t st, const double** out) {
-  *out = part;
-  if (nblk <= kRowsPerBlock) return nblk;
-  const int n2 = cdiv(nblk, kRowsPerBlock);
-  hipLaunchKernelGGL(bn_rows_reduce_kernel, dim3(n2, cdiv(C, 64)), dim3(256), 0, st, part, nblk, C, ws);
-  *out = ws;
-  return n2;
+// Fold part[nblk][2][C] (fixed order) and apply the stage-2 maths: one launch for <= 256 rows.
+static int fold_finalize(const double* part, int nblk, int C, double* ws, const FoldOut& o, hipStream_t st) {
+  const unsigned gy = (unsigned)cdiv(C, 64);
+  while (nblk > kFoldRows) {
+    const int n2 = cdiv(nblk, kFoldRows);
+    hipLaunchKernelGGL(bn_fold_kernel<false>, dim3(n2, gy), dim3(1024), 0, st, part, nblk, C, ws, o);
+    part = ws;
+    ws += (size_t)n2 * 2 * C;
+    nblk = n2;
+  }
+  hipLaunchKernelGGL(bn_fold_kernel<true>, dim3(1, gy), dim3(1024), 0, st, part, nblk, C, nullptr, o);
+  return launch_status();
 }
 
 DK_API int dk_bn_stats_from_partials_f32(const void* part, int nblk, int C, double count, float eps, float momentum,
                                          int first, float* mean, float* std_, float* invstd, float* run_mean,
                                          float* run_std, void* ws, size_t ws_bytes, void* stream) {
-  if (ws_bytes < dk_bn_partials_workspace_bytes(nblk, C)) return DK_ERR_WORKSPACE;
-  const double* p;
-  const int n = fold_partials(static_cast<const double*>(part), nblk, C, static_cast<double*>(ws),
-                              as_stream(stream), &p);
-  return dk_bn_stats_finalize_f32(p, n, C, count, eps, momentum, first, mean, std_, invstd, run_mean, run_std,
-                                  stream);
+  if (ws_bytes < dk_bn_partials_workspace_bytes(nblk, C) || nblk < 1) return DK_ERR_WORKSPACE;
+  FoldOut o{};
+  o.mode = 0;
+  o.count = count;
+  o.eps = eps;
+  o.momentum = momentum;
+  o.first = first;
+  o.mean = mean;
+  o.std_ = std_;
+  o.invstd = invstd;
+  o.run_mean = run_mean;
+  o.run_std = run_std;
+  return fold_finalize(static_cast<const double*>(part), nblk, C, static_cast<double*>(ws), o, as_stream(stream));
 }
 
 // out[2][C] = the column sums of part[nblk][2][C] (SyncBN: the vector each rank all-reduces).
 DK_API int dk_bn_reduce_partials_f64(const void* part, int nblk, int C, void* out, void* ws, size_t ws_bytes,
                                      void* stream) {
-  if (ws_bytes < dk_bn_partials_workspace_bytes(nblk, C)) return DK_ERR_WORKSPACE;
-  const double* p;
-  const int n = fold_partials(static_cast<const double*>(part), nblk, C, static_cast<double*>(ws),
-                              as_stream(stream), &p);
-  return dk_bn_collapse_f64(p, n, C, out, stream);
+  if (ws_bytes < dk_bn_partials_workspace_bytes(nblk, C) || nblk < 1) return DK_ERR_WORKSPACE;
+  FoldOut o{};
+  o.mode = 2;
+  o.sums = static_cast<double*>(out);
+  return fold_finalize(static_cast<const double*>(part), nblk, C, static_cast<double*>(ws), o, as_stream(stream));
 }
 
 DK_API int dk_bn_infer_params_f32(const float* run_std, int C, float* invstd, void* stream) {
@@ -632,11 +718,14 @@ DK_API int dk_relu_bwd_bn_partial_f64(const float* dy, const uint8_t* mask, cons
 // dgrad_ex epilogue, dk_relu_bwd_bn_partial_f64): fixed-order fold, then the finalize.
 DK_API int dk_bn_bwd_from_partials_f32(const void* part, int nblk, int C, double count, float* dgamma, float* dbeta,
                                        float* k12, void* ws, size_t ws_bytes, void* stream) {
-  if (ws_bytes < dk_bn_partials_workspace_bytes(nblk, C)) return DK_ERR_WORKSPACE;
-  const double* p;
-  const int n = fold_partials(static_cast<const double*>(part), nblk, C, static_cast<double*>(ws),
-                              as_stream(stream), &p);
-  return dk_bn_bwd_finalize_f32(p, n, p, n, C, count, dgamma, dbeta, k12, stream);
+  if (ws_bytes < dk_bn_partials_workspace_bytes(nblk, C) || nblk < 1) return DK_ERR_WORKSPACE;
+  FoldOut o{};
+  o.mode = 1;
+  o.count = count;
+  o.dgamma = dgamma;
+  o.dbeta = dbeta;
+  o.k12 = k12;
+  return fold_finalize(static_cast<const double*>(part), nblk, C, static_cast<double*>(ws), o, as_stream(stream));
 }
 
 // Backward stage 2: dgamma/dbeta from the local partials, k12 = [k1[C], k2[C]] from the global ones.
@@ -669,7 +758,7 @@ DK_API int dk_bn_bwd_apply_f32(const float* x, const float* dy, long long numel,
 }
 
 DK_API size_t dk_bn_bwd_workspace_bytes(int P, int C) {
-  return dk_bn_workspace_bytes(P, C) + 2 * (size_t)C * sizeof(float);
+  return bn_fold_offset(P, C) + 2 * (size_t)C * sizeof(float) + dk_bn_partials_workspace_bytes(bn_blocks(P, C), C);
 }
 
 // Backward (all stages, local statistics).  Writes dgamma/dbeta [C] and dx [P][C].
@@ -678,10 +767,13 @@ DK_API int dk_bn_bwd_f32(const float* x, const float* dy, int P, int C, const fl
                          void* ws, size_t ws_bytes, void* stream) {
   if (ws_bytes < dk_bn_bwd_workspace_bytes(P, C)) return DK_ERR_WORKSPACE;
   const int nblk = bn_blocks(P, C);
-  float* k12 = reinterpret_cast<float*>(static_cast<char*>(ws) + dk_bn_workspace_bytes(P, C));
+  char* base = static_cast<char*>(ws);
+  float* k12 = reinterpret_cast<float*>(base + bn_fold_offset(P, C));
+  const size_t fold_off = bn_fold_offset(P, C) + 2 * (size_t)C * sizeof(float);
   int rc = dk_bn_bwd_partial_f64(x, dy, P, C, mean, invstd, gamma, beta, relu, ws, ws_bytes, stream);
   if (rc) return rc;
-  rc = dk_bn_bwd_finalize_f32(ws, nblk, ws, nblk, C, (double)P, dgamma, dbeta, k12, stream);
+  rc = dk_bn_bwd_from_partials_f32(ws, nblk, C, (double)P, dgamma, dbeta, k12, base + fold_off, ws_bytes - fold_off,
+                                   stream);
   if (rc) return rc;
   return dk_bn_bwd_apply_f32(x, dy, (long long)P * C, C, mean, invstd, gamma, beta, relu, k12, dx, stream);
 }

@@ -42,6 +42,35 @@ __device__ __forceinline__ f32x4 bload4(__amdgpu_buffer_rsrc_t r, uint32_t off) 
   return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0));
 }
 
+// Per-thread filter taps for channels c..c+3: wl 0 = the [R][S][C] copy (dk_dw_weight_rsc_f32),
+// 1 = the reference layout W[C][R][S] read directly (4*R*S contiguous floats), 2 = W[C][R][S]
+// with the taps flipped (stride-1 dgrad).  No re-layout launch for layouts 1 and 2.
+template <int R, int S, int WL>
+__device__ __forceinline__ void load_dw_weights(f32x4 (&wv)[R][S], const float* __restrict__ w, int c, int C) {
+  if constexpr (WL == 0) {
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+      for (int s = 0; s < S; ++s) wv[r][s] = ld4(w + (r * S + s) * C + c);
+  } else {
+    constexpr int RS = R * S;
+    f32x4 f[RS];  // floats c*RS .. (c+4)*RS-1
+#pragma unroll
+    for (int i = 0; i < RS; ++i) f[i] = ld4(w + (size_t)c * RS + 4 * i);
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        const int tap = WL == 2 ? (R - 1 - r) * S + (S - 1 - s) : r * S + s;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int k = e * RS + tap;
+          wv[r][s][e] = f[k >> 2][k & 3];
+        }
+      }
+  }
+}
+
 // Outputs per thread along W: the input strip R x ((TW-1)*ST + S) float4s is loaded at once.
 template <int ST>
 struct DwTile {
@@ -85,7 +114,7 @@ __device__ __forceinline__ void load_strip(f32x4 (&strip)[R][NC], __amdgpu_buffe
 // STATS == 2 (this kernel computing a stride-1 dgrad): the BN-backward sums of the BatchNorm
 // whose output the layer consumed -- sum(g), sum(g * x_hat) with g = y masked by that BN's
 // fused ReLU (batch_norm.py:125-174, dk_bn_bwd_partial_f64); xo is that BN's raw input.
-template <int R, int S, int ST, bool BN, int STATS>
+template <int R, int S, int ST, bool BN, int STATS, int WL>
 __global__ __launch_bounds__(256) void dw_fwd_kernel(const float* __restrict__ x, uint32_t xbytes,
                                                      const float* __restrict__ wt, const float* __restrict__ bias,
                                                      float* __restrict__ y, int N, int H, int W, int C, int OH, int OW,
@@ -112,10 +141,7 @@ __global__ __launch_bounds__(256) void dw_fwd_kernel(const float* __restrict__ x
     f32x4 strip[R][NC];
     load_strip<R, NC, BN>(strip, make_rsrc(x, xbytes), n, oh * ST - pad, ow0 * ST - pad, H, W, C, c, bn);
     f32x4 wv[R][S];
-#pragma unroll
-    for (int r = 0; r < R; ++r)
-#pragma unroll
-      for (int s = 0; s < S; ++s) wv[r][s] = ld4(wt + (r * S + s) * C + c);
+    load_dw_weights<R, S, WL>(wv, wt, c, C);
     const f32x4 b0 = bias ? ld4(bias + c) : f32x4{0.f, 0.f, 0.f, 0.f};
     float* yrow = y + ((size_t)(n * OH + oh) * OW) * C + c;
     f32x4 om, oi, og, ob;
@@ -212,10 +238,7 @@ __global__ __launch_bounds__(256) void dw_dgrad_subpixel_kernel(const float* __r
     }
   }
   f32x4 wv[R][S];
-#pragma unroll
-  for (int r = 0; r < R; ++r)
-#pragma unroll
-    for (int s = 0; s < S; ++s) wv[r][s] = ld4(wt + (r * S + s) * C + c);
+  load_dw_weights<R, S, 1>(wv, wt, c, C);  // wt = W[C][R][S]
 #pragma unroll
   for (int q = 0; q < TWQ; ++q) {
     f32x4 acc[ST][ST];
@@ -376,43 +399,48 @@ static long long dw_fwd_threads(int N, int OH, int OW, int C) {
 }
 
 // part: per-block sums (mode 1: output statistics; mode 2 with xo/obn: BN-backward sums).
+// wl: weight layout (load_dw_weights).  Only the combinations the entry points use exist.
 template <int R, int S, int ST>
-static void launch_dw_fwd(const float* x, const float* wt, const float* bias, float* y, int N, int H, int W, int C,
-                          int OH, int OW, int pad, const BnIn& bn, double* part, const float* xo, const BnIn& obn,
-                          hipStream_t st) {
+static int launch_dw_fwd(const float* x, const float* wt, const float* bias, float* y, int N, int H, int W, int C,
+                         int OH, int OW, int pad, const BnIn& bn, double* part, const float* xo, const BnIn& obn,
+                         int wl, hipStream_t st) {
   const uint32_t xb = (uint32_t)((size_t)N * H * W * C * sizeof(float));
   const dim3 grid((unsigned)cdivll(dw_fwd_threads<ST>(N, OH, OW, C), 256));
-#define DW_LAUNCH(B, ST_)                                                                                            \
-  hipLaunchKernelGGL((dw_fwd_kernel<R, S, ST, B, ST_>), grid, dim3(256), 0, st, x, xb, wt, bias, y, N, H, W, C, OH, \
-                     OW, pad, bn, part, xo, obn)
+#define DW_LAUNCH(B, ST_, WL_)                                                                                        \
+  hipLaunchKernelGGL((dw_fwd_kernel<R, S, ST, B, ST_, WL_>), grid, dim3(256), 0, st, x, xb, wt, bias, y, N, H, W, C, \
+                     OH, OW, pad, bn, part, xo, obn)
   const int mode = part ? (xo ? 2 : 1) : 0;
-  if (bn.mean) {
-    if (mode == 1)
-      DW_LAUNCH(true, 1);
-    else if (mode == 0)
-      DW_LAUNCH(true, 0);
-  } else {
-    if (mode == 2)
-      DW_LAUNCH(false, 2);
-    else if (mode == 1)
-      DW_LAUNCH(false, 1);
-    else
-      DW_LAUNCH(false, 0);
-  }
+  if (wl == 0 && !bn.mean && mode == 0)
+    DW_LAUNCH(false, 0, 0);
+  else if (wl == 0 && bn.mean && mode == 0)
+    DW_LAUNCH(true, 0, 0);
+  else if (wl == 1 && bn.mean && mode == 1)
+    DW_LAUNCH(true, 1, 1);
+  else if (wl == 1 && bn.mean && mode == 0)
+    DW_LAUNCH(true, 0, 1);
+  else if (wl == 1 && !bn.mean && mode == 1)
+    DW_LAUNCH(false, 1, 1);
+  else if (wl == 1 && !bn.mean && mode == 0)
+    DW_LAUNCH(false, 0, 1);
+  else if (wl == 2 && !bn.mean && mode == 0)
+    DW_LAUNCH(false, 0, 2);
+  else if (wl == 2 && !bn.mean && mode == 2)
+    DW_LAUNCH(false, 2, 2);
+  else
+    return DK_ERR_ARGS;
 #undef DW_LAUNCH
+  return launch_status();
 }
 
 static int dw_fwd_dispatch(const float* x, const float* wt, const float* bias, float* y, int N, int H, int W, int C,
                            int R, int S, int stride, int OH, int OW, int pad, const BnIn& bn, hipStream_t st,
-                           double* part = nullptr, const float* xo = nullptr, const BnIn& obn = BnIn{}) {
+                           double* part = nullptr, const float* xo = nullptr, const BnIn& obn = BnIn{}, int wl = 0) {
   if (C % 4 || !aligned16(x) || !aligned16(wt) || !fits((size_t)N * H * W * C * 4) || !bn_ok(bn)) return DK_ERR_ARGS;
   if (part && (C / 4 > 256 || 256 % (C / 4))) return DK_ERR_ARGS;
   if (xo && (bn.mean || !obn.mean || !aligned16(xo) || !bn_ok(obn))) return DK_ERR_ARGS;
 #define DW_CASE(RR, SS, STR)                                                                     \
-  if (R == RR && S == SS && stride == STR) {                                                     \
-    launch_dw_fwd<RR, SS, STR>(x, wt, bias, y, N, H, W, C, OH, OW, pad, bn, part, xo, obn, st);  \
-    return launch_status();                                                                      \
-  }
+  if (R == RR && S == SS && stride == STR)                                                           \
+    return launch_dw_fwd<RR, SS, STR>(x, wt, bias, y, N, H, W, C, OH, OW, pad, bn, part, xo, obn, wl, st);
   DW_CASE(3, 3, 1)
   DW_CASE(3, 3, 2)
   DW_CASE(5, 5, 1)
@@ -460,13 +488,15 @@ DK_API int dk_dwconv_fwd_stats_rows(int N, int OH, int OW, int C, int stride) {
   return (int)cdivll(thr, 256);
 }
 
-DK_API int dk_dwconv_fwd_ex_f32(const float* x, int N, int H, int W, int C, const float* w_rsc, int R, int S,
+// Reads the filters in the reference layout W[C][R][S] (no re-layout copy).
+DK_API int dk_dwconv_fwd_ex_f32(const float* x, int N, int H, int W, int C, const float* w_crs, int R, int S,
                                 int stride, int pad, const float* bias, float* y, int OH, int OW,
                                 const float* bn_mean, const float* bn_invstd, const float* bn_gamma,
                                 const float* bn_beta, int bn_relu, double* stats, void* stream) {
   if (stride != 1 && stride != 2) return DK_ERR_ARGS;
-  return dw_fwd_dispatch(x, w_rsc, bias, y, N, H, W, C, R, S, stride, OH, OW, pad,
-                         BnIn{bn_mean, bn_invstd, bn_gamma, bn_beta, bn_relu}, as_stream(stream), stats);
+  return dw_fwd_dispatch(x, w_crs, bias, y, N, H, W, C, R, S, stride, OH, OW, pad,
+                         BnIn{bn_mean, bn_invstd, bn_gamma, bn_beta, bn_relu}, as_stream(stream), stats, nullptr,
+                         BnIn{}, 1);
 }
 
 // w_rsc is the (unflipped) [R][S][C] copy; stride-1 dgrad flips it internally into ws.
@@ -480,28 +510,26 @@ DK_API int dk_dwconv_dgrad_f32(const float* dy, int N, int OH, int OW, int C, co
   float* wt = static_cast<float*>(ws);
   const hipStream_t st = as_stream(stream);
   if (stride == 1 && pad <= R - 1 && pad <= S - 1 && R == S) {
-    // dx = correlation of dy with the flipped filter, padding R-1-pad, stride 1
-    hipLaunchKernelGGL(dw_weight_rsc_kernel, dim3(cdiv(C * R * S, 256)), dim3(256), 0, st, w_crs, C, R, S, 1, wt);
-    int rc = launch_status();
-    if (rc) return rc;
-    return dw_fwd_dispatch(dy, wt, nullptr, dx, N, OH, OW, C, R, S, 1, H, W, R - 1 - pad, BnIn{}, st);
+    // dx = correlation of dy with the flipped filter (read flipped from W[C][R][S]), padding R-1-pad
+    return dw_fwd_dispatch(dy, w_crs, nullptr, dx, N, OH, OW, C, R, S, 1, H, W, R - 1 - pad, BnIn{}, st, nullptr,
+                           nullptr, BnIn{}, 2);
   }
-  hipLaunchKernelGGL(dw_weight_rsc_kernel, dim3(cdiv(C * R * S, 256)), dim3(256), 0, st, w_crs, C, R, S, 0, wt);
-  int rc = launch_status();
-  if (rc) return rc;
-  if (!fits((size_t)N * OH * OW * C * 4) || !aligned16(dy) || !aligned16(dx)) return DK_ERR_ARGS;
+  if (!fits((size_t)N * OH * OW * C * 4) || !aligned16(dy) || !aligned16(dx) || !aligned16(w_crs)) return DK_ERR_ARGS;
   const uint32_t gb = (uint32_t)((size_t)N * OH * OW * C * 4);
 #define DW_SUBPIX(RR, SS, STR, PD)                                                                                   \
   if (R == RR && S == SS && stride == STR && pad == PD) {                                                            \
     const long long items = (long long)N * cdiv(H, STR) * cdiv(cdiv(W, STR), 4) * (C / 4);                         \
     hipLaunchKernelGGL((dw_dgrad_subpixel_kernel<RR, SS, STR, PD>), dim3((unsigned)cdivll(items, 256)), dim3(256), 0, \
-                       st, dy, gb, wt, dx, N, H, W, C, OH, OW);                                                      \
+                       st, dy, gb, w_crs, dx, N, H, W, C, OH, OW);                                                   \
     return launch_status();                                                                                          \
   }
   DW_SUBPIX(3, 3, 2, 1)
   DW_SUBPIX(5, 5, 2, 2)
   DW_SUBPIX(1, 1, 2, 0)
 #undef DW_SUBPIX
+  hipLaunchKernelGGL(dw_weight_rsc_kernel, dim3(cdiv(C * R * S, 256)), dim3(256), 0, st, w_crs, C, R, S, 0, wt);
+  int rc = launch_status();
+  if (rc) return rc;
   const long long total = (long long)N * H * W * (C / 4);
   const dim3 grid((unsigned)cdivll(total, 256));
   if (R == 3 && S == 3)
@@ -536,13 +564,9 @@ DK_API int dk_dwconv_dgrad_ex_f32(const float* dy, int N, int OH, int OW, int C,
   if (!(stride == 1 && pad <= R - 1 && pad <= S - 1 && R == S) || !part || !bn_x ||
       dk_dwconv_dgrad_stats_rows(N, H, W, C, 1) == 0)
     return DK_ERR_ARGS;
-  float* wt = static_cast<float*>(ws);
   const hipStream_t st = as_stream(stream);
-  hipLaunchKernelGGL(dw_weight_rsc_kernel, dim3(cdiv(C * R * S, 256)), dim3(256), 0, st, w_crs, C, R, S, 1, wt);
-  int rc = launch_status();
-  if (rc) return rc;
-  return dw_fwd_dispatch(dy, wt, nullptr, dx, N, OH, OW, C, R, S, 1, H, W, R - 1 - pad, BnIn{}, st, part, bn_x,
-                         BnIn{bn_mean, bn_invstd, bn_gamma, bn_beta, bn_relu});
+  return dw_fwd_dispatch(dy, w_crs, nullptr, dx, N, OH, OW, C, R, S, 1, H, W, R - 1 - pad, BnIn{}, st, part, bn_x,
+                         BnIn{bn_mean, bn_invstd, bn_gamma, bn_beta, bn_relu}, 2);
 }
 
 DK_API size_t dk_dwconv_wgrad_workspace_bytes(int N, int OH, int OW, int C, int R, int S) {

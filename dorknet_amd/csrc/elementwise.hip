@@ -139,36 +139,38 @@ __global__ void gap_bwd_kernel(const float* __restrict__ dy, int N, int HW, int 
 
 // p = e^x / sum e^x per row (no max subtraction, losses.py:15-16);
 // loss = mean_b -log(sum_j p[b][j] * y[b][j])  (losses.py:23-26).  One block.
-__global__ __launch_bounds__(256) void softmax_xent_fwd_kernel(const float* __restrict__ x,
-                                                               const float* __restrict__ y, int B, int K,
-                                                               float* __restrict__ p, float* __restrict__ loss) {
-  __shared__ double red[256];
+__global__ __launch_bounds__(1024) void softmax_xent_fwd_kernel(const float* __restrict__ x,
+                                                                const float* __restrict__ y, int B, int K,
+                                                                float* __restrict__ p, float* __restrict__ loss) {
+  // one wave per row (rows w, w + 16, ...); per-wave fp64 loss sums combined in a fixed order
+  __shared__ double red[16];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   double acc = 0.0;
-  for (int b = threadIdx.x; b < B; b += 256) {
+  for (int b = wv; b < B; b += 16) {
     const float* xr = x + (size_t)b * K;
     float* pr = p + (size_t)b * K;
     float s = 0.f;
-    for (int j = 0; j < K; ++j) {
-      const float e = expf(xr[j]);
-      pr[j] = e;
-      s += e;
-    }
+    for (int j = lane; j < K; j += 64) s += expf(xr[j]);
+    s = wave_sum(s);
     const float inv = 1.0f / s;
     float dot = 0.f;
-    for (int j = 0; j < K; ++j) {
-      const float v = inv * pr[j];
+    for (int j = lane; j < K; j += 64) {
+      const float v = inv * expf(xr[j]);
       pr[j] = v;
       if (y) dot += v * y[(size_t)b * K + j];
     }
-    if (y) acc += (double)(-logf(dot));
+    if (y) {
+      dot = wave_sum(dot);
+      acc += (double)(-logf(dot));
+    }
   }
-  red[threadIdx.x] = acc;
+  if (lane == 0) red[wv] = acc;
   __syncthreads();
-  for (int o = 128; o > 0; o >>= 1) {
-    if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
-    __syncthreads();
+  if (threadIdx.x == 0 && loss) {
+    double t = 0.0;
+    for (int w = 0; w < 16; ++w) t += red[w];
+    *loss = (float)((1.0 / (double)B) * t);
   }
-  if (threadIdx.x == 0 && loss) *loss = (float)((1.0 / (double)B) * red[0]);
 }
 
 // dx = (1/B) * (p - y)   (losses.py:29-34)
@@ -405,7 +407,7 @@ DK_API int dk_gap_bwd_f32(const float* dy, int N, int HW, int C, float* dx, void
 
 DK_API int dk_softmax_xent_fwd_f32(const float* x, const float* y_onehot, int B, int K, float* p, float* loss,
                                    void* stream) {
-  hipLaunchKernelGGL(softmax_xent_fwd_kernel, dim3(1), dim3(256), 0, as_stream(stream), x, y_onehot, B, K, p, loss);
+  hipLaunchKernelGGL(softmax_xent_fwd_kernel, dim3(1), dim3(1024), 0, as_stream(stream), x, y_onehot, B, K, p, loss);
   return launch_status();
 }
 

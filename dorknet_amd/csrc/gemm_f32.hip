@@ -366,14 +366,26 @@ struct LdImgIC : ICLayout<ROWS, BK> {
 // Epilogues
 // ----------------------------------------------------------------------------
 
+// The kernel stages its accumulator tile through LDS and hands every thread 16-byte row
+// chunks: put4(m, n, v) covers columns n..n+3 (all < N; only when the epilogue's v4 flag
+// says the destination allows 16-byte stores), put1 a single column otherwise.  Epilogues
+// with kColStats also fold a per-column reduction of what they store into a[e] / b[e].
+
 // out[m][n] = acc (+ bias[n]).
 struct EpStore {
   static constexpr bool kColStats = false;
   float* out;
   int ldo;
   const float* bias;
-  __device__ __forceinline__ float value(int n, float v) const { return bias ? v + bias[n] : v; }
-  __device__ __forceinline__ void put(int m, int n, float v, int) const { out[(size_t)m * ldo + n] = value(n, v); }
+  int v4;  // out, ldo and bias allow 16-byte access
+  __device__ __forceinline__ f32x4 value4(int n, f32x4 v) const { return bias ? v + ld4(bias + n) : v; }
+  __device__ __forceinline__ float value1(int n, float v) const { return bias ? v + bias[n] : v; }
+  __device__ __forceinline__ void put4(int m, int n, f32x4 v, int, double*, double*) const {
+    st4(out + (size_t)m * ldo + n, value4(n, v));
+  }
+  __device__ __forceinline__ void put1(int m, int n, float v, int, double&, double&) const {
+    out[(size_t)m * ldo + n] = value1(n, v);
+  }
 };
 
 // EpStore + the BatchNorm statistics of the stored output (layers/batch_norm.py:76-80's
@@ -383,22 +395,38 @@ struct EpStore {
 struct EpStoreStats : EpStore {
   static constexpr bool kColStats = true;
   double* part;
-  __device__ __forceinline__ void contrib(int, int n, float v, double& a, double& b) const {
-    a = (double)value(n, v);
-    b = a * a;
+  __device__ __forceinline__ void put4(int m, int n, f32x4 v, int, double* a, double* b) const {
+    const f32x4 o = value4(n, v);
+    st4(out + (size_t)m * ldo + n, o);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const double d = (double)o[e];
+      a[e] += d;
+      b[e] += d * d;
+    }
+  }
+  __device__ __forceinline__ void put1(int m, int n, float v, int, double& a, double& b) const {
+    const float o = value1(n, v);
+    out[(size_t)m * ldo + n] = o;
+    a += (double)o;
+    b += (double)o * (double)o;
   }
 };
 
 // The BatchNorm-backward reduction of the layer whose input gradient this GEMM produces
 // (batch_norm.py:125-174's sum(dy) and sum(dy * x_hat), with the fused ReLU's mask
 // recomputed from the BN's raw input x as in dk_bn_bwd_partial_f64): part[m_tile][2][N].
-// `pix(m)` maps the GEMM row to the pixel of x (identity, or the widened lattice point).
-__device__ __forceinline__ void bn_bwd_contrib(float g, float x, const BnIn& bn, int n, double& a, double& b) {
-  const float mu = bn.mean[n], is = bn.invstd[n];
+__device__ __forceinline__ void bn_bwd_contrib(float g, float x, float mu, float is, float ga, float be, int relu,
+                                               double& a, double& b) {
   const float xh = (x - mu) * is;
-  if (bn.relu && !(bn_out(x, mu, is, bn.gamma[n], bn.beta[n]) > 0.f)) g = 0.f;
-  a = (double)g;
-  b = (double)g * (double)xh;
+  if (relu && !(bn_out(x, mu, is, ga, be) > 0.f)) g = 0.f;
+  a += (double)g;
+  b += (double)g * (double)xh;
+}
+__device__ __forceinline__ void bn_bwd_contrib4(f32x4 g, f32x4 x, const BnIn& bn, int n, double* a, double* b) {
+  const f32x4 mu = ld4(bn.mean + n), is = ld4(bn.invstd + n), ga = ld4(bn.gamma + n), be = ld4(bn.beta + n);
+#pragma unroll
+  for (int e = 0; e < 4; ++e) bn_bwd_contrib(g[e], x[e], mu[e], is[e], ga[e], be[e], bn.relu, a[e], b[e]);
 }
 
 struct EpStoreBnBwd : EpStore {
@@ -406,8 +434,13 @@ struct EpStoreBnBwd : EpStore {
   double* part;
   const float* xbn;  // [M][ldo], the BN's raw input
   BnIn bn;
-  __device__ __forceinline__ void contrib(int m, int n, float v, double& a, double& b) const {
-    bn_bwd_contrib(v, xbn[(size_t)m * ldo + n], bn, n, a, b);
+  __device__ __forceinline__ void put4(int m, int n, f32x4 v, int, double* a, double* b) const {
+    st4(out + (size_t)m * ldo + n, v);
+    bn_bwd_contrib4(v, ld4(xbn + (size_t)m * ldo + n), bn, n, a, b);
+  }
+  __device__ __forceinline__ void put1(int m, int n, float v, int, double& a, double& b) const {
+    out[(size_t)m * ldo + n] = v;
+    bn_bwd_contrib(v, xbn[(size_t)m * ldo + n], bn.mean[n], bn.invstd[n], bn.gamma[n], bn.beta[n], bn.relu, a, b);
   }
 };
 
@@ -419,15 +452,26 @@ struct EpWiden {
   float* out;
   int ldo;
   int OH, OW, st;
-  __device__ __forceinline__ void put(int m, int n, float v, int) const {
+  int v4;
+  __device__ __forceinline__ size_t cell(int m) const {
     const int ow = m % OW;
     const int t = m / OW;
     const int oh = t % OH;
     const int b = t / OH;
-    const int OW2 = OW * st, OH2 = OH * st;
-    const size_t cell = (size_t)(b * OH2 + oh * st) * OW2 + (size_t)ow * st;
+    return (size_t)(b * OH * st + oh * st) * (OW * st) + (size_t)ow * st;
+  }
+  __device__ __forceinline__ void put4(int m, int n, f32x4 v, int, double*, double*) const {
+    const size_t c0 = cell(m);
+    const size_t W2 = (size_t)OW * st;
     for (int dy = 0; dy < st; ++dy)
-      for (int dx = 0; dx < st; ++dx) out[(cell + (size_t)dy * OW2 + dx) * ldo + n] = (dy | dx) ? 0.f : v;
+      for (int dx = 0; dx < st; ++dx)
+        st4(out + (c0 + dy * W2 + dx) * ldo + n, (dy | dx) ? f32x4{0.f, 0.f, 0.f, 0.f} : v);
+  }
+  __device__ __forceinline__ void put1(int m, int n, float v, int, double&, double&) const {
+    const size_t c0 = cell(m);
+    const size_t W2 = (size_t)OW * st;
+    for (int dy = 0; dy < st; ++dy)
+      for (int dx = 0; dx < st; ++dx) out[(c0 + dy * W2 + dx) * ldo + n] = (dy | dx) ? 0.f : v;
   }
 };
 
@@ -438,13 +482,13 @@ struct EpWidenBnBwd : EpWiden {
   double* part;
   const float* xbn;  // the BN's raw input on the widened grid
   BnIn bn;
-  __device__ __forceinline__ void contrib(int m, int n, float v, double& a, double& b) const {
-    const int ow = m % OW;
-    const int t = m / OW;
-    const int oh = t % OH;
-    const int bb = t / OH;
-    const size_t px = (size_t)(bb * OH * st + oh * st) * (OW * st) + (size_t)ow * st;
-    bn_bwd_contrib(v, xbn[px * ldo + n], bn, n, a, b);
+  __device__ __forceinline__ void put4(int m, int n, f32x4 v, int sp, double* a, double* b) const {
+    EpWiden::put4(m, n, v, sp, a, b);
+    bn_bwd_contrib4(v, ld4(xbn + cell(m) * ldo + n), bn, n, a, b);
+  }
+  __device__ __forceinline__ void put1(int m, int n, float v, int sp, double& a, double& b) const {
+    EpWiden::put1(m, n, v, sp, a, b);
+    bn_bwd_contrib(v, xbn[cell(m) * ldo + n], bn.mean[n], bn.invstd[n], bn.gamma[n], bn.beta[n], bn.relu, a, b);
   }
 };
 
@@ -453,7 +497,11 @@ struct EpPartial {
   static constexpr bool kColStats = false;
   float* ws;
   int M, N;
-  __device__ __forceinline__ void put(int m, int n, float v, int split) const {
+  int v4;
+  __device__ __forceinline__ void put4(int m, int n, f32x4 v, int split, double*, double*) const {
+    st4(ws + ((size_t)split * M + m) * N + n, v);
+  }
+  __device__ __forceinline__ void put1(int m, int n, float v, int split, double&, double&) const {
     ws[((size_t)split * M + m) * N + n] = v;
   }
 };
@@ -470,7 +518,14 @@ __global__ __launch_bounds__(64 * WM * WN) void igemm_f32(DA da, DB db, EP ep, i
   static_assert(TM >= 1 && TN >= 1 && BM == 32 * WM * TM && BN == 32 * WN * TN, "tile");
   static_assert(BK % 8 == 0, "BK");
   constexpr int ABUF = LA::BUF, BBUF = LB::BUF;
-  __shared__ float smem[2 * (ABUF + BBUF)];
+  // operand double buffers; the epilogue reuses the same LDS for the staged C tile
+  // ([BM][BN+8]) and, with kColStats, the fp64 column-sum scratch
+  constexpr int SMEM_OPS = 2 * (ABUF + BBUF);
+  constexpr int SMEM_EPI = BM * (BN + 8);
+  constexpr int SMEM_RED = EP::kColStats ? (64 * WM * WN / (BN / 4)) * BN * 4 : 0;
+  constexpr int SMEM = SMEM_OPS > SMEM_EPI ? (SMEM_OPS > SMEM_RED ? SMEM_OPS : SMEM_RED)
+                                           : (SMEM_EPI > SMEM_RED ? SMEM_EPI : SMEM_RED);
+  __shared__ float smem[SMEM];
   float* const As = smem;
   float* const Bs = smem + 2 * ABUF;
 
@@ -548,66 +603,80 @@ __global__ __launch_bounds__(64 * WM * WN) void igemm_f32(DA da, DB db, EP ep, i
     }
   }
 
+  // Epilogue: the accumulator tile goes through LDS ([BM][BN+8]; the +8 puts the two lane
+  // halves' rows 4 apart on opposite bank halves) so that each thread stores 16-byte row
+  // chunks -- 4x fewer store instructions than storing the MFMA C layout directly.
+  constexpr int NT = 64 * WM * WN;
+  constexpr int LDT = BN + 8;
+  constexpr int NC4 = BN / 4;
+  constexpr int RSTEP = NT / NC4;
+  static_assert(NT % NC4 == 0, "epilogue thread map");
+  __syncthreads();  // the MFMA loop's last LDS reads are done
 #pragma unroll
   for (int t = 0; t < TM; ++t)
 #pragma unroll
-    for (int u = 0; u < TN; ++u) {
-      const int col = n0 + wn * 32 * TN + u * 32 + l32;
+    for (int u = 0; u < TN; ++u)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = m0 + wm * 32 * TM + t * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        if (row < M && col < N) ep.put(row, col, acc[t][u][r], blockIdx.y);
-      }
+      for (int r = 0; r < 16; ++r)
+        smem[(wm * 32 * TM + t * 32 + (r & 3) + 8 * (r >> 2) + 4 * h) * LDT + wn * 32 * TN + u * 32 + l32] =
+            acc[t][u][r];
+  __syncthreads();
+  const int c4 = tid % NC4, rl0 = tid / NC4;
+  const int col = n0 + 4 * c4;
+  const bool full = ep.v4 && col + 3 < N;
+  double sa[4] = {0.0, 0.0, 0.0, 0.0}, sb[4] = {0.0, 0.0, 0.0, 0.0};
+  for (int rl = rl0; rl < BM; rl += RSTEP) {
+    const int row = m0 + rl;
+    if (row >= M) break;
+    const f32x4 v = ld4(smem + rl * LDT + 4 * c4);
+    if (full) {
+      ep.put4(row, col, v, blockIdx.y, sa, sb);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (col + e < N) ep.put1(row, col + e, v[e], blockIdx.y, sa[e], sb[e]);
     }
+  }
 
   if constexpr (EP::kColStats) {
-    static_assert(WM * BN * 4 <= 2 * (ABUF + BBUF), "stats scratch fits the operand LDS");
-    // Column sums of ep.contrib (the stored values and their squares, or the BN-backward
-    // terms) over this tile's valid rows, fp64, fixed order:
-    // lane's 16*TM rows -> lane halves (h) -> waves along M (wm) -> part[m_tile][.][col].
-    __syncthreads();  // the MFMA loop's last LDS reads are done; reuse smem
-    double* red = reinterpret_cast<double*>(smem);  // [WM][BN][2]
+    // per-column fp64 sums of this tile, fixed order: the thread's rows, then the RSTEP
+    // threads sharing its column chunk -> part[m_tile][.][col]
+    __syncthreads();  // done reading the staged tile
+    double* red = reinterpret_cast<double*>(smem);  // [RSTEP][BN][2]
 #pragma unroll
-    for (int u = 0; u < TN; ++u) {
-      const int lcol = wn * 32 * TN + u * 32 + l32;
-      const int col = n0 + lcol;
-      double s1 = 0.0, s2 = 0.0;
-      if (col < N) {
-#pragma unroll
-        for (int t = 0; t < TM; ++t)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int row = m0 + wm * 32 * TM + t * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-            if (row < M) {
-              double a, b;
-              ep.contrib(row, col, acc[t][u][r], a, b);
-              s1 += a;
-              s2 += b;
-            }
-          }
-      }
-      const double o1 = __shfl_xor(s1, 32, 64), o2 = __shfl_xor(s2, 32, 64);
-      if (h == 0) {
-        red[(wm * BN + lcol) * 2 + 0] = s1 + o1;
-        red[(wm * BN + lcol) * 2 + 1] = s2 + o2;
-      }
+    for (int e = 0; e < 4; ++e) {
+      red[(rl0 * BN + 4 * c4 + e) * 2 + 0] = sa[e];
+      red[(rl0 * BN + 4 * c4 + e) * 2 + 1] = sb[e];
     }
     __syncthreads();
     const int mt = blockIdx.x / tiles_n;
-    for (int i = tid; i < BN; i += 64 * WM * WN) {
-      const int col = n0 + i;
-      if (col >= N) continue;
+    for (int i = tid; i < BN; i += NT) {
+      const int cc = n0 + i;
+      if (cc >= N) continue;
       double s1 = 0.0, s2 = 0.0;
-#pragma unroll
-      for (int w = 0; w < WM; ++w) {
-        s1 += red[(w * BN + i) * 2 + 0];
-        s2 += red[(w * BN + i) * 2 + 1];
+      for (int k = 0; k < RSTEP; ++k) {
+        s1 += red[(k * BN + i) * 2 + 0];
+        s2 += red[(k * BN + i) * 2 + 1];
       }
-      ep.part[((size_t)mt * 2 + 0) * N + col] = s1;
-      ep.part[((size_t)mt * 2 + 1) * N + col] = s2;
+      ep.part[((size_t)mt * 2 + 0) * N + cc] = s1;
+      ep.part[((size_t)mt * 2 + 1) * N + cc] = s2;
     }
   }
 }
+
+static inline int aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+// Buffer resources address < 2 GiB (32-bit offsets with kOOB as the out-of-range marker).
+static inline bool fits(size_t bytes) { return bytes < ((size_t)1 << 31); }
+
+static inline int al4(int v) { return (v & 3) == 0; }
+static inline EpStore ep_store(float* out, int ldo, const float* bias) {
+  return EpStore{out, ldo, bias, al4(ldo) && aligned16(out) && (!bias || aligned16(bias))};
+}
+static inline EpWiden ep_widen(float* out, int ldo, int OH, int OW, int st) {
+  return EpWiden{out, ldo, OH, OW, st, al4(ldo) && aligned16(out)};
+}
+
 
 // ----------------------------------------------------------------------------
 // Host-side launch helpers and tile selection
@@ -682,7 +751,7 @@ static int row_config(int M, int N, int K) {
   (void)N;
   // Measured on MI355X (scripts/gemm_tune.py, profiles/r01c_gemm_tune.md): 64x64 tiles win on
   // every ResNet shape; a deeper k-tile pays once the reduction is longer than ~100.
-  return K <= 96 ? 6 : 8;
+  return K <= 128 ? 6 : 8;
 }
 
 // Output-stationary problems (fwd / dgrad).
@@ -725,7 +794,7 @@ static int igemm_splitk(const DA& da, const DB& db, float* ws, int M, int N, int
   if (id < 0 || id >= kNumSplitCfg) return DK_ERR_ARGS;
   const int splits = wgrad_splits(M, N, Kred, kSplitCfg[id]);
   *splits_out = splits;
-  EpPartial ep{ws, M, N};
+  EpPartial ep{ws, M, N, al4(N) && aligned16(ws)};
   switch (id) {
 #define DK_CASE(cid, bm, bn, bk, wm, wn) \
   case cid:                              \
@@ -804,11 +873,6 @@ __global__ void col2im_kernel(const float* __restrict__ cols, int N, int C, int 
   dx[idx] = acc;
 }
 
-static inline int aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
-
-// Buffer resources address < 2 GiB (32-bit offsets with kOOB as the out-of-range marker).
-static inline bool fits(size_t bytes) { return bytes < ((size_t)1 << 31); }
-
 // rows x ld matrix; ext = extent of the non-reduction index (rows for a K-contiguous
 // operand, valid columns for a row-contiguous one).
 static inline MatDesc mat(const float* p, int rows, int ld, int ext) {
@@ -876,13 +940,11 @@ static int conv_fwd(const D& a, const float* w_krsc, int K, int Ktot, const floa
   MatDesc b = mat(w_krsc, K, Ktot, K);
   if (stats) {
     EpStoreStats ep;
-    ep.out = y;
-    ep.ldo = K;
-    ep.bias = bias;
+    static_cast<EpStore&>(ep) = ep_store(y, K, bias);
     ep.part = stats;
     return igemm_rows<LdImgKC, D, LdMatKC, MatDesc, EpStoreStats>(a, b, ep, a.M, K, Ktot, as_stream(stream));
   }
-  EpStore ep{y, K, bias};
+  EpStore ep = ep_store(y, K, bias);
   return igemm_rows<LdImgKC, D, LdMatKC, MatDesc, EpStore>(a, b, ep, a.M, K, Ktot, as_stream(stream));
 }
 
@@ -941,7 +1003,7 @@ DK_API int dk_conv2d_dgrad_f32(const float* dy, int N, int OH, int OW, int K, co
   ImgDesc a = img(dy, N, OH, OW, K, H, W, R, S, 1, -1, pad, N * H * W);
   const int Ktot = R * S * K;
   MatDesc b = mat(w_crsk, C, Ktot, C);
-  EpStore ep{dx, C, nullptr};
+  EpStore ep = ep_store(dx, C, nullptr);
   return igemm_rows<LdImgKC, ImgDesc, LdMatKC, MatDesc, EpStore>(a, b, ep, N * H * W, C, Ktot, as_stream(stream));
 }
 
@@ -960,7 +1022,7 @@ DK_API int dk_conv2d_dgrad_strided_f32(const float* dy, int N, int OH, int OW, i
   float* cols = static_cast<float*>(ws);
   MatDesc a = mat(dy, M, K, M);
   MatDesc b = mat(w_kcrs, K, CRS, CRS);
-  EpStore ep{cols, CRS, nullptr};
+  EpStore ep = ep_store(cols, CRS, nullptr);
   const hipStream_t st = as_stream(stream);
   int rc;
   const bool va = vec_ok(a, K, 4), vb = vec_ok(b, 4, CRS);
@@ -1027,7 +1089,7 @@ DK_API int dk_pwconv_fwd_f32(const float* x, int N, int H, int W, int C, const f
                              const float* bias, float* y, int OH, int OW, void* stream) {
   if (!fits((size_t)N * H * W * C * 4)) return DK_ERR_ARGS;
   MatDesc b = mat(w_kc, K, C, K);
-  EpStore ep{y, K, bias};
+  EpStore ep = ep_store(y, K, bias);
   if (C % 4 || !aligned16(x) || !aligned16(w_kc)) {
     // Unaligned channel count: scalar loads, stride 1 only (the rows are then a plain matrix).
     if (stride != 1) return DK_ERR_ARGS;
@@ -1071,11 +1133,11 @@ DK_API int dk_pwconv_dgrad_f32(const float* dy, int N, int OH, int OW, int K, co
   const hipStream_t st = as_stream(stream);
   const bool vec = vec_ok(a, K, 4) && vec_ok(b, 4, C);
   if (stride == 1) {
-    EpStore ep{dx, C, nullptr};
+    EpStore ep = ep_store(dx, C, nullptr);
     if (vec) return igemm_rows<LdMatKC, MatDesc, LdMatIC, MatDesc, EpStore>(a, b, ep, M, C, K, st);
     return igemm_rows<LdMatKC1, MatDesc, LdMatIC1, MatDesc, EpStore>(a, b, ep, M, C, K, st);
   }
-  EpWiden ep{dx, C, OH, OW, stride};
+  EpWiden ep = ep_widen(dx, C, OH, OW, stride);
   if (vec) return igemm_rows<LdMatKC, MatDesc, LdMatIC, MatDesc, EpWiden>(a, b, ep, M, C, K, st);
   return igemm_rows<LdMatKC1, MatDesc, LdMatIC1, MatDesc, EpWiden>(a, b, ep, M, C, K, st);
 }
@@ -1096,11 +1158,11 @@ DK_API int dk_pwconv_dgrad_ex_f32(const float* dy, int N, int OH, int OW, int K,
   const hipStream_t st = as_stream(stream);
   const bool vec = vec_ok(a, K, 4) && vec_ok(b, 4, C);
   const BnIn bn{bn_mean, bn_invstd, bn_gamma, bn_beta, bn_relu};
+  const int xv4 = aligned16(bn_x) && bn_ok(bn_mean, bn_invstd, bn_gamma, bn_beta);
   if (stride == 1) {
     EpStoreBnBwd ep;
-    ep.out = dx;
-    ep.ldo = C;
-    ep.bias = nullptr;
+    static_cast<EpStore&>(ep) = ep_store(dx, C, nullptr);
+    ep.v4 = ep.v4 && xv4;
     ep.part = part;
     ep.xbn = bn_x;
     ep.bn = bn;
@@ -1108,11 +1170,8 @@ DK_API int dk_pwconv_dgrad_ex_f32(const float* dy, int N, int OH, int OW, int K,
     return igemm_rows<LdMatKC1, MatDesc, LdMatIC1, MatDesc, EpStoreBnBwd>(a, b, ep, M, C, K, st);
   }
   EpWidenBnBwd ep;
-  ep.out = dx;
-  ep.ldo = C;
-  ep.OH = OH;
-  ep.OW = OW;
-  ep.st = stride;
+  static_cast<EpWiden&>(ep) = ep_widen(dx, C, OH, OW, stride);
+  ep.v4 = ep.v4 && xv4;
   ep.part = part;
   ep.xbn = bn_x;
   ep.bn = bn;
@@ -1150,7 +1209,7 @@ DK_API int dk_dense_fwd_f32(const float* x, int B, int IN, const float* w_io, in
                             void* stream) {
   MatDesc a = mat(x, B, IN, B);
   MatDesc b = mat(w_io, IN, OUT, OUT);
-  EpStore ep{y, OUT, bias};
+  EpStore ep = ep_store(y, OUT, bias);
   const hipStream_t st = as_stream(stream);
   const bool va = vec_ok(a, IN, 4), vb = vec_ok(b, 4, OUT);
   if (va && vb) return igemm_rows<LdMatKC, MatDesc, LdMatIC, MatDesc, EpStore>(a, b, ep, B, OUT, IN, st);
@@ -1161,7 +1220,7 @@ DK_API int dk_dense_fwd_f32(const float* x, int B, int IN, const float* w_io, in
 DK_API int dk_dense_dgrad_f32(const float* dy, int B, int OUT, const float* w_io, int IN, float* dx, void* stream) {
   MatDesc a = mat(dy, B, OUT, B);
   MatDesc b = mat(w_io, IN, OUT, IN);
-  EpStore ep{dx, IN, nullptr};
+  EpStore ep = ep_store(dx, IN, nullptr);
   const hipStream_t st = as_stream(stream);
   if (vec_ok(a, OUT, 4) && vec_ok(b, OUT, 4))
     return igemm_rows<LdMatKC, MatDesc, LdMatKC, MatDesc, EpStore>(a, b, ep, B, IN, OUT, st);

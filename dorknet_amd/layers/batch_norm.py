@@ -103,7 +103,7 @@ class BatchNormLayer(Layer):
             nb = lib.dk_bn_partials_workspace_bytes(partials.rows, C)
             ws = workspace.get(nb)
         else:
-            nb = lib.dk_bn_workspace_bytes(P, C)
+            nb = lib.dk_bn_stats_workspace_bytes(P, C)
             ws = workspace.get(nb)
         if self.sync_group is None:
             if partials is not None:

@@ -83,15 +83,12 @@ class DepthwiseConvLayer(Layer):
             rows = lib.dk_dwconv_fwd_stats_rows(N, OH, OW, C, self.stride)
             if rows:
                 stats = torch.empty((rows, 2, C), dtype=torch.float64, device=x.device)
-        if bn is not None or stats is not None:
-            lib.dk_dwconv_fwd_ex_f32(x.data_ptr(), N, H, W, C, self._w_rsc(st).data_ptr(), R, S, self.stride,
-                                     self.padding, ptr(bias), y.data_ptr(), OH, OW,
-                                     *(bn.bn_args() if bn is not None else (0, 0, 0, 0, 0)), ptr(stats), st)
-            if stats is not None:
-                bn_stats.part, bn_stats.rows = stats, stats.shape[0]
-        else:
-            lib.dk_dwconv_fwd_f32(x.data_ptr(), N, H, W, C, self._w_rsc(st).data_ptr(), R, S, self.stride,
-                                  self.padding, ptr(bias), y.data_ptr(), OH, OW, st)
+        w = self.learned_params["weights"]  # W[C][R][S], read in place by the _ex entry
+        lib.dk_dwconv_fwd_ex_f32(x.data_ptr(), N, H, W, C, w.data_ptr(), R, S, self.stride, self.padding, ptr(bias),
+                                 y.data_ptr(), OH, OW, *(bn.bn_args() if bn is not None else (0, 0, 0, 0, 0)),
+                                 ptr(stats), st)
+        if stats is not None:
+            bn_stats.part, bn_stats.rows = stats, stats.shape[0]
         if not test_mode:
             # the reference keeps the *padded* input (:87-88); padding is implicit here, and
             # a BNOut input is kept as the BatchNorm's raw input + parameters

@@ -93,13 +93,14 @@ int dk_pwconv_wgrad_bnx_f32(const float* dy, const float* x, int N, int H, int W
  * output y (fp64 sum and sum of squares per output channel, per tile: stats[rows][2][K],
  * rows = the matching *_fwd_stats_rows()).  dk_bn_stats_from_partials_f32 turns them into
  * mean/std -- the separate statistics pass over y (batch_norm.py:76-80) disappears.
- * dk_dwconv_fwd_stats_rows returns 0 when C/4 does not divide 256 (no statistics variant). */
+ * dk_dwconv_fwd_stats_rows returns 0 when C/4 does not divide 256 (no statistics variant).
+ * dk_dwconv_fwd_ex_f32 takes the filters in the reference layout W[C][R][S] (no re-layout). */
 int dk_conv2d_fwd_stats_rows(int N, int OH, int OW, int K, int C, int R, int S);
 int dk_conv2d_fwd_ex_f32(const float* x, int N, int H, int W, int C, const float* w_krsc, int K, int R, int S, int stride, int pad, const float* bias, float* y, int OH, int OW, const float* bn_mean, const float* bn_invstd, const float* bn_gamma, const float* bn_beta, int bn_relu, double* stats, void* stream);
 int dk_pwconv_fwd_stats_rows(int N, int OH, int OW, int K, int C);
 int dk_pwconv_fwd_ex_f32(const float* x, int N, int H, int W, int C, const float* w_kc, int K, int stride, const float* bias, float* y, int OH, int OW, const float* bn_mean, const float* bn_invstd, const float* bn_gamma, const float* bn_beta, int bn_relu, double* stats, void* stream);
 int dk_dwconv_fwd_stats_rows(int N, int OH, int OW, int C, int stride);
-int dk_dwconv_fwd_ex_f32(const float* x, int N, int H, int W, int C, const float* w_rsc, int R, int S, int stride, int pad, const float* bias, float* y, int OH, int OW, const float* bn_mean, const float* bn_invstd, const float* bn_gamma, const float* bn_beta, int bn_relu, double* stats, void* stream);
+int dk_dwconv_fwd_ex_f32(const float* x, int N, int H, int W, int C, const float* w_crs, int R, int S, int stride, int pad, const float* bias, float* y, int OH, int OW, const float* bn_mean, const float* bn_invstd, const float* bn_gamma, const float* bn_beta, int bn_relu, double* stats, void* stream);
 /* Backward side: *_dgrad_ex_f32 = the input gradient plus stage 1 of the backward of the
  * BatchNorm whose output this layer consumed (the BN-on-load input of its forward): with
  * g = dx masked by that BN's fused ReLU (recomputed from bn_x, the BN's raw input, laid out
@@ -153,6 +154,7 @@ size_t dk_bn_bwd_workspace_bytes(int P, int C);
 int dk_bn_stats_partial_f64(const float* x, int P, int C, void* ws, size_t ws_bytes, void* stream);
 int dk_bn_collapse_f64(const void* part, int nblk, int C, void* out, void* stream);
 int dk_bn_stats_finalize_f32(const void* part, int nblk, int C, double count, float eps, float momentum, int first, float* mean, float* std_, float* invstd, float* run_mean, float* run_std, void* stream);
+size_t dk_bn_stats_workspace_bytes(int P, int C);
 int dk_bn_stats_f32(const float* x, int P, int C, float eps, float momentum, int first, float* mean, float* std_, float* invstd, float* run_mean, float* run_std, void* ws, size_t ws_bytes, void* stream);
 /* Statistics from a producer's partial sums (stats of *_fwd_ex_f32): fixed-order fold of
  * part[nblk][2][C] (workspace: dk_bn_partials_workspace_bytes) then the finalize above;

@@ -90,7 +90,7 @@ def main():
             y = torch.empty(P * C, device="cuda")
             p = bnp(C)
             mean, std, invstd, rm, rs = [torch.empty(C, device="cuda") for _ in range(5)]
-            nb = lib.dk_bn_workspace_bytes(P, C)
+            nb = lib.dk_bn_stats_workspace_bytes(P, C)
             sa = (x.data_ptr(), P, C, 1e-5, 0.95, 1, mean.data_ptr(), std.data_ptr(), invstd.data_ptr(), rm.data_ptr(),
                   rs.data_ptr(), workspace.get(nb), nb, st)
             report(name + " stats", timeit(lambda: lib.dk_bn_stats_f32(*sa)), "dk_bn_stats_f32", sa)

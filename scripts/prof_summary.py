@@ -39,7 +39,7 @@ def main():
     print("| kernel | calls | total us | avg us | % |" + (" us/step |" if a.steps else ""))
     print("|---|---:|---:|---:|---:|" + ("---:|" if a.steps else ""))
     for name, calls, tot, avg, pct in rows[:a.top]:
-        short = name.split("(")[0].replace("void ", "")
+        short = name.replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "")
         if len(short) > 110:
             short = short[:107] + "..."
         line = "| `{}` | {} | {:.1f} | {:.2f} | {:.2f} |".format(short, calls, tot, avg, 100 * tot / total)

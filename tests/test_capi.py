@@ -47,7 +47,10 @@ def test_library_loads_and_host_queries_work():
     nblk = lib.dk_bn_partial_blocks(802816, 64)
     assert 1 <= nblk <= 1024
     assert lib.dk_bn_workspace_bytes(802816, 64) == nblk * 2 * 64 * 8
-    assert lib.dk_bn_bwd_workspace_bytes(802816, 64) == nblk * 2 * 64 * 8 + 2 * 64 * 4
+    fold = lib.dk_bn_partials_workspace_bytes(nblk, 64)   # the fold rows of the fixed-order reduction
+    assert fold == -(-nblk // 256) * 2 * 64 * 8
+    assert lib.dk_bn_bwd_workspace_bytes(802816, 64) == nblk * 2 * 64 * 8 + 2 * 64 * 4 + fold
+    assert lib.dk_bn_stats_workspace_bytes(802816, 64) == nblk * 2 * 64 * 8 + fold
     assert lib.dk_colsum_workspace_bytes(1000, 10) >= 8 * 10
     assert lib.dk_l2_multi_workspace_bytes(100) == 800
     # argument errors are reported without touching the device

@@ -163,7 +163,7 @@ def _stats_pair(y, part, rows, C):
                                               std.data_ptr(), invstd.data_ptr(), rm.data_ptr(), rs.data_ptr(),
                                               workspace.get(nb), nb, st)
         else:
-            nb = lib.dk_bn_workspace_bytes(P, C)
+            nb = lib.dk_bn_stats_workspace_bytes(P, C)
             lib.dk_bn_stats_f32(y.data_ptr(), P, C, 1e-5, 0.95, 1, mean.data_ptr(), std.data_ptr(),
                                 invstd.data_ptr(), rm.data_ptr(), rs.data_ptr(), workspace.get(nb), nb, st)
         out.append((mean, std))
