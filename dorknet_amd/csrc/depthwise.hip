@@ -124,7 +124,8 @@ __global__ __launch_bounds__(256) void dw_fwd_kernel(const float* __restrict__ x
   constexpr int NC = (TW - 1) * ST + S;
   const int C4 = C >> 2;
   const int nwc = (OW + TW - 1) / TW;
-  const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  // XCD-contiguous block order: the output rows sharing input rows share an L2
+  const long long idx = (long long)xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
   const long long total = (long long)N * OH * nwc * C4;
   const bool live = idx < total;
   if (STATS == 0 && !live) return;

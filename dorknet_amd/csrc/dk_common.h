@@ -72,6 +72,14 @@ __device__ __forceinline__ f32x4 bn_in4(f32x4 v, f32x4 m, f32x4 is, f32x4 g, f32
   return o;
 }
 
+// XCD-aware block order.  Consecutive hardware block ids are dealt round-robin over the 8
+// XCDs, each with its own L2; this bijective remap gives every XCD a contiguous range of
+// logical blocks, so neighbouring tiles that share input rows (convolution halos) share an L2.
+__device__ __forceinline__ int xcd_block(int b, int n) {
+  const int q = n >> 3, r = n & 7, x = b & 7, i = b >> 3;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + i;
+}
+
 // Sub-pixel decomposition of a stride-ST correlation's input gradient (conv_subpixel.hip,
 // depthwise.hip): with h = ST*i + a, tap r reaches dx row h iff a == phase(r), and then
 // reads dy row i + nb(r).  dmin/dmax bound the dy neighbourhood of one ST x ST "quad".

@@ -536,8 +536,9 @@ __global__ __launch_bounds__(64 * WM * WN) void igemm_f32(DA da, DB db, EP ep, i
   const int l32 = lane & 31, h = lane >> 5;
 
   const int tiles_n = (N + BN - 1) / BN;
-  const int m0 = (blockIdx.x / tiles_n) * BM;
-  const int n0 = (blockIdx.x % tiles_n) * BN;
+  const int bid = xcd_block(blockIdx.x, gridDim.x);  // neighbouring M-tiles share an XCD's L2
+  const int m0 = (bid / tiles_n) * BM;
+  const int n0 = (bid % tiles_n) * BN;
   const int KT = (Ktot + BK - 1) / BK;
   const int kt0 = blockIdx.y * kt_per_split;
   const int kt1 = min(KT, kt0 + kt_per_split);
@@ -649,7 +650,7 @@ __global__ __launch_bounds__(64 * WM * WN) void igemm_f32(DA da, DB db, EP ep, i
       red[(rl0 * BN + 4 * c4 + e) * 2 + 1] = sb[e];
     }
     __syncthreads();
-    const int mt = blockIdx.x / tiles_n;
+    const int mt = bid / tiles_n;
     for (int i = tid; i < BN; i += NT) {
       const int cc = n0 + i;
       if (cc >= N) continue;

@@ -114,6 +114,13 @@ def main():
             report(name + " fwd", timeit(lambda: lib.dk_pwconv_fwd_f32(*fa)), "dk_pwconv_fwd_f32", fa)
             fb = fa[:-1] + tuple(t.data_ptr() for t in p) + (1, st)
             report(name + " fwd bnx", timeit(lambda: lib.dk_pwconv_fwd_bnx_f32(*fb)), "dk_pwconv_fwd_bnx_f32", fb)
+            rows = lib.dk_pwconv_fwd_stats_rows(B, OH, OH, K, C)
+            part = torch.empty(rows * 2 * K, dtype=torch.float64, device="cuda")
+            fe = fa[:-1] + (0, 0, 0, 0, 0, part.data_ptr(), st)
+            report(name + " fwd stats", timeit(lambda: lib.dk_pwconv_fwd_ex_f32(*fe)), "dk_pwconv_fwd_ex_f32", fe)
+            fe2 = fa[:-1] + tuple(t.data_ptr() for t in p) + (1, part.data_ptr(), st)
+            report(name + " fwd bnx+stats", timeit(lambda: lib.dk_pwconv_fwd_ex_f32(*fe2)), "dk_pwconv_fwd_ex_f32",
+                   fe2)
             dw = torch.empty(K * C, device="cuda")
             nb = lib.dk_pwconv_wgrad_workspace_bytes(B, OH, OH, K, C)
             wa = (dy.data_ptr(), x.data_ptr(), B, H, H, C, K, s, OH, OH, 0, 0.0, dw.data_ptr(), workspace.get(nb), nb,
