@@ -44,9 +44,13 @@ __global__ __launch_bounds__(256) void conv_dgrad_subpixel_kernel(const float* _
 
   const int tid = threadIdx.x;
   const int li = tid >> 6, lj = tid & 63;
-  const int i0 = blockIdx.y * kTI, j0 = blockIdx.x * kTJ;
-  const int n = blockIdx.z / ncg;
-  const int cg = blockIdx.z - n * ncg;
+  // XCD-contiguous block order (vertically adjacent tiles share dy halo rows)
+  const int lin = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+  const int L = xcd_block(lin, gridDim.x * gridDim.y * gridDim.z);
+  const int bx = L % gridDim.x, by = (L / gridDim.x) % gridDim.y, bz = L / (gridDim.x * gridDim.y);
+  const int i0 = by * kTI, j0 = bx * kTJ;
+  const int n = bz / ncg;
+  const int cg = bz - n * ncg;
   const float* dyn = dy + (size_t)n * OH * OW * K;
   const bool vec = (K & 3) == 0 && (reinterpret_cast<uintptr_t>(dy) & 15) == 0;
   const float* wcg = wt + (size_t)cg * KP * (R * S * CO * 2);

@@ -216,7 +216,7 @@ __global__ __launch_bounds__(256) void dw_dgrad_subpixel_kernel(const float* __r
   const int C4 = C >> 2;
   const int QH = (H + ST - 1) / ST, QW = (W + ST - 1) / ST;
   const int nqc = (QW + TWQ - 1) / TWQ;
-  const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long idx = (long long)xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
   if (idx >= (long long)N * QH * nqc * C4) return;
   const int cq = (int)(idx % C4);
   long long t = idx / C4;
@@ -310,6 +310,29 @@ struct DwWgTile {
   static constexpr int TW = ST == 1 ? 4 : 2;
 };
 
+// One input row of a strip: NC float4s at (ih, iw0 ..), BN-on-load applied, padding 0.
+template <int NC, bool BN>
+__device__ __forceinline__ void load_row(f32x4 (&row)[NC], __amdgpu_buffer_rsrc_t rs, int n, int ih, int iw0, int H,
+                                         int W, int C, int c, const BnIn& bn, f32x4 bm, f32x4 bi, f32x4 bg,
+                                         f32x4 bb) {
+  const bool rv = (unsigned)ih < (unsigned)H;
+#pragma unroll
+  for (int q = 0; q < NC; ++q) {
+    const int iw = iw0 + q;
+    const bool ok = rv && (unsigned)iw < (unsigned)W;
+    row[q] = bload4(rs, ok ? (uint32_t)(((n * H + ih) * W + iw) * C + c) * 4u : kOOB);
+    if constexpr (BN) {
+      const f32x4 t = bn_in4(row[q], bm, bi, bg, bb, bn.relu);
+      row[q] = ok ? t : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  }
+}
+
+// Items of the weight-gradient walk: (n, column chunk of TW outputs, segment of kWgSeg output
+// rows).  Down a segment the R-row input window slides by ST rows per output row, so each
+// output row loads ST new input rows instead of R.
+constexpr int kWgSeg = 8;
+
 template <int R, int S, int ST, bool BN>
 __global__ __launch_bounds__(256) void dw_wgrad_partial_kernel(const float* __restrict__ dy, uint32_t dybytes,
                                                                const float* __restrict__ x, uint32_t xbytes,
@@ -328,9 +351,18 @@ __global__ __launch_bounds__(256) void dw_wgrad_partial_kernel(const float* __re
   const bool active = pl < PL && cq < C4;
   const int c = cq * 4;
   const int nwc = (OW + TW - 1) / TW;
-  const int items = N * OH * nwc;
+  const int nseg = (OH + kWgSeg - 1) / kWgSeg;
+  const int items = N * nseg * nwc;
   const int i0 = blockIdx.x * ipb, i1 = min(items, i0 + ipb);
   const __amdgpu_buffer_rsrc_t rx = make_rsrc(x, xbytes), rg = make_rsrc(dy, dybytes);
+  f32x4 bm, bi, bg, bb;
+  if constexpr (BN) {
+    const int cc = active ? c : 0;
+    bm = ld4(bn.mean + cc);
+    bi = ld4(bn.invstd + cc);
+    bg = ld4(bn.gamma + cc);
+    bb = ld4(bn.beta + cc);
+  }
   f32x4 acc[R][S];
 #pragma unroll
   for (int r = 0; r < R; ++r)
@@ -340,21 +372,37 @@ __global__ __launch_bounds__(256) void dw_wgrad_partial_kernel(const float* __re
     for (int it = i0 + pl; it < i1; it += PL) {
       const int wc = it % nwc;
       const int t = it / nwc;
-      const int oh = t % OH;
-      const int n = t / OH;
+      const int sg = t % nseg;
+      const int n = t / nseg;
       const int ow0 = wc * TW;
-      f32x4 g[TW];
+      const int iw0 = ow0 * ST - pad;
+      const int oh0 = sg * kWgSeg, oh1 = min(OH, oh0 + kWgSeg);
+      f32x4 win[R][NC];
 #pragma unroll
-      for (int j = 0; j < TW; ++j)
-        g[j] = bload4(rg, ow0 + j < OW ? (uint32_t)(((n * OH + oh) * OW + ow0 + j) * C + c) * 4u : kOOB);
-      f32x4 strip[R][NC];
-      load_strip<R, NC, BN>(strip, rx, n, oh * ST - pad, ow0 * ST - pad, H, W, C, c, bn);
+      for (int r = 0; r < R; ++r) load_row<NC, BN>(win[r], rx, n, oh0 * ST - pad + r, iw0, H, W, C, c, bn, bm, bi, bg, bb);
+      for (int oh = oh0; oh < oh1; ++oh) {
+        if (oh > oh0) {
 #pragma unroll
-      for (int j = 0; j < TW; ++j)
+          for (int r = 0; r < R; ++r) {
+            if (r + ST < R) {
 #pragma unroll
-        for (int r = 0; r < R; ++r)
+              for (int q = 0; q < NC; ++q) win[r][q] = win[r + ST][q];
+            } else {
+              load_row<NC, BN>(win[r], rx, n, oh * ST - pad + r, iw0, H, W, C, c, bn, bm, bi, bg, bb);
+            }
+          }
+        }
+        f32x4 g[TW];
 #pragma unroll
-          for (int s = 0; s < S; ++s) acc[r][s] += g[j] * strip[r][j * ST + s];
+        for (int j = 0; j < TW; ++j)
+          g[j] = bload4(rg, ow0 + j < OW ? (uint32_t)(((n * OH + oh) * OW + ow0 + j) * C + c) * 4u : kOOB);
+#pragma unroll
+        for (int j = 0; j < TW; ++j)
+#pragma unroll
+          for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int s = 0; s < S; ++s) acc[r][s] += g[j] * win[r][j * ST + s];
+      }
     }
   }
 #pragma unroll
@@ -590,7 +638,7 @@ static int dw_wgrad(const float* dy, const float* x, int N, int H, int W, int C,
   const uint32_t xb = (uint32_t)((size_t)N * H * W * C * 4), gb = (uint32_t)((size_t)N * OH * OW * C * 4);
 #define DW_WG_LAUNCH(RR, SS, STR, B)                                                                                 \
   {                                                                                                                  \
-    const int items = N * OH * ((OW + DwWgTile<STR>::TW - 1) / DwWgTile<STR>::TW);                                   \
+    const int items = N * cdiv(OH, kWgSeg) * ((OW + DwWgTile<STR>::TW - 1) / DwWgTile<STR>::TW);                     \
     const int ipb = cdiv(items, nblk);                                                                               \
     if (shm > 65536)                                                                                                 \
       (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&dw_wgrad_partial_kernel<RR, SS, STR, B>),             \
