@@ -71,39 +71,30 @@ __device__ __forceinline__ void load_dw_weights(f32x4 (&wv)[R][S], const float* 
   }
 }
 
+// One input row of a strip: NC float4s at (ih, iw0 ..), BN-on-load applied, padding 0.
+template <int NC, bool BN>
+__device__ __forceinline__ void load_row(f32x4 (&row)[NC], __amdgpu_buffer_rsrc_t rs, int n, int ih, int iw0, int H,
+                                         int W, int C, int c, const BnIn& bn, f32x4 bm, f32x4 bi, f32x4 bg,
+                                         f32x4 bb) {
+  const bool rv = (unsigned)ih < (unsigned)H;
+#pragma unroll
+  for (int q = 0; q < NC; ++q) {
+    const int iw = iw0 + q;
+    const bool ok = rv && (unsigned)iw < (unsigned)W;
+    row[q] = bload4(rs, ok ? (uint32_t)(((n * H + ih) * W + iw) * C + c) * 4u : kOOB);
+    if constexpr (BN) {
+      const f32x4 t = bn_in4(row[q], bm, bi, bg, bb, bn.relu);
+      row[q] = ok ? t : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  }
+}
+
 // Outputs per thread along W: the input strip R x ((TW-1)*ST + S) float4s is loaded at once.
 template <int ST>
 struct DwTile {
-  static constexpr int TW = ST == 1 ? 8 : 4;
+  static constexpr int TW = 4;    // outputs per thread along W
+  static constexpr int SEG = 8;   // output rows per thread (the input window slides down)
 };
-
-// Loads the R x NC input strip whose top-left tap is (ih0, iw0); with BN, every in-image
-// element is replaced by bn(x) (+ReLU) -- padding stays 0.
-template <int R, int NC, bool BN>
-__device__ __forceinline__ void load_strip(f32x4 (&strip)[R][NC], __amdgpu_buffer_rsrc_t rs, int n, int ih0, int iw0,
-                                           int H, int W, int C, int c, const BnIn& bn) {
-  bool ok[R][NC];
-#pragma unroll
-  for (int r = 0; r < R; ++r) {
-    const int ih = ih0 + r;
-#pragma unroll
-    for (int q = 0; q < NC; ++q) {
-      const int iw = iw0 + q;
-      ok[r][q] = (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
-      strip[r][q] = bload4(rs, ok[r][q] ? (uint32_t)(((n * H + ih) * W + iw) * C + c) * 4u : kOOB);
-    }
-  }
-  if constexpr (BN) {
-    const f32x4 m = ld4(bn.mean + c), is = ld4(bn.invstd + c), g = ld4(bn.gamma + c), b = ld4(bn.beta + c);
-#pragma unroll
-    for (int r = 0; r < R; ++r)
-#pragma unroll
-      for (int q = 0; q < NC; ++q) {
-        const f32x4 t = bn_in4(strip[r][q], m, is, g, b, bn.relu);
-        strip[r][q] = ok[r][q] ? t : f32x4{0.f, 0.f, 0.f, 0.f};
-      }
-  }
-}
 
 // y[n,oh,ow,c] = sum_{r,s} w[r][s][c] * x[n, oh*ST + r - pad, ow*ST + s - pad, c] (+ bias[c])
 // Thread = (n, oh, TW-wide chunk of ow, 4 channels); consecutive threads take consecutive
@@ -120,13 +111,14 @@ __global__ __launch_bounds__(256) void dw_fwd_kernel(const float* __restrict__ x
                                                      float* __restrict__ y, int N, int H, int W, int C, int OH, int OW,
                                                      int pad, BnIn bn, double* __restrict__ part,
                                                      const float* __restrict__ xo, BnIn obn) {
-  constexpr int TW = DwTile<ST>::TW;
+  constexpr int TW = DwTile<ST>::TW, SEG = DwTile<ST>::SEG;
   constexpr int NC = (TW - 1) * ST + S;
   const int C4 = C >> 2;
   const int nwc = (OW + TW - 1) / TW;
-  // XCD-contiguous block order: the output rows sharing input rows share an L2
+  const int nseg = (OH + SEG - 1) / SEG;
+  // XCD-contiguous block order: the row segments sharing input rows share an L2
   const long long idx = (long long)xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
-  const long long total = (long long)N * OH * nwc * C4;
+  const long long total = (long long)N * nseg * nwc * C4;
   const bool live = idx < total;
   if (STATS == 0 && !live) return;
   const int cq = (int)(idx % C4);
@@ -136,15 +128,22 @@ __global__ __launch_bounds__(256) void dw_fwd_kernel(const float* __restrict__ x
     long long t = idx / C4;
     const int wc = (int)(t % nwc);
     t /= nwc;
-    const int oh = (int)(t % OH);
-    const int n = (int)(t / OH);
+    const int sg = (int)(t % nseg);
+    const int n = (int)(t / nseg);
     const int ow0 = wc * TW;
-    f32x4 strip[R][NC];
-    load_strip<R, NC, BN>(strip, make_rsrc(x, xbytes), n, oh * ST - pad, ow0 * ST - pad, H, W, C, c, bn);
+    const int iw0 = ow0 * ST - pad;
+    const int oh0 = sg * SEG, oh1 = min(OH, oh0 + SEG);
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc(x, xbytes);
+    f32x4 bm, bi, bg, bb;
+    if constexpr (BN) {
+      bm = ld4(bn.mean + c);
+      bi = ld4(bn.invstd + c);
+      bg = ld4(bn.gamma + c);
+      bb = ld4(bn.beta + c);
+    }
     f32x4 wv[R][S];
     load_dw_weights<R, S, WL>(wv, wt, c, C);
     const f32x4 b0 = bias ? ld4(bias + c) : f32x4{0.f, 0.f, 0.f, 0.f};
-    float* yrow = y + ((size_t)(n * OH + oh) * OW) * C + c;
     f32x4 om, oi, og, ob;
     if constexpr (STATS == 2) {
       om = ld4(obn.mean + c);
@@ -152,31 +151,48 @@ __global__ __launch_bounds__(256) void dw_fwd_kernel(const float* __restrict__ x
       og = ld4(obn.gamma + c);
       ob = ld4(obn.beta + c);
     }
+    f32x4 win[R][NC];
 #pragma unroll
-    for (int j = 0; j < TW; ++j) {
-      f32x4 acc = b0;
+    for (int r = 0; r < R; ++r) load_row<NC, BN>(win[r], rs, n, oh0 * ST - pad + r, iw0, H, W, C, c, bn, bm, bi, bg, bb);
+    for (int oh = oh0; oh < oh1; ++oh) {
+      if (oh > oh0) {
 #pragma unroll
-      for (int r = 0; r < R; ++r)
+        for (int r = 0; r < R; ++r) {
+          if (r + ST < R) {
 #pragma unroll
-        for (int s = 0; s < S; ++s) acc += strip[r][j * ST + s] * wv[r][s];
-      if (ow0 + j < OW) {
-        st4(yrow + (size_t)(ow0 + j) * C, acc);
-        if constexpr (STATS == 1) {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const double v = (double)acc[e];
-            s1[e] += v;
-            s2[e] += v * v;
+            for (int q = 0; q < NC; ++q) win[r][q] = win[r + ST][q];
+          } else {
+            load_row<NC, BN>(win[r], rs, n, oh * ST - pad + r, iw0, H, W, C, c, bn, bm, bi, bg, bb);
           }
-        } else if constexpr (STATS == 2) {
-          const f32x4 xv = ld4(xo + ((size_t)(n * OH + oh) * OW + ow0 + j) * C + c);
+        }
+      }
+      float* yrow = y + ((size_t)(n * OH + oh) * OW) * C + c;
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            float g = acc[e];
-            const float xh = (xv[e] - om[e]) * oi[e];
-            if (obn.relu && !(bn_out(xv[e], om[e], oi[e], og[e], ob[e]) > 0.f)) g = 0.f;
-            s1[e] += (double)g;
-            s2[e] += (double)g * (double)xh;
+      for (int j = 0; j < TW; ++j) {
+        f32x4 acc = b0;
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+          for (int s = 0; s < S; ++s) acc += win[r][j * ST + s] * wv[r][s];
+        if (ow0 + j < OW) {
+          st4(yrow + (size_t)(ow0 + j) * C, acc);
+          if constexpr (STATS == 1) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const double v = (double)acc[e];
+              s1[e] += v;
+              s2[e] += v * v;
+            }
+          } else if constexpr (STATS == 2) {
+            const f32x4 xv = ld4(xo + ((size_t)(n * OH + oh) * OW + ow0 + j) * C + c);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              float g = acc[e];
+              const float xh = (xv[e] - om[e]) * oi[e];
+              if (obn.relu && !(bn_out(xv[e], om[e], oi[e], og[e], ob[e]) > 0.f)) g = 0.f;
+              s1[e] += (double)g;
+              s2[e] += (double)g * (double)xh;
+            }
           }
         }
       }
@@ -310,24 +326,6 @@ struct DwWgTile {
   static constexpr int TW = ST == 1 ? 4 : 2;
 };
 
-// One input row of a strip: NC float4s at (ih, iw0 ..), BN-on-load applied, padding 0.
-template <int NC, bool BN>
-__device__ __forceinline__ void load_row(f32x4 (&row)[NC], __amdgpu_buffer_rsrc_t rs, int n, int ih, int iw0, int H,
-                                         int W, int C, int c, const BnIn& bn, f32x4 bm, f32x4 bi, f32x4 bg,
-                                         f32x4 bb) {
-  const bool rv = (unsigned)ih < (unsigned)H;
-#pragma unroll
-  for (int q = 0; q < NC; ++q) {
-    const int iw = iw0 + q;
-    const bool ok = rv && (unsigned)iw < (unsigned)W;
-    row[q] = bload4(rs, ok ? (uint32_t)(((n * H + ih) * W + iw) * C + c) * 4u : kOOB);
-    if constexpr (BN) {
-      const f32x4 t = bn_in4(row[q], bm, bi, bg, bb, bn.relu);
-      row[q] = ok ? t : f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-  }
-}
-
 // Items of the weight-gradient walk: (n, column chunk of TW outputs, segment of kWgSeg output
 // rows).  Down a segment the R-row input window slides by ST rows per output row, so each
 // output row loads ST new input rows instead of R.
@@ -443,8 +441,8 @@ static inline bool bn_ok(const BnIn& bn) {
 
 template <int ST>
 static long long dw_fwd_threads(int N, int OH, int OW, int C) {
-  constexpr int TW = DwTile<ST>::TW;
-  return (long long)N * OH * ((OW + TW - 1) / TW) * (C / 4);
+  constexpr int TW = DwTile<ST>::TW, SEG = DwTile<ST>::SEG;
+  return (long long)N * ((OH + SEG - 1) / SEG) * ((OW + TW - 1) / TW) * (C / 4);
 }
 
 // part: per-block sums (mode 1: output statistics; mode 2 with xo/obn: BN-backward sums).
