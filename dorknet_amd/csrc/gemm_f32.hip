@@ -556,6 +556,8 @@ __global__ __launch_bounds__(64 * WM * WN) void igemm_f32(DA da, DB db, EP ep, i
     LB lb;
     la.init(da, m0, tid);
     lb.init(db, n0, tid);
+    la.load(da, kt0 * BK, Ktot);  // first tile in flight before anything else
+    lb.load(db, kt0 * BK, Ktot);
     if constexpr (DA::kBnIn && LA::kTable) {
       // BN-on-load parameter table for the A operand: {mean, invstd, gamma, beta} per channel
       extern __shared__ f32x4 bn_tab[];
@@ -564,8 +566,6 @@ __global__ __launch_bounds__(64 * WM * WN) void igemm_f32(DA da, DB db, EP ep, i
       la.tab = bn_tab;
       __syncthreads();
     }
-    la.load(da, kt0 * BK, Ktot);
-    lb.load(db, kt0 * BK, Ktot);
     la.template store<DA>(As);
     lb.template store<DB>(Bs);
     __syncthreads();
