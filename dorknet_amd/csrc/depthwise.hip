@@ -99,6 +99,8 @@ struct DwTile {
 // y[n,oh,ow,c] = sum_{r,s} w[r][s][c] * x[n, oh*ST + r - pad, ow*ST + s - pad, c] (+ bias[c])
 // Thread = (n, oh, TW-wide chunk of ow, 4 channels); consecutive threads take consecutive
 // channel groups, so a wave reads whole pixel rows.
+// res (optional, laid out like y): added to every output -- the residual join's other
+// gradient term when this kernel computes a dgrad (residual_block.py:94-97).
 // STATS: also a per-channel reduction of this block's outputs -> part[block][2][C]; needs
 // 256 % (C/4) == 0 so that a block covers every channel (thread tid always has channel group
 // tid % (C/4)).  STATS == 1: BatchNorm statistics of y (fp64 sum, sum of squares);
@@ -110,7 +112,8 @@ __global__ __launch_bounds__(256) void dw_fwd_kernel(const float* __restrict__ x
                                                      const float* __restrict__ wt, const float* __restrict__ bias,
                                                      float* __restrict__ y, int N, int H, int W, int C, int OH, int OW,
                                                      int pad, BnIn bn, double* __restrict__ part,
-                                                     const float* __restrict__ xo, BnIn obn) {
+                                                     const float* __restrict__ xo, BnIn obn,
+                                                     const float* __restrict__ res) {
   constexpr int TW = DwTile<ST>::TW, SEG = DwTile<ST>::SEG;
   constexpr int NC = (TW - 1) * ST + S;
   const int C4 = C >> 2;
@@ -155,6 +158,18 @@ __global__ __launch_bounds__(256) void dw_fwd_kernel(const float* __restrict__ x
 #pragma unroll
     for (int r = 0; r < R; ++r) load_row<NC, BN>(win[r], rs, n, oh0 * ST - pad + r, iw0, H, W, C, c, bn, bm, bi, bg, bb);
     for (int oh = oh0; oh < oh1; ++oh) {
+      // this row's residual / BN-input operands (dgrad only), issued ahead of the window
+      // loads and FMAs
+      const size_t pix0 = (size_t)(n * OH + oh) * OW + ow0;
+      f32x4 rv[TW], xv[TW];
+      if constexpr (WL == 2) {
+#pragma unroll
+        for (int j = 0; j < TW; ++j) {
+          const bool in = ow0 + j < OW;
+          rv[j] = (res && in) ? ld4(res + (pix0 + j) * C + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+          if constexpr (STATS == 2) xv[j] = in ? ld4(xo + (pix0 + j) * C + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+      }
       if (oh > oh0) {
 #pragma unroll
         for (int r = 0; r < R; ++r) {
@@ -175,6 +190,9 @@ __global__ __launch_bounds__(256) void dw_fwd_kernel(const float* __restrict__ x
 #pragma unroll
           for (int s = 0; s < S; ++s) acc += win[r][j * ST + s] * wv[r][s];
         if (ow0 + j < OW) {
+          if constexpr (WL == 2) {
+            if (res) acc += rv[j];  // residual addend
+          }
           st4(yrow + (size_t)(ow0 + j) * C, acc);
           if constexpr (STATS == 1) {
 #pragma unroll
@@ -184,12 +202,11 @@ __global__ __launch_bounds__(256) void dw_fwd_kernel(const float* __restrict__ x
               s2[e] += v * v;
             }
           } else if constexpr (STATS == 2) {
-            const f32x4 xv = ld4(xo + ((size_t)(n * OH + oh) * OW + ow0 + j) * C + c);
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
               float g = acc[e];
-              const float xh = (xv[e] - om[e]) * oi[e];
-              if (obn.relu && !(bn_out(xv[e], om[e], oi[e], og[e], ob[e]) > 0.f)) g = 0.f;
+              const float xh = (xv[j][e] - om[e]) * oi[e];
+              if (obn.relu && !(bn_out(xv[j][e], om[e], oi[e], og[e], ob[e]) > 0.f)) g = 0.f;
               s1[e] += (double)g;
               s2[e] += (double)g * (double)xh;
             }
@@ -222,7 +239,8 @@ __global__ __launch_bounds__(256) void dw_fwd_kernel(const float* __restrict__ x
 template <int R, int S, int ST, int PAD>
 __global__ __launch_bounds__(256) void dw_dgrad_subpixel_kernel(const float* __restrict__ dy, uint32_t dybytes,
                                                                 const float* __restrict__ wt, float* __restrict__ dx,
-                                                                int N, int H, int W, int C, int OH, int OW) {
+                                                                int N, int H, int W, int C, int OH, int OW,
+                                                                const float* __restrict__ res) {
   using RP = SubPix<R, ST, PAD>;
   using SP = SubPix<S, ST, PAD>;
   constexpr int DR0 = RP::dmin(), NR = RP::dmax() - RP::dmin() + 1;
@@ -258,24 +276,33 @@ __global__ __launch_bounds__(256) void dw_dgrad_subpixel_kernel(const float* __r
   load_dw_weights<R, S, 1>(wv, wt, c, C);  // wt = W[C][R][S]
 #pragma unroll
   for (int q = 0; q < TWQ; ++q) {
-    f32x4 acc[ST][ST];
+    const int j = j0 + q;
+    f32x4 acc[ST][ST], rv[ST][ST];
 #pragma unroll
     for (int a = 0; a < ST; ++a)
 #pragma unroll
-      for (int b = 0; b < ST; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int b = 0; b < ST; ++b) {
+        // residual addend loads issued ahead of the FMAs (added last: same rounding as dgrad + add)
+        const int h = qi * ST + a, w = j * ST + b;
+        rv[a][b] = (res && j < QW && h < H && w < W) ? ld4(res + (((size_t)n * H + h) * W + w) * C + c)
+                                                     : f32x4{0.f, 0.f, 0.f, 0.f};
+        acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
 #pragma unroll
     for (int r = 0; r < R; ++r)
 #pragma unroll
       for (int s = 0; s < S; ++s)
         acc[RP::phase(r)][SP::phase(s)] += d[RP::nb(r) - DR0][q + SP::nb(s) - DS0] * wv[r][s];
-    const int j = j0 + q;
 #pragma unroll
     for (int a = 0; a < ST; ++a) {
       const int h = qi * ST + a;
 #pragma unroll
       for (int b = 0; b < ST; ++b) {
         const int w = j * ST + b;
-        if (j < QW && h < H && w < W) st4(dx + (((size_t)n * H + h) * W + w) * C + c, acc[a][b]);
+        if (j < QW && h < H && w < W) {
+          const size_t off = (((size_t)n * H + h) * W + w) * C + c;
+          st4(dx + off, res ? acc[a][b] + rv[a][b] : acc[a][b]);
+        }
       }
     }
   }
@@ -450,12 +477,12 @@ static long long dw_fwd_threads(int N, int OH, int OW, int C) {
 template <int R, int S, int ST>
 static int launch_dw_fwd(const float* x, const float* wt, const float* bias, float* y, int N, int H, int W, int C,
                          int OH, int OW, int pad, const BnIn& bn, double* part, const float* xo, const BnIn& obn,
-                         int wl, hipStream_t st) {
+                         int wl, const float* res, hipStream_t st) {
   const uint32_t xb = (uint32_t)((size_t)N * H * W * C * sizeof(float));
   const dim3 grid((unsigned)cdivll(dw_fwd_threads<ST>(N, OH, OW, C), 256));
 #define DW_LAUNCH(B, ST_, WL_)                                                                                        \
   hipLaunchKernelGGL((dw_fwd_kernel<R, S, ST, B, ST_, WL_>), grid, dim3(256), 0, st, x, xb, wt, bias, y, N, H, W, C, \
-                     OH, OW, pad, bn, part, xo, obn)
+                     OH, OW, pad, bn, part, xo, obn, res)
   const int mode = part ? (xo ? 2 : 1) : 0;
   if (wl == 0 && !bn.mean && mode == 0)
     DW_LAUNCH(false, 0, 0);
@@ -481,13 +508,15 @@ static int launch_dw_fwd(const float* x, const float* wt, const float* bias, flo
 
 static int dw_fwd_dispatch(const float* x, const float* wt, const float* bias, float* y, int N, int H, int W, int C,
                            int R, int S, int stride, int OH, int OW, int pad, const BnIn& bn, hipStream_t st,
-                           double* part = nullptr, const float* xo = nullptr, const BnIn& obn = BnIn{}, int wl = 0) {
+                           double* part = nullptr, const float* xo = nullptr, const BnIn& obn = BnIn{}, int wl = 0,
+                           const float* res = nullptr) {
+  if (res && (!aligned16(res) || wl != 2)) return DK_ERR_ARGS;  // residual addend: dgrad only
   if (C % 4 || !aligned16(x) || !aligned16(wt) || !fits((size_t)N * H * W * C * 4) || !bn_ok(bn)) return DK_ERR_ARGS;
   if (part && (C / 4 > 256 || 256 % (C / 4))) return DK_ERR_ARGS;
   if (xo && (bn.mean || !obn.mean || !aligned16(xo) || !bn_ok(obn))) return DK_ERR_ARGS;
 #define DW_CASE(RR, SS, STR)                                                                     \
   if (R == RR && S == SS && stride == STR)                                                           \
-    return launch_dw_fwd<RR, SS, STR>(x, wt, bias, y, N, H, W, C, OH, OW, pad, bn, part, xo, obn, wl, st);
+    return launch_dw_fwd<RR, SS, STR>(x, wt, bias, y, N, H, W, C, OH, OW, pad, bn, part, xo, obn, wl, res, st);
   DW_CASE(3, 3, 1)
   DW_CASE(3, 3, 2)
   DW_CASE(5, 5, 1)
@@ -549,31 +578,38 @@ DK_API int dk_dwconv_fwd_ex_f32(const float* x, int N, int H, int W, int C, cons
 // w_rsc is the (unflipped) [R][S][C] copy; stride-1 dgrad flips it internally into ws.
 DK_API size_t dk_dwconv_dgrad_workspace_bytes(int C, int R, int S) { return (size_t)C * R * S * sizeof(float); }
 
-DK_API int dk_dwconv_dgrad_f32(const float* dy, int N, int OH, int OW, int C, const float* w_crs, int R, int S,
-                               int stride, int pad, float* dx, int H, int W, void* ws, size_t ws_bytes,
-                               void* stream) {
+// Input gradient.  res (optional): added to dx (the residual join's other gradient term);
+// bn_x/obn/part (optional, stride 1 only): + stage 1 of the backward of the BatchNorm whose
+// output the layer consumed.
+static int dw_dgrad(const float* dy, int N, int OH, int OW, int C, const float* w_crs, int R, int S, int stride,
+                    int pad, float* dx, int H, int W, void* ws, size_t ws_bytes, const float* res, const float* bn_x,
+                    const BnIn& obn, double* part, hipStream_t st) {
   if (C % 4) return DK_ERR_ARGS;
   if (ws_bytes < dk_dwconv_dgrad_workspace_bytes(C, R, S)) return DK_ERR_WORKSPACE;
   float* wt = static_cast<float*>(ws);
-  const hipStream_t st = as_stream(stream);
   if (stride == 1 && pad <= R - 1 && pad <= S - 1 && R == S) {
     // dx = correlation of dy with the flipped filter (read flipped from W[C][R][S]), padding R-1-pad
-    return dw_fwd_dispatch(dy, w_crs, nullptr, dx, N, OH, OW, C, R, S, 1, H, W, R - 1 - pad, BnIn{}, st, nullptr,
-                           nullptr, BnIn{}, 2);
+    if (part && dk_dwconv_fwd_stats_rows(N, H, W, C, 1) == 0) return DK_ERR_ARGS;
+    return dw_fwd_dispatch(dy, w_crs, nullptr, dx, N, OH, OW, C, R, S, 1, H, W, R - 1 - pad, BnIn{}, st,
+                           part ? part : nullptr, part ? bn_x : nullptr, part ? obn : BnIn{}, 2, res);
   }
-  if (!fits((size_t)N * OH * OW * C * 4) || !aligned16(dy) || !aligned16(dx) || !aligned16(w_crs)) return DK_ERR_ARGS;
+  if (part) return DK_ERR_ARGS;  // the BN-backward fusion covers stride-1 geometries only
+  if (!fits((size_t)N * OH * OW * C * 4) || !aligned16(dy) || !aligned16(dx) || !aligned16(w_crs) ||
+      (res && !aligned16(res)))
+    return DK_ERR_ARGS;
   const uint32_t gb = (uint32_t)((size_t)N * OH * OW * C * 4);
 #define DW_SUBPIX(RR, SS, STR, PD)                                                                                   \
   if (R == RR && S == SS && stride == STR && pad == PD) {                                                            \
     const long long items = (long long)N * cdiv(H, STR) * cdiv(cdiv(W, STR), 4) * (C / 4);                         \
     hipLaunchKernelGGL((dw_dgrad_subpixel_kernel<RR, SS, STR, PD>), dim3((unsigned)cdivll(items, 256)), dim3(256), 0, \
-                       st, dy, gb, w_crs, dx, N, H, W, C, OH, OW);                                                   \
+                       st, dy, gb, w_crs, dx, N, H, W, C, OH, OW, res);                                              \
     return launch_status();                                                                                          \
   }
   DW_SUBPIX(3, 3, 2, 1)
   DW_SUBPIX(5, 5, 2, 2)
   DW_SUBPIX(1, 1, 2, 0)
 #undef DW_SUBPIX
+  if (res) return DK_ERR_ARGS;  // generic gather path: no residual fusion
   hipLaunchKernelGGL(dw_weight_rsc_kernel, dim3(cdiv(C * R * S, 256)), dim3(256), 0, st, w_crs, C, R, S, 0, wt);
   int rc = launch_status();
   if (rc) return rc;
@@ -593,9 +629,13 @@ DK_API int dk_dwconv_dgrad_f32(const float* dy, int N, int OH, int OW, int C, co
   return launch_status();
 }
 
-// Stride-1 dgrad + the BN-backward partial sums of the BatchNorm whose output the layer
-// consumed (bn_x = its raw input, same shape as dx).  Returns DK_ERR_ARGS for geometries this
-// fusion does not cover (stride != 1, or dk_dwconv_dgrad_stats_rows() == 0).
+DK_API int dk_dwconv_dgrad_f32(const float* dy, int N, int OH, int OW, int C, const float* w_crs, int R, int S,
+                               int stride, int pad, float* dx, int H, int W, void* ws, size_t ws_bytes,
+                               void* stream) {
+  return dw_dgrad(dy, N, OH, OW, C, w_crs, R, S, stride, pad, dx, H, W, ws, ws_bytes, nullptr, nullptr, BnIn{},
+                  nullptr, as_stream(stream));
+}
+
 DK_API int dk_dwconv_dgrad_stats_rows(int N, int H, int W, int C, int stride) {
   if (stride != 1) return 0;
   return dk_dwconv_fwd_stats_rows(N, H, W, C, 1);
@@ -603,17 +643,12 @@ DK_API int dk_dwconv_dgrad_stats_rows(int N, int H, int W, int C, int stride) {
 
 DK_API int dk_dwconv_dgrad_ex_f32(const float* dy, int N, int OH, int OW, int C, const float* w_crs, int R, int S,
                                   int stride, int pad, float* dx, int H, int W, void* ws, size_t ws_bytes,
-                                  const float* bn_x, const float* bn_mean, const float* bn_invstd,
-                                  const float* bn_gamma, const float* bn_beta, int bn_relu, double* part,
-                                  void* stream) {
-  if (C % 4) return DK_ERR_ARGS;
-  if (ws_bytes < dk_dwconv_dgrad_workspace_bytes(C, R, S)) return DK_ERR_WORKSPACE;
-  if (!(stride == 1 && pad <= R - 1 && pad <= S - 1 && R == S) || !part || !bn_x ||
-      dk_dwconv_dgrad_stats_rows(N, H, W, C, 1) == 0)
-    return DK_ERR_ARGS;
-  const hipStream_t st = as_stream(stream);
-  return dw_fwd_dispatch(dy, w_crs, nullptr, dx, N, OH, OW, C, R, S, 1, H, W, R - 1 - pad, BnIn{}, st, part, bn_x,
-                         BnIn{bn_mean, bn_invstd, bn_gamma, bn_beta, bn_relu}, 2);
+                                  const float* residual, const float* bn_x, const float* bn_mean,
+                                  const float* bn_invstd, const float* bn_gamma, const float* bn_beta, int bn_relu,
+                                  double* part, void* stream) {
+  if ((part != nullptr) != (bn_x != nullptr)) return DK_ERR_ARGS;
+  return dw_dgrad(dy, N, OH, OW, C, w_crs, R, S, stride, pad, dx, H, W, ws, ws_bytes, residual, bn_x,
+                  BnIn{bn_mean, bn_invstd, bn_gamma, bn_beta, bn_relu}, part, as_stream(stream));
 }
 
 DK_API size_t dk_dwconv_wgrad_workspace_bytes(int N, int OH, int OW, int C, int R, int S) {

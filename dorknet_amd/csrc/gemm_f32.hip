@@ -371,20 +371,39 @@ struct LdImgIC : ICLayout<ROWS, BK> {
 // says the destination allows 16-byte stores), put1 a single column otherwise.  Epilogues
 // with kColStats also fold a per-column reduction of what they store into a[e] / b[e].
 
-// out[m][n] = acc (+ bias[n]).
+// out[m][n] = acc (+ bias[n]) (+ res[m][n]: a residual addend laid out like out).
 struct EpStore {
   static constexpr bool kColStats = false;
   float* out;
   int ldo;
   const float* bias;
-  int v4;  // out, ldo and bias allow 16-byte access
-  __device__ __forceinline__ f32x4 value4(int n, f32x4 v) const { return bias ? v + ld4(bias + n) : v; }
-  __device__ __forceinline__ float value1(int n, float v) const { return bias ? v + bias[n] : v; }
-  __device__ __forceinline__ void put4(int m, int n, f32x4 v, int, double*, double*) const {
-    st4(out + (size_t)m * ldo + n, value4(n, v));
+  int v4;  // out, ldo, bias and res allow 16-byte access
+  const float* res;
+  // per-row operands the 16-byte path needs, loaded for all of a thread's rows before any
+  // store (loads cannot be hoisted over stores to a possibly aliasing output)
+  struct Pre {
+    f32x4 r, x;
+  };
+  __device__ __forceinline__ Pre pre4(int m, int n) const {
+    Pre p;
+    p.r = res ? ld4(res + (size_t)m * ldo + n) : f32x4{0.f, 0.f, 0.f, 0.f};
+    return p;
+  }
+  __device__ __forceinline__ f32x4 value4(int n, f32x4 v, const Pre& p) const {
+    if (bias) v += ld4(bias + n);
+    if (res) v += p.r;
+    return v;
+  }
+  __device__ __forceinline__ float value1(int m, int n, float v) const {
+    if (bias) v += bias[n];
+    if (res) v += res[(size_t)m * ldo + n];
+    return v;
+  }
+  __device__ __forceinline__ void put4(int m, int n, f32x4 v, const Pre& p, int, double*, double*) const {
+    st4(out + (size_t)m * ldo + n, value4(n, v, p));
   }
   __device__ __forceinline__ void put1(int m, int n, float v, int, double&, double&) const {
-    out[(size_t)m * ldo + n] = value1(n, v);
+    out[(size_t)m * ldo + n] = value1(m, n, v);
   }
 };
 
@@ -395,8 +414,8 @@ struct EpStore {
 struct EpStoreStats : EpStore {
   static constexpr bool kColStats = true;
   double* part;
-  __device__ __forceinline__ void put4(int m, int n, f32x4 v, int, double* a, double* b) const {
-    const f32x4 o = value4(n, v);
+  __device__ __forceinline__ void put4(int m, int n, f32x4 v, const Pre& p, int, double* a, double* b) const {
+    const f32x4 o = value4(n, v, p);
     st4(out + (size_t)m * ldo + n, o);
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
@@ -406,7 +425,7 @@ struct EpStoreStats : EpStore {
     }
   }
   __device__ __forceinline__ void put1(int m, int n, float v, int, double& a, double& b) const {
-    const float o = value1(n, v);
+    const float o = value1(m, n, v);
     out[(size_t)m * ldo + n] = o;
     a += (double)o;
     b += (double)o * (double)o;
@@ -434,11 +453,18 @@ struct EpStoreBnBwd : EpStore {
   double* part;
   const float* xbn;  // [M][ldo], the BN's raw input
   BnIn bn;
-  __device__ __forceinline__ void put4(int m, int n, f32x4 v, int, double* a, double* b) const {
+  __device__ __forceinline__ Pre pre4(int m, int n) const {
+    Pre p = EpStore::pre4(m, n);
+    p.x = ld4(xbn + (size_t)m * ldo + n);
+    return p;
+  }
+  __device__ __forceinline__ void put4(int m, int n, f32x4 v, const Pre& p, int, double* a, double* b) const {
+    v = value4(n, v, p);
     st4(out + (size_t)m * ldo + n, v);
-    bn_bwd_contrib4(v, ld4(xbn + (size_t)m * ldo + n), bn, n, a, b);
+    bn_bwd_contrib4(v, p.x, bn, n, a, b);
   }
   __device__ __forceinline__ void put1(int m, int n, float v, int, double& a, double& b) const {
+    v = value1(m, n, v);
     out[(size_t)m * ldo + n] = v;
     bn_bwd_contrib(v, xbn[(size_t)m * ldo + n], bn.mean[n], bn.invstd[n], bn.gamma[n], bn.beta[n], bn.relu, a, b);
   }
@@ -453,6 +479,7 @@ struct EpWiden {
   int ldo;
   int OH, OW, st;
   int v4;
+  const float* res;  // optional residual addend on the widened grid (off-lattice: out = res)
   __device__ __forceinline__ size_t cell(int m) const {
     const int ow = m % OW;
     const int t = m / OW;
@@ -460,18 +487,29 @@ struct EpWiden {
     const int b = t / OH;
     return (size_t)(b * OH * st + oh * st) * (OW * st) + (size_t)ow * st;
   }
-  __device__ __forceinline__ void put4(int m, int n, f32x4 v, int, double*, double*) const {
+  struct Pre {
+    f32x4 x;
+  };
+  __device__ __forceinline__ Pre pre4(int, int) const { return Pre{}; }
+  __device__ __forceinline__ void put4(int m, int n, f32x4 v, const Pre&, int, double*, double*) const {
     const size_t c0 = cell(m);
     const size_t W2 = (size_t)OW * st;
     for (int dy = 0; dy < st; ++dy)
-      for (int dx = 0; dx < st; ++dx)
-        st4(out + (c0 + dy * W2 + dx) * ldo + n, (dy | dx) ? f32x4{0.f, 0.f, 0.f, 0.f} : v);
+      for (int dx = 0; dx < st; ++dx) {
+        const size_t o = (c0 + dy * W2 + dx) * ldo + n;
+        f32x4 t = (dy | dx) ? f32x4{0.f, 0.f, 0.f, 0.f} : v;
+        if (res) t += ld4(res + o);
+        st4(out + o, t);
+      }
   }
   __device__ __forceinline__ void put1(int m, int n, float v, int, double&, double&) const {
     const size_t c0 = cell(m);
     const size_t W2 = (size_t)OW * st;
     for (int dy = 0; dy < st; ++dy)
-      for (int dx = 0; dx < st; ++dx) out[(c0 + dy * W2 + dx) * ldo + n] = (dy | dx) ? 0.f : v;
+      for (int dx = 0; dx < st; ++dx) {
+        const size_t o = (c0 + dy * W2 + dx) * ldo + n;
+        out[o] = ((dy | dx) ? 0.f : v) + (res ? res[o] : 0.f);
+      }
   }
 };
 
@@ -482,9 +520,10 @@ struct EpWidenBnBwd : EpWiden {
   double* part;
   const float* xbn;  // the BN's raw input on the widened grid
   BnIn bn;
-  __device__ __forceinline__ void put4(int m, int n, f32x4 v, int sp, double* a, double* b) const {
-    EpWiden::put4(m, n, v, sp, a, b);
-    bn_bwd_contrib4(v, ld4(xbn + cell(m) * ldo + n), bn, n, a, b);
+  __device__ __forceinline__ Pre pre4(int m, int n) const { return Pre{ld4(xbn + cell(m) * ldo + n)}; }
+  __device__ __forceinline__ void put4(int m, int n, f32x4 v, const Pre& p, int sp, double* a, double* b) const {
+    EpWiden::put4(m, n, v, p, sp, a, b);
+    bn_bwd_contrib4(v, p.x, bn, n, a, b);
   }
   __device__ __forceinline__ void put1(int m, int n, float v, int sp, double& a, double& b) const {
     EpWiden::put1(m, n, v, sp, a, b);
@@ -498,7 +537,9 @@ struct EpPartial {
   float* ws;
   int M, N;
   int v4;
-  __device__ __forceinline__ void put4(int m, int n, f32x4 v, int split, double*, double*) const {
+  struct Pre {};
+  __device__ __forceinline__ Pre pre4(int, int) const { return Pre{}; }
+  __device__ __forceinline__ void put4(int m, int n, f32x4 v, const Pre&, int split, double*, double*) const {
     st4(ws + ((size_t)split * M + m) * N + n, v);
   }
   __device__ __forceinline__ void put1(int m, int n, float v, int split, double&, double&) const {
@@ -626,13 +667,25 @@ __global__ __launch_bounds__(64 * WM * WN) void igemm_f32(DA da, DB db, EP ep, i
   const int col = n0 + 4 * c4;
   const bool full = ep.v4 && col + 3 < N;
   double sa[4] = {0.0, 0.0, 0.0, 0.0}, sb[4] = {0.0, 0.0, 0.0, 0.0};
-  for (int rl = rl0; rl < BM; rl += RSTEP) {
-    const int row = m0 + rl;
-    if (row >= M) break;
-    const f32x4 v = ld4(smem + rl * LDT + 4 * c4);
-    if (full) {
-      ep.put4(row, col, v, blockIdx.y, sa, sb);
-    } else {
+  constexpr int RPT = BM / RSTEP;  // rows per thread
+  static_assert(BM % RSTEP == 0, "epilogue rows");
+  if (full) {
+    typename EP::Pre pre[RPT];
+#pragma unroll
+    for (int i = 0; i < RPT; ++i) {
+      const int row = m0 + rl0 + i * RSTEP;
+      if (row < M) pre[i] = ep.pre4(row, col);
+    }
+#pragma unroll
+    for (int i = 0; i < RPT; ++i) {
+      const int rl = rl0 + i * RSTEP;
+      if (m0 + rl < M) ep.put4(m0 + rl, col, ld4(smem + rl * LDT + 4 * c4), pre[i], blockIdx.y, sa, sb);
+    }
+  } else {
+    for (int rl = rl0; rl < BM; rl += RSTEP) {
+      const int row = m0 + rl;
+      if (row >= M) break;
+      const f32x4 v = ld4(smem + rl * LDT + 4 * c4);
 #pragma unroll
       for (int e = 0; e < 4; ++e)
         if (col + e < N) ep.put1(row, col + e, v[e], blockIdx.y, sa[e], sb[e]);
@@ -671,11 +724,12 @@ static inline int aligned16(const void* p) { return (reinterpret_cast<uintptr_t>
 static inline bool fits(size_t bytes) { return bytes < ((size_t)1 << 31); }
 
 static inline int al4(int v) { return (v & 3) == 0; }
-static inline EpStore ep_store(float* out, int ldo, const float* bias) {
-  return EpStore{out, ldo, bias, al4(ldo) && aligned16(out) && (!bias || aligned16(bias))};
+static inline EpStore ep_store(float* out, int ldo, const float* bias, const float* res = nullptr) {
+  return EpStore{out, ldo, bias, al4(ldo) && aligned16(out) && (!bias || aligned16(bias)) && (!res || aligned16(res)),
+                 res};
 }
-static inline EpWiden ep_widen(float* out, int ldo, int OH, int OW, int st) {
-  return EpWiden{out, ldo, OH, OW, st, al4(ldo) && aligned16(out)};
+static inline EpWiden ep_widen(float* out, int ldo, int OH, int OW, int st, const float* res = nullptr) {
+  return EpWiden{out, ldo, OH, OW, st, al4(ldo) && aligned16(out) && (!res || aligned16(res)), res};
 }
 
 
@@ -1148,27 +1202,38 @@ DK_API int dk_pwconv_dgrad_stats_rows(int N, int OH, int OW, int K, int C) { ret
 // dgrad + the BN-backward partial sums of the BatchNorm whose output this layer consumed
 // (bn_x = that BN's raw input, on the dx grid; part: dk_pwconv_dgrad_stats_rows() x 2 x C).
 DK_API int dk_pwconv_dgrad_ex_f32(const float* dy, int N, int OH, int OW, int K, const float* w_kc, int C, int stride,
-                                  float* dx, const float* bn_x, const float* bn_mean, const float* bn_invstd,
-                                  const float* bn_gamma, const float* bn_beta, int bn_relu, double* part,
-                                  void* stream) {
+                                  float* dx, const float* residual, const float* bn_x, const float* bn_mean,
+                                  const float* bn_invstd, const float* bn_gamma, const float* bn_beta, int bn_relu,
+                                  double* part, void* stream) {
   const int M = N * OH * OW;
-  if (!fits((size_t)M * K * 4) || !bn_x || !part || !bn_mean || !bn_invstd || !bn_gamma || !bn_beta)
-    return DK_ERR_ARGS;
+  if (!fits((size_t)M * K * 4) || (part != nullptr) != (bn_x != nullptr)) return DK_ERR_ARGS;
+  if (part && (!bn_mean || !bn_invstd || !bn_gamma || !bn_beta)) return DK_ERR_ARGS;
+  if (part && residual && stride != 1) return DK_ERR_ARGS;  // off-lattice residual terms would need reducing
   MatDesc a = mat(dy, M, K, M);
   MatDesc b = mat(w_kc, K, C, C);
   const hipStream_t st = as_stream(stream);
   const bool vec = vec_ok(a, K, 4) && vec_ok(b, 4, C);
+#define DK_ROWS(EPT, ep)                                                              \
+  return vec ? igemm_rows<LdMatKC, MatDesc, LdMatIC, MatDesc, EPT>(a, b, ep, M, C, K, st) \
+             : igemm_rows<LdMatKC1, MatDesc, LdMatIC1, MatDesc, EPT>(a, b, ep, M, C, K, st)
+  if (!part) {
+    if (stride == 1) {
+      EpStore ep = ep_store(dx, C, nullptr, residual);
+      DK_ROWS(EpStore, ep);
+    }
+    EpWiden ep = ep_widen(dx, C, OH, OW, stride, residual);
+    DK_ROWS(EpWiden, ep);
+  }
   const BnIn bn{bn_mean, bn_invstd, bn_gamma, bn_beta, bn_relu};
   const int xv4 = aligned16(bn_x) && bn_ok(bn_mean, bn_invstd, bn_gamma, bn_beta);
   if (stride == 1) {
     EpStoreBnBwd ep;
-    static_cast<EpStore&>(ep) = ep_store(dx, C, nullptr);
+    static_cast<EpStore&>(ep) = ep_store(dx, C, nullptr, residual);
     ep.v4 = ep.v4 && xv4;
     ep.part = part;
     ep.xbn = bn_x;
     ep.bn = bn;
-    if (vec) return igemm_rows<LdMatKC, MatDesc, LdMatIC, MatDesc, EpStoreBnBwd>(a, b, ep, M, C, K, st);
-    return igemm_rows<LdMatKC1, MatDesc, LdMatIC1, MatDesc, EpStoreBnBwd>(a, b, ep, M, C, K, st);
+    DK_ROWS(EpStoreBnBwd, ep);
   }
   EpWidenBnBwd ep;
   static_cast<EpWiden&>(ep) = ep_widen(dx, C, OH, OW, stride);
@@ -1176,8 +1241,8 @@ DK_API int dk_pwconv_dgrad_ex_f32(const float* dy, int N, int OH, int OW, int K,
   ep.part = part;
   ep.xbn = bn_x;
   ep.bn = bn;
-  if (vec) return igemm_rows<LdMatKC, MatDesc, LdMatIC, MatDesc, EpWidenBnBwd>(a, b, ep, M, C, K, st);
-  return igemm_rows<LdMatKC1, MatDesc, LdMatIC1, MatDesc, EpWidenBnBwd>(a, b, ep, M, C, K, st);
+  DK_ROWS(EpWidenBnBwd, ep);
+#undef DK_ROWS
 }
 
 DK_API size_t dk_pwconv_wgrad_workspace_bytes(int N, int OH, int OW, int K, int C) {

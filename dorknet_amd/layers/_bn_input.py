@@ -76,3 +76,27 @@ def materialize(X):
 
 def accepts_bn_input(layer) -> bool:
     return bool(getattr(layer, "accepts_bn_input", False))
+
+
+def residual_operand(residual, like):
+    """`residual` as an NHWC device tensor shaped like `like` (for a fused residual addend),
+    or None when there is none or it cannot be fused."""
+    if residual is None:
+        return None
+    from .._tensor import is_nhwc
+    r = residual
+    if isinstance(r, torch.Tensor) and r.is_cuda and r.dtype == torch.float32 and tuple(r.shape) == tuple(
+            like.shape) and r.dim() == 4 and is_nhwc(r):
+        return r
+    return None
+
+
+def add_residual(dx, residual):
+    """dx + residual (the unfused residual join, residual_block.py:94-97)."""
+    from .._tensor import to_nhwc
+    a, b = to_nhwc(dx), to_nhwc(residual)
+    if a.shape != b.shape:
+        raise ValueError("residual backward shape mismatch: {} vs {}".format(tuple(a.shape), tuple(b.shape)))
+    out = empty_nhwc(*a.shape)
+    lib.dk_add_f32(a.data_ptr(), b.data_ptr(), a.numel(), 0, out.data_ptr(), 0, stream_handle())
+    return out

@@ -108,10 +108,21 @@ def chain_forward(layers, X, test_mode=False, out_accepts=False):
     return X, steps
 
 
-def chain_backward(steps, dy):
-    for step in reversed(steps):
+def chain_backward(steps, dy, residual=None):
+    """Backward through `steps` in reverse.  `residual`: a gradient to add to the result (the
+    residual join's other branch); the first layer adds it in its dgrad epilogue when it
+    can (``accepts_residual``), otherwise it is added separately."""
+    from ._bn_input import add_residual
+    last = len(steps) - 1
+    for i in range(last, -1, -1):
+        step = steps[i]
         if len(step) == 2:
             dy = step[0].backward_bn_relu(dy, step[1])
+        elif i == 0 and residual is not None and getattr(step[0], "accepts_residual", False):
+            dy = step[0].backward(dy, residual=residual)
+            residual = None
         else:
             dy = step[0].backward(dy)
+    if residual is not None:
+        dy = add_residual(dy, residual)
     return dy

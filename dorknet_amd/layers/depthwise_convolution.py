@@ -13,9 +13,9 @@ from __future__ import annotations
 
 import torch
 
-from .._hip import lib, stream_handle, workspace
+from .._hip import HipError, lib, stream_handle, workspace
 from .._tensor import empty_nhwc, ptr, to_nhwc
-from ._bn_input import BNOut
+from ._bn_input import BNOut, add_residual, residual_operand
 from ._common import add_regulariser_grad, grad_buffer, init_weights, l2_strength
 from .layer import Layer
 
@@ -96,7 +96,9 @@ class DepthwiseConvLayer(Layer):
             self._bn_in = bn
         return y
 
-    def backward(self, upstream_dx):
+    accepts_residual = True  # backward(dy, residual=R) returns dx + R (the residual join, fused)
+
+    def backward(self, upstream_dx, residual=None):
         self._require_on_gpu()
         st = stream_handle()
         dy = to_nhwc(upstream_dx)
@@ -125,18 +127,27 @@ class DepthwiseConvLayer(Layer):
         dx = empty_nhwc(N, C, H, W)
         nb = lib.dk_dwconv_dgrad_workspace_bytes(C, R, S)
         bn = self._bn_in
+        res = residual_operand(residual, dx)
         rows = lib.dk_dwconv_dgrad_stats_rows(N, H, W, C, self.stride) if bn is not None and R == S else 0
         if rows and self.padding <= R - 1:
-            # + stage 1 of the input BatchNorm's backward, in the dgrad epilogue
+            # + stage 1 of the input BatchNorm's backward, in the dgrad epilogue (+ the residual)
             part = torch.empty((rows, 2, C), dtype=torch.float64, device=dx.device)
             lib.dk_dwconv_dgrad_ex_f32(dy.data_ptr(), N, OH, OW, C, w.data_ptr(), R, S, self.stride, self.padding,
-                                       dx.data_ptr(), H, W, workspace.get(nb), nb, bn.x.data_ptr(), *bn.bn_args(),
-                                       part.data_ptr(), st)
+                                       dx.data_ptr(), H, W, workspace.get(nb), nb, ptr(res), bn.x.data_ptr(),
+                                       *bn.bn_args(), part.data_ptr(), st)
             bn.hand_backward_partials(dx, part)
-        else:
-            lib.dk_dwconv_dgrad_f32(dy.data_ptr(), N, OH, OW, C, w.data_ptr(), R, S, self.stride, self.padding,
-                                    dx.data_ptr(), H, W, workspace.get(nb), nb, st)
-        return dx
+            return dx
+        if res is not None:
+            try:
+                lib.dk_dwconv_dgrad_ex_f32(dy.data_ptr(), N, OH, OW, C, w.data_ptr(), R, S, self.stride,
+                                           self.padding, dx.data_ptr(), H, W, workspace.get(nb), nb, res.data_ptr(),
+                                           0, 0, 0, 0, 0, 0, 0, st)
+                return dx
+            except HipError:  # geometry without a fused residual (generic gather dgrad)
+                pass
+        lib.dk_dwconv_dgrad_f32(dy.data_ptr(), N, OH, OW, C, w.data_ptr(), R, S, self.stride, self.padding,
+                                dx.data_ptr(), H, W, workspace.get(nb), nb, st)
+        return add_residual(dx, residual) if residual is not None else dx
 
     def save_to_h5(self, open_f, save_grads=True):
         from ..network.checkpoint import save_layer

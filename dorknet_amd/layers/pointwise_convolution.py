@@ -16,7 +16,7 @@ import torch
 
 from .._hip import lib, stream_handle, workspace
 from .._tensor import empty_nhwc, ptr, to_nhwc
-from ._bn_input import BNOut
+from ._bn_input import BNOut, add_residual, residual_operand
 from ._common import add_regulariser_grad, grad_buffer, init_weights, l2_strength
 from .layer import Layer
 
@@ -91,7 +91,9 @@ class PointwiseConvLayer(Layer):
         self.out_hw = (OH, OW)
         return y
 
-    def backward(self, upstream_dx):
+    accepts_residual = True  # backward(dy, residual=R) returns dx + R (the residual join, fused)
+
+    def backward(self, upstream_dx, residual=None):
         self._require_on_gpu()
         st = stream_handle()
         dy = to_nhwc(upstream_dx)
@@ -119,15 +121,21 @@ class PointwiseConvLayer(Layer):
             add_regulariser_grad(gw, w, self.weight_regulariser)
         dx = empty_nhwc(N, C, OH * s, OW * s)  # widened shape, pointwise_convolution.py:68-72
         bn = self._bn_in
-        if bn is not None and (OH * s, OW * s) == (H, W):
+        res = residual_operand(residual, dx)
+        if bn is not None and (OH * s, OW * s) == (H, W) and (res is None or s == 1):
             # + stage 1 of the input BatchNorm's backward, in the dgrad epilogue
             rows = lib.dk_pwconv_dgrad_stats_rows(N, OH, OW, K, C)
             part = torch.empty((rows, 2, C), dtype=torch.float64, device=dx.device)
-            lib.dk_pwconv_dgrad_ex_f32(dy.data_ptr(), N, OH, OW, K, w.data_ptr(), C, s, dx.data_ptr(),
+            lib.dk_pwconv_dgrad_ex_f32(dy.data_ptr(), N, OH, OW, K, w.data_ptr(), C, s, dx.data_ptr(), ptr(res),
                                        bn.x.data_ptr(), *bn.bn_args(), part.data_ptr(), st)
             bn.hand_backward_partials(dx, part)
+        elif res is not None:
+            lib.dk_pwconv_dgrad_ex_f32(dy.data_ptr(), N, OH, OW, K, w.data_ptr(), C, s, dx.data_ptr(), res.data_ptr(),
+                                       0, 0, 0, 0, 0, 0, 0, st)
         else:
             lib.dk_pwconv_dgrad_f32(dy.data_ptr(), N, OH, OW, K, w.data_ptr(), C, s, dx.data_ptr(), st)
+            if residual is not None:
+                dx = add_residual(dx, residual)
         return dx
 
     def save_to_h5(self, open_f, save_grads=True):

@@ -13,7 +13,7 @@ from __future__ import annotations
 from .._hip import lib, stream_handle
 from .._tensor import empty_nhwc, to_nhwc
 from ._bn_input import accepts_bn_input, materialize
-from ._chain import chain_backward, chain_forward
+from ._chain import chain_backward, chain_forward, fusion_enabled
 from .activations import ReLu
 from .batch_norm import BatchNormLayer
 from .convolution import ConvLayer
@@ -90,10 +90,12 @@ class ResidualBlock(Layer):
 
     def backward(self, upstream_dx):
         joined_dx = self.post_skip_activation.backward(upstream_dx)
-        dx = chain_backward(self._steps, joined_dx)
-        if self.skip_projection is not None:
-            return _add(dx, self.skip_projection.backward(joined_dx))
-        return _add(dx, joined_dx)
+        # the skip branch's gradient goes in first, so the chain's first layer can add it in
+        # its dgrad epilogue instead of a separate join pass (residual_block.py:94-97)
+        skip_dx = self.skip_projection.backward(joined_dx) if self.skip_projection is not None else joined_dx
+        if fusion_enabled():
+            return chain_backward(self._steps, joined_dx, residual=skip_dx)
+        return _add(chain_backward(self._steps, joined_dx), skip_dx)
 
     def save_to_h5(self, open_f, save_grads=True):
         from ..network.checkpoint import save_layer

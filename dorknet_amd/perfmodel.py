@@ -174,12 +174,14 @@ MODEL = {
     "dk_pwconv_fwd_ex_f32": _ex(_pw_fwd),
     "dk_dwconv_fwd_ex_f32": _ex(_dw_fwd),
     # dgrad + BN-backward partials: also reads the BN's raw input (same size as dx)
-    "dk_pwconv_dgrad_ex_f32": lambda dy, N, OH, OW, K, w, C, s, dx, bx, m, i, g, b, r, part, st: (
+    # dgrad (+ the residual addend read) (+ the BN's raw input read for the BN-backward sums)
+    "dk_pwconv_dgrad_ex_f32": lambda dy, N, OH, OW, K, w, C, s, dx, res, bx, m, i, g, b, r, part, st: (
         _pw_dgrad(dy, N, OH, OW, K, w, C, s, dx, st)[0],
-        _pw_dgrad(dy, N, OH, OW, K, w, C, s, dx, st)[1] + E * N * OH * OW * C),
-    "dk_dwconv_dgrad_ex_f32": lambda dy, N, OH, OW, C, w, R, S, s, p, dx, H, W, ws, nb, bx, m, i, g, b, r, part, st: (
-        _dw_dgrad(dy, N, OH, OW, C, w, R, S, s, p, dx, H, W, ws, nb, st)[0],
-        _dw_dgrad(dy, N, OH, OW, C, w, R, S, s, p, dx, H, W, ws, nb, st)[1] + E * N * H * W * C),
+        _pw_dgrad(dy, N, OH, OW, K, w, C, s, dx, st)[1] + E * N * OH * OW * C * ((bx != 0) + (res != 0) * s * s)),
+    "dk_dwconv_dgrad_ex_f32": lambda dy, N, OH, OW, C, w, R, S, s, p, dx, H, W, ws, nb, res, bx, m, i, g, b, r, part,
+    st: (_dw_dgrad(dy, N, OH, OW, C, w, R, S, s, p, dx, H, W, ws, nb, st)[0],
+         _dw_dgrad(dy, N, OH, OW, C, w, R, S, s, p, dx, H, W, ws, nb, st)[1] + E * N * H * W * C * (
+             (bx != 0) + (res != 0))),
     "dk_relu_bwd_bn_partial_f64": lambda dy, mask, x, P, C, *rest: (4 * P * C, E * 3 * P * C + P * C),
     "dk_bn_bwd_apply_f32": lambda x, dy, n, C, *rest: (6 * n, E * 3 * n),
 }

@@ -107,11 +107,13 @@ int dk_dwconv_fwd_ex_f32(const float* x, int N, int H, int W, int C, const float
  * like dx), part[rows][2][C] = per-tile (sum g, sum g * x_hat) -- what dk_bn_bwd_partial_f64
  * computes in a separate pass over x and dx (batch_norm.py:125-174).  Consume with
  * dk_bn_bwd_from_partials_f32.  dk_dwconv_dgrad_stats_rows returns 0 (no fused variant)
- * unless stride == 1 and C/4 divides 256. */
+ * unless stride == 1 and C/4 divides 256.  The dgrad_ex entries also take an optional
+ * `residual` addend (dx = dgrad + residual: the residual join's other gradient term,
+ * residual_block.py:94-97; NULL = none) and make the BN part optional (bn_x == NULL). */
 int dk_pwconv_dgrad_stats_rows(int N, int OH, int OW, int K, int C);
-int dk_pwconv_dgrad_ex_f32(const float* dy, int N, int OH, int OW, int K, const float* w_kc, int C, int stride, float* dx, const float* bn_x, const float* bn_mean, const float* bn_invstd, const float* bn_gamma, const float* bn_beta, int bn_relu, double* part, void* stream);
+int dk_pwconv_dgrad_ex_f32(const float* dy, int N, int OH, int OW, int K, const float* w_kc, int C, int stride, float* dx, const float* residual, const float* bn_x, const float* bn_mean, const float* bn_invstd, const float* bn_gamma, const float* bn_beta, int bn_relu, double* part, void* stream);
 int dk_dwconv_dgrad_stats_rows(int N, int H, int W, int C, int stride);
-int dk_dwconv_dgrad_ex_f32(const float* dy, int N, int OH, int OW, int C, const float* w_crs, int R, int S, int stride, int pad, float* dx, int H, int W, void* ws, size_t ws_bytes, const float* bn_x, const float* bn_mean, const float* bn_invstd, const float* bn_gamma, const float* bn_beta, int bn_relu, double* part, void* stream);
+int dk_dwconv_dgrad_ex_f32(const float* dy, int N, int OH, int OW, int C, const float* w_crs, int R, int S, int stride, int pad, float* dx, int H, int W, void* ws, size_t ws_bytes, const float* residual, const float* bn_x, const float* bn_mean, const float* bn_invstd, const float* bn_gamma, const float* bn_beta, int bn_relu, double* part, void* stream);
 
 /* ---------------------------------------------------------------------------------------
  * Depthwise convolution, direct (no MFMA).

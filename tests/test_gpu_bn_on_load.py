@@ -261,8 +261,8 @@ def test_pointwise_dgrad_bn_partials(stride, relu):
     lib.dk_pwconv_dgrad_f32(dy.data_ptr(), N, OH, OW, K, w.data_ptr(), C, stride, dx0.data_ptr(), st)
     rows = lib.dk_pwconv_dgrad_stats_rows(N, OH, OW, K, C)
     part = torch.empty((rows, 2, C), dtype=torch.float64, device="cuda")
-    lib.dk_pwconv_dgrad_ex_f32(dy.data_ptr(), N, OH, OW, K, w.data_ptr(), C, stride, dx1.data_ptr(), xbn.data_ptr(),
-                               *args(p, relu), part.data_ptr(), st)
+    lib.dk_pwconv_dgrad_ex_f32(dy.data_ptr(), N, OH, OW, K, w.data_ptr(), C, stride, dx1.data_ptr(), 0,
+                               xbn.data_ptr(), *args(p, relu), part.data_ptr(), st)
     same(dx0, dx1)
     _close(_bwd_finalize(part, rows, C, N * H * W), _bwd_reference(xbn, dx0, p, relu))
 
@@ -283,7 +283,7 @@ def test_depthwise_dgrad_bn_partials():
     rows = lib.dk_dwconv_dgrad_stats_rows(N, H, W, C, 1)
     part = torch.empty((rows, 2, C), dtype=torch.float64, device="cuda")
     lib.dk_dwconv_dgrad_ex_f32(dy.data_ptr(), N, H, W, C, w.data_ptr(), 3, 3, 1, 1, dx1.data_ptr(), H, W,
-                               workspace.get(nb), nb, xbn.data_ptr(), *args(p, 1), part.data_ptr(), st)
+                               workspace.get(nb), nb, 0, xbn.data_ptr(), *args(p, 1), part.data_ptr(), st)
     same(dx0, dx1)
     _close(_bwd_finalize(part, rows, C, N * H * W), _bwd_reference(xbn, dx0, p, 1))
 
@@ -308,3 +308,38 @@ def test_relu_bwd_bn_partials():
                                    dx1.data_ptr(), part.data_ptr(), nb, st)
     same(dx0, dx1)
     _close(_bwd_finalize(part, lib.dk_bn_partial_blocks(P, C), C, P), _bwd_reference(xbn, dx0, p, 0))
+
+
+@pytest.mark.parametrize("kind,stride", [("pw", 1), ("pw", 2), ("dw", 1), ("dw", 2)])
+def test_dgrad_residual_bitwise(kind, stride):
+    """dgrad_ex with a residual addend == plain dgrad followed by dk_add_f32, bitwise."""
+    rng = np.random.RandomState(50 + stride)
+    st = stream_handle()
+    N, C = 2, 32
+    if kind == "pw":
+        K, OH, OW = 24, 7, 6
+        H, W = OH * stride, OW * stride
+        dy = nhwc(rng.randn(N, K, OH, OW))
+        w = torch.as_tensor(rng.randn(K, C).astype(np.float32), device="cuda")
+        r = nhwc(rng.randn(N, C, H, W))
+        dx0 = torch.empty_like(r)
+        dx1 = torch.empty_like(r)
+        lib.dk_pwconv_dgrad_f32(dy.data_ptr(), N, OH, OW, K, w.data_ptr(), C, stride, dx0.data_ptr(), st)
+        lib.dk_pwconv_dgrad_ex_f32(dy.data_ptr(), N, OH, OW, K, w.data_ptr(), C, stride, dx1.data_ptr(), r.data_ptr(),
+                                   0, 0, 0, 0, 0, 0, 0, st)
+    else:
+        H, W = 13, 12
+        OH, OW = (H + 2 - 3) // stride + 1, (W + 2 - 3) // stride + 1
+        dy = nhwc(rng.randn(N, C, OH, OW))
+        w = torch.as_tensor(rng.randn(C, 3, 3).astype(np.float32), device="cuda")
+        r = nhwc(rng.randn(N, C, H, W))
+        dx0 = torch.empty_like(r)
+        dx1 = torch.empty_like(r)
+        nb = lib.dk_dwconv_dgrad_workspace_bytes(C, 3, 3)
+        lib.dk_dwconv_dgrad_f32(dy.data_ptr(), N, OH, OW, C, w.data_ptr(), 3, 3, stride, 1, dx0.data_ptr(), H, W,
+                                workspace.get(nb), nb, st)
+        lib.dk_dwconv_dgrad_ex_f32(dy.data_ptr(), N, OH, OW, C, w.data_ptr(), 3, 3, stride, 1, dx1.data_ptr(), H, W,
+                                   workspace.get(nb), nb, r.data_ptr(), 0, 0, 0, 0, 0, 0, 0, st)
+    ref = torch.empty_like(r)
+    lib.dk_add_f32(dx0.data_ptr(), r.data_ptr(), r.numel(), 0, ref.data_ptr(), 0, st)
+    same(ref, dx1)
