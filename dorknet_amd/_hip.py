@@ -89,7 +89,7 @@ class _Lib:
             fn = getattr(lib, name)
             fn.restype = ctypes.c_size_t if ret == "size_t" else ctypes.c_int
             fn.argtypes = [_argtype(t) for t, _ in params]
-            if ret == "int" and not name.endswith(("_blocks", "_version", "_rows")) and not name.startswith("dk_debug"):
+            if ret == "int" and not name.endswith(("_blocks", "_version", "_rows", "_count")) and not name.startswith("dk_debug"):
                 fn.errcheck = _errcheck
         self._decls = decls
         self._lib = lib
@@ -144,3 +144,19 @@ class Workspace:
 
 
 workspace = Workspace()
+
+
+class Tickets:
+    """Zeroed ticket words for the one-launch folds (dk_bn_*_from_partials_f32 `tickets`).
+    Zeroed once when allocated; every call leaves them zero.  Calls on one stream only."""
+
+    def __init__(self):
+        self._buf = None
+
+    def get(self, n: int) -> int:
+        if self._buf is None or self._buf.numel() < n:
+            self._buf = torch.zeros(max(int(n), 256), dtype=torch.int32, device="cuda")
+        return self._buf.data_ptr()
+
+
+tickets = Tickets()

@@ -232,45 +232,97 @@ __device__ __forceinline__ void bn_finalize_channel(int c, int C, double s, doub
   }
 }
 
-template <bool FINAL>
+// Write-through (sc1) stores / loads for rows handed between blocks of one launch
+// (cdna_hip_programming.md section 6 Guideline 16, counter form with sc1 payload: no release
+// fence, whose L2 write-back in every block would cost more than the launch it saves).
+__device__ __forceinline__ void pub_store(double* p, double v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double pub_load(const double* p) {
+  return __hip_atomic_load(const_cast<double*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// LEVEL 0: fold up to kFoldRows rows per block into out[blockIdx.x] (a later launch folds
+// those).  1 (FINAL): one block along x folds every row and finalizes.  2 (TICKET): as 0,
+// then the last block of each 64-column group to arrive (agent-scope ticket, zeroed by the
+// caller once and put back to zero here) folds out[] and finalizes -- two levels, one launch.
+template <int LEVEL>
 __global__ __launch_bounds__(1024) void bn_fold_kernel(const double* __restrict__ part, int nblk, int C,
-                                                       double* __restrict__ out, FoldOut o) {
+                                                       double* __restrict__ out, FoldOut o, unsigned* tickets) {
   __shared__ double red[kFoldLanes][64][2];
+  __shared__ int last;
   const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
   const int c = blockIdx.y * 64 + cl;
-  const int b0 = blockIdx.x * kFoldRows + rl;
-  double s = 0.0, q = 0.0;
-  if (c < C) {
-    double vs[kFoldPerLane], vq[kFoldPerLane];
+  auto fold = [&](const double* src, int n, int b0, bool sc1) {
+    double s = 0.0, q = 0.0;
+    if (c < C) {
+      double vs[kFoldPerLane], vq[kFoldPerLane];
 #pragma unroll
-    for (int k = 0; k < kFoldPerLane; ++k) {
-      const int b = b0 + k * kFoldLanes;
-      const int bb = b < nblk ? b : nblk - 1;  // clamp, load unconditionally, mask after
-      vs[k] = part[((size_t)bb * 2 + 0) * C + c];
-      vq[k] = part[((size_t)bb * 2 + 1) * C + c];
+      for (int k = 0; k < kFoldPerLane; ++k) {
+        const int b = b0 + k * kFoldLanes;
+        const int bb = b < n ? b : n - 1;  // clamp, load unconditionally, mask after
+        vs[k] = sc1 ? pub_load(src + ((size_t)bb * 2 + 0) * C + c) : src[((size_t)bb * 2 + 0) * C + c];
+        vq[k] = sc1 ? pub_load(src + ((size_t)bb * 2 + 1) * C + c) : src[((size_t)bb * 2 + 1) * C + c];
+      }
+#pragma unroll
+      for (int k = 0; k < kFoldPerLane; ++k) {
+        const bool in = b0 + k * kFoldLanes < n;
+        s += in ? vs[k] : 0.0;
+        q += in ? vq[k] : 0.0;
+      }
     }
+    red[rl][cl][0] = s;
+    red[rl][cl][1] = q;
+    __syncthreads();
+  };
+  auto total = [&](double& S, double& Q) {
+    S = 0.0;
+    Q = 0.0;
 #pragma unroll
-    for (int k = 0; k < kFoldPerLane; ++k) {
-      const bool in = b0 + k * kFoldLanes < nblk;
-      s += in ? vs[k] : 0.0;
-      q += in ? vq[k] : 0.0;
+    for (int l = 0; l < kFoldLanes; ++l) {
+      S += red[l][cl][0];
+      Q += red[l][cl][1];
     }
-  }
-  red[rl][cl][0] = s;
-  red[rl][cl][1] = q;
-  __syncthreads();
-  if (rl != 0 || c >= C) return;
-  double S = 0.0, Q = 0.0;
-#pragma unroll
-  for (int l = 0; l < kFoldLanes; ++l) {
-    S += red[l][cl][0];
-    Q += red[l][cl][1];
-  }
-  if constexpr (FINAL) {
+  };
+  fold(part, nblk, blockIdx.x * kFoldRows + rl, false);
+  if constexpr (LEVEL == 1) {
+    if (rl != 0 || c >= C) return;
+    double S, Q;
+    total(S, Q);
     bn_finalize_channel(c, C, S, Q, o);
   } else {
-    out[((size_t)blockIdx.x * 2 + 0) * C + c] = S;
-    out[((size_t)blockIdx.x * 2 + 1) * C + c] = Q;
+    if (rl == 0 && c < C) {
+      double S, Q;
+      total(S, Q);
+      if constexpr (LEVEL == 0) {
+        out[((size_t)blockIdx.x * 2 + 0) * C + c] = S;
+        out[((size_t)blockIdx.x * 2 + 1) * C + c] = Q;
+      } else {
+        pub_store(out + ((size_t)blockIdx.x * 2 + 0) * C + c, S);
+        pub_store(out + ((size_t)blockIdx.x * 2 + 1) * C + c, Q);
+      }
+    }
+    if constexpr (LEVEL == 2) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        unsigned* t = tickets + blockIdx.y;
+        const unsigned old = __hip_atomic_fetch_add(t, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        last = old + 1u == gridDim.x;
+        if (last) {
+          __hip_atomic_store(t, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+      }
+      __syncthreads();
+      if (!last) return;
+      fold(out, gridDim.x, rl, true);  // gridDim.x <= kFoldRows rows (checked on the host)
+      if (rl != 0 || c >= C) return;
+      double S, Q;
+      total(S, Q);
+      bn_finalize_channel(c, C, S, Q, o);
+    }
   }
 }
 
@@ -592,7 +644,7 @@ DK_API int dk_bn_stats_f32(const float* x, int P, int C, float eps, float moment
   if (rc) return rc;
   return dk_bn_stats_from_partials_f32(ws, nblk, C, (double)P, eps, momentum, first, mean, std_, invstd, run_mean,
                                        run_std, static_cast<char*>(ws) + bn_fold_offset(P, C),
-                                       ws_bytes - bn_fold_offset(P, C), stream);
+                                       ws_bytes - bn_fold_offset(P, C), nullptr, stream);
 }
 
 // Workspace of dk_bn_stats_f32: the partials plus their fold rows.
@@ -608,23 +660,33 @@ DK_API size_t dk_bn_partials_workspace_bytes(int nblk, int C) {
   return (rows > 0 ? rows : 1) * 2 * C * sizeof(double);
 }
 
-// Fold part[nblk][2][C] (fixed order) and apply the stage-2 maths: one launch for <= 256 rows.
-static int fold_finalize(const double* part, int nblk, int C, double* ws, const FoldOut& o, hipStream_t st) {
+DK_API int dk_bn_fold_tickets_count(int C) { return C < 1 ? 0 : cdiv(C, 64); }
+
+// Fold part[nblk][2][C] (fixed order) and apply the stage-2 maths: one launch for <= 256 rows,
+// and with `tickets` (>= cdiv(C, 64) zeroed words) one launch for <= 256 * 256 rows.
+static int fold_finalize(const double* part, int nblk, int C, double* ws, const FoldOut& o, hipStream_t st,
+                         unsigned* tickets = nullptr) {
   const unsigned gy = (unsigned)cdiv(C, 64);
+  if (tickets && nblk > kFoldRows && nblk <= kFoldRows * kFoldRows) {
+    hipLaunchKernelGGL(bn_fold_kernel<2>, dim3(cdiv(nblk, kFoldRows), gy), dim3(1024), 0, st, part, nblk, C, ws, o,
+                       tickets);
+    return launch_status();
+  }
   while (nblk > kFoldRows) {
     const int n2 = cdiv(nblk, kFoldRows);
-    hipLaunchKernelGGL(bn_fold_kernel<false>, dim3(n2, gy), dim3(1024), 0, st, part, nblk, C, ws, o);
+    hipLaunchKernelGGL(bn_fold_kernel<0>, dim3(n2, gy), dim3(1024), 0, st, part, nblk, C, ws, o, nullptr);
     part = ws;
     ws += (size_t)n2 * 2 * C;
     nblk = n2;
   }
-  hipLaunchKernelGGL(bn_fold_kernel<true>, dim3(1, gy), dim3(1024), 0, st, part, nblk, C, nullptr, o);
+  hipLaunchKernelGGL(bn_fold_kernel<1>, dim3(1, gy), dim3(1024), 0, st, part, nblk, C, nullptr, o, nullptr);
   return launch_status();
 }
 
 DK_API int dk_bn_stats_from_partials_f32(const void* part, int nblk, int C, double count, float eps, float momentum,
                                          int first, float* mean, float* std_, float* invstd, float* run_mean,
-                                         float* run_std, void* ws, size_t ws_bytes, void* stream) {
+                                         float* run_std, void* ws, size_t ws_bytes, unsigned* tickets,
+                                         void* stream) {
   if (ws_bytes < dk_bn_partials_workspace_bytes(nblk, C) || nblk < 1) return DK_ERR_WORKSPACE;
   FoldOut o{};
   o.mode = 0;
@@ -637,7 +699,8 @@ DK_API int dk_bn_stats_from_partials_f32(const void* part, int nblk, int C, doub
   o.invstd = invstd;
   o.run_mean = run_mean;
   o.run_std = run_std;
-  return fold_finalize(static_cast<const double*>(part), nblk, C, static_cast<double*>(ws), o, as_stream(stream));
+  return fold_finalize(static_cast<const double*>(part), nblk, C, static_cast<double*>(ws), o, as_stream(stream),
+                       tickets);
 }
 
 // out[2][C] = the column sums of part[nblk][2][C] (SyncBN: the vector each rank all-reduces).
@@ -717,7 +780,7 @@ DK_API int dk_relu_bwd_bn_partial_f64(const float* dy, const uint8_t* mask, cons
 // Backward stage 2 from partials of any origin (dk_bn_bwd_partial_f64, a consumer's
 // dgrad_ex epilogue, dk_relu_bwd_bn_partial_f64): fixed-order fold, then the finalize.
 DK_API int dk_bn_bwd_from_partials_f32(const void* part, int nblk, int C, double count, float* dgamma, float* dbeta,
-                                       float* k12, void* ws, size_t ws_bytes, void* stream) {
+                                       float* k12, void* ws, size_t ws_bytes, unsigned* tickets, void* stream) {
   if (ws_bytes < dk_bn_partials_workspace_bytes(nblk, C) || nblk < 1) return DK_ERR_WORKSPACE;
   FoldOut o{};
   o.mode = 1;
@@ -725,7 +788,8 @@ DK_API int dk_bn_bwd_from_partials_f32(const void* part, int nblk, int C, double
   o.dgamma = dgamma;
   o.dbeta = dbeta;
   o.k12 = k12;
-  return fold_finalize(static_cast<const double*>(part), nblk, C, static_cast<double*>(ws), o, as_stream(stream));
+  return fold_finalize(static_cast<const double*>(part), nblk, C, static_cast<double*>(ws), o, as_stream(stream),
+                       tickets);
 }
 
 // Backward stage 2: dgamma/dbeta from the local partials, k12 = [k1[C], k2[C]] from the global ones.
@@ -773,7 +837,7 @@ DK_API int dk_bn_bwd_f32(const float* x, const float* dy, int P, int C, const fl
   int rc = dk_bn_bwd_partial_f64(x, dy, P, C, mean, invstd, gamma, beta, relu, ws, ws_bytes, stream);
   if (rc) return rc;
   rc = dk_bn_bwd_from_partials_f32(ws, nblk, C, (double)P, dgamma, dbeta, k12, base + fold_off, ws_bytes - fold_off,
-                                   stream);
+                                   nullptr, stream);
   if (rc) return rc;
   return dk_bn_bwd_apply_f32(x, dy, (long long)P * C, C, mean, invstd, gamma, beta, relu, k12, dx, stream);
 }

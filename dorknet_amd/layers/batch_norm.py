@@ -20,7 +20,7 @@ from __future__ import annotations
 
 import torch
 
-from .._hip import lib, stream_handle, workspace
+from .._hip import lib, stream_handle, tickets, workspace
 from .._tensor import as_device, empty_nhwc, rows, to_nhwc
 from ._common import grad_buffer
 from .layer import Layer
@@ -110,7 +110,8 @@ class BatchNormLayer(Layer):
                 lib.dk_bn_stats_from_partials_f32(partials.part.data_ptr(), partials.rows, C, float(P),
                                                   float(self.eps), float(self.run_momentum), int(first),
                                                   mean.data_ptr(), std.data_ptr(), invstd.data_ptr(), rm.data_ptr(),
-                                                  rs.data_ptr(), ws, nb, st)
+                                                  rs.data_ptr(), ws, nb, tickets.get(lib.dk_bn_fold_tickets_count(C)),
+                                                  st)
             else:
                 lib.dk_bn_stats_f32(x.data_ptr(), P, C, float(self.eps), float(self.run_momentum), int(first),
                                     mean.data_ptr(), std.data_ptr(), invstd.data_ptr(), rm.data_ptr(),
@@ -207,7 +208,8 @@ class BatchNormLayer(Layer):
             ws = workspace.get(nb)
             if self.sync_group is None:
                 lib.dk_bn_bwd_from_partials_f32(part.data_ptr(), nrows, C, float(P), dgamma.data_ptr(),
-                                                dbeta.data_ptr(), k12.data_ptr(), ws, nb, st)
+                                                dbeta.data_ptr(), k12.data_ptr(), ws, nb,
+                                                tickets.get(lib.dk_bn_fold_tickets_count(C)), st)
             else:
                 import torch.distributed as dist
                 local = torch.empty(2 * C, dtype=torch.float64, device=x.device)

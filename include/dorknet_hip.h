@@ -10,7 +10,7 @@
  *   - `stream` is a hipStream_t passed as void*; all work is stream-ordered on it;
  *   - the int return value is a hipError_t (0 = success); 10001 = bad arguments,
  *     10002 = workspace too small.  Nothing is checked on the device.  Exceptions: the
- *     count queries (*_blocks, *_rows, dk_abi_version, dk_debug_*) return a count;
+ *     count queries (*_blocks, *_rows, *_count, dk_abi_version, dk_debug_*) return a count;
  *   - reentrant: no global mutable state (except the dk_debug_* tuning knob).
  *
  * Each block cites the reference interface it replaces (file:line under the reference
@@ -159,17 +159,23 @@ int dk_bn_stats_finalize_f32(const void* part, int nblk, int C, double count, fl
 size_t dk_bn_stats_workspace_bytes(int P, int C);
 int dk_bn_stats_f32(const float* x, int P, int C, float eps, float momentum, int first, float* mean, float* std_, float* invstd, float* run_mean, float* run_std, void* ws, size_t ws_bytes, void* stream);
 /* Statistics from a producer's partial sums (stats of *_fwd_ex_f32): fixed-order fold of
- * part[nblk][2][C] (workspace: dk_bn_partials_workspace_bytes) then the finalize above;
+ * part[nblk][2][C] (workspace: dk_bn_partials_workspace_bytes) then the finalize above.
+ * tickets (optional, here and in dk_bn_bwd_from_partials_f32): >= dk_bn_fold_tickets_count(C)
+ * words that the caller zeroed once; every call leaves them zero.  With them a fold of more
+ * than 256 rows runs in ONE launch (the last block to arrive at an agent-scope ticket folds
+ * the level-2 rows), without them in one launch per level.  Calls sharing ticket words must
+ * not run concurrently (e.g. on two streams);
  * dk_bn_reduce_partials_f64 gives the [2][C] sums a SyncBN rank all-reduces. */
 size_t dk_bn_partials_workspace_bytes(int nblk, int C);
-int dk_bn_stats_from_partials_f32(const void* part, int nblk, int C, double count, float eps, float momentum, int first, float* mean, float* std_, float* invstd, float* run_mean, float* run_std, void* ws, size_t ws_bytes, void* stream);
+int dk_bn_fold_tickets_count(int C);
+int dk_bn_stats_from_partials_f32(const void* part, int nblk, int C, double count, float eps, float momentum, int first, float* mean, float* std_, float* invstd, float* run_mean, float* run_std, void* ws, size_t ws_bytes, unsigned* tickets, void* stream);
 int dk_bn_reduce_partials_f64(const void* part, int nblk, int C, void* out, void* ws, size_t ws_bytes, void* stream);
 /* Backward stage 2 from partials of any origin ([nblk][2][C]: dk_bn_bwd_partial_f64, a
  * consumer's *_dgrad_ex_f32, dk_relu_bwd_bn_partial_f64): dgamma, dbeta and k12 for
  * dk_bn_bwd_apply_f32.  The fused post-residual ReLU backward (residual_block.py:85-86) +
  * stage 1 of the backward of the BN feeding the join: dx = mask ? dy : 0 and part (sized
  * dk_bn_workspace_bytes(P, C), dk_bn_partial_blocks(P, C) rows). */
-int dk_bn_bwd_from_partials_f32(const void* part, int nblk, int C, double count, float* dgamma, float* dbeta, float* k12, void* ws, size_t ws_bytes, void* stream);
+int dk_bn_bwd_from_partials_f32(const void* part, int nblk, int C, double count, float* dgamma, float* dbeta, float* k12, void* ws, size_t ws_bytes, unsigned* tickets, void* stream);
 int dk_relu_bwd_bn_partial_f64(const float* dy, const uint8_t* mask, const float* x, int P, int C, const float* mean, const float* invstd, const float* gamma, const float* beta, int relu, float* dx, void* part, size_t part_bytes, void* stream);
 int dk_bn_infer_params_f32(const float* run_std, int C, float* invstd, void* stream);
 int dk_bn_apply_f32(const float* x, long long numel, int C, const float* mean, const float* invstd, const float* gamma, const float* beta, int relu, float* y, uint8_t* mask, void* stream);

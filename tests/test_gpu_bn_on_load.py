@@ -6,7 +6,7 @@ import numpy as np
 import pytest
 import torch
 
-from dorknet_amd._hip import lib, stream_handle, workspace
+from dorknet_amd._hip import lib, stream_handle, tickets, workspace
 
 pytestmark = pytest.mark.gpu
 
@@ -161,7 +161,7 @@ def _stats_pair(y, part, rows, C):
             nb = lib.dk_bn_partials_workspace_bytes(rows, C)
             lib.dk_bn_stats_from_partials_f32(part.data_ptr(), rows, C, float(P), 1e-5, 0.95, 1, mean.data_ptr(),
                                               std.data_ptr(), invstd.data_ptr(), rm.data_ptr(), rs.data_ptr(),
-                                              workspace.get(nb), nb, st)
+                                              workspace.get(nb), nb, 0, st)
         else:
             nb = lib.dk_bn_stats_workspace_bytes(P, C)
             lib.dk_bn_stats_f32(y.data_ptr(), P, C, 1e-5, 0.95, 1, mean.data_ptr(), std.data_ptr(),
@@ -223,7 +223,7 @@ def _bwd_finalize(part, rows, C, P):
     dg, db, k12 = torch.empty(C, device="cuda"), torch.empty(C, device="cuda"), torch.empty(2 * C, device="cuda")
     nb = lib.dk_bn_partials_workspace_bytes(rows, C)
     lib.dk_bn_bwd_from_partials_f32(part.data_ptr(), rows, C, float(P), dg.data_ptr(), db.data_ptr(), k12.data_ptr(),
-                                    workspace.get(nb), nb, st)
+                                    workspace.get(nb), nb, 0, st)
     return dg, db, k12
 
 
@@ -343,3 +343,29 @@ def test_dgrad_residual_bitwise(kind, stride):
     ref = torch.empty_like(r)
     lib.dk_add_f32(dx0.data_ptr(), r.data_ptr(), r.numel(), 0, ref.data_ptr(), 0, st)
     same(ref, dx1)
+
+
+@pytest.mark.parametrize("rows,C", [(300, 16), (1000, 64), (12544, 64), (40000, 200), (65536, 48)])
+def test_one_launch_fold(rows, C):
+    """With tickets, a fold of > 256 partial rows runs in one launch (the last block to arrive
+    folds the level-2 rows): bit-identical to the launch-per-level fold, twice in a row (the
+    tickets are left zeroed), for statistics and backward coefficients."""
+    rng = np.random.RandomState(rows % 97)
+    part = torch.as_tensor(rng.randn(rows, 2, C) * 100 + 1000, dtype=torch.float64, device="cuda")
+    part[:, 1, :] = part[:, 1, :].abs() * 1000
+    st = stream_handle()
+    nb = lib.dk_bn_partials_workspace_bytes(rows, C)
+    tk = tickets.get(lib.dk_bn_fold_tickets_count(C))
+    res = []
+    for t in (0, tk, tk):
+        o = [torch.full((C,), 3.0, device="cuda") for _ in range(5)]
+        lib.dk_bn_stats_from_partials_f32(part.data_ptr(), rows, C, float(rows * 64), 1e-5, 0.95, 0,
+                                          *[v.data_ptr() for v in o], workspace.get(nb), nb, t, st)
+        b = [torch.empty(C, device="cuda"), torch.empty(C, device="cuda"), torch.empty(2 * C, device="cuda")]
+        lib.dk_bn_bwd_from_partials_f32(part.data_ptr(), rows, C, float(rows * 64), *[v.data_ptr() for v in b],
+                                        workspace.get(nb), nb, t, st)
+        res.append(o + b)
+    torch.cuda.synchronize()
+    for r in res[1:]:
+        for u, v in zip(res[0], r):
+            same(u, v)
