@@ -44,6 +44,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default="gpurun_out/gemm_tune.json")
     ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--fused-only", action="store_true", help="pw shapes: only the fused (ex / bnx) variants")
     args = ap.parse_args()
     st = torch.cuda.current_stream().cuda_stream
     nrow = lib.dk_debug_set_gemm_config(0, -1)
@@ -68,9 +69,32 @@ def main():
                 nb = lib.dk_pwconv_wgrad_workspace_bytes(N, OH, OH, K, C)
                 lib.dk_pwconv_wgrad_f32(dy.data_ptr(), x.data_ptr(), N, H, H, C, K, s, OH, OH, 0, 0.0, dw.data_ptr(),
                                         workspace.get(nb), nb, st)
+            # the fused variants the training step runs: BN on load + output statistics (fwd),
+            # BN-backward partials of the input BN (dgrad), BN on load (wgrad)
+            bnp = [torch.randn(C, device="cuda", generator=g), torch.rand(C, device="cuda", generator=g) + 0.5,
+                   torch.randn(C, device="cuda", generator=g), torch.randn(C, device="cuda", generator=g)]
+            bna = tuple(t.data_ptr() for t in bnp) + (1,)
+            part = torch.empty(max(lib.dk_pwconv_fwd_stats_rows(N, OH, OH, K, C) * 2 * K,
+                                   lib.dk_pwconv_dgrad_stats_rows(N, OH, OH, K, C) * 2 * C), dtype=torch.float64,
+                               device="cuda")
+            fwdx = lambda: lib.dk_pwconv_fwd_ex_f32(x.data_ptr(), N, H, H, C, w.data_ptr(), K, s, 0, y.data_ptr(), OH,
+                                                    OH, *bna, part.data_ptr(), st)
+
+            def dgrx():
+                if s != 1:
+                    raise RuntimeError("strided: not fused")
+                lib.dk_pwconv_dgrad_ex_f32(dy.data_ptr(), N, OH, OH, K, w.data_ptr(), C, s, dx.data_ptr(), 0,
+                                           x.data_ptr(), *bna, part.data_ptr(), st)
+
+            def wgrx():
+                nb = lib.dk_pwconv_wgrad_workspace_bytes(N, OH, OH, K, C)
+                lib.dk_pwconv_wgrad_bnx_f32(dy.data_ptr(), x.data_ptr(), N, H, H, C, K, s, OH, OH, 0, 0.0,
+                                            dw.data_ptr(), workspace.get(nb), nb, *bna, st)
             work = {"fwd": perfmodel.work("dk_pwconv_fwd_f32", (0, N, H, H, C, 0, K, s, 0, 0, OH, OH, 0)),
                     "dgrad": perfmodel.work("dk_pwconv_dgrad_f32", (0, N, OH, OH, K, 0, C, s, 0, 0)),
                     "wgrad": perfmodel.work("dk_pwconv_wgrad_f32", (0, 0, N, H, H, C, K, s, OH, OH, 0, 0, 0, 0, 0, 0))}
+            work["fwdx"], work["dgrx"], work["wgrx"] = work["fwd"], work["dgrad"], work["wgrad"]
+            extra = (("fwdx", fwdx, 0), ("dgrx", dgrx, 0), ("wgrx", wgrx, 1))
         else:
             R, s, pd, Cr = sh["R"], sh["st"], sh["pad"], sh["Creal"]
             OH = int((H + 2 * pd - R) / s + 1)
@@ -100,7 +124,12 @@ def main():
             a = (0, N, H, H, C, 0, K, R, R, s, pd, 0, 0, OH, OH, 0)
             work = {"fwd": perfmodel.work("dk_conv2d_fwd_f32", a), "dgrad": perfmodel.work("dk_conv2d_fwd_f32", a),
                     "wgrad": perfmodel.work("dk_conv2d_fwd_f32", a)}
-        for op, fn, kind, n in (("fwd", fwd, 0, nrow), ("dgrad", dgr, 0, nrow), ("wgrad", wgr, 1, nsplit)):
+            extra = ()
+        ops = [("fwd", fwd, 0), ("dgrad", dgr, 0), ("wgrad", wgr, 1)] + list(extra)
+        if args.fused_only:
+            ops = list(extra) or ops
+        for op, fn, kind in ops:
+            n = nrow if kind == 0 else nsplit
             row = {"shape": sh["name"], "op": op, "cfg": {}}
             for cfg in [-1] + list(range(n)):
                 lib.dk_debug_set_gemm_config(kind, cfg)
@@ -112,6 +141,8 @@ def main():
                 f, b = work[op]
                 row["cfg"][str(cfg)] = {"us": round(us, 1), "GBs": round(b / us / 1e3, 1), "TFs": round(f / us / 1e6, 1)}
             lib.dk_debug_set_gemm_config(kind, -1)
+            if not isinstance(row["cfg"].get("-1"), dict):
+                continue
             best = min((v["us"], k) for k, v in row["cfg"].items() if isinstance(v, dict) and k != "-1")
             row["best"] = best[1]
             results.append(row)
