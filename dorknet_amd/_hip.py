@@ -89,7 +89,8 @@ class _Lib:
             fn = getattr(lib, name)
             fn.restype = ctypes.c_size_t if ret == "size_t" else ctypes.c_int
             fn.argtypes = [_argtype(t) for t, _ in params]
-            if ret == "int" and not name.endswith(("_blocks", "_version", "_rows", "_count")) and not name.startswith("dk_debug"):
+            counts = name.endswith(("_blocks", "_version", "_rows", "_count")) or name.startswith("dk_debug")
+            if ret == "int" and not counts:
                 fn.errcheck = _errcheck
         self._decls = decls
         self._lib = lib
@@ -122,25 +123,29 @@ def stream_handle() -> int:
 
 
 class Workspace:
-    """A grow-only device scratch buffer shared by kernels issued on one stream.
+    """Grow-only device scratch buffers, one per stream.
 
     Kernels on the same stream run in order, so consecutive launches may reuse the
     same bytes; torch's caching allocator keeps a replaced buffer alive until the
-    work queued before the replacement has run (same-stream reuse semantics).
+    work queued before the replacement has run (same-stream reuse semantics).  Work on
+    the weight-gradient side stream (see weight_grad_stream) gets its own buffer.
     """
 
     def __init__(self):
-        self._buf = None
+        self._bufs = {}
 
     def get(self, nbytes: int) -> int:
         nbytes = max(int(nbytes), 256)
-        if self._buf is None or self._buf.numel() < nbytes:
-            grow = nbytes if self._buf is None else max(nbytes, int(self._buf.numel() * 1.25))
-            self._buf = torch.empty(grow, dtype=torch.uint8, device="cuda")
-        return self._buf.data_ptr()
+        key = torch.cuda.current_stream().cuda_stream
+        buf = self._bufs.get(key)
+        if buf is None or buf.numel() < nbytes:
+            grow = nbytes if buf is None else max(nbytes, int(buf.numel() * 1.25))
+            buf = torch.empty(grow, dtype=torch.uint8, device="cuda")
+            self._bufs[key] = buf
+        return buf.data_ptr()
 
     def nbytes(self) -> int:
-        return 0 if self._buf is None else self._buf.numel()
+        return sum(b.numel() for b in self._bufs.values())
 
 
 workspace = Workspace()
@@ -160,3 +165,94 @@ class Tickets:
 
 
 tickets = Tickets()
+
+
+# ---------------------------------------------------------------------------------------
+# Weight gradients on a side stream.  A layer's weight gradient and its input gradient
+# are independent (both read dy); the input gradient is on the critical path of the
+# backward pass, the weight gradient only has to be done before the update (or its
+# all-reduce bucket).  Running the weight gradients on a second stream lets them fill the
+# GPU beside the small and tail-heavy kernels of the critical path.
+# DORKNET_ASYNC_WGRAD=0 keeps everything on the caller's stream.
+# ---------------------------------------------------------------------------------------
+_SIDE = {}
+_ASYNC_DEPTH = [0]
+
+
+def async_wgrad_enabled() -> bool:
+    """Side-stream weight gradients are used only inside async_weight_grads() (the network /
+    data-parallel backward), which joins them before it returns: a layer's backward called
+    on its own keeps the reference's contract that grads are final when it returns."""
+    return _ASYNC_DEPTH[0] > 0 and os.environ.get("DORKNET_ASYNC_WGRAD", "1") != "0"
+
+
+def side_stream():
+    dev = torch.cuda.current_device()
+    s = _SIDE.get(dev)
+    if s is None:
+        s = _SIDE[dev] = torch.cuda.Stream(device=dev)
+    return s
+
+
+class weight_grad_stream:
+    """with weight_grad_stream(dy, x, ...): launches inside go to the side stream, after
+    everything already queued on the current stream.  The listed tensors are marked as in
+    use by the side stream (so the caching allocator does not recycle them early)."""
+
+    def __init__(self, *tensors):
+        self.tensors = tensors
+        self.ctx = None
+
+    def __enter__(self):
+        if not async_wgrad_enabled():
+            return self
+        main = torch.cuda.current_stream()
+        side = side_stream()
+        if main == side:
+            return self
+        side.wait_stream(main)
+        self.ctx = torch.cuda.stream(side)
+        self.ctx.__enter__()
+        return self
+
+    def __exit__(self, *exc):
+        if self.ctx is None:
+            return False
+        self.ctx.__exit__(*exc)
+        side = side_stream()
+        for t in self.tensors:
+            if isinstance(t, torch.Tensor) and t.is_cuda:
+                t.record_stream(side)
+        return False
+
+
+class async_weight_grads:
+    """with async_weight_grads(): layers' weight gradients inside go to the side stream; the
+    outermost exit makes the current stream wait for them."""
+
+    def __enter__(self):
+        _ASYNC_DEPTH[0] += 1
+        return self
+
+    def __exit__(self, *exc):
+        _ASYNC_DEPTH[0] -= 1
+        if _ASYNC_DEPTH[0] == 0:
+            join_weight_grads()
+        return False
+
+
+def side_stream_context():
+    """torch.cuda.stream(side) while weight gradients run on the side stream (for work that
+    must follow them, e.g. a gradient all-reduce), else a no-op context."""
+    import contextlib
+    if async_wgrad_enabled():
+        return torch.cuda.stream(side_stream())
+    return contextlib.nullcontext()
+
+
+def join_weight_grads() -> None:
+    """Make the current stream wait for every weight gradient queued on the side stream."""
+    dev = torch.cuda.current_device() if torch.cuda.is_available() else None
+    s = _SIDE.get(dev)
+    if s is not None and s != torch.cuda.current_stream():
+        torch.cuda.current_stream().wait_stream(s)

@@ -17,7 +17,7 @@ from __future__ import annotations
 
 import torch
 
-from .._hip import lib, stream_handle, workspace
+from .._hip import lib, stream_handle, weight_grad_stream, workspace
 from .._tensor import empty_nhwc, ptr, to_nhwc
 from ._bn_input import BNOut
 from ._common import add_regulariser_grad, grad_buffer, init_weights, l2_strength
@@ -114,24 +114,27 @@ class ConvLayer(Layer):
         OH, OW = int(self.num_row_patches), int(self.num_col_patches)
         w = self.learned_params["weights"]
         P = N * OH * OW
-        if self.with_bias:
-            gb = grad_buffer(self, "bias", (K,))
-            nb = lib.dk_colsum_workspace_bytes(P, K)
-            lib.dk_colsum_f32(dy.data_ptr(), P, K, gb.data_ptr(), workspace.get(nb), nb, st)
-        # weight gradient (+ l2 folded in, convolution.py:93-100)
-        gw = grad_buffer(self, "weights", (K, C, R, S))
-        s = l2_strength(self.weight_regulariser)
-        nb = lib.dk_conv2d_wgrad_workspace_bytes(N, OH, OW, K, Cp, R, S)
-        if self._bn_in is not None:
-            lib.dk_conv2d_wgrad_bnx_f32(dy.data_ptr(), x.data_ptr(), N, H, W, Cp, C, K, R, S, self.stride,
+        # the weight gradient runs on the side stream (_hip.weight_grad_stream)
+        with weight_grad_stream(dy, x, *self._bn_tensors()):
+            sst = stream_handle()
+            if self.with_bias:
+                gb = grad_buffer(self, "bias", (K,))
+                nb = lib.dk_colsum_workspace_bytes(P, K)
+                lib.dk_colsum_f32(dy.data_ptr(), P, K, gb.data_ptr(), workspace.get(nb), nb, sst)
+            # weight gradient (+ l2 folded in, convolution.py:93-100)
+            gw = grad_buffer(self, "weights", (K, C, R, S))
+            s = l2_strength(self.weight_regulariser)
+            nb = lib.dk_conv2d_wgrad_workspace_bytes(N, OH, OW, K, Cp, R, S)
+            if self._bn_in is not None:
+                lib.dk_conv2d_wgrad_bnx_f32(dy.data_ptr(), x.data_ptr(), N, H, W, Cp, C, K, R, S, self.stride,
+                                            self.padding, OH, OW, w.data_ptr() if s else 0, s or 0.0, gw.data_ptr(),
+                                            workspace.get(nb), nb, *self._bn_in.bn_args(), sst)
+            else:
+                lib.dk_conv2d_wgrad_f32(dy.data_ptr(), x.data_ptr(), N, H, W, Cp, C, K, R, S, self.stride,
                                         self.padding, OH, OW, w.data_ptr() if s else 0, s or 0.0, gw.data_ptr(),
-                                        workspace.get(nb), nb, *self._bn_in.bn_args(), st)
-        else:
-            lib.dk_conv2d_wgrad_f32(dy.data_ptr(), x.data_ptr(), N, H, W, Cp, C, K, R, S, self.stride, self.padding,
-                                    OH, OW, w.data_ptr() if s else 0, s or 0.0, gw.data_ptr(), workspace.get(nb), nb,
-                                    st)
-        if s is None:
-            add_regulariser_grad(gw, w, self.weight_regulariser)
+                                        workspace.get(nb), nb, sst)
+            if s is None:
+                add_regulariser_grad(gw, w, self.weight_regulariser)
         # input gradient (convolution.py:101-117); shape = the forward input's shape
         Hin, Win = self.input_shape[2], self.input_shape[3]
         dx = empty_nhwc(N, C, Hin, Win)

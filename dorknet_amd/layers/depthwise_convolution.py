@@ -13,7 +13,7 @@ from __future__ import annotations
 
 import torch
 
-from .._hip import HipError, lib, stream_handle, workspace
+from .._hip import HipError, lib, stream_handle, weight_grad_stream, workspace
 from .._tensor import empty_nhwc, ptr, to_nhwc
 from ._bn_input import BNOut, add_residual, residual_operand
 from ._common import add_regulariser_grad, grad_buffer, init_weights, l2_strength
@@ -108,22 +108,26 @@ class DepthwiseConvLayer(Layer):
         OH, OW = int(self.num_row_patches), int(self.num_col_patches)
         P = N * OH * OW
         w = self.learned_params["weights"]
-        if self.with_bias:
-            gb = grad_buffer(self, "bias", (C,))
-            nb = lib.dk_colsum_workspace_bytes(P, C)
-            lib.dk_colsum_f32(dy.data_ptr(), P, C, gb.data_ptr(), workspace.get(nb), nb, st)
-        gw = grad_buffer(self, "weights", (C, R, S))
-        s = l2_strength(self.weight_regulariser)
-        nb = lib.dk_dwconv_wgrad_workspace_bytes(N, OH, OW, C, R, S)
-        if self._bn_in is not None:
-            lib.dk_dwconv_wgrad_bnx_f32(dy.data_ptr(), x.data_ptr(), N, H, W, C, R, S, self.stride, self.padding,
-                                        OH, OW, w.data_ptr() if s else 0, s or 0.0, gw.data_ptr(), workspace.get(nb),
-                                        nb, *self._bn_in.bn_args(), st)
-        else:
-            lib.dk_dwconv_wgrad_f32(dy.data_ptr(), x.data_ptr(), N, H, W, C, R, S, self.stride, self.padding, OH, OW,
-                                    w.data_ptr() if s else 0, s or 0.0, gw.data_ptr(), workspace.get(nb), nb, st)
-        if s is None:
-            add_regulariser_grad(gw, w, self.weight_regulariser)
+        # the weight gradient runs on the side stream (_hip.weight_grad_stream)
+        with weight_grad_stream(dy, x, *self._bn_tensors()):
+            sst = stream_handle()
+            if self.with_bias:
+                gb = grad_buffer(self, "bias", (C,))
+                nb = lib.dk_colsum_workspace_bytes(P, C)
+                lib.dk_colsum_f32(dy.data_ptr(), P, C, gb.data_ptr(), workspace.get(nb), nb, sst)
+            gw = grad_buffer(self, "weights", (C, R, S))
+            s = l2_strength(self.weight_regulariser)
+            nb = lib.dk_dwconv_wgrad_workspace_bytes(N, OH, OW, C, R, S)
+            if self._bn_in is not None:
+                lib.dk_dwconv_wgrad_bnx_f32(dy.data_ptr(), x.data_ptr(), N, H, W, C, R, S, self.stride,
+                                            self.padding, OH, OW, w.data_ptr() if s else 0, s or 0.0, gw.data_ptr(),
+                                            workspace.get(nb), nb, *self._bn_in.bn_args(), sst)
+            else:
+                lib.dk_dwconv_wgrad_f32(dy.data_ptr(), x.data_ptr(), N, H, W, C, R, S, self.stride, self.padding, OH,
+                                        OW, w.data_ptr() if s else 0, s or 0.0, gw.data_ptr(), workspace.get(nb), nb,
+                                        sst)
+            if s is None:
+                add_regulariser_grad(gw, w, self.weight_regulariser)
         dx = empty_nhwc(N, C, H, W)
         nb = lib.dk_dwconv_dgrad_workspace_bytes(C, R, S)
         bn = self._bn_in

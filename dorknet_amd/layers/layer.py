@@ -39,6 +39,12 @@ class Layer:
                     d[k] = to_param(v)
         self.is_on_gpu = True
 
+    def _bn_tensors(self):
+        """Device tensors of the BNOut this layer's forward consumed (kept alive for work on
+        the weight-gradient side stream)."""
+        b = self._bn_in
+        return () if b is None else (b.x, b.mean, b.invstd, b.gamma, b.beta)
+
     def _require_on_gpu(self):
         if not self.is_on_gpu:
             raise RuntimeError(

@@ -14,7 +14,7 @@ from __future__ import annotations
 
 import torch
 
-from .._hip import lib, stream_handle, workspace
+from .._hip import lib, stream_handle, weight_grad_stream, workspace
 from .._tensor import empty_nhwc, ptr, to_nhwc
 from ._bn_input import BNOut, add_residual, residual_operand
 from ._common import add_regulariser_grad, grad_buffer, init_weights, l2_strength
@@ -103,22 +103,26 @@ class PointwiseConvLayer(Layer):
         OH, OW = self.out_hw
         P = N * OH * OW
         w = self.learned_params["weights"]
-        if self.with_bias:
-            gb = grad_buffer(self, "bias", (K,))
-            nb = lib.dk_colsum_workspace_bytes(P, K)
-            lib.dk_colsum_f32(dy.data_ptr(), P, K, gb.data_ptr(), workspace.get(nb), nb, st)
-        gw = grad_buffer(self, "weights", (K, C))
-        l2s = l2_strength(self.weight_regulariser)
-        nb = lib.dk_pwconv_wgrad_workspace_bytes(N, OH, OW, K, C)
-        if self._bn_in is not None:
-            lib.dk_pwconv_wgrad_bnx_f32(dy.data_ptr(), x.data_ptr(), N, H, W, C, K, s, OH, OW,
+        # the weight gradient runs on the side stream (_hip.weight_grad_stream)
+        with weight_grad_stream(dy, x, *self._bn_tensors()):
+            sst = stream_handle()
+            if self.with_bias:
+                gb = grad_buffer(self, "bias", (K,))
+                nb = lib.dk_colsum_workspace_bytes(P, K)
+                lib.dk_colsum_f32(dy.data_ptr(), P, K, gb.data_ptr(), workspace.get(nb), nb, sst)
+            gw = grad_buffer(self, "weights", (K, C))
+            l2s = l2_strength(self.weight_regulariser)
+            nb = lib.dk_pwconv_wgrad_workspace_bytes(N, OH, OW, K, C)
+            if self._bn_in is not None:
+                lib.dk_pwconv_wgrad_bnx_f32(dy.data_ptr(), x.data_ptr(), N, H, W, C, K, s, OH, OW,
+                                            w.data_ptr() if l2s else 0, l2s or 0.0, gw.data_ptr(), workspace.get(nb),
+                                            nb, *self._bn_in.bn_args(), sst)
+            else:
+                lib.dk_pwconv_wgrad_f32(dy.data_ptr(), x.data_ptr(), N, H, W, C, K, s, OH, OW,
                                         w.data_ptr() if l2s else 0, l2s or 0.0, gw.data_ptr(), workspace.get(nb), nb,
-                                        *self._bn_in.bn_args(), st)
-        else:
-            lib.dk_pwconv_wgrad_f32(dy.data_ptr(), x.data_ptr(), N, H, W, C, K, s, OH, OW, w.data_ptr() if l2s else 0,
-                                    l2s or 0.0, gw.data_ptr(), workspace.get(nb), nb, st)
-        if l2s is None:
-            add_regulariser_grad(gw, w, self.weight_regulariser)
+                                        sst)
+            if l2s is None:
+                add_regulariser_grad(gw, w, self.weight_regulariser)
         dx = empty_nhwc(N, C, OH * s, OW * s)  # widened shape, pointwise_convolution.py:68-72
         bn = self._bn_in
         res = residual_operand(residual, dx)

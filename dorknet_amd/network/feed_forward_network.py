@@ -23,6 +23,7 @@ from ..layers.losses import SoftmaxWithCrossEntropy  # noqa: F401
 from ..layers.pointwise_convolution import PointwiseConvLayer  # noqa: F401
 from ..layers.pooling import GlobalAveragePoolingLayer  # noqa: F401
 from ..layers.residual_block import ResidualBlock  # noqa: F401
+from .._hip import async_weight_grads
 from .._tensor import as_device
 
 
@@ -152,7 +153,8 @@ class FeedForwardNetwork:
             upstream_dx = self.loss_layer.backward()
         else:
             raise ValueError("Network doesn't have a loss, can't run backward pass.")
-        chain_backward(self._steps, upstream_dx)
+        with async_weight_grads():  # weight gradients on the side stream, joined on exit
+            chain_backward(self._steps, upstream_dx)
 
     def test(self, data_loader, batch_size, test_set_size):
         from tqdm import tqdm

@@ -20,6 +20,7 @@ from __future__ import annotations
 import torch
 import torch.distributed as dist
 
+from ._hip import async_weight_grads, side_stream_context
 from .layers._chain import chain_backward
 
 
@@ -106,13 +107,20 @@ class DataParallel:
     def _launch(self, lo, hi):
         view = self.flat[lo:hi]
         if view.is_cuda:
-            work = dist.all_reduce(view, op=dist.ReduceOp.AVG, group=self.group, async_op=True)
+            # issued from the weight-gradient side stream (when in use): RCCL then waits for
+            # the wgrad kernels that wrote this bucket, not for the whole critical path
+            with side_stream_context():
+                work = dist.all_reduce(view, op=dist.ReduceOp.AVG, group=self.group, async_op=True)
         else:  # gloo (CPU tests): no AVG; sum then scale after wait
             work = dist.all_reduce(view, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
         self._works.append((work, view))
 
     def backward(self):
         """network.backward() with gradient all-reduce overlapped per bucket."""
+        with async_weight_grads():
+            self._backward()
+
+    def _backward(self):
         net = self.network
         dy = net.loss_layer.backward()
         steps = net._steps
