@@ -1,0 +1,66 @@
+"""Weight gradients on the side stream (dorknet_amd._hip.weight_grad_stream): the network
+backward with DORKNET_ASYNC_WGRAD=1 must give bit-identical gradients to the single-stream
+run (same kernels, only their stream changes), and the data-parallel backward, whose
+RCCL buckets are issued from the side stream, must deliver them through the flat buffer
+(RCCL, world size 1 on the one GPU: the average is the identity)."""
+import socket
+
+import numpy as np
+import pytest
+import torch
+
+from tests._convert import all_layers
+
+pytestmark = pytest.mark.gpu
+
+
+def _grads(net):
+    return [l.grads[k].detach().clone() for l in all_layers(net.layers) for k in sorted(l.grads or {})]
+
+
+def _step(net, X, onehot, dp=None):
+    net.forward(torch.as_tensor(X, device="cuda"), torch.as_tensor(onehot, device="cuda"))
+    (dp or net).backward()
+    return _grads(net)
+
+
+def test_async_weight_grads_bitwise(monkeypatch):
+    from examples.resnet18_depsep import ResNet18, synthetic_batch
+    X, _, onehot = synthetic_batch(4, seed=7)
+    np.random.seed(9)
+    net = ResNet18("r18")
+    net.to_gpu()
+    runs = []
+    for flag in ("1", "0", "1"):
+        monkeypatch.setenv("DORKNET_ASYNC_WGRAD", flag)
+        runs.append(_step(net, X, onehot))
+    torch.cuda.synchronize()
+    for other in runs[1:]:
+        for a, b in zip(runs[0], other):
+            assert torch.equal(a, b)
+
+
+def test_data_parallel_rccl_world1():
+    import torch.distributed as dist
+    from dorknet_amd.parallel import DataParallel
+    from examples.resnet18_depsep import ResNet18, synthetic_batch
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    dist.init_process_group("nccl", init_method="tcp://127.0.0.1:%d" % port, rank=0, world_size=1)
+    try:
+        X, _, onehot = synthetic_batch(4, seed=8)
+        np.random.seed(10)
+        net = ResNet18("r18")
+        net.to_gpu()
+        ref = _step(net, X, onehot)
+        dp = DataParallel(net, bucket_bytes=1 << 20)
+        got = _step(net, X, onehot, dp)
+        torch.cuda.synchronize()
+        for a, b in zip(ref, got):
+            assert torch.equal(a, b)
+        assert all(l.grads[k].data_ptr() >= dp.flat.data_ptr() for l in all_layers(net.layers)
+                   for k in (l.grads or {}))
+    finally:
+        dist.destroy_process_group()
