@@ -506,7 +506,7 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const double* __re
 
 // dx = gamma * invstd * (dy_e - k1 - x_hat * k2)   (batch_norm.py:125-156, rearranged:
 // (1/M) * X_demean / std^2 * sum(dy * X_demean) == x_hat * sum(dy * x_hat) / M)
-template <int V>
+template <int V, int U = 4, bool NT = false>
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const float* __restrict__ x, const float* __restrict__ dy,
                                                            int P, int C, int ppb, const float* __restrict__ mean,
                                                            const float* __restrict__ invstd,
@@ -541,21 +541,24 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const float* __restri
       const float xh = (xe - mu[e]) * is[e];
       set_el(o, e, f[e] * (ge - k1[e] - xh * k2[e]));
     }
-    VT::store(dx + off, o);
+    if constexpr (NT && V == 4)
+      __builtin_nontemporal_store(o, reinterpret_cast<f32x4*>(dx + off));
+    else
+      VT::store(dx + off, o);
   };
   const int p0 = blockIdx.x * ppb, p1 = min(P, p0 + ppb);
   const int PL = g.PL;
   int p = p0 + pl;
-  for (; p + 3 * PL < p1; p += 4 * PL) {
-    typename VT::T xv[4], gv[4];
+  for (; p + (U - 1) * PL < p1; p += U * PL) {
+    typename VT::T xv[U], gv[U];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < U; ++u) {
       const size_t off = (size_t)(p + u * PL) * C + c0;
       xv[u] = VT::load(x + off);
       gv[u] = VT::load(dy + off);
     }
 #pragma unroll
-    for (int u = 0; u < 4; ++u) one(xv[u], gv[u], (size_t)(p + u * PL) * C + c0);
+    for (int u = 0; u < U; ++u) one(xv[u], gv[u], (size_t)(p + u * PL) * C + c0);
   }
   for (; p < p1; p += PL) {
     const size_t off = (size_t)p * C + c0;
@@ -581,6 +584,12 @@ static int bn_blocks(int P, int C) {
 }
 
 // Blocks for the streaming apply passes (no partials to keep small): up to 4096.
+// Launch variant of dk_bn_bwd_apply_f32 (dk_debug_set_ew_variant).  Default 22 = rows in
+// flight 4, nontemporal dx stores, 8 rows per pixel lane, up to 16384 blocks: measured
+// best or within 1 % of best on every ResNet BatchNorm shape (scripts/ew_tune.py; -10 % on
+// res1/res3 vs the row-loop defaults of the other BN passes).
+static int g_ew_variant = 22;
+
 static int bn_apply_blocks(int P, int C, int V) {
   const RowGeom g = row_geom(C, V);
   int nblk = cdiv(P, g.PL * 16);
@@ -658,6 +667,12 @@ DK_API size_t dk_bn_partials_workspace_bytes(int nblk, int C) {
   size_t rows = 0;
   for (int n = nblk; n > kFoldRows; n = cdiv(n, kFoldRows)) rows += (size_t)cdiv(n, kFoldRows);
   return (rows > 0 ? rows : 1) * 2 * C * sizeof(double);
+}
+
+// Tuning knob (not thread-safe): launch variant of dk_bn_bwd_apply_f32 (-1 = built-in).
+DK_API int dk_debug_set_ew_variant(int v) {
+  g_ew_variant = v < 0 ? 22 : v;
+  return 32;
 }
 
 DK_API int dk_bn_fold_tickets_count(int C) { return C < 1 ? 0 : cdiv(C, 64); }
@@ -809,10 +824,28 @@ DK_API int dk_bn_bwd_apply_f32(const float* x, const float* dy, long long numel,
   const bool vec = vec_ok(x, C) && vec_ok(dy, C) && vec_ok(dx, C);
   const int V = vec ? 4 : 1;
   const RowGeom g = row_geom(C, V);
-  const int nblk = bn_apply_blocks(P, C, V);
+  const int var = g_ew_variant;
+  int nblk = bn_apply_blocks(P, C, V);
+  if (var >= 0) {  // tuning knob: rows per pixel lane 16 / 8 / 32 / 64, cap 4096 / 16384
+    const int rpl[4] = {16, 8, 32, 64};
+    nblk = cdiv(P, g.PL * rpl[(var >> 2) & 3]);
+    const int cap = (var & 16) ? 16384 : 4096;
+    nblk = nblk < 1 ? 1 : (nblk > cap ? cap : nblk);
+  }
   const dim3 grid(nblk, cdiv(g.CG, g.cgt));
   const int ppb = cdiv(P, nblk);
-  if (vec)
+  if (vec && var >= 0) {
+#define BBA(U_, NT_)                                                                                              \
+  hipLaunchKernelGGL((bn_bwd_apply_kernel<4, U_, NT_>), grid, dim3(256), 0, as_stream(stream), x, dy, P, C, ppb, mean, \
+                     invstd, gamma, beta, relu, k12, dx)
+    switch (var & 3) {
+      case 0: BBA(4, false); break;
+      case 1: BBA(8, false); break;
+      case 2: BBA(4, true); break;
+      default: BBA(8, true); break;
+    }
+#undef BBA
+  } else if (vec)
     hipLaunchKernelGGL(bn_bwd_apply_kernel<4>, grid, dim3(256), 0, as_stream(stream), x, dy, P, C, ppb, mean, invstd,
                        gamma, beta, relu, k12, dx);
   else

@@ -36,6 +36,10 @@ int dk_abi_version(void);
  * `cfg` for kind 0 = forward/dgrad problems or 1 = split-K weight-gradient problems;
  * cfg = -1 restores the built-in heuristic.  Returns the number of configurations. */
 int dk_debug_set_gemm_config(int kind, int cfg);
+/* Tuning knob (same caveats): launch variant of dk_bn_bwd_apply_f32 (bits 0-1: rows in flight
+ * 4/8 x plain/nontemporal stores; bits 2-3: rows per lane 16/8/32/64; bit 4: block cap 16384);
+ * -1 restores the default (22).  Returns the number of variants. */
+int dk_debug_set_ew_variant(int v);
 
 /* ---------------------------------------------------------------------------------------
  * Dense convolution, implicit GEMM on fp32 MFMA.
