@@ -754,7 +754,11 @@ static inline EpWiden ep_widen(float* out, int ldo, int OH, int OW, int st, cons
   X(8, 64, 64, 32, 2, 2)   \
   X(9, 256, 128, 16, 4, 2) \
   X(10, 64, 64, 64, 2, 2)  \
-  X(11, 128, 64, 64, 2, 1)
+  X(11, 128, 64, 64, 2, 1) \
+  X(12, 64, 128, 16, 2, 2) \
+  X(13, 64, 128, 32, 2, 2) \
+  X(14, 128, 64, 16, 2, 2) \
+  X(15, 128, 64, 32, 2, 2)
 #define DK_SPLITK_CONFIGS(X) \
   X(0, 64, 64, 16, 2, 2)     \
   X(1, 64, 64, 32, 2, 2)     \
