@@ -12,7 +12,9 @@ Prints ONE JSON line (rank 0).  Besides the driver's contract fields it carries
   cpu_baseline  -- the reference's CPU path restated (oracle/cpu_path.py: C/OpenMP versions
                    of its Cython kernels + numpy BLAS), timed on this host at N=1 on a small
                    sample of the same workload;
-  breakdown     -- per entry point: ms per step and roofline fraction (one instrumented step).
+  breakdown     -- per entry point: ms per step and roofline fraction (one instrumented step,
+                   run single-stream; the timed steps run the weight gradients on a side
+                   stream, so the breakdown sums to more than ms_per_step).
 """
 from __future__ import annotations
 
@@ -228,8 +230,18 @@ def main():
 
     breakdown, dominant = None, None
     if not args.no_roofline:
-        with Instrument(perfmodel.MODEL.keys()) as ins:
-            step()
+        # the per-entry attribution step runs single-stream (weight gradients not on the side
+        # stream), so each entry's events bracket only its own kernels
+        prev = os.environ.get("DORKNET_ASYNC_WGRAD")
+        os.environ["DORKNET_ASYNC_WGRAD"] = "0"
+        try:
+            with Instrument(perfmodel.MODEL.keys()) as ins:
+                step()
+        finally:
+            if prev is None:
+                os.environ.pop("DORKNET_ASYNC_WGRAD")
+            else:
+                os.environ["DORKNET_ASYNC_WGRAD"] = prev
         summ = ins.summary()
         dominant = max(summ, key=lambda n: summ[n]["ms"])
         tot = sum(s["ms"] for s in summ.values())
