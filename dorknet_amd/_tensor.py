@@ -30,8 +30,18 @@ def as_device(x, dtype=F32) -> torch.Tensor:
     return torch.as_tensor(np.asarray(x), dtype=dtype, device=device())
 
 
-def empty_nhwc(n: int, c: int, h: int, w: int) -> torch.Tensor:
-    return torch.empty((n, c, h, w), dtype=F32, device=device(), memory_format=torch.channels_last)
+BF16 = torch.bfloat16
+
+
+def act_dtype(x) -> torch.dtype:
+    """Storage type of an activation: bf16 if the tensor (or a BNOut's raw input) is bf16
+    (BASELINE config 5: the layers then run their _bf16 entry points), else fp32."""
+    t = getattr(x, "x", x) if hasattr(x, "materialize") else x
+    return BF16 if isinstance(t, torch.Tensor) and t.dtype == BF16 else F32
+
+
+def empty_nhwc(n: int, c: int, h: int, w: int, dtype=F32) -> torch.Tensor:
+    return torch.empty((n, c, h, w), dtype=dtype, device=device(), memory_format=torch.channels_last)
 
 
 def is_nhwc(x: torch.Tensor) -> bool:
@@ -39,15 +49,22 @@ def is_nhwc(x: torch.Tensor) -> bool:
 
 
 def to_nhwc(x, cpad: int = 1) -> torch.Tensor:
-    """Return a channels_last fp32 device tensor whose channel count is padded (with
-    zeros) up to a multiple of `cpad`.  No copy when `x` already qualifies."""
-    x = as_device(x)
+    """Return a channels_last device tensor (fp32, or bf16 for a bf16 input) whose channel
+    count is padded (with zeros) up to a multiple of `cpad`.  No copy when `x` already
+    qualifies."""
+    x = as_device(x, act_dtype(x))
     if x.dim() != 4:
         raise ValueError(f"expected a 4-D (N, C, H, W) tensor, got shape {tuple(x.shape)}")
     n, c, h, w = x.shape
     cp = -(-c // cpad) * cpad
     if cp == c and is_nhwc(x):
         return x
+    if x.dtype == BF16:
+        # layout plumbing for a bf16 input given in NCHW: a copy into channels_last (+ zero
+        # channels), no arithmetic
+        out = torch.zeros((n, cp, h, w), dtype=BF16, device=x.device, memory_format=torch.channels_last)
+        out[:, :c].copy_(x)
+        return out
     if cp == c and x.is_contiguous():
         src = x
     else:

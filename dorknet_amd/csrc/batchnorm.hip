@@ -20,19 +20,22 @@
 namespace dk {
 
 
-template <int V>
+// V elements of storage type E (float, or bf16_t for BASELINE config 5) as fp32 values.
+template <int V, class E = float>
 struct VecT;
-template <>
-struct VecT<4> {
+template <class E>
+struct VecT<4, E> {
   using T = f32x4;
-  __device__ static T load(const float* p) { return ld4(p); }
-  __device__ static void store(float* p, T v) { st4(p, v); }
+  __device__ static T load(const E* p) { return ld4(p); }
+  __device__ static void store(E* p, T v) { st4(p, v); }
+  __device__ static T stored(T v) { return rnd4<E>(v); }
 };
-template <>
-struct VecT<1> {
+template <class E>
+struct VecT<1, E> {
   using T = float;
-  __device__ static T load(const float* p) { return *p; }
-  __device__ static void store(float* p, T v) { *p = v; }
+  __device__ static T load(const E* p) { return ld1(p); }
+  __device__ static void store(E* p, T v) { st1(p, v); }
+  __device__ static T stored(T v) { return rnd1<E>(v); }
 };
 
 __device__ __forceinline__ float el(const f32x4& v, int e) { return v[e]; }
@@ -58,10 +61,10 @@ __host__ __device__ inline RowGeom row_geom(int C, int V) {
 // ---------------------------------------------------------------------------------------
 // forward statistics: part[blk][0][c] = sum x, part[blk][1][c] = sum x^2 (fp64)
 // ---------------------------------------------------------------------------------------
-template <int V>
-__global__ __launch_bounds__(256) void bn_stats_partial_kernel(const float* __restrict__ x, int P, int C, int ppb,
+template <int V, class E = float>
+__global__ __launch_bounds__(256) void bn_stats_partial_kernel(const E* __restrict__ x, int P, int C, int ppb,
                                                                double* __restrict__ part) {
-  using VT = VecT<V>;
+  using VT = VecT<V, E>;
   __shared__ double red[2][256][V];
   const RowGeom g = row_geom(C, V);
   const int tid = threadIdx.x;
@@ -73,7 +76,7 @@ __global__ __launch_bounds__(256) void bn_stats_partial_kernel(const float* __re
 #pragma unroll
   for (int e = 0; e < V; ++e) s[e] = q[e] = 0.0;
   if (active) {
-    const float* base = x + cg * V;
+    const E* base = x + cg * V;
     const int PL = g.PL;
     int p = p0 + pl;
     for (; p + 3 * PL < p1; p += 4 * PL) {
@@ -329,14 +332,14 @@ __global__ __launch_bounds__(1024) void bn_fold_kernel(const double* __restrict_
 // ---------------------------------------------------------------------------------------
 // forward apply: y = gamma * (x - mean) * invstd + beta  [+ ReLU, optional uint8 mask]
 // ---------------------------------------------------------------------------------------
-template <int V>
-__global__ __launch_bounds__(256) void bn_apply_kernel(const float* __restrict__ x, int P, int C, int ppb,
+template <int V, class E = float>
+__global__ __launch_bounds__(256) void bn_apply_kernel(const E* __restrict__ x, int P, int C, int ppb,
                                                        const float* __restrict__ mean,
                                                        const float* __restrict__ invstd,
                                                        const float* __restrict__ gamma,
                                                        const float* __restrict__ beta, int relu,
-                                                       float* __restrict__ y, uint8_t* __restrict__ mask) {
-  using VT = VecT<V>;
+                                                       E* __restrict__ y, uint8_t* __restrict__ mask) {
+  using VT = VecT<V, E>;
   const RowGeom g = row_geom(C, V);
   const int tid = threadIdx.x;
   const int cg = blockIdx.y * g.cgt + tid % g.cgt;
@@ -392,17 +395,17 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const float* __restrict__
 // MASKED: dy is the upstream gradient of a ReLU that follows (the post-residual join's,
 // residual_block.py:86): g = mask ? dy : 0 is written to gout and reduced -- the ReLU
 // backward and this BN's backward reduction in one pass.
-template <int V, bool MASKED = false>
-__global__ __launch_bounds__(256) void bn_bwd_partial_kernel(const float* __restrict__ x,
-                                                             const float* __restrict__ dy, int P, int C, int ppb,
+template <int V, bool MASKED = false, class E = float>
+__global__ __launch_bounds__(256) void bn_bwd_partial_kernel(const E* __restrict__ x,
+                                                             const E* __restrict__ dy, int P, int C, int ppb,
                                                              const float* __restrict__ mean,
                                                              const float* __restrict__ invstd,
                                                              const float* __restrict__ gamma,
                                                              const float* __restrict__ beta, int relu,
                                                              double* __restrict__ part,
                                                              const uint8_t* __restrict__ mask = nullptr,
-                                                             float* __restrict__ gout = nullptr) {
-  using VT = VecT<V>;
+                                                             E* __restrict__ gout = nullptr) {
+  using VT = VecT<V, E>;
   __shared__ double red[2][256][V];
   const RowGeom g = row_geom(C, V);
   const int tid = threadIdx.x;
@@ -506,14 +509,14 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const double* __re
 
 // dx = gamma * invstd * (dy_e - k1 - x_hat * k2)   (batch_norm.py:125-156, rearranged:
 // (1/M) * X_demean / std^2 * sum(dy * X_demean) == x_hat * sum(dy * x_hat) / M)
-template <int V, int U = 4, bool NT = false>
-__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const float* __restrict__ x, const float* __restrict__ dy,
+template <int V, int U = 4, bool NT = false, class E = float>
+__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const E* __restrict__ x, const E* __restrict__ dy,
                                                            int P, int C, int ppb, const float* __restrict__ mean,
                                                            const float* __restrict__ invstd,
                                                            const float* __restrict__ gamma,
                                                            const float* __restrict__ beta, int relu,
-                                                           const float* __restrict__ k12, float* __restrict__ dx) {
-  using VT = VecT<V>;
+                                                           const float* __restrict__ k12, E* __restrict__ dx) {
+  using VT = VecT<V, E>;
   const RowGeom g = row_geom(C, V);
   const int tid = threadIdx.x;
   const int cg = blockIdx.y * g.cgt + tid % g.cgt;
@@ -541,7 +544,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const float* __restri
       const float xh = (xe - mu[e]) * is[e];
       set_el(o, e, f[e] * (ge - k1[e] - xh * k2[e]));
     }
-    if constexpr (NT && V == 4)
+    if constexpr (NT && V == 4 && sizeof(E) == 4)
       __builtin_nontemporal_store(o, reinterpret_cast<f32x4*>(dx + off));
     else
       VT::store(dx + off, o);
@@ -599,6 +602,11 @@ static int bn_apply_blocks(int P, int C, int V) {
 }
 
 static inline bool vec_ok(const void* p, int C) { return (C % 4 == 0) && ((reinterpret_cast<uintptr_t>(p) & 15) == 0); }
+// 4-element (float4 / 4 x bf16) access allowed for this storage type
+template <class E>
+static inline bool vec_ok_e(const E* p, int C) {
+  return (C % 4 == 0) && ((reinterpret_cast<uintptr_t>(p) & (4 * sizeof(E) - 1)) == 0);
+}
 
 }  // namespace dk
 
@@ -610,20 +618,25 @@ DK_API size_t dk_bn_workspace_bytes(int P, int C) { return (size_t)bn_blocks(P, 
 static size_t bn_fold_offset(int P, int C) { return (size_t)bn_blocks(P, C) * 2 * C * sizeof(double); }
 
 // Stage 1 of forward statistics: part[nblk][2][C] (fp64 sum x, sum x^2) over x[P][C].
-DK_API int dk_bn_stats_partial_f64(const float* x, int P, int C, void* ws, size_t ws_bytes, void* stream) {
+template <class E>
+static int bn_stats_partial_t(const E* x, int P, int C, void* ws, size_t ws_bytes, void* stream) {
   if (ws_bytes < dk_bn_workspace_bytes(P, C)) return DK_ERR_WORKSPACE;
   const int nblk = bn_blocks(P, C);
   const int ppb = cdiv(P, nblk);
-  const bool vec = vec_ok(x, C);
+  const bool vec = vec_ok_e(x, C);
+  if (!vec && sizeof(E) != 4) return DK_ERR_ARGS;
   const RowGeom g = row_geom(C, vec ? 4 : 1);
   const dim3 grid(nblk, cdiv(g.CG, g.cgt));
   if (vec)
-    hipLaunchKernelGGL(bn_stats_partial_kernel<4>, grid, dim3(256), 0, as_stream(stream), x, P, C, ppb,
+    hipLaunchKernelGGL((bn_stats_partial_kernel<4, E>), grid, dim3(256), 0, as_stream(stream), x, P, C, ppb,
                        static_cast<double*>(ws));
   else
-    hipLaunchKernelGGL(bn_stats_partial_kernel<1>, grid, dim3(256), 0, as_stream(stream), x, P, C, ppb,
+    hipLaunchKernelGGL((bn_stats_partial_kernel<1, E>), grid, dim3(256), 0, as_stream(stream), x, P, C, ppb,
                        static_cast<double*>(ws));
   return launch_status();
+}
+DK_API int dk_bn_stats_partial_f64(const float* x, int P, int C, void* ws, size_t ws_bytes, void* stream) {
+  return bn_stats_partial_t(x, P, C, ws, ws_bytes, stream);
 }
 
 // out[2][C] = fixed-order sum of part[nblk][2][C].
@@ -644,16 +657,26 @@ DK_API int dk_bn_stats_finalize_f32(const void* part, int nblk, int C, double co
 }
 
 // Forward statistics (both stages).  x is [P][C] (NHWC with P = N*H*W, or [rows][features]).
-DK_API int dk_bn_stats_f32(const float* x, int P, int C, float eps, float momentum, int first, float* mean,
-                           float* std_, float* invstd, float* run_mean, float* run_std, void* ws, size_t ws_bytes,
-                           void* stream) {
+template <class E>
+static int bn_stats_t(const E* x, int P, int C, float eps, float momentum, int first, float* mean, float* std_,
+                      float* invstd, float* run_mean, float* run_std, void* ws, size_t ws_bytes, void* stream) {
   const int nblk = bn_blocks(P, C);
   if (ws_bytes < bn_fold_offset(P, C) + dk_bn_partials_workspace_bytes(nblk, C)) return DK_ERR_WORKSPACE;
-  int rc = dk_bn_stats_partial_f64(x, P, C, ws, ws_bytes, stream);
+  int rc = bn_stats_partial_t(x, P, C, ws, ws_bytes, stream);
   if (rc) return rc;
   return dk_bn_stats_from_partials_f32(ws, nblk, C, (double)P, eps, momentum, first, mean, std_, invstd, run_mean,
                                        run_std, static_cast<char*>(ws) + bn_fold_offset(P, C),
                                        ws_bytes - bn_fold_offset(P, C), nullptr, stream);
+}
+DK_API int dk_bn_stats_f32(const float* x, int P, int C, float eps, float momentum, int first, float* mean,
+                           float* std_, float* invstd, float* run_mean, float* run_std, void* ws, size_t ws_bytes,
+                           void* stream) {
+  return bn_stats_t(x, P, C, eps, momentum, first, mean, std_, invstd, run_mean, run_std, ws, ws_bytes, stream);
+}
+DK_API int dk_bn_stats_bf16(const bf16_t* x, int P, int C, float eps, float momentum, int first, float* mean,
+                            float* std_, float* invstd, float* run_mean, float* run_std, void* ws, size_t ws_bytes,
+                            void* stream) {
+  return bn_stats_t(x, P, C, eps, momentum, first, mean, std_, invstd, run_mean, run_std, ws, ws_bytes, stream);
 }
 
 // Workspace of dk_bn_stats_f32: the partials plus their fold rows.
@@ -734,42 +757,58 @@ DK_API int dk_bn_infer_params_f32(const float* run_std, int C, float* invstd, vo
 }
 
 // y = gamma * (x - mean) * invstd + beta  [+ ReLU; mask (uint8) may be null]
-DK_API int dk_bn_apply_f32(const float* x, long long numel, int C, const float* mean, const float* invstd,
-                           const float* gamma, const float* beta, int relu, float* y, uint8_t* mask, void* stream) {
+template <class E>
+static int bn_apply_t(const E* x, long long numel, int C, const float* mean, const float* invstd, const float* gamma,
+                      const float* beta, int relu, E* y, uint8_t* mask, void* stream) {
   const int P = (int)(numel / C);
-  const bool vec = vec_ok(x, C) && vec_ok(y, C);
+  const bool vec = vec_ok_e(x, C) && vec_ok_e(y, C);
+  if (!vec && sizeof(E) != 4) return DK_ERR_ARGS;
   const int V = vec ? 4 : 1;
   const RowGeom g = row_geom(C, V);
   const int nblk = bn_apply_blocks(P, C, V);
   const dim3 grid(nblk, cdiv(g.CG, g.cgt));
   const int ppb = cdiv(P, nblk);
   if (vec)
-    hipLaunchKernelGGL(bn_apply_kernel<4>, grid, dim3(256), 0, as_stream(stream), x, P, C, ppb, mean, invstd, gamma,
-                       beta, relu, y, mask);
+    hipLaunchKernelGGL((bn_apply_kernel<4, E>), grid, dim3(256), 0, as_stream(stream), x, P, C, ppb, mean, invstd,
+                       gamma, beta, relu, y, mask);
   else
-    hipLaunchKernelGGL(bn_apply_kernel<1>, grid, dim3(256), 0, as_stream(stream), x, P, C, ppb, mean, invstd, gamma,
-                       beta, relu, y, mask);
+    hipLaunchKernelGGL((bn_apply_kernel<1, E>), grid, dim3(256), 0, as_stream(stream), x, P, C, ppb, mean, invstd,
+                       gamma, beta, relu, y, mask);
   return launch_status();
+}
+DK_API int dk_bn_apply_f32(const float* x, long long numel, int C, const float* mean, const float* invstd,
+                           const float* gamma, const float* beta, int relu, float* y, uint8_t* mask, void* stream) {
+  return bn_apply_t(x, numel, C, mean, invstd, gamma, beta, relu, y, mask, stream);
+}
+DK_API int dk_bn_apply_bf16(const bf16_t* x, long long numel, int C, const float* mean, const float* invstd,
+                            const float* gamma, const float* beta, int relu, bf16_t* y, uint8_t* mask, void* stream) {
+  return bn_apply_t(x, numel, C, mean, invstd, gamma, beta, relu, y, mask, stream);
 }
 
 // Backward stage 1: part[nblk][2][C] = (sum dy_e, sum dy_e * x_hat); relu != 0 fuses the
 // following ReLU's backward (its mask is recomputed from x).
-DK_API int dk_bn_bwd_partial_f64(const float* x, const float* dy, int P, int C, const float* mean,
-                                 const float* invstd, const float* gamma, const float* beta, int relu, void* ws,
-                                 size_t ws_bytes, void* stream) {
+template <class E>
+static int bn_bwd_partial_t(const E* x, const E* dy, int P, int C, const float* mean, const float* invstd,
+                            const float* gamma, const float* beta, int relu, void* ws, size_t ws_bytes, void* stream) {
   if (ws_bytes < dk_bn_workspace_bytes(P, C)) return DK_ERR_WORKSPACE;
   const int nblk = bn_blocks(P, C);
   const int ppb = cdiv(P, nblk);
-  const bool vec = vec_ok(x, C) && vec_ok(dy, C);
+  const bool vec = vec_ok_e(x, C) && vec_ok_e(dy, C);
+  if (!vec && sizeof(E) != 4) return DK_ERR_ARGS;
   const RowGeom g = row_geom(C, vec ? 4 : 1);
   const dim3 grid(nblk, cdiv(g.CG, g.cgt));
   if (vec)
-    hipLaunchKernelGGL(bn_bwd_partial_kernel<4>, grid, dim3(256), 0, as_stream(stream), x, dy, P, C, ppb, mean,
-                       invstd, gamma, beta, relu, static_cast<double*>(ws));
+    hipLaunchKernelGGL((bn_bwd_partial_kernel<4, false, E>), grid, dim3(256), 0, as_stream(stream), x, dy, P, C, ppb,
+                       mean, invstd, gamma, beta, relu, static_cast<double*>(ws), nullptr, nullptr);
   else
-    hipLaunchKernelGGL(bn_bwd_partial_kernel<1>, grid, dim3(256), 0, as_stream(stream), x, dy, P, C, ppb, mean,
-                       invstd, gamma, beta, relu, static_cast<double*>(ws));
+    hipLaunchKernelGGL((bn_bwd_partial_kernel<1, false, E>), grid, dim3(256), 0, as_stream(stream), x, dy, P, C, ppb,
+                       mean, invstd, gamma, beta, relu, static_cast<double*>(ws), nullptr, nullptr);
   return launch_status();
+}
+DK_API int dk_bn_bwd_partial_f64(const float* x, const float* dy, int P, int C, const float* mean,
+                                 const float* invstd, const float* gamma, const float* beta, int relu, void* ws,
+                                 size_t ws_bytes, void* stream) {
+  return bn_bwd_partial_t(x, dy, P, C, mean, invstd, gamma, beta, relu, ws, ws_bytes, stream);
 }
 
 // ReLU backward (mask from the forward join) fused with stage 1 of the backward of the BN
@@ -817,11 +856,12 @@ DK_API int dk_bn_bwd_finalize_f32(const void* part_local, int nblk_local, const 
 }
 
 // Backward stage 3: dx = gamma * invstd * (dy_e - k1 - x_hat * k2).
-DK_API int dk_bn_bwd_apply_f32(const float* x, const float* dy, long long numel, int C, const float* mean,
-                               const float* invstd, const float* gamma, const float* beta, int relu,
-                               const float* k12, float* dx, void* stream) {
+template <class E>
+static int bn_bwd_apply_t(const E* x, const E* dy, long long numel, int C, const float* mean, const float* invstd,
+                          const float* gamma, const float* beta, int relu, const float* k12, E* dx, void* stream) {
   const int P = (int)(numel / C);
-  const bool vec = vec_ok(x, C) && vec_ok(dy, C) && vec_ok(dx, C);
+  const bool vec = vec_ok_e(x, C) && vec_ok_e(dy, C) && vec_ok_e(dx, C);
+  if (!vec && sizeof(E) != 4) return DK_ERR_ARGS;
   const int V = vec ? 4 : 1;
   const RowGeom g = row_geom(C, V);
   const int var = g_ew_variant;
@@ -836,7 +876,8 @@ DK_API int dk_bn_bwd_apply_f32(const float* x, const float* dy, long long numel,
   const int ppb = cdiv(P, nblk);
   if (vec && var >= 0) {
 #define BBA(U_, NT_)                                                                                              \
-  hipLaunchKernelGGL((bn_bwd_apply_kernel<4, U_, NT_>), grid, dim3(256), 0, as_stream(stream), x, dy, P, C, ppb, mean, \
+  hipLaunchKernelGGL((bn_bwd_apply_kernel<4, U_, NT_, E>), grid, dim3(256), 0, as_stream(stream), x, dy, P, C, ppb,   \
+                     mean, \
                      invstd, gamma, beta, relu, k12, dx)
     switch (var & 3) {
       case 0: BBA(4, false); break;
@@ -846,12 +887,22 @@ DK_API int dk_bn_bwd_apply_f32(const float* x, const float* dy, long long numel,
     }
 #undef BBA
   } else if (vec)
-    hipLaunchKernelGGL(bn_bwd_apply_kernel<4>, grid, dim3(256), 0, as_stream(stream), x, dy, P, C, ppb, mean, invstd,
-                       gamma, beta, relu, k12, dx);
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<4, 4, false, E>), grid, dim3(256), 0, as_stream(stream), x, dy, P, C, ppb,
+                       mean, invstd, gamma, beta, relu, k12, dx);
   else
-    hipLaunchKernelGGL(bn_bwd_apply_kernel<1>, grid, dim3(256), 0, as_stream(stream), x, dy, P, C, ppb, mean, invstd,
-                       gamma, beta, relu, k12, dx);
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<1, 4, false, E>), grid, dim3(256), 0, as_stream(stream), x, dy, P, C, ppb,
+                       mean, invstd, gamma, beta, relu, k12, dx);
   return launch_status();
+}
+DK_API int dk_bn_bwd_apply_f32(const float* x, const float* dy, long long numel, int C, const float* mean,
+                               const float* invstd, const float* gamma, const float* beta, int relu,
+                               const float* k12, float* dx, void* stream) {
+  return bn_bwd_apply_t(x, dy, numel, C, mean, invstd, gamma, beta, relu, k12, dx, stream);
+}
+DK_API int dk_bn_bwd_apply_bf16(const bf16_t* x, const bf16_t* dy, long long numel, int C, const float* mean,
+                                const float* invstd, const float* gamma, const float* beta, int relu,
+                                const float* k12, bf16_t* dx, void* stream) {
+  return bn_bwd_apply_t(x, dy, numel, C, mean, invstd, gamma, beta, relu, k12, dx, stream);
 }
 
 DK_API size_t dk_bn_bwd_workspace_bytes(int P, int C) {
@@ -859,18 +910,29 @@ DK_API size_t dk_bn_bwd_workspace_bytes(int P, int C) {
 }
 
 // Backward (all stages, local statistics).  Writes dgamma/dbeta [C] and dx [P][C].
-DK_API int dk_bn_bwd_f32(const float* x, const float* dy, int P, int C, const float* mean, const float* invstd,
-                         const float* gamma, const float* beta, int relu, float* dgamma, float* dbeta, float* dx,
-                         void* ws, size_t ws_bytes, void* stream) {
+template <class E>
+static int bn_bwd_t(const E* x, const E* dy, int P, int C, const float* mean, const float* invstd, const float* gamma,
+                    const float* beta, int relu, float* dgamma, float* dbeta, E* dx, void* ws, size_t ws_bytes,
+                    void* stream) {
   if (ws_bytes < dk_bn_bwd_workspace_bytes(P, C)) return DK_ERR_WORKSPACE;
   const int nblk = bn_blocks(P, C);
   char* base = static_cast<char*>(ws);
   float* k12 = reinterpret_cast<float*>(base + bn_fold_offset(P, C));
   const size_t fold_off = bn_fold_offset(P, C) + 2 * (size_t)C * sizeof(float);
-  int rc = dk_bn_bwd_partial_f64(x, dy, P, C, mean, invstd, gamma, beta, relu, ws, ws_bytes, stream);
+  int rc = bn_bwd_partial_t(x, dy, P, C, mean, invstd, gamma, beta, relu, ws, ws_bytes, stream);
   if (rc) return rc;
   rc = dk_bn_bwd_from_partials_f32(ws, nblk, C, (double)P, dgamma, dbeta, k12, base + fold_off, ws_bytes - fold_off,
                                    nullptr, stream);
   if (rc) return rc;
-  return dk_bn_bwd_apply_f32(x, dy, (long long)P * C, C, mean, invstd, gamma, beta, relu, k12, dx, stream);
+  return bn_bwd_apply_t(x, dy, (long long)P * C, C, mean, invstd, gamma, beta, relu, k12, dx, stream);
+}
+DK_API int dk_bn_bwd_f32(const float* x, const float* dy, int P, int C, const float* mean, const float* invstd,
+                         const float* gamma, const float* beta, int relu, float* dgamma, float* dbeta, float* dx,
+                         void* ws, size_t ws_bytes, void* stream) {
+  return bn_bwd_t(x, dy, P, C, mean, invstd, gamma, beta, relu, dgamma, dbeta, dx, ws, ws_bytes, stream);
+}
+DK_API int dk_bn_bwd_bf16(const bf16_t* x, const bf16_t* dy, int P, int C, const float* mean, const float* invstd,
+                          const float* gamma, const float* beta, int relu, float* dgamma, float* dbeta, bf16_t* dx,
+                          void* ws, size_t ws_bytes, void* stream) {
+  return bn_bwd_t(x, dy, P, C, mean, invstd, gamma, beta, relu, dgamma, dbeta, dx, ws, ws_bytes, stream);
 }

@@ -32,15 +32,8 @@ __global__ void dw_weight_rsc_kernel(const float* __restrict__ w, int C, int R, 
   wt[idx] = w[((size_t)c * R + r) * S + s];
 }
 
-// Buffer loads: out-of-range offsets (kOOB) return 0 in hardware, so the padding needs no
-// branches and every load of a thread can be in flight at once.
-constexpr uint32_t kOOB = 0x80000000u;
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const float* p, uint32_t bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p), (short)0, (int)bytes, 0x00020000);
-}
-__device__ __forceinline__ f32x4 bload4(__amdgpu_buffer_rsrc_t r, uint32_t off) {
-  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0));
-}
+// Activation reads are buffer loads (bload4e, dk_common.h): out-of-range offsets return 0 in
+// hardware, so the padding needs no branches and every load of a thread can be in flight.
 
 // Per-thread filter taps for channels c..c+3: wl 0 = the [R][S][C] copy (dk_dw_weight_rsc_f32),
 // 1 = the reference layout W[C][R][S] read directly (4*R*S contiguous floats), 2 = W[C][R][S]
@@ -72,7 +65,7 @@ __device__ __forceinline__ void load_dw_weights(f32x4 (&wv)[R][S], const float* 
 }
 
 // One input row of a strip: NC float4s at (ih, iw0 ..), BN-on-load applied, padding 0.
-template <int NC, bool BN>
+template <int NC, bool BN, class T = float>
 __device__ __forceinline__ void load_row(f32x4 (&row)[NC], __amdgpu_buffer_rsrc_t rs, int n, int ih, int iw0, int H,
                                          int W, int C, int c, const BnIn& bn, f32x4 bm, f32x4 bi, f32x4 bg,
                                          f32x4 bb) {
@@ -81,7 +74,7 @@ __device__ __forceinline__ void load_row(f32x4 (&row)[NC], __amdgpu_buffer_rsrc_
   for (int q = 0; q < NC; ++q) {
     const int iw = iw0 + q;
     const bool ok = rv && (unsigned)iw < (unsigned)W;
-    row[q] = bload4(rs, ok ? (uint32_t)(((n * H + ih) * W + iw) * C + c) * 4u : kOOB);
+    row[q] = bload4e<T>(rs, ok, (uint32_t)(((n * H + ih) * W + iw) * C + c));
     if constexpr (BN) {
       const f32x4 t = bn_in4(row[q], bm, bi, bg, bb, bn.relu);
       row[q] = ok ? t : f32x4{0.f, 0.f, 0.f, 0.f};
@@ -107,13 +100,15 @@ struct DwTile {
 // STATS == 2 (this kernel computing a stride-1 dgrad): the BN-backward sums of the BatchNorm
 // whose output the layer consumed -- sum(g), sum(g * x_hat) with g = y masked by that BN's
 // fused ReLU (batch_norm.py:125-174, dk_bn_bwd_partial_f64); xo is that BN's raw input.
-template <int R, int S, int ST, bool BN, int STATS, int WL>
-__global__ __launch_bounds__(256) void dw_fwd_kernel(const float* __restrict__ x, uint32_t xbytes,
+// T: activation storage (float, or bf16_t for BASELINE config 5); compute is fp32, and the
+// statistics see the stored (rounded) outputs.
+template <int R, int S, int ST, bool BN, int STATS, int WL, class T = float>
+__global__ __launch_bounds__(256) void dw_fwd_kernel(const T* __restrict__ x, uint32_t xbytes,
                                                      const float* __restrict__ wt, const float* __restrict__ bias,
-                                                     float* __restrict__ y, int N, int H, int W, int C, int OH, int OW,
+                                                     T* __restrict__ y, int N, int H, int W, int C, int OH, int OW,
                                                      int pad, BnIn bn, double* __restrict__ part,
-                                                     const float* __restrict__ xo, BnIn obn,
-                                                     const float* __restrict__ res) {
+                                                     const T* __restrict__ xo, BnIn obn,
+                                                     const T* __restrict__ res) {
   constexpr int TW = DwTile<ST>::TW, SEG = DwTile<ST>::SEG;
   constexpr int NC = (TW - 1) * ST + S;
   const int C4 = C >> 2;
@@ -136,7 +131,7 @@ __global__ __launch_bounds__(256) void dw_fwd_kernel(const float* __restrict__ x
     const int ow0 = wc * TW;
     const int iw0 = ow0 * ST - pad;
     const int oh0 = sg * SEG, oh1 = min(OH, oh0 + SEG);
-    const __amdgpu_buffer_rsrc_t rs = make_rsrc(x, xbytes);
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc_v(x, xbytes);
     f32x4 bm, bi, bg, bb;
     if constexpr (BN) {
       bm = ld4(bn.mean + c);
@@ -156,7 +151,8 @@ __global__ __launch_bounds__(256) void dw_fwd_kernel(const float* __restrict__ x
     }
     f32x4 win[R][NC];
 #pragma unroll
-    for (int r = 0; r < R; ++r) load_row<NC, BN>(win[r], rs, n, oh0 * ST - pad + r, iw0, H, W, C, c, bn, bm, bi, bg, bb);
+    for (int r = 0; r < R; ++r)
+      load_row<NC, BN, T>(win[r], rs, n, oh0 * ST - pad + r, iw0, H, W, C, c, bn, bm, bi, bg, bb);
     for (int oh = oh0; oh < oh1; ++oh) {
       // this row's residual / BN-input operands (dgrad only), issued ahead of the window
       // loads and FMAs
@@ -177,11 +173,11 @@ __global__ __launch_bounds__(256) void dw_fwd_kernel(const float* __restrict__ x
 #pragma unroll
             for (int q = 0; q < NC; ++q) win[r][q] = win[r + ST][q];
           } else {
-            load_row<NC, BN>(win[r], rs, n, oh * ST - pad + r, iw0, H, W, C, c, bn, bm, bi, bg, bb);
+            load_row<NC, BN, T>(win[r], rs, n, oh * ST - pad + r, iw0, H, W, C, c, bn, bm, bi, bg, bb);
           }
         }
       }
-      float* yrow = y + ((size_t)(n * OH + oh) * OW) * C + c;
+      T* yrow = y + ((size_t)(n * OH + oh) * OW) * C + c;
 #pragma unroll
       for (int j = 0; j < TW; ++j) {
         f32x4 acc = b0;
@@ -193,6 +189,7 @@ __global__ __launch_bounds__(256) void dw_fwd_kernel(const float* __restrict__ x
           if constexpr (WL == 2) {
             if (res) acc += rv[j];  // residual addend
           }
+          acc = rnd4<T>(acc);  // what the store keeps (identity for fp32)
           st4(yrow + (size_t)(ow0 + j) * C, acc);
           if constexpr (STATS == 1) {
 #pragma unroll
@@ -236,11 +233,11 @@ __global__ __launch_bounds__(256) void dw_fwd_kernel(const float* __restrict__ x
 
 // Stride > 1 dgrad by sub-pixel decomposition (see SubPix): thread = 4 channels of TWQ
 // consecutive ST x ST quads of dx; the dy neighbourhood columns are shared by adjacent quads.
-template <int R, int S, int ST, int PAD>
-__global__ __launch_bounds__(256) void dw_dgrad_subpixel_kernel(const float* __restrict__ dy, uint32_t dybytes,
-                                                                const float* __restrict__ wt, float* __restrict__ dx,
+template <int R, int S, int ST, int PAD, class T = float>
+__global__ __launch_bounds__(256) void dw_dgrad_subpixel_kernel(const T* __restrict__ dy, uint32_t dybytes,
+                                                                const float* __restrict__ wt, T* __restrict__ dx,
                                                                 int N, int H, int W, int C, int OH, int OW,
-                                                                const float* __restrict__ res) {
+                                                                const T* __restrict__ res) {
   using RP = SubPix<R, ST, PAD>;
   using SP = SubPix<S, ST, PAD>;
   constexpr int DR0 = RP::dmin(), NR = RP::dmax() - RP::dmin() + 1;
@@ -260,7 +257,7 @@ __global__ __launch_bounds__(256) void dw_dgrad_subpixel_kernel(const float* __r
   const int n = (int)(t / QH);
   const int c = cq * 4;
   const int j0 = qc * TWQ;
-  const __amdgpu_buffer_rsrc_t rs = make_rsrc(dy, dybytes);
+  const __amdgpu_buffer_rsrc_t rs = make_rsrc_v(dy, dybytes);
   f32x4 d[NR][NCOL];
 #pragma unroll
   for (int a = 0; a < NR; ++a) {
@@ -269,7 +266,7 @@ __global__ __launch_bounds__(256) void dw_dgrad_subpixel_kernel(const float* __r
     for (int b = 0; b < NCOL; ++b) {
       const int ow = j0 + DS0 + b;
       const bool ok = (unsigned)oh < (unsigned)OH && (unsigned)ow < (unsigned)OW;
-      d[a][b] = bload4(rs, ok ? (uint32_t)(((n * OH + oh) * OW + ow) * C + c) * 4u : kOOB);
+      d[a][b] = bload4e<T>(rs, ok, (uint32_t)(((n * OH + oh) * OW + ow) * C + c));
     }
   }
   f32x4 wv[R][S];
@@ -358,9 +355,9 @@ struct DwWgTile {
 // output row loads ST new input rows instead of R.
 constexpr int kWgSeg = 8;
 
-template <int R, int S, int ST, bool BN>
-__global__ __launch_bounds__(256) void dw_wgrad_partial_kernel(const float* __restrict__ dy, uint32_t dybytes,
-                                                               const float* __restrict__ x, uint32_t xbytes,
+template <int R, int S, int ST, bool BN, class T = float>
+__global__ __launch_bounds__(256) void dw_wgrad_partial_kernel(const T* __restrict__ dy, uint32_t dybytes,
+                                                               const T* __restrict__ x, uint32_t xbytes,
                                                                float* __restrict__ part, int N, int H, int W,
                                                                int C, int OH, int OW, int pad, int ipb, BnIn bn) {
   constexpr int RS = R * S;
@@ -379,7 +376,7 @@ __global__ __launch_bounds__(256) void dw_wgrad_partial_kernel(const float* __re
   const int nseg = (OH + kWgSeg - 1) / kWgSeg;
   const int items = N * nseg * nwc;
   const int i0 = blockIdx.x * ipb, i1 = min(items, i0 + ipb);
-  const __amdgpu_buffer_rsrc_t rx = make_rsrc(x, xbytes), rg = make_rsrc(dy, dybytes);
+  const __amdgpu_buffer_rsrc_t rx = make_rsrc_v(x, xbytes), rg = make_rsrc_v(dy, dybytes);
   f32x4 bm, bi, bg, bb;
   if constexpr (BN) {
     const int cc = active ? c : 0;
@@ -404,7 +401,8 @@ __global__ __launch_bounds__(256) void dw_wgrad_partial_kernel(const float* __re
       const int oh0 = sg * kWgSeg, oh1 = min(OH, oh0 + kWgSeg);
       f32x4 win[R][NC];
 #pragma unroll
-      for (int r = 0; r < R; ++r) load_row<NC, BN>(win[r], rx, n, oh0 * ST - pad + r, iw0, H, W, C, c, bn, bm, bi, bg, bb);
+      for (int r = 0; r < R; ++r)
+        load_row<NC, BN, T>(win[r], rx, n, oh0 * ST - pad + r, iw0, H, W, C, c, bn, bm, bi, bg, bb);
       for (int oh = oh0; oh < oh1; ++oh) {
         if (oh > oh0) {
 #pragma unroll
@@ -413,14 +411,14 @@ __global__ __launch_bounds__(256) void dw_wgrad_partial_kernel(const float* __re
 #pragma unroll
               for (int q = 0; q < NC; ++q) win[r][q] = win[r + ST][q];
             } else {
-              load_row<NC, BN>(win[r], rx, n, oh * ST - pad + r, iw0, H, W, C, c, bn, bm, bi, bg, bb);
+              load_row<NC, BN, T>(win[r], rx, n, oh * ST - pad + r, iw0, H, W, C, c, bn, bm, bi, bg, bb);
             }
           }
         }
         f32x4 g[TW];
 #pragma unroll
         for (int j = 0; j < TW; ++j)
-          g[j] = bload4(rg, ow0 + j < OW ? (uint32_t)(((n * OH + oh) * OW + ow0 + j) * C + c) * 4u : kOOB);
+          g[j] = bload4e<T>(rg, ow0 + j < OW, (uint32_t)(((n * OH + oh) * OW + ow0 + j) * C + c));
 #pragma unroll
         for (int j = 0; j < TW; ++j)
 #pragma unroll
@@ -474,15 +472,15 @@ static long long dw_fwd_threads(int N, int OH, int OW, int C) {
 
 // part: per-block sums (mode 1: output statistics; mode 2 with xo/obn: BN-backward sums).
 // wl: weight layout (load_dw_weights).  Only the combinations the entry points use exist.
-template <int R, int S, int ST>
-static int launch_dw_fwd(const float* x, const float* wt, const float* bias, float* y, int N, int H, int W, int C,
-                         int OH, int OW, int pad, const BnIn& bn, double* part, const float* xo, const BnIn& obn,
-                         int wl, const float* res, hipStream_t st) {
-  const uint32_t xb = (uint32_t)((size_t)N * H * W * C * sizeof(float));
+template <int R, int S, int ST, class T>
+static int launch_dw_fwd(const T* x, const float* wt, const float* bias, T* y, int N, int H, int W, int C, int OH,
+                         int OW, int pad, const BnIn& bn, double* part, const T* xo, const BnIn& obn, int wl,
+                         const T* res, hipStream_t st) {
+  const uint32_t xb = (uint32_t)((size_t)N * H * W * C * sizeof(T));
   const dim3 grid((unsigned)cdivll(dw_fwd_threads<ST>(N, OH, OW, C), 256));
 #define DW_LAUNCH(B, ST_, WL_)                                                                                        \
-  hipLaunchKernelGGL((dw_fwd_kernel<R, S, ST, B, ST_, WL_>), grid, dim3(256), 0, st, x, xb, wt, bias, y, N, H, W, C, \
-                     OH, OW, pad, bn, part, xo, obn, res)
+  hipLaunchKernelGGL((dw_fwd_kernel<R, S, ST, B, ST_, WL_, T>), grid, dim3(256), 0, st, x, xb, wt, bias, y, N, H, W, \
+                     C, OH, OW, pad, bn, part, xo, obn, res)
   const int mode = part ? (xo ? 2 : 1) : 0;
   if (wl == 0 && !bn.mean && mode == 0)
     DW_LAUNCH(false, 0, 0);
@@ -506,17 +504,18 @@ static int launch_dw_fwd(const float* x, const float* wt, const float* bias, flo
   return launch_status();
 }
 
-static int dw_fwd_dispatch(const float* x, const float* wt, const float* bias, float* y, int N, int H, int W, int C,
-                           int R, int S, int stride, int OH, int OW, int pad, const BnIn& bn, hipStream_t st,
-                           double* part = nullptr, const float* xo = nullptr, const BnIn& obn = BnIn{}, int wl = 0,
-                           const float* res = nullptr) {
+template <class T>
+static int dw_fwd_dispatch(const T* x, const float* wt, const float* bias, T* y, int N, int H, int W, int C, int R,
+                           int S, int stride, int OH, int OW, int pad, const BnIn& bn, hipStream_t st,
+                           double* part = nullptr, const T* xo = nullptr, const BnIn& obn = BnIn{}, int wl = 0,
+                           const T* res = nullptr) {
   if (res && (!aligned16(res) || wl != 2)) return DK_ERR_ARGS;  // residual addend: dgrad only
   if (C % 4 || !aligned16(x) || !aligned16(wt) || !fits((size_t)N * H * W * C * 4) || !bn_ok(bn)) return DK_ERR_ARGS;
   if (part && (C / 4 > 256 || 256 % (C / 4))) return DK_ERR_ARGS;
   if (xo && (bn.mean || !obn.mean || !aligned16(xo) || !bn_ok(obn))) return DK_ERR_ARGS;
 #define DW_CASE(RR, SS, STR)                                                                     \
   if (R == RR && S == SS && stride == STR)                                                           \
-    return launch_dw_fwd<RR, SS, STR>(x, wt, bias, y, N, H, W, C, OH, OW, pad, bn, part, xo, obn, wl, res, st);
+    return launch_dw_fwd<RR, SS, STR, T>(x, wt, bias, y, N, H, W, C, OH, OW, pad, bn, part, xo, obn, wl, res, st);
   DW_CASE(3, 3, 1)
   DW_CASE(3, 3, 2)
   DW_CASE(5, 5, 1)
@@ -527,9 +526,10 @@ static int dw_fwd_dispatch(const float* x, const float* wt, const float* bias, f
   return DK_ERR_ARGS;
 }
 
-static int dw_wgrad(const float* dy, const float* x, int N, int H, int W, int C, int R, int S, int stride, int pad,
-                    int OH, int OW, const float* w_crs, float l2, float* dw_crs, void* ws, size_t ws_bytes,
-                    const BnIn& bn, hipStream_t st);
+template <class T>
+static int dw_wgrad(const T* dy, const T* x, int N, int H, int W, int C, int R, int S, int stride, int pad, int OH,
+                    int OW, const float* w_crs, float l2, float* dw_crs, void* ws, size_t ws_bytes, const BnIn& bn,
+                    hipStream_t st);
 
 }  // namespace dk
 
@@ -570,7 +570,7 @@ DK_API int dk_dwconv_fwd_ex_f32(const float* x, int N, int H, int W, int C, cons
                                 const float* bn_mean, const float* bn_invstd, const float* bn_gamma,
                                 const float* bn_beta, int bn_relu, double* stats, void* stream) {
   if (stride != 1 && stride != 2) return DK_ERR_ARGS;
-  return dw_fwd_dispatch(x, w_crs, bias, y, N, H, W, C, R, S, stride, OH, OW, pad,
+  return dw_fwd_dispatch<float>(x, w_crs, bias, y, N, H, W, C, R, S, stride, OH, OW, pad,
                          BnIn{bn_mean, bn_invstd, bn_gamma, bn_beta, bn_relu}, as_stream(stream), stats, nullptr,
                          BnIn{}, 1);
 }
@@ -581,9 +581,10 @@ DK_API size_t dk_dwconv_dgrad_workspace_bytes(int C, int R, int S) { return (siz
 // Input gradient.  res (optional): added to dx (the residual join's other gradient term);
 // bn_x/obn/part (optional, stride 1 only): + stage 1 of the backward of the BatchNorm whose
 // output the layer consumed.
-static int dw_dgrad(const float* dy, int N, int OH, int OW, int C, const float* w_crs, int R, int S, int stride,
-                    int pad, float* dx, int H, int W, void* ws, size_t ws_bytes, const float* res, const float* bn_x,
-                    const BnIn& obn, double* part, hipStream_t st) {
+template <class T>
+static int dw_dgrad(const T* dy, int N, int OH, int OW, int C, const float* w_crs, int R, int S, int stride, int pad,
+                    T* dx, int H, int W, void* ws, size_t ws_bytes, const T* res, const T* bn_x, const BnIn& obn,
+                    double* part, hipStream_t st) {
   if (C % 4) return DK_ERR_ARGS;
   if (ws_bytes < dk_dwconv_dgrad_workspace_bytes(C, R, S)) return DK_ERR_WORKSPACE;
   float* wt = static_cast<float*>(ws);
@@ -597,12 +598,12 @@ static int dw_dgrad(const float* dy, int N, int OH, int OW, int C, const float* 
   if (!fits((size_t)N * OH * OW * C * 4) || !aligned16(dy) || !aligned16(dx) || !aligned16(w_crs) ||
       (res && !aligned16(res)))
     return DK_ERR_ARGS;
-  const uint32_t gb = (uint32_t)((size_t)N * OH * OW * C * 4);
+  const uint32_t gb = (uint32_t)((size_t)N * OH * OW * C * sizeof(T));
 #define DW_SUBPIX(RR, SS, STR, PD)                                                                                   \
   if (R == RR && S == SS && stride == STR && pad == PD) {                                                            \
     const long long items = (long long)N * cdiv(H, STR) * cdiv(cdiv(W, STR), 4) * (C / 4);                         \
-    hipLaunchKernelGGL((dw_dgrad_subpixel_kernel<RR, SS, STR, PD>), dim3((unsigned)cdivll(items, 256)), dim3(256), 0, \
-                       st, dy, gb, w_crs, dx, N, H, W, C, OH, OW, res);                                              \
+    hipLaunchKernelGGL((dw_dgrad_subpixel_kernel<RR, SS, STR, PD, T>), dim3((unsigned)cdivll(items, 256)), dim3(256), \
+                       0, st, dy, gb, w_crs, dx, N, H, W, C, OH, OW, res);                                           \
     return launch_status();                                                                                          \
   }
   DW_SUBPIX(3, 3, 2, 1)
@@ -610,6 +611,9 @@ static int dw_dgrad(const float* dy, int N, int OH, int OW, int C, const float* 
   DW_SUBPIX(1, 1, 2, 0)
 #undef DW_SUBPIX
   if (res) return DK_ERR_ARGS;  // generic gather path: no residual fusion
+  if constexpr (sizeof(T) != sizeof(float)) {
+    return DK_ERR_ARGS;  // generic gather path: fp32 storage only
+  } else {
   hipLaunchKernelGGL(dw_weight_rsc_kernel, dim3(cdiv(C * R * S, 256)), dim3(256), 0, st, w_crs, C, R, S, 0, wt);
   int rc = launch_status();
   if (rc) return rc;
@@ -627,12 +631,13 @@ static int dw_dgrad(const float* dy, int N, int OH, int OW, int C, const float* 
   else
     return DK_ERR_ARGS;
   return launch_status();
+  }
 }
 
 DK_API int dk_dwconv_dgrad_f32(const float* dy, int N, int OH, int OW, int C, const float* w_crs, int R, int S,
                                int stride, int pad, float* dx, int H, int W, void* ws, size_t ws_bytes,
                                void* stream) {
-  return dw_dgrad(dy, N, OH, OW, C, w_crs, R, S, stride, pad, dx, H, W, ws, ws_bytes, nullptr, nullptr, BnIn{},
+  return dw_dgrad<float>(dy, N, OH, OW, C, w_crs, R, S, stride, pad, dx, H, W, ws, ws_bytes, nullptr, nullptr, BnIn{},
                   nullptr, as_stream(stream));
 }
 
@@ -656,8 +661,9 @@ DK_API size_t dk_dwconv_wgrad_workspace_bytes(int N, int OH, int OW, int C, int 
 }
 
 namespace dk {
-static int dw_wgrad(const float* dy, const float* x, int N, int H, int W, int C, int R, int S, int stride, int pad,
-                    int OH, int OW, const float* w_crs, float l2, float* dw_crs, void* ws, size_t ws_bytes,
+template <class T>
+static int dw_wgrad(const T* dy, const T* x, int N, int H, int W, int C, int R, int S, int stride, int pad, int OH,
+                    int OW, const float* w_crs, float l2, float* dw_crs, void* ws, size_t ws_bytes,
                     const BnIn& bn, hipStream_t st) {
   if (C % 4 || !aligned16(x) || !aligned16(dy) || !bn_ok(bn)) return DK_ERR_ARGS;
   if (!fits((size_t)N * H * W * C * 4) || !fits((size_t)N * OH * OW * C * 4)) return DK_ERR_ARGS;
@@ -668,15 +674,15 @@ static int dw_wgrad(const float* dy, const float* x, int N, int H, int W, int C,
   const dim3 grid(nblk, cdiv(C4, cgt));
   float* part = static_cast<float*>(ws);
   const size_t shm = (size_t)256 * R * S * 4 * sizeof(float);
-  const uint32_t xb = (uint32_t)((size_t)N * H * W * C * 4), gb = (uint32_t)((size_t)N * OH * OW * C * 4);
+  const uint32_t xb = (uint32_t)((size_t)N * H * W * C * sizeof(T)), gb = (uint32_t)((size_t)N * OH * OW * C * sizeof(T));
 #define DW_WG_LAUNCH(RR, SS, STR, B)                                                                                 \
   {                                                                                                                  \
     const int items = N * cdiv(OH, kWgSeg) * ((OW + DwWgTile<STR>::TW - 1) / DwWgTile<STR>::TW);                     \
     const int ipb = cdiv(items, nblk);                                                                               \
     if (shm > 65536)                                                                                                 \
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&dw_wgrad_partial_kernel<RR, SS, STR, B>),             \
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&dw_wgrad_partial_kernel<RR, SS, STR, B, T>),          \
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);                               \
-    hipLaunchKernelGGL((dw_wgrad_partial_kernel<RR, SS, STR, B>), grid, dim3(256), shm, st, dy, gb, x, xb, part, N,  \
+    hipLaunchKernelGGL((dw_wgrad_partial_kernel<RR, SS, STR, B, T>), grid, dim3(256), shm, st, dy, gb, x, xb, part, N, \
                        H, W, C, OH, OW, pad, ipb, bn);                                                               \
   }
 #define DW_WG(RR, SS, STR)                 \
@@ -715,4 +721,36 @@ DK_API int dk_dwconv_wgrad_bnx_f32(const float* dy, const float* x, int N, int H
   if (!bn_mean) return DK_ERR_ARGS;
   return dw_wgrad(dy, x, N, H, W, C, R, S, stride, pad, OH, OW, w_crs, l2, dw_crs, ws, ws_bytes,
                   BnIn{bn_mean, bn_invstd, bn_gamma, bn_beta, bn_relu}, as_stream(stream));
+}
+
+// ---------------------------------------------------------------------------------------
+// bf16 storage (BASELINE config 5): activations / gradients bf16, weights and their
+// gradients fp32, all arithmetic fp32 (same kernels, T = bf16_t).
+// ---------------------------------------------------------------------------------------
+DK_API int dk_dwconv_fwd_ex_bf16(const bf16_t* x, int N, int H, int W, int C, const float* w_crs, int R, int S,
+                                 int stride, int pad, const float* bias, bf16_t* y, int OH, int OW,
+                                 const float* bn_mean, const float* bn_invstd, const float* bn_gamma,
+                                 const float* bn_beta, int bn_relu, double* stats, void* stream) {
+  if (stride != 1 && stride != 2) return DK_ERR_ARGS;
+  return dw_fwd_dispatch<bf16_t>(x, w_crs, bias, y, N, H, W, C, R, S, stride, OH, OW, pad,
+                                 BnIn{bn_mean, bn_invstd, bn_gamma, bn_beta, bn_relu}, as_stream(stream), stats,
+                                 nullptr, BnIn{}, 1);
+}
+
+DK_API int dk_dwconv_dgrad_ex_bf16(const bf16_t* dy, int N, int OH, int OW, int C, const float* w_crs, int R, int S,
+                                   int stride, int pad, bf16_t* dx, int H, int W, void* ws, size_t ws_bytes,
+                                   const bf16_t* residual, const bf16_t* bn_x, const float* bn_mean,
+                                   const float* bn_invstd, const float* bn_gamma, const float* bn_beta, int bn_relu,
+                                   double* part, void* stream) {
+  if ((part != nullptr) != (bn_x != nullptr)) return DK_ERR_ARGS;
+  return dw_dgrad<bf16_t>(dy, N, OH, OW, C, w_crs, R, S, stride, pad, dx, H, W, ws, ws_bytes, residual, bn_x,
+                          BnIn{bn_mean, bn_invstd, bn_gamma, bn_beta, bn_relu}, part, as_stream(stream));
+}
+
+DK_API int dk_dwconv_wgrad_bnx_bf16(const bf16_t* dy, const bf16_t* x, int N, int H, int W, int C, int R, int S,
+                                    int stride, int pad, int OH, int OW, const float* w_crs, float l2, float* dw_crs,
+                                    void* ws, size_t ws_bytes, const float* bn_mean, const float* bn_invstd,
+                                    const float* bn_gamma, const float* bn_beta, int bn_relu, void* stream) {
+  return dw_wgrad<bf16_t>(dy, x, N, H, W, C, R, S, stride, pad, OH, OW, w_crs, l2, dw_crs, ws, ws_bytes,
+                          BnIn{bn_mean, bn_invstd, bn_gamma, bn_beta, bn_relu}, as_stream(stream));
 }

@@ -31,6 +31,57 @@ static inline long long cdivll(long long a, long long b) { return (a + b - 1) / 
 __device__ __forceinline__ f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
 __device__ __forceinline__ void st4(float* p, f32x4 v) { *reinterpret_cast<f32x4*>(p) = v; }
 
+// bf16 storage (BASELINE config 5): activations held as bf16 bits, every kernel computes
+// in fp32 -- loads widen (exact), stores round to nearest even (v_cvt_pk_bf16_f32).
+typedef uint16_t bf16_t;
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ f32x4 bf16x4_to_f32(uint2 u) {
+  return __builtin_convertvector(__builtin_bit_cast(bf16x4, u), f32x4);
+}
+__device__ __forceinline__ uint2 f32_to_bf16x4(f32x4 v) {
+  return __builtin_bit_cast(uint2, __builtin_convertvector(v, bf16x4));
+}
+__device__ __forceinline__ f32x4 ld4(const bf16_t* p) { return bf16x4_to_f32(*reinterpret_cast<const uint2*>(p)); }
+__device__ __forceinline__ void st4(bf16_t* p, f32x4 v) { *reinterpret_cast<uint2*>(p) = f32_to_bf16x4(v); }
+__device__ __forceinline__ float ld1(const float* p) { return *p; }
+__device__ __forceinline__ float ld1(const bf16_t* p) {
+  return __builtin_bit_cast(float, (uint32_t)*p << 16);
+}
+__device__ __forceinline__ void st1(float* p, float v) { *p = v; }
+__device__ __forceinline__ void st1(bf16_t* p, float v) { *p = __builtin_bit_cast(bf16_t, (__bf16)v); }
+// The value a store of v to T-typed storage keeps (what a consumer reads back).
+template <class T>
+__device__ __forceinline__ f32x4 rnd4(f32x4 v) {
+  if constexpr (sizeof(T) == 2)
+    return bf16x4_to_f32(f32_to_bf16x4(v));
+  else
+    return v;
+}
+template <class T>
+__device__ __forceinline__ float rnd1(float v) {
+  if constexpr (sizeof(T) == 2)
+    return (float)(__bf16)v;
+  else
+    return v;
+}
+
+// Buffer loads (out-of-range byte offsets return 0 in hardware: padding needs no branch).
+constexpr uint32_t kOOBBytes = 0x80000000u;  // past any buffer we build (tensors < 2 GiB)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc_v(const void* p, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
+}
+// 4 consecutive elements at element index e (ok == false: zeros)
+template <class T>
+__device__ __forceinline__ f32x4 bload4e(__amdgpu_buffer_rsrc_t r, bool ok, uint32_t e) {
+  if constexpr (sizeof(T) == 2) {
+    const uint32_t off = ok ? e * 2u : kOOBBytes;
+    return bf16x4_to_f32(__builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(r, (int)off, 0, 0)));
+  } else {
+    const uint32_t off = ok ? e * 4u : kOOBBytes;
+    return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0));
+  }
+}
+
 // Wave-level (64 lanes) sum.
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

@@ -12,7 +12,8 @@ namespace dk {
 
 // Vectorised elementwise kernels: each thread handles float4 chunks (grid-stride), the
 // uint8 masks as one 32-bit word per chunk; a scalar tail handles n % 4.
-__global__ __launch_bounds__(256) void relu_fwd_kernel(const float* __restrict__ x, long long n, float* __restrict__ y,
+template <class E = float>  // E: activation storage (float or bf16_t)
+__global__ __launch_bounds__(256) void relu_fwd_kernel(const E* __restrict__ x, long long n, E* __restrict__ y,
                                                        uint8_t* __restrict__ mask, int vec) {
   const long long nv = vec ? (n >> 2) : 0;
   const long long stride = (long long)gridDim.x * blockDim.x;
@@ -29,14 +30,16 @@ __global__ __launch_bounds__(256) void relu_fwd_kernel(const float* __restrict__
     if (mask) reinterpret_cast<uint32_t*>(mask)[i] = m;
   }
   for (long long i = 4 * nv + (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-    const bool pos = x[i] > 0.f;
-    y[i] = pos ? x[i] : 0.f;
+    const float v = ld1(x + i);
+    const bool pos = v > 0.f;
+    st1(y + i, pos ? v : 0.f);
     if (mask) mask[i] = pos;
   }
 }
 
-__global__ __launch_bounds__(256) void relu_bwd_kernel(const float* __restrict__ dy, const uint8_t* __restrict__ mask,
-                                                       long long n, float* __restrict__ dx, int vec) {
+template <class E = float>
+__global__ __launch_bounds__(256) void relu_bwd_kernel(const E* __restrict__ dy, const uint8_t* __restrict__ mask,
+                                                       long long n, E* __restrict__ dx, int vec) {
   const long long nv = vec ? (n >> 2) : 0;
   const long long stride = (long long)gridDim.x * blockDim.x;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += stride) {
@@ -47,7 +50,7 @@ __global__ __launch_bounds__(256) void relu_bwd_kernel(const float* __restrict__
     st4(dx + 4 * i, g);
   }
   for (long long i = 4 * nv + (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
-    dx[i] = mask[i] ? dy[i] : 0.f;
+    st1(dx + i, mask[i] ? ld1(dy + i) : 0.f);
 }
 
 __global__ void mask_to_f32_kernel(const uint8_t* __restrict__ mask, long long n, float* __restrict__ out) {
@@ -358,14 +361,28 @@ static inline dim3 grid4(long long n) {
 using namespace dk;
 
 DK_API int dk_relu_fwd_f32(const float* x, long long n, float* y, uint8_t* mask, void* stream) {
-  hipLaunchKernelGGL(relu_fwd_kernel, grid4(n), dim3(256), 0, as_stream(stream), x, n, y, mask,
+  hipLaunchKernelGGL(relu_fwd_kernel<float>, grid4(n), dim3(256), 0, as_stream(stream), x, n, y, mask,
                      (int)(al16(x) && al16(y) && al4(mask)));
   return launch_status();
 }
 
 DK_API int dk_relu_bwd_f32(const float* dy, const uint8_t* mask, long long n, float* dx, void* stream) {
-  hipLaunchKernelGGL(relu_bwd_kernel, grid4(n), dim3(256), 0, as_stream(stream), dy, mask, n, dx,
+  hipLaunchKernelGGL(relu_bwd_kernel<float>, grid4(n), dim3(256), 0, as_stream(stream), dy, mask, n, dx,
                      (int)(al16(dy) && al16(dx) && al4(mask)));
+  return launch_status();
+}
+
+static inline bool al8(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 7) == 0; }
+
+DK_API int dk_relu_fwd_bf16(const bf16_t* x, long long n, bf16_t* y, uint8_t* mask, void* stream) {
+  hipLaunchKernelGGL(relu_fwd_kernel<bf16_t>, grid4(n), dim3(256), 0, as_stream(stream), x, n, y, mask,
+                     (int)(al8(x) && al8(y) && al4(mask)));
+  return launch_status();
+}
+
+DK_API int dk_relu_bwd_bf16(const bf16_t* dy, const uint8_t* mask, long long n, bf16_t* dx, void* stream) {
+  hipLaunchKernelGGL(relu_bwd_kernel<bf16_t>, grid4(n), dim3(256), 0, as_stream(stream), dy, mask, n, dx,
+                     (int)(al8(dy) && al8(dx) && al4(mask)));
   return launch_status();
 }
 
@@ -484,3 +501,41 @@ DK_API int dk_scale_f32(const float* x, long long n, float s, float* y, void* st
 }
 
 DK_API int dk_abi_version(void) { return 1; }
+
+// ---------------------------------------------------------------------------------------
+// fp32 <-> bf16 storage casts (BASELINE config 5 inputs / checks): round to nearest even.
+// ---------------------------------------------------------------------------------------
+namespace dk {
+__global__ void cast_f32_bf16_kernel(const float* __restrict__ x, long long n, bf16_t* __restrict__ y) {
+  const long long i = ((long long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  if (i + 3 < n && ((n & 3) == 0)) {
+    st4(y + i, ld4(x + i));
+  } else {
+    for (long long k = i; k < n && k < i + 4; ++k) st1(y + k, x[k]);
+  }
+}
+__global__ void cast_bf16_f32_kernel(const bf16_t* __restrict__ x, long long n, float* __restrict__ y) {
+  const long long i = ((long long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  if (i + 3 < n && ((n & 3) == 0)) {
+    st4(y + i, ld4(x + i));
+  } else {
+    for (long long k = i; k < n && k < i + 4; ++k) y[k] = ld1(x + k);
+  }
+}
+}  // namespace dk
+
+DK_API int dk_cast_f32_to_bf16(const float* x, long long n, uint16_t* y, void* stream) {
+  if (n <= 0) return 0;
+  if ((reinterpret_cast<uintptr_t>(x) & 15) || (reinterpret_cast<uintptr_t>(y) & 7)) return DK_ERR_ARGS;
+  hipLaunchKernelGGL(dk::cast_f32_bf16_kernel, dim3((unsigned)dk::cdivll(n, 1024)), dim3(256), 0,
+                     dk::as_stream(stream), x, n, y);
+  return dk::launch_status();
+}
+
+DK_API int dk_cast_bf16_to_f32(const uint16_t* x, long long n, float* y, void* stream) {
+  if (n <= 0) return 0;
+  if ((reinterpret_cast<uintptr_t>(x) & 7) || (reinterpret_cast<uintptr_t>(y) & 15)) return DK_ERR_ARGS;
+  hipLaunchKernelGGL(dk::cast_bf16_f32_kernel, dim3((unsigned)dk::cdivll(n, 1024)), dim3(256), 0,
+                     dk::as_stream(stream), x, n, y);
+  return dk::launch_status();
+}

@@ -35,12 +35,6 @@ namespace dk {
 
 constexpr uint32_t kOOB = 0x80000000u;  // an offset past any buffer we build (tensors < 2 GiB)
 
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const float* p, uint32_t bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p), (short)0, (int)bytes, 0x00020000);
-}
-__device__ __forceinline__ f32x4 bload4(__amdgpu_buffer_rsrc_t r, uint32_t off) {
-  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0));
-}
 __device__ __forceinline__ float bload1(__amdgpu_buffer_rsrc_t r, uint32_t off) {
   return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, 0));
 }
@@ -52,9 +46,13 @@ __device__ __forceinline__ float bload1(__amdgpu_buffer_rsrc_t r, uint32_t off) 
 // Implicit-im2col view of an NHWC tensor x[n][ih][iw][c] (C % 4 == 0, < 2 GiB).
 // Row/pixel index m -> (n, oh, ow) over an OH x OW grid; tap (r,s) reads
 // (ih, iw) = (oh*sa + dr*r + off, ow*sa + dr*s + off), zero outside [0,H)x[0,W).
-struct ImgDesc {
+// E: element type of the tensor (float, or bf16_t for BASELINE config 5's bf16 storage); the
+// loaders widen to fp32 as they load.
+template <class E>
+struct ImgDescE {
   static constexpr bool kBnIn = false;
-  const float* x;
+  using Elem = E;
+  const E* x;
   uint32_t bytes;
   int H, W, C;
   int OH, OW;
@@ -62,23 +60,29 @@ struct ImgDesc {
   int sa, dr, off;
   int M;  // N * OH * OW
 };
+using ImgDesc = ImgDescE<float>;
 
 // The same view of bn(x) (+ReLU): the loaders apply the BatchNorm of the layer that
 // produced x to every in-image element (padding stays exactly 0, as in the reference,
 // which pads the BN output).
-struct ImgBnDesc : ImgDesc {
+template <class E>
+struct ImgBnDescE : ImgDescE<E> {
   static constexpr bool kBnIn = true;
   BnIn bn;
 };
+using ImgBnDesc = ImgBnDescE<float>;
 
 // Row-major matrix p[row][ld]; `ext` bounds the non-reduction index.
-struct MatDesc {
+template <class E>
+struct MatDescE {
   static constexpr bool kBnIn = false;
-  const float* p;
+  using Elem = E;
+  const E* p;
   uint32_t bytes;
   int ld;
   int ext;
 };
+using MatDesc = MatDescE<float>;
 
 // ----------------------------------------------------------------------------
 // Loaders.  K-contiguous ("KC") loaders fill T[ROWS][BK+4]; row-contiguous ("IC")
@@ -151,7 +155,7 @@ struct LdImgKC : KCLayout<ROWS, BK> {
 
   template <class D>
   __device__ __forceinline__ void load(const D& d, int k0, int Ktot) {
-    const __amdgpu_buffer_rsrc_t rs = make_rsrc(d.x, d.bytes);
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc_v(d.x, d.bytes);
     const int k = k0 + 4 * kq;
     const bool kv = k < Ktot;
     const int tap = k / d.C;
@@ -165,8 +169,7 @@ struct LdImgKC : KCLayout<ROWS, BK> {
     for (int j = 0; j < NR; ++j) {
       const int ih = ih0[j] + dri, iw = iw0[j] + dsi;
       const bool ok = kv && (unsigned)ih < (unsigned)d.H && (unsigned)iw < (unsigned)d.W;
-      const uint32_t off = ok ? (uint32_t)((base[j] + doff) * d.C + c) * 4u : kOOB;
-      v[j] = bload4(rs, off);
+      v[j] = bload4e<typename D::Elem>(rs, ok, (uint32_t)((base[j] + doff) * d.C + c));
       om |= (uint32_t)ok << j;
     }
     if constexpr (D::kBnIn) {
@@ -205,23 +208,26 @@ struct LdMatKCT : KCLayout<ROWS, BK> {
   bool active;
   f32x4 v[NR];
 
-  __device__ __forceinline__ void init(const MatDesc&, int row0_, int tid) {
+  template <class D>
+  __device__ __forceinline__ void init(const D&, int row0_, int tid) {
     kq = tid % KQ;
     rb = tid / KQ;
     row0 = row0_;
     active = rb < ROWS;
   }
 
-  __device__ __forceinline__ void load(const MatDesc& d, int k0, int Ktot) {
-    const __amdgpu_buffer_rsrc_t rs = make_rsrc(d.p, d.bytes);
+  template <class D>
+  __device__ __forceinline__ void load(const D& d, int k0, int Ktot) {
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc_v(d.p, d.bytes);
     const int k = k0 + 4 * kq;
+    static_assert(VEC || sizeof(typename D::Elem) == 4, "scalar loads: fp32 storage only");
 #pragma unroll
     for (int j = 0; j < NR; ++j) {
       const int i = row0 + rb + j * RSTEP;
       const bool iv = active && i < d.ext;
       const uint32_t base = (uint32_t)(i * d.ld + k) * 4u;
       if constexpr (VEC) {
-        v[j] = bload4(rs, (iv && k < Ktot) ? base : kOOB);
+        v[j] = bload4e<typename D::Elem>(rs, iv && k < Ktot, (uint32_t)(i * d.ld + k));
       } else {
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[j][e] = bload1(rs, (iv && k + e < Ktot) ? base + 4u * e : kOOB);
@@ -253,22 +259,25 @@ struct LdMatICT : ICLayout<ROWS, BK> {
   bool active;
   f32x4 v[NK];
 
-  __device__ __forceinline__ void init(const MatDesc&, int row0, int tid) {
+  template <class D>
+  __device__ __forceinline__ void init(const D&, int row0, int tid) {
     iq = tid % IQ;
     kb = tid / IQ;
     i0 = row0 + 4 * iq;
     active = kb < BK;
   }
 
-  __device__ __forceinline__ void load(const MatDesc& d, int k0, int Ktot) {
-    const __amdgpu_buffer_rsrc_t rs = make_rsrc(d.p, d.bytes);
+  template <class D>
+  __device__ __forceinline__ void load(const D& d, int k0, int Ktot) {
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc_v(d.p, d.bytes);
+    static_assert(VEC || sizeof(typename D::Elem) == 4, "scalar loads: fp32 storage only");
 #pragma unroll
     for (int j = 0; j < NK; ++j) {
       const int k = k0 + kb + j * KSTEP;
       const bool kv = active && k < Ktot;
       const uint32_t base = (uint32_t)(k * d.ld + i0) * 4u;
       if constexpr (VEC) {
-        v[j] = bload4(rs, (kv && i0 < d.ext) ? base : kOOB);
+        v[j] = bload4e<typename D::Elem>(rs, kv && i0 < d.ext, (uint32_t)(k * d.ld + i0));
       } else {
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[j][e] = bload1(rs, (kv && i0 + e < d.ext) ? base + 4u * e : kOOB);
@@ -330,7 +339,7 @@ struct LdImgIC : ICLayout<ROWS, BK> {
 
   template <class D>
   __device__ __forceinline__ void load(const D& d, int k0, int Ktot) {
-    const __amdgpu_buffer_rsrc_t rs = make_rsrc(d.x, d.bytes);
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc_v(d.x, d.bytes);
     uint32_t om = 0;
 #pragma unroll
     for (int jj = 0; jj < NK; ++jj) {
@@ -342,7 +351,7 @@ struct LdImgIC : ICLayout<ROWS, BK> {
       const int ih = oh * d.sa + dri + d.off;
       const int iw = ow * d.sa + dsi + d.off;
       const bool ok = colv && m < d.M && (unsigned)ih < (unsigned)d.H && (unsigned)iw < (unsigned)d.W;
-      v[jj] = bload4(rs, ok ? (uint32_t)(((n * d.H + ih) * d.W + iw) * d.C + c) * 4u : kOOB);
+      v[jj] = bload4e<typename D::Elem>(rs, ok, (uint32_t)(((n * d.H + ih) * d.W + iw) * d.C + c));
       om |= (uint32_t)ok << jj;
     }
     if constexpr (D::kBnIn) okm = om;
@@ -372,13 +381,14 @@ struct LdImgIC : ICLayout<ROWS, BK> {
 // with kColStats also fold a per-column reduction of what they store into a[e] / b[e].
 
 // out[m][n] = acc (+ bias[n]) (+ res[m][n]: a residual addend laid out like out).
-struct EpStore {
+template <class O>
+struct EpStoreT {  // O: output element type (float, or bf16_t: rounded on store)
   static constexpr bool kColStats = false;
-  float* out;
+  O* out;
   int ldo;
   const float* bias;
-  int v4;  // out, ldo, bias and res allow 16-byte access
-  const float* res;
+  int v4;  // out, ldo, bias and res allow 16-byte (4-element) access
+  const O* res;
   // per-row operands the 16-byte path needs, loaded for all of a thread's rows before any
   // store (loads cannot be hoisted over stores to a possibly aliasing output)
   struct Pre {
@@ -392,31 +402,34 @@ struct EpStore {
   __device__ __forceinline__ f32x4 value4(int n, f32x4 v, const Pre& p) const {
     if (bias) v += ld4(bias + n);
     if (res) v += p.r;
-    return v;
+    return rnd4<O>(v);  // the value the store keeps
   }
   __device__ __forceinline__ float value1(int m, int n, float v) const {
     if (bias) v += bias[n];
-    if (res) v += res[(size_t)m * ldo + n];
-    return v;
+    if (res) v += ld1(res + (size_t)m * ldo + n);
+    return rnd1<O>(v);
   }
   __device__ __forceinline__ void put4(int m, int n, f32x4 v, const Pre& p, int, double*, double*) const {
     st4(out + (size_t)m * ldo + n, value4(n, v, p));
   }
   __device__ __forceinline__ void put1(int m, int n, float v, int, double&, double&) const {
-    out[(size_t)m * ldo + n] = value1(m, n, v);
+    st1(out + (size_t)m * ldo + n, value1(m, n, v));
   }
 };
+using EpStore = EpStoreT<float>;
 
 // EpStore + the BatchNorm statistics of the stored output (layers/batch_norm.py:76-80's
 // mean/var, as fp64 sum / sum of squares per column): part[m_tile][2][N], one row per
 // BM-row tile, reduced in a fixed order by dk_bn_stats_from_partials_f32.  Saves the
 // separate statistics pass over y.
-struct EpStoreStats : EpStore {
+template <class O>
+struct EpStoreStatsT : EpStoreT<O> {
   static constexpr bool kColStats = true;
+  using Pre = typename EpStoreT<O>::Pre;
   double* part;
   __device__ __forceinline__ void put4(int m, int n, f32x4 v, const Pre& p, int, double* a, double* b) const {
-    const f32x4 o = value4(n, v, p);
-    st4(out + (size_t)m * ldo + n, o);
+    const f32x4 o = this->value4(n, v, p);
+    st4(this->out + (size_t)m * this->ldo + n, o);
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const double d = (double)o[e];
@@ -425,12 +438,13 @@ struct EpStoreStats : EpStore {
     }
   }
   __device__ __forceinline__ void put1(int m, int n, float v, int, double& a, double& b) const {
-    const float o = value1(m, n, v);
-    out[(size_t)m * ldo + n] = o;
+    const float o = this->value1(m, n, v);
+    st1(this->out + (size_t)m * this->ldo + n, o);
     a += (double)o;
     b += (double)o * (double)o;
   }
 };
+using EpStoreStats = EpStoreStatsT<float>;
 
 // The BatchNorm-backward reduction of the layer whose input gradient this GEMM produces
 // (batch_norm.py:125-174's sum(dy) and sum(dy * x_hat), with the fused ReLU's mask
@@ -448,27 +462,31 @@ __device__ __forceinline__ void bn_bwd_contrib4(f32x4 g, f32x4 x, const BnIn& bn
   for (int e = 0; e < 4; ++e) bn_bwd_contrib(g[e], x[e], mu[e], is[e], ga[e], be[e], bn.relu, a[e], b[e]);
 }
 
-struct EpStoreBnBwd : EpStore {
+template <class O>
+struct EpStoreBnBwdT : EpStoreT<O> {
   static constexpr bool kColStats = true;
+  using Pre = typename EpStoreT<O>::Pre;
   double* part;
-  const float* xbn;  // [M][ldo], the BN's raw input
+  const O* xbn;  // [M][ldo], the BN's raw input
   BnIn bn;
   __device__ __forceinline__ Pre pre4(int m, int n) const {
-    Pre p = EpStore::pre4(m, n);
-    p.x = ld4(xbn + (size_t)m * ldo + n);
+    Pre p = EpStoreT<O>::pre4(m, n);
+    p.x = ld4(xbn + (size_t)m * this->ldo + n);
     return p;
   }
   __device__ __forceinline__ void put4(int m, int n, f32x4 v, const Pre& p, int, double* a, double* b) const {
-    v = value4(n, v, p);
-    st4(out + (size_t)m * ldo + n, v);
+    v = this->value4(n, v, p);
+    st4(this->out + (size_t)m * this->ldo + n, v);
     bn_bwd_contrib4(v, p.x, bn, n, a, b);
   }
   __device__ __forceinline__ void put1(int m, int n, float v, int, double& a, double& b) const {
-    v = value1(m, n, v);
-    out[(size_t)m * ldo + n] = v;
-    bn_bwd_contrib(v, xbn[(size_t)m * ldo + n], bn.mean[n], bn.invstd[n], bn.gamma[n], bn.beta[n], bn.relu, a, b);
+    v = this->value1(m, n, v);
+    const size_t o = (size_t)m * this->ldo + n;
+    st1(this->out + o, v);
+    bn_bwd_contrib(v, ld1(xbn + o), bn.mean[n], bn.invstd[n], bn.gamma[n], bn.beta[n], bn.relu, a, b);
   }
 };
+using EpStoreBnBwd = EpStoreBnBwdT<float>;
 
 // Pointwise stride-st backward "widen" (pointwise_convolution.py:68-72) fused: the GEMM
 // row m = (b, oh, ow) of an OH x OW grid lands at (b, oh*st, ow*st) of an
@@ -1314,4 +1332,105 @@ DK_API int dk_dense_wgrad_f32(const float* x, const float* dy, int B, int IN, in
     rc = igemm_splitk<LdMatIC1, MatDesc, LdMatIC1, MatDesc>(a, b, static_cast<float*>(ws), IN, OUT, B, st, &splits);
   if (rc) return rc;
   return splitk_reduce(static_cast<float*>(ws), splits, IN, OUT, dw_io, w_io, l2, 0, OUT, OUT, 1, 1, st);
+}
+
+// ---------------------------------------------------------------------------------------
+// bf16 storage twins of the pointwise entries (BASELINE config 5).  Activations bf16,
+// weights / statistics / weight gradients fp32; the loaders widen bf16 to fp32 on load and
+// the MFMAs are the exact-fp32 v_mfma_f32_32x32x2_f32 of the fp32 path, so the only
+// numerical difference from fp32 storage is the rounding of each stored activation.
+// ---------------------------------------------------------------------------------------
+namespace dk {
+static inline MatDescE<bf16_t> mat_h(const bf16_t* p, int rows, int ld, int ext) {
+  return MatDescE<bf16_t>{p, (uint32_t)((size_t)rows * ld * sizeof(bf16_t)), ld, ext};
+}
+static inline ImgDescE<bf16_t> img_h(const bf16_t* x, int N, int H, int W, int C, int OH, int OW, int R, int S,
+                                     int sa, int dr, int off, int M) {
+  return ImgDescE<bf16_t>{x,  (uint32_t)((size_t)N * H * W * C * sizeof(bf16_t)), H, W, C, OH, OW, R, S, sa, dr, off,
+                          M};
+}
+static inline bool al8(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 7) == 0; }
+}  // namespace dk
+
+DK_API int dk_pwconv_fwd_ex_bf16(const bf16_t* x, int N, int H, int W, int C, const float* w_kc, int K, int stride,
+                                 const float* bias, bf16_t* y, int OH, int OW, const float* bn_mean,
+                                 const float* bn_invstd, const float* bn_gamma, const float* bn_beta, int bn_relu,
+                                 double* stats, void* stream) {
+  if (C % 4 || K % 4 || !al8(x) || !al8(y) || !aligned16(w_kc) || (bias && !aligned16(bias))) return DK_ERR_ARGS;
+  if (!fits((size_t)N * H * W * C * 4) || !fits((size_t)N * OH * OW * K * 4)) return DK_ERR_ARGS;
+  const ImgDescE<bf16_t> a = img_h(x, N, H, W, C, OH, OW, 1, 1, stride, 1, 0, N * OH * OW);
+  const MatDesc b = mat(w_kc, K, C, K);
+  const hipStream_t st = as_stream(stream);
+  const int M = a.M;
+  auto run = [&](const auto& da) -> int {
+    using DA = std::decay_t<decltype(da)>;
+    if (stats) {
+      EpStoreStatsT<bf16_t> ep{};
+      ep.out = y, ep.ldo = K, ep.bias = bias, ep.v4 = 1, ep.res = nullptr, ep.part = stats;
+      return igemm_rows<LdImgKC, DA, LdMatKC, MatDesc, EpStoreStatsT<bf16_t>>(da, b, ep, M, K, C, st);
+    }
+    EpStoreT<bf16_t> ep{y, K, bias, 1, nullptr};
+    return igemm_rows<LdImgKC, DA, LdMatKC, MatDesc, EpStoreT<bf16_t>>(da, b, ep, M, K, C, st);
+  };
+  if (bn_mean) {
+    if (!bn_ok(bn_mean, bn_invstd, bn_gamma, bn_beta) || C > 2048) return DK_ERR_ARGS;
+    ImgBnDescE<bf16_t> ab;
+    static_cast<ImgDescE<bf16_t>&>(ab) = a;
+    ab.bn = BnIn{bn_mean, bn_invstd, bn_gamma, bn_beta, bn_relu};
+    return run(ab);
+  }
+  return run(a);
+}
+
+// Stride-1 pointwise dgrad (bf16): dx = dy . W (+ residual) and, with bn_x/part, the
+// BN-backward partials of the BatchNorm whose output the layer consumed.
+DK_API int dk_pwconv_dgrad_ex_bf16(const bf16_t* dy, int N, int OH, int OW, int K, const float* w_kc, int C,
+                                   int stride, bf16_t* dx, const bf16_t* residual, const bf16_t* bn_x,
+                                   const float* bn_mean, const float* bn_invstd, const float* bn_gamma,
+                                   const float* bn_beta, int bn_relu, double* part, void* stream) {
+  const int M = N * OH * OW;
+  if (stride != 1 || C % 4 || K % 4 || !al8(dy) || !al8(dx) || !aligned16(w_kc)) return DK_ERR_ARGS;
+  if ((residual && !al8(residual)) || (bn_x && !al8(bn_x))) return DK_ERR_ARGS;
+  if (!fits((size_t)M * K * 4) || !fits((size_t)M * C * 4) || (part != nullptr) != (bn_x != nullptr)) return DK_ERR_ARGS;
+  const MatDescE<bf16_t> a = mat_h(dy, M, K, M);
+  const MatDesc b = mat(w_kc, K, C, C);
+  const hipStream_t st = as_stream(stream);
+  if (!part) {
+    EpStoreT<bf16_t> ep{dx, C, nullptr, 1, residual};
+    return igemm_rows<LdMatKC, MatDescE<bf16_t>, LdMatIC, MatDesc, EpStoreT<bf16_t>>(a, b, ep, M, C, K, st);
+  }
+  if (!bn_ok(bn_mean, bn_invstd, bn_gamma, bn_beta)) return DK_ERR_ARGS;
+  EpStoreBnBwdT<bf16_t> ep{};
+  ep.out = dx, ep.ldo = C, ep.bias = nullptr, ep.v4 = 1, ep.res = residual;
+  ep.part = part;
+  ep.xbn = bn_x;
+  ep.bn = BnIn{bn_mean, bn_invstd, bn_gamma, bn_beta, bn_relu};
+  return igemm_rows<LdMatKC, MatDescE<bf16_t>, LdMatIC, MatDesc, EpStoreBnBwdT<bf16_t>>(a, b, ep, M, C, K, st);
+}
+
+// dw[k][c] = sum dy[m][k] * bn(x)[m][c] (+ l2 * w), bf16 activations, fp32 result.
+DK_API int dk_pwconv_wgrad_bnx_bf16(const bf16_t* dy, const bf16_t* x, int N, int H, int W, int C, int K, int stride,
+                                    int OH, int OW, const float* w_kc, float l2, float* dw_kc, void* ws,
+                                    size_t ws_bytes, const float* bn_mean, const float* bn_invstd,
+                                    const float* bn_gamma, const float* bn_beta, int bn_relu, void* stream) {
+  const int Kred = N * OH * OW;
+  if (C % 4 || K % 4 || !al8(x) || !al8(dy) || !fits((size_t)N * H * W * C * 4) || !fits((size_t)Kred * K * 4))
+    return DK_ERR_ARGS;
+  if (ws_bytes < splitk_ws_bytes(K, C, Kred)) return DK_ERR_WORKSPACE;
+  const MatDescE<bf16_t> a = mat_h(dy, Kred, K, K);
+  const ImgDescE<bf16_t> bi = img_h(x, N, H, W, C, OH, OW, 1, 1, stride, 1, 0, Kred);
+  float* part = static_cast<float*>(ws);
+  const hipStream_t st = as_stream(stream);
+  int splits = 1, rc;
+  if (bn_mean) {
+    if (!bn_ok(bn_mean, bn_invstd, bn_gamma, bn_beta)) return DK_ERR_ARGS;
+    ImgBnDescE<bf16_t> b;
+    static_cast<ImgDescE<bf16_t>&>(b) = bi;
+    b.bn = BnIn{bn_mean, bn_invstd, bn_gamma, bn_beta, bn_relu};
+    rc = igemm_splitk<LdMatIC, MatDescE<bf16_t>, LdImgIC, ImgBnDescE<bf16_t>>(a, b, part, K, C, Kred, st, &splits);
+  } else {
+    rc = igemm_splitk<LdMatIC, MatDescE<bf16_t>, LdImgIC, ImgDescE<bf16_t>>(a, bi, part, K, C, Kred, st, &splits);
+  }
+  if (rc) return rc;
+  return splitk_reduce(part, splits, K, C, dw_kc, w_kc, l2, 0, C, C, 1, 1, st);
 }

@@ -62,10 +62,10 @@ class BNOut:
         """The normalised tensor itself (computed once)."""
         if self._y is None:
             x = self.x
-            y = empty_nhwc(*x.shape) if x.dim() == 4 else torch.empty_like(x)
-            lib.dk_bn_apply_f32(x.data_ptr(), x.numel(), x.shape[1], self.mean.data_ptr(), self.invstd.data_ptr(),
-                                self.gamma.data_ptr(), self.beta.data_ptr(), int(self.relu), y.data_ptr(), 0,
-                                stream_handle())
+            y = empty_nhwc(*x.shape, dtype=x.dtype) if x.dim() == 4 else torch.empty_like(x)
+            apply = lib.dk_bn_apply_bf16 if x.dtype == torch.bfloat16 else lib.dk_bn_apply_f32
+            apply(x.data_ptr(), x.numel(), x.shape[1], self.mean.data_ptr(), self.invstd.data_ptr(),
+                  self.gamma.data_ptr(), self.beta.data_ptr(), int(self.relu), y.data_ptr(), 0, stream_handle())
             self._y = y
         return self._y
 
@@ -85,7 +85,7 @@ def residual_operand(residual, like):
         return None
     from .._tensor import is_nhwc
     r = residual
-    if isinstance(r, torch.Tensor) and r.is_cuda and r.dtype == torch.float32 and tuple(r.shape) == tuple(
+    if isinstance(r, torch.Tensor) and r.is_cuda and r.dtype == like.dtype and tuple(r.shape) == tuple(
             like.shape) and r.dim() == 4 and is_nhwc(r):
         return r
     return None

@@ -11,13 +11,13 @@ from __future__ import annotations
 import torch
 
 from .._hip import lib, stream_handle
-from .._tensor import as_device, empty_nhwc, is_nhwc as is_nhwc_t, rows, to_nhwc
+from .._tensor import act_dtype, as_device, empty_nhwc, is_nhwc as is_nhwc_t, rows, to_nhwc
 from ._bn_input import BNOut
 from .layer import Layer
 
 
 def _same_layout(X):
-    X = as_device(X)
+    X = as_device(X, act_dtype(X))
     return to_nhwc(X) if X.dim() == 4 else rows(X)
 
 
@@ -33,7 +33,7 @@ class ReLu(Layer):
         return "ReLu({})".format(self.layer_name)
 
     def _empty_like(self, x):
-        return empty_nhwc(*x.shape) if x.dim() == 4 else torch.empty_like(x)
+        return empty_nhwc(*x.shape, dtype=x.dtype) if x.dim() == 4 else torch.empty_like(x)
 
     def forward(self, X, test_mode=False):
         self._require_on_gpu()
@@ -44,7 +44,8 @@ class ReLu(Layer):
         if not test_mode:
             mask = torch.empty(x.shape, dtype=torch.uint8, device=x.device,
                                memory_format=torch.channels_last if x.dim() == 4 else torch.contiguous_format)
-        lib.dk_relu_fwd_f32(x.data_ptr(), x.numel(), y.data_ptr(), 0 if mask is None else mask.data_ptr(), st)
+        fwd = lib.dk_relu_fwd_bf16 if x.dtype == torch.bfloat16 else lib.dk_relu_fwd_f32
+        fwd(x.data_ptr(), x.numel(), y.data_ptr(), 0 if mask is None else mask.data_ptr(), st)
         if not test_mode:
             self._mask, self._fused_out, self._join_bn = mask, None, None
         return y
@@ -135,7 +136,8 @@ class ReLu(Layer):
                                            *bn.bn_args(), dx.data_ptr(), part.data_ptr(), nb, stream_handle())
             bn.hand_backward_partials(dx, part)
             return dx
-        lib.dk_relu_bwd_f32(dy.data_ptr(), self._mask.data_ptr(), dy.numel(), dx.data_ptr(), stream_handle())
+        bwd = lib.dk_relu_bwd_bf16 if dy.dtype == torch.bfloat16 else lib.dk_relu_bwd_f32
+        bwd(dy.data_ptr(), self._mask.data_ptr(), dy.numel(), dx.data_ptr(), stream_handle())
         return dx
 
     def save_to_h5(self, open_f, save_grads=True):

@@ -21,7 +21,7 @@ from __future__ import annotations
 import torch
 
 from .._hip import lib, stream_handle, tickets, workspace
-from .._tensor import as_device, empty_nhwc, rows, to_nhwc
+from .._tensor import BF16, act_dtype, as_device, empty_nhwc, rows, to_nhwc
 from ._common import grad_buffer
 from .layer import Layer
 
@@ -78,7 +78,7 @@ class BatchNormLayer(Layer):
 
     def _out_like(self, x):
         if x.dim() == 4:
-            return empty_nhwc(*x.shape)
+            return empty_nhwc(*x.shape, dtype=x.dtype)
         return torch.empty_like(x)
 
     def _world(self):
@@ -113,9 +113,10 @@ class BatchNormLayer(Layer):
                                                   rs.data_ptr(), ws, nb, tickets.get(lib.dk_bn_fold_tickets_count(C)),
                                                   st)
             else:
-                lib.dk_bn_stats_f32(x.data_ptr(), P, C, float(self.eps), float(self.run_momentum), int(first),
-                                    mean.data_ptr(), std.data_ptr(), invstd.data_ptr(), rm.data_ptr(),
-                                    rs.data_ptr(), ws, nb, st)
+                stats_fn = lib.dk_bn_stats_bf16 if x.dtype == BF16 else lib.dk_bn_stats_f32
+                stats_fn(x.data_ptr(), P, C, float(self.eps), float(self.run_momentum), int(first),
+                         mean.data_ptr(), std.data_ptr(), invstd.data_ptr(), rm.data_ptr(), rs.data_ptr(), ws, nb,
+                         st)
         else:
             import torch.distributed as dist
             sums = torch.empty(2 * C, dtype=torch.float64, device=dev)
@@ -140,7 +141,9 @@ class BatchNormLayer(Layer):
         already computed by the layer that produced it (layers/_chain.StatsRequest)."""
         self._require_on_gpu()
         st = stream_handle()
-        x, P, C = self._prep_input(as_device(X))
+        x, P, C = self._prep_input(as_device(X, act_dtype(X)))
+        if x.dtype == BF16 and (x.dim() != 4 or self.sync_group is not None):
+            raise NotImplementedError("bf16 storage: 4-D inputs, local statistics only")
         self.input_shape = tuple(x.shape)
         self._pending_bwd = None
         if not test_mode:
@@ -160,8 +163,9 @@ class BatchNormLayer(Layer):
         x, mean, invstd = self._normalisation(X, test_mode, stats)
         gamma, beta = self.learned_params["gamma"], self.learned_params["beta"]
         y = self._out_like(x)
-        lib.dk_bn_apply_f32(x.data_ptr(), x.numel(), x.shape[1], mean.data_ptr(), invstd.data_ptr(),
-                            gamma.data_ptr(), beta.data_ptr(), int(relu), y.data_ptr(), 0, stream_handle())
+        apply = lib.dk_bn_apply_bf16 if x.dtype == BF16 else lib.dk_bn_apply_f32
+        apply(x.data_ptr(), x.numel(), x.shape[1], mean.data_ptr(), invstd.data_ptr(), gamma.data_ptr(),
+              beta.data_ptr(), int(relu), y.data_ptr(), 0, stream_handle())
         return y
 
     def forward_deferred(self, X, relu_layer=None, test_mode=False, stats=None):
@@ -192,6 +196,9 @@ class BatchNormLayer(Layer):
         st = stream_handle()
         x = self.X
         dy = to_nhwc(upstream_dx) if x.dim() == 4 else rows(upstream_dx)
+        bf = x.dtype == BF16
+        if bf and dy.dtype != BF16:
+            raise ValueError("{}: bf16 activations need a bf16 gradient".format(self.layer_name))
         C = x.shape[1]
         P = x.numel() // C
         gamma, beta = self.learned_params["gamma"], self.learned_params["beta"]
@@ -218,14 +225,15 @@ class BatchNormLayer(Layer):
                 dist.all_reduce(glob, group=self.sync_group)
                 lib.dk_bn_bwd_finalize_f32(local.data_ptr(), 1, glob.data_ptr(), 1, C, float(P) * self._world(),
                                            dgamma.data_ptr(), dbeta.data_ptr(), k12.data_ptr(), st)
-            lib.dk_bn_bwd_apply_f32(x.data_ptr(), dy.data_ptr(), x.numel(), C, self._mean.data_ptr(),
-                                    self._invstd.data_ptr(), gamma.data_ptr(), beta.data_ptr(), int(relu),
-                                    k12.data_ptr(), dx.data_ptr(), st)
+            (lib.dk_bn_bwd_apply_bf16 if bf else lib.dk_bn_bwd_apply_f32)(
+                x.data_ptr(), dy.data_ptr(), x.numel(), C, self._mean.data_ptr(), self._invstd.data_ptr(),
+                gamma.data_ptr(), beta.data_ptr(), int(relu), k12.data_ptr(), dx.data_ptr(), st)
         elif self.sync_group is None:
             nb = lib.dk_bn_bwd_workspace_bytes(P, C)
-            lib.dk_bn_bwd_f32(x.data_ptr(), dy.data_ptr(), P, C, self._mean.data_ptr(), self._invstd.data_ptr(),
-                              gamma.data_ptr(), beta.data_ptr(), int(relu), dgamma.data_ptr(), dbeta.data_ptr(),
-                              dx.data_ptr(), workspace.get(nb), nb, st)
+            (lib.dk_bn_bwd_bf16 if bf else lib.dk_bn_bwd_f32)(
+                x.data_ptr(), dy.data_ptr(), P, C, self._mean.data_ptr(), self._invstd.data_ptr(), gamma.data_ptr(),
+                beta.data_ptr(), int(relu), dgamma.data_ptr(), dbeta.data_ptr(), dx.data_ptr(), workspace.get(nb), nb,
+                st)
         else:
             import torch.distributed as dist
             nb = lib.dk_bn_workspace_bytes(P, C)
@@ -242,9 +250,9 @@ class BatchNormLayer(Layer):
             k12 = torch.empty(2 * C, dtype=torch.float32, device=x.device)
             lib.dk_bn_bwd_finalize_f32(local.data_ptr(), 1, glob.data_ptr(), 1, C, float(P) * self._world(),
                                        dgamma.data_ptr(), dbeta.data_ptr(), k12.data_ptr(), st)
-            lib.dk_bn_bwd_apply_f32(x.data_ptr(), dy.data_ptr(), x.numel(), C, self._mean.data_ptr(),
-                                    self._invstd.data_ptr(), gamma.data_ptr(), beta.data_ptr(), int(relu),
-                                    k12.data_ptr(), dx.data_ptr(), st)
+            (lib.dk_bn_bwd_apply_bf16 if bf else lib.dk_bn_bwd_apply_f32)(
+                x.data_ptr(), dy.data_ptr(), x.numel(), C, self._mean.data_ptr(), self._invstd.data_ptr(),
+                gamma.data_ptr(), beta.data_ptr(), int(relu), k12.data_ptr(), dx.data_ptr(), st)
         return dx
 
     def backward(self, upstream_dx):

@@ -14,7 +14,7 @@ from __future__ import annotations
 import torch
 
 from .._hip import HipError, lib, stream_handle, weight_grad_stream, workspace
-from .._tensor import empty_nhwc, ptr, to_nhwc
+from .._tensor import BF16, empty_nhwc, ptr, to_nhwc
 from ._bn_input import BNOut, add_residual, residual_operand
 from ._common import add_regulariser_grad, grad_buffer, init_weights, l2_strength
 from .layer import Layer
@@ -76,7 +76,8 @@ class DepthwiseConvLayer(Layer):
         self.num_row_patches = ((H + 2 * self.padding - R) / self.stride) + 1
         self.num_col_patches = ((W + 2 * self.padding - S) / self.stride) + 1
         OH, OW = int(self.num_row_patches), int(self.num_col_patches)
-        y = empty_nhwc(N, C, OH, OW)
+        bf = x.dtype == BF16  # bf16 storage (BASELINE config 5): the _bf16 entry points
+        y = empty_nhwc(N, C, OH, OW, x.dtype)
         bias = self.learned_params["bias"] if self.with_bias else None
         stats = None
         if bn_stats is not None and not test_mode and self.stride in (1, 2):
@@ -84,9 +85,9 @@ class DepthwiseConvLayer(Layer):
             if rows:
                 stats = torch.empty((rows, 2, C), dtype=torch.float64, device=x.device)
         w = self.learned_params["weights"]  # W[C][R][S], read in place by the _ex entry
-        lib.dk_dwconv_fwd_ex_f32(x.data_ptr(), N, H, W, C, w.data_ptr(), R, S, self.stride, self.padding, ptr(bias),
-                                 y.data_ptr(), OH, OW, *(bn.bn_args() if bn is not None else (0, 0, 0, 0, 0)),
-                                 ptr(stats), st)
+        fwd = lib.dk_dwconv_fwd_ex_bf16 if bf else lib.dk_dwconv_fwd_ex_f32
+        fwd(x.data_ptr(), N, H, W, C, w.data_ptr(), R, S, self.stride, self.padding, ptr(bias), y.data_ptr(), OH, OW,
+            *(bn.bn_args() if bn is not None else (0, 0, 0, 0, 0)), ptr(stats), st)
         if stats is not None:
             bn_stats.part, bn_stats.rows = stats, stats.shape[0]
         if not test_mode:
@@ -108,6 +109,9 @@ class DepthwiseConvLayer(Layer):
         OH, OW = int(self.num_row_patches), int(self.num_col_patches)
         P = N * OH * OW
         w = self.learned_params["weights"]
+        bf = x.dtype == BF16
+        if bf and (dy.dtype != BF16 or self.with_bias):
+            raise NotImplementedError("{}: bf16 storage needs a bf16 gradient and no bias".format(self.layer_name))
         # the weight gradient runs on the side stream (_hip.weight_grad_stream)
         with weight_grad_stream(dy, x, *self._bn_tensors()):
             sst = stream_handle()
@@ -118,7 +122,12 @@ class DepthwiseConvLayer(Layer):
             gw = grad_buffer(self, "weights", (C, R, S))
             s = l2_strength(self.weight_regulariser)
             nb = lib.dk_dwconv_wgrad_workspace_bytes(N, OH, OW, C, R, S)
-            if self._bn_in is not None:
+            if bf:
+                lib.dk_dwconv_wgrad_bnx_bf16(
+                    dy.data_ptr(), x.data_ptr(), N, H, W, C, R, S, self.stride, self.padding, OH, OW,
+                    w.data_ptr() if s else 0, s or 0.0, gw.data_ptr(), workspace.get(nb), nb,
+                    *(self._bn_in.bn_args() if self._bn_in is not None else (0, 0, 0, 0, 0)), sst)
+            elif self._bn_in is not None:
                 lib.dk_dwconv_wgrad_bnx_f32(dy.data_ptr(), x.data_ptr(), N, H, W, C, R, S, self.stride,
                                             self.padding, OH, OW, w.data_ptr() if s else 0, s or 0.0, gw.data_ptr(),
                                             workspace.get(nb), nb, *self._bn_in.bn_args(), sst)
@@ -128,18 +137,24 @@ class DepthwiseConvLayer(Layer):
                                         sst)
             if s is None:
                 add_regulariser_grad(gw, w, self.weight_regulariser)
-        dx = empty_nhwc(N, C, H, W)
+        dx = empty_nhwc(N, C, H, W, x.dtype)
         nb = lib.dk_dwconv_dgrad_workspace_bytes(C, R, S)
+        dgrad_ex = lib.dk_dwconv_dgrad_ex_bf16 if bf else lib.dk_dwconv_dgrad_ex_f32
         bn = self._bn_in
         res = residual_operand(residual, dx)
         rows = lib.dk_dwconv_dgrad_stats_rows(N, H, W, C, self.stride) if bn is not None and R == S else 0
         if rows and self.padding <= R - 1:
             # + stage 1 of the input BatchNorm's backward, in the dgrad epilogue (+ the residual)
             part = torch.empty((rows, 2, C), dtype=torch.float64, device=dx.device)
-            lib.dk_dwconv_dgrad_ex_f32(dy.data_ptr(), N, OH, OW, C, w.data_ptr(), R, S, self.stride, self.padding,
-                                       dx.data_ptr(), H, W, workspace.get(nb), nb, ptr(res), bn.x.data_ptr(),
-                                       *bn.bn_args(), part.data_ptr(), st)
+            dgrad_ex(dy.data_ptr(), N, OH, OW, C, w.data_ptr(), R, S, self.stride, self.padding, dx.data_ptr(), H, W,
+                     workspace.get(nb), nb, ptr(res), bn.x.data_ptr(), *bn.bn_args(), part.data_ptr(), st)
             bn.hand_backward_partials(dx, part)
+            return dx
+        if bf:
+            if residual is not None and res is None:
+                raise NotImplementedError("{}: bf16 residual must be a bf16 NHWC tensor".format(self.layer_name))
+            dgrad_ex(dy.data_ptr(), N, OH, OW, C, w.data_ptr(), R, S, self.stride, self.padding, dx.data_ptr(), H, W,
+                     workspace.get(nb), nb, ptr(res), 0, 0, 0, 0, 0, 0, 0, st)
             return dx
         if res is not None:
             try:

@@ -15,7 +15,7 @@ from __future__ import annotations
 import torch
 
 from .._hip import lib, stream_handle, weight_grad_stream, workspace
-from .._tensor import empty_nhwc, ptr, to_nhwc
+from .._tensor import BF16, empty_nhwc, ptr, to_nhwc
 from ._bn_input import BNOut, add_residual, residual_operand
 from ._common import add_regulariser_grad, grad_buffer, init_weights, l2_strength
 from .layer import Layer
@@ -67,7 +67,8 @@ class PointwiseConvLayer(Layer):
         K = self.num_filters
         s = self.stride
         OH, OW = -(-H // s), -(-W // s)  # len(range(0, H, s)), as X[:, :, ::s, ::s]
-        y = empty_nhwc(N, K, OH, OW)
+        bf = x.dtype == BF16  # bf16 storage (BASELINE config 5): the _bf16 entry points
+        y = empty_nhwc(N, K, OH, OW, x.dtype)
         w = self.learned_params["weights"]
         if Cp != self.num_channels:
             raise ValueError("PointwiseConvLayer {}: input has {} channels, weights expect {} (a multiple of 4 "
@@ -77,9 +78,10 @@ class PointwiseConvLayer(Layer):
         if bn_stats is not None and not test_mode:
             rows = lib.dk_pwconv_fwd_stats_rows(N, OH, OW, K, Cp)
             stats = torch.empty((rows, 2, K), dtype=torch.float64, device=x.device)
-        if bn is not None or stats is not None:
-            lib.dk_pwconv_fwd_ex_f32(x.data_ptr(), N, H, W, Cp, w.data_ptr(), K, s, ptr(bias), y.data_ptr(), OH, OW,
-                                     *(bn.bn_args() if bn is not None else (0, 0, 0, 0, 0)), ptr(stats), st)
+        if bn is not None or stats is not None or bf:
+            fwd = lib.dk_pwconv_fwd_ex_bf16 if bf else lib.dk_pwconv_fwd_ex_f32
+            fwd(x.data_ptr(), N, H, W, Cp, w.data_ptr(), K, s, ptr(bias), y.data_ptr(), OH, OW,
+                *(bn.bn_args() if bn is not None else (0, 0, 0, 0, 0)), ptr(stats), st)
             if stats is not None:
                 bn_stats.part, bn_stats.rows = stats, stats.shape[0]
         else:
@@ -103,6 +105,10 @@ class PointwiseConvLayer(Layer):
         OH, OW = self.out_hw
         P = N * OH * OW
         w = self.learned_params["weights"]
+        bf = x.dtype == BF16
+        if bf and (dy.dtype != BF16 or self.with_bias or s != 1):
+            raise NotImplementedError("{}: bf16 storage needs a bf16 gradient, no bias, stride 1".format(
+                self.layer_name))
         # the weight gradient runs on the side stream (_hip.weight_grad_stream)
         with weight_grad_stream(dy, x, *self._bn_tensors()):
             sst = stream_handle()
@@ -113,7 +119,12 @@ class PointwiseConvLayer(Layer):
             gw = grad_buffer(self, "weights", (K, C))
             l2s = l2_strength(self.weight_regulariser)
             nb = lib.dk_pwconv_wgrad_workspace_bytes(N, OH, OW, K, C)
-            if self._bn_in is not None:
+            if bf:
+                lib.dk_pwconv_wgrad_bnx_bf16(
+                    dy.data_ptr(), x.data_ptr(), N, H, W, C, K, s, OH, OW, w.data_ptr() if l2s else 0, l2s or 0.0,
+                    gw.data_ptr(), workspace.get(nb), nb,
+                    *(self._bn_in.bn_args() if self._bn_in is not None else (0, 0, 0, 0, 0)), sst)
+            elif self._bn_in is not None:
                 lib.dk_pwconv_wgrad_bnx_f32(dy.data_ptr(), x.data_ptr(), N, H, W, C, K, s, OH, OW,
                                             w.data_ptr() if l2s else 0, l2s or 0.0, gw.data_ptr(), workspace.get(nb),
                                             nb, *self._bn_in.bn_args(), sst)
@@ -123,9 +134,22 @@ class PointwiseConvLayer(Layer):
                                         sst)
             if l2s is None:
                 add_regulariser_grad(gw, w, self.weight_regulariser)
-        dx = empty_nhwc(N, C, OH * s, OW * s)  # widened shape, pointwise_convolution.py:68-72
+        dx = empty_nhwc(N, C, OH * s, OW * s, x.dtype)  # widened shape, pointwise_convolution.py:68-72
         bn = self._bn_in
         res = residual_operand(residual, dx)
+        if bf:
+            if residual is not None and res is None:
+                raise NotImplementedError("{}: bf16 residual must be a bf16 NHWC tensor".format(self.layer_name))
+            if bn is not None and (OH, OW) == (H, W):
+                rows = lib.dk_pwconv_dgrad_stats_rows(N, OH, OW, K, C)
+                part = torch.empty((rows, 2, C), dtype=torch.float64, device=dx.device)
+                lib.dk_pwconv_dgrad_ex_bf16(dy.data_ptr(), N, OH, OW, K, w.data_ptr(), C, s, dx.data_ptr(), ptr(res),
+                                            bn.x.data_ptr(), *bn.bn_args(), part.data_ptr(), st)
+                bn.hand_backward_partials(dx, part)
+            else:
+                lib.dk_pwconv_dgrad_ex_bf16(dy.data_ptr(), N, OH, OW, K, w.data_ptr(), C, s, dx.data_ptr(), ptr(res),
+                                            0, 0, 0, 0, 0, 0, 0, st)
+            return dx
         if bn is not None and (OH * s, OW * s) == (H, W) and (res is None or s == 1):
             # + stage 1 of the input BatchNorm's backward, in the dgrad epilogue
             rows = lib.dk_pwconv_dgrad_stats_rows(N, OH, OW, K, C)

@@ -148,8 +148,13 @@ class FeedForwardNetwork:
             loss += sum(regularisation_terms)
         return loss, X  # NB if test_mode=True, you get softmax scores ("logits")
 
-    def backward(self):
-        if self.loss_layer is not None:
+    def backward(self, upstream_dx=None):
+        """Reference behaviour (feed_forward_network.py:62-70): backward from the loss layer.
+        Extension: an explicit output gradient for a network without a loss layer (BASELINE
+        config 5's stack is driven this way)."""
+        if upstream_dx is not None:
+            pass
+        elif self.loss_layer is not None:
             upstream_dx = self.loss_layer.backward()
         else:
             raise ValueError("Network doesn't have a loss, can't run backward pass.")

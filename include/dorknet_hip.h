@@ -120,6 +120,31 @@ int dk_dwconv_dgrad_stats_rows(int N, int H, int W, int C, int stride);
 int dk_dwconv_dgrad_ex_f32(const float* dy, int N, int OH, int OW, int C, const float* w_crs, int R, int S, int stride, int pad, float* dx, int H, int W, void* ws, size_t ws_bytes, const float* residual, const float* bn_x, const float* bn_mean, const float* bn_invstd, const float* bn_gamma, const float* bn_beta, int bn_relu, double* part, void* stream);
 
 /* ---------------------------------------------------------------------------------------
+ * bf16 storage twins (BASELINE config 5: the depthwise-separable stack with bf16 activations).
+ * Same contracts as the _f32 entries above, except that every activation / activation-
+ * gradient tensor (x, y, dy, dx, bn_x, residual) is bf16 (raw uint16_t bits, NHWC, C % 4 == 0);
+ * weights, biases, BatchNorm parameters / statistics and weight gradients stay fp32, and all
+ * arithmetic is fp32 (bf16 -> fp32 on load; fp32 -> bf16 round-to-nearest-even on store, the
+ * BatchNorm statistics / partials are taken over the rounded stored values).  Reference:
+ * the same layer methods as the _f32 twins (depthwise_convolution.py:85-102, :198-221;
+ * pointwise_convolution.py:46-75; batch_norm.py:54-174), which compute in fp32 throughout.
+ * ------------------------------------------------------------------------------------- */
+int dk_cast_f32_to_bf16(const float* x, long long n, uint16_t* y, void* stream);
+int dk_cast_bf16_to_f32(const uint16_t* x, long long n, float* y, void* stream);
+int dk_bn_stats_bf16(const uint16_t* x, int P, int C, float eps, float momentum, int first, float* mean, float* std_, float* invstd, float* run_mean, float* run_std, void* ws, size_t ws_bytes, void* stream);
+int dk_bn_apply_bf16(const uint16_t* x, long long numel, int C, const float* mean, const float* invstd, const float* gamma, const float* beta, int relu, uint16_t* y, uint8_t* mask, void* stream);
+int dk_bn_bwd_apply_bf16(const uint16_t* x, const uint16_t* dy, long long numel, int C, const float* mean, const float* invstd, const float* gamma, const float* beta, int relu, const float* k12, uint16_t* dx, void* stream);
+int dk_bn_bwd_bf16(const uint16_t* x, const uint16_t* dy, int P, int C, const float* mean, const float* invstd, const float* gamma, const float* beta, int relu, float* dgamma, float* dbeta, uint16_t* dx, void* ws, size_t ws_bytes, void* stream);
+int dk_relu_fwd_bf16(const uint16_t* x, long long n, uint16_t* y, uint8_t* mask, void* stream);
+int dk_relu_bwd_bf16(const uint16_t* dy, const uint8_t* mask, long long n, uint16_t* dx, void* stream);
+int dk_pwconv_fwd_ex_bf16(const uint16_t* x, int N, int H, int W, int C, const float* w_kc, int K, int stride, const float* bias, uint16_t* y, int OH, int OW, const float* bn_mean, const float* bn_invstd, const float* bn_gamma, const float* bn_beta, int bn_relu, double* stats, void* stream);
+int dk_pwconv_dgrad_ex_bf16(const uint16_t* dy, int N, int OH, int OW, int K, const float* w_kc, int C, int stride, uint16_t* dx, const uint16_t* residual, const uint16_t* bn_x, const float* bn_mean, const float* bn_invstd, const float* bn_gamma, const float* bn_beta, int bn_relu, double* part, void* stream);
+int dk_pwconv_wgrad_bnx_bf16(const uint16_t* dy, const uint16_t* x, int N, int H, int W, int C, int K, int stride, int OH, int OW, const float* w_kc, float l2, float* dw_kc, void* ws, size_t ws_bytes, const float* bn_mean, const float* bn_invstd, const float* bn_gamma, const float* bn_beta, int bn_relu, void* stream);
+int dk_dwconv_fwd_ex_bf16(const uint16_t* x, int N, int H, int W, int C, const float* w_crs, int R, int S, int stride, int pad, const float* bias, uint16_t* y, int OH, int OW, const float* bn_mean, const float* bn_invstd, const float* bn_gamma, const float* bn_beta, int bn_relu, double* stats, void* stream);
+int dk_dwconv_dgrad_ex_bf16(const uint16_t* dy, int N, int OH, int OW, int C, const float* w_crs, int R, int S, int stride, int pad, uint16_t* dx, int H, int W, void* ws, size_t ws_bytes, const uint16_t* residual, const uint16_t* bn_x, const float* bn_mean, const float* bn_invstd, const float* bn_gamma, const float* bn_beta, int bn_relu, double* part, void* stream);
+int dk_dwconv_wgrad_bnx_bf16(const uint16_t* dy, const uint16_t* x, int N, int H, int W, int C, int R, int S, int stride, int pad, int OH, int OW, const float* w_crs, float l2, float* dw_crs, void* ws, size_t ws_bytes, const float* bn_mean, const float* bn_invstd, const float* bn_gamma, const float* bn_beta, int bn_relu, void* stream);
+
+/* ---------------------------------------------------------------------------------------
  * Depthwise convolution, direct (no MFMA).
  * Replaces DepthwiseConvLayer.forward_cp (layers/depthwise_convolution.py:85-102, CUDA
  * forward_conv :105-121) and backward_cp (:198-221, CUDA backward_conv :122-140).
