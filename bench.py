@@ -40,6 +40,10 @@ def parse():
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=64, help="images in the CPU-baseline sample (0 = skip)")
     ap.add_argument("--cpu-steps", type=int, default=3, help="timed CPU-baseline steps (after one warm-up)")
+    ap.add_argument("--config", type=int, choices=[2, 3, 5], default=3,
+                    help="BASELINE config: 3 (default; 4 with --gpus N) = ResNet-18-depsep training step; "
+                         "2 = single 3x3 ConvLayer fwd+dgrad+wgrad; 5 = bf16 depthwise-separable stack "
+                         "(secondary lines, not the headline metric)")
     ap.add_argument("--pmc", default=None,
                     help="per-kernel HBM traffic from rocprofv3 FETCH_SIZE/WRITE_SIZE passes of this same command "
                          "(scripts/pmc_summary.py output; default: the newest profiles/*_pmc.json)")
@@ -180,8 +184,78 @@ def cpu_baseline(batch, steps=3):
                       "Cython kernels + numpy BLAS), {:.1f} s".format(steps, batch, dt)}
 
 
+def other_config(args):
+    """BASELINE configs 2 and 5 (one GPU): a secondary JSON line each, same timing rules
+    (warm-up, then K steps between synchronizations; inputs resident in HBM)."""
+    import numpy as np
+    import torch
+    from dorknet_amd import perfmodel
+    torch.cuda.set_device(0)
+    if args.config == 2:
+        from dorknet_amd.layers.convolution import ConvLayer
+        np.random.seed(0)
+        conv = ConvLayer("c", filter_block_shape=(64, 64, 3, 3), stride=1, padding=1, with_bias=False)
+        conv.to_gpu()
+        g = torch.Generator(device="cuda").manual_seed(0)
+        B = args.batch
+        X = torch.randn((B, 64, 56, 56), device="cuda", generator=g).contiguous(memory_format=torch.channels_last)
+        dY = torch.randn((B, 64, 56, 56), device="cuda", generator=g).contiguous(memory_format=torch.channels_last)
+
+        def step():
+            conv.forward(X)
+            conv.backward(dY)
+        flops = 3 * 2 * B * 56 * 56 * 64 * 64 * 9
+        unit, metric = "passes/s", "fwd+dgrad+wgrad passes/sec, ConvLayer(64,64,3,3) s1 p1 on 256x64x56x56"
+        dtype, workload = "fp32", "single 3x3 ConvLayer fwd+bwd, BASELINE config 2"
+    else:
+        from examples.mobilenet_stack import MobileNetStack, synthetic_input
+        from dorknet_amd.optimisers.SGDMomentum import SGDMomentum
+        np.random.seed(0)
+        net = MobileNetStack("mobilenet_style_bf16")
+        net.to_gpu()
+        sgd = SGDMomentum(net, 0.05 * args.batch / 200.0, 0.9)
+        X = synthetic_input(args.batch, seed=0)
+        g = torch.Generator(device="cuda").manual_seed(1)
+        dY = torch.randn((args.batch, 512, 7, 7), device="cuda", generator=g).to(torch.bfloat16)
+        dY = dY.contiguous(memory_format=torch.channels_last)
+
+        def step():
+            net.forward(X, None)
+            net.backward(dY)
+            sgd.update_weights()
+        flops = None
+        unit, metric = "images/s", "images/sec training step, MobileNet-style dw+pw stack bs=512 bf16, 1 MI355X"
+        dtype, workload = "bf16 storage / fp32 arithmetic", "16 depthwise-separable units (dw3x3-BN-pw-BN-ReLU), " \
+            "ResNet-18-depsep schedule, 64x56x56 input, fwd + bwd (given output gradient) + SGD-momentum, " \
+            "BASELINE config 5"
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    per = elapsed / args.steps
+    out = {"metric": metric, "value": round((1.0 if args.config == 2 else args.batch) / per, 2), "unit": unit,
+           "n_gpus": 1, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * per, 3),
+           "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": dtype,
+           "data": "synthetic (N(0,1) inputs and output gradients, seed 0; random-init weights)",
+           "config": {"workload": workload, "global_batch": args.batch, "parallelism": "dp1"}}
+    if flops:
+        out["achieved_tflops"] = round(flops / per / 1e12, 2)
+        out["mfma_frac"] = round(flops / per / 1e12 / perfmodel.PEAK_F32_TFLOPS, 4)
+    print(json.dumps(out), flush=True)
+
+
 def main():
     args = parse()
+    if args.config != 3:
+        if args.gpus != 1:
+            raise SystemExit("--config {} is a one-GPU configuration".format(args.config))
+        if args.config == 5 and args.batch == 256:
+            args.batch = 512  # the configuration's batch (SURVEY.md 8d)
+        return other_config(args)
     import numpy as np
     import torch
     import torch.distributed as dist
