@@ -48,9 +48,11 @@ __device__ __forceinline__ float bload1(__amdgpu_buffer_rsrc_t r, uint32_t off) 
 // (ih, iw) = (oh*sa + dr*r + off, ow*sa + dr*s + off), zero outside [0,H)x[0,W).
 // E: element type of the tensor (float, or bf16_t for BASELINE config 5's bf16 storage); the
 // loaders widen to fp32 as they load.
-template <class E>
+// K1: a 1x1 filter (pointwise): k is the channel, no tap arithmetic per K-tile.
+template <class E, bool K1 = false>
 struct ImgDescE {
   static constexpr bool kBnIn = false;
+  static constexpr bool k1x1 = K1;
   using Elem = E;
   const E* x;
   uint32_t bytes;
@@ -59,14 +61,21 @@ struct ImgDescE {
   int R, S;
   int sa, dr, off;
   int M;  // N * OH * OW
+  // division-free index arithmetic in the per-K-tile loader paths: q = umulhi(n, m) for
+  // the divisors C, S, OW, OH (set_magics; 0 = divide).  Exact while n * d < 2^32.
+  uint32_t mC, mS, mOW, mOH;
 };
 using ImgDesc = ImgDescE<float>;
+
+__device__ __forceinline__ int fdiv(int n, int d, uint32_t m) {
+  return m ? (int)__umulhi((uint32_t)n, m) : n / d;
+}
 
 // The same view of bn(x) (+ReLU): the loaders apply the BatchNorm of the layer that
 // produced x to every in-image element (padding stays exactly 0, as in the reference,
 // which pads the BN output).
-template <class E>
-struct ImgBnDescE : ImgDescE<E> {
+template <class E, bool K1 = false>
+struct ImgBnDescE : ImgDescE<E, K1> {
   static constexpr bool kBnIn = true;
   BnIn bn;
 };
@@ -158,12 +167,16 @@ struct LdImgKC : KCLayout<ROWS, BK> {
     const __amdgpu_buffer_rsrc_t rs = make_rsrc_v(d.x, d.bytes);
     const int k = k0 + 4 * kq;
     const bool kv = k < Ktot;
-    const int tap = k / d.C;
-    const int c = k - tap * d.C;
-    const int r = tap / d.S;
-    const int s = tap - r * d.S;
-    const int dri = d.dr * r, dsi = d.dr * s;
-    const int doff = dri * d.W + dsi;
+    int c = k, dri = 0, dsi = 0, doff = 0;
+    if constexpr (!D::k1x1) {
+      const int tap = fdiv(k, d.C, d.mC);
+      c = k - tap * d.C;
+      const int r = fdiv(tap, d.S, d.mS);
+      const int s = tap - r * d.S;
+      dri = d.dr * r;
+      dsi = d.dr * s;
+      doff = dri * d.W + dsi;
+    }
     uint32_t om = 0;
 #pragma unroll
     for (int j = 0; j < NR; ++j) {
@@ -344,10 +357,10 @@ struct LdImgIC : ICLayout<ROWS, BK> {
 #pragma unroll
     for (int jj = 0; jj < NK; ++jj) {
       const int m = k0 + kb + jj * KSTEP;
-      const int ow = m % d.OW;
-      const int t = m / d.OW;
-      const int oh = t % d.OH;
-      const int n = t / d.OH;
+      const int t = fdiv(m, d.OW, d.mOW);
+      const int ow = m - t * d.OW;
+      const int n = fdiv(t, d.OH, d.mOH);
+      const int oh = t - n * d.OH;
       const int ih = oh * d.sa + dri + d.off;
       const int iw = ow * d.sa + dsi + d.off;
       const bool ok = colv && m < d.M && (unsigned)ih < (unsigned)d.H && (unsigned)iw < (unsigned)d.W;
@@ -776,7 +789,9 @@ static inline EpWiden ep_widen(float* out, int ldo, int OH, int OW, int st, cons
   X(12, 64, 128, 16, 2, 2) \
   X(13, 64, 128, 32, 2, 2) \
   X(14, 128, 64, 16, 2, 2) \
-  X(15, 128, 64, 32, 2, 2)
+  X(15, 128, 64, 32, 2, 2) \
+  X(16, 128, 128, 32, 2, 4) \
+  X(17, 128, 128, 16, 2, 4)
 #define DK_SPLITK_CONFIGS(X) \
   X(0, 64, 64, 16, 2, 2)     \
   X(1, 64, 64, 32, 2, 2)     \
@@ -959,9 +974,29 @@ static inline bool vec_ok(const MatDesc& d, int kext, int iext) {
   return d.ld % 4 == 0 && kext % 4 == 0 && iext % 4 == 0 && aligned16(d.p);
 }
 
+// Magic multiplier for q = umulhi(n, m) == n / d (exact for n * d < 2^32); 0 = not usable.
+static inline uint32_t magic(long long d, long long nmax) {
+  if (d <= 1 || nmax * d >= (1ll << 32)) return 0;
+  return (uint32_t)((1ull << 32) / (unsigned long long)d + 1);
+}
+template <class Dsc>
+static inline Dsc set_magics(Dsc d) {
+  const long long ktot = (long long)d.R * d.S * d.C;
+  d.mC = magic(d.C, ktot);
+  d.mS = magic(d.S, ktot);
+  d.mOW = magic(d.OW, d.M);
+  d.mOH = magic(d.OH, d.M);
+  return d;
+}
 static inline ImgDesc img(const float* x, int N, int H, int W, int C, int OH, int OW, int R, int S, int sa, int dr,
                           int off, int M) {
-  return ImgDesc{x, (uint32_t)((size_t)N * H * W * C * sizeof(float)), H, W, C, OH, OW, R, S, sa, dr, off, M};
+  return set_magics(
+      ImgDesc{x, (uint32_t)((size_t)N * H * W * C * sizeof(float)), H, W, C, OH, OW, R, S, sa, dr, off, M});
+}
+// A pointwise (1x1, stride sa) view: k = channel.
+static inline ImgDescE<float, true> img1(const float* x, int N, int H, int W, int C, int OH, int OW, int sa, int M) {
+  return set_magics(ImgDescE<float, true>{x, (uint32_t)((size_t)N * H * W * C * sizeof(float)), H, W, C, OH, OW, 1,
+                                          1, sa, 1, 0, M});
 }
 
 }  // namespace dk
@@ -996,10 +1031,11 @@ DK_API int dk_conv_weight_crsk_f32(const float* w_kcrs, int K, int C, int R, int
 }
 
 // y[n,oh,ow,k] = sum_{r,s,c} x[n, oh*stride + r - pad, ow*stride + s - pad, c] * w[k][r][s][c] (+ bias[k])
-static inline ImgBnDesc with_bn(const ImgDesc& d, const float* mean, const float* invstd, const float* gamma,
-                                const float* beta, int relu) {
-  ImgBnDesc o;
-  static_cast<ImgDesc&>(o) = d;
+template <class E, bool K1>
+static inline ImgBnDescE<E, K1> with_bn(const ImgDescE<E, K1>& d, const float* mean, const float* invstd,
+                                        const float* gamma, const float* beta, int relu) {
+  ImgBnDescE<E, K1> o;
+  static_cast<ImgDescE<E, K1>&>(o) = d;
   o.bn = BnIn{mean, invstd, gamma, beta, relu};
   return o;
 }
@@ -1030,7 +1066,8 @@ static int stats_rows(int M, int N, int Ktot) { return cdiv(M, kRowCfg[row_confi
 
 // Forward with an optional input BatchNorm (bn_mean != NULL, see *_bnx_*) and optional output
 // statistics (stats != NULL: stats_rows x 2 x K doubles).
-static int conv_fwd_ex(const ImgDesc& base, const float* w, int K, int Ktot, const float* bias, float* y,
+template <class D0>
+static int conv_fwd_ex(const D0& base, const float* w, int K, int Ktot, const float* bias, float* y,
                        const float* bn_mean, const float* bn_invstd, const float* bn_gamma, const float* bn_beta,
                        int bn_relu, double* stats, void* stream) {
   if (bn_mean) {
@@ -1173,7 +1210,7 @@ DK_API int dk_pwconv_fwd_f32(const float* x, int N, int H, int W, int C, const f
     MatDesc a = mat(x, N * H * W, C, N * H * W);
     return igemm_rows<LdMatKC1, MatDesc, LdMatKC1, MatDesc, EpStore>(a, b, ep, N * H * W, K, C, as_stream(stream));
   }
-  return conv_fwd(img(x, N, H, W, C, OH, OW, 1, 1, stride, 1, 0, N * OH * OW), w_kc, K, C, bias, y, stream);
+  return conv_fwd(img1(x, N, H, W, C, OH, OW, stride, N * OH * OW), w_kc, K, C, bias, y, stream);
 }
 
 // The same with x = the raw output of the previous layer and y = pw(bn(x)) (+ReLU inside).
@@ -1183,7 +1220,7 @@ DK_API int dk_pwconv_fwd_bnx_f32(const float* x, int N, int H, int W, int C, con
                                  void* stream) {
   if (C % 4 || !aligned16(x) || !aligned16(w_kc) || !fits((size_t)N * H * W * C * 4)) return DK_ERR_ARGS;
   if (!bn_ok(bn_mean, bn_invstd, bn_gamma, bn_beta)) return DK_ERR_ARGS;
-  return conv_fwd(with_bn(img(x, N, H, W, C, OH, OW, 1, 1, stride, 1, 0, N * OH * OW), bn_mean, bn_invstd, bn_gamma,
+  return conv_fwd(with_bn(img1(x, N, H, W, C, OH, OW, stride, N * OH * OW), bn_mean, bn_invstd, bn_gamma,
                           bn_beta, bn_relu),
                   w_kc, K, C, bias, y, stream);
 }
@@ -1195,7 +1232,7 @@ DK_API int dk_pwconv_fwd_ex_f32(const float* x, int N, int H, int W, int C, cons
                                 const float* bn_invstd, const float* bn_gamma, const float* bn_beta, int bn_relu,
                                 double* stats, void* stream) {
   if (C % 4 || !aligned16(x) || !aligned16(w_kc) || !fits((size_t)N * H * W * C * 4)) return DK_ERR_ARGS;
-  return conv_fwd_ex(img(x, N, H, W, C, OH, OW, 1, 1, stride, 1, 0, N * OH * OW), w_kc, K, C, bias, y, bn_mean,
+  return conv_fwd_ex(img1(x, N, H, W, C, OH, OW, stride, N * OH * OW), w_kc, K, C, bias, y, bn_mean,
                      bn_invstd, bn_gamma, bn_beta, bn_relu, stats, stream);
 }
 
@@ -1346,8 +1383,12 @@ static inline MatDescE<bf16_t> mat_h(const bf16_t* p, int rows, int ld, int ext)
 }
 static inline ImgDescE<bf16_t> img_h(const bf16_t* x, int N, int H, int W, int C, int OH, int OW, int R, int S,
                                      int sa, int dr, int off, int M) {
-  return ImgDescE<bf16_t>{x,  (uint32_t)((size_t)N * H * W * C * sizeof(bf16_t)), H, W, C, OH, OW, R, S, sa, dr, off,
-                          M};
+  return set_magics(ImgDescE<bf16_t>{x, (uint32_t)((size_t)N * H * W * C * sizeof(bf16_t)), H, W, C, OH, OW, R, S,
+                                     sa, dr, off, M});
+}
+static inline ImgDescE<bf16_t, true> img1_h(const bf16_t* x, int N, int H, int W, int C, int OH, int OW, int sa, int M) {
+  return set_magics(ImgDescE<bf16_t, true>{x, (uint32_t)((size_t)N * H * W * C * sizeof(bf16_t)), H, W, C, OH, OW,
+                                           1, 1, sa, 1, 0, M});
 }
 static inline bool al8(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 7) == 0; }
 }  // namespace dk
@@ -1358,7 +1399,7 @@ DK_API int dk_pwconv_fwd_ex_bf16(const bf16_t* x, int N, int H, int W, int C, co
                                  double* stats, void* stream) {
   if (C % 4 || K % 4 || !al8(x) || !al8(y) || !aligned16(w_kc) || (bias && !aligned16(bias))) return DK_ERR_ARGS;
   if (!fits((size_t)N * H * W * C * 4) || !fits((size_t)N * OH * OW * K * 4)) return DK_ERR_ARGS;
-  const ImgDescE<bf16_t> a = img_h(x, N, H, W, C, OH, OW, 1, 1, stride, 1, 0, N * OH * OW);
+  const ImgDescE<bf16_t, true> a = img1_h(x, N, H, W, C, OH, OW, stride, N * OH * OW);
   const MatDesc b = mat(w_kc, K, C, K);
   const hipStream_t st = as_stream(stream);
   const int M = a.M;
@@ -1374,8 +1415,8 @@ DK_API int dk_pwconv_fwd_ex_bf16(const bf16_t* x, int N, int H, int W, int C, co
   };
   if (bn_mean) {
     if (!bn_ok(bn_mean, bn_invstd, bn_gamma, bn_beta) || C > 2048) return DK_ERR_ARGS;
-    ImgBnDescE<bf16_t> ab;
-    static_cast<ImgDescE<bf16_t>&>(ab) = a;
+    ImgBnDescE<bf16_t, true> ab;
+    static_cast<ImgDescE<bf16_t, true>&>(ab) = a;
     ab.bn = BnIn{bn_mean, bn_invstd, bn_gamma, bn_beta, bn_relu};
     return run(ab);
   }
