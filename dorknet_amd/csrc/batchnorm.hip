@@ -541,8 +541,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const E* __restrict__
       const float xe = el(xv, e);
       float ge = el(gv, e);
       if (relu && !(bn_out(xe, mu[e], is[e], ga[e], be[e]) > 0.f)) ge = 0.f;
-      const float xh = (xe - mu[e]) * is[e];
-      set_el(o, e, f[e] * (ge - k1[e] - xh * k2[e]));
+      set_el(o, e, bn_bwd_elem(xe, ge, mu[e], is[e], f[e], k1[e], k2[e]));
     }
     if constexpr (NT && V == 4 && sizeof(E) == 4)
       __builtin_nontemporal_store(o, reinterpret_cast<f32x4*>(dx + off));

@@ -106,6 +106,16 @@ __device__ __forceinline__ float bn_relu_out(float x, float mean, float invstd, 
   return (relu && !(r > 0.f)) ? 0.f : r;
 }
 
+// The BN input gradient for one element, given the folded coefficients (stage 3 of
+// layers/batch_norm.py:125-174): dx = gamma*invstd * (g - k1 - x_hat*k2), g already masked
+// by a fused ReLU.  Written with an explicit fma so that dk_bn_bwd_apply_* and the dgrad
+// loaders that form it on load (*_dgrad_bnbwd_f32) round identically.
+__device__ __forceinline__ float bn_bwd_elem(float x, float g, float mean, float invstd, float f, float k1,
+                                             float k2) {
+  const float xh = (x - mean) * invstd;
+  return f * __builtin_fmaf(-xh, k2, g - k1);
+}
+
 // A BatchNorm (+ ReLU) applied to an operand as it is loaded: the producer's raw output x
 // plus per-channel statistics and affine parameters.  mean == nullptr: no transform.
 struct BnIn {

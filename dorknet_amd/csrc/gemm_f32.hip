@@ -52,6 +52,7 @@ __device__ __forceinline__ float bload1(__amdgpu_buffer_rsrc_t r, uint32_t off) 
 template <class E, bool K1 = false>
 struct ImgDescE {
   static constexpr bool kBnIn = false;
+  static constexpr bool kBnBwd = false;
   static constexpr bool k1x1 = K1;
   using Elem = E;
   const E* x;
@@ -85,6 +86,7 @@ using ImgBnDesc = ImgBnDescE<float>;
 template <class E>
 struct MatDescE {
   static constexpr bool kBnIn = false;
+  static constexpr bool kBnBwd = false;
   using Elem = E;
   const E* p;
   uint32_t bytes;
@@ -92,6 +94,28 @@ struct MatDescE {
   int ext;
 };
 using MatDesc = MatDescE<float>;
+
+// The backward of the BatchNorm that followed this layer, applied as its gradient is loaded
+// (stage 3 of batch_norm.py:125-174, = dk_bn_bwd_apply_f32, bit for bit): p holds
+// g, the gradient w.r.t. the BN (+ReLU) output; x is the BN's raw input (same layout); the
+// loader forms dy = gamma*invstd * (g' - k1 - x_hat*k2) (g' = g masked by the fused ReLU,
+// recomputed from x) and the blocks of the first column tile also store dy to dy_out (for
+// the weight gradient, which reads it afterwards).
+struct BnBwdIn {
+  const float* mean;
+  const float* invstd;
+  const float* gamma;
+  const float* beta;
+  const float* k12;  // [k1[C], k2[C]] (dk_bn_bwd_from_partials_f32)
+  int relu;
+  int C;
+};
+struct MatBwdDesc : MatDescE<float> {
+  static constexpr bool kBnBwd = true;
+  const float* x;
+  BnBwdIn bwd;
+  float* dy_out;
+};
 
 // ----------------------------------------------------------------------------
 // Loaders.  K-contiguous ("KC") loaders fill T[ROWS][BK+4]; row-contiguous ("IC")
@@ -220,6 +244,15 @@ struct LdMatKCT : KCLayout<ROWS, BK> {
   int kq, rb, row0;
   bool active;
   f32x4 v[NR];
+  // BN backward on load (MatBwdDesc): the BN's raw input, the parameter table in LDS
+  // ({mean, invstd, gamma, beta}, {k1, k2, gamma*invstd, 0} per channel), dy write-through
+  f32x4 xv[NR];
+  const f32x4* tab;
+  float* dyo;
+  bool writer;
+  int kcur;
+  uint32_t eoff[NR];
+  uint32_t okm;
 
   template <class D>
   __device__ __forceinline__ void init(const D&, int row0_, int tid) {
@@ -234,6 +267,8 @@ struct LdMatKCT : KCLayout<ROWS, BK> {
     const __amdgpu_buffer_rsrc_t rs = make_rsrc_v(d.p, d.bytes);
     const int k = k0 + 4 * kq;
     static_assert(VEC || sizeof(typename D::Elem) == 4, "scalar loads: fp32 storage only");
+    static_assert(VEC || !D::kBnBwd, "BN backward on load: 16-byte loads only");
+    uint32_t om = 0;
 #pragma unroll
     for (int j = 0; j < NR; ++j) {
       const int i = row0 + rb + j * RSTEP;
@@ -241,19 +276,55 @@ struct LdMatKCT : KCLayout<ROWS, BK> {
       const uint32_t base = (uint32_t)(i * d.ld + k) * 4u;
       if constexpr (VEC) {
         v[j] = bload4e<typename D::Elem>(rs, iv && k < Ktot, (uint32_t)(i * d.ld + k));
+        if constexpr (D::kBnBwd) {
+          const __amdgpu_buffer_rsrc_t rx = make_rsrc_v(d.x, d.bytes);
+          xv[j] = bload4e<float>(rx, iv && k < Ktot, (uint32_t)(i * d.ld + k));
+          eoff[j] = (uint32_t)(i * d.ld + k);
+          om |= (uint32_t)(iv && k < Ktot) << j;
+        }
       } else {
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[j][e] = bload1(rs, (iv && k + e < Ktot) ? base + 4u * e : kOOB);
       }
     }
+    if constexpr (D::kBnBwd) {
+      kcur = k;
+      okm = om;
+    }
   }
 
-  template <class>
-  __device__ __forceinline__ void store(float* T) const {
+  template <class D>
+  __device__ __forceinline__ void store(float* T) {
     if (!active) return;
+    if constexpr (D::kBnBwd) {
+      if (okm) {
+        // dy for channels kcur..kcur+3 (all four < Ktot when any row is valid: Ktot % 4 == 0)
+        f32x4 p[4], q[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          p[e] = tab[2 * (kcur + e)];
+          q[e] = tab[2 * (kcur + e) + 1];
+        }
+#pragma unroll
+        for (int j = 0; j < NR; ++j) {
+          if (!((okm >> j) & 1u)) continue;
+          f32x4 o;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float xe = xv[j][e];
+            float ge = v[j][e];
+            if (relu_flag && !(bn_out(xe, p[e][0], p[e][1], p[e][2], p[e][3]) > 0.f)) ge = 0.f;
+            o[e] = bn_bwd_elem(xe, ge, p[e][0], p[e][1], q[e][2], q[e][0], q[e][1]);
+          }
+          v[j] = o;
+          if (writer) st4(dyo + eoff[j], o);
+        }
+      }
+    }
 #pragma unroll
     for (int j = 0; j < NR; ++j) st4(T + (rb + j * RSTEP) * L::SK + 4 * kq, v[j]);
   }
+  int relu_flag = 0;
 };
 template <int ROWS, int BK, int NT>
 using LdMatKC = LdMatKCT<ROWS, BK, NT, true>;
@@ -638,6 +709,21 @@ __global__ __launch_bounds__(64 * WM * WN) void igemm_f32(DA da, DB db, EP ep, i
       la.tab = bn_tab;
       __syncthreads();
     }
+    if constexpr (DA::kBnBwd) {
+      // BN-backward-on-load table for the A operand (channel = k)
+      extern __shared__ f32x4 bwd_tab[];
+      const BnBwdIn& b = da.bwd;
+      for (int c = tid; c < b.C; c += 64 * WM * WN) {
+        const float ga = b.gamma[c], is = b.invstd[c];
+        bwd_tab[2 * c] = f32x4{b.mean[c], is, ga, b.beta[c]};
+        bwd_tab[2 * c + 1] = f32x4{b.k12[c], b.k12[b.C + c], ga * is, 0.f};
+      }
+      la.tab = bwd_tab;
+      la.dyo = da.dy_out;
+      la.writer = da.dy_out != nullptr && n0 == 0;
+      la.relu_flag = b.relu;
+      __syncthreads();
+    }
     la.template store<DA>(As);
     lb.template store<DB>(Bs);
     __syncthreads();
@@ -829,6 +915,11 @@ static int launch_igemm(const DA& da, const DB& db, const EP& ep, int M, int N, 
   size_t dyn = 0;
   if constexpr (DA::kBnIn && A::kTable) {
     dyn = (size_t)da.C * sizeof(f32x4);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&igemm_f32<BM, BN, BK, WM, WN, A, DA, B, DB, EP>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn);
+  }
+  if constexpr (DA::kBnBwd) {
+    dyn = (size_t)da.bwd.C * 2 * sizeof(f32x4);
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&igemm_f32<BM, BN, BK, WM, WN, A, DA, B, DB, EP>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn);
   }
@@ -1302,6 +1393,47 @@ DK_API int dk_pwconv_dgrad_ex_f32(const float* dy, int N, int OH, int OW, int K,
   ep.bn = bn;
   DK_ROWS(EpWidenBnBwd, ep);
 #undef DK_ROWS
+}
+
+// dgrad of a stride-1 pointwise layer whose output fed a BatchNorm (+ReLU), with that BN's
+// backward apply (dk_bn_bwd_apply_f32) done on load: g = the gradient w.r.t. the BN(+ReLU)
+// output, bn_x = the BN's raw input (= this layer's output), k12 from
+// dk_bn_bwd_from_partials_f32.  dy_out (nullable) receives dy = the gradient w.r.t. bn_x,
+// bit-identical to dk_bn_bwd_apply_f32's, for this layer's weight gradient.  The epilogue
+// options (residual, the partials of the BN before this layer) are those of
+// dk_pwconv_dgrad_ex_f32 at stride 1.
+DK_API int dk_pwconv_dgrad_bnbwd_f32(const float* g, const float* bn_x, int N, int OH, int OW, int K,
+                                     const float* out_mean, const float* out_invstd, const float* out_gamma,
+                                     const float* out_beta, int out_relu, const float* k12, float* dy_out,
+                                     const float* w_kc, int C, float* dx, const float* residual, const float* x,
+                                     const float* bn_mean, const float* bn_invstd, const float* bn_gamma,
+                                     const float* bn_beta, int bn_relu, double* part, void* stream) {
+  const int M = N * OH * OW;
+  if (!fits((size_t)M * K * 4) || (part != nullptr) != (x != nullptr)) return DK_ERR_ARGS;
+  if (part && (!bn_mean || !bn_invstd || !bn_gamma || !bn_beta)) return DK_ERR_ARGS;
+  if (!out_mean || !out_invstd || !out_gamma || !out_beta || !k12 || !bn_x) return DK_ERR_ARGS;
+  MatBwdDesc a;
+  static_cast<MatDesc&>(a) = mat(g, M, K, M);
+  a.x = bn_x;
+  a.bwd = BnBwdIn{out_mean, out_invstd, out_gamma, out_beta, k12, out_relu, K};
+  a.dy_out = dy_out;
+  MatDesc b = mat(w_kc, K, C, C);
+  const hipStream_t st = as_stream(stream);
+  // 16-byte loads of g, bn_x and dy_out; the LDS table holds 2 float4 per channel
+  if (!vec_ok(b, 4, C) || K % 4 || !aligned16(g) || !aligned16(bn_x) || (dy_out && !aligned16(dy_out)) ||
+      (size_t)K * 32 > 64 * 1024)
+    return DK_ERR_ARGS;
+  if (!part) {
+    EpStore ep = ep_store(dx, C, nullptr, residual);
+    return igemm_rows<LdMatKC, MatBwdDesc, LdMatIC, MatDesc, EpStore>(a, b, ep, M, C, K, st);
+  }
+  EpStoreBnBwd ep;
+  static_cast<EpStore&>(ep) = ep_store(dx, C, nullptr, residual);
+  ep.v4 = ep.v4 && aligned16(x) && bn_ok(bn_mean, bn_invstd, bn_gamma, bn_beta);
+  ep.part = part;
+  ep.xbn = x;
+  ep.bn = BnIn{bn_mean, bn_invstd, bn_gamma, bn_beta, bn_relu};
+  return igemm_rows<LdMatKC, MatBwdDesc, LdMatIC, MatDesc, EpStoreBnBwd>(a, b, ep, M, C, K, st);
 }
 
 DK_API size_t dk_pwconv_wgrad_workspace_bytes(int N, int OH, int OW, int K, int C) {

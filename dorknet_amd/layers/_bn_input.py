@@ -70,8 +70,61 @@ class BNOut:
         return self._y
 
 
+class BNGrad:
+    """The gradient w.r.t. a BatchNormLayer's input with its last stage (the per-element
+    apply, dk_bn_bwd_apply_f32) left to the producer of that input.
+
+    BatchNormLayer._backward(defer=True) reduces its partial sums into k12 and returns this
+    instead of writing dx; a producer with ``accepts_bn_grad`` forms dx = f(g, x) as its dgrad
+    loads it (the *_dgrad_bnbwd_f32 entries) and stores it once for its weight gradient.
+    ``materialize()`` is the unfused apply (bit-identical)."""
+    __slots__ = ("g", "x", "mean", "invstd", "gamma", "beta", "relu", "k12", "_dx")
+
+    def __init__(self, g, x, mean, invstd, gamma, beta, relu, k12):
+        self.g = g            # gradient w.r.t. the BN (+ReLU) output, NHWC like x
+        self.x = x            # the BN's raw input
+        self.mean = mean
+        self.invstd = invstd
+        self.gamma = gamma
+        self.beta = beta
+        self.relu = bool(relu)
+        self.k12 = k12        # [k1[C], k2[C]] from dk_bn_bwd_from_partials_f32 / _finalize_f32
+        self._dx = None
+
+    @property
+    def shape(self):
+        return self.x.shape
+
+    def dim(self):
+        return self.x.dim()
+
+    @property
+    def dtype(self):
+        return self.x.dtype
+
+    def bnbwd_args(self):
+        """(mean, invstd, gamma, beta, relu, k12) for a *_dgrad_bnbwd_f32 call."""
+        return (self.mean.data_ptr(), self.invstd.data_ptr(), self.gamma.data_ptr(), self.beta.data_ptr(),
+                int(self.relu), self.k12.data_ptr())
+
+    def materialize(self):
+        if self._dx is None:
+            x = self.x
+            dx = empty_nhwc(*x.shape, dtype=x.dtype) if x.dim() == 4 else torch.empty_like(x)
+            apply = lib.dk_bn_bwd_apply_bf16 if x.dtype == torch.bfloat16 else lib.dk_bn_bwd_apply_f32
+            apply(x.data_ptr(), self.g.data_ptr(), x.numel(), x.shape[1], *self.bnbwd_args()[:5],
+                  self.k12.data_ptr(), dx.data_ptr(), stream_handle())
+            self._dx = dx
+        return self._dx
+
+
+def accepts_bn_grad(layer, bn_layer) -> bool:
+    f = getattr(layer, "accepts_bn_grad", None)
+    return bool(f(bn_layer)) if f is not None else False
+
+
 def materialize(X):
-    return X.materialize() if isinstance(X, BNOut) else X
+    return X.materialize() if isinstance(X, (BNOut, BNGrad)) else X
 
 
 def accepts_bn_input(layer) -> bool:

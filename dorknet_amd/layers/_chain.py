@@ -112,12 +112,20 @@ def chain_backward(steps, dy, residual=None):
     """Backward through `steps` in reverse.  `residual`: a gradient to add to the result (the
     residual join's other branch); the first layer adds it in its dgrad epilogue when it
     can (``accepts_residual``), otherwise it is added separately."""
-    from ._bn_input import add_residual
+    from ._bn_input import accepts_bn_grad, add_residual
+    from .batch_norm import BatchNormLayer
     last = len(steps) - 1
+    fuse = fusion_enabled()
     for i in range(last, -1, -1):
         step = steps[i]
+        # a BatchNorm whose producer can apply its backward while loading the gradient
+        # (layers/_bn_input.py BNGrad) hands over a deferred gradient instead of writing it
+        defer = (fuse and type(step[0]) is BatchNormLayer and i > 0 and len(steps[i - 1]) == 1
+                 and accepts_bn_grad(steps[i - 1][0], step[0]))
         if len(step) == 2:
-            dy = step[0].backward_bn_relu(dy, step[1])
+            dy = step[0].backward_bn_relu(dy, step[1], defer=defer)
+        elif defer:
+            dy = step[0].backward(dy, defer=True)
         elif i == 0 and residual is not None and getattr(step[0], "accepts_residual", False):
             dy = step[0].backward(dy, residual=residual)
             residual = None

@@ -22,6 +22,7 @@ import torch
 
 from .._hip import lib, stream_handle, tickets, workspace
 from .._tensor import BF16, act_dtype, as_device, empty_nhwc, rows, to_nhwc
+from ._bn_input import BNGrad
 from ._common import grad_buffer
 from .layer import Layer
 
@@ -191,7 +192,10 @@ class BatchNormLayer(Layer):
 
     # -- backward ------------------------------------------------------------------------
 
-    def _backward(self, upstream_dx, relu):
+    def _backward(self, upstream_dx, relu, defer=False):
+        """defer: when the coefficients come from a separate reduction (the partial sums of the
+        consumer's dgrad epilogue, or the synchronised path), return a BNGrad and leave the
+        apply to the producer of this layer's input (chain_backward)."""
         self._require_on_gpu()
         st = stream_handle()
         x = self.X
@@ -225,6 +229,8 @@ class BatchNormLayer(Layer):
                 dist.all_reduce(glob, group=self.sync_group)
                 lib.dk_bn_bwd_finalize_f32(local.data_ptr(), 1, glob.data_ptr(), 1, C, float(P) * self._world(),
                                            dgamma.data_ptr(), dbeta.data_ptr(), k12.data_ptr(), st)
+            if defer and not bf:
+                return BNGrad(dy, x, self._mean, self._invstd, gamma, beta, relu, k12)
             (lib.dk_bn_bwd_apply_bf16 if bf else lib.dk_bn_bwd_apply_f32)(
                 x.data_ptr(), dy.data_ptr(), x.numel(), C, self._mean.data_ptr(), self._invstd.data_ptr(),
                 gamma.data_ptr(), beta.data_ptr(), int(relu), k12.data_ptr(), dx.data_ptr(), st)
@@ -250,17 +256,19 @@ class BatchNormLayer(Layer):
             k12 = torch.empty(2 * C, dtype=torch.float32, device=x.device)
             lib.dk_bn_bwd_finalize_f32(local.data_ptr(), 1, glob.data_ptr(), 1, C, float(P) * self._world(),
                                        dgamma.data_ptr(), dbeta.data_ptr(), k12.data_ptr(), st)
+            if defer and not bf:
+                return BNGrad(dy, x, self._mean, self._invstd, gamma, beta, relu, k12)
             (lib.dk_bn_bwd_apply_bf16 if bf else lib.dk_bn_bwd_apply_f32)(
                 x.data_ptr(), dy.data_ptr(), x.numel(), C, self._mean.data_ptr(), self._invstd.data_ptr(),
                 gamma.data_ptr(), beta.data_ptr(), int(relu), k12.data_ptr(), dx.data_ptr(), st)
         return dx
 
-    def backward(self, upstream_dx):
-        return self._backward(upstream_dx, relu=False)
+    def backward(self, upstream_dx, defer=False):
+        return self._backward(upstream_dx, relu=False, defer=defer)
 
-    def backward_bn_relu(self, upstream_dx, relu_layer):
+    def backward_bn_relu(self, upstream_dx, relu_layer, defer=False):
         """Backward of the fused BN+ReLU pair; upstream_dx is the gradient w.r.t. the ReLU output."""
-        return self._backward(upstream_dx, relu=True)
+        return self._backward(upstream_dx, relu=True, defer=defer)
 
     def save_to_h5(self, open_f, save_grads=True):
         from ..network.checkpoint import save_layer

@@ -16,7 +16,7 @@ import torch
 
 from .._hip import lib, stream_handle, weight_grad_stream, workspace
 from .._tensor import BF16, empty_nhwc, ptr, to_nhwc
-from ._bn_input import BNOut, add_residual, residual_operand
+from ._bn_input import BNGrad, BNOut, add_residual, residual_operand
 from ._common import add_regulariser_grad, grad_buffer, init_weights, l2_strength
 from .layer import Layer
 
@@ -95,20 +95,70 @@ class PointwiseConvLayer(Layer):
 
     accepts_residual = True  # backward(dy, residual=R) returns dx + R (the residual join, fused)
 
+    def accepts_bn_grad(self, bn_layer):
+        """backward(BNGrad): the following BatchNorm's apply runs in this layer's dgrad loader
+        (dk_pwconv_dgrad_bnbwd_f32) -- fp32, stride 1, 4-D, channel counts the 16-byte loads
+        and the LDS coefficient table take."""
+        x = getattr(self, "X", None)
+        bx = getattr(bn_layer, "X", None)
+        return (x is not None and bx is not None and x.dtype == torch.float32 and self.stride == 1
+                and x.dim() == 4 and self._takes_bn_grad(bx))
+
+    def _takes_bn_grad(self, bx):
+        return (bx.dim() == 4 and bx.dtype == torch.float32 and self.stride == 1 and self.X.dtype == torch.float32
+                and tuple(bx.shape) == (self.X.shape[0], self.num_filters, *self.out_hw)
+                and self.num_filters % 4 == 0 and self.num_filters <= 2048)
+
     def backward(self, upstream_dx, residual=None):
         self._require_on_gpu()
         st = stream_handle()
-        dy = to_nhwc(upstream_dx)
         x = self.X
         N, C, H, W = x.shape
         K, s = self.num_filters, self.stride
         OH, OW = self.out_hw
         P = N * OH * OW
         w = self.learned_params["weights"]
+        if isinstance(upstream_dx, BNGrad):
+            if self._takes_bn_grad(upstream_dx.x):
+                # dgrad first: it forms (and stores) dy from the BatchNorm's gradient as it loads it
+                dy = empty_nhwc(N, K, OH, OW)
+                dx = self._dgrad_bnbwd(upstream_dx, dy, residual, st)
+                self._wgrad(dy, x, N, H, W, C, K, s, OH, OW, P, w, False)
+                return dx
+            upstream_dx = upstream_dx.materialize()
+        dy = to_nhwc(upstream_dx)
         bf = x.dtype == BF16
         if bf and (dy.dtype != BF16 or self.with_bias or s != 1):
             raise NotImplementedError("{}: bf16 storage needs a bf16 gradient, no bias, stride 1".format(
                 self.layer_name))
+        self._wgrad(dy, x, N, H, W, C, K, s, OH, OW, P, w, bf)
+        return self._dgrad(dy, residual, st)
+
+    def _dgrad_bnbwd(self, bg, dy_out, residual, st):
+        x = self.X
+        N, C, H, W = x.shape
+        K = self.num_filters
+        OH, OW = self.out_hw
+        w = self.learned_params["weights"]
+        dx = empty_nhwc(N, C, OH, OW)
+        bn = self._bn_in
+        res = residual_operand(residual, dx)
+        g = to_nhwc(bg.g)
+        part = None
+        if bn is not None:
+            rows = lib.dk_pwconv_dgrad_stats_rows(N, OH, OW, K, C)
+            part = torch.empty((rows, 2, C), dtype=torch.float64, device=dx.device)
+        lib.dk_pwconv_dgrad_bnbwd_f32(g.data_ptr(), bg.x.data_ptr(), N, OH, OW, K, *bg.bnbwd_args(),
+                                      dy_out.data_ptr(), w.data_ptr(), C, dx.data_ptr(), ptr(res),
+                                      *((bn.x.data_ptr(), *bn.bn_args(), part.data_ptr()) if bn is not None
+                                        else (0, 0, 0, 0, 0, 0, 0)), st)
+        if bn is not None:
+            bn.hand_backward_partials(dx, part)
+        if residual is not None and res is None:
+            dx = add_residual(dx, residual)
+        return dx
+
+    def _wgrad(self, dy, x, N, H, W, C, K, s, OH, OW, P, w, bf):
         # the weight gradient runs on the side stream (_hip.weight_grad_stream)
         with weight_grad_stream(dy, x, *self._bn_tensors()):
             sst = stream_handle()
@@ -134,6 +184,14 @@ class PointwiseConvLayer(Layer):
                                         sst)
             if l2s is None:
                 add_regulariser_grad(gw, w, self.weight_regulariser)
+
+    def _dgrad(self, dy, residual, st):
+        x = self.X
+        N, C, H, W = x.shape
+        K, s = self.num_filters, self.stride
+        OH, OW = self.out_hw
+        w = self.learned_params["weights"]
+        bf = x.dtype == BF16
         dx = empty_nhwc(N, C, OH * s, OW * s, x.dtype)  # widened shape, pointwise_convolution.py:68-72
         bn = self._bn_in
         res = residual_operand(residual, dx)

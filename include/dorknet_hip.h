@@ -118,6 +118,17 @@ int dk_pwconv_dgrad_stats_rows(int N, int OH, int OW, int K, int C);
 int dk_pwconv_dgrad_ex_f32(const float* dy, int N, int OH, int OW, int K, const float* w_kc, int C, int stride, float* dx, const float* residual, const float* bn_x, const float* bn_mean, const float* bn_invstd, const float* bn_gamma, const float* bn_beta, int bn_relu, double* part, void* stream);
 int dk_dwconv_dgrad_stats_rows(int N, int H, int W, int C, int stride);
 int dk_dwconv_dgrad_ex_f32(const float* dy, int N, int OH, int OW, int C, const float* w_crs, int R, int S, int stride, int pad, float* dx, int H, int W, void* ws, size_t ws_bytes, const float* residual, const float* bn_x, const float* bn_mean, const float* bn_invstd, const float* bn_gamma, const float* bn_beta, int bn_relu, double* part, void* stream);
+/* The other side of the same BatchNorm pair: *_dgrad_bnbwd_f32 = a stride-1 layer's input
+ * gradient when its OUTPUT fed a BatchNorm (+ReLU).  g is the gradient w.r.t. that BN's
+ * output, bn_x its raw input (= this layer's output), out_* its parameters and k12 its
+ * folded backward coefficients (dk_bn_bwd_from_partials_f32).  The layer's gradient
+ * dy = dk_bn_bwd_apply_f32(bn_x, g) is formed as the operand is loaded (stage 3 of
+ * batch_norm.py:125-174) and, when dy_out != NULL, also stored there (bit-identical to the
+ * separate pass) for the layer's weight gradient.  The remaining arguments are those of the
+ * matching *_dgrad_ex_f32 (x / bn_* / part: the BN before this layer; residual addend).
+ * (No depthwise form: that dgrad is HBM-bound, and forming dy on load costs it more than
+ * the separate apply pass saves -- measured, DESIGN.md.) */
+int dk_pwconv_dgrad_bnbwd_f32(const float* g, const float* bn_x, int N, int OH, int OW, int K, const float* out_mean, const float* out_invstd, const float* out_gamma, const float* out_beta, int out_relu, const float* k12, float* dy_out, const float* w_kc, int C, float* dx, const float* residual, const float* x, const float* bn_mean, const float* bn_invstd, const float* bn_gamma, const float* bn_beta, int bn_relu, double* part, void* stream);
 
 /* ---------------------------------------------------------------------------------------
  * bf16 storage twins (BASELINE config 5: the depthwise-separable stack with bf16 activations).

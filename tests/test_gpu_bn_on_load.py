@@ -369,3 +369,88 @@ def test_one_launch_fold(rows, C):
     for r in res[1:]:
         for u, v in zip(res[0], r):
             same(u, v)
+
+
+def _k12(C, rng):
+    return torch.as_tensor(rng.randn(2 * C).astype(np.float32) * 0.1, device="cuda")
+
+
+def bwd_apply(xo, g, p, relu, k12):
+    out = torch.empty_like(g)
+    lib.dk_bn_bwd_apply_f32(xo.data_ptr(), g.data_ptr(), g.numel(), g.shape[1], *args(p, relu)[:4], int(relu),
+                            k12.data_ptr(), out.data_ptr(), stream_handle())
+    return out
+
+
+@pytest.mark.parametrize("relu,bn_in,resid,K", [(1, True, False, 40), (0, False, False, 64), (1, False, True, 200),
+                                                 (1, True, True, 16)])
+def test_pointwise_dgrad_bnbwd_bitwise(relu, bn_in, resid, K):
+    """dk_pwconv_dgrad_bnbwd_f32 == dk_bn_bwd_apply_f32 -> dk_pwconv_dgrad_ex_f32, bitwise, for
+    dx, the written-through dy, and the input BN's partial sums."""
+    rng = np.random.RandomState(relu + 2 * bn_in + 4 * resid + K)
+    N, C, H, W = 3, 24, 13, 11
+    xo = nhwc(rng.randn(N, K, H, W))        # this layer's output = the following BN's input
+    g = nhwc(rng.randn(N, K, H, W))         # gradient w.r.t. that BN's (+ReLU) output
+    po = bn_params(K, rng)
+    k12 = _k12(K, rng)
+    w = torch.as_tensor(rng.randn(K, C).astype(np.float32), device="cuda")
+    xin = nhwc(rng.randn(N, C, H, W))       # this layer's input BN's raw input
+    pi = bn_params(C, rng)
+    res = nhwc(rng.randn(N, C, H, W)) if resid else None
+    st = stream_handle()
+    rows = lib.dk_pwconv_dgrad_stats_rows(N, H, W, K, C)
+    dy0 = bwd_apply(xo, g, po, relu, k12)
+    dx0 = torch.empty_like(xin)
+    part0 = torch.zeros((rows, 2, C), dtype=torch.float64, device="cuda")
+    bn_args = (xin.data_ptr(), *args(pi, 1), part0.data_ptr()) if bn_in else (0, 0, 0, 0, 0, 0, 0)
+    assert lib.dk_pwconv_dgrad_ex_f32(dy0.data_ptr(), N, H, W, K, w.data_ptr(), C, 1, dx0.data_ptr(),
+                                      res.data_ptr() if resid else 0, *bn_args, st) == 0
+    dy1 = torch.full_like(g, float("nan"))
+    dx1 = torch.empty_like(xin)
+    part1 = torch.zeros_like(part0)
+    bn_args = (xin.data_ptr(), *args(pi, 1), part1.data_ptr()) if bn_in else (0, 0, 0, 0, 0, 0, 0)
+    assert lib.dk_pwconv_dgrad_bnbwd_f32(g.data_ptr(), xo.data_ptr(), N, H, W, K, *args(po, relu), k12.data_ptr(),
+                                         dy1.data_ptr(), w.data_ptr(), C, dx1.data_ptr(),
+                                         res.data_ptr() if resid else 0, *bn_args, st) == 0
+    same(dy0, dy1)
+    same(dx0, dx1)
+    if bn_in:
+        same(part0, part1)
+
+
+def test_network_bn_grad_deferral_bitwise(monkeypatch):
+    """pw -> BN -> ReLU -> dw -> BN -> pw -> BN -> ReLU: the fused backward (the apply of each BN
+    that follows a pw layer runs in that layer's dgrad loader) equals the layer-by-layer backward
+    bit for bit."""
+    from dorknet_amd.layers.activations import ReLu
+    from dorknet_amd.layers.batch_norm import BatchNormLayer
+    from dorknet_amd.layers.depthwise_convolution import DepthwiseConvLayer
+    from dorknet_amd.layers.pointwise_convolution import PointwiseConvLayer
+    from dorknet_amd.layers._chain import chain_backward, chain_forward
+    rng = np.random.RandomState(5)
+
+    def build():
+        r = np.random.RandomState(11)
+        ls = [PointwiseConvLayer("p1", 1, (32, 16), with_bias=False), BatchNormLayer("b1", incoming_chans=32), ReLu("r1"),
+              DepthwiseConvLayer("d1", filter_block_shape=(32, 3, 3), stride=1, padding=1, with_bias=False),
+              BatchNormLayer("bd", incoming_chans=32),
+              PointwiseConvLayer("p2", 1, (48, 32), with_bias=False), BatchNormLayer("b2", incoming_chans=48), ReLu("r2")]
+        for l in ls:
+            for k in list(l.learned_params or {}):
+                l.learned_params[k] = r.randn(*l.learned_params[k].shape).astype(np.float32)
+            l.to_gpu()
+        return ls
+
+    x = rng.randn(4, 16, 9, 10).astype(np.float32)
+    dy = rng.randn(4, 48, 9, 10).astype(np.float32)
+    outs = []
+    for fuse in ("1", "0"):
+        monkeypatch.setenv("DORKNET_FUSE", fuse)
+        ls = build()
+        _, steps = chain_forward(ls, nhwc(x))
+        dx = chain_backward(steps, nhwc(dy))
+        torch.cuda.synchronize()
+        outs.append([dx.float().cpu()] + [torch.as_tensor(l.grads[k]).float().cpu() if not torch.is_tensor(l.grads[k])
+                                          else l.grads[k].float().cpu() for l in ls for k in sorted(l.grads or {})])
+    for a, b in zip(*outs):
+        assert torch.equal(a, b), float((a - b).abs().max())
