@@ -368,7 +368,9 @@ def main():
                "config": {"workload": "ResNet-18-depsep 225x225 training step (fwd+loss+bwd+SGD-momentum), "
                                       "BASELINE config {}".format(3 if world == 1 else 4),
                           "global_batch": world * args.batch, "per_gpu_batch": args.batch,
-                          "parallelism": "dp{}".format(world), "batch_norm": args.bn if world > 1 else "local"},
+                          "parallelism": "dp{}".format(world), "batch_norm": args.bn if world > 1 else "local",
+                          "input_grad": "not computed (network.backward returns nothing, as in the reference, "
+                                        "which computes the image gradient and drops it)"},
                "roofline": roof, "cpu_baseline": cpu}
         if breakdown is not None:
             out["breakdown"] = breakdown

@@ -108,10 +108,15 @@ def chain_forward(layers, X, test_mode=False, out_accepts=False):
     return X, steps
 
 
-def chain_backward(steps, dy, residual=None):
+def chain_backward(steps, dy, residual=None, after_step=None, need_input_grad=True):
     """Backward through `steps` in reverse.  `residual`: a gradient to add to the result (the
     residual join's other branch); the first layer adds it in its dgrad epilogue when it
-    can (``accepts_residual``), otherwise it is added separately."""
+    can (``accepts_residual``), otherwise it is added separately.  `after_step(i)` runs after
+    step i's backward has been issued (DataParallel launches its gradient buckets there).
+    need_input_grad=False: the caller discards the gradient w.r.t. the chain's input (the
+    network's image gradient, which the reference's network.backward computes and drops,
+    feed_forward_network.py:64-70), so a first layer with ``skips_input_grad`` computes only
+    its parameter gradients and None is returned."""
     from ._bn_input import accepts_bn_grad, add_residual
     from .batch_norm import BatchNormLayer
     last = len(steps) - 1
@@ -126,11 +131,15 @@ def chain_backward(steps, dy, residual=None):
             dy = step[0].backward_bn_relu(dy, step[1], defer=defer)
         elif defer:
             dy = step[0].backward(dy, defer=True)
+        elif i == 0 and not need_input_grad and residual is None and getattr(step[0], "skips_input_grad", False):
+            dy = step[0].backward(dy, need_dx=False)
         elif i == 0 and residual is not None and getattr(step[0], "accepts_residual", False):
             dy = step[0].backward(dy, residual=residual)
             residual = None
         else:
             dy = step[0].backward(dy)
+        if after_step is not None:
+            after_step(i)
     if residual is not None:
         dy = add_residual(dy, residual)
     return dy

@@ -104,7 +104,9 @@ class ConvLayer(Layer):
         self._bn_in = bn
         return y
 
-    def backward(self, upstream_dx):
+    skips_input_grad = True  # backward(dy, need_dx=False): parameter gradients only (chain_backward)
+
+    def backward(self, upstream_dx, need_dx=True):
         self._require_on_gpu()
         st = stream_handle()
         dy = to_nhwc(upstream_dx)
@@ -135,6 +137,8 @@ class ConvLayer(Layer):
                                         workspace.get(nb), nb, sst)
             if s is None:
                 add_regulariser_grad(gw, w, self.weight_regulariser)
+        if not need_dx:
+            return None
         # input gradient (convolution.py:101-117); shape = the forward input's shape
         Hin, Win = self.input_shape[2], self.input_shape[3]
         dx = empty_nhwc(N, C, Hin, Win)

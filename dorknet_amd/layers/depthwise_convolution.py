@@ -99,7 +99,9 @@ class DepthwiseConvLayer(Layer):
 
     accepts_residual = True  # backward(dy, residual=R) returns dx + R (the residual join, fused)
 
-    def backward(self, upstream_dx, residual=None):
+    skips_input_grad = True  # backward(dy, need_dx=False): parameter gradients only (chain_backward)
+
+    def backward(self, upstream_dx, residual=None, need_dx=True):
         self._require_on_gpu()
         st = stream_handle()
         dy = to_nhwc(upstream_dx)
@@ -137,6 +139,8 @@ class DepthwiseConvLayer(Layer):
                                         sst)
             if s is None:
                 add_regulariser_grad(gw, w, self.weight_regulariser)
+        if not need_dx:
+            return None
         dx = empty_nhwc(N, C, H, W, x.dtype)
         nb = lib.dk_dwconv_dgrad_workspace_bytes(C, R, S)
         dgrad_ex = lib.dk_dwconv_dgrad_ex_bf16 if bf else lib.dk_dwconv_dgrad_ex_f32

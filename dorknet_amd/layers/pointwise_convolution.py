@@ -109,7 +109,9 @@ class PointwiseConvLayer(Layer):
                 and tuple(bx.shape) == (self.X.shape[0], self.num_filters, *self.out_hw)
                 and self.num_filters % 4 == 0 and self.num_filters <= 2048)
 
-    def backward(self, upstream_dx, residual=None):
+    skips_input_grad = True  # backward(dy, need_dx=False): parameter gradients only (chain_backward)
+
+    def backward(self, upstream_dx, residual=None, need_dx=True):
         self._require_on_gpu()
         st = stream_handle()
         x = self.X
@@ -119,7 +121,7 @@ class PointwiseConvLayer(Layer):
         P = N * OH * OW
         w = self.learned_params["weights"]
         if isinstance(upstream_dx, BNGrad):
-            if self._takes_bn_grad(upstream_dx.x):
+            if need_dx and self._takes_bn_grad(upstream_dx.x):
                 # dgrad first: it forms (and stores) dy from the BatchNorm's gradient as it loads it
                 dy = empty_nhwc(N, K, OH, OW)
                 dx = self._dgrad_bnbwd(upstream_dx, dy, residual, st)
@@ -132,7 +134,7 @@ class PointwiseConvLayer(Layer):
             raise NotImplementedError("{}: bf16 storage needs a bf16 gradient, no bias, stride 1".format(
                 self.layer_name))
         self._wgrad(dy, x, N, H, W, C, K, s, OH, OW, P, w, bf)
-        return self._dgrad(dy, residual, st)
+        return self._dgrad(dy, residual, st) if need_dx else None
 
     def _dgrad_bnbwd(self, bg, dy_out, residual, st):
         x = self.X

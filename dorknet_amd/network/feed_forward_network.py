@@ -148,10 +148,12 @@ class FeedForwardNetwork:
             loss += sum(regularisation_terms)
         return loss, X  # NB if test_mode=True, you get softmax scores ("logits")
 
-    def backward(self, upstream_dx=None):
+    def backward(self, upstream_dx=None, input_grad=False):
         """Reference behaviour (feed_forward_network.py:62-70): backward from the loss layer.
         Extension: an explicit output gradient for a network without a loss layer (BASELINE
-        config 5's stack is driven this way)."""
+        config 5's stack is driven this way).  Like the reference this returns nothing, so the
+        gradient w.r.t. the network input (which the reference computes and drops) is not
+        computed; input_grad=True computes and returns it."""
         if upstream_dx is not None:
             pass
         elif self.loss_layer is not None:
@@ -159,7 +161,8 @@ class FeedForwardNetwork:
         else:
             raise ValueError("Network doesn't have a loss, can't run backward pass.")
         with async_weight_grads():  # weight gradients on the side stream, joined on exit
-            chain_backward(self._steps, upstream_dx)
+            dx = chain_backward(self._steps, upstream_dx, need_input_grad=input_grad)
+        return dx if input_grad else None
 
     def test(self, data_loader, batch_size, test_set_size):
         from tqdm import tqdm

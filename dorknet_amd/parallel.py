@@ -125,19 +125,23 @@ class DataParallel:
         dy = net.loss_layer.backward()
         steps = net._steps
         top_index = {id(l): i for i, l in enumerate(net.layers)}
-        pending = list(self.buckets)
+        state = {"pending": list(self.buckets)}
         self._works = []
-        for step in reversed(steps):
-            dy = chain_backward([step], dy)
-            done_idx = min(top_index[id(l)] for l in step)
+
+        def after_step(i):
+            # the buckets whose layers have all been through backward (the deferred BatchNorm
+            # apply runs inside the producer's step, so a bucket is complete only after it)
+            done_idx = min(top_index[id(l)] for l in steps[i])
             still = []
-            for lo, hi, ready_after in pending:
+            for lo, hi, ready_after in state["pending"]:
                 if done_idx <= ready_after:
                     self._launch(lo, hi)
                 else:
                     still.append((lo, hi, ready_after))
-            pending = still
-        for lo, hi, _ in pending:
+            state["pending"] = still
+
+        chain_backward(steps, dy, after_step=after_step, need_input_grad=False)
+        for lo, hi, _ in state["pending"]:
             self._launch(lo, hi)
         self.finish()
 

@@ -194,3 +194,30 @@ def test_regularisation_fast_path_matches_per_layer_terms():
     net._l2_plan = lambda: None          # force the per-layer reference path
     slow, _ = net.forward(dev(X), dev(onehot))
     assert abs(float(fast) - float(slow)) <= 1e-6 * abs(float(slow))
+
+
+def test_input_gradient_on_request():
+    """network.backward() skips the image gradient (the reference computes and drops it);
+    backward(input_grad=True) computes it, matches the oracle, and leaves every parameter
+    gradient bit-identical to the default call."""
+    from examples.mnist_convnet import MNISTNet
+    np.random.seed(3)
+    net = MNISTNet("mnist")
+    onet = network_to_oracle(net)
+    net.to_gpu()
+    rng = np.random.default_rng(4)
+    X = rng.uniform(0, 1, size=(8, 1, 28, 28)).astype(np.float32)
+    onehot = np.eye(10, dtype=np.float32)[rng.integers(0, 10, 8)]
+    grads = []
+    for want in (False, True):
+        net.forward(dev(X), dev(onehot))
+        dx = net.backward(input_grad=want)
+        torch.cuda.synchronize()
+        assert (dx is None) == (not want)
+        grads.append([host(l.grads[k]) for l in all_layers(net.layers) for k in (l.grads or {})])
+    for a, b in zip(*grads):
+        assert np.array_equal(a, b)
+    onet.forward(X.astype(np.float64), onehot.astype(np.float64))
+    odx = onet.backward()
+    assert tuple(dx.shape) == X.shape
+    assert rel_err(host(dx), odx) <= 1e-4
