@@ -127,6 +127,8 @@ ENTRY_KERNEL = {
     "dk_bn_add_f32": "dk::bn_add_kernel",
     "dk_relu_bwd_f32": "dk::relu_bwd_kernel",
     "dk_relu_bwd_bn_partial_f64": "dk::bn_bwd_partial_kernel",
+    # (prefix, substring): the GEMM instantiations whose A operand applies a BN backward
+    "dk_pwconv_dgrad_bnbwd_f32": ("dk::igemm_f32", "dk::MatBwdDesc"),
 }
 
 
@@ -143,8 +145,9 @@ def pmc_traffic(entry, path):
     with open(path) as f:
         d = json.load(f)
     n = t = 0
+    pre, sub = kern if isinstance(kern, tuple) else (kern, "")
     for name, v in d.get("kernels", {}).items():
-        if name.startswith(kern + "<") or name == kern:
+        if (name.startswith(pre + "<") or name == pre) and sub in name:
             n += v["dispatches"]
             t += v["traffic_bytes"] * v["dispatches"]
     if n == 0:

@@ -182,6 +182,12 @@ MODEL = {
     st: (_dw_dgrad(dy, N, OH, OW, C, w, R, S, s, p, dx, H, W, ws, nb, st)[0],
          _dw_dgrad(dy, N, OH, OW, C, w, R, S, s, p, dx, H, W, ws, nb, st)[1] + E * N * H * W * C * (
              (bx != 0) + (res != 0))),
+    # dgrad with the following BN's backward apply on load: reads g and that BN's input
+    # (P x K each), writes dy (P x K) once for the weight gradient, + the dgrad_ex terms
+    "dk_pwconv_dgrad_bnbwd_f32": lambda g, ox, N, OH, OW, K, om, oi, og, ob, orl, k12, dyo, w, C, dx, res, bx, m, i,
+    ga, b, r, part, st: (
+        2 * N * OH * OW * K * C + 6 * N * OH * OW * K,
+        E * (N * OH * OW * K * (2 + (dyo != 0)) + N * OH * OW * C * (1 + (bx != 0) + (res != 0)) + K * C)),
     "dk_relu_bwd_bn_partial_f64": lambda dy, mask, x, P, C, *rest: (4 * P * C, E * 3 * P * C + P * C),
     "dk_bn_bwd_apply_f32": lambda x, dy, n, C, *rest: (6 * n, E * 3 * n),
 }

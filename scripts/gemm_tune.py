@@ -94,7 +94,25 @@ def main():
                     "dgrad": perfmodel.work("dk_pwconv_dgrad_f32", (0, N, OH, OH, K, 0, C, s, 0, 0)),
                     "wgrad": perfmodel.work("dk_pwconv_wgrad_f32", (0, 0, N, H, H, C, K, s, OH, OH, 0, 0, 0, 0, 0, 0))}
             work["fwdx"], work["dgrx"], work["wgrx"] = work["fwd"], work["dgrad"], work["wgrad"]
-            extra = (("fwdx", fwdx, 0), ("dgrx", dgrx, 0), ("wgrx", wgrx, 1))
+            extra = [("fwdx", fwdx, 0), ("dgrx", dgrx, 0), ("wgrx", wgrx, 1)]
+            if s == 1:
+                # dgrad with the following BN's backward applied on load (+ dy write-through),
+                # vs. the separate apply pass it replaces
+                ox = torch.randn(N * OH * OH * K, device="cuda", generator=g)
+                dyo = torch.empty_like(ox)
+                obp = [torch.randn(K, device="cuda", generator=g), torch.rand(K, device="cuda", generator=g) + 0.5,
+                       torch.randn(K, device="cuda", generator=g), torch.randn(K, device="cuda", generator=g)]
+                k12 = torch.randn(2 * K, device="cuda", generator=g) * 0.1
+                oba = tuple(t.data_ptr() for t in obp) + (0, k12.data_ptr())
+                dgrb = lambda: lib.dk_pwconv_dgrad_bnbwd_f32(dy.data_ptr(), ox.data_ptr(), N, OH, OH, K, *oba,
+                                                             dyo.data_ptr(), w.data_ptr(), C, dx.data_ptr(), 0,
+                                                             x.data_ptr(), *bna, part.data_ptr(), st)
+                bapp = lambda: lib.dk_bn_bwd_apply_f32(ox.data_ptr(), dy.data_ptr(), N * OH * OH * K, K, *oba[:5],
+                                                       k12.data_ptr(), dyo.data_ptr(), st)
+                work["dgrb"] = perfmodel.work("dk_pwconv_dgrad_bnbwd_f32", (0, 0, N, OH, OH, K) + (0,) * 6 + (
+                    1, 0, C, 0, 0, 1) + (0,) * 7)
+                work["bapp"] = perfmodel.work("dk_bn_bwd_apply_f32", (0, 0, N * OH * OH * K, K))
+                extra += [("dgrb", dgrb, 0), ("bapp", bapp, 2)]
         else:
             R, s, pd, Cr = sh["R"], sh["st"], sh["pad"], sh["Creal"]
             OH = int((H + 2 * pd - R) / s + 1)
@@ -129,10 +147,10 @@ def main():
         if args.fused_only:
             ops = list(extra) or ops
         for op, fn, kind in ops:
-            n = nrow if kind == 0 else nsplit
+            n = nrow if kind == 0 else (nsplit if kind == 1 else 0)
             row = {"shape": sh["name"], "op": op, "cfg": {}}
             for cfg in [-1] + list(range(n)):
-                lib.dk_debug_set_gemm_config(kind, cfg)
+                lib.dk_debug_set_gemm_config(min(kind, 1), cfg)
                 try:
                     us = timeit(fn)
                 except Exception as e:  # config not applicable
@@ -140,10 +158,11 @@ def main():
                     continue
                 f, b = work[op]
                 row["cfg"][str(cfg)] = {"us": round(us, 1), "GBs": round(b / us / 1e3, 1), "TFs": round(f / us / 1e6, 1)}
-            lib.dk_debug_set_gemm_config(kind, -1)
+            lib.dk_debug_set_gemm_config(min(kind, 1), -1)
             if not isinstance(row["cfg"].get("-1"), dict):
                 continue
-            best = min((v["us"], k) for k, v in row["cfg"].items() if isinstance(v, dict) and k != "-1")
+            best = min(((v["us"], k) for k, v in row["cfg"].items() if isinstance(v, dict) and k != "-1"),
+                       default=(row["cfg"]["-1"]["us"], "-1"))
             row["best"] = best[1]
             results.append(row)
             d = row["cfg"]["-1"]
