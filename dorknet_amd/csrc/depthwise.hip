@@ -447,6 +447,205 @@ __global__ __launch_bounds__(256) void dw_wgrad_partial_kernel(const T* __restri
   }
 }
 
+// The whole stride-1 depthwise backward in one pass, when the layer's output fed a BatchNorm
+// (the depthwise_sep_layer's dw -> BN -> pw, example :34-70): the layer's gradient
+// dy = BN backward(g, x1) (stage 3 of batch_norm.py:125-174, = dk_bn_bwd_apply_f32 bit for bit)
+// is formed once per element in LDS and never stored; the same 3x3 window of it feeds
+//   dx[h][w]   = sum_{r,s} W[2-r][2-s] * dy[h-1+r][w-1+s]                      (pad 1)
+//   dW[a][b]  += xb[h][w] * dy[h+1-a][w+1-b]                                  (per-block partials)
+// where xb is the layer's input (bn_in(X) when it consumed a BNOut).  Reindexing the weight
+// gradient (depthwise_convolution.py:198-221) by input pixel makes its dy taps exactly the
+// dgrad's window.
+// Block = one image, a CL-column strip, CG channel groups of 4 (CG * CL = 256); it walks the
+// rows top to bottom.  Per row: the block forms dy row h+1 for its CL + 2 columns into one of two
+// LDS slots (g and x1 for the row after were loaded one iteration earlier), one barrier, then
+// each thread slides its 3x3 register window down by that row and produces dx[h][w] for its 4
+// channels.  dx is bit-identical to dk_bn_bwd_apply_f32 -> dk_dwconv_dgrad_ex_f32 (same tap
+// order); the input BatchNorm's backward partials (spart) and the weight-gradient partials
+// (wpart) are per-block fixed-order sums, one row per (image, strip), each block writing its
+// channel range.
+struct BnBwdOut {  // the BatchNorm after this layer: dy = bn_bwd_elem(x1, g)
+  const float* mean;
+  const float* invstd;
+  const float* gamma;
+  const float* beta;
+  const float* k12;
+  int relu;
+};
+
+template <bool BNX, bool STATS, bool RELU1>
+__global__ __launch_bounds__(256) void dw_bwd_fused_kernel(const float* __restrict__ g, const float* __restrict__ x1,
+                                                           uint32_t bytes, BnBwdOut ob, const float* __restrict__ x,
+                                                           BnIn bn, const float* __restrict__ w_crs,
+                                                           float* __restrict__ dx, const float* __restrict__ res,
+                                                           double* __restrict__ spart, float* __restrict__ wpart,
+                                                           int N, int H, int W, int C, int CL) {
+  static_assert(!STATS || BNX, "input-BN partials need the input BN");
+  const int CG = 256 / CL;              // channel groups per block
+  const int NI = (CL + 2) * CG;         // dy float4s per LDS row (with the 1-column halos)
+  constexpr int R = 3, S = 3, RS = 9;
+  extern __shared__ f32x4 ring[];       // [2][NI]; reused by the final reductions
+  const int tid = threadIdx.x;
+  const int cg = tid % CG, cl = tid / CG;
+  const int nct = (W + CL - 1) / CL, ncht = (C >> 2) / CG;
+  const int bid = xcd_block(blockIdx.x, gridDim.x);
+  const int cht = bid % ncht;
+  const int strip = bid / ncht;  // (image, column strip): the partial-sum row
+  const int ct = strip % nct, n = strip / nct;
+  const int c = (cht * CG + cg) * 4;
+  const int w = ct * CL + cl;
+  const bool win_ok = w < W;
+  const int wl = ct * CL - 1;  // LDS column 0
+  // this thread's dy items: columns wl + tid / CG and (tid < 2 CG) wl + CL + tid / CG, channel c
+  const bool two = tid < 2 * CG;
+  const int col0 = wl + cl, col1 = wl + CL + cl;
+  const bool cok0 = (unsigned)col0 < (unsigned)W, cok1 = two && (unsigned)col1 < (unsigned)W;
+  const __amdgpu_buffer_rsrc_t rg = make_rsrc_v(g, bytes), r1 = make_rsrc_v(x1, bytes), rx = make_rsrc_v(x, bytes);
+  const f32x4 om = ld4(ob.mean + c), oi = ld4(ob.invstd + c), ok1 = ld4(ob.k12 + c), ok2 = ld4(ob.k12 + C + c);
+  const f32x4 of = ld4(ob.gamma + c) * oi;
+  f32x4 og, obt;
+  if constexpr (RELU1) {
+    og = ld4(ob.gamma + c);
+    obt = ld4(ob.beta + c);
+  }
+  f32x4 bm, bi, bg, bb;
+  if constexpr (BNX) {
+    bm = ld4(bn.mean + c);
+    bi = ld4(bn.invstd + c);
+    bg = ld4(bn.gamma + c);
+    bb = ld4(bn.beta + c);
+  }
+  f32x4 wv[R][S];
+  load_dw_weights<R, S, 2>(wv, w_crs, c, C);  // flipped taps
+  auto xform = [&](f32x4 gv, f32x4 xv, bool ok) {
+    f32x4 o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float ge = gv[e];
+      if constexpr (RELU1) {
+        if (!(bn_out(xv[e], om[e], oi[e], og[e], obt[e]) > 0.f)) ge = 0.f;
+      }
+      o[e] = bn_bwd_elem(xv[e], ge, om[e], oi[e], of[e], ok1[e], ok2[e]);
+    }
+    return ok ? o : f32x4{0.f, 0.f, 0.f, 0.f};
+  };
+  auto pix = [&](int hh, int ww) { return (uint32_t)(((n * H + hh) * W + ww) * C + c); };
+  // raw g / x1 of the next dy row to publish, and this thread's input / residual of the next dx row
+  f32x4 g0, x0, g1, x1v, xr, rv;
+  auto load_dy_row = [&](int hh) {
+    const bool rok = (unsigned)hh < (unsigned)H;
+    g0 = bload4e<float>(rg, rok && cok0, pix(hh, col0));
+    x0 = bload4e<float>(r1, rok && cok0, pix(hh, col0));
+    g1 = bload4e<float>(rg, rok && cok1, pix(hh, col1));
+    x1v = bload4e<float>(r1, rok && cok1, pix(hh, col1));
+  };
+  auto load_x_row = [&](int hh) {
+    const bool ok = win_ok && hh < H;
+    xr = bload4e<float>(rx, ok, pix(hh, w));
+    rv = (res && ok) ? ld4(res + pix(hh, w)) : f32x4{0.f, 0.f, 0.f, 0.f};
+  };
+  double s1[4] = {0.0, 0.0, 0.0, 0.0}, s2[4] = {0.0, 0.0, 0.0, 0.0};
+  f32x4 wacc[R][S];
+  f32x4 d[R][S];
+#pragma unroll
+  for (int r = 0; r < R; ++r)
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      wacc[r][s] = f32x4{0.f, 0.f, 0.f, 0.f};
+      d[r][s] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  load_dy_row(0);  // row -1 is all padding
+  load_x_row(0);
+  float* dxcol = dx ? dx + (size_t)pix(0, w) : nullptr;
+  for (int rr = 0; rr <= H; ++rr) {  // publish dy row rr, then finish dx row rr - 1
+    const int rowok = rr < H;
+    const f32x4 d0 = xform(g0, x0, rowok && cok0), d1 = xform(g1, x1v, rowok && cok1);
+    if (rr + 1 < H) load_dy_row(rr + 1);
+    f32x4* slot = ring + (rr & 1) * NI;
+    slot[tid] = d0;
+    if (two) slot[tid + 256] = d1;
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      d[0][s] = d[1][s];
+      d[1][s] = d[2][s];
+      d[2][s] = slot[(cl + s) * CG + cg];
+    }
+    if (rr == 0) continue;
+    const int h = rr - 1;
+    const f32x4 xh = xr, rh = rv;
+    if (h + 1 < H) load_x_row(h + 1);
+    f32x4 xb = xh;
+    if constexpr (BNX) xb = win_ok ? bn_in4(xh, bm, bi, bg, bb, bn.relu) : f32x4{0.f, 0.f, 0.f, 0.f};
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        acc += d[r][s] * wv[r][s];
+        wacc[r][s] += d[r][s] * xb;
+      }
+    if (win_ok) {
+      if (res) acc += rh;
+      if (dxcol) st4(dxcol + (size_t)h * W * C, acc);
+      if constexpr (STATS) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float ge = acc[e];
+          const float xn = (xh[e] - bm[e]) * bi[e];
+          if (bn.relu && !(bn_out(xh[e], bm[e], bi[e], bg[e], bb[e]) > 0.f)) ge = 0.f;
+          s1[e] += (double)ge;
+          s2[e] += (double)ge * (double)xn;
+        }
+      }
+    }
+  }
+  // fixed-order block reductions over the CL column lanes of each channel group
+  __syncthreads();
+  if constexpr (STATS) {
+    double(*red)[8] = reinterpret_cast<double(*)[8]>(ring);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      red[tid][e] = s1[e];
+      red[tid][4 + e] = s2[e];
+    }
+    __syncthreads();
+    for (int i = tid; i < CG * 8; i += 256) {
+      const int gq = i >> 3, e = i & 7;
+      double a = 0.0;
+      for (int k = 0; k < CL; ++k) a += red[k * CG + gq][e];
+      spart[((size_t)strip * 2 + (e >> 2)) * C + (cht * CG + gq) * 4 + (e & 3)] = a;
+    }
+    __syncthreads();
+  }
+  float* wred = reinterpret_cast<float*>(ring);  // [256][RS][4]
+#pragma unroll
+  for (int r = 0; r < R; ++r)
+#pragma unroll
+    for (int s = 0; s < S; ++s) st4(wred + (tid * RS + r * S + s) * 4, wacc[r][s]);
+  __syncthreads();
+  // wpart[strip][c][a][b], (a, b) = (2-r, 2-s)
+  for (int i = tid; i < CG * 4 * RS; i += 256) {
+    const int cc = i / RS, tap = i - cc * RS;
+    const int a = tap / S, b = tap - a * S;
+    const int gq = cc >> 2, e = cc & 3;
+    const int fl = (R - 1 - a) * S + (S - 1 - b);
+    float sum = 0.f;
+    for (int k = 0; k < CL; ++k) sum += wred[((k * CG + gq) * RS + fl) * 4 + e];
+    wpart[((size_t)strip * C + cht * CG * 4) * RS + i] = sum;
+  }
+}
+
+// Column-strip width CL (CG = 256 / CL channel groups per block): 16 columns x 64 channels, or
+// 8 x 128 for narrow images; fewer channel groups (wider strips) when C / 4 has no such factor.
+static inline int dwb_cl(int W, int C) {
+  const int C4 = C / 4;
+  int cg = W > 8 ? 16 : 32;
+  while (cg > 1 && C4 % cg) cg >>= 1;
+  return 256 / cg;
+}
+static inline int dwb_strips(int N, int W, int cl) { return N * ((W + cl - 1) / cl); }
+
 static int dw_wgrad_blocks(int N, int OH, int OW, int C) {
   const int C4 = C / 4;
   const int cgt = C4 < 256 ? C4 : 256;
@@ -712,6 +911,67 @@ DK_API int dk_dwconv_wgrad_f32(const float* dy, const float* x, int N, int H, in
                                size_t ws_bytes, void* stream) {
   return dw_wgrad(dy, x, N, H, W, C, R, S, stride, pad, OH, OW, w_crs, l2, dw_crs, ws, ws_bytes, BnIn{},
                   as_stream(stream));
+}
+
+// Fused stride-1 backward (dw_bwd_fused_kernel).  Workspace: the weight-gradient partials.
+DK_API int dk_dwconv_bwd_bnbwd_stats_rows(int N, int H, int W, int C) {
+  (void)H;
+  return (C < 4 || C % 4) ? 0 : dwb_strips(N, W, dwb_cl(W, C));
+}
+
+DK_API size_t dk_dwconv_bwd_bnbwd_workspace_bytes(int N, int H, int W, int C, int R, int S) {
+  return (size_t)dk_dwconv_bwd_bnbwd_stats_rows(N, H, W, C) * C * R * S * sizeof(float);
+}
+
+DK_API int dk_dwconv_bwd_bnbwd_f32(const float* g, const float* bn_x, int N, int H, int W, int C,
+                                   const float* out_mean, const float* out_invstd, const float* out_gamma,
+                                   const float* out_beta, int out_relu, const float* k12, const float* x,
+                                   const float* w_crs, int R, int S, int pad, float l2, float* dw_crs, float* dx,
+                                   const float* residual, const float* bn_mean, const float* bn_invstd,
+                                   const float* bn_gamma, const float* bn_beta, int bn_relu, double* part,
+                                   void* ws, size_t ws_bytes, void* stream) {
+  const hipStream_t st = as_stream(stream);
+  if (R != 3 || S != 3 || pad != 1 || C % 4 || N < 1 || H < 1 || W < 1) return DK_ERR_ARGS;
+  const int cl = dwb_cl(W, C);
+  if (!g || !bn_x || !x || !w_crs || !dw_crs || !out_mean || !out_invstd || !out_gamma || !out_beta || !k12)
+    return DK_ERR_ARGS;
+  const BnIn bn{bn_mean, bn_invstd, bn_gamma, bn_beta, bn_relu};
+  if (part && !bn_mean) return DK_ERR_ARGS;  // the input BN's partials need the input BN
+  if (!aligned16(g) || !aligned16(bn_x) || !aligned16(x) || (dx && !aligned16(dx)) ||
+      (residual && !aligned16(residual)) || !bn_ok(bn) || !aligned16(out_mean) || !aligned16(out_invstd) ||
+      !aligned16(out_gamma) || !aligned16(out_beta) || !aligned16(k12) || !aligned16(w_crs))
+    return DK_ERR_ARGS;
+  const size_t bytes = (size_t)N * H * W * C * sizeof(float);
+  if (!fits(bytes)) return DK_ERR_ARGS;
+  if (ws_bytes < dk_dwconv_bwd_bnbwd_workspace_bytes(N, H, W, C, R, S)) return DK_ERR_WORKSPACE;
+  const int strips = dwb_strips(N, W, cl);
+  const int ncht = (C / 4) / (256 / cl);
+  float* wpart = static_cast<float*>(ws);
+  const BnBwdOut ob{out_mean, out_invstd, out_gamma, out_beta, k12, out_relu};
+  const dim3 grid((unsigned)(strips * ncht));
+  size_t shm = (size_t)256 * 9 * 4 * sizeof(float);  // the weight-gradient reduction
+  const size_t ring = (size_t)2 * (cl + 2) * (256 / cl) * sizeof(f32x4);
+  if (ring > shm) shm = ring;
+#define DWB_LAUNCH(BNX_, STATS_, RELU1_)                                                                             \
+  {                                                                                                                  \
+    auto k = dw_bwd_fused_kernel<BNX_, STATS_, RELU1_>;                                                              \
+    if (shm > 65536)                                                                                                 \
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,       \
+                                (int)shm);                                                                           \
+    hipLaunchKernelGGL(k, grid, dim3(256), shm, st, g, bn_x, (uint32_t)bytes, ob, x, bn, w_crs, dx, residual, part,  \
+                       wpart, N, H, W, C, cl);                                                                       \
+  }
+  if (out_relu) {
+    if (part) DWB_LAUNCH(true, true, true) else if (bn_mean) DWB_LAUNCH(true, false, true)
+    else DWB_LAUNCH(false, false, true)
+  } else {
+    if (part) DWB_LAUNCH(true, true, false) else if (bn_mean) DWB_LAUNCH(true, false, false)
+    else DWB_LAUNCH(false, false, false)
+  }
+#undef DWB_LAUNCH
+  int rc = launch_status();
+  if (rc) return rc;
+  return splitk_reduce(wpart, strips, 1, C * R * S, dw_crs, l2 != 0.f ? w_crs : nullptr, l2, 0, C, C, 1, 1, st);
 }
 
 DK_API int dk_dwconv_wgrad_bnx_f32(const float* dy, const float* x, int N, int H, int W, int C, int R, int S,

@@ -58,7 +58,12 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
 int splitk_reduce(const float* ws, int splits, int M, int N, float* out, const float* w, float l2, int mode, int C,
                   int Cp, int R, int S, hipStream_t st) {
   const long long total = (long long)M * N;
-  if (splits >= 64) {
+  if (splits >= 512) {
+    // long slabs (one row per block of a fused backward): 64 lanes per column
+    constexpr int TPO = 64, CPB = 256 / TPO;
+    hipLaunchKernelGGL(splitk_reduce_kernel<TPO>, dim3((unsigned)cdivll(total, CPB)), dim3(256), 0, st, ws, splits,
+                       M, N, out, w, l2, mode, C, Cp, R, S);
+  } else if (splits >= 64) {
     constexpr int TPO = 16, CPB = 256 / TPO;
     hipLaunchKernelGGL(splitk_reduce_kernel<TPO>, dim3((unsigned)cdivll(total, CPB)), dim3(256), 0, st, ws, splits,
                        M, N, out, w, l2, mode, C, Cp, R, S);

@@ -15,7 +15,7 @@ import torch
 
 from .._hip import HipError, lib, stream_handle, weight_grad_stream, workspace
 from .._tensor import BF16, empty_nhwc, ptr, to_nhwc
-from ._bn_input import BNOut, add_residual, residual_operand
+from ._bn_input import BNGrad, BNOut, add_residual, residual_operand
 from ._common import add_regulariser_grad, grad_buffer, init_weights, l2_strength
 from .layer import Layer
 
@@ -101,8 +101,63 @@ class DepthwiseConvLayer(Layer):
 
     skips_input_grad = True  # backward(dy, need_dx=False): parameter gradients only (chain_backward)
 
+    def accepts_bn_grad(self, bn_layer):
+        """backward(BNGrad): the following BatchNorm's apply, this layer's dgrad and its weight
+        gradient run as one pass (dk_dwconv_bwd_bnbwd_f32) -- fp32, stride 1, 3x3 'same'
+        padding, no bias, C % 4 == 0."""
+        bx = getattr(bn_layer, "X", None)
+        return getattr(self, "X", None) is not None and bx is not None and self._takes_bn_grad(bx)
+
+    def _takes_bn_grad(self, bx):
+        x = self.X
+        if x.dim() != 4 or bx.dim() != 4 or x.dtype != torch.float32 or bx.dtype != torch.float32:
+            return False
+        C = x.shape[1]
+        return (self.stride == 1 and self.f_rows == 3 and self.f_cols == 3 and self.padding == 1
+                and not self.with_bias and C % 4 == 0 and tuple(bx.shape) == tuple(x.shape))
+
+    def _backward_bn_grad(self, G, residual, need_dx):
+        """One-pass backward from the following BatchNorm's deferred gradient (see
+        accepts_bn_grad): dx (+ the residual addend, + the input BatchNorm's backward partial
+        sums) and the weight gradient; dy itself is never written."""
+        st = stream_handle()
+        x = self.X
+        N, C, H, W = x.shape
+        R, S = self.f_rows, self.f_cols
+        w = self.learned_params["weights"]
+        gw = grad_buffer(self, "weights", (C, R, S))
+        s = l2_strength(self.weight_regulariser)
+        bn = self._bn_in
+        dx = empty_nhwc(N, C, H, W, x.dtype) if need_dx else None
+        res = residual_operand(residual, dx) if need_dx else None
+        if need_dx and residual is not None and res is None:
+            res = residual_operand(to_nhwc(residual), dx)
+        part = None
+        if need_dx and bn is not None:
+            rows = lib.dk_dwconv_bwd_bnbwd_stats_rows(N, H, W, C)
+            part = torch.empty((rows, 2, C), dtype=torch.float64, device=x.device)
+        g = to_nhwc(G.g)
+        nb = lib.dk_dwconv_bwd_bnbwd_workspace_bytes(N, H, W, C, R, S)
+        lib.dk_dwconv_bwd_bnbwd_f32(g.data_ptr(), G.x.data_ptr(), N, H, W, C, *G.bnbwd_args(), x.data_ptr(),
+                                    w.data_ptr(), R, S, self.padding, s or 0.0, gw.data_ptr(), ptr(dx), ptr(res),
+                                    *(bn.bn_args() if bn is not None else (0, 0, 0, 0, 0)), ptr(part),
+                                    workspace.get(nb), nb, st)
+        if s is None:
+            add_regulariser_grad(gw, w, self.weight_regulariser)
+        if not need_dx:
+            return None
+        if part is not None:
+            bn.hand_backward_partials(dx, part)
+        if residual is not None and res is None:
+            dx = add_residual(dx, residual)  # (a new tensor: the BN then recomputes its sums)
+        return dx
+
     def backward(self, upstream_dx, residual=None, need_dx=True):
         self._require_on_gpu()
+        if isinstance(upstream_dx, BNGrad):
+            if self._takes_bn_grad(upstream_dx.x):
+                return self._backward_bn_grad(upstream_dx, residual, need_dx)
+            upstream_dx = upstream_dx.materialize()
         st = stream_handle()
         dy = to_nhwc(upstream_dx)
         x = self.X

@@ -188,6 +188,12 @@ MODEL = {
     ga, b, r, part, st: (
         2 * N * OH * OW * K * C + 6 * N * OH * OW * K,
         E * (N * OH * OW * K * (2 + (dyo != 0)) + N * OH * OW * C * (1 + (bx != 0) + (res != 0)) + K * C)),
+    # fused depthwise backward: reads g and the following BN's input (to form dy), the layer's
+    # input (weight gradient; the input BN's partials), the residual addend; writes dx
+    "dk_dwconv_bwd_bnbwd_f32": lambda g, ox, N, H, W, C, om, oi, og, ob, orl, k12, x, w, R, S, pad, l2, dw, dx, res,
+    m, i, ga, b, r, part, ws, nb, st: (
+        2 * 2 * N * H * W * C * R * S + 6 * N * H * W * C,
+        E * (N * H * W * C * (3 + (dx != 0) + (res != 0)) + 2 * C * R * S)),
     "dk_relu_bwd_bn_partial_f64": lambda dy, mask, x, P, C, *rest: (4 * P * C, E * 3 * P * C + P * C),
     "dk_bn_bwd_apply_f32": lambda x, dy, n, C, *rest: (6 * n, E * 3 * n),
 }

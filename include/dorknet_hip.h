@@ -172,6 +172,19 @@ int dk_dwconv_wgrad_f32(const float* dy, const float* x, int N, int H, int W, in
 /* BN-on-load variants (see the *_bnx_* note after the pointwise block). */
 int dk_dwconv_fwd_bnx_f32(const float* x, int N, int H, int W, int C, const float* w_rsc, int R, int S, int stride, int pad, const float* bias, float* y, int OH, int OW, const float* bn_mean, const float* bn_invstd, const float* bn_gamma, const float* bn_beta, int bn_relu, void* stream);
 int dk_dwconv_wgrad_bnx_f32(const float* dy, const float* x, int N, int H, int W, int C, int R, int S, int stride, int pad, int OH, int OW, const float* w_crs, float l2, float* dw_crs, void* ws, size_t ws_bytes, const float* bn_mean, const float* bn_invstd, const float* bn_gamma, const float* bn_beta, int bn_relu, void* stream);
+/* Fused stride-1 depthwise backward for a layer whose OUTPUT fed a BatchNorm (+ReLU): replaces
+ * dk_bn_bwd_apply_f32 -> dk_dwconv_dgrad_ex_f32 + dk_dwconv_wgrad_bnx_f32 (batch_norm.py:125-174
+ * stage 3; depthwise_convolution.py:198-221 backward_cp) with one pass.  g: gradient w.r.t. that
+ * BN's output; bn_x: its raw input (= this layer's output, N x H x W x C: stride 1, same size as
+ * the input); out_* / k12: its parameters and folded coefficients.  dy is formed as it is loaded
+ * and never stored.  x: this layer's stored input, with bn_* its input BatchNorm applied on load
+ * (bn_mean NULL: none); part (NULL: none; needs bn_*): that input BN's backward partial sums,
+ * dk_dwconv_bwd_bnbwd_stats_rows rows [rows][2][C] (fp64).  dx NULL: weight gradient only.
+ * dw_crs = weight gradient (+ l2 * w_crs).  3x3 filters, pad 1, C % 4 == 0.  dx is bit-identical
+ * to the unfused sequence; part and dw_crs differ from it by summation order only. */
+int dk_dwconv_bwd_bnbwd_stats_rows(int N, int H, int W, int C);
+size_t dk_dwconv_bwd_bnbwd_workspace_bytes(int N, int H, int W, int C, int R, int S);
+int dk_dwconv_bwd_bnbwd_f32(const float* g, const float* bn_x, int N, int H, int W, int C, const float* out_mean, const float* out_invstd, const float* out_gamma, const float* out_beta, int out_relu, const float* k12, const float* x, const float* w_crs, int R, int S, int pad, float l2, float* dw_crs, float* dx, const float* residual, const float* bn_mean, const float* bn_invstd, const float* bn_gamma, const float* bn_beta, int bn_relu, double* part, void* ws, size_t ws_bytes, void* stream);
 
 /* ---------------------------------------------------------------------------------------
  * Dense layer (layers/dense_layer.py:46-67; W stored (in, out) as the reference).

@@ -43,7 +43,7 @@ PW = [("pw0", 112, 64, 64, 2), ("res1_pw", 56, 64, 64, 1), ("res3_dw2_pw", 28, 1
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=256)
-    ap.add_argument("--only", default="dw,bn,pw")
+    ap.add_argument("--only", default="dw,dwb,bn,pw")
     a = ap.parse_args()
     B = a.batch
     st = torch.cuda.current_stream().cuda_stream
@@ -83,6 +83,42 @@ def main():
             report(name + " wgrad bnx", timeit(lambda: lib.dk_dwconv_wgrad_bnx_f32(*wb)), "dk_dwconv_wgrad_bnx_f32",
                    wb)
             del x, dy, y, dx
+    if "dwb" in only:
+        # stride-1 depthwise backward when the layer fed a BatchNorm: the unfused chain
+        # (BN-backward apply -> dgrad_ex with the input BN's partials -> wgrad_bnx) vs one pass
+        for name, H, C, s in DW:
+            if s != 1:
+                continue
+            n = B * H * H * C
+            gg, xo, xin = rnd(n), rnd(n), rnd(n)
+            dy, dx = torch.empty(n, device="cuda"), torch.empty(n, device="cuda")
+            w = rnd(C * 9)
+            po, pi = bnp(C), bnp(C)
+            k12 = rnd(2 * C) * 0.1
+            rows = lib.dk_dwconv_dgrad_stats_rows(B, H, H, C, 1)
+            part = torch.empty(rows * 2 * C, dtype=torch.float64, device="cuda")
+            dw = torch.empty(C * 9, device="cuda")
+            oa = tuple(t.data_ptr() for t in po) + (0, k12.data_ptr())
+            ia = tuple(t.data_ptr() for t in pi) + (1,)
+            ap = (xo.data_ptr(), gg.data_ptr(), n, C) + oa[:4] + (0, k12.data_ptr(), dy.data_ptr(), st)
+            nbd = lib.dk_dwconv_dgrad_workspace_bytes(C, 3, 3)
+            dga = (dy.data_ptr(), B, H, H, C, w.data_ptr(), 3, 3, 1, 1, dx.data_ptr(), H, H, workspace.get(nbd), nbd,
+                   0, xin.data_ptr()) + ia + (part.data_ptr(), st)
+            nbw = lib.dk_dwconv_wgrad_workspace_bytes(B, H, H, C, 3, 3)
+            wga = (dy.data_ptr(), xin.data_ptr(), B, H, H, C, 3, 3, 1, 1, H, H, 0, 0.0, dw.data_ptr(),
+                   workspace.get(nbw), nbw) + ia + (st,)
+
+            def unfused():
+                lib.dk_bn_bwd_apply_f32(*ap)
+                lib.dk_dwconv_dgrad_ex_f32(*dga)
+                lib.dk_dwconv_wgrad_bnx_f32(*wga)
+            nbf = lib.dk_dwconv_bwd_bnbwd_workspace_bytes(B, H, H, C, 3, 3)
+            fa = (gg.data_ptr(), xo.data_ptr(), B, H, H, C) + oa + (xin.data_ptr(), w.data_ptr(), 3, 3, 1, 0.0,
+                                                                  dw.data_ptr(), dx.data_ptr(), 0) + ia + (
+                part.data_ptr(), workspace.get(nbf), nbf, st)
+            report(name + " bwd unfused", timeit(unfused), "dk_dwconv_bwd_bnbwd_f32", fa)
+            report(name + " bwd fused", timeit(lambda: lib.dk_dwconv_bwd_bnbwd_f32(*fa)), "dk_dwconv_bwd_bnbwd_f32", fa)
+            del gg, xo, xin, dy, dx
     if "bn" in only:
         for name, H, C in BN:
             P = B * H * H

@@ -418,10 +418,64 @@ def test_pointwise_dgrad_bnbwd_bitwise(relu, bn_in, resid, K):
         same(part0, part1)
 
 
-def test_network_bn_grad_deferral_bitwise(monkeypatch):
+@pytest.mark.parametrize("relu,bn_in,resid,C,need_dx", [(0, True, False, 64, True), (0, True, True, 32, True),
+                                                         (1, False, False, 16, True), (0, False, True, 128, True),
+                                                         (0, True, False, 8, False), (1, True, True, 256, True)])
+def test_depthwise_bwd_bnbwd(relu, bn_in, resid, C, need_dx):
+    """dk_dwconv_bwd_bnbwd_f32 (BN-backward apply + dgrad + wgrad in one pass) against the unfused
+    sequence dk_bn_bwd_apply_f32 -> dk_dwconv_dgrad_ex_f32 + dk_dwconv_wgrad_bnx_f32: dx bitwise;
+    the input BN's partial sums and the weight gradient (other summation orders) to fp32
+    rounding."""
+    rng = np.random.RandomState(relu + 2 * bn_in + 4 * resid + C + 8 * need_dx)
+    N, H, W, R = 3, 13, 11, 3
+    xo = nhwc(rng.randn(N, C, H, W))        # this layer's output = the following BN's input
+    g = nhwc(rng.randn(N, C, H, W))         # gradient w.r.t. that BN's (+ReLU) output
+    po = bn_params(C, rng)
+    k12 = _k12(C, rng)
+    w = torch.as_tensor(rng.randn(C, R, R).astype(np.float32), device="cuda")
+    xin = nhwc(rng.randn(N, C, H, W))       # this layer's stored input (raw input of its input BN)
+    pi = bn_params(C, rng)
+    res = nhwc(rng.randn(N, C, H, W)) if resid else None
+    st = stream_handle()
+    rows = lib.dk_dwconv_dgrad_stats_rows(N, H, W, C, 1)
+    dy0 = bwd_apply(xo, g, po, relu, k12)
+    dx0 = torch.empty_like(xin)
+    part0 = torch.zeros((rows, 2, C), dtype=torch.float64, device="cuda")
+    nb = lib.dk_dwconv_dgrad_workspace_bytes(C, R, R)
+    bnd = (xin.data_ptr(), *args(pi, 1), part0.data_ptr()) if bn_in else (0, 0, 0, 0, 0, 0, 0)
+    assert lib.dk_dwconv_dgrad_ex_f32(dy0.data_ptr(), N, H, W, C, w.data_ptr(), R, R, 1, 1, dx0.data_ptr(), H, W,
+                                      workspace.get(nb), nb, res.data_ptr() if resid else 0, *bnd, st) == 0
+    dw0 = torch.empty_like(w)
+    nb = lib.dk_dwconv_wgrad_workspace_bytes(N, H, W, C, R, R)
+    wa = (dy0.data_ptr(), xin.data_ptr(), N, H, W, C, R, R, 1, 1, H, W, 0, 0.0, dw0.data_ptr(), workspace.get(nb), nb)
+    if bn_in:
+        assert lib.dk_dwconv_wgrad_bnx_f32(*wa, *args(pi, 1), st) == 0
+    else:
+        assert lib.dk_dwconv_wgrad_f32(*wa, st) == 0
+    dx1 = torch.full_like(xin, float("nan")) if need_dx else None
+    rows1 = lib.dk_dwconv_bwd_bnbwd_stats_rows(N, H, W, C)
+    part1 = torch.zeros((rows1, 2, C), dtype=torch.float64, device="cuda") if (bn_in and need_dx) else None
+    dw1 = torch.full_like(w, float("nan"))
+    nb = lib.dk_dwconv_bwd_bnbwd_workspace_bytes(N, H, W, C, R, R)
+    assert lib.dk_dwconv_bwd_bnbwd_f32(g.data_ptr(), xo.data_ptr(), N, H, W, C, *args(po, relu), k12.data_ptr(),
+                                       xin.data_ptr(), w.data_ptr(), R, R, 1, 0.0, dw1.data_ptr(),
+                                       dx1.data_ptr() if need_dx else 0, res.data_ptr() if (resid and need_dx) else 0,
+                                       *(args(pi, 1) if bn_in else (0, 0, 0, 0, 0)),
+                                       part1.data_ptr() if part1 is not None else 0, workspace.get(nb), nb, st) == 0
+    torch.cuda.synchronize()
+    if need_dx:
+        same(dx0, dx1)
+        if bn_in:
+            s0, s1 = part0.sum(0), part1.sum(0)
+            assert float((s1 - s0).norm() / s0.norm()) < 1e-12
+    err = float((dw1 - dw0).norm() / dw0.norm())
+    assert err < 1e-6, err
+
+
+def test_network_bn_grad_deferral(monkeypatch):
     """pw -> BN -> ReLU -> dw -> BN -> pw -> BN -> ReLU: the fused backward (the apply of each BN
-    that follows a pw layer runs in that layer's dgrad loader) equals the layer-by-layer backward
-    bit for bit."""
+    that follows a pw layer runs in that layer's dgrad loader, the one after the dw layer in its
+    one-pass backward) equals the layer-by-layer backward."""
     from dorknet_amd.layers.activations import ReLu
     from dorknet_amd.layers.batch_norm import BatchNormLayer
     from dorknet_amd.layers.depthwise_convolution import DepthwiseConvLayer
@@ -452,5 +506,9 @@ def test_network_bn_grad_deferral_bitwise(monkeypatch):
         torch.cuda.synchronize()
         outs.append([dx.float().cpu()] + [torch.as_tensor(l.grads[k]).float().cpu() if not torch.is_tensor(l.grads[k])
                                           else l.grads[k].float().cpu() for l in ls for k in sorted(l.grads or {})])
-    for a, b in zip(*outs):
-        assert torch.equal(a, b), float((a - b).abs().max())
+    names = ["dx"] + ["{}.{}".format(l.layer_name, k) for l in build() for k in sorted(l.grads or {})]
+    for n, a, b in zip(names, *outs):
+        # the fused depthwise backward (dk_dwconv_bwd_bnbwd_f32) sums its weight gradient and the
+        # input BatchNorm's backward partials in other orders than the layer-by-layer kernels, so
+        # everything upstream of d1 agrees to fp32 rounding rather than bitwise
+        assert float((a - b).norm() / b.norm()) < 1e-5, n
