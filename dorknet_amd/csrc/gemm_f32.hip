@@ -342,6 +342,14 @@ struct LdMatICT : ICLayout<ROWS, BK> {
   int iq, kb, i0;
   bool active;
   f32x4 v[NK];
+  // BN backward on load (MatBwdDesc; wgrad's dy operand, i = channel): the BN's raw input and
+  // the coefficient table in LDS, as LdMatKCT
+  f32x4 xv[NK];
+  uint32_t okm;
+  const f32x4* tab;
+  float* dyo;
+  bool writer;
+  int relu_flag = 0;
 
   template <class D>
   __device__ __forceinline__ void init(const D&, int row0, int tid) {
@@ -355,6 +363,8 @@ struct LdMatICT : ICLayout<ROWS, BK> {
   __device__ __forceinline__ void load(const D& d, int k0, int Ktot) {
     const __amdgpu_buffer_rsrc_t rs = make_rsrc_v(d.p, d.bytes);
     static_assert(VEC || sizeof(typename D::Elem) == 4, "scalar loads: fp32 storage only");
+    static_assert(VEC || !D::kBnBwd, "BN backward on load: 16-byte loads only");
+    uint32_t om = 0;
 #pragma unroll
     for (int j = 0; j < NK; ++j) {
       const int k = k0 + kb + j * KSTEP;
@@ -362,16 +372,47 @@ struct LdMatICT : ICLayout<ROWS, BK> {
       const uint32_t base = (uint32_t)(k * d.ld + i0) * 4u;
       if constexpr (VEC) {
         v[j] = bload4e<typename D::Elem>(rs, kv && i0 < d.ext, (uint32_t)(k * d.ld + i0));
+        if constexpr (D::kBnBwd) {
+          const __amdgpu_buffer_rsrc_t rx = make_rsrc_v(d.x, d.bytes);
+          xv[j] = bload4e<float>(rx, kv && i0 < d.ext, (uint32_t)(k * d.ld + i0));
+          om |= (uint32_t)(kv && i0 < d.ext) << j;
+        }
       } else {
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[j][e] = bload1(rs, (kv && i0 + e < d.ext) ? base + 4u * e : kOOB);
       }
     }
+    if constexpr (D::kBnBwd) okm = om;
   }
 
-  template <class>
-  __device__ __forceinline__ void store(float* T) const {
+  template <class D>
+  __device__ __forceinline__ void store(float* T) {
     if (!active) return;
+    if constexpr (D::kBnBwd) {
+      if (okm) {
+        // dy for channels i0..i0+3 (all < ext when any pixel is valid: ext % 4 == 0)
+        f32x4 p[4], q[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          p[e] = tab[2 * (i0 + e)];
+          q[e] = tab[2 * (i0 + e) + 1];
+        }
+#pragma unroll
+        for (int j = 0; j < NK; ++j) {
+          f32x4 o = {0.f, 0.f, 0.f, 0.f};
+          if ((okm >> j) & 1u) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const float xe = xv[j][e];
+              float ge = v[j][e];
+              if (relu_flag && !(bn_out(xe, p[e][0], p[e][1], p[e][2], p[e][3]) > 0.f)) ge = 0.f;
+              o[e] = bn_bwd_elem(xe, ge, p[e][0], p[e][1], q[e][2], q[e][0], q[e][1]);
+            }
+          }
+          v[j] = o;
+        }
+      }
+    }
 #pragma unroll
     for (int j = 0; j < NK; ++j) st4(T + (kb + j * KSTEP) * L::S + 4 * iq, v[j]);
   }
@@ -1273,6 +1314,55 @@ DK_API int dk_conv2d_wgrad_f32(const float* dy, const float* x, int N, int H, in
   if (Cp % 4 || !aligned16(x) || !fits((size_t)N * H * W * Cp * 4)) return DK_ERR_ARGS;
   return wgrad(dy, img(x, N, H, W, Cp, OH, OW, R, S, stride, 1, -pad, N * OH * OW), K, R * S * Cp, w_kcrs, l2,
                dw_kcrs, 1, C, Cp, R, S, ws, ws_bytes, stream);
+}
+
+// Weight gradient with the following BatchNorm's backward applied as dy is loaded: g is the
+// gradient w.r.t. that BN's (+ReLU) output, bn_x its raw input (= this layer's output), out_* /
+// k12 its parameters and folded coefficients -- dy = dk_bn_bwd_apply_f32(bn_x, g) bit for bit,
+// never stored (the stem, whose input gradient is not needed: the apply pass over its
+// 64 x 112 x 112 output per image and the re-read of dy become one read of g and bn_x).
+// bn_* (optional): this layer's input BatchNorm applied on load, as dk_conv2d_wgrad_bnx_f32.
+template <class D>
+static int wgrad_bnbwd(const float* g, const float* bn_x, const D& b, int K, int Ncol, const BnBwdIn& bw,
+                       const float* w, float l2, float* dw, int C, int Cp, int R, int S, void* ws, size_t ws_bytes,
+                       void* stream) {
+  const int Kred = b.M;
+  if (!fits((size_t)Kred * K * 4)) return DK_ERR_ARGS;
+  if (ws_bytes < splitk_ws_bytes(K, Ncol, Kred)) return DK_ERR_WORKSPACE;
+  MatDesc a0 = mat(g, Kred, K, K);
+  if (!vec_ok(a0, 4, K) || !aligned16(bn_x)) return DK_ERR_ARGS;
+  MatBwdDesc a;
+  static_cast<MatDesc&>(a) = a0;
+  a.x = bn_x;
+  a.bwd = bw;
+  a.dy_out = nullptr;
+  int splits = 1;
+  float* part = static_cast<float*>(ws);
+  const hipStream_t st = as_stream(stream);
+  int rc = igemm_splitk<LdMatIC, MatBwdDesc, LdImgIC, D>(a, b, part, K, Ncol, Kred, st, &splits);
+  if (rc) return rc;
+  return splitk_reduce(part, splits, K, Ncol, dw, w, l2, 1, C, Cp, R, S, st);
+}
+
+DK_API int dk_conv2d_wgrad_bnbwd_f32(const float* g, const float* bn_x, const float* x, int N, int H, int W, int Cp,
+                                     int C, int K,
+                                     int R, int S, int stride, int pad, int OH, int OW, const float* out_mean,
+                                     const float* out_invstd, const float* out_gamma, const float* out_beta,
+                                     int out_relu, const float* k12, const float* w_kcrs, float l2, float* dw_kcrs,
+                                     void* ws, size_t ws_bytes, const float* bn_mean, const float* bn_invstd,
+                                     const float* bn_gamma, const float* bn_beta, int bn_relu, void* stream) {
+  if (Cp % 4 || K % 4 || !aligned16(x) || !fits((size_t)N * H * W * Cp * 4)) return DK_ERR_ARGS;
+  if (!out_mean || !out_invstd || !out_gamma || !out_beta || !k12) return DK_ERR_ARGS;
+  const BnBwdIn bw{out_mean, out_invstd, out_gamma, out_beta, k12, out_relu, K};
+  if (bn_mean) {
+    if (!bn_ok(bn_mean, bn_invstd, bn_gamma, bn_beta)) return DK_ERR_ARGS;
+    return wgrad_bnbwd(g, bn_x,
+                       with_bn(img(x, N, H, W, Cp, OH, OW, R, S, stride, 1, -pad, N * OH * OW), bn_mean,
+                               bn_invstd, bn_gamma, bn_beta, bn_relu),
+                       K, R * S * Cp, bw, w_kcrs, l2, dw_kcrs, C, Cp, R, S, ws, ws_bytes, stream);
+  }
+  return wgrad_bnbwd(g, bn_x, img(x, N, H, W, Cp, OH, OW, R, S, stride, 1, -pad, N * OH * OW), K,
+                     R * S * Cp, bw, w_kcrs, l2, dw_kcrs, C, Cp, R, S, ws, ws_bytes, stream);
 }
 
 DK_API int dk_conv2d_wgrad_bnx_f32(const float* dy, const float* x, int N, int H, int W, int Cp, int C, int K, int R,

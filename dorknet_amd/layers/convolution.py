@@ -19,7 +19,7 @@ import torch
 
 from .._hip import lib, stream_handle, weight_grad_stream, workspace
 from .._tensor import empty_nhwc, ptr, to_nhwc
-from ._bn_input import BNOut
+from ._bn_input import BNGrad, BNOut
 from ._common import add_regulariser_grad, grad_buffer, init_weights, l2_strength
 from .layer import Layer
 
@@ -106,8 +106,45 @@ class ConvLayer(Layer):
 
     skips_input_grad = True  # backward(dy, need_dx=False): parameter gradients only (chain_backward)
 
+    def accepts_bn_grad(self, bn_layer):
+        """backward(BNGrad, need_dx=False): the following BatchNorm's apply runs in this layer's
+        weight-gradient loader (dk_conv2d_wgrad_bnbwd_f32) -- the stem, whose input gradient
+        the network drops.  With need_dx the gradient is materialised (the dgrad reads it)."""
+        bx = getattr(bn_layer, "X", None)
+        return getattr(self, "X", None) is not None and bx is not None and self._takes_bn_grad(bx)
+
+    def _takes_bn_grad(self, bx):
+        x = self.X
+        OH, OW = int(self.num_row_patches), int(self.num_col_patches)
+        return (bx.dim() == 4 and bx.dtype == torch.float32 and x.dtype == torch.float32 and not self.with_bias
+                and self.num_filters % 4 == 0 and tuple(bx.shape) == (x.shape[0], self.num_filters, OH, OW))
+
+    def _wgrad_bn_grad(self, G):
+        """Weight gradient straight from the following BatchNorm's deferred gradient."""
+        st = stream_handle()
+        x = self.X
+        N, Cp, H, W = x.shape
+        K, C, R, S = self.num_filters, self.filter_chans, self.f_rows, self.f_cols
+        OH, OW = int(self.num_row_patches), int(self.num_col_patches)
+        w = self.learned_params["weights"]
+        gw = grad_buffer(self, "weights", (K, C, R, S))
+        s = l2_strength(self.weight_regulariser)
+        nb = lib.dk_conv2d_wgrad_workspace_bytes(N, OH, OW, K, Cp, R, S)
+        g = to_nhwc(G.g)
+        lib.dk_conv2d_wgrad_bnbwd_f32(g.data_ptr(), G.x.data_ptr(), x.data_ptr(), N, H, W, Cp, C, K, R, S,
+                                      self.stride, self.padding, OH, OW, *G.bnbwd_args(), w.data_ptr() if s else 0,
+                                      s or 0.0, gw.data_ptr(), workspace.get(nb), nb,
+                                      *(self._bn_in.bn_args() if self._bn_in is not None else (0, 0, 0, 0, 0)), st)
+        if s is None:
+            add_regulariser_grad(gw, w, self.weight_regulariser)
+
     def backward(self, upstream_dx, need_dx=True):
         self._require_on_gpu()
+        if isinstance(upstream_dx, BNGrad):
+            if not need_dx and self._takes_bn_grad(upstream_dx.x):
+                self._wgrad_bn_grad(upstream_dx)
+                return None
+            upstream_dx = upstream_dx.materialize()
         st = stream_handle()
         dy = to_nhwc(upstream_dx)
         x = self.X

@@ -165,6 +165,11 @@ MODEL = {
     "dk_nchw_to_nhwc_f32": _nchw_to_nhwc,
     "dk_conv2d_fwd_bnx_f32": _bnx(_conv_fwd),
     "dk_conv2d_wgrad_bnx_f32": _bnx(_conv_wgrad),
+    # wgrad with the following BN's backward apply on load: reads g and that BN's input
+    # (N*OH*OW*K each) instead of dy
+    "dk_conv2d_wgrad_bnbwd_f32": lambda g, ox, x, N, H, W, Cp, C, K, R, S, st_, pad, OH, OW, *rest: (
+        2 * N * OH * OW * K * C * R * S + 6 * N * OH * OW * K,
+        E * (2 * N * OH * OW * K + N * H * W * Cp + K * R * S * C)),
     "dk_pwconv_fwd_bnx_f32": _bnx(_pw_fwd),
     "dk_pwconv_wgrad_bnx_f32": _bnx(_pw_wgrad),
     "dk_dwconv_fwd_bnx_f32": _bnx(_dw_fwd),

@@ -89,6 +89,13 @@ int dk_pwconv_wgrad_f32(const float* dy, const float* x, int N, int H, int W, in
  * bn_*: per-channel mean, 1/std, gamma, beta (C floats each, 16-byte aligned).
  * ------------------------------------------------------------------------------------- */
 int dk_conv2d_fwd_bnx_f32(const float* x, int N, int H, int W, int C, const float* w_krsc, int K, int R, int S, int stride, int pad, const float* bias, float* y, int OH, int OW, const float* bn_mean, const float* bn_invstd, const float* bn_gamma, const float* bn_beta, int bn_relu, void* stream);
+/* Weight gradient with the following BatchNorm's backward applied as dy is loaded (g: the
+ * gradient w.r.t. that BN's (+ReLU) output; bn_x: its raw input = this layer's output; out_* /
+ * k12: its parameters and folded coefficients): dy = dk_bn_bwd_apply_f32(bn_x, g) bit for bit,
+ * never stored.  Replaces dk_bn_bwd_apply_f32 -> dk_conv2d_wgrad[_bnx]_f32 for a layer whose
+ * input gradient is not needed (the stem: feed_forward_network.py:64-70 drops it).  bn_* (optional):
+ * this layer's input BatchNorm, as dk_conv2d_wgrad_bnx_f32.  Workspace: dk_conv2d_wgrad_workspace_bytes. */
+int dk_conv2d_wgrad_bnbwd_f32(const float* g, const float* bn_x, const float* x, int N, int H, int W, int Cp, int C, int K, int R, int S, int stride, int pad, int OH, int OW, const float* out_mean, const float* out_invstd, const float* out_gamma, const float* out_beta, int out_relu, const float* k12, const float* w_kcrs, float l2, float* dw_kcrs, void* ws, size_t ws_bytes, const float* bn_mean, const float* bn_invstd, const float* bn_gamma, const float* bn_beta, int bn_relu, void* stream);
 int dk_conv2d_wgrad_bnx_f32(const float* dy, const float* x, int N, int H, int W, int Cp, int C, int K, int R, int S, int stride, int pad, int OH, int OW, const float* w_kcrs, float l2, float* dw_kcrs, void* ws, size_t ws_bytes, const float* bn_mean, const float* bn_invstd, const float* bn_gamma, const float* bn_beta, int bn_relu, void* stream);
 int dk_pwconv_fwd_bnx_f32(const float* x, int N, int H, int W, int C, const float* w_kc, int K, int stride, const float* bias, float* y, int OH, int OW, const float* bn_mean, const float* bn_invstd, const float* bn_gamma, const float* bn_beta, int bn_relu, void* stream);
 int dk_pwconv_wgrad_bnx_f32(const float* dy, const float* x, int N, int H, int W, int C, int K, int stride, int OH, int OW, const float* w_kc, float l2, float* dw_kc, void* ws, size_t ws_bytes, const float* bn_mean, const float* bn_invstd, const float* bn_gamma, const float* bn_beta, int bn_relu, void* stream);

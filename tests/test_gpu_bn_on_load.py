@@ -472,6 +472,38 @@ def test_depthwise_bwd_bnbwd(relu, bn_in, resid, C, need_dx):
     assert err < 1e-6, err
 
 
+@pytest.mark.parametrize("relu,bn_in,Cp,K,R,stride", [(1, False, 4, 64, 5, 2), (0, True, 8, 16, 3, 1),
+                                                        (1, True, 12, 32, 3, 2)])
+def test_conv_wgrad_bnbwd_bitwise(relu, bn_in, Cp, K, R, stride):
+    """dk_conv2d_wgrad_bnbwd_f32 == dk_bn_bwd_apply_f32 -> dk_conv2d_wgrad[_bnx]_f32, bitwise (dy is
+    formed as it is loaded; the GEMM, its split and its reduction are unchanged)."""
+    rng = np.random.RandomState(relu + 2 * bn_in + Cp + K + R)
+    N, H, W, pad = 3, 17, 15, 1
+    OH, OW = (H + 2 * pad - R) // stride + 1, (W + 2 * pad - R) // stride + 1
+    x = nhwc(rng.randn(N, Cp, H, W))
+    xo = nhwc(rng.randn(N, K, OH, OW))
+    g = nhwc(rng.randn(N, K, OH, OW))
+    po = bn_params(K, rng)
+    pi = bn_params(Cp, rng)
+    k12 = _k12(K, rng)
+    st = stream_handle()
+    nb = lib.dk_conv2d_wgrad_workspace_bytes(N, OH, OW, K, Cp, R, R)
+    dy = bwd_apply(xo, g, po, relu, k12)
+    dw0 = torch.empty((K, Cp, R, R), device="cuda")
+    a = (dy.data_ptr(), x.data_ptr(), N, H, W, Cp, Cp, K, R, R, stride, pad, OH, OW, 0, 0.0, dw0.data_ptr(),
+         workspace.get(nb), nb)
+    if bn_in:
+        assert lib.dk_conv2d_wgrad_bnx_f32(*a, *args(pi, 1), st) == 0
+    else:
+        assert lib.dk_conv2d_wgrad_f32(*a, st) == 0
+    dw1 = torch.full_like(dw0, float("nan"))
+    assert lib.dk_conv2d_wgrad_bnbwd_f32(g.data_ptr(), xo.data_ptr(), x.data_ptr(), N, H, W, Cp, Cp, K, R, R, stride,
+                                         pad, OH, OW, *args(po, relu), k12.data_ptr(), 0, 0.0, dw1.data_ptr(),
+                                         workspace.get(nb), nb, *(args(pi, 1) if bn_in else (0, 0, 0, 0, 0)),
+                                         st) == 0
+    same(dw0, dw1)
+
+
 def test_network_bn_grad_deferral(monkeypatch):
     """pw -> BN -> ReLU -> dw -> BN -> pw -> BN -> ReLU: the fused backward (the apply of each BN
     that follows a pw layer runs in that layer's dgrad loader, the one after the dw layer in its
