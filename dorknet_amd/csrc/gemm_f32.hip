@@ -969,19 +969,31 @@ static int launch_igemm(const DA& da, const DB& db, const EP& ep, int M, int N, 
   return launch_status();
 }
 
-static int row_config(int M, int N, int K) {
+// Row-problem kinds with their own tile choice: plain loaders, and the BN-backward-on-load A
+// operand (dk_pwconv_dgrad_bnbwd_f32), whose per-element transform is repeated for every column
+// tile -- wide column tiles amortise it.
+enum : int { kRowPlain = 0, kRowBnBwd = 1 };
+
+static int row_config(int M, int N, int K, int kind = kRowPlain) {
   if (g_cfg_override[0] >= 0) return g_cfg_override[0];
   (void)M;
-  (void)N;
+  if (kind == kRowBnBwd) {
+    // Measured on MI355X (scripts/gemm_tune.py --fused-only, profiles/r01h_gemm_tune_fused.txt)
+    if (N <= 64) return 8;                // 64x64x32
+    if (N <= 128) return 16;              // 128x128x32, 2x4 waves
+    if (N <= 256) return K >= 512 ? 13 : 6;
+    return 9;                             // 256x128x16
+  }
   // Measured on MI355X (scripts/gemm_tune.py, profiles/r01c_gemm_tune.md): 64x64 tiles win on
   // every ResNet shape; a deeper k-tile pays once the reduction is longer than ~100.
   return K <= 128 ? 6 : 8;
 }
 
 // Output-stationary problems (fwd / dgrad).
-template <template <int, int, int> class LA, class DA, template <int, int, int> class LB, class DB, class EP>
+template <template <int, int, int> class LA, class DA, template <int, int, int> class LB, class DB, class EP,
+          int KIND = kRowPlain>
 static int igemm_rows(const DA& da, const DB& db, const EP& ep, int M, int N, int Ktot, hipStream_t st) {
-  switch (row_config(M, N, Ktot)) {
+  switch (row_config(M, N, Ktot, KIND)) {
 #define DK_CASE(id, bm, bn, bk, wm, wn) \
   case id:                              \
     return launch_igemm<bm, bn, bk, wm, wn, LA, DA, LB, DB, EP>(da, db, ep, M, N, Ktot, 1, st);
@@ -1194,7 +1206,9 @@ static int conv_fwd(const D& a, const float* w_krsc, int K, int Ktot, const floa
 }
 
 // Rows of BatchNorm partial statistics a *_fwd_ex_f32 call writes (one per output tile row).
-static int stats_rows(int M, int N, int Ktot) { return cdiv(M, kRowCfg[row_config(M, N, Ktot)].BM); }
+static int stats_rows(int M, int N, int Ktot, int kind = kRowPlain) {
+  return cdiv(M, kRowCfg[row_config(M, N, Ktot, kind)].BM);
+}
 
 // Forward with an optional input BatchNorm (bn_mean != NULL, see *_bnx_*) and optional output
 // statistics (stats != NULL: stats_rows x 2 x K doubles).
@@ -1438,6 +1452,9 @@ DK_API int dk_pwconv_dgrad_f32(const float* dy, int N, int OH, int OW, int K, co
 }
 
 DK_API int dk_pwconv_dgrad_stats_rows(int N, int OH, int OW, int K, int C) { return stats_rows(N * OH * OW, C, K); }
+DK_API int dk_pwconv_dgrad_bnbwd_stats_rows(int N, int OH, int OW, int K, int C) {
+  return stats_rows(N * OH * OW, C, K, kRowBnBwd);
+}
 
 // dgrad + the BN-backward partial sums of the BatchNorm whose output this layer consumed
 // (bn_x = that BN's raw input, on the dx grid; part: dk_pwconv_dgrad_stats_rows() x 2 x C).
@@ -1491,7 +1508,7 @@ DK_API int dk_pwconv_dgrad_ex_f32(const float* dy, int N, int OH, int OW, int K,
 // dk_bn_bwd_from_partials_f32.  dy_out (nullable) receives dy = the gradient w.r.t. bn_x,
 // bit-identical to dk_bn_bwd_apply_f32's, for this layer's weight gradient.  The epilogue
 // options (residual, the partials of the BN before this layer) are those of
-// dk_pwconv_dgrad_ex_f32 at stride 1.
+// dk_pwconv_dgrad_ex_f32 at stride 1; part has dk_pwconv_dgrad_bnbwd_stats_rows() rows.
 DK_API int dk_pwconv_dgrad_bnbwd_f32(const float* g, const float* bn_x, int N, int OH, int OW, int K,
                                      const float* out_mean, const float* out_invstd, const float* out_gamma,
                                      const float* out_beta, int out_relu, const float* k12, float* dy_out,
@@ -1515,7 +1532,7 @@ DK_API int dk_pwconv_dgrad_bnbwd_f32(const float* g, const float* bn_x, int N, i
     return DK_ERR_ARGS;
   if (!part) {
     EpStore ep = ep_store(dx, C, nullptr, residual);
-    return igemm_rows<LdMatKC, MatBwdDesc, LdMatIC, MatDesc, EpStore>(a, b, ep, M, C, K, st);
+    return igemm_rows<LdMatKC, MatBwdDesc, LdMatIC, MatDesc, EpStore, kRowBnBwd>(a, b, ep, M, C, K, st);
   }
   EpStoreBnBwd ep;
   static_cast<EpStore&>(ep) = ep_store(dx, C, nullptr, residual);
@@ -1523,7 +1540,7 @@ DK_API int dk_pwconv_dgrad_bnbwd_f32(const float* g, const float* bn_x, int N, i
   ep.part = part;
   ep.xbn = x;
   ep.bn = BnIn{bn_mean, bn_invstd, bn_gamma, bn_beta, bn_relu};
-  return igemm_rows<LdMatKC, MatBwdDesc, LdMatIC, MatDesc, EpStoreBnBwd>(a, b, ep, M, C, K, st);
+  return igemm_rows<LdMatKC, MatBwdDesc, LdMatIC, MatDesc, EpStoreBnBwd, kRowBnBwd>(a, b, ep, M, C, K, st);
 }
 
 DK_API size_t dk_pwconv_wgrad_workspace_bytes(int N, int OH, int OW, int K, int C) {

@@ -148,7 +148,7 @@ class PointwiseConvLayer(Layer):
         g = to_nhwc(bg.g)
         part = None
         if bn is not None:
-            rows = lib.dk_pwconv_dgrad_stats_rows(N, OH, OW, K, C)
+            rows = lib.dk_pwconv_dgrad_bnbwd_stats_rows(N, OH, OW, K, C)
             part = torch.empty((rows, 2, C), dtype=torch.float64, device=dx.device)
         lib.dk_pwconv_dgrad_bnbwd_f32(g.data_ptr(), bg.x.data_ptr(), N, OH, OW, K, *bg.bnbwd_args(),
                                       dy_out.data_ptr(), w.data_ptr(), C, dx.data_ptr(), ptr(res),

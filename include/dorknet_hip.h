@@ -135,6 +135,7 @@ int dk_dwconv_dgrad_ex_f32(const float* dy, int N, int OH, int OW, int C, const 
  * matching *_dgrad_ex_f32 (x / bn_* / part: the BN before this layer; residual addend).
  * (No depthwise form: that dgrad is HBM-bound, and forming dy on load costs it more than
  * the separate apply pass saves -- measured, DESIGN.md.) */
+int dk_pwconv_dgrad_bnbwd_stats_rows(int N, int OH, int OW, int K, int C);
 int dk_pwconv_dgrad_bnbwd_f32(const float* g, const float* bn_x, int N, int OH, int OW, int K, const float* out_mean, const float* out_invstd, const float* out_gamma, const float* out_beta, int out_relu, const float* k12, float* dy_out, const float* w_kc, int C, float* dx, const float* residual, const float* x, const float* bn_mean, const float* bn_invstd, const float* bn_gamma, const float* bn_beta, int bn_relu, double* part, void* stream);
 
 /* ---------------------------------------------------------------------------------------

@@ -386,7 +386,7 @@ def bwd_apply(xo, g, p, relu, k12):
                                                  (1, True, True, 16)])
 def test_pointwise_dgrad_bnbwd_bitwise(relu, bn_in, resid, K):
     """dk_pwconv_dgrad_bnbwd_f32 == dk_bn_bwd_apply_f32 -> dk_pwconv_dgrad_ex_f32, bitwise, for
-    dx, the written-through dy, and the input BN's partial sums."""
+    dx and the written-through dy; the input BN's partial sums to fp64 rounding (other tiles)."""
     rng = np.random.RandomState(relu + 2 * bn_in + 4 * resid + K)
     N, C, H, W = 3, 24, 13, 11
     xo = nhwc(rng.randn(N, K, H, W))        # this layer's output = the following BN's input
@@ -407,7 +407,8 @@ def test_pointwise_dgrad_bnbwd_bitwise(relu, bn_in, resid, K):
                                       res.data_ptr() if resid else 0, *bn_args, st) == 0
     dy1 = torch.full_like(g, float("nan"))
     dx1 = torch.empty_like(xin)
-    part1 = torch.zeros_like(part0)
+    part1 = torch.zeros((lib.dk_pwconv_dgrad_bnbwd_stats_rows(N, H, W, K, C), 2, C), dtype=torch.float64,
+                        device="cuda")
     bn_args = (xin.data_ptr(), *args(pi, 1), part1.data_ptr()) if bn_in else (0, 0, 0, 0, 0, 0, 0)
     assert lib.dk_pwconv_dgrad_bnbwd_f32(g.data_ptr(), xo.data_ptr(), N, H, W, K, *args(po, relu), k12.data_ptr(),
                                          dy1.data_ptr(), w.data_ptr(), C, dx1.data_ptr(),
@@ -415,7 +416,9 @@ def test_pointwise_dgrad_bnbwd_bitwise(relu, bn_in, resid, K):
     same(dy0, dy1)
     same(dx0, dx1)
     if bn_in:
-        same(part0, part1)
+        # its own column-tile width (row count): the per-tile partials fold to the same sums
+        s0, s1 = part0.sum(0), part1.sum(0)
+        assert float((s1 - s0).norm() / s0.norm()) < 1e-12
 
 
 @pytest.mark.parametrize("relu,bn_in,resid,C,need_dx", [(0, True, False, 64, True), (0, True, True, 32, True),
