@@ -145,26 +145,72 @@ __global__ void gap_bwd_kernel(const float* __restrict__ dy, int N, int HW, int 
 __global__ __launch_bounds__(1024) void softmax_xent_fwd_kernel(const float* __restrict__ x,
                                                                 const float* __restrict__ y, int B, int K,
                                                                 float* __restrict__ p, float* __restrict__ loss) {
-  // one wave per row (rows w, w + 16, ...); per-wave fp64 loss sums combined in a fixed order
+  // one wave per row (rows w, w + 16, ...); per-wave fp64 loss sums combined in a fixed order.
+  // K <= 128 (every model here): a wave loads RB rows (x and y) before computing any, so the
+  // 16 rows a wave owns cost B / (16 RB) load latencies instead of B / 16.
+  constexpr int RB = 8;
   __shared__ double red[16];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   double acc = 0.0;
-  for (int b = wv; b < B; b += 16) {
-    const float* xr = x + (size_t)b * K;
-    float* pr = p + (size_t)b * K;
-    float s = 0.f;
-    for (int j = lane; j < K; j += 64) s += expf(xr[j]);
-    s = wave_sum(s);
-    const float inv = 1.0f / s;
-    float dot = 0.f;
-    for (int j = lane; j < K; j += 64) {
-      const float v = inv * expf(xr[j]);
-      pr[j] = v;
-      if (y) dot += v * y[(size_t)b * K + j];
+  if (K <= 128) {
+    for (int b0 = wv * RB; b0 < B; b0 += 16 * RB) {
+      float xv[RB][2], yv[RB][2];
+#pragma unroll
+      for (int i = 0; i < RB; ++i) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int j = lane + 64 * h;
+          const bool in = b0 + i < B && j < K;
+          xv[i][h] = in ? x[(size_t)(b0 + i) * K + j] : 0.f;
+          yv[i][h] = in && y ? y[(size_t)(b0 + i) * K + j] : 0.f;
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < RB; ++i) {
+        if (b0 + i >= B) break;
+        const int b = b0 + i;
+        float e[2], s = 0.f;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          e[h] = lane + 64 * h < K ? expf(xv[i][h]) : 0.f;
+          s += e[h];
+        }
+        s = wave_sum(s);
+        const float inv = 1.0f / s;
+        float dot = 0.f;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int j = lane + 64 * h;
+          if (j < K) {
+            const float v = inv * e[h];
+            p[(size_t)b * K + j] = v;
+            dot += v * yv[i][h];
+          }
+        }
+        if (y) {
+          dot = wave_sum(dot);
+          acc += (double)(-logf(dot));
+        }
+      }
     }
-    if (y) {
-      dot = wave_sum(dot);
-      acc += (double)(-logf(dot));
+  } else {
+    for (int b = wv; b < B; b += 16) {
+      const float* xr = x + (size_t)b * K;
+      float* pr = p + (size_t)b * K;
+      float s = 0.f;
+      for (int j = lane; j < K; j += 64) s += expf(xr[j]);
+      s = wave_sum(s);
+      const float inv = 1.0f / s;
+      float dot = 0.f;
+      for (int j = lane; j < K; j += 64) {
+        const float v = inv * expf(xr[j]);
+        pr[j] = v;
+        if (y) dot += v * y[(size_t)b * K + j];
+      }
+      if (y) {
+        dot = wave_sum(dot);
+        acc += (double)(-logf(dot));
+      }
     }
   }
   if (lane == 0) red[wv] = acc;
@@ -194,12 +240,32 @@ struct SgdEntry {
   long long block0;  // first block index owned by this tensor
 };
 
+constexpr int kSgdLdsTable = 1024;
 __global__ __launch_bounds__(256) void sgd_momentum_multi_kernel(const SgdEntry* __restrict__ tab, int ntens,
                                                                  float lr, float mom, float gscale) {
-  // find the tensor owning this block (ntens ~ 100: linear scan of a cached table)
-  int t = 0;
+  // find the tensor owning this block: the block0 column is loaded into LDS in parallel (one
+  // load latency) and searched there; the old linear scan of the global table was ~100
+  // dependent loads for the last blocks.
+  __shared__ long long b0s[kSgdLdsTable];
+  __shared__ int owner;
   const long long b = blockIdx.x;
-  while (t + 1 < ntens && tab[t + 1].block0 <= b) ++t;
+  int t = 0;
+  if (ntens <= kSgdLdsTable) {
+    for (int i = threadIdx.x; i < ntens; i += blockDim.x) b0s[i] = tab[i].block0;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int lo = 0, hi = ntens - 1;  // last entry with block0 <= b
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (b0s[mid] <= b) lo = mid; else hi = mid - 1;
+      }
+      owner = lo;
+    }
+    __syncthreads();
+    t = owner;
+  } else {
+    while (t + 1 < ntens && tab[t + 1].block0 <= b) ++t;
+  }
   const SgdEntry e = tab[t];
   const long long i = (b - e.block0) * 256 + threadIdx.x;
   if (i >= e.n) return;
@@ -291,7 +357,15 @@ __global__ void colsum_partial_kernel(const float* __restrict__ in, int M, int N
   if (n >= N) return;
   const int r0 = blockIdx.y * rpc, r1 = min(M, r0 + rpc);
   double s = 0.0;
-  for (int r = r0; r < r1; ++r) s += (double)in[(size_t)r * N + n];
+  int r = r0;
+  for (; r + 8 <= r1; r += 8) {  // 8 loads in flight, added in row order
+    float v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = in[(size_t)(r + k) * N + n];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) s += (double)v[k];
+  }
+  for (; r < r1; ++r) s += (double)in[(size_t)r * N + n];
   ws[(size_t)blockIdx.y * N + n] = s;
 }
 
@@ -301,6 +375,19 @@ __global__ void colsum_final_kernel(const double* __restrict__ ws, int chunks, i
   double s = 0.0;
   for (int k = 0; k < chunks; ++k) s += ws[(size_t)k * N + n];
   out[n] = (float)s;
+}
+
+// NCHW -> NHWC with channel padding to 4 (C <= 4, the stem): thread = one pixel, C coalesced
+// plane reads (consecutive threads, consecutive w) and one 16-byte store.
+__global__ void nchw_to_nhwc4_kernel(const float* __restrict__ x, int N, int C, long long HW,
+                                     float* __restrict__ y) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long long)N * HW) return;
+  const long long n = i / HW, p = i - n * HW;
+  const float* xs = x + (size_t)n * C * HW + p;
+  f32x4 v = {0.f, 0.f, 0.f, 0.f};
+  for (int c = 0; c < C; ++c) v[c] = __builtin_nontemporal_load(xs + (size_t)c * HW);
+  st4(y + (size_t)i * 4, v);
 }
 
 // NCHW -> NHWC with channel padding to Cp (zeros).
@@ -337,7 +424,7 @@ __global__ __launch_bounds__(256) void scale_kernel(const float* __restrict__ x,
 }
 
 static int colsum_chunks(int M) {
-  int chunks = cdiv(M, 2048);
+  int chunks = cdiv(M, 64);
   if (chunks > 512) chunks = 512;
   if (chunks < 1) chunks = 1;
   return chunks;
@@ -484,6 +571,11 @@ DK_API int dk_colsum_f32(const float* in, int M, int N, float* out, void* ws, si
 }
 
 DK_API int dk_nchw_to_nhwc_f32(const float* x, int N, int C, int H, int W, int Cp, float* y, void* stream) {
+  if (Cp == 4 && C <= 4 && al16(y)) {
+    hipLaunchKernelGGL(nchw_to_nhwc4_kernel, grid1((long long)N * H * W), dim3(256), 0, as_stream(stream), x, N, C,
+                       (long long)H * W, y);
+    return launch_status();
+  }
   hipLaunchKernelGGL(nchw_to_nhwc_kernel, grid1((long long)N * H * W * Cp), dim3(256), 0, as_stream(stream), x, N, C, H,
                      W, Cp, y);
   return launch_status();

@@ -720,159 +720,188 @@ __global__ __launch_bounds__(64 * WM * WN) void igemm_f32(DA da, DB db, EP ep, i
   const int l32 = lane & 31, h = lane >> 5;
 
   const int tiles_n = (N + BN - 1) / BN;
-  const int bid = xcd_block(blockIdx.x, gridDim.x);  // neighbouring M-tiles share an XCD's L2
-  const int m0 = (bid / tiles_n) * BM;
-  const int n0 = (bid % tiles_n) * BN;
+  const int ntiles = ((M + BM - 1) / BM) * tiles_n;
+  // Persistent over output tiles: block b takes virtual tiles xcd_block(b) + i * gridDim.x
+  // (neighbouring M-tiles run on one XCD and share its L2).  With gridDim.x == ntiles this is
+  // one tile per block; with fewer blocks, the next tile's first k-tile is loaded into
+  // registers before this tile's epilogue, so its latency hides behind the stores.
+  int vt = xcd_block(blockIdx.x, gridDim.x);
   const int KT = (Ktot + BK - 1) / BK;
   const int kt0 = blockIdx.y * kt_per_split;
   const int kt1 = min(KT, kt0 + kt_per_split);
+  if (vt >= ntiles) return;
+  int m0 = (vt / tiles_n) * BM;
+  int n0 = (vt % tiles_n) * BN;
+  constexpr int NT = 64 * WM * WN;
 
-  f32x16 acc[TM][TN];
-#pragma unroll
-  for (int t = 0; t < TM; ++t)
-#pragma unroll
-    for (int u = 0; u < TN; ++u)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[t][u][r] = 0.f;
-
-  if (kt0 < kt1) {
-    LA la;
-    LB lb;
+  LA la;
+  LB lb;
+  const bool kwork = kt0 < kt1;
+  if (kwork) {
     la.init(da, m0, tid);
     lb.init(db, n0, tid);
     la.load(da, kt0 * BK, Ktot);  // first tile in flight before anything else
     lb.load(db, kt0 * BK, Ktot);
-    if constexpr (DA::kBnIn && LA::kTable) {
-      // BN-on-load parameter table for the A operand: {mean, invstd, gamma, beta} per channel
-      extern __shared__ f32x4 bn_tab[];
-      for (int c = tid; c < da.C; c += 64 * WM * WN)
-        bn_tab[c] = f32x4{da.bn.mean[c], da.bn.invstd[c], da.bn.gamma[c], da.bn.beta[c]};
-      la.tab = bn_tab;
-      __syncthreads();
-    }
-    if constexpr (DA::kBnBwd) {
-      // BN-backward-on-load table for the A operand (channel = k)
-      extern __shared__ f32x4 bwd_tab[];
-      const BnBwdIn& b = da.bwd;
-      for (int c = tid; c < b.C; c += 64 * WM * WN) {
-        const float ga = b.gamma[c], is = b.invstd[c];
-        bwd_tab[2 * c] = f32x4{b.mean[c], is, ga, b.beta[c]};
-        bwd_tab[2 * c + 1] = f32x4{b.k12[c], b.k12[b.C + c], ga * is, 0.f};
-      }
-      la.tab = bwd_tab;
-      la.dyo = da.dy_out;
-      la.writer = da.dy_out != nullptr && n0 == 0;
-      la.relu_flag = b.relu;
-      __syncthreads();
-    }
-    la.template store<DA>(As);
-    lb.template store<DB>(Bs);
+  }
+  if constexpr (DA::kBnIn && LA::kTable) {
+    // BN-on-load parameter table for the A operand: {mean, invstd, gamma, beta} per channel
+    extern __shared__ f32x4 bn_tab[];
+    for (int c = tid; c < da.C; c += NT)
+      bn_tab[c] = f32x4{da.bn.mean[c], da.bn.invstd[c], da.bn.gamma[c], da.bn.beta[c]};
+    la.tab = bn_tab;
     __syncthreads();
-    int cur = 0;
-    const int arow = wm * 32 * TM + l32;
-    const int brow = wn * 32 * TN + l32;
-    for (int kt = kt0; kt < kt1; ++kt) {
-      const bool more = kt + 1 < kt1;
-      if (more) {
-        la.load(da, (kt + 1) * BK, Ktot);
-        lb.load(db, (kt + 1) * BK, Ktot);
+  }
+  if constexpr (DA::kBnBwd) {
+    // BN-backward-on-load table for the A operand (channel = k)
+    extern __shared__ f32x4 bwd_tab[];
+    const BnBwdIn& b = da.bwd;
+    for (int c = tid; c < b.C; c += NT) {
+      const float ga = b.gamma[c], is = b.invstd[c];
+      bwd_tab[2 * c] = f32x4{b.mean[c], is, ga, b.beta[c]};
+      bwd_tab[2 * c + 1] = f32x4{b.k12[c], b.k12[b.C + c], ga * is, 0.f};
+    }
+    la.tab = bwd_tab;
+    la.dyo = da.dy_out;
+    la.relu_flag = b.relu;
+    __syncthreads();
+  }
+
+  while (true) {
+    if constexpr (DA::kBnBwd) la.writer = da.dy_out != nullptr && n0 == 0;
+    f32x16 acc[TM][TN];
+#pragma unroll
+    for (int t = 0; t < TM; ++t)
+#pragma unroll
+      for (int u = 0; u < TN; ++u)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[t][u][r] = 0.f;
+
+    if (kwork) {
+      la.template store<DA>(As);
+      lb.template store<DB>(Bs);
+      __syncthreads();
+      int cur = 0;
+      const int arow = wm * 32 * TM + l32;
+      const int brow = wn * 32 * TN + l32;
+      for (int kt = kt0; kt < kt1; ++kt) {
+        const bool more = kt + 1 < kt1;
+        if (more) {
+          la.load(da, (kt + 1) * BK, Ktot);
+          lb.load(db, (kt + 1) * BK, Ktot);
+        }
+        const float* A_t = As + cur * ABUF;
+        const float* B_t = Bs + cur * BBUF;
+#pragma unroll
+        for (int q = 0; q < BK / 8; ++q) {
+          f32x4 af[TM], bf[TN];
+#pragma unroll
+          for (int t = 0; t < TM; ++t) af[t] = LA::frag(A_t, arow + 32 * t, q, h);
+#pragma unroll
+          for (int u = 0; u < TN; ++u) bf[u] = LB::frag(B_t, brow + 32 * u, q, h);
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+#pragma unroll
+            for (int t = 0; t < TM; ++t)
+#pragma unroll
+              for (int u = 0; u < TN; ++u)
+                acc[t][u] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[t][e], bf[u][e], acc[t][u], 0, 0, 0);
+        }
+        if (more) {
+          la.template store<DA>(As + (cur ^ 1) * ABUF);
+          lb.template store<DB>(Bs + (cur ^ 1) * BBUF);
+        }
+        __syncthreads();
+        cur ^= 1;
       }
-      const float* A_t = As + cur * ABUF;
-      const float* B_t = Bs + cur * BBUF;
+    }
+
+    // next tile: its first k-tile goes into registers now and lands in LDS after the epilogue
+    const int vn = vt + (int)gridDim.x;
+    const bool next = vn < ntiles;
+    const int m0n = next ? (vn / tiles_n) * BM : 0;
+    const int n0n = next ? (vn % tiles_n) * BN : 0;
+    if (next && kwork) {
+      la.init(da, m0n, tid);
+      lb.init(db, n0n, tid);
+      la.load(da, kt0 * BK, Ktot);
+      lb.load(db, kt0 * BK, Ktot);
+    }
+
+    // Epilogue: the accumulator tile goes through LDS ([BM][BN+8]; the +8 puts the two lane
+    // halves' rows 4 apart on opposite bank halves) so that each thread stores 16-byte row
+    // chunks -- 4x fewer store instructions than storing the MFMA C layout directly.
+    constexpr int LDT = BN + 8;
+    constexpr int NC4 = BN / 4;
+    constexpr int RSTEP = NT / NC4;
+    static_assert(NT % NC4 == 0, "epilogue thread map");
+    __syncthreads();  // the MFMA loop's last LDS reads are done
 #pragma unroll
-      for (int q = 0; q < BK / 8; ++q) {
-        f32x4 af[TM], bf[TN];
+    for (int t = 0; t < TM; ++t)
 #pragma unroll
-        for (int t = 0; t < TM; ++t) af[t] = LA::frag(A_t, arow + 32 * t, q, h);
+      for (int u = 0; u < TN; ++u)
 #pragma unroll
-        for (int u = 0; u < TN; ++u) bf[u] = LB::frag(B_t, brow + 32 * u, q, h);
+        for (int r = 0; r < 16; ++r)
+          smem[(wm * 32 * TM + t * 32 + (r & 3) + 8 * (r >> 2) + 4 * h) * LDT + wn * 32 * TN + u * 32 + l32] =
+              acc[t][u][r];
+    __syncthreads();
+    const int c4 = tid % NC4, rl0 = tid / NC4;
+    const int col = n0 + 4 * c4;
+    const bool full = ep.v4 && col + 3 < N;
+    double sa[4] = {0.0, 0.0, 0.0, 0.0}, sb[4] = {0.0, 0.0, 0.0, 0.0};
+    constexpr int RPT = BM / RSTEP;  // rows per thread
+    static_assert(BM % RSTEP == 0, "epilogue rows");
+    if (full) {
+      typename EP::Pre pre[RPT];
+#pragma unroll
+      for (int i = 0; i < RPT; ++i) {
+        const int row = m0 + rl0 + i * RSTEP;
+        if (row < M) pre[i] = ep.pre4(row, col);
+      }
+#pragma unroll
+      for (int i = 0; i < RPT; ++i) {
+        const int rl = rl0 + i * RSTEP;
+        if (m0 + rl < M) ep.put4(m0 + rl, col, ld4(smem + rl * LDT + 4 * c4), pre[i], blockIdx.y, sa, sb);
+      }
+    } else {
+      for (int rl = rl0; rl < BM; rl += RSTEP) {
+        const int row = m0 + rl;
+        if (row >= M) break;
+        const f32x4 v = ld4(smem + rl * LDT + 4 * c4);
 #pragma unroll
         for (int e = 0; e < 4; ++e)
-#pragma unroll
-          for (int t = 0; t < TM; ++t)
-#pragma unroll
-            for (int u = 0; u < TN; ++u)
-              acc[t][u] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[t][e], bf[u][e], acc[t][u], 0, 0, 0);
+          if (col + e < N) ep.put1(row, col + e, v[e], blockIdx.y, sa[e], sb[e]);
       }
-      if (more) {
-        la.template store<DA>(As + (cur ^ 1) * ABUF);
-        lb.template store<DB>(Bs + (cur ^ 1) * BBUF);
+    }
+
+    if constexpr (EP::kColStats) {
+      // per-column fp64 sums of this tile, fixed order: the thread's rows, then the RSTEP
+      // threads sharing its column chunk -> part[m_tile][.][col]
+      __syncthreads();  // done reading the staged tile
+      double* red = reinterpret_cast<double*>(smem);  // [RSTEP][BN][2]
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        red[(rl0 * BN + 4 * c4 + e) * 2 + 0] = sa[e];
+        red[(rl0 * BN + 4 * c4 + e) * 2 + 1] = sb[e];
       }
       __syncthreads();
-      cur ^= 1;
-    }
-  }
-
-  // Epilogue: the accumulator tile goes through LDS ([BM][BN+8]; the +8 puts the two lane
-  // halves' rows 4 apart on opposite bank halves) so that each thread stores 16-byte row
-  // chunks -- 4x fewer store instructions than storing the MFMA C layout directly.
-  constexpr int NT = 64 * WM * WN;
-  constexpr int LDT = BN + 8;
-  constexpr int NC4 = BN / 4;
-  constexpr int RSTEP = NT / NC4;
-  static_assert(NT % NC4 == 0, "epilogue thread map");
-  __syncthreads();  // the MFMA loop's last LDS reads are done
-#pragma unroll
-  for (int t = 0; t < TM; ++t)
-#pragma unroll
-    for (int u = 0; u < TN; ++u)
-#pragma unroll
-      for (int r = 0; r < 16; ++r)
-        smem[(wm * 32 * TM + t * 32 + (r & 3) + 8 * (r >> 2) + 4 * h) * LDT + wn * 32 * TN + u * 32 + l32] =
-            acc[t][u][r];
-  __syncthreads();
-  const int c4 = tid % NC4, rl0 = tid / NC4;
-  const int col = n0 + 4 * c4;
-  const bool full = ep.v4 && col + 3 < N;
-  double sa[4] = {0.0, 0.0, 0.0, 0.0}, sb[4] = {0.0, 0.0, 0.0, 0.0};
-  constexpr int RPT = BM / RSTEP;  // rows per thread
-  static_assert(BM % RSTEP == 0, "epilogue rows");
-  if (full) {
-    typename EP::Pre pre[RPT];
-#pragma unroll
-    for (int i = 0; i < RPT; ++i) {
-      const int row = m0 + rl0 + i * RSTEP;
-      if (row < M) pre[i] = ep.pre4(row, col);
-    }
-#pragma unroll
-    for (int i = 0; i < RPT; ++i) {
-      const int rl = rl0 + i * RSTEP;
-      if (m0 + rl < M) ep.put4(m0 + rl, col, ld4(smem + rl * LDT + 4 * c4), pre[i], blockIdx.y, sa, sb);
-    }
-  } else {
-    for (int rl = rl0; rl < BM; rl += RSTEP) {
-      const int row = m0 + rl;
-      if (row >= M) break;
-      const f32x4 v = ld4(smem + rl * LDT + 4 * c4);
-#pragma unroll
-      for (int e = 0; e < 4; ++e)
-        if (col + e < N) ep.put1(row, col + e, v[e], blockIdx.y, sa[e], sb[e]);
-    }
-  }
-
-  if constexpr (EP::kColStats) {
-    // per-column fp64 sums of this tile, fixed order: the thread's rows, then the RSTEP
-    // threads sharing its column chunk -> part[m_tile][.][col]
-    __syncthreads();  // done reading the staged tile
-    double* red = reinterpret_cast<double*>(smem);  // [RSTEP][BN][2]
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      red[(rl0 * BN + 4 * c4 + e) * 2 + 0] = sa[e];
-      red[(rl0 * BN + 4 * c4 + e) * 2 + 1] = sb[e];
-    }
-    __syncthreads();
-    const int mt = bid / tiles_n;
-    for (int i = tid; i < BN; i += NT) {
-      const int cc = n0 + i;
-      if (cc >= N) continue;
-      double s1 = 0.0, s2 = 0.0;
-      for (int k = 0; k < RSTEP; ++k) {
-        s1 += red[(k * BN + i) * 2 + 0];
-        s2 += red[(k * BN + i) * 2 + 1];
+      const int mt = vt / tiles_n;
+      for (int i = tid; i < BN; i += NT) {
+        const int cc = n0 + i;
+        if (cc >= N) continue;
+        double s1 = 0.0, s2 = 0.0;
+        for (int k = 0; k < RSTEP; ++k) {
+          s1 += red[(k * BN + i) * 2 + 0];
+          s2 += red[(k * BN + i) * 2 + 1];
+        }
+        ep.part[((size_t)mt * 2 + 0) * N + cc] = s1;
+        ep.part[((size_t)mt * 2 + 1) * N + cc] = s2;
       }
-      ep.part[((size_t)mt * 2 + 0) * N + cc] = s1;
-      ep.part[((size_t)mt * 2 + 1) * N + cc] = s2;
     }
+    if (!next) break;
+    __syncthreads();  // the epilogue is done with the LDS before the next tile's operands land
+    vt = vn;
+    m0 = m0n;
+    n0 = n0n;
   }
 }
 
@@ -939,6 +968,12 @@ static const int kNumRowCfg = sizeof(kRowCfg) / sizeof(kRowCfg[0]);
 static const int kNumSplitCfg = sizeof(kSplitCfg) / sizeof(kSplitCfg[0]);
 
 static int g_cfg_override[2] = {-1, -1};  // tuning knob only (see header)
+// Persistent row GEMMs: grid = min(tiles, g_persist x resident blocks per CU x CUs); 0 = one
+// block per tile.  Tuning knob: dk_debug_set_gemm_config(2, v).  Measured on the ResNet step
+// (scripts/ab_step.py): 11.77 ms/step with one block per tile, 11.89 / 11.98 with 1 / 2
+// resident waves of persistent blocks, so the default is off.
+static int g_persist = 0;
+constexpr int kNumCUs = 256;  // MI355X
 
 template <int BM, int BN, int BK, int WM, int WN, template <int, int, int> class LA, class DA,
           template <int, int, int> class LB, class DB, class EP>
@@ -964,7 +999,22 @@ static int launch_igemm(const DA& da, const DB& db, const EP& ep, int M, int N, 
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&igemm_f32<BM, BN, BK, WM, WN, A, DA, B, DB, EP>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn);
   }
-  hipLaunchKernelGGL((igemm_f32<BM, BN, BK, WM, WN, A, DA, B, DB, EP>), dim3(tiles, splits), dim3(NT), dyn, st, da,
+  int gx = tiles;
+  if (splits == 1 && g_persist) {
+    // persistent row problems: one resident wave of blocks (occupancy per CU x 256 CUs)
+    static int occ = -1;  // per kernel instantiation; immutable after the first launch
+    if (occ < 0) {
+      int o = 0;
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
+              &o, reinterpret_cast<const void*>(&igemm_f32<BM, BN, BK, WM, WN, A, DA, B, DB, EP>), NT, dyn) !=
+              hipSuccess || o < 1)
+        o = 1;
+      occ = o;
+    }
+    const int cap = occ * kNumCUs * g_persist;
+    if (gx > cap) gx = cap;
+  }
+  hipLaunchKernelGGL((igemm_f32<BM, BN, BK, WM, WN, A, DA, B, DB, EP>), dim3(gx, splits), dim3(NT), dyn, st, da,
                      db, ep, M, N, Ktot, kps);
   return launch_status();
 }
@@ -1007,10 +1057,11 @@ static int igemm_rows(const DA& da, const DB& db, const EP& ep, int M, int N, in
 // Reduction-heavy problems (wgrad): split K over enough blocks to fill the chip.
 static int splitk_config(int M, int N, int Kred) {
   if (g_cfg_override[1] >= 0) return g_cfg_override[1];
-  (void)M;
-  (void)N;
   (void)Kred;
-  return 1;  // 64x64x32: best or within 3% of best on every measured wgrad shape
+  // One column tile for 64 < N <= 128 (the stem: N = R*S*Cp = 100): the A operand -- for the
+  // stem the BN-backward-on-load dy, formed from 2 x 822 MB -- is then streamed once, not twice.
+  if (M <= 64 && N > 64 && N <= 128) return 6;  // 64x128x32
+  return 1;  // 64x64x32: best or within 3% of best on every other measured wgrad shape
 }
 
 static int wgrad_splits(int M, int N, int Kred, const TileCfg& c) {
@@ -1154,6 +1205,10 @@ using namespace dk;
 // Tuning knob: kind 0 = row problems (fwd/dgrad), 1 = split-K (wgrad); cfg -1 = heuristic.
 // Returns the number of configurations of that kind.  Not thread-safe; for tuning runs.
 DK_API int dk_debug_set_gemm_config(int kind, int cfg) {
+  if (kind == 2) {
+    g_persist = cfg < 0 ? 0 : cfg;
+    return 0;
+  }
   if (kind < 0 || kind > 1) return -1;
   g_cfg_override[kind] = cfg;
   return kind == 0 ? kNumRowCfg : kNumSplitCfg;

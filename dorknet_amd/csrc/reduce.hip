@@ -55,9 +55,89 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
   out[o] = v;
 }
 
+// Float4-column variant: thread (j, q) owns 4 adjacent columns (one 16-byte load per row) and
+// sums rows q, q + TPO, ...; a wave reads 64 / CG rows of CG * 16 contiguous bytes, so the
+// slab streams at full line width.  Four rows are loaded before they are added (same order).
+template <int CG, int TPO>
+__global__ __launch_bounds__(CG* TPO) void splitk_reduce4_kernel(const float* __restrict__ ws, int splits, int M,
+                                                                  int N, float* __restrict__ out,
+                                                                  const float* __restrict__ w, float l2, int mode,
+                                                                  int C, int Cp, int R, int S) {
+  __shared__ double red[TPO][CG][4];
+  const int j = threadIdx.x % CG;
+  const int q = threadIdx.x / CG;
+  const long long total = (long long)M * N;
+  const long long idx = ((long long)blockIdx.x * CG + j) * 4;
+  double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+  if (idx < total) {
+    const float* p = ws + idx;
+    int s = q;
+    for (; s + 3 * TPO < splits; s += 4 * TPO) {
+      f32x4 v[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) v[k] = ld4(p + (size_t)(s + k * TPO) * total);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        a0 += (double)v[k].x;
+        a1 += (double)v[k].y;
+        a2 += (double)v[k].z;
+        a3 += (double)v[k].w;
+      }
+    }
+    for (; s < splits; s += TPO) {
+      const f32x4 v = ld4(p + (size_t)s * total);
+      a0 += (double)v.x;
+      a1 += (double)v.y;
+      a2 += (double)v.z;
+      a3 += (double)v.w;
+    }
+  }
+  red[q][j][0] = a0;
+  red[q][j][1] = a1;
+  red[q][j][2] = a2;
+  red[q][j][3] = a3;
+  __syncthreads();
+  // 4 * CG results per block, finalized in a fixed order over the TPO lane sums
+  for (int t = threadIdx.x; t < 4 * CG; t += CG * TPO) {
+    const int jj = t >> 2, e = t & 3;
+    const long long o_idx = ((long long)blockIdx.x * CG + jj) * 4 + e;
+    if (o_idx >= total) break;
+    double sum = 0.0;
+#pragma unroll 8
+    for (int k = 0; k < TPO; ++k) sum += red[k][jj][e];
+    const int m = (int)(o_idx / N), n = (int)(o_idx - (long long)m * N);
+    size_t o;
+    if (mode == 0) {
+      o = (size_t)o_idx;
+    } else {
+      const int tap = n / Cp;
+      const int c = n - tap * Cp;
+      if (c >= C) continue;
+      const int r = tap / S, s2 = tap - r * S;
+      o = (((size_t)m * C + c) * R + r) * S + s2;
+    }
+    float v = (float)sum;
+    if (w) v = v + l2 * w[o];
+    out[o] = v;
+  }
+}
+
 int splitk_reduce(const float* ws, int splits, int M, int N, float* out, const float* w, float l2, int mode, int C,
                   int Cp, int R, int S, hipStream_t st) {
   const long long total = (long long)M * N;
+  if ((total & 3) == 0 && (reinterpret_cast<uintptr_t>(ws) & 15) == 0) {
+    if (splits >= 256) {
+      hipLaunchKernelGGL((splitk_reduce4_kernel<16, 64>), dim3((unsigned)cdivll(total, 64)), dim3(1024), 0, st, ws,
+                         splits, M, N, out, w, l2, mode, C, Cp, R, S);
+    } else if (splits >= 32) {
+      hipLaunchKernelGGL((splitk_reduce4_kernel<16, 16>), dim3((unsigned)cdivll(total, 64)), dim3(256), 0, st, ws,
+                         splits, M, N, out, w, l2, mode, C, Cp, R, S);
+    } else {
+      hipLaunchKernelGGL((splitk_reduce4_kernel<64, 4>), dim3((unsigned)cdivll(total, 256)), dim3(256), 0, st, ws,
+                         splits, M, N, out, w, l2, mode, C, Cp, R, S);
+    }
+    return launch_status();
+  }
   if (splits >= 512) {
     // long slabs (one row per block of a fused backward): 64 lanes per column
     constexpr int TPO = 64, CPB = 256 / TPO;

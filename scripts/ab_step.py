@@ -1,0 +1,61 @@
+"""A/B timing of the ResNet-18-depsep training step (bs=256) under C-ABI tuning knobs.
+
+    python scripts/ab_step.py --knob 2:0 --knob 2:1 --knob 2:2     # dk_debug_set_gemm_config(kind, cfg)
+Each setting is timed `--rounds` times interleaved (median ms per step reported).
+"""
+import argparse
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--knob", action="append", default=[], help="kind:cfg for dk_debug_set_gemm_config")
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=256)
+    args = ap.parse_args()
+    from examples.resnet18_depsep import ResNet18, synthetic_batch
+    from dorknet_amd._tensor import as_device
+    from dorknet_amd._hip import lib
+    from dorknet_amd.optimisers.SGDMomentum import SGDMomentum
+    torch.cuda.set_device(0)
+    np.random.seed(0)
+    net = ResNet18("r")
+    net.to_gpu()
+    sgd = SGDMomentum(net, 0.05 * args.batch / 200.0, 0.9)
+    X, _, onehot = synthetic_batch(args.batch, seed=1000)
+    X, onehot = as_device(X), as_device(onehot)
+
+    def step():
+        net.forward(X, onehot)
+        net.backward()
+        sgd.update_weights()
+
+    knobs = [tuple(int(v) for v in k.split(":")) for k in args.knob] or [(2, -1)]
+    res = {k: [] for k in knobs}
+    for _ in range(args.rounds):
+        for k in knobs:
+            lib.dk_debug_set_gemm_config(*k)
+            for _ in range(2):
+                step()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(args.steps):
+                step()
+            torch.cuda.synchronize()
+            res[k].append(1e3 * (time.perf_counter() - t0) / args.steps)
+            lib.dk_debug_set_gemm_config(k[0], -1)
+    for k, v in res.items():
+        print(f"knob {k[0]}:{k[1]:3d}  {np.median(v):7.3f} ms/step  ({', '.join(f'{x:.3f}' for x in v)})  "
+              f"{args.batch / np.median(v) * 1e3:9.1f} img/s", flush=True)
+
+
+if __name__ == "__main__":
+    main()
