@@ -20,6 +20,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import re
 import os
 import sys
 import time
@@ -127,8 +128,10 @@ ENTRY_KERNEL = {
     "dk_bn_add_f32": "dk::bn_add_kernel",
     "dk_relu_bwd_f32": "dk::relu_bwd_kernel",
     "dk_relu_bwd_bn_partial_f64": "dk::bn_bwd_partial_kernel",
-    # (prefix, substring): the GEMM instantiations whose A operand applies a BN backward
-    "dk_pwconv_dgrad_bnbwd_f32": ("dk::igemm_f32", "dk::MatBwdDesc"),
+    # (prefix, regex): the GEMM instantiations whose A operand is the K-contiguous matrix
+    # loader applying a BN backward (dgrad); the stem's weight gradient applies one on its
+    # row-contiguous loader (LdMatICT) and is a different entry point
+    "dk_pwconv_dgrad_bnbwd_f32": ("dk::igemm_f32", r"dk::LdMatKCT<[^>]*>, dk::MatBwdDesc"),
 }
 
 
@@ -147,7 +150,7 @@ def pmc_traffic(entry, path):
     n = t = 0
     pre, sub = kern if isinstance(kern, tuple) else (kern, "")
     for name, v in d.get("kernels", {}).items():
-        if (name.startswith(pre + "<") or name == pre) and sub in name:
+        if (name.startswith(pre + "<") or name == pre) and re.search(sub, name):
             n += v["dispatches"]
             t += v["traffic_bytes"] * v["dispatches"]
     if n == 0:

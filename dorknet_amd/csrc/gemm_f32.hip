@@ -720,188 +720,159 @@ __global__ __launch_bounds__(64 * WM * WN) void igemm_f32(DA da, DB db, EP ep, i
   const int l32 = lane & 31, h = lane >> 5;
 
   const int tiles_n = (N + BN - 1) / BN;
-  const int ntiles = ((M + BM - 1) / BM) * tiles_n;
-  // Persistent over output tiles: block b takes virtual tiles xcd_block(b) + i * gridDim.x
-  // (neighbouring M-tiles run on one XCD and share its L2).  With gridDim.x == ntiles this is
-  // one tile per block; with fewer blocks, the next tile's first k-tile is loaded into
-  // registers before this tile's epilogue, so its latency hides behind the stores.
-  int vt = xcd_block(blockIdx.x, gridDim.x);
+  const int bid = xcd_block(blockIdx.x, gridDim.x);  // neighbouring M-tiles share an XCD's L2
+  const int m0 = (bid / tiles_n) * BM;
+  const int n0 = (bid % tiles_n) * BN;
   const int KT = (Ktot + BK - 1) / BK;
   const int kt0 = blockIdx.y * kt_per_split;
   const int kt1 = min(KT, kt0 + kt_per_split);
-  if (vt >= ntiles) return;
-  int m0 = (vt / tiles_n) * BM;
-  int n0 = (vt % tiles_n) * BN;
-  constexpr int NT = 64 * WM * WN;
 
-  LA la;
-  LB lb;
-  const bool kwork = kt0 < kt1;
-  if (kwork) {
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int t = 0; t < TM; ++t)
+#pragma unroll
+    for (int u = 0; u < TN; ++u)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[t][u][r] = 0.f;
+
+  if (kt0 < kt1) {
+    LA la;
+    LB lb;
     la.init(da, m0, tid);
     lb.init(db, n0, tid);
     la.load(da, kt0 * BK, Ktot);  // first tile in flight before anything else
     lb.load(db, kt0 * BK, Ktot);
-  }
-  if constexpr (DA::kBnIn && LA::kTable) {
-    // BN-on-load parameter table for the A operand: {mean, invstd, gamma, beta} per channel
-    extern __shared__ f32x4 bn_tab[];
-    for (int c = tid; c < da.C; c += NT)
-      bn_tab[c] = f32x4{da.bn.mean[c], da.bn.invstd[c], da.bn.gamma[c], da.bn.beta[c]};
-    la.tab = bn_tab;
-    __syncthreads();
-  }
-  if constexpr (DA::kBnBwd) {
-    // BN-backward-on-load table for the A operand (channel = k)
-    extern __shared__ f32x4 bwd_tab[];
-    const BnBwdIn& b = da.bwd;
-    for (int c = tid; c < b.C; c += NT) {
-      const float ga = b.gamma[c], is = b.invstd[c];
-      bwd_tab[2 * c] = f32x4{b.mean[c], is, ga, b.beta[c]};
-      bwd_tab[2 * c + 1] = f32x4{b.k12[c], b.k12[b.C + c], ga * is, 0.f};
-    }
-    la.tab = bwd_tab;
-    la.dyo = da.dy_out;
-    la.relu_flag = b.relu;
-    __syncthreads();
-  }
-
-  while (true) {
-    if constexpr (DA::kBnBwd) la.writer = da.dy_out != nullptr && n0 == 0;
-    f32x16 acc[TM][TN];
-#pragma unroll
-    for (int t = 0; t < TM; ++t)
-#pragma unroll
-      for (int u = 0; u < TN; ++u)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[t][u][r] = 0.f;
-
-    if (kwork) {
-      la.template store<DA>(As);
-      lb.template store<DB>(Bs);
+    if constexpr (DA::kBnIn && LA::kTable) {
+      // BN-on-load parameter table for the A operand: {mean, invstd, gamma, beta} per channel
+      extern __shared__ f32x4 bn_tab[];
+      for (int c = tid; c < da.C; c += 64 * WM * WN)
+        bn_tab[c] = f32x4{da.bn.mean[c], da.bn.invstd[c], da.bn.gamma[c], da.bn.beta[c]};
+      la.tab = bn_tab;
       __syncthreads();
-      int cur = 0;
-      const int arow = wm * 32 * TM + l32;
-      const int brow = wn * 32 * TN + l32;
-      for (int kt = kt0; kt < kt1; ++kt) {
-        const bool more = kt + 1 < kt1;
-        if (more) {
-          la.load(da, (kt + 1) * BK, Ktot);
-          lb.load(db, (kt + 1) * BK, Ktot);
-        }
-        const float* A_t = As + cur * ABUF;
-        const float* B_t = Bs + cur * BBUF;
-#pragma unroll
-        for (int q = 0; q < BK / 8; ++q) {
-          f32x4 af[TM], bf[TN];
-#pragma unroll
-          for (int t = 0; t < TM; ++t) af[t] = LA::frag(A_t, arow + 32 * t, q, h);
-#pragma unroll
-          for (int u = 0; u < TN; ++u) bf[u] = LB::frag(B_t, brow + 32 * u, q, h);
-#pragma unroll
-          for (int e = 0; e < 4; ++e)
-#pragma unroll
-            for (int t = 0; t < TM; ++t)
-#pragma unroll
-              for (int u = 0; u < TN; ++u)
-                acc[t][u] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[t][e], bf[u][e], acc[t][u], 0, 0, 0);
-        }
-        if (more) {
-          la.template store<DA>(As + (cur ^ 1) * ABUF);
-          lb.template store<DB>(Bs + (cur ^ 1) * BBUF);
-        }
-        __syncthreads();
-        cur ^= 1;
+    }
+    if constexpr (DA::kBnBwd) {
+      // BN-backward-on-load table for the A operand (channel = k)
+      extern __shared__ f32x4 bwd_tab[];
+      const BnBwdIn& b = da.bwd;
+      for (int c = tid; c < b.C; c += 64 * WM * WN) {
+        const float ga = b.gamma[c], is = b.invstd[c];
+        bwd_tab[2 * c] = f32x4{b.mean[c], is, ga, b.beta[c]};
+        bwd_tab[2 * c + 1] = f32x4{b.k12[c], b.k12[b.C + c], ga * is, 0.f};
       }
+      la.tab = bwd_tab;
+      la.dyo = da.dy_out;
+      la.writer = da.dy_out != nullptr && n0 == 0;
+      la.relu_flag = b.relu;
+      __syncthreads();
     }
-
-    // next tile: its first k-tile goes into registers now and lands in LDS after the epilogue
-    const int vn = vt + (int)gridDim.x;
-    const bool next = vn < ntiles;
-    const int m0n = next ? (vn / tiles_n) * BM : 0;
-    const int n0n = next ? (vn % tiles_n) * BN : 0;
-    if (next && kwork) {
-      la.init(da, m0n, tid);
-      lb.init(db, n0n, tid);
-      la.load(da, kt0 * BK, Ktot);
-      lb.load(db, kt0 * BK, Ktot);
-    }
-
-    // Epilogue: the accumulator tile goes through LDS ([BM][BN+8]; the +8 puts the two lane
-    // halves' rows 4 apart on opposite bank halves) so that each thread stores 16-byte row
-    // chunks -- 4x fewer store instructions than storing the MFMA C layout directly.
-    constexpr int LDT = BN + 8;
-    constexpr int NC4 = BN / 4;
-    constexpr int RSTEP = NT / NC4;
-    static_assert(NT % NC4 == 0, "epilogue thread map");
-    __syncthreads();  // the MFMA loop's last LDS reads are done
-#pragma unroll
-    for (int t = 0; t < TM; ++t)
-#pragma unroll
-      for (int u = 0; u < TN; ++u)
-#pragma unroll
-        for (int r = 0; r < 16; ++r)
-          smem[(wm * 32 * TM + t * 32 + (r & 3) + 8 * (r >> 2) + 4 * h) * LDT + wn * 32 * TN + u * 32 + l32] =
-              acc[t][u][r];
+    la.template store<DA>(As);
+    lb.template store<DB>(Bs);
     __syncthreads();
-    const int c4 = tid % NC4, rl0 = tid / NC4;
-    const int col = n0 + 4 * c4;
-    const bool full = ep.v4 && col + 3 < N;
-    double sa[4] = {0.0, 0.0, 0.0, 0.0}, sb[4] = {0.0, 0.0, 0.0, 0.0};
-    constexpr int RPT = BM / RSTEP;  // rows per thread
-    static_assert(BM % RSTEP == 0, "epilogue rows");
-    if (full) {
-      typename EP::Pre pre[RPT];
-#pragma unroll
-      for (int i = 0; i < RPT; ++i) {
-        const int row = m0 + rl0 + i * RSTEP;
-        if (row < M) pre[i] = ep.pre4(row, col);
+    int cur = 0;
+    const int arow = wm * 32 * TM + l32;
+    const int brow = wn * 32 * TN + l32;
+    for (int kt = kt0; kt < kt1; ++kt) {
+      const bool more = kt + 1 < kt1;
+      if (more) {
+        la.load(da, (kt + 1) * BK, Ktot);
+        lb.load(db, (kt + 1) * BK, Ktot);
       }
+      const float* A_t = As + cur * ABUF;
+      const float* B_t = Bs + cur * BBUF;
 #pragma unroll
-      for (int i = 0; i < RPT; ++i) {
-        const int rl = rl0 + i * RSTEP;
-        if (m0 + rl < M) ep.put4(m0 + rl, col, ld4(smem + rl * LDT + 4 * c4), pre[i], blockIdx.y, sa, sb);
-      }
-    } else {
-      for (int rl = rl0; rl < BM; rl += RSTEP) {
-        const int row = m0 + rl;
-        if (row >= M) break;
-        const f32x4 v = ld4(smem + rl * LDT + 4 * c4);
+      for (int q = 0; q < BK / 8; ++q) {
+        f32x4 af[TM], bf[TN];
+#pragma unroll
+        for (int t = 0; t < TM; ++t) af[t] = LA::frag(A_t, arow + 32 * t, q, h);
+#pragma unroll
+        for (int u = 0; u < TN; ++u) bf[u] = LB::frag(B_t, brow + 32 * u, q, h);
 #pragma unroll
         for (int e = 0; e < 4; ++e)
-          if (col + e < N) ep.put1(row, col + e, v[e], blockIdx.y, sa[e], sb[e]);
-      }
-    }
-
-    if constexpr (EP::kColStats) {
-      // per-column fp64 sums of this tile, fixed order: the thread's rows, then the RSTEP
-      // threads sharing its column chunk -> part[m_tile][.][col]
-      __syncthreads();  // done reading the staged tile
-      double* red = reinterpret_cast<double*>(smem);  // [RSTEP][BN][2]
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        red[(rl0 * BN + 4 * c4 + e) * 2 + 0] = sa[e];
-        red[(rl0 * BN + 4 * c4 + e) * 2 + 1] = sb[e];
+          for (int t = 0; t < TM; ++t)
+#pragma unroll
+            for (int u = 0; u < TN; ++u)
+              acc[t][u] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[t][e], bf[u][e], acc[t][u], 0, 0, 0);
+      }
+      if (more) {
+        la.template store<DA>(As + (cur ^ 1) * ABUF);
+        lb.template store<DB>(Bs + (cur ^ 1) * BBUF);
       }
       __syncthreads();
-      const int mt = vt / tiles_n;
-      for (int i = tid; i < BN; i += NT) {
-        const int cc = n0 + i;
-        if (cc >= N) continue;
-        double s1 = 0.0, s2 = 0.0;
-        for (int k = 0; k < RSTEP; ++k) {
-          s1 += red[(k * BN + i) * 2 + 0];
-          s2 += red[(k * BN + i) * 2 + 1];
-        }
-        ep.part[((size_t)mt * 2 + 0) * N + cc] = s1;
-        ep.part[((size_t)mt * 2 + 1) * N + cc] = s2;
-      }
+      cur ^= 1;
     }
-    if (!next) break;
-    __syncthreads();  // the epilogue is done with the LDS before the next tile's operands land
-    vt = vn;
-    m0 = m0n;
-    n0 = n0n;
+  }
+
+  // Epilogue: the accumulator tile goes through LDS ([BM][BN+8]; the +8 puts the two lane
+  // halves' rows 4 apart on opposite bank halves) so that each thread stores 16-byte row
+  // chunks -- 4x fewer store instructions than storing the MFMA C layout directly.
+  constexpr int NT = 64 * WM * WN;
+  constexpr int LDT = BN + 8;
+  constexpr int NC4 = BN / 4;
+  constexpr int RSTEP = NT / NC4;
+  static_assert(NT % NC4 == 0, "epilogue thread map");
+  __syncthreads();  // the MFMA loop's last LDS reads are done
+#pragma unroll
+  for (int t = 0; t < TM; ++t)
+#pragma unroll
+    for (int u = 0; u < TN; ++u)
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        smem[(wm * 32 * TM + t * 32 + (r & 3) + 8 * (r >> 2) + 4 * h) * LDT + wn * 32 * TN + u * 32 + l32] =
+            acc[t][u][r];
+  __syncthreads();
+  const int c4 = tid % NC4, rl0 = tid / NC4;
+  const int col = n0 + 4 * c4;
+  const bool full = ep.v4 && col + 3 < N;
+  double sa[4] = {0.0, 0.0, 0.0, 0.0}, sb[4] = {0.0, 0.0, 0.0, 0.0};
+  constexpr int RPT = BM / RSTEP;  // rows per thread
+  static_assert(BM % RSTEP == 0, "epilogue rows");
+  if (full) {
+    typename EP::Pre pre[RPT];
+#pragma unroll
+    for (int i = 0; i < RPT; ++i) {
+      const int row = m0 + rl0 + i * RSTEP;
+      if (row < M) pre[i] = ep.pre4(row, col);
+    }
+#pragma unroll
+    for (int i = 0; i < RPT; ++i) {
+      const int rl = rl0 + i * RSTEP;
+      if (m0 + rl < M) ep.put4(m0 + rl, col, ld4(smem + rl * LDT + 4 * c4), pre[i], blockIdx.y, sa, sb);
+    }
+  } else {
+    for (int rl = rl0; rl < BM; rl += RSTEP) {
+      const int row = m0 + rl;
+      if (row >= M) break;
+      const f32x4 v = ld4(smem + rl * LDT + 4 * c4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (col + e < N) ep.put1(row, col + e, v[e], blockIdx.y, sa[e], sb[e]);
+    }
+  }
+
+  if constexpr (EP::kColStats) {
+    // per-column fp64 sums of this tile, fixed order: the thread's rows, then the RSTEP
+    // threads sharing its column chunk -> part[m_tile][.][col]
+    __syncthreads();  // done reading the staged tile
+    double* red = reinterpret_cast<double*>(smem);  // [RSTEP][BN][2]
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      red[(rl0 * BN + 4 * c4 + e) * 2 + 0] = sa[e];
+      red[(rl0 * BN + 4 * c4 + e) * 2 + 1] = sb[e];
+    }
+    __syncthreads();
+    const int mt = bid / tiles_n;
+    for (int i = tid; i < BN; i += NT) {
+      const int cc = n0 + i;
+      if (cc >= N) continue;
+      double s1 = 0.0, s2 = 0.0;
+      for (int k = 0; k < RSTEP; ++k) {
+        s1 += red[(k * BN + i) * 2 + 0];
+        s2 += red[(k * BN + i) * 2 + 1];
+      }
+      ep.part[((size_t)mt * 2 + 0) * N + cc] = s1;
+      ep.part[((size_t)mt * 2 + 1) * N + cc] = s2;
+    }
   }
 }
 
@@ -968,17 +939,18 @@ static const int kNumRowCfg = sizeof(kRowCfg) / sizeof(kRowCfg[0]);
 static const int kNumSplitCfg = sizeof(kSplitCfg) / sizeof(kSplitCfg[0]);
 
 static int g_cfg_override[2] = {-1, -1};  // tuning knob only (see header)
-// Persistent row GEMMs: grid = min(tiles, g_persist x resident blocks per CU x CUs); 0 = one
-// block per tile.  Tuning knob: dk_debug_set_gemm_config(2, v).  Measured on the ResNet step
-// (scripts/ab_step.py): 11.77 ms/step with one block per tile, 11.89 / 11.98 with 1 / 2
-// resident waves of persistent blocks, so the default is off.
-static int g_persist = 0;
+// Split-K grids fill the resident block slots once (g_fill_splits; tuning knob
+// dk_debug_set_gemm_config(2, 0/1)).  A persistent tile loop for the row problems was measured
+// and dropped (scripts/ab_step.py: 11.77 ms/step with one block per tile, 11.89 / 11.98 with
+// 1 / 2 resident waves of persistent blocks, and the loop slowed the one-tile case too).
+static int g_fill_splits = 1;
 constexpr int kNumCUs = 256;  // MI355X
 
 template <int BM, int BN, int BK, int WM, int WN, template <int, int, int> class LA, class DA,
           template <int, int, int> class LB, class DB, class EP>
 static int launch_igemm(const DA& da, const DB& db, const EP& ep, int M, int N, int Ktot, int splits,
-                        hipStream_t st) {
+                        hipStream_t st,
+                        int* splits_used = nullptr) {
   constexpr int NT = 64 * WM * WN;
   using A = LA<BM, BK, NT>;
   using B = LB<BN, BK, NT>;
@@ -986,8 +958,6 @@ static int launch_igemm(const DA& da, const DB& db, const EP& ep, int M, int N, 
   const int KT = cdiv(Ktot, BK);
   if (splits < 1) splits = 1;
   if (splits > KT) splits = KT > 0 ? KT : 1;
-  const int kps = KT > 0 ? cdiv(KT, splits) : 1;
-  splits = KT > 0 ? cdiv(KT, kps) : 1;
   size_t dyn = 0;
   if constexpr (DA::kBnIn && A::kTable) {
     dyn = (size_t)da.C * sizeof(f32x4);
@@ -999,22 +969,26 @@ static int launch_igemm(const DA& da, const DB& db, const EP& ep, int M, int N, 
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&igemm_f32<BM, BN, BK, WM, WN, A, DA, B, DB, EP>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn);
   }
-  int gx = tiles;
-  if (splits == 1 && g_persist) {
-    // persistent row problems: one resident wave of blocks (occupancy per CU x 256 CUs)
-    static int occ = -1;  // per kernel instantiation; immutable after the first launch
-    if (occ < 0) {
-      int o = 0;
-      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
-              &o, reinterpret_cast<const void*>(&igemm_f32<BM, BN, BK, WM, WN, A, DA, B, DB, EP>), NT, dyn) !=
-              hipSuccess || o < 1)
-        o = 1;
-      occ = o;
-    }
-    const int cap = occ * kNumCUs * g_persist;
-    if (gx > cap) gx = cap;
+  // resident blocks per CU of this instantiation (queried once; immutable afterwards)
+  static int occ = -1;
+  if (occ < 0) {
+    int o = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
+            &o, reinterpret_cast<const void*>(&igemm_f32<BM, BN, BK, WM, WN, A, DA, B, DB, EP>), NT, dyn) !=
+            hipSuccess || o < 1)
+      o = 1;
+    occ = o;
   }
-  hipLaunchKernelGGL((igemm_f32<BM, BN, BK, WM, WN, A, DA, B, DB, EP>), dim3(gx, splits), dim3(NT), dyn, st, da,
+  const int slots = occ * kNumCUs;
+  if (g_fill_splits && splits_used && splits > 1 && tiles * splits > slots && tiles <= slots) {
+    // split-K: no second, partly filled round of blocks (the stem's 64x128 weight-gradient
+    // tiles fit 3 per CU: 1024 splits ran as 768 + 256 blocks)
+    splits = slots / tiles;
+  }
+  const int kps = KT > 0 ? cdiv(KT, splits) : 1;
+  splits = KT > 0 ? cdiv(KT, kps) : 1;
+  if (splits_used) *splits_used = splits;
+  hipLaunchKernelGGL((igemm_f32<BM, BN, BK, WM, WN, A, DA, B, DB, EP>), dim3(tiles, splits), dim3(NT), dyn, st, da,
                      db, ep, M, N, Ktot, kps);
   return launch_status();
 }
@@ -1079,13 +1053,13 @@ static int igemm_splitk(const DA& da, const DB& db, float* ws, int M, int N, int
                         int* splits_out) {
   const int id = splitk_config(M, N, Kred);
   if (id < 0 || id >= kNumSplitCfg) return DK_ERR_ARGS;
-  const int splits = wgrad_splits(M, N, Kred, kSplitCfg[id]);
+  const int splits = wgrad_splits(M, N, Kred, kSplitCfg[id]);  // the workspace's upper bound
   *splits_out = splits;
   EpPartial ep{ws, M, N, al4(N) && aligned16(ws)};
   switch (id) {
 #define DK_CASE(cid, bm, bn, bk, wm, wn) \
   case cid:                              \
-    return launch_igemm<bm, bn, bk, wm, wn, LA, DA, LB, DB, EpPartial>(da, db, ep, M, N, Kred, splits, st);
+    return launch_igemm<bm, bn, bk, wm, wn, LA, DA, LB, DB, EpPartial>(da, db, ep, M, N, Kred, splits, st, splits_out);
     DK_SPLITK_CONFIGS(DK_CASE)
 #undef DK_CASE
     default:
@@ -1206,7 +1180,7 @@ using namespace dk;
 // Returns the number of configurations of that kind.  Not thread-safe; for tuning runs.
 DK_API int dk_debug_set_gemm_config(int kind, int cfg) {
   if (kind == 2) {
-    g_persist = cfg < 0 ? 0 : cfg;
+    g_fill_splits = cfg < 0 ? 1 : cfg;
     return 0;
   }
   if (kind < 0 || kind > 1) return -1;

@@ -35,8 +35,8 @@ int dk_abi_version(void);
 /* Tuning knob (not for production use; not thread-safe): force GEMM tile configuration
  * `cfg` for kind 0 = forward/dgrad problems or 1 = split-K weight-gradient problems;
  * cfg = -1 restores the built-in heuristic.  Returns the number of configurations.
- * kind 2: persistent forward/dgrad grids, cfg = resident waves of blocks (0 = one block per
- * output tile = the default, also for -1); returns 0. */
+ * kind 2: split-K grids sized to one round of resident blocks (1 = default, also for -1) or
+ * the fixed ~1024-block split (0); returns 0. */
 int dk_debug_set_gemm_config(int kind, int cfg);
 /* Tuning knob (same caveats): launch variant of dk_bn_bwd_apply_f32 (bits 0-1: rows in flight
  * 4/8 x plain/nontemporal stores; bits 2-3: rows per lane 16/8/32/64; bit 4: block cap 16384);

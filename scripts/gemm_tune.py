@@ -45,6 +45,7 @@ def main():
     ap.add_argument("--out", default="gpurun_out/gemm_tune.json")
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--fused-only", action="store_true", help="pw shapes: only the fused (ex / bnx) variants")
+    ap.add_argument("--only", default=None, help="comma-separated shape names (e.g. conv0,res1_pw)")
     args = ap.parse_args()
     st = torch.cuda.current_stream().cuda_stream
     nrow = lib.dk_debug_set_gemm_config(0, -1)
@@ -52,6 +53,8 @@ def main():
     results = []
     g = torch.Generator(device="cuda").manual_seed(0)
     for sh in shapes(args.batch):
+        if args.only and sh["name"] not in args.only.split(","):
+            continue
         N, H, C, K = sh["N"], sh["H"], sh["C"], sh["K"]
         if sh["kind"] == "pw":
             s = sh["st"]
