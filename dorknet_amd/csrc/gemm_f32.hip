@@ -996,7 +996,7 @@ static int launch_igemm(const DA& da, const DB& db, const EP& ep, int M, int N, 
 // Row-problem kinds with their own tile choice: plain loaders, and the BN-backward-on-load A
 // operand (dk_pwconv_dgrad_bnbwd_f32), whose per-element transform is repeated for every column
 // tile -- wide column tiles amortise it.
-enum : int { kRowPlain = 0, kRowBnBwd = 1 };
+enum : int { kRowPlain = 0, kRowBnBwd = 1, kRowConv = 2 };  // kRowConv: R x S > 1 image forward
 
 static int row_config(int M, int N, int K, int kind = kRowPlain) {
   if (g_cfg_override[0] >= 0) return g_cfg_override[0];
@@ -1008,6 +1008,9 @@ static int row_config(int M, int N, int K, int kind = kRowPlain) {
     if (N <= 256) return K >= 512 ? 13 : 6;
     return 9;                             // 256x128x16
   }
+  // The stem (K = 5*5*4 = 100, 64 filters): 128x64x16 with 2x2 waves, 555 vs 687 us
+  // (scripts/gemm_tune.py --only conv0, profiles/r01j_gemm_tune_conv.txt)
+  if (kind == kRowConv && K <= 128 && N <= 64) return 14;
   // Measured on MI355X (scripts/gemm_tune.py, profiles/r01c_gemm_tune.md): 64x64 tiles win on
   // every ResNet shape; a deeper k-tile pays once the reduction is longer than ~100.
   return K <= 128 ? 6 : 8;
@@ -1224,14 +1227,15 @@ static int conv_fwd(const D& a, const float* w_krsc, int K, int Ktot, const floa
     if (a.C > 2048) return DK_ERR_ARGS;  // the LDS parameter table holds <= 2048 channels (32 KB)
   }
   MatDesc b = mat(w_krsc, K, Ktot, K);
+  constexpr int kind = D::k1x1 ? kRowPlain : kRowConv;
   if (stats) {
     EpStoreStats ep;
     static_cast<EpStore&>(ep) = ep_store(y, K, bias);
     ep.part = stats;
-    return igemm_rows<LdImgKC, D, LdMatKC, MatDesc, EpStoreStats>(a, b, ep, a.M, K, Ktot, as_stream(stream));
+    return igemm_rows<LdImgKC, D, LdMatKC, MatDesc, EpStoreStats, kind>(a, b, ep, a.M, K, Ktot, as_stream(stream));
   }
   EpStore ep = ep_store(y, K, bias);
-  return igemm_rows<LdImgKC, D, LdMatKC, MatDesc, EpStore>(a, b, ep, a.M, K, Ktot, as_stream(stream));
+  return igemm_rows<LdImgKC, D, LdMatKC, MatDesc, EpStore, kind>(a, b, ep, a.M, K, Ktot, as_stream(stream));
 }
 
 // Rows of BatchNorm partial statistics a *_fwd_ex_f32 call writes (one per output tile row).
@@ -1271,7 +1275,7 @@ DK_API int dk_conv2d_fwd_bnx_f32(const float* x, int N, int H, int W, int C, con
 }
 
 DK_API int dk_conv2d_fwd_stats_rows(int N, int OH, int OW, int K, int C, int R, int S) {
-  return stats_rows(N * OH * OW, K, R * S * C);
+  return stats_rows(N * OH * OW, K, R * S * C, kRowConv);
 }
 
 // Forward with optional BN on load (bn_mean != NULL) and optional output statistics
