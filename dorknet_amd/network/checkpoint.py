@@ -312,23 +312,35 @@ def _save_residual(layer, open_f, save_grads):
 
 
 def _load_residual(layer, open_f, load_grads):
+    """residual_block.py:116-151.  Sub-layers are created from the stored types and names; a
+    block that already holds a sub-layer of that name and type (e.g. one already on the GPU)
+    loads into it in place instead."""
     a = _attrs(open_f, layer)
+
+    def sub(t, n, current):
+        have = {l.layer_name: l for l in current if l is not None}
+        l = have.get(n)
+        if l is None or type(l).__name__ != t:
+            l = _new_layer(t, n)
+            if getattr(layer, "is_on_gpu", False):
+                l.load_from_h5(open_f, load_grads=load_grads)
+                l.to_gpu()
+                return l
+        l.load_from_h5(open_f, load_grads=load_grads)
+        return l
+
     types = [_as_str(t) for t in a["layer_type_list"]]
     names = [_as_str(n) for n in a["layer_name_list"]]
-    layer.layer_list = [_new_layer(t, n) for t, n in zip(types, names)]
-    for l in layer.layer_list:
-        l.load_from_h5(open_f, load_grads=load_grads)
+    layer.layer_list = [sub(t, n, layer.layer_list or []) for t, n in zip(types, names)]
     if a.get("skip_projection_type", None):
         t = _as_str(a["skip_projection_type"])
         if t != "PointwiseConvLayer":
             raise ValueError("ResidualBlock: unrecognised skip_projection type {}".format(t))
-        layer.skip_projection = _new_layer(t, _as_str(a["skip_projection_name"]))
-        layer.skip_projection.load_from_h5(open_f, load_grads=load_grads)
+        layer.skip_projection = sub(t, _as_str(a["skip_projection_name"]), [layer.skip_projection])
     t = _as_str(a["post_skip_activation_type"])
     if t != "ReLu":
         raise ValueError("ResidualBlock: unrecognised post_skip_activation type {}".format(t))
-    layer.post_skip_activation = _new_layer(t, _as_str(a["post_skip_activation_name"]))
-    layer.post_skip_activation.load_from_h5(open_f, load_grads=load_grads)
+    layer.post_skip_activation = sub(t, _as_str(a["post_skip_activation_name"]), [layer.post_skip_activation])
 
 
 _HANDLERS = {
