@@ -12,6 +12,8 @@ output spatial size ceil(H/s), and the backward output size (s*OH, s*OW).
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from .._hip import lib, stream_handle, weight_grad_stream, workspace
@@ -121,6 +123,10 @@ class PointwiseConvLayer(Layer):
         P = N * OH * OW
         w = self.learned_params["weights"]
         if isinstance(upstream_dx, BNGrad):
+            if need_dx and self._fused_bwd_ok(upstream_dx, residual):
+                # input gradient, weight gradient and the input BN's partials in one pass; dy
+                # is formed from the BatchNorm's gradient as it is loaded and never stored
+                return self._bwd_fused(upstream_dx, residual, st)
             if need_dx and self._takes_bn_grad(upstream_dx.x):
                 # dgrad first: it forms (and stores) dy from the BatchNorm's gradient as it loads it
                 dy = empty_nhwc(N, K, OH, OW)
@@ -135,6 +141,54 @@ class PointwiseConvLayer(Layer):
                 self.layer_name))
         self._wgrad(dy, x, N, H, W, C, K, s, OH, OW, P, w, bf)
         return self._dgrad(dy, residual, st) if need_dx else None
+
+    def _fused_bwd_ok(self, bg, residual):
+        """dk_pwconv_bwd_bnbwd_f32 applies: DORKNET_PW_FUSED_BWD=1, fp32, stride 1, no bias, K and C
+        in {64, 128}, a residual (if any) that fuses.  Off by default: measured 0.75 % slower on
+        the ResNet-18-depsep step (10.72 vs 10.64 ms, scripts/ab_step.py) -- its 64-pixel tiles
+        run at 1-2 resident blocks per CU (VGPR / LDS bound), too few to hide HBM latency, while
+        the unfused pair overlaps the weight gradient on the side stream."""
+        x = self.X
+        if os.environ.get("DORKNET_PW_FUSED_BWD", "0") != "1" or self.with_bias or not self._takes_bn_grad(bg.x):
+            return False
+        N, C, H, W = x.shape
+        OH, OW = self.out_hw
+        if lib.dk_pwconv_bwd_fused_rows(N, OH, OW, self.num_filters, C) <= 0:
+            return False
+        if residual is not None and residual_operand(residual, x) is None:
+            return False
+        return True
+
+    def _bwd_fused(self, bg, residual, st):
+        x = self.X
+        N, C, H, W = x.shape
+        K = self.num_filters
+        OH, OW = self.out_hw
+        w = self.learned_params["weights"]
+        dx = empty_nhwc(N, C, OH, OW)
+        bn = self._bn_in
+        res = residual_operand(residual, dx)
+        g = to_nhwc(bg.g)
+        part = None
+        if bn is not None:
+            rows = lib.dk_pwconv_bwd_fused_rows(N, OH, OW, K, C)
+            part = torch.empty((rows, 2, C), dtype=torch.float64, device=dx.device)
+        gw = grad_buffer(self, "weights", (K, C))
+        l2s = l2_strength(self.weight_regulariser)
+        nb = lib.dk_pwconv_bwd_fused_workspace_bytes(N, OH, OW, K, C)
+        lib.dk_pwconv_bwd_bnbwd_f32(g.data_ptr(), bg.x.data_ptr(), N, OH, OW, K, *bg.bnbwd_args(), w.data_ptr(), C,
+                                    l2s or 0.0, gw.data_ptr(), dx.data_ptr(), ptr(res), x.data_ptr(),
+                                    *((*bn.bn_args(), part.data_ptr()) if bn is not None else (0, 0, 0, 0, 0, 0)),
+                                    workspace.get(nb), nb, st)
+        if l2s is None:
+            add_regulariser_grad(gw, w, self.weight_regulariser)
+        # the weight gradient was written on this stream: work queued on the side stream from
+        # here on (a data-parallel bucket's all-reduce) must follow it
+        with weight_grad_stream():
+            pass
+        if bn is not None:
+            bn.hand_backward_partials(dx, part)
+        return dx
 
     def _dgrad_bnbwd(self, bg, dy_out, residual, st):
         x = self.X

@@ -193,6 +193,13 @@ MODEL = {
     ga, b, r, part, st: (
         2 * N * OH * OW * K * C + 6 * N * OH * OW * K,
         E * (N * OH * OW * K * (2 + (dyo != 0)) + N * OH * OW * C * (1 + (bx != 0) + (res != 0)) + K * C)),
+    # fused pointwise backward (dgrad + wgrad): reads g and the following BN's input (to form
+    # dy), the layer's input x once (weight-gradient operand and the input BN's partials) and
+    # the residual; writes dx; dW partials are per block (small)
+    "dk_pwconv_bwd_bnbwd_f32": lambda g, ox, N, OH, OW, K, om, oi, og, ob, orl, k12, w, C, l2, dw, dx, res, x, m,
+    i, ga, b, r, part, ws, nb, st: (
+        2 * 2 * N * OH * OW * K * C + 6 * N * OH * OW * K,
+        E * (2 * N * OH * OW * K + N * OH * OW * C * (2 + (res != 0)) + 2 * K * C)),
     # fused depthwise backward: reads g and the following BN's input (to form dy), the layer's
     # input (weight gradient; the input BN's partials), the residual addend; writes dx
     "dk_dwconv_bwd_bnbwd_f32": lambda g, ox, N, H, W, C, om, oi, og, ob, orl, k12, x, w, R, S, pad, l2, dw, dx, res,

@@ -139,6 +139,17 @@ int dk_dwconv_dgrad_ex_f32(const float* dy, int N, int OH, int OW, int C, const 
  * the separate apply pass saves -- measured, DESIGN.md.) */
 int dk_pwconv_dgrad_bnbwd_stats_rows(int N, int OH, int OW, int K, int C);
 int dk_pwconv_dgrad_bnbwd_f32(const float* g, const float* bn_x, int N, int OH, int OW, int K, const float* out_mean, const float* out_invstd, const float* out_gamma, const float* out_beta, int out_relu, const float* k12, float* dy_out, const float* w_kc, int C, float* dx, const float* residual, const float* x, const float* bn_mean, const float* bn_invstd, const float* bn_gamma, const float* bn_beta, int bn_relu, double* part, void* stream);
+/* Fused stride-1 pointwise backward (dorknet_amd/csrc/pw_bwd_fused.hip), replacing
+ * dk_pwconv_dgrad_bnbwd_f32 + dk_pwconv_wgrad_bnx_f32 (pointwise_convolution.py:57-75 with the
+ * following BatchNorm's backward, batch_norm.py:125-174, applied as dy is formed): one pass
+ * reads g, bn_x (the following BN's raw input) and x (this layer's raw input) and writes dx
+ * (+ residual), the weight gradient dw_kc = dy^T . bn_in(x) + l2 * w_kc (fixed-order reduce of
+ * per-block partials in ws) and, when part != NULL, the input BN's backward partials
+ * part[rows][2][C], rows = dk_pwconv_bwd_fused_rows().  dy itself is never stored.
+ * K, C in {64, 128} (dk_pwconv_bwd_fused_rows() returns 0 for other shapes); fp32 NHWC. */
+int dk_pwconv_bwd_fused_rows(int N, int OH, int OW, int K, int C);
+size_t dk_pwconv_bwd_fused_workspace_bytes(int N, int OH, int OW, int K, int C);
+int dk_pwconv_bwd_bnbwd_f32(const float* g, const float* bn_x, int N, int OH, int OW, int K, const float* out_mean, const float* out_invstd, const float* out_gamma, const float* out_beta, int out_relu, const float* k12, const float* w_kc, int C, float l2, float* dw_kc, float* dx, const float* residual, const float* x, const float* bn_mean, const float* bn_invstd, const float* bn_gamma, const float* bn_beta, int bn_relu, double* part, void* ws, size_t ws_bytes, void* stream);
 
 /* ---------------------------------------------------------------------------------------
  * bf16 storage twins (BASELINE config 5: the depthwise-separable stack with bf16 activations).

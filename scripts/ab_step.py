@@ -38,11 +38,17 @@ def main():
         net.backward()
         sgd.update_weights()
 
-    knobs = [tuple(int(v) for v in k.split(":")) for k in args.knob] or [(2, -1)]
+    # kind:cfg (dk_debug_set_gemm_config) or env:NAME=VALUE (read per call by the layers)
+    knobs = [tuple(k.split(":", 1)) if k.startswith("env:") else tuple(int(v) for v in k.split(":"))
+             for k in args.knob] or [(2, -1)]
     res = {k: [] for k in knobs}
     for _ in range(args.rounds):
         for k in knobs:
-            lib.dk_debug_set_gemm_config(*k)
+            if k[0] == "env":
+                name, val = k[1].split("=", 1)
+                os.environ[name] = val
+            else:
+                lib.dk_debug_set_gemm_config(*k)
             for _ in range(2):
                 step()
             torch.cuda.synchronize()
@@ -51,9 +57,10 @@ def main():
                 step()
             torch.cuda.synchronize()
             res[k].append(1e3 * (time.perf_counter() - t0) / args.steps)
-            lib.dk_debug_set_gemm_config(k[0], -1)
+            if k[0] != "env":
+                lib.dk_debug_set_gemm_config(k[0], -1)
     for k, v in res.items():
-        print(f"knob {k[0]}:{k[1]:3d}  {np.median(v):7.3f} ms/step  ({', '.join(f'{x:.3f}' for x in v)})  "
+        print(f"knob {k[0]}:{k[1]:>3}  {np.median(v):7.3f} ms/step  ({', '.join(f'{x:.3f}' for x in v)})  "
               f"{args.batch / np.median(v) * 1e3:9.1f} img/s", flush=True)
 
 
