@@ -32,6 +32,21 @@ extern "C" {
 
 int dk_abi_version(void);
 
+/* ---------------------------------------------------------------------------------------
+ * Device-side input pipeline (dorknet_amd/csrc/input_pipeline.hip),
+ * replacing the per-image CPU work of data_loading/image_preprocessor.py:16-39 and the mixup
+ * of data_loading/image_data_loader.py:101-111 for a whole batch:
+ *  - dk_resize_bilinear_u8: cv2.resize(im, (OW, OH)) INTER_LINEAR geometry (half-pixel centres,
+ *    edge replication), fp32 interpolation rounded to nearest-even, uint8 NHWC in and out;
+ *  - dk_u8_nhwc_to_nchw_f32: im[r:r+OH, c:c+OW, :].astype(float32).transpose(2,0,1) - shift for
+ *    every image; crop_rc = device int32 [N][2] (row, col) offsets (NULL: 0, 0; clamped into the
+ *    image); dst fp32 NCHW [N][C][OH][OW];
+ *  - dk_mixup_f32: ab = p*b + (1-p)*a and ba = p*a + (1-p)*b elementwise, with p and 1-p
+ *    passed as the fp32 values numpy multiplies by (X_batch = a, X_batch_m = b). */
+int dk_resize_bilinear_u8(const uint8_t* src, int N, int H, int W, int C, int OH, int OW, uint8_t* dst, void* stream);
+int dk_u8_nhwc_to_nchw_f32(const uint8_t* src, int N, int H, int W, int C, const int* crop_rc, int OH, int OW, float shift, float* dst, void* stream);
+int dk_mixup_f32(const float* a, const float* b, long long n, float p, float one_minus_p, float* ab, float* ba, void* stream);
+
 /* Tuning knob (not for production use; not thread-safe): force GEMM tile configuration
  * `cfg` for kind 0 = forward/dgrad problems or 1 = split-K weight-gradient problems;
  * cfg = -1 restores the built-in heuristic.  Returns the number of configurations.
