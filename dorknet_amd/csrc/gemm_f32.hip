@@ -25,6 +25,8 @@
 // row-contiguous (wgrad operands) is kept [BK][rows] and read with ds_read_b32.  Because
 // the MFMA sums over k in any order, the four MFMAs of a q-block use k = 8q + 4h + t
 // (h = lane half, t = 0..3) on both operands.
+#include <stdlib.h>
+
 #include "dk_common.h"
 
 namespace dk {
@@ -1041,10 +1043,20 @@ static int splitk_config(int M, int N, int Kred) {
   return 1;  // 64x64x32: best or within 3% of best on every other measured wgrad shape
 }
 
+// Blocks a split-K weight gradient aims for (tuning knob DORKNET_WGRAD_BLOCKS, read once).
+static int wgrad_target_blocks() {
+  static int v = -1;
+  if (v < 0) {
+    const char* s = getenv("DORKNET_WGRAD_BLOCKS");
+    v = (s && atoi(s) > 0) ? atoi(s) : 1024;
+  }
+  return v;
+}
+
 static int wgrad_splits(int M, int N, int Kred, const TileCfg& c) {
   const int tiles = cdiv(M, c.BM) * cdiv(N, c.BN);
   const int KT = cdiv(Kred, c.BK);
-  int splits = cdiv(1024, tiles);
+  int splits = cdiv(wgrad_target_blocks(), tiles);
   if (splits > KT) splits = KT;
   if (splits < 1) splits = 1;
   const int kps = cdiv(KT, splits);
