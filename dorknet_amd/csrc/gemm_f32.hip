@@ -1037,9 +1037,10 @@ static int igemm_rows(const DA& da, const DB& db, const EP& ep, int M, int N, in
 static int splitk_config(int M, int N, int Kred) {
   if (g_cfg_override[1] >= 0) return g_cfg_override[1];
   (void)Kred;
-  // One column tile for 64 < N <= 128 (the stem: N = R*S*Cp = 100): the A operand -- for the
-  // stem the BN-backward-on-load dy, formed from 2 x 822 MB -- is then streamed once, not twice.
-  if (M <= 64 && N > 64 && N <= 128) return 6;  // 64x128x32
+  // Wide column tiles when M <= 64 < N: the A operand (for the stem the BN-backward-on-load dy,
+  // formed from 2 x 822 MB) is streamed half as often -- the stem (N = R*S*Cp = 100) in one
+  // column tile; BASELINE config 2's 3x3 conv (N = 576): 594 vs 628 us (profiles/r01j_gemm_tune_all.txt).
+  if (M <= 64 && N > 64) return 6;  // 64x128x32
   return 1;  // 64x64x32: best or within 3% of best on every other measured wgrad shape
 }
 
