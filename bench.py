@@ -39,8 +39,9 @@ def parse():
     ap.add_argument("--batch", type=int, default=256, help="images per GPU")
     ap.add_argument("--bn", choices=["local", "sync"], default="local")
     ap.add_argument("--no-roofline", action="store_true")
-    ap.add_argument("--cpu-sample", type=int, default=64, help="images in the CPU-baseline sample (0 = skip)")
-    ap.add_argument("--cpu-steps", type=int, default=3, help="timed CPU-baseline steps (after one warm-up)")
+    ap.add_argument("--cpu-sample", type=int, default=32, help="images per CPU-baseline step (0 = skip)")
+    ap.add_argument("--cpu-steps", type=int, default=10, help="timed CPU-baseline steps (median reported)")
+    ap.add_argument("--cpu-warmup", type=int, default=2, help="untimed CPU-baseline steps")
     ap.add_argument("--config", type=int, choices=[2, 3, 5], default=3,
                     help="BASELINE config: 3 (default; 4 with --gpus N) = ResNet-18-depsep training step; "
                          "2 = single 3x3 ConvLayer fwd+dgrad+wgrad; 5 = bf16 depthwise-separable stack "
@@ -158,36 +159,73 @@ def pmc_traffic(entry, path):
     return t / n, os.path.relpath(path, ROOT)
 
 
-def cpu_baseline(batch, steps=3):
-    """Reference CPU path (restated) on `batch` images: 1 warm-up + `steps` timed steps."""
+def cpu_info():
+    """(model name, physical cores, logical CPUs) of this host, from lscpu."""
+    import subprocess
+    model, cores_per_socket, sockets, logical = None, None, None, os.cpu_count()
+    try:
+        out = subprocess.run(["lscpu"], stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, text=True,
+                             timeout=10).stdout
+        for line in out.splitlines():
+            k, _, v = line.partition(":")
+            k, v = k.strip(), v.strip()
+            if k == "Model name":
+                model = v
+            elif k == "Core(s) per socket":
+                cores_per_socket = int(v)
+            elif k == "Socket(s)":
+                sockets = int(v)
+    except (OSError, ValueError, subprocess.SubprocessError):
+        pass
+    phys = cores_per_socket * sockets if cores_per_socket and sockets else None
+    return model, phys, logical
+
+
+def cpu_baseline(batch, steps=10, warmup=2):
+    """Reference CPU path (restated, oracle/cpu_path.py: C/OpenMP versions of its Cython kernels
+    + numpy BLAS) on `batch` images per step, timed per BASELINE.md section 3: every core this
+    process may use (the GPU box gives one GPU's job a 16-CPU share: OMP_NUM_THREADS=16 and the
+    affinity mask; the whole-machine physical core count is reported beside it),
+    OMP_MAX_ACTIVE_LEVELS=1 (the reference's nested pranges serialised, as libgomp does by
+    default), `warmup` untimed steps, then the median of `steps` timed steps."""
     import numpy as np
     try:
-        cores = min(16, len(os.sched_getaffinity(0)))
+        avail = len(os.sched_getaffinity(0))
     except AttributeError:
-        cores = min(16, os.cpu_count() or 1)
-    os.environ.setdefault("OMP_NUM_THREADS", str(cores))
-    cores = int(os.environ["OMP_NUM_THREADS"])
+        avail = os.cpu_count() or 1
+    cores = int(os.environ.get("OMP_NUM_THREADS", avail))
+    cores = max(1, min(cores, avail))
+    os.environ["OMP_NUM_THREADS"] = str(cores)
+    os.environ["OMP_MAX_ACTIVE_LEVELS"] = "1"
     from threadpoolctl import threadpool_limits
     from oracle import models
     from oracle.net import OSGDMomentum
     from examples.resnet18_depsep import synthetic_batch
+    from oracle._clib import lib as oracle_lib
+    got = oracle_lib().oracle_set_threads(cores)
+    if got != cores:
+        raise RuntimeError("cpu_baseline: asked for {} OpenMP threads, got {}".format(cores, got))
+    times = []
     with threadpool_limits(limits=cores):
         net = models.resnet18_depsep(backend="cy", rng=np.random.RandomState(0))
         sgd = OSGDMomentum(net, 0.05 * batch / 200.0, 0.9)
         X, _, onehot = synthetic_batch(batch, seed=0)
-        net.forward(X, onehot)
-        net.backward()
-        sgd.update_weights()
-        t0 = time.perf_counter()
-        for _ in range(steps):
+        for i in range(warmup + steps):
+            t0 = time.perf_counter()
             net.forward(X, onehot)
             net.backward()
             sgd.update_weights()
-        dt = time.perf_counter() - t0
-    return {"value": round(steps * batch / dt, 3), "unit": "images/s", "cores": cores, "kind": "port",
-            "sample": "{} timed training steps (fwd+bwd+SGD, after 1 warm-up) on a {}-image batch of "
-                      "ResNet-18-depsep 225x225 fp32, reference CPU path restated (C/OpenMP versions of its "
-                      "Cython kernels + numpy BLAS), {:.1f} s".format(steps, batch, dt)}
+            if i >= warmup:
+                times.append(time.perf_counter() - t0)
+    med = float(np.median(times))
+    model, phys, logical = cpu_info()
+    return {"value": round(batch / med, 3), "unit": "images/s", "cores": cores, "kind": "port",
+            "cpu_model": model, "host_physical_cores": phys, "host_logical_cpus": logical,
+            "omp": {"OMP_NUM_THREADS": cores, "OMP_MAX_ACTIVE_LEVELS": 1},
+            "sample": "median of {} timed training steps (fwd+bwd+SGD-momentum; after {} untimed) on a {}-image "
+                      "batch of ResNet-18-depsep 225x225 fp32 -- the reference's CPU path restated (C/OpenMP "
+                      "versions of its Cython kernels, -O3 -ffast-math -fopenmp, + numpy BLAS); median step "
+                      "{:.3f} s, {:.1f} s in all".format(steps, warmup, batch, med, sum(times))}
 
 
 def other_config(args):
@@ -254,8 +292,28 @@ def other_config(args):
     print(json.dumps(out), flush=True)
 
 
+def spawn_ranks(args):
+    """`bench.py --gpus N` (N > 1) started without a torch.distributed environment: start N
+    rank processes with torch.distributed.run (one per GPU, rendezvous on 127.0.0.1) and exit
+    with its status.  Runs before anything initialises the GPU, and starts the ranks as child
+    processes (no exec)."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(args.gpus),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("OMP_NUM_THREADS", "4")
+    return subprocess.call(cmd, env=env)
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args))
     if args.config != 3:
         if args.gpus != 1:
             raise SystemExit("--config {} is a one-GPU configuration".format(args.config))
@@ -270,10 +328,20 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        raise SystemExit("--gpus {} but WORLD_SIZE={} (launch N>1 with torch.distributed.run)".format(args.gpus, world))
-    torch.cuda.set_device(local_rank)
+        raise SystemExit("--gpus {} but WORLD_SIZE={}".format(args.gpus, world))
+    ndev = torch.cuda.device_count()
+    if ndev < 1:
+        raise SystemExit("bench.py needs a HIP device")
+    # one rank per GPU; a box with fewer GPUs than ranks (a launch test) shares them, and RCCL
+    # cannot put two ranks on one device, so such a run uses gloo for the gradient exchange
+    shared = world > ndev
+    dev_index = local_rank % ndev
+    torch.cuda.set_device(dev_index)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if shared:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev_index))
 
     from examples.resnet18_depsep import ResNet18, synthetic_batch
     from dorknet_amd._tensor import as_device
@@ -364,7 +432,7 @@ def main():
     ms_per_step = 1e3 * elapsed / args.steps
     cpu = None
     if rank == 0 and world == 1 and args.cpu_sample > 0:
-        cpu = cpu_baseline(args.cpu_sample, args.cpu_steps)
+        cpu = cpu_baseline(args.cpu_sample, args.cpu_steps, args.cpu_warmup)
     if rank == 0:
         out = {"metric": METRIC, "value": round(value, 2), "unit": "images/s", "n_gpus": world,
                "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
@@ -375,6 +443,10 @@ def main():
                                       "BASELINE config {}".format(3 if world == 1 else 4),
                           "global_batch": world * args.batch, "per_gpu_batch": args.batch,
                           "parallelism": "dp{}".format(world), "batch_norm": args.bn if world > 1 else "local",
+                          "grad_allreduce": (None if world == 1 else
+                                             "RCCL over xGMI" if not shared else
+                                             "gloo: {} ranks shared {} GPU(s) (launch test, not a scaling "
+                                             "point)".format(world, ndev)),
                           "input_grad": "not computed (network.backward returns nothing, as in the reference, "
                                         "which computes the image gradient and drops it)"},
                "roofline": roof, "cpu_baseline": cpu}

@@ -9,6 +9,12 @@ gather in the A-tile loader and the widen is fused into the dgrad epilogue.
 Public surface identical to the reference: constructor (:7-8, note ``stride`` is the
 second positional argument), weights (K, C), bias (K,), ``__repr__`` (:35-44), the
 output spatial size ceil(H/s), and the backward output size (s*OH, s*OW).
+
+Any channel count C is accepted, as by the reference's cp.dot over (K, C).  The kernels load
+16 bytes per lane, so for C % 4 != 0 the input is zero-padded to Cp = 4*ceil(C/4) channels
+(layout conversion), the weights to (K, Cp) (dk_conv_weight_krsc_f32 with R = S = 1), the
+weight gradient is scattered back to (K, C) by the conv weight-gradient reduce, and the
+input gradient is computed on Cp channels and returned as its first C.
 """
 from __future__ import annotations
 
@@ -60,9 +66,20 @@ class PointwiseConvLayer(Layer):
     accepts_bn_input = True   # forward(BNOut): the preceding BatchNorm is applied on load
     produces_bn_stats = True  # forward(..., bn_stats=StatsRequest): emits the next BN's statistics
 
+    def _padded_weights(self, w, Cp):
+        """(K, C) weights zero-padded to (K, Cp) for a C % 4 != 0 input (a fresh copy per
+        forward, so it always reflects the current weights)."""
+        K, C = self.num_filters, self.num_channels
+        wp = torch.empty((K, Cp), dtype=torch.float32, device=w.device)
+        lib.dk_conv_weight_krsc_f32(w.data_ptr(), K, C, 1, 1, Cp, wp.data_ptr(), stream_handle())
+        return wp
+
     def forward(self, X, test_mode=False, bn_stats=None):
         self._require_on_gpu()
         st = stream_handle()
+        if X.shape[1] != self.num_channels:
+            raise ValueError("PointwiseConvLayer {}: input has {} channels, weights expect {}".format(
+                self.layer_name, X.shape[1], self.num_channels))
         bn = X if isinstance(X, BNOut) and X.dim() == 4 and X.shape[1] % 4 == 0 else None
         x = bn.x if bn is not None else to_nhwc(X, cpad=4)
         N, Cp, H, W = x.shape
@@ -73,8 +90,10 @@ class PointwiseConvLayer(Layer):
         y = empty_nhwc(N, K, OH, OW, x.dtype)
         w = self.learned_params["weights"]
         if Cp != self.num_channels:
-            raise ValueError("PointwiseConvLayer {}: input has {} channels, weights expect {} (a multiple of 4 "
-                             "is required)".format(self.layer_name, X.shape[1], self.num_channels))
+            if bf:
+                raise NotImplementedError("{}: bf16 storage needs C % 4 == 0".format(self.layer_name))
+            w = self._padded_weights(w, Cp)
+        self._wp = w
         bias = self.learned_params["bias"] if self.with_bias else None
         stats = None
         if bn_stats is not None and not test_mode:
@@ -104,10 +123,11 @@ class PointwiseConvLayer(Layer):
         x = getattr(self, "X", None)
         bx = getattr(bn_layer, "X", None)
         return (x is not None and bx is not None and x.dtype == torch.float32 and self.stride == 1
-                and x.dim() == 4 and self._takes_bn_grad(bx))
+                and x.dim() == 4 and x.shape[1] == self.num_channels and self._takes_bn_grad(bx))
 
     def _takes_bn_grad(self, bx):
         return (bx.dim() == 4 and bx.dtype == torch.float32 and self.stride == 1 and self.X.dtype == torch.float32
+                and self.X.shape[1] == self.num_channels
                 and tuple(bx.shape) == (self.X.shape[0], self.num_filters, *self.out_hw)
                 and self.num_filters % 4 == 0 and self.num_filters <= 2048)
 
@@ -136,11 +156,45 @@ class PointwiseConvLayer(Layer):
             upstream_dx = upstream_dx.materialize()
         dy = to_nhwc(upstream_dx)
         bf = x.dtype == BF16
+        if C != self.num_channels:
+            return self._backward_padded(dy, residual, need_dx, st)
         if bf and (dy.dtype != BF16 or self.with_bias or s != 1):
             raise NotImplementedError("{}: bf16 storage needs a bf16 gradient, no bias, stride 1".format(
                 self.layer_name))
         self._wgrad(dy, x, N, H, W, C, K, s, OH, OW, P, w, bf)
         return self._dgrad(dy, residual, st) if need_dx else None
+
+    def _backward_padded(self, dy, residual, need_dx, st):
+        """Backward for C % 4 != 0: the input was padded to Cp channels in forward."""
+        x = self.X
+        N, Cp, H, W = x.shape
+        C, K, s = self.num_channels, self.num_filters, self.stride
+        OH, OW = self.out_hw
+        P = N * OH * OW
+        w = self.learned_params["weights"]
+        with weight_grad_stream(dy, x):
+            sst = stream_handle()
+            if self.with_bias:
+                gb = grad_buffer(self, "bias", (K,))
+                nb = lib.dk_colsum_workspace_bytes(P, K)
+                lib.dk_colsum_f32(dy.data_ptr(), P, K, gb.data_ptr(), workspace.get(nb), nb, sst)
+            gw = grad_buffer(self, "weights", (K, C))
+            l2s = l2_strength(self.weight_regulariser)
+            # the conv weight gradient with R = S = 1, pad 0: its reduce scatters (K, Cp) -> (K, C)
+            nb = lib.dk_conv2d_wgrad_workspace_bytes(N, OH, OW, K, Cp, 1, 1)
+            lib.dk_conv2d_wgrad_f32(dy.data_ptr(), x.data_ptr(), N, H, W, Cp, C, K, 1, 1, s, 0, OH, OW,
+                                    w.data_ptr() if l2s else 0, l2s or 0.0, gw.data_ptr(), workspace.get(nb), nb,
+                                    sst)
+            if l2s is None:
+                add_regulariser_grad(gw, w, self.weight_regulariser)
+        if not need_dx:
+            return None
+        dxp = empty_nhwc(N, Cp, OH * s, OW * s)
+        lib.dk_pwconv_dgrad_f32(dy.data_ptr(), N, OH, OW, K, self._wp.data_ptr(), Cp, s, dxp.data_ptr(), st)
+        dx = dxp[:, :C]
+        if residual is not None:
+            dx = add_residual(dx, residual)
+        return dx
 
     def _fused_bwd_ok(self, bg, residual):
         """dk_pwconv_bwd_bnbwd_f32 applies: DORKNET_PW_FUSED_BWD=1, fp32, stride 1, no bias, K and C

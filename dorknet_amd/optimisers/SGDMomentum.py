@@ -2,7 +2,10 @@
 
 Parameter discovery is the reference's (:7-14): every top-level layer with
 ``learned_params`` plus one level of ``layer_list`` -- so ResidualBlock skip
-projections are *not* updated (a reference quirk, kept).  ``update_weights`` computes,
+projections are *not* updated (a reference quirk, kept as the default).
+``update_skip_projections=True`` (an extension, not in the reference) also updates each
+ResidualBlock's ``skip_projection``; pass the same flag to ``parallel.DataParallel`` so
+their gradients are all-reduced.  ``update_weights`` computes,
 per parameter tensor, ``d = -lr * g + momentum * v;  W += d;  v = d`` (:31-39) -- as one
 multi-tensor HIP launch over all tensors instead of ~4 CuPy kernels per tensor.
 """
@@ -15,8 +18,9 @@ from .._hip import lib, stream_handle
 
 
 class SGDMomentum:
-    def __init__(self, network, learning_rate, momentum):
+    def __init__(self, network, learning_rate, momentum, update_skip_projections=False):
         self.network = network
+        self.update_skip_projections = update_skip_projections
         self.learnable_layers = []
         for layer in network.layers:
             if layer.learned_params is not None:
@@ -25,6 +29,9 @@ class SGDMomentum:
                 for l in layer.layer_list:
                     if l.learned_params is not None:
                         self.learnable_layers.append(l)
+                skip = getattr(layer, "skip_projection", None)
+                if update_skip_projections and skip is not None and skip.learned_params:
+                    self.learnable_layers.append(skip)
         self.learning_rate = learning_rate
         self.momentum = momentum
         self.grad_cache = {}

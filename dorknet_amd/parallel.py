@@ -14,6 +14,18 @@ the result equals single-process training on the concatenated batch).
 Averaging: the reference's loss gradient is already divided by the local batch
 (layers/losses.py:34), so the mean over ranks equals the full-batch gradient, and the
 per-layer `+ strength * W` l2 term stays correct (a sum would scale it by world size).
+
+Skip projections: the reference's SGDMomentum never updates them (optimisers/
+SGDMomentum.py:7-14; `SGDMomentum(update_skip_projections=False)`, the default).  With the
+same flag False here their gradients are left out of the buckets -- nothing reads them for
+the update, so they stay rank-local (per-rank batch) instead of costing 172,032 floats of
+all-reduce per step on ResNet-18-depsep.  Pass True together with the optimiser's True.
+
+Stream ordering: weight gradients are written on two streams (the main stream -- BatchNorm
+dgamma/dbeta, dense, the fused depthwise backward, the stem -- and the weight-gradient side
+stream).  A bucket's all-reduce is issued from the side stream after making it wait for the
+main stream, so RCCL reads the bucket only once every kernel issued so far on either stream
+has written it.
 """
 from __future__ import annotations
 
@@ -24,24 +36,25 @@ from ._hip import async_weight_grads, side_stream_context
 from .layers._chain import chain_backward
 
 
-def _all_layers(layers):
+def _all_layers(layers, skips=True):
     """Every layer (depth-first, forward order), including ResidualBlock children and
-    skip projections."""
+    (skips=True) skip projections."""
     out = []
     for l in layers:
         out.append(l)
         if hasattr(l, "layer_list"):
-            out.extend(_all_layers(l.layer_list))
-            if getattr(l, "skip_projection", None) is not None:
+            out.extend(_all_layers(l.layer_list, skips))
+            if skips and getattr(l, "skip_projection", None) is not None:
                 out.append(l.skip_projection)
     return out
 
 
-def grad_slots(network):
-    """[(top_level_index, layer, key, shape)] for every gradient, in forward order."""
+def grad_slots(network, skips=True):
+    """[(top_level_index, layer, key, shape)] for every gradient, in forward order
+    (skips=False: without the ResidualBlock skip projections' gradients)."""
     slots = []
     for ti, top in enumerate(network.layers):
-        for l in _all_layers([top]):
+        for l in _all_layers([top], skips):
             if not l.grads:
                 continue
             for k, g in l.grads.items():
@@ -67,14 +80,18 @@ def plan_buckets(slot_numels, slot_owner, bucket_bytes):
 
 
 class DataParallel:
-    def __init__(self, network, group=None, batch_norm="local", bucket_bytes=2 << 20, device=None):
+    def __init__(self, network, group=None, batch_norm="local", bucket_bytes=2 << 20, device=None,
+                 update_skip_projections=False):
         if batch_norm not in ("local", "sync"):
             raise ValueError("batch_norm must be 'local' or 'sync'")
         self.network = network
         self.group = group
         self.world = dist.get_world_size(group)
         self.batch_norm = batch_norm
-        slots = grad_slots(network)
+        self.update_skip_projections = update_skip_projections
+        # RCCL ("nccl") averages in the collective; gloo has no AVG: sum, then scale after wait
+        self.native_avg = dist.get_backend(group) == "nccl"
+        slots = grad_slots(network, skips=update_skip_projections)
         numels = [int(torch.Size(s[3]).numel()) for s in slots]
         self.total = sum(numels)
         dev = device if device is not None else (torch.device("cuda", torch.cuda.current_device())
@@ -106,13 +123,21 @@ class DataParallel:
 
     def _launch(self, lo, hi):
         view = self.flat[lo:hi]
+        op = dist.ReduceOp.AVG if self.native_avg else dist.ReduceOp.SUM
         if view.is_cuda:
-            # issued from the weight-gradient side stream (when in use): RCCL then waits for
-            # the wgrad kernels that wrote this bucket, not for the whole critical path
+            # issued from the weight-gradient side stream (when in use), after it has waited
+            # for the main stream: the bucket's gradients are written on both (BatchNorm
+            # dgamma/dbeta, dense, fused depthwise and stem weight gradients on main; the
+            # GEMM weight gradients on the side stream), and the collective follows only the
+            # stream it is issued from
+            main = torch.cuda.current_stream()
             with side_stream_context():
-                work = dist.all_reduce(view, op=dist.ReduceOp.AVG, group=self.group, async_op=True)
-        else:  # gloo (CPU tests): no AVG; sum then scale after wait
-            work = dist.all_reduce(view, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+                cur = torch.cuda.current_stream()
+                if cur != main:
+                    cur.wait_stream(main)
+                work = dist.all_reduce(view, op=op, group=self.group, async_op=True)
+        else:
+            work = dist.all_reduce(view, op=op, group=self.group, async_op=True)
         self._works.append((work, view))
 
     def backward(self):
@@ -155,7 +180,7 @@ class DataParallel:
     def finish(self):
         for work, view in self._works:
             work.wait()
-            if not view.is_cuda:
+            if not self.native_avg:
                 view.div_(self.world)
         self._works = []
 

@@ -21,6 +21,7 @@ _SIGS = {
     "oracle_bn_stats": [_P, _I, _I, _I, _I, _P, _P],
     "oracle_relu_forward_train": [_P, _L, _P, _P],
     "oracle_num_threads": [],
+    "oracle_set_threads": [_I],
 }
 
 
@@ -38,7 +39,7 @@ def lib():
         for name, args in _SIGS.items():
             fn = getattr(l, name)
             fn.argtypes = args
-            fn.restype = ctypes.c_int if name == "oracle_num_threads" else None
+            fn.restype = ctypes.c_int if name in ("oracle_num_threads", "oracle_set_threads") else None
         _lib = l
     return _lib
 

@@ -129,3 +129,13 @@ int oracle_num_threads(void) {
   }
   return n;
 }
+
+/* The CPU-baseline thread configuration (bench.py cpu_baseline):
+ * `threads` OpenMP threads and max-active-levels 1 (nested pranges serialised).  Set through
+ * the API because libgomp reads OMP_* only once, when it is first loaded (possibly by torch
+ * before this library).  Returns the thread count a parallel region then gets. */
+int oracle_set_threads(int threads) {
+  if (threads > 0) omp_set_num_threads(threads);
+  omp_set_max_active_levels(1);
+  return oracle_num_threads();
+}

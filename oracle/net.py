@@ -217,7 +217,7 @@ class ONetwork:
 class OSGDMomentum:
     """SGDMomentum.py:4-39 including the top-level + one-level-of-layer_list discovery."""
 
-    def __init__(self, net, lr, momentum):
+    def __init__(self, net, lr, momentum, update_skip_projections=False):
         self.lr, self.momentum = lr, momentum
         self.learnable = []
         for l in net.layers:
@@ -227,6 +227,10 @@ class OSGDMomentum:
                 for c in l.layer_list:
                     if c.learned_params is not None:
                         self.learnable.append(c)
+                # the build's update_skip_projections extension (default False = the reference)
+                skip = getattr(l, "skip_projection", None)
+                if update_skip_projections and skip is not None and skip.learned_params:
+                    self.learnable.append(skip)
         self.cache = {id(l): {k: np.zeros_like(v) for k, v in l.grads.items()} for l in self.learnable}
 
     def update_weights(self):

@@ -127,6 +127,8 @@ PW_CASES = [
     (24, 40, 1, 3, 5, 6, True, 0.0),
     (512, 256, 2, 2, 14, 14, False, 1e-4),  # res7 skip
     (512, 512, 1, 4, 7, 7, False, 1e-4),    # res8 pw
+    (16, 3, 1, 2, 9, 7, True, 1e-4),        # C % 4 != 0: zero-padded channels (the reference takes any C)
+    (8, 6, 2, 3, 10, 10, False, 1e-4),      # C % 4 != 0 with stride 2 + widen
 ]
 
 

@@ -28,13 +28,14 @@ def _excess(got, want64, want32, tol):
     return 0.0 if err == 0 else err / max(bound, 1e-300)
 
 
-def _compare_step(net, onet, o32, X, onehot, lr, steps=2, tol=1e-4):
+def _compare_step(net, onet, o32, X, onehot, lr, steps=2, tol=1e-4, skips=False):
     """Training steps on the HIP path vs the fp64 oracle, with the reference-faithful fp32
-    oracle (o32) bounding quantities that vanish in exact arithmetic."""
+    oracle (o32) bounding quantities that vanish in exact arithmetic.  skips: the optimisers'
+    update_skip_projections flag."""
     from dorknet_amd.optimisers.SGDMomentum import SGDMomentum
-    sgd = SGDMomentum(net, lr, 0.9)
-    osgd = O.OSGDMomentum(onet, lr, 0.9)
-    osgd32 = O.OSGDMomentum(o32, lr, 0.9)
+    sgd = SGDMomentum(net, lr, 0.9, update_skip_projections=skips)
+    osgd = O.OSGDMomentum(onet, lr, 0.9, update_skip_projections=skips)
+    osgd32 = O.OSGDMomentum(o32, lr, 0.9, update_skip_projections=skips)
     triples = list(zip(all_layers(net.layers), all_layers(onet.layers), all_layers(o32.layers)))
     for step in range(steps):
         loss, P = net.forward(dev(X), dev(onehot))
@@ -75,6 +76,25 @@ def test_resnet18_depsep_training_steps():
     net.to_gpu()
     X, _, onehot = synthetic_batch(2, seed=1)
     _compare_step(net, onet, o32, X, onehot, lr=0.05 * 2 / 200.0)
+
+
+def test_resnet18_update_skip_projections():
+    """SGDMomentum(update_skip_projections=True): the skip projections move (they stay put by
+    default, the reference's quirk) and every weight after two steps matches the oracle run
+    with the same flag."""
+    from examples.resnet18_depsep import ResNet18, synthetic_batch
+    np.random.seed(11)
+    net = ResNet18("r18")
+    skip0 = [l.skip_projection.learned_params["weights"].copy() for l in net.layers
+             if getattr(l, "skip_projection", None) is not None]
+    onet = network_to_oracle(net)
+    o32 = network_to_oracle(net, np.float32)
+    net.to_gpu()
+    X, _, onehot = synthetic_batch(2, seed=12)
+    _compare_step(net, onet, o32, X, onehot, lr=0.05 * 2 / 200.0, skips=True)
+    skip1 = [host(l.skip_projection.learned_params["weights"]) for l in net.layers
+             if getattr(l, "skip_projection", None) is not None]
+    assert len(skip1) == 3 and all(not np.array_equal(a, b) for a, b in zip(skip0, skip1))
 
 
 def test_mnist_training_steps():

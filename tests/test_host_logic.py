@@ -99,6 +99,19 @@ def test_sgd_discovery_excludes_skip_projections():
     assert ntens == 104 and nparam == 1336312
 
 
+def test_sgd_update_skip_projections_flag():
+    """The quirk as an explicit flag: True also updates every
+    ResidualBlock's skip projection (3 more tensors, the 172,032 skip parameters)."""
+    np.random.seed(0)
+    net = ResNet18("r18")
+    sgd = SGDMomentum(net, 0.064, 0.9, update_skip_projections=True)
+    names = [l.layer_name for l in sgd.learnable_layers]
+    assert sum(n.endswith("_pw_skip") for n in names) == 3
+    ntens = sum(len(l.learned_params) for l in sgd.learnable_layers)
+    nparam = sum(v.size for l in sgd.learnable_layers for v in l.learned_params.values())
+    assert ntens == 107 and nparam == 1336312 + 172032
+
+
 def test_compute_requires_gpu():
     layer = ConvLayer("c", (4, 4, 3, 3))
     with pytest.raises(RuntimeError, match="to_gpu"):
