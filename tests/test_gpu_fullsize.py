@@ -1,0 +1,152 @@
+"""Config 3's size-dependent kernel paths at the real batch-256 shapes, through the layer API with
+the network's fusions, against the torch fp64 twin (tests/_torch_twin.py, cross-checked against
+the numpy oracle in tests/test_torch_twin.py).
+
+The small-batch network tests cannot reach these paths' large-size behaviour: split-K grids
+sized to one round of resident blocks, the XCD block remap on grids of thousands of tiles, BN
+partial-row folds of thousands of rows (one-launch ticketed folds), the pointwise entries at
+P = 802,816 pixels, the fused depthwise backward at res1's 256 x 64 x 56 x 56, and the stem
+weight gradient with conv0_bn's backward on load at 256 x 3 x 225 x 225.  Each test also
+records which C-ABI entry points ran, so it fails if a fusion stops being taken.
+
+Tolerance: normwise relative 1e-4 for outputs, input and weight gradients.  A
+BatchNorm whose output feeds a pointwise layer and another BatchNorm has dbeta = 0 in exact
+arithmetic (the later BN's backward sums to zero); such sums are bounded by 1e-6 of their l1
+scale sum|g| (fp64 partials on the GPU: far below fp32 summation error).
+"""
+import numpy as np
+import pytest
+import torch
+
+from tests._convert import all_layers, rel_err
+from tests._torch_twin import TorchTwin
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-4
+
+
+class Calls:
+    """Records the dk_* entry points called (wrapping dorknet_amd._hip.lib attributes)."""
+
+    def __init__(self, monkeypatch, names):
+        from dorknet_amd import _hip
+        self.seen = set()
+        for n in names:
+            orig = getattr(_hip.lib, n)
+
+            def w(*a, _o=orig, _n=n):
+                self.seen.add(_n)
+                return _o(*a)
+            monkeypatch.setattr(_hip.lib, n, w)
+
+
+def _perturb_bn(layers, rng):
+    for l in TorchTwin._all(layers):
+        if type(l).__name__ == "BatchNormLayer":
+            C = l.incoming_chans
+            l.learned_params["gamma"] = (1 + 0.2 * rng.standard_normal((1, C, 1, 1))).astype(np.float32)
+            l.learned_params["beta"] = (0.1 * rng.standard_normal((1, C, 1, 1))).astype(np.float32)
+
+
+def _run(layers, X, dY, input_grad):
+    from dorknet_amd.network.feed_forward_network import FeedForwardNetwork
+    twin = TorchTwin(layers)                       # numpy parameters, before to_gpu
+    net = FeedForwardNetwork("fullsize")
+    for l in layers:
+        net.add_layer(l)
+    net.to_gpu()
+    Xd = torch.as_tensor(X, device="cuda")
+    dYd = torch.as_tensor(dY, device="cuda")
+    _, Y = net.forward(Xd, None)
+    dX = net.backward(dYd, input_grad=input_grad)
+    torch.cuda.synchronize()
+    Yg = Y.float().cpu().numpy()
+    dXg = dX.float().cpu().numpy() if input_grad else None
+    grads = {(l.layer_name, k): l.grads[k].float().cpu().numpy()
+             for l in all_layers(layers) for k in (l.grads or {})}
+    del Xd, dYd, Y, dX
+    Yt, dXt, gt = twin.run(X, dY, input_grad=input_grad)
+    return (Yg, dXg, grads), (Yt, dXt, gt), twin, net
+
+
+def _check(got, want, twin, layers):
+    (Yg, dXg, gg), (Yt, dXt, gt) = got, want
+    assert rel_err(Yg, Yt) <= TOL, ("Y", rel_err(Yg, Yt))
+    if dXg is not None:
+        assert rel_err(dXg, dXt) <= TOL, ("dX", rel_err(dXg, dXt))
+    bad = []
+    for (name, k), w in gt.items():
+        g = gg[(name, k)].reshape(w.shape).astype(np.float64)
+        err = np.linalg.norm((g - w).ravel())
+        bound = TOL * np.linalg.norm(w.ravel())
+        if name in twin.bn_l1:
+            bound = max(bound, 1e-6 * float(torch.linalg.norm(twin.bn_l1[name])))
+        if err > bound:
+            bad.append((name, k, err, bound, rel_err(g, w)))
+    assert not bad, bad
+    # running statistics (first batch: running mean = batch mean, running std = batch std)
+    for l in TorchTwin._all(layers):
+        if l.layer_name in twin.bn_stats:
+            m, s = twin.bn_stats[l.layer_name]
+            assert rel_err(l.non_learned_params["running_mean"].cpu().numpy().ravel(), m.numpy()) <= 1e-6
+            assert rel_err(l.non_learned_params["running_std"].cpu().numpy().ravel(), s.numpy()) <= 1e-6
+
+
+FUSED = ["dk_pwconv_fwd_ex_f32", "dk_pwconv_dgrad_bnbwd_f32", "dk_pwconv_wgrad_bnx_f32", "dk_dwconv_bwd_bnbwd_f32",
+         "dk_dwconv_fwd_ex_f32", "dk_bn_add_f32", "dk_relu_bwd_bn_partial_f64", "dk_conv2d_wgrad_bnbwd_f32",
+         "dk_conv2d_fwd_ex_f32", "dk_bn_stats_from_partials_f32", "dk_bn_bwd_from_partials_f32"]
+
+
+def test_res1_full_size(monkeypatch):
+    """pw0_bn + ReLU (applied on load by res1) and residual block res1 at 256 x 64 x 56 x 56:
+    P = 802,816 pixels per pointwise GEMM, the fused stride-1 depthwise backward, BN folds of
+    12,544 partial rows."""
+    from dorknet_amd._hip import lib
+    from examples.resnet18_depsep import ResNet18
+    np.random.seed(31)
+    layers = ResNet18("r18").layers[4:7]
+    rng = np.random.default_rng(32)
+    _perturb_bn(layers, rng)
+    assert lib.dk_pwconv_fwd_stats_rows(256, 56, 56, 64, 64) > 256
+    X = (0.5 + 2.0 * rng.standard_normal((256, 64, 56, 56), dtype=np.float32))
+    dY = rng.standard_normal((256, 64, 56, 56), dtype=np.float32)
+    calls = Calls(monkeypatch, FUSED)
+    got, want, twin, _ = _run(layers, X, dY, input_grad=True)
+    assert {"dk_pwconv_fwd_ex_f32", "dk_pwconv_dgrad_bnbwd_f32", "dk_pwconv_wgrad_bnx_f32",
+            "dk_dwconv_bwd_bnbwd_f32", "dk_dwconv_fwd_ex_f32", "dk_bn_add_f32",
+            "dk_relu_bwd_bn_partial_f64"} <= calls.seen, calls.seen
+    _check(got, want, twin, layers)
+
+
+def test_res7_res8_full_size(monkeypatch):
+    """res7 (stride-2 depthwise, 256 -> 512 pointwise, stride-2 skip projection with the fused
+    widen) and res8 (512 -> 512 pointwise at 7 x 7, P = 12,544) at batch 256."""
+    from examples.resnet18_depsep import ResNet18
+    np.random.seed(33)
+    layers = ResNet18("r18").layers[12:14]
+    rng = np.random.default_rng(34)
+    _perturb_bn(layers, rng)
+    X = np.abs(rng.standard_normal((256, 256, 14, 14), dtype=np.float32))   # a ReLU output
+    dY = rng.standard_normal((256, 512, 7, 7), dtype=np.float32)
+    calls = Calls(monkeypatch, FUSED)
+    got, want, twin, _ = _run(layers, X, dY, input_grad=True)
+    assert {"dk_pwconv_fwd_ex_f32", "dk_pwconv_dgrad_bnbwd_f32", "dk_pwconv_wgrad_bnx_f32"} <= calls.seen
+    _check(got, want, twin, layers)
+
+
+def test_stem_full_size(monkeypatch):
+    """conv0 (64 x 3 x 5 x 5, stride 2) + conv0_bn + ReLU + pw0 (stride 2) + pw0_bn + ReLU on
+    256 x 3 x 225 x 225: the stem weight gradient with conv0_bn's backward applied on load
+    (dk_conv2d_wgrad_bnbwd_f32; the image gradient is not computed, as in the network's
+    backward), conv0_bn folds of 25,088 partial rows."""
+    from examples.resnet18_depsep import ResNet18
+    np.random.seed(35)
+    layers = ResNet18("r18").layers[0:6]
+    rng = np.random.default_rng(36)
+    _perturb_bn(layers, rng)
+    X = rng.uniform(-128, 128, size=(256, 3, 225, 225)).astype(np.float32)
+    dY = rng.standard_normal((256, 64, 56, 56), dtype=np.float32)
+    calls = Calls(monkeypatch, FUSED)
+    got, want, twin, _ = _run(layers, X, dY, input_grad=False)
+    assert {"dk_conv2d_wgrad_bnbwd_f32", "dk_conv2d_fwd_ex_f32"} <= calls.seen, calls.seen
+    _check(got, want, twin, layers)
