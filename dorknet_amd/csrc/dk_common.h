@@ -170,4 +170,15 @@ enum : int { DK_ERR_ARGS = 10001, DK_ERR_WORKSPACE = 10002 };
 int splitk_reduce(const float* ws, int splits, int M, int N, float* out, const float* w, float l2, int mode, int C,
                   int Cp, int R, int S, hipStream_t st);
 
+// Streaming pointwise kernels (pw_stream.hip) for the K = C = 64 shapes.
+bool pw_stream_enabled();  // DORKNET_PW_STREAM (default 1; 0 = the tiled engine everywhere, for A/B runs)
+void pw_stream_set(int v);  // tuning knob (dk_debug_set_gemm_config kind 3)
+bool pw_stream_dgrad_ok(int K, int C, int M);
+int pw_stream_dgrad_rows(int M);
+int pw_stream_dgrad_bnbwd(const float* g, const float* bn_x, int M, const float* om, const float* ois,
+                          const float* og, const float* ob, int orelu, const float* k12, float* dy_out,
+                          const float* w, float* dx, const float* res, const float* x, const float* im,
+                          const float* iis, const float* ig, const float* ib, int irelu, double* part,
+                          hipStream_t st);
+
 }  // namespace dk

@@ -1199,6 +1199,10 @@ DK_API int dk_debug_set_gemm_config(int kind, int cfg) {
     g_fill_splits = cfg < 0 ? 1 : cfg;
     return 0;
   }
+  if (kind == 3) {  // streaming pointwise kernels (pw_stream.hip) on / off
+    pw_stream_set(cfg < 0 ? 1 : cfg);
+    return 0;
+  }
   if (kind < 0 || kind > 1) return -1;
   g_cfg_override[kind] = cfg;
   return kind == 0 ? kNumRowCfg : kNumSplitCfg;
@@ -1499,7 +1503,9 @@ DK_API int dk_pwconv_dgrad_f32(const float* dy, int N, int OH, int OW, int K, co
 
 DK_API int dk_pwconv_dgrad_stats_rows(int N, int OH, int OW, int K, int C) { return stats_rows(N * OH * OW, C, K); }
 DK_API int dk_pwconv_dgrad_bnbwd_stats_rows(int N, int OH, int OW, int K, int C) {
-  return stats_rows(N * OH * OW, C, K, kRowBnBwd);
+  const int M = N * OH * OW;
+  if (pw_stream_dgrad_ok(K, C, M)) return pw_stream_dgrad_rows(M);
+  return stats_rows(M, C, K, kRowBnBwd);
 }
 
 // dgrad + the BN-backward partial sums of the BatchNorm whose output this layer consumed
@@ -1576,6 +1582,13 @@ DK_API int dk_pwconv_dgrad_bnbwd_f32(const float* g, const float* bn_x, int N, i
   if (!vec_ok(b, 4, C) || K % 4 || !aligned16(g) || !aligned16(bn_x) || (dy_out && !aligned16(dy_out)) ||
       (size_t)K * 32 > 64 * 1024)
     return DK_ERR_ARGS;
+  if (pw_stream_dgrad_ok(K, C, M)) {
+    // K = C = 64: the persistent streaming kernel (pw_stream.hip), bit-identical results
+    if (part && !bn_ok(bn_mean, bn_invstd, bn_gamma, bn_beta)) return DK_ERR_ARGS;
+    return pw_stream_dgrad_bnbwd(g, bn_x, M, out_mean, out_invstd, out_gamma, out_beta, out_relu, k12, dy_out, w_kc,
+                                 dx, residual, part ? x : nullptr, bn_mean, bn_invstd, bn_gamma, bn_beta, bn_relu,
+                                 part, st);
+  }
   if (!part) {
     EpStore ep = ep_store(dx, C, nullptr, residual);
     return igemm_rows<LdMatKC, MatBwdDesc, LdMatIC, MatDesc, EpStore, kRowBnBwd>(a, b, ep, M, C, K, st);

@@ -1,0 +1,325 @@
+// Streaming pointwise kernels for the memory-bound 1x1 shapes (K = C = 64: res1/res2 of
+// ResNet-18-depsep, P = N*H*W = 802,816 pixels at batch 256).
+//
+// The general implicit-GEMM engine (gemm_f32.hip) stages every operand tile through LDS and
+// runs one block per 64-row tile: at K = 64 that is two K-tiles, a prologue and an epilogue
+// per 16 KB of input, and the block's dependent global round trips (operand loads, BN-table
+// fill, epilogue operand loads, stores) are exposed at 3-4 resident blocks per CU.  Here:
+//
+//   * persistent waves: a grid of (resident blocks x CUs) blocks of 4 waves; wave w streams
+//     row tiles w, w + W, w + 2W, ... (W = all waves) of 32 pixels each;
+//   * the MFMA A operand goes global -> registers directly (no LDS): lane (l32, h) loads the
+//     float4s k = 8q + 4h .. +3 of row l32 -- exactly its v_mfma_f32_32x32x2_f32 fragments, in
+//     the k order of gemm_f32.hip's engine (k = 8q + 4h + e), so results are bit-identical to
+//     it; the B operand (the weights, 16 KB) is loaded into LDS once per block;
+//   * software pipeline per wave: tile t+W's operand loads and tile t's epilogue operand loads
+//     are in flight while tile t's MFMAs run;
+//   * the epilogue works in the MFMA's C layout: each lane owns two output columns for the
+//     whole kernel, so the BatchNorm partial sums accumulate in registers across all of a
+//     wave's tiles and the kernel writes ONE partial row per block (gridDim.x rows instead of
+//     one per 64-pixel tile: the following fold reads 1/25th of the bytes).
+//
+// dk_pwconv_dgrad_bnbwd_f32 (the step's dominant entry point, layers/pointwise_convolution.py
+// :57-75 + layers/batch_norm.py:125-174): dx = dy . W (+ residual) with
+// dy = the following BatchNorm's backward applied to its gradient g on load (bn_bwd_elem,
+// bit-identical to dk_bn_bwd_apply_f32), dy written through for the weight gradient, and the
+// input BatchNorm's backward partial sums (sum g', sum g' x_hat) of dx.
+#include <stdlib.h>
+
+#include "dk_common.h"
+
+namespace dk {
+namespace pws {
+
+constexpr int KR = 64;          // reduction length (the pointwise layer's output channels K)
+constexpr int NO = 64;          // output columns (its input channels C)
+constexpr int WAVES = 4;        // waves per block
+constexpr int TR = 32;          // rows (pixels) per wave tile
+constexpr int SKB = KR + 4;     // LDS row stride of the B image Bs[n][k]: (KR+4)/4 odd -> conflict-free b128
+constexpr int KQ = KR / 8;      // float4 groups per lane per operand row
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+struct DgradArgs {
+  const float* g;     // [M][KR] gradient w.r.t. the following BN's (+ReLU) output
+  const float* xo;    // [M][KR] that BN's raw input (= this layer's output)
+  float* dy_out;      // [M][KR] dy write-through (nullable)
+  const float* w;     // [KR][NO] pointwise weights W[k][c]
+  float* dx;          // [M][NO]
+  const float* res;   // [M][NO] residual addend (nullable)
+  const float* xi;    // [M][NO] the input BN's raw input (nullable: no partials)
+  const float* om;    // following BN: mean, invstd, gamma, beta, k12 = [k1[KR], k2[KR]]
+  const float* ois;
+  const float* og;
+  const float* ob;
+  const float* k12;
+  int orelu;
+  const float* im;    // input BN (partials): mean, invstd, gamma, beta
+  const float* iis;
+  const float* ig;
+  const float* ib;
+  int irelu;
+  double* part;       // [gridDim.x][2][NO]
+  int M;
+};
+
+__device__ __forceinline__ uint32_t row_off_bytes(int m, int ld, int c) { return ((uint32_t)m * ld + c) * 4u; }
+// Every global access of the streaming kernels is a buffer access whose resource covers exactly
+// the tensor's M rows: rows >= M (the ragged last tile, the prefetch past the last tile) fall
+// outside it in hardware -- loads return 0, stores are dropped -- so the loop needs no
+// per-row conditions (which the compiler turns into control flow and conservative vmcnt(0)
+// waits) and each access is a base register plus an immediate offset.
+
+template <bool RES, bool PART>
+__global__ __launch_bounds__(256, 2) void dgrad_bnbwd_kernel(DgradArgs a) {
+  // B image: Bs[c][k] = W[k][c]; the following BN's per-channel table as 7 SoA rows
+  __shared__ float Bs[NO * SKB];
+  __shared__ float tab[7][KR];
+  __shared__ double red[WAVES][2][NO];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int l32 = lane & 31, h = lane >> 5;
+  for (int i = tid; i < KR * NO; i += 256) {
+    const int k = i / NO, c = i - k * NO;
+    Bs[c * SKB + k] = a.w[i];
+  }
+  for (int k = tid; k < KR; k += 256) {
+    const float is = a.ois[k], ga = a.og[k];
+    tab[0][k] = a.om[k];
+    tab[1][k] = is;
+    tab[2][k] = ga;
+    tab[3][k] = a.ob[k];
+    tab[4][k] = a.k12[k];
+    tab[5][k] = a.k12[KR + k];
+    tab[6][k] = ga * is;
+  }
+  // this lane's two output columns: the input BN's parameters for the partials
+  constexpr bool parts = PART;
+  const bool orelu = a.orelu != 0, irelu = a.irelu != 0;
+  float pm[2], pis[2], pga[2], pbe[2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int c = 32 * u + l32;
+    pm[u] = parts ? a.im[c] : 0.f;
+    pis[u] = parts ? a.iis[c] : 0.f;
+    pga[u] = parts ? a.ig[c] : 0.f;
+    pbe[u] = parts ? a.ib[c] : 0.f;
+  }
+  __syncthreads();
+
+  const uint32_t kbytes = (uint32_t)a.M * KR * 4u, nbytes = (uint32_t)a.M * NO * 4u;
+  const __amdgpu_buffer_rsrc_t rg = make_rsrc_v(a.g, kbytes), rx = make_rsrc_v(a.xo, kbytes);
+  const __amdgpu_buffer_rsrc_t rxi = make_rsrc_v(PART ? a.xi : a.g, PART ? nbytes : 0u);
+  const __amdgpu_buffer_rsrc_t rr = make_rsrc_v(RES ? a.res : a.g, RES ? nbytes : 0u);
+  const __amdgpu_buffer_rsrc_t rdx = make_rsrc_v(a.dx, nbytes);
+  // no dy_out: a zero-size resource, every store dropped
+  const __amdgpu_buffer_rsrc_t rdy = make_rsrc_v(a.dy_out ? a.dy_out : a.dx, a.dy_out ? kbytes : 0u);
+  const int ntiles = (a.M + TR - 1) / TR;
+  const int W = gridDim.x * WAVES;
+  int t = blockIdx.x * WAVES + wave;
+
+  double ps[2] = {0.0, 0.0}, pq[2] = {0.0, 0.0};
+  // A operands (raw g, x of the following BN) of a tile: lane (l32, h) reads row l32's float4s
+  // k = 8q + 4h .. +3; rows >= M (incl. tiles past the end) read zeros
+  auto load_a = [&](int tile, f32x4* lg, f32x4* lx) {
+    const int m = tile * TR + l32;
+    const uint32_t base = row_off_bytes(m, KR, 4 * h);
+#pragma unroll
+    for (int q = 0; q < KQ; ++q) {
+      lg[q] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rg, (int)(base + 32u * q), 0, 0));
+      lx[q] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rx, (int)(base + 32u * q), 0, 0));
+    }
+  };
+  f32x4 cg[KQ], cx[KQ];  // this tile's raw A operands (loaded one iteration ahead)
+  load_a(t, cg, cx);
+  for (; t < ntiles; t += W) {
+    const int m0 = t * TR;
+    // an opaque zero: keeps the (loop-invariant) LDS table and weight reads inside the loop,
+    // where they cost a few LDS cycles, instead of hoisted into ~290 long-lived registers
+    int z = 0;
+    asm volatile("" : "+s"(z));
+    const float* tb = &tab[0][0] + z;
+    const float* bs = Bs + z;
+
+    // (1) issue: tile t's epilogue operands (C layout: column 32u + l32, rows (r&3) + 8(r>>2) + 4h),
+    //     then tile t+W's A operands -- in flight during this tile's transform and MFMAs
+    float exi[2][16], ers[2][16];
+    const int mb = m0 + 4 * h;
+    // rows (r&3) + 8(r>>2) of the lane half: two base registers (r < 8, r >= 8), the rest in
+    // the 12-bit immediate offset
+    const uint32_t eb0 = row_off_bytes(mb, NO, l32), eb1 = eb0 + 16u * NO * 4u;
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const uint32_t imm = (uint32_t)(((r & 3) + 8 * ((r >> 2) & 1)) * NO + 32 * u) * 4u;
+        const uint32_t eb = r < 8 ? eb0 : eb1;
+        if constexpr (PART)
+          exi[u][r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rxi, (int)eb, (int)imm, 0));
+        if constexpr (RES)
+          ers[u][r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rr, (int)eb, (int)imm, 0));
+      }
+    f32x4 ng[KQ], nx[KQ];
+    load_a(t + W, ng, nx);
+    __builtin_amdgcn_sched_barrier(0);
+
+    // (2) dy = the following BN's backward applied to g (bit-identical to dk_bn_bwd_apply_f32),
+    //     written through for the weight gradient
+    f32x4 af[KQ];
+#pragma unroll
+    for (int q = 0; q < KQ; ++q) {
+      const int k0 = 8 * q + 4 * h;
+      const f32x4 mu = ld4(tb + 0 * KR + k0), is = ld4(tb + 1 * KR + k0), ga = ld4(tb + 2 * KR + k0),
+                  be = ld4(tb + 3 * KR + k0);
+      const f32x4 k1 = ld4(tb + 4 * KR + k0), k2 = ld4(tb + 5 * KR + k0), f = ld4(tb + 6 * KR + k0);
+      f32x4 o;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float xe = cx[q][e];
+        float ge = cg[q][e];
+        // branch-free ReLU mask (a branch on the uniform flag would split the loop into blocks
+        // with conservative vmcnt(0) waits)
+        const bool kill = (!(bn_out(xe, mu[e], is[e], ga[e], be[e]) > 0.f)) & orelu;
+        ge = kill ? 0.f : ge;
+        o[e] = bn_bwd_elem(xe, ge, mu[e], is[e], f[e], k1[e], k2[e]);
+      }
+      af[q] = o;
+    }
+    {
+      const int mrow = m0 + l32;
+      const uint32_t dbase = row_off_bytes(mrow, KR, 4 * h);
+#pragma unroll
+      for (int q = 0; q < KQ; ++q)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, af[q]), rdy, (int)dbase, 32 * q, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+
+    // (3) dx tile = dy . W : 32 rows x 64 columns, k order 8q + 4h + e as gemm_f32.hip
+    f32x16 acc[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[u][r] = 0.f;
+#pragma unroll
+    for (int q = 0; q < KQ; ++q) {
+      f32x4 bf[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) bf[u] = ld4(bs + (32 * u + l32) * SKB + 8 * q + 4 * h);
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int u = 0; u < 2; ++u) acc[u] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[q][e], bf[u][e], acc[u], 0, 0, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+
+    // (4) epilogue: dx (+ residual), and the input BN's partial sums of what is stored
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int dm = (r & 3) + 8 * (r >> 2);
+        const uint32_t imm = (uint32_t)(((r & 3) + 8 * ((r >> 2) & 1)) * NO + 32 * u) * 4u;
+        float v = acc[u][r];
+        if constexpr (RES) v += ers[u][r];
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), rdx, (int)(r < 8 ? eb0 : eb1),
+                                              (int)imm, 0);
+        if constexpr (PART) {
+          const float x = exi[u][r];
+          const float xh = (x - pm[u]) * pis[u];
+          float gv = v;
+          const bool kill = ((!(bn_out(x, pm[u], pis[u], pga[u], pbe[u]) > 0.f)) & irelu) | (mb + dm >= a.M);
+          gv = kill ? 0.f : gv;  // rows past M contribute nothing
+          ps[u] += (double)gv;
+          pq[u] += (double)gv * (double)xh;
+        }
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < KQ; ++q) {
+      cg[q] = ng[q];
+      cx[q] = nx[q];
+    }
+  }
+  if constexpr (!PART) return;
+  // the block's partial row: lane halves, then the 4 waves in order
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    ps[u] += __shfl_xor(ps[u], 32, 64);
+    pq[u] += __shfl_xor(pq[u], 32, 64);
+    if (h == 0) {
+      red[wave][0][32 * u + l32] = ps[u];
+      red[wave][1][32 * u + l32] = pq[u];
+    }
+  }
+  __syncthreads();
+  if (tid < 2 * NO) {
+    const int which = tid / NO, c = tid - which * NO;
+    double s = 0.0;
+#pragma unroll
+    for (int w = 0; w < WAVES; ++w) s += red[w][which][c];
+    a.part[((size_t)blockIdx.x * 2 + which) * NO + c] = s;
+  }
+}
+
+// Blocks of the persistent grid: every resident slot once (queried once), at most one
+// block per 4 tiles.
+int dgrad_blocks(int M) {
+  static int occ = -1;
+  if (occ < 0) {
+    // every instantiation is built for 2 waves per SIMD (launch bounds); take the smallest
+    int o = 1 << 20;
+    const void* fs[] = {reinterpret_cast<const void*>(&dgrad_bnbwd_kernel<false, false>),
+                        reinterpret_cast<const void*>(&dgrad_bnbwd_kernel<false, true>),
+                        reinterpret_cast<const void*>(&dgrad_bnbwd_kernel<true, false>),
+                        reinterpret_cast<const void*>(&dgrad_bnbwd_kernel<true, true>)};
+    for (const void* f : fs) {
+      int v = 0;
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, f, 256, 0) != hipSuccess || v < 1) v = 1;
+      o = v < o ? v : o;
+    }
+    occ = o;
+  }
+  const int ntiles = (M + TR - 1) / TR;
+  const int want = (ntiles + WAVES - 1) / WAVES;
+  const int slots = occ * 256;
+  return want < slots ? (want > 0 ? want : 1) : slots;
+}
+
+}  // namespace pws
+
+static int g_pw_stream = -1;  // -1: from DORKNET_PW_STREAM (default on); dk_debug_set_gemm_config(3, v)
+void pw_stream_set(int v) { g_pw_stream = v; }
+bool pw_stream_enabled() {
+  if (g_pw_stream < 0) {
+    const char* e = getenv("DORKNET_PW_STREAM");
+    g_pw_stream = (e && e[0] == '0') ? 0 : 1;
+  }
+  return g_pw_stream == 1;
+}
+
+// Shapes the streaming dgrad takes (the rest go to the tiled engine).
+bool pw_stream_dgrad_ok(int K, int C, int M) {
+  if (!pw_stream_enabled()) return false;
+  return K == pws::KR && C == pws::NO && M > 0 && (size_t)M * 64 * 4 < ((size_t)1 << 31);
+}
+
+int pw_stream_dgrad_rows(int M) { return pws::dgrad_blocks(M); }
+
+int pw_stream_dgrad_bnbwd(const float* g, const float* bn_x, int M, const float* om, const float* ois,
+                          const float* og, const float* ob, int orelu, const float* k12, float* dy_out,
+                          const float* w, float* dx, const float* res, const float* x, const float* im,
+                          const float* iis, const float* ig, const float* ib, int irelu, double* part,
+                          hipStream_t st) {
+  pws::DgradArgs a{g, bn_x, dy_out, w, dx, res, x, om, ois, og, ob, k12, orelu, im, iis, ig, ib, irelu, part, M};
+  const dim3 grid(pws::dgrad_blocks(M));
+  if (res && x)
+    hipLaunchKernelGGL((pws::dgrad_bnbwd_kernel<true, true>), grid, dim3(256), 0, st, a);
+  else if (res)
+    hipLaunchKernelGGL((pws::dgrad_bnbwd_kernel<true, false>), grid, dim3(256), 0, st, a);
+  else if (x)
+    hipLaunchKernelGGL((pws::dgrad_bnbwd_kernel<false, true>), grid, dim3(256), 0, st, a);
+  else
+    hipLaunchKernelGGL((pws::dgrad_bnbwd_kernel<false, false>), grid, dim3(256), 0, st, a);
+  return launch_status();
+}
+
+}  // namespace dk

@@ -51,7 +51,9 @@ int dk_mixup_f32(const float* a, const float* b, long long n, float p, float one
  * `cfg` for kind 0 = forward/dgrad problems or 1 = split-K weight-gradient problems;
  * cfg = -1 restores the built-in heuristic.  Returns the number of configurations.
  * kind 2: split-K grids sized to one round of resident blocks (1 = default, also for -1) or
- * the fixed ~1024-block split (0); returns 0. */
+ * the fixed ~1024-block split (0); returns 0.
+ * kind 3: the streaming pointwise kernels for K = C = 64 (1 = default, also for -1; 0 = the
+ * tiled engine for every shape, as DORKNET_PW_STREAM=0); returns 0. */
 int dk_debug_set_gemm_config(int kind, int cfg);
 /* Tuning knob (same caveats): launch variant of dk_bn_bwd_apply_f32 (bits 0-1: rows in flight
  * 4/8 x plain/nontemporal stores; bits 2-3: rows per lane 16/8/32/64; bit 4: block cap 16384);

@@ -24,22 +24,27 @@ import torch
 import torch.nn.functional as F
 
 
-def _np(v):
+def _np(v, dtype=np.float64):
     if isinstance(v, torch.Tensor):
         v = v.detach().cpu().numpy()
-    return np.asarray(v, dtype=np.float64)
+    return np.asarray(v, dtype=dtype)
 
 
 class TorchTwin:
-    def __init__(self, layers):
+    """dtype float64: the checker; float32: the same maths in fp32, whose distance from the
+    fp64 twin measures the problem's own fp32 conditioning (at batch 256, ReLU masks of
+    elements within an ulp of the threshold flip between any two fp32 pipelines)."""
+
+    def __init__(self, layers, dtype=np.float64):
         self.layers = layers
+        self.dtype = dtype
         self.params = {}      # (layer_name, key) -> leaf float64 tensor
         self.l2 = {}          # layer_name -> strength
         self.bn_l1 = {}       # bn layer_name -> per-channel sum |dL/dy|
         self.bn_stats = {}    # bn layer_name -> (mean, std)
         for l in self._all(layers):
             for k, v in (l.learned_params or {}).items():
-                self.params[(l.layer_name, k)] = torch.tensor(_np(v), requires_grad=True)
+                self.params[(l.layer_name, k)] = torch.tensor(_np(v, dtype), requires_grad=True)
             reg = getattr(l, "weight_regulariser", None)
             if reg is not None:
                 self.l2[l.layer_name] = float(reg.strength)
@@ -116,15 +121,16 @@ class TorchTwin:
     def run(self, X, dY, input_grad=True):
         """Forward on X (numpy/tensor), backward of dY; returns (Y, dX or None, grads) with
         grads[(layer_name, key)] including the l2 term."""
-        x = torch.tensor(_np(X), requires_grad=input_grad)
+        x = torch.tensor(_np(X, self.dtype), requires_grad=input_grad)
         h = x
         for l in self.layers:
             h = self._layer(l, h)
-        h.backward(torch.as_tensor(_np(dY)))
+        h.backward(torch.as_tensor(_np(dY, self.dtype)))
         grads = {}
         for (name, k), p in self.params.items():
             g = p.grad.detach().clone() if p.grad is not None else torch.zeros_like(p)
             if k == "weights" and name in self.l2:
                 g = g + self.l2[name] * p.detach()
-            grads[(name, k)] = g.numpy()
-        return h.detach().numpy(), (x.grad.numpy() if input_grad else None), grads
+            grads[(name, k)] = g.numpy().astype(np.float64)
+        return (h.detach().numpy().astype(np.float64), (x.grad.numpy().astype(np.float64) if input_grad else None),
+                grads)

@@ -9,7 +9,12 @@ P = 802,816 pixels, the fused depthwise backward at res1's 256 x 64 x 56 x 56, a
 weight gradient with conv0_bn's backward on load at 256 x 3 x 225 x 225.  Each test also
 records which C-ABI entry points ran, so it fails if a fusion stops being taken.
 
-Tolerance: normwise relative 1e-4 for outputs, input and weight gradients.  A
+Tolerance: normwise relative 1e-4 for outputs, input and weight gradients, or
+10x the error of the same maths evaluated in fp32 (the twin in float32, an independent fp32
+pipeline) where that is larger.  At batch 256 the fp32 error itself reaches ~6e-4 on some
+gradients: tens of millions of BN outputs per layer put a few within an ulp of the ReLU
+threshold, and their masks flip between any two fp32 pipelines (measured: scripts/diag_fullsize.py,
+profiles/r02_fullsize_conditioning.txt; at batch 16 every gradient agrees to ~1e-6).  A
 BatchNorm whose output feeds a pointwise layer and another BatchNorm has dbeta = 0 in exact
 arithmetic (the later BN's backward sums to zero); such sums are bounded by 1e-6 of their l1
 scale sum|g| (fp64 partials on the GPU: far below fp32 summation error).
@@ -66,23 +71,38 @@ def _run(layers, X, dY, input_grad):
              for l in all_layers(layers) for k in (l.grads or {})}
     del Xd, dYd, Y, dX
     Yt, dXt, gt = twin.run(X, dY, input_grad=input_grad)
-    return (Yg, dXg, grads), (Yt, dXt, gt), twin, net
+    twin32 = TorchTwin(layers, np.float32)
+    Y32, dX32, g32 = twin32.run(X, dY, input_grad=input_grad)
+    return (Yg, dXg, grads), (Yt, dXt, gt), (Y32, dX32, g32), twin, net
 
 
-def _check(got, want, twin, layers):
-    (Yg, dXg, gg), (Yt, dXt, gt) = got, want
-    assert rel_err(Yg, Yt) <= TOL, ("Y", rel_err(Yg, Yt))
+def _bound(w, w32, extra=0.0):
+    w = np.asarray(w, np.float64)
+    return max(TOL * np.linalg.norm(w.ravel()), 10 * np.linalg.norm((np.asarray(w32) - w).ravel()), extra)
+
+
+def _check(got, want, fp32, twin, layers):
+    (Yg, dXg, gg), (Yt, dXt, gt), (Y32, dX32, g32) = got, want, fp32
+    errs = {}
+    e = np.linalg.norm((Yg - Yt).ravel())
+    assert e <= _bound(Yt, Y32), ("Y", rel_err(Yg, Yt), rel_err(Y32, Yt))
+    errs["Y"] = (rel_err(Yg, Yt), rel_err(Y32, Yt))
     if dXg is not None:
-        assert rel_err(dXg, dXt) <= TOL, ("dX", rel_err(dXg, dXt))
+        e = np.linalg.norm((dXg - dXt).ravel())
+        assert e <= _bound(dXt, dX32), ("dX", rel_err(dXg, dXt), rel_err(dX32, dXt))
+        errs["dX"] = (rel_err(dXg, dXt), rel_err(dX32, dXt))
     bad = []
     for (name, k), w in gt.items():
         g = gg[(name, k)].reshape(w.shape).astype(np.float64)
         err = np.linalg.norm((g - w).ravel())
-        bound = TOL * np.linalg.norm(w.ravel())
-        if name in twin.bn_l1:
-            bound = max(bound, 1e-6 * float(torch.linalg.norm(twin.bn_l1[name])))
+        extra = 1e-6 * float(torch.linalg.norm(twin.bn_l1[name])) if name in twin.bn_l1 else 0.0
+        bound = _bound(w, g32[(name, k)].reshape(w.shape), extra)
+        errs[(name, k)] = (rel_err(g, w), rel_err(g32[(name, k)].reshape(w.shape), w))
         if err > bound:
             bad.append((name, k, err, bound, rel_err(g, w)))
+    print("errors (GPU vs fp64 twin, fp32 twin vs fp64 twin):")
+    for k, (a, b) in errs.items():
+        print("  {:40s} {:.3e} {:.3e}".format(str(k), a, b))
     assert not bad, bad
     # running statistics (first batch: running mean = batch mean, running std = batch std)
     for l in TorchTwin._all(layers):
@@ -111,11 +131,11 @@ def test_res1_full_size(monkeypatch):
     X = (0.5 + 2.0 * rng.standard_normal((256, 64, 56, 56), dtype=np.float32))
     dY = rng.standard_normal((256, 64, 56, 56), dtype=np.float32)
     calls = Calls(monkeypatch, FUSED)
-    got, want, twin, _ = _run(layers, X, dY, input_grad=True)
+    got, want, f32, twin, _ = _run(layers, X, dY, input_grad=True)
     assert {"dk_pwconv_fwd_ex_f32", "dk_pwconv_dgrad_bnbwd_f32", "dk_pwconv_wgrad_bnx_f32",
             "dk_dwconv_bwd_bnbwd_f32", "dk_dwconv_fwd_ex_f32", "dk_bn_add_f32",
             "dk_relu_bwd_bn_partial_f64"} <= calls.seen, calls.seen
-    _check(got, want, twin, layers)
+    _check(got, want, f32, twin, layers)
 
 
 def test_res7_res8_full_size(monkeypatch):
@@ -129,9 +149,9 @@ def test_res7_res8_full_size(monkeypatch):
     X = np.abs(rng.standard_normal((256, 256, 14, 14), dtype=np.float32))   # a ReLU output
     dY = rng.standard_normal((256, 512, 7, 7), dtype=np.float32)
     calls = Calls(monkeypatch, FUSED)
-    got, want, twin, _ = _run(layers, X, dY, input_grad=True)
+    got, want, f32, twin, _ = _run(layers, X, dY, input_grad=True)
     assert {"dk_pwconv_fwd_ex_f32", "dk_pwconv_dgrad_bnbwd_f32", "dk_pwconv_wgrad_bnx_f32"} <= calls.seen
-    _check(got, want, twin, layers)
+    _check(got, want, f32, twin, layers)
 
 
 def test_stem_full_size(monkeypatch):
@@ -147,6 +167,6 @@ def test_stem_full_size(monkeypatch):
     X = rng.uniform(-128, 128, size=(256, 3, 225, 225)).astype(np.float32)
     dY = rng.standard_normal((256, 64, 56, 56), dtype=np.float32)
     calls = Calls(monkeypatch, FUSED)
-    got, want, twin, _ = _run(layers, X, dY, input_grad=False)
+    got, want, f32, twin, _ = _run(layers, X, dY, input_grad=False)
     assert {"dk_conv2d_wgrad_bnbwd_f32", "dk_conv2d_fwd_ex_f32"} <= calls.seen, calls.seen
-    _check(got, want, twin, layers)
+    _check(got, want, f32, twin, layers)

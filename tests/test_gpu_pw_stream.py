@@ -1,0 +1,68 @@
+"""The streaming pointwise kernels (csrc/pw_stream.hip, K = C = 64) against the tiled engine
+they replace: dk_pwconv_dgrad_bnbwd_f32 == dk_bn_bwd_apply_f32 -> dk_pwconv_dgrad_ex_f32
+bitwise for dx and the written-through dy (same MFMA k order), the input BatchNorm's partial
+sums to fp64 rounding (one partial row per persistent block instead of one per tile); ragged
+pixel counts, every epilogue option, and a large grid (several tiles per wave)."""
+import numpy as np
+import pytest
+import torch
+
+from dorknet_amd._hip import lib, stream_handle
+
+pytestmark = pytest.mark.gpu
+
+
+def nhwc(a):
+    return torch.as_tensor(np.ascontiguousarray(a, dtype=np.float32), device="cuda").contiguous(
+        memory_format=torch.channels_last)
+
+
+def bn_params(C, rng):
+    return [torch.as_tensor(v.astype(np.float32), device="cuda") for v in
+            (rng.randn(C) * 0.3, rng.rand(C) + 0.5, 1 + 0.3 * rng.randn(C), 0.2 * rng.randn(C))]
+
+
+@pytest.mark.parametrize("relu,bn_in,resid,N,H,W", [(1, True, False, 3, 13, 11), (0, True, False, 2, 8, 8),
+                                                    (1, False, True, 3, 13, 11), (1, True, True, 5, 7, 9),
+                                                    (0, False, False, 1, 1, 3), (1, True, False, 64, 56, 56)])
+def test_stream_dgrad_bnbwd_matches_tiled_engine(relu, bn_in, resid, N, H, W):
+    K = C = 64
+    rng = np.random.RandomState(relu + 2 * bn_in + 4 * resid + N)
+    xo = nhwc(rng.randn(N, K, H, W))
+    g = nhwc(rng.randn(N, K, H, W))
+    po = bn_params(K, rng)
+    k12 = torch.as_tensor(rng.randn(2 * K).astype(np.float32) * 0.1, device="cuda")
+    w = torch.as_tensor(rng.randn(K, C).astype(np.float32), device="cuda")
+    xin = nhwc(rng.randn(N, C, H, W))
+    pi = bn_params(C, rng)
+    res = nhwc(rng.randn(N, C, H, W)) if resid else None
+    st = stream_handle()
+    # reference: the tiled engine (streaming kernels off)
+    lib.dk_debug_set_gemm_config(3, 0)
+    try:
+        dy0 = torch.empty_like(g)
+        lib.dk_bn_bwd_apply_f32(xo.data_ptr(), g.data_ptr(), g.numel(), K, *(t.data_ptr() for t in po), relu,
+                                k12.data_ptr(), dy0.data_ptr(), st)
+        dx0 = torch.empty_like(xin)
+        rows0 = lib.dk_pwconv_dgrad_stats_rows(N, H, W, K, C)
+        part0 = torch.zeros((rows0, 2, C), dtype=torch.float64, device="cuda")
+        bn_args = (xin.data_ptr(), *(t.data_ptr() for t in pi), 1, part0.data_ptr()) if bn_in else (0,) * 7
+        assert lib.dk_pwconv_dgrad_ex_f32(dy0.data_ptr(), N, H, W, K, w.data_ptr(), C, 1, dx0.data_ptr(),
+                                          res.data_ptr() if resid else 0, *bn_args, st) == 0
+    finally:
+        lib.dk_debug_set_gemm_config(3, -1)
+    rows1 = lib.dk_pwconv_dgrad_bnbwd_stats_rows(N, H, W, K, C)
+    dy1 = torch.full_like(g, float("nan"))
+    dx1 = torch.full_like(xin, float("nan"))
+    part1 = torch.full((rows1, 2, C), float("nan"), dtype=torch.float64, device="cuda")
+    bn_args = (xin.data_ptr(), *(t.data_ptr() for t in pi), 1, part1.data_ptr()) if bn_in else (0,) * 7
+    assert lib.dk_pwconv_dgrad_bnbwd_f32(g.data_ptr(), xo.data_ptr(), N, H, W, K, *(t.data_ptr() for t in po), relu,
+                                         k12.data_ptr(), dy1.data_ptr(), w.data_ptr(), C, dx1.data_ptr(),
+                                         res.data_ptr() if resid else 0, *bn_args, st) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(dy0, dy1)
+    assert torch.equal(dx0, dx1)
+    if bn_in:
+        assert rows1 < max(rows0, 2) or N * H * W <= 128  # one row per persistent block
+        s0, s1 = part0.sum(0), part1.sum(0)
+        assert float((s1 - s0).norm() / s0.norm()) < 1e-12
