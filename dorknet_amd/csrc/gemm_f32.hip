@@ -1470,13 +1470,22 @@ DK_API int dk_pwconv_fwd_bnx_f32(const float* x, int N, int H, int W, int C, con
                   w_kc, K, C, bias, y, stream);
 }
 
-DK_API int dk_pwconv_fwd_stats_rows(int N, int OH, int OW, int K, int C) { return stats_rows(N * OH * OW, K, C); }
+DK_API int dk_pwconv_fwd_stats_rows(int N, int OH, int OW, int K, int C) {
+  const int M = N * OH * OW;
+  // (the input extent does not change the choice for the shapes the network uses)
+  if (pw_stream_fwd_ok(K, C, M, 0)) return pw_stream_fwd_rows(M);
+  return stats_rows(M, K, C);
+}
 
 DK_API int dk_pwconv_fwd_ex_f32(const float* x, int N, int H, int W, int C, const float* w_kc, int K, int stride,
                                 const float* bias, float* y, int OH, int OW, const float* bn_mean,
                                 const float* bn_invstd, const float* bn_gamma, const float* bn_beta, int bn_relu,
                                 double* stats, void* stream) {
   if (C % 4 || !aligned16(x) || !aligned16(w_kc) || !fits((size_t)N * H * W * C * 4)) return DK_ERR_ARGS;
+  if (pw_stream_fwd_ok(K, C, N * OH * OW, (size_t)N * H * W * C * 4) && (!bn_mean || bn_ok(bn_mean, bn_invstd, bn_gamma, bn_beta)))
+    // K = C = 64: the persistent streaming kernel (pw_stream.hip), bit-identical outputs
+    return pw_stream_fwd(x, N, H, W, stride, OH, OW, w_kc, bias, y, bn_mean, bn_invstd, bn_gamma, bn_beta, bn_relu,
+                         stats, as_stream(stream));
   return conv_fwd_ex(img1(x, N, H, W, C, OH, OW, stride, N * OH * OW), w_kc, K, C, bias, y, bn_mean,
                      bn_invstd, bn_gamma, bn_beta, bn_relu, stats, stream);
 }

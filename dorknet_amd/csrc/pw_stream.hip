@@ -260,28 +260,217 @@ __global__ __launch_bounds__(256, 2) void dgrad_bnbwd_kernel(DgradArgs a) {
   }
 }
 
-// Blocks of the persistent grid: every resident slot once (queried once), at most one
-// block per 4 tiles.
-int dgrad_blocks(int M) {
-  static int occ = -1;
-  if (occ < 0) {
-    // every instantiation is built for 2 waves per SIMD (launch bounds); take the smallest
-    int o = 1 << 20;
-    const void* fs[] = {reinterpret_cast<const void*>(&dgrad_bnbwd_kernel<false, false>),
-                        reinterpret_cast<const void*>(&dgrad_bnbwd_kernel<false, true>),
-                        reinterpret_cast<const void*>(&dgrad_bnbwd_kernel<true, false>),
-                        reinterpret_cast<const void*>(&dgrad_bnbwd_kernel<true, true>)};
-    for (const void* f : fs) {
-      int v = 0;
-      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, f, 256, 0) != hipSuccess || v < 1) v = 1;
-      o = v < o ? v : o;
-    }
-    occ = o;
+
+// ---------------------------------------------------------------------------------------
+// dk_pwconv_fwd_ex_f32 (layers/pointwise_convolution.py:46-55 with the preceding BatchNorm(+ReLU)
+// applied on load and the following BatchNorm's statistics emitted): y = bn(x) . W^T (+ bias),
+// sa = 2: the reference's X[:, :, ::2, ::2] subsampling as a strided row map.  A operand lane
+// (l32, h): bn_relu_out of x[row l32][c = 8q + 4h .. +3] (bit-identical to the tiled engine's
+// LdImgKC with its LDS parameter table); B image Bs[k][c] = W[k][c] as stored.
+// ---------------------------------------------------------------------------------------
+struct FwdArgs {
+  const float* x;     // [N*H*W][KR] raw input (the preceding BN's input when bn)
+  const float* w;     // [NO][KR]
+  const float* bias;  // [NO] nullable
+  float* y;           // [M][NO], M = N*OH*OW
+  const float* im;    // input BN: mean, invstd, gamma, beta (im == nullptr: no transform)
+  const float* iis;
+  const float* ig;
+  const float* ib;
+  int irelu;
+  double* part;       // [gridDim.x][2][NO] (sum y, sum y^2) nullable
+  int M, H, W, OH, OW, sa;
+  uint32_t xbytes;
+};
+
+template <bool BN, bool STATS, bool STRIDED>
+__global__ __launch_bounds__(256, 3) void fwd_kernel(FwdArgs a) {
+  __shared__ float Bs[NO * SKB];
+  __shared__ float tab[4][KR];
+  __shared__ double red[WAVES][2][NO];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int l32 = lane & 31, h = lane >> 5;
+  for (int i = tid; i < KR * NO; i += 256) {
+    const int n = i / KR, k = i - n * KR;
+    Bs[n * SKB + k] = a.w[i];
   }
+  if constexpr (BN) {
+    for (int c = tid; c < KR; c += 256) {
+      tab[0][c] = a.im[c];
+      tab[1][c] = a.iis[c];
+      tab[2][c] = a.ig[c];
+      tab[3][c] = a.ib[c];
+    }
+  }
+  float bias[2] = {0.f, 0.f};
+  if (a.bias) {
+    bias[0] = a.bias[l32];
+    bias[1] = a.bias[32 + l32];
+  }
+  const bool irelu = a.irelu != 0;
+  __syncthreads();
+
+  const uint32_t nbytes = (uint32_t)a.M * NO * 4u;
+  const __amdgpu_buffer_rsrc_t rx = make_rsrc_v(a.x, a.xbytes), ry = make_rsrc_v(a.y, nbytes);
+  const int ntiles = (a.M + TR - 1) / TR;
+  const int W = gridDim.x * WAVES;
+  int t = blockIdx.x * WAVES + wave;
+  double ps[2] = {0.0, 0.0}, pq[2] = {0.0, 0.0};
+
+  auto load_a = [&](int tile, f32x4* lx) {
+    const int m = tile * TR + l32;
+    int row = m;
+    if constexpr (STRIDED) {
+      // output pixel (n, oh, ow) reads input pixel (n, sa*oh, sa*ow); rows past M read past the
+      // buffer (zeros): n >= N maps beyond N*H*W
+      const int ow = m % a.OW, q = m / a.OW, oh = q % a.OH, n = q / a.OH;
+      row = (n * a.H + oh * a.sa) * a.W + ow * a.sa;
+    }
+    const uint32_t base = row_off_bytes(row, KR, 4 * h);
+#pragma unroll
+    for (int q = 0; q < KQ; ++q)
+      lx[q] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rx, (int)base, 32 * q, 0));
+  };
+  f32x4 cx[KQ];
+  load_a(t, cx);
+  for (; t < ntiles; t += W) {
+    const int m0 = t * TR;
+    int z = 0;
+    asm volatile("" : "+s"(z));
+    const float* tb = &tab[0][0] + z;
+    const float* bs = Bs + z;
+
+    f32x4 nx[KQ];
+    load_a(t + W, nx);
+    __builtin_amdgcn_sched_barrier(0);
+
+    f32x4 af[KQ];
+#pragma unroll
+    for (int q = 0; q < KQ; ++q) {
+      f32x4 v = cx[q];
+      if constexpr (BN) {
+        const int k0 = 8 * q + 4 * h;
+        const f32x4 mu = ld4(tb + 0 * KR + k0), is = ld4(tb + 1 * KR + k0), ga = ld4(tb + 2 * KR + k0),
+                    be = ld4(tb + 3 * KR + k0);
+        // rows past M hold zeros, transformed like any other: their outputs are never stored
+        // and are masked out of the statistics
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float r = bn_out(v[e], mu[e], is[e], ga[e], be[e]);
+          v[e] = (irelu & !(r > 0.f)) ? 0.f : r;
+        }
+      }
+      af[q] = v;
+    }
+    __builtin_amdgcn_sched_barrier(0);
+
+    f32x16 acc[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[u][r] = 0.f;
+#pragma unroll
+    for (int q = 0; q < KQ; ++q) {
+      f32x4 bf[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) bf[u] = ld4(bs + (32 * u + l32) * SKB + 8 * q + 4 * h);
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int u = 0; u < 2; ++u) acc[u] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[q][e], bf[u][e], acc[u], 0, 0, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+
+    const int mb = m0 + 4 * h;
+    const uint32_t eb0 = row_off_bytes(mb, NO, l32), eb1 = eb0 + 16u * NO * 4u;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int dm = (r & 3) + 8 * (r >> 2);
+        const uint32_t imm = (uint32_t)(((r & 3) + 8 * ((r >> 2) & 1)) * NO + 32 * u) * 4u;
+        float v = acc[u][r];
+        if (a.bias) v += bias[u];
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), ry, (int)(r < 8 ? eb0 : eb1),
+                                              (int)imm, 0);
+        if constexpr (STATS) {
+          const double d = (mb + dm < a.M) ? (double)v : 0.0;
+          ps[u] += d;
+          pq[u] += d * d;
+        }
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < KQ; ++q) cx[q] = nx[q];
+  }
+  if constexpr (!STATS) return;
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    ps[u] += __shfl_xor(ps[u], 32, 64);
+    pq[u] += __shfl_xor(pq[u], 32, 64);
+    if (h == 0) {
+      red[wave][0][32 * u + l32] = ps[u];
+      red[wave][1][32 * u + l32] = pq[u];
+    }
+  }
+  __syncthreads();
+  if (tid < 2 * NO) {
+    const int which = tid / NO, c = tid - which * NO;
+    double s = 0.0;
+#pragma unroll
+    for (int w = 0; w < WAVES; ++w) s += red[w][which][c];
+    a.part[((size_t)blockIdx.x * 2 + which) * NO + c] = s;
+  }
+}
+
+// Resident blocks per CU of a family of instantiations (the smallest; queried once per family).
+static int min_occupancy(const void* const* fs, int n) {
+  int o = 1 << 20;
+  for (int i = 0; i < n; ++i) {
+    int v = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, fs[i], 256, 0) != hipSuccess || v < 1) v = 1;
+    o = v < o ? v : o;
+  }
+  return o;
+}
+
+// Blocks of a persistent grid: every resident slot once, at most one block per 4 tiles.  The
+// count depends only on M and the (fixed) occupancy, so the partial-row count a caller
+// allocates for is the count the launch uses, and the summation order is reproducible.
+static int grid_blocks(int M, int occ) {
   const int ntiles = (M + TR - 1) / TR;
   const int want = (ntiles + WAVES - 1) / WAVES;
   const int slots = occ * 256;
   return want < slots ? (want > 0 ? want : 1) : slots;
+}
+
+int dgrad_blocks(int M) {
+  static int occ = -1;
+  if (occ < 0) {
+    const void* fs[] = {reinterpret_cast<const void*>(&dgrad_bnbwd_kernel<false, false>),
+                        reinterpret_cast<const void*>(&dgrad_bnbwd_kernel<false, true>),
+                        reinterpret_cast<const void*>(&dgrad_bnbwd_kernel<true, false>),
+                        reinterpret_cast<const void*>(&dgrad_bnbwd_kernel<true, true>)};
+    occ = min_occupancy(fs, 4);
+  }
+  return grid_blocks(M, occ);
+}
+
+int fwd_blocks(int M) {
+  static int occ = -1;
+  if (occ < 0) {
+    const void* fs[] = {reinterpret_cast<const void*>(&fwd_kernel<true, true, true>),
+                        reinterpret_cast<const void*>(&fwd_kernel<true, true, false>),
+                        reinterpret_cast<const void*>(&fwd_kernel<true, false, true>),
+                        reinterpret_cast<const void*>(&fwd_kernel<true, false, false>),
+                        reinterpret_cast<const void*>(&fwd_kernel<false, true, true>),
+                        reinterpret_cast<const void*>(&fwd_kernel<false, true, false>),
+                        reinterpret_cast<const void*>(&fwd_kernel<false, false, true>),
+                        reinterpret_cast<const void*>(&fwd_kernel<false, false, false>)};
+    occ = min_occupancy(fs, 8);
+  }
+  return grid_blocks(M, occ);
 }
 
 }  // namespace pws
@@ -303,6 +492,39 @@ bool pw_stream_dgrad_ok(int K, int C, int M) {
 }
 
 int pw_stream_dgrad_rows(int M) { return pws::dgrad_blocks(M); }
+
+bool pw_stream_fwd_ok(int K, int C, int M, size_t xbytes) {
+  if (!pw_stream_enabled()) return false;
+  return K == pws::NO && C == pws::KR && M > 0 && xbytes < ((size_t)1 << 31) &&
+         (size_t)M * 64 * 4 < ((size_t)1 << 31);
+}
+int pw_stream_fwd_rows(int M) { return pws::fwd_blocks(M); }
+
+int pw_stream_fwd(const float* x, int N, int H, int W, int stride, int OH, int OW, const float* w,
+                  const float* bias, float* y, const float* im, const float* iis, const float* ig,
+                  const float* ib, int irelu, double* part, hipStream_t st) {
+  const int M = N * OH * OW;
+  pws::FwdArgs a{x, w, bias, y, im, iis, ig, ib, irelu, part, M, H, W, OH, OW, stride,
+                 (uint32_t)((size_t)N * H * W * 64 * 4)};
+  const dim3 grid(pws::fwd_blocks(M));
+  const bool strided = stride != 1;
+#define DK_FWD(BN_, ST_)                                                                   \
+  if (strided)                                                                             \
+    hipLaunchKernelGGL((pws::fwd_kernel<BN_, ST_, true>), grid, dim3(256), 0, st, a);     \
+  else                                                                                     \
+    hipLaunchKernelGGL((pws::fwd_kernel<BN_, ST_, false>), grid, dim3(256), 0, st, a);
+  if (im && part) {
+    DK_FWD(true, true)
+  } else if (im) {
+    DK_FWD(true, false)
+  } else if (part) {
+    DK_FWD(false, true)
+  } else {
+    DK_FWD(false, false)
+  }
+#undef DK_FWD
+  return launch_status();
+}
 
 int pw_stream_dgrad_bnbwd(const float* g, const float* bn_x, int M, const float* om, const float* ois,
                           const float* og, const float* ob, int orelu, const float* k12, float* dy_out,

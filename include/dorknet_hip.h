@@ -55,6 +55,11 @@ int dk_mixup_f32(const float* a, const float* b, long long n, float p, float one
  * kind 3: the streaming pointwise kernels for K = C = 64 (1 = default, also for -1; 0 = the
  * tiled engine for every shape, as DORKNET_PW_STREAM=0); returns 0. */
 int dk_debug_set_gemm_config(int kind, int cfg);
+
+/* Bandwidth ceiling probe (not on the training path; scripts/stream_ceiling.py): reads nin
+ * (1..3) fp32 arrays a, b, c and writes nout (0..2) arrays o0, o1 of numel elements each, 16
+ * bytes per lane per access, on `blocks` blocks of 256 threads (<= 0: 2048). */
+int dk_debug_stream_mix(const float* a, const float* b, const float* c, float* o0, float* o1, int nin, int nout, long long numel, int blocks, void* stream);
 /* Tuning knob (same caveats): launch variant of dk_bn_bwd_apply_f32 (bits 0-1: rows in flight
  * 4/8 x plain/nontemporal stores; bits 2-3: rows per lane 16/8/32/64; bit 4: block cap 16384);
  * -1 restores the default (22).  Returns the number of variants. */

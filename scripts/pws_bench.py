@@ -64,6 +64,27 @@ def main():
                     "stream" if mode else "tiled ", us, by / us / 1e3, rows))
             lib.dk_debug_set_gemm_config(3, -1)
             print("{:28s} res={:d} | {}".format(name, res, " | ".join(line)), flush=True)
+    # forward with BN on load + output statistics (res1 pw; pw0: stride 2 from 112x112)
+    for name, H, s in (("fwd_ex res1 pw (56x56)", 56, 1), ("fwd_ex pw0 (112->56, s2)", 112, 2)):
+        K = C = 64
+        OH = -(-H // s)
+        x = rnd(B * H * H * C)
+        y = torch.empty(B * OH * OH * K, device="cuda")
+        w = rnd(K * C) * 0.1
+        pi = [rnd(C), rnd(C).abs() + 0.5, rnd(C), rnd(C)]
+        line = []
+        for mode in (0, 1):
+            lib.dk_debug_set_gemm_config(3, mode)
+            rows = lib.dk_pwconv_fwd_stats_rows(B, OH, OH, K, C)
+            part = torch.empty(rows * 2 * K, dtype=torch.float64, device="cuda")
+            args = (x.data_ptr(), B, H, H, C, w.data_ptr(), K, s, 0, y.data_ptr(), OH, OH,
+                    *(t.data_ptr() for t in pi), 1, part.data_ptr(), st)
+            us = timeit(lambda: lib.dk_pwconv_fwd_ex_f32(*args))
+            f, by = perfmodel.work("dk_pwconv_fwd_ex_f32", args)
+            line.append("{}: {:7.1f} us {:6.0f} GB/s ({} rows)".format("stream" if mode else "tiled ", us,
+                                                                       by / us / 1e3, rows))
+        lib.dk_debug_set_gemm_config(3, -1)
+        print("{:28s}       | {}".format(name, " | ".join(line)), flush=True)
 
 
 if __name__ == "__main__":

@@ -66,3 +66,42 @@ def test_stream_dgrad_bnbwd_matches_tiled_engine(relu, bn_in, resid, N, H, W):
         assert rows1 < max(rows0, 2) or N * H * W <= 128  # one row per persistent block
         s0, s1 = part0.sum(0), part1.sum(0)
         assert float((s1 - s0).norm() / s0.norm()) < 1e-12
+
+
+@pytest.mark.parametrize("bn,relu,stats,stride,bias,N,H,W", [(True, 1, True, 1, False, 3, 13, 11),
+                                                           (True, 0, True, 2, False, 2, 13, 9),
+                                                           (False, 0, True, 1, True, 2, 8, 8),
+                                                           (True, 1, False, 1, False, 1, 1, 5),
+                                                           (False, 0, False, 2, True, 3, 6, 7),
+                                                           (True, 1, True, 2, False, 32, 112, 112)])
+def test_stream_fwd_ex_matches_tiled_engine(bn, relu, stats, stride, bias, N, H, W):
+    """dk_pwconv_fwd_ex_f32 at K = C = 64: y bitwise equal to the tiled engine (BN + ReLU on
+    load, bias, stride-2 subsampling), output statistics to fp64 rounding."""
+    K = C = 64
+    rng = np.random.RandomState(int(bn) + 2 * relu + 4 * stats + 8 * stride + N)
+    x = nhwc(rng.randn(N, C, H, W) * 2 + 0.3)
+    w = torch.as_tensor(rng.randn(K, C).astype(np.float32), device="cuda")
+    b = torch.as_tensor(rng.randn(K).astype(np.float32), device="cuda") if bias else None
+    pi = bn_params(C, rng)
+    OH, OW = -(-H // stride), -(-W // stride)
+    st = stream_handle()
+    bn_args = (*(t.data_ptr() for t in pi), relu) if bn else (0, 0, 0, 0, 0)
+    outs = []
+    for mode in (0, 1):
+        lib.dk_debug_set_gemm_config(3, mode)
+        try:
+            rows = lib.dk_pwconv_fwd_stats_rows(N, OH, OW, K, C)
+            part = torch.full((rows, 2, K), float("nan"), dtype=torch.float64, device="cuda") if stats else None
+            y = torch.full((N, K, OH, OW), float("nan"), device="cuda").contiguous(memory_format=torch.channels_last)
+            assert lib.dk_pwconv_fwd_ex_f32(x.data_ptr(), N, H, W, C, w.data_ptr(), K, stride,
+                                            b.data_ptr() if bias else 0, y.data_ptr(), OH, OW, *bn_args,
+                                            part.data_ptr() if stats else 0, st) == 0
+            torch.cuda.synchronize()
+            outs.append((y, part, rows))
+        finally:
+            lib.dk_debug_set_gemm_config(3, -1)
+    (y0, p0, r0), (y1, p1, r1) = outs
+    assert torch.equal(y0, y1)
+    if stats:
+        s0, s1 = p0.sum(0), p1.sum(0)
+        assert float((s1 - s0).norm() / s0.norm()) < 1e-12
