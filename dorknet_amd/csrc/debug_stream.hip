@@ -7,7 +7,7 @@
 
 namespace dk {
 
-template <int NIN, int NOUT>
+template <int NIN, int NOUT, int NT>
 __global__ __launch_bounds__(256) void stream_mix_kernel(const f32x4* __restrict__ a, const f32x4* __restrict__ b,
                                                          const f32x4* __restrict__ c, f32x4* __restrict__ o0,
                                                          f32x4* __restrict__ o1, long long n4) {
@@ -27,8 +27,13 @@ __global__ __launch_bounds__(256) void stream_mix_kernel(const f32x4* __restrict
       f32x4 s = va[u];
       if constexpr (NIN > 1) s += vb[u];
       if constexpr (NIN > 2) s += vc[u];
-      if constexpr (NOUT > 0) o0[i + u * stride] = s;
-      if constexpr (NOUT > 1) o1[i + u * stride] = s * 2.f;
+      if constexpr (NT) {
+        if constexpr (NOUT > 0) __builtin_nontemporal_store(s, o0 + i + u * stride);
+        if constexpr (NOUT > 1) __builtin_nontemporal_store(s * 2.f, o1 + i + u * stride);
+      } else {
+        if constexpr (NOUT > 0) o0[i + u * stride] = s;
+        if constexpr (NOUT > 1) o1[i + u * stride] = s * 2.f;
+      }
       if constexpr (NOUT == 0) {
         if (s[0] == 12345.678f) o0[0] = s;  // keep the loads alive
       }
@@ -49,14 +54,17 @@ using namespace dk;
 
 DK_API int dk_debug_stream_mix(const float* a, const float* b, const float* c, float* o0, float* o1, int nin,
                                int nout, long long numel, int blocks, void* stream) {
+  const int nt = nout >= 10;  // nout + 10: nontemporal stores
+  nout %= 10;
   const long long n4 = numel / 4;
   const dim3 grid(blocks > 0 ? blocks : 2048), blk(256);
   const hipStream_t st = as_stream(stream);
   const f32x4 *A = reinterpret_cast<const f32x4*>(a), *B = reinterpret_cast<const f32x4*>(b),
               *C = reinterpret_cast<const f32x4*>(c);
   f32x4 *O0 = reinterpret_cast<f32x4*>(o0), *O1 = reinterpret_cast<f32x4*>(o1);
-#define DK_MIX(I, O) \
-  if (nin == I && nout == O) hipLaunchKernelGGL((stream_mix_kernel<I, O>), grid, blk, 0, st, A, B, C, O0, O1, n4); else
+#define DK_MIX(I, O)                                                                                       \
+  if (nin == I && nout == O && !nt) hipLaunchKernelGGL((stream_mix_kernel<I, O, 0>), grid, blk, 0, st, A, B, C, O0, O1, n4); \
+  else if (nin == I && nout == O) hipLaunchKernelGGL((stream_mix_kernel<I, O, 1>), grid, blk, 0, st, A, B, C, O0, O1, n4); else
   DK_MIX(1, 0) DK_MIX(1, 1) DK_MIX(2, 1) DK_MIX(2, 2) DK_MIX(3, 1) DK_MIX(3, 2) DK_MIX(1, 2) return DK_ERR_ARGS;
 #undef DK_MIX
   return launch_status();

@@ -58,7 +58,8 @@ int dk_debug_set_gemm_config(int kind, int cfg);
 
 /* Bandwidth ceiling probe (not on the training path; scripts/stream_ceiling.py): reads nin
  * (1..3) fp32 arrays a, b, c and writes nout (0..2) arrays o0, o1 of numel elements each, 16
- * bytes per lane per access, on `blocks` blocks of 256 threads (<= 0: 2048). */
+ * bytes per lane per access, on `blocks` blocks of 256 threads (<= 0: 2048); nout + 10 = the same
+ * with nontemporal stores. */
 int dk_debug_stream_mix(const float* a, const float* b, const float* c, float* o0, float* o1, int nin, int nout, long long numel, int blocks, void* stream);
 /* Tuning knob (same caveats): launch variant of dk_bn_bwd_apply_f32 (bits 0-1: rows in flight
  * 4/8 x plain/nontemporal stores; bits 2-3: rows per lane 16/8/32/64; bit 4: block cap 16384);

@@ -20,8 +20,8 @@ def main():
     st = torch.cuda.current_stream().cuda_stream
     bufs = [torch.randn(n, device="cuda") for _ in range(5)]
     p = [b.data_ptr() for b in bufs]
-    for nin, nout in ((1, 0), (1, 1), (2, 1), (1, 2), (2, 2), (3, 1), (3, 2)):
-        for blocks in (1024, 2048, 4096):
+    for nin, nout in ((1, 0), (1, 1), (2, 1), (1, 2), (2, 2), (3, 1), (3, 2), (1, 11), (2, 11), (3, 12)):
+        for blocks in (1024, 2048):
             f = lambda: lib.dk_debug_stream_mix(p[0], p[1], p[2], p[3], p[4], nin, nout, n, blocks, st)
             for _ in range(3):
                 f()
@@ -32,9 +32,9 @@ def main():
                 b.record()
             torch.cuda.synchronize()
             t = sorted(a.elapsed_time(b) for a, b in ev)[5] * 1e-3
-            gbs = (nin + nout) * n * 4 / t / 1e9
-            print("reads {} writes {} blocks {:5d}: {:7.1f} us  {:6.0f} GB/s".format(nin, nout, blocks, t * 1e6, gbs),
-                  flush=True)
+            gbs = (nin + nout % 10) * n * 4 / t / 1e9
+            print("reads {} writes {}{} blocks {:5d}: {:7.1f} us  {:6.0f} GB/s".format(
+                nin, nout % 10, " (nt)" if nout >= 10 else "", blocks, t * 1e6, gbs), flush=True)
 
 
 if __name__ == "__main__":
