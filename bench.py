@@ -136,6 +136,43 @@ ENTRY_KERNEL = {
 }
 
 
+# Read / write stream counts of an entry point's dominant traffic (for the measured ceiling of
+# that mix, dk_debug_stream_mix): dk_pwconv_dgrad_bnbwd_f32 reads g, the following BN's input and
+# the input BN's raw input, and writes dy and dx.
+ENTRY_MIX = {"dk_pwconv_dgrad_bnbwd_f32": (3, 2), "dk_pwconv_fwd_ex_f32": (1, 1), "dk_pwconv_wgrad_bnx_f32": (2, 0),
+             "dk_dwconv_bwd_bnbwd_f32": (3, 1), "dk_dwconv_fwd_ex_f32": (1, 1), "dk_bn_add_f32": (2, 1)}
+
+
+def stream_ceiling(entry):
+    """The achievable HBM rate for `entry`'s read/write mix, measured now on this GPU with the
+    float4 streaming probe (dk_debug_stream_mix, 205 MB per stream, 2048 x 256 threads): the
+    practical peak a memory-bound kernel with that mix can reach (8 TB/s is the spec)."""
+    import torch
+    from dorknet_amd._hip import lib
+    mix = ENTRY_MIX.get(entry)
+    if mix is None:
+        return None
+    nin, nout = mix
+    n = 256 * 56 * 56 * 64
+    bufs = [torch.empty(n, device="cuda").fill_(1.0) for _ in range(nin + nout)] + [None] * 5
+    p = [b.data_ptr() if b is not None else 0 for b in bufs]
+    ins, outs = p[:nin] + [0] * (3 - nin), p[nin:nin + nout] + [0] * (2 - nout)
+    st = torch.cuda.current_stream().cuda_stream
+    f = lambda: lib.dk_debug_stream_mix(ins[0], ins[1], ins[2], outs[0], outs[1], nin, nout, n, 2048, st)
+    for _ in range(3):
+        f()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(10)]
+    for a, b in ev:
+        a.record()
+        f()
+        b.record()
+    torch.cuda.synchronize()
+    t = sorted(a.elapsed_time(b) for a, b in ev)[5] * 1e-3
+    del bufs
+    return {"value": round((nin + nout) * n * 4 / t / 1e9, 1), "unit": "GB/s", "reads": nin, "writes": nout,
+            "probe": "dk_debug_stream_mix: float4 streams of 205 MB, median of 10"}
+
+
 def pmc_traffic(entry, path):
     """Average HBM bytes per dispatch of `entry`'s kernel from a committed PMC summary, or
     (None, None) when there is none for it."""
@@ -423,6 +460,11 @@ def main():
     if ins:
         s = ins.summary()[dominant]
         roof = roofline_entry(dominant, s, args.steps)
+        if roof["bound"] == "hbm":
+            ceil = stream_ceiling(dominant)
+            if ceil is not None:
+                ceil["frac"] = round(roof["achieved"] / ceil["value"], 4)
+                roof["practical_peak"] = ceil
         traffic, src = pmc_traffic(dominant, args.pmc)
         if traffic is not None:
             roof["traffic"] = round(traffic / 1e6, 2)

@@ -175,6 +175,13 @@ bool pw_stream_enabled();  // DORKNET_PW_STREAM (default 1; 0 = the tiled engine
 void pw_stream_set(int v);  // tuning knob (dk_debug_set_gemm_config kind 3)
 bool pw_stream_dgrad_ok(int K, int C, int M);
 int pw_stream_dgrad_rows(int M);
+bool pw_stream_bwd_ok(int K, int C, int M);
+int pw_stream_bwd_rows(int M);
+int pw_stream_bwd_fused(const float* g, const float* bn_x, int M, const float* om, const float* ois,
+                        const float* og, const float* ob, int orelu, const float* k12, const float* w, float* dx,
+                        const float* res, const float* x, const float* im, const float* iis, const float* ig,
+                        const float* ib, int irelu, double* part, const float* bm, const float* bis,
+                        const float* bgm, const float* bbt, int brelu, float* wpart, hipStream_t st);
 bool pw_stream_fwd_ok(int K, int C, int M, size_t xbytes);
 int pw_stream_fwd_rows(int M);
 int pw_stream_fwd(const float* x, int N, int H, int W, int stride, int OH, int OW, const float* w,

@@ -321,7 +321,14 @@ using namespace dk;
 
 DK_API int dk_pwconv_bwd_fused_rows(int N, int OH, int OW, int K, int C) {
   if (!pwf_supported(K, C) || N < 1 || OH < 1 || OW < 1) return 0;
+  if (pw_stream_bwd_ok(K, C, N * OH * OW)) return pw_stream_bwd_rows(N * OH * OW);
   return pwf_blocks((long long)N * OH * OW, K, C, nullptr);
+}
+
+// 1 when the fused backward is the faster path for this shape (the streaming kernel of
+// pw_stream.hip, K = C = 64); the layers use it by default there.
+DK_API int dk_pwconv_bwd_fused_preferred(int N, int OH, int OW, int K, int C) {
+  return (N > 0 && OH > 0 && OW > 0 && pw_stream_bwd_ok(K, C, N * OH * OW)) ? 1 : 0;
 }
 
 DK_API size_t dk_pwconv_bwd_fused_workspace_bytes(int N, int OH, int OW, int K, int C) {
@@ -347,6 +354,17 @@ DK_API int dk_pwconv_bwd_bnbwd_f32(const float* g, const float* bn_x, int N, int
   if (!al(g) || !al(bn_x) || !al(x) || !al(out_mean) || !al(out_invstd) || !al(out_gamma) || !al(out_beta) ||
       !al(k12) || !al(ws))
     return DK_ERR_ARGS;
+  if (pw_stream_bwd_ok(K, C, (int)P)) {
+    // K = C = 64: the persistent streaming kernel (pw_stream.hip)
+    const int nb = pw_stream_bwd_rows((int)P);
+    if (ws_bytes < (size_t)nb * K * C * sizeof(float)) return DK_ERR_WORKSPACE;
+    float* wp = static_cast<float*>(ws);
+    int rc = pw_stream_bwd_fused(g, bn_x, (int)P, out_mean, out_invstd, out_gamma, out_beta, out_relu, k12, w_kc, dx,
+                                 residual, x, bn_mean, bn_invstd, bn_gamma, bn_beta, bn_relu, part, bn_mean,
+                                 bn_invstd, bn_gamma, bn_beta, bn_relu, wp, st);
+    if (rc) return rc;
+    return splitk_reduce(wp, nb, K, C, dw_kc, l2 != 0.f ? w_kc : nullptr, l2, 0, C, C, 1, 1, st);
+  }
   int tpb = 1;
   const int nblk = pwf_blocks(P, K, C, &tpb);
   if (ws_bytes < (size_t)nblk * K * C * sizeof(float)) return DK_ERR_WORKSPACE;

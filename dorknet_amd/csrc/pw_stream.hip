@@ -473,6 +473,281 @@ int fwd_blocks(int M) {
   return grid_blocks(M, occ);
 }
 
+
+// ---------------------------------------------------------------------------------------
+// dk_pwconv_bwd_bnbwd_f32 at K = C = 64: the whole backward of a stride-1 pointwise layer whose
+// output fed a BatchNorm (+ReLU) in one pass (layers/pointwise_convolution.py:57-75 +
+// layers/batch_norm.py:125-174): dy = that BN's backward applied to g on load (never stored),
+// dx = dy . W (+ residual) with the input BN's backward partials, and the weight gradient
+// dW = dy^T . bn(x) accumulated in registers over every tile of the wave.
+//   * dgrad as dgrad_bnbwd_kernel (bit-identical dx);
+//   * wgrad on v_mfma_f32_32x32x2_f32 with the pixel (reduction) index in MFMA k: for MFMA r the
+//     lane half h supplies pixel (r&3) + 8(r>>2) + 4h -- exactly the rows of the C layout, so the
+//     input x values the dx epilogue loads for the partials (column 32u + l32 on the lane) ARE
+//     the wgrad's B operand; the A operand dy[pixel][32t + l32] is read back from the wave's LDS
+//     image of the dy tile (written once per tile, 16-byte stores);
+//   * one wave per SIMD (acc dgrad 32 + acc wgrad 64 registers), a tile of operands in flight;
+//   * each block leaves one 64 x 64 partial weight gradient (its waves summed in a fixed order)
+//     in ws; splitk_reduce folds them in a fixed order and adds l2 * W.
+// Bytes per pixel: g, x_out, x_in read, dx written (+ residual read): the unfused pair also
+// writes dy and reads dy and x_in again.
+// ---------------------------------------------------------------------------------------
+struct BwdArgs {
+  DgradArgs d;       // g, xo, (dy_out unused), w, dx, res, xi (required), BN params, part, M
+  const float* bm;   // the input BN applied to x for the weight gradient (nullable: raw x)
+  const float* bis;
+  const float* bg;
+  const float* bb;
+  int brelu;
+  float* wpart;      // [gridDim.x][KR][NO]
+};
+
+constexpr int SKD = KR + 4;  // row stride of the wave's dy image
+
+template <bool RES, bool PART, bool BNIN>
+__global__ __launch_bounds__(256, 1) void bwd_fused_kernel(BwdArgs ba) {
+  const DgradArgs& a = ba.d;
+  __shared__ float Bs[NO * SKB];
+  __shared__ float tab[7][KR];
+  __shared__ double red[WAVES][2][NO];
+  __shared__ float Td[WAVES][TR * SKD];  // per-wave dy tile image (also the dW combine buffer)
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int l32 = lane & 31, h = lane >> 5;
+  for (int i = tid; i < KR * NO; i += 256) {
+    const int k = i / NO, c = i - k * NO;
+    Bs[c * SKB + k] = a.w[i];
+  }
+  for (int k = tid; k < KR; k += 256) {
+    const float is = a.ois[k], ga = a.og[k];
+    tab[0][k] = a.om[k];
+    tab[1][k] = is;
+    tab[2][k] = ga;
+    tab[3][k] = a.ob[k];
+    tab[4][k] = a.k12[k];
+    tab[5][k] = a.k12[KR + k];
+    tab[6][k] = ga * is;
+  }
+  const bool orelu = a.orelu != 0, irelu = a.irelu != 0, brelu = ba.brelu != 0;
+  // this lane's two columns 32u + l32: the input BN (partials) and the wgrad operand's BN
+  float pm[2], pis[2], pga[2], pbe[2], qm[2], qis[2], qga[2], qbe[2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int c = 32 * u + l32;
+    pm[u] = PART ? a.im[c] : 0.f;
+    pis[u] = PART ? a.iis[c] : 0.f;
+    pga[u] = PART ? a.ig[c] : 0.f;
+    pbe[u] = PART ? a.ib[c] : 0.f;
+    qm[u] = BNIN ? ba.bm[c] : 0.f;
+    qis[u] = BNIN ? ba.bis[c] : 0.f;
+    qga[u] = BNIN ? ba.bg[c] : 0.f;
+    qbe[u] = BNIN ? ba.bb[c] : 0.f;
+  }
+  __syncthreads();
+
+  const uint32_t kbytes = (uint32_t)a.M * KR * 4u, nbytes = (uint32_t)a.M * NO * 4u;
+  const __amdgpu_buffer_rsrc_t rg = make_rsrc_v(a.g, kbytes), rx = make_rsrc_v(a.xo, kbytes);
+  const __amdgpu_buffer_rsrc_t rxi = make_rsrc_v(a.xi, nbytes);
+  const __amdgpu_buffer_rsrc_t rr = make_rsrc_v(RES ? a.res : a.g, RES ? nbytes : 0u);
+  const __amdgpu_buffer_rsrc_t rdx = make_rsrc_v(a.dx, nbytes);
+  const int ntiles = (a.M + TR - 1) / TR;
+  const int W = gridDim.x * WAVES;
+  int t = blockIdx.x * WAVES + wave;
+  float* const td = &Td[wave][0];
+
+  double ps[2] = {0.0, 0.0}, pq[2] = {0.0, 0.0};
+  f32x16 aw[2][2];  // weight gradient: rows k = 32t + (C-layout row), columns c = 32u + l32
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) aw[i][u][r] = 0.f;
+
+  auto load_a = [&](int tile, f32x4* lg, f32x4* lx) {
+    const int m = tile * TR + l32;
+    const uint32_t base = row_off_bytes(m, KR, 4 * h);
+#pragma unroll
+    for (int q = 0; q < KQ; ++q) {
+      lg[q] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rg, (int)base, 32 * q, 0));
+      lx[q] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rx, (int)base, 32 * q, 0));
+    }
+  };
+  f32x4 cg[KQ], cx[KQ];
+  load_a(t, cg, cx);
+  for (; t < ntiles; t += W) {
+    const int m0 = t * TR;
+    int z = 0;
+    asm volatile("" : "+s"(z));
+    const float* tb = &tab[0][0] + z;
+    const float* bs = Bs + z;
+
+    // (1) tile t's x (and residual) in the C layout, tile t+W's A operands
+    float exi[2][16], ers[2][16];
+    const int mb = m0 + 4 * h;
+    const uint32_t eb0 = row_off_bytes(mb, NO, l32), eb1 = eb0 + 16u * NO * 4u;
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const uint32_t imm = (uint32_t)(((r & 3) + 8 * ((r >> 2) & 1)) * NO + 32 * u) * 4u;
+        const uint32_t eb = r < 8 ? eb0 : eb1;
+        exi[u][r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rxi, (int)eb, (int)imm, 0));
+        if constexpr (RES)
+          ers[u][r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rr, (int)eb, (int)imm, 0));
+      }
+    f32x4 ng[KQ], nx[KQ];
+    load_a(t + W, ng, nx);
+    __builtin_amdgcn_sched_barrier(0);
+
+    // (2) dy (bit-identical to dk_bn_bwd_apply_f32) into registers and the wave's LDS image
+    f32x4 af[KQ];
+#pragma unroll
+    for (int q = 0; q < KQ; ++q) {
+      const int k0 = 8 * q + 4 * h;
+      const f32x4 mu = ld4(tb + 0 * KR + k0), is = ld4(tb + 1 * KR + k0), ga = ld4(tb + 2 * KR + k0),
+                  be = ld4(tb + 3 * KR + k0);
+      const f32x4 k1 = ld4(tb + 4 * KR + k0), k2 = ld4(tb + 5 * KR + k0), f = ld4(tb + 6 * KR + k0);
+      f32x4 o;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float xe = cx[q][e];
+        float ge = cg[q][e];
+        const bool kill = (!(bn_out(xe, mu[e], is[e], ga[e], be[e]) > 0.f)) & orelu;
+        ge = kill ? 0.f : ge;
+        o[e] = bn_bwd_elem(xe, ge, mu[e], is[e], f[e], k1[e], k2[e]);
+      }
+      af[q] = o;
+      st4(td + l32 * SKD + k0, o);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+
+    // (3) dgrad: dx tile = dy . W
+    f32x16 acc[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[u][r] = 0.f;
+#pragma unroll
+    for (int q = 0; q < KQ; ++q) {
+      f32x4 bf[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) bf[u] = ld4(bs + (32 * u + l32) * SKB + 8 * q + 4 * h);
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int u = 0; u < 2; ++u) acc[u] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[q][e], bf[u][e], acc[u], 0, 0, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+
+    // (4) wgrad: aw[t][u] += dy[pixels]^T . bn(x)[pixels]; pixels past M contribute nothing
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int dm = (r & 3) + 8 * (r >> 2);
+      const bool in = mb + dm < a.M;
+      float bx[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        float v = exi[u][r];
+        if constexpr (BNIN) {
+          const float o = bn_out(v, qm[u], qis[u], qga[u], qbe[u]);
+          v = (brelu & !(o > 0.f)) ? 0.f : o;
+        }
+        bx[u] = in ? v : 0.f;
+      }
+      const float a0 = td[(dm + 4 * h) * SKD + l32], a1 = td[(dm + 4 * h) * SKD + 32 + l32];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        aw[0][u] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, bx[u], aw[0][u], 0, 0, 0);
+        aw[1][u] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, bx[u], aw[1][u], 0, 0, 0);
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+
+    // (5) dx epilogue (+ residual), the input BN's partials
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int dm = (r & 3) + 8 * (r >> 2);
+        const uint32_t imm = (uint32_t)(((r & 3) + 8 * ((r >> 2) & 1)) * NO + 32 * u) * 4u;
+        float v = acc[u][r];
+        if constexpr (RES) v += ers[u][r];
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), rdx, (int)(r < 8 ? eb0 : eb1),
+                                              (int)imm, 0);
+        if constexpr (PART) {
+          const float x = exi[u][r];
+          const float xh = (x - pm[u]) * pis[u];
+          const bool kill = ((!(bn_out(x, pm[u], pis[u], pga[u], pbe[u]) > 0.f)) & irelu) | (mb + dm >= a.M);
+          const float gv = kill ? 0.f : v;
+          ps[u] += (double)gv;
+          pq[u] += (double)gv * (double)xh;
+        }
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < KQ; ++q) {
+      cg[q] = ng[q];
+      cx[q] = nx[q];
+    }
+  }
+
+  // the block's weight-gradient partial: the 4 waves summed in order through LDS
+  __syncthreads();
+  float* const wb = &Td[0][0];  // [KR][NO + 1]
+#pragma unroll 1
+  for (int w = 0; w < WAVES; ++w) {
+    if (wave == w) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            float* p = wb + (32 * i + (r & 3) + 8 * (r >> 2) + 4 * h) * (NO + 1) + 32 * u + l32;
+            *p = (w == 0) ? aw[i][u][r] : *p + aw[i][u][r];
+          }
+    }
+    __syncthreads();
+  }
+  for (int i = tid; i < KR * NO; i += 256) {
+    const int k = i / NO, c = i - k * NO;
+    ba.wpart[(size_t)blockIdx.x * KR * NO + i] = wb[k * (NO + 1) + c];
+  }
+  if constexpr (PART) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      ps[u] += __shfl_xor(ps[u], 32, 64);
+      pq[u] += __shfl_xor(pq[u], 32, 64);
+      if (h == 0) {
+        red[wave][0][32 * u + l32] = ps[u];
+        red[wave][1][32 * u + l32] = pq[u];
+      }
+    }
+    __syncthreads();
+    if (tid < 2 * NO) {
+      const int which = tid / NO, c = tid - which * NO;
+      double s2 = 0.0;
+#pragma unroll
+      for (int w = 0; w < WAVES; ++w) s2 += red[w][which][c];
+      a.part[((size_t)blockIdx.x * 2 + which) * NO + c] = s2;
+    }
+  }
+}
+
+int bwd_fused_blocks(int M) {
+  static int occ = -1;
+  if (occ < 0) {
+    const void* fs[] = {reinterpret_cast<const void*>(&bwd_fused_kernel<false, true, true>),
+                        reinterpret_cast<const void*>(&bwd_fused_kernel<true, true, true>),
+                        reinterpret_cast<const void*>(&bwd_fused_kernel<false, false, true>),
+                        reinterpret_cast<const void*>(&bwd_fused_kernel<true, false, true>),
+                        reinterpret_cast<const void*>(&bwd_fused_kernel<false, false, false>),
+                        reinterpret_cast<const void*>(&bwd_fused_kernel<true, false, false>)};
+    occ = min_occupancy(fs, 6);
+  }
+  return grid_blocks(M, occ);
+}
 }  // namespace pws
 
 static int g_pw_stream = -1;  // -1: from DORKNET_PW_STREAM (default on); dk_debug_set_gemm_config(3, v)
@@ -499,6 +774,31 @@ bool pw_stream_fwd_ok(int K, int C, int M, size_t xbytes) {
          (size_t)M * 64 * 4 < ((size_t)1 << 31);
 }
 int pw_stream_fwd_rows(int M) { return pws::fwd_blocks(M); }
+
+bool pw_stream_bwd_ok(int K, int C, int M) { return pw_stream_dgrad_ok(K, C, M); }
+int pw_stream_bwd_rows(int M) { return pws::bwd_fused_blocks(M); }
+
+int pw_stream_bwd_fused(const float* g, const float* bn_x, int M, const float* om, const float* ois,
+                        const float* og, const float* ob, int orelu, const float* k12, const float* w, float* dx,
+                        const float* res, const float* x, const float* im, const float* iis, const float* ig,
+                        const float* ib, int irelu, double* part, const float* bm, const float* bis,
+                        const float* bgm, const float* bbt, int brelu, float* wpart, hipStream_t st) {
+  pws::BwdArgs a{{g, bn_x, nullptr, w, dx, res, x, om, ois, og, ob, k12, orelu, im, iis, ig, ib, irelu, part, M},
+                 bm, bis, bgm, bbt, brelu, wpart};
+  const dim3 grid(pws::bwd_fused_blocks(M));
+  const bool r = res != nullptr, pt = part != nullptr, bn = bm != nullptr;
+  if (pt && !bn) return DK_ERR_ARGS;
+#define DK_BWD(R_, P_, B_) hipLaunchKernelGGL((pws::bwd_fused_kernel<R_, P_, B_>), grid, dim3(256), 0, st, a)
+  if (pt) {
+    if (r) DK_BWD(true, true, true); else DK_BWD(false, true, true);
+  } else if (bn) {
+    if (r) DK_BWD(true, false, true); else DK_BWD(false, false, true);
+  } else {
+    if (r) DK_BWD(true, false, false); else DK_BWD(false, false, false);
+  }
+#undef DK_BWD
+  return launch_status();
+}
 
 int pw_stream_fwd(const float* x, int N, int H, int W, int stride, int OH, int OW, const float* w,
                   const float* bias, float* y, const float* im, const float* iis, const float* ig,

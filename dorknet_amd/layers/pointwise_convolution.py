@@ -197,17 +197,23 @@ class PointwiseConvLayer(Layer):
         return dx
 
     def _fused_bwd_ok(self, bg, residual):
-        """dk_pwconv_bwd_bnbwd_f32 applies: DORKNET_PW_FUSED_BWD=1, fp32, stride 1, no bias, K and C
-        in {64, 128}, a residual (if any) that fuses.  Off by default: measured 0.75 % slower on
-        the ResNet-18-depsep step (10.72 vs 10.64 ms, scripts/ab_step.py) -- its 64-pixel tiles
-        run at 1-2 resident blocks per CU (VGPR / LDS bound), too few to hide HBM latency, while
-        the unfused pair overlaps the weight gradient on the side stream."""
+        """dk_pwconv_bwd_bnbwd_f32 applies: fp32, stride 1, no bias, K and C in {64, 128}, a
+        residual (if any) that fuses; taken by default where the library prefers it (K = C = 64:
+        the streaming kernel of pw_stream.hip, which never stores dy), DORKNET_PW_FUSED_BWD=1 / 0
+        forces it on / off.  The round-1 tiled fused kernel (K or C = 128) was measured 0.75 %
+        slower on the step than the unfused pair, so it is not the default."""
         x = self.X
-        if os.environ.get("DORKNET_PW_FUSED_BWD", "0") != "1" or self.with_bias or not self._takes_bn_grad(bg.x):
+        if self.with_bias or not self._takes_bn_grad(bg.x):
             return False
         N, C, H, W = x.shape
         OH, OW = self.out_hw
         if lib.dk_pwconv_bwd_fused_rows(N, OH, OW, self.num_filters, C) <= 0:
+            return False
+        env = os.environ.get("DORKNET_PW_FUSED_BWD")
+        if env is not None:
+            if env != "1":
+                return False
+        elif not lib.dk_pwconv_bwd_fused_preferred(N, OH, OW, self.num_filters, C):
             return False
         if residual is not None and residual_operand(residual, x) is None:
             return False

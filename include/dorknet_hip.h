@@ -171,6 +171,9 @@ int dk_pwconv_dgrad_bnbwd_f32(const float* g, const float* bn_x, int N, int OH, 
  * part[rows][2][C], rows = dk_pwconv_bwd_fused_rows().  dy itself is never stored.
  * K, C in {64, 128} (dk_pwconv_bwd_fused_rows() returns 0 for other shapes); fp32 NHWC. */
 int dk_pwconv_bwd_fused_rows(int N, int OH, int OW, int K, int C);
+/* 1 when the fused backward is the faster path for the shape (K = C = 64: the streaming kernel;
+ * the layers then take it by default), else 0. */
+int dk_pwconv_bwd_fused_preferred(int N, int OH, int OW, int K, int C);
 size_t dk_pwconv_bwd_fused_workspace_bytes(int N, int OH, int OW, int K, int C);
 int dk_pwconv_bwd_bnbwd_f32(const float* g, const float* bn_x, int N, int OH, int OW, int K, const float* out_mean, const float* out_invstd, const float* out_gamma, const float* out_beta, int out_relu, const float* k12, const float* w_kc, int C, float l2, float* dw_kc, float* dx, const float* residual, const float* x, const float* bn_mean, const float* bn_invstd, const float* bn_gamma, const float* bn_beta, int bn_relu, double* part, void* ws, size_t ws_bytes, void* stream);
 

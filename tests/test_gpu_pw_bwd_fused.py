@@ -19,6 +19,7 @@ pytestmark = pytest.mark.gpu
 @pytest.mark.parametrize("K,C,relu,bn_in,resid,shape", [
     (64, 64, 1, True, False, (3, 13, 11)),      # ragged last 64-pixel tile
     (64, 64, 0, True, True, (4, 56, 56)),       # the res1 layer's per-image shape
+    (64, 64, 1, True, False, (64, 56, 56)),     # streaming kernel: many tiles per wave
     (128, 64, 1, True, True, (2, 28, 28)),
     (64, 128, 0, False, False, (3, 9, 7)),
     (128, 128, 1, True, False, (5, 28, 28)),
