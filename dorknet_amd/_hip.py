@@ -89,7 +89,7 @@ class _Lib:
             fn = getattr(lib, name)
             fn.restype = ctypes.c_size_t if ret == "size_t" else ctypes.c_int
             fn.argtypes = [_argtype(t) for t, _ in params]
-            counts = name.endswith(("_blocks", "_version", "_rows", "_count")) or name.startswith("dk_debug")
+            counts = name.endswith(("_blocks", "_version", "_rows", "_count", "_preferred")) or name.startswith("dk_debug")
             if ret == "int" and not counts:
                 fn.errcheck = _errcheck
         self._decls = decls
