@@ -20,10 +20,12 @@ NCHW, already in HBM -- 4x fewer bytes over PCIe than shipping the fp32 batch.
 - ``mixup_batches(X, X_m, y, y_m, prop)``: the mixup step of load_batch (:101-111) for images
   and one-hot labels, returning both mixed batches.
 
-Decoding (cv2.imread) and file I/O stay on the host.  Resize geometry follows cv2's
-INTER_LINEAR; cv2's uint8 fixed-point interpolation is not reproduced (cv2 is not in this image
-to pin against), so pixel values may differ from cv2's by one level -- parity unpinned
-(DESIGN.md).  Crop, cast, layout and mixup are exact.
+Decoding (cv2.imread) and file I/O stay on the host.  The resize restates cv2.resize's uint8
+INTER_LINEAR as OpenCV 4.3 (the reference's pin) defines it: 11-bit fixed-point weights, integer
+horizontal pass, FixedPtCast vertical rounding, INTER_AREA for an exact 2x downscale -- integer
+work, bit-exact to oracle/pipeline.py.  cv2 is not in this image to pin against (its x86 SIMD
+vertical pass can round differently in the last bit), so agreement with cv2 itself is parity
+unpinned.  Crop, cast, layout and mixup are exact.
 """
 from __future__ import annotations
 

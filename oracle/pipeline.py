@@ -8,12 +8,12 @@ numpy restatement of the reference's per-image preprocessing and mixup:
   "center": int((size - crop) / 2)), astype(float32), transpose(2, 0, 1), - 128.0.  The
   augmenter call (:33-34) discards its result in the reference, so augmentation has no effect
   and is not restated.
-- resize_bilinear(im, OW, OH): cv2's INTER_LINEAR geometry (source coordinate
-  (float)((o + 0.5) * scale - 0.5) computed in double, floor, clamps to [0, L - 1] with zero
-  weight at the edges), interpolated in fp32 (every operation rounded to fp32, the same order as
-  dorknet_amd/csrc/input_pipeline.hip), rounded to nearest-even, saturated to uint8.  cv2 itself
-  interpolates uint8 in 11-bit fixed point and is not installed here: agreement with cv2 is
-  parity unpinned; this restatement pins the GPU kernel bit for bit.
+- resize_bilinear(im, OW, OH): cv2.resize INTER_LINEAR for uint8 as OpenCV 4.3 (the reference's
+  pin, requirements.txt: opencv-python==4.3.0.36) computes it in imgproc/src/resize.cpp's generic
+  path: the geometry above, 11-bit fixed-point weights (INTER_RESIZE_COEF_BITS), an integer
+  horizontal pass and the FixedPtCast vertical rounding, INTER_AREA for an exact 2x downscale.
+  cv2 is not installed here, so agreement with cv2 itself is parity unpinned (OpenCV's x86 SIMD
+  vertical pass can differ in the last bit); this restatement pins the GPU kernel bit for bit.
 - mixup(X, Xm, p): data_loading/image_data_loader.py:101-111 -- p * X_m + (1 - p) * X and the
   mirror, numpy semantics (a Python float times a float32 array stays float32).
 """
@@ -22,34 +22,51 @@ from __future__ import annotations
 import numpy as np
 
 
-def _coords(O, L):
-    s = np.float64(L) / np.float64(O)
-    v = ((np.arange(O, dtype=np.float64) + 0.5) * s - 0.5).astype(np.float32)
-    k = np.floor(v).astype(np.int64)
-    f = (v - k.astype(np.float32)).astype(np.float32)
-    lo = k < 0
-    k[lo], f[lo] = 0, 0
-    hi = k >= L - 1
-    k[hi], f[hi] = L - 1, 0
-    return k, np.minimum(k + 1, L - 1), f
+def _axis(O, L, is_x):
+    """cv::resize INTER_LINEAR coordinates and 11-bit weights (imgproc/src/resize.cpp, OpenCV 4.3):
+    scale = 1 / (O / L); f = float((o + 0.5) * scale - 0.5); s = floor(f); f -= s.  x axis: s < 0 ->
+    (0, 0); s >= L - 1 -> (L - 1, 0); outputs at or past the first s + 1 >= L take src[s] * 2048.
+    y axis: no weight clamping, the two rows clipped to [0, L - 1].  Weights cvRound((1 - f) * 2048),
+    cvRound(f * 2048) (round half to even)."""
+    scale = 1.0 / (O / L)
+    f = ((np.arange(O, dtype=np.float64) + 0.5) * scale - 0.5).astype(np.float32)
+    s = np.floor(f).astype(np.int64)
+    f = (f - s.astype(np.float32)).astype(np.float32)
+    if is_x:
+        lo = s < 0
+        s[lo], f[lo] = 0, 0
+        edge = s + 1 >= L
+        hi = s >= L - 1
+        s[hi], f[hi] = L - 1, 0
+    a0 = np.rint((np.float32(1) - f) * np.float32(2048)).astype(np.int64)
+    a1 = np.rint(f * np.float32(2048)).astype(np.int64)
+    if is_x:
+        a0[edge], a1[edge] = 2048, 0
+    return np.clip(s, 0, L - 1), np.clip(s + 1, 0, L - 1), a0, a1
 
 
 def resize_bilinear(im, OW, OH):
-    """im: uint8 (H, W, C) -> uint8 (OH, OW, C)."""
+    """cv2.resize(im, (OW, OH)) with INTER_LINEAR for uint8 (H, W, C) -> uint8 (OH, OW, C): OpenCV's
+    fixed-point path -- integer horizontal pass S = src[x0] * a0 + src[x1] * a1, vertical
+    FixedPtCast (S0 * b0 + S1 * b1 + 2^21) >> 22 saturated; an exact 2x downscale of both axes is
+    INTER_AREA ((a + b + c + d + 2) >> 2); the same size is a copy."""
     H, W = im.shape[:2]
-    y0, y1, fy = _coords(OH, H)
-    x0, x1, fx = _coords(OW, W)
-    one = np.float32(1.0)
-    gy, gx = (one - fy).astype(np.float32), (one - fx).astype(np.float32)
-    f = im.astype(np.float32)
-    p00, p01 = f[y0][:, x0], f[y0][:, x1]
-    p10, p11 = f[y1][:, x0], f[y1][:, x1]
-    gx3, fx3 = gx[None, :, None], fx[None, :, None]
-    gy3, fy3 = gy[:, None, None], fy[:, None, None]
-    top = (gx3 * p00).astype(np.float32) + (fx3 * p01).astype(np.float32)
-    bot = (gx3 * p10).astype(np.float32) + (fx3 * p11).astype(np.float32)
-    v = (gy3 * top.astype(np.float32)).astype(np.float32) + (fy3 * bot.astype(np.float32)).astype(np.float32)
-    return np.clip(np.rint(v.astype(np.float32)), 0, 255).astype(np.uint8)
+    if (OH, OW) == (H, W):
+        return im.copy()
+    sy, sx = 1.0 / (OH / H), 1.0 / (OW / W)
+    eps = np.finfo(np.float64).eps
+    if abs(sx - round(sx)) < eps and abs(sy - round(sy)) < eps and round(sx) == 2 and round(sy) == 2:
+        v = im.astype(np.int64)
+        t = v[0:2 * OH:2, 0:2 * OW:2] + v[0:2 * OH:2, 1:2 * OW:2] + v[1:2 * OH:2, 0:2 * OW:2] + v[1:2 * OH:2, 1:2 * OW:2]
+        return ((t + 2) >> 2).astype(np.uint8)
+    y0, y1, b0, b1 = _axis(OH, H, False)
+    x0, x1, a0, a1 = _axis(OW, W, True)
+    v = im.astype(np.int64)
+    A0, A1 = a0[None, :, None], a1[None, :, None]
+    S0 = v[y0][:, x0] * A0 + v[y0][:, x1] * A1
+    S1 = v[y1][:, x0] * A0 + v[y1][:, x1] * A1
+    out = (S0 * b0[:, None, None] + S1 * b1[:, None, None] + (1 << 21)) >> 22
+    return np.clip(out, 0, 255).astype(np.uint8)
 
 
 def crop_offsets(shape, image_size, crop_mode, rng=np.random):

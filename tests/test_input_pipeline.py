@@ -1,7 +1,8 @@
 """Device-side input pipeline: the oracle restatement of the reference's
 preprocessing on CPU (analytic cases), and the HIP kernels bit-exact against it on the GPU.
-cv2 (the reference's resize) is not installed, so agreement with cv2's fixed-point
-interpolation is unpinned; the geometry and the exact cases below pin the restatement."""
+The resize restates cv2's INTER_LINEAR for uint8 (11-bit fixed point, OpenCV 4.3); cv2 itself
+is not installed, so agreement with cv2 is unpinned; the geometry and the exact cases below pin
+the restatement."""
 import numpy as np
 import pytest
 
@@ -25,10 +26,28 @@ def test_resize_2x_upsample_geometry():
 
 
 def test_resize_2x_downsample_averages_pairs():
-    # source x = (o + 0.5) * 2 - 0.5 = 2o + 0.5: the mean of each pixel pair (round half even)
+    # source x = (o + 0.5) * 2 - 0.5 = 2o + 0.5: weights 1024/1024, the mean of each pixel pair,
+    # fixed-point rounding half up ((S * 2048 + 2^21) >> 22)
     row = np.array([10, 20, 30, 41, 0, 255], np.uint8)
     out = op.resize_bilinear(row.reshape(1, 6, 1), 3, 1)
     assert out[0, :, 0].tolist() == [15, 36, 128]   # 15, 35.5 -> 36, 127.5 -> 128
+
+
+def test_resize_exact_2x_is_area():
+    # an exact 2x downscale of both axes is INTER_AREA in cv::resize: (a + b + c + d + 2) >> 2
+    im = np.array([[1, 2, 200, 201], [3, 5, 202, 255], [0, 0, 9, 9], [0, 1, 9, 10]], np.uint8)[:, :, None]
+    out = op.resize_bilinear(im, 2, 2)[:, :, 0]
+    assert out.tolist() == [[(1 + 2 + 3 + 5 + 2) >> 2, (200 + 201 + 202 + 255 + 2) >> 2], [0, (9 + 9 + 9 + 10 + 2) >> 2]]
+
+
+def test_resize_fixed_point_weights():
+    # 3 -> 2 pixels: scale 1.5, x = 0.25 and 1.75: weights cvRound(0.75 * 2048) = 1536 / 512 and
+    # 512 / 1536; (S * 2048 + 2^21) >> 22
+    row = np.array([0, 100, 201], np.uint8).reshape(1, 3, 1)
+    out = op.resize_bilinear(row, 2, 1)[0, :, 0]
+    s0 = 0 * 1536 + 100 * 512
+    s1 = 100 * 512 + 201 * 1536
+    assert out.tolist() == [(s0 * 2048 + (1 << 21)) >> 22, (s1 * 2048 + (1 << 21)) >> 22]
 
 
 def test_preprocess_center_crop_matches_reference_formula():
@@ -71,7 +90,8 @@ def test_device_resize_bit_exact_many_scales():
     import torch
     from dorknet_amd._hip import lib, stream_handle
     rng = np.random.RandomState(4)
-    for (H, W, OH, OW) in [(225, 225, 281, 281), (300, 200, 225, 225), (10, 10, 3, 7), (1, 5, 4, 9), (31, 17, 31, 40)]:
+    for (H, W, OH, OW) in [(225, 225, 281, 281), (300, 200, 225, 225), (10, 10, 3, 7), (1, 5, 4, 9), (31, 17, 31, 40),
+                           (40, 60, 20, 30), (375, 500, 281, 281), (7, 9, 7, 9)]:
         im = rng.randint(0, 256, size=(2, H, W, 3)).astype(np.uint8)
         x = torch.as_tensor(im, device="cuda")
         y = torch.empty((2, OH, OW, 3), dtype=torch.uint8, device="cuda")
