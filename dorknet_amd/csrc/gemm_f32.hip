@@ -7,7 +7,8 @@
 //       m = output pixel (n,oh,ow), n = output channel, k = (r,s,c) with c innermost
 //   * conv dgrad    (replaces cp.dot + row2im, convolution.py:101-117, :205-222)
 //       stride 1: m = input pixel, k = (r,s,k_out), A gathers dy at (h+p-r, w+p-s)
-//       stride >1: dx_cols = dy_rows . W_flat (a plain GEMM) + a deterministic col2im gather
+//       stride >1: one such GEMM per sub-pixel phase (a, b) of dx, with the phase's sub-filter
+//       (dk_conv2d_dgrad_phase_f32): no column matrix, no scatter
 //   * conv wgrad    (replaces cp.dot(upstream.T, patches), convolution.py:93-100)
 //       m = output channel, n = (r,s,c), k = output pixel; split-K over pixels with a
 //       fixed-order second stage (no atomics, deterministic)
@@ -63,6 +64,7 @@ struct ImgDescE {
   int OH, OW;
   int R, S;
   int sa, dr, off;
+  int offw;  // column offset (= off except for the sub-pixel phase views of the strided dgrad)
   int M;  // N * OH * OW
   // division-free index arithmetic in the per-K-tile loader paths: q = umulhi(n, m) for
   // the divisors C, S, OW, OH (set_magics; 0 = divide).  Exact while n * d < 2^32.
@@ -177,7 +179,7 @@ struct LdImgKC : KCLayout<ROWS, BK> {
         const int oh = t % d.OH;
         const int n = t / d.OH;
         ih0[j] = oh * d.sa + d.off;
-        iw0[j] = ow * d.sa + d.off;
+        iw0[j] = ow * d.sa + d.offw;
         base[j] = (n * d.H + ih0[j]) * d.W + iw0[j];
       } else {
         ih0[j] = -(1 << 28);
@@ -692,6 +694,31 @@ struct EpPartial {
   }
 };
 
+// The output rows of one sub-pixel phase (a, b) of a stride-st input gradient: GEMM row
+// m = (n, i, j) of an OHp x OWp grid is dx pixel (n, st*i + a, st*j + b) of an H x W image.
+struct EpPhase {
+  static constexpr bool kColStats = false;
+  float* out;
+  int ldo;
+  int OHp, OWp, H, W, st, a, b;
+  int v4;
+  struct Pre {};
+  __device__ __forceinline__ size_t pix(int m) const {
+    const int j = m % OWp;
+    const int t = m / OWp;
+    const int i = t % OHp;
+    const int n = t / OHp;
+    return ((size_t)n * H + st * i + a) * W + (size_t)st * j + b;
+  }
+  __device__ __forceinline__ Pre pre4(int, int) const { return Pre{}; }
+  __device__ __forceinline__ void put4(int m, int n, f32x4 v, const Pre&, int, double*, double*) const {
+    st4(out + pix(m) * ldo + n, v);
+  }
+  __device__ __forceinline__ void put1(int m, int n, float v, int, double&, double&) const {
+    out[pix(m) * ldo + n] = v;
+  }
+};
+
 // ----------------------------------------------------------------------------
 // The kernel
 // ----------------------------------------------------------------------------
@@ -1118,36 +1145,39 @@ __global__ void w_kcrs_to_crsk_kernel(const float* __restrict__ w, int K, int C,
   out[idx] = w[(((size_t)k * C + c) * R + r) * S + s];
 }
 
-// dx[n,h,w,c] = sum over taps (r,s) with h + pad - r = oh*stride (and w likewise) of
-// cols[(n,oh,ow)][(c,r,s)] -- the deterministic gather form of row2im
-// (convolution.py:205-222, which scatters with atomicAdd).
-__global__ void col2im_kernel(const float* __restrict__ cols, int N, int C, int H, int W, int OH, int OW, int R,
-                              int S, int stride, int pad, float* __restrict__ dx) {
-  const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  const long long total = (long long)N * H * W * C;
-  if (idx >= total) return;
-  const int c = (int)(idx % C);
-  long long t = idx / C;
-  const int w = (int)(t % W);
-  t /= W;
-  const int h = (int)(t % H);
-  const int n = (int)(t / H);
-  const int CRS = C * R * S;
-  float acc = 0.f;
-  for (int r = 0; r < R; ++r) {
-    const int hh = h + pad - r;
-    if (hh < 0 || hh % stride) continue;
-    const int oh = hh / stride;
-    if (oh >= OH) continue;
-    for (int s = 0; s < S; ++s) {
-      const int ww = w + pad - s;
-      if (ww < 0 || ww % stride) continue;
-      const int ow = ww / stride;
-      if (ow >= OW) continue;
-      acc += cols[((size_t)(n * OH + oh) * OW + ow) * CRS + (c * R + r) * S + s];
-    }
-  }
-  dx[idx] = acc;
+// Taps of sub-pixel phase a along an axis of length-R filters (stride st, padding pad): r0 + st*t.
+__host__ __device__ __forceinline__ int phase_r0(int a, int st, int pad) { return (a + pad) % st; }
+__host__ __device__ __forceinline__ int phase_taps(int a, int R, int st, int pad) {
+  const int r0 = phase_r0(a, st, pad);
+  return r0 < R ? (R - r0 + st - 1) / st : 0;
+}
+// Offset (floats) of phase (a, b)'s sub-filter block: the blocks are laid out in (a, b) order.
+__host__ __device__ __forceinline__ size_t phase_block_offset(int a, int b, int C, int R, int S, int st, int pad,
+                                                              int Kp) {
+  size_t off = 0;
+  for (int i = 0; i < a * st + b; ++i)
+    off += (size_t)C * phase_taps(i / st, R, st, pad) * phase_taps(i % st, S, st, pad) * Kp;
+  return off;
+}
+
+// Sub-pixel phase sub-filters of a stride-st dgrad: for phase (a, b) the taps r = r0(a) + st*r',
+// s = s0(b) + st*s' as a [C][R'][S'][Kp] matrix (Kp = K rounded up to 4, zero-filled).
+__global__ void w_phase_kernel(const float* __restrict__ w, int K, int C, int R, int S, int st, int pad, int Kp,
+                               float* __restrict__ out) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;  // over C * R * S * Kp
+  if (idx >= C * R * S * Kp) return;
+  const int k = idx % Kp;
+  int t = idx / Kp;
+  const int s_ = t % S;
+  t /= S;
+  const int r = t % R;
+  const int c = t / R;
+  const int a = ((r - pad) % st + st) % st, b = ((s_ - pad) % st + st) % st;
+  const int r0 = phase_r0(a, st, pad), s0 = phase_r0(b, st, pad);
+  const int Rp = phase_taps(a, R, st, pad), Sp = phase_taps(b, S, st, pad);
+  const int rp = (r - r0) / st, sp = (s_ - s0) / st;
+  out[phase_block_offset(a, b, C, R, S, st, pad, Kp) + ((size_t)(c * Rp + rp) * Sp + sp) * Kp + k] =
+      k < K ? w[(((size_t)k * C + c) * R + r) * S + s_] : 0.f;
 }
 
 // rows x ld matrix; ext = extent of the non-reduction index (rows for a K-contiguous
@@ -1176,12 +1206,12 @@ static inline Dsc set_magics(Dsc d) {
 static inline ImgDesc img(const float* x, int N, int H, int W, int C, int OH, int OW, int R, int S, int sa, int dr,
                           int off, int M) {
   return set_magics(
-      ImgDesc{x, (uint32_t)((size_t)N * H * W * C * sizeof(float)), H, W, C, OH, OW, R, S, sa, dr, off, M});
+      ImgDesc{x, (uint32_t)((size_t)N * H * W * C * sizeof(float)), H, W, C, OH, OW, R, S, sa, dr, off, off, M});
 }
 // A pointwise (1x1, stride sa) view: k = channel.
 static inline ImgDescE<float, true> img1(const float* x, int N, int H, int W, int C, int OH, int OW, int sa, int M) {
   return set_magics(ImgDescE<float, true>{x, (uint32_t)((size_t)N * H * W * C * sizeof(float)), H, W, C, OH, OW, 1,
-                                          1, sa, 1, 0, M});
+                                          1, sa, 1, 0, 0, M});
 }
 
 }  // namespace dk
@@ -1317,36 +1347,61 @@ DK_API int dk_conv2d_dgrad_f32(const float* dy, int N, int OH, int OW, int K, co
   return igemm_rows<LdImgKC, ImgDesc, LdMatKC, MatDesc, EpStore>(a, b, ep, N * H * W, C, Ktot, as_stream(stream));
 }
 
-DK_API size_t dk_conv2d_dgrad_cols_workspace_bytes(int N, int OH, int OW, int C, int R, int S) {
-  return (size_t)N * OH * OW * C * R * S * sizeof(float);
+// Sub-pixel phase geometry of a stride-st, pad-p correlation's input gradient along one axis:
+// phase a's taps are r0 + st*t (t < Rp), reading dy row i + nb0 - t for dx row st*i + a.
+struct PhaseAxis {
+  int r0, Rp, nb0, Op;
+};
+static inline PhaseAxis phase_axis(int a, int R, int st, int pad, int L) {
+  PhaseAxis p;
+  p.r0 = phase_r0(a, st, pad);
+  p.Rp = phase_taps(a, R, st, pad);
+  p.nb0 = (a + pad - p.r0) / st;
+  p.Op = a < L ? (L - a + st - 1) / st : 0;
+  return p;
 }
 
-// Any-stride dgrad: cols = dy_rows . W_flat (GEMM, convolution.py:101-104) then a gather col2im.
-DK_API int dk_conv2d_dgrad_strided_f32(const float* dy, int N, int OH, int OW, int K, const float* w_kcrs, int C,
-                                       int R, int S, int stride, int pad, float* dx, int H, int W, void* ws,
-                                       size_t ws_bytes, void* stream) {
-  const int M = N * OH * OW;
-  const int CRS = C * R * S;
-  if (ws_bytes < dk_conv2d_dgrad_cols_workspace_bytes(N, OH, OW, C, R, S)) return DK_ERR_WORKSPACE;
-  if (!fits((size_t)M * K * 4) || !fits((size_t)M * CRS * 4)) return DK_ERR_ARGS;
-  float* cols = static_cast<float*>(ws);
-  MatDesc a = mat(dy, M, K, M);
-  MatDesc b = mat(w_kcrs, K, CRS, CRS);
-  EpStore ep = ep_store(cols, CRS, nullptr);
+DK_API size_t dk_conv2d_dgrad_phase_workspace_bytes(int K, int C, int R, int S, int stride) {
+  if (K < 1 || C < 1 || R < 1 || S < 1 || stride < 1) return 0;
+  const size_t kp = (size_t)((K + 3) / 4 * 4);
+  return (size_t)C * R * S * kp * sizeof(float);
+}
+
+// Input gradient of any-stride convolution as one implicit GEMM per sub-pixel phase (replaces
+// cp.dot(dy, W_flat) + row2im, convolution.py:101-117 / :205-222: no column matrix, no atomics):
+// phase (a, b) is a stride-1 correlation of dy with its sub-filter, written to the dx pixels
+// (st*i + a, st*j + b).  dy has Kp = K rounded up to 4 channels (zero-padded by the caller when
+// K % 4 != 0); phases with no taps (R or S < stride) write zeros.
+DK_API int dk_conv2d_dgrad_phase_f32(const float* dy, int N, int OH, int OW, int Kp, int K, const float* w_kcrs,
+                                     int C, int R, int S, int stride, int pad, float* dx, int H, int W, void* ws,
+                                     size_t ws_bytes, void* stream) {
+  if (Kp % 4 || Kp < K || stride < 1 || stride > 8 || N < 1 || C < 1 || !aligned16(dy) || !aligned16(ws))
+    return DK_ERR_ARGS;
+  if (ws_bytes < dk_conv2d_dgrad_phase_workspace_bytes(K, C, R, S, stride) || Kp != (K + 3) / 4 * 4)
+    return DK_ERR_WORKSPACE;
+  if (!fits((size_t)N * OH * OW * Kp * 4) || !fits((size_t)N * H * W * C * 4)) return DK_ERR_ARGS;
   const hipStream_t st = as_stream(stream);
-  int rc;
-  const bool va = vec_ok(a, K, 4), vb = vec_ok(b, 4, CRS);
-  if (va && vb)
-    rc = igemm_rows<LdMatKC, MatDesc, LdMatIC, MatDesc, EpStore>(a, b, ep, M, CRS, K, st);
-  else if (va)
-    rc = igemm_rows<LdMatKC, MatDesc, LdMatIC1, MatDesc, EpStore>(a, b, ep, M, CRS, K, st);
-  else
-    rc = igemm_rows<LdMatKC1, MatDesc, LdMatIC1, MatDesc, EpStore>(a, b, ep, M, CRS, K, st);
+  float* wsub = static_cast<float*>(ws);
+  const int total = C * R * S * Kp;
+  hipLaunchKernelGGL(w_phase_kernel, dim3(cdiv(total, 256)), dim3(256), 0, st, w_kcrs, K, C, R, S, stride, pad, Kp,
+                     wsub);
+  int rc = launch_status();
   if (rc) return rc;
-  const long long total = (long long)N * H * W * C;
-  hipLaunchKernelGGL(col2im_kernel, dim3((unsigned)cdivll(total, 256)), dim3(256), 0, st, cols, N, C, H, W, OH, OW, R,
-                     S, stride, pad, dx);
-  return launch_status();
+  for (int a = 0; a < stride; ++a)
+    for (int b = 0; b < stride; ++b) {
+      const PhaseAxis pa = phase_axis(a, R, stride, pad, H), pb = phase_axis(b, S, stride, pad, W);
+      if (pa.Op == 0 || pb.Op == 0) continue;  // no dx pixels of this phase
+      const int M = N * pa.Op * pb.Op;
+      ImgDesc d = img(dy, N, OH, OW, Kp, pa.Op, pb.Op, pa.Rp, pb.Rp, 1, -1, pa.nb0, M);
+      d.offw = pb.nb0;
+      const int Ktot = pa.Rp * pb.Rp * Kp;
+      const float* wp = wsub + phase_block_offset(a, b, C, R, S, stride, pad, Kp);
+      MatDesc bm = mat(wp, C, Ktot > 0 ? Ktot : 4, C);
+      EpPhase ep{dx, C, pa.Op, pb.Op, H, W, stride, a, b, al4(C) && aligned16(dx)};
+      rc = igemm_rows<LdImgKC, ImgDesc, LdMatKC, MatDesc, EpPhase>(d, bm, ep, M, C, Ktot, st);
+      if (rc) return rc;
+    }
+  return 0;
 }
 
 DK_API size_t dk_conv2d_wgrad_workspace_bytes(int N, int OH, int OW, int K, int Cp, int R, int S) {
@@ -1691,11 +1746,11 @@ static inline MatDescE<bf16_t> mat_h(const bf16_t* p, int rows, int ld, int ext)
 static inline ImgDescE<bf16_t> img_h(const bf16_t* x, int N, int H, int W, int C, int OH, int OW, int R, int S,
                                      int sa, int dr, int off, int M) {
   return set_magics(ImgDescE<bf16_t>{x, (uint32_t)((size_t)N * H * W * C * sizeof(bf16_t)), H, W, C, OH, OW, R, S,
-                                     sa, dr, off, M});
+                                     sa, dr, off, off, M});
 }
 static inline ImgDescE<bf16_t, true> img1_h(const bf16_t* x, int N, int H, int W, int C, int OH, int OW, int sa, int M) {
   return set_magics(ImgDescE<bf16_t, true>{x, (uint32_t)((size_t)N * H * W * C * sizeof(bf16_t)), H, W, C, OH, OW,
-                                           1, 1, sa, 1, 0, M});
+                                           1, 1, sa, 1, 0, 0, M});
 }
 static inline bool al8(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 7) == 0; }
 }  // namespace dk

@@ -620,9 +620,10 @@ __global__ __launch_bounds__(256, 1) void bwd_fused_kernel(BwdArgs ba) {
       af[q] = o;
       st4(td + l32 * SKD + k0, o);
     }
-    __builtin_amdgcn_sched_barrier(0);
 
-    // (3) dgrad: dx tile = dy . W
+    // (3) dgrad: dx tile = dy . W (no scheduling barrier around (2)-(4): the transform of
+    //     q + 1, the wgrad operand work and the epilogue VALU fill the MFMA issue gaps of the
+    //     wave, the only one on its SIMD)
     f32x16 acc[2];
 #pragma unroll
     for (int u = 0; u < 2; ++u)
@@ -638,9 +639,10 @@ __global__ __launch_bounds__(256, 1) void bwd_fused_kernel(BwdArgs ba) {
 #pragma unroll
         for (int u = 0; u < 2; ++u) acc[u] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[q][e], bf[u][e], acc[u], 0, 0, 0);
     }
-    __builtin_amdgcn_sched_barrier(0);
 
-    // (4) wgrad: aw[t][u] += dy[pixels]^T . bn(x)[pixels]; pixels past M contribute nothing
+    // (4) per pixel pair r: wgrad aw[t][u] += dy[pixels]^T . bn(x)[pixels] (pixels past M contribute
+    //     nothing), then (5) the dx epilogue rows of register r (+ residual) and the input BN's
+    //     partials
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int dm = (r & 3) + 8 * (r >> 2);
@@ -661,15 +663,8 @@ __global__ __launch_bounds__(256, 1) void bwd_fused_kernel(BwdArgs ba) {
         aw[0][u] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, bx[u], aw[0][u], 0, 0, 0);
         aw[1][u] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, bx[u], aw[1][u], 0, 0, 0);
       }
-    }
-    __builtin_amdgcn_sched_barrier(0);
-
-    // (5) dx epilogue (+ residual), the input BN's partials
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int dm = (r & 3) + 8 * (r >> 2);
+      for (int u = 0; u < 2; ++u) {
         const uint32_t imm = (uint32_t)(((r & 3) + 8 * ((r >> 2) & 1)) * NO + 32 * u) * 4u;
         float v = acc[u][r];
         if constexpr (RES) v += ers[u][r];

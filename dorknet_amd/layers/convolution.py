@@ -184,15 +184,19 @@ class ConvLayer(Layer):
             lib.dk_conv_weight_crsk_f32(w.data_ptr(), K, C, R, S, w_crsk.data_ptr(), st)
             lib.dk_conv2d_dgrad_f32(dy.data_ptr(), N, OH, OW, K, w_crsk.data_ptr(), C, R, S, self.padding,
                                     dx.data_ptr(), Hin, Win, st)
-        elif lib.dk_conv2d_dgrad_subpixel_workspace_bytes(K, C, R, S, self.stride, self.padding):
+        elif self.stride > 1 and lib.dk_conv2d_dgrad_subpixel_workspace_bytes(K, C, R, S, self.stride, self.padding):
             # strided, narrow input (the stem): sub-pixel gather, no column matrix
             nb = lib.dk_conv2d_dgrad_subpixel_workspace_bytes(K, C, R, S, self.stride, self.padding)
             lib.dk_conv2d_dgrad_subpixel_f32(dy.data_ptr(), N, OH, OW, K, w.data_ptr(), C, R, S, self.stride,
                                              self.padding, dx.data_ptr(), Hin, Win, workspace.get(nb), nb, st)
         else:
-            nb = lib.dk_conv2d_dgrad_cols_workspace_bytes(N, OH, OW, C, R, S)
-            lib.dk_conv2d_dgrad_strided_f32(dy.data_ptr(), N, OH, OW, K, w.data_ptr(), C, R, S, self.stride,
-                                            self.padding, dx.data_ptr(), Hin, Win, workspace.get(nb), nb, st)
+            # any stride (and stride 1 with K % 4 != 0): one implicit GEMM per sub-pixel phase of dx,
+            # dy zero-padded to a multiple of 4 channels for the 16-byte loads
+            Kp = -(-K // 4) * 4
+            dyp = dy if Kp == K else to_nhwc(dy, cpad=4)
+            nb = lib.dk_conv2d_dgrad_phase_workspace_bytes(K, C, R, S, self.stride)
+            lib.dk_conv2d_dgrad_phase_f32(dyp.data_ptr(), N, OH, OW, Kp, K, w.data_ptr(), C, R, S, self.stride,
+                                          self.padding, dx.data_ptr(), Hin, Win, workspace.get(nb), nb, st)
         return dx
 
     # -- checkpoint hooks (h5py is not available in this image; kept for API parity) ------

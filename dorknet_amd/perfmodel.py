@@ -139,7 +139,8 @@ def _bn_add(a, am, ai, ag, ab, ar, b, bm, bi, bg, bb, br, n, C, relu, y, mask, s
 MODEL = {
     "dk_conv2d_fwd_f32": _conv_fwd,
     "dk_conv2d_dgrad_f32": _conv_dgrad,
-    "dk_conv2d_dgrad_strided_f32": _conv_dgrad_strided,
+    "dk_conv2d_dgrad_phase_f32": lambda dy, N, OH, OW, Kp, K, w, C, R, S, stride, pad, dx, H, W, ws, nb, st:
+        _conv_dgrad_strided(dy, N, OH, OW, K, w, C, R, S, stride, pad, dx, H, W, ws, nb, st),
     "dk_conv2d_dgrad_subpixel_f32": _conv_dgrad_strided,
     "dk_conv2d_wgrad_f32": _conv_wgrad,
     "dk_pwconv_fwd_f32": _pw_fwd,

@@ -80,15 +80,19 @@ int dk_conv_weight_krsc_f32(const float* w_kcrs, int K, int C, int R, int S, int
 int dk_conv_weight_crsk_f32(const float* w_kcrs, int K, int C, int R, int S, float* w_crsk, void* stream);
 int dk_conv2d_fwd_f32(const float* x, int N, int H, int W, int C, const float* w_krsc, int K, int R, int S, int stride, int pad, const float* bias, float* y, int OH, int OW, void* stream);
 int dk_conv2d_dgrad_f32(const float* dy, int N, int OH, int OW, int K, const float* w_crsk, int C, int R, int S, int pad, float* dx, int H, int W, void* stream);
-size_t dk_conv2d_dgrad_cols_workspace_bytes(int N, int OH, int OW, int C, int R, int S);
-int dk_conv2d_dgrad_strided_f32(const float* dy, int N, int OH, int OW, int K, const float* w_kcrs, int C, int R, int S, int stride, int pad, float* dx, int H, int W, void* ws, size_t ws_bytes, void* stream);
 /* Strided dgrad without a column matrix (sub-pixel decomposition; conv_subpixel.hip), for
  * narrow inputs (C <= 16) and the instantiated (R, S, stride, pad) geometries: (5,5,2,1), (5,5,2,2),
- * (3,3,2,1), (4,4,2,1), (7,7,2,3), (3,3,2,0), (2,2,2,0).  Same contract as
- * dk_conv2d_dgrad_strided_f32 (replaces convolution.py:101-111 + row2im :205-222).
- * The workspace query returns 0 when the geometry is not covered (use the column path). */
+ * (3,3,2,1), (4,4,2,1), (7,7,2,3), (3,3,2,0), (2,2,2,0) (replaces convolution.py:101-111 +
+ * row2im :205-222).  The workspace query returns 0 when the geometry is not covered (use
+ * dk_conv2d_dgrad_phase_f32). */
 size_t dk_conv2d_dgrad_subpixel_workspace_bytes(int K, int C, int R, int S, int stride, int pad);
 int dk_conv2d_dgrad_subpixel_f32(const float* dy, int N, int OH, int OW, int K, const float* w_kcrs, int C, int R, int S, int stride, int pad, float* dx, int H, int W, void* ws, size_t ws_bytes, void* stream);
+/* Any-stride input gradient as one implicit GEMM per sub-pixel phase (no column matrix, no atomics;
+ * replaces cp.dot(dy, W_flat) + row2im, layers/convolution.py:101-117, :205-222).  dy: NHWC with
+ * Kp = K rounded up to 4 channels (zero-padded when K % 4 != 0); w_kcrs: the reference layout;
+ * dx: NHWC (N, H, W, C).  Workspace: dk_conv2d_dgrad_phase_workspace_bytes(). */
+size_t dk_conv2d_dgrad_phase_workspace_bytes(int K, int C, int R, int S, int stride);
+int dk_conv2d_dgrad_phase_f32(const float* dy, int N, int OH, int OW, int Kp, int K, const float* w_kcrs, int C, int R, int S, int stride, int pad, float* dx, int H, int W, void* ws, size_t ws_bytes, void* stream);
 size_t dk_conv2d_wgrad_workspace_bytes(int N, int OH, int OW, int K, int Cp, int R, int S);
 int dk_conv2d_wgrad_f32(const float* dy, const float* x, int N, int H, int W, int Cp, int C, int K, int R, int S, int stride, int pad, int OH, int OW, const float* w_kcrs, float l2, float* dw_kcrs, void* ws, size_t ws_bytes, void* stream);
 

@@ -134,8 +134,8 @@ def main():
                                                       dx.data_ptr(), H, H, st)
             else:
                 def dgr():
-                    nb = lib.dk_conv2d_dgrad_cols_workspace_bytes(N, OH, OH, Cr, R, R)
-                    lib.dk_conv2d_dgrad_strided_f32(dy.data_ptr(), N, OH, OH, K, w.data_ptr(), Cr, R, R, s, pd,
+                    nb = lib.dk_conv2d_dgrad_phase_workspace_bytes(K, Cr, R, R, s)
+                    lib.dk_conv2d_dgrad_phase_f32(dy.data_ptr(), N, OH, OH, K, K, w.data_ptr(), Cr, R, R, s, pd,
                                                     dx.data_ptr(), H, H, workspace.get(nb), nb, st)
 
             def wgr():

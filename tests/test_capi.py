@@ -43,7 +43,7 @@ def test_library_loads_and_host_queries_work():
     assert lib.dk_pwconv_wgrad_workspace_bytes(256, 56, 56, 64, 64) > 0
     assert lib.dk_dwconv_wgrad_workspace_bytes(256, 56, 56, 64, 3, 3) > 0
     assert lib.dk_dense_wgrad_workspace_bytes(256, 512, 120) > 0
-    assert lib.dk_conv2d_dgrad_cols_workspace_bytes(2, 4, 4, 3, 5, 5) == 2 * 16 * 75 * 4
+    assert lib.dk_conv2d_dgrad_phase_workspace_bytes(6, 3, 5, 5, 2) == 3 * 5 * 5 * 8 * 4  # K padded to 8
     nblk = lib.dk_bn_partial_blocks(802816, 64)
     assert 1 <= nblk <= 1024
     assert lib.dk_bn_workspace_bytes(802816, 64) == nblk * 2 * 64 * 8

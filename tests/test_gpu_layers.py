@@ -68,7 +68,11 @@ CONV_CASES = [
     (130, 68, 3, 3, 1, 1, 1, 6, 5, False, 1e-4),    # K > 128 tile, ragged M
     (70, 5, 3, 3, 2, 1, 2, 33, 150, False, 0.0),    # sub-pixel dgrad: K % 4 != 0, 2 channel groups, 2 column tiles
     (8, 3, 7, 7, 2, 3, 1, 20, 19, True, 0.0),       # sub-pixel dgrad, 7x7 stem geometry
-    (6, 20, 3, 3, 2, 1, 2, 9, 9, False, 0.0),       # strided, C > 16: column-matrix dgrad path
+    (6, 20, 3, 3, 2, 1, 2, 9, 9, False, 0.0),       # strided, C > 16, K % 4 != 0: phase dgrad (dy padded)
+    (128, 64, 3, 3, 2, 1, 2, 56, 56, False, 1e-4),  # the non-depthwise ResNet block's strided conv: phase dgrad
+    (12, 24, 1, 1, 2, 0, 2, 10, 9, True, 0.0),      # 1x1 stride 2: phases without taps write zeros
+    (6, 8, 3, 3, 1, 1, 2, 9, 9, False, 0.0),        # stride 1, K % 4 != 0: one phase, dy padded
+    (16, 20, 4, 4, 3, 2, 1, 17, 13, False, 0.0),    # stride 3, even filter, ragged phases
 ]
 
 
