@@ -63,8 +63,11 @@ def _argtype(ctype: str):
     return _SCALARS[base]
 
 
+DK_FOLDED = 10100  # success, and the launch folded the armed BN partials (dk_bn_fold_arm_*)
+
+
 def _errcheck(result, func, args):
-    if result != 0:
+    if result != 0 and result != DK_FOLDED:
         what = {DK_ERR_ARGS: "bad arguments", DK_ERR_WORKSPACE: "workspace too small"}.get(result, "hipError")
         raise HipError(f"{func.__name__} failed with status {result} ({what})")
     return result
@@ -165,6 +168,35 @@ class Tickets:
 
 
 tickets = Tickets()
+
+
+class FoldResources:
+    """Ticket words and group-row scratch for in-launch BN folds (dk_bn_fold_arm_*), one set
+    per stream (the folding launches of a stream run in order; the tickets are left zero).
+    DORKNET_INLAUNCH_FOLD=0 turns the in-launch folds off (the separate fold launches run)."""
+
+    TICKETS = 16384
+    SCRATCH = 8 << 20
+
+    def __init__(self):
+        self._res = {}
+
+    def get(self):
+        """(tickets ptr, ticket words, scratch ptr, scratch bytes) for the current stream."""
+        key = torch.cuda.current_stream().cuda_stream
+        r = self._res.get(key)
+        if r is None:
+            t = torch.zeros(self.TICKETS, dtype=torch.int32, device="cuda")
+            sc = torch.empty(self.SCRATCH, dtype=torch.uint8, device="cuda")
+            r = self._res[key] = (t, sc, (t.data_ptr(), self.TICKETS, sc.data_ptr(), self.SCRATCH))
+        return r[2]
+
+
+fold_resources = FoldResources()
+
+
+def inlaunch_folds_enabled() -> bool:
+    return os.environ.get("DORKNET_INLAUNCH_FOLD", "1") != "0"
 
 
 # ---------------------------------------------------------------------------------------

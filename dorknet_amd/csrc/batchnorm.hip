@@ -16,6 +16,7 @@
 // walks rows pl, pl + PL, ... with four rows of loads in flight.  Per-channel
 // parameters live in registers, so there is no per-element index arithmetic.
 #include "dk_common.h"
+#include "fold_tail.h"
 
 namespace dk {
 
@@ -195,56 +196,6 @@ __global__ __launch_bounds__(256) void bn_collapse_kernel(const double* __restri
 // 2 plain sums.  Otherwise it writes one folded row per block and runs again on those.
 constexpr int kFoldLanes = 16, kFoldPerLane = 16, kFoldRows = kFoldLanes * kFoldPerLane;
 
-struct FoldOut {
-  int mode;
-  double count;
-  float eps, momentum;
-  int first;
-  float *mean, *std_, *invstd, *run_mean, *run_std;  // mode 0
-  float *dgamma, *dbeta, *k12;                        // mode 1
-  double* sums;                                       // mode 2: [2][C]
-};
-
-__device__ __forceinline__ void bn_finalize_channel(int c, int C, double s, double q, const FoldOut& o) {
-  if (o.mode == 0) {
-    const double mean = s / o.count;
-    double var = q / o.count - mean * mean;
-    if (var < 0.0) var = 0.0;
-    const float meanf = (float)mean;
-    const float stdf = sqrtf((float)var + o.eps);
-    o.mean[c] = meanf;
-    o.std_[c] = stdf;
-    o.invstd[c] = 1.0f / stdf;
-    if (o.run_mean) {
-      if (o.first) {
-        o.run_mean[c] = meanf;
-        o.run_std[c] = stdf;
-      } else {
-        o.run_mean[c] = o.momentum * o.run_mean[c] + (1.0f - o.momentum) * meanf;
-        o.run_std[c] = o.momentum * o.run_std[c] + (1.0f - o.momentum) * stdf;
-      }
-    }
-  } else if (o.mode == 1) {
-    o.dgamma[c] = (float)q;
-    o.dbeta[c] = (float)s;
-    o.k12[c] = (float)(s / o.count);
-    o.k12[C + c] = (float)(q / o.count);
-  } else {
-    o.sums[c] = s;
-    o.sums[C + c] = q;
-  }
-}
-
-// Write-through (sc1) stores / loads for rows handed between blocks of one launch
-// (cdna_hip_programming.md section 6 Guideline 16, counter form with sc1 payload: no release
-// fence, whose L2 write-back in every block would cost more than the launch it saves).
-__device__ __forceinline__ void pub_store(double* p, double v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ double pub_load(const double* p) {
-  return __hip_atomic_load(const_cast<double*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
 // LEVEL 0: fold up to kFoldRows rows per block into out[blockIdx.x] (a later launch folds
 // those).  1 (FINAL): one block along x folds every row and finalizes.  2 (TICKET): as 0,
 // then the last block of each 64-column group to arrive (agent-scope ticket, zeroed by the
@@ -404,7 +355,7 @@ __global__ __launch_bounds__(256) void bn_bwd_partial_kernel(const E* __restrict
                                                              const float* __restrict__ beta, int relu,
                                                              double* __restrict__ part,
                                                              const uint8_t* __restrict__ mask = nullptr,
-                                                             E* __restrict__ gout = nullptr) {
+                                                             E* __restrict__ gout = nullptr, FoldTail ft = FoldTail{}) {
   using VT = VecT<V, E>;
   __shared__ double red[2][256][V];
   const RowGeom g = row_geom(C, V);
@@ -487,7 +438,11 @@ __global__ __launch_bounds__(256) void bn_bwd_partial_kernel(const E* __restrict
     if (cgg >= g.CG) continue;
     double a = 0.0;
     for (int qq = 0; qq < g.PL; ++qq) a += red[which][qq * g.cgt + gg][e];
-    part[((size_t)blockIdx.x * 2 + which) * C + cgg * V + e] = a;
+    pub_store(part + ((size_t)blockIdx.x * 2 + which) * C + cgg * V + e, a);
+  }
+  if (ft.part) {
+    const int c0 = blockIdx.y * g.cgt * V;
+    fold_tail<256>(ft, blockIdx.x, c0, min(g.cgt * V, C - c0), blockIdx.y);
   }
 }
 
@@ -707,6 +662,110 @@ DK_API int dk_debug_set_ew_variant(int v) {
 
 DK_API int dk_bn_fold_tickets_count(int C) { return C < 1 ? 0 : cdiv(C, 64); }
 
+// ---- in-launch folds (fold_tail.h): the arming of one partials buffer at a time per thread ----
+namespace {
+struct Armed {
+  const void* part = nullptr;
+  int nrows = 0, C = 0;
+  FoldOut o{};
+  unsigned* tickets = nullptr;
+  int ntickets = 0;
+  double* scratch = nullptr;
+  size_t scratch_bytes = 0;
+};
+thread_local Armed g_armed;
+
+int fold_group_rows(int nrows) {
+  int g = 1;
+  while ((long long)g * g < nrows) ++g;  // ceil(sqrt(nrows)): balances the two levels
+  return g;
+}
+}  // namespace
+
+bool dk::fold_take(const void* part, int nrows, int C, int nslices, FoldTail* ft) {
+  ft->part = nullptr;
+  Armed& a = g_armed;
+  if (!part || a.part != part) return false;
+  a.part = nullptr;  // one launch takes it
+  if (a.nrows != nrows || a.C != C || C % 2 || nslices < 1 || nrows < 1) return false;
+  const int G = fold_group_rows(nrows);
+  const int ng = cdiv(nrows, G);
+  if ((long long)ng * nslices + nslices > a.ntickets) return false;
+  if ((size_t)ng * 2 * C * sizeof(double) > a.scratch_bytes) return false;
+  ft->o = a.o;
+  ft->part = static_cast<const double*>(part);
+  ft->grp = a.scratch;
+  ft->tickets = a.tickets;
+  ft->nrows = nrows;
+  ft->C = C;
+  ft->G = G;
+  ft->ngroups = ng;
+  ft->nslices = nslices;
+  return true;
+}
+
+int dk::fold_status(int rc, const FoldTail& ft) { return rc == 0 && ft.part ? DK_FOLDED : rc; }
+
+static int fold_arm(const void* part, int nrows, int C, const FoldOut& o, unsigned* tickets, int ntickets,
+                    void* scratch, size_t scratch_bytes) {
+  if (!part || nrows < 1 || C < 1 || !tickets || ntickets < 2 || !scratch) return DK_ERR_ARGS;
+  Armed& a = g_armed;
+  a.part = part;
+  a.nrows = nrows;
+  a.C = C;
+  a.o = o;
+  a.tickets = tickets;
+  a.ntickets = ntickets;
+  a.scratch = static_cast<double*>(scratch);
+  a.scratch_bytes = scratch_bytes;
+  return 0;
+}
+
+DK_API int dk_bn_fold_arm_stats(const void* part, int nrows, int C, double count, float eps, float momentum,
+                                int first, float* mean, float* std_, float* invstd, float* run_mean, float* run_std,
+                                unsigned* tickets, int ntickets, void* scratch, size_t scratch_bytes) {
+  FoldOut o{};
+  o.mode = 0;
+  o.count = count;
+  o.eps = eps;
+  o.momentum = momentum;
+  o.first = first;
+  o.mean = mean;
+  o.std_ = std_;
+  o.invstd = invstd;
+  o.run_mean = run_mean;
+  o.run_std = run_std;
+  if (!mean || !std_ || !invstd) return DK_ERR_ARGS;
+  return fold_arm(part, nrows, C, o, tickets, ntickets, scratch, scratch_bytes);
+}
+
+DK_API int dk_bn_fold_arm_bwd(const void* part, int nrows, int C, double count, float* dgamma, float* dbeta,
+                              float* k12, unsigned* tickets, int ntickets, void* scratch, size_t scratch_bytes) {
+  FoldOut o{};
+  o.mode = 1;
+  o.count = count;
+  o.dgamma = dgamma;
+  o.dbeta = dbeta;
+  o.k12 = k12;
+  if (!dgamma || !dbeta || !k12) return DK_ERR_ARGS;
+  return fold_arm(part, nrows, C, o, tickets, ntickets, scratch, scratch_bytes);
+}
+
+DK_API int dk_bn_fold_disarm(void) {
+  g_armed.part = nullptr;
+  return 0;
+}
+
+// Scratch bytes / ticket words an in-launch fold of nrows x C in nslices slices needs.
+DK_API size_t dk_bn_fold_scratch_bytes(int nrows, int C) {
+  if (nrows < 1 || C < 1) return 0;
+  return (size_t)cdiv(nrows, fold_group_rows(nrows)) * 2 * C * sizeof(double);
+}
+DK_API int dk_bn_fold_tickets_needed_count(int nrows, int nslices) {
+  if (nrows < 1 || nslices < 1) return 0;
+  return cdiv(nrows, fold_group_rows(nrows)) * nslices + nslices;
+}
+
 // Fold part[nblk][2][C] (fixed order) and apply the stage-2 maths: one launch for <= 256 rows,
 // and with `tickets` (>= cdiv(C, 64) zeroed words) one launch for <= 256 * 256 rows.
 static int fold_finalize(const double* part, int nblk, int C, double* ws, const FoldOut& o, hipStream_t st,
@@ -829,13 +888,15 @@ DK_API int dk_relu_bwd_bn_partial_f64(const float* dy, const uint8_t* mask, cons
   const bool vec = vec_ok(x, C) && vec_ok(dy, C) && vec_ok(dx, C) && (reinterpret_cast<uintptr_t>(mask) & 3) == 0;
   const RowGeom g = row_geom(C, vec ? 4 : 1);
   const dim3 grid(nblk, cdiv(g.CG, g.cgt));
+  FoldTail ft;  // an armed in-launch fold of the partial rows (fold_tail.h)
+  if (!fold_take(part, nblk, C, (int)grid.y, &ft) || ((g.cgt * (vec ? 4 : 1)) & 1)) ft.part = nullptr;
   if (vec)
     hipLaunchKernelGGL((bn_bwd_partial_kernel<4, true>), grid, dim3(256), 0, as_stream(stream), x, dy, P, C, ppb,
-                       mean, invstd, gamma, beta, relu, static_cast<double*>(part), mask, dx);
+                       mean, invstd, gamma, beta, relu, static_cast<double*>(part), mask, dx, ft);
   else
     hipLaunchKernelGGL((bn_bwd_partial_kernel<1, true>), grid, dim3(256), 0, as_stream(stream), x, dy, P, C, ppb,
-                       mean, invstd, gamma, beta, relu, static_cast<double*>(part), mask, dx);
-  return launch_status();
+                       mean, invstd, gamma, beta, relu, static_cast<double*>(part), mask, dx, ft);
+  return fold_status(launch_status(), ft);
 }
 
 // Backward stage 2 from partials of any origin (dk_bn_bwd_partial_f64, a consumer's

@@ -13,6 +13,7 @@
 //   * wgrad reduces per-block partials in a fixed order (reduce.hip) -- the reference
 //     issues N*OH*OW atomicAdds on each of the C*R*S weight addresses.
 #include "dk_common.h"
+#include "fold_tail.h"
 
 namespace dk {
 
@@ -108,7 +109,7 @@ __global__ __launch_bounds__(256) void dw_fwd_kernel(const T* __restrict__ x, ui
                                                      T* __restrict__ y, int N, int H, int W, int C, int OH, int OW,
                                                      int pad, BnIn bn, double* __restrict__ part,
                                                      const T* __restrict__ xo, BnIn obn,
-                                                     const T* __restrict__ res) {
+                                                     const T* __restrict__ res, FoldTail ft) {
   constexpr int TW = DwTile<ST>::TW, SEG = DwTile<ST>::SEG;
   constexpr int NC = (TW - 1) * ST + S;
   const int C4 = C >> 2;
@@ -226,8 +227,9 @@ __global__ __launch_bounds__(256) void dw_fwd_kernel(const T* __restrict__ x, ui
       const int g = i >> 3, e = i & 7;
       double a = 0.0;
       for (int k = 0; k < per; ++k) a += red[k * C4 + g][e];
-      part[((size_t)blockIdx.x * 2 + (e >> 2)) * C + g * 4 + (e & 3)] = a;
+      pub_store(part + ((size_t)blockIdx.x * 2 + (e >> 2)) * C + g * 4 + (e & 3), a);
     }
+    if (ft.part) fold_tail<256>(ft, blockIdx.x, 0, C, 0);
   }
 }
 
@@ -479,7 +481,7 @@ __global__ __launch_bounds__(256) void dw_bwd_fused_kernel(const float* __restri
                                                            BnIn bn, const float* __restrict__ w_crs,
                                                            float* __restrict__ dx, const float* __restrict__ res,
                                                            double* __restrict__ spart, float* __restrict__ wpart,
-                                                           int N, int H, int W, int C, int CL) {
+                                                           int N, int H, int W, int C, int CL, FoldTail ft) {
   static_assert(!STATS || BNX, "input-BN partials need the input BN");
   const int CG = 256 / CL;              // channel groups per block
   const int NI = (CL + 2) * CG;         // dy float4s per LDS row (with the 1-column halos)
@@ -614,7 +616,7 @@ __global__ __launch_bounds__(256) void dw_bwd_fused_kernel(const float* __restri
       const int gq = i >> 3, e = i & 7;
       double a = 0.0;
       for (int k = 0; k < CL; ++k) a += red[k * CG + gq][e];
-      spart[((size_t)strip * 2 + (e >> 2)) * C + (cht * CG + gq) * 4 + (e & 3)] = a;
+      pub_store(spart + ((size_t)strip * 2 + (e >> 2)) * C + (cht * CG + gq) * 4 + (e & 3), a);
     }
     __syncthreads();
   }
@@ -633,6 +635,9 @@ __global__ __launch_bounds__(256) void dw_bwd_fused_kernel(const float* __restri
     float sum = 0.f;
     for (int k = 0; k < CL; ++k) sum += wred[((k * CG + gq) * RS + fl) * 4 + e];
     wpart[((size_t)strip * C + cht * CG * 4) * RS + i] = sum;
+  }
+  if constexpr (STATS) {
+    if (ft.part) fold_tail<256>(ft, strip, cht * CG * 4, CG * 4, cht);
   }
 }
 
@@ -677,9 +682,11 @@ static int launch_dw_fwd(const T* x, const float* wt, const float* bias, T* y, i
                          const T* res, hipStream_t st) {
   const uint32_t xb = (uint32_t)((size_t)N * H * W * C * sizeof(T));
   const dim3 grid((unsigned)cdivll(dw_fwd_threads<ST>(N, OH, OW, C), 256));
+  FoldTail ft;  // an armed in-launch fold of the partial rows (fold_tail.h)
+  if (!part || !fold_take(part, (int)grid.x, C, 1, &ft)) ft.part = nullptr;
 #define DW_LAUNCH(B, ST_, WL_)                                                                                        \
   hipLaunchKernelGGL((dw_fwd_kernel<R, S, ST, B, ST_, WL_, T>), grid, dim3(256), 0, st, x, xb, wt, bias, y, N, H, W, \
-                     C, OH, OW, pad, bn, part, xo, obn, res)
+                     C, OH, OW, pad, bn, part, xo, obn, res, ft)
   const int mode = part ? (xo ? 2 : 1) : 0;
   if (wl == 0 && !bn.mean && mode == 0)
     DW_LAUNCH(false, 0, 0);
@@ -700,7 +707,7 @@ static int launch_dw_fwd(const T* x, const float* wt, const float* bias, T* y, i
   else
     return DK_ERR_ARGS;
 #undef DW_LAUNCH
-  return launch_status();
+  return fold_status(launch_status(), ft);
 }
 
 template <class T>
@@ -949,6 +956,8 @@ DK_API int dk_dwconv_bwd_bnbwd_f32(const float* g, const float* bn_x, int N, int
   float* wpart = static_cast<float*>(ws);
   const BnBwdOut ob{out_mean, out_invstd, out_gamma, out_beta, k12, out_relu};
   const dim3 grid((unsigned)(strips * ncht));
+  FoldTail ft;  // an armed in-launch fold of the input BN's partial rows (fold_tail.h)
+  if (!part || !fold_take(part, strips, C, ncht, &ft)) ft.part = nullptr;
   size_t shm = (size_t)256 * 9 * 4 * sizeof(float);  // the weight-gradient reduction
   const size_t ring = (size_t)2 * (cl + 2) * (256 / cl) * sizeof(f32x4);
   if (ring > shm) shm = ring;
@@ -959,7 +968,7 @@ DK_API int dk_dwconv_bwd_bnbwd_f32(const float* g, const float* bn_x, int N, int
       (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,       \
                                 (int)shm);                                                                           \
     hipLaunchKernelGGL(k, grid, dim3(256), shm, st, g, bn_x, (uint32_t)bytes, ob, x, bn, w_crs, dx, residual, part,  \
-                       wpart, N, H, W, C, cl);                                                                       \
+                       wpart, N, H, W, C, cl, ft);                                                                   \
   }
   if (out_relu) {
     if (part) DWB_LAUNCH(true, true, true) else if (bn_mean) DWB_LAUNCH(true, false, true)
@@ -971,7 +980,8 @@ DK_API int dk_dwconv_bwd_bnbwd_f32(const float* g, const float* bn_x, int N, int
 #undef DWB_LAUNCH
   int rc = launch_status();
   if (rc) return rc;
-  return splitk_reduce(wpart, strips, 1, C * R * S, dw_crs, l2 != 0.f ? w_crs : nullptr, l2, 0, C, C, 1, 1, st);
+  return fold_status(
+      splitk_reduce(wpart, strips, 1, C * R * S, dw_crs, l2 != 0.f ? w_crs : nullptr, l2, 0, C, C, 1, 1, st), ft);
 }
 
 DK_API int dk_dwconv_wgrad_bnx_f32(const float* dy, const float* x, int N, int H, int W, int C, int R, int S,

@@ -164,6 +164,8 @@ struct SubPix {
 // live above the hipError_t range used by the runtime so callers can tell
 // "bad call" from "device fault".
 enum : int { DK_ERR_ARGS = 10001, DK_ERR_WORKSPACE = 10002 };
+// Success, and the launch also folded the BN partials armed for it (dk_bn_fold_arm_*).
+enum : int { DK_FOLDED = 10100 };
 
 // Split-K second stage (reduce.hip): out = sum_s ws[s][M][N] (+ l2 * w), fixed order.
 //   mode 0: out[m][n];  mode 1: columns (r, s, c) with c padded to Cp -> out KCRS.
@@ -177,20 +179,22 @@ bool pw_stream_dgrad_ok(int K, int C, int M);
 int pw_stream_dgrad_rows(int M);
 bool pw_stream_bwd_ok(int K, int C, int M);
 int pw_stream_bwd_rows(int M);
+struct FoldTail;  // fold_tail.h
 int pw_stream_bwd_fused(const float* g, const float* bn_x, int M, const float* om, const float* ois,
                         const float* og, const float* ob, int orelu, const float* k12, const float* w, float* dx,
                         const float* res, const float* x, const float* im, const float* iis, const float* ig,
                         const float* ib, int irelu, double* part, const float* bm, const float* bis,
-                        const float* bgm, const float* bbt, int brelu, float* wpart, hipStream_t st);
+                        const float* bgm, const float* bbt, int brelu, float* wpart, hipStream_t st,
+                        const struct FoldTail* ft = nullptr);
 bool pw_stream_fwd_ok(int K, int C, int M, size_t xbytes);
 int pw_stream_fwd_rows(int M);
 int pw_stream_fwd(const float* x, int N, int H, int W, int stride, int OH, int OW, const float* w,
                   const float* bias, float* y, const float* im, const float* iis, const float* ig,
-                  const float* ib, int irelu, double* part, hipStream_t st);
+                  const float* ib, int irelu, double* part, hipStream_t st, const struct FoldTail* ft = nullptr);
 int pw_stream_dgrad_bnbwd(const float* g, const float* bn_x, int M, const float* om, const float* ois,
                           const float* og, const float* ob, int orelu, const float* k12, float* dy_out,
                           const float* w, float* dx, const float* res, const float* x, const float* im,
                           const float* iis, const float* ig, const float* ib, int irelu, double* part,
-                          hipStream_t st);
+                          hipStream_t st, const struct FoldTail* ft = nullptr);
 
 }  // namespace dk

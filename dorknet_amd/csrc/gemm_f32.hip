@@ -29,6 +29,7 @@
 #include <stdlib.h>
 
 #include "dk_common.h"
+#include "fold_tail.h"
 
 namespace dk {
 
@@ -556,6 +557,7 @@ struct EpStoreStatsT : EpStoreT<O> {
   static constexpr bool kColStats = true;
   using Pre = typename EpStoreT<O>::Pre;
   double* part;
+  FoldTail ft{};  // armed in-launch fold of part (fold_tail.h; set by launch_igemm)
   __device__ __forceinline__ void put4(int m, int n, f32x4 v, const Pre& p, int, double* a, double* b) const {
     const f32x4 o = this->value4(n, v, p);
     st4(this->out + (size_t)m * this->ldo + n, o);
@@ -596,6 +598,7 @@ struct EpStoreBnBwdT : EpStoreT<O> {
   static constexpr bool kColStats = true;
   using Pre = typename EpStoreT<O>::Pre;
   double* part;
+  FoldTail ft{};  // armed in-launch fold of part (fold_tail.h; set by launch_igemm)
   const O* xbn;  // [M][ldo], the BN's raw input
   BnIn bn;
   __device__ __forceinline__ Pre pre4(int m, int n) const {
@@ -665,6 +668,7 @@ struct EpWiden {
 struct EpWidenBnBwd : EpWiden {
   static constexpr bool kColStats = true;
   double* part;
+  FoldTail ft{};
   const float* xbn;  // the BN's raw input on the widened grid
   BnIn bn;
   __device__ __forceinline__ Pre pre4(int m, int n) const { return Pre{ld4(xbn + cell(m) * ldo + n)}; }
@@ -738,7 +742,7 @@ __global__ __launch_bounds__(64 * WM * WN) void igemm_f32(DA da, DB db, EP ep, i
   constexpr int SMEM_RED = EP::kColStats ? (64 * WM * WN / (BN / 4)) * BN * 4 : 0;
   constexpr int SMEM = SMEM_OPS > SMEM_EPI ? (SMEM_OPS > SMEM_RED ? SMEM_OPS : SMEM_RED)
                                            : (SMEM_EPI > SMEM_RED ? SMEM_EPI : SMEM_RED);
-  __shared__ float smem[SMEM];
+  __shared__ __attribute__((aligned(16))) float smem[SMEM];
   float* const As = smem;
   float* const Bs = smem + 2 * ABUF;
 
@@ -899,8 +903,12 @@ __global__ __launch_bounds__(64 * WM * WN) void igemm_f32(DA da, DB db, EP ep, i
         s1 += red[(k * BN + i) * 2 + 0];
         s2 += red[(k * BN + i) * 2 + 1];
       }
-      ep.part[((size_t)mt * 2 + 0) * N + cc] = s1;
-      ep.part[((size_t)mt * 2 + 1) * N + cc] = s2;
+      pub_store(ep.part + ((size_t)mt * 2 + 0) * N + cc, s1);
+      pub_store(ep.part + ((size_t)mt * 2 + 1) * N + cc, s2);
+    }
+    if (ep.ft.part) {
+      __syncthreads();  // done with red[]: the fold reuses the tile's LDS
+      fold_tail<64 * WM * WN>(ep.ft, mt, n0, min(BN, N - n0), bid % tiles_n, reinterpret_cast<double2*>(smem));
     }
   }
 }
@@ -1017,6 +1025,15 @@ static int launch_igemm(const DA& da, const DB& db, const EP& ep, int M, int N, 
   const int kps = KT > 0 ? cdiv(KT, splits) : 1;
   splits = KT > 0 ? cdiv(KT, kps) : 1;
   if (splits_used) *splits_used = splits;
+  if constexpr (EP::kColStats) {
+    // an armed in-launch fold of the column statistics (fold_tail.h): rows = M tiles, one
+    // channel slice per N tile
+    EP e = ep;
+    if (!e.part || splits != 1 || !fold_take(e.part, cdiv(M, BM), N, cdiv(N, BN), &e.ft)) e.ft.part = nullptr;
+    hipLaunchKernelGGL((igemm_f32<BM, BN, BK, WM, WN, A, DA, B, DB, EP>), dim3(tiles, splits), dim3(NT), dyn, st, da,
+                       db, e, M, N, Ktot, kps);
+    return fold_status(launch_status(), e.ft);
+  }
   hipLaunchKernelGGL((igemm_f32<BM, BN, BK, WM, WN, A, DA, B, DB, EP>), dim3(tiles, splits), dim3(NT), dyn, st, da,
                      db, ep, M, N, Ktot, kps);
   return launch_status();
@@ -1539,8 +1556,13 @@ DK_API int dk_pwconv_fwd_ex_f32(const float* x, int N, int H, int W, int C, cons
   if (C % 4 || !aligned16(x) || !aligned16(w_kc) || !fits((size_t)N * H * W * C * 4)) return DK_ERR_ARGS;
   if (pw_stream_fwd_ok(K, C, N * OH * OW, (size_t)N * H * W * C * 4) && (!bn_mean || bn_ok(bn_mean, bn_invstd, bn_gamma, bn_beta)))
     // K = C = 64: the persistent streaming kernel (pw_stream.hip), bit-identical outputs
-    return pw_stream_fwd(x, N, H, W, stride, OH, OW, w_kc, bias, y, bn_mean, bn_invstd, bn_gamma, bn_beta, bn_relu,
-                         stats, as_stream(stream));
+  {
+    FoldTail ft;
+    if (stats) fold_take(stats, pw_stream_fwd_rows(N * OH * OW), K, 1, &ft);
+    return fold_status(pw_stream_fwd(x, N, H, W, stride, OH, OW, w_kc, bias, y, bn_mean, bn_invstd, bn_gamma,
+                                     bn_beta, bn_relu, stats, as_stream(stream), stats ? &ft : nullptr),
+                       stats ? ft : FoldTail{});
+  }
   return conv_fwd_ex(img1(x, N, H, W, C, OH, OW, stride, N * OH * OW), w_kc, K, C, bias, y, bn_mean,
                      bn_invstd, bn_gamma, bn_beta, bn_relu, stats, stream);
 }
@@ -1649,9 +1671,12 @@ DK_API int dk_pwconv_dgrad_bnbwd_f32(const float* g, const float* bn_x, int N, i
   if (pw_stream_dgrad_ok(K, C, M)) {
     // K = C = 64: the persistent streaming kernel (pw_stream.hip), bit-identical results
     if (part && !bn_ok(bn_mean, bn_invstd, bn_gamma, bn_beta)) return DK_ERR_ARGS;
-    return pw_stream_dgrad_bnbwd(g, bn_x, M, out_mean, out_invstd, out_gamma, out_beta, out_relu, k12, dy_out, w_kc,
-                                 dx, residual, part ? x : nullptr, bn_mean, bn_invstd, bn_gamma, bn_beta, bn_relu,
-                                 part, st);
+    FoldTail ft;
+    if (part) fold_take(part, pw_stream_dgrad_rows(M), C, 1, &ft);
+    return fold_status(pw_stream_dgrad_bnbwd(g, bn_x, M, out_mean, out_invstd, out_gamma, out_beta, out_relu, k12,
+                                             dy_out, w_kc, dx, residual, part ? x : nullptr, bn_mean, bn_invstd,
+                                             bn_gamma, bn_beta, bn_relu, part, st, part ? &ft : nullptr),
+                       part ? ft : FoldTail{});
   }
   if (!part) {
     EpStore ep = ep_store(dx, C, nullptr, residual);
@@ -1754,6 +1779,9 @@ static inline ImgDescE<bf16_t, true> img1_h(const bf16_t* x, int N, int H, int W
 }
 static inline bool al8(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 7) == 0; }
 }  // namespace dk
+
+// partial-statistics rows of dk_pwconv_fwd_ex_bf16 (always the tiled engine: one row per M tile)
+DK_API int dk_pwconv_fwd_bf16_stats_rows(int N, int OH, int OW, int K, int C) { return stats_rows(N * OH * OW, K, C); }
 
 DK_API int dk_pwconv_fwd_ex_bf16(const bf16_t* x, int N, int H, int W, int C, const float* w_kc, int K, int stride,
                                  const float* bias, bf16_t* y, int OH, int OW, const float* bn_mean,

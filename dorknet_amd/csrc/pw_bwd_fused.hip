@@ -29,6 +29,7 @@
 #include <stdlib.h>
 
 #include "dk_common.h"
+#include "fold_tail.h"
 
 namespace dk {
 
@@ -359,11 +360,14 @@ DK_API int dk_pwconv_bwd_bnbwd_f32(const float* g, const float* bn_x, int N, int
     const int nb = pw_stream_bwd_rows((int)P);
     if (ws_bytes < (size_t)nb * K * C * sizeof(float)) return DK_ERR_WORKSPACE;
     float* wp = static_cast<float*>(ws);
+    FoldTail ft;
+    if (part) fold_take(part, nb, C, 1, &ft);
     int rc = pw_stream_bwd_fused(g, bn_x, (int)P, out_mean, out_invstd, out_gamma, out_beta, out_relu, k12, w_kc, dx,
                                  residual, x, bn_mean, bn_invstd, bn_gamma, bn_beta, bn_relu, part, bn_mean,
-                                 bn_invstd, bn_gamma, bn_beta, bn_relu, wp, st);
+                                 bn_invstd, bn_gamma, bn_beta, bn_relu, wp, st, part ? &ft : nullptr);
     if (rc) return rc;
-    return splitk_reduce(wp, nb, K, C, dw_kc, l2 != 0.f ? w_kc : nullptr, l2, 0, C, C, 1, 1, st);
+    return fold_status(splitk_reduce(wp, nb, K, C, dw_kc, l2 != 0.f ? w_kc : nullptr, l2, 0, C, C, 1, 1, st),
+                       part ? ft : FoldTail{});
   }
   int tpb = 1;
   const int nblk = pwf_blocks(P, K, C, &tpb);

@@ -27,6 +27,7 @@
 #include <stdlib.h>
 
 #include "dk_common.h"
+#include "fold_tail.h"
 
 namespace dk {
 namespace pws {
@@ -60,6 +61,7 @@ struct DgradArgs {
   int irelu;
   double* part;       // [gridDim.x][2][NO]
   int M;
+  FoldTail ft;        // ft.part != nullptr: fold the partial rows in this launch (fold_tail.h)
 };
 
 __device__ __forceinline__ uint32_t row_off_bytes(int m, int ld, int c) { return ((uint32_t)m * ld + c) * 4u; }
@@ -256,8 +258,9 @@ __global__ __launch_bounds__(256, 2) void dgrad_bnbwd_kernel(DgradArgs a) {
     double s = 0.0;
 #pragma unroll
     for (int w = 0; w < WAVES; ++w) s += red[w][which][c];
-    a.part[((size_t)blockIdx.x * 2 + which) * NO + c] = s;
+    pub_store(a.part + ((size_t)blockIdx.x * 2 + which) * NO + c, s);
   }
+  if (a.ft.part) fold_tail<256>(a.ft, blockIdx.x, 0, NO, 0);
 }
 
 
@@ -281,6 +284,7 @@ struct FwdArgs {
   double* part;       // [gridDim.x][2][NO] (sum y, sum y^2) nullable
   int M, H, W, OH, OW, sa;
   uint32_t xbytes;
+  FoldTail ft;        // ft.part != nullptr: fold the statistics rows in this launch
 };
 
 template <bool BN, bool STATS, bool STRIDED>
@@ -420,8 +424,9 @@ __global__ __launch_bounds__(256, 3) void fwd_kernel(FwdArgs a) {
     double s = 0.0;
 #pragma unroll
     for (int w = 0; w < WAVES; ++w) s += red[w][which][c];
-    a.part[((size_t)blockIdx.x * 2 + which) * NO + c] = s;
+    pub_store(a.part + ((size_t)blockIdx.x * 2 + which) * NO + c, s);
   }
+  if (a.ft.part) fold_tail<256>(a.ft, blockIdx.x, 0, NO, 0);
 }
 
 // Resident blocks per CU of a family of instantiations (the smallest; queried once per family).
@@ -725,8 +730,9 @@ __global__ __launch_bounds__(256, 1) void bwd_fused_kernel(BwdArgs ba) {
       double s2 = 0.0;
 #pragma unroll
       for (int w = 0; w < WAVES; ++w) s2 += red[w][which][c];
-      a.part[((size_t)blockIdx.x * 2 + which) * NO + c] = s2;
+      pub_store(a.part + ((size_t)blockIdx.x * 2 + which) * NO + c, s2);
     }
+    if (a.ft.part) fold_tail<256>(a.ft, blockIdx.x, 0, NO, 0);
   }
 }
 
@@ -777,9 +783,11 @@ int pw_stream_bwd_fused(const float* g, const float* bn_x, int M, const float* o
                         const float* og, const float* ob, int orelu, const float* k12, const float* w, float* dx,
                         const float* res, const float* x, const float* im, const float* iis, const float* ig,
                         const float* ib, int irelu, double* part, const float* bm, const float* bis,
-                        const float* bgm, const float* bbt, int brelu, float* wpart, hipStream_t st) {
+                        const float* bgm, const float* bbt, int brelu, float* wpart, hipStream_t st,
+                        const FoldTail* ft) {
   pws::BwdArgs a{{g, bn_x, nullptr, w, dx, res, x, om, ois, og, ob, k12, orelu, im, iis, ig, ib, irelu, part, M},
                  bm, bis, bgm, bbt, brelu, wpart};
+  if (ft && part) a.d.ft = *ft;
   const dim3 grid(pws::bwd_fused_blocks(M));
   const bool r = res != nullptr, pt = part != nullptr, bn = bm != nullptr;
   if (pt && !bn) return DK_ERR_ARGS;
@@ -797,10 +805,11 @@ int pw_stream_bwd_fused(const float* g, const float* bn_x, int M, const float* o
 
 int pw_stream_fwd(const float* x, int N, int H, int W, int stride, int OH, int OW, const float* w,
                   const float* bias, float* y, const float* im, const float* iis, const float* ig,
-                  const float* ib, int irelu, double* part, hipStream_t st) {
+                  const float* ib, int irelu, double* part, hipStream_t st, const FoldTail* ft) {
   const int M = N * OH * OW;
   pws::FwdArgs a{x, w, bias, y, im, iis, ig, ib, irelu, part, M, H, W, OH, OW, stride,
                  (uint32_t)((size_t)N * H * W * 64 * 4)};
+  if (ft && part) a.ft = *ft;
   const dim3 grid(pws::fwd_blocks(M));
   const bool strided = stride != 1;
 #define DK_FWD(BN_, ST_)                                                                   \
@@ -825,8 +834,9 @@ int pw_stream_dgrad_bnbwd(const float* g, const float* bn_x, int M, const float*
                           const float* og, const float* ob, int orelu, const float* k12, float* dy_out,
                           const float* w, float* dx, const float* res, const float* x, const float* im,
                           const float* iis, const float* ig, const float* ib, int irelu, double* part,
-                          hipStream_t st) {
+                          hipStream_t st, const FoldTail* ft) {
   pws::DgradArgs a{g, bn_x, dy_out, w, dx, res, x, om, ois, og, ob, k12, orelu, im, iis, ig, ib, irelu, part, M};
+  if (ft && part) a.ft = *ft;
   const dim3 grid(pws::dgrad_blocks(M));
   if (res && x)
     hipLaunchKernelGGL((pws::dgrad_bnbwd_kernel<true, true>), grid, dim3(256), 0, st, a);

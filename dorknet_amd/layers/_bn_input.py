@@ -52,11 +52,28 @@ class BNOut:
         return (self.mean.data_ptr(), self.invstd.data_ptr(), self.gamma.data_ptr(), self.beta.data_ptr(),
                 int(self.relu))
 
-    def hand_backward_partials(self, dx, part):
+    def arm_partials(self, part):
+        """Before a consumer's backward launch that writes stage 1 of this BatchNorm's backward
+        into `part`: arm an in-launch fold (dorknet_amd/csrc/fold_tail.h), so that the launch
+        also finalizes dgamma / dbeta / k12.  Returns a token for hand_backward_partials."""
+        from .._hip import inlaunch_folds_enabled
+        if self.owner is None or not inlaunch_folds_enabled():
+            return None
+        return self.owner.arm_bwd_fold(part)
+
+    def hand_backward_partials(self, dx, part, status=0, token=None):
         """A consumer's backward computed stage 1 of this BatchNorm's backward (the
-        *_dgrad_ex_f32 epilogue) while producing `dx`, the gradient w.r.t. this BNOut."""
+        *_dgrad_ex_f32 epilogue) while producing `dx`, the gradient w.r.t. this BNOut;
+        `status` / `token`: the launch's return value and arm_partials' token."""
+        from .._hip import DK_FOLDED
+        folded = None
+        if token is not None:
+            if status == DK_FOLDED:
+                folded = token
+            else:
+                lib.dk_bn_fold_disarm()
         if self.owner is not None:
-            self.owner._pending_bwd = (dx, part)
+            self.owner._pending_bwd = (dx, part, folded)
 
     def materialize(self):
         """The normalised tensor itself (computed once)."""

@@ -54,12 +54,39 @@ def plan_group(layers, i, fuse, out_accepts=False, keep=()):
 class StatsRequest:
     """Asks a producer layer (``produces_bn_stats``) to emit, with its forward output, the
     BatchNorm partial statistics of that output (the *_fwd_ex_f32 entry points); the
-    BatchNormLayer that follows then skips its own statistics pass."""
-    __slots__ = ("part", "rows")
+    BatchNormLayer that follows then skips its own statistics pass.
 
-    def __init__(self):
+    With ``bn`` (the BatchNormLayer that will consume them) the producer also arms an in-launch
+    fold (``arm`` before its launch, ``launched`` after it; dorknet_amd/csrc/fold_tail.h): the
+    producer's last blocks then finalize the statistics themselves and the BatchNormLayer skips
+    the fold launch too."""
+    __slots__ = ("part", "rows", "bn", "armed", "folded")
+
+    def __init__(self, bn=None):
         self.part = None   # fp64 device tensor [rows, 2, C], set by the producer
         self.rows = 0
+        self.bn = bn
+        self.armed = None   # (mean, std, invstd) the armed fold will write
+        self.folded = None  # the same, once the producer's launch has folded
+
+    def arm(self, part, P):
+        """Before the producer's launch: `part` [rows, 2, C] will hold its partial sums over P
+        pixels per channel."""
+        from .._hip import inlaunch_folds_enabled
+        if self.bn is not None and inlaunch_folds_enabled():
+            self.armed = self.bn.arm_stats_fold(part, P)
+
+    def launched(self, part, status):
+        """After the producer's launch (`status`: the entry point's return value)."""
+        from .._hip import DK_FOLDED, lib
+        self.part, self.rows = part, part.shape[0]
+        if self.armed is not None:
+            if status == DK_FOLDED:
+                self.folded = self.armed
+                self.bn._first_pending = False
+            else:
+                lib.dk_bn_fold_disarm()
+            self.armed = None
 
 
 def run_group(group, mode, X, test_mode=False, stats_req=None, bn_stats=None):
@@ -91,7 +118,7 @@ def execute(layers, X, test_mode=False, out_accepts=False, keep=(), visit=None):
         req = None
         if (fuse and not test_mode and mode == "single" and getattr(group[0], "produces_bn_stats", False)
                 and nxt < len(layers) and type(layers[nxt]) is BatchNormLayer):
-            req = StatsRequest()
+            req = StatsRequest(layers[nxt])
         X = run_group(group, mode, X, test_mode, stats_req=req, bn_stats=pending)
         pending = req if req is not None and req.part is not None else None
         steps.append(group)

@@ -132,9 +132,10 @@ class ReLu(Layer):
             P = dy.numel() // C
             nb = lib.dk_bn_workspace_bytes(P, C)
             part = torch.empty((lib.dk_bn_partial_blocks(P, C), 2, C), dtype=torch.float64, device=dy.device)
-            lib.dk_relu_bwd_bn_partial_f64(dy.data_ptr(), self._mask.data_ptr(), bn.x.data_ptr(), P, C,
-                                           *bn.bn_args(), dx.data_ptr(), part.data_ptr(), nb, stream_handle())
-            bn.hand_backward_partials(dx, part)
+            tok = bn.arm_partials(part)
+            r = lib.dk_relu_bwd_bn_partial_f64(dy.data_ptr(), self._mask.data_ptr(), bn.x.data_ptr(), P, C,
+                                               *bn.bn_args(), dx.data_ptr(), part.data_ptr(), nb, stream_handle())
+            bn.hand_backward_partials(dx, part, r, tok)
             return dx
         bwd = lib.dk_relu_bwd_bf16 if dy.dtype == torch.bfloat16 else lib.dk_relu_bwd_f32
         bwd(dy.data_ptr(), self._mask.data_ptr(), dy.numel(), dx.data_ptr(), stream_handle())

@@ -20,7 +20,7 @@ from __future__ import annotations
 
 import torch
 
-from .._hip import lib, stream_handle, tickets, workspace
+from .._hip import fold_resources, lib, stream_handle, tickets, workspace
 from .._tensor import BF16, act_dtype, as_device, empty_nhwc, rows, to_nhwc
 from ._bn_input import BNGrad
 from ._common import grad_buffer
@@ -86,18 +86,63 @@ class BatchNormLayer(Layer):
         import torch.distributed as dist
         return dist.get_world_size(self.sync_group)
 
-    def _stats(self, x, P, C, st, partials=None):
-        dev = x.device
+    def _stats_outputs(self, C, dev):
+        """Fresh mean / std / invstd and the running statistics (allocated on the first batch)."""
         mean = torch.empty(C, dtype=torch.float32, device=dev)
         std = torch.empty(C, dtype=torch.float32, device=dev)
         invstd = torch.empty(C, dtype=torch.float32, device=dev)
         nlp = self.non_learned_params
-        first = nlp["running_mean"] is None
-        if first:
+        # _first_pending: an armed in-launch fold allocated the running statistics but did not run
+        first = nlp["running_mean"] is None or getattr(self, "_first_pending", False)
+        if nlp["running_mean"] is None:
             nlp["running_mean"] = torch.empty(self._param_shape(C), dtype=torch.float32, device=dev)
             nlp["running_std"] = torch.empty(self._param_shape(C), dtype=torch.float32, device=dev)
         rm, rs = as_device(nlp["running_mean"]), as_device(nlp["running_std"])
         nlp["running_mean"], nlp["running_std"] = rm, rs
+        return mean, std, invstd, rm, rs, first
+
+    def arm_stats_fold(self, part, P):
+        """Arm the producer's launch that writes `part` ([rows, 2, C] partial sums over P pixels)
+        to finalize this layer's batch statistics itself (dk_bn_fold_arm_stats, fold_tail.h).
+        Returns the (mean, std, invstd) it will write, or None (SyncBN, or a mismatch)."""
+        C = part.shape[-1]
+        if self.sync_group is not None or part.dtype != torch.float64:
+            return None
+        mean, std, invstd, rm, rs, first = self._stats_outputs(C, part.device)
+        self._first_pending = bool(first)
+        t, nt, sc, nsc = fold_resources.get()
+        lib.dk_bn_fold_arm_stats(part.data_ptr(), part.shape[0], C, float(P), float(self.eps),
+                                 float(self.run_momentum), int(first), mean.data_ptr(), std.data_ptr(),
+                                 invstd.data_ptr(), rm.data_ptr(), rs.data_ptr(), t, nt, sc, nsc)
+        return mean, std, invstd
+
+    def arm_bwd_fold(self, part):
+        """Arm the consumer's backward launch that writes stage 1 of this layer's backward into
+        `part` to finalize dgamma, dbeta and k12 itself (dk_bn_fold_arm_bwd).  Returns k12, or
+        None (SyncBN: the partial sums are all-reduced first)."""
+        x = getattr(self, "X", None)
+        if self.sync_group is not None or x is None or part.dtype != torch.float64:
+            return None
+        C = x.shape[1]
+        if part.shape[-1] != C:
+            return None
+        P = x.numel() // C
+        gamma, beta = self.learned_params["gamma"], self.learned_params["beta"]
+        dgamma = grad_buffer(self, "gamma", gamma.shape)
+        dbeta = grad_buffer(self, "beta", beta.shape)
+        k12 = torch.empty(2 * C, dtype=torch.float32, device=x.device)
+        t, nt, sc, nsc = fold_resources.get()
+        lib.dk_bn_fold_arm_bwd(part.data_ptr(), part.shape[0], C, float(P), dgamma.data_ptr(), dbeta.data_ptr(),
+                               k12.data_ptr(), t, nt, sc, nsc)
+        return k12
+
+    def _stats(self, x, P, C, st, partials=None):
+        dev = x.device
+        if partials is not None and getattr(partials, "folded", None) is not None:
+            # the producer's launch folded them (fold_tail.h) -- running statistics included
+            return partials.folded
+        mean, std, invstd, rm, rs, first = self._stats_outputs(C, dev)
+        self._first_pending = False
         if partials is not None and partials.part.shape[-1] != C:
             partials = None
         if partials is not None:
@@ -214,15 +259,19 @@ class BatchNormLayer(Layer):
             # stage 1 was computed by the consumer's dgrad epilogue (layers/_bn_input.py)
             part = pending[1]
             nrows = part.shape[0]
-            k12 = torch.empty(2 * C, dtype=torch.float32, device=x.device)
+            k12 = pending[2]
             nb = lib.dk_bn_partials_workspace_bytes(nrows, C)
             ws = workspace.get(nb)
-            if self.sync_group is None:
+            if k12 is not None:
+                pass  # folded (and dgamma / dbeta written) inside the consumer's launch
+            elif self.sync_group is None:
+                k12 = torch.empty(2 * C, dtype=torch.float32, device=x.device)
                 lib.dk_bn_bwd_from_partials_f32(part.data_ptr(), nrows, C, float(P), dgamma.data_ptr(),
                                                 dbeta.data_ptr(), k12.data_ptr(), ws, nb,
                                                 tickets.get(lib.dk_bn_fold_tickets_count(C)), st)
             else:
                 import torch.distributed as dist
+                k12 = torch.empty(2 * C, dtype=torch.float32, device=x.device)
                 local = torch.empty(2 * C, dtype=torch.float64, device=x.device)
                 lib.dk_bn_reduce_partials_f64(part.data_ptr(), nrows, C, local.data_ptr(), ws, nb, st)
                 glob = local.clone()

@@ -90,11 +90,13 @@ class ConvLayer(Layer):
             rows = lib.dk_conv2d_fwd_stats_rows(N, OH, OW, K, Cp, R, S)
             stats = torch.empty((rows, 2, K), dtype=torch.float64, device=x.device)
         if bn is not None or stats is not None:
-            lib.dk_conv2d_fwd_ex_f32(x.data_ptr(), N, H, W, Cp, w_krsc.data_ptr(), K, R, S, self.stride,
-                                     self.padding, ptr(bias), y.data_ptr(), OH, OW,
-                                     *(bn.bn_args() if bn is not None else (0, 0, 0, 0, 0)), ptr(stats), st)
             if stats is not None:
-                bn_stats.part, bn_stats.rows = stats, stats.shape[0]
+                bn_stats.arm(stats, N * OH * OW)
+            r = lib.dk_conv2d_fwd_ex_f32(x.data_ptr(), N, H, W, Cp, w_krsc.data_ptr(), K, R, S, self.stride,
+                                         self.padding, ptr(bias), y.data_ptr(), OH, OW,
+                                         *(bn.bn_args() if bn is not None else (0, 0, 0, 0, 0)), ptr(stats), st)
+            if stats is not None:
+                bn_stats.launched(stats, r)
         else:
             lib.dk_conv2d_fwd_f32(x.data_ptr(), N, H, W, Cp, w_krsc.data_ptr(), K, R, S, self.stride, self.padding,
                                   ptr(bias), y.data_ptr(), OH, OW, st)

@@ -86,10 +86,12 @@ class DepthwiseConvLayer(Layer):
                 stats = torch.empty((rows, 2, C), dtype=torch.float64, device=x.device)
         w = self.learned_params["weights"]  # W[C][R][S], read in place by the _ex entry
         fwd = lib.dk_dwconv_fwd_ex_bf16 if bf else lib.dk_dwconv_fwd_ex_f32
-        fwd(x.data_ptr(), N, H, W, C, w.data_ptr(), R, S, self.stride, self.padding, ptr(bias), y.data_ptr(), OH, OW,
-            *(bn.bn_args() if bn is not None else (0, 0, 0, 0, 0)), ptr(stats), st)
+        if stats is not None and not bf:
+            bn_stats.arm(stats, N * OH * OW)
+        r = fwd(x.data_ptr(), N, H, W, C, w.data_ptr(), R, S, self.stride, self.padding, ptr(bias), y.data_ptr(), OH,
+                OW, *(bn.bn_args() if bn is not None else (0, 0, 0, 0, 0)), ptr(stats), st)
         if stats is not None:
-            bn_stats.part, bn_stats.rows = stats, stats.shape[0]
+            bn_stats.launched(stats, r)
         if not test_mode:
             # the reference keeps the *padded* input (:87-88); padding is implicit here, and
             # a BNOut input is kept as the BatchNorm's raw input + parameters
@@ -138,16 +140,17 @@ class DepthwiseConvLayer(Layer):
             part = torch.empty((rows, 2, C), dtype=torch.float64, device=x.device)
         g = to_nhwc(G.g)
         nb = lib.dk_dwconv_bwd_bnbwd_workspace_bytes(N, H, W, C, R, S)
-        lib.dk_dwconv_bwd_bnbwd_f32(g.data_ptr(), G.x.data_ptr(), N, H, W, C, *G.bnbwd_args(), x.data_ptr(),
-                                    w.data_ptr(), R, S, self.padding, s or 0.0, gw.data_ptr(), ptr(dx), ptr(res),
-                                    *(bn.bn_args() if bn is not None else (0, 0, 0, 0, 0)), ptr(part),
-                                    workspace.get(nb), nb, st)
+        tok = bn.arm_partials(part) if part is not None else None
+        r = lib.dk_dwconv_bwd_bnbwd_f32(g.data_ptr(), G.x.data_ptr(), N, H, W, C, *G.bnbwd_args(), x.data_ptr(),
+                                        w.data_ptr(), R, S, self.padding, s or 0.0, gw.data_ptr(), ptr(dx), ptr(res),
+                                        *(bn.bn_args() if bn is not None else (0, 0, 0, 0, 0)), ptr(part),
+                                        workspace.get(nb), nb, st)
         if s is None:
             add_regulariser_grad(gw, w, self.weight_regulariser)
         if not need_dx:
             return None
         if part is not None:
-            bn.hand_backward_partials(dx, part)
+            bn.hand_backward_partials(dx, part, r, tok)
         if residual is not None and res is None:
             dx = add_residual(dx, residual)  # (a new tensor: the BN then recomputes its sums)
         return dx
@@ -205,9 +208,10 @@ class DepthwiseConvLayer(Layer):
         if rows and self.padding <= R - 1:
             # + stage 1 of the input BatchNorm's backward, in the dgrad epilogue (+ the residual)
             part = torch.empty((rows, 2, C), dtype=torch.float64, device=dx.device)
-            dgrad_ex(dy.data_ptr(), N, OH, OW, C, w.data_ptr(), R, S, self.stride, self.padding, dx.data_ptr(), H, W,
-                     workspace.get(nb), nb, ptr(res), bn.x.data_ptr(), *bn.bn_args(), part.data_ptr(), st)
-            bn.hand_backward_partials(dx, part)
+            tok = bn.arm_partials(part) if not bf else None
+            r = dgrad_ex(dy.data_ptr(), N, OH, OW, C, w.data_ptr(), R, S, self.stride, self.padding, dx.data_ptr(), H,
+                         W, workspace.get(nb), nb, ptr(res), bn.x.data_ptr(), *bn.bn_args(), part.data_ptr(), st)
+            bn.hand_backward_partials(dx, part, r, tok)
             return dx
         if bf:
             if residual is not None and res is None:

@@ -97,14 +97,16 @@ class PointwiseConvLayer(Layer):
         bias = self.learned_params["bias"] if self.with_bias else None
         stats = None
         if bn_stats is not None and not test_mode:
-            rows = lib.dk_pwconv_fwd_stats_rows(N, OH, OW, K, Cp)
+            rows = (lib.dk_pwconv_fwd_bf16_stats_rows if bf else lib.dk_pwconv_fwd_stats_rows)(N, OH, OW, K, Cp)
             stats = torch.empty((rows, 2, K), dtype=torch.float64, device=x.device)
         if bn is not None or stats is not None or bf:
             fwd = lib.dk_pwconv_fwd_ex_bf16 if bf else lib.dk_pwconv_fwd_ex_f32
-            fwd(x.data_ptr(), N, H, W, Cp, w.data_ptr(), K, s, ptr(bias), y.data_ptr(), OH, OW,
-                *(bn.bn_args() if bn is not None else (0, 0, 0, 0, 0)), ptr(stats), st)
+            if stats is not None and not bf:
+                bn_stats.arm(stats, N * OH * OW)
+            r = fwd(x.data_ptr(), N, H, W, Cp, w.data_ptr(), K, s, ptr(bias), y.data_ptr(), OH, OW,
+                    *(bn.bn_args() if bn is not None else (0, 0, 0, 0, 0)), ptr(stats), st)
             if stats is not None:
-                bn_stats.part, bn_stats.rows = stats, stats.shape[0]
+                bn_stats.launched(stats, r)
         else:
             lib.dk_pwconv_fwd_f32(x.data_ptr(), N, H, W, Cp, w.data_ptr(), K, s, ptr(bias), y.data_ptr(), OH, OW, st)
         # the reference keeps the NHWC row copy as self.patches (:50); here the input itself
@@ -236,10 +238,11 @@ class PointwiseConvLayer(Layer):
         gw = grad_buffer(self, "weights", (K, C))
         l2s = l2_strength(self.weight_regulariser)
         nb = lib.dk_pwconv_bwd_fused_workspace_bytes(N, OH, OW, K, C)
-        lib.dk_pwconv_bwd_bnbwd_f32(g.data_ptr(), bg.x.data_ptr(), N, OH, OW, K, *bg.bnbwd_args(), w.data_ptr(), C,
-                                    l2s or 0.0, gw.data_ptr(), dx.data_ptr(), ptr(res), x.data_ptr(),
-                                    *((*bn.bn_args(), part.data_ptr()) if bn is not None else (0, 0, 0, 0, 0, 0)),
-                                    workspace.get(nb), nb, st)
+        tok = bn.arm_partials(part) if bn is not None else None
+        r = lib.dk_pwconv_bwd_bnbwd_f32(g.data_ptr(), bg.x.data_ptr(), N, OH, OW, K, *bg.bnbwd_args(), w.data_ptr(),
+                                        C, l2s or 0.0, gw.data_ptr(), dx.data_ptr(), ptr(res), x.data_ptr(),
+                                        *((*bn.bn_args(), part.data_ptr()) if bn is not None else (0, 0, 0, 0, 0, 0)),
+                                        workspace.get(nb), nb, st)
         if l2s is None:
             add_regulariser_grad(gw, w, self.weight_regulariser)
         # the weight gradient was written on this stream: work queued on the side stream from
@@ -247,7 +250,7 @@ class PointwiseConvLayer(Layer):
         with weight_grad_stream():
             pass
         if bn is not None:
-            bn.hand_backward_partials(dx, part)
+            bn.hand_backward_partials(dx, part, r, tok)
         return dx
 
     def _dgrad_bnbwd(self, bg, dy_out, residual, st):
@@ -264,12 +267,13 @@ class PointwiseConvLayer(Layer):
         if bn is not None:
             rows = lib.dk_pwconv_dgrad_bnbwd_stats_rows(N, OH, OW, K, C)
             part = torch.empty((rows, 2, C), dtype=torch.float64, device=dx.device)
-        lib.dk_pwconv_dgrad_bnbwd_f32(g.data_ptr(), bg.x.data_ptr(), N, OH, OW, K, *bg.bnbwd_args(),
-                                      dy_out.data_ptr(), w.data_ptr(), C, dx.data_ptr(), ptr(res),
-                                      *((bn.x.data_ptr(), *bn.bn_args(), part.data_ptr()) if bn is not None
-                                        else (0, 0, 0, 0, 0, 0, 0)), st)
+        tok = bn.arm_partials(part) if bn is not None else None
+        r = lib.dk_pwconv_dgrad_bnbwd_f32(g.data_ptr(), bg.x.data_ptr(), N, OH, OW, K, *bg.bnbwd_args(),
+                                          dy_out.data_ptr(), w.data_ptr(), C, dx.data_ptr(), ptr(res),
+                                          *((bn.x.data_ptr(), *bn.bn_args(), part.data_ptr()) if bn is not None
+                                            else (0, 0, 0, 0, 0, 0, 0)), st)
         if bn is not None:
-            bn.hand_backward_partials(dx, part)
+            bn.hand_backward_partials(dx, part, r, tok)
         if residual is not None and res is None:
             dx = add_residual(dx, residual)
         return dx
@@ -328,9 +332,10 @@ class PointwiseConvLayer(Layer):
             # + stage 1 of the input BatchNorm's backward, in the dgrad epilogue
             rows = lib.dk_pwconv_dgrad_stats_rows(N, OH, OW, K, C)
             part = torch.empty((rows, 2, C), dtype=torch.float64, device=dx.device)
-            lib.dk_pwconv_dgrad_ex_f32(dy.data_ptr(), N, OH, OW, K, w.data_ptr(), C, s, dx.data_ptr(), ptr(res),
-                                       bn.x.data_ptr(), *bn.bn_args(), part.data_ptr(), st)
-            bn.hand_backward_partials(dx, part)
+            tok = bn.arm_partials(part)
+            r = lib.dk_pwconv_dgrad_ex_f32(dy.data_ptr(), N, OH, OW, K, w.data_ptr(), C, s, dx.data_ptr(), ptr(res),
+                                           bn.x.data_ptr(), *bn.bn_args(), part.data_ptr(), st)
+            bn.hand_backward_partials(dx, part, r, tok)
         elif res is not None:
             lib.dk_pwconv_dgrad_ex_f32(dy.data_ptr(), N, OH, OW, K, w.data_ptr(), C, s, dx.data_ptr(), res.data_ptr(),
                                        0, 0, 0, 0, 0, 0, 0, st)

@@ -199,6 +199,7 @@ int dk_bn_bwd_apply_bf16(const uint16_t* x, const uint16_t* dy, long long numel,
 int dk_bn_bwd_bf16(const uint16_t* x, const uint16_t* dy, int P, int C, const float* mean, const float* invstd, const float* gamma, const float* beta, int relu, float* dgamma, float* dbeta, uint16_t* dx, void* ws, size_t ws_bytes, void* stream);
 int dk_relu_fwd_bf16(const uint16_t* x, long long n, uint16_t* y, uint8_t* mask, void* stream);
 int dk_relu_bwd_bf16(const uint16_t* dy, const uint8_t* mask, long long n, uint16_t* dx, void* stream);
+int dk_pwconv_fwd_bf16_stats_rows(int N, int OH, int OW, int K, int C);
 int dk_pwconv_fwd_ex_bf16(const uint16_t* x, int N, int H, int W, int C, const float* w_kc, int K, int stride, const float* bias, uint16_t* y, int OH, int OW, const float* bn_mean, const float* bn_invstd, const float* bn_gamma, const float* bn_beta, int bn_relu, double* stats, void* stream);
 int dk_pwconv_dgrad_ex_bf16(const uint16_t* dy, int N, int OH, int OW, int K, const float* w_kc, int C, int stride, uint16_t* dx, const uint16_t* residual, const uint16_t* bn_x, const float* bn_mean, const float* bn_invstd, const float* bn_gamma, const float* bn_beta, int bn_relu, double* part, void* stream);
 int dk_pwconv_wgrad_bnx_bf16(const uint16_t* dy, const uint16_t* x, int N, int H, int W, int C, int K, int stride, int OH, int OW, const float* w_kc, float l2, float* dw_kc, void* ws, size_t ws_bytes, const float* bn_mean, const float* bn_invstd, const float* bn_gamma, const float* bn_beta, int bn_relu, void* stream);
@@ -280,6 +281,23 @@ int dk_bn_reduce_partials_f64(const void* part, int nblk, int C, void* out, void
  * stage 1 of the backward of the BN feeding the join: dx = mask ? dy : 0 and part (sized
  * dk_bn_workspace_bytes(P, C), dk_bn_partial_blocks(P, C) rows). */
 int dk_bn_bwd_from_partials_f32(const void* part, int nblk, int C, double count, float* dgamma, float* dbeta, float* k12, void* ws, size_t ws_bytes, unsigned* tickets, void* stream);
+/* In-launch folds.  Arm a partials buffer before the entry point that writes it: that launch's
+ * last-arriving blocks then fold the rows (two ticketed levels, fixed order) and finalize
+ * exactly what dk_bn_stats_from_partials_f32 (arm_stats) or dk_bn_bwd_from_partials_f32
+ * (arm_bwd) would, and the entry point returns DK_FOLDED (10100) instead of 0 -- the caller
+ * skips the separate fold launch.  Entry points that take an arming: dk_pwconv_fwd_ex_f32,
+ * dk_dwconv_fwd_ex_f32, dk_conv2d_fwd_ex_f32, dk_pwconv_dgrad_bnbwd_f32, dk_pwconv_dgrad_ex_f32,
+ * dk_pwconv_bwd_bnbwd_f32, dk_dwconv_bwd_bnbwd_f32, dk_dwconv_dgrad_ex_f32,
+ * dk_relu_bwd_bn_partial_f64 (for the paths that implement it; otherwise they return 0 and
+ * the caller folds as before and calls dk_bn_fold_disarm).  One arming per host thread; the
+ * next entry point that writes that buffer consumes it.  tickets: >= ntickets zeroed words
+ * (dk_bn_fold_tickets_needed_count(nrows, channel slices of the producer), left zero), not shared
+ * with concurrent launches; scratch: >= dk_bn_fold_scratch_bytes(nrows, C). */
+int dk_bn_fold_arm_stats(const void* part, int nrows, int C, double count, float eps, float momentum, int first, float* mean, float* std_, float* invstd, float* run_mean, float* run_std, unsigned* tickets, int ntickets, void* scratch, size_t scratch_bytes);
+int dk_bn_fold_arm_bwd(const void* part, int nrows, int C, double count, float* dgamma, float* dbeta, float* k12, unsigned* tickets, int ntickets, void* scratch, size_t scratch_bytes);
+int dk_bn_fold_disarm(void);
+size_t dk_bn_fold_scratch_bytes(int nrows, int C);
+int dk_bn_fold_tickets_needed_count(int nrows, int nslices);
 int dk_relu_bwd_bn_partial_f64(const float* dy, const uint8_t* mask, const float* x, int P, int C, const float* mean, const float* invstd, const float* gamma, const float* beta, int relu, float* dx, void* part, size_t part_bytes, void* stream);
 int dk_bn_infer_params_f32(const float* run_std, int C, float* invstd, void* stream);
 int dk_bn_apply_f32(const float* x, long long numel, int C, const float* mean, const float* invstd, const float* gamma, const float* beta, int relu, float* y, uint8_t* mask, void* stream);

@@ -10,7 +10,7 @@ OUT=$ROOT/gpurun_out
 mkdir -p "$OUT"
 step() { echo "== $1 rc=$2"; if [ "$2" -gt 1 ]; then echo "stopping after rc=$2"; exit "$2"; fi; }
 
-timeout -k 10 900 python -m pytest tests -m gpu -q -p no:cacheprovider > "$OUT/tests_$TAG.log" 2>&1
+timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 150 --timeout-method thread -p no:cacheprovider > "$OUT/tests_$TAG.log" 2>&1
 rc=$?; tail -15 "$OUT/tests_$TAG.log"; step tests $rc
 
 cd /tmp && export TMPDIR=/tmp
@@ -30,3 +30,6 @@ cp "$OUT/${TAG}_pmc.json" "$ROOT/profiles/" 2>/dev/null
 
 timeout -k 10 900 python bench.py --steps 10 --warmup 3 > "$OUT/bench_$TAG.json" 2> "$OUT/bench_$TAG.err"
 rc=$?; cat "$OUT/bench_$TAG.json"; tail -5 "$OUT/bench_$TAG.err"; step bench $rc
+
+timeout -k 10 300 python bench.py --gpus 2 --steps 3 --warmup 1 --no-roofline > "$OUT/bench2_$TAG.json" 2> "$OUT/bench2_$TAG.err"
+rc=$?; cat "$OUT/bench2_$TAG.json"; tail -3 "$OUT/bench2_$TAG.err"; step bench2 $rc

@@ -114,14 +114,18 @@ def _check(got, want, fp32, twin, layers):
 
 FUSED = ["dk_pwconv_fwd_ex_f32", "dk_pwconv_dgrad_bnbwd_f32", "dk_pwconv_wgrad_bnx_f32", "dk_dwconv_bwd_bnbwd_f32",
          "dk_dwconv_fwd_ex_f32", "dk_bn_add_f32", "dk_relu_bwd_bn_partial_f64", "dk_conv2d_wgrad_bnbwd_f32",
-         "dk_conv2d_fwd_ex_f32", "dk_bn_stats_from_partials_f32", "dk_bn_bwd_from_partials_f32"]
+         "dk_conv2d_fwd_ex_f32", "dk_bn_stats_from_partials_f32", "dk_bn_bwd_from_partials_f32",
+         "dk_pwconv_bwd_bnbwd_f32"]
 
 
-def test_res1_full_size(monkeypatch):
+@pytest.mark.parametrize("pw_fused_bwd", ["0", "1"])
+def test_res1_full_size(monkeypatch, pw_fused_bwd):
     """pw0_bn + ReLU (applied on load by res1) and residual block res1 at 256 x 64 x 56 x 56:
     P = 802,816 pixels per pointwise GEMM, the fused stride-1 depthwise backward, BN folds of
-    12,544 partial rows."""
+    12,544 partial rows; the pointwise backward both as separate dgrad / wgrad launches and as
+    the fused single pass."""
     from dorknet_amd._hip import lib
+    monkeypatch.setenv("DORKNET_PW_FUSED_BWD", pw_fused_bwd)
     from examples.resnet18_depsep import ResNet18
     np.random.seed(31)
     layers = ResNet18("r18").layers[4:7]
@@ -132,9 +136,10 @@ def test_res1_full_size(monkeypatch):
     dY = rng.standard_normal((256, 64, 56, 56), dtype=np.float32)
     calls = Calls(monkeypatch, FUSED)
     got, want, f32, twin, _ = _run(layers, X, dY, input_grad=True)
-    assert {"dk_pwconv_fwd_ex_f32", "dk_pwconv_dgrad_bnbwd_f32", "dk_pwconv_wgrad_bnx_f32",
-            "dk_dwconv_bwd_bnbwd_f32", "dk_dwconv_fwd_ex_f32", "dk_bn_add_f32",
-            "dk_relu_bwd_bn_partial_f64"} <= calls.seen, calls.seen
+    pw_bwd = {"dk_pwconv_bwd_bnbwd_f32"} if pw_fused_bwd == "1" else {"dk_pwconv_dgrad_bnbwd_f32",
+                                                                       "dk_pwconv_wgrad_bnx_f32"}
+    assert pw_bwd | {"dk_pwconv_fwd_ex_f32", "dk_dwconv_bwd_bnbwd_f32", "dk_dwconv_fwd_ex_f32", "dk_bn_add_f32",
+                     "dk_relu_bwd_bn_partial_f64"} <= calls.seen, calls.seen
     _check(got, want, f32, twin, layers)
 
 
