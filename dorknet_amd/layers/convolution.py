@@ -5,7 +5,9 @@ materialises a [N*OH*OW, C*R*S] patch matrix (convolution.py:69-74), multiplies 
 the flattened filters (:75), and in backward multiplies again and scatters the result
 back with atomics (:101-111).  Here the same contraction runs as an implicit GEMM on the
 fp32 MFMA units: patches are gathered straight from the NHWC activation into LDS tiles
-and never exist in HBM (dk_conv2d_fwd_f32 / _dgrad_f32 / _wgrad_f32).
+and never exist in HBM (dk_conv2d_fwd_f32 / _dgrad_f32 / _wgrad_f32).  A narrow input (C <= 4:
+the stem on the 3-channel image) takes the narrow-input kernels instead, which read the NCHW
+image as given and reduce over k = (c, r, s) without channel padding (dk_conv2d_*_narrow_f32).
 
 Public surface identical to the reference: constructor signature and defaults
 (:13-14), ``learned_params`` / ``grads`` keys and shapes (weights (K, C, R, S), bias (K,)),
@@ -15,10 +17,12 @@ arithmetic (:67-68, :105-106).
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from .._hip import lib, stream_handle, weight_grad_stream, workspace
-from .._tensor import empty_nhwc, ptr, to_nhwc
+from .._tensor import as_device, empty_nhwc, ptr, to_nhwc
 from ._bn_input import BNGrad, BNOut
 from ._common import add_regulariser_grad, grad_buffer, init_weights, l2_strength
 from .layer import Layer
@@ -71,10 +75,52 @@ class ConvLayer(Layer):
     accepts_bn_input = True   # forward(BNOut): the preceding BatchNorm is applied on load
     produces_bn_stats = True  # forward(..., bn_stats=StatsRequest): emits the next BN's statistics
 
+    def _narrow_ok(self, X):
+        """The narrow-input kernels take this input (raw NCHW, C <= 4: the stem).
+        DORKNET_NARROW=0 keeps every input on the implicit-GEMM path (A/B runs)."""
+        if os.environ.get("DORKNET_NARROW", "1") == "0":
+            return False
+        if isinstance(X, BNOut) or len(getattr(X, "shape", ())) != 4 or X.shape[1] != self.filter_chans:
+            return False
+        if isinstance(X, torch.Tensor) and X.dtype != torch.float32:
+            return False
+        N, C, H, W = (int(v) for v in X.shape)
+        OH, OW = self._out_size(H, W)
+        return bool(lib.dk_conv2d_narrow_preferred(N, C, H, W, self.num_filters, self.f_rows, self.f_cols,
+                                                   self.stride, self.padding, OH, OW))
+
+    def _forward_narrow(self, X, test_mode, bn_stats):
+        st = stream_handle()
+        x = as_device(X, torch.float32).contiguous()  # NCHW, as given
+        N, C, H, W = x.shape
+        K, R, S = self.num_filters, self.f_rows, self.f_cols
+        OH, OW = self._out_size(H, W)
+        y = empty_nhwc(N, K, OH, OW)
+        bias = self.learned_params["bias"] if self.with_bias else None
+        stats = None
+        if bn_stats is not None and not test_mode:
+            rows = lib.dk_conv2d_fwd_narrow_stats_rows(N, C, H, W, K, R, S, self.stride, self.padding, OH, OW)
+            stats = torch.empty((rows, 2, K), dtype=torch.float64, device=x.device)
+            bn_stats.arm(stats, N * OH * OW)
+        r = lib.dk_conv2d_fwd_narrow_f32(x.data_ptr(), N, C, H, W, self.learned_params["weights"].data_ptr(), K, R,
+                                         S, self.stride, self.padding, ptr(bias), y.data_ptr(), OH, OW, ptr(stats),
+                                         st)
+        if stats is not None:
+            bn_stats.launched(stats, r)
+        elif r:
+            raise RuntimeError(f"dk_conv2d_fwd_narrow_f32 failed: {r}")
+        self.X = x
+        self._bn_in = None
+        self._narrow = True
+        return y
+
     def forward(self, X, test_mode=False, bn_stats=None):
         self._require_on_gpu()
         st = stream_handle()
         self.input_shape = tuple(X.shape)
+        if self._narrow_ok(X):
+            return self._forward_narrow(X, test_mode, bn_stats)
+        self._narrow = False
         bn = X if isinstance(X, BNOut) and X.dim() == 4 and X.shape[1] % 4 == 0 else None
         x = bn.x if bn is not None else to_nhwc(X, cpad=4)
         N, Cp, H, W = x.shape
@@ -131,8 +177,19 @@ class ConvLayer(Layer):
         w = self.learned_params["weights"]
         gw = grad_buffer(self, "weights", (K, C, R, S))
         s = l2_strength(self.weight_regulariser)
-        nb = lib.dk_conv2d_wgrad_workspace_bytes(N, OH, OW, K, Cp, R, S)
         g = to_nhwc(G.g)
+        if self._narrow:
+            nb = lib.dk_conv2d_wgrad_narrow_workspace_bytes(N, Cp, H, W, K, R, S, self.stride, self.padding, OH, OW)
+            r = lib.dk_conv2d_wgrad_bnbwd_narrow_f32(g.data_ptr(), G.x.data_ptr(), x.data_ptr(), N, Cp, H, W, K, R, S,
+                                                     self.stride, self.padding, OH, OW, *G.bnbwd_args(),
+                                                     w.data_ptr() if s else 0, s or 0.0, gw.data_ptr(),
+                                                     workspace.get(nb), nb, st)
+            if r:
+                raise RuntimeError(f"dk_conv2d_wgrad_bnbwd_narrow_f32 failed: {r}")
+            if s is None:
+                add_regulariser_grad(gw, w, self.weight_regulariser)
+            return
+        nb = lib.dk_conv2d_wgrad_workspace_bytes(N, OH, OW, K, Cp, R, S)
         lib.dk_conv2d_wgrad_bnbwd_f32(g.data_ptr(), G.x.data_ptr(), x.data_ptr(), N, H, W, Cp, C, K, R, S,
                                       self.stride, self.padding, OH, OW, *G.bnbwd_args(), w.data_ptr() if s else 0,
                                       s or 0.0, gw.data_ptr(), workspace.get(nb), nb,
@@ -165,12 +222,21 @@ class ConvLayer(Layer):
             # weight gradient (+ l2 folded in, convolution.py:93-100)
             gw = grad_buffer(self, "weights", (K, C, R, S))
             s = l2_strength(self.weight_regulariser)
-            nb = lib.dk_conv2d_wgrad_workspace_bytes(N, OH, OW, K, Cp, R, S)
-            if self._bn_in is not None:
+            if self._narrow:
+                nb = lib.dk_conv2d_wgrad_narrow_workspace_bytes(N, Cp, H, W, K, R, S, self.stride, self.padding,
+                                                                OH, OW)
+                r = lib.dk_conv2d_wgrad_narrow_f32(dy.data_ptr(), x.data_ptr(), N, Cp, H, W, K, R, S, self.stride,
+                                                   self.padding, OH, OW, w.data_ptr() if s else 0, s or 0.0,
+                                                   gw.data_ptr(), workspace.get(nb), nb, sst)
+                if r:
+                    raise RuntimeError(f"dk_conv2d_wgrad_narrow_f32 failed: {r}")
+            elif self._bn_in is not None:
+                nb = lib.dk_conv2d_wgrad_workspace_bytes(N, OH, OW, K, Cp, R, S)
                 lib.dk_conv2d_wgrad_bnx_f32(dy.data_ptr(), x.data_ptr(), N, H, W, Cp, C, K, R, S, self.stride,
                                             self.padding, OH, OW, w.data_ptr() if s else 0, s or 0.0, gw.data_ptr(),
                                             workspace.get(nb), nb, *self._bn_in.bn_args(), sst)
             else:
+                nb = lib.dk_conv2d_wgrad_workspace_bytes(N, OH, OW, K, Cp, R, S)
                 lib.dk_conv2d_wgrad_f32(dy.data_ptr(), x.data_ptr(), N, H, W, Cp, C, K, R, S, self.stride,
                                         self.padding, OH, OW, w.data_ptr() if s else 0, s or 0.0, gw.data_ptr(),
                                         workspace.get(nb), nb, sst)

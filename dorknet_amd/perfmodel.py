@@ -171,6 +171,14 @@ MODEL = {
     "dk_conv2d_wgrad_bnbwd_f32": lambda g, ox, x, N, H, W, Cp, C, K, R, S, st_, pad, OH, OW, *rest: (
         2 * N * OH * OW * K * C * R * S + 6 * N * OH * OW * K,
         E * (2 * N * OH * OW * K + N * H * W * Cp + K * R * S * C)),
+    # narrow-input stem kernels (conv_narrow.hip): the NCHW image read as given (C channels)
+    "dk_conv2d_fwd_narrow_f32": lambda x, N, C, H, W, w, K, R, S, st_, pad, b, y, OH, OW, stats, st: (
+        2 * N * OH * OW * K * C * R * S, E * (N * C * H * W + N * OH * OW * K + K * C * R * S)),
+    "dk_conv2d_wgrad_narrow_f32": lambda dy, x, N, C, H, W, K, R, S, st_, pad, OH, OW, *rest: (
+        2 * N * OH * OW * K * C * R * S, E * (N * OH * OW * K + N * C * H * W + K * C * R * S)),
+    "dk_conv2d_wgrad_bnbwd_narrow_f32": lambda g, ox, x, N, C, H, W, K, R, S, st_, pad, OH, OW, *rest: (
+        2 * N * OH * OW * K * C * R * S + 6 * N * OH * OW * K,
+        E * (2 * N * OH * OW * K + N * C * H * W + K * C * R * S)),
     "dk_pwconv_fwd_bnx_f32": _bnx(_pw_fwd),
     "dk_pwconv_wgrad_bnx_f32": _bnx(_pw_wgrad),
     "dk_dwconv_fwd_bnx_f32": _bnx(_dw_fwd),

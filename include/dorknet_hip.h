@@ -128,6 +128,23 @@ int dk_conv2d_wgrad_bnbwd_f32(const float* g, const float* bn_x, const float* x,
 int dk_conv2d_wgrad_bnx_f32(const float* dy, const float* x, int N, int H, int W, int Cp, int C, int K, int R, int S, int stride, int pad, int OH, int OW, const float* w_kcrs, float l2, float* dw_kcrs, void* ws, size_t ws_bytes, const float* bn_mean, const float* bn_invstd, const float* bn_gamma, const float* bn_beta, int bn_relu, void* stream);
 int dk_pwconv_fwd_bnx_f32(const float* x, int N, int H, int W, int C, const float* w_kc, int K, int stride, const float* bias, float* y, int OH, int OW, const float* bn_mean, const float* bn_invstd, const float* bn_gamma, const float* bn_beta, int bn_relu, void* stream);
 int dk_pwconv_wgrad_bnx_f32(const float* dy, const float* x, int N, int H, int W, int C, int K, int stride, int OH, int OW, const float* w_kc, float l2, float* dw_kc, void* ws, size_t ws_bytes, const float* bn_mean, const float* bn_invstd, const float* bn_gamma, const float* bn_beta, int bn_relu, void* stream);
+/* Narrow-input convolution (dorknet_amd/csrc/conv_narrow.hip): the stem -- conv0, 64 x 3 x 5 x 5
+ * stride 2 on the NCHW image (convolution.py:58-100, examples/imagenet_dogs_225_resnet_18_depsep.py
+ * :112-116) -- forward and weight gradient read the NCHW input directly (no NHWC copy, no channel
+ * padding: the reduction is k = (c, r, s), the reference's KCRS order, padded only to 4).
+ * dk_conv2d_narrow_preferred: 1 when these entry points take the shape (C <= 4, K % 4 == 0,
+ * K <= 64, R, S <= 7, C*R*S <= 160, stride <= 2, st*(16*ceil(OW/16) - 1) + S <= 256).
+ * dk_conv2d_fwd_narrow_f32: y NHWC; bias optional; stats (optional) = the output BatchNorm's
+ * partial rows [dk_conv2d_fwd_narrow_stats_rows()][2][K] (in-launch fold: dk_bn_fold_arm_stats).
+ * dk_conv2d_wgrad_narrow_f32 / _bnbwd_narrow_f32: as dk_conv2d_wgrad_f32 /
+ * dk_conv2d_wgrad_bnbwd_f32 (dy given, or formed on load from the following BatchNorm's
+ * deferred gradient), x NCHW; workspace: dk_conv2d_wgrad_narrow_workspace_bytes. */
+int dk_conv2d_narrow_preferred(int N, int C, int H, int W, int K, int R, int S, int stride, int pad, int OH, int OW);
+int dk_conv2d_fwd_narrow_stats_rows(int N, int C, int H, int W, int K, int R, int S, int stride, int pad, int OH, int OW);
+int dk_conv2d_fwd_narrow_f32(const float* x_nchw, int N, int C, int H, int W, const float* w_kcrs, int K, int R, int S, int stride, int pad, const float* bias, float* y, int OH, int OW, double* stats, void* stream);
+size_t dk_conv2d_wgrad_narrow_workspace_bytes(int N, int C, int H, int W, int K, int R, int S, int stride, int pad, int OH, int OW);
+int dk_conv2d_wgrad_narrow_f32(const float* dy, const float* x_nchw, int N, int C, int H, int W, int K, int R, int S, int stride, int pad, int OH, int OW, const float* w_kcrs, float l2, float* dw_kcrs, void* ws, size_t ws_bytes, void* stream);
+int dk_conv2d_wgrad_bnbwd_narrow_f32(const float* g, const float* bn_x, const float* x_nchw, int N, int C, int H, int W, int K, int R, int S, int stride, int pad, int OH, int OW, const float* out_mean, const float* out_invstd, const float* out_gamma, const float* out_beta, int out_relu, const float* k12, const float* w_kcrs, float l2, float* dw_kcrs, void* ws, size_t ws_bytes, void* stream);
 /* Producer side of the same fusion: *_fwd_ex_f32 = forward with an optional input BN
  * (bn_mean == NULL: raw input) and, when stats != NULL, the BatchNorm statistics of the
  * output y (fp64 sum and sum of squares per output channel, per tile: stats[rows][2][K],
@@ -286,7 +303,7 @@ int dk_bn_bwd_from_partials_f32(const void* part, int nblk, int C, double count,
  * exactly what dk_bn_stats_from_partials_f32 (arm_stats) or dk_bn_bwd_from_partials_f32
  * (arm_bwd) would, and the entry point returns DK_FOLDED (10100) instead of 0 -- the caller
  * skips the separate fold launch.  Entry points that take an arming: dk_pwconv_fwd_ex_f32,
- * dk_dwconv_fwd_ex_f32, dk_conv2d_fwd_ex_f32, dk_pwconv_dgrad_bnbwd_f32, dk_pwconv_dgrad_ex_f32,
+ * dk_dwconv_fwd_ex_f32, dk_conv2d_fwd_ex_f32, dk_conv2d_fwd_narrow_f32, dk_pwconv_dgrad_bnbwd_f32, dk_pwconv_dgrad_ex_f32,
  * dk_pwconv_bwd_bnbwd_f32, dk_dwconv_bwd_bnbwd_f32, dk_dwconv_dgrad_ex_f32,
  * dk_relu_bwd_bn_partial_f64 (for the paths that implement it; otherwise they return 0 and
  * the caller folds as before and calls dk_bn_fold_disarm).  One arming per host thread; the

@@ -507,6 +507,39 @@ def test_conv_wgrad_bnbwd_bitwise(relu, bn_in, Cp, K, R, stride):
     same(dw0, dw1)
 
 
+@pytest.mark.parametrize("relu,C,K,R,stride,N,H,W", [(1, 3, 64, 5, 2, 3, 17, 15), (0, 1, 32, 3, 1, 2, 28, 28),
+                                                       (1, 3, 16, 7, 2, 2, 30, 21)])
+def test_conv_wgrad_bnbwd_narrow_bitwise(relu, C, K, R, stride, N, H, W):
+    """dk_conv2d_wgrad_bnbwd_narrow_f32 == dk_bn_bwd_apply_f32 -> dk_conv2d_wgrad_narrow_f32, bitwise
+    (dy is formed as it is staged; the row loop and the reduction are unchanged)."""
+    rng = np.random.RandomState(relu + C + K + R)
+    pad = 1
+    OH, OW = (H + 2 * pad - R) // stride + 1, (W + 2 * pad - R) // stride + 1
+    x = torch.from_numpy(rng.randn(N, C, H, W).astype(np.float32)).cuda()  # NCHW
+    xo = nhwc(rng.randn(N, K, OH, OW))
+    g = nhwc(rng.randn(N, K, OH, OW))
+    po = bn_params(K, rng)
+    k12 = _k12(K, rng)
+    w = torch.as_tensor(rng.randn(K, C, R, R).astype(np.float32), device="cuda")
+    st = stream_handle()
+    assert lib.dk_conv2d_narrow_preferred(N, C, H, W, K, R, R, stride, pad, OH, OW) == 1
+    nb = lib.dk_conv2d_wgrad_narrow_workspace_bytes(N, C, H, W, K, R, R, stride, pad, OH, OW)
+    dy = bwd_apply(xo, g, po, relu, k12)
+    dw0 = torch.empty((K, C, R, R), device="cuda")
+    assert lib.dk_conv2d_wgrad_narrow_f32(dy.data_ptr(), x.data_ptr(), N, C, H, W, K, R, R, stride, pad, OH, OW,
+                                          w.data_ptr(), 1e-3, dw0.data_ptr(), workspace.get(nb), nb, st) == 0
+    dw1 = torch.full_like(dw0, float("nan"))
+    assert lib.dk_conv2d_wgrad_bnbwd_narrow_f32(g.data_ptr(), xo.data_ptr(), x.data_ptr(), N, C, H, W, K, R, R,
+                                                stride, pad, OH, OW, *args(po, relu), k12.data_ptr(), w.data_ptr(),
+                                                1e-3, dw1.data_ptr(), workspace.get(nb), nb, st) == 0
+    same(dw0, dw1)
+    # and the weight gradient itself against a float64 torch reference
+    ref = torch.nn.grad.conv2d_weight(x.double(), (K, C, R, R), dy.double().contiguous(), stride=stride,
+                                      padding=pad) + 1e-3 * w.double()
+    err = float((dw0.double() - ref).norm() / ref.norm())
+    assert err < 1e-5, err
+
+
 def test_network_bn_grad_deferral(monkeypatch):
     """pw -> BN -> ReLU -> dw -> BN -> pw -> BN -> ReLU: the fused backward (the apply of each BN
     that follows a pw layer runs in that layer's dgrad loader, the one after the dw layer in its

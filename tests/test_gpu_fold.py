@@ -129,6 +129,23 @@ def test_stem_fwd_fold():
                 rows, K, N * OH * OH, rng)
 
 
+@pytest.mark.parametrize("N,H", [(8, 65), (64, 225)])
+def test_stem_narrow_fwd_fold(N, H):
+    """The narrow-input stem forward (NCHW image, one partial row per persistent block)."""
+    rng = np.random.RandomState(N + H)
+    C, K, R, s, pad = 3, 64, 5, 2, 1
+    OH = (H + 2 * pad - R) // s + 1
+    x = torch.from_numpy(rng.randn(N, C, H, H).astype(np.float32)).cuda()
+    w = vec(rng.randn(K, C, R, R) * 0.1)
+    y = torch.empty((N, K, OH, OH), device="cuda").contiguous(memory_format=torch.channels_last)
+    rows = lib.dk_conv2d_fwd_narrow_stats_rows(N, C, H, H, K, R, R, s, pad, OH, OH)
+    assert rows > 0
+    st = stream_handle()
+    check_stats(lambda p: lib.dk_conv2d_fwd_narrow_f32(x.data_ptr(), N, C, H, H, w.data_ptr(), K, R, R, s, pad, 0,
+                                                       y.data_ptr(), OH, OH, p, st),
+                rows, K, N * OH * OH, rng)
+
+
 @pytest.mark.parametrize("C,N,H,stride", [(64, 64, 56, 1), (128, 16, 28, 2), (512, 8, 7, 1), (256, 2, 3, 1)])
 def test_dw_fwd_fold(C, N, H, stride):
     rng = np.random.RandomState(C + N + stride)

@@ -115,7 +115,7 @@ def _check(got, want, fp32, twin, layers):
 FUSED = ["dk_pwconv_fwd_ex_f32", "dk_pwconv_dgrad_bnbwd_f32", "dk_pwconv_wgrad_bnx_f32", "dk_dwconv_bwd_bnbwd_f32",
          "dk_dwconv_fwd_ex_f32", "dk_bn_add_f32", "dk_relu_bwd_bn_partial_f64", "dk_conv2d_wgrad_bnbwd_f32",
          "dk_conv2d_fwd_ex_f32", "dk_bn_stats_from_partials_f32", "dk_bn_bwd_from_partials_f32",
-         "dk_pwconv_bwd_bnbwd_f32"]
+         "dk_pwconv_bwd_bnbwd_f32", "dk_conv2d_fwd_narrow_f32", "dk_conv2d_wgrad_bnbwd_narrow_f32"]
 
 
 @pytest.mark.parametrize("pw_fused_bwd", ["0", "1"])
@@ -159,11 +159,15 @@ def test_res7_res8_full_size(monkeypatch):
     _check(got, want, f32, twin, layers)
 
 
-def test_stem_full_size(monkeypatch):
+@pytest.mark.parametrize("narrow", ["1", "0"])
+def test_stem_full_size(monkeypatch, narrow):
     """conv0 (64 x 3 x 5 x 5, stride 2) + conv0_bn + ReLU + pw0 (stride 2) + pw0_bn + ReLU on
     256 x 3 x 225 x 225: the stem weight gradient with conv0_bn's backward applied on load
-    (dk_conv2d_wgrad_bnbwd_f32; the image gradient is not computed, as in the network's
-    backward), conv0_bn folds of 25,088 partial rows."""
+    (the image gradient is not computed, as in the network's backward), conv0_bn's statistics
+    folded in the forward launch -- through the narrow-input kernels on the NCHW image
+    (dk_conv2d_*_narrow_f32, one partial row per block) and through the implicit GEMM on the
+    NHWC4 copy (DORKNET_NARROW=0: dk_conv2d_wgrad_bnbwd_f32, 25,088 partial rows)."""
+    monkeypatch.setenv("DORKNET_NARROW", narrow)
     from examples.resnet18_depsep import ResNet18
     np.random.seed(35)
     layers = ResNet18("r18").layers[0:6]
@@ -173,5 +177,7 @@ def test_stem_full_size(monkeypatch):
     dY = rng.standard_normal((256, 64, 56, 56), dtype=np.float32)
     calls = Calls(monkeypatch, FUSED)
     got, want, f32, twin, _ = _run(layers, X, dY, input_grad=False)
-    assert {"dk_conv2d_wgrad_bnbwd_f32", "dk_conv2d_fwd_ex_f32"} <= calls.seen, calls.seen
+    expect = ({"dk_conv2d_wgrad_bnbwd_narrow_f32", "dk_conv2d_fwd_narrow_f32"} if narrow == "1" else
+              {"dk_conv2d_wgrad_bnbwd_f32", "dk_conv2d_fwd_ex_f32"})
+    assert expect <= calls.seen, calls.seen
     _check(got, want, f32, twin, layers)

@@ -73,7 +73,16 @@ CONV_CASES = [
     (12, 24, 1, 1, 2, 0, 2, 10, 9, True, 0.0),      # 1x1 stride 2: phases without taps write zeros
     (6, 8, 3, 3, 1, 1, 2, 9, 9, False, 0.0),        # stride 1, K % 4 != 0: one phase, dy padded
     (16, 20, 4, 4, 3, 2, 1, 17, 13, False, 0.0),    # stride 3, even filter, ragged phases
+    (64, 3, 5, 5, 2, 1, 2, 45, 61, False, 1e-4),    # the stem's filters, ragged 16-pixel row tiles (narrow path)
+    (48, 1, 3, 3, 1, 2, 2, 9, 40, True, 0.0),       # narrow path: stride 1, pad 2, K not a multiple of 16
 ]
+
+
+@pytest.mark.parametrize("narrow", ["1", "0"])
+def test_conv_stem_paths(narrow, monkeypatch):
+    """The stem shape through the narrow-input kernels and through the implicit GEMM."""
+    monkeypatch.setenv("DORKNET_NARROW", narrow)
+    test_conv_layer((64, 3, 5, 5, 2, 1, 2, 33, 35, False, 1e-4))
 
 
 @pytest.mark.parametrize("case", CONV_CASES)
