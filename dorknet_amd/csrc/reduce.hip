@@ -126,12 +126,24 @@ int splitk_reduce(const float* ws, int splits, int M, int N, float* out, const f
                   int Cp, int R, int S, hipStream_t st) {
   const long long total = (long long)M * N;
   if ((total & 3) == 0 && (reinterpret_cast<uintptr_t>(ws) & 15) == 0) {
+    // Narrow outputs (a 64 x 64 weight gradient is 4096 floats) get 4-column-group blocks, so the
+    // grid still spans the CUs (64 blocks of 16 groups left 3/4 of the chip idle).  Each
+    // column's sum order is the same for every CG.
+    const bool narrow = cdivll(total, 64) < 512;
     if (splits >= 256) {
-      hipLaunchKernelGGL((splitk_reduce4_kernel<16, 64>), dim3((unsigned)cdivll(total, 64)), dim3(1024), 0, st, ws,
-                         splits, M, N, out, w, l2, mode, C, Cp, R, S);
+      if (narrow)
+        hipLaunchKernelGGL((splitk_reduce4_kernel<4, 64>), dim3((unsigned)cdivll(total, 16)), dim3(256), 0, st, ws,
+                           splits, M, N, out, w, l2, mode, C, Cp, R, S);
+      else
+        hipLaunchKernelGGL((splitk_reduce4_kernel<16, 64>), dim3((unsigned)cdivll(total, 64)), dim3(1024), 0, st, ws,
+                           splits, M, N, out, w, l2, mode, C, Cp, R, S);
     } else if (splits >= 32) {
-      hipLaunchKernelGGL((splitk_reduce4_kernel<16, 16>), dim3((unsigned)cdivll(total, 64)), dim3(256), 0, st, ws,
-                         splits, M, N, out, w, l2, mode, C, Cp, R, S);
+      if (narrow)
+        hipLaunchKernelGGL((splitk_reduce4_kernel<4, 16>), dim3((unsigned)cdivll(total, 16)), dim3(64), 0, st, ws,
+                           splits, M, N, out, w, l2, mode, C, Cp, R, S);
+      else
+        hipLaunchKernelGGL((splitk_reduce4_kernel<16, 16>), dim3((unsigned)cdivll(total, 64)), dim3(256), 0, st, ws,
+                           splits, M, N, out, w, l2, mode, C, Cp, R, S);
     } else {
       hipLaunchKernelGGL((splitk_reduce4_kernel<64, 4>), dim3((unsigned)cdivll(total, 256)), dim3(256), 0, st, ws,
                          splits, M, N, out, w, l2, mode, C, Cp, R, S);
