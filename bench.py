@@ -133,6 +133,12 @@ ENTRY_KERNEL = {
     # loader applying a BN backward (dgrad); the stem's weight gradient applies one on its
     # row-contiguous loader (LdMatICT) and is a different entry point
     "dk_pwconv_dgrad_bnbwd_f32": ("dk::igemm_f32", r"dk::LdMatKCT<[^>]*>, dk::MatBwdDesc"),
+    # the pointwise forward with output statistics: the tiled engine's instantiations (1x1 image
+    # view, statistics epilogue) and the streaming K = C = 64 kernel
+    "dk_pwconv_fwd_ex_f32": [("dk::igemm_f32", r"Img(Bn)?DescE<float, true>.*EpStoreStatsT<float>"),
+                             ("dk::pws::fwd_kernel", "")],
+    "dk_conv2d_fwd_narrow_f32": ("dk::nar::fwd_kernel", ""),
+    "dk_conv2d_wgrad_bnbwd_narrow_f32": ("dk::nar::wgrad_kernel", ""),
 }
 
 
@@ -186,9 +192,9 @@ def pmc_traffic(entry, path):
     with open(path) as f:
         d = json.load(f)
     n = t = 0
-    pre, sub = kern if isinstance(kern, tuple) else (kern, "")
+    pats = kern if isinstance(kern, list) else [kern if isinstance(kern, tuple) else (kern, "")]
     for name, v in d.get("kernels", {}).items():
-        if (name.startswith(pre + "<") or name == pre) and re.search(sub, name):
+        if any((name.startswith(pre + "<") or name == pre) and re.search(sub, name) for pre, sub in pats):
             n += v["dispatches"]
             t += v["traffic_bytes"] * v["dispatches"]
     if n == 0:
@@ -312,12 +318,39 @@ def other_config(args):
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
+    breakdown, dominant = None, None
+    if not args.no_roofline:
+        # per-entry attribution on one single-stream step, as for config 3
+        prev = os.environ.get("DORKNET_ASYNC_WGRAD")
+        os.environ["DORKNET_ASYNC_WGRAD"] = "0"
+        try:
+            with Instrument(perfmodel.MODEL.keys()) as ins:
+                step()
+        finally:
+            if prev is None:
+                os.environ.pop("DORKNET_ASYNC_WGRAD")
+            else:
+                os.environ["DORKNET_ASYNC_WGRAD"] = prev
+        summ = ins.summary()
+        dominant = max(summ, key=lambda n: summ[n]["ms"])
+        breakdown = {n: {"ms": round(v["ms"], 3), "calls": v["calls"],
+                         "frac_of_roofline": round(v["bound_ms"] / v["ms"], 3) if v["ms"] else None}
+                     for n, v in sorted(summ.items(), key=lambda kv: -kv[1]["ms"])}
+        torch.cuda.synchronize()
+    ins = Instrument([dominant]) if dominant else None
+    if ins:
+        ins.__enter__()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
+    try:
+        for _ in range(args.steps):
+            step()
+        torch.cuda.synchronize()
+    finally:
+        if ins:
+            ins.__exit__(None, None, None)
     elapsed = time.perf_counter() - t0
     per = elapsed / args.steps
+    roof = roofline_entry(dominant, ins.summary()[dominant], args.steps) if ins else None
     out = {"metric": metric, "value": round((1.0 if args.config == 2 else args.batch) / per, 2), "unit": unit,
            "n_gpus": 1, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * per, 3),
            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": dtype,
@@ -326,6 +359,9 @@ def other_config(args):
     if flops:
         out["achieved_tflops"] = round(flops / per / 1e12, 2)
         out["mfma_frac"] = round(flops / per / 1e12 / perfmodel.PEAK_F32_TFLOPS, 4)
+    if roof:
+        out["roofline"] = roof
+        out["breakdown"] = breakdown
     print(json.dumps(out), flush=True)
 
 

@@ -230,3 +230,20 @@ def work(name: str, args) -> tuple[int, int]:
 def bound_time_s(flops: float, nbytes: float) -> float:
     """Roofline lower bound on time for one call: max(flops / peak, bytes / BW)."""
     return max(flops / (PEAK_F32_TFLOPS * 1e12), nbytes / (PEAK_HBM_GBS * 1e9))
+
+
+def _half(f):
+    """A *_bf16 twin: the fp32 entry's arguments and flops; activations move as 2-byte bf16,
+    so the compulsory bytes halve (weights and BN parameters, < 1 % of the bytes here, are
+    counted at 2 bytes too -- a slight undercount, i.e. a conservative achieved rate)."""
+    def g(*a):
+        fl, by = f(*a)
+        return fl, by // 2
+    return g
+
+
+for _n in ("dk_pwconv_fwd_ex", "dk_pwconv_dgrad_ex", "dk_pwconv_wgrad_bnx", "dk_dwconv_fwd_ex", "dk_dwconv_dgrad_ex",
+           "dk_dwconv_wgrad_bnx", "dk_bn_stats", "dk_bn_apply", "dk_bn_bwd", "dk_bn_bwd_apply", "dk_relu_fwd",
+           "dk_relu_bwd"):
+    if _n + "_f32" in MODEL:
+        MODEL[_n + "_bf16"] = _half(MODEL[_n + "_f32"])
