@@ -162,6 +162,7 @@ struct LdImgKC : KCLayout<ROWS, BK> {
   // input BatchNorm (ImgBnDesc): per-channel {mean, invstd, gamma, beta} table in LDS
   // (filled by the kernel prologue), this k-tile's channel, in-image rows
   const f32x4* tab;
+  int tc;  // table stride (channels)
   int cch;
   uint32_t okm;
   int relu;
@@ -227,9 +228,8 @@ struct LdImgKC : KCLayout<ROWS, BK> {
     for (int j = 0; j < NR; ++j) {
       f32x4 o = v[j];
       if constexpr (D::kBnIn) {
-        const f32x4 p0 = tab[cch], p1 = tab[cch + 1], p2 = tab[cch + 2], p3 = tab[cch + 3];
-        const f32x4 t = bn_in4(o, f32x4{p0[0], p1[0], p2[0], p3[0]}, f32x4{p0[1], p1[1], p2[1], p3[1]},
-                               f32x4{p0[2], p1[2], p2[2], p3[2]}, f32x4{p0[3], p1[3], p2[3], p3[3]}, relu);
+        const float* tb = reinterpret_cast<const float*>(tab) + cch;
+        const f32x4 t = bn_in4(o, ld4(tb), ld4(tb + tc), ld4(tb + 2 * tc), ld4(tb + 3 * tc), relu);
         if ((okm >> j) & 1u) o = t;
       }
       st4(T + (rb + j * RSTEP) * L::SK + 4 * kq, o);
@@ -253,6 +253,7 @@ struct LdMatKCT : KCLayout<ROWS, BK> {
   // ({mean, invstd, gamma, beta}, {k1, k2, gamma*invstd, 0} per channel), dy write-through
   f32x4 xv[NR];
   const f32x4* tab;
+  int tc;  // table stride (channels)
   float* dyo;
   bool writer;
   int kcur;
@@ -304,12 +305,9 @@ struct LdMatKCT : KCLayout<ROWS, BK> {
     if constexpr (D::kBnBwd) {
       if (okm) {
         // dy for channels kcur..kcur+3 (all four < Ktot when any row is valid: Ktot % 4 == 0)
-        f32x4 p[4], q[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          p[e] = tab[2 * (kcur + e)];
-          q[e] = tab[2 * (kcur + e) + 1];
-        }
+        const float* tb = reinterpret_cast<const float*>(tab) + kcur;
+        const f32x4 mu = ld4(tb), is = ld4(tb + tc), ga = ld4(tb + 2 * tc), be = ld4(tb + 3 * tc);
+        const f32x4 k1 = ld4(tb + 4 * tc), k2 = ld4(tb + 5 * tc), ff = ld4(tb + 6 * tc);
 #pragma unroll
         for (int j = 0; j < NR; ++j) {
           if (!((okm >> j) & 1u)) continue;
@@ -318,8 +316,8 @@ struct LdMatKCT : KCLayout<ROWS, BK> {
           for (int e = 0; e < 4; ++e) {
             const float xe = xv[j][e];
             float ge = v[j][e];
-            if (relu_flag && !(bn_out(xe, p[e][0], p[e][1], p[e][2], p[e][3]) > 0.f)) ge = 0.f;
-            o[e] = bn_bwd_elem(xe, ge, p[e][0], p[e][1], q[e][2], q[e][0], q[e][1]);
+            if (relu_flag && !(bn_out(xe, mu[e], is[e], ga[e], be[e]) > 0.f)) ge = 0.f;
+            o[e] = bn_bwd_elem(xe, ge, mu[e], is[e], ff[e], k1[e], k2[e]);
           }
           v[j] = o;
           if (writer) st4(dyo + eoff[j], o);
@@ -352,6 +350,7 @@ struct LdMatICT : ICLayout<ROWS, BK> {
   f32x4 xv[NK];
   uint32_t okm;
   const f32x4* tab;
+  int tc;  // table stride (channels)
   float* dyo;
   bool writer;
   int relu_flag = 0;
@@ -396,12 +395,9 @@ struct LdMatICT : ICLayout<ROWS, BK> {
     if constexpr (D::kBnBwd) {
       if (okm) {
         // dy for channels i0..i0+3 (all < ext when any pixel is valid: ext % 4 == 0)
-        f32x4 p[4], q[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          p[e] = tab[2 * (i0 + e)];
-          q[e] = tab[2 * (i0 + e) + 1];
-        }
+        const float* tb = reinterpret_cast<const float*>(tab) + i0;
+        const f32x4 mu = ld4(tb), is = ld4(tb + tc), ga = ld4(tb + 2 * tc), be = ld4(tb + 3 * tc);
+        const f32x4 k1 = ld4(tb + 4 * tc), k2 = ld4(tb + 5 * tc), ff = ld4(tb + 6 * tc);
 #pragma unroll
         for (int j = 0; j < NK; ++j) {
           f32x4 o = {0.f, 0.f, 0.f, 0.f};
@@ -410,8 +406,8 @@ struct LdMatICT : ICLayout<ROWS, BK> {
             for (int e = 0; e < 4; ++e) {
               const float xe = xv[j][e];
               float ge = v[j][e];
-              if (relu_flag && !(bn_out(xe, p[e][0], p[e][1], p[e][2], p[e][3]) > 0.f)) ge = 0.f;
-              o[e] = bn_bwd_elem(xe, ge, p[e][0], p[e][1], q[e][2], q[e][0], q[e][1]);
+              if (relu_flag && !(bn_out(xe, mu[e], is[e], ga[e], be[e]) > 0.f)) ge = 0.f;
+              o[e] = bn_bwd_elem(xe, ge, mu[e], is[e], ff[e], k1[e], k2[e]);
             }
           }
           v[j] = o;
@@ -777,22 +773,40 @@ __global__ __launch_bounds__(64 * WM * WN) void igemm_f32(DA da, DB db, EP ep, i
     lb.load(db, kt0 * BK, Ktot);
     if constexpr (DA::kBnIn && LA::kTable) {
       // BN-on-load parameter table for the A operand: {mean, invstd, gamma, beta} per channel
+      // ([4][C]: consecutive channel quads of a lane group in consecutive 16-byte slots)
       extern __shared__ f32x4 bn_tab[];
-      for (int c = tid; c < da.C; c += 64 * WM * WN)
-        bn_tab[c] = f32x4{da.bn.mean[c], da.bn.invstd[c], da.bn.gamma[c], da.bn.beta[c]};
+      float* const bt = reinterpret_cast<float*>(bn_tab);
+      for (int c = tid; c < da.C; c += 64 * WM * WN) {
+        bt[c] = da.bn.mean[c];
+        bt[da.C + c] = da.bn.invstd[c];
+        bt[2 * da.C + c] = da.bn.gamma[c];
+        bt[3 * da.C + c] = da.bn.beta[c];
+      }
       la.tab = bn_tab;
+      la.tc = da.C;
       __syncthreads();
     }
     if constexpr (DA::kBnBwd) {
-      // BN-backward-on-load table for the A operand (channel = k)
+      // BN-backward-on-load table for the A operand (channel = k), one array per coefficient
+      // ([7][C]: mean, invstd, gamma, beta, k1, k2, gamma*invstd) so that the lanes of a
+      // 16-lane group, which hold consecutive channel quads, read consecutive 16-byte slots
+      // (the per-channel {.,.,.,.}{.,.,.,.} pairs put those quads 128 bytes apart: 4-way bank
+      // conflicts on every ds_read_b128)
       extern __shared__ f32x4 bwd_tab[];
+      float* const bt = reinterpret_cast<float*>(bwd_tab);
       const BnBwdIn& b = da.bwd;
       for (int c = tid; c < b.C; c += 64 * WM * WN) {
         const float ga = b.gamma[c], is = b.invstd[c];
-        bwd_tab[2 * c] = f32x4{b.mean[c], is, ga, b.beta[c]};
-        bwd_tab[2 * c + 1] = f32x4{b.k12[c], b.k12[b.C + c], ga * is, 0.f};
+        bt[c] = b.mean[c];
+        bt[b.C + c] = is;
+        bt[2 * b.C + c] = ga;
+        bt[3 * b.C + c] = b.beta[c];
+        bt[4 * b.C + c] = b.k12[c];
+        bt[5 * b.C + c] = b.k12[b.C + c];
+        bt[6 * b.C + c] = ga * is;
       }
       la.tab = bwd_tab;
+      la.tc = b.C;
       la.dyo = da.dy_out;
       la.writer = da.dy_out != nullptr && n0 == 0;
       la.relu_flag = b.relu;
