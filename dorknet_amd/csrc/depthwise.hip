@@ -475,14 +475,29 @@ struct BnBwdOut {  // the BatchNorm after this layer: dy = bn_bwd_elem(x1, g)
   int relu;
 };
 
-template <bool BNX, bool STATS, bool RELU1>
+// JOIN: this layer's input is a residual block's output y = ReLU(bn_j(xj) + skip) (the join,
+// residual_block.py:75) and the join's ReLU backward and stage 1 of bn_j's backward ride on the
+// dx store: dx = (dgrad + res) * mask (the join's stored ReLU mask), partials (sum dx,
+// sum dx * xhat_j) -- what dk_relu_bwd_bn_partial_f64 computes from the stored dx, bit for bit
+// for dx (activations.py:44-47, batch_norm.py:125-147).
+struct JoinBwd {
+  const uint8_t* mask;
+  const float* x;  // bn_j's raw input
+  const float* mean;
+  const float* invstd;
+};
+
+template <bool BNX, bool STATS, bool RELU1, bool JOIN = false>
 __global__ __launch_bounds__(256) void dw_bwd_fused_kernel(const float* __restrict__ g, const float* __restrict__ x1,
                                                            uint32_t bytes, BnBwdOut ob, const float* __restrict__ x,
                                                            BnIn bn, const float* __restrict__ w_crs,
                                                            float* __restrict__ dx, const float* __restrict__ res,
                                                            double* __restrict__ spart, float* __restrict__ wpart,
-                                                           int N, int H, int W, int C, int CL, FoldTail ft) {
+                                                           int N, int H, int W, int C, int CL, FoldTail ft,
+                                                           JoinBwd jn = JoinBwd{}) {
   static_assert(!STATS || BNX, "input-BN partials need the input BN");
+  static_assert(!(JOIN && (STATS || BNX)), "the join's partials replace the input BN's");
+  constexpr bool PART = STATS || JOIN;
   const int CG = 256 / CL;              // channel groups per block
   const int NI = (CL + 2) * CG;         // dy float4s per LDS row (with the 1-column halos)
   constexpr int R = 3, S = 3, RS = 9;
@@ -517,6 +532,11 @@ __global__ __launch_bounds__(256) void dw_bwd_fused_kernel(const float* __restri
     bg = ld4(bn.gamma + c);
     bb = ld4(bn.beta + c);
   }
+  f32x4 jm, ji;
+  if constexpr (JOIN) {
+    jm = ld4(jn.mean + c);
+    ji = ld4(jn.invstd + c);
+  }
   f32x4 wv[R][S];
   load_dw_weights<R, S, 2>(wv, w_crs, c, C);  // flipped taps
   auto xform = [&](f32x4 gv, f32x4 xv, bool ok) {
@@ -532,8 +552,10 @@ __global__ __launch_bounds__(256) void dw_bwd_fused_kernel(const float* __restri
     return ok ? o : f32x4{0.f, 0.f, 0.f, 0.f};
   };
   auto pix = [&](int hh, int ww) { return (uint32_t)(((n * H + hh) * W + ww) * C + c); };
-  // raw g / x1 of the next dy row to publish, and this thread's input / residual of the next dx row
-  f32x4 g0, x0, g1, x1v, xr, rv;
+  // raw g / x1 of the next dy row to publish, and this thread's input / residual (/ join mask and
+  // bn_j input) of the next dx row
+  f32x4 g0, x0, g1, x1v, xr, rv, jxv;
+  uint32_t jmv = 0;
   auto load_dy_row = [&](int hh) {
     const bool rok = (unsigned)hh < (unsigned)H;
     g0 = bload4e<float>(rg, rok && cok0, pix(hh, col0));
@@ -545,6 +567,10 @@ __global__ __launch_bounds__(256) void dw_bwd_fused_kernel(const float* __restri
     const bool ok = win_ok && hh < H;
     xr = bload4e<float>(rx, ok, pix(hh, w));
     rv = (res && ok) ? ld4(res + pix(hh, w)) : f32x4{0.f, 0.f, 0.f, 0.f};
+    if constexpr (JOIN) {
+      jmv = ok ? *reinterpret_cast<const uint32_t*>(jn.mask + pix(hh, w)) : 0u;  // the 4 mask bytes
+      jxv = ok ? ld4(jn.x + pix(hh, w)) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
   };
   double s1[4] = {0.0, 0.0, 0.0, 0.0}, s2[4] = {0.0, 0.0, 0.0, 0.0};
   f32x4 wacc[R][S];
@@ -575,7 +601,8 @@ __global__ __launch_bounds__(256) void dw_bwd_fused_kernel(const float* __restri
     }
     if (rr == 0) continue;
     const int h = rr - 1;
-    const f32x4 xh = xr, rh = rv;
+    const f32x4 xh = xr, rh = rv, jh = jxv;
+    const uint32_t jmh = jmv;
     if (h + 1 < H) load_x_row(h + 1);
     f32x4 xb = xh;
     if constexpr (BNX) xb = win_ok ? bn_in4(xh, bm, bi, bg, bb, bn.relu) : f32x4{0.f, 0.f, 0.f, 0.f};
@@ -589,6 +616,15 @@ __global__ __launch_bounds__(256) void dw_bwd_fused_kernel(const float* __restri
       }
     if (win_ok) {
       if (res) acc += rh;
+      if constexpr (JOIN) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          if (!((jmh >> (8 * e)) & 0xffu)) acc[e] = 0.f;  // dy * mask (activations.py:46)
+          const float xn = (jh[e] - jm[e]) * ji[e];
+          s1[e] += (double)acc[e];
+          s2[e] += (double)acc[e] * (double)xn;
+        }
+      }
       if (dxcol) st4(dxcol + (size_t)h * W * C, acc);
       if constexpr (STATS) {
 #pragma unroll
@@ -604,7 +640,7 @@ __global__ __launch_bounds__(256) void dw_bwd_fused_kernel(const float* __restri
   }
   // fixed-order block reductions over the CL column lanes of each channel group
   __syncthreads();
-  if constexpr (STATS) {
+  if constexpr (PART) {
     double(*red)[8] = reinterpret_cast<double(*)[8]>(ring);
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
@@ -636,7 +672,7 @@ __global__ __launch_bounds__(256) void dw_bwd_fused_kernel(const float* __restri
     for (int k = 0; k < CL; ++k) sum += wred[((k * CG + gq) * RS + fl) * 4 + e];
     wpart[((size_t)strip * C + cht * CG * 4) * RS + i] = sum;
   }
-  if constexpr (STATS) {
+  if constexpr (PART) {
     if (ft.part) fold_tail<256>(ft, strip, cht * CG * 4, CG * 4, cht);
   }
 }
@@ -968,7 +1004,7 @@ DK_API int dk_dwconv_bwd_bnbwd_f32(const float* g, const float* bn_x, int N, int
       (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,       \
                                 (int)shm);                                                                           \
     hipLaunchKernelGGL(k, grid, dim3(256), shm, st, g, bn_x, (uint32_t)bytes, ob, x, bn, w_crs, dx, residual, part,  \
-                       wpart, N, H, W, C, cl, ft);                                                                   \
+                       wpart, N, H, W, C, cl, ft, JoinBwd{});                                                        \
   }
   if (out_relu) {
     if (part) DWB_LAUNCH(true, true, true) else if (bn_mean) DWB_LAUNCH(true, false, true)
@@ -978,6 +1014,62 @@ DK_API int dk_dwconv_bwd_bnbwd_f32(const float* g, const float* bn_x, int N, int
     else DWB_LAUNCH(false, false, false)
   }
 #undef DWB_LAUNCH
+  int rc = launch_status();
+  if (rc) return rc;
+  return fold_status(
+      splitk_reduce(wpart, strips, 1, C * R * S, dw_crs, l2 != 0.f ? w_crs : nullptr, l2, 0, C, C, 1, 1, st), ft);
+}
+
+// dk_dwconv_bwd_bnbwd_f32 for a layer whose input is a residual join's output (no input BN): dx
+// is the gradient w.r.t. the join's pre-ReLU sum, dx = (dgrad + residual) * join_mask, and part
+// (stats_rows x 2 x C) gets stage 1 of the backward of the join's BatchNorm (join_x: its raw
+// input; join_mean / join_invstd) -- dk_relu_bwd_bn_partial_f64's work, without re-reading dx.
+DK_API int dk_dwconv_bwd_bnbwd_join_f32(const float* g, const float* bn_x, int N, int H, int W, int C,
+                                        const float* out_mean, const float* out_invstd, const float* out_gamma,
+                                        const float* out_beta, int out_relu, const float* k12, const float* x,
+                                        const float* w_crs, int R, int S, int pad, float l2, float* dw_crs, float* dx,
+                                        const float* residual, const uint8_t* join_mask, const float* join_x,
+                                        const float* join_mean, const float* join_invstd, double* part, void* ws,
+                                        size_t ws_bytes, void* stream) {
+  const hipStream_t st = as_stream(stream);
+  if (R != 3 || S != 3 || pad != 1 || C % 4 || N < 1 || H < 1 || W < 1) return DK_ERR_ARGS;
+  const int cl = dwb_cl(W, C);
+  if (!g || !bn_x || !x || !w_crs || !dw_crs || !dx || !out_mean || !out_invstd || !out_gamma || !out_beta ||
+      !k12 || !join_mask || !join_x || !join_mean || !join_invstd || !part)
+    return DK_ERR_ARGS;
+  if (!aligned16(g) || !aligned16(bn_x) || !aligned16(x) || !aligned16(dx) || (residual && !aligned16(residual)) ||
+      !aligned16(out_mean) || !aligned16(out_invstd) || !aligned16(out_gamma) || !aligned16(out_beta) ||
+      !aligned16(k12) || !aligned16(w_crs) || !aligned16(join_x) || !aligned16(join_mean) ||
+      !aligned16(join_invstd) || (reinterpret_cast<uintptr_t>(join_mask) & 3))
+    return DK_ERR_ARGS;
+  const size_t bytes = (size_t)N * H * W * C * sizeof(float);
+  if (!fits(bytes)) return DK_ERR_ARGS;
+  if (ws_bytes < dk_dwconv_bwd_bnbwd_workspace_bytes(N, H, W, C, R, S)) return DK_ERR_WORKSPACE;
+  const int strips = dwb_strips(N, W, cl);
+  const int ncht = (C / 4) / (256 / cl);
+  float* wpart = static_cast<float*>(ws);
+  const BnBwdOut ob{out_mean, out_invstd, out_gamma, out_beta, k12, out_relu};
+  const JoinBwd jn{join_mask, join_x, join_mean, join_invstd};
+  const dim3 grid((unsigned)(strips * ncht));
+  FoldTail ft;  // an armed in-launch fold of the join BN's partial rows (fold_tail.h)
+  if (!fold_take(part, strips, C, ncht, &ft)) ft.part = nullptr;
+  size_t shm = (size_t)256 * 9 * 4 * sizeof(float);
+  const size_t ring = (size_t)2 * (cl + 2) * (256 / cl) * sizeof(f32x4);
+  if (ring > shm) shm = ring;
+#define DWJ_LAUNCH(RELU1_)                                                                                           \
+  {                                                                                                                  \
+    auto k = dw_bwd_fused_kernel<false, false, RELU1_, true>;                                                        \
+    if (shm > 65536)                                                                                                 \
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,       \
+                                (int)shm);                                                                           \
+    hipLaunchKernelGGL(k, grid, dim3(256), shm, st, g, bn_x, (uint32_t)bytes, ob, x, BnIn{}, w_crs, dx, residual,    \
+                       part, wpart, N, H, W, C, cl, ft, jn);                                                         \
+  }
+  if (out_relu)
+    DWJ_LAUNCH(true)
+  else
+    DWJ_LAUNCH(false)
+#undef DWJ_LAUNCH
   int rc = launch_status();
   if (rc) return rc;
   return fold_status(

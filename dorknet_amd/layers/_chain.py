@@ -135,7 +135,18 @@ def chain_forward(layers, X, test_mode=False, out_accepts=False):
     return X, steps
 
 
-def chain_backward(steps, dy, residual=None, after_step=None, need_input_grad=True):
+def _join_of(step):
+    """The post-skip ReLu of a residual block step whose join can be fused into the next
+    block's first dgrad (its BatchNorm-on-load join: ReLu._join_bn), else None."""
+    if len(step) != 1 or os.environ.get("DORKNET_FUSE_JOIN", "1") == "0":
+        return None
+    act = getattr(step[0], "post_skip_activation", None)
+    if act is None or getattr(act, "_join_bn", None) is None or getattr(act, "_mask", None) is None:
+        return None
+    return act
+
+
+def chain_backward(steps, dy, residual=None, after_step=None, need_input_grad=True, join=None):
     """Backward through `steps` in reverse.  `residual`: a gradient to add to the result (the
     residual join's other branch); the first layer adds it in its dgrad epilogue when it
     can (``accepts_residual``), otherwise it is added separately.  `after_step(i)` runs after
@@ -143,7 +154,9 @@ def chain_backward(steps, dy, residual=None, after_step=None, need_input_grad=Tr
     need_input_grad=False: the caller discards the gradient w.r.t. the chain's input (the
     network's image gradient, which the reference's network.backward computes and drops,
     feed_forward_network.py:64-70), so a first layer with ``skips_input_grad`` computes only
-    its parameter gradients and None is returned."""
+    its parameter gradients and None is returned.  `join`: the residual join whose output is
+    the chain's input (passed to a first layer that ``accepts_join``); a residual-block step
+    likewise receives the previous block's join."""
     from ._bn_input import accepts_bn_grad, add_residual
     from .batch_norm import BatchNormLayer
     last = len(steps) - 1
@@ -161,8 +174,14 @@ def chain_backward(steps, dy, residual=None, after_step=None, need_input_grad=Tr
         elif i == 0 and not need_input_grad and residual is None and getattr(step[0], "skips_input_grad", False):
             dy = step[0].backward(dy, need_dx=False)
         elif i == 0 and residual is not None and getattr(step[0], "accepts_residual", False):
-            dy = step[0].backward(dy, residual=residual)
+            if join is not None and getattr(step[0], "accepts_join", False):
+                dy = step[0].backward(dy, residual=residual, join=join)
+            else:
+                dy = step[0].backward(dy, residual=residual)
             residual = None
+        elif fuse and i > 0 and len(step) == 1 and getattr(step[0], "accepts_join", False) and \
+                _join_of(steps[i - 1]) is not None:
+            dy = step[0].backward(dy, join=_join_of(steps[i - 1]))
         else:
             dy = step[0].backward(dy)
         if after_step is not None:

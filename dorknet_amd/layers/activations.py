@@ -28,6 +28,13 @@ class ReLu(Layer):
         self._mask = None
         self._fused_out = None
         self._join_bn = None
+        self._join_done = False
+
+    def join_backward_done(self):
+        """The consumer of this residual join's output applied this ReLU's backward (and stage 1
+        of the join BatchNorm's) in its own dgrad epilogue (DepthwiseConvLayer, accepts_join):
+        the gradient it returned is already dx, so backward() passes it through."""
+        self._join_done = True
 
     def __repr__(self):
         return "ReLu({})".format(self.layer_name)
@@ -48,6 +55,7 @@ class ReLu(Layer):
         fwd(x.data_ptr(), x.numel(), y.data_ptr(), 0 if mask is None else mask.data_ptr(), st)
         if not test_mode:
             self._mask, self._fused_out, self._join_bn = mask, None, None
+            self._join_done = False
         return y
 
     def forward_add(self, A, B, test_mode=False):
@@ -92,6 +100,7 @@ class ReLu(Layer):
         if not test_mode:
             self._mask, self._fused_out = mask, None
             self._join_bn = A if isinstance(A, BNOut) else None
+            self._join_done = False
         return y
 
     def _attach_fused(self, y, test_mode):
@@ -119,6 +128,9 @@ class ReLu(Layer):
 
     def backward(self, upstream_dx):
         self._require_on_gpu()
+        if self._join_done:
+            self._join_done = False
+            return upstream_dx
         if self._mask is None:
             raise RuntimeError("ReLu {}: backward without a training-mode forward (or the layer ran fused with "
                                "the preceding BatchNormLayer; its backward is BatchNormLayer.backward_bn_relu)"

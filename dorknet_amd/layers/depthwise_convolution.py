@@ -118,10 +118,25 @@ class DepthwiseConvLayer(Layer):
         return (self.stride == 1 and self.f_rows == 3 and self.f_cols == 3 and self.padding == 1
                 and not self.with_bias and C % 4 == 0 and tuple(bx.shape) == tuple(x.shape))
 
-    def _backward_bn_grad(self, G, residual, need_dx):
+    accepts_join = True  # backward(BNGrad, residual=R, join=relu): the input's residual join rides on dx
+
+    def _join_ok(self, join, need_dx):
+        """`join`: the ReLu that closed the residual block whose output is this layer's input
+        (residual_block.py:75).  The fused backward takes over its backward and stage 1 of its
+        BatchNorm's (dk_dwconv_bwd_bnbwd_join_f32) when this layer has no input BatchNorm."""
+        x = self.X
+        jb = getattr(join, "_join_bn", None)
+        mask = getattr(join, "_mask", None)
+        return (need_dx and self._bn_in is None and jb is not None and mask is not None
+                and tuple(mask.shape) == tuple(x.shape) and tuple(jb.x.shape) == tuple(x.shape)
+                and jb.x.dtype == torch.float32 and mask.is_contiguous(memory_format=torch.channels_last)
+                and jb.x.is_contiguous(memory_format=torch.channels_last))
+
+    def _backward_bn_grad(self, G, residual, need_dx, join=None):
         """One-pass backward from the following BatchNorm's deferred gradient (see
         accepts_bn_grad): dx (+ the residual addend, + the input BatchNorm's backward partial
-        sums) and the weight gradient; dy itself is never written."""
+        sums, or the input's residual join: see _join_ok) and the weight gradient; dy itself is
+        never written."""
         st = stream_handle()
         x = self.X
         N, C, H, W = x.shape
@@ -134,6 +149,26 @@ class DepthwiseConvLayer(Layer):
         res = residual_operand(residual, dx) if need_dx else None
         if need_dx and residual is not None and res is None:
             res = residual_operand(to_nhwc(residual), dx)
+        if join is not None and self._join_ok(join, need_dx):
+            jb = join._join_bn
+            rows = lib.dk_dwconv_bwd_bnbwd_stats_rows(N, H, W, C)
+            part = torch.empty((rows, 2, C), dtype=torch.float64, device=x.device)
+            g = to_nhwc(G.g)
+            nb = lib.dk_dwconv_bwd_bnbwd_workspace_bytes(N, H, W, C, R, S)
+            tok = jb.arm_partials(part)
+            r = lib.dk_dwconv_bwd_bnbwd_join_f32(g.data_ptr(), G.x.data_ptr(), N, H, W, C, *G.bnbwd_args(),
+                                                 x.data_ptr(), w.data_ptr(), R, S, self.padding, s or 0.0,
+                                                 gw.data_ptr(), dx.data_ptr(), ptr(res), join._mask.data_ptr(),
+                                                 jb.x.data_ptr(), jb.mean.data_ptr(), jb.invstd.data_ptr(),
+                                                 part.data_ptr(), workspace.get(nb), nb, st)
+            if s is None:
+                add_regulariser_grad(gw, w, self.weight_regulariser)
+            jb.hand_backward_partials(dx, part, r, tok)
+            join.join_backward_done()
+            if residual is not None and res is None:
+                raise RuntimeError("{}: the fused join needs the residual in the dgrad epilogue".format(
+                    self.layer_name))
+            return dx
         part = None
         if need_dx and bn is not None:
             rows = lib.dk_dwconv_bwd_bnbwd_stats_rows(N, H, W, C)
@@ -155,11 +190,11 @@ class DepthwiseConvLayer(Layer):
             dx = add_residual(dx, residual)  # (a new tensor: the BN then recomputes its sums)
         return dx
 
-    def backward(self, upstream_dx, residual=None, need_dx=True):
+    def backward(self, upstream_dx, residual=None, need_dx=True, join=None):
         self._require_on_gpu()
         if isinstance(upstream_dx, BNGrad):
             if self._takes_bn_grad(upstream_dx.x):
-                return self._backward_bn_grad(upstream_dx, residual, need_dx)
+                return self._backward_bn_grad(upstream_dx, residual, need_dx, join)
             upstream_dx = upstream_dx.materialize()
         st = stream_handle()
         dy = to_nhwc(upstream_dx)

@@ -88,13 +88,18 @@ class ResidualBlock(Layer):
                 regularisation += l.regulariser_forward()
         return regularisation
 
-    def backward(self, upstream_dx):
+    accepts_join = True  # backward(dy, join=relu): the previous block's join may ride on the first dgrad
+
+    def backward(self, upstream_dx, join=None):
+        """`join` (optional): the previous block's post-skip ReLu -- this block's input is that
+        join's output, so the chain's first layer may apply its backward in the dgrad epilogue
+        (DepthwiseConvLayer.accepts_join; the ReLu then passes the gradient through)."""
         joined_dx = self.post_skip_activation.backward(upstream_dx)
         # the skip branch's gradient goes in first, so the chain's first layer can add it in
         # its dgrad epilogue instead of a separate join pass (residual_block.py:94-97)
         skip_dx = self.skip_projection.backward(joined_dx) if self.skip_projection is not None else joined_dx
         if fusion_enabled():
-            return chain_backward(self._steps, joined_dx, residual=skip_dx)
+            return chain_backward(self._steps, joined_dx, residual=skip_dx, join=join)
         return _add(chain_backward(self._steps, joined_dx), skip_dx)
 
     def save_to_h5(self, open_f, save_grads=True):

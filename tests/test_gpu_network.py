@@ -250,3 +250,31 @@ def test_input_gradient_on_request():
     odx = onet.backward()
     assert tuple(dx.shape) == X.shape
     assert rel_err(host(dx), odx) <= 1e-4
+
+
+def test_join_fusion_agrees(monkeypatch):
+    """The residual join's ReLU backward and its BatchNorm's backward partials fused into the next
+    block's depthwise backward (dk_dwconv_bwd_bnbwd_join_f32) vs the separate
+    dk_relu_bwd_bn_partial_f64 pass (DORKNET_FUSE_JOIN=0): same dx bits, the fp64 partial sums
+    regrouped, so every gradient agrees to fp32 rounding."""
+    from examples.resnet18_depsep import ResNet18, synthetic_batch
+    from dorknet_amd import _hip
+    X, _, onehot = synthetic_batch(2, seed=2)
+    grads = {}
+    for fuse in ("1", "0"):
+        monkeypatch.setenv("DORKNET_FUSE_JOIN", fuse)
+        seen = set()
+        orig = _hip.lib.dk_dwconv_bwd_bnbwd_join_f32
+        monkeypatch.setattr(_hip.lib, "dk_dwconv_bwd_bnbwd_join_f32", lambda *a: seen.add(1) or orig(*a))
+        np.random.seed(0)
+        net = ResNet18("r18")
+        net.to_gpu()
+        net.forward(dev(X), dev(onehot))
+        net.backward()
+        torch.cuda.synchronize()
+        assert bool(seen) == (fuse == "1")
+        grads[fuse] = {(l.layer_name, k): host(v) for l in all_layers(net.layers) for k, v in (l.grads or {}).items()}
+    for key, a in grads["1"].items():
+        b = grads["0"][key]
+        err = np.linalg.norm((a - b).ravel()) / max(np.linalg.norm(b.ravel()), 1e-30)
+        assert err <= 1e-5 or np.linalg.norm(b.ravel()) < 1e-6, (key, err)
