@@ -235,11 +235,24 @@ __global__ __launch_bounds__(256) void dw_fwd_kernel(const T* __restrict__ x, ui
 
 // Stride > 1 dgrad by sub-pixel decomposition (see SubPix): thread = 4 channels of TWQ
 // consecutive ST x ST quads of dx; the dy neighbourhood columns are shared by adjacent quads.
-template <int R, int S, int ST, int PAD, class T = float>
+// JOIN: this layer's input is a residual block's output y = ReLU(bn_j(xj) + skip) (the join,
+// residual_block.py:75) and the join's ReLU backward and stage 1 of bn_j's backward ride on the
+// dx store: dx = (dgrad + res) * mask (the join's stored ReLU mask), partials (sum dx,
+// sum dx * xhat_j) -- what dk_relu_bwd_bn_partial_f64 computes from the stored dx, bit for bit
+// for dx (activations.py:44-47, batch_norm.py:125-147).
+struct JoinBwd {
+  const uint8_t* mask;
+  const float* x;  // bn_j's raw input
+  const float* mean;
+  const float* invstd;
+};
+
+template <int R, int S, int ST, int PAD, class T = float, bool JOIN = false>
 __global__ __launch_bounds__(256) void dw_dgrad_subpixel_kernel(const T* __restrict__ dy, uint32_t dybytes,
                                                                 const float* __restrict__ wt, T* __restrict__ dx,
                                                                 int N, int H, int W, int C, int OH, int OW,
-                                                                const T* __restrict__ res) {
+                                                                const T* __restrict__ res, JoinBwd jn,
+                                                                double* __restrict__ part, FoldTail ft) {
   using RP = SubPix<R, ST, PAD>;
   using SP = SubPix<S, ST, PAD>;
   constexpr int DR0 = RP::dmin(), NR = RP::dmax() - RP::dmin() + 1;
@@ -249,8 +262,10 @@ __global__ __launch_bounds__(256) void dw_dgrad_subpixel_kernel(const T* __restr
   const int C4 = C >> 2;
   const int QH = (H + ST - 1) / ST, QW = (W + ST - 1) / ST;
   const int nqc = (QW + TWQ - 1) / TWQ;
-  const long long idx = (long long)xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
-  if (idx >= (long long)N * QH * nqc * C4) return;
+  const int blk = xcd_block(blockIdx.x, gridDim.x);
+  const long long idx = (long long)blk * blockDim.x + threadIdx.x;
+  const bool live = idx < (long long)N * QH * nqc * C4;
+  if (!JOIN && !live) return;
   const int cq = (int)(idx % C4);
   long long t = idx / C4;
   const int qc = (int)(t % nqc);
@@ -259,51 +274,97 @@ __global__ __launch_bounds__(256) void dw_dgrad_subpixel_kernel(const T* __restr
   const int n = (int)(t / QH);
   const int c = cq * 4;
   const int j0 = qc * TWQ;
-  const __amdgpu_buffer_rsrc_t rs = make_rsrc_v(dy, dybytes);
-  f32x4 d[NR][NCOL];
-#pragma unroll
-  for (int a = 0; a < NR; ++a) {
-    const int oh = qi + DR0 + a;
-#pragma unroll
-    for (int b = 0; b < NCOL; ++b) {
-      const int ow = j0 + DS0 + b;
-      const bool ok = (unsigned)oh < (unsigned)OH && (unsigned)ow < (unsigned)OW;
-      d[a][b] = bload4e<T>(rs, ok, (uint32_t)(((n * OH + oh) * OW + ow) * C + c));
+  // JOIN (see JoinBwd): the join's mask and bn_j statistics ride on the store; per-thread fp64
+  // sums, then a fixed-order block reduction into part[blk][2][C] (a block spans whole pixels:
+  // C/4 divides 256)
+  double s1[4] = {0.0, 0.0, 0.0, 0.0}, s2[4] = {0.0, 0.0, 0.0, 0.0};
+  f32x4 jm{}, ji{};
+  if constexpr (JOIN) {
+    if (live) {
+      jm = ld4(jn.mean + c);
+      ji = ld4(jn.invstd + c);
     }
   }
-  f32x4 wv[R][S];
-  load_dw_weights<R, S, 1>(wv, wt, c, C);  // wt = W[C][R][S]
+  if (live) {
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc_v(dy, dybytes);
+    f32x4 d[NR][NCOL];
 #pragma unroll
-  for (int q = 0; q < TWQ; ++q) {
-    const int j = j0 + q;
-    f32x4 acc[ST][ST], rv[ST][ST];
+    for (int a = 0; a < NR; ++a) {
+      const int oh = qi + DR0 + a;
 #pragma unroll
-    for (int a = 0; a < ST; ++a)
-#pragma unroll
-      for (int b = 0; b < ST; ++b) {
-        // residual addend loads issued ahead of the FMAs (added last: same rounding as dgrad + add)
-        const int h = qi * ST + a, w = j * ST + b;
-        rv[a][b] = (res && j < QW && h < H && w < W) ? ld4(res + (((size_t)n * H + h) * W + w) * C + c)
-                                                     : f32x4{0.f, 0.f, 0.f, 0.f};
-        acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int b = 0; b < NCOL; ++b) {
+        const int ow = j0 + DS0 + b;
+        const bool ok = (unsigned)oh < (unsigned)OH && (unsigned)ow < (unsigned)OW;
+        d[a][b] = bload4e<T>(rs, ok, (uint32_t)(((n * OH + oh) * OW + ow) * C + c));
       }
+    }
+    f32x4 wv[R][S];
+    load_dw_weights<R, S, 1>(wv, wt, c, C);  // wt = W[C][R][S]
 #pragma unroll
-    for (int r = 0; r < R; ++r)
+    for (int q = 0; q < TWQ; ++q) {
+      const int j = j0 + q;
+      f32x4 acc[ST][ST], rv[ST][ST], jx[ST][ST];
+      uint32_t jmk[ST][ST];
 #pragma unroll
-      for (int s = 0; s < S; ++s)
-        acc[RP::phase(r)][SP::phase(s)] += d[RP::nb(r) - DR0][q + SP::nb(s) - DS0] * wv[r][s];
+      for (int a = 0; a < ST; ++a)
 #pragma unroll
-    for (int a = 0; a < ST; ++a) {
-      const int h = qi * ST + a;
-#pragma unroll
-      for (int b = 0; b < ST; ++b) {
-        const int w = j * ST + b;
-        if (j < QW && h < H && w < W) {
+        for (int b = 0; b < ST; ++b) {
+          // residual addend loads issued ahead of the FMAs (added last: same rounding as dgrad + add)
+          const int h = qi * ST + a, w = j * ST + b;
+          const bool ok = j < QW && h < H && w < W;
           const size_t off = (((size_t)n * H + h) * W + w) * C + c;
-          st4(dx + off, res ? acc[a][b] + rv[a][b] : acc[a][b]);
+          rv[a][b] = (res && ok) ? ld4(res + off) : f32x4{0.f, 0.f, 0.f, 0.f};
+          if constexpr (JOIN) {
+            jmk[a][b] = ok ? *reinterpret_cast<const uint32_t*>(jn.mask + off) : 0u;
+            jx[a][b] = ok ? ld4(jn.x + off) : f32x4{0.f, 0.f, 0.f, 0.f};
+          }
+          acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+#pragma unroll
+      for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int s = 0; s < S; ++s)
+          acc[RP::phase(r)][SP::phase(s)] += d[RP::nb(r) - DR0][q + SP::nb(s) - DS0] * wv[r][s];
+#pragma unroll
+      for (int a = 0; a < ST; ++a) {
+        const int h = qi * ST + a;
+#pragma unroll
+        for (int b = 0; b < ST; ++b) {
+          const int w = j * ST + b;
+          if (j < QW && h < H && w < W) {
+            const size_t off = (((size_t)n * H + h) * W + w) * C + c;
+            f32x4 o = res ? acc[a][b] + rv[a][b] : acc[a][b];
+            if constexpr (JOIN) {
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                if (!((jmk[a][b] >> (8 * e)) & 0xffu)) o[e] = 0.f;  // dy * mask (activations.py:46)
+                const float xn = (jx[a][b][e] - jm[e]) * ji[e];
+                s1[e] += (double)o[e];
+                s2[e] += (double)o[e] * (double)xn;
+              }
+            }
+            st4(dx + off, o);
+          }
         }
       }
     }
+  }
+  if constexpr (JOIN) {
+    __shared__ double red[256][8];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      red[threadIdx.x][e] = s1[e];
+      red[threadIdx.x][4 + e] = s2[e];
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < C * 2; i += 256) {  // i = (which, channel)
+      const int which = i / C, ch = i - which * C;
+      const int q4 = ch >> 2, e = ch & 3;
+      double a = 0.0;
+      for (int k = q4; k < 256; k += C4) a += red[k][4 * which + e];
+      pub_store(part + ((size_t)blk * 2 + which) * C + ch, a);
+    }
+    if (ft.part) fold_tail<256>(ft, blk, 0, C, 0);
   }
 }
 
@@ -473,18 +534,6 @@ struct BnBwdOut {  // the BatchNorm after this layer: dy = bn_bwd_elem(x1, g)
   const float* beta;
   const float* k12;
   int relu;
-};
-
-// JOIN: this layer's input is a residual block's output y = ReLU(bn_j(xj) + skip) (the join,
-// residual_block.py:75) and the join's ReLU backward and stage 1 of bn_j's backward ride on the
-// dx store: dx = (dgrad + res) * mask (the join's stored ReLU mask), partials (sum dx,
-// sum dx * xhat_j) -- what dk_relu_bwd_bn_partial_f64 computes from the stored dx, bit for bit
-// for dx (activations.py:44-47, batch_norm.py:125-147).
-struct JoinBwd {
-  const uint8_t* mask;
-  const float* x;  // bn_j's raw input
-  const float* mean;
-  const float* invstd;
 };
 
 template <bool BNX, bool STATS, bool RELU1, bool JOIN = false>
@@ -826,7 +875,7 @@ DK_API size_t dk_dwconv_dgrad_workspace_bytes(int C, int R, int S) { return (siz
 template <class T>
 static int dw_dgrad(const T* dy, int N, int OH, int OW, int C, const float* w_crs, int R, int S, int stride, int pad,
                     T* dx, int H, int W, void* ws, size_t ws_bytes, const T* res, const T* bn_x, const BnIn& obn,
-                    double* part, hipStream_t st) {
+                    double* part, hipStream_t st, const JoinBwd* jn = nullptr) {
   if (C % 4) return DK_ERR_ARGS;
   if (ws_bytes < dk_dwconv_dgrad_workspace_bytes(C, R, S)) return DK_ERR_WORKSPACE;
   float* wt = static_cast<float*>(ws);
@@ -836,7 +885,7 @@ static int dw_dgrad(const T* dy, int N, int OH, int OW, int C, const float* w_cr
     return dw_fwd_dispatch(dy, w_crs, nullptr, dx, N, OH, OW, C, R, S, 1, H, W, R - 1 - pad, BnIn{}, st,
                            part ? part : nullptr, part ? bn_x : nullptr, part ? obn : BnIn{}, 2, res);
   }
-  if (part) return DK_ERR_ARGS;  // the BN-backward fusion covers stride-1 geometries only
+  if (part && !jn) return DK_ERR_ARGS;  // the BN-backward fusion covers stride-1 geometries only
   if (!fits((size_t)N * OH * OW * C * 4) || !aligned16(dy) || !aligned16(dx) || !aligned16(w_crs) ||
       (res && !aligned16(res)))
     return DK_ERR_ARGS;
@@ -844,15 +893,27 @@ static int dw_dgrad(const T* dy, int N, int OH, int OW, int C, const float* w_cr
 #define DW_SUBPIX(RR, SS, STR, PD)                                                                                   \
   if (R == RR && S == SS && stride == STR && pad == PD) {                                                            \
     const long long items = (long long)N * cdiv(H, STR) * cdiv(cdiv(W, STR), 4) * (C / 4);                         \
-    hipLaunchKernelGGL((dw_dgrad_subpixel_kernel<RR, SS, STR, PD, T>), dim3((unsigned)cdivll(items, 256)), dim3(256), \
-                       0, st, dy, gb, w_crs, dx, N, H, W, C, OH, OW, res);                                           \
+    const dim3 grid((unsigned)cdivll(items, 256));                                                                   \
+    if (jn) {                                                                                                        \
+      if constexpr (sizeof(T) == sizeof(float)) {                                                                    \
+        FoldTail ft;                                                                                                 \
+        if (!fold_take(part, (int)grid.x, C, 1, &ft)) ft.part = nullptr;                                            \
+        hipLaunchKernelGGL((dw_dgrad_subpixel_kernel<RR, SS, STR, PD, T, true>), grid, dim3(256), 0, st, dy, gb,    \
+                           w_crs, dx, N, H, W, C, OH, OW, res, *jn, part, ft);                                       \
+        return fold_status(launch_status(), ft);                                                                     \
+      } else {                                                                                                       \
+        return DK_ERR_ARGS;                                                                                          \
+      }                                                                                                              \
+    }                                                                                                                \
+    hipLaunchKernelGGL((dw_dgrad_subpixel_kernel<RR, SS, STR, PD, T>), grid, dim3(256), 0, st, dy, gb, w_crs, dx, N, \
+                       H, W, C, OH, OW, res, JoinBwd{}, nullptr, FoldTail{});                                        \
     return launch_status();                                                                                          \
   }
   DW_SUBPIX(3, 3, 2, 1)
   DW_SUBPIX(5, 5, 2, 2)
   DW_SUBPIX(1, 1, 2, 0)
 #undef DW_SUBPIX
-  if (res) return DK_ERR_ARGS;  // generic gather path: no residual fusion
+  if (res || jn) return DK_ERR_ARGS;  // generic gather path: no residual / join fusion
   if constexpr (sizeof(T) != sizeof(float)) {
     return DK_ERR_ARGS;  // generic gather path: fp32 storage only
   } else {
@@ -1018,6 +1079,35 @@ DK_API int dk_dwconv_bwd_bnbwd_f32(const float* g, const float* bn_x, int N, int
   if (rc) return rc;
   return fold_status(
       splitk_reduce(wpart, strips, 1, C * R * S, dw_crs, l2 != 0.f ? w_crs : nullptr, l2, 0, C, C, 1, 1, st), ft);
+}
+
+// Rows of join partials dk_dwconv_dgrad_join_f32 writes (0: the geometry has no join variant).
+DK_API int dk_dwconv_dgrad_join_rows(int N, int H, int W, int C, int R, int S, int stride, int pad) {
+  if (C % 4 || C / 4 > 256 || 256 % (C / 4)) return 0;
+  const bool ok = (R == 3 && S == 3 && stride == 2 && pad == 1) || (R == 5 && S == 5 && stride == 2 && pad == 2) ||
+                  (R == 1 && S == 1 && stride == 2 && pad == 0);
+  if (!ok) return 0;
+  const long long items = (long long)N * cdiv(H, stride) * cdiv(cdiv(W, stride), 4) * (C / 4);
+  return (int)cdivll(items, 256);
+}
+
+// Strided (sub-pixel) input gradient whose input is a residual join's output: dx = (dgrad +
+// residual) * join_mask and part (dk_dwconv_dgrad_join_rows x 2 x C) = stage 1 of the join
+// BatchNorm's backward over that dx (see dk_dwconv_bwd_bnbwd_join_f32).  Takes an in-launch fold
+// arming (dk_bn_fold_arm_bwd).
+DK_API int dk_dwconv_dgrad_join_f32(const float* dy, int N, int OH, int OW, int C, const float* w_crs, int R, int S,
+                                    int stride, int pad, float* dx, int H, int W, void* ws, size_t ws_bytes,
+                                    const float* residual, const uint8_t* join_mask, const float* join_x,
+                                    const float* join_mean, const float* join_invstd, double* part, void* stream) {
+  if (!join_mask || !join_x || !join_mean || !join_invstd || !part ||
+      dk_dwconv_dgrad_join_rows(N, H, W, C, R, S, stride, pad) == 0)
+    return DK_ERR_ARGS;
+  if (!aligned16(join_x) || !aligned16(join_mean) || !aligned16(join_invstd) ||
+      (reinterpret_cast<uintptr_t>(join_mask) & 3))
+    return DK_ERR_ARGS;
+  const JoinBwd jn{join_mask, join_x, join_mean, join_invstd};
+  return dw_dgrad<float>(dy, N, OH, OW, C, w_crs, R, S, stride, pad, dx, H, W, ws, ws_bytes, residual, nullptr,
+                         BnIn{}, part, as_stream(stream), &jn);
 }
 
 // dk_dwconv_bwd_bnbwd_f32 for a layer whose input is a residual join's output (no input BN): dx

@@ -248,6 +248,21 @@ class DepthwiseConvLayer(Layer):
                          W, workspace.get(nb), nb, ptr(res), bn.x.data_ptr(), *bn.bn_args(), part.data_ptr(), st)
             bn.hand_backward_partials(dx, part, r, tok)
             return dx
+        jrows = (lib.dk_dwconv_dgrad_join_rows(N, H, W, C, R, S, self.stride, self.padding)
+                 if join is not None and not bf and self._join_ok(join, True) and (residual is None or res is not None)
+                 else 0)
+        if jrows:
+            # the input's residual join: its ReLU backward and its BatchNorm's stage 1 on the store
+            jb = join._join_bn
+            part = torch.empty((jrows, 2, C), dtype=torch.float64, device=dx.device)
+            tok = jb.arm_partials(part)
+            r = lib.dk_dwconv_dgrad_join_f32(dy.data_ptr(), N, OH, OW, C, w.data_ptr(), R, S, self.stride,
+                                             self.padding, dx.data_ptr(), H, W, workspace.get(nb), nb, ptr(res),
+                                             join._mask.data_ptr(), jb.x.data_ptr(), jb.mean.data_ptr(),
+                                             jb.invstd.data_ptr(), part.data_ptr(), st)
+            jb.hand_backward_partials(dx, part, r, tok)
+            join.join_backward_done()
+            return dx
         if bf:
             if residual is not None and res is None:
                 raise NotImplementedError("{}: bf16 residual must be a bf16 NHWC tensor".format(self.layer_name))
