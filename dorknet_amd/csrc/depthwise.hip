@@ -567,27 +567,53 @@ __global__ __launch_bounds__(256) void dw_bwd_fused_kernel(const float* __restri
   const int col0 = wl + cl, col1 = wl + CL + cl;
   const bool cok0 = (unsigned)col0 < (unsigned)W, cok1 = two && (unsigned)col1 < (unsigned)W;
   const __amdgpu_buffer_rsrc_t rg = make_rsrc_v(g, bytes), r1 = make_rsrc_v(x1, bytes), rx = make_rsrc_v(x, bytes);
-  const f32x4 om = ld4(ob.mean + c), oi = ld4(ob.invstd + c), ok1 = ld4(ob.k12 + c), ok2 = ld4(ob.k12 + C + c);
-  const f32x4 of = ld4(ob.gamma + c) * oi;
-  f32x4 og, obt;
-  if constexpr (RELU1) {
-    og = ld4(ob.gamma + c);
-    obt = ld4(ob.beta + c);
+  // the per-channel BatchNorm terms and the (flipped) filters live in LDS, read where used:
+  // held in registers they kept the kernel at 2 waves per SIMD, too few to hide a row's loads
+  __shared__ f32x4 ptab[13 + RS][32];  // [term][channel group]; CG <= 32 (dwb_cl)
+  for (int i = tid; i < 13 * CG; i += 256) {
+    const int t = i / CG, q = i - t * CG;
+    const int cc = (cht * CG + q) * 4;
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+    switch (t) {
+      case 0: v = ld4(ob.mean + cc); break;
+      case 1: v = ld4(ob.invstd + cc); break;
+      case 2: v = ld4(ob.k12 + cc); break;
+      case 3: v = ld4(ob.k12 + C + cc); break;
+      case 4: v = ld4(ob.gamma + cc) * ld4(ob.invstd + cc); break;
+      case 5: if (RELU1) v = ld4(ob.gamma + cc); break;
+      case 6: if (RELU1) v = ld4(ob.beta + cc); break;
+      case 7: if (BNX) v = ld4(bn.mean + cc); break;
+      case 8: if (BNX) v = ld4(bn.invstd + cc); break;
+      case 9: if (BNX) v = ld4(bn.gamma + cc); break;
+      case 10: if (BNX) v = ld4(bn.beta + cc); break;
+      case 11: if (JOIN) v = ld4(jn.mean + cc); break;
+      default: if (JOIN) v = ld4(jn.invstd + cc); break;
+    }
+    ptab[t][q] = v;
   }
-  f32x4 bm, bi, bg, bb;
-  if constexpr (BNX) {
-    bm = ld4(bn.mean + c);
-    bi = ld4(bn.invstd + c);
-    bg = ld4(bn.gamma + c);
-    bb = ld4(bn.beta + c);
+  if (tid < CG) {
+    f32x4 wv0[R][S];
+    load_dw_weights<R, S, 2>(wv0, w_crs, c, C);  // flipped taps
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+      for (int s = 0; s < S; ++s) ptab[13 + r * S + s][cg] = wv0[r][s];
   }
-  f32x4 jm, ji;
-  if constexpr (JOIN) {
-    jm = ld4(jn.mean + c);
-    ji = ld4(jn.invstd + c);
-  }
-  f32x4 wv[R][S];
-  load_dw_weights<R, S, 2>(wv, w_crs, c, C);  // flipped taps
+  __syncthreads();
+#define om ptab[0][cg]
+#define oi ptab[1][cg]
+#define ok1 ptab[2][cg]
+#define ok2 ptab[3][cg]
+#define of ptab[4][cg]
+#define og ptab[5][cg]
+#define obt ptab[6][cg]
+#define bm ptab[7][cg]
+#define bi ptab[8][cg]
+#define bg ptab[9][cg]
+#define bb ptab[10][cg]
+#define jm ptab[11][cg]
+#define ji ptab[12][cg]
+#define WV(r, s) ptab[13 + (r) * S + (s)][cg]
   auto xform = [&](f32x4 gv, f32x4 xv, bool ok) {
     f32x4 o;
 #pragma unroll
@@ -660,7 +686,7 @@ __global__ __launch_bounds__(256) void dw_bwd_fused_kernel(const float* __restri
     for (int r = 0; r < R; ++r)
 #pragma unroll
       for (int s = 0; s < S; ++s) {
-        acc += d[r][s] * wv[r][s];
+        acc += d[r][s] * WV(r, s);
         wacc[r][s] += d[r][s] * xb;
       }
     if (win_ok) {
@@ -724,6 +750,20 @@ __global__ __launch_bounds__(256) void dw_bwd_fused_kernel(const float* __restri
   if constexpr (PART) {
     if (ft.part) fold_tail<256>(ft, strip, cht * CG * 4, CG * 4, cht);
   }
+#undef om
+#undef oi
+#undef ok1
+#undef ok2
+#undef of
+#undef og
+#undef obt
+#undef bm
+#undef bi
+#undef bg
+#undef bb
+#undef jm
+#undef ji
+#undef WV
 }
 
 // Column-strip width CL (CG = 256 / CL channel groups per block): 16 columns x 64 channels, or
