@@ -155,6 +155,7 @@ struct DyIn {
   const float* bnx;  // BNDEF: the BN's raw input (= this layer's output)
   const float *mean, *invstd, *gamma, *beta, *k12;
   int relu;
+  int lat;  // BNDEF: g given on the stride-lat lattice only (1 or 2; compact, zero elsewhere)
 };
 
 // Weight gradient.  MFMA C[filter][n] += A[filter][pixel] * B[pixel][n] over the pixels of the
@@ -174,16 +175,37 @@ struct DyRow {
   // voff: the lane's byte offset (lg * K + filt) * 4 within a pixel quad, kOOBBytes for a filter
   // past K.  Pixels past OW (a ragged or padded quad) read the next row (or 0 past the tensor)
   // and are zeroed by the caller.
-  __device__ __forceinline__ void load(const DyIn& d, const Geo& g, int row, int voff) {
+  // voffg: the lane's offset in a lattice g (d.lat == 2: even pixels only, compact -- the
+  // pointwise stride-2 layer after the stem hands over its gradient without the zeros of the
+  // widen, pointwise_convolution.py:68-72).
+  __device__ __forceinline__ void load(const DyIn& d, const Geo& g, int row, int voff, int voffg) {
     const uint32_t bytes = (uint32_t)((size_t)g.rows * g.OW * g.K * 4);
-    const __amdgpu_buffer_rsrc_t rg = make_rsrc_v(d.g, bytes), rx = make_rsrc_v(d.bnx, bytes);
+    const __amdgpu_buffer_rsrc_t rx = make_rsrc_v(d.bnx, bytes);
     const int rbase = row * g.OW * g.K * 4;
     const int qstep = 16 * g.K;  // bytes per pixel quad
+    if (d.lat == 1) {
+      const __amdgpu_buffer_rsrc_t rg = make_rsrc_v(d.g, bytes);
 #pragma unroll
-    for (int q = 0; q < QC; ++q) {
-      const int vo = voff + q * qstep;
-      gq[q] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rg, vo, rbase, 0));
-      if constexpr (BNDEF) xq[q] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rx, vo, rbase, 0));
+      for (int q = 0; q < QC; ++q)
+        gq[q] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rg, voff + q * qstep, rbase, 0));
+    } else {
+      const int n = row / g.OH, oh = row - n * g.OH;
+      const int OHc = (g.OH + 1) / 2, OWc = (g.OW + 1) / 2;
+      if (oh & 1) {  // an off-lattice row: g is zero
+#pragma unroll
+        for (int q = 0; q < QC; ++q) gq[q] = 0.f;
+      } else {
+        const __amdgpu_buffer_rsrc_t rg = make_rsrc_v(d.g, (uint32_t)((size_t)g.N * OHc * OWc * g.K * 4));
+        const int rb = ((n * OHc + (oh >> 1)) * OWc) * g.K * 4;
+#pragma unroll
+        for (int q = 0; q < QC; ++q)
+          gq[q] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rg, voffg + q * (qstep >> 1), rb, 0));
+      }
+    }
+    if constexpr (BNDEF) {
+#pragma unroll
+      for (int q = 0; q < QC; ++q)
+        xq[q] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rx, voff + q * qstep, rbase, 0));
     }
   }
 };
@@ -200,6 +222,8 @@ __global__ __launch_bounds__(NT, 3) void wgrad_kernel(DyIn d, const float* __res
   const int li = lane & 15, lg = lane >> 4;
   const int filt = 16 * wave + li;  // this lane's filter (A row)
   const int voff = filt < g.K ? (lg * g.K + filt) * 4 : (int)kOOBBytes;
+  // lattice g: lanes of odd pixels (lg odd) read nothing; even ones the compact pixel lg / 2
+  const int voffg = d.lat == 1 ? voff : ((filt < g.K && !(lg & 1)) ? ((lg >> 1) * g.K + filt) * 4 : (int)kOOBBytes);
   int offn[NTN];
 #pragma unroll
   for (int nt = 0; nt < NTN; ++nt) offn[nt] = koff<C, R, S>(16 * nt + li, g.CS) + ST * lg;
@@ -223,7 +247,7 @@ __global__ __launch_bounds__(NT, 3) void wgrad_kernel(DyIn d, const float* __res
   DyRow<BNDEF, QC> dr;
   if (r0 < r1) {
     rs.load(x, g, r0 / g.OH, r0 % g.OH);
-    dr.load(d, g, r0, voff);
+    dr.load(d, g, r0, voff, voffg);
   }
   for (int row = r0; row < r1; ++row) {
     __syncthreads();  // the previous row's LDS reads are done
@@ -242,7 +266,7 @@ __global__ __launch_bounds__(NT, 3) void wgrad_kernel(DyIn d, const float* __res
     __syncthreads();
     if (row + 1 < r1) {  // in flight under this row's MFMAs
       rs.load(x, g, (row + 1) / g.OH, (row + 1) % g.OH);
-      dr.load(d, g, row + 1, voff);
+      dr.load(d, g, row + 1, voff, voffg);
     }
 #pragma unroll
     for (int q = 0; q < QC; ++q) {
@@ -428,6 +452,7 @@ DK_API int dk_conv2d_wgrad_narrow_f32(const float* dy, const float* x_nchw, int 
                                       float* dw_kcrs, void* ws, size_t ws_bytes, void* stream) {
   DyIn d{};
   d.g = dy;
+  d.lat = 1;
   return wgrad_narrow(d, false, x_nchw, N, C, H, W, K, R, S, stride, pad, OH, OW, w_kcrs, l2, dw_kcrs, ws, ws_bytes,
                       stream);
 }
@@ -435,15 +460,16 @@ DK_API int dk_conv2d_wgrad_narrow_f32(const float* dy, const float* x_nchw, int 
 DK_API int dk_conv2d_wgrad_bnbwd_narrow_f32(const float* g, const float* bn_x, const float* x_nchw, int N, int C,
                                             int H, int W, int K, int R, int S, int stride, int pad, int OH, int OW,
                                             const float* out_mean, const float* out_invstd, const float* out_gamma,
-                                            const float* out_beta, int out_relu, const float* k12,
+                                            const float* out_beta, int out_relu, const float* k12, int g_lattice,
                                             const float* w_kcrs, float l2, float* dw_kcrs, void* ws,
                                             size_t ws_bytes, void* stream) {
   if (!bn_x || !out_mean || !out_invstd || !out_gamma || !out_beta || !k12) return DK_ERR_ARGS;
+  if (g_lattice != 1 && g_lattice != 2) return DK_ERR_ARGS;
   if ((reinterpret_cast<uintptr_t>(out_mean) | reinterpret_cast<uintptr_t>(out_invstd) |
        reinterpret_cast<uintptr_t>(out_gamma) | reinterpret_cast<uintptr_t>(out_beta) |
        reinterpret_cast<uintptr_t>(k12)) & 15)
     return DK_ERR_ARGS;
-  DyIn d{g, bn_x, out_mean, out_invstd, out_gamma, out_beta, k12, out_relu};
+  DyIn d{g, bn_x, out_mean, out_invstd, out_gamma, out_beta, k12, out_relu, g_lattice};
   return wgrad_narrow(d, true, x_nchw, N, C, H, W, K, R, S, stride, pad, OH, OW, w_kcrs, l2, dw_kcrs, ws, ws_bytes,
                       stream);
 }

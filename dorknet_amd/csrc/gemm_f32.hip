@@ -678,6 +678,27 @@ struct EpWidenBnBwd : EpWiden {
   }
 };
 
+// EpWidenBnBwd with the widened gradient kept compact: only the lattice points are stored, as
+// the OH x OW grid out[m][n]; the BN-backward sums read the BN's input at the lattice points of
+// the widened grid.  The consumer takes the off-lattice zeros as implied (dk_conv2d_wgrad_bnbwd_
+// narrow_f32 with g_lattice = 2), so they are neither written nor read.
+struct EpLatticeBnBwd : EpWiden {
+  static constexpr bool kColStats = true;
+  double* part;
+  FoldTail ft{};
+  const float* xbn;  // the BN's raw input on the widened grid
+  BnIn bn;
+  __device__ __forceinline__ Pre pre4(int m, int n) const { return Pre{ld4(xbn + cell(m) * ldo + n)}; }
+  __device__ __forceinline__ void put4(int m, int n, f32x4 v, const Pre& p, int, double* a, double* b) const {
+    st4(out + (size_t)m * ldo + n, v);
+    bn_bwd_contrib4(v, p.x, bn, n, a, b);
+  }
+  __device__ __forceinline__ void put1(int m, int n, float v, int, double& a, double& b) const {
+    out[(size_t)m * ldo + n] = v;
+    bn_bwd_contrib(v, xbn[cell(m) * ldo + n], bn.mean[n], bn.invstd[n], bn.gamma[n], bn.beta[n], bn.relu, a, b);
+  }
+};
+
 // Split-K partial tile: ws[split][M][N].
 struct EpPartial {
   static constexpr bool kColStats = false;
@@ -1652,6 +1673,31 @@ DK_API int dk_pwconv_dgrad_ex_f32(const float* dy, int N, int OH, int OW, int K,
   ep.bn = bn;
   DK_ROWS(EpWidenBnBwd, ep);
 #undef DK_ROWS
+}
+
+// dk_pwconv_dgrad_ex_f32 with the input BN's partials for stride > 1, the widened gradient kept
+// compact (EpLatticeBnBwd): dx_lat[n][oh][ow][c] = the widened dx at (n, s*oh, s*ow, c), the
+// rest of the widened grid being zero; part has dk_pwconv_dgrad_stats_rows() rows.
+DK_API int dk_pwconv_dgrad_lattice_f32(const float* dy, int N, int OH, int OW, int K, const float* w_kc, int C,
+                                       int stride, float* dx_lat, const float* bn_x, const float* bn_mean,
+                                       const float* bn_invstd, const float* bn_gamma, const float* bn_beta,
+                                       int bn_relu, double* part, void* stream) {
+  const int M = N * OH * OW;
+  if (!fits((size_t)M * K * 4) || !fits((size_t)M * C * 4) || stride < 2 || !dx_lat || !bn_x || !part)
+    return DK_ERR_ARGS;
+  if (!bn_mean || !bn_invstd || !bn_gamma || !bn_beta) return DK_ERR_ARGS;
+  MatDesc a = mat(dy, M, K, M);
+  MatDesc b = mat(w_kc, K, C, C);
+  const hipStream_t st = as_stream(stream);
+  const bool vec = vec_ok(a, K, 4) && vec_ok(b, 4, C);
+  EpLatticeBnBwd ep;
+  static_cast<EpWiden&>(ep) = ep_widen(dx_lat, C, OH, OW, stride);
+  ep.v4 = ep.v4 && aligned16(bn_x) && bn_ok(bn_mean, bn_invstd, bn_gamma, bn_beta);
+  ep.part = part;
+  ep.xbn = bn_x;
+  ep.bn = BnIn{bn_mean, bn_invstd, bn_gamma, bn_beta, bn_relu};
+  return vec ? igemm_rows<LdMatKC, MatDesc, LdMatIC, MatDesc, EpLatticeBnBwd>(a, b, ep, M, C, K, st)
+             : igemm_rows<LdMatKC1, MatDesc, LdMatIC1, MatDesc, EpLatticeBnBwd>(a, b, ep, M, C, K, st);
 }
 
 // dgrad of a stride-1 pointwise layer whose output fed a BatchNorm (+ReLU), with that BN's

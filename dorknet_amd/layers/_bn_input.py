@@ -95,10 +95,11 @@ class BNGrad:
     instead of writing dx; a producer with ``accepts_bn_grad`` forms dx = f(g, x) as its dgrad
     loads it (the *_dgrad_bnbwd_f32 entries) and stores it once for its weight gradient.
     ``materialize()`` is the unfused apply (bit-identical)."""
-    __slots__ = ("g", "x", "mean", "invstd", "gamma", "beta", "relu", "k12", "_dx")
+    __slots__ = ("_g", "x", "mean", "invstd", "gamma", "beta", "relu", "k12", "_dx", "lattice")
 
-    def __init__(self, g, x, mean, invstd, gamma, beta, relu, k12):
-        self.g = g            # gradient w.r.t. the BN (+ReLU) output, NHWC like x
+    def __init__(self, g, x, mean, invstd, gamma, beta, relu, k12, lattice=1):
+        self._g = g           # gradient w.r.t. the BN (+ReLU) output, NHWC like x
+        self.lattice = int(lattice)  # > 1: _g holds only the stride-`lattice` lattice, compact (see g_compact)
         self.x = x            # the BN's raw input
         self.mean = mean
         self.invstd = invstd
@@ -119,6 +120,18 @@ class BNGrad:
     def dtype(self):
         return self.x.dtype
 
+    @property
+    def g(self):
+        """The dense gradient (a lattice gradient is widened here: zeros off the lattice)."""
+        if self.lattice > 1:
+            self._g, self.lattice = widen_lattice(self._g, self.lattice, self.x.shape), 1
+        return self._g
+
+    @property
+    def g_compact(self):
+        """The gradient as held: with lattice > 1, [N][C][ceil(H/s)][ceil(W/s)] (NHWC)."""
+        return self._g
+
     def bnbwd_args(self):
         """(mean, invstd, gamma, beta, relu, k12) for a *_dgrad_bnbwd_f32 call."""
         return (self.mean.data_ptr(), self.invstd.data_ptr(), self.gamma.data_ptr(), self.beta.data_ptr(),
@@ -133,6 +146,16 @@ class BNGrad:
                   self.k12.data_ptr(), dx.data_ptr(), stream_handle())
             self._dx = dx
         return self._dx
+
+
+def widen_lattice(g, s, shape):
+    """Layout plumbing for a consumer that needs the dense gradient: the stride-s lattice gradient
+    `g` placed on a zero grid of `shape` (what the reference's widen builds,
+    pointwise_convolution.py:68-72)."""
+    out = empty_nhwc(*shape, dtype=g.dtype)
+    out.zero_()
+    out[:, :, ::s, ::s] = g
+    return out
 
 
 def accepts_bn_grad(layer, bn_layer) -> bool:

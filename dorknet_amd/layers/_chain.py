@@ -179,6 +179,14 @@ def chain_backward(steps, dy, residual=None, after_step=None, need_input_grad=Tr
             else:
                 dy = step[0].backward(dy, residual=residual)
             residual = None
+        elif (fuse and i >= 2 and len(step) == 1 and getattr(step[0], "lattice_ok", None) is not None
+              and step[0].lattice_ok() and type(steps[i - 1][0]) is BatchNormLayer and len(steps[i - 2]) == 1
+              and getattr(steps[i - 2][0], "accepts_lattice_grad", False)
+              and accepts_bn_grad(steps[i - 2][0], steps[i - 1][0])
+              and os.environ.get("DORKNET_LATTICE", "1") != "0"):
+            # a stride-2 pointwise layer whose input gradient goes (through a deferred BatchNorm) to a
+            # consumer that takes the lattice form: the widen's zeros are never written
+            dy = step[0].backward(dy, lattice_out=True)
         elif fuse and i > 0 and len(step) == 1 and getattr(step[0], "accepts_join", False) and \
                 _join_of(steps[i - 1]) is not None:
             dy = step[0].backward(dy, join=_join_of(steps[i - 1]))

@@ -244,6 +244,7 @@ class BatchNormLayer(Layer):
         self._require_on_gpu()
         st = stream_handle()
         x = self.X
+        lattice = getattr(upstream_dx, "_dk_lattice", 1)  # a compact stride-s lattice gradient (widen elided)
         dy = to_nhwc(upstream_dx) if x.dim() == 4 else rows(upstream_dx)
         bf = x.dtype == BF16
         if bf and dy.dtype != BF16:
@@ -255,6 +256,10 @@ class BatchNormLayer(Layer):
         dbeta = grad_buffer(self, "beta", beta.shape)
         dx = self._out_like(x)
         pending, self._pending_bwd = getattr(self, "_pending_bwd", None), None
+        if lattice > 1 and not (defer and not bf and pending is not None and pending[0] is upstream_dx):
+            # only a deferred hand-over keeps the lattice form: everything else takes the dense gradient
+            from ._bn_input import widen_lattice
+            dy, lattice, pending = widen_lattice(dy, lattice, x.shape), 1, None
         if pending is not None and pending[0].data_ptr() == dy.data_ptr() and pending[0].shape == dy.shape:
             # stage 1 was computed by the consumer's dgrad epilogue (layers/_bn_input.py)
             part = pending[1]
@@ -279,7 +284,7 @@ class BatchNormLayer(Layer):
                 lib.dk_bn_bwd_finalize_f32(local.data_ptr(), 1, glob.data_ptr(), 1, C, float(P) * self._world(),
                                            dgamma.data_ptr(), dbeta.data_ptr(), k12.data_ptr(), st)
             if defer and not bf:
-                return BNGrad(dy, x, self._mean, self._invstd, gamma, beta, relu, k12)
+                return BNGrad(dy, x, self._mean, self._invstd, gamma, beta, relu, k12, lattice=lattice)
             (lib.dk_bn_bwd_apply_bf16 if bf else lib.dk_bn_bwd_apply_f32)(
                 x.data_ptr(), dy.data_ptr(), x.numel(), C, self._mean.data_ptr(), self._invstd.data_ptr(),
                 gamma.data_ptr(), beta.data_ptr(), int(relu), k12.data_ptr(), dx.data_ptr(), st)

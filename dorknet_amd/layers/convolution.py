@@ -154,6 +154,11 @@ class ConvLayer(Layer):
 
     skips_input_grad = True  # backward(dy, need_dx=False): parameter gradients only (chain_backward)
 
+    @property
+    def accepts_lattice_grad(self):
+        """The BN-deferred weight gradient takes a stride-2 lattice gradient (the narrow kernels)."""
+        return bool(getattr(self, "_narrow", False))
+
     def accepts_bn_grad(self, bn_layer):
         """backward(BNGrad, need_dx=False): the following BatchNorm's apply runs in this layer's
         weight-gradient loader (dk_conv2d_wgrad_bnbwd_f32) -- the stem, whose input gradient
@@ -177,11 +182,12 @@ class ConvLayer(Layer):
         w = self.learned_params["weights"]
         gw = grad_buffer(self, "weights", (K, C, R, S))
         s = l2_strength(self.weight_regulariser)
-        g = to_nhwc(G.g)
         if self._narrow:
+            lat = G.lattice if G.lattice == 2 else 1
+            g = G.g_compact if lat == 2 else to_nhwc(G.g)
             nb = lib.dk_conv2d_wgrad_narrow_workspace_bytes(N, Cp, H, W, K, R, S, self.stride, self.padding, OH, OW)
             r = lib.dk_conv2d_wgrad_bnbwd_narrow_f32(g.data_ptr(), G.x.data_ptr(), x.data_ptr(), N, Cp, H, W, K, R, S,
-                                                     self.stride, self.padding, OH, OW, *G.bnbwd_args(),
+                                                     self.stride, self.padding, OH, OW, *G.bnbwd_args(), lat,
                                                      w.data_ptr() if s else 0, s or 0.0, gw.data_ptr(),
                                                      workspace.get(nb), nb, st)
             if r:
@@ -189,6 +195,7 @@ class ConvLayer(Layer):
             if s is None:
                 add_regulariser_grad(gw, w, self.weight_regulariser)
             return
+        g = to_nhwc(G.g)
         nb = lib.dk_conv2d_wgrad_workspace_bytes(N, OH, OW, K, Cp, R, S)
         lib.dk_conv2d_wgrad_bnbwd_f32(g.data_ptr(), G.x.data_ptr(), x.data_ptr(), N, H, W, Cp, C, K, R, S,
                                       self.stride, self.padding, OH, OW, *G.bnbwd_args(), w.data_ptr() if s else 0,

@@ -135,7 +135,19 @@ class PointwiseConvLayer(Layer):
 
     skips_input_grad = True  # backward(dy, need_dx=False): parameter gradients only (chain_backward)
 
-    def backward(self, upstream_dx, residual=None, need_dx=True):
+    def lattice_ok(self):
+        """backward(dy, lattice_out=True) can hand over its widened input gradient as the compact
+        stride-s lattice (dk_pwconv_dgrad_lattice_f32): stride > 1, fp32, the input consumed as a
+        BNOut (the partials of that BN ride on the dgrad)."""
+        x = getattr(self, "X", None)
+        return (self.stride > 1 and x is not None and x.dtype == torch.float32 and self._bn_in is not None
+                and x.shape[1] == self.num_channels and not self.with_bias
+                and tuple(x.shape[2:]) == (self.out_hw[0] * self.stride, self.out_hw[1] * self.stride))
+
+    def backward(self, upstream_dx, residual=None, need_dx=True, lattice_out=False):
+        """lattice_out: return the input gradient as the compact stride-s lattice (a tensor tagged
+        `_dk_lattice = s`) when lattice_ok(); chain_backward asks for it only when the consumer of
+        that gradient takes the lattice form."""
         self._require_on_gpu()
         st = stream_handle()
         x = self.X
@@ -164,7 +176,26 @@ class PointwiseConvLayer(Layer):
             raise NotImplementedError("{}: bf16 storage needs a bf16 gradient, no bias, stride 1".format(
                 self.layer_name))
         self._wgrad(dy, x, N, H, W, C, K, s, OH, OW, P, w, bf)
+        if need_dx and lattice_out and residual is None and not bf and self.lattice_ok():
+            return self._dgrad_lattice(dy, st)
         return self._dgrad(dy, residual, st) if need_dx else None
+
+    def _dgrad_lattice(self, dy, st):
+        """The widened input gradient kept as its lattice (+ the input BN's partials)."""
+        x = self.X
+        N, C = x.shape[0], x.shape[1]
+        K, s = self.num_filters, self.stride
+        OH, OW = self.out_hw
+        bn = self._bn_in
+        dx = empty_nhwc(N, C, OH, OW)
+        rows = lib.dk_pwconv_dgrad_stats_rows(N, OH, OW, K, C)
+        part = torch.empty((rows, 2, C), dtype=torch.float64, device=dx.device)
+        tok = bn.arm_partials(part)
+        r = lib.dk_pwconv_dgrad_lattice_f32(dy.data_ptr(), N, OH, OW, K, self.learned_params["weights"].data_ptr(), C,
+                                            s, dx.data_ptr(), bn.x.data_ptr(), *bn.bn_args(), part.data_ptr(), st)
+        dx._dk_lattice = s
+        bn.hand_backward_partials(dx, part, r, tok)
+        return dx
 
     def _backward_padded(self, dy, residual, need_dx, st):
         """Backward for C % 4 != 0: the input was padded to Cp channels in forward."""

@@ -176,9 +176,14 @@ MODEL = {
         2 * N * OH * OW * K * C * R * S, E * (N * C * H * W + N * OH * OW * K + K * C * R * S)),
     "dk_conv2d_wgrad_narrow_f32": lambda dy, x, N, C, H, W, K, R, S, st_, pad, OH, OW, *rest: (
         2 * N * OH * OW * K * C * R * S, E * (N * OH * OW * K + N * C * H * W + K * C * R * S)),
-    "dk_conv2d_wgrad_bnbwd_narrow_f32": lambda g, ox, x, N, C, H, W, K, R, S, st_, pad, OH, OW, *rest: (
+    # (g read on its lattice only when g_lattice = 2: a quarter of the pixels)
+    "dk_conv2d_wgrad_bnbwd_narrow_f32": lambda g, ox, x, N, C, H, W, K, R, S, st_, pad, OH, OW, m, i, ga, b, relu,
+    k12, lat, *rest: (
         2 * N * OH * OW * K * C * R * S + 6 * N * OH * OW * K,
-        E * (2 * N * OH * OW * K + N * C * H * W + K * C * R * S)),
+        E * (N * OH * OW * K + N * (-(-OH // lat)) * (-(-OW // lat)) * K + N * C * H * W + K * C * R * S)),
+    # stride-s pointwise dgrad kept as its lattice (+ the input BN's partials at the lattice points)
+    "dk_pwconv_dgrad_lattice_f32": lambda dy, N, OH, OW, K, w, C, s, dx, bx, *rest: (
+        2 * N * OH * OW * K * C, E * (N * OH * OW * K + 2 * N * OH * OW * C + K * C)),
     "dk_pwconv_fwd_bnx_f32": _bnx(_pw_fwd),
     "dk_pwconv_wgrad_bnx_f32": _bnx(_pw_wgrad),
     "dk_dwconv_fwd_bnx_f32": _bnx(_dw_fwd),

@@ -138,13 +138,15 @@ int dk_pwconv_wgrad_bnx_f32(const float* dy, const float* x, int N, int H, int W
  * partial rows [dk_conv2d_fwd_narrow_stats_rows()][2][K] (in-launch fold: dk_bn_fold_arm_stats).
  * dk_conv2d_wgrad_narrow_f32 / _bnbwd_narrow_f32: as dk_conv2d_wgrad_f32 /
  * dk_conv2d_wgrad_bnbwd_f32 (dy given, or formed on load from the following BatchNorm's
- * deferred gradient), x NCHW; workspace: dk_conv2d_wgrad_narrow_workspace_bytes. */
+ * deferred gradient), x NCHW; workspace: dk_conv2d_wgrad_narrow_workspace_bytes.  g_lattice = 2: g is
+ * given compact on the even (oh, ow) lattice only ([N][ceil(OH/2)][ceil(OW/2)][K], zero elsewhere: the
+ * un-widened gradient of a following stride-2 pointwise layer, dk_pwconv_dgrad_lattice_f32); 1: dense. */
 int dk_conv2d_narrow_preferred(int N, int C, int H, int W, int K, int R, int S, int stride, int pad, int OH, int OW);
 int dk_conv2d_fwd_narrow_stats_rows(int N, int C, int H, int W, int K, int R, int S, int stride, int pad, int OH, int OW);
 int dk_conv2d_fwd_narrow_f32(const float* x_nchw, int N, int C, int H, int W, const float* w_kcrs, int K, int R, int S, int stride, int pad, const float* bias, float* y, int OH, int OW, double* stats, void* stream);
 size_t dk_conv2d_wgrad_narrow_workspace_bytes(int N, int C, int H, int W, int K, int R, int S, int stride, int pad, int OH, int OW);
 int dk_conv2d_wgrad_narrow_f32(const float* dy, const float* x_nchw, int N, int C, int H, int W, int K, int R, int S, int stride, int pad, int OH, int OW, const float* w_kcrs, float l2, float* dw_kcrs, void* ws, size_t ws_bytes, void* stream);
-int dk_conv2d_wgrad_bnbwd_narrow_f32(const float* g, const float* bn_x, const float* x_nchw, int N, int C, int H, int W, int K, int R, int S, int stride, int pad, int OH, int OW, const float* out_mean, const float* out_invstd, const float* out_gamma, const float* out_beta, int out_relu, const float* k12, const float* w_kcrs, float l2, float* dw_kcrs, void* ws, size_t ws_bytes, void* stream);
+int dk_conv2d_wgrad_bnbwd_narrow_f32(const float* g, const float* bn_x, const float* x_nchw, int N, int C, int H, int W, int K, int R, int S, int stride, int pad, int OH, int OW, const float* out_mean, const float* out_invstd, const float* out_gamma, const float* out_beta, int out_relu, const float* k12, int g_lattice, const float* w_kcrs, float l2, float* dw_kcrs, void* ws, size_t ws_bytes, void* stream);
 /* Producer side of the same fusion: *_fwd_ex_f32 = forward with an optional input BN
  * (bn_mean == NULL: raw input) and, when stats != NULL, the BatchNorm statistics of the
  * output y (fp64 sum and sum of squares per output channel, per tile: stats[rows][2][K],
@@ -169,6 +171,11 @@ int dk_dwconv_fwd_ex_f32(const float* x, int N, int H, int W, int C, const float
  * residual_block.py:94-97; NULL = none) and make the BN part optional (bn_x == NULL). */
 int dk_pwconv_dgrad_stats_rows(int N, int OH, int OW, int K, int C);
 int dk_pwconv_dgrad_ex_f32(const float* dy, int N, int OH, int OW, int K, const float* w_kc, int C, int stride, float* dx, const float* residual, const float* bn_x, const float* bn_mean, const float* bn_invstd, const float* bn_gamma, const float* bn_beta, int bn_relu, double* part, void* stream);
+/* dk_pwconv_dgrad_ex_f32 (with the input BN's partials) for stride > 1, the widened gradient kept
+ * compact: dx_lat[n][oh][ow][c] = the widened dx (pointwise_convolution.py:68-72) at (n, s*oh, s*ow, c);
+ * every other point of the widened grid is zero and is neither written nor handed on (the
+ * consumer is dk_conv2d_wgrad_bnbwd_narrow_f32 with g_lattice = 2).  Rows: dk_pwconv_dgrad_stats_rows. */
+int dk_pwconv_dgrad_lattice_f32(const float* dy, int N, int OH, int OW, int K, const float* w_kc, int C, int stride, float* dx_lat, const float* bn_x, const float* bn_mean, const float* bn_invstd, const float* bn_gamma, const float* bn_beta, int bn_relu, double* part, void* stream);
 int dk_dwconv_dgrad_stats_rows(int N, int H, int W, int C, int stride);
 int dk_dwconv_dgrad_ex_f32(const float* dy, int N, int OH, int OW, int C, const float* w_crs, int R, int S, int stride, int pad, float* dx, int H, int W, void* ws, size_t ws_bytes, const float* residual, const float* bn_x, const float* bn_mean, const float* bn_invstd, const float* bn_gamma, const float* bn_beta, int bn_relu, double* part, void* stream);
 /* The other side of the same BatchNorm pair: *_dgrad_bnbwd_f32 = a stride-1 layer's input

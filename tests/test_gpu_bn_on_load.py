@@ -530,9 +530,21 @@ def test_conv_wgrad_bnbwd_narrow_bitwise(relu, C, K, R, stride, N, H, W):
                                           w.data_ptr(), 1e-3, dw0.data_ptr(), workspace.get(nb), nb, st) == 0
     dw1 = torch.full_like(dw0, float("nan"))
     assert lib.dk_conv2d_wgrad_bnbwd_narrow_f32(g.data_ptr(), xo.data_ptr(), x.data_ptr(), N, C, H, W, K, R, R,
-                                                stride, pad, OH, OW, *args(po, relu), k12.data_ptr(), w.data_ptr(),
+                                                stride, pad, OH, OW, *args(po, relu), k12.data_ptr(), 1, w.data_ptr(),
                                                 1e-3, dw1.data_ptr(), workspace.get(nb), nb, st) == 0
     same(dw0, dw1)
+    # g on the stride-2 lattice only (compact): the same weight gradient as the widened g, bitwise
+    gc = nhwc(rng.randn(N, K, (OH + 1) // 2, (OW + 1) // 2))
+    gw = torch.zeros((N, K, OH, OW), device="cuda").contiguous(memory_format=torch.channels_last)
+    gw[:, :, ::2, ::2] = gc
+    dw2 = torch.full_like(dw0, float("nan"))
+    dw3 = torch.full_like(dw0, float("nan"))
+    for gg, lat, out in ((gw, 1, dw2), (gc, 2, dw3)):
+        assert lib.dk_conv2d_wgrad_bnbwd_narrow_f32(gg.data_ptr(), xo.data_ptr(), x.data_ptr(), N, C, H, W, K, R, R,
+                                                    stride, pad, OH, OW, *args(po, relu), k12.data_ptr(), lat,
+                                                    w.data_ptr(), 1e-3, out.data_ptr(), workspace.get(nb), nb,
+                                                    st) == 0
+    same(dw2, dw3)
     # and the weight gradient itself against a float64 torch reference
     ref = torch.nn.grad.conv2d_weight(x.double(), (K, C, R, R), dy.double().contiguous(), stride=stride,
                                       padding=pad) + 1e-3 * w.double()
