@@ -307,9 +307,17 @@ static bool shape_ok(int C, int R, int S, int st) {
   return false;
 }
 
+static int quads(int OW) {  // the compiled pixel-quad counts (wgrad_kernel QC)
+  const int q = cdiv(OW, 4);
+  return q <= 4 ? 4 : q <= 8 ? 8 : q <= 16 ? 16 : q <= 28 ? 28 : 32;
+}
+
 static bool supported(int N, int C, int H, int W, int K, int R, int S, int st, int pad, int OH, int OW) {
-  // staged columns st * (16 * ceil(OW / 16) - 1) + S: one per thread
-  if (!shape_ok(C, R, S, st) || OW < 1 || st * (16 * cdiv(OW, 16) - 1) + S > NT) return false;
+  // staged columns: one per thread -- the forward's st * (16 * ceil(OW / 16) - 1) + S and the weight
+  // gradient's st * (4 * quads(OW) - 1) + S (its padded pixel quads read staged zeros)
+  if (!shape_ok(C, R, S, st) || OW < 1 || OW > 128 || st * (16 * cdiv(OW, 16) - 1) + S > NT ||
+      st * (4 * quads(OW) - 1) + S > NT)
+    return false;
   return N > 0 && K >= 4 && K <= 64 && K % 4 == 0 && pad >= 0 && OH >= 1 && OW <= 128 && H >= 1 && W >= 1 &&
          (size_t)N * OH * OW * K * 4 < ((size_t)1 << 31) && (size_t)N * C * H * W * 4 < ((size_t)1 << 31);
 }
@@ -320,7 +328,9 @@ static Geo geo(int N, int C, int H, int W, int K, int R, int S, int st, int pad,
   g.Kred = C * R * S;
   g.KK = cdiv(g.Kred, 4);
   const int T = cdiv(OW, 16);
-  g.Wp = st * (16 * T - 1) + S;
+  // staged columns: every pixel the kernel's tiles touch (the weight gradient's padded quads
+  // included: their B reads must see zeros -- a * 0 is not 0 for uninitialised LDS)
+  g.Wp = wgrad ? st * (4 * quads(OW) - 1) + S : st * (16 * T - 1) + S;
   g.CS = wgrad ? (g.Wp + 23) / 32 * 32 + 8 : (g.Wp | 1);  // wgrad: 8 (mod 32); forward: odd
   g.rows = N * OH;
   return g;
@@ -328,10 +338,6 @@ static Geo geo(int N, int C, int H, int W, int K, int R, int S, int st, int pad,
 
 static size_t rows_lds(const Geo& g) { return (size_t)(g.C * g.R + 1) * g.CS * sizeof(float); }
 static size_t fwd_lds(const Geo& g) { return rows_lds(g); }
-static int quads(int OW) {  // the compiled pixel-quad counts (wgrad_kernel QC)
-  const int q = cdiv(OW, 4);
-  return q <= 4 ? 4 : q <= 8 ? 8 : q <= 16 ? 16 : q <= 28 ? 28 : 32;
-}
 static size_t wgrad_lds(const Geo& g) { return rows_lds(g) + (size_t)4 * quads(g.OW) * 64 * sizeof(float); }
 
 using FwdFn = void (*)(const float*, const float*, const float*, float*, Geo, double*, FoldTail);
