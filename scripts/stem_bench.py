@@ -52,7 +52,7 @@ def main():
         out.append(("narrow fwd", t, fl / t / 1e6, (N * C * H * W + P * K) * 4 / t / 1e3))
         f = lambda: lib.dk_conv2d_wgrad_bnbwd_narrow_f32(gy.data_ptr(), y.data_ptr(), x.data_ptr(), N, C, H, W, K, R,
                                                          S, st, pad, OH, OW, *(p.data_ptr() for p in par), 1,
-                                                         k12.data_ptr(), w.data_ptr(), 1e-4, dw.data_ptr(), ws, nb, s)
+                                                         k12.data_ptr(), 1, w.data_ptr(), 1e-4, dw.data_ptr(), ws, nb, s)
         t = timeit(f)
         out.append(("narrow wgrad_bnbwd", t, fl / t / 1e6, (N * C * H * W + 2 * P * K) * 4 / t / 1e3))
     if a.only in (None, "gemm"):
