@@ -143,6 +143,24 @@ def test_res1_full_size(monkeypatch, pw_fused_bwd):
     _check(got, want, f32, twin, layers)
 
 
+def test_joins_full_size(monkeypatch):
+    """res1 -> res2 -> res3 at batch 256: both residual-join fusions at full size -- res1's join
+    backward in res2's fused stride-1 depthwise backward and res2's in res3's strided sub-pixel
+    dgrad (dk_dwconv_bwd_bnbwd_join_f32 / dk_dwconv_dgrad_join_f32: the join ReLU mask and the
+    join BatchNorm's stage-1 partials on the dgrad store)."""
+    from examples.resnet18_depsep import ResNet18
+    np.random.seed(37)
+    layers = ResNet18("r18").layers[6:9]
+    rng = np.random.default_rng(38)
+    _perturb_bn(layers, rng)
+    X = np.abs(rng.standard_normal((256, 64, 56, 56), dtype=np.float32))   # a ReLU output
+    dY = rng.standard_normal((256, 128, 28, 28), dtype=np.float32)
+    calls = Calls(monkeypatch, FUSED + ["dk_dwconv_bwd_bnbwd_join_f32", "dk_dwconv_dgrad_join_f32"])
+    got, want, f32, twin, _ = _run(layers, X, dY, input_grad=True)
+    assert {"dk_dwconv_bwd_bnbwd_join_f32", "dk_dwconv_dgrad_join_f32"} <= calls.seen, calls.seen
+    _check(got, want, f32, twin, layers)
+
+
 def test_res7_res8_full_size(monkeypatch):
     """res7 (stride-2 depthwise, 256 -> 512 pointwise, stride-2 skip projection with the fused
     widen) and res8 (512 -> 512 pointwise at 7 x 7, P = 12,544) at batch 256."""
