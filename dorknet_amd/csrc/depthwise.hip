@@ -245,6 +245,7 @@ struct JoinBwd {
   const float* x;  // bn_j's raw input
   const float* mean;
   const float* invstd;
+  int res_lat;  // sub-pixel dgrad: the residual given on the stride-ST lattice only (phase (0, 0)), compact
 };
 
 template <int R, int S, int ST, int PAD, class T = float, bool JOIN = false>
@@ -313,7 +314,11 @@ __global__ __launch_bounds__(256) void dw_dgrad_subpixel_kernel(const T* __restr
           const int h = qi * ST + a, w = j * ST + b;
           const bool ok = j < QW && h < H && w < W;
           const size_t off = (((size_t)n * H + h) * W + w) * C + c;
-          rv[a][b] = (res && ok) ? ld4(res + off) : f32x4{0.f, 0.f, 0.f, 0.f};
+          if (JOIN && jn.res_lat)  // compact lattice residual: phase (0, 0) only, at quad (qi, j)
+            rv[a][b] = (res && ok && a == 0 && b == 0) ? ld4(res + (((size_t)n * QH + qi) * QW + j) * C + c)
+                                                      : f32x4{0.f, 0.f, 0.f, 0.f};
+          else
+            rv[a][b] = (res && ok) ? ld4(res + off) : f32x4{0.f, 0.f, 0.f, 0.f};
           if constexpr (JOIN) {
             jmk[a][b] = ok ? *reinterpret_cast<const uint32_t*>(jn.mask + off) : 0u;
             jx[a][b] = ok ? ld4(jn.x + off) : f32x4{0.f, 0.f, 0.f, 0.f};
@@ -1137,15 +1142,17 @@ DK_API int dk_dwconv_dgrad_join_rows(int N, int H, int W, int C, int R, int S, i
 // arming (dk_bn_fold_arm_bwd).
 DK_API int dk_dwconv_dgrad_join_f32(const float* dy, int N, int OH, int OW, int C, const float* w_crs, int R, int S,
                                     int stride, int pad, float* dx, int H, int W, void* ws, size_t ws_bytes,
-                                    const float* residual, const uint8_t* join_mask, const float* join_x,
-                                    const float* join_mean, const float* join_invstd, double* part, void* stream) {
+                                    const float* residual, int residual_lattice, const uint8_t* join_mask,
+                                    const float* join_x, const float* join_mean, const float* join_invstd,
+                                    double* part, void* stream) {
+  if (residual_lattice != 0 && residual_lattice != stride) return DK_ERR_ARGS;
   if (!join_mask || !join_x || !join_mean || !join_invstd || !part ||
       dk_dwconv_dgrad_join_rows(N, H, W, C, R, S, stride, pad) == 0)
     return DK_ERR_ARGS;
   if (!aligned16(join_x) || !aligned16(join_mean) || !aligned16(join_invstd) ||
       (reinterpret_cast<uintptr_t>(join_mask) & 3))
     return DK_ERR_ARGS;
-  const JoinBwd jn{join_mask, join_x, join_mean, join_invstd};
+  const JoinBwd jn{join_mask, join_x, join_mean, join_invstd, residual_lattice ? 1 : 0};
   return dw_dgrad<float>(dy, N, OH, OW, C, w_crs, R, S, stride, pad, dx, H, W, ws, ws_bytes, residual, nullptr,
                          BnIn{}, part, as_stream(stream), &jn);
 }

@@ -158,6 +158,31 @@ def widen_lattice(g, s, shape):
     return out
 
 
+def lattice_tag(t) -> int:
+    """The stride s of a gradient handed over as its compact stride-s lattice (0: dense)."""
+    return int(getattr(t, "_dk_lattice", 0) or 0) if isinstance(t, torch.Tensor) else 0
+
+
+def dense_residual(residual, shape):
+    """`residual` on the dense grid `shape` (N, C, H, W): a lattice-tagged gradient is widened."""
+    s = lattice_tag(residual)
+    return widen_lattice(residual, s, tuple(shape)) if s else residual
+
+
+def lattice_operand(residual, like, s):
+    """`residual` as the compact stride-s lattice operand for a dgrad shaped like `like` (the
+    skip projection's un-widened input gradient: [N][ceil(H/s)][ceil(W/s)][C] NHWC), or None."""
+    from .._tensor import is_nhwc
+    if lattice_tag(residual) != s or s < 2:
+        return None
+    N, C, H, W = like.shape
+    r = residual
+    if (r.is_cuda and r.dtype == like.dtype and r.dim() == 4 and is_nhwc(r)
+            and tuple(r.shape) == (N, C, -(-H // s), -(-W // s))):
+        return r
+    return None
+
+
 def accepts_bn_grad(layer, bn_layer) -> bool:
     f = getattr(layer, "accepts_bn_grad", None)
     return bool(f(bn_layer)) if f is not None else False
@@ -187,7 +212,8 @@ def residual_operand(residual, like):
 def add_residual(dx, residual):
     """dx + residual (the unfused residual join, residual_block.py:94-97)."""
     from .._tensor import to_nhwc
-    a, b = to_nhwc(dx), to_nhwc(residual)
+    a = to_nhwc(dx)
+    b = to_nhwc(dense_residual(residual, a.shape))
     if a.shape != b.shape:
         raise ValueError("residual backward shape mismatch: {} vs {}".format(tuple(a.shape), tuple(b.shape)))
     out = empty_nhwc(*a.shape)

@@ -15,7 +15,7 @@ import torch
 
 from .._hip import HipError, lib, stream_handle, weight_grad_stream, workspace
 from .._tensor import BF16, empty_nhwc, ptr, to_nhwc
-from ._bn_input import BNGrad, BNOut, add_residual, residual_operand
+from ._bn_input import BNGrad, BNOut, add_residual, dense_residual, lattice_operand, residual_operand
 from ._common import add_regulariser_grad, grad_buffer, init_weights, l2_strength
 from .layer import Layer
 
@@ -132,6 +132,18 @@ class DepthwiseConvLayer(Layer):
                 and jb.x.dtype == torch.float32 and mask.is_contiguous(memory_format=torch.channels_last)
                 and jb.x.is_contiguous(memory_format=torch.channels_last))
 
+    def takes_lattice_residual(self, join, s):
+        """backward(dy, residual=R, join=relu) adds R given as the compact stride-s lattice (a
+        strided pointwise skip projection's un-widened input gradient) in the fused join dgrad
+        (dk_dwconv_dgrad_join_f32, residual_lattice = s): fp32, this layer's stride is s, and the
+        join fuses.  Any other path widens such a residual first (dense_residual)."""
+        x = getattr(self, "X", None)
+        if (x is None or x.dim() != 4 or x.dtype != torch.float32 or self.stride != s or s < 2 or join is None
+                or self.with_bias or not self._join_ok(join, True)):
+            return False
+        N, C, H, W = x.shape
+        return lib.dk_dwconv_dgrad_join_rows(N, H, W, C, self.f_rows, self.f_cols, s, self.padding) > 0
+
     def _backward_bn_grad(self, G, residual, need_dx, join=None):
         """One-pass backward from the following BatchNorm's deferred gradient (see
         accepts_bn_grad): dx (+ the residual addend, + the input BatchNorm's backward partial
@@ -146,6 +158,8 @@ class DepthwiseConvLayer(Layer):
         s = l2_strength(self.weight_regulariser)
         bn = self._bn_in
         dx = empty_nhwc(N, C, H, W, x.dtype) if need_dx else None
+        if residual is not None:
+            residual = dense_residual(residual, (N, C, H, W))
         res = residual_operand(residual, dx) if need_dx else None
         if need_dx and residual is not None and res is None:
             res = residual_operand(to_nhwc(residual), dx)
@@ -238,9 +252,17 @@ class DepthwiseConvLayer(Layer):
         nb = lib.dk_dwconv_dgrad_workspace_bytes(C, R, S)
         dgrad_ex = lib.dk_dwconv_dgrad_ex_bf16 if bf else lib.dk_dwconv_dgrad_ex_f32
         bn = self._bn_in
-        res = residual_operand(residual, dx)
+        jrows = (lib.dk_dwconv_dgrad_join_rows(N, H, W, C, R, S, self.stride, self.padding)
+                 if join is not None and not bf and self._join_ok(join, True) else 0)
+        # a residual handed over as its compact lattice is added as such by the join dgrad only
+        lat = lattice_operand(residual, dx, self.stride) if jrows else None
+        if lat is None and residual is not None:
+            residual = dense_residual(residual, (N, C, H, W))
+        res = lat if lat is not None else residual_operand(residual, dx)
+        if residual is not None and res is None:
+            jrows = 0
         rows = lib.dk_dwconv_dgrad_stats_rows(N, H, W, C, self.stride) if bn is not None and R == S else 0
-        if rows and self.padding <= R - 1:
+        if rows and self.padding <= R - 1 and (residual is None or res is not None):
             # + stage 1 of the input BatchNorm's backward, in the dgrad epilogue (+ the residual)
             part = torch.empty((rows, 2, C), dtype=torch.float64, device=dx.device)
             tok = bn.arm_partials(part) if not bf else None
@@ -248,9 +270,6 @@ class DepthwiseConvLayer(Layer):
                          W, workspace.get(nb), nb, ptr(res), bn.x.data_ptr(), *bn.bn_args(), part.data_ptr(), st)
             bn.hand_backward_partials(dx, part, r, tok)
             return dx
-        jrows = (lib.dk_dwconv_dgrad_join_rows(N, H, W, C, R, S, self.stride, self.padding)
-                 if join is not None and not bf and self._join_ok(join, True) and (residual is None or res is not None)
-                 else 0)
         if jrows:
             # the input's residual join: its ReLU backward and its BatchNorm's stage 1 on the store
             jb = join._join_bn
@@ -258,7 +277,7 @@ class DepthwiseConvLayer(Layer):
             tok = jb.arm_partials(part)
             r = lib.dk_dwconv_dgrad_join_f32(dy.data_ptr(), N, OH, OW, C, w.data_ptr(), R, S, self.stride,
                                              self.padding, dx.data_ptr(), H, W, workspace.get(nb), nb, ptr(res),
-                                             join._mask.data_ptr(), jb.x.data_ptr(), jb.mean.data_ptr(),
+                                             self.stride if lat is not None else 0, join._mask.data_ptr(), jb.x.data_ptr(), jb.mean.data_ptr(),
                                              jb.invstd.data_ptr(), part.data_ptr(), st)
             jb.hand_backward_partials(dx, part, r, tok)
             join.join_backward_done()

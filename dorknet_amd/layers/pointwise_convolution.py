@@ -137,10 +137,11 @@ class PointwiseConvLayer(Layer):
 
     def lattice_ok(self):
         """backward(dy, lattice_out=True) can hand over its widened input gradient as the compact
-        stride-s lattice (dk_pwconv_dgrad_lattice_f32): stride > 1, fp32, the input consumed as a
-        BNOut (the partials of that BN ride on the dgrad)."""
+        stride-s lattice: stride > 1, fp32, no bias.  With the input consumed as a BNOut the
+        partials of that BN ride on the dgrad (dk_pwconv_dgrad_lattice_f32); a plain input (a
+        residual block's skip projection) gets the stride-1 GEMM into the compact grid."""
         x = getattr(self, "X", None)
-        return (self.stride > 1 and x is not None and x.dtype == torch.float32 and self._bn_in is not None
+        return (self.stride > 1 and x is not None and x.dim() == 4 and x.dtype == torch.float32
                 and x.shape[1] == self.num_channels and not self.with_bias
                 and tuple(x.shape[2:]) == (self.out_hw[0] * self.stride, self.out_hw[1] * self.stride))
 
@@ -181,13 +182,20 @@ class PointwiseConvLayer(Layer):
         return self._dgrad(dy, residual, st) if need_dx else None
 
     def _dgrad_lattice(self, dy, st):
-        """The widened input gradient kept as its lattice (+ the input BN's partials)."""
+        """The widened input gradient kept as its lattice (+ the input BN's partials).  The values
+        are the widened dgrad's at the lattice points bit for bit (the same GEMM tiles; only the
+        epilogue's addressing differs)."""
         x = self.X
         N, C = x.shape[0], x.shape[1]
         K, s = self.num_filters, self.stride
         OH, OW = self.out_hw
         bn = self._bn_in
         dx = empty_nhwc(N, C, OH, OW)
+        if bn is None:
+            lib.dk_pwconv_dgrad_f32(dy.data_ptr(), N, OH, OW, K, self.learned_params["weights"].data_ptr(), C, 1,
+                                    dx.data_ptr(), st)
+            dx._dk_lattice = s
+            return dx
         rows = lib.dk_pwconv_dgrad_stats_rows(N, OH, OW, K, C)
         part = torch.empty((rows, 2, C), dtype=torch.float64, device=dx.device)
         tok = bn.arm_partials(part)

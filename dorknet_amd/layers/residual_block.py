@@ -10,6 +10,8 @@ gets the l2 term in its own backward; and SGDMomentum never updates the skip pro
 """
 from __future__ import annotations
 
+import os
+
 from .._hip import lib, stream_handle
 from .._tensor import empty_nhwc, to_nhwc
 from ._bn_input import accepts_bn_input, materialize
@@ -97,10 +99,29 @@ class ResidualBlock(Layer):
         joined_dx = self.post_skip_activation.backward(upstream_dx)
         # the skip branch's gradient goes in first, so the chain's first layer can add it in
         # its dgrad epilogue instead of a separate join pass (residual_block.py:94-97)
-        skip_dx = self.skip_projection.backward(joined_dx) if self.skip_projection is not None else joined_dx
+        skip = self.skip_projection
+        if skip is None:
+            skip_dx = joined_dx
+        elif fusion_enabled() and self._lattice_skip(join):
+            # a strided skip's gradient stays its compact lattice: the first dgrad adds it there
+            skip_dx = skip.backward(joined_dx, lattice_out=True)
+        else:
+            skip_dx = skip.backward(joined_dx)
         if fusion_enabled():
             return chain_backward(self._steps, joined_dx, residual=skip_dx, join=join)
         return _add(chain_backward(self._steps, joined_dx), skip_dx)
+
+    def _lattice_skip(self, join):
+        """The skip projection may hand over its gradient as the stride-s lattice: it is a strided
+        pointwise layer that can (lattice_ok), and the chain's first layer adds such a residual
+        in its fused join dgrad (DepthwiseConvLayer.takes_lattice_residual).  DORKNET_LATTICE=0
+        turns the hand-overs off."""
+        skip = self.skip_projection
+        if os.environ.get("DORKNET_LATTICE") == "0" or not getattr(skip, "lattice_ok", None) or not skip.lattice_ok():
+            return False
+        first = self._steps[0][0] if self._steps else None
+        f = getattr(first, "takes_lattice_residual", None)
+        return bool(f is not None and f(join, skip.stride))
 
     def save_to_h5(self, open_f, save_grads=True):
         from ..network.checkpoint import save_layer

@@ -220,6 +220,18 @@ MODEL = {
     m, i, ga, b, r, part, ws, nb, st: (
         2 * 2 * N * H * W * C * R * S + 6 * N * H * W * C,
         E * (N * H * W * C * (3 + (dx != 0) + (res != 0)) + 2 * C * R * S)),
+    # + the input's residual join: its ReLU mask (bytes) and its BatchNorm's raw input are read
+    "dk_dwconv_bwd_bnbwd_join_f32": lambda g, ox, N, H, W, C, om, oi, og, ob, orl, k12, x, w, R, S, pad, l2, dw, dx,
+    res, mask, jx, jm, ji, part, ws, nb, st: (
+        2 * 2 * N * H * W * C * R * S + 10 * N * H * W * C,
+        E * (N * H * W * C * (5 + (res != 0)) + 2 * C * R * S) + N * H * W * C),
+    # strided dgrad + the join: dy, the residual (dense, or its compact lattice when
+    # residual_lattice = s), the mask and bn_j's input read; dx written
+    "dk_dwconv_dgrad_join_f32": lambda dy, N, OH, OW, C, w, R, S, s, p, dx, H, W, ws, nb, res, rl, mask, jx, jm, ji,
+    part, st: (
+        _dw_dgrad(dy, N, OH, OW, C, w, R, S, s, p, dx, H, W, ws, nb, st)[0] + 4 * N * H * W * C,
+        E * (N * OH * OW * C + 2 * N * H * W * C + (res != 0) * (N * OH * OW * C if rl else N * H * W * C))
+        + N * H * W * C),
     "dk_relu_bwd_bn_partial_f64": lambda dy, mask, x, P, C, *rest: (4 * P * C, E * 3 * P * C + P * C),
     "dk_bn_bwd_apply_f32": lambda x, dy, n, C, *rest: (6 * n, E * 3 * n),
 }

@@ -268,9 +268,11 @@ int dk_dwconv_bwd_bnbwd_f32(const float* g, const float* bn_x, int N, int H, int
  * Takes an in-launch fold arming (dk_bn_fold_arm_bwd). */
 int dk_dwconv_bwd_bnbwd_join_f32(const float* g, const float* bn_x, int N, int H, int W, int C, const float* out_mean, const float* out_invstd, const float* out_gamma, const float* out_beta, int out_relu, const float* k12, const float* x, const float* w_crs, int R, int S, int pad, float l2, float* dw_crs, float* dx, const float* residual, const uint8_t* join_mask, const float* join_x, const float* join_mean, const float* join_invstd, double* part, void* ws, size_t ws_bytes, void* stream);
 /* The strided (sub-pixel) depthwise input gradient with the same join fusion (the first layer of a
- * downsampling residual block); rows: dk_dwconv_dgrad_join_rows (0 = no join variant for the geometry). */
+ * downsampling residual block); rows: dk_dwconv_dgrad_join_rows (0 = no join variant for the geometry).
+ * residual_lattice = stride: the residual is the skip projection's un-widened gradient, compact on the
+ * stride lattice ([N][ceil(H/s)][ceil(W/s)][C], zero elsewhere); 0: dense [N][H][W][C]. */
 int dk_dwconv_dgrad_join_rows(int N, int H, int W, int C, int R, int S, int stride, int pad);
-int dk_dwconv_dgrad_join_f32(const float* dy, int N, int OH, int OW, int C, const float* w_crs, int R, int S, int stride, int pad, float* dx, int H, int W, void* ws, size_t ws_bytes, const float* residual, const uint8_t* join_mask, const float* join_x, const float* join_mean, const float* join_invstd, double* part, void* stream);
+int dk_dwconv_dgrad_join_f32(const float* dy, int N, int OH, int OW, int C, const float* w_crs, int R, int S, int stride, int pad, float* dx, int H, int W, void* ws, size_t ws_bytes, const float* residual, int residual_lattice, const uint8_t* join_mask, const float* join_x, const float* join_mean, const float* join_invstd, double* part, void* stream);
 
 /* ---------------------------------------------------------------------------------------
  * Dense layer (layers/dense_layer.py:46-67; W stored (in, out) as the reference).

@@ -261,11 +261,11 @@ def test_join_fusion_agrees(monkeypatch):
     from dorknet_amd import _hip
     X, _, onehot = synthetic_batch(2, seed=2)
     grads = {}
+    orig = _hip.lib.dk_dwconv_bwd_bnbwd_join_f32
     for fuse in ("1", "0"):
         monkeypatch.setenv("DORKNET_FUSE_JOIN", fuse)
         seen = set()
-        orig = _hip.lib.dk_dwconv_bwd_bnbwd_join_f32
-        monkeypatch.setattr(_hip.lib, "dk_dwconv_bwd_bnbwd_join_f32", lambda *a: seen.add(1) or orig(*a))
+        monkeypatch.setattr(_hip.lib, "dk_dwconv_bwd_bnbwd_join_f32", lambda *a, seen=seen: seen.add(1) or orig(*a))
         np.random.seed(0)
         net = ResNet18("r18")
         net.to_gpu()
@@ -274,6 +274,37 @@ def test_join_fusion_agrees(monkeypatch):
         torch.cuda.synchronize()
         assert bool(seen) == (fuse == "1")
         grads[fuse] = {(l.layer_name, k): host(v) for l in all_layers(net.layers) for k, v in (l.grads or {}).items()}
+    for key, a in grads["1"].items():
+        b = grads["0"][key]
+        err = np.linalg.norm((a - b).ravel()) / max(np.linalg.norm(b.ravel()), 1e-30)
+        assert err <= 1e-5 or np.linalg.norm(b.ravel()) < 1e-6, (key, err)
+
+
+@pytest.mark.gpu
+def test_lattice_skip_agrees(monkeypatch):
+    """A downsampling block's strided skip projection hands its input gradient over as the
+    compact stride-2 lattice and the next dgrad (dk_dwconv_dgrad_join_f32, residual_lattice = 2)
+    adds it there, vs the widened gradient (DORKNET_LATTICE=0, which also turns off the stem's
+    lattice hand-over): every gradient agrees to fp32 rounding (the lattice values are the
+    widened ones bit for bit; the BN partial sums regroup)."""
+    from examples.resnet18_depsep import ResNet18, synthetic_batch
+    from dorknet_amd import _hip
+    X, _, onehot = synthetic_batch(2, seed=2)
+    grads = {}
+    orig = _hip.lib.dk_dwconv_dgrad_join_f32
+    for lat in ("1", "0"):
+        monkeypatch.setenv("DORKNET_LATTICE", lat)
+        seen = []
+        monkeypatch.setattr(_hip.lib, "dk_dwconv_dgrad_join_f32", lambda *a, seen=seen: seen.append(a[16]) or orig(*a))
+        np.random.seed(0)
+        net = ResNet18("r18")
+        net.to_gpu()
+        net.forward(dev(X), dev(onehot))
+        net.backward()
+        torch.cuda.synchronize()
+        assert seen, "the strided join dgrad did not run"
+        assert (2 in seen) == (lat == "1"), seen
+        grads[lat] = {(l.layer_name, k): host(v) for l in all_layers(net.layers) for k, v in (l.grads or {}).items()}
     for key, a in grads["1"].items():
         b = grads["0"][key]
         err = np.linalg.norm((a - b).ravel()) / max(np.linalg.norm(b.ravel()), 1e-30)
