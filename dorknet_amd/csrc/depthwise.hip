@@ -648,7 +648,7 @@ __global__ __launch_bounds__(256) void dw_bwd_fused_kernel(const float* __restri
     xr = bload4e<float>(rx, ok, pix(hh, w));
     rv = (res && ok) ? ld4(res + pix(hh, w)) : f32x4{0.f, 0.f, 0.f, 0.f};
     if constexpr (JOIN) {
-      jmv = ok ? *reinterpret_cast<const uint32_t*>(jn.mask + pix(hh, w)) : 0u;  // the 4 mask bytes
+      if (jn.mask) jmv = ok ? *reinterpret_cast<const uint32_t*>(jn.mask + pix(hh, w)) : 0u;  // the 4 mask bytes
       jxv = ok ? ld4(jn.x + pix(hh, w)) : f32x4{0.f, 0.f, 0.f, 0.f};
     }
   };
@@ -699,7 +699,10 @@ __global__ __launch_bounds__(256) void dw_bwd_fused_kernel(const float* __restri
       if constexpr (JOIN) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          if (!((jmh >> (8 * e)) & 0xffu)) acc[e] = 0.f;  // dy * mask (activations.py:46)
+          // dy * mask (activations.py:46); no mask given: this layer's input is the join's output
+          // y = max(v, 0), and y > 0 is exactly the stored mask (v > 0)
+          const bool keep = jn.mask ? ((jmh >> (8 * e)) & 0xffu) != 0u : xh[e] > 0.f;
+          if (!keep) acc[e] = 0.f;
           const float xn = (jh[e] - jm[e]) * ji[e];
           s1[e] += (double)acc[e];
           s2[e] += (double)acc[e] * (double)xn;
@@ -1161,6 +1164,7 @@ DK_API int dk_dwconv_dgrad_join_f32(const float* dy, int N, int OH, int OW, int 
 // is the gradient w.r.t. the join's pre-ReLU sum, dx = (dgrad + residual) * join_mask, and part
 // (stats_rows x 2 x C) gets stage 1 of the backward of the join's BatchNorm (join_x: its raw
 // input; join_mean / join_invstd) -- dk_relu_bwd_bn_partial_f64's work, without re-reading dx.
+// join_mask == nullptr: x is the join's output itself and the mask is x > 0 (not read).
 DK_API int dk_dwconv_bwd_bnbwd_join_f32(const float* g, const float* bn_x, int N, int H, int W, int C,
                                         const float* out_mean, const float* out_invstd, const float* out_gamma,
                                         const float* out_beta, int out_relu, const float* k12, const float* x,
@@ -1172,7 +1176,7 @@ DK_API int dk_dwconv_bwd_bnbwd_join_f32(const float* g, const float* bn_x, int N
   if (R != 3 || S != 3 || pad != 1 || C % 4 || N < 1 || H < 1 || W < 1) return DK_ERR_ARGS;
   const int cl = dwb_cl(W, C);
   if (!g || !bn_x || !x || !w_crs || !dw_crs || !dx || !out_mean || !out_invstd || !out_gamma || !out_beta ||
-      !k12 || !join_mask || !join_x || !join_mean || !join_invstd || !part)
+      !k12 || !join_x || !join_mean || !join_invstd || !part)
     return DK_ERR_ARGS;
   if (!aligned16(g) || !aligned16(bn_x) || !aligned16(x) || !aligned16(dx) || (residual && !aligned16(residual)) ||
       !aligned16(out_mean) || !aligned16(out_invstd) || !aligned16(out_gamma) || !aligned16(out_beta) ||

@@ -29,6 +29,7 @@ class ReLu(Layer):
         self._fused_out = None
         self._join_bn = None
         self._join_done = False
+        self._join_y_ptr = None  # data_ptr of the fused join's output (_bn_add)
 
     def join_backward_done(self):
         """The consumer of this residual join's output applied this ReLU's backward (and stage 1
@@ -101,6 +102,7 @@ class ReLu(Layer):
             self._mask, self._fused_out = mask, None
             self._join_bn = A if isinstance(A, BNOut) else None
             self._join_done = False
+            self._join_y_ptr = y.data_ptr()  # a consumer holding y itself may take the mask as y > 0
         return y
 
     def _attach_fused(self, y, test_mode):

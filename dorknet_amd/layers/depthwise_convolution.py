@@ -11,6 +11,8 @@ bias (C,), ``forward`` / ``backward`` / ``__repr__`` (:41-51).
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from .._hip import HipError, lib, stream_handle, weight_grad_stream, workspace
@@ -169,10 +171,14 @@ class DepthwiseConvLayer(Layer):
             part = torch.empty((rows, 2, C), dtype=torch.float64, device=x.device)
             g = to_nhwc(G.g)
             nb = lib.dk_dwconv_bwd_bnbwd_workspace_bytes(N, H, W, C, R, S)
+            # x IS the join's output: the kernel takes the mask as x > 0 instead of reading it
+            # (DORKNET_JOIN_MASK=1 reads the stored mask)
+            from_y = getattr(join, "_join_y_ptr", None) == x.data_ptr() and os.environ.get("DORKNET_JOIN_MASK") != "1"
             tok = jb.arm_partials(part)
             r = lib.dk_dwconv_bwd_bnbwd_join_f32(g.data_ptr(), G.x.data_ptr(), N, H, W, C, *G.bnbwd_args(),
                                                  x.data_ptr(), w.data_ptr(), R, S, self.padding, s or 0.0,
-                                                 gw.data_ptr(), dx.data_ptr(), ptr(res), join._mask.data_ptr(),
+                                                 gw.data_ptr(), dx.data_ptr(), ptr(res),
+                                                 0 if from_y else join._mask.data_ptr(),
                                                  jb.x.data_ptr(), jb.mean.data_ptr(), jb.invstd.data_ptr(),
                                                  part.data_ptr(), workspace.get(nb), nb, st)
             if s is None:

@@ -224,7 +224,7 @@ MODEL = {
     "dk_dwconv_bwd_bnbwd_join_f32": lambda g, ox, N, H, W, C, om, oi, og, ob, orl, k12, x, w, R, S, pad, l2, dw, dx,
     res, mask, jx, jm, ji, part, ws, nb, st: (
         2 * 2 * N * H * W * C * R * S + 10 * N * H * W * C,
-        E * (N * H * W * C * (5 + (res != 0)) + 2 * C * R * S) + N * H * W * C),
+        E * (N * H * W * C * (5 + (res != 0)) + 2 * C * R * S) + N * H * W * C * (mask != 0)),
     # strided dgrad + the join: dy, the residual (dense, or its compact lattice when
     # residual_lattice = s), the mask and bn_j's input read; dx written
     "dk_dwconv_dgrad_join_f32": lambda dy, N, OH, OW, C, w, R, S, s, p, dx, H, W, ws, nb, res, rl, mask, jx, jm, ji,

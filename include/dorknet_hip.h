@@ -265,6 +265,8 @@ int dk_dwconv_bwd_bnbwd_f32(const float* g, const float* bn_x, int N, int H, int
  * (residual_block.py:75, no input BN): dx = (dgrad + residual) * join_mask -- the join's ReLU backward
  * (activations.py:44-47) -- and part (dk_dwconv_bwd_bnbwd_stats_rows x 2 x C) = stage 1 of bn_j's
  * backward over that dx (batch_norm.py:125-147), replacing dk_relu_bwd_bn_partial_f64's pass over it.
+ * join_mask may be NULL when x IS the join's output: the mask is then x > 0 (bit-identical to the
+ * stored one, y = max(v, 0) > 0 iff v > 0) and is not read.
  * Takes an in-launch fold arming (dk_bn_fold_arm_bwd). */
 int dk_dwconv_bwd_bnbwd_join_f32(const float* g, const float* bn_x, int N, int H, int W, int C, const float* out_mean, const float* out_invstd, const float* out_gamma, const float* out_beta, int out_relu, const float* k12, const float* x, const float* w_crs, int R, int S, int pad, float l2, float* dw_crs, float* dx, const float* residual, const uint8_t* join_mask, const float* join_x, const float* join_mean, const float* join_invstd, double* part, void* ws, size_t ws_bytes, void* stream);
 /* The strided (sub-pixel) depthwise input gradient with the same join fusion (the first layer of a

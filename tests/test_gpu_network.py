@@ -309,3 +309,30 @@ def test_lattice_skip_agrees(monkeypatch):
         b = grads["0"][key]
         err = np.linalg.norm((a - b).ravel()) / max(np.linalg.norm(b.ravel()), 1e-30)
         assert err <= 1e-5 or np.linalg.norm(b.ravel()) < 1e-6, (key, err)
+
+
+@pytest.mark.gpu
+def test_join_mask_from_output_bitwise(monkeypatch):
+    """The fused join backward takes the join's ReLU mask as (its output > 0) from the layer input
+    it already reads, instead of the stored mask bytes (DORKNET_JOIN_MASK=1): every gradient is
+    bit-identical."""
+    from examples.resnet18_depsep import ResNet18, synthetic_batch
+    from dorknet_amd import _hip
+    X, _, onehot = synthetic_batch(2, seed=2)
+    grads = {}
+    orig = _hip.lib.dk_dwconv_bwd_bnbwd_join_f32
+    for read in ("0", "1"):
+        monkeypatch.setenv("DORKNET_JOIN_MASK", read)
+        masks = []
+        monkeypatch.setattr(_hip.lib, "dk_dwconv_bwd_bnbwd_join_f32",
+                            lambda *a, masks=masks: masks.append(a[21]) or orig(*a))
+        np.random.seed(0)
+        net = ResNet18("r18")
+        net.to_gpu()
+        net.forward(dev(X), dev(onehot))
+        net.backward()
+        torch.cuda.synchronize()
+        assert masks and all((m == 0) == (read == "0") for m in masks), masks
+        grads[read] = {(l.layer_name, k): host(v) for l in all_layers(net.layers) for k, v in (l.grads or {}).items()}
+    for key, a in grads["0"].items():
+        np.testing.assert_array_equal(a, grads["1"][key], err_msg=str(key))
