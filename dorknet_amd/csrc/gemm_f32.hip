@@ -1580,7 +1580,7 @@ DK_API int dk_pwconv_fwd_bnx_f32(const float* x, int N, int H, int W, int C, con
 DK_API int dk_pwconv_fwd_stats_rows(int N, int OH, int OW, int K, int C) {
   const int M = N * OH * OW;
   // (the input extent does not change the choice for the shapes the network uses)
-  if (pw_stream_fwd_ok(K, C, M, 0)) return pw_stream_fwd_rows(M);
+  if (pw_stream_fwd_ok(K, C, M, 0)) return pw_stream_fwd_rows(M, K);
   return stats_rows(M, K, C);
 }
 
@@ -1590,11 +1590,11 @@ DK_API int dk_pwconv_fwd_ex_f32(const float* x, int N, int H, int W, int C, cons
                                 double* stats, void* stream) {
   if (C % 4 || !aligned16(x) || !aligned16(w_kc) || !fits((size_t)N * H * W * C * 4)) return DK_ERR_ARGS;
   if (pw_stream_fwd_ok(K, C, N * OH * OW, (size_t)N * H * W * C * 4) && (!bn_mean || bn_ok(bn_mean, bn_invstd, bn_gamma, bn_beta)))
-    // K = C = 64: the persistent streaming kernel (pw_stream.hip), bit-identical outputs
+    // K = C = 64 / 128: the persistent streaming kernel (pw_stream.hip), bit-identical outputs
   {
     FoldTail ft;
-    if (stats) fold_take(stats, pw_stream_fwd_rows(N * OH * OW), K, 1, &ft);
-    return fold_status(pw_stream_fwd(x, N, H, W, stride, OH, OW, w_kc, bias, y, bn_mean, bn_invstd, bn_gamma,
+    if (stats) fold_take(stats, pw_stream_fwd_rows(N * OH * OW, K), K, 1, &ft);
+    return fold_status(pw_stream_fwd(x, N, H, W, stride, OH, OW, w_kc, K, bias, y, bn_mean, bn_invstd, bn_gamma,
                                      bn_beta, bn_relu, stats, as_stream(stream), stats ? &ft : nullptr),
                        stats ? ft : FoldTail{});
   }

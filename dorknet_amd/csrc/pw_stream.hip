@@ -40,6 +40,12 @@ constexpr int SKB = KR + 4;     // LDS row stride of the B image Bs[n][k]: (KR+4
 constexpr int KQ = KR / 8;      // float4 groups per lane per operand row
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
+// vmcnt(0) (expcnt, lgkmcnt left alone; gfx9 encoding).  Issued once after the loop's first
+// operand loads: the waitcnt pass then sees no VMEM result pending on the preheader path and
+// does not put a wait at the loop head -- which, merged with the back edge, waited for the
+// previous tile's output stores before every tile's first MFMA.
+__device__ __forceinline__ void drain_vmem_loads() { __builtin_amdgcn_s_waitcnt(0x0F70); }
+
 struct DgradArgs {
   const float* g;     // [M][KR] gradient w.r.t. the following BN's (+ReLU) output
   const float* xo;    // [M][KR] that BN's raw input (= this layer's output)
@@ -133,6 +139,7 @@ __global__ __launch_bounds__(256, 2) void dgrad_bnbwd_kernel(DgradArgs a) {
   };
   f32x4 cg[KQ], cx[KQ];  // this tile's raw A operands (loaded one iteration ahead)
   load_a(t, cg, cx);
+  drain_vmem_loads();
   for (; t < ntiles; t += W) {
     const int m0 = t * TR;
     // an opaque zero: keeps the (loop-invariant) LDS table and weight reads inside the loop,
@@ -287,11 +294,18 @@ struct FwdArgs {
   FoldTail ft;        // ft.part != nullptr: fold the statistics rows in this launch
 };
 
-template <bool BN, bool STATS, bool STRIDED>
-__global__ __launch_bounds__(256, 3) void fwd_kernel(FwdArgs a) {
-  __shared__ float Bs[NO * SKB];
+template <int KR_, int NO_, bool BN, bool STATS, bool STRIDED>
+__global__ __launch_bounds__(256, KR_ == 64 ? 3 : 2) void fwd_kernel(FwdArgs a) {
+  // K = C = 64 (res1/res2) or 128 (res3/res4): the reduction KR, the output columns NO, NU MFMA
+  // column blocks of 32; at 128 the transformed A operand overwrites its registers in place
+  constexpr int KR = KR_, NO = NO_, SKB = KR + 4, KQ = KR / 8, NU = NO / 32;
+  static_assert(KR % 32 == 0 && NO % 32 == 0 && (SKB / 4) % 2 == 1, "pws::fwd_kernel shape");
+  __shared__ __attribute__((aligned(16))) float Bs[NO * SKB];
   __shared__ float tab[4][KR];
-  __shared__ double red[WAVES][2][NO];
+  // the statistics' block reduction reuses the B image once every wave has left the loop (at
+  // K = C = 128 a separate buffer would push the block past 80 KB: one block per CU)
+  double(*const red)[2][NO] = reinterpret_cast<double(*)[2][NO]>(Bs);
+  static_assert(sizeof(double) * WAVES * 2 * NO <= sizeof(float) * NO * SKB, "red fits in Bs");
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int l32 = lane & 31, h = lane >> 5;
@@ -307,11 +321,9 @@ __global__ __launch_bounds__(256, 3) void fwd_kernel(FwdArgs a) {
       tab[3][c] = a.ib[c];
     }
   }
-  float bias[2] = {0.f, 0.f};
-  if (a.bias) {
-    bias[0] = a.bias[l32];
-    bias[1] = a.bias[32 + l32];
-  }
+  float bias[NU];
+#pragma unroll
+  for (int u = 0; u < NU; ++u) bias[u] = a.bias ? a.bias[32 * u + l32] : 0.f;
   const bool irelu = a.irelu != 0;
   __syncthreads();
 
@@ -320,7 +332,9 @@ __global__ __launch_bounds__(256, 3) void fwd_kernel(FwdArgs a) {
   const int ntiles = (a.M + TR - 1) / TR;
   const int W = gridDim.x * WAVES;
   int t = blockIdx.x * WAVES + wave;
-  double ps[2] = {0.0, 0.0}, pq[2] = {0.0, 0.0};
+  double ps[NU], pq[NU];
+#pragma unroll
+  for (int u = 0; u < NU; ++u) ps[u] = pq[u] = 0.0;
 
   auto load_a = [&](int tile, f32x4* lx) {
     const int m = tile * TR + l32;
@@ -338,6 +352,7 @@ __global__ __launch_bounds__(256, 3) void fwd_kernel(FwdArgs a) {
   };
   f32x4 cx[KQ];
   load_a(t, cx);
+  drain_vmem_loads();
   for (; t < ntiles; t += W) {
     const int m0 = t * TR;
     int z = 0;
@@ -349,7 +364,8 @@ __global__ __launch_bounds__(256, 3) void fwd_kernel(FwdArgs a) {
     load_a(t + W, nx);
     __builtin_amdgcn_sched_barrier(0);
 
-    f32x4 af[KQ];
+    f32x4 afs[KR == 64 ? KQ : 1];
+    f32x4* const af = KR == 64 ? afs : cx;  // (in place at 128: cx is dead after the transform)
 #pragma unroll
     for (int q = 0; q < KQ; ++q) {
       f32x4 v = cx[q];
@@ -369,27 +385,27 @@ __global__ __launch_bounds__(256, 3) void fwd_kernel(FwdArgs a) {
     }
     __builtin_amdgcn_sched_barrier(0);
 
-    f32x16 acc[2];
+    f32x16 acc[NU];
 #pragma unroll
-    for (int u = 0; u < 2; ++u)
+    for (int u = 0; u < NU; ++u)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[u][r] = 0.f;
 #pragma unroll
     for (int q = 0; q < KQ; ++q) {
-      f32x4 bf[2];
+      f32x4 bf[NU];
 #pragma unroll
-      for (int u = 0; u < 2; ++u) bf[u] = ld4(bs + (32 * u + l32) * SKB + 8 * q + 4 * h);
+      for (int u = 0; u < NU; ++u) bf[u] = ld4(bs + (32 * u + l32) * SKB + 8 * q + 4 * h);
 #pragma unroll
       for (int e = 0; e < 4; ++e)
 #pragma unroll
-        for (int u = 0; u < 2; ++u) acc[u] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[q][e], bf[u][e], acc[u], 0, 0, 0);
+        for (int u = 0; u < NU; ++u) acc[u] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[q][e], bf[u][e], acc[u], 0, 0, 0);
     }
     __builtin_amdgcn_sched_barrier(0);
 
     const int mb = m0 + 4 * h;
     const uint32_t eb0 = row_off_bytes(mb, NO, l32), eb1 = eb0 + 16u * NO * 4u;
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < NU; ++u) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int dm = (r & 3) + 8 * (r >> 2);
@@ -409,8 +425,9 @@ __global__ __launch_bounds__(256, 3) void fwd_kernel(FwdArgs a) {
     for (int q = 0; q < KQ; ++q) cx[q] = nx[q];
   }
   if constexpr (!STATS) return;
+  __syncthreads();  // Bs becomes red
 #pragma unroll
-  for (int u = 0; u < 2; ++u) {
+  for (int u = 0; u < NU; ++u) {
     ps[u] += __shfl_xor(ps[u], 32, 64);
     pq[u] += __shfl_xor(pq[u], 32, 64);
     if (h == 0) {
@@ -462,22 +479,24 @@ int dgrad_blocks(int M) {
   return grid_blocks(M, occ);
 }
 
-int fwd_blocks(int M) {
+template <int KR_>
+static int fwd_occ() {
   static int occ = -1;
   if (occ < 0) {
-    const void* fs[] = {reinterpret_cast<const void*>(&fwd_kernel<true, true, true>),
-                        reinterpret_cast<const void*>(&fwd_kernel<true, true, false>),
-                        reinterpret_cast<const void*>(&fwd_kernel<true, false, true>),
-                        reinterpret_cast<const void*>(&fwd_kernel<true, false, false>),
-                        reinterpret_cast<const void*>(&fwd_kernel<false, true, true>),
-                        reinterpret_cast<const void*>(&fwd_kernel<false, true, false>),
-                        reinterpret_cast<const void*>(&fwd_kernel<false, false, true>),
-                        reinterpret_cast<const void*>(&fwd_kernel<false, false, false>)};
+    const void* fs[] = {reinterpret_cast<const void*>(&fwd_kernel<KR_, KR_, true, true, true>),
+                        reinterpret_cast<const void*>(&fwd_kernel<KR_, KR_, true, true, false>),
+                        reinterpret_cast<const void*>(&fwd_kernel<KR_, KR_, true, false, true>),
+                        reinterpret_cast<const void*>(&fwd_kernel<KR_, KR_, true, false, false>),
+                        reinterpret_cast<const void*>(&fwd_kernel<KR_, KR_, false, true, true>),
+                        reinterpret_cast<const void*>(&fwd_kernel<KR_, KR_, false, true, false>),
+                        reinterpret_cast<const void*>(&fwd_kernel<KR_, KR_, false, false, true>),
+                        reinterpret_cast<const void*>(&fwd_kernel<KR_, KR_, false, false, false>)};
     occ = min_occupancy(fs, 8);
   }
-  return grid_blocks(M, occ);
+  return occ;
 }
 
+int fwd_blocks(int M, int KC) { return grid_blocks(M, KC == 128 ? fwd_occ<128>() : fwd_occ<64>()); }
 
 // ---------------------------------------------------------------------------------------
 // dk_pwconv_bwd_bnbwd_f32 at K = C = 64: the whole backward of a stride-1 pointwise layer whose
@@ -580,6 +599,7 @@ __global__ __launch_bounds__(256, 1) void bwd_fused_kernel(BwdArgs ba) {
   };
   f32x4 cg[KQ], cx[KQ];
   load_a(t, cg, cx);
+  drain_vmem_loads();
   for (; t < ntiles; t += W) {
     const int m0 = t * TR;
     int z = 0;
@@ -769,12 +789,22 @@ bool pw_stream_dgrad_ok(int K, int C, int M) {
 
 int pw_stream_dgrad_rows(int M) { return pws::dgrad_blocks(M); }
 
+// K = C = 128 on the streaming forward (tuning knob DORKNET_PW_STREAM128=0: the tiled engine)
+static bool pw_stream128() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("DORKNET_PW_STREAM128");
+    v = (e && e[0] == '0') ? 0 : 1;
+  }
+  return v == 1;
+}
+
 bool pw_stream_fwd_ok(int K, int C, int M, size_t xbytes) {
   if (!pw_stream_enabled()) return false;
-  return K == pws::NO && C == pws::KR && M > 0 && xbytes < ((size_t)1 << 31) &&
-         (size_t)M * 64 * 4 < ((size_t)1 << 31);
+  const bool shape = (K == 64 && C == 64) || (K == 128 && C == 128 && pw_stream128());
+  return shape && M > 0 && xbytes < ((size_t)1 << 31) && (size_t)M * K * 4 < ((size_t)1 << 31);
 }
-int pw_stream_fwd_rows(int M) { return pws::fwd_blocks(M); }
+int pw_stream_fwd_rows(int M, int K) { return pws::fwd_blocks(M, K); }
 
 bool pw_stream_bwd_ok(int K, int C, int M) { return pw_stream_dgrad_ok(K, C, M); }
 int pw_stream_bwd_rows(int M) { return pws::bwd_fused_blocks(M); }
@@ -803,20 +833,26 @@ int pw_stream_bwd_fused(const float* g, const float* bn_x, int M, const float* o
   return launch_status();
 }
 
-int pw_stream_fwd(const float* x, int N, int H, int W, int stride, int OH, int OW, const float* w,
+int pw_stream_fwd(const float* x, int N, int H, int W, int stride, int OH, int OW, const float* w, int KC,
                   const float* bias, float* y, const float* im, const float* iis, const float* ig,
                   const float* ib, int irelu, double* part, hipStream_t st, const FoldTail* ft) {
+  if (KC != 64 && KC != 128) return DK_ERR_ARGS;
   const int M = N * OH * OW;
   pws::FwdArgs a{x, w, bias, y, im, iis, ig, ib, irelu, part, M, H, W, OH, OW, stride,
-                 (uint32_t)((size_t)N * H * W * 64 * 4)};
+                 (uint32_t)((size_t)N * H * W * KC * 4)};
   if (ft && part) a.ft = *ft;
-  const dim3 grid(pws::fwd_blocks(M));
+  const dim3 grid(pws::fwd_blocks(M, KC));
   const bool strided = stride != 1;
-#define DK_FWD(BN_, ST_)                                                                   \
-  if (strided)                                                                             \
-    hipLaunchKernelGGL((pws::fwd_kernel<BN_, ST_, true>), grid, dim3(256), 0, st, a);     \
-  else                                                                                     \
-    hipLaunchKernelGGL((pws::fwd_kernel<BN_, ST_, false>), grid, dim3(256), 0, st, a);
+#define DK_FWD(BN_, ST_)                                                                                \
+  if (KC == 128) {                                                                                      \
+    if (strided)                                                                                        \
+      hipLaunchKernelGGL((pws::fwd_kernel<128, 128, BN_, ST_, true>), grid, dim3(256), 0, st, a);       \
+    else                                                                                                \
+      hipLaunchKernelGGL((pws::fwd_kernel<128, 128, BN_, ST_, false>), grid, dim3(256), 0, st, a);      \
+  } else if (strided)                                                                                   \
+    hipLaunchKernelGGL((pws::fwd_kernel<64, 64, BN_, ST_, true>), grid, dim3(256), 0, st, a);           \
+  else                                                                                                  \
+    hipLaunchKernelGGL((pws::fwd_kernel<64, 64, BN_, ST_, false>), grid, dim3(256), 0, st, a);
   if (im && part) {
     DK_FWD(true, true)
   } else if (im) {

@@ -74,10 +74,11 @@ def test_stream_dgrad_bnbwd_matches_tiled_engine(relu, bn_in, resid, N, H, W):
                                                            (True, 1, False, 1, False, 1, 1, 5),
                                                            (False, 0, False, 2, True, 3, 6, 7),
                                                            (True, 1, True, 2, False, 32, 112, 112)])
-def test_stream_fwd_ex_matches_tiled_engine(bn, relu, stats, stride, bias, N, H, W):
-    """dk_pwconv_fwd_ex_f32 at K = C = 64: y bitwise equal to the tiled engine (BN + ReLU on
-    load, bias, stride-2 subsampling), output statistics to fp64 rounding."""
-    K = C = 64
+@pytest.mark.parametrize("KC", [64, 128])
+def test_stream_fwd_ex_matches_tiled_engine(bn, relu, stats, stride, bias, N, H, W, KC):
+    """dk_pwconv_fwd_ex_f32 at K = C = 64 and 128: y bitwise equal to the tiled engine (BN + ReLU
+    on load, bias, stride-2 subsampling), output statistics to fp64 rounding."""
+    K = C = KC
     rng = np.random.RandomState(int(bn) + 2 * relu + 4 * stats + 8 * stride + N)
     x = nhwc(rng.randn(N, C, H, W) * 2 + 0.3)
     w = torch.as_tensor(rng.randn(K, C).astype(np.float32), device="cuda")
