@@ -572,6 +572,13 @@ __global__ __launch_bounds__(256) void dw_bwd_fused_kernel(const float* __restri
   const int col0 = wl + cl, col1 = wl + CL + cl;
   const bool cok0 = (unsigned)col0 < (unsigned)W, cok1 = two && (unsigned)col1 < (unsigned)W;
   const __amdgpu_buffer_rsrc_t rg = make_rsrc_v(g, bytes), r1 = make_rsrc_v(x1, bytes), rx = make_rsrc_v(x, bytes);
+  // the optional operands as buffers too (an absent one covers 0 bytes: its loads return 0), so
+  // every load of the row loop is an unconditional buffer load and the waitcnt pass keeps the
+  // dx store of a row in flight across the loop's back edge (a branch around a global load made
+  // it wait for everything, stores included, at the end of every row)
+  const __amdgpu_buffer_rsrc_t rres = make_rsrc_v(res, res ? bytes : 0u);
+  const __amdgpu_buffer_rsrc_t rjx = make_rsrc_v(JOIN ? jn.x : nullptr, JOIN ? bytes : 0u);
+  const __amdgpu_buffer_rsrc_t rjm = make_rsrc_v(JOIN ? jn.mask : nullptr, (JOIN && jn.mask) ? bytes / 4u : 0u);
   // the per-channel BatchNorm terms and the (flipped) filters live in LDS, read where used:
   // held in registers they kept the kernel at 2 waves per SIMD, too few to hide a row's loads
   __shared__ f32x4 ptab[13 + RS][32];  // [term][channel group]; CG <= 32 (dwb_cl)
@@ -646,10 +653,10 @@ __global__ __launch_bounds__(256) void dw_bwd_fused_kernel(const float* __restri
   auto load_x_row = [&](int hh) {
     const bool ok = win_ok && hh < H;
     xr = bload4e<float>(rx, ok, pix(hh, w));
-    rv = (res && ok) ? ld4(res + pix(hh, w)) : f32x4{0.f, 0.f, 0.f, 0.f};
+    rv = bload4e<float>(rres, ok, pix(hh, w));
     if constexpr (JOIN) {
-      if (jn.mask) jmv = ok ? *reinterpret_cast<const uint32_t*>(jn.mask + pix(hh, w)) : 0u;  // the 4 mask bytes
-      jxv = ok ? ld4(jn.x + pix(hh, w)) : f32x4{0.f, 0.f, 0.f, 0.f};
+      jmv = __builtin_amdgcn_raw_buffer_load_b32(rjm, (int)(ok ? pix(hh, w) : kOOBBytes), 0, 0);  // 4 mask bytes
+      jxv = bload4e<float>(rjx, ok, pix(hh, w));
     }
   };
   double s1[4] = {0.0, 0.0, 0.0, 0.0}, s2[4] = {0.0, 0.0, 0.0, 0.0};
