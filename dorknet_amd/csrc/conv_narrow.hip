@@ -52,15 +52,18 @@ struct RowStage {
     const bool wok = (int)threadIdx.x < g.Wp && (unsigned)iw < (unsigned)g.W;
     const int voff = wok ? iw * 4 : (int)kOOBBytes;  // lane part of the offset (bytes)
     const int ih0 = ST * oh - g.pad;
+    // rows outside the image read nothing (lane offset past the buffer, scalar offset 0): every
+    // load is unconditional, so the waitcnt pass counts them exactly instead of draining all
+    // memory operations -- the previous row's output stores included -- before the LDS staging
 #pragma unroll
-    for (int c = 0; c < C; ++c)
+    for (int r = 0; r < R; ++r) {
+      const bool rok = (unsigned)(ih0 + r) < (unsigned)g.H;  // uniform
+      const int vo = rok ? voff : (int)kOOBBytes;
 #pragma unroll
-      for (int r = 0; r < R; ++r) {
-        v[c][r] = 0.f;
-        if ((unsigned)(ih0 + r) < (unsigned)g.H)  // uniform: a scalar branch
-          v[c][r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-                                                  rsx, voff, (((n * C + c) * g.H + ih0 + r) * g.W) * 4, 0));
-      }
+      for (int c = 0; c < C; ++c)
+        v[c][r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                rsx, vo, rok ? (((n * C + c) * g.H + ih0 + r) * g.W) * 4 : 0, 0));
+    }
   }
   __device__ __forceinline__ void store(float* xin, const Geo& g) const {
     if ((int)threadIdx.x >= g.Wp) return;
