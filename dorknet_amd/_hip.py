@@ -68,9 +68,19 @@ DK_FOLDED = 10100  # success, and the launch folded the armed BN partials (dk_bn
 
 def _errcheck(result, func, args):
     if result != 0 and result != DK_FOLDED:
+        # a failed entry point may not have taken an in-launch fold armed for it: drop the
+        # arming, or a later partials buffer at the same address would fold into stale outputs
+        disarm_folds()
         what = {DK_ERR_ARGS: "bad arguments", DK_ERR_WORKSPACE: "workspace too small"}.get(result, "hipError")
         raise HipError(f"{func.__name__} failed with status {result} ({what})")
     return result
+
+
+def disarm_folds() -> None:
+    """Drop any in-launch BN fold arming (dk_bn_fold_disarm; thread-local C++ state)."""
+    raw = lib._lib
+    if raw is not None:
+        raw.dk_bn_fold_disarm()
 
 
 class _Lib:

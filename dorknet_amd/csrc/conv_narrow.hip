@@ -176,21 +176,23 @@ template <bool BNDEF, int QC>
 struct DyRow {
   float gq[QC], xq[QC];
   // voff: the lane's byte offset (lg * K + filt) * 4 within a pixel quad, kOOBBytes for a filter
-  // past K.  Pixels past OW (a ragged or padded quad) read the next row (or 0 past the tensor)
-  // and are zeroed by the caller.
+  // past K.  Pixels past OW (a ragged or padded quad) read the next row (or 0 past the tensor:
+  // the whole offset is in the range-checked vector offset) and are zeroed by the caller.
   // voffg: the lane's offset in a lattice g (d.lat == 2: even pixels only, compact -- the
   // pointwise stride-2 layer after the stem hands over its gradient without the zeros of the
   // widen, pointwise_convolution.py:68-72).
   __device__ __forceinline__ void load(const DyIn& d, const Geo& g, int row, int voff, int voffg) {
     const uint32_t bytes = (uint32_t)((size_t)g.rows * g.OW * g.K * 4);
     const __amdgpu_buffer_rsrc_t rx = make_rsrc_v(d.bnx, bytes);
-    const int rbase = row * g.OW * g.K * 4;
+    // the row base goes into the range-checked vector offset (a scalar offset is not checked:
+    // the padded quads of the last row would read past the tensor)
+    const uint32_t rbase = (uint32_t)row * g.OW * g.K * 4;
     const int qstep = 16 * g.K;  // bytes per pixel quad
     if (d.lat == 1) {
       const __amdgpu_buffer_rsrc_t rg = make_rsrc_v(d.g, bytes);
 #pragma unroll
       for (int q = 0; q < QC; ++q)
-        gq[q] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rg, voff + q * qstep, rbase, 0));
+        gq[q] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rg, (int)((uint32_t)voff + rbase + q * qstep), 0, 0));
     } else {
       const int n = row / g.OH, oh = row - n * g.OH;
       const int OHc = (g.OH + 1) / 2, OWc = (g.OW + 1) / 2;
@@ -199,16 +201,16 @@ struct DyRow {
         for (int q = 0; q < QC; ++q) gq[q] = 0.f;
       } else {
         const __amdgpu_buffer_rsrc_t rg = make_rsrc_v(d.g, (uint32_t)((size_t)g.N * OHc * OWc * g.K * 4));
-        const int rb = ((n * OHc + (oh >> 1)) * OWc) * g.K * 4;
+        const uint32_t rb = (uint32_t)((n * OHc + (oh >> 1)) * OWc) * g.K * 4;
 #pragma unroll
         for (int q = 0; q < QC; ++q)
-          gq[q] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rg, voffg + q * (qstep >> 1), rb, 0));
+          gq[q] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rg, (int)((uint32_t)voffg + rb + q * (qstep >> 1)), 0, 0));
       }
     }
     if constexpr (BNDEF) {
 #pragma unroll
       for (int q = 0; q < QC; ++q)
-        xq[q] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rx, voff + q * qstep, rbase, 0));
+        xq[q] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rx, (int)((uint32_t)voff + rbase + q * qstep), 0, 0));
     }
   }
 };

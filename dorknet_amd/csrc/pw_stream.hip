@@ -163,9 +163,9 @@ __global__ __launch_bounds__(256, 2) void dgrad_bnbwd_kernel(DgradArgs a) {
         const uint32_t imm = (uint32_t)(((r & 3) + 8 * ((r >> 2) & 1)) * NO + 32 * u) * 4u;
         const uint32_t eb = r < 8 ? eb0 : eb1;
         if constexpr (PART)
-          exi[u][r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rxi, (int)eb, (int)imm, 0));
+          exi[u][r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rxi, (int)(eb + imm), 0, 0));
         if constexpr (RES)
-          ers[u][r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rr, (int)eb, (int)imm, 0));
+          ers[u][r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rr, (int)(eb + imm), 0, 0));
       }
     f32x4 ng[KQ], nx[KQ];
     load_a(t + W, ng, nx);
@@ -198,7 +198,7 @@ __global__ __launch_bounds__(256, 2) void dgrad_bnbwd_kernel(DgradArgs a) {
       const uint32_t dbase = row_off_bytes(mrow, KR, 4 * h);
 #pragma unroll
       for (int q = 0; q < KQ; ++q)
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, af[q]), rdy, (int)dbase, 32 * q, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, af[q]), rdy, (int)(dbase + 32u * q), 0, 0);
     }
     __builtin_amdgcn_sched_barrier(0);
 
@@ -229,8 +229,7 @@ __global__ __launch_bounds__(256, 2) void dgrad_bnbwd_kernel(DgradArgs a) {
         const uint32_t imm = (uint32_t)(((r & 3) + 8 * ((r >> 2) & 1)) * NO + 32 * u) * 4u;
         float v = acc[u][r];
         if constexpr (RES) v += ers[u][r];
-        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), rdx, (int)(r < 8 ? eb0 : eb1),
-                                              (int)imm, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), rdx, (int)((r < 8 ? eb0 : eb1) + imm), 0, 0);
         if constexpr (PART) {
           const float x = exi[u][r];
           const float xh = (x - pm[u]) * pis[u];
@@ -348,7 +347,7 @@ __global__ __launch_bounds__(256, KR_ == 64 ? 3 : 2) void fwd_kernel(FwdArgs a) 
     const uint32_t base = row_off_bytes(row, KR, 4 * h);
 #pragma unroll
     for (int q = 0; q < KQ; ++q)
-      lx[q] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rx, (int)base, 32 * q, 0));
+      lx[q] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rx, (int)(base + 32u * q), 0, 0));
   };
   f32x4 cx[KQ];
   load_a(t, cx);
@@ -412,8 +411,7 @@ __global__ __launch_bounds__(256, KR_ == 64 ? 3 : 2) void fwd_kernel(FwdArgs a) 
         const uint32_t imm = (uint32_t)(((r & 3) + 8 * ((r >> 2) & 1)) * NO + 32 * u) * 4u;
         float v = acc[u][r];
         if (a.bias) v += bias[u];
-        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), ry, (int)(r < 8 ? eb0 : eb1),
-                                              (int)imm, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), ry, (int)((r < 8 ? eb0 : eb1) + imm), 0, 0);
         if constexpr (STATS) {
           const double d = (mb + dm < a.M) ? (double)v : 0.0;
           ps[u] += d;
@@ -593,8 +591,8 @@ __global__ __launch_bounds__(256, 1) void bwd_fused_kernel(BwdArgs ba) {
     const uint32_t base = row_off_bytes(m, KR, 4 * h);
 #pragma unroll
     for (int q = 0; q < KQ; ++q) {
-      lg[q] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rg, (int)base, 32 * q, 0));
-      lx[q] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rx, (int)base, 32 * q, 0));
+      lg[q] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rg, (int)(base + 32u * q), 0, 0));
+      lx[q] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rx, (int)(base + 32u * q), 0, 0));
     }
   };
   f32x4 cg[KQ], cx[KQ];
@@ -617,9 +615,9 @@ __global__ __launch_bounds__(256, 1) void bwd_fused_kernel(BwdArgs ba) {
       for (int r = 0; r < 16; ++r) {
         const uint32_t imm = (uint32_t)(((r & 3) + 8 * ((r >> 2) & 1)) * NO + 32 * u) * 4u;
         const uint32_t eb = r < 8 ? eb0 : eb1;
-        exi[u][r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rxi, (int)eb, (int)imm, 0));
+        exi[u][r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rxi, (int)(eb + imm), 0, 0));
         if constexpr (RES)
-          ers[u][r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rr, (int)eb, (int)imm, 0));
+          ers[u][r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rr, (int)(eb + imm), 0, 0));
       }
     f32x4 ng[KQ], nx[KQ];
     load_a(t + W, ng, nx);
@@ -693,8 +691,7 @@ __global__ __launch_bounds__(256, 1) void bwd_fused_kernel(BwdArgs ba) {
         const uint32_t imm = (uint32_t)(((r & 3) + 8 * ((r >> 2) & 1)) * NO + 32 * u) * 4u;
         float v = acc[u][r];
         if constexpr (RES) v += ers[u][r];
-        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), rdx, (int)(r < 8 ? eb0 : eb1),
-                                              (int)imm, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), rdx, (int)((r < 8 ? eb0 : eb1) + imm), 0, 0);
         if constexpr (PART) {
           const float x = exi[u][r];
           const float xh = (x - pm[u]) * pis[u];

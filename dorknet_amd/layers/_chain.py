@@ -19,6 +19,7 @@ from __future__ import annotations
 
 import os
 
+from .._hip import disarm_folds
 from ._bn_input import accepts_bn_input
 
 
@@ -119,7 +120,11 @@ def execute(layers, X, test_mode=False, out_accepts=False, keep=(), visit=None):
         if (fuse and not test_mode and mode == "single" and getattr(group[0], "produces_bn_stats", False)
                 and nxt < len(layers) and type(layers[nxt]) is BatchNormLayer):
             req = StatsRequest(layers[nxt])
-        X = run_group(group, mode, X, test_mode, stats_req=req, bn_stats=pending)
+        try:
+            X = run_group(group, mode, X, test_mode, stats_req=req, bn_stats=pending)
+        except BaseException:
+            disarm_folds()  # an arming the failed group left behind must not outlive it
+            raise
         pending = req if req is not None and req.part is not None else None
         steps.append(group)
         i = nxt
@@ -157,6 +162,15 @@ def chain_backward(steps, dy, residual=None, after_step=None, need_input_grad=Tr
     its parameter gradients and None is returned.  `join`: the residual join whose output is
     the chain's input (passed to a first layer that ``accepts_join``); a residual-block step
     likewise receives the previous block's join."""
+    try:
+        dy = _backward_steps(steps, dy, residual, after_step, need_input_grad, join)
+    except BaseException:
+        disarm_folds()  # an arming the failed step left behind must not outlive it
+        raise
+    return dy
+
+
+def _backward_steps(steps, dy, residual, after_step, need_input_grad, join):
     from ._bn_input import accepts_bn_grad, add_residual
     from .batch_norm import BatchNormLayer
     last = len(steps) - 1

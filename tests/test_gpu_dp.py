@@ -20,7 +20,7 @@ import numpy as np
 import pytest
 import torch
 
-from tests._convert import all_layers, network_to_oracle, rel_err
+from tests._convert import all_layers, network_to_oracle, rel_err, slack_bound
 
 pytestmark = pytest.mark.gpu
 
@@ -43,8 +43,7 @@ def _grads(net):
 def _excess(got, want64, want32, tol=1e-4):
     got = np.asarray(got, dtype=np.float64)
     err = np.linalg.norm((got - want64).ravel())
-    bound = max(tol * np.linalg.norm(want64.ravel()),
-                10 * np.linalg.norm((np.asarray(want32, np.float64) - want64).ravel()))
+    bound = slack_bound(want64, want32, tol)
     return 0.0 if err == 0 else err / max(bound, 1e-300)
 
 

@@ -23,7 +23,7 @@ import numpy as np
 import pytest
 import torch
 
-from tests._convert import all_layers, rel_err
+from tests._convert import all_layers, log_slack, rel_err, slack_bound
 from tests._torch_twin import TorchTwin
 
 pytestmark = pytest.mark.gpu
@@ -78,7 +78,7 @@ def _run(layers, X, dY, input_grad):
 
 def _bound(w, w32, extra=0.0):
     w = np.asarray(w, np.float64)
-    return max(TOL * np.linalg.norm(w.ravel()), 10 * np.linalg.norm((np.asarray(w32) - w).ravel()), extra)
+    return max(TOL * np.linalg.norm(w.ravel()), slack_bound(w, w32, 0.0), extra)
 
 
 def _check(got, want, fp32, twin, layers):
@@ -97,6 +97,7 @@ def _check(got, want, fp32, twin, layers):
         err = np.linalg.norm((g - w).ravel())
         extra = 1e-6 * float(torch.linalg.norm(twin.bn_l1[name])) if name in twin.bn_l1 else 0.0
         bound = _bound(w, g32[(name, k)].reshape(w.shape), extra)
+        log_slack("fullsize {} {}".format(name, k), err, w, g32[(name, k)].reshape(w.shape))
         errs[(name, k)] = (rel_err(g, w), rel_err(g32[(name, k)].reshape(w.shape), w))
         if err > bound:
             bad.append((name, k, err, bound, rel_err(g, w)))

@@ -4,7 +4,7 @@ import pytest
 import torch
 
 from oracle import net as O
-from tests._convert import all_layers, network_to_oracle, rel_err
+from tests._convert import all_layers, network_to_oracle, log_slack, rel_err, slack_bound
 
 pytestmark = pytest.mark.gpu
 
@@ -18,13 +18,13 @@ def host(t):
 
 
 def _excess(got, want64, want32, tol):
-    """err / bound with bound = max(tol * ||want64||, 10 * ||want32 - want64||) (see
+    """err / bound with bound = max(tol * ||want64||, FP32_SLACK * ||want32 - want64||) (see
     test_gpu_layers.check): <= 1 passes."""
     got = np.asarray(got, dtype=np.float64)
     want64 = np.asarray(want64, dtype=np.float64)
     err = np.linalg.norm((got - want64).ravel())
-    bound = max(tol * np.linalg.norm(want64.ravel()),
-                10 * np.linalg.norm((np.asarray(want32, dtype=np.float64) - want64).ravel()))
+    bound = slack_bound(want64, want32, tol)
+    log_slack("network", err, want64, want32)
     return 0.0 if err == 0 else err / max(bound, 1e-300)
 
 

@@ -106,3 +106,85 @@ def test_stream_fwd_ex_matches_tiled_engine(bn, relu, stats, stride, bias, N, H,
     if stats:
         s0, s1 = p0.sum(0), p1.sum(0)
         assert float((s1 - s0).norm() / s0.norm()) < 1e-12
+
+
+def carve(shape, rng, tail=4096, fill=None):
+    """An NHWC tensor of `shape` (N, C, H, W) at the start of a larger buffer whose `tail` floats
+    after it hold a sentinel: returns (view, whole buffer, number of leading floats)."""
+    N, C, H, W = shape
+    n = N * C * H * W
+    buf = torch.full((n + tail,), float("nan") if fill is None else 0.0, device="cuda")
+    if fill is not None:
+        buf[:n] = torch.as_tensor(np.ascontiguousarray(fill(N, H, W, C), dtype=np.float32).ravel(), device="cuda")
+    buf[n:] = 12345.0
+    view = buf[:n].view(N, H, W, C).permute(0, 3, 1, 2)  # NCHW logical, NHWC bytes
+    return view, buf, n
+
+
+def tail_ok(buf, n):
+    return bool((buf[n:] == 12345.0).all())
+
+
+@pytest.mark.parametrize("N,H,W", [(3, 13, 11), (1, 5, 7), (2, 9, 9)])
+def test_stream_kernels_ragged_tail_untouched(N, H, W):
+    """M = N*H*W not a multiple of 32: the streaming kernels' ragged last tile must neither write
+    past y / dx / dy nor let rows past M reach the results (row offsets live in the
+    range-checked vector offset of every buffer access).  Operands are carved from the start of
+    larger buffers whose tails hold a sentinel; outputs must match the exactly-sized run."""
+    assert (N * H * W) % 32
+    K = C = 64
+    rng = np.random.RandomState(N * 100 + H)
+    nh = lambda N_, H_, W_, C_: rng.randn(N_, H_, W_, C_)  # noqa: E731
+    st = stream_handle()
+    # forward (BN on load, statistics)
+    x, xb, xn = carve((N, C, H, W), rng, fill=nh)
+    w = torch.as_tensor(rng.randn(K, C).astype(np.float32), device="cuda")
+    pi = bn_params(C, rng)
+    y, yb, yn = carve((N, K, H, W), rng)
+    rows = lib.dk_pwconv_fwd_stats_rows(N, H, W, K, C)
+    part = torch.zeros((rows, 2, K), dtype=torch.float64, device="cuda")
+    assert lib.dk_pwconv_fwd_ex_f32(x.data_ptr(), N, H, W, C, w.data_ptr(), K, 1, 0, y.data_ptr(), H, W,
+                                    *(t.data_ptr() for t in pi), 1, part.data_ptr(), st) == 0
+    y_exact = torch.full((N, K, H, W), float("nan"), device="cuda").contiguous(memory_format=torch.channels_last)
+    part2 = torch.zeros_like(part)
+    xc = x.contiguous(memory_format=torch.channels_last)
+    assert lib.dk_pwconv_fwd_ex_f32(xc.data_ptr(), N, H, W, C, w.data_ptr(), K, 1, 0, y_exact.data_ptr(), H, W,
+                                    *(t.data_ptr() for t in pi), 1, part2.data_ptr(), st) == 0
+    torch.cuda.synchronize()
+    assert tail_ok(yb, yn)
+    assert torch.equal(y, y_exact)
+    assert torch.equal(part, part2)
+
+    # dgrad with BN backward on load (dy written through, residual, input partials)
+    xo, _, _ = carve((N, K, H, W), rng, fill=nh)
+    g, _, _ = carve((N, K, H, W), rng, fill=nh)
+    po = bn_params(K, rng)
+    k12 = torch.as_tensor(rng.randn(2 * K).astype(np.float32) * 0.1, device="cuda")
+    res, _, _ = carve((N, C, H, W), rng, fill=nh)
+    dy, dyb, dyn = carve((N, K, H, W), rng)
+    dx, dxb, dxn = carve((N, C, H, W), rng)
+    rows = lib.dk_pwconv_dgrad_bnbwd_stats_rows(N, H, W, K, C)
+    part = torch.zeros((rows, 2, C), dtype=torch.float64, device="cuda")
+    assert lib.dk_pwconv_dgrad_bnbwd_f32(g.data_ptr(), xo.data_ptr(), N, H, W, K, *(t.data_ptr() for t in po), 1,
+                                         k12.data_ptr(), dy.data_ptr(), w.data_ptr(), C, dx.data_ptr(),
+                                         res.data_ptr(), x.data_ptr(), *(t.data_ptr() for t in pi), 1,
+                                         part.data_ptr(), st) == 0
+    torch.cuda.synchronize()
+    assert tail_ok(dyb, dyn) and tail_ok(dxb, dxn)
+    assert bool(torch.isfinite(dx).all()) and bool(torch.isfinite(part).all())
+
+    # fused backward (dgrad + wgrad)
+    dx2, dx2b, dx2n = carve((N, C, H, W), rng)
+    dw = torch.full_like(w, float("nan"))
+    rows = lib.dk_pwconv_bwd_fused_rows(N, H, W, K, C)
+    part = torch.zeros((rows, 2, C), dtype=torch.float64, device="cuda")
+    from dorknet_amd._hip import workspace
+    nb = lib.dk_pwconv_bwd_fused_workspace_bytes(N, H, W, K, C)
+    assert lib.dk_pwconv_bwd_bnbwd_f32(g.data_ptr(), xo.data_ptr(), N, H, W, K, *(t.data_ptr() for t in po), 1,
+                                       k12.data_ptr(), w.data_ptr(), C, 0.0, dw.data_ptr(), dx2.data_ptr(),
+                                       res.data_ptr(), x.data_ptr(), *(t.data_ptr() for t in pi), 1,
+                                       part.data_ptr(), workspace.get(nb), nb, st) == 0
+    torch.cuda.synchronize()
+    assert tail_ok(dx2b, dx2n)
+    assert torch.equal(dx, dx2)
+    assert bool(torch.isfinite(dw).all())
