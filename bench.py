@@ -96,13 +96,31 @@ class Instrument:
             ms = [a.elapsed_time(b) for a, b, _ in calls]
             fl, by = 0, 0
             bound = 0.0
-            for _, _, args in calls:
+            shapes = {}  # (flops, bytes) of a call -> [calls, ms]: the entry's distinct shapes
+            for (_, _, args), t in zip(calls, ms):
                 f, b = perfmodel.work(n, args)
                 fl += f
                 by += b
-                bound += perfmodel.bound_time_s(f, b)
-            out[n] = dict(calls=len(calls), ms=sum(ms), flops=fl, bytes=by, bound_ms=1e3 * bound)
+                bound += perfmodel.bound_time_s(f, b, n)
+                sh = shapes.setdefault((f, b), [0, 0.0])
+                sh[0] += 1
+                sh[1] += t
+            out[n] = dict(calls=len(calls), ms=sum(ms), flops=fl, bytes=by, bound_ms=1e3 * bound, shapes=shapes)
         return out
+
+
+def shape_bounds(name, s):
+    """Each distinct call shape of an entry with its own bound (HBM or MFMA) and its fraction of
+    that bound, largest time first."""
+    from dorknet_amd import perfmodel
+    rows = []
+    for (f, b), (n, ms) in sorted(s.get("shapes", {}).items(), key=lambda kv: -kv[1][1]):
+        t = ms / 1e3 / n
+        mf = perfmodel.is_mfma_bound(f, b, name)
+        rows.append({"calls": n, "avg_call_us": round(1e6 * t, 2), "flops": int(f), "bytes": int(b),
+                     "bound": "mfma" if mf else "hbm",
+                     "frac": round(perfmodel.bound_time_s(f, b, name) / t, 4)})
+    return rows
 
 
 def roofline_entry(name, s, steps):
@@ -110,15 +128,17 @@ def roofline_entry(name, s, steps):
     t = s["ms"] / 1e3 / s["calls"]
     flops = s["flops"] / s["calls"]
     nbytes = s["bytes"] / s["calls"]
-    mfma = flops / (perfmodel.PEAK_F32_TFLOPS * 1e12) > nbytes / (perfmodel.PEAK_HBM_GBS * 1e9)
+    mfma = perfmodel.is_mfma_bound(flops, nbytes, name)
     if mfma:
-        achieved, peak, unit = flops / t / 1e12, perfmodel.PEAK_F32_TFLOPS, "TFLOP/s"
+        achieved, peak, unit = flops / t / 1e12, perfmodel.peak_tflops(name), "TFLOP/s"
     else:
         achieved, peak, unit = nbytes / t / 1e9, perfmodel.PEAK_HBM_GBS, "GB/s"
     return {"kernel": name, "bound": "mfma" if mfma else "hbm", "achieved": round(achieved, 2), "peak": peak,
             "unit": unit, "frac": round(achieved / peak, 4), "traffic": None,
             "calls_per_step": s["calls"] // max(steps, 1), "avg_call_us": round(1e6 * t, 2),
-            "algorithmic_per_call": {"flops": int(flops), "bytes": int(nbytes)}}
+            "algorithmic_per_call": {"flops": int(flops), "bytes": int(nbytes)},
+            # the averaged label above hides shapes with different bounds: each shape on its own
+            "by_shape": shape_bounds(name, s)}
 
 
 # The kernel each single-kernel entry point launches (for the PMC traffic lookup).
@@ -312,7 +332,8 @@ def other_config(args):
             sgd.update_weights()
         flops = None
         unit, metric = "images/s", "images/sec training step, MobileNet-style dw+pw stack bs=512 bf16, 1 MI355X"
-        dtype, workload = "bf16 storage / fp32 arithmetic", "16 depthwise-separable units (dw3x3-BN-pw-BN-ReLU), " \
+        dtype, workload = "bf16 (activations stored bf16; pointwise GEMMs on bf16 MFMA with fp32 accumulation; " \
+            "depthwise, BatchNorm and weights fp32)", "16 depthwise-separable units (dw3x3-BN-pw-BN-ReLU), " \
             "ResNet-18-depsep schedule, 64x56x56 input, fwd + bwd (given output gradient) + SGD-momentum, " \
             "BASELINE config 5"
     for _ in range(args.warmup):

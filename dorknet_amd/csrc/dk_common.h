@@ -35,6 +35,7 @@ __device__ __forceinline__ void st4(float* p, f32x4 v) { *reinterpret_cast<f32x4
 // in fp32 -- loads widen (exact), stores round to nearest even (v_cvt_pk_bf16_f32).
 typedef uint16_t bf16_t;
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));  // a v_mfma_f32_*_bf16 operand fragment
 __device__ __forceinline__ f32x4 bf16x4_to_f32(uint2 u) {
   return __builtin_convertvector(__builtin_bit_cast(bf16x4, u), f32x4);
 }

@@ -1,4 +1,6 @@
-// Implicit-GEMM engine on fp32 MFMA (v_mfma_f32_32x32x2_f32) for gfx950.
+// Implicit-GEMM engine for gfx950: fp32 MFMA (v_mfma_f32_32x32x2_f32), and a bf16 MFMA mode
+// (v_mfma_f32_32x32x16_bf16, operands rounded to bf16 as they are staged; BASELINE config 5).
+// The entry points live in gemm_conv.hip, gemm_pw.hip, gemm_dense.hip and gemm_bf16.hip.
 //
 // Every dense contraction on the hot path is one instance of
 //     C[m][n] (+)= sum_k  A(m, k) * B(n, k)
@@ -26,7 +28,10 @@
 // row-contiguous (wgrad operands) is kept [BK][rows] and read with ds_read_b32.  Because
 // the MFMA sums over k in any order, the four MFMAs of a q-block use k = 8q + 4h + t
 // (h = lane half, t = 0..3) on both operands.
+#pragma once
 #include <stdlib.h>
+
+#include <type_traits>
 
 #include "dk_common.h"
 #include "fold_tail.h"
@@ -128,22 +133,56 @@ struct MatBwdDesc : MatDescE<float> {
 // 8q + 4h + {0,1,2,3} of `row` for the MFMA loop.
 // ----------------------------------------------------------------------------
 
+// LDS element type TT: float (the f32 MFMA engine) or bf16_t (the bf16 MFMA engine, BASELINE
+// config 5: operands rounded to bf16 as they are staged).  Row strides per element type:
+//   KC fp32: BK+4 floats, (BK+4)/4 odd -> conflict-free ds_read_b128;
+//   KC bf16: BK+8 elements = an odd multiple of 16 bytes -> the 16 rows of a ds_read_b128 lane group
+//            start on 16 distinct 4-bank groups;
+//   IC bf16: a row stride of an odd multiple of 64 bytes -> the 4 k-rows of each 32-lane half of
+//            a ds_read_b64_tr_b16 fall on 4 distinct 16-bank groups (MI355X_MICROARCH.md LDS).
 template <int ROWS, int BK>
 struct KCLayout {
+  static constexpr bool kIC = false;
   static constexpr int SK = BK + 4;  // row stride in floats: (BK+4)/4 odd -> conflict-free b128 reads
   static constexpr int BUF = ROWS * SK;
+  static constexpr int SKH = BK + 8;  // bf16 row stride (elements)
+  static constexpr int BUFH = ROWS * SKH;
+  template <class TT>
+  __device__ static constexpr int stride() { return sizeof(TT) == 4 ? SK : SKH; }
   __device__ static __forceinline__ f32x4 frag(const float* T, int row, int q, int h) {
     return ld4(T + row * SK + 8 * q + 4 * h);
+  }
+  // bf16 operand of v_mfma_f32_32x32x16_bf16, k-step s: k = 16s + 8h + j, j = 0..7 of `row`
+  __device__ static __forceinline__ bf16x8 fragh(const bf16_t* T, int row, int s, int h) {
+    return *reinterpret_cast<const bf16x8*>(T + row * SKH + 16 * s + 8 * h);
   }
 };
 
 template <int ROWS, int BK>
 struct ICLayout {
+  static constexpr bool kIC = true;
   static constexpr int S = ROWS;
   static constexpr int BUF = BK * ROWS;
+  static constexpr int SH = 2 * ((ROWS / 2 + 15) / 32 * 32 + 16);  // bf16 row stride: 2*(16 mod 32) elements
+  static constexpr int BUFH = BK * SH;
+  template <class TT>
+  __device__ static constexpr int stride() { return sizeof(TT) == 4 ? S : SH; }
   __device__ static __forceinline__ f32x4 frag(const float* T, int row, int q, int h) {
     const float* p = T + (8 * q + 4 * h) * S + row;
     return f32x4{p[0], p[S], p[2 * S], p[3 * S]};
+  }
+  // bf16 operand, k-step s: the 8 k-rows 16s + 8h .. +7 of column `row`, gathered by two
+  // ds_read_b64_tr_b16 (each delivers 4 k-rows of 16 consecutive columns to a 16-lane group:
+  // lane 4q+p supplies the address of k-row q, columns 4p..4p+3 of its group's block).
+  // row0: the 32-column tile's first column (row = row0 + lane & 31).
+  __device__ static __forceinline__ bf16x8 fragh(const bf16_t* T, int row0, int s, int h, int lane) {
+    const int i = lane & 15, g = (lane >> 4) & 1;
+    const bf16_t* p = T + (16 * s + 8 * h + (i >> 2)) * SH + row0 + 16 * g + 4 * (i & 3);
+    typedef short s16x4 __attribute__((ext_vector_type(4)));
+    typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p));
+    const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p + 4 * SH));
+    return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
   }
 };
 
@@ -221,8 +260,8 @@ struct LdImgKC : KCLayout<ROWS, BK> {
     }
   }
 
-  template <class D>
-  __device__ __forceinline__ void store(float* T) const {
+  template <class D, class TT>
+  __device__ __forceinline__ void store(TT* T) const {
     if (!active) return;
 #pragma unroll
     for (int j = 0; j < NR; ++j) {
@@ -232,7 +271,7 @@ struct LdImgKC : KCLayout<ROWS, BK> {
         const f32x4 t = bn_in4(o, ld4(tb), ld4(tb + tc), ld4(tb + 2 * tc), ld4(tb + 3 * tc), relu);
         if ((okm >> j) & 1u) o = t;
       }
-      st4(T + (rb + j * RSTEP) * L::SK + 4 * kq, o);
+      st4(T + (rb + j * RSTEP) * L::template stride<TT>() + 4 * kq, o);
     }
   }
 };
@@ -299,8 +338,8 @@ struct LdMatKCT : KCLayout<ROWS, BK> {
     }
   }
 
-  template <class D>
-  __device__ __forceinline__ void store(float* T) {
+  template <class D, class TT>
+  __device__ __forceinline__ void store(TT* T) {
     if (!active) return;
     if constexpr (D::kBnBwd) {
       if (okm) {
@@ -325,7 +364,7 @@ struct LdMatKCT : KCLayout<ROWS, BK> {
       }
     }
 #pragma unroll
-    for (int j = 0; j < NR; ++j) st4(T + (rb + j * RSTEP) * L::SK + 4 * kq, v[j]);
+    for (int j = 0; j < NR; ++j) st4(T + (rb + j * RSTEP) * L::template stride<TT>() + 4 * kq, v[j]);
   }
   int relu_flag = 0;
 };
@@ -389,8 +428,8 @@ struct LdMatICT : ICLayout<ROWS, BK> {
     if constexpr (D::kBnBwd) okm = om;
   }
 
-  template <class D>
-  __device__ __forceinline__ void store(float* T) {
+  template <class D, class TT>
+  __device__ __forceinline__ void store(TT* T) {
     if (!active) return;
     if constexpr (D::kBnBwd) {
       if (okm) {
@@ -415,7 +454,7 @@ struct LdMatICT : ICLayout<ROWS, BK> {
       }
     }
 #pragma unroll
-    for (int j = 0; j < NK; ++j) st4(T + (kb + j * KSTEP) * L::S + 4 * iq, v[j]);
+    for (int j = 0; j < NK; ++j) st4(T + (kb + j * KSTEP) * L::template stride<TT>() + 4 * iq, v[j]);
   }
 };
 template <int ROWS, int BK, int NT>
@@ -483,8 +522,8 @@ struct LdImgIC : ICLayout<ROWS, BK> {
     if constexpr (D::kBnIn) okm = om;
   }
 
-  template <class D>
-  __device__ __forceinline__ void store(float* T) const {
+  template <class D, class TT>
+  __device__ __forceinline__ void store(TT* T) const {
     if (!active) return;
 #pragma unroll
     for (int j = 0; j < NK; ++j) {
@@ -492,7 +531,7 @@ struct LdImgIC : ICLayout<ROWS, BK> {
       if constexpr (D::kBnIn) {
         if ((okm >> j) & 1u) o = bn_in4(o, bm, bi, bg, bb, relu);
       }
-      st4(T + (kb + j * KSTEP) * L::S + 4 * iq, o);
+      st4(T + (kb + j * KSTEP) * L::template stride<TT>() + 4 * iq, o);
     }
   }
 };
@@ -744,24 +783,41 @@ struct EpPhase {
 // The kernel
 // ----------------------------------------------------------------------------
 
-template <int BM, int BN, int BK, int WM, int WN, class LA, class DA, class LB, class DB, class EP>
+// The bf16 operand fragment of a loader's layout (KC: one ds_read_b128; IC: two transposing
+// ds_read_b64_tr_b16 of the 32-column tile starting at row - lane & 31).
+template <class L>
+__device__ __forceinline__ bf16x8 frag_h(const bf16_t* T, int row, int s, int h, int lane) {
+  if constexpr (L::kIC)
+    return L::fragh(T, row - (lane & 31), s, h, lane);
+  else
+    return L::fragh(T, row, s, h);
+}
+
+// MF: the MFMA the operands feed -- kMfF32 (v_mfma_f32_32x32x2_f32 on fp32 LDS tiles, exact fp32)
+// or kMfBf16 (v_mfma_f32_32x32x16_bf16 on bf16 LDS tiles: each operand element rounded to bf16
+// (RNE) as it is staged, products exact, fp32 accumulation; BASELINE config 5's bf16 path).
+enum : int { kMfF32 = 0, kMfBf16 = 1 };
+
+template <int BM, int BN, int BK, int WM, int WN, class LA, class DA, class LB, class DB, class EP, int MF = kMfF32>
 __global__ __launch_bounds__(64 * WM * WN) void igemm_f32(DA da, DB db, EP ep, int M, int N, int Ktot,
                                                            int kt_per_split) {
   constexpr int TM = BM / (32 * WM);
   constexpr int TN = BN / (32 * WN);
+  constexpr bool H = MF == kMfBf16;
   static_assert(TM >= 1 && TN >= 1 && BM == 32 * WM * TM && BN == 32 * WN * TN, "tile");
-  static_assert(BK % 8 == 0, "BK");
-  constexpr int ABUF = LA::BUF, BBUF = LB::BUF;
+  static_assert(BK % (H ? 16 : 8) == 0, "BK");
+  using TT = typename std::conditional<H, bf16_t, float>::type;  // LDS operand element
+  constexpr int ABUF = H ? LA::BUFH : LA::BUF, BBUF = H ? LB::BUFH : LB::BUF;  // elements
   // operand double buffers; the epilogue reuses the same LDS for the staged C tile
-  // ([BM][BN+8]) and, with kColStats, the fp64 column-sum scratch
-  constexpr int SMEM_OPS = 2 * (ABUF + BBUF);
+  // ([BM][BN+8]) and, with kColStats, the fp64 column-sum scratch (sizes in floats)
+  constexpr int SMEM_OPS = (2 * (ABUF + BBUF) * (int)sizeof(TT) + 3) / 4;
   constexpr int SMEM_EPI = BM * (BN + 8);
   constexpr int SMEM_RED = EP::kColStats ? (64 * WM * WN / (BN / 4)) * BN * 4 : 0;
   constexpr int SMEM = SMEM_OPS > SMEM_EPI ? (SMEM_OPS > SMEM_RED ? SMEM_OPS : SMEM_RED)
                                            : (SMEM_EPI > SMEM_RED ? SMEM_EPI : SMEM_RED);
   __shared__ __attribute__((aligned(16))) float smem[SMEM];
-  float* const As = smem;
-  float* const Bs = smem + 2 * ABUF;
+  TT* const As = reinterpret_cast<TT*>(smem);
+  TT* const Bs = As + 2 * ABUF;
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -845,22 +901,38 @@ __global__ __launch_bounds__(64 * WM * WN) void igemm_f32(DA da, DB db, EP ep, i
         la.load(da, (kt + 1) * BK, Ktot);
         lb.load(db, (kt + 1) * BK, Ktot);
       }
-      const float* A_t = As + cur * ABUF;
-      const float* B_t = Bs + cur * BBUF;
+      const TT* A_t = As + cur * ABUF;
+      const TT* B_t = Bs + cur * BBUF;
+      if constexpr (H) {
 #pragma unroll
-      for (int q = 0; q < BK / 8; ++q) {
-        f32x4 af[TM], bf[TN];
+        for (int s = 0; s < BK / 16; ++s) {
+          bf16x8 af[TM], bf[TN];
 #pragma unroll
-        for (int t = 0; t < TM; ++t) af[t] = LA::frag(A_t, arow + 32 * t, q, h);
+          for (int t = 0; t < TM; ++t) af[t] = frag_h<LA>(A_t, arow + 32 * t, s, h, lane);
 #pragma unroll
-        for (int u = 0; u < TN; ++u) bf[u] = LB::frag(B_t, brow + 32 * u, q, h);
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
+          for (int u = 0; u < TN; ++u) bf[u] = frag_h<LB>(B_t, brow + 32 * u, s, h, lane);
 #pragma unroll
           for (int t = 0; t < TM; ++t)
 #pragma unroll
             for (int u = 0; u < TN; ++u)
-              acc[t][u] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[t][e], bf[u][e], acc[t][u], 0, 0, 0);
+              acc[t][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[t], bf[u], acc[t][u], 0, 0, 0);
+        }
+      } else {
+#pragma unroll
+        for (int q = 0; q < BK / 8; ++q) {
+          f32x4 af[TM], bf[TN];
+#pragma unroll
+          for (int t = 0; t < TM; ++t) af[t] = LA::frag(A_t, arow + 32 * t, q, h);
+#pragma unroll
+          for (int u = 0; u < TN; ++u) bf[u] = LB::frag(B_t, brow + 32 * u, q, h);
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+#pragma unroll
+            for (int t = 0; t < TM; ++t)
+#pragma unroll
+              for (int u = 0; u < TN; ++u)
+                acc[t][u] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[t][e], bf[u][e], acc[t][u], 0, 0, 0);
+        }
       }
       if (more) {
         la.template store<DA>(As + (cur ^ 1) * ABUF);
@@ -1010,16 +1082,16 @@ static const TileCfg kSplitCfg[] = {DK_SPLITK_CONFIGS(DK_CFG_ENTRY)};
 static const int kNumRowCfg = sizeof(kRowCfg) / sizeof(kRowCfg[0]);
 static const int kNumSplitCfg = sizeof(kSplitCfg) / sizeof(kSplitCfg[0]);
 
-static int g_cfg_override[2] = {-1, -1};  // tuning knob only (see header)
+extern int g_cfg_override[2];  // tuning knobs only (dk_debug_set_gemm_config, gemm_conv.hip)
 // Split-K grids fill the resident block slots once (g_fill_splits; tuning knob
 // dk_debug_set_gemm_config(2, 0/1)).  A persistent tile loop for the row problems was measured
 // and dropped (scripts/ab_step.py: 11.77 ms/step with one block per tile, 11.89 / 11.98 with
 // 1 / 2 resident waves of persistent blocks, and the loop slowed the one-tile case too).
-static int g_fill_splits = 1;
+extern int g_fill_splits;
 constexpr int kNumCUs = 256;  // MI355X
 
 template <int BM, int BN, int BK, int WM, int WN, template <int, int, int> class LA, class DA,
-          template <int, int, int> class LB, class DB, class EP>
+          template <int, int, int> class LB, class DB, class EP, int MF = kMfF32>
 static int launch_igemm(const DA& da, const DB& db, const EP& ep, int M, int N, int Ktot, int splits,
                         hipStream_t st,
                         int* splits_used = nullptr) {
@@ -1033,12 +1105,12 @@ static int launch_igemm(const DA& da, const DB& db, const EP& ep, int M, int N, 
   size_t dyn = 0;
   if constexpr (DA::kBnIn && A::kTable) {
     dyn = (size_t)da.C * sizeof(f32x4);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&igemm_f32<BM, BN, BK, WM, WN, A, DA, B, DB, EP>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&igemm_f32<BM, BN, BK, WM, WN, A, DA, B, DB, EP, MF>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn);
   }
   if constexpr (DA::kBnBwd) {
     dyn = (size_t)da.bwd.C * 2 * sizeof(f32x4);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&igemm_f32<BM, BN, BK, WM, WN, A, DA, B, DB, EP>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&igemm_f32<BM, BN, BK, WM, WN, A, DA, B, DB, EP, MF>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn);
   }
   // resident blocks per CU of this instantiation (queried once; immutable afterwards)
@@ -1046,7 +1118,7 @@ static int launch_igemm(const DA& da, const DB& db, const EP& ep, int M, int N, 
   if (occ < 0) {
     int o = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            &o, reinterpret_cast<const void*>(&igemm_f32<BM, BN, BK, WM, WN, A, DA, B, DB, EP>), NT, dyn) !=
+            &o, reinterpret_cast<const void*>(&igemm_f32<BM, BN, BK, WM, WN, A, DA, B, DB, EP, MF>), NT, dyn) !=
             hipSuccess || o < 1)
       o = 1;
     occ = o;
@@ -1065,11 +1137,11 @@ static int launch_igemm(const DA& da, const DB& db, const EP& ep, int M, int N, 
     // channel slice per N tile
     EP e = ep;
     if (!e.part || splits != 1 || !fold_take(e.part, cdiv(M, BM), N, cdiv(N, BN), &e.ft)) e.ft.part = nullptr;
-    hipLaunchKernelGGL((igemm_f32<BM, BN, BK, WM, WN, A, DA, B, DB, EP>), dim3(tiles, splits), dim3(NT), dyn, st, da,
+    hipLaunchKernelGGL((igemm_f32<BM, BN, BK, WM, WN, A, DA, B, DB, EP, MF>), dim3(tiles, splits), dim3(NT), dyn, st, da,
                        db, e, M, N, Ktot, kps);
     return fold_status(launch_status(), e.ft);
   }
-  hipLaunchKernelGGL((igemm_f32<BM, BN, BK, WM, WN, A, DA, B, DB, EP>), dim3(tiles, splits), dim3(NT), dyn, st, da,
+  hipLaunchKernelGGL((igemm_f32<BM, BN, BK, WM, WN, A, DA, B, DB, EP, MF>), dim3(tiles, splits), dim3(NT), dyn, st, da,
                      db, ep, M, N, Ktot, kps);
   return launch_status();
 }
@@ -1079,7 +1151,7 @@ static int launch_igemm(const DA& da, const DB& db, const EP& ep, int M, int N, 
 // tile -- wide column tiles amortise it.
 enum : int { kRowPlain = 0, kRowBnBwd = 1, kRowConv = 2 };  // kRowConv: R x S > 1 image forward
 
-static int row_config(int M, int N, int K, int kind = kRowPlain) {
+static inline int row_config(int M, int N, int K, int kind = kRowPlain) {
   if (g_cfg_override[0] >= 0) return g_cfg_override[0];
   (void)M;
   if (kind == kRowBnBwd) {
@@ -1099,12 +1171,12 @@ static int row_config(int M, int N, int K, int kind = kRowPlain) {
 
 // Output-stationary problems (fwd / dgrad).
 template <template <int, int, int> class LA, class DA, template <int, int, int> class LB, class DB, class EP,
-          int KIND = kRowPlain>
+          int KIND = kRowPlain, int MF = kMfF32>
 static int igemm_rows(const DA& da, const DB& db, const EP& ep, int M, int N, int Ktot, hipStream_t st) {
   switch (row_config(M, N, Ktot, KIND)) {
 #define DK_CASE(id, bm, bn, bk, wm, wn) \
   case id:                              \
-    return launch_igemm<bm, bn, bk, wm, wn, LA, DA, LB, DB, EP>(da, db, ep, M, N, Ktot, 1, st);
+    return launch_igemm<bm, bn, bk, wm, wn, LA, DA, LB, DB, EP, MF>(da, db, ep, M, N, Ktot, 1, st);
     DK_ROW_CONFIGS(DK_CASE)
 #undef DK_CASE
     default:
@@ -1113,7 +1185,7 @@ static int igemm_rows(const DA& da, const DB& db, const EP& ep, int M, int N, in
 }
 
 // Reduction-heavy problems (wgrad): split K over enough blocks to fill the chip.
-static int splitk_config(int M, int N, int Kred) {
+static inline int splitk_config(int M, int N, int Kred) {
   if (g_cfg_override[1] >= 0) return g_cfg_override[1];
   (void)Kred;
   // Wide column tiles when M <= 64 < N: the A operand (for the stem the BN-backward-on-load dy,
@@ -1124,7 +1196,7 @@ static int splitk_config(int M, int N, int Kred) {
 }
 
 // Blocks a split-K weight gradient aims for (tuning knob DORKNET_WGRAD_BLOCKS, read once).
-static int wgrad_target_blocks() {
+static inline int wgrad_target_blocks() {
   static int v = -1;
   if (v < 0) {
     const char* s = getenv("DORKNET_WGRAD_BLOCKS");
@@ -1133,7 +1205,7 @@ static int wgrad_target_blocks() {
   return v;
 }
 
-static int wgrad_splits(int M, int N, int Kred, const TileCfg& c) {
+static inline int wgrad_splits(int M, int N, int Kred, const TileCfg& c) {
   const int tiles = cdiv(M, c.BM) * cdiv(N, c.BN);
   const int KT = cdiv(Kred, c.BK);
   int splits = cdiv(wgrad_target_blocks(), tiles);
@@ -1143,7 +1215,7 @@ static int wgrad_splits(int M, int N, int Kred, const TileCfg& c) {
   return cdiv(KT, kps);
 }
 
-template <template <int, int, int> class LA, class DA, template <int, int, int> class LB, class DB>
+template <template <int, int, int> class LA, class DA, template <int, int, int> class LB, class DB, int MF = kMfF32>
 static int igemm_splitk(const DA& da, const DB& db, float* ws, int M, int N, int Kred, hipStream_t st,
                         int* splits_out) {
   const int id = splitk_config(M, N, Kred);
@@ -1154,7 +1226,8 @@ static int igemm_splitk(const DA& da, const DB& db, float* ws, int M, int N, int
   switch (id) {
 #define DK_CASE(cid, bm, bn, bk, wm, wn) \
   case cid:                              \
-    return launch_igemm<bm, bn, bk, wm, wn, LA, DA, LB, DB, EpPartial>(da, db, ep, M, N, Kred, splits, st, splits_out);
+    return launch_igemm<bm, bn, bk, wm, wn, LA, DA, LB, DB, EpPartial, MF>(da, db, ep, M, N, Kred, splits, st, \
+                                                                           splits_out);
     DK_SPLITK_CONFIGS(DK_CASE)
 #undef DK_CASE
     default:
@@ -1162,39 +1235,10 @@ static int igemm_splitk(const DA& da, const DB& db, float* ws, int M, int N, int
   }
 }
 
-static size_t splitk_ws_bytes(int M, int N, int Kred) {
+static inline size_t splitk_ws_bytes(int M, int N, int Kred) {
   int id = splitk_config(M, N, Kred);
   if (id < 0 || id >= kNumSplitCfg) id = 0;
   return (size_t)wgrad_splits(M, N, Kred, kSplitCfg[id]) * (size_t)M * (size_t)N * sizeof(float);
-}
-
-// Weight re-layouts (tiny; run once per call on the caller's stream).
-__global__ void w_kcrs_to_krsc_kernel(const float* __restrict__ w, int K, int C, int R, int S, int Cp,
-                                      float* __restrict__ out) {
-  const int idx = blockIdx.x * blockDim.x + threadIdx.x;  // over K*R*S*Cp
-  const int total = K * R * S * Cp;
-  if (idx >= total) return;
-  const int c = idx % Cp;
-  int t = idx / Cp;
-  const int s = t % S;
-  t /= S;
-  const int r = t % R;
-  const int k = t / R;
-  out[idx] = c < C ? w[(((size_t)k * C + c) * R + r) * S + s] : 0.f;
-}
-
-__global__ void w_kcrs_to_crsk_kernel(const float* __restrict__ w, int K, int C, int R, int S,
-                                      float* __restrict__ out) {
-  const int idx = blockIdx.x * blockDim.x + threadIdx.x;  // over C*R*S*K
-  const int total = K * R * S * C;
-  if (idx >= total) return;
-  const int k = idx % K;
-  int t = idx / K;
-  const int s = t % S;
-  t /= S;
-  const int r = t % R;
-  const int c = t / R;
-  out[idx] = w[(((size_t)k * C + c) * R + r) * S + s];
 }
 
 // Taps of sub-pixel phase a along an axis of length-R filters (stride st, padding pad): r0 + st*t.
@@ -1212,25 +1256,6 @@ __host__ __device__ __forceinline__ size_t phase_block_offset(int a, int b, int 
   return off;
 }
 
-// Sub-pixel phase sub-filters of a stride-st dgrad: for phase (a, b) the taps r = r0(a) + st*r',
-// s = s0(b) + st*s' as a [C][R'][S'][Kp] matrix (Kp = K rounded up to 4, zero-filled).
-__global__ void w_phase_kernel(const float* __restrict__ w, int K, int C, int R, int S, int st, int pad, int Kp,
-                               float* __restrict__ out) {
-  const int idx = blockIdx.x * blockDim.x + threadIdx.x;  // over C * R * S * Kp
-  if (idx >= C * R * S * Kp) return;
-  const int k = idx % Kp;
-  int t = idx / Kp;
-  const int s_ = t % S;
-  t /= S;
-  const int r = t % R;
-  const int c = t / R;
-  const int a = ((r - pad) % st + st) % st, b = ((s_ - pad) % st + st) % st;
-  const int r0 = phase_r0(a, st, pad), s0 = phase_r0(b, st, pad);
-  const int Rp = phase_taps(a, R, st, pad), Sp = phase_taps(b, S, st, pad);
-  const int rp = (r - r0) / st, sp = (s_ - s0) / st;
-  out[phase_block_offset(a, b, C, R, S, st, pad, Kp) + ((size_t)(c * Rp + rp) * Sp + sp) * Kp + k] =
-      k < K ? w[(((size_t)k * C + c) * R + r) * S + s_] : 0.f;
-}
 
 // rows x ld matrix; ext = extent of the non-reduction index (rows for a K-contiguous
 // operand, valid columns for a row-contiguous one).
@@ -1266,45 +1291,6 @@ static inline ImgDescE<float, true> img1(const float* x, int N, int H, int W, in
                                           1, sa, 1, 0, 0, M});
 }
 
-}  // namespace dk
-
-using namespace dk;
-
-// ============================================================================
-// C ABI
-// ============================================================================
-
-// Tuning knob: kind 0 = row problems (fwd/dgrad), 1 = split-K (wgrad); cfg -1 = heuristic.
-// Returns the number of configurations of that kind.  Not thread-safe; for tuning runs.
-DK_API int dk_debug_set_gemm_config(int kind, int cfg) {
-  if (kind == 2) {
-    g_fill_splits = cfg < 0 ? 1 : cfg;
-    return 0;
-  }
-  if (kind == 3) {  // streaming pointwise kernels (pw_stream.hip) on / off
-    pw_stream_set(cfg < 0 ? 1 : cfg);
-    return 0;
-  }
-  if (kind < 0 || kind > 1) return -1;
-  g_cfg_override[kind] = cfg;
-  return kind == 0 ? kNumRowCfg : kNumSplitCfg;
-}
-
-DK_API int dk_conv_weight_krsc_f32(const float* w_kcrs, int K, int C, int R, int S, int Cp, float* w_krsc,
-                                   void* stream) {
-  const int total = K * R * S * Cp;
-  hipLaunchKernelGGL(w_kcrs_to_krsc_kernel, dim3(cdiv(total, 256)), dim3(256), 0, as_stream(stream), w_kcrs, K, C, R,
-                     S, Cp, w_krsc);
-  return launch_status();
-}
-
-DK_API int dk_conv_weight_crsk_f32(const float* w_kcrs, int K, int C, int R, int S, float* w_crsk, void* stream) {
-  const int total = K * R * S * C;
-  hipLaunchKernelGGL(w_kcrs_to_crsk_kernel, dim3(cdiv(total, 256)), dim3(256), 0, as_stream(stream), w_kcrs, K, C, R,
-                     S, w_crsk);
-  return launch_status();
-}
-
 // y[n,oh,ow,k] = sum_{r,s,c} x[n, oh*stride + r - pad, ow*stride + s - pad, c] * w[k][r][s][c] (+ bias[k])
 template <class E, bool K1>
 static inline ImgBnDescE<E, K1> with_bn(const ImgDescE<E, K1>& d, const float* mean, const float* invstd,
@@ -1338,7 +1324,7 @@ static int conv_fwd(const D& a, const float* w_krsc, int K, int Ktot, const floa
 }
 
 // Rows of BatchNorm partial statistics a *_fwd_ex_f32 call writes (one per output tile row).
-static int stats_rows(int M, int N, int Ktot, int kind = kRowPlain) {
+static inline int stats_rows(int M, int N, int Ktot, int kind = kRowPlain) {
   return cdiv(M, kRowCfg[row_config(M, N, Ktot, kind)].BM);
 }
 
@@ -1353,111 +1339,6 @@ static int conv_fwd_ex(const D0& base, const float* w, int K, int Ktot, const fl
     return conv_fwd(with_bn(base, bn_mean, bn_invstd, bn_gamma, bn_beta, bn_relu), w, K, Ktot, bias, y, stream, stats);
   }
   return conv_fwd(base, w, K, Ktot, bias, y, stream, stats);
-}
-
-DK_API int dk_conv2d_fwd_f32(const float* x, int N, int H, int W, int C, const float* w_krsc, int K, int R, int S,
-                             int stride, int pad, const float* bias, float* y, int OH, int OW, void* stream) {
-  if (C % 4 || !aligned16(x) || !aligned16(w_krsc) || !fits((size_t)N * H * W * C * 4)) return DK_ERR_ARGS;
-  return conv_fwd(img(x, N, H, W, C, OH, OW, R, S, stride, 1, -pad, N * OH * OW), w_krsc, K, R * S * C, bias, y,
-                  stream);
-}
-
-DK_API int dk_conv2d_fwd_bnx_f32(const float* x, int N, int H, int W, int C, const float* w_krsc, int K, int R, int S,
-                                 int stride, int pad, const float* bias, float* y, int OH, int OW,
-                                 const float* bn_mean, const float* bn_invstd, const float* bn_gamma,
-                                 const float* bn_beta, int bn_relu, void* stream) {
-  if (C % 4 || !aligned16(x) || !aligned16(w_krsc) || !fits((size_t)N * H * W * C * 4)) return DK_ERR_ARGS;
-  if (!bn_ok(bn_mean, bn_invstd, bn_gamma, bn_beta)) return DK_ERR_ARGS;
-  return conv_fwd(with_bn(img(x, N, H, W, C, OH, OW, R, S, stride, 1, -pad, N * OH * OW), bn_mean, bn_invstd,
-                          bn_gamma, bn_beta, bn_relu),
-                  w_krsc, K, R * S * C, bias, y, stream);
-}
-
-DK_API int dk_conv2d_fwd_stats_rows(int N, int OH, int OW, int K, int C, int R, int S) {
-  return stats_rows(N * OH * OW, K, R * S * C, kRowConv);
-}
-
-// Forward with optional BN on load (bn_mean != NULL) and optional output statistics
-// (stats != NULL: dk_conv2d_fwd_stats_rows() x 2 x K doubles, for dk_bn_stats_from_partials_f32).
-DK_API int dk_conv2d_fwd_ex_f32(const float* x, int N, int H, int W, int C, const float* w_krsc, int K, int R, int S,
-                                int stride, int pad, const float* bias, float* y, int OH, int OW,
-                                const float* bn_mean, const float* bn_invstd, const float* bn_gamma,
-                                const float* bn_beta, int bn_relu, double* stats, void* stream) {
-  if (C % 4 || !aligned16(x) || !aligned16(w_krsc) || !fits((size_t)N * H * W * C * 4)) return DK_ERR_ARGS;
-  return conv_fwd_ex(img(x, N, H, W, C, OH, OW, R, S, stride, 1, -pad, N * OH * OW), w_krsc, K, R * S * C, bias, y,
-                     bn_mean, bn_invstd, bn_gamma, bn_beta, bn_relu, stats, stream);
-}
-
-// Stride-1 dgrad as an implicit GEMM: dx[n,h,w,c] = sum_{r,s,k} dy[n, h+pad-r, w+pad-s, k] * w[k][c][r][s]
-DK_API int dk_conv2d_dgrad_f32(const float* dy, int N, int OH, int OW, int K, const float* w_crsk, int C, int R,
-                               int S, int pad, float* dx, int H, int W, void* stream) {
-  if (K % 4 || !aligned16(dy) || !aligned16(w_crsk) || !fits((size_t)N * OH * OW * K * 4)) return DK_ERR_ARGS;
-  ImgDesc a = img(dy, N, OH, OW, K, H, W, R, S, 1, -1, pad, N * H * W);
-  const int Ktot = R * S * K;
-  MatDesc b = mat(w_crsk, C, Ktot, C);
-  EpStore ep = ep_store(dx, C, nullptr);
-  return igemm_rows<LdImgKC, ImgDesc, LdMatKC, MatDesc, EpStore>(a, b, ep, N * H * W, C, Ktot, as_stream(stream));
-}
-
-// Sub-pixel phase geometry of a stride-st, pad-p correlation's input gradient along one axis:
-// phase a's taps are r0 + st*t (t < Rp), reading dy row i + nb0 - t for dx row st*i + a.
-struct PhaseAxis {
-  int r0, Rp, nb0, Op;
-};
-static inline PhaseAxis phase_axis(int a, int R, int st, int pad, int L) {
-  PhaseAxis p;
-  p.r0 = phase_r0(a, st, pad);
-  p.Rp = phase_taps(a, R, st, pad);
-  p.nb0 = (a + pad - p.r0) / st;
-  p.Op = a < L ? (L - a + st - 1) / st : 0;
-  return p;
-}
-
-DK_API size_t dk_conv2d_dgrad_phase_workspace_bytes(int K, int C, int R, int S, int stride) {
-  if (K < 1 || C < 1 || R < 1 || S < 1 || stride < 1) return 0;
-  const size_t kp = (size_t)((K + 3) / 4 * 4);
-  return (size_t)C * R * S * kp * sizeof(float);
-}
-
-// Input gradient of any-stride convolution as one implicit GEMM per sub-pixel phase (replaces
-// cp.dot(dy, W_flat) + row2im, convolution.py:101-117 / :205-222: no column matrix, no atomics):
-// phase (a, b) is a stride-1 correlation of dy with its sub-filter, written to the dx pixels
-// (st*i + a, st*j + b).  dy has Kp = K rounded up to 4 channels (zero-padded by the caller when
-// K % 4 != 0); phases with no taps (R or S < stride) write zeros.
-DK_API int dk_conv2d_dgrad_phase_f32(const float* dy, int N, int OH, int OW, int Kp, int K, const float* w_kcrs,
-                                     int C, int R, int S, int stride, int pad, float* dx, int H, int W, void* ws,
-                                     size_t ws_bytes, void* stream) {
-  if (Kp % 4 || Kp < K || stride < 1 || stride > 8 || N < 1 || C < 1 || !aligned16(dy) || !aligned16(ws))
-    return DK_ERR_ARGS;
-  if (ws_bytes < dk_conv2d_dgrad_phase_workspace_bytes(K, C, R, S, stride) || Kp != (K + 3) / 4 * 4)
-    return DK_ERR_WORKSPACE;
-  if (!fits((size_t)N * OH * OW * Kp * 4) || !fits((size_t)N * H * W * C * 4)) return DK_ERR_ARGS;
-  const hipStream_t st = as_stream(stream);
-  float* wsub = static_cast<float*>(ws);
-  const int total = C * R * S * Kp;
-  hipLaunchKernelGGL(w_phase_kernel, dim3(cdiv(total, 256)), dim3(256), 0, st, w_kcrs, K, C, R, S, stride, pad, Kp,
-                     wsub);
-  int rc = launch_status();
-  if (rc) return rc;
-  for (int a = 0; a < stride; ++a)
-    for (int b = 0; b < stride; ++b) {
-      const PhaseAxis pa = phase_axis(a, R, stride, pad, H), pb = phase_axis(b, S, stride, pad, W);
-      if (pa.Op == 0 || pb.Op == 0) continue;  // no dx pixels of this phase
-      const int M = N * pa.Op * pb.Op;
-      ImgDesc d = img(dy, N, OH, OW, Kp, pa.Op, pb.Op, pa.Rp, pb.Rp, 1, -1, pa.nb0, M);
-      d.offw = pb.nb0;
-      const int Ktot = pa.Rp * pb.Rp * Kp;
-      const float* wp = wsub + phase_block_offset(a, b, C, R, S, stride, pad, Kp);
-      MatDesc bm = mat(wp, C, Ktot > 0 ? Ktot : 4, C);
-      EpPhase ep{dx, C, pa.Op, pb.Op, H, W, stride, a, b, al4(C) && aligned16(dx)};
-      rc = igemm_rows<LdImgKC, ImgDesc, LdMatKC, MatDesc, EpPhase>(d, bm, ep, M, C, Ktot, st);
-      if (rc) return rc;
-    }
-  return 0;
-}
-
-DK_API size_t dk_conv2d_wgrad_workspace_bytes(int N, int OH, int OW, int K, int Cp, int R, int S) {
-  return splitk_ws_bytes(K, R * S * Cp, N * OH * OW);
 }
 
 // dw[k][c][r][s] = sum_{n,oh,ow} dy[n,oh,ow,k] * x[n, oh*stride + r - pad, ow*stride + s - pad, c]  (+ l2 * w)
@@ -1477,14 +1358,6 @@ static int wgrad(const float* dy, const D& b, int K, int Ncol, const float* w, f
                            : igemm_splitk<LdMatIC1, MatDesc, LdImgIC, D>(a, b, part, K, Ncol, Kred, st, &splits);
   if (rc) return rc;
   return splitk_reduce(part, splits, K, Ncol, dw, w, l2, mode, C, Cp, R, S, st);
-}
-
-DK_API int dk_conv2d_wgrad_f32(const float* dy, const float* x, int N, int H, int W, int Cp, int C, int K, int R,
-                               int S, int stride, int pad, int OH, int OW, const float* w_kcrs, float l2,
-                               float* dw_kcrs, void* ws, size_t ws_bytes, void* stream) {
-  if (Cp % 4 || !aligned16(x) || !fits((size_t)N * H * W * Cp * 4)) return DK_ERR_ARGS;
-  return wgrad(dy, img(x, N, H, W, Cp, OH, OW, R, S, stride, 1, -pad, N * OH * OW), K, R * S * Cp, w_kcrs, l2,
-               dw_kcrs, 1, C, Cp, R, S, ws, ws_bytes, stream);
 }
 
 // Weight gradient with the following BatchNorm's backward applied as dy is loaded: g is the
@@ -1515,413 +1388,4 @@ static int wgrad_bnbwd(const float* g, const float* bn_x, const D& b, int K, int
   return splitk_reduce(part, splits, K, Ncol, dw, w, l2, 1, C, Cp, R, S, st);
 }
 
-DK_API int dk_conv2d_wgrad_bnbwd_f32(const float* g, const float* bn_x, const float* x, int N, int H, int W, int Cp,
-                                     int C, int K,
-                                     int R, int S, int stride, int pad, int OH, int OW, const float* out_mean,
-                                     const float* out_invstd, const float* out_gamma, const float* out_beta,
-                                     int out_relu, const float* k12, const float* w_kcrs, float l2, float* dw_kcrs,
-                                     void* ws, size_t ws_bytes, const float* bn_mean, const float* bn_invstd,
-                                     const float* bn_gamma, const float* bn_beta, int bn_relu, void* stream) {
-  if (Cp % 4 || K % 4 || !aligned16(x) || !fits((size_t)N * H * W * Cp * 4)) return DK_ERR_ARGS;
-  if (!out_mean || !out_invstd || !out_gamma || !out_beta || !k12) return DK_ERR_ARGS;
-  const BnBwdIn bw{out_mean, out_invstd, out_gamma, out_beta, k12, out_relu, K};
-  if (bn_mean) {
-    if (!bn_ok(bn_mean, bn_invstd, bn_gamma, bn_beta)) return DK_ERR_ARGS;
-    return wgrad_bnbwd(g, bn_x,
-                       with_bn(img(x, N, H, W, Cp, OH, OW, R, S, stride, 1, -pad, N * OH * OW), bn_mean,
-                               bn_invstd, bn_gamma, bn_beta, bn_relu),
-                       K, R * S * Cp, bw, w_kcrs, l2, dw_kcrs, C, Cp, R, S, ws, ws_bytes, stream);
-  }
-  return wgrad_bnbwd(g, bn_x, img(x, N, H, W, Cp, OH, OW, R, S, stride, 1, -pad, N * OH * OW), K,
-                     R * S * Cp, bw, w_kcrs, l2, dw_kcrs, C, Cp, R, S, ws, ws_bytes, stream);
-}
-
-DK_API int dk_conv2d_wgrad_bnx_f32(const float* dy, const float* x, int N, int H, int W, int Cp, int C, int K, int R,
-                                   int S, int stride, int pad, int OH, int OW, const float* w_kcrs, float l2,
-                                   float* dw_kcrs, void* ws, size_t ws_bytes, const float* bn_mean,
-                                   const float* bn_invstd, const float* bn_gamma, const float* bn_beta, int bn_relu,
-                                   void* stream) {
-  if (Cp % 4 || !aligned16(x) || !fits((size_t)N * H * W * Cp * 4)) return DK_ERR_ARGS;
-  if (!bn_ok(bn_mean, bn_invstd, bn_gamma, bn_beta)) return DK_ERR_ARGS;
-  return wgrad(dy,
-               with_bn(img(x, N, H, W, Cp, OH, OW, R, S, stride, 1, -pad, N * OH * OW), bn_mean, bn_invstd, bn_gamma,
-                       bn_beta, bn_relu),
-               K, R * S * Cp, w_kcrs, l2, dw_kcrs, 1, C, Cp, R, S, ws, ws_bytes, stream);
-}
-
-// Pointwise (1x1) forward with optional stride-s subsampling (pointwise_convolution.py:46-55):
-// y[n,oh,ow,k] = sum_c x[n, oh*s, ow*s, c] * w[k][c] (+ bias)
-DK_API int dk_pwconv_fwd_f32(const float* x, int N, int H, int W, int C, const float* w_kc, int K, int stride,
-                             const float* bias, float* y, int OH, int OW, void* stream) {
-  if (!fits((size_t)N * H * W * C * 4)) return DK_ERR_ARGS;
-  MatDesc b = mat(w_kc, K, C, K);
-  EpStore ep = ep_store(y, K, bias);
-  if (C % 4 || !aligned16(x) || !aligned16(w_kc)) {
-    // Unaligned channel count: scalar loads, stride 1 only (the rows are then a plain matrix).
-    if (stride != 1) return DK_ERR_ARGS;
-    MatDesc a = mat(x, N * H * W, C, N * H * W);
-    return igemm_rows<LdMatKC1, MatDesc, LdMatKC1, MatDesc, EpStore>(a, b, ep, N * H * W, K, C, as_stream(stream));
-  }
-  return conv_fwd(img1(x, N, H, W, C, OH, OW, stride, N * OH * OW), w_kc, K, C, bias, y, stream);
-}
-
-// The same with x = the raw output of the previous layer and y = pw(bn(x)) (+ReLU inside).
-DK_API int dk_pwconv_fwd_bnx_f32(const float* x, int N, int H, int W, int C, const float* w_kc, int K, int stride,
-                                 const float* bias, float* y, int OH, int OW, const float* bn_mean,
-                                 const float* bn_invstd, const float* bn_gamma, const float* bn_beta, int bn_relu,
-                                 void* stream) {
-  if (C % 4 || !aligned16(x) || !aligned16(w_kc) || !fits((size_t)N * H * W * C * 4)) return DK_ERR_ARGS;
-  if (!bn_ok(bn_mean, bn_invstd, bn_gamma, bn_beta)) return DK_ERR_ARGS;
-  return conv_fwd(with_bn(img1(x, N, H, W, C, OH, OW, stride, N * OH * OW), bn_mean, bn_invstd, bn_gamma,
-                          bn_beta, bn_relu),
-                  w_kc, K, C, bias, y, stream);
-}
-
-DK_API int dk_pwconv_fwd_stats_rows(int N, int OH, int OW, int K, int C) {
-  const int M = N * OH * OW;
-  // (the input extent does not change the choice for the shapes the network uses)
-  if (pw_stream_fwd_ok(K, C, M, 0)) return pw_stream_fwd_rows(M, K);
-  return stats_rows(M, K, C);
-}
-
-DK_API int dk_pwconv_fwd_ex_f32(const float* x, int N, int H, int W, int C, const float* w_kc, int K, int stride,
-                                const float* bias, float* y, int OH, int OW, const float* bn_mean,
-                                const float* bn_invstd, const float* bn_gamma, const float* bn_beta, int bn_relu,
-                                double* stats, void* stream) {
-  if (C % 4 || !aligned16(x) || !aligned16(w_kc) || !fits((size_t)N * H * W * C * 4)) return DK_ERR_ARGS;
-  if (pw_stream_fwd_ok(K, C, N * OH * OW, (size_t)N * H * W * C * 4) && (!bn_mean || bn_ok(bn_mean, bn_invstd, bn_gamma, bn_beta)))
-    // K = C = 64 / 128: the persistent streaming kernel (pw_stream.hip), bit-identical outputs
-  {
-    FoldTail ft;
-    if (stats) fold_take(stats, pw_stream_fwd_rows(N * OH * OW, K), K, 1, &ft);
-    return fold_status(pw_stream_fwd(x, N, H, W, stride, OH, OW, w_kc, K, bias, y, bn_mean, bn_invstd, bn_gamma,
-                                     bn_beta, bn_relu, stats, as_stream(stream), stats ? &ft : nullptr),
-                       stats ? ft : FoldTail{});
-  }
-  return conv_fwd_ex(img1(x, N, H, W, C, OH, OW, stride, N * OH * OW), w_kc, K, C, bias, y, bn_mean,
-                     bn_invstd, bn_gamma, bn_beta, bn_relu, stats, stream);
-}
-
-// Pointwise dgrad (pointwise_convolution.py:65-72): dx_rows = dy_rows . W; for stride > 1 the
-// result is widened to (OH*s, OW*s) with zeros off the sampling lattice.
-DK_API int dk_pwconv_dgrad_f32(const float* dy, int N, int OH, int OW, int K, const float* w_kc, int C, int stride,
-                               float* dx, void* stream) {
-  const int M = N * OH * OW;
-  if (!fits((size_t)M * K * 4)) return DK_ERR_ARGS;
-  MatDesc a = mat(dy, M, K, M);
-  MatDesc b = mat(w_kc, K, C, C);
-  const hipStream_t st = as_stream(stream);
-  const bool vec = vec_ok(a, K, 4) && vec_ok(b, 4, C);
-  if (stride == 1) {
-    EpStore ep = ep_store(dx, C, nullptr);
-    if (vec) return igemm_rows<LdMatKC, MatDesc, LdMatIC, MatDesc, EpStore>(a, b, ep, M, C, K, st);
-    return igemm_rows<LdMatKC1, MatDesc, LdMatIC1, MatDesc, EpStore>(a, b, ep, M, C, K, st);
-  }
-  EpWiden ep = ep_widen(dx, C, OH, OW, stride);
-  if (vec) return igemm_rows<LdMatKC, MatDesc, LdMatIC, MatDesc, EpWiden>(a, b, ep, M, C, K, st);
-  return igemm_rows<LdMatKC1, MatDesc, LdMatIC1, MatDesc, EpWiden>(a, b, ep, M, C, K, st);
-}
-
-DK_API int dk_pwconv_dgrad_stats_rows(int N, int OH, int OW, int K, int C) { return stats_rows(N * OH * OW, C, K); }
-DK_API int dk_pwconv_dgrad_bnbwd_stats_rows(int N, int OH, int OW, int K, int C) {
-  const int M = N * OH * OW;
-  if (pw_stream_dgrad_ok(K, C, M)) return pw_stream_dgrad_rows(M);
-  return stats_rows(M, C, K, kRowBnBwd);
-}
-
-// dgrad + the BN-backward partial sums of the BatchNorm whose output this layer consumed
-// (bn_x = that BN's raw input, on the dx grid; part: dk_pwconv_dgrad_stats_rows() x 2 x C).
-DK_API int dk_pwconv_dgrad_ex_f32(const float* dy, int N, int OH, int OW, int K, const float* w_kc, int C, int stride,
-                                  float* dx, const float* residual, const float* bn_x, const float* bn_mean,
-                                  const float* bn_invstd, const float* bn_gamma, const float* bn_beta, int bn_relu,
-                                  double* part, void* stream) {
-  const int M = N * OH * OW;
-  if (!fits((size_t)M * K * 4) || (part != nullptr) != (bn_x != nullptr)) return DK_ERR_ARGS;
-  if (part && (!bn_mean || !bn_invstd || !bn_gamma || !bn_beta)) return DK_ERR_ARGS;
-  if (part && residual && stride != 1) return DK_ERR_ARGS;  // off-lattice residual terms would need reducing
-  MatDesc a = mat(dy, M, K, M);
-  MatDesc b = mat(w_kc, K, C, C);
-  const hipStream_t st = as_stream(stream);
-  const bool vec = vec_ok(a, K, 4) && vec_ok(b, 4, C);
-#define DK_ROWS(EPT, ep)                                                              \
-  return vec ? igemm_rows<LdMatKC, MatDesc, LdMatIC, MatDesc, EPT>(a, b, ep, M, C, K, st) \
-             : igemm_rows<LdMatKC1, MatDesc, LdMatIC1, MatDesc, EPT>(a, b, ep, M, C, K, st)
-  if (!part) {
-    if (stride == 1) {
-      EpStore ep = ep_store(dx, C, nullptr, residual);
-      DK_ROWS(EpStore, ep);
-    }
-    EpWiden ep = ep_widen(dx, C, OH, OW, stride, residual);
-    DK_ROWS(EpWiden, ep);
-  }
-  const BnIn bn{bn_mean, bn_invstd, bn_gamma, bn_beta, bn_relu};
-  const int xv4 = aligned16(bn_x) && bn_ok(bn_mean, bn_invstd, bn_gamma, bn_beta);
-  if (stride == 1) {
-    EpStoreBnBwd ep;
-    static_cast<EpStore&>(ep) = ep_store(dx, C, nullptr, residual);
-    ep.v4 = ep.v4 && xv4;
-    ep.part = part;
-    ep.xbn = bn_x;
-    ep.bn = bn;
-    DK_ROWS(EpStoreBnBwd, ep);
-  }
-  EpWidenBnBwd ep;
-  static_cast<EpWiden&>(ep) = ep_widen(dx, C, OH, OW, stride);
-  ep.v4 = ep.v4 && xv4;
-  ep.part = part;
-  ep.xbn = bn_x;
-  ep.bn = bn;
-  DK_ROWS(EpWidenBnBwd, ep);
-#undef DK_ROWS
-}
-
-// dk_pwconv_dgrad_ex_f32 with the input BN's partials for stride > 1, the widened gradient kept
-// compact (EpLatticeBnBwd): dx_lat[n][oh][ow][c] = the widened dx at (n, s*oh, s*ow, c), the
-// rest of the widened grid being zero; part has dk_pwconv_dgrad_stats_rows() rows.
-DK_API int dk_pwconv_dgrad_lattice_f32(const float* dy, int N, int OH, int OW, int K, const float* w_kc, int C,
-                                       int stride, float* dx_lat, const float* bn_x, const float* bn_mean,
-                                       const float* bn_invstd, const float* bn_gamma, const float* bn_beta,
-                                       int bn_relu, double* part, void* stream) {
-  const int M = N * OH * OW;
-  if (!fits((size_t)M * K * 4) || !fits((size_t)M * C * 4) || stride < 2 || !dx_lat || !bn_x || !part)
-    return DK_ERR_ARGS;
-  if (!bn_mean || !bn_invstd || !bn_gamma || !bn_beta) return DK_ERR_ARGS;
-  MatDesc a = mat(dy, M, K, M);
-  MatDesc b = mat(w_kc, K, C, C);
-  const hipStream_t st = as_stream(stream);
-  const bool vec = vec_ok(a, K, 4) && vec_ok(b, 4, C);
-  EpLatticeBnBwd ep;
-  static_cast<EpWiden&>(ep) = ep_widen(dx_lat, C, OH, OW, stride);
-  ep.v4 = ep.v4 && aligned16(bn_x) && bn_ok(bn_mean, bn_invstd, bn_gamma, bn_beta);
-  ep.part = part;
-  ep.xbn = bn_x;
-  ep.bn = BnIn{bn_mean, bn_invstd, bn_gamma, bn_beta, bn_relu};
-  return vec ? igemm_rows<LdMatKC, MatDesc, LdMatIC, MatDesc, EpLatticeBnBwd>(a, b, ep, M, C, K, st)
-             : igemm_rows<LdMatKC1, MatDesc, LdMatIC1, MatDesc, EpLatticeBnBwd>(a, b, ep, M, C, K, st);
-}
-
-// dgrad of a stride-1 pointwise layer whose output fed a BatchNorm (+ReLU), with that BN's
-// backward apply (dk_bn_bwd_apply_f32) done on load: g = the gradient w.r.t. the BN(+ReLU)
-// output, bn_x = the BN's raw input (= this layer's output), k12 from
-// dk_bn_bwd_from_partials_f32.  dy_out (nullable) receives dy = the gradient w.r.t. bn_x,
-// bit-identical to dk_bn_bwd_apply_f32's, for this layer's weight gradient.  The epilogue
-// options (residual, the partials of the BN before this layer) are those of
-// dk_pwconv_dgrad_ex_f32 at stride 1; part has dk_pwconv_dgrad_bnbwd_stats_rows() rows.
-DK_API int dk_pwconv_dgrad_bnbwd_f32(const float* g, const float* bn_x, int N, int OH, int OW, int K,
-                                     const float* out_mean, const float* out_invstd, const float* out_gamma,
-                                     const float* out_beta, int out_relu, const float* k12, float* dy_out,
-                                     const float* w_kc, int C, float* dx, const float* residual, const float* x,
-                                     const float* bn_mean, const float* bn_invstd, const float* bn_gamma,
-                                     const float* bn_beta, int bn_relu, double* part, void* stream) {
-  const int M = N * OH * OW;
-  if (!fits((size_t)M * K * 4) || (part != nullptr) != (x != nullptr)) return DK_ERR_ARGS;
-  if (part && (!bn_mean || !bn_invstd || !bn_gamma || !bn_beta)) return DK_ERR_ARGS;
-  if (!out_mean || !out_invstd || !out_gamma || !out_beta || !k12 || !bn_x) return DK_ERR_ARGS;
-  MatBwdDesc a;
-  static_cast<MatDesc&>(a) = mat(g, M, K, M);
-  a.x = bn_x;
-  a.bwd = BnBwdIn{out_mean, out_invstd, out_gamma, out_beta, k12, out_relu, K};
-  a.dy_out = dy_out;
-  MatDesc b = mat(w_kc, K, C, C);
-  const hipStream_t st = as_stream(stream);
-  // 16-byte loads of g, bn_x and dy_out; the LDS table holds 2 float4 per channel
-  if (!vec_ok(b, 4, C) || K % 4 || !aligned16(g) || !aligned16(bn_x) || (dy_out && !aligned16(dy_out)) ||
-      (size_t)K * 32 > 64 * 1024)
-    return DK_ERR_ARGS;
-  if (pw_stream_dgrad_ok(K, C, M)) {
-    // K = C = 64: the persistent streaming kernel (pw_stream.hip), bit-identical results
-    if (part && !bn_ok(bn_mean, bn_invstd, bn_gamma, bn_beta)) return DK_ERR_ARGS;
-    FoldTail ft;
-    if (part) fold_take(part, pw_stream_dgrad_rows(M), C, 1, &ft);
-    return fold_status(pw_stream_dgrad_bnbwd(g, bn_x, M, out_mean, out_invstd, out_gamma, out_beta, out_relu, k12,
-                                             dy_out, w_kc, dx, residual, part ? x : nullptr, bn_mean, bn_invstd,
-                                             bn_gamma, bn_beta, bn_relu, part, st, part ? &ft : nullptr),
-                       part ? ft : FoldTail{});
-  }
-  if (!part) {
-    EpStore ep = ep_store(dx, C, nullptr, residual);
-    return igemm_rows<LdMatKC, MatBwdDesc, LdMatIC, MatDesc, EpStore, kRowBnBwd>(a, b, ep, M, C, K, st);
-  }
-  EpStoreBnBwd ep;
-  static_cast<EpStore&>(ep) = ep_store(dx, C, nullptr, residual);
-  ep.v4 = ep.v4 && aligned16(x) && bn_ok(bn_mean, bn_invstd, bn_gamma, bn_beta);
-  ep.part = part;
-  ep.xbn = x;
-  ep.bn = BnIn{bn_mean, bn_invstd, bn_gamma, bn_beta, bn_relu};
-  return igemm_rows<LdMatKC, MatBwdDesc, LdMatIC, MatDesc, EpStoreBnBwd, kRowBnBwd>(a, b, ep, M, C, K, st);
-}
-
-DK_API size_t dk_pwconv_wgrad_workspace_bytes(int N, int OH, int OW, int K, int C) {
-  return splitk_ws_bytes(K, C, N * OH * OW);
-}
-
-// dw[k][c] = sum_{n,oh,ow} dy[n,oh,ow,k] * x[n, oh*s, ow*s, c]  (+ l2 * w)   (pointwise_convolution.py:61-64)
-DK_API int dk_pwconv_wgrad_f32(const float* dy, const float* x, int N, int H, int W, int C, int K, int stride,
-                               int OH, int OW, const float* w_kc, float l2, float* dw_kc, void* ws, size_t ws_bytes,
-                               void* stream) {
-  if (C % 4 || !aligned16(x) || !fits((size_t)N * H * W * C * 4)) return DK_ERR_ARGS;
-  return wgrad(dy, img(x, N, H, W, C, OH, OW, 1, 1, stride, 1, 0, N * OH * OW), K, C, w_kc, l2, dw_kc, 0, C, C, 1, 1,
-               ws, ws_bytes, stream);
-}
-
-DK_API int dk_pwconv_wgrad_bnx_f32(const float* dy, const float* x, int N, int H, int W, int C, int K, int stride,
-                                   int OH, int OW, const float* w_kc, float l2, float* dw_kc, void* ws,
-                                   size_t ws_bytes, const float* bn_mean, const float* bn_invstd,
-                                   const float* bn_gamma, const float* bn_beta, int bn_relu, void* stream) {
-  if (C % 4 || !aligned16(x) || !fits((size_t)N * H * W * C * 4)) return DK_ERR_ARGS;
-  if (!bn_ok(bn_mean, bn_invstd, bn_gamma, bn_beta)) return DK_ERR_ARGS;
-  return wgrad(dy,
-               with_bn(img(x, N, H, W, C, OH, OW, 1, 1, stride, 1, 0, N * OH * OW), bn_mean, bn_invstd, bn_gamma,
-                       bn_beta, bn_relu),
-               K, C, w_kc, l2, dw_kc, 0, C, C, 1, 1, ws, ws_bytes, stream);
-}
-
-// Dense (dense_layer.py:46-55): y[b][o] = sum_i x[b][i] * w[i][o] (+ bias[o]);  w stored (in, out).
-DK_API int dk_dense_fwd_f32(const float* x, int B, int IN, const float* w_io, int OUT, const float* bias, float* y,
-                            void* stream) {
-  MatDesc a = mat(x, B, IN, B);
-  MatDesc b = mat(w_io, IN, OUT, OUT);
-  EpStore ep = ep_store(y, OUT, bias);
-  const hipStream_t st = as_stream(stream);
-  const bool va = vec_ok(a, IN, 4), vb = vec_ok(b, 4, OUT);
-  if (va && vb) return igemm_rows<LdMatKC, MatDesc, LdMatIC, MatDesc, EpStore>(a, b, ep, B, OUT, IN, st);
-  return igemm_rows<LdMatKC1, MatDesc, LdMatIC1, MatDesc, EpStore>(a, b, ep, B, OUT, IN, st);
-}
-
-// dx[b][i] = sum_o dy[b][o] * w[i][o]   (dense_layer.py:67)
-DK_API int dk_dense_dgrad_f32(const float* dy, int B, int OUT, const float* w_io, int IN, float* dx, void* stream) {
-  MatDesc a = mat(dy, B, OUT, B);
-  MatDesc b = mat(w_io, IN, OUT, IN);
-  EpStore ep = ep_store(dx, IN, nullptr);
-  const hipStream_t st = as_stream(stream);
-  if (vec_ok(a, OUT, 4) && vec_ok(b, OUT, 4))
-    return igemm_rows<LdMatKC, MatDesc, LdMatKC, MatDesc, EpStore>(a, b, ep, B, IN, OUT, st);
-  return igemm_rows<LdMatKC1, MatDesc, LdMatKC1, MatDesc, EpStore>(a, b, ep, B, IN, OUT, st);
-}
-
-DK_API size_t dk_dense_wgrad_workspace_bytes(int B, int IN, int OUT) { return splitk_ws_bytes(IN, OUT, B); }
-
-// dw[i][o] = sum_b x[b][i] * dy[b][o] (+ l2 * w)   (dense_layer.py:61-66)
-DK_API int dk_dense_wgrad_f32(const float* x, const float* dy, int B, int IN, int OUT, const float* w_io, float l2,
-                              float* dw_io, void* ws, size_t ws_bytes, void* stream) {
-  if (ws_bytes < splitk_ws_bytes(IN, OUT, B)) return DK_ERR_WORKSPACE;
-  MatDesc a = mat(x, B, IN, IN);
-  MatDesc b = mat(dy, B, OUT, OUT);
-  int splits = 1;
-  const hipStream_t st = as_stream(stream);
-  int rc;
-  if (vec_ok(a, 4, IN) && vec_ok(b, 4, OUT))
-    rc = igemm_splitk<LdMatIC, MatDesc, LdMatIC, MatDesc>(a, b, static_cast<float*>(ws), IN, OUT, B, st, &splits);
-  else
-    rc = igemm_splitk<LdMatIC1, MatDesc, LdMatIC1, MatDesc>(a, b, static_cast<float*>(ws), IN, OUT, B, st, &splits);
-  if (rc) return rc;
-  return splitk_reduce(static_cast<float*>(ws), splits, IN, OUT, dw_io, w_io, l2, 0, OUT, OUT, 1, 1, st);
-}
-
-// ---------------------------------------------------------------------------------------
-// bf16 storage twins of the pointwise entries (BASELINE config 5).  Activations bf16,
-// weights / statistics / weight gradients fp32; the loaders widen bf16 to fp32 on load and
-// the MFMAs are the exact-fp32 v_mfma_f32_32x32x2_f32 of the fp32 path, so the only
-// numerical difference from fp32 storage is the rounding of each stored activation.
-// ---------------------------------------------------------------------------------------
-namespace dk {
-static inline MatDescE<bf16_t> mat_h(const bf16_t* p, int rows, int ld, int ext) {
-  return MatDescE<bf16_t>{p, (uint32_t)((size_t)rows * ld * sizeof(bf16_t)), ld, ext};
-}
-static inline ImgDescE<bf16_t> img_h(const bf16_t* x, int N, int H, int W, int C, int OH, int OW, int R, int S,
-                                     int sa, int dr, int off, int M) {
-  return set_magics(ImgDescE<bf16_t>{x, (uint32_t)((size_t)N * H * W * C * sizeof(bf16_t)), H, W, C, OH, OW, R, S,
-                                     sa, dr, off, off, M});
-}
-static inline ImgDescE<bf16_t, true> img1_h(const bf16_t* x, int N, int H, int W, int C, int OH, int OW, int sa, int M) {
-  return set_magics(ImgDescE<bf16_t, true>{x, (uint32_t)((size_t)N * H * W * C * sizeof(bf16_t)), H, W, C, OH, OW,
-                                           1, 1, sa, 1, 0, 0, M});
-}
-static inline bool al8(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 7) == 0; }
 }  // namespace dk
-
-// partial-statistics rows of dk_pwconv_fwd_ex_bf16 (always the tiled engine: one row per M tile)
-DK_API int dk_pwconv_fwd_bf16_stats_rows(int N, int OH, int OW, int K, int C) { return stats_rows(N * OH * OW, K, C); }
-
-DK_API int dk_pwconv_fwd_ex_bf16(const bf16_t* x, int N, int H, int W, int C, const float* w_kc, int K, int stride,
-                                 const float* bias, bf16_t* y, int OH, int OW, const float* bn_mean,
-                                 const float* bn_invstd, const float* bn_gamma, const float* bn_beta, int bn_relu,
-                                 double* stats, void* stream) {
-  if (C % 4 || K % 4 || !al8(x) || !al8(y) || !aligned16(w_kc) || (bias && !aligned16(bias))) return DK_ERR_ARGS;
-  if (!fits((size_t)N * H * W * C * 4) || !fits((size_t)N * OH * OW * K * 4)) return DK_ERR_ARGS;
-  const ImgDescE<bf16_t, true> a = img1_h(x, N, H, W, C, OH, OW, stride, N * OH * OW);
-  const MatDesc b = mat(w_kc, K, C, K);
-  const hipStream_t st = as_stream(stream);
-  const int M = a.M;
-  auto run = [&](const auto& da) -> int {
-    using DA = std::decay_t<decltype(da)>;
-    if (stats) {
-      EpStoreStatsT<bf16_t> ep{};
-      ep.out = y, ep.ldo = K, ep.bias = bias, ep.v4 = 1, ep.res = nullptr, ep.part = stats;
-      return igemm_rows<LdImgKC, DA, LdMatKC, MatDesc, EpStoreStatsT<bf16_t>>(da, b, ep, M, K, C, st);
-    }
-    EpStoreT<bf16_t> ep{y, K, bias, 1, nullptr};
-    return igemm_rows<LdImgKC, DA, LdMatKC, MatDesc, EpStoreT<bf16_t>>(da, b, ep, M, K, C, st);
-  };
-  if (bn_mean) {
-    if (!bn_ok(bn_mean, bn_invstd, bn_gamma, bn_beta) || C > 2048) return DK_ERR_ARGS;
-    ImgBnDescE<bf16_t, true> ab;
-    static_cast<ImgDescE<bf16_t, true>&>(ab) = a;
-    ab.bn = BnIn{bn_mean, bn_invstd, bn_gamma, bn_beta, bn_relu};
-    return run(ab);
-  }
-  return run(a);
-}
-
-// Stride-1 pointwise dgrad (bf16): dx = dy . W (+ residual) and, with bn_x/part, the
-// BN-backward partials of the BatchNorm whose output the layer consumed.
-DK_API int dk_pwconv_dgrad_ex_bf16(const bf16_t* dy, int N, int OH, int OW, int K, const float* w_kc, int C,
-                                   int stride, bf16_t* dx, const bf16_t* residual, const bf16_t* bn_x,
-                                   const float* bn_mean, const float* bn_invstd, const float* bn_gamma,
-                                   const float* bn_beta, int bn_relu, double* part, void* stream) {
-  const int M = N * OH * OW;
-  if (stride != 1 || C % 4 || K % 4 || !al8(dy) || !al8(dx) || !aligned16(w_kc)) return DK_ERR_ARGS;
-  if ((residual && !al8(residual)) || (bn_x && !al8(bn_x))) return DK_ERR_ARGS;
-  if (!fits((size_t)M * K * 4) || !fits((size_t)M * C * 4) || (part != nullptr) != (bn_x != nullptr)) return DK_ERR_ARGS;
-  const MatDescE<bf16_t> a = mat_h(dy, M, K, M);
-  const MatDesc b = mat(w_kc, K, C, C);
-  const hipStream_t st = as_stream(stream);
-  if (!part) {
-    EpStoreT<bf16_t> ep{dx, C, nullptr, 1, residual};
-    return igemm_rows<LdMatKC, MatDescE<bf16_t>, LdMatIC, MatDesc, EpStoreT<bf16_t>>(a, b, ep, M, C, K, st);
-  }
-  if (!bn_ok(bn_mean, bn_invstd, bn_gamma, bn_beta)) return DK_ERR_ARGS;
-  EpStoreBnBwdT<bf16_t> ep{};
-  ep.out = dx, ep.ldo = C, ep.bias = nullptr, ep.v4 = 1, ep.res = residual;
-  ep.part = part;
-  ep.xbn = bn_x;
-  ep.bn = BnIn{bn_mean, bn_invstd, bn_gamma, bn_beta, bn_relu};
-  return igemm_rows<LdMatKC, MatDescE<bf16_t>, LdMatIC, MatDesc, EpStoreBnBwdT<bf16_t>>(a, b, ep, M, C, K, st);
-}
-
-// dw[k][c] = sum dy[m][k] * bn(x)[m][c] (+ l2 * w), bf16 activations, fp32 result.
-DK_API int dk_pwconv_wgrad_bnx_bf16(const bf16_t* dy, const bf16_t* x, int N, int H, int W, int C, int K, int stride,
-                                    int OH, int OW, const float* w_kc, float l2, float* dw_kc, void* ws,
-                                    size_t ws_bytes, const float* bn_mean, const float* bn_invstd,
-                                    const float* bn_gamma, const float* bn_beta, int bn_relu, void* stream) {
-  const int Kred = N * OH * OW;
-  if (C % 4 || K % 4 || !al8(x) || !al8(dy) || !fits((size_t)N * H * W * C * 4) || !fits((size_t)Kred * K * 4))
-    return DK_ERR_ARGS;
-  if (ws_bytes < splitk_ws_bytes(K, C, Kred)) return DK_ERR_WORKSPACE;
-  const MatDescE<bf16_t> a = mat_h(dy, Kred, K, K);
-  const ImgDescE<bf16_t> bi = img_h(x, N, H, W, C, OH, OW, 1, 1, stride, 1, 0, Kred);
-  float* part = static_cast<float*>(ws);
-  const hipStream_t st = as_stream(stream);
-  int splits = 1, rc;
-  if (bn_mean) {
-    if (!bn_ok(bn_mean, bn_invstd, bn_gamma, bn_beta)) return DK_ERR_ARGS;
-    ImgBnDescE<bf16_t> b;
-    static_cast<ImgDescE<bf16_t>&>(b) = bi;
-    b.bn = BnIn{bn_mean, bn_invstd, bn_gamma, bn_beta, bn_relu};
-    rc = igemm_splitk<LdMatIC, MatDescE<bf16_t>, LdImgIC, ImgBnDescE<bf16_t>>(a, b, part, K, C, Kred, st, &splits);
-  } else {
-    rc = igemm_splitk<LdMatIC, MatDescE<bf16_t>, LdImgIC, ImgDescE<bf16_t>>(a, bi, part, K, C, Kred, st, &splits);
-  }
-  if (rc) return rc;
-  return splitk_reduce(part, splits, K, C, dw_kc, w_kc, l2, 0, C, C, 1, 1, st);
-}

@@ -15,6 +15,7 @@ E = 4  # fp32
 
 PEAK_F32_TFLOPS = 157.3   # MI355X fp32 MFMA / vector, dense (MI355X_MICROARCH.md)
 PEAK_HBM_GBS = 8000.0     # MI355X HBM3E spec
+PEAK_BF16_TFLOPS = 2500.0  # MI355X bf16 MFMA, dense (no sparsity)
 
 
 def _conv_fwd(x, N, H, W, C, w, K, R, S, stride, pad, bias, y, OH, OW, st):
@@ -244,9 +245,22 @@ def work(name: str, args) -> tuple[int, int]:
     return f(*args)
 
 
-def bound_time_s(flops: float, nbytes: float) -> float:
+# Entry points whose flops run on bf16 MFMA (v_mfma_f32_32x32x16_bf16): their compute roof is the
+# bf16 dense peak; every other entry computes in fp32 (f32 MFMA or VALU, the same 157.3 TF/s).
+BF16_MFMA = {"dk_pwconv_fwd_ex_bf16", "dk_pwconv_dgrad_ex_bf16", "dk_pwconv_wgrad_bnx_bf16"}
+
+
+def peak_tflops(name: str | None = None) -> float:
+    return PEAK_BF16_TFLOPS if name in BF16_MFMA else PEAK_F32_TFLOPS
+
+
+def bound_time_s(flops: float, nbytes: float, name: str | None = None) -> float:
     """Roofline lower bound on time for one call: max(flops / peak, bytes / BW)."""
-    return max(flops / (PEAK_F32_TFLOPS * 1e12), nbytes / (PEAK_HBM_GBS * 1e9))
+    return max(flops / (peak_tflops(name) * 1e12), nbytes / (PEAK_HBM_GBS * 1e9))
+
+
+def is_mfma_bound(flops: float, nbytes: float, name: str | None = None) -> bool:
+    return flops / (peak_tflops(name) * 1e12) > nbytes / (PEAK_HBM_GBS * 1e9)
 
 
 def _half(f):
