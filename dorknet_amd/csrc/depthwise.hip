@@ -541,14 +541,17 @@ struct BnBwdOut {  // the BatchNorm after this layer: dy = bn_bwd_elem(x1, g)
   int relu;
 };
 
-template <bool BNX, bool STATS, bool RELU1, bool JOIN = false>
-__global__ __launch_bounds__(256) void dw_bwd_fused_kernel(const float* __restrict__ g, const float* __restrict__ x1,
-                                                           uint32_t bytes, BnBwdOut ob, const float* __restrict__ x,
+// T: activation storage (float, or bf16_t for BASELINE config 5): g, x1, x, dx and res are T,
+// dy stays fp32 (LDS ring), and the input BN's partials see dx as stored (rounded).
+template <bool BNX, bool STATS, bool RELU1, bool JOIN = false, class T = float>
+__global__ __launch_bounds__(256) void dw_bwd_fused_kernel(const T* __restrict__ g, const T* __restrict__ x1,
+                                                           uint32_t bytes, BnBwdOut ob, const T* __restrict__ x,
                                                            BnIn bn, const float* __restrict__ w_crs,
-                                                           float* __restrict__ dx, const float* __restrict__ res,
+                                                           T* __restrict__ dx, const T* __restrict__ res,
                                                            double* __restrict__ spart, float* __restrict__ wpart,
                                                            int N, int H, int W, int C, int CL, FoldTail ft,
                                                            JoinBwd jn = JoinBwd{}) {
+  static_assert(!(JOIN && sizeof(T) != 4), "the join fusion is fp32 only");
   static_assert(!STATS || BNX, "input-BN partials need the input BN");
   static_assert(!(JOIN && (STATS || BNX)), "the join's partials replace the input BN's");
   constexpr bool PART = STATS || JOIN;
@@ -645,15 +648,15 @@ __global__ __launch_bounds__(256) void dw_bwd_fused_kernel(const float* __restri
   uint32_t jmv = 0;
   auto load_dy_row = [&](int hh) {
     const bool rok = (unsigned)hh < (unsigned)H;
-    g0 = bload4e<float>(rg, rok && cok0, pix(hh, col0));
-    x0 = bload4e<float>(r1, rok && cok0, pix(hh, col0));
-    g1 = bload4e<float>(rg, rok && cok1, pix(hh, col1));
-    x1v = bload4e<float>(r1, rok && cok1, pix(hh, col1));
+    g0 = bload4e<T>(rg, rok && cok0, pix(hh, col0));
+    x0 = bload4e<T>(r1, rok && cok0, pix(hh, col0));
+    g1 = bload4e<T>(rg, rok && cok1, pix(hh, col1));
+    x1v = bload4e<T>(r1, rok && cok1, pix(hh, col1));
   };
   auto load_x_row = [&](int hh) {
     const bool ok = win_ok && hh < H;
-    xr = bload4e<float>(rx, ok, pix(hh, w));
-    rv = bload4e<float>(rres, ok, pix(hh, w));
+    xr = bload4e<T>(rx, ok, pix(hh, w));
+    rv = bload4e<T>(rres, ok, pix(hh, w));
     if constexpr (JOIN) {
       jmv = __builtin_amdgcn_raw_buffer_load_b32(rjm, (int)(ok ? pix(hh, w) : kOOBBytes), 0, 0);  // 4 mask bytes
       jxv = bload4e<float>(rjx, ok, pix(hh, w));
@@ -671,7 +674,7 @@ __global__ __launch_bounds__(256) void dw_bwd_fused_kernel(const float* __restri
     }
   load_dy_row(0);  // row -1 is all padding
   load_x_row(0);
-  float* dxcol = dx ? dx + (size_t)pix(0, w) : nullptr;
+  T* dxcol = dx ? dx + (size_t)pix(0, w) : nullptr;
   for (int rr = 0; rr <= H; ++rr) {  // publish dy row rr, then finish dx row rr - 1
     const int rowok = rr < H;
     const f32x4 d0 = xform(g0, x0, rowok && cok0), d1 = xform(g1, x1v, rowok && cok1);
@@ -703,6 +706,7 @@ __global__ __launch_bounds__(256) void dw_bwd_fused_kernel(const float* __restri
       }
     if (win_ok) {
       if (res) acc += rh;
+      acc = rnd4<T>(acc);  // what the store keeps (identity for fp32)
       if constexpr (JOIN) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
@@ -1082,13 +1086,14 @@ DK_API size_t dk_dwconv_bwd_bnbwd_workspace_bytes(int N, int H, int W, int C, in
   return (size_t)dk_dwconv_bwd_bnbwd_stats_rows(N, H, W, C) * C * R * S * sizeof(float);
 }
 
-DK_API int dk_dwconv_bwd_bnbwd_f32(const float* g, const float* bn_x, int N, int H, int W, int C,
-                                   const float* out_mean, const float* out_invstd, const float* out_gamma,
-                                   const float* out_beta, int out_relu, const float* k12, const float* x,
-                                   const float* w_crs, int R, int S, int pad, float l2, float* dw_crs, float* dx,
-                                   const float* residual, const float* bn_mean, const float* bn_invstd,
-                                   const float* bn_gamma, const float* bn_beta, int bn_relu, double* part,
-                                   void* ws, size_t ws_bytes, void* stream) {
+namespace dk {
+template <class T>
+static int dw_bwd_fused(const T* g, const T* bn_x, int N, int H, int W, int C, const float* out_mean,
+                        const float* out_invstd, const float* out_gamma, const float* out_beta, int out_relu,
+                        const float* k12, const T* x, const float* w_crs, int R, int S, int pad, float l2,
+                        float* dw_crs, T* dx, const T* residual, const float* bn_mean, const float* bn_invstd,
+                        const float* bn_gamma, const float* bn_beta, int bn_relu, double* part, void* ws,
+                        size_t ws_bytes, void* stream) {
   const hipStream_t st = as_stream(stream);
   if (R != 3 || S != 3 || pad != 1 || C % 4 || N < 1 || H < 1 || W < 1) return DK_ERR_ARGS;
   const int cl = dwb_cl(W, C);
@@ -1100,7 +1105,7 @@ DK_API int dk_dwconv_bwd_bnbwd_f32(const float* g, const float* bn_x, int N, int
       (residual && !aligned16(residual)) || !bn_ok(bn) || !aligned16(out_mean) || !aligned16(out_invstd) ||
       !aligned16(out_gamma) || !aligned16(out_beta) || !aligned16(k12) || !aligned16(w_crs))
     return DK_ERR_ARGS;
-  const size_t bytes = (size_t)N * H * W * C * sizeof(float);
+  const size_t bytes = (size_t)N * H * W * C * sizeof(T);
   if (!fits(bytes)) return DK_ERR_ARGS;
   if (ws_bytes < dk_dwconv_bwd_bnbwd_workspace_bytes(N, H, W, C, R, S)) return DK_ERR_WORKSPACE;
   const int strips = dwb_strips(N, W, cl);
@@ -1115,7 +1120,7 @@ DK_API int dk_dwconv_bwd_bnbwd_f32(const float* g, const float* bn_x, int N, int
   if (ring > shm) shm = ring;
 #define DWB_LAUNCH(BNX_, STATS_, RELU1_)                                                                             \
   {                                                                                                                  \
-    auto k = dw_bwd_fused_kernel<BNX_, STATS_, RELU1_>;                                                              \
+    auto k = dw_bwd_fused_kernel<BNX_, STATS_, RELU1_, false, T>;                                                    \
     if (shm > 65536)                                                                                                 \
       (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,       \
                                 (int)shm);                                                                           \
@@ -1134,6 +1139,32 @@ DK_API int dk_dwconv_bwd_bnbwd_f32(const float* g, const float* bn_x, int N, int
   if (rc) return rc;
   return fold_status(
       splitk_reduce(wpart, strips, 1, C * R * S, dw_crs, l2 != 0.f ? w_crs : nullptr, l2, 0, C, C, 1, 1, st), ft);
+}
+}  // namespace dk
+
+DK_API int dk_dwconv_bwd_bnbwd_f32(const float* g, const float* bn_x, int N, int H, int W, int C,
+                                   const float* out_mean, const float* out_invstd, const float* out_gamma,
+                                   const float* out_beta, int out_relu, const float* k12, const float* x,
+                                   const float* w_crs, int R, int S, int pad, float l2, float* dw_crs, float* dx,
+                                   const float* residual, const float* bn_mean, const float* bn_invstd,
+                                   const float* bn_gamma, const float* bn_beta, int bn_relu, double* part,
+                                   void* ws, size_t ws_bytes, void* stream) {
+  return dw_bwd_fused(g, bn_x, N, H, W, C, out_mean, out_invstd, out_gamma, out_beta, out_relu, k12, x, w_crs, R, S,
+                      pad, l2, dw_crs, dx, residual, bn_mean, bn_invstd, bn_gamma, bn_beta, bn_relu, part, ws,
+                      ws_bytes, stream);
+}
+
+// bf16 storage twin (BASELINE config 5): g, bn_x, x, dx, residual bf16; dy formed in fp32.
+DK_API int dk_dwconv_bwd_bnbwd_bf16(const bf16_t* g, const bf16_t* bn_x, int N, int H, int W, int C,
+                                    const float* out_mean, const float* out_invstd, const float* out_gamma,
+                                    const float* out_beta, int out_relu, const float* k12, const bf16_t* x,
+                                    const float* w_crs, int R, int S, int pad, float l2, float* dw_crs, bf16_t* dx,
+                                    const bf16_t* residual, const float* bn_mean, const float* bn_invstd,
+                                    const float* bn_gamma, const float* bn_beta, int bn_relu, double* part,
+                                    void* ws, size_t ws_bytes, void* stream) {
+  return dw_bwd_fused(g, bn_x, N, H, W, C, out_mean, out_invstd, out_gamma, out_beta, out_relu, k12, x, w_crs, R, S,
+                      pad, l2, dw_crs, dx, residual, bn_mean, bn_invstd, bn_gamma, bn_beta, bn_relu, part, ws,
+                      ws_bytes, stream);
 }
 
 // Rows of join partials dk_dwconv_dgrad_join_f32 writes (0: the geometry has no join variant).

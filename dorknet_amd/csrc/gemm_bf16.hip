@@ -116,3 +116,44 @@ DK_API int dk_pwconv_wgrad_bnx_bf16(const bf16_t* dy, const bf16_t* x, int N, in
   return splitk_reduce(part, splits, K, C, dw_kc, w_kc, l2, 0, C, C, 1, 1, st);
 }
 
+DK_API int dk_pwconv_dgrad_bnbwd_bf16_stats_rows(int N, int OH, int OW, int K, int C) {
+  return stats_rows(N * OH * OW, C, K, kRowBnBwd);
+}
+
+// dk_pwconv_dgrad_bnbwd_f32 for bf16 storage: dy = the following BatchNorm's backward applied
+// to (g, bn_x) as they are loaded (fp32), rounded to bf16 as the MFMA operand and as stored to
+// dy_out (nullable) for the weight gradient; dx = dy . W (+ residual) stored bf16 with, given
+// x / part, the input BatchNorm's backward partials over the stored dx.  Stride 1.
+DK_API int dk_pwconv_dgrad_bnbwd_bf16(const bf16_t* g, const bf16_t* bn_x, int N, int OH, int OW, int K,
+                                      const float* out_mean, const float* out_invstd, const float* out_gamma,
+                                      const float* out_beta, int out_relu, const float* k12, bf16_t* dy_out,
+                                      const float* w_kc, int C, bf16_t* dx, const bf16_t* residual, const bf16_t* x,
+                                      const float* bn_mean, const float* bn_invstd, const float* bn_gamma,
+                                      const float* bn_beta, int bn_relu, double* part, void* stream) {
+  const int M = N * OH * OW;
+  if (C % 4 || K % 4 || !al8(g) || !al8(bn_x) || !al8(dx) || (dy_out && !al8(dy_out)) || !aligned16(w_kc))
+    return DK_ERR_ARGS;
+  if ((residual && !al8(residual)) || (x && !al8(x))) return DK_ERR_ARGS;
+  if (!fits((size_t)M * K * 4) || !fits((size_t)M * C * 4) || (part != nullptr) != (x != nullptr)) return DK_ERR_ARGS;
+  if (!out_mean || !out_invstd || !out_gamma || !out_beta || !k12 || (size_t)K * 32 > 64 * 1024) return DK_ERR_ARGS;
+  MatBwdDescE<bf16_t> a;
+  static_cast<MatDescE<bf16_t>&>(a) = mat_h(g, M, K, M);
+  a.x = bn_x;
+  a.bwd = BnBwdIn{out_mean, out_invstd, out_gamma, out_beta, k12, out_relu, K};
+  a.dy_out = dy_out;
+  const MatDesc b = mat(w_kc, K, C, C);
+  const hipStream_t st = as_stream(stream);
+  if (!part) {
+    EpStoreT<bf16_t> ep{dx, C, nullptr, 1, residual};
+    return igemm_rows<LdMatKC, MatBwdDescE<bf16_t>, LdMatIC, MatDesc, EpStoreT<bf16_t>, kRowBnBwd, kMfBf16>(
+        a, b, ep, M, C, K, st);
+  }
+  if (!bn_ok(bn_mean, bn_invstd, bn_gamma, bn_beta)) return DK_ERR_ARGS;
+  EpStoreBnBwdT<bf16_t> ep{};
+  ep.out = dx, ep.ldo = C, ep.bias = nullptr, ep.v4 = 1, ep.res = residual;
+  ep.part = part;
+  ep.xbn = x;
+  ep.bn = BnIn{bn_mean, bn_invstd, bn_gamma, bn_beta, bn_relu};
+  return igemm_rows<LdMatKC, MatBwdDescE<bf16_t>, LdMatIC, MatDesc, EpStoreBnBwdT<bf16_t>, kRowBnBwd, kMfBf16>(
+      a, b, ep, M, C, K, st);
+}

@@ -120,12 +120,14 @@ struct BnBwdIn {
   int relu;
   int C;
 };
-struct MatBwdDesc : MatDescE<float> {
+template <class E>
+struct MatBwdDescE : MatDescE<E> {
   static constexpr bool kBnBwd = true;
-  const float* x;
+  const E* x;       // the BN's raw input, laid out like p (same element type)
   BnBwdIn bwd;
-  float* dy_out;
+  E* dy_out;        // dy write-through (rounded to E when E is bf16)
 };
+using MatBwdDesc = MatBwdDescE<float>;
 
 // ----------------------------------------------------------------------------
 // Loaders.  K-contiguous ("KC") loaders fill T[ROWS][BK+4]; row-contiguous ("IC")
@@ -293,7 +295,7 @@ struct LdMatKCT : KCLayout<ROWS, BK> {
   f32x4 xv[NR];
   const f32x4* tab;
   int tc;  // table stride (channels)
-  float* dyo;
+  void* dyo;  // D::Elem* (MatBwdDescE)
   bool writer;
   int kcur;
   uint32_t eoff[NR];
@@ -323,7 +325,7 @@ struct LdMatKCT : KCLayout<ROWS, BK> {
         v[j] = bload4e<typename D::Elem>(rs, iv && k < Ktot, (uint32_t)(i * d.ld + k));
         if constexpr (D::kBnBwd) {
           const __amdgpu_buffer_rsrc_t rx = make_rsrc_v(d.x, d.bytes);
-          xv[j] = bload4e<float>(rx, iv && k < Ktot, (uint32_t)(i * d.ld + k));
+          xv[j] = bload4e<typename D::Elem>(rx, iv && k < Ktot, (uint32_t)(i * d.ld + k));
           eoff[j] = (uint32_t)(i * d.ld + k);
           om |= (uint32_t)(iv && k < Ktot) << j;
         }
@@ -359,7 +361,7 @@ struct LdMatKCT : KCLayout<ROWS, BK> {
             o[e] = bn_bwd_elem(xe, ge, mu[e], is[e], ff[e], k1[e], k2[e]);
           }
           v[j] = o;
-          if (writer) st4(dyo + eoff[j], o);
+          if (writer) st4(static_cast<typename D::Elem*>(dyo) + eoff[j], o);
         }
       }
     }
@@ -390,7 +392,7 @@ struct LdMatICT : ICLayout<ROWS, BK> {
   uint32_t okm;
   const f32x4* tab;
   int tc;  // table stride (channels)
-  float* dyo;
+  void* dyo;
   bool writer;
   int relu_flag = 0;
 
@@ -417,7 +419,7 @@ struct LdMatICT : ICLayout<ROWS, BK> {
         v[j] = bload4e<typename D::Elem>(rs, kv && i0 < d.ext, (uint32_t)(k * d.ld + i0));
         if constexpr (D::kBnBwd) {
           const __amdgpu_buffer_rsrc_t rx = make_rsrc_v(d.x, d.bytes);
-          xv[j] = bload4e<float>(rx, kv && i0 < d.ext, (uint32_t)(k * d.ld + i0));
+          xv[j] = bload4e<typename D::Elem>(rx, kv && i0 < d.ext, (uint32_t)(k * d.ld + i0));
           om |= (uint32_t)(kv && i0 < d.ext) << j;
         }
       } else {

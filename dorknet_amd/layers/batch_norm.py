@@ -283,7 +283,7 @@ class BatchNormLayer(Layer):
                 dist.all_reduce(glob, group=self.sync_group)
                 lib.dk_bn_bwd_finalize_f32(local.data_ptr(), 1, glob.data_ptr(), 1, C, float(P) * self._world(),
                                            dgamma.data_ptr(), dbeta.data_ptr(), k12.data_ptr(), st)
-            if defer and not bf:
+            if defer:
                 return BNGrad(dy, x, self._mean, self._invstd, gamma, beta, relu, k12, lattice=lattice)
             (lib.dk_bn_bwd_apply_bf16 if bf else lib.dk_bn_bwd_apply_f32)(
                 x.data_ptr(), dy.data_ptr(), x.numel(), C, self._mean.data_ptr(), self._invstd.data_ptr(),

@@ -114,7 +114,7 @@ class DepthwiseConvLayer(Layer):
 
     def _takes_bn_grad(self, bx):
         x = self.X
-        if x.dim() != 4 or bx.dim() != 4 or x.dtype != torch.float32 or bx.dtype != torch.float32:
+        if x.dim() != 4 or bx.dim() != 4 or x.dtype not in (torch.float32, BF16) or bx.dtype != x.dtype:
             return False
         C = x.shape[1]
         return (self.stride == 1 and self.f_rows == 3 and self.f_cols == 3 and self.padding == 1
@@ -195,11 +195,12 @@ class DepthwiseConvLayer(Layer):
             part = torch.empty((rows, 2, C), dtype=torch.float64, device=x.device)
         g = to_nhwc(G.g)
         nb = lib.dk_dwconv_bwd_bnbwd_workspace_bytes(N, H, W, C, R, S)
-        tok = bn.arm_partials(part) if part is not None else None
-        r = lib.dk_dwconv_bwd_bnbwd_f32(g.data_ptr(), G.x.data_ptr(), N, H, W, C, *G.bnbwd_args(), x.data_ptr(),
-                                        w.data_ptr(), R, S, self.padding, s or 0.0, gw.data_ptr(), ptr(dx), ptr(res),
-                                        *(bn.bn_args() if bn is not None else (0, 0, 0, 0, 0)), ptr(part),
-                                        workspace.get(nb), nb, st)
+        bf = x.dtype == BF16
+        tok = bn.arm_partials(part) if part is not None and not bf else None
+        r = (lib.dk_dwconv_bwd_bnbwd_bf16 if bf else lib.dk_dwconv_bwd_bnbwd_f32)(
+            g.data_ptr(), G.x.data_ptr(), N, H, W, C, *G.bnbwd_args(), x.data_ptr(), w.data_ptr(), R, S,
+            self.padding, s or 0.0, gw.data_ptr(), ptr(dx), ptr(res),
+            *(bn.bn_args() if bn is not None else (0, 0, 0, 0, 0)), ptr(part), workspace.get(nb), nb, st)
         if s is None:
             add_regulariser_grad(gw, w, self.weight_regulariser)
         if not need_dx:

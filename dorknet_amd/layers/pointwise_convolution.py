@@ -120,18 +120,19 @@ class PointwiseConvLayer(Layer):
 
     def accepts_bn_grad(self, bn_layer):
         """backward(BNGrad): the following BatchNorm's apply runs in this layer's dgrad loader
-        (dk_pwconv_dgrad_bnbwd_f32) -- fp32, stride 1, 4-D, channel counts the 16-byte loads
-        and the LDS coefficient table take."""
+        (dk_pwconv_dgrad_bnbwd_f32, or _bf16 for bf16 storage) -- stride 1, 4-D, channel counts
+        the 16-byte loads and the LDS coefficient table take."""
         x = getattr(self, "X", None)
         bx = getattr(bn_layer, "X", None)
-        return (x is not None and bx is not None and x.dtype == torch.float32 and self.stride == 1
+        return (x is not None and bx is not None and x.dtype in (torch.float32, BF16) and self.stride == 1
                 and x.dim() == 4 and x.shape[1] == self.num_channels and self._takes_bn_grad(bx))
 
     def _takes_bn_grad(self, bx):
-        return (bx.dim() == 4 and bx.dtype == torch.float32 and self.stride == 1 and self.X.dtype == torch.float32
-                and self.X.shape[1] == self.num_channels
+        bf = self.X.dtype == BF16
+        return (bx.dim() == 4 and bx.dtype == self.X.dtype and self.X.dtype in (torch.float32, BF16)
+                and self.stride == 1 and self.X.shape[1] == self.num_channels
                 and tuple(bx.shape) == (self.X.shape[0], self.num_filters, *self.out_hw)
-                and self.num_filters % 4 == 0 and self.num_filters <= 2048)
+                and self.num_filters % 4 == 0 and self.num_filters <= 2048 and not (bf and self.with_bias))
 
     skips_input_grad = True  # backward(dy, need_dx=False): parameter gradients only (chain_backward)
 
@@ -164,9 +165,10 @@ class PointwiseConvLayer(Layer):
                 return self._bwd_fused(upstream_dx, residual, st)
             if need_dx and self._takes_bn_grad(upstream_dx.x):
                 # dgrad first: it forms (and stores) dy from the BatchNorm's gradient as it loads it
-                dy = empty_nhwc(N, K, OH, OW)
-                dx = self._dgrad_bnbwd(upstream_dx, dy, residual, st)
-                self._wgrad(dy, x, N, H, W, C, K, s, OH, OW, P, w, False)
+                bf = x.dtype == BF16
+                dy = empty_nhwc(N, K, OH, OW, x.dtype)
+                dx = (self._dgrad_bnbwd_bf16 if bf else self._dgrad_bnbwd)(upstream_dx, dy, residual, st)
+                self._wgrad(dy, x, N, H, W, C, K, s, OH, OW, P, w, bf)
                 return dx
             upstream_dx = upstream_dx.materialize()
         dy = to_nhwc(upstream_dx)
@@ -244,7 +246,7 @@ class PointwiseConvLayer(Layer):
         forces it on / off.  The round-1 tiled fused kernel (K or C = 128) was measured 0.75 %
         slower on the step than the unfused pair, so it is not the default."""
         x = self.X
-        if self.with_bias or not self._takes_bn_grad(bg.x):
+        if self.with_bias or x.dtype != torch.float32 or not self._takes_bn_grad(bg.x):
             return False
         N, C, H, W = x.shape
         OH, OW = self.out_hw
@@ -315,6 +317,30 @@ class PointwiseConvLayer(Layer):
             bn.hand_backward_partials(dx, part, r, tok)
         if residual is not None and res is None:
             dx = add_residual(dx, residual)
+        return dx
+
+    def _dgrad_bnbwd_bf16(self, bg, dy_out, residual, st):
+        """bf16 storage: dk_pwconv_dgrad_bnbwd_bf16 (dy formed on load, rounded to bf16 for the
+        MFMA and for dy_out; the input BatchNorm's partials over the stored dx)."""
+        x = self.X
+        N, C, H, W = x.shape
+        K = self.num_filters
+        OH, OW = self.out_hw
+        dx = empty_nhwc(N, C, OH, OW, x.dtype)
+        bn = self._bn_in
+        res = residual_operand(residual, dx)
+        if residual is not None and res is None:
+            raise NotImplementedError("{}: bf16 residual must be a bf16 NHWC tensor".format(self.layer_name))
+        part = None
+        if bn is not None:
+            rows = lib.dk_pwconv_dgrad_bnbwd_bf16_stats_rows(N, OH, OW, K, C)
+            part = torch.empty((rows, 2, C), dtype=torch.float64, device=dx.device)
+        lib.dk_pwconv_dgrad_bnbwd_bf16(to_nhwc(bg.g).data_ptr(), bg.x.data_ptr(), N, OH, OW, K, *bg.bnbwd_args(),
+                                       dy_out.data_ptr(), self.learned_params["weights"].data_ptr(), C, dx.data_ptr(),
+                                       ptr(res), *((bn.x.data_ptr(), *bn.bn_args(), part.data_ptr()) if bn is not None
+                                                   else (0, 0, 0, 0, 0, 0, 0)), st)
+        if bn is not None:
+            bn.hand_backward_partials(dx, part)
         return dx
 
     def _wgrad(self, dy, x, N, H, W, C, K, s, OH, OW, P, w, bf):

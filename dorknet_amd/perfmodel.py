@@ -247,7 +247,8 @@ def work(name: str, args) -> tuple[int, int]:
 
 # Entry points whose flops run on bf16 MFMA (v_mfma_f32_32x32x16_bf16): their compute roof is the
 # bf16 dense peak; every other entry computes in fp32 (f32 MFMA or VALU, the same 157.3 TF/s).
-BF16_MFMA = {"dk_pwconv_fwd_ex_bf16", "dk_pwconv_dgrad_ex_bf16", "dk_pwconv_wgrad_bnx_bf16"}
+BF16_MFMA = {"dk_pwconv_fwd_ex_bf16", "dk_pwconv_dgrad_ex_bf16", "dk_pwconv_wgrad_bnx_bf16",
+             "dk_pwconv_dgrad_bnbwd_bf16"}
 
 
 def peak_tflops(name: str | None = None) -> float:
@@ -275,6 +276,6 @@ def _half(f):
 
 for _n in ("dk_pwconv_fwd_ex", "dk_pwconv_dgrad_ex", "dk_pwconv_wgrad_bnx", "dk_dwconv_fwd_ex", "dk_dwconv_dgrad_ex",
            "dk_dwconv_wgrad_bnx", "dk_bn_stats", "dk_bn_apply", "dk_bn_bwd", "dk_bn_bwd_apply", "dk_relu_fwd",
-           "dk_relu_bwd"):
+           "dk_relu_bwd", "dk_pwconv_dgrad_bnbwd", "dk_dwconv_bwd_bnbwd"):
     if _n + "_f32" in MODEL:
         MODEL[_n + "_bf16"] = _half(MODEL[_n + "_f32"])

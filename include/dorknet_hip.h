@@ -229,7 +229,15 @@ int dk_pwconv_dgrad_ex_bf16(const uint16_t* dy, int N, int OH, int OW, int K, co
 int dk_pwconv_wgrad_bnx_bf16(const uint16_t* dy, const uint16_t* x, int N, int H, int W, int C, int K, int stride, int OH, int OW, const float* w_kc, float l2, float* dw_kc, void* ws, size_t ws_bytes, const float* bn_mean, const float* bn_invstd, const float* bn_gamma, const float* bn_beta, int bn_relu, void* stream);
 int dk_dwconv_fwd_ex_bf16(const uint16_t* x, int N, int H, int W, int C, const float* w_crs, int R, int S, int stride, int pad, const float* bias, uint16_t* y, int OH, int OW, const float* bn_mean, const float* bn_invstd, const float* bn_gamma, const float* bn_beta, int bn_relu, double* stats, void* stream);
 int dk_dwconv_dgrad_ex_bf16(const uint16_t* dy, int N, int OH, int OW, int C, const float* w_crs, int R, int S, int stride, int pad, uint16_t* dx, int H, int W, void* ws, size_t ws_bytes, const uint16_t* residual, const uint16_t* bn_x, const float* bn_mean, const float* bn_invstd, const float* bn_gamma, const float* bn_beta, int bn_relu, double* part, void* stream);
-int dk_dwconv_wgrad_bnx_bf16(const uint16_t* dy, const uint16_t* x, int N, int H, int W, int C, int R, int S, int stride, int pad, int OH, int OW, const float* w_crs, float l2, float* dw_crs, void* ws, size_t ws_bytes, const float* bn_mean, const float* bn_invstd, const float* bn_gamma, const float* bn_beta, int bn_relu, void* stream);
+
+/* BatchNorm-backward-on-load fusions for bf16 storage (as dk_pwconv_dgrad_bnbwd_f32 and
+ * dk_dwconv_bwd_bnbwd_f32; reference layers/pointwise_convolution.py:57-75,
+ * layers/depthwise_convolution.py:198-221, layers/batch_norm.py:125-174): dy is formed in fp32
+ * from the following BN's gradient g and input bn_x; the pointwise dgrad rounds it to bf16 as its
+ * MFMA operand and as written to dy_out; the depthwise backward keeps it fp32. */
+int dk_pwconv_dgrad_bnbwd_bf16_stats_rows(int N, int OH, int OW, int K, int C);
+int dk_pwconv_dgrad_bnbwd_bf16(const uint16_t* g, const uint16_t* bn_x, int N, int OH, int OW, int K, const float* out_mean, const float* out_invstd, const float* out_gamma, const float* out_beta, int out_relu, const float* k12, uint16_t* dy_out, const float* w_kc, int C, uint16_t* dx, const uint16_t* residual, const uint16_t* x, const float* bn_mean, const float* bn_invstd, const float* bn_gamma, const float* bn_beta, int bn_relu, double* part, void* stream);
+int dk_dwconv_bwd_bnbwd_bf16(const uint16_t* g, const uint16_t* bn_x, int N, int H, int W, int C, const float* out_mean, const float* out_invstd, const float* out_gamma, const float* out_beta, int out_relu, const float* k12, const uint16_t* x, const float* w_crs, int R, int S, int pad, float l2, float* dw_crs, uint16_t* dx, const uint16_t* residual, const float* bn_mean, const float* bn_invstd, const float* bn_gamma, const float* bn_beta, int bn_relu, double* part, void* ws, size_t ws_bytes, void* stream);int dk_dwconv_wgrad_bnx_bf16(const uint16_t* dy, const uint16_t* x, int N, int H, int W, int C, int R, int S, int stride, int pad, int OH, int OW, const float* w_crs, float l2, float* dw_crs, void* ws, size_t ws_bytes, const float* bn_mean, const float* bn_invstd, const float* bn_gamma, const float* bn_beta, int bn_relu, void* stream);
 
 /* ---------------------------------------------------------------------------------------
  * Depthwise convolution, direct (no MFMA).

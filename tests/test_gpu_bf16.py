@@ -193,3 +193,85 @@ def test_mobilenet_stack_bf16_vs_oracle(monkeypatch, fuse):
             # the remaining differences are rounding-boundary flips of the same size
             assert err <= max(1e-2, sens), report[-1]
     assert max(r[2] for r in report) > 0
+
+
+def _bn(C, rng):
+    return [torch.as_tensor(v.astype(np.float32), device="cuda") for v in
+            (rng.randn(C) * 0.3, rng.rand(C) + 0.5, 1 + 0.3 * rng.randn(C), 0.2 * rng.randn(C))]
+
+
+def _h(a):
+    return nhwc(torch.as_tensor(np.ascontiguousarray(a, dtype=np.float32), device="cuda").to(BF16))
+
+
+@pytest.mark.parametrize("relu", [0, 1])
+def test_bf16_bnbwd_fusions_match_unfused(relu):
+    """The BatchNorm-backward-on-load fusions of the bf16 path against the unfused sequence
+    (dk_bn_bwd_apply_bf16 writing dy, then the dgrad / wgrad on it):
+      * pointwise dgrad (dk_pwconv_dgrad_bnbwd_bf16): dy is rounded to bf16 exactly as the apply
+        pass stores it, so dy_out is bit-identical and dx agrees to the MFMA accumulation order;
+      * depthwise backward (dk_dwconv_bwd_bnbwd_bf16): dy stays fp32 (never stored), so dx, the
+        weight gradient and the input BN's partials differ from the unfused path by dy's bf16
+        rounding only -- normwise <= 1e-2."""
+    rng = np.random.RandomState(11 + relu)
+    N, H, W, C, K = 3, 14, 10, 64, 128
+    st = stream_handle()
+    # pointwise C -> K; its output xo fed a BN(+ReLU) whose output gradient is g
+    xo, g = _h(rng.randn(N, K, H, W)), _h(rng.randn(N, K, H, W))
+    po = _bn(K, rng)
+    k12 = torch.as_tensor(rng.randn(2 * K).astype(np.float32) * 0.1, device="cuda")
+    w = torch.as_tensor(rng.randn(K, C).astype(np.float32) * 0.1, device="cuda")
+    xin = _h(rng.randn(N, C, H, W))
+    pi = _bn(C, rng)
+    dy0 = torch.empty_like(g)
+    lib.dk_bn_bwd_apply_bf16(xo.data_ptr(), g.data_ptr(), g.numel(), K, *(t.data_ptr() for t in po), relu,
+                             k12.data_ptr(), dy0.data_ptr(), st)
+    dx0 = torch.empty_like(xin)
+    rows0 = lib.dk_pwconv_dgrad_stats_rows(N, H, W, K, C)
+    part0 = torch.zeros((rows0, 2, C), dtype=torch.float64, device="cuda")
+    lib.dk_pwconv_dgrad_ex_bf16(dy0.data_ptr(), N, H, W, K, w.data_ptr(), C, 1, dx0.data_ptr(), 0, xin.data_ptr(),
+                                *(t.data_ptr() for t in pi), 1, part0.data_ptr(), st)
+    dy1, dx1 = torch.empty_like(g), torch.empty_like(xin)
+    rows1 = lib.dk_pwconv_dgrad_bnbwd_bf16_stats_rows(N, H, W, K, C)
+    part1 = torch.zeros((rows1, 2, C), dtype=torch.float64, device="cuda")
+    lib.dk_pwconv_dgrad_bnbwd_bf16(g.data_ptr(), xo.data_ptr(), N, H, W, K, *(t.data_ptr() for t in po), relu,
+                                   k12.data_ptr(), dy1.data_ptr(), w.data_ptr(), C, dx1.data_ptr(), 0,
+                                   xin.data_ptr(), *(t.data_ptr() for t in pi), 1, part1.data_ptr(), st)
+    torch.cuda.synchronize()
+    assert torch.equal(dy0, dy1)
+    assert rel_err(host(dx1), host(dx0)) <= 1e-5
+    s0, s1 = part0.sum(0), part1.sum(0)
+    assert float((s1 - s0).norm() / s0.norm()) < 1e-4
+
+    # depthwise 3x3 stride 1 on C channels, its output x1 fed a BN(+ReLU) with output gradient g1
+    x = _h(rng.randn(N, C, H, W))
+    x1, g1 = _h(rng.randn(N, C, H, W)), _h(rng.randn(N, C, H, W))
+    po = _bn(C, rng)
+    k12 = torch.as_tensor(rng.randn(2 * C).astype(np.float32) * 0.1, device="cuda")
+    wd = torch.as_tensor(rng.randn(C, 3, 3).astype(np.float32) * 0.3, device="cuda")
+    dyd = torch.empty_like(g1)
+    lib.dk_bn_bwd_apply_bf16(x1.data_ptr(), g1.data_ptr(), g1.numel(), C, *(t.data_ptr() for t in po), relu,
+                             k12.data_ptr(), dyd.data_ptr(), st)
+    nbd = lib.dk_dwconv_dgrad_workspace_bytes(C, 3, 3)
+    rowsd = lib.dk_dwconv_dgrad_stats_rows(N, H, W, C, 1)
+    pd0 = torch.zeros((rowsd, 2, C), dtype=torch.float64, device="cuda")
+    dxd0 = torch.empty_like(x)
+    lib.dk_dwconv_dgrad_ex_bf16(dyd.data_ptr(), N, H, W, C, wd.data_ptr(), 3, 3, 1, 1, dxd0.data_ptr(), H, W,
+                                workspace.get(nbd), nbd, 0, xin.data_ptr(), *(t.data_ptr() for t in pi), 1,
+                                pd0.data_ptr(), st)
+    dw0 = torch.empty_like(wd)
+    nbw = lib.dk_dwconv_wgrad_workspace_bytes(N, H, W, C, 3, 3)
+    lib.dk_dwconv_wgrad_bnx_bf16(dyd.data_ptr(), x.data_ptr(), N, H, W, C, 3, 3, 1, 1, H, W, 0, 0.0, dw0.data_ptr(),
+                                 workspace.get(nbw), nbw, 0, 0, 0, 0, 0, st)
+    torch.cuda.synchronize()
+    rows = lib.dk_dwconv_bwd_bnbwd_stats_rows(N, H, W, C)
+    pd1 = torch.zeros((rows, 2, C), dtype=torch.float64, device="cuda")
+    dxd1, dw1 = torch.empty_like(x), torch.empty_like(wd)
+    nb = lib.dk_dwconv_bwd_bnbwd_workspace_bytes(N, H, W, C, 3, 3)
+    # x as the layer input (no input BN on load, no input-BN partials)
+    lib.dk_dwconv_bwd_bnbwd_bf16(g1.data_ptr(), x1.data_ptr(), N, H, W, C, *(t.data_ptr() for t in po), relu,
+                                 k12.data_ptr(), x.data_ptr(), wd.data_ptr(), 3, 3, 1, 0.0, dw1.data_ptr(),
+                                 dxd1.data_ptr(), 0, 0, 0, 0, 0, 0, 0, workspace.get(nb), nb, st)
+    torch.cuda.synchronize()
+    assert rel_err(host(dxd1), host(dxd0)) <= 1e-2
+    assert rel_err(host(dw1), host(dw0)) <= 1e-2
