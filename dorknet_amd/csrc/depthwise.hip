@@ -109,7 +109,7 @@ __global__ __launch_bounds__(256) void dw_fwd_kernel(const T* __restrict__ x, ui
                                                      T* __restrict__ y, int N, int H, int W, int C, int OH, int OW,
                                                      int pad, BnIn bn, double* __restrict__ part,
                                                      const T* __restrict__ xo, BnIn obn,
-                                                     const T* __restrict__ res, FoldTail ft) {
+                                                     const T* __restrict__ res, FoldTail ft, int nt) {
   constexpr int TW = DwTile<ST>::TW, SEG = DwTile<ST>::SEG;
   constexpr int NC = (TW - 1) * ST + S;
   const int C4 = C >> 2;
@@ -191,7 +191,10 @@ __global__ __launch_bounds__(256) void dw_fwd_kernel(const T* __restrict__ x, ui
             if (res) acc += rv[j];  // residual addend
           }
           acc = rnd4<T>(acc);  // what the store keeps (identity for fp32)
-          st4(yrow + (size_t)(ow0 + j) * C, acc);
+          if (nt)
+            st4nt(yrow + (size_t)(ow0 + j) * C, acc);
+          else
+            st4(yrow + (size_t)(ow0 + j) * C, acc);
           if constexpr (STATS == 1) {
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
@@ -830,7 +833,7 @@ static int launch_dw_fwd(const T* x, const float* wt, const float* bias, T* y, i
   if (!part || !fold_take(part, (int)grid.x, C, 1, &ft)) ft.part = nullptr;
 #define DW_LAUNCH(B, ST_, WL_)                                                                                        \
   hipLaunchKernelGGL((dw_fwd_kernel<R, S, ST, B, ST_, WL_, T>), grid, dim3(256), 0, st, x, xb, wt, bias, y, N, H, W, \
-                     C, OH, OW, pad, bn, part, xo, obn, res, ft)
+                     C, OH, OW, pad, bn, part, xo, obn, res, ft, nt_stores())
   const int mode = part ? (xo ? 2 : 1) : 0;
   if (wl == 0 && !bn.mean && mode == 0)
     DW_LAUNCH(false, 0, 0);

@@ -48,6 +48,12 @@ __device__ __forceinline__ float ld1(const float* p) { return *p; }
 __device__ __forceinline__ float ld1(const bf16_t* p) {
   return __builtin_bit_cast(float, (uint32_t)*p << 16);
 }
+// Nontemporal 16-byte / 8-byte stores (global_store ... nt): streamed past the caches.
+__device__ __forceinline__ void st4nt(float* p, f32x4 v) { __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(p)); }
+__device__ __forceinline__ void st4nt(bf16_t* p, f32x4 v) {
+  typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+  __builtin_nontemporal_store(__builtin_bit_cast(u32x2, f32_to_bf16x4(v)), reinterpret_cast<u32x2*>(p));
+}
 __device__ __forceinline__ void st1(float* p, float v) { *p = v; }
 __device__ __forceinline__ void st1(bf16_t* p, float v) { *p = __builtin_bit_cast(bf16_t, (__bf16)v); }
 // The value a store of v to T-typed storage keeps (what a consumer reads back).
@@ -167,6 +173,9 @@ struct SubPix {
 enum : int { DK_ERR_ARGS = 10001, DK_ERR_WORKSPACE = 10002 };
 // Success, and the launch also folded the BN partials armed for it (dk_bn_fold_arm_*).
 enum : int { DK_FOLDED = 10100 };
+// Tuning knob (dk_debug_set_gemm_config kind 4): kernels that support it store their main output
+// nontemporally when set (A/B runs only; default from DORKNET_NT_STORES, else 0).
+int nt_stores();
 
 // Split-K second stage (reduce.hip): out = sum_s ws[s][M][N] (+ l2 * w), fixed order.
 //   mode 0: out[m][n];  mode 1: columns (r, s, c) with c padded to Cp -> out KCRS.

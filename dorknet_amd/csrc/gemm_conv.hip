@@ -7,6 +7,14 @@ using namespace dk;
 namespace dk {
 int g_cfg_override[2] = {-1, -1};
 int g_fill_splits = 1;
+static int g_nt_stores = -1;
+int nt_stores() {
+  if (g_nt_stores < 0) {
+    const char* e = getenv("DORKNET_NT_STORES");
+    g_nt_stores = (e && e[0] == '1') ? 1 : 0;
+  }
+  return g_nt_stores;
+}
 
 // Weight re-layouts (tiny; run once per call on the caller's stream).
 __global__ void w_kcrs_to_krsc_kernel(const float* __restrict__ w, int K, int C, int R, int S, int Cp,
@@ -66,6 +74,10 @@ DK_API int dk_debug_set_gemm_config(int kind, int cfg) {
   }
   if (kind == 3) {  // streaming pointwise kernels (pw_stream.hip) on / off
     pw_stream_set(cfg < 0 ? 1 : cfg);
+    return 0;
+  }
+  if (kind == 4) {  // nontemporal output stores (kernels that support them)
+    g_nt_stores = cfg < 0 ? 0 : cfg;
     return 0;
   }
   if (kind < 0 || kind > 1) return -1;

@@ -291,6 +291,7 @@ struct FwdArgs {
   int M, H, W, OH, OW, sa;
   uint32_t xbytes;
   FoldTail ft;        // ft.part != nullptr: fold the statistics rows in this launch
+  int nt;             // nontemporal y stores (tuning knob, nt_stores())
 };
 
 template <int KR_, int NO_, bool BN, bool STATS, bool STRIDED>
@@ -411,7 +412,12 @@ __global__ __launch_bounds__(256, KR_ == 64 ? 3 : 2) void fwd_kernel(FwdArgs a) 
         const uint32_t imm = (uint32_t)(((r & 3) + 8 * ((r >> 2) & 1)) * NO + 32 * u) * 4u;
         float v = acc[u][r];
         if (a.bias) v += bias[u];
-        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), ry, (int)((r < 8 ? eb0 : eb1) + imm), 0, 0);
+        if (a.nt)
+          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), ry, (int)((r < 8 ? eb0 : eb1) + imm), 0,
+                                                2);
+        else
+          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), ry, (int)((r < 8 ? eb0 : eb1) + imm), 0,
+                                                0);
         if constexpr (STATS) {
           const double d = (mb + dm < a.M) ? (double)v : 0.0;
           ps[u] += d;
@@ -838,6 +844,7 @@ int pw_stream_fwd(const float* x, int N, int H, int W, int stride, int OH, int O
   pws::FwdArgs a{x, w, bias, y, im, iis, ig, ib, irelu, part, M, H, W, OH, OW, stride,
                  (uint32_t)((size_t)N * H * W * KC * 4)};
   if (ft && part) a.ft = *ft;
+  a.nt = nt_stores();
   const dim3 grid(pws::fwd_blocks(M, KC));
   const bool strided = stride != 1;
 #define DK_FWD(BN_, ST_)                                                                                \

@@ -23,6 +23,34 @@ from .._hip import disarm_folds
 from ._bn_input import accepts_bn_input
 
 
+# Backward-progress listeners: f(layers) is called once the backward of `layers` (leaf layers of
+# a chain step, or a residual block's skip projection) has been issued, i.e. their gradients are
+# queued on the streams.  DataParallel launches a gradient bucket's all-reduce as soon as every
+# layer it covers has been reported -- at sub-layer granularity inside residual blocks
+# (residual_block.py:86-97), not once per top-level step.
+_progress = []
+
+
+class backward_progress:
+    """with backward_progress(fn): fn(layers) after each step's backward (see _progress)."""
+
+    def __init__(self, fn):
+        self.fn = fn
+
+    def __enter__(self):
+        _progress.append(self.fn)
+        return self
+
+    def __exit__(self, *exc):
+        _progress.remove(self.fn)
+        return False
+
+
+def notify_backward_done(layers):
+    for f in list(_progress):
+        f(layers)
+
+
 def fusion_enabled() -> bool:
     return os.environ.get("DORKNET_FUSE", "1") != "0"
 
@@ -206,6 +234,8 @@ def _backward_steps(steps, dy, residual, after_step, need_input_grad, join):
             dy = step[0].backward(dy, join=_join_of(steps[i - 1]))
         else:
             dy = step[0].backward(dy)
+        if _progress:
+            notify_backward_done(step)
         if after_step is not None:
             after_step(i)
     if residual is not None:

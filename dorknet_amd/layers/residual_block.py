@@ -15,7 +15,7 @@ import os
 from .._hip import lib, stream_handle
 from .._tensor import empty_nhwc, to_nhwc
 from ._bn_input import accepts_bn_input, materialize
-from ._chain import chain_backward, chain_forward, fusion_enabled
+from ._chain import chain_backward, chain_forward, fusion_enabled, notify_backward_done
 from .activations import ReLu
 from .batch_norm import BatchNormLayer
 from .convolution import ConvLayer
@@ -107,6 +107,8 @@ class ResidualBlock(Layer):
             skip_dx = skip.backward(joined_dx, lattice_out=True)
         else:
             skip_dx = skip.backward(joined_dx)
+        if skip is not None:
+            notify_backward_done((skip,))
         if fusion_enabled():
             return chain_backward(self._steps, joined_dx, residual=skip_dx, join=join)
         return _add(chain_backward(self._steps, joined_dx), skip_dx)

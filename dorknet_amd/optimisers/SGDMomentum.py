@@ -21,6 +21,17 @@ class SGDMomentum:
     def __init__(self, network, learning_rate, momentum, update_skip_projections=False):
         self.network = network
         self.update_skip_projections = update_skip_projections
+        # a data-parallel wrapper must all-reduce exactly the gradients this optimiser applies
+        # (parallel.DataParallel checks the same pair from its side)
+        dp_flag = getattr(network, "_dp_update_skip_projections", None)
+        if dp_flag is not None and dp_flag != update_skip_projections:
+            raise ValueError("SGDMomentum(update_skip_projections={}) disagrees with DataParallel's "
+                             "update_skip_projections={}: skip-projection gradients would be applied "
+                             "un-averaged".format(update_skip_projections, dp_flag))
+        try:
+            network._opt_update_skip_projections = update_skip_projections
+        except AttributeError:
+            pass
         self.learnable_layers = []
         for layer in network.layers:
             if layer.learned_params is not None:

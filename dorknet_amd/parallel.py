@@ -33,7 +33,7 @@ import torch
 import torch.distributed as dist
 
 from ._hip import async_weight_grads, side_stream_context
-from .layers._chain import chain_backward
+from .layers._chain import backward_progress, chain_backward
 
 
 def _all_layers(layers, skips=True):
@@ -113,7 +113,19 @@ class DataParallel:
         for idxs, ready_after in plan_buckets(numels, [s[0] for s in slots], bucket_bytes):
             lo = min(offs[i] for i in idxs)
             hi = max(offs[i] + numels[i] for i in idxs)
-            self.buckets.append((lo, hi, ready_after))
+            # the leaf layers whose gradients the bucket holds: it is complete once all of them
+            # have been through backward (layers/_chain.py backward_progress)
+            owners = frozenset(id(slots[i][1]) for i in idxs)
+            self.buckets.append((lo, hi, ready_after, owners))
+        self.launch_log = []  # (bucket index, layers reported so far) per launch, for tests
+        # the optimiser must agree on which gradients are all-reduced (SGDMomentum checks too)
+        network._dp_update_skip_projections = update_skip_projections
+        opt_flag = getattr(network, "_opt_update_skip_projections", None)
+        if opt_flag is not None and opt_flag != update_skip_projections:
+            raise ValueError("DataParallel(update_skip_projections={}) disagrees with the optimiser's "
+                             "update_skip_projections={}: skip-projection gradients would be updated "
+                             "without being all-reduced (or all-reduced for nothing)".format(
+                                 update_skip_projections, opt_flag))
         if batch_norm == "sync":
             from .layers.batch_norm import BatchNormLayer
             for l in _all_layers(network.layers):
@@ -149,31 +161,36 @@ class DataParallel:
         net = self.network
         dy = net.loss_layer.backward()
         steps = net._steps
-        top_index = {id(l): i for i, l in enumerate(net.layers)}
-        state = {"pending": list(self.buckets)}
+        pending = list(enumerate(self.buckets))
+        done = set()
         self._works = []
+        self.launch_log = []
 
-        def after_step(i):
-            # the buckets whose layers have all been through backward (the deferred BatchNorm
-            # apply runs inside the producer's step, so a bucket is complete only after it)
-            done_idx = min(top_index[id(l)] for l in steps[i])
+        def progress(layers):
+            # leaf layers (a chain step's, or a skip projection) whose gradients are now queued:
+            # launch every bucket all of whose layers are done -- inside a residual block too, so
+            # a block's buckets go out while the rest of its backward still runs
+            done.update(id(l) for l in layers)
             still = []
-            for lo, hi, ready_after in state["pending"]:
-                if done_idx <= ready_after:
+            for bi, (lo, hi, _, owners) in pending:
+                if owners <= done:
                     self._launch(lo, hi)
+                    self.launch_log.append((bi, len(done)))
                 else:
-                    still.append((lo, hi, ready_after))
-            state["pending"] = still
+                    still.append((bi, (lo, hi, _, owners)))
+            pending[:] = still
 
-        chain_backward(steps, dy, after_step=after_step, need_input_grad=False)
-        for lo, hi, _ in state["pending"]:
+        with backward_progress(progress):
+            chain_backward(steps, dy, need_input_grad=False)
+        for bi, (lo, hi, _, _) in pending:
             self._launch(lo, hi)
+            self.launch_log.append((bi, len(done)))
         self.finish()
 
     def allreduce_grads(self):
         """All-reduce every bucket now (for callers that ran network.backward() themselves)."""
         self._works = []
-        for lo, hi, _ in self.buckets:
+        for lo, hi, _, _ in self.buckets:
             self._launch(lo, hi)
         self.finish()
 

@@ -2,6 +2,11 @@
 into a markdown table: kernel, calls, total/avg duration, share.
 
     python scripts/prof_summary.py gpurun_out/prof_r01b [--steps 8] > profiles/r01_kernel_stats.md
+
+With --steps N and a kernel trace (*_kernel_trace.csv) present, only the kernels of the last N
+training steps are counted: a step ends at the SGD-momentum update kernel, so setup work (the
+warm-up, the instrumented roofline step's event records, probes, the CPU baseline's transfers)
+does not leak into the per-step numbers.
 """
 import argparse
 import csv
@@ -25,6 +30,25 @@ def rows_from_csv(path):
     return out
 
 
+def rows_from_trace(path, steps, marker="sgd_momentum"):
+    """Per-kernel (name, calls, total us, avg us, pct) over the last `steps` step windows."""
+    with open(path) as f:
+        tr = list(csv.DictReader(f))
+    tr.sort(key=lambda r: int(r["Start_Timestamp"]))
+    ends = [i for i, r in enumerate(tr) if marker in r["Kernel_Name"]]
+    if len(ends) < steps + 1:
+        return None
+    lo, hi = ends[-steps - 1] + 1, ends[-1] + 1
+    agg = {}
+    for r in tr[lo:hi]:
+        d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+        a = agg.setdefault(r["Kernel_Name"], [0, 0.0])
+        a[0] += 1
+        a[1] += d
+    tot = sum(v[1] for v in agg.values())
+    return [(n, c, t, t / c, 100 * t / tot) for n, (c, t) in agg.items()]
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("dir")
@@ -33,7 +57,12 @@ def main():
     a = ap.parse_args()
     dbs = glob.glob(os.path.join(a.dir, "**", "*.db"), recursive=True)
     csvs = glob.glob(os.path.join(a.dir, "**", "*kernel_stats.csv"), recursive=True)
-    rows = rows_from_csv(csvs[0]) if csvs else rows_from_db(dbs[0])
+    traces = glob.glob(os.path.join(a.dir, "**", "*kernel_trace.csv"), recursive=True)
+    rows = rows_from_trace(traces[0], a.steps) if (traces and a.steps) else None
+    if rows is None:
+        rows = rows_from_csv(csvs[0]) if csvs else rows_from_db(dbs[0])
+    else:
+        print("(last {} training steps of the kernel trace, delimited by the SGD-momentum kernel)\n".format(a.steps))
     rows.sort(key=lambda r: -r[2])
     total = sum(r[2] for r in rows)
     print("| kernel | calls | total us | avg us | % |" + (" us/step |" if a.steps else ""))

@@ -146,3 +146,113 @@ def test_syncbn_backward_recipe_matches_full_batch():
         dxr = g / std * (gr - sums_g[0] / M - xh * sums_g[1] / M)
         assert np.allclose(dxr / world, dX_full[r * n:(r + 1) * n])
     assert np.allclose(dg_avg, dg_full) and np.allclose(db_avg, db_full)
+
+
+class FakeBlock:
+    """A residual-block stand-in: a chain of FakeLayers run by chain_backward plus a skip projection
+    (residual_block.py:86-97), reporting its skip's backward like ResidualBlock does."""
+
+    def __init__(self, name, layers, skip, log):
+        self.layer_name = name
+        self.layer_list = layers
+        self.skip_projection = skip
+        self.learned_params = None
+        self.grads = None
+        self.non_learned_params = None
+        self._steps = [(l,) for l in layers]
+        self.log = log
+
+    def backward(self, dy):
+        from dorknet_amd.layers._chain import chain_backward, notify_backward_done
+        dy = self.skip_projection.backward(dy)
+        notify_backward_done((self.skip_projection,))
+        return chain_backward(self._steps, dy)
+
+
+class LoggedLayer(FakeLayer):
+    def __init__(self, name, shapes, idx, log):
+        super().__init__(name, shapes, idx)
+        self.log = log
+
+    def backward(self, dy):
+        self.log.append(("bwd", self.layer_name))
+        return super().backward(dy)
+
+
+def _block_worker(rank, world, port, q):
+    try:
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        log = []
+        L = lambda name, i: LoggedLayer(name, {"weights": (8, 50)}, i, log)  # noqa: E731
+        inner = [L("b_a", 1), L("b_b", 2), L("b_c", 3)]
+        blk = FakeBlock("blk", inner, L("b_skip", 4), log)
+        net = FakeNet()
+        net.layers = [L("stem", 0), blk, L("head", 5)]
+        net._steps = [(l,) for l in net.layers]
+        # one bucket per layer (1600 B each); skips included so the skip projection is bucketed
+        dp = DataParallel(net, bucket_bytes=1000, device=torch.device("cpu"), update_skip_projections=True)
+        orig = dp._launch
+
+        def launch(lo, hi):
+            log.append(("launch", lo))
+            orig(lo, hi)
+        dp._launch = launch
+        dp.backward()
+        names = [e[1] for e in log if e[0] == "bwd"]
+        assert names == ["head", "b_skip", "b_c", "b_b", "b_a", "stem"], names
+        # every bucket goes out right after its (only) layer's backward -- inside the block too,
+        # before the block's remaining layers run
+        pos = {e[1]: i for i, e in enumerate(log) if e[0] == "bwd"}
+        launches = [i for i, e in enumerate(log) if e[0] == "launch"]
+        assert len(launches) == 6
+        for name in ("b_c", "b_b", "b_skip"):
+            nxt = min(p for p in pos.values() if p > pos[name])
+            assert any(pos[name] < li < nxt for li in launches), (name, log)
+        for l in inner + [blk.skip_projection]:
+            g = l.grads["weights"]
+            base = torch.arange(g.numel(), dtype=torch.float32).view(g.shape)
+            assert torch.allclose(g, base * 1.5 + l.idx)
+        dist.destroy_process_group()
+        q.put((rank, "ok"))
+    except Exception:  # pragma: no cover - reported to the parent
+        import traceback
+        q.put((rank, traceback.format_exc()))
+        raise
+
+
+def test_buckets_launch_inside_residual_blocks_gloo_world2():
+    """A bucket's all-reduce is issued as soon as the last layer it covers has been through
+    backward, at sub-layer granularity inside a residual block (not after the whole block)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_block_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    results = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    assert results == {0: "ok", 1: "ok"}, results
+
+
+def test_skip_projection_flag_mismatch_raises():
+    """DataParallel and SGDMomentum must agree on update_skip_projections (either order)."""
+    from dorknet_amd.optimisers.SGDMomentum import SGDMomentum
+    import torch.distributed as d
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(_free_port())
+    d.init_process_group("gloo", rank=0, world_size=1)
+    try:
+        net = FakeNet()
+        DataParallel(net, device=torch.device("cpu"), update_skip_projections=False)
+        with pytest.raises(ValueError):
+            SGDMomentum(net, 0.1, 0.9, update_skip_projections=True)
+        SGDMomentum(net, 0.1, 0.9)  # agreeing flags are fine
+        net2 = FakeNet()
+        SGDMomentum(net2, 0.1, 0.9, update_skip_projections=True)
+        with pytest.raises(ValueError):
+            DataParallel(net2, device=torch.device("cpu"))
+    finally:
+        d.destroy_process_group()
