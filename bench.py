@@ -42,10 +42,10 @@ def parse():
     ap.add_argument("--cpu-sample", type=int, default=32, help="images per CPU-baseline step (0 = skip)")
     ap.add_argument("--cpu-steps", type=int, default=10, help="timed CPU-baseline steps (median reported)")
     ap.add_argument("--cpu-warmup", type=int, default=2, help="untimed CPU-baseline steps")
-    ap.add_argument("--config", type=int, choices=[2, 3, 5], default=3,
+    ap.add_argument("--config", type=int, choices=[1, 2, 3, 5], default=3,
                     help="BASELINE config: 3 (default; 4 with --gpus N) = ResNet-18-depsep training step; "
-                         "2 = single 3x3 ConvLayer fwd+dgrad+wgrad; 5 = bf16 depthwise-separable stack "
-                         "(secondary lines, not the headline metric)")
+                         "1 = MNISTNet bs=64 training step; 2 = single 3x3 ConvLayer fwd+dgrad+wgrad; "
+                         "5 = bf16 depthwise-separable stack (secondary lines, not the headline metric)")
     ap.add_argument("--pmc", default=None,
                     help="per-kernel HBM traffic from rocprofv3 FETCH_SIZE/WRITE_SIZE passes of this same command "
                          "(scripts/pmc_summary.py output; default: the newest profiles/*_pmc.json)")
@@ -291,14 +291,113 @@ def cpu_baseline(batch, steps=10, warmup=2):
                       "{:.3f} s, {:.1f} s in all".format(steps, warmup, batch, med, sum(times))}
 
 
+def _cpu_threads():
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = os.cpu_count() or 1
+    cores = max(1, min(int(os.environ.get("OMP_NUM_THREADS", avail)), avail))
+    os.environ["OMP_NUM_THREADS"] = str(cores)
+    os.environ["OMP_MAX_ACTIVE_LEVELS"] = "1"
+    return cores
+
+
+def _timed_median(fn, steps, warmup):
+    import numpy as np
+    times = []
+    for i in range(warmup + steps):
+        t0 = time.perf_counter()
+        fn()
+        if i >= warmup:
+            times.append(time.perf_counter() - t0)
+    return float(np.median(times)), sum(times)
+
+
+def cpu_baseline_mnist(steps=10, warmup=2):
+    """BASELINE config 1 on the reference's CPU path restated (oracle/cpu_path.py: its Cython kernels
+    in C/OpenMP + numpy BLAS): MNISTNet (MNIST_basic_convnet.py:15-69), batch 64, SGD-momentum."""
+    import numpy as np
+    cores = _cpu_threads()
+    from threadpoolctl import threadpool_limits
+    from oracle import models
+    from oracle.net import OSGDMomentum
+    from oracle._clib import lib as oracle_lib
+    oracle_lib().oracle_set_threads(cores)
+    rng = np.random.default_rng(0)
+    X = rng.uniform(0, 1, (64, 1, 28, 28)).astype(np.float32)
+    y = np.eye(10, dtype=np.float32)[rng.integers(0, 10, 64)]
+    with threadpool_limits(limits=cores):
+        net = models.mnist_net("cy", rng=np.random.RandomState(0))
+        sgd = OSGDMomentum(net, 0.01, 0.9)
+
+        def step():
+            net.forward(X, y)
+            net.backward()
+            sgd.update_weights()
+        med, tot = _timed_median(step, steps, warmup)
+    model, phys, logical = cpu_info()
+    return {"value": round(64 / med, 2), "unit": "images/s", "cores": cores, "kind": "port", "cpu_model": model,
+            "host_physical_cores": phys, "host_logical_cpus": logical,
+            "sample": "median of {} timed MNISTNet bs=64 training steps after {} untimed, reference CPU path "
+                      "restated; {:.1f} s in all".format(steps, warmup, tot)}
+
+
+def cpu_baseline_conv(batch=16, steps=5, warmup=1):
+    """BASELINE config 2 on the reference's CPU path restated: im2col_cy + numpy SGEMM forward,
+    SGEMMs + row2im_cy backward (convolution.py:58-126), on a `batch`-image slice of the
+    256 x 64 x 56 x 56 input; reported as full-size passes/s (per-image time x 256)."""
+    import numpy as np
+    cores = _cpu_threads()
+    from threadpoolctl import threadpool_limits
+    from oracle import cpu_path
+    from oracle._clib import lib as oracle_lib
+    oracle_lib().oracle_set_threads(cores)
+    rng = np.random.default_rng(0)
+    X = rng.standard_normal((batch, 64, 56, 56)).astype(np.float32)
+    dY = rng.standard_normal((batch, 64, 56, 56)).astype(np.float32)
+    W = (0.01 * rng.standard_normal((64, 64, 3, 3))).astype(np.float32)
+    with threadpool_limits(limits=cores):
+        conv = cpu_path.CyConv("c", W, None, 1, 1)
+
+        def step():
+            conv.forward(X)
+            conv.backward(dY)
+        med, tot = _timed_median(step, steps, warmup)
+    model, phys, logical = cpu_info()
+    return {"value": round(batch / 256.0 / med, 4), "unit": "passes/s", "cores": cores, "kind": "port",
+            "cpu_model": model, "host_physical_cores": phys, "host_logical_cpus": logical,
+            "sample": "median of {} timed fwd+dgrad+wgrad passes on a {}-image slice (after {} untimed), scaled to "
+                      "256 images; reference CPU path restated (im2col_cy/row2im_cy in C/OpenMP + numpy SGEMM); "
+                      "{:.1f} s in all".format(steps, batch, warmup, tot)}
+
+
 def other_config(args):
-    """BASELINE configs 2 and 5 (one GPU): a secondary JSON line each, same timing rules
+    """BASELINE configs 1, 2 and 5 (one GPU): a secondary JSON line each, same timing rules
     (warm-up, then K steps between synchronizations; inputs resident in HBM)."""
     import numpy as np
     import torch
     from dorknet_amd import perfmodel
     torch.cuda.set_device(0)
-    if args.config == 2:
+    if args.config == 1:
+        from examples.mnist_convnet import MNISTNet
+        from dorknet_amd.optimisers.SGDMomentum import SGDMomentum
+        np.random.seed(0)
+        net = MNISTNet("mnist")
+        net.to_gpu()
+        sgd = SGDMomentum(net, 0.01, 0.9)
+        rng = np.random.default_rng(0)
+        B = args.batch
+        X = torch.as_tensor(rng.uniform(0, 1, (B, 1, 28, 28)).astype(np.float32), device="cuda")
+        Y = torch.as_tensor(np.eye(10, dtype=np.float32)[rng.integers(0, 10, B)], device="cuda")
+
+        def step():
+            net.forward(X, Y)
+            net.backward()
+            sgd.update_weights()
+        flops = None
+        unit, metric = "images/s", "images/sec training step, MNISTNet bs=64, 1 MI355X (reference: CPU path)"
+        dtype, workload = "fp32", "MNISTNet (MNIST_basic_convnet.py:15-69) fwd+loss+bwd+SGD-momentum, BASELINE config 1"
+    elif args.config == 2:
         from dorknet_amd.layers.convolution import ConvLayer
         np.random.seed(0)
         conv = ConvLayer("c", filter_block_shape=(64, 64, 3, 3), stride=1, padding=1, with_bias=False)
@@ -383,6 +482,8 @@ def other_config(args):
     if roof:
         out["roofline"] = roof
         out["breakdown"] = breakdown
+    if args.cpu_sample and args.config in (1, 2):
+        out["cpu_baseline"] = cpu_baseline_mnist() if args.config == 1 else cpu_baseline_conv()
     print(json.dumps(out), flush=True)
 
 
@@ -413,6 +514,8 @@ def main():
             raise SystemExit("--config {} is a one-GPU configuration".format(args.config))
         if args.config == 5 and args.batch == 256:
             args.batch = 512  # the configuration's batch
+        if args.config == 1 and args.batch == 256:
+            args.batch = 64
         return other_config(args)
     import numpy as np
     import torch

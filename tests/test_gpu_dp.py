@@ -128,6 +128,56 @@ def test_bucket_allreduce_waits_for_main_stream(monkeypatch):
         dist.destroy_process_group()
 
 
+def test_bucket_launch_order_rccl_world1():
+    """RCCL world 1: the order in which gradient buckets go to the collective against the order in
+    which layers finish backward.  Each bucket is launched as soon as every leaf layer it covers
+    has been through backward -- so inside a residual block, before the block's first layer is
+    done -- and the buckets go out in flat-buffer order (reverse layer order)."""
+    import torch.distributed as dist
+    from dorknet_amd.layers._chain import backward_progress
+    from dorknet_amd.parallel import DataParallel
+    from examples.resnet18_depsep import ResNet18, synthetic_batch
+    _rccl_world1()
+    try:
+        X, _, onehot = synthetic_batch(2, seed=SEED_X)
+        np.random.seed(SEED_W)
+        net = ResNet18("r18")
+        net.to_gpu()
+        dp = DataParallel(net, bucket_bytes=64 << 10)
+        net.forward(torch.as_tensor(X, device="cuda"), torch.as_tensor(onehot, device="cuda"))
+        events = []  # ("done", layer names) / ("launch", lo)
+        orig = dp._launch
+
+        def launch(lo, hi):
+            events.append(("launch", lo))
+            orig(lo, hi)
+        dp._launch = launch
+        with backward_progress(lambda layers: events.append(("done", tuple(l.layer_name for l in layers)))):
+            dp.backward()
+        torch.cuda.synchronize()
+        launches = [e[1] for e in events if e[0] == "launch"]
+        assert launches == sorted(launches) and len(launches) == len(dp.buckets) > 8
+        # a bucket launched before the first layer of res8's chain finished backward holds only
+        # gradients of layers already reported done
+        first_res8 = next(i for i, e in enumerate(events) if e[0] == "done" and e[1][0] == "res8_dw1_dw")
+        early = [i for i, e in enumerate(events) if e[0] == "launch" and i < first_res8]
+        assert early, "no bucket went out while res8's backward was still running"
+        done_before = set()
+        for i, e in enumerate(events):
+            if e[0] == "done":
+                done_before.update(e[1])
+        names = {id(l): l.layer_name for l in all_layers(net.layers)}
+        for bi, (lo, hi, _, owners) in enumerate(dp.buckets):
+            li = next(i for i, e in enumerate(events) if e == ("launch", lo))
+            seen = set()
+            for e in events[:li]:
+                if e[0] == "done":
+                    seen.update(e[1])
+            assert {names[o] for o in owners} <= seen, (bi, {names[o] for o in owners} - seen)
+    finally:
+        dist.destroy_process_group()
+
+
 def _gloo_rank(rank, world, port, outdir, q):
     try:
         os.environ["MASTER_ADDR"] = "127.0.0.1"
