@@ -553,7 +553,7 @@ __global__ __launch_bounds__(256) void dw_bwd_fused_kernel(const T* __restrict__
                                                            T* __restrict__ dx, const T* __restrict__ res,
                                                            double* __restrict__ spart, float* __restrict__ wpart,
                                                            int N, int H, int W, int C, int CL, FoldTail ft,
-                                                           JoinBwd jn = JoinBwd{}) {
+                                                           JoinBwd jn = JoinBwd{}, int nt = 0) {
   static_assert(!(JOIN && sizeof(T) != 4), "the join fusion is fp32 only");
   static_assert(!STATS || BNX, "input-BN partials need the input BN");
   static_assert(!(JOIN && (STATS || BNX)), "the join's partials replace the input BN's");
@@ -722,7 +722,12 @@ __global__ __launch_bounds__(256) void dw_bwd_fused_kernel(const T* __restrict__
           s2[e] += (double)acc[e] * (double)xn;
         }
       }
-      if (dxcol) st4(dxcol + (size_t)h * W * C, acc);
+      if (dxcol) {
+        if (nt)
+          st4nt(dxcol + (size_t)h * W * C, acc);
+        else
+          st4(dxcol + (size_t)h * W * C, acc);
+      }
       if constexpr (STATS) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
@@ -1128,7 +1133,7 @@ static int dw_bwd_fused(const T* g, const T* bn_x, int N, int H, int W, int C, c
       (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,       \
                                 (int)shm);                                                                           \
     hipLaunchKernelGGL(k, grid, dim3(256), shm, st, g, bn_x, (uint32_t)bytes, ob, x, bn, w_crs, dx, residual, part,  \
-                       wpart, N, H, W, C, cl, ft, JoinBwd{});                                                        \
+                       wpart, N, H, W, C, cl, ft, JoinBwd{}, nt_stores());                                                        \
   }
   if (out_relu) {
     if (part) DWB_LAUNCH(true, true, true) else if (bn_mean) DWB_LAUNCH(true, false, true)
@@ -1245,7 +1250,7 @@ DK_API int dk_dwconv_bwd_bnbwd_join_f32(const float* g, const float* bn_x, int N
       (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,       \
                                 (int)shm);                                                                           \
     hipLaunchKernelGGL(k, grid, dim3(256), shm, st, g, bn_x, (uint32_t)bytes, ob, x, BnIn{}, w_crs, dx, residual,    \
-                       part, wpart, N, H, W, C, cl, ft, jn);                                                         \
+                       part, wpart, N, H, W, C, cl, ft, jn, nt_stores());                                                         \
   }
   if (out_relu)
     DWJ_LAUNCH(true)

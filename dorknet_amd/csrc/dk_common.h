@@ -185,6 +185,7 @@ int splitk_reduce(const float* ws, int splits, int M, int N, float* out, const f
 // Streaming pointwise kernels (pw_stream.hip) for the K = C = 64 shapes.
 bool pw_stream_enabled();  // DORKNET_PW_STREAM (default 1; 0 = the tiled engine everywhere, for A/B runs)
 void pw_stream_set(int v);  // tuning knob (dk_debug_set_gemm_config kind 3)
+void pw_stream_bwd_pf_set(int v);  // tuning knob (kind 5): the fused backward's operand prefetch
 bool pw_stream_dgrad_ok(int K, int C, int M);
 int pw_stream_dgrad_rows(int M);
 bool pw_stream_bwd_ok(int K, int C, int M);

@@ -99,7 +99,7 @@ __device__ __forceinline__ f32x4 bn_in4_at(f32x4 v, const BnIn& bn, int c) {
 
 __global__ __launch_bounds__(256) void bn_add_kernel(const float* __restrict__ a, BnIn ba, const float* __restrict__ b,
                                                      BnIn bb, long long n, int C, int relu, float* __restrict__ y,
-                                                     uint8_t* __restrict__ mask) {
+                                                     uint8_t* __restrict__ mask, int nt) {
   const long long nv = n >> 2;
   const long long stride = (long long)gridDim.x * blockDim.x;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += stride) {
@@ -115,7 +115,10 @@ __global__ __launch_bounds__(256) void bn_add_kernel(const float* __restrict__ a
       }
       if (mask) reinterpret_cast<uint32_t*>(mask)[i] = m;
     }
-    st4(y + 4 * i, v);
+    if (nt)
+      st4nt(y + 4 * i, v);
+    else
+      st4(y + 4 * i, v);
   }
 }
 
@@ -495,7 +498,8 @@ DK_API int dk_bn_add_f32(const float* a, const float* a_mean, const float* a_inv
   };
   if (C < 4 || C % 4 || n % C || n >= (1ll << 31) || !al16(a) || !al16(b) || !al16(y) || !al4(mask) || !params_ok(ba) || !params_ok(bb))
     return DK_ERR_ARGS;
-  hipLaunchKernelGGL(bn_add_kernel, grid4(n), dim3(256), 0, as_stream(stream), a, ba, b, bb, n, C, relu, y, mask);
+  hipLaunchKernelGGL(bn_add_kernel, grid4(n), dim3(256), 0, as_stream(stream), a, ba, b, bb, n, C, relu, y, mask,
+                     nt_stores());
   return launch_status();
 }
 

@@ -76,6 +76,10 @@ DK_API int dk_debug_set_gemm_config(int kind, int cfg) {
     pw_stream_set(cfg < 0 ? 1 : cfg);
     return 0;
   }
+  if (kind == 5) {  // the streaming fused pointwise backward's operand prefetch (pw_stream.hip)
+    pw_stream_bwd_pf_set(cfg < 0 ? 0 : cfg);
+    return 0;
+  }
   if (kind == 4) {  // nontemporal output stores (kernels that support them)
     g_nt_stores = cfg < 0 ? 0 : cfg;
     return 0;

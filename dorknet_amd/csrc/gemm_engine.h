@@ -556,6 +556,13 @@ struct EpStoreT {  // O: output element type (float, or bf16_t: rounded on store
   const float* bias;
   int v4;  // out, ldo, bias and res allow 16-byte (4-element) access
   const O* res;
+  int nt = 0;  // nontemporal 16-byte stores (tuning knob nt_stores(), set by launch_igemm)
+  __device__ __forceinline__ void store4(O* p, f32x4 v) const {
+    if (nt)
+      st4nt(p, v);
+    else
+      st4(p, v);
+  }
   // per-row operands the 16-byte path needs, loaded for all of a thread's rows before any
   // store (loads cannot be hoisted over stores to a possibly aliasing output)
   struct Pre {
@@ -577,7 +584,7 @@ struct EpStoreT {  // O: output element type (float, or bf16_t: rounded on store
     return rnd1<O>(v);
   }
   __device__ __forceinline__ void put4(int m, int n, f32x4 v, const Pre& p, int, double*, double*) const {
-    st4(out + (size_t)m * ldo + n, value4(n, v, p));
+    store4(out + (size_t)m * ldo + n, value4(n, v, p));
   }
   __device__ __forceinline__ void put1(int m, int n, float v, int, double&, double&) const {
     st1(out + (size_t)m * ldo + n, value1(m, n, v));
@@ -597,7 +604,7 @@ struct EpStoreStatsT : EpStoreT<O> {
   FoldTail ft{};  // armed in-launch fold of part (fold_tail.h; set by launch_igemm)
   __device__ __forceinline__ void put4(int m, int n, f32x4 v, const Pre& p, int, double* a, double* b) const {
     const f32x4 o = this->value4(n, v, p);
-    st4(this->out + (size_t)m * this->ldo + n, o);
+    this->store4(this->out + (size_t)m * this->ldo + n, o);
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const double d = (double)o[e];
@@ -645,7 +652,7 @@ struct EpStoreBnBwdT : EpStoreT<O> {
   }
   __device__ __forceinline__ void put4(int m, int n, f32x4 v, const Pre& p, int, double* a, double* b) const {
     v = this->value4(n, v, p);
-    st4(this->out + (size_t)m * this->ldo + n, v);
+    this->store4(this->out + (size_t)m * this->ldo + n, v);
     bn_bwd_contrib4(v, p.x, bn, n, a, b);
   }
   __device__ __forceinline__ void put1(int m, int n, float v, int, double& a, double& b) const {
@@ -1092,6 +1099,14 @@ extern int g_cfg_override[2];  // tuning knobs only (dk_debug_set_gemm_config, g
 extern int g_fill_splits;
 constexpr int kNumCUs = 256;  // MI355X
 
+// Epilogues with an `nt` member take the nontemporal-store knob (nt_stores()).
+template <class E>
+static inline auto set_nt(E& e, int) -> decltype(e.nt = 0, void()) {
+  e.nt = nt_stores();
+}
+template <class E>
+static inline void set_nt(E&, long) {}
+
 template <int BM, int BN, int BK, int WM, int WN, template <int, int, int> class LA, class DA,
           template <int, int, int> class LB, class DB, class EP, int MF = kMfF32>
 static int launch_igemm(const DA& da, const DB& db, const EP& ep, int M, int N, int Ktot, int splits,
@@ -1138,13 +1153,16 @@ static int launch_igemm(const DA& da, const DB& db, const EP& ep, int M, int N, 
     // an armed in-launch fold of the column statistics (fold_tail.h): rows = M tiles, one
     // channel slice per N tile
     EP e = ep;
+    set_nt(e, 0);
     if (!e.part || splits != 1 || !fold_take(e.part, cdiv(M, BM), N, cdiv(N, BN), &e.ft)) e.ft.part = nullptr;
     hipLaunchKernelGGL((igemm_f32<BM, BN, BK, WM, WN, A, DA, B, DB, EP, MF>), dim3(tiles, splits), dim3(NT), dyn, st, da,
                        db, e, M, N, Ktot, kps);
     return fold_status(launch_status(), e.ft);
   }
+  EP e = ep;
+  set_nt(e, 0);
   hipLaunchKernelGGL((igemm_f32<BM, BN, BK, WM, WN, A, DA, B, DB, EP, MF>), dim3(tiles, splits), dim3(NT), dyn, st, da,
-                     db, ep, M, N, Ktot, kps);
+                     db, e, M, N, Ktot, kps);
   return launch_status();
 }
 

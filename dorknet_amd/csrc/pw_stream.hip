@@ -68,6 +68,7 @@ struct DgradArgs {
   double* part;       // [gridDim.x][2][NO]
   int M;
   FoldTail ft;        // ft.part != nullptr: fold the partial rows in this launch (fold_tail.h)
+  int nt;             // nontemporal dx stores (tuning knob, nt_stores())
 };
 
 __device__ __forceinline__ uint32_t row_off_bytes(int m, int ld, int c) { return ((uint32_t)m * ld + c) * 4u; }
@@ -229,7 +230,12 @@ __global__ __launch_bounds__(256, 2) void dgrad_bnbwd_kernel(DgradArgs a) {
         const uint32_t imm = (uint32_t)(((r & 3) + 8 * ((r >> 2) & 1)) * NO + 32 * u) * 4u;
         float v = acc[u][r];
         if constexpr (RES) v += ers[u][r];
-        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), rdx, (int)((r < 8 ? eb0 : eb1) + imm), 0, 0);
+        if (a.nt)
+          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), rdx, (int)((r < 8 ? eb0 : eb1) + imm),
+                                                0, 2);
+        else
+          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), rdx, (int)((r < 8 ? eb0 : eb1) + imm),
+                                                0, 0);
         if constexpr (PART) {
           const float x = exi[u][r];
           const float xh = (x - pm[u]) * pis[u];
@@ -532,8 +538,11 @@ struct BwdArgs {
 
 constexpr int SKD = KR + 4;  // row stride of the wave's dy image
 
-template <bool RES, bool PART, bool BNIN>
-__global__ __launch_bounds__(256, 1) void bwd_fused_kernel(BwdArgs ba) {
+// PF: prefetch the next tile's A operands (g, x of the following BN) into registers during this
+// tile (one wave per SIMD: 256 VGPRs + 88 AGPRs); !PF: load them at the top of each tile and let a
+// second wave on the SIMD cover the latency (2 waves per SIMD).
+template <bool RES, bool PART, bool BNIN, bool PF = true>
+__global__ __launch_bounds__(256, PF ? 1 : 2) void bwd_fused_kernel(BwdArgs ba) {
   const DgradArgs& a = ba.d;
   __shared__ float Bs[NO * SKB];
   __shared__ float tab[7][KR];
@@ -602,14 +611,17 @@ __global__ __launch_bounds__(256, 1) void bwd_fused_kernel(BwdArgs ba) {
     }
   };
   f32x4 cg[KQ], cx[KQ];
-  load_a(t, cg, cx);
-  drain_vmem_loads();
+  if constexpr (PF) {
+    load_a(t, cg, cx);
+    drain_vmem_loads();
+  }
   for (; t < ntiles; t += W) {
     const int m0 = t * TR;
     int z = 0;
     asm volatile("" : "+s"(z));
     const float* tb = &tab[0][0] + z;
     const float* bs = Bs + z;
+    if constexpr (!PF) load_a(t, cg, cx);
 
     // (1) tile t's x (and residual) in the C layout, tile t+W's A operands
     float exi[2][16], ers[2][16];
@@ -626,11 +638,12 @@ __global__ __launch_bounds__(256, 1) void bwd_fused_kernel(BwdArgs ba) {
           ers[u][r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rr, (int)(eb + imm), 0, 0));
       }
     f32x4 ng[KQ], nx[KQ];
-    load_a(t + W, ng, nx);
+    if constexpr (PF) load_a(t + W, ng, nx);
     __builtin_amdgcn_sched_barrier(0);
 
     // (2) dy (bit-identical to dk_bn_bwd_apply_f32) into registers and the wave's LDS image
-    f32x4 af[KQ];
+    f32x4 afs[PF ? KQ : 1];
+    f32x4* const af = PF ? afs : cg;  // (in place without the prefetch: cg is dead after the transform)
 #pragma unroll
     for (int q = 0; q < KQ; ++q) {
       const int k0 = 8 * q + 4 * h;
@@ -697,7 +710,12 @@ __global__ __launch_bounds__(256, 1) void bwd_fused_kernel(BwdArgs ba) {
         const uint32_t imm = (uint32_t)(((r & 3) + 8 * ((r >> 2) & 1)) * NO + 32 * u) * 4u;
         float v = acc[u][r];
         if constexpr (RES) v += ers[u][r];
-        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), rdx, (int)((r < 8 ? eb0 : eb1) + imm), 0, 0);
+        if (a.nt)
+          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), rdx, (int)((r < 8 ? eb0 : eb1) + imm),
+                                                0, 2);
+        else
+          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), rdx, (int)((r < 8 ? eb0 : eb1) + imm),
+                                                0, 0);
         if constexpr (PART) {
           const float x = exi[u][r];
           const float xh = (x - pm[u]) * pis[u];
@@ -708,10 +726,12 @@ __global__ __launch_bounds__(256, 1) void bwd_fused_kernel(BwdArgs ba) {
         }
       }
     }
+    if constexpr (PF) {
 #pragma unroll
-    for (int q = 0; q < KQ; ++q) {
-      cg[q] = ng[q];
-      cx[q] = nx[q];
+      for (int q = 0; q < KQ; ++q) {
+        cg[q] = ng[q];
+        cx[q] = nx[q];
+      }
     }
   }
 
@@ -759,20 +779,36 @@ __global__ __launch_bounds__(256, 1) void bwd_fused_kernel(BwdArgs ba) {
   }
 }
 
-int bwd_fused_blocks(int M) {
+// The backward's A-operand prefetch (tuning knob DORKNET_PWS_BWD_PF, dk_debug_set_gemm_config(5, v)).
+static int g_bwd_pf = -1;
+void bwd_pf_set(int v) { g_bwd_pf = v; }
+static bool bwd_pf() {
+  if (g_bwd_pf < 0) {
+    // default: no prefetch, 2 waves per SIMD (whole step 9.12 -> 9.02 ms, scripts/ab_step.py, r03)
+    const char* e = getenv("DORKNET_PWS_BWD_PF");
+    g_bwd_pf = (e && e[0] == '1') ? 1 : 0;
+  }
+  return g_bwd_pf == 1;
+}
+
+template <bool PF>
+static int bwd_fused_occ() {
   static int occ = -1;
   if (occ < 0) {
-    const void* fs[] = {reinterpret_cast<const void*>(&bwd_fused_kernel<false, true, true>),
-                        reinterpret_cast<const void*>(&bwd_fused_kernel<true, true, true>),
-                        reinterpret_cast<const void*>(&bwd_fused_kernel<false, false, true>),
-                        reinterpret_cast<const void*>(&bwd_fused_kernel<true, false, true>),
-                        reinterpret_cast<const void*>(&bwd_fused_kernel<false, false, false>),
-                        reinterpret_cast<const void*>(&bwd_fused_kernel<true, false, false>)};
-    occ = min_occupancy(fs, 6);
+    const void* fs[] = {reinterpret_cast<const void*>(&bwd_fused_kernel<false, true, true, PF>),
+                        reinterpret_cast<const void*>(&bwd_fused_kernel<false, false, true, PF>),
+                        reinterpret_cast<const void*>(&bwd_fused_kernel<false, false, false, PF>)};
+    occ = min_occupancy(fs, 3);
   }
-  return grid_blocks(M, occ);
+  return occ;
 }
+
+int bwd_fused_blocks(int M) { return grid_blocks(M, bwd_pf() ? bwd_fused_occ<true>() : bwd_fused_occ<false>()); }
+// (the grid of a residual variant, which always prefetches, follows the same count: a block count
+// above its occupancy only adds a second partial round of blocks, never changes the results' order)
 }  // namespace pws
+
+void pw_stream_bwd_pf_set(int v) { pws::bwd_pf_set(v); }
 
 static int g_pw_stream = -1;  // -1: from DORKNET_PW_STREAM (default on); dk_debug_set_gemm_config(3, v)
 void pw_stream_set(int v) { g_pw_stream = v; }
@@ -821,16 +857,34 @@ int pw_stream_bwd_fused(const float* g, const float* bn_x, int M, const float* o
   pws::BwdArgs a{{g, bn_x, nullptr, w, dx, res, x, om, ois, og, ob, k12, orelu, im, iis, ig, ib, irelu, part, M},
                  bm, bis, bgm, bbt, brelu, wpart};
   if (ft && part) a.d.ft = *ft;
+  a.d.nt = nt_stores();
   const dim3 grid(pws::bwd_fused_blocks(M));
   const bool r = res != nullptr, pt = part != nullptr, bn = bm != nullptr;
   if (pt && !bn) return DK_ERR_ARGS;
-#define DK_BWD(R_, P_, B_) hipLaunchKernelGGL((pws::bwd_fused_kernel<R_, P_, B_>), grid, dim3(256), 0, st, a)
+  // (the residual variants keep the prefetch: without it they spill at 2 waves per SIMD)
+#define DK_BWD(R_, P_, B_)                                                                    \
+  if (R_ || pws::bwd_pf())                                                                    \
+    hipLaunchKernelGGL((pws::bwd_fused_kernel<R_, P_, B_, true>), grid, dim3(256), 0, st, a); \
+  else                                                                                        \
+    hipLaunchKernelGGL((pws::bwd_fused_kernel<R_, P_, B_, false>), grid, dim3(256), 0, st, a)
   if (pt) {
-    if (r) DK_BWD(true, true, true); else DK_BWD(false, true, true);
+    if (r) {
+      DK_BWD(true, true, true);
+    } else {
+      DK_BWD(false, true, true);
+    }
   } else if (bn) {
-    if (r) DK_BWD(true, false, true); else DK_BWD(false, false, true);
+    if (r) {
+      DK_BWD(true, false, true);
+    } else {
+      DK_BWD(false, false, true);
+    }
   } else {
-    if (r) DK_BWD(true, false, false); else DK_BWD(false, false, false);
+    if (r) {
+      DK_BWD(true, false, false);
+    } else {
+      DK_BWD(false, false, false);
+    }
   }
 #undef DK_BWD
   return launch_status();
@@ -877,6 +931,7 @@ int pw_stream_dgrad_bnbwd(const float* g, const float* bn_x, int M, const float*
                           hipStream_t st, const FoldTail* ft) {
   pws::DgradArgs a{g, bn_x, dy_out, w, dx, res, x, om, ois, og, ob, k12, orelu, im, iis, ig, ib, irelu, part, M};
   if (ft && part) a.ft = *ft;
+  a.nt = nt_stores();
   const dim3 grid(pws::dgrad_blocks(M));
   if (res && x)
     hipLaunchKernelGGL((pws::dgrad_bnbwd_kernel<true, true>), grid, dim3(256), 0, st, a);
