@@ -1,0 +1,66 @@
+"""Every C-ABI call of one ResNet-18-depsep training step (bs=256) in issue order: entry point,
+its integer arguments (the shape), HIP-event time on the launch stream and the fraction of
+its own roofline bound (perfmodel).  python scripts/call_shapes.py [--config 3|5] [--min-us 20]
+"""
+import argparse
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--min-us", type=float, default=20.0)
+    ap.add_argument("--batch", type=int, default=256)
+    a = ap.parse_args()
+    from bench import Instrument
+    from dorknet_amd import perfmodel
+    from dorknet_amd._tensor import as_device
+    from dorknet_amd.optimisers.SGDMomentum import SGDMomentum
+    from examples.resnet18_depsep import ResNet18, synthetic_batch
+    torch.cuda.set_device(0)
+    np.random.seed(0)
+    net = ResNet18("r")
+    net.to_gpu()
+    sgd = SGDMomentum(net, 0.05 * a.batch / 200.0, 0.9)
+    X, _, onehot = synthetic_batch(a.batch, seed=1000)
+    X, onehot = as_device(X), as_device(onehot)
+
+    def step():
+        net.forward(X, onehot)
+        net.backward()
+        sgd.update_weights()
+
+    for _ in range(3):
+        step()
+    torch.cuda.synchronize()
+    with Instrument(perfmodel.MODEL.keys()) as ins:
+        step()
+    torch.cuda.synchronize()
+    rows = []
+    for n, calls in ins.calls.items():
+        for e0, e1, args in calls:
+            rows.append((e0, n, args, e0.elapsed_time(e1)))
+    # issue order: by the start event's time relative to the first event recorded
+    first = min(rows, key=lambda r: 0)[0]
+    rows.sort(key=lambda r: first.elapsed_time(r[0]))
+    tot = 0.0
+    for _, n, args, ms in rows:
+        us = 1e3 * ms
+        tot += us
+        if us < a.min_us:
+            continue
+        f, b = perfmodel.work(n, args)
+        frac = perfmodel.bound_time_s(f, b, n) / (ms / 1e3) if ms > 0 else 0.0
+        ints = [x for x in args if isinstance(x, int) and abs(x) < 1 << 20]
+        print(f"{us:8.1f} us  frac {frac:5.3f}  {'mfma' if perfmodel.is_mfma_bound(f, b, n) else 'hbm '}  "
+              f"{n:34s} {ints[:10]}", flush=True)
+    print(f"total {tot:.1f} us over {len(rows)} calls")
+
+
+if __name__ == "__main__":
+    main()
