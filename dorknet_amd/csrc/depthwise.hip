@@ -527,8 +527,11 @@ __global__ __launch_bounds__(256) void dw_wgrad_partial_kernel(const T* __restri
 // where xb is the layer's input (bn_in(X) when it consumed a BNOut).  Reindexing the weight
 // gradient (depthwise_convolution.py:198-221) by input pixel makes its dy taps exactly the
 // dgrad's window.
-// Block = one image, a CL-column strip, CG channel groups of 4 (CG * CL = 256); it walks the
-// rows top to bottom.  Per row: the block forms dy row h+1 for its CL + 2 columns into one of two
+// Block = a run of images (nranges runs over the batch; one image each when the grid fits the
+// chip anyway), a CL-column strip, CG channel groups of 4 (CG * CL = 256); it walks the rows of
+// its images top to bottom as one tall image -- the zero dy row H of an image is row -1 of the
+// next, so the 3x3 window and the one-row prefetch run on across image boundaries and a small
+// image's blocks do not each pay the prologue and the reductions.  Per row: the block forms dy row h+1 for its CL + 2 columns into one of two
 // LDS slots (g and x1 for the row after were loaded one iteration earlier), one barrier, then
 // each thread slides its 3x3 register window down by that row and produces dx[h][w] for its 4
 // channels.  dx is bit-identical to dk_bn_bwd_apply_f32 -> dk_dwconv_dgrad_ex_f32 (same tap
@@ -553,7 +556,7 @@ __global__ __launch_bounds__(256) void dw_bwd_fused_kernel(const T* __restrict__
                                                            T* __restrict__ dx, const T* __restrict__ res,
                                                            double* __restrict__ spart, float* __restrict__ wpart,
                                                            int N, int H, int W, int C, int CL, FoldTail ft,
-                                                           JoinBwd jn = JoinBwd{}, int nt = 0) {
+                                                           JoinBwd jn = JoinBwd{}, int nt = 0, int nranges = 0) {
   static_assert(!(JOIN && sizeof(T) != 4), "the join fusion is fp32 only");
   static_assert(!STATS || BNX, "input-BN partials need the input BN");
   static_assert(!(JOIN && (STATS || BNX)), "the join's partials replace the input BN's");
@@ -567,8 +570,10 @@ __global__ __launch_bounds__(256) void dw_bwd_fused_kernel(const T* __restrict__
   const int nct = (W + CL - 1) / CL, ncht = (C >> 2) / CG;
   const int bid = xcd_block(blockIdx.x, gridDim.x);
   const int cht = bid % ncht;
-  const int strip = bid / ncht;  // (image, column strip): the partial-sum row
-  const int ct = strip % nct, n = strip / nct;
+  const int strip = bid / ncht;  // (image run, column strip): the partial-sum row
+  const int ct = strip % nct, nr = strip / nct;
+  const int n0 = nranges ? (int)((long long)nr * N / nranges) : nr;
+  const int n1 = nranges ? (int)((long long)(nr + 1) * N / nranges) : nr + 1;
   const int c = (cht * CG + cg) * 4;
   const int w = ct * CL + cl;
   const bool win_ok = w < W;
@@ -644,25 +649,25 @@ __global__ __launch_bounds__(256) void dw_bwd_fused_kernel(const T* __restrict__
     }
     return ok ? o : f32x4{0.f, 0.f, 0.f, 0.f};
   };
-  auto pix = [&](int hh, int ww) { return (uint32_t)(((n * H + hh) * W + ww) * C + c); };
+  auto pix = [&](int nn, int hh, int ww) { return (uint32_t)(((nn * H + hh) * W + ww) * C + c); };
   // raw g / x1 of the next dy row to publish, and this thread's input / residual (/ join mask and
   // bn_j input) of the next dx row
   f32x4 g0, x0, g1, x1v, xr, rv, jxv;
   uint32_t jmv = 0;
-  auto load_dy_row = [&](int hh) {
+  auto load_dy_row = [&](int nn, int hh) {
     const bool rok = (unsigned)hh < (unsigned)H;
-    g0 = bload4e<T>(rg, rok && cok0, pix(hh, col0));
-    x0 = bload4e<T>(r1, rok && cok0, pix(hh, col0));
-    g1 = bload4e<T>(rg, rok && cok1, pix(hh, col1));
-    x1v = bload4e<T>(r1, rok && cok1, pix(hh, col1));
+    g0 = bload4e<T>(rg, rok && cok0, pix(nn, hh, col0));
+    x0 = bload4e<T>(r1, rok && cok0, pix(nn, hh, col0));
+    g1 = bload4e<T>(rg, rok && cok1, pix(nn, hh, col1));
+    x1v = bload4e<T>(r1, rok && cok1, pix(nn, hh, col1));
   };
-  auto load_x_row = [&](int hh) {
+  auto load_x_row = [&](int nn, int hh) {
     const bool ok = win_ok && hh < H;
-    xr = bload4e<T>(rx, ok, pix(hh, w));
-    rv = bload4e<T>(rres, ok, pix(hh, w));
+    xr = bload4e<T>(rx, ok, pix(nn, hh, w));
+    rv = bload4e<T>(rres, ok, pix(nn, hh, w));
     if constexpr (JOIN) {
-      jmv = __builtin_amdgcn_raw_buffer_load_b32(rjm, (int)(ok ? pix(hh, w) : kOOBBytes), 0, 0);  // 4 mask bytes
-      jxv = bload4e<float>(rjx, ok, pix(hh, w));
+      jmv = __builtin_amdgcn_raw_buffer_load_b32(rjm, (int)(ok ? pix(nn, hh, w) : kOOBBytes), 0, 0);  // 4 mask bytes
+      jxv = bload4e<float>(rjx, ok, pix(nn, hh, w));
     }
   };
   double s1[4] = {0.0, 0.0, 0.0, 0.0}, s2[4] = {0.0, 0.0, 0.0, 0.0};
@@ -675,14 +680,20 @@ __global__ __launch_bounds__(256) void dw_bwd_fused_kernel(const T* __restrict__
       wacc[r][s] = f32x4{0.f, 0.f, 0.f, 0.f};
       d[r][s] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
-  load_dy_row(0);  // row -1 is all padding
-  load_x_row(0);
-  T* dxcol = dx ? dx + (size_t)pix(0, w) : nullptr;
-  for (int rr = 0; rr <= H; ++rr) {  // publish dy row rr, then finish dx row rr - 1
+  load_dy_row(n0, 0);  // row -1 is all padding
+  load_x_row(n0, 0);
+  // flattened (image, row) loop: publish dy row rr of image n, then finish dx row rr - 1
+  const int iters = (n1 - n0) * (H + 1);
+  int n = n0, rr = 0;
+  for (int it = 0; it < iters; ++it) {
     const int rowok = rr < H;
     const f32x4 d0 = xform(g0, x0, rowok && cok0), d1 = xform(g1, x1v, rowok && cok1);
-    if (rr + 1 < H) load_dy_row(rr + 1);
-    f32x4* slot = ring + (rr & 1) * NI;
+    // the next row; the next image's row 0 two iterations ahead (dy row H is zero, not loaded)
+    if (rr + 1 < H)
+      load_dy_row(n, rr + 1);
+    else if (rr + 1 == H && n + 1 < n1)
+      load_dy_row(n + 1, 0);
+    f32x4* slot = ring + (it & 1) * NI;
     slot[tid] = d0;
     if (two) slot[tid + 256] = d1;
     __syncthreads();
@@ -692,11 +703,20 @@ __global__ __launch_bounds__(256) void dw_bwd_fused_kernel(const T* __restrict__
       d[1][s] = d[2][s];
       d[2][s] = slot[(cl + s) * CG + cg];
     }
-    if (rr == 0) continue;
-    const int h = rr - 1;
+    const int nn = n;
+    if (++rr > H) {
+      rr = 0;
+      ++n;
+    }
+    if (rr == 1) continue;  // just published row 0 of an image: no dx row to finish yet
+    const int h = (rr == 0 ? H + 1 : rr) - 2;  // the dx row of image nn finished now
     const f32x4 xh = xr, rh = rv, jh = jxv;
     const uint32_t jmh = jmv;
-    if (h + 1 < H) load_x_row(h + 1);
+    if (h + 1 < H)
+      load_x_row(nn, h + 1);
+    else if (nn + 1 < n1)
+      load_x_row(nn + 1, 0);
+    T* dxcol = dx ? dx + (size_t)pix(nn, 0, w) : nullptr;
     f32x4 xb = xh;
     if constexpr (BNX) xb = win_ok ? bn_in4(xh, bm, bi, bg, bb, bn.relu) : f32x4{0.f, 0.f, 0.f, 0.f};
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
@@ -801,7 +821,28 @@ static inline int dwb_cl(int W, int C) {
   while (cg > 1 && C4 % cg) cg >>= 1;
   return 256 / cg;
 }
-static inline int dwb_strips(int N, int W, int cl) { return N * ((W + cl - 1) / cl); }
+// Image runs of the fused stride-1 backward: one image per block while N * column strips * channel
+// tiles blocks fit DORKNET_DWB_BLOCKS (default 768 = three resident blocks per CU: its LDS and
+// registers allow three); above that the batch is dealt into runs so the grid is one round (a
+// second, partial round of blocks cost small images up to twice the time: 7 x 7 x 512 ran 1024
+// one-image blocks).  0 = one image per block always.
+static int g_dwb_blocks = -1;  // tuning knob dk_debug_set_gemm_config(7, v)
+void dwb_blocks_set(int v) { g_dwb_blocks = v; }
+static inline int dwb_target_blocks() {
+  if (g_dwb_blocks < 0) {
+    const char* e = getenv("DORKNET_DWB_BLOCKS");
+    g_dwb_blocks = e ? atoi(e) : 768;
+  }
+  return g_dwb_blocks;
+}
+static inline int dwb_nranges(int N, int W, int C, int cl) {
+  const int per_image = ((W + cl - 1) / cl) * ((C / 4) / (256 / cl));
+  const int t = dwb_target_blocks();
+  if (t <= 0 || (long long)N * per_image <= t) return N;
+  const int r = t / per_image;
+  return r < 1 ? 1 : (r > N ? N : r);
+}
+static inline int dwb_strips(int N, int W, int C, int cl) { return dwb_nranges(N, W, C, cl) * ((W + cl - 1) / cl); }
 
 static int dw_wgrad_blocks(int N, int OH, int OW, int C) {
   const int C4 = C / 4;
@@ -1087,7 +1128,7 @@ DK_API int dk_dwconv_wgrad_f32(const float* dy, const float* x, int N, int H, in
 // Fused stride-1 backward (dw_bwd_fused_kernel).  Workspace: the weight-gradient partials.
 DK_API int dk_dwconv_bwd_bnbwd_stats_rows(int N, int H, int W, int C) {
   (void)H;
-  return (C < 4 || C % 4) ? 0 : dwb_strips(N, W, dwb_cl(W, C));
+  return (C < 4 || C % 4) ? 0 : dwb_strips(N, W, C, dwb_cl(W, C));
 }
 
 DK_API size_t dk_dwconv_bwd_bnbwd_workspace_bytes(int N, int H, int W, int C, int R, int S) {
@@ -1116,7 +1157,8 @@ static int dw_bwd_fused(const T* g, const T* bn_x, int N, int H, int W, int C, c
   const size_t bytes = (size_t)N * H * W * C * sizeof(T);
   if (!fits(bytes)) return DK_ERR_ARGS;
   if (ws_bytes < dk_dwconv_bwd_bnbwd_workspace_bytes(N, H, W, C, R, S)) return DK_ERR_WORKSPACE;
-  const int strips = dwb_strips(N, W, cl);
+  const int strips = dwb_strips(N, W, C, cl);
+  const int nranges = dwb_nranges(N, W, C, cl);
   const int ncht = (C / 4) / (256 / cl);
   float* wpart = static_cast<float*>(ws);
   const BnBwdOut ob{out_mean, out_invstd, out_gamma, out_beta, k12, out_relu};
@@ -1133,7 +1175,7 @@ static int dw_bwd_fused(const T* g, const T* bn_x, int N, int H, int W, int C, c
       (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,       \
                                 (int)shm);                                                                           \
     hipLaunchKernelGGL(k, grid, dim3(256), shm, st, g, bn_x, (uint32_t)bytes, ob, x, bn, w_crs, dx, residual, part,  \
-                       wpart, N, H, W, C, cl, ft, JoinBwd{}, nt_stores());                                                        \
+                       wpart, N, H, W, C, cl, ft, JoinBwd{}, nt_stores(), nranges);                                                        \
   }
   if (out_relu) {
     if (part) DWB_LAUNCH(true, true, true) else if (bn_mean) DWB_LAUNCH(true, false, true)
@@ -1232,7 +1274,8 @@ DK_API int dk_dwconv_bwd_bnbwd_join_f32(const float* g, const float* bn_x, int N
   const size_t bytes = (size_t)N * H * W * C * sizeof(float);
   if (!fits(bytes)) return DK_ERR_ARGS;
   if (ws_bytes < dk_dwconv_bwd_bnbwd_workspace_bytes(N, H, W, C, R, S)) return DK_ERR_WORKSPACE;
-  const int strips = dwb_strips(N, W, cl);
+  const int strips = dwb_strips(N, W, C, cl);
+  const int nranges = dwb_nranges(N, W, C, cl);
   const int ncht = (C / 4) / (256 / cl);
   float* wpart = static_cast<float*>(ws);
   const BnBwdOut ob{out_mean, out_invstd, out_gamma, out_beta, k12, out_relu};
@@ -1250,7 +1293,7 @@ DK_API int dk_dwconv_bwd_bnbwd_join_f32(const float* g, const float* bn_x, int N
       (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,       \
                                 (int)shm);                                                                           \
     hipLaunchKernelGGL(k, grid, dim3(256), shm, st, g, bn_x, (uint32_t)bytes, ob, x, BnIn{}, w_crs, dx, residual,    \
-                       part, wpart, N, H, W, C, cl, ft, jn, nt_stores());                                                         \
+                       part, wpart, N, H, W, C, cl, ft, jn, nt_stores(), nranges);                                                         \
   }
   if (out_relu)
     DWJ_LAUNCH(true)

@@ -182,6 +182,9 @@ int nt_stores();
 int splitk_reduce(const float* ws, int splits, int M, int N, float* out, const float* w, float l2, int mode, int C,
                   int Cp, int R, int S, hipStream_t st);
 
+// Blocks the fused stride-1 depthwise backward aims for (depthwise.hip; knob kind 7, -1 = default).
+void dwb_blocks_set(int v);
+
 // Streaming pointwise kernels (pw_stream.hip) for the K = C = 64 shapes.
 bool pw_stream_enabled();  // DORKNET_PW_STREAM (default 1; 0 = the tiled engine everywhere, for A/B runs)
 void pw_stream_set(int v);  // tuning knob (dk_debug_set_gemm_config kind 3)

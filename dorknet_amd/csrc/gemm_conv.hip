@@ -80,6 +80,10 @@ DK_API int dk_debug_set_gemm_config(int kind, int cfg) {
     pw_stream_bwd_pf_set(cfg < 0 ? 0 : cfg);
     return 0;
   }
+  if (kind == 7) {  // blocks the fused stride-1 depthwise backward aims for (0: one image per block)
+    dwb_blocks_set(cfg < 0 ? 768 : cfg);
+    return 0;
+  }
   if (kind == 4) {  // nontemporal output stores (kernels that support them)
     g_nt_stores = cfg < 0 ? 0 : cfg;
     return 0;

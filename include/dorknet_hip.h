@@ -53,7 +53,10 @@ int dk_mixup_f32(const float* a, const float* b, long long n, float p, float one
  * kind 2: split-K grids sized to one round of resident blocks (1 = default, also for -1) or
  * the fixed ~1024-block split (0); returns 0.
  * kind 3: the streaming pointwise kernels for K = C = 64 (1 = default, also for -1; 0 = the
- * tiled engine for every shape, as DORKNET_PW_STREAM=0); returns 0. */
+ * tiled engine for every shape, as DORKNET_PW_STREAM=0); returns 0.
+ * kind 4: nontemporal output stores; kind 5: the streaming fused pointwise backward's operand
+ * prefetch; kind 6: unused; kind 7: blocks the fused stride-1 depthwise backward aims for (its
+ * batch is dealt into image runs above that; 0 = one image per block; -1 = default 768). */
 int dk_debug_set_gemm_config(int kind, int cfg);
 
 /* Bandwidth ceiling probe (not on the training path; scripts/stream_ceiling.py): reads nin

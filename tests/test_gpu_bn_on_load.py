@@ -421,14 +421,28 @@ def test_pointwise_dgrad_bnbwd_bitwise(relu, bn_in, resid, K):
         assert float((s1 - s0).norm() / s0.norm()) < 1e-12
 
 
-@pytest.mark.parametrize("relu,bn_in,resid,C,need_dx", [(0, True, False, 64, True), (0, True, True, 32, True),
-                                                         (1, False, False, 16, True), (0, False, True, 128, True),
-                                                         (0, True, False, 8, False), (1, True, True, 256, True)])
-def test_depthwise_bwd_bnbwd(relu, bn_in, resid, C, need_dx):
+@pytest.mark.parametrize("relu,bn_in,resid,C,need_dx,runs", [(0, True, False, 64, True, -1),
+                                                              (0, True, True, 32, True, -1),
+                                                              (1, False, False, 16, True, -1),
+                                                              (0, False, True, 128, True, -1),
+                                                              (0, True, False, 8, False, -1),
+                                                              (1, True, True, 256, True, -1),
+                                                              (0, True, True, 64, True, 2),
+                                                              (1, True, False, 256, True, 5)])
+def test_depthwise_bwd_bnbwd(relu, bn_in, resid, C, need_dx, runs):
     """dk_dwconv_bwd_bnbwd_f32 (BN-backward apply + dgrad + wgrad in one pass) against the unfused
     sequence dk_bn_bwd_apply_f32 -> dk_dwconv_dgrad_ex_f32 + dk_dwconv_wgrad_bnx_f32: dx bitwise;
     the input BN's partial sums and the weight gradient (other summation orders) to fp32
-    rounding."""
+    rounding.  runs > 0: the kernel's block target (knob 7) forces blocks that walk runs of
+    several images (uneven: 3 images over 2 runs), as the full-size small-image layers do."""
+    lib.dk_debug_set_gemm_config(7, runs)
+    try:
+        _depthwise_bwd_bnbwd(relu, bn_in, resid, C, need_dx)
+    finally:
+        lib.dk_debug_set_gemm_config(7, -1)
+
+
+def _depthwise_bwd_bnbwd(relu, bn_in, resid, C, need_dx):
     rng = np.random.RandomState(relu + 2 * bn_in + 4 * resid + C + 8 * need_dx)
     N, H, W, R = 3, 13, 11, 3
     xo = nhwc(rng.randn(N, C, H, W))        # this layer's output = the following BN's input
