@@ -211,4 +211,19 @@ int pw_stream_dgrad_bnbwd(const float* g, const float* bn_x, int M, const float*
                           const float* iis, const float* ig, const float* ib, int irelu, double* part,
                           hipStream_t st, const struct FoldTail* ft = nullptr);
 
+// bf16 streaming pointwise kernels (pw_stream_bf16.hip, BASELINE config 5): K, C in {64, 128}.
+bool pw_stream_bf16_fwd_ok(int K, int C, int M);
+int pw_stream_bf16_fwd_rows(int M, int K, int C);
+int pw_stream_bf16_fwd(const bf16_t* x, int M, const float* w, int K, int C, const float* bias, bf16_t* y,
+                       const float* im, const float* iis, const float* ig, const float* ib, int irelu, double* part,
+                       hipStream_t st, const struct FoldTail* ft = nullptr);
+bool pw_stream_bf16_dgrad_ok(int K, int C, int M);
+int pw_stream_bf16_dgrad_rows(int M, int K, int C);
+int pw_stream_bf16_dgrad_bnbwd(const bf16_t* g, const bf16_t* bn_x, int M, int K, int C, const float* om,
+                               const float* ois, const float* og, const float* ob, int orelu, const float* k12,
+                               bf16_t* dy_out, const float* w, bf16_t* dx, const bf16_t* res, const bf16_t* x,
+                               const float* im, const float* iis, const float* ig, const float* ib, int irelu,
+                               double* part, hipStream_t st, const struct FoldTail* ft = nullptr);
+void pw_stream_bf16_set(int v);  // tuning knob (dk_debug_set_gemm_config kind 9)
+
 }  // namespace dk

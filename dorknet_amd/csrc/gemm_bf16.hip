@@ -26,8 +26,13 @@ static inline ImgDescE<bf16_t, true> img1_h(const bf16_t* x, int N, int H, int W
 static inline bool al8(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 7) == 0; }
 }  // namespace dk
 
-// partial-statistics rows of dk_pwconv_fwd_ex_bf16 (always the tiled engine: one row per M tile)
-DK_API int dk_pwconv_fwd_bf16_stats_rows(int N, int OH, int OW, int K, int C) { return stats_rows(N * OH * OW, K, C); }
+// partial-statistics rows of dk_pwconv_fwd_ex_bf16: one per streaming block (K, C in {64, 128},
+// pw_stream_bf16.hip), else one per M tile of the tiled engine
+DK_API int dk_pwconv_fwd_bf16_stats_rows(int N, int OH, int OW, int K, int C) {
+  const int M = N * OH * OW;
+  if (pw_stream_bf16_fwd_ok(K, C, M)) return pw_stream_bf16_fwd_rows(M, K, C);
+  return stats_rows(M, K, C, kRowFwdH, kMfBf16);
+}
 
 DK_API int dk_pwconv_fwd_ex_bf16(const bf16_t* x, int N, int H, int W, int C, const float* w_kc, int K, int stride,
                                  const float* bias, bf16_t* y, int OH, int OW, const float* bn_mean,
@@ -35,19 +40,29 @@ DK_API int dk_pwconv_fwd_ex_bf16(const bf16_t* x, int N, int H, int W, int C, co
                                  double* stats, void* stream) {
   if (C % 4 || K % 4 || !al8(x) || !al8(y) || !aligned16(w_kc) || (bias && !aligned16(bias))) return DK_ERR_ARGS;
   if (!fits((size_t)N * H * W * C * 4) || !fits((size_t)N * OH * OW * K * 4)) return DK_ERR_ARGS;
+  const hipStream_t st = as_stream(stream);
+  if (stride == 1 && H == OH && W == OW && pw_stream_bf16_fwd_ok(K, C, N * OH * OW) && aligned16(x) &&
+      (!bn_mean || bn_ok(bn_mean, bn_invstd, bn_gamma, bn_beta))) {
+    // the streaming kernel (pw_stream_bf16.hip): bit-identical y, its own partial-row grouping
+    const int M = N * OH * OW;
+    FoldTail ft;
+    if (stats) fold_take(stats, pw_stream_bf16_fwd_rows(M, K, C), K, 1, &ft);
+    return fold_status(pw_stream_bf16_fwd(x, M, w_kc, K, C, bias, y, bn_mean, bn_invstd, bn_gamma, bn_beta, bn_relu,
+                                          stats, st, stats ? &ft : nullptr),
+                       stats ? ft : FoldTail{});
+  }
   const ImgDescE<bf16_t, true> a = img1_h(x, N, H, W, C, OH, OW, stride, N * OH * OW);
   const MatDesc b = mat(w_kc, K, C, K);
-  const hipStream_t st = as_stream(stream);
   const int M = a.M;
   auto run = [&](const auto& da) -> int {
     using DA = std::decay_t<decltype(da)>;
     if (stats) {
       EpStoreStatsT<bf16_t> ep{};
       ep.out = y, ep.ldo = K, ep.bias = bias, ep.v4 = 1, ep.res = nullptr, ep.part = stats;
-      return igemm_rows<LdImgKC, DA, LdMatKC, MatDesc, EpStoreStatsT<bf16_t>, kRowPlain, kMfBf16>(da, b, ep, M, K, C, st);
+      return igemm_rows<LdImgKC, DA, LdMatKC, MatDesc, EpStoreStatsT<bf16_t>, kRowFwdH, kMfBf16>(da, b, ep, M, K, C, st);
     }
     EpStoreT<bf16_t> ep{y, K, bias, 1, nullptr};
-    return igemm_rows<LdImgKC, DA, LdMatKC, MatDesc, EpStoreT<bf16_t>, kRowPlain, kMfBf16>(da, b, ep, M, K, C, st);
+    return igemm_rows<LdImgKC, DA, LdMatKC, MatDesc, EpStoreT<bf16_t>, kRowFwdH, kMfBf16>(da, b, ep, M, K, C, st);
   };
   if (bn_mean) {
     if (!bn_ok(bn_mean, bn_invstd, bn_gamma, bn_beta) || C > 2048) return DK_ERR_ARGS;
@@ -95,7 +110,7 @@ DK_API int dk_pwconv_wgrad_bnx_bf16(const bf16_t* dy, const bf16_t* x, int N, in
   const int Kred = N * OH * OW;
   if (C % 4 || K % 4 || !al8(x) || !al8(dy) || !fits((size_t)N * H * W * C * 4) || !fits((size_t)Kred * K * 4))
     return DK_ERR_ARGS;
-  if (ws_bytes < splitk_ws_bytes(K, C, Kred)) return DK_ERR_WORKSPACE;
+  if (ws_bytes < splitk_ws_bytes(K, C, Kred, kMfBf16)) return DK_ERR_WORKSPACE;
   const MatDescE<bf16_t> a = mat_h(dy, Kred, K, K);
   const ImgDescE<bf16_t> bi = img_h(x, N, H, W, C, OH, OW, 1, 1, stride, 1, 0, Kred);
   float* part = static_cast<float*>(ws);
@@ -117,7 +132,9 @@ DK_API int dk_pwconv_wgrad_bnx_bf16(const bf16_t* dy, const bf16_t* x, int N, in
 }
 
 DK_API int dk_pwconv_dgrad_bnbwd_bf16_stats_rows(int N, int OH, int OW, int K, int C) {
-  return stats_rows(N * OH * OW, C, K, kRowBnBwd);
+  const int M = N * OH * OW;
+  if (pw_stream_bf16_dgrad_ok(K, C, M)) return pw_stream_bf16_dgrad_rows(M, K, C);
+  return stats_rows(M, C, K, kRowBnBwd, kMfBf16);
 }
 
 // dk_pwconv_dgrad_bnbwd_f32 for bf16 storage: dy = the following BatchNorm's backward applied
@@ -136,6 +153,17 @@ DK_API int dk_pwconv_dgrad_bnbwd_bf16(const bf16_t* g, const bf16_t* bn_x, int N
   if ((residual && !al8(residual)) || (x && !al8(x))) return DK_ERR_ARGS;
   if (!fits((size_t)M * K * 4) || !fits((size_t)M * C * 4) || (part != nullptr) != (x != nullptr)) return DK_ERR_ARGS;
   if (!out_mean || !out_invstd || !out_gamma || !out_beta || !k12 || (size_t)K * 32 > 64 * 1024) return DK_ERR_ARGS;
+  if (pw_stream_bf16_dgrad_ok(K, C, M) && aligned16(g) && aligned16(bn_x) && (!dy_out || aligned16(dy_out)) &&
+      (!part || bn_ok(bn_mean, bn_invstd, bn_gamma, bn_beta))) {
+    // the streaming kernel (pw_stream_bf16.hip): bit-identical dy and dx, its own partial rows
+    FoldTail ft;
+    if (part) fold_take(part, pw_stream_bf16_dgrad_rows(M, K, C), C, 1, &ft);
+    return fold_status(pw_stream_bf16_dgrad_bnbwd(g, bn_x, M, K, C, out_mean, out_invstd, out_gamma, out_beta,
+                                                  out_relu, k12, dy_out, w_kc, dx, residual, x, bn_mean, bn_invstd,
+                                                  bn_gamma, bn_beta, bn_relu, part, as_stream(stream),
+                                                  part ? &ft : nullptr),
+                       part ? ft : FoldTail{});
+  }
   MatBwdDescE<bf16_t> a;
   static_cast<MatDescE<bf16_t>&>(a) = mat_h(g, M, K, M);
   a.x = bn_x;

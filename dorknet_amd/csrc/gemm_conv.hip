@@ -84,6 +84,10 @@ DK_API int dk_debug_set_gemm_config(int kind, int cfg) {
     dwb_blocks_set(cfg < 0 ? 768 : cfg);
     return 0;
   }
+  if (kind == 9) {  // the bf16 streaming pointwise kernels (pw_stream_bf16.hip) on / off
+    pw_stream_bf16_set(cfg);
+    return 0;
+  }
   if (kind == 4) {  // nontemporal output stores (kernels that support them)
     g_nt_stores = cfg < 0 ? 0 : cfg;
     return 0;

@@ -1169,11 +1169,20 @@ static int launch_igemm(const DA& da, const DB& db, const EP& ep, int M, int N, 
 // Row-problem kinds with their own tile choice: plain loaders, and the BN-backward-on-load A
 // operand (dk_pwconv_dgrad_bnbwd_f32), whose per-element transform is repeated for every column
 // tile -- wide column tiles amortise it.
-enum : int { kRowPlain = 0, kRowBnBwd = 1, kRowConv = 2 };  // kRowConv: R x S > 1 image forward
+// kRowConv: R x S > 1 image forward; kRowFwdH: the bf16 pointwise forward (its own tuning)
+enum : int { kRowPlain = 0, kRowBnBwd = 1, kRowConv = 2, kRowFwdH = 3 };
 
-static inline int row_config(int M, int N, int K, int kind = kRowPlain) {
+static inline int row_config(int M, int N, int K, int kind = kRowPlain, int mf = kMfF32) {
   if (g_cfg_override[0] >= 0) return g_cfg_override[0];
   (void)M;
+  if (mf == kMfBf16) {
+    // bf16 MFMA (config 5's 14 x 14 and 7 x 7 units at batch 512; scripts/bf16_gemm_tune.py,
+    // profiles/r03k_bf16_gemm_tune.txt): the tiles with 8 waves or 128 columns, whose blocks run
+    // more MFMAs per dependent load round trip
+    if (kind == kRowBnBwd) return N <= 128 ? 16 : (N <= 256 ? (K >= 512 ? 13 : 16) : 13);
+    if (kind == kRowFwdH && N >= 256) return (K >= 512 && N >= 512) ? 16 : 13;
+  }
+  if (kind == kRowFwdH) kind = kRowPlain;
   if (kind == kRowBnBwd) {
     // Measured on MI355X (scripts/gemm_tune.py --fused-only, profiles/r01h_gemm_tune_fused.txt)
     if (N <= 64) return 8;                // 64x64x32
@@ -1193,7 +1202,7 @@ static inline int row_config(int M, int N, int K, int kind = kRowPlain) {
 template <template <int, int, int> class LA, class DA, template <int, int, int> class LB, class DB, class EP,
           int KIND = kRowPlain, int MF = kMfF32>
 static int igemm_rows(const DA& da, const DB& db, const EP& ep, int M, int N, int Ktot, hipStream_t st) {
-  switch (row_config(M, N, Ktot, KIND)) {
+  switch (row_config(M, N, Ktot, KIND, MF)) {
 #define DK_CASE(id, bm, bn, bk, wm, wn) \
   case id:                              \
     return launch_igemm<bm, bn, bk, wm, wn, LA, DA, LB, DB, EP, MF>(da, db, ep, M, N, Ktot, 1, st);
@@ -1205,9 +1214,11 @@ static int igemm_rows(const DA& da, const DB& db, const EP& ep, int M, int N, in
 }
 
 // Reduction-heavy problems (wgrad): split K over enough blocks to fill the chip.
-static inline int splitk_config(int M, int N, int Kred) {
+static inline int splitk_config(int M, int N, int Kred, int mf = kMfF32) {
   if (g_cfg_override[1] >= 0) return g_cfg_override[1];
   (void)Kred;
+  // bf16 MFMA: 128 x 128 tiles for the 14 x 14 / 7 x 7 weight gradients (profiles/r03k_bf16_gemm_tune.txt)
+  if (mf == kMfBf16 && M >= 128 && N >= 128) return 4;
   // Wide column tiles when M <= 64 < N: the A operand (for the stem the BN-backward-on-load dy,
   // formed from 2 x 822 MB) is streamed half as often -- the stem (N = R*S*Cp = 100) in one
   // column tile; BASELINE config 2's 3x3 conv (N = 576): 594 vs 628 us (profiles/r01j_gemm_tune_all.txt).
@@ -1238,7 +1249,7 @@ static inline int wgrad_splits(int M, int N, int Kred, const TileCfg& c) {
 template <template <int, int, int> class LA, class DA, template <int, int, int> class LB, class DB, int MF = kMfF32>
 static int igemm_splitk(const DA& da, const DB& db, float* ws, int M, int N, int Kred, hipStream_t st,
                         int* splits_out) {
-  const int id = splitk_config(M, N, Kred);
+  const int id = splitk_config(M, N, Kred, MF);
   if (id < 0 || id >= kNumSplitCfg) return DK_ERR_ARGS;
   const int splits = wgrad_splits(M, N, Kred, kSplitCfg[id]);  // the workspace's upper bound
   *splits_out = splits;
@@ -1255,8 +1266,8 @@ static int igemm_splitk(const DA& da, const DB& db, float* ws, int M, int N, int
   }
 }
 
-static inline size_t splitk_ws_bytes(int M, int N, int Kred) {
-  int id = splitk_config(M, N, Kred);
+static inline size_t splitk_ws_bytes(int M, int N, int Kred, int mf = kMfF32) {
+  int id = splitk_config(M, N, Kred, mf);
   if (id < 0 || id >= kNumSplitCfg) id = 0;
   return (size_t)wgrad_splits(M, N, Kred, kSplitCfg[id]) * (size_t)M * (size_t)N * sizeof(float);
 }
@@ -1344,8 +1355,8 @@ static int conv_fwd(const D& a, const float* w_krsc, int K, int Ktot, const floa
 }
 
 // Rows of BatchNorm partial statistics a *_fwd_ex_f32 call writes (one per output tile row).
-static inline int stats_rows(int M, int N, int Ktot, int kind = kRowPlain) {
-  return cdiv(M, kRowCfg[row_config(M, N, Ktot, kind)].BM);
+static inline int stats_rows(int M, int N, int Ktot, int kind = kRowPlain, int mf = kMfF32) {
+  return cdiv(M, kRowCfg[row_config(M, N, Ktot, kind, mf)].BM);
 }
 
 // Forward with an optional input BatchNorm (bn_mean != NULL, see *_bnx_*) and optional output

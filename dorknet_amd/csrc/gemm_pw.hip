@@ -206,7 +206,9 @@ DK_API int dk_pwconv_dgrad_bnbwd_f32(const float* g, const float* bn_x, int N, i
 }
 
 DK_API size_t dk_pwconv_wgrad_workspace_bytes(int N, int OH, int OW, int K, int C) {
-  return splitk_ws_bytes(K, C, N * OH * OW);
+  // (the bf16 twin's tiles can differ: the larger of the two)
+  const size_t a = splitk_ws_bytes(K, C, N * OH * OW), b = splitk_ws_bytes(K, C, N * OH * OW, kMfBf16);
+  return a > b ? a : b;
 }
 
 // dw[k][c] = sum_{n,oh,ow} dy[n,oh,ow,k] * x[n, oh*s, ow*s, c]  (+ l2 * w)   (pointwise_convolution.py:61-64)

@@ -88,7 +88,7 @@ class DepthwiseConvLayer(Layer):
                 stats = torch.empty((rows, 2, C), dtype=torch.float64, device=x.device)
         w = self.learned_params["weights"]  # W[C][R][S], read in place by the _ex entry
         fwd = lib.dk_dwconv_fwd_ex_bf16 if bf else lib.dk_dwconv_fwd_ex_f32
-        if stats is not None and not bf:
+        if stats is not None:
             bn_stats.arm(stats, N * OH * OW)
         r = fwd(x.data_ptr(), N, H, W, C, w.data_ptr(), R, S, self.stride, self.padding, ptr(bias), y.data_ptr(), OH,
                 OW, *(bn.bn_args() if bn is not None else (0, 0, 0, 0, 0)), ptr(stats), st)
@@ -196,7 +196,7 @@ class DepthwiseConvLayer(Layer):
         g = to_nhwc(G.g)
         nb = lib.dk_dwconv_bwd_bnbwd_workspace_bytes(N, H, W, C, R, S)
         bf = x.dtype == BF16
-        tok = bn.arm_partials(part) if part is not None and not bf else None
+        tok = bn.arm_partials(part) if part is not None else None
         r = (lib.dk_dwconv_bwd_bnbwd_bf16 if bf else lib.dk_dwconv_bwd_bnbwd_f32)(
             g.data_ptr(), G.x.data_ptr(), N, H, W, C, *G.bnbwd_args(), x.data_ptr(), w.data_ptr(), R, S,
             self.padding, s or 0.0, gw.data_ptr(), ptr(dx), ptr(res),
@@ -272,7 +272,7 @@ class DepthwiseConvLayer(Layer):
         if rows and self.padding <= R - 1 and (residual is None or res is not None):
             # + stage 1 of the input BatchNorm's backward, in the dgrad epilogue (+ the residual)
             part = torch.empty((rows, 2, C), dtype=torch.float64, device=dx.device)
-            tok = bn.arm_partials(part) if not bf else None
+            tok = bn.arm_partials(part)
             r = dgrad_ex(dy.data_ptr(), N, OH, OW, C, w.data_ptr(), R, S, self.stride, self.padding, dx.data_ptr(), H,
                          W, workspace.get(nb), nb, ptr(res), bn.x.data_ptr(), *bn.bn_args(), part.data_ptr(), st)
             bn.hand_backward_partials(dx, part, r, tok)

@@ -101,7 +101,7 @@ class PointwiseConvLayer(Layer):
             stats = torch.empty((rows, 2, K), dtype=torch.float64, device=x.device)
         if bn is not None or stats is not None or bf:
             fwd = lib.dk_pwconv_fwd_ex_bf16 if bf else lib.dk_pwconv_fwd_ex_f32
-            if stats is not None and not bf:
+            if stats is not None:
                 bn_stats.arm(stats, N * OH * OW)
             r = fwd(x.data_ptr(), N, H, W, Cp, w.data_ptr(), K, s, ptr(bias), y.data_ptr(), OH, OW,
                     *(bn.bn_args() if bn is not None else (0, 0, 0, 0, 0)), ptr(stats), st)
@@ -335,12 +335,14 @@ class PointwiseConvLayer(Layer):
         if bn is not None:
             rows = lib.dk_pwconv_dgrad_bnbwd_bf16_stats_rows(N, OH, OW, K, C)
             part = torch.empty((rows, 2, C), dtype=torch.float64, device=dx.device)
-        lib.dk_pwconv_dgrad_bnbwd_bf16(to_nhwc(bg.g).data_ptr(), bg.x.data_ptr(), N, OH, OW, K, *bg.bnbwd_args(),
-                                       dy_out.data_ptr(), self.learned_params["weights"].data_ptr(), C, dx.data_ptr(),
-                                       ptr(res), *((bn.x.data_ptr(), *bn.bn_args(), part.data_ptr()) if bn is not None
-                                                   else (0, 0, 0, 0, 0, 0, 0)), st)
+        tok = bn.arm_partials(part) if bn is not None else None
+        r = lib.dk_pwconv_dgrad_bnbwd_bf16(to_nhwc(bg.g).data_ptr(), bg.x.data_ptr(), N, OH, OW, K, *bg.bnbwd_args(),
+                                           dy_out.data_ptr(), self.learned_params["weights"].data_ptr(), C,
+                                           dx.data_ptr(), ptr(res),
+                                           *((bn.x.data_ptr(), *bn.bn_args(), part.data_ptr()) if bn is not None
+                                             else (0, 0, 0, 0, 0, 0, 0)), st)
         if bn is not None:
-            bn.hand_backward_partials(dx, part)
+            bn.hand_backward_partials(dx, part, r, tok)
         return dx
 
     def _wgrad(self, dy, x, N, H, W, C, K, s, OH, OW, P, w, bf):
@@ -386,9 +388,10 @@ class PointwiseConvLayer(Layer):
             if bn is not None and (OH, OW) == (H, W):
                 rows = lib.dk_pwconv_dgrad_stats_rows(N, OH, OW, K, C)
                 part = torch.empty((rows, 2, C), dtype=torch.float64, device=dx.device)
-                lib.dk_pwconv_dgrad_ex_bf16(dy.data_ptr(), N, OH, OW, K, w.data_ptr(), C, s, dx.data_ptr(), ptr(res),
-                                            bn.x.data_ptr(), *bn.bn_args(), part.data_ptr(), st)
-                bn.hand_backward_partials(dx, part)
+                tok = bn.arm_partials(part)
+                r = lib.dk_pwconv_dgrad_ex_bf16(dy.data_ptr(), N, OH, OW, K, w.data_ptr(), C, s, dx.data_ptr(),
+                                                ptr(res), bn.x.data_ptr(), *bn.bn_args(), part.data_ptr(), st)
+                bn.hand_backward_partials(dx, part, r, tok)
             else:
                 lib.dk_pwconv_dgrad_ex_bf16(dy.data_ptr(), N, OH, OW, K, w.data_ptr(), C, s, dx.data_ptr(), ptr(res),
                                             0, 0, 0, 0, 0, 0, 0, st)

@@ -1,6 +1,8 @@
-"""Every C-ABI call of one ResNet-18-depsep training step (bs=256) in issue order: entry point,
-its integer arguments (the shape), HIP-event time on the launch stream and the fraction of
-its own roofline bound (perfmodel).  python scripts/call_shapes.py [--config 3|5] [--min-us 20]
+"""Every C-ABI call of one training step in issue order: entry point, its integer arguments (the
+shape), HIP-event time on the launch stream and the fraction of its own roofline bound
+(perfmodel).  The step runs single-stream (DORKNET_ASYNC_WGRAD=0) so that no call's time
+includes a concurrent weight gradient.
+    python scripts/call_shapes.py [--config 3|5] [--min-us 20]
 """
 import argparse
 import os
@@ -15,8 +17,11 @@ import torch  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--min-us", type=float, default=20.0)
-    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--batch", type=int, default=0, help="default: 256 (config 3), 512 (config 5)")
+    ap.add_argument("--config", type=int, choices=[3, 5], default=3)
     a = ap.parse_args()
+    os.environ["DORKNET_ASYNC_WGRAD"] = "0"
+    a.batch = a.batch or (256 if a.config == 3 else 512)
     from bench import Instrument
     from dorknet_amd import perfmodel
     from dorknet_amd._tensor import as_device
@@ -24,15 +29,30 @@ def main():
     from examples.resnet18_depsep import ResNet18, synthetic_batch
     torch.cuda.set_device(0)
     np.random.seed(0)
-    net = ResNet18("r")
-    net.to_gpu()
+    if a.config == 3:
+        net = ResNet18("r")
+        net.to_gpu()
+        X, _, onehot = synthetic_batch(a.batch, seed=1000)
+        X, onehot = as_device(X), as_device(onehot)
+
+        def fb():
+            net.forward(X, onehot)
+            net.backward()
+    else:
+        from examples.mobilenet_stack import MobileNetStack, synthetic_input
+        net = MobileNetStack("m")
+        net.to_gpu()
+        X = synthetic_input(a.batch, seed=0)
+        dY = torch.randn((a.batch, 512, 7, 7), device="cuda").to(torch.bfloat16)
+        dY = dY.contiguous(memory_format=torch.channels_last)
+
+        def fb():
+            net.forward(X, None)
+            net.backward(dY)
     sgd = SGDMomentum(net, 0.05 * a.batch / 200.0, 0.9)
-    X, _, onehot = synthetic_batch(a.batch, seed=1000)
-    X, onehot = as_device(X), as_device(onehot)
 
     def step():
-        net.forward(X, onehot)
-        net.backward()
+        fb()
         sgd.update_weights()
 
     for _ in range(3):

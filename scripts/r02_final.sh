@@ -25,7 +25,7 @@ timeout -k 10 240 rocprofv3 --pmc WRITE_SIZE --kernel-trace -f csv -d "$OUT/pmc_
     > "$OUT/pmc_${TAG}_write.log" 2>&1
 step write $?
 cd "$ROOT"
-python scripts/prof_summary.py "$OUT/prof_$TAG" --steps 7 > "$OUT/kstats_$TAG.md" && head -12 "$OUT/kstats_$TAG.md"
+python scripts/prof_summary.py "$OUT/prof_$TAG" --steps 6 > "$OUT/kstats_$TAG.md" && head -12 "$OUT/kstats_$TAG.md"
 python scripts/pmc_summary.py "$OUT/pmc_$TAG/fetch" "$OUT/pmc_$TAG/write" --out "$OUT/${TAG}_pmc.json" \
     > "$OUT/${TAG}_pmc_summary.txt" 2>&1
 step summary $?

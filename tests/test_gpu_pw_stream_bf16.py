@@ -1,0 +1,123 @@
+"""The bf16 streaming pointwise kernels (csrc/pw_stream_bf16.hip, BASELINE config 5) against the
+tiled engine's bf16 MFMA mode they replace (knob 9 off): y, dy (written through) and dx bitwise
+(same operand rounding, same MFMA k order, same fp32 epilogue), the BatchNorm partial sums to
+fp64 rounding (one row per persistent block instead of one per 64-pixel tile).  Ragged pixel
+counts, every (K, C) pair in {64, 128}, every epilogue option; outputs carved out of NaN-filled
+buffers so that a store past the last row would show."""
+import numpy as np
+import pytest
+import torch
+
+from dorknet_amd._hip import lib, stream_handle
+
+pytestmark = pytest.mark.gpu
+BF16 = torch.bfloat16
+
+
+def padded(M, C, rng=None):
+    """An [M][C] bf16 tensor (random, or NaN when rng is None) inside a buffer 7 rows longer that
+    is NaN past it: (view, whole buffer)."""
+    buf = torch.full(((M + 7) * C,), float("nan"), dtype=BF16, device="cuda")
+    if rng is not None:
+        buf[:M * C] = torch.as_tensor(rng.randn(M * C).astype(np.float32), device="cuda").to(BF16)
+    return buf[:M * C], buf
+
+
+def bn_params(C, rng):
+    return [torch.as_tensor(v.astype(np.float32), device="cuda") for v in
+            (rng.randn(C) * 0.3, rng.rand(C) + 0.5, 1 + 0.3 * rng.randn(C), 0.2 * rng.randn(C))]
+
+
+def tail_is_nan(buf, M, C):
+    return bool(torch.isnan(buf[M * C:].float()).all())
+
+
+@pytest.mark.parametrize("K,C", [(64, 64), (128, 64), (64, 128), (128, 128)])
+@pytest.mark.parametrize("bn,relu,stats,bias,N,H,W", [(True, 1, True, False, 3, 13, 11),
+                                                    (True, 0, True, False, 2, 8, 8),
+                                                    (False, 0, True, True, 2, 7, 5),
+                                                    (True, 1, False, False, 1, 1, 5),
+                                                    (True, 1, True, False, 16, 56, 56)])
+def test_bf16_stream_fwd_matches_tiled_engine(K, C, bn, relu, stats, bias, N, H, W):
+    rng = np.random.RandomState(K + C + 2 * bn + relu + 4 * stats + N)
+    M = N * H * W
+    x, _ = padded(M, C, rng)
+    w = torch.as_tensor(rng.randn(K, C).astype(np.float32) * 0.2, device="cuda")
+    b = torch.as_tensor(rng.randn(K).astype(np.float32), device="cuda") if bias else None
+    p = bn_params(C, rng)
+    st = stream_handle()
+
+    def run(stream_on):
+        lib.dk_debug_set_gemm_config(9, 1 if stream_on else 0)
+        try:
+            y, ybuf = padded(M, K)
+            rows = lib.dk_pwconv_fwd_bf16_stats_rows(N, H, W, K, C)
+            part = torch.zeros((rows, 2, K), dtype=torch.float64, device="cuda") if stats else None
+            bn_args = (*(t.data_ptr() for t in p), relu) if bn else (0, 0, 0, 0, 0)
+            assert lib.dk_pwconv_fwd_ex_bf16(x.data_ptr(), N, H, W, C, w.data_ptr(), K, 1,
+                                             b.data_ptr() if bias else 0, y.data_ptr(), H, W, *bn_args,
+                                             part.data_ptr() if stats else 0, st) == 0
+            torch.cuda.synchronize()
+            return y, ybuf, rows, part
+        finally:
+            lib.dk_debug_set_gemm_config(9, -1)
+
+    y0, _, rows0, part0 = run(False)
+    y1, ybuf1, rows1, part1 = run(True)
+    assert torch.equal(y0, y1)
+    assert tail_is_nan(ybuf1, M, K)
+    if stats:
+        assert rows1 <= max(rows0, 1) or M <= 128
+        s0, s1 = part0.sum(0), part1.sum(0)
+        assert float((s1 - s0).norm() / s0.norm()) < 1e-12
+
+
+@pytest.mark.parametrize("K,C", [(64, 64), (128, 64), (64, 128), (128, 128)])
+@pytest.mark.parametrize("relu,bn_in,resid,dyout,N,H,W", [(1, True, False, True, 3, 13, 11),
+                                                        (0, True, False, True, 2, 8, 8),
+                                                        (1, False, True, True, 3, 13, 11),
+                                                        (1, True, True, False, 5, 7, 9),
+                                                        (0, False, False, True, 1, 1, 3),
+                                                        (1, True, False, True, 16, 56, 56)])
+def test_bf16_stream_dgrad_bnbwd_matches_tiled_engine(K, C, relu, bn_in, resid, dyout, N, H, W):
+    rng = np.random.RandomState(K + C + relu + 2 * bn_in + 4 * resid + N)
+    M = N * H * W
+    xo, _ = padded(M, K, rng)
+    g, _ = padded(M, K, rng)
+    po = bn_params(K, rng)
+    k12 = torch.as_tensor(rng.randn(2 * K).astype(np.float32) * 0.1, device="cuda")
+    w = torch.as_tensor(rng.randn(K, C).astype(np.float32) * 0.2, device="cuda")
+    xin, _ = padded(M, C, rng)
+    pi = bn_params(C, rng)
+    res = padded(M, C, rng)[0] if resid else None
+    st = stream_handle()
+
+    def run(stream_on):
+        lib.dk_debug_set_gemm_config(9, 1 if stream_on else 0)
+        try:
+            dy, dybuf = padded(M, K)
+            dx, dxbuf = padded(M, C)
+            rows = lib.dk_pwconv_dgrad_bnbwd_bf16_stats_rows(N, H, W, K, C)
+            part = torch.zeros((rows, 2, C), dtype=torch.float64, device="cuda")
+            bn_args = (xin.data_ptr(), *(t.data_ptr() for t in pi), 1, part.data_ptr()) if bn_in else (0,) * 7
+            assert lib.dk_pwconv_dgrad_bnbwd_bf16(g.data_ptr(), xo.data_ptr(), N, H, W, K,
+                                                  *(t.data_ptr() for t in po), relu, k12.data_ptr(),
+                                                  dy.data_ptr() if dyout else 0, w.data_ptr(), C, dx.data_ptr(),
+                                                  res.data_ptr() if resid else 0, *bn_args, st) == 0
+            torch.cuda.synchronize()
+            return dy, dybuf, dx, dxbuf, part
+        finally:
+            lib.dk_debug_set_gemm_config(9, -1)
+
+    dy0, _, dx0, _, part0 = run(False)
+    dy1, dybuf1, dx1, dxbuf1, part1 = run(True)
+    assert torch.equal(dx0, dx1)
+    assert tail_is_nan(dxbuf1, M, C)
+    if dyout:
+        assert torch.equal(dy0, dy1)
+        assert tail_is_nan(dybuf1, M, K)
+    else:
+        assert bool(torch.isnan(dybuf1.float()).all())
+    if bn_in:
+        s0, s1 = part0.sum(0), part1.sum(0)
+        assert float((s1 - s0).norm() / s0.norm()) < 1e-12
