@@ -56,12 +56,17 @@ class Instrument:
     """Wraps C-ABI entry points so every call is bracketed by HIP events on the current
     stream (the stream the kernels are launched on)."""
 
-    def __init__(self, names):
+    def __init__(self, names, reserve=0):
+        """reserve: event pairs created up front (the timed region's calls), so that the wrapper
+        only records them -- creating two events per call costs host time in the timed loop."""
+        import torch
         from dorknet_amd._hip import lib
         self.lib = lib
         self.names = list(names)
         self.calls = {n: [] for n in self.names}
         self.orig = {}
+        self.pool = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                     for _ in range(reserve)]
 
     def __enter__(self):
         import torch
@@ -70,9 +75,12 @@ class Instrument:
             self.orig[n] = orig
             calls = self.calls[n]
 
-            def wrapped(*args, _orig=orig, _calls=calls):
-                e0 = torch.cuda.Event(enable_timing=True)
-                e1 = torch.cuda.Event(enable_timing=True)
+            def wrapped(*args, _orig=orig, _calls=calls, _pool=self.pool):
+                if _pool:
+                    e0, e1 = _pool.pop()
+                else:
+                    e0 = torch.cuda.Event(enable_timing=True)
+                    e1 = torch.cuda.Event(enable_timing=True)
                 e0.record()
                 r = _orig(*args)
                 e1.record()
@@ -457,7 +465,7 @@ def other_config(args):
                          "frac_of_roofline": round(v["bound_ms"] / v["ms"], 3) if v["ms"] else None}
                      for n, v in sorted(summ.items(), key=lambda kv: -kv[1]["ms"])}
         torch.cuda.synchronize()
-    ins = Instrument([dominant]) if dominant else None
+    ins = Instrument([dominant], reserve=(breakdown[dominant]["calls"] * args.steps + 8)) if dominant else None
     if ins:
         ins.__enter__()
     t0 = time.perf_counter()
@@ -598,7 +606,7 @@ def main():
         breakdown["_step_roofline_bound_ms"] = round(step_bound, 3)
         barrier()
 
-    ins = Instrument([dominant]) if dominant else None
+    ins = Instrument([dominant], reserve=(breakdown[dominant]["calls"] * args.steps + 8)) if dominant else None
     barrier()
     t0 = time.perf_counter()
     if ins:
