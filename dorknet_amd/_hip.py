@@ -16,7 +16,8 @@ import re
 import torch  # noqa: F401  -- loads torch's HIP runtime first; our .so binds to the same one
 
 _PKG_DIR = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_PKG_DIR, "lib", "libdorknet_hip.so")
+# DORKNET_HIP_LIB: another build of the same library (A/B runs of two builds on one box)
+LIB_PATH = os.environ.get("DORKNET_HIP_LIB") or os.path.join(_PKG_DIR, "lib", "libdorknet_hip.so")
 HEADER_PATH = os.path.join(os.path.dirname(_PKG_DIR), "include", "dorknet_hip.h")
 
 DK_ERR_ARGS = 10001

@@ -650,24 +650,50 @@ __global__ __launch_bounds__(256) void dw_bwd_fused_kernel(const T* __restrict__
     return ok ? o : f32x4{0.f, 0.f, 0.f, 0.f};
   };
   auto pix = [&](int nn, int hh, int ww) { return (uint32_t)(((nn * H + hh) * W + ww) * C + c); };
-  // raw g / x1 of the next dy row to publish, and this thread's input / residual (/ join mask and
-  // bn_j input) of the next dx row
-  f32x4 g0, x0, g1, x1v, xr, rv, jxv;
-  uint32_t jmv = 0;
-  auto load_dy_row = [&](int nn, int hh) {
-    const bool rok = (unsigned)hh < (unsigned)H;
-    g0 = bload4e<T>(rg, rok && cok0, pix(nn, hh, col0));
-    x0 = bload4e<T>(r1, rok && cok0, pix(nn, hh, col0));
-    g1 = bload4e<T>(rg, rok && cok1, pix(nn, hh, col1));
-    x1v = bload4e<T>(r1, rok && cok1, pix(nn, hh, col1));
+  // Prefetched operands, PF rows ahead: raw g / x1 of the dy rows to publish, and this thread's
+  // input / residual (/ join mask and bn_j input) of the dx rows to finish.  bf16 keeps them packed
+  // (2 registers per 4 channels, widened where used) two rows ahead -- the same registers one fp32
+  // row takes -- so twice the bytes are in flight per row step; fp32 stays one row ahead.
+  using Raw = typename std::conditional<sizeof(T) == 2, uint2, f32x4>::type;
+  constexpr int PF = sizeof(T) == 2 ? 2 : 1;
+  struct DyQ {
+    Raw g0, x0, g1, x1;
   };
-  auto load_x_row = [&](int nn, int hh) {
-    const bool ok = win_ok && hh < H;
-    xr = bload4e<T>(rx, ok, pix(nn, hh, w));
-    rv = bload4e<T>(rres, ok, pix(nn, hh, w));
+  struct XQ {
+    Raw xr, rv;
+    f32x4 jxin;    // (the kernel's #defines take jm / ji)
+    uint32_t jmask;
+  };
+  DyQ dq[PF];
+  XQ xq[PF];
+  auto raw_load = [&](__amdgpu_buffer_rsrc_t r, bool ok, uint32_t e) -> Raw {
+    if constexpr (sizeof(T) == 2)
+      return __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(r, (int)(ok ? e * 2u : kOOBBytes), 0, 0));
+    else
+      return bload4e<float>(r, ok, e);
+  };
+  auto widen = [](Raw v) -> f32x4 {
+    if constexpr (sizeof(T) == 2)
+      return bf16x4_to_f32(v);
+    else
+      return v;
+  };
+  // unconditional loads (rows past the run or the zero row H read nothing): no branch around a
+  // load, so the waitcnt pass counts them instead of draining every memory operation
+  auto load_dy_row = [&](DyQ& q, int nn, int hh) {
+    const bool rok = (unsigned)hh < (unsigned)H && nn < n1;
+    q.g0 = raw_load(rg, rok && cok0, pix(nn, hh, col0));
+    q.x0 = raw_load(r1, rok && cok0, pix(nn, hh, col0));
+    q.g1 = raw_load(rg, rok && cok1, pix(nn, hh, col1));
+    q.x1 = raw_load(r1, rok && cok1, pix(nn, hh, col1));
+  };
+  auto load_x_row = [&](XQ& q, int nn, int hh) {
+    const bool ok = win_ok && hh < H && nn < n1;
+    q.xr = raw_load(rx, ok, pix(nn, hh, w));
+    q.rv = raw_load(rres, ok, pix(nn, hh, w));
     if constexpr (JOIN) {
-      jmv = __builtin_amdgcn_raw_buffer_load_b32(rjm, (int)(ok ? pix(nn, hh, w) : kOOBBytes), 0, 0);  // 4 mask bytes
-      jxv = bload4e<float>(rjx, ok, pix(nn, hh, w));
+      q.jmask = __builtin_amdgcn_raw_buffer_load_b32(rjm, (int)(ok ? pix(nn, hh, w) : kOOBBytes), 0, 0);  // 4 mask bytes
+      q.jxin = bload4e<float>(rjx, ok, pix(nn, hh, w));
     }
   };
   double s1[4] = {0.0, 0.0, 0.0, 0.0}, s2[4] = {0.0, 0.0, 0.0, 0.0};
@@ -680,19 +706,27 @@ __global__ __launch_bounds__(256) void dw_bwd_fused_kernel(const T* __restrict__
       wacc[r][s] = f32x4{0.f, 0.f, 0.f, 0.f};
       d[r][s] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
-  load_dy_row(n0, 0);  // row -1 is all padding
-  load_x_row(n0, 0);
+  // load cursors: the (image, row) of the dy row PF steps ahead (row H = the zero row) and of the
+  // next x row (rows 0 .. H-1 of each image of the run)
+  int pn = n0, prr = 0, xn = n0, xhh = 0;
+#pragma unroll
+  for (int k = 0; k < PF; ++k) {
+    load_dy_row(dq[k], pn, prr);
+    if (++prr > H) prr = 0, ++pn;
+    load_x_row(xq[k], xn, xhh);
+    if (++xhh == H) xhh = 0, ++xn;
+  }
   // flattened (image, row) loop: publish dy row rr of image n, then finish dx row rr - 1
   const int iters = (n1 - n0) * (H + 1);
   int n = n0, rr = 0;
   for (int it = 0; it < iters; ++it) {
     const int rowok = rr < H;
-    const f32x4 d0 = xform(g0, x0, rowok && cok0), d1 = xform(g1, x1v, rowok && cok1);
-    // the next row; the next image's row 0 two iterations ahead (dy row H is zero, not loaded)
-    if (rr + 1 < H)
-      load_dy_row(n, rr + 1);
-    else if (rr + 1 == H && n + 1 < n1)
-      load_dy_row(n + 1, 0);
+    const f32x4 d0 = xform(widen(dq[0].g0), widen(dq[0].x0), rowok && cok0);
+    const f32x4 d1 = xform(widen(dq[0].g1), widen(dq[0].x1), rowok && cok1);
+#pragma unroll
+    for (int k = 0; k + 1 < PF; ++k) dq[k] = dq[k + 1];
+    load_dy_row(dq[PF - 1], pn, prr);
+    if (++prr > H) prr = 0, ++pn;
     f32x4* slot = ring + (it & 1) * NI;
     slot[tid] = d0;
     if (two) slot[tid + 256] = d1;
@@ -710,12 +744,12 @@ __global__ __launch_bounds__(256) void dw_bwd_fused_kernel(const T* __restrict__
     }
     if (rr == 1) continue;  // just published row 0 of an image: no dx row to finish yet
     const int h = (rr == 0 ? H + 1 : rr) - 2;  // the dx row of image nn finished now
-    const f32x4 xh = xr, rh = rv, jh = jxv;
-    const uint32_t jmh = jmv;
-    if (h + 1 < H)
-      load_x_row(nn, h + 1);
-    else if (nn + 1 < n1)
-      load_x_row(nn + 1, 0);
+    const f32x4 xh = widen(xq[0].xr), rh = widen(xq[0].rv), jh = xq[0].jxin;
+    const uint32_t jmh = xq[0].jmask;
+#pragma unroll
+    for (int k = 0; k + 1 < PF; ++k) xq[k] = xq[k + 1];
+    load_x_row(xq[PF - 1], xn, xhh);
+    if (++xhh == H) xhh = 0, ++xn;
     T* dxcol = dx ? dx + (size_t)pix(nn, 0, w) : nullptr;
     f32x4 xb = xh;
     if constexpr (BNX) xb = win_ok ? bn_in4(xh, bm, bi, bg, bb, bn.relu) : f32x4{0.f, 0.f, 0.f, 0.f};
