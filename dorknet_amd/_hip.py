@@ -132,7 +132,16 @@ def require_gpu() -> None:
                            "no HIP device is visible")
 
 
+# The current device / stream as raw values straight from torch's C layer: every entry-point call
+# asks for the stream, and torch.cuda.current_stream() (a Stream object, device-index resolution,
+# availability checks) cost ~2.5 us of host time per call -- 300 calls per training step.
+_get_dev = getattr(torch._C, "_cuda_getDevice", None)
+_get_raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+
+
 def stream_handle() -> int:
+    if _get_raw_stream is not None:
+        return _get_raw_stream(_get_dev())
     return torch.cuda.current_stream().cuda_stream
 
 
@@ -150,7 +159,7 @@ class Workspace:
 
     def get(self, nbytes: int) -> int:
         nbytes = max(int(nbytes), 256)
-        key = torch.cuda.current_stream().cuda_stream
+        key = stream_handle()
         buf = self._bufs.get(key)
         if buf is None or buf.numel() < nbytes:
             grow = nbytes if buf is None else max(nbytes, int(buf.numel() * 1.25))
@@ -194,7 +203,7 @@ class FoldResources:
 
     def get(self):
         """(tickets ptr, ticket words, scratch ptr, scratch bytes) for the current stream."""
-        key = torch.cuda.current_stream().cuda_stream
+        key = stream_handle()
         r = self._res.get(key)
         if r is None:
             t = torch.zeros(self.TICKETS, dtype=torch.int32, device="cuda")
@@ -230,7 +239,7 @@ def async_wgrad_enabled() -> bool:
 
 
 def side_stream():
-    dev = torch.cuda.current_device()
+    dev = _get_dev() if _get_dev is not None else torch.cuda.current_device()
     s = _SIDE.get(dev)
     if s is None:
         s = _SIDE[dev] = torch.cuda.Stream(device=dev)

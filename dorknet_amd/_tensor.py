@@ -14,7 +14,13 @@ from ._hip import lib, stream_handle
 F32 = torch.float32
 
 
+_get_dev = getattr(torch._C, "_cuda_getDevice", None)
+
+
 def device() -> torch.device:
+    # (the raw C query: torch.cuda.current_device() re-checks initialisation on every call)
+    if _get_dev is not None and torch.cuda.is_initialized():
+        return torch.device("cuda", _get_dev())
     return torch.device("cuda", torch.cuda.current_device())
 
 

@@ -31,11 +31,17 @@ def grad_buffer(layer, key: str, shape) -> torch.Tensor:
     reference's "backward overwrites self.grads[k]" semantics while the tensor object
     stays stable for the optimiser table and data-parallel gradient buckets."""
     g = layer.grads.get(key)
-    shape = tuple(int(s) for s in shape)
-    if not isinstance(g, torch.Tensor) or g.device.type != "cuda" or tuple(g.shape) != shape \
+    # fast path (every backward): the tensor this function handed out last time, same shape
+    cache = layer.__dict__.setdefault("_grad_buffer_cache", {})
+    hit = cache.get(key)
+    if hit is not None and hit[0] is g and hit[1] == shape:
+        return g
+    shape_t = tuple(int(s) for s in shape)
+    if not isinstance(g, torch.Tensor) or g.device.type != "cuda" or tuple(g.shape) != shape_t \
             or not g.is_contiguous():
-        g = torch.empty(shape, dtype=torch.float32, device=torch.device("cuda", torch.cuda.current_device()))
+        g = torch.empty(shape_t, dtype=torch.float32, device=torch.device("cuda", torch.cuda.current_device()))
         layer.grads[key] = g
+    cache[key] = (g, shape)
     return g
 
 
