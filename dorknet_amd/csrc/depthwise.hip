@@ -154,6 +154,24 @@ __global__ __launch_bounds__(256) void dw_fwd_kernel(const T* __restrict__ x, ui
 #pragma unroll
     for (int r = 0; r < R; ++r)
       load_row<NC, BN, T>(win[r], rs, n, oh0 * ST - pad + r, iw0, H, W, C, c, bn, bm, bi, bg, bb);
+    // bf16, stride 1: the next output row's new input row is loaded one row ahead, kept packed (2
+    // registers per 4 channels) and widened / normalised when it enters the window; fp32 and
+    // stride 2 load it in the row that uses it (their windows leave no registers for a prefetch)
+    constexpr bool PFR = sizeof(T) == 2 && ST == 1;
+    uint2 pre[PFR ? NC : 1];
+    auto load_pre = [&](int ih) {
+      if constexpr (PFR) {
+        const bool rv = (unsigned)ih < (unsigned)H;
+#pragma unroll
+        for (int q = 0; q < NC; ++q) {
+          const bool ok = rv && (unsigned)(iw0 + q) < (unsigned)W;
+          pre[q] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(
+                                                 rs, (int)(ok ? (uint32_t)(((n * H + ih) * W + iw0 + q) * C + c) * 2u
+                                                              : kOOBBytes), 0, 0));
+        }
+      }
+    };
+    if (oh0 + 1 < oh1) load_pre((oh0 + 1) * ST - pad + R - 1);
     for (int oh = oh0; oh < oh1; ++oh) {
       // this row's residual / BN-input operands (dgrad only), issued ahead of the window
       // loads and FMAs
@@ -173,6 +191,21 @@ __global__ __launch_bounds__(256) void dw_fwd_kernel(const T* __restrict__ x, ui
           if (r + ST < R) {
 #pragma unroll
             for (int q = 0; q < NC; ++q) win[r][q] = win[r + ST][q];
+          } else if constexpr (PFR) {
+            // the prefetched row: widened, BN applied on the in-image elements (as load_row)
+            const int ih = oh * ST - pad + r;
+            const bool rv = (unsigned)ih < (unsigned)H;
+#pragma unroll
+            for (int q = 0; q < NC; ++q) {
+              f32x4 v = bf16x4_to_f32(pre[q]);
+              if constexpr (BN) {
+                const bool ok = rv && (unsigned)(iw0 + q) < (unsigned)W;
+                const f32x4 t = bn_in4(v, bm, bi, bg, bb, bn.relu);
+                v = ok ? t : f32x4{0.f, 0.f, 0.f, 0.f};
+              }
+              win[r][q] = v;
+            }
+            if (oh + 1 < oh1) load_pre((oh + 1) * ST - pad + R - 1);
           } else {
             load_row<NC, BN, T>(win[r], rs, n, oh * ST - pad + r, iw0, H, W, C, c, bn, bm, bi, bg, bb);
           }
@@ -243,12 +276,20 @@ __global__ __launch_bounds__(256) void dw_fwd_kernel(const T* __restrict__ x, ui
 // dx store: dx = (dgrad + res) * mask (the join's stored ReLU mask), partials (sum dx,
 // sum dx * xhat_j) -- what dk_relu_bwd_bn_partial_f64 computes from the stored dx, bit for bit
 // for dx (activations.py:44-47, batch_norm.py:125-147).
+// bnmode (sub-pixel dgrad only): the layer's input is instead a BatchNorm (+ReLU) output applied on
+// load (a BNOut); dx is stored as computed (the gradient w.r.t. that BN's output) and the partials
+// are stage 1 of that BN's backward, its ReLU mask recomputed from its raw input x
+// (dk_bn_bwd_partial_f64, batch_norm.py:125-147) -- x is then of the kernel's storage type.
 struct JoinBwd {
   const uint8_t* mask;
-  const float* x;  // bn_j's raw input
+  const void* x;  // bn_j's raw input (fp32; bnmode: the BN's raw input, storage type)
   const float* mean;
   const float* invstd;
   int res_lat;  // sub-pixel dgrad: the residual given on the stride-ST lattice only (phase (0, 0)), compact
+  const float* gamma;  // bnmode: the BN's affine parameters and ReLU flag
+  const float* beta;
+  int relu;
+  int bnmode;
 };
 
 template <int R, int S, int ST, int PAD, class T = float, bool JOIN = false>
@@ -282,11 +323,15 @@ __global__ __launch_bounds__(256) void dw_dgrad_subpixel_kernel(const T* __restr
   // sums, then a fixed-order block reduction into part[blk][2][C] (a block spans whole pixels:
   // C/4 divides 256)
   double s1[4] = {0.0, 0.0, 0.0, 0.0}, s2[4] = {0.0, 0.0, 0.0, 0.0};
-  f32x4 jm{}, ji{};
+  f32x4 jm{}, ji{}, jg{}, jb{};
   if constexpr (JOIN) {
     if (live) {
       jm = ld4(jn.mean + c);
       ji = ld4(jn.invstd + c);
+      if (jn.bnmode) {
+        jg = ld4(jn.gamma + c);
+        jb = ld4(jn.beta + c);
+      }
     }
   }
   if (live) {
@@ -304,30 +349,50 @@ __global__ __launch_bounds__(256) void dw_dgrad_subpixel_kernel(const T* __restr
     }
     f32x4 wv[R][S];
     load_dw_weights<R, S, 1>(wv, wt, c, C);  // wt = W[C][R][S]
-#pragma unroll
-    for (int q = 0; q < TWQ; ++q) {
-      const int j = j0 + q;
-      f32x4 acc[ST][ST], rv[ST][ST], jx[ST][ST];
+    // a quad's store operands (residual addend; JOIN: the join mask / BN raw input), as buffer
+    // loads one quad ahead: no branch around a load (which made the waitcnt pass drain every
+    // memory operation per quad) and the next quad's loads in flight under this quad's FMAs
+    const size_t pixels = (size_t)N * H * W;
+    const __amdgpu_buffer_rsrc_t rres = make_rsrc_v(
+        res, res ? (uint32_t)((JOIN && jn.res_lat ? (size_t)N * QH * QW : pixels) * C * sizeof(T)) : 0u);
+    const __amdgpu_buffer_rsrc_t rjx = make_rsrc_v(JOIN ? jn.x : nullptr, JOIN ? (uint32_t)(pixels * C * sizeof(T)) : 0u);
+    const __amdgpu_buffer_rsrc_t rjm = make_rsrc_v(JOIN ? jn.mask : nullptr, (JOIN && jn.mask) ? (uint32_t)(pixels * C) : 0u);
+    struct QOps {
+      f32x4 rv[ST][ST], jx[ST][ST];
       uint32_t jmk[ST][ST];
+    };
+    auto load_q = [&](int q, QOps& o) {
+      const int j = j0 + q;
 #pragma unroll
       for (int a = 0; a < ST; ++a)
 #pragma unroll
         for (int b = 0; b < ST; ++b) {
-          // residual addend loads issued ahead of the FMAs (added last: same rounding as dgrad + add)
           const int h = qi * ST + a, w = j * ST + b;
           const bool ok = j < QW && h < H && w < W;
-          const size_t off = (((size_t)n * H + h) * W + w) * C + c;
+          const uint32_t off = (uint32_t)((((size_t)n * H + h) * W + w) * C + c);
           if (JOIN && jn.res_lat)  // compact lattice residual: phase (0, 0) only, at quad (qi, j)
-            rv[a][b] = (res && ok && a == 0 && b == 0) ? ld4(res + (((size_t)n * QH + qi) * QW + j) * C + c)
-                                                      : f32x4{0.f, 0.f, 0.f, 0.f};
+            o.rv[a][b] = bload4e<T>(rres, ok && a == 0 && b == 0, (uint32_t)((((size_t)n * QH + qi) * QW + j) * C + c));
           else
-            rv[a][b] = (res && ok) ? ld4(res + off) : f32x4{0.f, 0.f, 0.f, 0.f};
+            o.rv[a][b] = bload4e<T>(rres, ok, off);
           if constexpr (JOIN) {
-            jmk[a][b] = ok ? *reinterpret_cast<const uint32_t*>(jn.mask + off) : 0u;
-            jx[a][b] = ok ? ld4(jn.x + off) : f32x4{0.f, 0.f, 0.f, 0.f};
+            o.jmk[a][b] = __builtin_amdgcn_raw_buffer_load_b32(rjm, (int)(ok ? off : kOOBBytes), 0, 0);
+            o.jx[a][b] = bload4e<T>(rjx, ok, off);
           }
-          acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
         }
+    };
+    const __amdgpu_buffer_rsrc_t rdx = make_rsrc_v(dx, (uint32_t)(pixels * C * sizeof(T)));
+    QOps qo[2];
+    load_q(0, qo[0]);
+#pragma unroll
+    for (int q = 0; q < TWQ; ++q) {
+      const int j = j0 + q;
+      if (q + 1 < TWQ) load_q(q + 1, qo[(q + 1) & 1]);
+      f32x4 acc[ST][ST];
+      const QOps& cur = qo[q & 1];
+#pragma unroll
+      for (int a = 0; a < ST; ++a)
+#pragma unroll
+        for (int b = 0; b < ST; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int r = 0; r < R; ++r)
 #pragma unroll
@@ -339,20 +404,34 @@ __global__ __launch_bounds__(256) void dw_dgrad_subpixel_kernel(const T* __restr
 #pragma unroll
         for (int b = 0; b < ST; ++b) {
           const int w = j * ST + b;
-          if (j < QW && h < H && w < W) {
-            const size_t off = (((size_t)n * H + h) * W + w) * C + c;
-            f32x4 o = res ? acc[a][b] + rv[a][b] : acc[a][b];
-            if constexpr (JOIN) {
+          // unconditional: a pixel outside dx is dropped by the buffer store and adds 0 to the sums
+          const bool ok = j < QW && h < H && w < W;
+          const uint32_t off = (uint32_t)((((size_t)n * H + h) * W + w) * C + c);
+          f32x4 o = res ? acc[a][b] + cur.rv[a][b] : acc[a][b];
+          if constexpr (JOIN) {
+            if (jn.bnmode) {
+              o = rnd4<T>(o);  // the partials see dx as stored
 #pragma unroll
               for (int e = 0; e < 4; ++e) {
-                if (!((jmk[a][b] >> (8 * e)) & 0xffu)) o[e] = 0.f;  // dy * mask (activations.py:46)
-                const float xn = (jx[a][b][e] - jm[e]) * ji[e];
-                s1[e] += (double)o[e];
-                s2[e] += (double)o[e] * (double)xn;
+                const float xv = cur.jx[a][b][e];
+                const float xn = (xv - jm[e]) * ji[e];
+                const bool kill = !ok || (jn.relu && !(bn_out(xv, jm[e], ji[e], jg[e], jb[e]) > 0.f));
+                const float g = kill ? 0.f : o[e];
+                s1[e] += (double)g;
+                s2[e] += (double)g * (double)xn;
+              }
+            } else {
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                if (!((cur.jmk[a][b] >> (8 * e)) & 0xffu)) o[e] = 0.f;  // dy * mask (activations.py:46)
+                const float xn = (cur.jx[a][b][e] - jm[e]) * ji[e];
+                const float g = ok ? o[e] : 0.f;
+                s1[e] += (double)g;
+                s2[e] += (double)g * (double)xn;
               }
             }
-            st4(dx + off, o);
           }
+          bstore4e<T>(rdx, ok, off, o);
         }
       }
     }
@@ -1027,7 +1106,14 @@ static int dw_dgrad(const T* dy, int N, int OH, int OW, int C, const float* w_cr
     return dw_fwd_dispatch(dy, w_crs, nullptr, dx, N, OH, OW, C, R, S, 1, H, W, R - 1 - pad, BnIn{}, st,
                            part ? part : nullptr, part ? bn_x : nullptr, part ? obn : BnIn{}, 2, res);
   }
-  if (part && !jn) return DK_ERR_ARGS;  // the BN-backward fusion covers stride-1 geometries only
+  JoinBwd bnj{};
+  if (part && !jn) {
+    // the input BatchNorm's stage-1 partials on the sub-pixel store (JoinBwd::bnmode)
+    if (!bn_x || !obn.mean || !obn.invstd || !obn.gamma || !obn.beta || (C / 4) > 256 || 256 % (C / 4))
+      return DK_ERR_ARGS;
+    bnj = JoinBwd{nullptr, bn_x, obn.mean, obn.invstd, 0, obn.gamma, obn.beta, obn.relu, 1};
+    jn = &bnj;
+  }
   if (!fits((size_t)N * OH * OW * C * 4) || !aligned16(dy) || !aligned16(dx) || !aligned16(w_crs) ||
       (res && !aligned16(res)))
     return DK_ERR_ARGS;
@@ -1037,15 +1123,12 @@ static int dw_dgrad(const T* dy, int N, int OH, int OW, int C, const float* w_cr
     const long long items = (long long)N * cdiv(H, STR) * cdiv(cdiv(W, STR), 4) * (C / 4);                         \
     const dim3 grid((unsigned)cdivll(items, 256));                                                                   \
     if (jn) {                                                                                                        \
-      if constexpr (sizeof(T) == sizeof(float)) {                                                                    \
-        FoldTail ft;                                                                                                 \
-        if (!fold_take(part, (int)grid.x, C, 1, &ft)) ft.part = nullptr;                                            \
-        hipLaunchKernelGGL((dw_dgrad_subpixel_kernel<RR, SS, STR, PD, T, true>), grid, dim3(256), 0, st, dy, gb,    \
-                           w_crs, dx, N, H, W, C, OH, OW, res, *jn, part, ft);                                       \
-        return fold_status(launch_status(), ft);                                                                     \
-      } else {                                                                                                       \
-        return DK_ERR_ARGS;                                                                                          \
-      }                                                                                                              \
+      if (sizeof(T) != sizeof(float) && !jn->bnmode) return DK_ERR_ARGS; /* the join fusion: fp32 only */            \
+      FoldTail ft;                                                                                                   \
+      if (!fold_take(part, (int)grid.x, C, 1, &ft)) ft.part = nullptr;                                              \
+      hipLaunchKernelGGL((dw_dgrad_subpixel_kernel<RR, SS, STR, PD, T, true>), grid, dim3(256), 0, st, dy, gb,      \
+                         w_crs, dx, N, H, W, C, OH, OW, res, *jn, part, ft);                                         \
+      return fold_status(launch_status(), ft);                                                                       \
     }                                                                                                                \
     hipLaunchKernelGGL((dw_dgrad_subpixel_kernel<RR, SS, STR, PD, T>), grid, dim3(256), 0, st, dy, gb, w_crs, dx, N, \
                        H, W, C, OH, OW, res, JoinBwd{}, nullptr, FoldTail{});                                        \

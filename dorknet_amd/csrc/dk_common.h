@@ -89,6 +89,20 @@ __device__ __forceinline__ f32x4 bload4e(__amdgpu_buffer_rsrc_t r, bool ok, uint
   }
 }
 
+// 4 consecutive elements stored at element index e (ok == false: dropped), RNE for bf16
+template <class T>
+__device__ __forceinline__ void bstore4e(__amdgpu_buffer_rsrc_t r, bool ok, uint32_t e, f32x4 v) {
+  if constexpr (sizeof(T) == 2) {
+    const uint32_t off = ok ? e * 2u : kOOBBytes;
+    typedef uint32_t u32x2_ __attribute__((ext_vector_type(2)));
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_, f32_to_bf16x4(v)), r, (int)off, 0, 0);
+  } else {
+    typedef uint32_t u32x4_ __attribute__((ext_vector_type(4)));
+    const uint32_t off = ok ? e * 4u : kOOBBytes;
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_, v), r, (int)off, 0, 0);
+  }
+}
+
 // Wave-level (64 lanes) sum.
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

@@ -268,7 +268,14 @@ class DepthwiseConvLayer(Layer):
         res = lat if lat is not None else residual_operand(residual, dx)
         if residual is not None and res is None:
             jrows = 0
-        rows = lib.dk_dwconv_dgrad_stats_rows(N, H, W, C, self.stride) if bn is not None and R == S else 0
+        # the input BatchNorm's stage-1 partials ride on the dgrad store: stride 1 in the dgrad's
+        # epilogue, stride > 1 on the sub-pixel dgrad's store (same row count as its join form)
+        rows = 0
+        if bn is not None and R == S:
+            if self.stride == 1:
+                rows = lib.dk_dwconv_dgrad_stats_rows(N, H, W, C, 1)
+            elif os.environ.get("DORKNET_DW_STRIDED_BN", "1") != "0":  # (0: the BN runs its own backward)
+                rows = lib.dk_dwconv_dgrad_join_rows(N, H, W, C, R, S, self.stride, self.padding)
         if rows and self.padding <= R - 1 and (residual is None or res is not None):
             # + stage 1 of the input BatchNorm's backward, in the dgrad epilogue (+ the residual)
             part = torch.empty((rows, 2, C), dtype=torch.float64, device=dx.device)

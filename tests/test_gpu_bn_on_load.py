@@ -288,6 +288,61 @@ def test_depthwise_dgrad_bn_partials():
     _close(_bwd_finalize(part, rows, C, N * H * W), _bwd_reference(xbn, dx0, p, 1))
 
 
+@pytest.mark.parametrize("relu,C,H,W,R,pad", [(1, 32, 11, 13, 3, 1), (0, 64, 14, 14, 3, 1), (1, 16, 9, 10, 5, 2),
+                                               (1, 128, 7, 7, 1, 0)])
+def test_depthwise_strided_dgrad_bn_partials(relu, C, H, W, R, pad):
+    """Stride 2 (the sub-pixel dgrad): dx bit-identical to the plain strided dgrad, and the input
+    BatchNorm's stage-1 sums of its store (ReLU mask recomputed from the BN's raw input) equal
+    the standalone reduction over (bn_x, dx)."""
+    rng = np.random.RandomState(33 + C + R)
+    N, st_ = 3, 2
+    OH, OW = (H + 2 * pad - R) // st_ + 1, (W + 2 * pad - R) // st_ + 1
+    dy = nhwc(rng.randn(N, C, OH, OW))
+    w = torch.as_tensor(rng.randn(C, R, R).astype(np.float32), device="cuda")
+    xbn = nhwc(rng.randn(N, C, H, W))
+    p = bn_params(C, rng)
+    st = stream_handle()
+    nb = lib.dk_dwconv_dgrad_workspace_bytes(C, R, R)
+    dx0 = torch.empty_like(xbn)
+    dx1 = torch.full_like(xbn, float("nan"))
+    lib.dk_dwconv_dgrad_f32(dy.data_ptr(), N, OH, OW, C, w.data_ptr(), R, R, st_, pad, dx0.data_ptr(), H, W,
+                            workspace.get(nb), nb, st)
+    rows = lib.dk_dwconv_dgrad_join_rows(N, H, W, C, R, R, st_, pad)
+    assert rows > 0
+    part = torch.empty((rows, 2, C), dtype=torch.float64, device="cuda")
+    lib.dk_dwconv_dgrad_ex_f32(dy.data_ptr(), N, OH, OW, C, w.data_ptr(), R, R, st_, pad, dx1.data_ptr(), H, W,
+                               workspace.get(nb), nb, 0, xbn.data_ptr(), *args(p, relu), part.data_ptr(), st)
+    same(dx0, dx1)
+    _close(_bwd_finalize(part, rows, C, N * H * W), _bwd_reference(xbn, dx0, p, relu))
+
+
+def test_depthwise_strided_dgrad_bn_partials_bf16():
+    """The same for bf16 storage: dx equal to the plain bf16 strided dgrad, the partials over the
+    stored (rounded) dx against the standalone reduction on the widened tensors."""
+    rng = np.random.RandomState(77)
+    N, C, H, W, R, pad, st_ = 4, 64, 14, 14, 3, 1, 2
+    OH, OW = 7, 7
+    bf = torch.bfloat16
+    dy = nhwc(rng.randn(N, C, OH, OW)).to(bf).contiguous(memory_format=torch.channels_last)
+    w = torch.as_tensor(rng.randn(C, R, R).astype(np.float32), device="cuda")
+    xbn = nhwc(rng.randn(N, C, H, W)).to(bf).contiguous(memory_format=torch.channels_last)
+    p = bn_params(C, rng)
+    st = stream_handle()
+    nb = lib.dk_dwconv_dgrad_workspace_bytes(C, R, R)
+    dx0 = torch.empty_like(xbn)
+    dx1 = torch.full_like(xbn, float("nan"))
+    lib.dk_dwconv_dgrad_ex_bf16(dy.data_ptr(), N, OH, OW, C, w.data_ptr(), R, R, st_, pad, dx0.data_ptr(), H, W,
+                                workspace.get(nb), nb, 0, 0, 0, 0, 0, 0, 0, 0, st)
+    rows = lib.dk_dwconv_dgrad_join_rows(N, H, W, C, R, R, st_, pad)
+    part = torch.empty((rows, 2, C), dtype=torch.float64, device="cuda")
+    lib.dk_dwconv_dgrad_ex_bf16(dy.data_ptr(), N, OH, OW, C, w.data_ptr(), R, R, st_, pad, dx1.data_ptr(), H, W,
+                                workspace.get(nb), nb, 0, xbn.data_ptr(), *args(p, 1), part.data_ptr(), st)
+    same(dx0, dx1)
+    _close(_bwd_finalize(part, rows, C, N * H * W),
+           _bwd_reference(xbn.float().contiguous(memory_format=torch.channels_last),
+                          dx0.float().contiguous(memory_format=torch.channels_last), p, 1))
+
+
 def test_relu_bwd_bn_partials():
     rng = np.random.RandomState(41)
     N, C, H, W = 2, 48, 9, 10
