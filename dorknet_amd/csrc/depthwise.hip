@@ -87,8 +87,15 @@ __device__ __forceinline__ void load_row(f32x4 (&row)[NC], __amdgpu_buffer_rsrc_
 template <int ST>
 struct DwTile {
   static constexpr int TW = 4;    // outputs per thread along W
-  static constexpr int SEG = 8;   // output rows per thread (the input window slides down)
 };
+
+// Output rows per thread (the input window slides down a segment of them).  8 measured best or
+// within noise of best on every training shape of configs 3 and 5 (scripts/dw_fwd_seg.py,
+// profiles/r03q_dw_seg_{f32,bf16}.txt: fewer rows per thread re-load the window more often and the
+// extra blocks do not pay for it).
+static int g_dw_seg = -1;  // tuning knob dk_debug_set_gemm_config(8, rows); -1 = the default
+void dw_seg_set(int v) { g_dw_seg = v; }
+static inline int dw_fwd_seg() { return g_dw_seg > 0 ? g_dw_seg : 8; }
 
 // y[n,oh,ow,c] = sum_{r,s} w[r][s][c] * x[n, oh*ST + r - pad, ow*ST + s - pad, c] (+ bias[c])
 // Thread = (n, oh, TW-wide chunk of ow, 4 channels); consecutive threads take consecutive
@@ -109,8 +116,8 @@ __global__ __launch_bounds__(256) void dw_fwd_kernel(const T* __restrict__ x, ui
                                                      T* __restrict__ y, int N, int H, int W, int C, int OH, int OW,
                                                      int pad, BnIn bn, double* __restrict__ part,
                                                      const T* __restrict__ xo, BnIn obn,
-                                                     const T* __restrict__ res, FoldTail ft, int nt) {
-  constexpr int TW = DwTile<ST>::TW, SEG = DwTile<ST>::SEG;
+                                                     const T* __restrict__ res, FoldTail ft, int nt, int SEG) {
+  constexpr int TW = DwTile<ST>::TW;
   constexpr int NC = (TW - 1) * ST + S;
   const int C4 = C >> 2;
   const int nwc = (OW + TW - 1) / TW;
@@ -976,7 +983,8 @@ static inline bool bn_ok(const BnIn& bn) {
 
 template <int ST>
 static long long dw_fwd_threads(int N, int OH, int OW, int C) {
-  constexpr int TW = DwTile<ST>::TW, SEG = DwTile<ST>::SEG;
+  constexpr int TW = DwTile<ST>::TW;
+  const int SEG = dw_fwd_seg();
   return (long long)N * ((OH + SEG - 1) / SEG) * ((OW + TW - 1) / TW) * (C / 4);
 }
 
@@ -992,7 +1000,7 @@ static int launch_dw_fwd(const T* x, const float* wt, const float* bias, T* y, i
   if (!part || !fold_take(part, (int)grid.x, C, 1, &ft)) ft.part = nullptr;
 #define DW_LAUNCH(B, ST_, WL_)                                                                                        \
   hipLaunchKernelGGL((dw_fwd_kernel<R, S, ST, B, ST_, WL_, T>), grid, dim3(256), 0, st, x, xb, wt, bias, y, N, H, W, \
-                     C, OH, OW, pad, bn, part, xo, obn, res, ft, nt_stores())
+                     C, OH, OW, pad, bn, part, xo, obn, res, ft, nt_stores(), dw_fwd_seg())
   const int mode = part ? (xo ? 2 : 1) : 0;
   if (wl == 0 && !bn.mean && mode == 0)
     DW_LAUNCH(false, 0, 0);

@@ -198,6 +198,7 @@ int splitk_reduce(const float* ws, int splits, int M, int N, float* out, const f
 
 // Blocks the fused stride-1 depthwise backward aims for (depthwise.hip; knob kind 7, -1 = default).
 void dwb_blocks_set(int v);
+void dw_seg_set(int v);
 
 // Streaming pointwise kernels (pw_stream.hip) for the K = C = 64 shapes.
 bool pw_stream_enabled();  // DORKNET_PW_STREAM (default 1; 0 = the tiled engine everywhere, for A/B runs)

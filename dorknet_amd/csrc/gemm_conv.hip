@@ -84,6 +84,10 @@ DK_API int dk_debug_set_gemm_config(int kind, int cfg) {
     dwb_blocks_set(cfg < 0 ? 768 : cfg);
     return 0;
   }
+  if (kind == 8) {  // output rows per thread of the depthwise forward (depthwise.hip dw_fwd_seg; -1 = rule)
+    dw_seg_set(cfg);
+    return 0;
+  }
   if (kind == 9) {  // the bf16 streaming pointwise kernels (pw_stream_bf16.hip) on / off
     pw_stream_bf16_set(cfg);
     return 0;

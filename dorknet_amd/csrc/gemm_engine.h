@@ -1176,7 +1176,7 @@ static inline int row_config(int M, int N, int K, int kind = kRowPlain, int mf =
   if (g_cfg_override[0] >= 0) return g_cfg_override[0];
   (void)M;
   if (mf == kMfBf16) {
-    // bf16 MFMA (config 5's 14 x 14 and 7 x 7 units at batch 512; scripts/bf16_gemm_tune.py,
+    // bf16 MFMA (config 5's 14 x 14 and 7 x 7 units at batch 512; scripts/gemm_tune_deep.py --bf16,
     // profiles/r03k_bf16_gemm_tune.txt): the tiles with 8 waves or 128 columns, whose blocks run
     // more MFMAs per dependent load round trip
     if (kind == kRowBnBwd) return N <= 128 ? 16 : (N <= 256 ? (K >= 512 ? 13 : 16) : 13);
@@ -1187,7 +1187,8 @@ static inline int row_config(int M, int N, int K, int kind = kRowPlain, int mf =
     // Measured on MI355X (scripts/gemm_tune.py --fused-only, profiles/r01h_gemm_tune_fused.txt)
     if (N <= 64) return 8;                // 64x64x32
     if (N <= 128) return 16;              // 128x128x32, 2x4 waves
-    if (N <= 256) return K >= 512 ? 13 : 6;
+    // C = K = 256 at 14 x 14, batch 256: 98 vs 107 us (scripts/gemm_tune_deep.py, profiles/r03q_f32_tune.txt)
+    if (N <= 256) return K >= 512 ? 13 : 16;
     return 9;                             // 256x128x16
   }
   // The stem (K = 5*5*4 = 100, 64 filters): 128x64x16 with 2x2 waves, 555 vs 687 us

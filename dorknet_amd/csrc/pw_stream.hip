@@ -601,13 +601,15 @@ __global__ __launch_bounds__(256, PF ? 1 : 2) void bwd_fused_kernel(BwdArgs ba) 
 #pragma unroll
       for (int r = 0; r < 16; ++r) aw[i][u][r] = 0.f;
 
+  // the tile's g and x rows as whole 1 KB wave loads: load q gives lane (pr, cq) = (lane / 16, lane % 16)
+  // pixel pr + 4q, channels 4cq .. 4cq + 3 (the MFMA operand layout comes back from the LDS dy image)
+  const int pr = lane >> 4, cq = lane & 15;
   auto load_a = [&](int tile, f32x4* lg, f32x4* lx) {
-    const int m = tile * TR + l32;
-    const uint32_t base = row_off_bytes(m, KR, 4 * h);
+    const uint32_t base = row_off_bytes(tile * TR, KR, 0) + 16u * lane;
 #pragma unroll
     for (int q = 0; q < KQ; ++q) {
-      lg[q] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rg, (int)(base + 32u * q), 0, 0));
-      lx[q] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rx, (int)(base + 32u * q), 0, 0));
+      lg[q] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rg, (int)(base + 1024u * q), 0, 0));
+      lx[q] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rx, (int)(base + 1024u * q), 0, 0));
     }
   };
   f32x4 cg[KQ], cx[KQ];
@@ -641,27 +643,30 @@ __global__ __launch_bounds__(256, PF ? 1 : 2) void bwd_fused_kernel(BwdArgs ba) 
     if constexpr (PF) load_a(t + W, ng, nx);
     __builtin_amdgcn_sched_barrier(0);
 
-    // (2) dy (bit-identical to dk_bn_bwd_apply_f32) into registers and the wave's LDS image
-    f32x4 afs[PF ? KQ : 1];
-    f32x4* const af = PF ? afs : cg;  // (in place without the prefetch: cg is dead after the transform)
-#pragma unroll
-    for (int q = 0; q < KQ; ++q) {
-      const int k0 = 8 * q + 4 * h;
+    // (2) dy (bit-identical to dk_bn_bwd_apply_f32) into the wave's LDS image, whose rows give back
+    //     the MFMA operand layout (lane (l32, h): pixel l32, channels 8q + 4h ..)
+    {
+      const int k0 = 4 * cq;  // this lane's channels, the same for every q
       const f32x4 mu = ld4(tb + 0 * KR + k0), is = ld4(tb + 1 * KR + k0), ga = ld4(tb + 2 * KR + k0),
                   be = ld4(tb + 3 * KR + k0);
       const f32x4 k1 = ld4(tb + 4 * KR + k0), k2 = ld4(tb + 5 * KR + k0), f = ld4(tb + 6 * KR + k0);
-      f32x4 o;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float xe = cx[q][e];
-        float ge = cg[q][e];
-        const bool kill = (!(bn_out(xe, mu[e], is[e], ga[e], be[e]) > 0.f)) & orelu;
-        ge = kill ? 0.f : ge;
-        o[e] = bn_bwd_elem(xe, ge, mu[e], is[e], f[e], k1[e], k2[e]);
+      for (int q = 0; q < KQ; ++q) {
+        f32x4 o;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float xe = cx[q][e];
+          float ge = cg[q][e];
+          const bool kill = (!(bn_out(xe, mu[e], is[e], ga[e], be[e]) > 0.f)) & orelu;
+          ge = kill ? 0.f : ge;
+          o[e] = bn_bwd_elem(xe, ge, mu[e], is[e], f[e], k1[e], k2[e]);
+        }
+        st4(td + (pr + 4 * q) * SKD + k0, o);
       }
-      af[q] = o;
-      st4(td + l32 * SKD + k0, o);
     }
+    f32x4 af[KQ];
+#pragma unroll
+    for (int q = 0; q < KQ; ++q) af[q] = ld4(td + l32 * SKD + 8 * q + 4 * h);
 
     // (3) dgrad: dx tile = dy . W (no scheduling barrier around (2)-(4): the transform of
     //     q + 1, the wgrad operand work and the epilogue VALU fill the MFMA issue gaps of the

@@ -1,8 +1,9 @@
-"""Tile configurations for config 5's bf16 pointwise GEMMs that stay on the tiled engine (the
-14 x 14 and 7 x 7 units, K or C >= 256, batch 512): every row configuration (knob 0) for the
-forward with BN on load + statistics and for the BN-backward-on-load dgrad, every split-K
-configuration (knob 1) for the weight gradient; median of 7 timed calls each.
-    python scripts/bf16_gemm_tune.py
+"""Tile configurations for the pointwise GEMMs that stay on the tiled engine (the 14 x 14 and 7 x 7
+layers, K or C >= 256): every row configuration (knob 0) for the forward with BN on load +
+statistics and for the BN-backward-on-load dgrad, every split-K configuration (knob 1) for the
+weight gradient; median of 7 timed calls each.  fp32 at batch 256 (config 3) or, with --bf16,
+bf16 at batch 512 (config 5).
+    python scripts/gemm_tune_deep.py [--bf16]
 """
 import os
 import sys
@@ -14,7 +15,11 @@ import torch  # noqa: E402
 from dorknet_amd._hip import lib, workspace  # noqa: E402
 
 BF16 = torch.bfloat16
-SHAPES = [(512, 14, 256, 256), (512, 14, 128, 256), (512, 7, 512, 512), (512, 7, 256, 512)]  # N, HW, C, K
+HALF = "--bf16" in sys.argv
+B = 512 if HALF else 256
+SHAPES = [(B, 14, 256, 256), (B, 14, 128, 256), (B, 7, 512, 512), (B, 7, 256, 512)]  # N, HW, C, K
+DT = BF16 if HALF else torch.float32
+SUF = "bf16" if HALF else "f32"
 
 
 def timeit(fn, reps=7):
@@ -41,9 +46,9 @@ def main():
     nsplit = lib.dk_debug_set_gemm_config(1, -1)
     for N, HW, C, K in SHAPES:
         M = N * HW * HW
-        x, y = rnd(M * C, dt=BF16), torch.empty(M * K, dtype=BF16, device="cuda")
-        gy, xo = rnd(M * K, dt=BF16), rnd(M * K, dt=BF16)
-        dy, dx = torch.empty(M * K, dtype=BF16, device="cuda"), torch.empty(M * C, dtype=BF16, device="cuda")
+        x, y = rnd(M * C, dt=DT), torch.empty(M * K, dtype=DT, device="cuda")
+        gy, xo = rnd(M * K, dt=DT), rnd(M * K, dt=DT)
+        dy, dx = torch.empty(M * K, dtype=DT, device="cuda"), torch.empty(M * C, dtype=DT, device="cuda")
         w = rnd(K * C) * 0.05
         pi = [rnd(C), rnd(C).abs() + 0.5, rnd(C), rnd(C)]
         po = [rnd(K), rnd(K).abs() + 0.5, rnd(K), rnd(K)]
@@ -52,17 +57,17 @@ def main():
         res = {}
         for cfg in list(range(nrow)) + [-1]:
             lib.dk_debug_set_gemm_config(0, cfg)
-            rows = lib.dk_pwconv_fwd_bf16_stats_rows(N, HW, HW, K, C)
+            rows = (lib.dk_pwconv_fwd_bf16_stats_rows if HALF else lib.dk_pwconv_fwd_stats_rows)(N, HW, HW, K, C)
             part = torch.empty(rows * 2 * K, dtype=torch.float64, device="cuda")
             fa = (x.data_ptr(), N, HW, HW, C, w.data_ptr(), K, 1, 0, y.data_ptr(), HW, HW,
                   *(t.data_ptr() for t in pi), 1, part.data_ptr(), st)
-            tf = timeit(lambda: lib.dk_pwconv_fwd_ex_bf16(*fa))
-            rows = lib.dk_pwconv_dgrad_bnbwd_bf16_stats_rows(N, HW, HW, K, C)
+            tf = timeit(lambda: getattr(lib, "dk_pwconv_fwd_ex_" + SUF)(*fa))
+            rows = (lib.dk_pwconv_dgrad_bnbwd_bf16_stats_rows if HALF else lib.dk_pwconv_dgrad_bnbwd_stats_rows)(N, HW, HW, K, C)
             partd = torch.empty(rows * 2 * C, dtype=torch.float64, device="cuda")
             da = (gy.data_ptr(), xo.data_ptr(), N, HW, HW, K, *(t.data_ptr() for t in po), 1, k12.data_ptr(),
                   dy.data_ptr(), w.data_ptr(), C, dx.data_ptr(), 0, x.data_ptr(), *(t.data_ptr() for t in pi), 1,
                   partd.data_ptr(), st)
-            td = timeit(lambda: lib.dk_pwconv_dgrad_bnbwd_bf16(*da))
+            td = timeit(lambda: getattr(lib, "dk_pwconv_dgrad_bnbwd_" + SUF)(*da))
             res[cfg] = (tf, td)
             print(f"{N}x{HW}x{HW} C={C} K={K} row cfg {cfg:3d}: fwd {tf:7.1f} us  dgrad_bnbwd {td:7.1f} us", flush=True)
         lib.dk_debug_set_gemm_config(0, -1)
@@ -71,7 +76,7 @@ def main():
             nb = lib.dk_pwconv_wgrad_workspace_bytes(N, HW, HW, K, C)
             wa = (dy.data_ptr(), x.data_ptr(), N, HW, HW, C, K, 1, HW, HW, 0, 0.0, dw.data_ptr(), workspace.get(nb), nb,
                   *(t.data_ptr() for t in pi), 1, st)
-            tw = timeit(lambda: lib.dk_pwconv_wgrad_bnx_bf16(*wa))
+            tw = timeit(lambda: getattr(lib, "dk_pwconv_wgrad_bnx_" + SUF)(*wa))
             print(f"{N}x{HW}x{HW} C={C} K={K} split cfg {cfg:3d}: wgrad {tw:7.1f} us", flush=True)
         lib.dk_debug_set_gemm_config(1, -1)
         del x, y, gy, xo, dy, dx
