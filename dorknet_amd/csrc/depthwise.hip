@@ -1000,7 +1000,7 @@ static int launch_dw_fwd(const T* x, const float* wt, const float* bias, T* y, i
   if (!part || !fold_take(part, (int)grid.x, C, 1, &ft)) ft.part = nullptr;
 #define DW_LAUNCH(B, ST_, WL_)                                                                                        \
   hipLaunchKernelGGL((dw_fwd_kernel<R, S, ST, B, ST_, WL_, T>), grid, dim3(256), 0, st, x, xb, wt, bias, y, N, H, W, \
-                     C, OH, OW, pad, bn, part, xo, obn, res, ft, nt_stores(), dw_fwd_seg())
+                     C, OH, OW, pad, bn, part, xo, obn, res, ft, nt_stores(kNtDwFwd), dw_fwd_seg())
   const int mode = part ? (xo ? 2 : 1) : 0;
   if (wl == 0 && !bn.mean && mode == 0)
     DW_LAUNCH(false, 0, 0);
@@ -1300,7 +1300,7 @@ static int dw_bwd_fused(const T* g, const T* bn_x, int N, int H, int W, int C, c
       (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,       \
                                 (int)shm);                                                                           \
     hipLaunchKernelGGL(k, grid, dim3(256), shm, st, g, bn_x, (uint32_t)bytes, ob, x, bn, w_crs, dx, residual, part,  \
-                       wpart, N, H, W, C, cl, ft, JoinBwd{}, nt_stores(), nranges);                                                        \
+                       wpart, N, H, W, C, cl, ft, JoinBwd{}, nt_stores(kNtDwBwd), nranges);                                                        \
   }
   if (out_relu) {
     if (part) DWB_LAUNCH(true, true, true) else if (bn_mean) DWB_LAUNCH(true, false, true)
@@ -1418,7 +1418,7 @@ DK_API int dk_dwconv_bwd_bnbwd_join_f32(const float* g, const float* bn_x, int N
       (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,       \
                                 (int)shm);                                                                           \
     hipLaunchKernelGGL(k, grid, dim3(256), shm, st, g, bn_x, (uint32_t)bytes, ob, x, BnIn{}, w_crs, dx, residual,    \
-                       part, wpart, N, H, W, C, cl, ft, jn, nt_stores(), nranges);                                                         \
+                       part, wpart, N, H, W, C, cl, ft, jn, nt_stores(kNtDwBwd), nranges);                                                         \
   }
   if (out_relu)
     DWJ_LAUNCH(true)

@@ -499,7 +499,7 @@ DK_API int dk_bn_add_f32(const float* a, const float* a_mean, const float* a_inv
   if (C < 4 || C % 4 || n % C || n >= (1ll << 31) || !al16(a) || !al16(b) || !al16(y) || !al4(mask) || !params_ok(ba) || !params_ok(bb))
     return DK_ERR_ARGS;
   hipLaunchKernelGGL(bn_add_kernel, grid4(n), dim3(256), 0, as_stream(stream), a, ba, b, bb, n, C, relu, y, mask,
-                     nt_stores());
+                     nt_stores(kNtBnAdd));
   return launch_status();
 }
 

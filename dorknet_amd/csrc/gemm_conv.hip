@@ -8,12 +8,12 @@ namespace dk {
 int g_cfg_override[2] = {-1, -1};
 int g_fill_splits = 1;
 static int g_nt_stores = -1;
-int nt_stores() {
+int nt_stores(int fam) {
   if (g_nt_stores < 0) {
-    const char* e = getenv("DORKNET_NT_STORES");
-    g_nt_stores = (e && e[0] == '1') ? 1 : 0;
+    const char* e = getenv("DORKNET_NT_STORES");  // a bitmask of NtFam families
+    g_nt_stores = e ? atoi(e) : kNtDefault;
   }
-  return g_nt_stores;
+  return (g_nt_stores >> fam) & 1;
 }
 
 // Weight re-layouts (tiny; run once per call on the caller's stream).
@@ -93,7 +93,7 @@ DK_API int dk_debug_set_gemm_config(int kind, int cfg) {
     return 0;
   }
   if (kind == 4) {  // nontemporal output stores (kernels that support them)
-    g_nt_stores = cfg < 0 ? 0 : cfg;
+    g_nt_stores = cfg < 0 ? kNtDefault : cfg;
     return 0;
   }
   if (kind < 0 || kind > 1) return -1;

@@ -1102,7 +1102,7 @@ constexpr int kNumCUs = 256;  // MI355X
 // Epilogues with an `nt` member take the nontemporal-store knob (nt_stores()).
 template <class E>
 static inline auto set_nt(E& e, int) -> decltype(e.nt = 0, void()) {
-  e.nt = nt_stores();
+  e.nt = nt_stores(kNtGemm);
 }
 template <class E>
 static inline void set_nt(E&, long) {}

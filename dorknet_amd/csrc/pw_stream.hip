@@ -312,6 +312,13 @@ __global__ __launch_bounds__(256, KR_ == 64 ? 3 : 2) void fwd_kernel(FwdArgs a) 
   // K = C = 128 a separate buffer would push the block past 80 KB: one block per CU)
   double(*const red)[2][NO] = reinterpret_cast<double(*)[2][NO]>(Bs);
   static_assert(sizeof(double) * WAVES * 2 * NO <= sizeof(float) * NO * SKB, "red fits in Bs");
+  // CO (K = 64, stride 1): the A rows arrive as whole 1 KB wave loads (lane (pr, cq) = (lane / 16,
+  // lane % 16) holds pixel pr + 4q, channels 4cq ..) instead of 32-byte pieces of 32 rows, and the
+  // transformed tile goes through a per-wave LDS image into the MFMA operand layout (as the fused
+  // backward's dy image); 52 KB per block, still 3 blocks per CU
+  constexpr bool CO = KR == 64 && !STRIDED;
+  constexpr int SKA = KR + 4;
+  __shared__ __attribute__((aligned(16))) float Ta[CO ? WAVES * TR * SKA : 4];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int l32 = lane & 31, h = lane >> 5;
@@ -342,7 +349,16 @@ __global__ __launch_bounds__(256, KR_ == 64 ? 3 : 2) void fwd_kernel(FwdArgs a) 
 #pragma unroll
   for (int u = 0; u < NU; ++u) ps[u] = pq[u] = 0.0;
 
+  const int pr = lane >> 4, cq = lane & 15;
+  float* const ta = Ta + (CO ? wave * TR * SKA : 0);
   auto load_a = [&](int tile, f32x4* lx) {
+    if constexpr (CO) {
+      const uint32_t base = row_off_bytes(tile * TR, KR, 0) + 16u * lane;
+#pragma unroll
+      for (int q = 0; q < KQ; ++q)
+        lx[q] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rx, (int)(base + 1024u * q), 0, 0));
+      return;
+    }
     const int m = tile * TR + l32;
     int row = m;
     if constexpr (STRIDED) {
@@ -372,8 +388,31 @@ __global__ __launch_bounds__(256, KR_ == 64 ? 3 : 2) void fwd_kernel(FwdArgs a) 
 
     f32x4 afs[KR == 64 ? KQ : 1];
     f32x4* const af = KR == 64 ? afs : cx;  // (in place at 128: cx is dead after the transform)
+    if constexpr (CO) {
+      f32x4 mu, is, ga, be;
+      if constexpr (BN) {
+        mu = ld4(tb + 0 * KR + 4 * cq);
+        is = ld4(tb + 1 * KR + 4 * cq);
+        ga = ld4(tb + 2 * KR + 4 * cq);
+        be = ld4(tb + 3 * KR + 4 * cq);
+      }
 #pragma unroll
-    for (int q = 0; q < KQ; ++q) {
+      for (int q = 0; q < KQ; ++q) {
+        f32x4 v = cx[q];
+        if constexpr (BN) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float r = bn_out(v[e], mu[e], is[e], ga[e], be[e]);
+            v[e] = (irelu & !(r > 0.f)) ? 0.f : r;
+          }
+        }
+        st4(ta + (pr + 4 * q) * SKA + 4 * cq, v);
+      }
+#pragma unroll
+      for (int q = 0; q < KQ; ++q) af[q] = ld4(ta + l32 * SKA + 8 * q + 4 * h);
+    }
+#pragma unroll
+    for (int q = 0; q < (CO ? 0 : KQ); ++q) {
       f32x4 v = cx[q];
       if constexpr (BN) {
         const int k0 = 8 * q + 4 * h;
@@ -453,7 +492,12 @@ __global__ __launch_bounds__(256, KR_ == 64 ? 3 : 2) void fwd_kernel(FwdArgs a) 
     for (int w = 0; w < WAVES; ++w) s += red[w][which][c];
     pub_store(a.part + ((size_t)blockIdx.x * 2 + which) * NO + c, s);
   }
-  if (a.ft.part) fold_tail<256>(a.ft, blockIdx.x, 0, NO, 0);
+  if (a.ft.part) {
+    if constexpr (CO)
+      fold_tail<256>(a.ft, blockIdx.x, 0, NO, 0, reinterpret_cast<double2*>(Ta));  // (the image is free)
+    else
+      fold_tail<256>(a.ft, blockIdx.x, 0, NO, 0);
+  }
 }
 
 // Resident blocks per CU of a family of instantiations (the smallest; queried once per family).
@@ -862,7 +906,7 @@ int pw_stream_bwd_fused(const float* g, const float* bn_x, int M, const float* o
   pws::BwdArgs a{{g, bn_x, nullptr, w, dx, res, x, om, ois, og, ob, k12, orelu, im, iis, ig, ib, irelu, part, M},
                  bm, bis, bgm, bbt, brelu, wpart};
   if (ft && part) a.d.ft = *ft;
-  a.d.nt = nt_stores();
+  a.d.nt = nt_stores(kNtPwsBwd);
   const dim3 grid(pws::bwd_fused_blocks(M));
   const bool r = res != nullptr, pt = part != nullptr, bn = bm != nullptr;
   if (pt && !bn) return DK_ERR_ARGS;
@@ -903,7 +947,7 @@ int pw_stream_fwd(const float* x, int N, int H, int W, int stride, int OH, int O
   pws::FwdArgs a{x, w, bias, y, im, iis, ig, ib, irelu, part, M, H, W, OH, OW, stride,
                  (uint32_t)((size_t)N * H * W * KC * 4)};
   if (ft && part) a.ft = *ft;
-  a.nt = nt_stores();
+  a.nt = nt_stores(kNtPwsFwd);
   const dim3 grid(pws::fwd_blocks(M, KC));
   const bool strided = stride != 1;
 #define DK_FWD(BN_, ST_)                                                                                \
@@ -936,7 +980,7 @@ int pw_stream_dgrad_bnbwd(const float* g, const float* bn_x, int M, const float*
                           hipStream_t st, const FoldTail* ft) {
   pws::DgradArgs a{g, bn_x, dy_out, w, dx, res, x, om, ois, og, ob, k12, orelu, im, iis, ig, ib, irelu, part, M};
   if (ft && part) a.ft = *ft;
-  a.nt = nt_stores();
+  a.nt = nt_stores(kNtPwsDgrad);
   const dim3 grid(pws::dgrad_blocks(M));
   if (res && x)
     hipLaunchKernelGGL((pws::dgrad_bnbwd_kernel<true, true>), grid, dim3(256), 0, st, a);

@@ -48,7 +48,7 @@ def main():
     for _ in range(5):
         for nt in (0, 1):
             for r in (0, 1):
-                lib.dk_debug_set_gemm_config(4, nt)
+                lib.dk_debug_set_gemm_config(4, nt << 3)  # bit 3: the fused pointwise backward
                 args = (gg.data_ptr(), xo.data_ptr(), B, H, H, K, *(t.data_ptr() for t in po), 1, k12.data_ptr(),
                         w.data_ptr(), C, 1e-4, dw.data_ptr(), dx.data_ptr(), res.data_ptr() if r else 0,
                         xin.data_ptr(), *(t.data_ptr() for t in pi), 1, part.data_ptr(), ws.data_ptr(), nbf, st)
