@@ -243,6 +243,9 @@ int pw_stream_bf16_dgrad_bnbwd(const bf16_t* g, const bf16_t* bn_x, int M, int K
                                bf16_t* dy_out, const float* w, bf16_t* dx, const bf16_t* res, const bf16_t* x,
                                const float* im, const float* iis, const float* ig, const float* ib, int irelu,
                                double* part, hipStream_t st, const struct FoldTail* ft = nullptr);
+int pw_stream_bf16_fwd_slices(int K, int C);    // channel slices of the partial rows (fold_take)
+int pw_stream_bf16_dgrad_slices(int K, int C);
+void pw_stream_bf16_deep_set(int v);  // tuning knob (dk_debug_set_gemm_config kind 10)
 void pw_stream_bf16_set(int v);  // tuning knob (dk_debug_set_gemm_config kind 9)
 
 }  // namespace dk

@@ -46,7 +46,7 @@ DK_API int dk_pwconv_fwd_ex_bf16(const bf16_t* x, int N, int H, int W, int C, co
     // the streaming kernel (pw_stream_bf16.hip): bit-identical y, its own partial-row grouping
     const int M = N * OH * OW;
     FoldTail ft;
-    if (stats) fold_take(stats, pw_stream_bf16_fwd_rows(M, K, C), K, 1, &ft);
+    if (stats) fold_take(stats, pw_stream_bf16_fwd_rows(M, K, C), K, pw_stream_bf16_fwd_slices(K, C), &ft);
     return fold_status(pw_stream_bf16_fwd(x, M, w_kc, K, C, bias, y, bn_mean, bn_invstd, bn_gamma, bn_beta, bn_relu,
                                           stats, st, stats ? &ft : nullptr),
                        stats ? ft : FoldTail{});
@@ -157,7 +157,7 @@ DK_API int dk_pwconv_dgrad_bnbwd_bf16(const bf16_t* g, const bf16_t* bn_x, int N
       (!part || bn_ok(bn_mean, bn_invstd, bn_gamma, bn_beta))) {
     // the streaming kernel (pw_stream_bf16.hip): bit-identical dy and dx, its own partial rows
     FoldTail ft;
-    if (part) fold_take(part, pw_stream_bf16_dgrad_rows(M, K, C), C, 1, &ft);
+    if (part) fold_take(part, pw_stream_bf16_dgrad_rows(M, K, C), C, pw_stream_bf16_dgrad_slices(K, C), &ft);
     return fold_status(pw_stream_bf16_dgrad_bnbwd(g, bn_x, M, K, C, out_mean, out_invstd, out_gamma, out_beta,
                                                   out_relu, k12, dy_out, w_kc, dx, residual, x, bn_mean, bn_invstd,
                                                   bn_gamma, bn_beta, bn_relu, part, as_stream(stream),

@@ -88,6 +88,10 @@ DK_API int dk_debug_set_gemm_config(int kind, int cfg) {
     dw_seg_set(cfg);
     return 0;
   }
+  if (kind == 10) {  // the bf16 deep (column-sliced) streaming pointwise kernels on / off
+    pw_stream_bf16_deep_set(cfg);
+    return 0;
+  }
   if (kind == 9) {  // the bf16 streaming pointwise kernels (pw_stream_bf16.hip) on / off
     pw_stream_bf16_set(cfg);
     return 0;

@@ -60,7 +60,8 @@ int dk_mixup_f32(const float* a, const float* b, long long n, float p, float one
  * prefetch; kind 6: unused; kind 7: blocks the fused stride-1 depthwise backward aims for (its
  * batch is dealt into image runs above that; 0 = one image per block; -1 = default 768);
  * kind 8: output rows per thread of the depthwise forward / stride-1 dgrad (-1 = the shape rule);
- * kind 9: the bf16 streaming pointwise kernels (1 / -1 = on, the default; 0 = the tiled engine). */
+ * kind 9: the bf16 streaming pointwise kernels (1 / -1 = on, the default; 0 = the tiled engine);
+ * kind 10: their column-sliced variants for K or C of 256 / 512 (1 / -1 = on; 0 = the tiled engine). */
 int dk_debug_set_gemm_config(int kind, int cfg);
 
 /* Bandwidth ceiling probe (not on the training path; scripts/stream_ceiling.py): reads nin

@@ -121,3 +121,38 @@ def test_bf16_stream_dgrad_bnbwd_matches_tiled_engine(K, C, relu, bn_in, resid, 
     if bn_in:
         s0, s1 = part0.sum(0), part1.sum(0)
         assert float((s1 - s0).norm() / s0.norm()) < 1e-12
+
+
+# The deep (column-sliced, k-chunked) kernels: K or C of 256 / 512 (config 5's 14 x 14 and 7 x 7 units).
+DEEP = [(256, 128), (256, 256), (512, 256), (512, 512), (128, 256)]
+
+
+@pytest.mark.parametrize("K,C", DEEP)
+@pytest.mark.parametrize("bn,relu,stats,bias,N,H,W", [(True, 1, True, False, 3, 13, 11),
+                                                    (False, 0, True, True, 2, 7, 5),
+                                                    (True, 0, False, False, 1, 1, 5),
+                                                    (True, 1, True, False, 16, 7, 7)])
+def test_bf16_deep_fwd_matches_tiled_engine(K, C, bn, relu, stats, bias, N, H, W):
+    test_bf16_stream_fwd_matches_tiled_engine(K, C, bn, relu, stats, bias, N, H, W)
+
+
+@pytest.mark.parametrize("K,C", [(k, c) for c, k in DEEP])
+@pytest.mark.parametrize("relu,bn_in,resid,dyout,N,H,W", [(1, True, False, True, 3, 13, 11),
+                                                        (1, False, True, True, 3, 13, 11),
+                                                        (1, True, True, False, 5, 7, 9),
+                                                        (0, False, False, True, 1, 1, 3),
+                                                        (1, True, False, True, 16, 7, 7)])
+def test_bf16_deep_dgrad_bnbwd_matches_tiled_engine(K, C, relu, bn_in, resid, dyout, N, H, W):
+    test_bf16_stream_dgrad_bnbwd_matches_tiled_engine(K, C, relu, bn_in, resid, dyout, N, H, W)
+
+
+def test_bf16_deep_kernels_dispatch():
+    """The deep shapes go to the streaming kernels: one partial row per walker block, not per tile."""
+    M = 512 * 7 * 7
+    lib.dk_debug_set_gemm_config(9, 0)
+    try:
+        tiled = lib.dk_pwconv_fwd_bf16_stats_rows(512, 7, 7, 512, 512)
+    finally:
+        lib.dk_debug_set_gemm_config(9, -1)
+    streamed = lib.dk_pwconv_fwd_bf16_stats_rows(512, 7, 7, 512, 512)
+    assert streamed != tiled and streamed <= 256 and tiled >= M // 256
