@@ -34,8 +34,8 @@ METRIC = "images/sec training step, ResNet-18-depsep 225x225 bs=256, 1/2/4/8 MI3
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=None, help="default 20 (config 2: 50)")
+    ap.add_argument("--warmup", type=int, default=None, help="default 10 (config 2: 20)")
     ap.add_argument("--batch", type=int, default=256, help="images per GPU")
     ap.add_argument("--bn", choices=["local", "sync"], default="local")
     ap.add_argument("--no-roofline", action="store_true")
@@ -49,7 +49,14 @@ def parse():
     ap.add_argument("--pmc", default=None,
                     help="per-kernel HBM traffic from rocprofv3 FETCH_SIZE/WRITE_SIZE passes of this same command "
                          "(scripts/pmc_summary.py output; default: the newest profiles/*_pmc.json)")
-    return ap.parse_args()
+    a = ap.parse_args()
+    # enough warmup for the clocks to settle (the first timed steps after 3 warmups ran up to 5 %
+    # slow, profiles/r03s_cfg2_rows.txt round 1), and more steps for config 2's 1.6 ms pass
+    if a.steps is None:
+        a.steps = 50 if a.config == 2 else 20
+    if a.warmup is None:
+        a.warmup = 20 if a.config == 2 else 10
+    return a
 
 
 class Instrument:
