@@ -161,20 +161,25 @@ __global__ __launch_bounds__(256) void dw_fwd_kernel(const T* __restrict__ x, ui
 #pragma unroll
     for (int r = 0; r < R; ++r)
       load_row<NC, BN, T>(win[r], rs, n, oh0 * ST - pad + r, iw0, H, W, C, c, bn, bm, bi, bg, bb);
-    // bf16, stride 1: the next output row's new input row is loaded one row ahead, kept packed (2
-    // registers per 4 channels) and widened / normalised when it enters the window; fp32 and
-    // stride 2 load it in the row that uses it (their windows leave no registers for a prefetch)
-    constexpr bool PFR = sizeof(T) == 2 && ST == 1;
-    uint2 pre[PFR ? NC : 1];
+    // stride 1: the next output row's new input row is loaded one row ahead (bf16 kept packed, 2
+    // registers per 4 channels) and widened / normalised when it enters the window; stride 2 loads
+    // it in the row that uses it (its window leaves no registers for a prefetch)
+    constexpr bool PFR = ST == 1 && R == 3;
+    using PT = typename std::conditional<sizeof(T) == 2, uint2, f32x4>::type;
+    PT pre[PFR ? NC : 1];
     auto load_pre = [&](int ih) {
       if constexpr (PFR) {
         const bool rv = (unsigned)ih < (unsigned)H;
 #pragma unroll
         for (int q = 0; q < NC; ++q) {
           const bool ok = rv && (unsigned)(iw0 + q) < (unsigned)W;
-          pre[q] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(
-                                                 rs, (int)(ok ? (uint32_t)(((n * H + ih) * W + iw0 + q) * C + c) * 2u
-                                                              : kOOBBytes), 0, 0));
+          const uint32_t e = (uint32_t)(((n * H + ih) * W + iw0 + q) * C + c);
+          if constexpr (sizeof(T) == 2)
+            pre[q] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rs, (int)(ok ? e * 2u : kOOBBytes),
+                                                                                    0, 0));
+          else
+            pre[q] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(ok ? e * 4u : kOOBBytes),
+                                                                                     0, 0));
         }
       }
     };
@@ -204,7 +209,11 @@ __global__ __launch_bounds__(256) void dw_fwd_kernel(const T* __restrict__ x, ui
             const bool rv = (unsigned)ih < (unsigned)H;
 #pragma unroll
             for (int q = 0; q < NC; ++q) {
-              f32x4 v = bf16x4_to_f32(pre[q]);
+              f32x4 v;
+              if constexpr (sizeof(T) == 2)
+                v = bf16x4_to_f32(pre[q]);
+              else
+                v = pre[q];
               if constexpr (BN) {
                 const bool ok = rv && (unsigned)(iw0 + q) < (unsigned)W;
                 const f32x4 t = bn_in4(v, bm, bi, bg, bb, bn.relu);
