@@ -87,9 +87,9 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(FwdArgs a) {
   __shared__ double red[WAVES][2][NO];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int l32 = lane & 31, h = lane >> 5;
-  for (int i = tid; i < KR * NO; i += 256) {
-    const int n = i / KR, k = i - n * KR;
-    Bs[n * SKB + k] = bf16_bits(a.w[i]);
+  for (int i = tid; i < KR * NO / 4; i += 256) {  // 4 k at a time
+    const int n = i / (KR / 4), k = 4 * (i - n * (KR / 4));
+    *reinterpret_cast<uint2*>(Bs + n * SKB + k) = f32_to_bf16x4(ld4(a.w + (size_t)n * KR + k));
   }
   if constexpr (BN) {
     for (int c = tid; c < KR; c += 256) {
@@ -248,9 +248,14 @@ __global__ __launch_bounds__(256, 2) void dgrad_bnbwd_kernel(DgradArgs a) {
   __shared__ double red[WAVES][2][NO];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int l32 = lane & 31, h = lane >> 5;
-  for (int i = tid; i < KR * NO; i += 256) {
-    const int k = i / NO, c = i - k * NO;
-    Bs[c * SKB + k] = bf16_bits(a.w[i]);
+  for (int i = tid; i < KR * NO / 16; i += 256) {  // 4 k x 4 c blocks, transposed
+    const int kq = i / (NO / 4), c = 4 * (i - kq * (NO / 4)), k = 4 * kq;
+    f32x4 r[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) r[j] = ld4(a.w + (size_t)(k + j) * NO + c);
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      *reinterpret_cast<uint2*>(Bs + (c + e) * SKB + k) = f32_to_bf16x4(f32x4{r[0][e], r[1][e], r[2][e], r[3][e]});
   }
   for (int k = tid; k < KR; k += 256) {
     const float is = a.ois[k], ga = a.og[k];
@@ -460,9 +465,11 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void fwd_deep_kernel(Deep
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int l32 = lane & 31, h = lane >> 5;
   const int n0 = blockIdx.y * NO, N = a.N;
-  for (int i = tid; i < KR * NO; i += NT) {
-    const int n = i / KR, k = i - n * KR;
-    Bs[n * SKB + k] = bf16_bits(a.w[(size_t)(n0 + n) * KR + k]);
+  // the weight slice, 4 k at a time (16-byte loads, 8-byte LDS stores)
+  for (int i = tid; i < KR * NO / 4; i += NT) {
+    const int n = i / (KR / 4), k = 4 * (i - n * (KR / 4));
+    const f32x4 v = ld4(a.w + (size_t)(n0 + n) * KR + k);
+    *reinterpret_cast<uint2*>(Bs + n * SKB + k) = f32_to_bf16x4(v);
   }
   if constexpr (BN) {
     for (int c = tid; c < KR; c += NT) {
@@ -602,9 +609,16 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void dgrad_deep_kernel(De
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int l32 = lane & 31, h = lane >> 5;
   const int n0 = blockIdx.y * NO, N = a.N;
-  for (int i = tid; i < KR * NO; i += NT) {
-    const int k = i / NO, c = i - k * NO;
-    Bs[c * SKB + k] = bf16_bits(a.w[(size_t)k * N + n0 + c]);
+  // the weight slice transposed, a 4 x 4 block (4 k x 4 c) per step: 16-byte loads along c,
+  // 8-byte LDS stores along k
+  for (int i = tid; i < KR * NO / 16; i += NT) {
+    const int kq = i / (NO / 4), c = 4 * (i - kq * (NO / 4)), k = 4 * kq;
+    f32x4 r[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) r[j] = ld4(a.w + (size_t)(k + j) * N + n0 + c);
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      *reinterpret_cast<uint2*>(Bs + (c + e) * SKB + k) = f32_to_bf16x4(f32x4{r[0][e], r[1][e], r[2][e], r[3][e]});
   }
   for (int k = tid; k < KR; k += NT) {
     const float is = a.is0[k], ga = a.g0[k];

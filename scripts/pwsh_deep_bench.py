@@ -2,7 +2,7 @@
 (pw_stream_bf16.hip, knob 10 on) against the tiled engine (knob 10 off), forward with BN on load +
 statistics and the BN-backward-on-load dgrad with dy write-through and the input BN's partials;
 median of 9 calls, HBM rate of the algorithmic bytes.
-    python scripts/pwsh_deep_bench.py
+    python scripts/pwsh_deep_bench.py [--no-bn]    (--no-bn: forward without the input BN)
 """
 import os
 import sys
@@ -51,8 +51,8 @@ def main():
             lib.dk_debug_set_gemm_config(10, deep)
             rows = lib.dk_pwconv_fwd_bf16_stats_rows(B, HW, HW, K, C)
             part = torch.empty(rows * 2 * K, dtype=torch.float64, device="cuda")
-            fa = (x.data_ptr(), B, HW, HW, C, w.data_ptr(), K, 1, 0, y.data_ptr(), HW, HW,
-                  *(t.data_ptr() for t in pi), 1, part.data_ptr(), st)
+            bn = (0, 0, 0, 0, 0) if "--no-bn" in sys.argv else (*(t.data_ptr() for t in pi), 1)
+            fa = (x.data_ptr(), B, HW, HW, C, w.data_ptr(), K, 1, 0, y.data_ptr(), HW, HW, *bn, part.data_ptr(), st)
             tf = timeit(lambda: lib.dk_pwconv_fwd_ex_bf16(*fa))
             rows = lib.dk_pwconv_dgrad_bnbwd_bf16_stats_rows(B, HW, HW, K, C)
             partd = torch.empty(rows * 2 * C, dtype=torch.float64, device="cuda")
