@@ -453,8 +453,9 @@ struct DeepArgs {
   FoldTail ft;
 };
 
-template <int KR, int NW, int CK, bool BN, bool STATS>
+template <int KR, int NW, int CK0, bool BN, bool STATS>
 __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void fwd_deep_kernel(DeepArgs a) {
+  constexpr int CK = CK0 < KR ? CK0 : KR;
   constexpr int NO = NOD, SKB = KR + 8, NU = NO / 32, CS = CK / 16, NCH = KR / CK, NT = 64 * NW;
   static_assert(KR % CK == 0 && CK % 16 == 0, "chunks");
   __shared__ __attribute__((aligned(16))) bf16_t Bs[NO * SKB];
@@ -598,8 +599,9 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void fwd_deep_kernel(Deep
   if (a.ft.part) fold_tail<NT>(a.ft, blockIdx.x, n0, NO, blockIdx.y);
 }
 
-template <int KR, int NW, int CK, bool RES, bool PART>
+template <int KR, int NW, int CK0, bool RES, bool PART>
 __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void dgrad_deep_kernel(DeepArgs a) {
+  constexpr int CK = CK0 < KR ? CK0 : KR;
   constexpr int NO = NOD, SKB = KR + 8, NU = NO / 32, CS = CK / 16, NCH = KR / CK, NT = 64 * NW;
   static_assert(KR % CK == 0 && CK % 16 == 0, "chunks");
   __shared__ __attribute__((aligned(16))) bf16_t Bs[NO * SKB];  // Bs[c][k] = W[k][n0 + c]
@@ -819,7 +821,7 @@ template <int KR>
 constexpr int deep_nw() {
   return KR >= 512 ? 8 : 4;
 }
-constexpr int kFwdCK = 128, kDgradCK = 64;
+constexpr int kFwdCK = 64, kDgradCK = 64;
 static bool deep_shape(int KR, int N) {
   return (KR == 128 || KR == 256 || KR == 512) && N % NOD == 0 && N >= NOD && N <= 4096 && (KR >= 256 || N >= 256);
 }
