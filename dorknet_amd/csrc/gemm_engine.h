@@ -1130,16 +1130,20 @@ static int launch_igemm(const DA& da, const DB& db, const EP& ep, int M, int N, 
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&igemm_f32<BM, BN, BK, WM, WN, A, DA, B, DB, EP, MF>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn);
   }
-  // resident blocks per CU of this instantiation (queried once; immutable afterwards)
+  // resident blocks per CU of this instantiation (queried once; immutable afterwards), and its
+  // static LDS: a launch whose static + dynamic LDS exceeds the CU's 160 KB is refused here (the
+  // runtime would abort the queue)
   static int occ = -1;
+  static size_t lds_static = 0;
   if (occ < 0) {
+    const void* fn = reinterpret_cast<const void*>(&igemm_f32<BM, BN, BK, WM, WN, A, DA, B, DB, EP, MF>);
+    hipFuncAttributes fa{};
+    if (hipFuncGetAttributes(&fa, fn) == hipSuccess) lds_static = fa.sharedSizeBytes;
     int o = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            &o, reinterpret_cast<const void*>(&igemm_f32<BM, BN, BK, WM, WN, A, DA, B, DB, EP, MF>), NT, dyn) !=
-            hipSuccess || o < 1)
-      o = 1;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, fn, NT, dyn) != hipSuccess || o < 1) o = 1;
     occ = o;
   }
+  if (lds_static + dyn > (size_t)160 * 1024) return DK_ERR_ARGS;
   const int slots = occ * kNumCUs;
   if (g_fill_splits && splits_used && splits > 1 && tiles * splits > slots && tiles <= slots) {
     // split-K: no second, partly filled round of blocks (the stem's 64x128 weight-gradient

@@ -460,6 +460,7 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void fwd_deep_kernel(Deep
   static_assert(KR % CK == 0 && CK % 16 == 0, "chunks");
   __shared__ __attribute__((aligned(16))) bf16_t Bs[NO * SKB];
   __shared__ __attribute__((aligned(16))) float tab[4][KR];
+  static_assert(sizeof(bf16_t) * NO * SKB + sizeof(float) * 4 * KR <= 159 * 1024, "LDS of one CU");
   // the statistics' block reduction reuses the weight slice once every wave has left the loop
   double(*const red)[2][NO] = reinterpret_cast<double(*)[2][NO]>(Bs);
   static_assert(sizeof(double) * NW * 2 * NO <= sizeof(bf16_t) * NO * SKB, "red fits in Bs");
@@ -606,6 +607,7 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void dgrad_deep_kernel(De
   static_assert(KR % CK == 0 && CK % 16 == 0, "chunks");
   __shared__ __attribute__((aligned(16))) bf16_t Bs[NO * SKB];  // Bs[c][k] = W[k][n0 + c]
   __shared__ __attribute__((aligned(16))) float tab[7][KR];
+  static_assert(sizeof(bf16_t) * NO * SKB + sizeof(float) * 7 * KR <= 159 * 1024, "LDS of one CU");
   double(*const red)[2][NO] = reinterpret_cast<double(*)[2][NO]>(Bs);
   static_assert(sizeof(double) * NW * 2 * NO <= sizeof(bf16_t) * NO * SKB, "red fits in Bs");
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
