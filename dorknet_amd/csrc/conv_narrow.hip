@@ -34,6 +34,7 @@ struct Geo {
   int CS;    // LDS row stride (odd: consecutive k land on opposite bank parities)
   int rows;  // N * OH output rows
   int rpb;   // output rows per block
+  int nt;    // forward: nontemporal output stores (nt_stores(kNtStem))
 };
 
 __device__ __forceinline__ f32x4 mfma16(float a, float b, f32x4 c) {
@@ -133,7 +134,10 @@ __global__ __launch_bounds__(NT, 2) void fwd_kernel(const float* __restrict__ x,
         const int ow = 16 * t + 4 * lg + v;
         if (cok && ow < g.OW) {
           const float o = acc[t][v] + bv;
-          yr[(size_t)ow * g.K] = o;
+          if (g.nt)
+            __builtin_nontemporal_store(o, yr + (size_t)ow * g.K);
+          else
+            yr[(size_t)ow * g.K] = o;
           sa += (double)o;
           sb += (double)o * (double)o;
         }
@@ -417,6 +421,7 @@ DK_API int dk_conv2d_fwd_narrow_f32(const float* x_nchw, int N, int C, int H, in
                                     double* stats, void* stream) {
   if (!supported(N, C, H, W, K, R, S, stride, pad, OH, OW) || !x_nchw || !w_kcrs || !y) return DK_ERR_ARGS;
   Geo g = geo(N, C, H, W, K, R, S, stride, pad, OH, OW);
+  g.nt = nt_stores(kNtStem);
   const FwdFn fn = fwd_fn(g);
   const size_t lds = fwd_lds(g);
   const int grid = grid_for(reinterpret_cast<const void*>(fn), lds, g);

@@ -191,8 +191,8 @@ enum : int { DK_FOLDED = 10100 };
 // nontemporally when set (A/B runs only; default from DORKNET_NT_STORES, else 0).
 // Nontemporal output stores per kernel family (tuning knob dk_debug_set_gemm_config(4, mask), env
 // DORKNET_NT_STORES=mask): bit kNt* set = that family's main output stores are nontemporal.
-enum NtFam : int { kNtDwFwd = 0, kNtDwBwd = 1, kNtBnAdd = 2, kNtPwsBwd = 3, kNtPwsFwd = 4, kNtPwsDgrad = 5, kNtGemm = 6 };
-constexpr int kNtDefault = 127;  // all families: config 3 8.868 -> 8.819 ms, config 5 7.596 -> 7.566 (profiles/r03q_ntfam_config*.txt)
+enum NtFam : int { kNtDwFwd = 0, kNtDwBwd = 1, kNtBnAdd = 2, kNtPwsBwd = 3, kNtPwsFwd = 4, kNtPwsDgrad = 5, kNtGemm = 6, kNtStem = 7 };
+constexpr int kNtDefault = 127;  // families 0-6: config 3 8.868 -> 8.819 ms, config 5 7.596 -> 7.566 (profiles/r03q_ntfam_config*.txt)
 int nt_stores(int fam);
 
 // Split-K second stage (reduce.hip): out = sum_s ws[s][M][N] (+ l2 * w), fixed order.

@@ -56,7 +56,8 @@ int dk_mixup_f32(const float* a, const float* b, long long n, float p, float one
  * tiled engine for every shape, as DORKNET_PW_STREAM=0); returns 0.
  * kind 4: nontemporal output stores, a bitmask over kernel families (bit 0 depthwise forward, 1 fused
  * depthwise backward, 2 bn_add, 3 fused pointwise backward, 4 streaming pointwise forward, 5 streaming
- * BN-backward dgrad, 6 tiled GEMM epilogues; -1 = the default mask); kind 5: the streaming fused pointwise backward's operand
+ * BN-backward dgrad, 6 tiled GEMM epilogues, 7 the narrow stem forward; -1 = the default mask, bits
+ * 0-6); kind 5: the streaming fused pointwise backward's operand
  * prefetch; kind 6: unused; kind 7: blocks the fused stride-1 depthwise backward aims for (its
  * batch is dealt into image runs above that; 0 = one image per block; -1 = default 768);
  * kind 8: output rows per thread of the depthwise forward / stride-1 dgrad (-1 = the shape rule);
