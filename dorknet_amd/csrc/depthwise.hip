@@ -228,6 +228,11 @@ __global__ __launch_bounds__(256) void dw_fwd_kernel(const T* __restrict__ x, ui
         }
       }
       T* yrow = y + ((size_t)(n * OH + oh) * OW) * C + c;
+      // bf16 statistics: the row's (at most TW) stored values summed in fp32 first -- their 8-bit
+      // significands (16-bit squares) add exactly unless they span more than ~8 binades -- and
+      // added to the fp64 sums once per row: a third of the fp64 work of this VALU-bound kernel
+      constexpr bool RS = STATS == 1 && sizeof(T) == 2;
+      f32x4 r1 = {0.f, 0.f, 0.f, 0.f}, r2 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int j = 0; j < TW; ++j) {
         f32x4 acc = b0;
@@ -244,7 +249,11 @@ __global__ __launch_bounds__(256) void dw_fwd_kernel(const T* __restrict__ x, ui
             st4nt(yrow + (size_t)(ow0 + j) * C, acc);
           else
             st4(yrow + (size_t)(ow0 + j) * C, acc);
-          if constexpr (STATS == 1) {
+          if constexpr (RS) {
+            r1 += acc;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) r2[e] = __builtin_fmaf(acc[e], acc[e], r2[e]);
+          } else if constexpr (STATS == 1) {
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
               const double v = (double)acc[e];
@@ -261,6 +270,13 @@ __global__ __launch_bounds__(256) void dw_fwd_kernel(const T* __restrict__ x, ui
               s2[e] += (double)g * (double)xh;
             }
           }
+        }
+      }
+      if constexpr (RS) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          s1[e] += (double)r1[e];
+          s2[e] += (double)r2[e];
         }
       }
     }
