@@ -308,3 +308,88 @@ def join_weight_grads() -> None:
     s = _SIDE.get(dev)
     if s is not None and s != torch.cuda.current_stream():
         torch.cuda.current_stream().wait_stream(s)
+
+
+# ---------------------------------------------------------------------------------------
+# A residual block's skip projection on a branch stream.  The skip branch (a strided pointwise
+# layer: its forward, and in backward its input gradient) depends only on the block's input (or
+# the join's gradient), so it can run beside the main branch's chain instead of before it; the
+# main stream waits for it only where the two branches meet (the join; the chain's first dgrad,
+# which adds the skip gradient).  DORKNET_BRANCH_STREAM=0 keeps everything on one stream.
+# ---------------------------------------------------------------------------------------
+_BRANCH = {}
+
+
+def branch_stream_enabled() -> bool:
+    return os.environ.get("DORKNET_BRANCH_STREAM", "1") != "0" and torch.cuda.is_available()
+
+
+def branch_stream():
+    dev = _get_dev() if _get_dev is not None else torch.cuda.current_device()
+    s = _BRANCH.get(dev)
+    if s is None:
+        s = _BRANCH[dev] = torch.cuda.Stream(device=dev)
+    return s
+
+
+def _tensors(obj):
+    """The CUDA tensors an activation-like object holds (a tensor, or a BNOut / BNGrad record)."""
+    if isinstance(obj, torch.Tensor):
+        return [obj] if obj.is_cuda else []
+    return [v for v in vars(obj).values() if isinstance(v, torch.Tensor) and v.is_cuda] if hasattr(obj, "__dict__") else []
+
+
+def record_on(stream, *objs) -> None:
+    """Mark the tensors of `objs` as in use by `stream` (the caching allocator keeps them until
+    the work queued there so far is done)."""
+    for o in objs:
+        for t in _tensors(o):
+            t.record_stream(stream)
+
+
+class Branch:
+    """A value computed on the branch stream: `resolve()` makes the current stream wait for it
+    and returns it (marked as used by the current stream)."""
+
+    def __init__(self, value, event):
+        self.value = value
+        self.event = event
+
+    def resolve(self):
+        cur = torch.cuda.current_stream()
+        cur.wait_event(self.event)
+        record_on(cur, self.value)
+        return self.value
+
+
+def resolve(v):
+    return v.resolve() if isinstance(v, Branch) else v
+
+
+class on_branch:
+    """with on_branch(*inputs) as b: launches inside go to the branch stream, after everything
+    already queued on the current stream; the inputs are marked as used there.  b.done(value)
+    records the branch's completion and returns a Branch for the consumer to resolve()."""
+
+    def __init__(self, *inputs):
+        self.inputs = inputs
+        self.ctx = None
+
+    def __enter__(self):
+        main = torch.cuda.current_stream()
+        br = branch_stream()
+        br.wait_stream(main)
+        record_on(br, *self.inputs)
+        self.ctx = torch.cuda.stream(br)
+        self.ctx.__enter__()
+        return self
+
+    def __exit__(self, *exc):
+        self.ctx.__exit__(*exc)
+        return False
+
+    def done(self, value):
+        ev = torch.cuda.Event()
+        ev.record(branch_stream())
+        return Branch(value, ev)
+

@@ -201,6 +201,7 @@ def chain_backward(steps, dy, residual=None, after_step=None, need_input_grad=Tr
 def _backward_steps(steps, dy, residual, after_step, need_input_grad, join):
     from ._bn_input import accepts_bn_grad, add_residual
     from .batch_norm import BatchNormLayer
+    from .._hip import resolve
     last = len(steps) - 1
     fuse = fusion_enabled()
     for i in range(last, -1, -1):
@@ -216,6 +217,7 @@ def _backward_steps(steps, dy, residual, after_step, need_input_grad, join):
         elif i == 0 and not need_input_grad and residual is None and getattr(step[0], "skips_input_grad", False):
             dy = step[0].backward(dy, need_dx=False)
         elif i == 0 and residual is not None and getattr(step[0], "accepts_residual", False):
+            residual = resolve(residual)  # a skip gradient from the branch stream: wait for it here
             if join is not None and getattr(step[0], "accepts_join", False):
                 dy = step[0].backward(dy, residual=residual, join=join)
             else:
@@ -239,5 +241,5 @@ def _backward_steps(steps, dy, residual, after_step, need_input_grad, join):
         if after_step is not None:
             after_step(i)
     if residual is not None:
-        dy = add_residual(dy, residual)
+        dy = add_residual(dy, resolve(residual))
     return dy

@@ -12,7 +12,7 @@ from __future__ import annotations
 
 import os
 
-from .._hip import lib, stream_handle
+from .._hip import branch_stream_enabled, lib, on_branch, resolve, stream_handle
 from .._tensor import empty_nhwc, to_nhwc
 from ._bn_input import accepts_bn_input, materialize
 from ._chain import chain_backward, chain_forward, fusion_enabled, notify_backward_done
@@ -73,10 +73,18 @@ class ResidualBlock(Layer):
     def forward(self, X, test_mode=False):
         post = self.post_skip_activation
         join_fused = type(post) is ReLu
+        skip = self.skip_projection
+        branch = skip is not None and branch_stream_enabled()
+        if branch:
+            # the skip projection on the branch stream, beside the chain; joined at the join
+            Xs = X if accepts_bn_input(skip) else materialize(X)
+            with on_branch(Xs) as b:
+                skippee = b.done(skip.forward(Xs, test_mode=test_mode))
         X_tmp, self._steps = chain_forward(self.layer_list, X, test_mode=test_mode, out_accepts=join_fused)
-        if self.skip_projection is not None:
-            skippee = self.skip_projection.forward(X if accepts_bn_input(self.skip_projection) else materialize(X),
-                                                   test_mode=test_mode)
+        if branch:
+            skippee = skippee.resolve()
+        elif skip is not None:
+            skippee = skip.forward(X if accepts_bn_input(skip) else materialize(X), test_mode=test_mode)
         else:
             skippee = X
         if join_fused:
@@ -100,9 +108,15 @@ class ResidualBlock(Layer):
         # the skip branch's gradient goes in first, so the chain's first layer can add it in
         # its dgrad epilogue instead of a separate join pass (residual_block.py:94-97)
         skip = self.skip_projection
+        lattice = skip is not None and fusion_enabled() and self._lattice_skip(join)
         if skip is None:
             skip_dx = joined_dx
-        elif fusion_enabled() and self._lattice_skip(join):
+        elif branch_stream_enabled():
+            # the skip gradient on the branch stream, beside the chain's backward; the chain's
+            # first dgrad (or the separate add) waits for it
+            with on_branch(joined_dx) as b:
+                skip_dx = b.done(skip.backward(joined_dx, lattice_out=True) if lattice else skip.backward(joined_dx))
+        elif lattice:
             # a strided skip's gradient stays its compact lattice: the first dgrad adds it there
             skip_dx = skip.backward(joined_dx, lattice_out=True)
         else:
@@ -111,7 +125,7 @@ class ResidualBlock(Layer):
             notify_backward_done((skip,))
         if fusion_enabled():
             return chain_backward(self._steps, joined_dx, residual=skip_dx, join=join)
-        return _add(chain_backward(self._steps, joined_dx), skip_dx)
+        return _add(chain_backward(self._steps, joined_dx), resolve(skip_dx))
 
     def _lattice_skip(self, join):
         """The skip projection may hand over its gradient as the stride-s lattice: it is a strided

@@ -1,4 +1,5 @@
-"""Weight gradients on the side stream (dorknet_amd._hip.weight_grad_stream): the network
+"""Weight gradients on the side stream (dorknet_amd._hip.weight_grad_stream) and the skip
+projections on the branch stream (dorknet_amd._hip.on_branch): the network
 backward with DORKNET_ASYNC_WGRAD=1 must give bit-identical gradients to the single-stream
 run (same kernels, only their stream changes), and the data-parallel backward, whose
 RCCL buckets are issued from the side stream, must deliver them through the flat buffer
@@ -33,6 +34,26 @@ def test_async_weight_grads_bitwise(monkeypatch):
     runs = []
     for flag in ("1", "0", "1"):
         monkeypatch.setenv("DORKNET_ASYNC_WGRAD", flag)
+        runs.append(_step(net, X, onehot))
+    torch.cuda.synchronize()
+    for other in runs[1:]:
+        for a, b in zip(runs[0], other):
+            assert torch.equal(a, b)
+
+
+def test_branch_stream_bitwise(monkeypatch):
+    """The residual blocks' skip projections on the branch stream (forward and input gradient,
+    DORKNET_BRANCH_STREAM=1) give the same gradients bit for bit as the single-stream run, at a
+    batch where the skip kernels overlap the chain, with and without side-stream weight gradients."""
+    from examples.resnet18_depsep import ResNet18, synthetic_batch
+    X, _, onehot = synthetic_batch(16, seed=11)
+    np.random.seed(12)
+    net = ResNet18("r18")
+    net.to_gpu()
+    runs = []
+    for branch, wgrad in (("1", "1"), ("0", "1"), ("1", "0"), ("0", "0"), ("1", "1")):
+        monkeypatch.setenv("DORKNET_BRANCH_STREAM", branch)
+        monkeypatch.setenv("DORKNET_ASYNC_WGRAD", wgrad)
         runs.append(_step(net, X, onehot))
     torch.cuda.synchronize()
     for other in runs[1:]:
