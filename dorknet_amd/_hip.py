@@ -15,6 +15,8 @@ import re
 
 import torch  # noqa: F401  -- loads torch's HIP runtime first; our .so binds to the same one
 
+from ._env import enabled
+
 _PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 # DORKNET_HIP_LIB: another build of the same library (A/B runs of two builds on one box)
 LIB_PATH = os.environ.get("DORKNET_HIP_LIB") or os.path.join(_PKG_DIR, "lib", "libdorknet_hip.so")
@@ -145,6 +147,48 @@ def stream_handle() -> int:
     return torch.cuda.current_stream().cuda_stream
 
 
+# The same for the stream objects the side / branch streams are joined with: torch.cuda.current_stream()
+# and the torch.cuda.stream() context resolve the device index through Python on every call (~9 us
+# and ~20 us); these go to the C layer directly.  One process drives one device (the current one).
+_get_cur_stream = getattr(torch._C, "_cuda_getCurrentStream", None)
+_set_cur_stream = getattr(torch._C, "_cuda_setStream", None)
+
+
+def cur_stream():
+    """torch.cuda.current_stream() for the current device."""
+    if _get_cur_stream is None or _get_dev is None:
+        return torch.cuda.current_stream()
+    sid, di, dt = _get_cur_stream(_get_dev())
+    return torch.cuda.Stream(stream_id=sid, device_index=di, device_type=dt)
+
+
+class use_stream:
+    """with use_stream(s): torch.cuda.stream(s) for a stream of the current device."""
+    __slots__ = ("s", "prev", "ctx")
+
+    def __init__(self, s):
+        self.s = s
+        self.prev = None
+        self.ctx = None
+
+    def __enter__(self):
+        if _get_cur_stream is None or _set_cur_stream is None or _get_dev is None:
+            self.ctx = torch.cuda.stream(self.s)
+            self.ctx.__enter__()
+            return self
+        self.prev = _get_cur_stream(_get_dev())
+        s = self.s
+        _set_cur_stream(stream_id=s.stream_id, device_index=s.device_index, device_type=s.device_type)
+        return self
+
+    def __exit__(self, *exc):
+        if self.ctx is not None:
+            return self.ctx.__exit__(*exc)
+        sid, di, dt = self.prev
+        _set_cur_stream(stream_id=sid, device_index=di, device_type=dt)
+        return False
+
+
 class Workspace:
     """Grow-only device scratch buffers, one per stream.
 
@@ -216,7 +260,7 @@ fold_resources = FoldResources()
 
 
 def inlaunch_folds_enabled() -> bool:
-    return os.environ.get("DORKNET_INLAUNCH_FOLD", "1") != "0"
+    return enabled("DORKNET_INLAUNCH_FOLD")
 
 
 # ---------------------------------------------------------------------------------------
@@ -235,7 +279,7 @@ def async_wgrad_enabled() -> bool:
     """Side-stream weight gradients are used only inside async_weight_grads() (the network /
     data-parallel backward), which joins them before it returns: a layer's backward called
     on its own keeps the reference's contract that grads are final when it returns."""
-    return _ASYNC_DEPTH[0] > 0 and os.environ.get("DORKNET_ASYNC_WGRAD", "1") != "0"
+    return _ASYNC_DEPTH[0] > 0 and enabled("DORKNET_ASYNC_WGRAD")
 
 
 def side_stream():
@@ -258,12 +302,12 @@ class weight_grad_stream:
     def __enter__(self):
         if not async_wgrad_enabled():
             return self
-        main = torch.cuda.current_stream()
+        main = cur_stream()
         side = side_stream()
         if main == side:
             return self
         side.wait_stream(main)
-        self.ctx = torch.cuda.stream(side)
+        self.ctx = use_stream(side)
         self.ctx.__enter__()
         return self
 
@@ -298,16 +342,19 @@ def side_stream_context():
     must follow them, e.g. a gradient all-reduce), else a no-op context."""
     import contextlib
     if async_wgrad_enabled():
-        return torch.cuda.stream(side_stream())
+        return use_stream(side_stream())
     return contextlib.nullcontext()
 
 
 def join_weight_grads() -> None:
     """Make the current stream wait for every weight gradient queued on the side stream."""
-    dev = torch.cuda.current_device() if torch.cuda.is_available() else None
-    s = _SIDE.get(dev)
-    if s is not None and s != torch.cuda.current_stream():
-        torch.cuda.current_stream().wait_stream(s)
+    if not _SIDE:
+        return
+    s = _SIDE.get(_get_dev() if _get_dev is not None else torch.cuda.current_device())
+    if s is not None:
+        cur = cur_stream()
+        if s != cur:
+            cur.wait_stream(s)
 
 
 # ---------------------------------------------------------------------------------------
@@ -318,10 +365,15 @@ def join_weight_grads() -> None:
 # which adds the skip gradient).  DORKNET_BRANCH_STREAM=0 keeps everything on one stream.
 # ---------------------------------------------------------------------------------------
 _BRANCH = {}
+_CUDA_OK = []
 
 
 def branch_stream_enabled() -> bool:
-    return os.environ.get("DORKNET_BRANCH_STREAM", "1") != "0" and torch.cuda.is_available()
+    if not enabled("DORKNET_BRANCH_STREAM"):
+        return False
+    if not _CUDA_OK:
+        _CUDA_OK.append(torch.cuda.is_available())
+    return _CUDA_OK[0]
 
 
 def branch_stream():
@@ -356,7 +408,7 @@ class Branch:
         self.event = event
 
     def resolve(self):
-        cur = torch.cuda.current_stream()
+        cur = cur_stream()
         cur.wait_event(self.event)
         record_on(cur, self.value)
         return self.value
@@ -376,11 +428,11 @@ class on_branch:
         self.ctx = None
 
     def __enter__(self):
-        main = torch.cuda.current_stream()
+        main = cur_stream()
         br = branch_stream()
         br.wait_stream(main)
         record_on(br, *self.inputs)
-        self.ctx = torch.cuda.stream(br)
+        self.ctx = use_stream(br)
         self.ctx.__enter__()
         return self
 

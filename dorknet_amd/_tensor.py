@@ -46,8 +46,11 @@ def act_dtype(x) -> torch.dtype:
     return BF16 if isinstance(t, torch.Tensor) and t.dtype == BF16 else F32
 
 
+_CUDA = torch.device("cuda")  # the current device (one process drives one GPU)
+
+
 def empty_nhwc(n: int, c: int, h: int, w: int, dtype=F32) -> torch.Tensor:
-    return torch.empty((n, c, h, w), dtype=dtype, device=device(), memory_format=torch.channels_last)
+    return torch.empty((n, c, h, w), dtype=dtype, device=_CUDA, memory_format=torch.channels_last)
 
 
 def is_nhwc(x: torch.Tensor) -> bool:

@@ -15,8 +15,8 @@ from __future__ import annotations
 
 import torch
 
-from .._hip import lib, stream_handle
-from .._tensor import empty_nhwc
+from .._hip import DK_FOLDED, inlaunch_folds_enabled, lib, stream_handle
+from .._tensor import empty_nhwc, is_nhwc, to_nhwc
 
 
 class BNOut:
@@ -56,7 +56,6 @@ class BNOut:
         """Before a consumer's backward launch that writes stage 1 of this BatchNorm's backward
         into `part`: arm an in-launch fold (dorknet_amd/csrc/fold_tail.h), so that the launch
         also finalizes dgamma / dbeta / k12.  Returns a token for hand_backward_partials."""
-        from .._hip import inlaunch_folds_enabled
         if self.owner is None or not inlaunch_folds_enabled():
             return None
         return self.owner.arm_bwd_fold(part)
@@ -65,7 +64,6 @@ class BNOut:
         """A consumer's backward computed stage 1 of this BatchNorm's backward (the
         *_dgrad_ex_f32 epilogue) while producing `dx`, the gradient w.r.t. this BNOut;
         `status` / `token`: the launch's return value and arm_partials' token."""
-        from .._hip import DK_FOLDED
         folded = None
         if token is not None:
             if status == DK_FOLDED:
@@ -172,7 +170,6 @@ def dense_residual(residual, shape):
 def lattice_operand(residual, like, s):
     """`residual` as the compact stride-s lattice operand for a dgrad shaped like `like` (the
     skip projection's un-widened input gradient: [N][ceil(H/s)][ceil(W/s)][C] NHWC), or None."""
-    from .._tensor import is_nhwc
     if lattice_tag(residual) != s or s < 2:
         return None
     N, C, H, W = like.shape
@@ -201,7 +198,6 @@ def residual_operand(residual, like):
     or None when there is none or it cannot be fused."""
     if residual is None:
         return None
-    from .._tensor import is_nhwc
     r = residual
     if isinstance(r, torch.Tensor) and r.is_cuda and r.dtype == like.dtype and tuple(r.shape) == tuple(
             like.shape) and r.dim() == 4 and is_nhwc(r):
@@ -211,7 +207,6 @@ def residual_operand(residual, like):
 
 def add_residual(dx, residual):
     """dx + residual (the unfused residual join, residual_block.py:94-97)."""
-    from .._tensor import to_nhwc
     a = to_nhwc(dx)
     b = to_nhwc(dense_residual(residual, a.shape))
     if a.shape != b.shape:

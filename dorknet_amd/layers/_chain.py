@@ -17,10 +17,20 @@ the per-layer parity tests; results are bit-identical either way).
 """
 from __future__ import annotations
 
-import os
+from .._env import enabled
+from .._hip import DK_FOLDED, disarm_folds, inlaunch_folds_enabled, lib, resolve
+from ._bn_input import accepts_bn_grad, accepts_bn_input, add_residual
 
-from .._hip import disarm_folds
-from ._bn_input import accepts_bn_input
+# BatchNormLayer / ReLu (their modules import this one): bound on first use
+_BN_RELU = []
+
+
+def _bn_relu():
+    if not _BN_RELU:
+        from .activations import ReLu
+        from .batch_norm import BatchNormLayer
+        _BN_RELU.extend((BatchNormLayer, ReLu))
+    return _BN_RELU
 
 
 # Backward-progress listeners: f(layers) is called once the backward of `layers` (leaf layers of
@@ -52,12 +62,11 @@ def notify_backward_done(layers):
 
 
 def fusion_enabled() -> bool:
-    return os.environ.get("DORKNET_FUSE", "1") != "0"
+    return enabled("DORKNET_FUSE")
 
 
 def fusable_pair(layer, nxt) -> bool:
-    from .activations import ReLu
-    from .batch_norm import BatchNormLayer
+    BatchNormLayer, ReLu = _bn_relu()
     return type(layer) is BatchNormLayer and type(nxt) is ReLu
 
 
@@ -65,8 +74,7 @@ def plan_group(layers, i, fuse, out_accepts=False, keep=()):
     """How to run layers[i:]: returns (group, mode).  `out_accepts`: whether whatever consumes
     the end of the list takes a BNOut; `keep`: layer names whose output must be materialised
     (e.g. a terminal layer)."""
-    from .activations import ReLu
-    from .batch_norm import BatchNormLayer
+    BatchNormLayer, ReLu = _bn_relu()
     layer = layers[i]
     if fuse and type(layer) is BatchNormLayer:
         relu = layers[i + 1] if i + 1 < len(layers) and type(layers[i + 1]) is ReLu else None
@@ -101,13 +109,11 @@ class StatsRequest:
     def arm(self, part, P):
         """Before the producer's launch: `part` [rows, 2, C] will hold its partial sums over P
         pixels per channel."""
-        from .._hip import inlaunch_folds_enabled
         if self.bn is not None and inlaunch_folds_enabled():
             self.armed = self.bn.arm_stats_fold(part, P)
 
     def launched(self, part, status):
         """After the producer's launch (`status`: the entry point's return value)."""
-        from .._hip import DK_FOLDED, lib
         self.part, self.rows = part, part.shape[0]
         if self.armed is not None:
             if status == DK_FOLDED:
@@ -119,13 +125,12 @@ class StatsRequest:
 
 
 def run_group(group, mode, X, test_mode=False, stats_req=None, bn_stats=None):
-    from .batch_norm import BatchNormLayer
     if mode == "defer":
         return group[0].forward_deferred(X, group[1] if len(group) == 2 else None, test_mode=test_mode,
                                          stats=bn_stats)
     if mode == "pair":
         return group[0].forward_bn_relu(X, group[1], test_mode=test_mode, stats=bn_stats)
-    if bn_stats is not None and type(group[0]) is BatchNormLayer:
+    if bn_stats is not None and type(group[0]) is _bn_relu()[0]:
         return group[0].forward(X, test_mode=test_mode, stats=bn_stats)
     if stats_req is not None:
         return group[0].forward(X, test_mode=test_mode, bn_stats=stats_req)
@@ -136,7 +141,7 @@ def execute(layers, X, test_mode=False, out_accepts=False, keep=(), visit=None):
     """Run `layers` in order with the fusions above; also lets a producer hand the next
     BatchNormLayer its output statistics.  `visit(group, X)` is called after each group and
     may return True to stop early.  Returns (X, steps, stopped)."""
-    from .batch_norm import BatchNormLayer
+    BatchNormLayer = _bn_relu()[0]
     steps = []
     fuse = fusion_enabled()
     pending = None
@@ -171,7 +176,7 @@ def chain_forward(layers, X, test_mode=False, out_accepts=False):
 def _join_of(step):
     """The post-skip ReLu of a residual block step whose join can be fused into the next
     block's first dgrad (its BatchNorm-on-load join: ReLu._join_bn), else None."""
-    if len(step) != 1 or os.environ.get("DORKNET_FUSE_JOIN", "1") == "0":
+    if len(step) != 1 or not enabled("DORKNET_FUSE_JOIN"):
         return None
     act = getattr(step[0], "post_skip_activation", None)
     if act is None or getattr(act, "_join_bn", None) is None or getattr(act, "_mask", None) is None:
@@ -199,9 +204,7 @@ def chain_backward(steps, dy, residual=None, after_step=None, need_input_grad=Tr
 
 
 def _backward_steps(steps, dy, residual, after_step, need_input_grad, join):
-    from ._bn_input import accepts_bn_grad, add_residual
-    from .batch_norm import BatchNormLayer
-    from .._hip import resolve
+    BatchNormLayer = _bn_relu()[0]
     last = len(steps) - 1
     fuse = fusion_enabled()
     for i in range(last, -1, -1):
@@ -227,7 +230,7 @@ def _backward_steps(steps, dy, residual, after_step, need_input_grad, join):
               and step[0].lattice_ok() and type(steps[i - 1][0]) is BatchNormLayer and len(steps[i - 2]) == 1
               and getattr(steps[i - 2][0], "accepts_lattice_grad", False)
               and accepts_bn_grad(steps[i - 2][0], steps[i - 1][0])
-              and os.environ.get("DORKNET_LATTICE", "1") != "0"):
+              and enabled("DORKNET_LATTICE")):
             # a stride-2 pointwise layer whose input gradient goes (through a deferred BatchNorm) to a
             # consumer that takes the lattice form: the widen's zeros are never written
             dy = step[0].backward(dy, lattice_out=True)

@@ -22,7 +22,7 @@ import torch
 
 from .._hip import fold_resources, lib, stream_handle, tickets, workspace
 from .._tensor import BF16, act_dtype, as_device, empty_nhwc, rows, to_nhwc
-from ._bn_input import BNGrad
+from ._bn_input import BNGrad, BNOut, widen_lattice
 from ._common import grad_buffer
 from .layer import Layer
 
@@ -217,7 +217,6 @@ class BatchNormLayer(Layer):
     def forward_deferred(self, X, relu_layer=None, test_mode=False, stats=None):
         """Statistics only; the normalisation (and the following ReLu, if given) is applied
         by the consumer as it loads its input (layers/_bn_input.py)."""
-        from ._bn_input import BNOut
         x, mean, invstd = self._normalisation(X, test_mode, stats)
         out = BNOut(x, mean, invstd, self.learned_params["gamma"], self.learned_params["beta"],
                     relu_layer is not None, owner=self)
@@ -258,7 +257,6 @@ class BatchNormLayer(Layer):
         pending, self._pending_bwd = getattr(self, "_pending_bwd", None), None
         if lattice > 1 and not (defer and not bf and pending is not None and pending[0] is upstream_dx):
             # only a deferred hand-over keeps the lattice form: everything else takes the dense gradient
-            from ._bn_input import widen_lattice
             dy, lattice, pending = widen_lattice(dy, lattice, x.shape), 1, None
         if pending is not None and pending[0].data_ptr() == dy.data_ptr() and pending[0].shape == dy.shape:
             # stage 1 was computed by the consumer's dgrad epilogue (layers/_bn_input.py)

@@ -17,10 +17,10 @@ arithmetic (:67-68, :105-106).
 """
 from __future__ import annotations
 
-import os
 
 import torch
 
+from .._env import getenv
 from .._hip import lib, stream_handle, weight_grad_stream, workspace
 from .._tensor import as_device, empty_nhwc, ptr, to_nhwc
 from ._bn_input import BNGrad, BNOut
@@ -78,7 +78,7 @@ class ConvLayer(Layer):
     def _narrow_ok(self, X):
         """The narrow-input kernels take this input (raw NCHW, C <= 4: the stem).
         DORKNET_NARROW=0 keeps every input on the implicit-GEMM path (A/B runs)."""
-        if os.environ.get("DORKNET_NARROW", "1") == "0":
+        if getenv("DORKNET_NARROW", "1") == "0":
             return False
         if isinstance(X, BNOut) or len(getattr(X, "shape", ())) != 4 or X.shape[1] != self.filter_chans:
             return False

@@ -11,10 +11,10 @@ bias (C,), ``forward`` / ``backward`` / ``__repr__`` (:41-51).
 """
 from __future__ import annotations
 
-import os
 
 import torch
 
+from .._env import getenv
 from .._hip import HipError, lib, stream_handle, weight_grad_stream, workspace
 from .._tensor import BF16, empty_nhwc, ptr, to_nhwc
 from ._bn_input import BNGrad, BNOut, add_residual, dense_residual, lattice_operand, residual_operand
@@ -173,7 +173,7 @@ class DepthwiseConvLayer(Layer):
             nb = lib.dk_dwconv_bwd_bnbwd_workspace_bytes(N, H, W, C, R, S)
             # x IS the join's output: the kernel takes the mask as x > 0 instead of reading it
             # (DORKNET_JOIN_MASK=1 reads the stored mask)
-            from_y = getattr(join, "_join_y_ptr", None) == x.data_ptr() and os.environ.get("DORKNET_JOIN_MASK") != "1"
+            from_y = getattr(join, "_join_y_ptr", None) == x.data_ptr() and getenv("DORKNET_JOIN_MASK") != "1"
             tok = jb.arm_partials(part)
             r = lib.dk_dwconv_bwd_bnbwd_join_f32(g.data_ptr(), G.x.data_ptr(), N, H, W, C, *G.bnbwd_args(),
                                                  x.data_ptr(), w.data_ptr(), R, S, self.padding, s or 0.0,
@@ -274,7 +274,7 @@ class DepthwiseConvLayer(Layer):
         if bn is not None and R == S:
             if self.stride == 1:
                 rows = lib.dk_dwconv_dgrad_stats_rows(N, H, W, C, 1)
-            elif os.environ.get("DORKNET_DW_STRIDED_BN", "1") != "0":  # (0: the BN runs its own backward)
+            elif getenv("DORKNET_DW_STRIDED_BN", "1") != "0":  # (0: the BN runs its own backward)
                 rows = lib.dk_dwconv_dgrad_join_rows(N, H, W, C, R, S, self.stride, self.padding)
         if rows and self.padding <= R - 1 and (residual is None or res is not None):
             # + stage 1 of the input BatchNorm's backward, in the dgrad epilogue (+ the residual)

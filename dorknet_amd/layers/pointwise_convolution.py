@@ -18,10 +18,10 @@ input gradient is computed on Cp channels and returned as its first C.
 """
 from __future__ import annotations
 
-import os
 
 import torch
 
+from .._env import getenv
 from .._hip import lib, stream_handle, weight_grad_stream, workspace
 from .._tensor import BF16, empty_nhwc, ptr, to_nhwc
 from ._bn_input import BNGrad, BNOut, add_residual, residual_operand
@@ -252,7 +252,7 @@ class PointwiseConvLayer(Layer):
         OH, OW = self.out_hw
         if lib.dk_pwconv_bwd_fused_rows(N, OH, OW, self.num_filters, C) <= 0:
             return False
-        env = os.environ.get("DORKNET_PW_FUSED_BWD")
+        env = getenv("DORKNET_PW_FUSED_BWD")
         if env is not None:
             if env != "1":
                 return False

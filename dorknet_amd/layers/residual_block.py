@@ -10,8 +10,8 @@ gets the l2 term in its own backward; and SGDMomentum never updates the skip pro
 """
 from __future__ import annotations
 
-import os
 
+from .._env import getenv
 from .._hip import branch_stream_enabled, lib, on_branch, resolve, stream_handle
 from .._tensor import empty_nhwc, to_nhwc
 from ._bn_input import accepts_bn_input, materialize
@@ -133,7 +133,7 @@ class ResidualBlock(Layer):
         in its fused join dgrad (DepthwiseConvLayer.takes_lattice_residual).  DORKNET_LATTICE=0
         turns the hand-overs off."""
         skip = self.skip_projection
-        if os.environ.get("DORKNET_LATTICE") == "0" or not getattr(skip, "lattice_ok", None) or not skip.lattice_ok():
+        if getenv("DORKNET_LATTICE") == "0" or not getattr(skip, "lattice_ok", None) or not skip.lattice_ok():
             return False
         first = self._steps[0][0] if self._steps else None
         f = getattr(first, "takes_lattice_residual", None)
