@@ -346,6 +346,49 @@ def side_stream_context():
     return contextlib.nullcontext()
 
 
+class deferred_wgrad_reduce:
+    """A fused backward entry point (dk_dwconv_bwd_bnbwd_*, dk_pwconv_bwd_bnbwd_f32) whose weight-
+    gradient reduce goes to the side stream: its partial slab lives in a per-layer buffer instead of
+    the stream workspace (the main stream's next launches would overwrite that before the side
+    stream has read it), the entry point only records the reduce (dk_wgrad_reduce_defer) and
+    flush() launches it on the side stream, ordered after the entry point.  Off (the reduce stays in
+    the entry point) without side-stream weight gradients or with `defer` False.
+
+        d = deferred_wgrad_reduce(layer, nbytes, defer)
+        with d:
+            entry(..., d.ws, nbytes, stream)
+        d.flush()
+    """
+    __slots__ = ("on", "slab", "ws")
+
+    def __init__(self, layer, nbytes, defer=True):
+        self.on = bool(defer) and async_wgrad_enabled() and enabled("DORKNET_WGRAD_REDUCE_SIDE")
+        if self.on:
+            slab = layer.__dict__.get("_dk_wgrad_slab")
+            if slab is None or slab.numel() < nbytes:
+                slab = layer._dk_wgrad_slab = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device="cuda")
+            self.slab = slab
+            self.ws = slab.data_ptr()
+        else:
+            self.slab = None
+            self.ws = workspace.get(nbytes)
+
+    def __enter__(self):
+        if self.on:
+            lib.dk_wgrad_reduce_defer(1)
+        return self
+
+    def __exit__(self, exc_type, *exc):
+        if self.on:
+            lib.dk_wgrad_reduce_defer(0 if exc_type is None else -1)
+        return False
+
+    def flush(self):
+        if self.on:
+            with weight_grad_stream():
+                lib.dk_wgrad_reduce_flush(stream_handle())
+
+
 def join_weight_grads() -> None:
     """Make the current stream wait for every weight gradient queued on the side stream."""
     if not _SIDE:

@@ -1337,8 +1337,7 @@ static int dw_bwd_fused(const T* g, const T* bn_x, int N, int H, int W, int C, c
 #undef DWB_LAUNCH
   int rc = launch_status();
   if (rc) return rc;
-  return fold_status(
-      splitk_reduce(wpart, strips, 1, C * R * S, dw_crs, l2 != 0.f ? w_crs : nullptr, l2, 0, C, C, 1, 1, st), ft);
+  return fold_status(wgrad_reduce(wpart, strips, 1, C * R * S, dw_crs, l2 != 0.f ? w_crs : nullptr, l2, st), ft);
 }
 }  // namespace dk
 
@@ -1452,8 +1451,7 @@ DK_API int dk_dwconv_bwd_bnbwd_join_f32(const float* g, const float* bn_x, int N
 #undef DWJ_LAUNCH
   int rc = launch_status();
   if (rc) return rc;
-  return fold_status(
-      splitk_reduce(wpart, strips, 1, C * R * S, dw_crs, l2 != 0.f ? w_crs : nullptr, l2, 0, C, C, 1, 1, st), ft);
+  return fold_status(wgrad_reduce(wpart, strips, 1, C * R * S, dw_crs, l2 != 0.f ? w_crs : nullptr, l2, st), ft);
 }
 
 DK_API int dk_dwconv_wgrad_bnx_f32(const float* dy, const float* x, int N, int H, int W, int C, int R, int S,

@@ -199,6 +199,10 @@ int nt_stores(int fam);
 //   mode 0: out[m][n];  mode 1: columns (r, s, c) with c padded to Cp -> out KCRS.
 int splitk_reduce(const float* ws, int splits, int M, int N, float* out, const float* w, float l2, int mode, int C,
                   int Cp, int R, int S, hipStream_t st);
+// The weight-gradient reduce (mode 0) at the end of a fused backward entry point: launched on st, or,
+// while dk_wgrad_reduce_defer(1) is in effect on this host thread, recorded for dk_wgrad_reduce_flush
+// to launch on another stream (the weight-gradient side stream).
+int wgrad_reduce(const float* ws, int splits, int M, int N, float* out, const float* w, float l2, hipStream_t st);
 
 // Blocks the fused stride-1 depthwise backward aims for (depthwise.hip; knob kind 7, -1 = default).
 void dwb_blocks_set(int v);

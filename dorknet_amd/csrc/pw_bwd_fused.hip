@@ -366,7 +366,7 @@ DK_API int dk_pwconv_bwd_bnbwd_f32(const float* g, const float* bn_x, int N, int
                                  residual, x, bn_mean, bn_invstd, bn_gamma, bn_beta, bn_relu, part, bn_mean,
                                  bn_invstd, bn_gamma, bn_beta, bn_relu, wp, st, part ? &ft : nullptr);
     if (rc) return rc;
-    return fold_status(splitk_reduce(wp, nb, K, C, dw_kc, l2 != 0.f ? w_kc : nullptr, l2, 0, C, C, 1, 1, st),
+    return fold_status(wgrad_reduce(wp, nb, K, C, dw_kc, l2 != 0.f ? w_kc : nullptr, l2, st),
                        part ? ft : FoldTail{});
   }
   int tpb = 1;
@@ -395,5 +395,5 @@ DK_API int dk_pwconv_bwd_bnbwd_f32(const float* g, const float* bn_x, int N, int
 #undef PWF_LAUNCH1
   int rc = launch_status();
   if (rc) return rc;
-  return splitk_reduce(wpart, nblk, K, C, dw_kc, l2 != 0.f ? w_kc : nullptr, l2, 0, C, C, 1, 1, st);
+  return wgrad_reduce(wpart, nblk, K, C, dw_kc, l2 != 0.f ? w_kc : nullptr, l2, st);
 }

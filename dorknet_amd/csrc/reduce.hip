@@ -170,4 +170,44 @@ int splitk_reduce(const float* ws, int splits, int M, int N, float* out, const f
   return launch_status();
 }
 
+namespace {
+struct PendingReduce {
+  const float* ws;
+  int splits, M, N;
+  float* out;
+  const float* w;
+  float l2;
+  bool set;
+};
+thread_local int t_defer = 0;
+thread_local PendingReduce t_pending{};
+}  // namespace
+
+int wgrad_reduce(const float* ws, int splits, int M, int N, float* out, const float* w, float l2, hipStream_t st) {
+  if (!t_defer) return splitk_reduce(ws, splits, M, N, out, w, l2, 0, N, N, 1, 1, st);
+  if (t_pending.set) return DK_ERR_ARGS;  // the previous deferred reduce was never flushed
+  t_pending = PendingReduce{ws, splits, M, N, out, w, l2, true};
+  return 0;
+}
+
 }  // namespace dk
+
+// Deferred weight-gradient reduce.  mode 1: the fused backward entry points called next on this
+// host thread (dk_dwconv_bwd_bnbwd_f32 / _bf16 / _join_f32, dk_pwconv_bwd_bnbwd_f32) leave their
+// weight-gradient partial slab unreduced and record the reduce; mode 0: back to reducing in the
+// entry point (a recorded reduce stays for dk_wgrad_reduce_flush); mode -1: as 0 and drop it.
+DK_API int dk_wgrad_reduce_defer(int mode) {
+  if (mode < -1 || mode > 1) return dk::DK_ERR_ARGS;
+  dk::t_defer = mode == 1;
+  if (mode == -1) dk::t_pending.set = false;
+  return 0;
+}
+
+// Launch the recorded reduce on `stream` (fixed order, the same result as in the entry point).
+// The slab must stay untouched until it has run; DK_ERR_ARGS if none is recorded.
+DK_API int dk_wgrad_reduce_flush(void* stream) {
+  if (!dk::t_pending.set) return dk::DK_ERR_ARGS;
+  const dk::PendingReduce p = dk::t_pending;
+  dk::t_pending.set = false;
+  return dk::splitk_reduce(p.ws, p.splits, p.M, p.N, p.out, p.w, p.l2, 0, p.N, p.N, 1, 1, dk::as_stream(stream));
+}

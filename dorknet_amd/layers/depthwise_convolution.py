@@ -15,7 +15,7 @@ from __future__ import annotations
 import torch
 
 from .._env import getenv
-from .._hip import HipError, lib, stream_handle, weight_grad_stream, workspace
+from .._hip import HipError, deferred_wgrad_reduce, lib, stream_handle, weight_grad_stream, workspace
 from .._tensor import BF16, empty_nhwc, ptr, to_nhwc
 from ._bn_input import BNGrad, BNOut, add_residual, dense_residual, lattice_operand, residual_operand
 from ._common import add_regulariser_grad, grad_buffer, init_weights, l2_strength
@@ -175,12 +175,17 @@ class DepthwiseConvLayer(Layer):
             # (DORKNET_JOIN_MASK=1 reads the stored mask)
             from_y = getattr(join, "_join_y_ptr", None) == x.data_ptr() and getenv("DORKNET_JOIN_MASK") != "1"
             tok = jb.arm_partials(part)
-            r = lib.dk_dwconv_bwd_bnbwd_join_f32(g.data_ptr(), G.x.data_ptr(), N, H, W, C, *G.bnbwd_args(),
-                                                 x.data_ptr(), w.data_ptr(), R, S, self.padding, s or 0.0,
-                                                 gw.data_ptr(), dx.data_ptr(), ptr(res),
-                                                 0 if from_y else join._mask.data_ptr(),
-                                                 jb.x.data_ptr(), jb.mean.data_ptr(), jb.invstd.data_ptr(),
-                                                 part.data_ptr(), workspace.get(nb), nb, st)
+            # the weight-gradient reduce on the side stream (not with a non-l2 regulariser, whose
+            # term is added to gw on this stream right after)
+            red = deferred_wgrad_reduce(self, nb, s is not None)
+            with red:
+                r = lib.dk_dwconv_bwd_bnbwd_join_f32(g.data_ptr(), G.x.data_ptr(), N, H, W, C, *G.bnbwd_args(),
+                                                     x.data_ptr(), w.data_ptr(), R, S, self.padding, s or 0.0,
+                                                     gw.data_ptr(), dx.data_ptr(), ptr(res),
+                                                     0 if from_y else join._mask.data_ptr(),
+                                                     jb.x.data_ptr(), jb.mean.data_ptr(), jb.invstd.data_ptr(),
+                                                     part.data_ptr(), red.ws, nb, st)
+            red.flush()
             if s is None:
                 add_regulariser_grad(gw, w, self.weight_regulariser)
             jb.hand_backward_partials(dx, part, r, tok)
@@ -197,10 +202,13 @@ class DepthwiseConvLayer(Layer):
         nb = lib.dk_dwconv_bwd_bnbwd_workspace_bytes(N, H, W, C, R, S)
         bf = x.dtype == BF16
         tok = bn.arm_partials(part) if part is not None else None
-        r = (lib.dk_dwconv_bwd_bnbwd_bf16 if bf else lib.dk_dwconv_bwd_bnbwd_f32)(
-            g.data_ptr(), G.x.data_ptr(), N, H, W, C, *G.bnbwd_args(), x.data_ptr(), w.data_ptr(), R, S,
-            self.padding, s or 0.0, gw.data_ptr(), ptr(dx), ptr(res),
-            *(bn.bn_args() if bn is not None else (0, 0, 0, 0, 0)), ptr(part), workspace.get(nb), nb, st)
+        red = deferred_wgrad_reduce(self, nb, s is not None)
+        with red:
+            r = (lib.dk_dwconv_bwd_bnbwd_bf16 if bf else lib.dk_dwconv_bwd_bnbwd_f32)(
+                g.data_ptr(), G.x.data_ptr(), N, H, W, C, *G.bnbwd_args(), x.data_ptr(), w.data_ptr(), R, S,
+                self.padding, s or 0.0, gw.data_ptr(), ptr(dx), ptr(res),
+                *(bn.bn_args() if bn is not None else (0, 0, 0, 0, 0)), ptr(part), red.ws, nb, st)
+        red.flush()
         if s is None:
             add_regulariser_grad(gw, w, self.weight_regulariser)
         if not need_dx:

@@ -22,7 +22,7 @@ from __future__ import annotations
 import torch
 
 from .._env import getenv
-from .._hip import lib, stream_handle, weight_grad_stream, workspace
+from .._hip import deferred_wgrad_reduce, lib, stream_handle, weight_grad_stream, workspace
 from .._tensor import BF16, empty_nhwc, ptr, to_nhwc
 from ._bn_input import BNGrad, BNOut, add_residual, residual_operand
 from ._common import add_regulariser_grad, grad_buffer, init_weights, l2_strength
@@ -280,16 +280,23 @@ class PointwiseConvLayer(Layer):
         l2s = l2_strength(self.weight_regulariser)
         nb = lib.dk_pwconv_bwd_fused_workspace_bytes(N, OH, OW, K, C)
         tok = bn.arm_partials(part) if bn is not None else None
-        r = lib.dk_pwconv_bwd_bnbwd_f32(g.data_ptr(), bg.x.data_ptr(), N, OH, OW, K, *bg.bnbwd_args(), w.data_ptr(),
-                                        C, l2s or 0.0, gw.data_ptr(), dx.data_ptr(), ptr(res), x.data_ptr(),
-                                        *((*bn.bn_args(), part.data_ptr()) if bn is not None else (0, 0, 0, 0, 0, 0)),
-                                        workspace.get(nb), nb, st)
+        # the weight-gradient reduce on the side stream (not with a non-l2 regulariser, whose term
+        # is added to gw on this stream right after)
+        red = deferred_wgrad_reduce(self, nb, l2s is not None)
+        with red:
+            r = lib.dk_pwconv_bwd_bnbwd_f32(g.data_ptr(), bg.x.data_ptr(), N, OH, OW, K, *bg.bnbwd_args(),
+                                            w.data_ptr(), C, l2s or 0.0, gw.data_ptr(), dx.data_ptr(), ptr(res),
+                                            x.data_ptr(),
+                                            *((*bn.bn_args(), part.data_ptr()) if bn is not None else (0,) * 6),
+                                            red.ws, nb, st)
+        red.flush()
         if l2s is None:
             add_regulariser_grad(gw, w, self.weight_regulariser)
-        # the weight gradient was written on this stream: work queued on the side stream from
-        # here on (a data-parallel bucket's all-reduce) must follow it
-        with weight_grad_stream():
-            pass
+        if not red.on:
+            # the weight gradient was written on this stream: work queued on the side stream from
+            # here on (a data-parallel bucket's all-reduce) must follow it
+            with weight_grad_stream():
+                pass
         if bn is not None:
             bn.hand_backward_partials(dx, part, r, tok)
         return dx

@@ -351,6 +351,15 @@ int dk_bn_bwd_from_partials_f32(const void* part, int nblk, int C, double count,
 int dk_bn_fold_arm_stats(const void* part, int nrows, int C, double count, float eps, float momentum, int first, float* mean, float* std_, float* invstd, float* run_mean, float* run_std, unsigned* tickets, int ntickets, void* scratch, size_t scratch_bytes);
 int dk_bn_fold_arm_bwd(const void* part, int nrows, int C, double count, float* dgamma, float* dbeta, float* k12, unsigned* tickets, int ntickets, void* scratch, size_t scratch_bytes);
 int dk_bn_fold_disarm(void);
+/* Deferred weight-gradient reduce.  dk_wgrad_reduce_defer(1): the fused backward entry points
+ * called next on this host thread (dk_dwconv_bwd_bnbwd_f32 / _bf16, dk_dwconv_bwd_bnbwd_join_f32,
+ * dk_pwconv_bwd_bnbwd_f32) leave the weight-gradient partial slab in their workspace and record its
+ * fixed-order reduce instead of launching it; dk_wgrad_reduce_flush(stream) launches it on `stream`
+ * (the caller orders that stream after the entry point's and keeps the workspace untouched until
+ * the reduce has run).  (0): reduce in the entry point again; (-1): as 0, dropping a recorded
+ * reduce.  One recorded reduce per host thread (a second one is DK_ERR_ARGS until flushed). */
+int dk_wgrad_reduce_defer(int mode);
+int dk_wgrad_reduce_flush(void* stream);
 size_t dk_bn_fold_scratch_bytes(int nrows, int C);
 int dk_bn_fold_tickets_needed_count(int nrows, int nslices);
 int dk_relu_bwd_bn_partial_f64(const float* dy, const uint8_t* mask, const float* x, int P, int C, const float* mean, const float* invstd, const float* gamma, const float* beta, int relu, float* dx, void* part, size_t part_bytes, void* stream);

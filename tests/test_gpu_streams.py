@@ -61,6 +61,38 @@ def test_branch_stream_bitwise(monkeypatch):
             assert torch.equal(a, b)
 
 
+def test_wgrad_reduce_side_stream_bitwise(monkeypatch):
+    """The fused backward entry points' weight-gradient reduces deferred to the side stream
+    (dk_wgrad_reduce_defer / _flush, DORKNET_WGRAD_REDUCE_SIDE=1, the default) give the same
+    gradients bit for bit as reducing in the entry point, with the branch stream on and off."""
+    from examples.resnet18_depsep import ResNet18, synthetic_batch
+    X, _, onehot = synthetic_batch(16, seed=13)
+    np.random.seed(14)
+    net = ResNet18("r18")
+    net.to_gpu()
+    runs = []
+    for side, branch in (("1", "1"), ("0", "1"), ("1", "0"), ("0", "0"), ("1", "1")):
+        monkeypatch.setenv("DORKNET_WGRAD_REDUCE_SIDE", side)
+        monkeypatch.setenv("DORKNET_BRANCH_STREAM", branch)
+        runs.append(_step(net, X, onehot))
+    torch.cuda.synchronize()
+    for other in runs[1:]:
+        for a, b in zip(runs[0], other):
+            assert torch.equal(a, b)
+
+
+def test_wgrad_reduce_defer_protocol():
+    """A second deferred reduce before a flush is refused, a flush with none recorded is refused,
+    and mode -1 drops a recorded one."""
+    from dorknet_amd._hip import HipError, lib
+    lib.dk_wgrad_reduce_defer(-1)
+    with pytest.raises(HipError):
+        lib.dk_wgrad_reduce_flush(0)
+    with pytest.raises(HipError):
+        lib.dk_wgrad_reduce_defer(2)
+    lib.dk_wgrad_reduce_defer(0)
+
+
 def test_data_parallel_rccl_world1():
     import torch.distributed as dist
     from dorknet_amd.parallel import DataParallel
