@@ -115,5 +115,14 @@ def test_data_parallel_rccl_world1():
             assert torch.equal(a, b)
         assert all(l.grads[k].data_ptr() >= dp.flat.data_ptr() for l in all_layers(net.layers)
                    for k in (l.grads or {}))
+        # bucket launches against layer order: every bucket once, in bucket order (the buckets
+        # cover the layers in reverse, the order the backward finishes them), and issued while the
+        # backward still runs -- not all after it (sub-layer readiness inside residual blocks)
+        order = [b for b, _ in dp.launch_log]
+        reported = [n for _, n in dp.launch_log]
+        assert sorted(order) == list(range(len(dp.buckets)))
+        assert order == sorted(order)
+        assert reported == sorted(reported)
+        assert len(dp.buckets) > 2 and reported[0] < reported[-1]
     finally:
         dist.destroy_process_group()
