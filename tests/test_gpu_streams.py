@@ -81,6 +81,21 @@ def test_wgrad_reduce_side_stream_bitwise(monkeypatch):
             assert torch.equal(a, b)
 
 
+def test_stream_helpers_match_torch():
+    """_hip.cur_stream / use_stream (torch's C layer directly) agree with torch.cuda.current_stream /
+    torch.cuda.stream: the stream is switched inside the block and restored after it, nested too."""
+    from dorknet_amd._hip import cur_stream, stream_handle, use_stream
+    main = torch.cuda.current_stream()
+    assert cur_stream() == main
+    a, b = torch.cuda.Stream(), torch.cuda.Stream()
+    with use_stream(a):
+        assert torch.cuda.current_stream() == a and cur_stream() == a and stream_handle() == a.cuda_stream
+        with use_stream(b):
+            assert torch.cuda.current_stream() == b
+        assert torch.cuda.current_stream() == a
+    assert torch.cuda.current_stream() == main and stream_handle() == main.cuda_stream
+
+
 def test_wgrad_reduce_defer_protocol():
     """A second deferred reduce before a flush is refused, a flush with none recorded is refused,
     and mode -1 drops a recorded one."""

@@ -193,3 +193,18 @@ def test_bn_fusion_plan_keeps_terminal_output():
     assert mode == "pair"
     group, mode = plan_group(net.layers, 1, False)
     assert mode == "single"
+
+
+def test_env_switches_follow_runtime_changes(monkeypatch):
+    """dorknet_amd._env.getenv reads os.environ's backing dict: a switch set, changed or removed at
+    run time (as the tests' monkeypatch does) is seen on the next call, like os.environ.get."""
+    from dorknet_amd._env import enabled, getenv
+    monkeypatch.delenv("DORKNET_TEST_SWITCH", raising=False)
+    assert getenv("DORKNET_TEST_SWITCH") is None and getenv("DORKNET_TEST_SWITCH", "d") == "d"
+    assert enabled("DORKNET_TEST_SWITCH")
+    monkeypatch.setenv("DORKNET_TEST_SWITCH", "0")
+    assert getenv("DORKNET_TEST_SWITCH") == "0" and not enabled("DORKNET_TEST_SWITCH")
+    monkeypatch.setenv("DORKNET_TEST_SWITCH", "1")
+    assert enabled("DORKNET_TEST_SWITCH")
+    monkeypatch.delenv("DORKNET_TEST_SWITCH")
+    assert getenv("DORKNET_TEST_SWITCH") is None
