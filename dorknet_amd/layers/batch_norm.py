@@ -86,11 +86,23 @@ class BatchNormLayer(Layer):
         import torch.distributed as dist
         return dist.get_world_size(self.sync_group)
 
+    def _persist(self, key, n, dev):
+        """A per-layer fp32 device buffer reused every step: the batch statistics and the backward
+        coefficients are rewritten by each forward / backward and read only within that step (every
+        reader on another stream is joined into the main stream before the step ends), so a fresh
+        allocation per call (~4 per layer and step) buys nothing but host time."""
+        b = self.__dict__.get(key)
+        if b is None or b.numel() != n or b.device != dev:
+            b = torch.empty(n, dtype=torch.float32, device=dev)
+            self.__dict__[key] = b
+        return b
+
     def _stats_outputs(self, C, dev):
-        """Fresh mean / std / invstd and the running statistics (allocated on the first batch)."""
-        mean = torch.empty(C, dtype=torch.float32, device=dev)
-        std = torch.empty(C, dtype=torch.float32, device=dev)
-        invstd = torch.empty(C, dtype=torch.float32, device=dev)
+        """mean / std / invstd (this layer's per-step buffers) and the running statistics (allocated
+        on the first batch)."""
+        mean = self._persist("_dk_mean", C, dev)
+        std = self._persist("_dk_std", C, dev)
+        invstd = self._persist("_dk_invstd", C, dev)
         nlp = self.non_learned_params
         # _first_pending: an armed in-launch fold allocated the running statistics but did not run
         first = nlp["running_mean"] is None or getattr(self, "_first_pending", False)
@@ -130,7 +142,7 @@ class BatchNormLayer(Layer):
         gamma, beta = self.learned_params["gamma"], self.learned_params["beta"]
         dgamma = grad_buffer(self, "gamma", gamma.shape)
         dbeta = grad_buffer(self, "beta", beta.shape)
-        k12 = torch.empty(2 * C, dtype=torch.float32, device=x.device)
+        k12 = self._persist("_dk_k12", 2 * C, x.device)
         t, nt, sc, nsc = fold_resources.get()
         lib.dk_bn_fold_arm_bwd(part.data_ptr(), part.shape[0], C, float(P), dgamma.data_ptr(), dbeta.data_ptr(),
                                k12.data_ptr(), t, nt, sc, nsc)
@@ -268,13 +280,13 @@ class BatchNormLayer(Layer):
             if k12 is not None:
                 pass  # folded (and dgamma / dbeta written) inside the consumer's launch
             elif self.sync_group is None:
-                k12 = torch.empty(2 * C, dtype=torch.float32, device=x.device)
+                k12 = self._persist("_dk_k12", 2 * C, x.device)
                 lib.dk_bn_bwd_from_partials_f32(part.data_ptr(), nrows, C, float(P), dgamma.data_ptr(),
                                                 dbeta.data_ptr(), k12.data_ptr(), ws, nb,
                                                 tickets.get(lib.dk_bn_fold_tickets_count(C)), st)
             else:
                 import torch.distributed as dist
-                k12 = torch.empty(2 * C, dtype=torch.float32, device=x.device)
+                k12 = self._persist("_dk_k12", 2 * C, x.device)
                 local = torch.empty(2 * C, dtype=torch.float64, device=x.device)
                 lib.dk_bn_reduce_partials_f64(part.data_ptr(), nrows, C, local.data_ptr(), ws, nb, st)
                 glob = local.clone()
@@ -305,7 +317,7 @@ class BatchNormLayer(Layer):
             lib.dk_bn_collapse_f64(ws, nblk, C, local.data_ptr(), st)
             lib.dk_bn_collapse_f64(ws, nblk, C, glob.data_ptr(), st)
             dist.all_reduce(glob, group=self.sync_group)
-            k12 = torch.empty(2 * C, dtype=torch.float32, device=x.device)
+            k12 = self._persist("_dk_k12", 2 * C, x.device)
             lib.dk_bn_bwd_finalize_f32(local.data_ptr(), 1, glob.data_ptr(), 1, C, float(P) * self._world(),
                                        dgamma.data_ptr(), dbeta.data_ptr(), k12.data_ptr(), st)
             if defer and not bf:
