@@ -124,6 +124,29 @@ class Instrument:
         return out
 
 
+class single_stream:
+    """Everything on the launch stream for the per-entry attribution step: weight gradients not
+    on the side stream (DORKNET_ASYNC_WGRAD=0) and skip projections not on the branch stream
+    (DORKNET_BRANCH_STREAM=0).  Otherwise an entry's events would also time the other streams'
+    kernels running beside it (the skip projections' entries read 0.15 of their
+    bound while they overlapped the chain)."""
+    KEYS = ("DORKNET_ASYNC_WGRAD", "DORKNET_BRANCH_STREAM")
+
+    def __enter__(self):
+        self.prev = {k: os.environ.get(k) for k in self.KEYS}
+        for k in self.KEYS:
+            os.environ[k] = "0"
+        return self
+
+    def __exit__(self, *exc):
+        for k, v in self.prev.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+        return False
+
+
 def shape_bounds(name, s):
     """Each distinct call shape of an entry with its own bound (HBM or MFMA) and its fraction of
     that bound, largest time first."""
@@ -456,16 +479,9 @@ def other_config(args):
     breakdown, dominant = None, None
     if not args.no_roofline:
         # per-entry attribution on one single-stream step, as for config 3
-        prev = os.environ.get("DORKNET_ASYNC_WGRAD")
-        os.environ["DORKNET_ASYNC_WGRAD"] = "0"
-        try:
+        with single_stream():
             with Instrument(perfmodel.MODEL.keys()) as ins:
                 step()
-        finally:
-            if prev is None:
-                os.environ.pop("DORKNET_ASYNC_WGRAD")
-            else:
-                os.environ["DORKNET_ASYNC_WGRAD"] = prev
         summ = ins.summary()
         dominant = max(summ, key=lambda n: summ[n]["ms"])
         breakdown = {n: {"ms": round(v["ms"], 3), "calls": v["calls"],
@@ -590,18 +606,11 @@ def main():
 
     breakdown, dominant = None, None
     if not args.no_roofline:
-        # the per-entry attribution step runs single-stream (weight gradients not on the side
-        # stream), so each entry's events bracket only its own kernels
-        prev = os.environ.get("DORKNET_ASYNC_WGRAD")
-        os.environ["DORKNET_ASYNC_WGRAD"] = "0"
-        try:
+        # the per-entry attribution step runs single-stream, so each entry's events bracket only
+        # its own kernels
+        with single_stream():
             with Instrument(perfmodel.MODEL.keys()) as ins:
                 step()
-        finally:
-            if prev is None:
-                os.environ.pop("DORKNET_ASYNC_WGRAD")
-            else:
-                os.environ["DORKNET_ASYNC_WGRAD"] = prev
         summ = ins.summary()
         dominant = max(summ, key=lambda n: summ[n]["ms"])
         tot = sum(s["ms"] for s in summ.values())

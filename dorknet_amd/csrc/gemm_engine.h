@@ -31,6 +31,7 @@
 #pragma once
 #include <stdlib.h>
 
+#include <mutex>
 #include <type_traits>
 
 #include "dk_common.h"
@@ -1107,6 +1108,48 @@ static inline auto set_nt(E& e, int) -> decltype(e.nt = 0, void()) {
 template <class E>
 static inline void set_nt(E&, long) {}
 
+// Launch facts of one kernel instantiation, by dynamic LDS size: its static LDS (queried once),
+// the largest dynamic size set on it so far (hipFuncSetAttribute only when a launch needs more),
+// and resident blocks per CU for each distinct dynamic size it has been launched with (the
+// BN-on-load tables make the dynamic LDS a function of the layer's channel count, and with it the
+// occupancy that sizes split-K grids).  Thread-safe: one mutex per instantiation; the table is
+// small (one entry per distinct channel count) and a full table falls back to querying.
+struct LaunchFacts {
+  std::mutex mu;
+  bool init = false;
+  size_t lds_static = 0, dyn_set = 0;
+  static constexpr int kMax = 16;
+  int n = 0;
+  size_t dyn[kMax];
+  int occ[kMax];
+};
+
+// Resident blocks per CU of `fn` at `dyn` bytes of dynamic LDS, or -1 when static + dynamic LDS
+// exceeds the CU's 160 KB (the runtime would abort the queue on such a launch).
+static int launch_occupancy(LaunchFacts& f, const void* fn, int nt, size_t dyn) {
+  std::lock_guard<std::mutex> lock(f.mu);
+  if (!f.init) {
+    hipFuncAttributes fa{};
+    if (hipFuncGetAttributes(&fa, fn) == hipSuccess) f.lds_static = fa.sharedSizeBytes;
+    f.init = true;
+  }
+  if (f.lds_static + dyn > (size_t)160 * 1024) return -1;
+  if (dyn > f.dyn_set) {
+    (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn);
+    f.dyn_set = dyn;
+  }
+  for (int i = 0; i < f.n; ++i)
+    if (f.dyn[i] == dyn) return f.occ[i];
+  int o = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, fn, nt, dyn) != hipSuccess || o < 1) o = 1;
+  if (f.n < LaunchFacts::kMax) {
+    f.dyn[f.n] = dyn;
+    f.occ[f.n] = o;
+    ++f.n;
+  }
+  return o;
+}
+
 template <int BM, int BN, int BK, int WM, int WN, template <int, int, int> class LA, class DA,
           template <int, int, int> class LB, class DB, class EP, int MF = kMfF32>
 static int launch_igemm(const DA& da, const DB& db, const EP& ep, int M, int N, int Ktot, int splits,
@@ -1120,30 +1163,12 @@ static int launch_igemm(const DA& da, const DB& db, const EP& ep, int M, int N, 
   if (splits < 1) splits = 1;
   if (splits > KT) splits = KT > 0 ? KT : 1;
   size_t dyn = 0;
-  if constexpr (DA::kBnIn && A::kTable) {
-    dyn = (size_t)da.C * sizeof(f32x4);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&igemm_f32<BM, BN, BK, WM, WN, A, DA, B, DB, EP, MF>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn);
-  }
-  if constexpr (DA::kBnBwd) {
-    dyn = (size_t)da.bwd.C * 2 * sizeof(f32x4);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&igemm_f32<BM, BN, BK, WM, WN, A, DA, B, DB, EP, MF>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn);
-  }
-  // resident blocks per CU of this instantiation (queried once; immutable afterwards), and its
-  // static LDS: a launch whose static + dynamic LDS exceeds the CU's 160 KB is refused here (the
-  // runtime would abort the queue)
-  static int occ = -1;
-  static size_t lds_static = 0;
-  if (occ < 0) {
-    const void* fn = reinterpret_cast<const void*>(&igemm_f32<BM, BN, BK, WM, WN, A, DA, B, DB, EP, MF>);
-    hipFuncAttributes fa{};
-    if (hipFuncGetAttributes(&fa, fn) == hipSuccess) lds_static = fa.sharedSizeBytes;
-    int o = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, fn, NT, dyn) != hipSuccess || o < 1) o = 1;
-    occ = o;
-  }
-  if (lds_static + dyn > (size_t)160 * 1024) return DK_ERR_ARGS;
+  if constexpr (DA::kBnIn && A::kTable) dyn = (size_t)da.C * sizeof(f32x4);
+  if constexpr (DA::kBnBwd) dyn = (size_t)da.bwd.C * 2 * sizeof(f32x4);
+  static LaunchFacts facts;
+  const int occ = launch_occupancy(facts, reinterpret_cast<const void*>(&igemm_f32<BM, BN, BK, WM, WN, A, DA, B, DB, EP, MF>),
+                                   NT, dyn);
+  if (occ < 0) return DK_ERR_ARGS;
   const int slots = occ * kNumCUs;
   if (g_fill_splits && splits_used && splits > 1 && tiles * splits > slots && tiles <= slots) {
     // split-K: no second, partly filled round of blocks (the stem's 64x128 weight-gradient

@@ -28,6 +28,8 @@
 // 28x28 depthwise-separable units of ResNet-18-depsep, whose separate kernels are HBM-bound.
 #include <stdlib.h>
 
+#include <atomic>
+
 #include "dk_common.h"
 #include "fold_tail.h"
 
@@ -292,9 +294,11 @@ static bool pwf_supported(int K, int C) { return (K == 64 || K == 128) && (C == 
 // Blocks (= partial rows): one round of resident blocks, each taking a contiguous run of
 // 64-pixel tiles.  Resident blocks per CU come from the occupancy of the K, C instantiation.
 static int pwf_blocks(long long P, int K, int C, int* tpb_out) {
-  static int occ[2][2][2] = {{{-1, -1}, {-1, -1}}, {{-1, -1}, {-1, -1}}};
+  // (atomic: concurrent first calls may both query, and store the same value)
+  static std::atomic<int> occ[8] = {-1, -1, -1, -1, -1, -1, -1, -1};
   const bool pf = pwf_prefetch(K, C);
-  int& o = occ[K == 128][C == 128][pf];
+  std::atomic<int>& oc = occ[4 * (K == 128) + 2 * (C == 128) + pf];
+  int o = oc.load(std::memory_order_relaxed);
   if (o < 0) {
     const void* f = K == 64 ? (C == 64 ? pwf_kernel<64, 64, true>(pf) : pwf_kernel<64, 128, true>(pf))
                             : (C == 64 ? pwf_kernel<128, 64, true>(pf) : pwf_kernel<128, 128, true>(pf));
@@ -303,6 +307,7 @@ static int pwf_blocks(long long P, int K, int C, int* tpb_out) {
     const char* s = getenv("DORKNET_PWF_BLOCKS_PER_CU");  // tuning knob
     if (s && atoi(s) > 0) v = atoi(s);
     o = v;
+    oc.store(v, std::memory_order_relaxed);
   }
   const long long ntiles = (P + 63) / 64;
   long long nblk = (long long)o * 256;

@@ -522,21 +522,21 @@ static int grid_blocks(int M, int occ) {
 }
 
 int dgrad_blocks(int M) {
-  static int occ = -1;
-  if (occ < 0) {
+  // thread-safe one-time query (a function-local static initialised once)
+  static const int occ = [] {
     const void* fs[] = {reinterpret_cast<const void*>(&dgrad_bnbwd_kernel<false, false>),
                         reinterpret_cast<const void*>(&dgrad_bnbwd_kernel<false, true>),
                         reinterpret_cast<const void*>(&dgrad_bnbwd_kernel<true, false>),
                         reinterpret_cast<const void*>(&dgrad_bnbwd_kernel<true, true>)};
-    occ = min_occupancy(fs, 4);
-  }
+    return min_occupancy(fs, 4);
+  }();
   return grid_blocks(M, occ);
 }
 
 template <int KR_>
 static int fwd_occ() {
-  static int occ = -1;
-  if (occ < 0) {
+  // thread-safe one-time query (a function-local static initialised once)
+  static const int occ = [] {
     const void* fs[] = {reinterpret_cast<const void*>(&fwd_kernel<KR_, KR_, true, true, true>),
                         reinterpret_cast<const void*>(&fwd_kernel<KR_, KR_, true, true, false>),
                         reinterpret_cast<const void*>(&fwd_kernel<KR_, KR_, true, false, true>),
@@ -545,8 +545,8 @@ static int fwd_occ() {
                         reinterpret_cast<const void*>(&fwd_kernel<KR_, KR_, false, true, false>),
                         reinterpret_cast<const void*>(&fwd_kernel<KR_, KR_, false, false, true>),
                         reinterpret_cast<const void*>(&fwd_kernel<KR_, KR_, false, false, false>)};
-    occ = min_occupancy(fs, 8);
-  }
+    return min_occupancy(fs, 8);
+  }();
   return occ;
 }
 
@@ -842,13 +842,13 @@ static bool bwd_pf() {
 
 template <bool PF>
 static int bwd_fused_occ() {
-  static int occ = -1;
-  if (occ < 0) {
+  // thread-safe one-time query (a function-local static initialised once)
+  static const int occ = [] {
     const void* fs[] = {reinterpret_cast<const void*>(&bwd_fused_kernel<false, true, true, PF>),
                         reinterpret_cast<const void*>(&bwd_fused_kernel<false, false, true, PF>),
                         reinterpret_cast<const void*>(&bwd_fused_kernel<false, false, false, PF>)};
-    occ = min_occupancy(fs, 3);
-  }
+    return min_occupancy(fs, 3);
+  }();
   return occ;
 }
 

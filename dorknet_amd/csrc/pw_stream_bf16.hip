@@ -791,26 +791,26 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void dgrad_deep_kernel(De
 
 template <int KR, int NO>
 static int fwd_occ() {
-  static int occ = -1;
-  if (occ < 0) {
+  // thread-safe one-time query (a function-local static initialised once)
+  static const int occ = [] {
     const void* fs[] = {reinterpret_cast<const void*>(&fwd_kernel<KR, NO, true, true>),
                         reinterpret_cast<const void*>(&fwd_kernel<KR, NO, true, false>),
                         reinterpret_cast<const void*>(&fwd_kernel<KR, NO, false, true>),
                         reinterpret_cast<const void*>(&fwd_kernel<KR, NO, false, false>)};
-    occ = min_occupancy(fs, 4);
-  }
+    return min_occupancy(fs, 4);
+  }();
   return occ;
 }
 template <int KR, int NO>
 static int dgrad_occ() {
-  static int occ = -1;
-  if (occ < 0) {
+  // thread-safe one-time query (a function-local static initialised once)
+  static const int occ = [] {
     const void* fs[] = {reinterpret_cast<const void*>(&dgrad_bnbwd_kernel<KR, NO, true, true>),
                         reinterpret_cast<const void*>(&dgrad_bnbwd_kernel<KR, NO, true, false>),
                         reinterpret_cast<const void*>(&dgrad_bnbwd_kernel<KR, NO, false, true>),
                         reinterpret_cast<const void*>(&dgrad_bnbwd_kernel<KR, NO, false, false>)};
-    occ = min_occupancy(fs, 4);
-  }
+    return min_occupancy(fs, 4);
+  }();
   return occ;
 }
 
@@ -829,28 +829,28 @@ static bool deep_shape(int KR, int N) {
 }
 template <int KR>
 static int fwd_deep_occ() {
-  static int occ = -1;
-  if (occ < 0) {
+  // thread-safe one-time query (a function-local static initialised once)
+  static const int occ = [] {
     constexpr int NW = deep_nw<KR>();
     const void* fs[] = {reinterpret_cast<const void*>(&fwd_deep_kernel<KR, NW, kFwdCK, true, true>),
                         reinterpret_cast<const void*>(&fwd_deep_kernel<KR, NW, kFwdCK, true, false>),
                         reinterpret_cast<const void*>(&fwd_deep_kernel<KR, NW, kFwdCK, false, true>),
                         reinterpret_cast<const void*>(&fwd_deep_kernel<KR, NW, kFwdCK, false, false>)};
-    occ = min_occupancy(fs, 4, 64 * NW);
-  }
+    return min_occupancy(fs, 4, 64 * NW);
+  }();
   return occ;
 }
 template <int KR>
 static int dgrad_deep_occ() {
-  static int occ = -1;
-  if (occ < 0) {
+  // thread-safe one-time query (a function-local static initialised once)
+  static const int occ = [] {
     constexpr int NW = deep_nw<KR>();
     const void* fs[] = {reinterpret_cast<const void*>(&dgrad_deep_kernel<KR, NW, kDgradCK, true, true>),
                         reinterpret_cast<const void*>(&dgrad_deep_kernel<KR, NW, kDgradCK, true, false>),
                         reinterpret_cast<const void*>(&dgrad_deep_kernel<KR, NW, kDgradCK, false, true>),
                         reinterpret_cast<const void*>(&dgrad_deep_kernel<KR, NW, kDgradCK, false, false>)};
-    occ = min_occupancy(fs, 4, 64 * NW);
-  }
+    return min_occupancy(fs, 4, 64 * NW);
+  }();
   return occ;
 }
 // Row walkers per slice: the slices share the resident slots; when the tiles need more than one

@@ -23,8 +23,10 @@ all-reduce per step on ResNet-18-depsep.  Pass True together with the optimiser'
 
 Stream ordering: weight gradients are written on two streams (the main stream -- BatchNorm
 dgamma/dbeta, dense, the fused depthwise backward, the stem -- and the weight-gradient side
-stream).  A bucket's all-reduce is issued from the side stream after making it wait for the
-main stream, so RCCL reads the bucket only once every kernel issued so far on either stream
+stream), and a downsampling block's skip projection runs its backward on the branch stream
+(with side-stream weight gradients off, its weight gradient is written there).  A bucket's
+all-reduce is issued from the side stream after making it wait for the main stream and the
+branch stream, so RCCL reads the bucket only once every kernel issued so far on any of them
 has written it.
 """
 from __future__ import annotations
@@ -32,7 +34,7 @@ from __future__ import annotations
 import torch
 import torch.distributed as dist
 
-from ._hip import async_weight_grads, side_stream_context
+from ._hip import async_weight_grads, branch_stream, branch_stream_enabled, side_stream_context
 from .layers._chain import backward_progress, chain_backward
 
 
@@ -147,6 +149,11 @@ class DataParallel:
                 cur = torch.cuda.current_stream()
                 if cur != main:
                     cur.wait_stream(main)
+                if branch_stream_enabled():
+                    # a skip projection's backward runs on the branch stream; without side-stream
+                    # weight gradients its weight gradient is written there too
+                    # (residual_block.py), so the collective also follows the branch stream
+                    cur.wait_stream(branch_stream())
                 work = dist.all_reduce(view, op=op, group=self.group, async_op=True)
         else:
             work = dist.all_reduce(view, op=op, group=self.group, async_op=True)

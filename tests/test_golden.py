@@ -9,6 +9,7 @@ import os
 import numpy as np
 import pytest
 
+from tests._convert import slack_bound
 from tests.golden import make_golden
 
 HERE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
@@ -118,5 +119,5 @@ def test_hip_matches_fixture(path):
         want32 = fx[k + "_f32"].astype(np.float64)
         assert v.shape == want.shape, k
         err = np.linalg.norm((v.astype(np.float64) - want).ravel())
-        bound = max(1e-4 * np.linalg.norm(want.ravel()), 10 * np.linalg.norm((want32 - want).ravel()))
+        bound = slack_bound(want, want32, 1e-4)  # max(1e-4 ||want||, FP32_SLACK ||want32 - want||)
         assert err <= bound or err == 0, (os.path.basename(path), k, err, bound)

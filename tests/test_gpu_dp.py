@@ -128,6 +128,55 @@ def test_bucket_allreduce_waits_for_main_stream(monkeypatch):
         dist.destroy_process_group()
 
 
+def test_bucket_allreduce_waits_for_branch_stream(monkeypatch):
+    """with side-stream weight gradients off (DORKNET_ASYNC_WGRAD=0), the skip
+    projections' backward -- weight gradient included -- runs on the branch stream
+    (residual_block.py), and update_skip_projections=True puts those gradients in the buckets.
+    The branch stream is held back (a device-side spin) right before each skip projection's
+    weight gradient; every bucket the collective is given, snapshotted on the stream it is issued
+    from, must already hold the final gradients (the buffer starts as NaN)."""
+    import torch.distributed as dist
+    from dorknet_amd import _hip
+    from dorknet_amd.parallel import DataParallel
+    from examples.resnet18_depsep import ResNet18, synthetic_batch
+    monkeypatch.setenv("DORKNET_ASYNC_WGRAD", "0")
+    monkeypatch.setenv("DORKNET_BRANCH_STREAM", "1")
+    _rccl_world1()
+    try:
+        X, _, onehot = synthetic_batch(2, seed=SEED_X)
+        np.random.seed(SEED_W)
+        net = ResNet18("r18")
+        net.to_gpu()
+        dp = DataParallel(net, bucket_bytes=256 << 10, update_skip_projections=True)
+        net.forward(torch.as_tensor(X, device="cuda"), torch.as_tensor(onehot, device="cuda"))
+        dp.flat.fill_(float("nan"))
+        orig = _hip.lib.dk_pwconv_wgrad_f32
+        calls = []
+
+        def slow_wgrad(*args):
+            calls.append(torch.cuda.current_stream() == _hip.branch_stream())
+            torch.cuda._sleep(20_000_000)  # ~10 ms of spinning on the current (branch) stream
+            return orig(*args)
+        monkeypatch.setattr(_hip.lib, "dk_pwconv_wgrad_f32", slow_wgrad)
+        snaps = []
+        real = dist.all_reduce
+
+        def spy(t, *a, **k):
+            snaps.append((t, t.clone()))
+            return real(t, *a, **k)
+        monkeypatch.setattr(dist, "all_reduce", spy)
+        dp.backward()
+        torch.cuda.synchronize()
+        # the three skip projections' weight gradients ran on the branch stream
+        assert calls == [True, True, True], calls
+        assert len(snaps) == len(dp.buckets) > 3
+        for t, snap in snaps:
+            assert not torch.isnan(snap).any()
+            assert torch.equal(snap, t)
+    finally:
+        dist.destroy_process_group()
+
+
 def test_bucket_launch_order_rccl_world1():
     """RCCL world 1: the order in which gradient buckets go to the collective against the order in
     which layers finish backward.  Each bucket is launched as soon as every leaf layer it covers
@@ -178,10 +227,11 @@ def test_bucket_launch_order_rccl_world1():
         dist.destroy_process_group()
 
 
-def _gloo_rank(rank, world, port, outdir, q):
+def _gloo_rank(rank, world, port, outdir, q, env=None):
     try:
         os.environ["MASTER_ADDR"] = "127.0.0.1"
         os.environ["MASTER_PORT"] = str(port)
+        os.environ.update(env or {})
         import torch.distributed as dist
         torch.cuda.set_device(0)
         dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -212,14 +262,18 @@ def _gloo_rank(rank, world, port, outdir, q):
         q.put((rank, traceback.format_exc()))
 
 
-def test_data_parallel_gloo_world2_equals_full_batch(tmp_path):
+@pytest.mark.parametrize("env", [{}, {"DORKNET_ASYNC_WGRAD": "0", "DORKNET_BRANCH_STREAM": "1"}],
+                         ids=["default", "sync_wgrad_branch"])
+def test_data_parallel_gloo_world2_equals_full_batch(tmp_path, env):
+    """`sync_wgrad_branch`: weight gradients on the issuing stream, skip projections on
+    the branch stream, their gradients all-reduced (update_skip_projections=True)."""
     import torch.multiprocessing as mp
     from examples.resnet18_depsep import ResNet18, synthetic_batch
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    procs = [ctx.Process(target=_gloo_rank, args=(r, world, port, str(tmp_path), q)) for r in range(world)]
+    procs = [ctx.Process(target=_gloo_rank, args=(r, world, port, str(tmp_path), q, env)) for r in range(world)]
     for p in procs:
         p.start()
     try:

@@ -10,8 +10,8 @@ weight gradient with conv0_bn's backward on load at 256 x 3 x 225 x 225.  Each t
 records which C-ABI entry points ran, so it fails if a fusion stops being taken.
 
 Tolerance: normwise relative 1e-4 for outputs, input and weight gradients, or
-10x the error of the same maths evaluated in fp32 (the twin in float32, an independent fp32
-pipeline) where that is larger.  At batch 256 the fp32 error itself reaches ~6e-4 on some
+FP32_SLACK = 3x the error of the same maths evaluated in fp32 (the twin in float32, an
+independent fp32 pipeline) where that is larger (tests/_convert.slack_bound).  At batch 256 the fp32 error itself reaches ~6e-4 on some
 gradients: tens of millions of BN outputs per layer put a few within an ulp of the ReLU
 threshold, and their masks flip between any two fp32 pipelines (measured: scripts/diag_fullsize.py,
 profiles/r02_fullsize_conditioning.txt; at batch 16 every gradient agrees to ~1e-6).  A
@@ -53,26 +53,41 @@ def _perturb_bn(layers, rng):
             l.learned_params["beta"] = (0.1 * rng.standard_normal((1, C, 1, 1))).astype(np.float32)
 
 
-def _run(layers, X, dY, input_grad):
+def _run(layers, X, dY, input_grad, onehot=None):
+    """The layers as a FeedForwardNetwork on the GPU and the fp64 / fp32 twins.  With `onehot`
+    the network ends in the reference's loss layer (SoftmaxWithCrossEntropy): Y = the
+    probabilities, backward from the loss, and the losses are returned as twin.loss / twin32.loss
+    / net._dk_loss."""
+    from dorknet_amd.layers.losses import SoftmaxWithCrossEntropy
     from dorknet_amd.network.feed_forward_network import FeedForwardNetwork
     twin = TorchTwin(layers)                       # numpy parameters, before to_gpu
     net = FeedForwardNetwork("fullsize")
     for l in layers:
         net.add_layer(l)
+    if onehot is not None:
+        net.set_loss_layer(SoftmaxWithCrossEntropy("softmax1"))
     net.to_gpu()
     Xd = torch.as_tensor(X, device="cuda")
-    dYd = torch.as_tensor(dY, device="cuda")
-    _, Y = net.forward(Xd, None)
-    dX = net.backward(dYd, input_grad=input_grad)
+    if onehot is None:
+        dYd = torch.as_tensor(dY, device="cuda")
+        _, Y = net.forward(Xd, None)
+        dX = net.backward(dYd, input_grad=input_grad)
+    else:
+        dYd = None
+        loss, Y = net.forward(Xd, torch.as_tensor(onehot, device="cuda"))
+        dX = net.backward(input_grad=input_grad)
+        net._dk_loss = float(loss)
     torch.cuda.synchronize()
     Yg = Y.float().cpu().numpy()
     dXg = dX.float().cpu().numpy() if input_grad else None
     grads = {(l.layer_name, k): l.grads[k].float().cpu().numpy()
              for l in all_layers(layers) for k in (l.grads or {})}
     del Xd, dYd, Y, dX
-    Yt, dXt, gt = twin.run(X, dY, input_grad=input_grad)
+    Yt, dXt, gt = twin.run(X, dY, input_grad=input_grad, onehot=onehot)
     twin32 = TorchTwin(layers, np.float32)
-    Y32, dX32, g32 = twin32.run(X, dY, input_grad=input_grad)
+    Y32, dX32, g32 = twin32.run(X, dY, input_grad=input_grad, onehot=onehot)
+    if onehot is not None:
+        twin.loss32 = twin32.loss
     return (Yg, dXg, grads), (Yt, dXt, gt), (Y32, dX32, g32), twin, net
 
 
@@ -199,4 +214,47 @@ def test_stem_full_size(monkeypatch, narrow):
     expect = ({"dk_conv2d_wgrad_bnbwd_narrow_f32", "dk_conv2d_fwd_narrow_f32"} if narrow == "1" else
               {"dk_conv2d_wgrad_bnbwd_f32", "dk_conv2d_fwd_ex_f32"})
     assert expect <= calls.seen, calls.seen
+    _check(got, want, f32, twin, layers)
+
+
+def test_res4_res6_full_size(monkeypatch):
+    """res4 (28 x 28 x 128), res5 (the stride-2 128 -> 256 block: strided depthwise, 128 -> 256
+    pointwise, stride-2 skip projection) and res6 (14 x 14 x 256) at batch 256 through the fused
+    network path (the middle blocks had no full-size check)."""
+    from examples.resnet18_depsep import ResNet18
+    np.random.seed(41)
+    layers = ResNet18("r18").layers[9:12]
+    assert [l.layer_name for l in layers] == ["res4", "res5", "res6"]
+    rng = np.random.default_rng(42)
+    _perturb_bn(layers, rng)
+    X = np.abs(rng.standard_normal((256, 128, 28, 28), dtype=np.float32))   # res3's ReLU output
+    dY = rng.standard_normal((256, 256, 14, 14), dtype=np.float32)
+    calls = Calls(monkeypatch, FUSED + ["dk_dwconv_bwd_bnbwd_join_f32", "dk_dwconv_dgrad_join_f32"])
+    got, want, f32, twin, _ = _run(layers, X, dY, input_grad=True)
+    assert {"dk_pwconv_fwd_ex_f32", "dk_pwconv_dgrad_bnbwd_f32", "dk_pwconv_wgrad_bnx_f32", "dk_dwconv_fwd_ex_f32",
+            "dk_bn_add_f32", "dk_dwconv_bwd_bnbwd_join_f32", "dk_dwconv_dgrad_join_f32"} <= calls.seen, calls.seen
+    _check(got, want, f32, twin, layers)
+
+
+def test_res8_head_full_size(monkeypatch):
+    """res8 (7 x 7 x 512) -> global average pooling -> dense 512 -> 120 -> softmax + cross-entropy
+    at batch 256, backward from the loss ((p - y) / N, layers/losses.py:29-34): the network's
+    head at the configuration's batch, loss with the l2 terms
+    (feed_forward_network.py:54-60) against the twins'."""
+    from examples.resnet18_depsep import ResNet18
+    np.random.seed(43)
+    layers = ResNet18("r18").layers[13:16]
+    assert [l.layer_name for l in layers] == ["res8", "global_pool1", "dense1"]
+    rng = np.random.default_rng(44)
+    _perturb_bn(layers, rng)
+    X = np.abs(rng.standard_normal((256, 512, 7, 7), dtype=np.float32))     # res7's ReLU output
+    onehot = np.eye(120, dtype=np.float32)[rng.integers(0, 120, 256)]
+    calls = Calls(monkeypatch, FUSED + ["dk_gap_fwd_f32", "dk_gap_bwd_f32", "dk_dense_fwd_f32", "dk_dense_dgrad_f32",
+                                        "dk_dense_wgrad_f32", "dk_softmax_xent_fwd_f32", "dk_softmax_xent_bwd_f32"])
+    got, want, f32, twin, net = _run(layers, X, None, input_grad=True, onehot=onehot)
+    assert {"dk_pwconv_fwd_ex_f32", "dk_pwconv_dgrad_bnbwd_f32", "dk_gap_fwd_f32", "dk_gap_bwd_f32", "dk_dense_fwd_f32",
+            "dk_dense_dgrad_f32", "dk_dense_wgrad_f32", "dk_softmax_xent_fwd_f32",
+            "dk_softmax_xent_bwd_f32"} <= calls.seen, calls.seen
+    assert abs(net._dk_loss - twin.loss) <= max(TOL * abs(twin.loss), 3.0 * abs(twin.loss32 - twin.loss)), \
+        (net._dk_loss, twin.loss, twin.loss32)
     _check(got, want, f32, twin, layers)
