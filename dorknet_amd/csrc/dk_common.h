@@ -234,6 +234,23 @@ int pw_stream_dgrad_bnbwd(const float* g, const float* bn_x, int M, const float*
                           const float* iis, const float* ig, const float* ib, int irelu, double* part,
                           hipStream_t st, const struct FoldTail* ft = nullptr);
 
+// fp32 deep streaming pointwise kernels (pw_deep.hip): reduction 64-512 with 128+ channels on a side.
+void pw_deep_set(int v);  // tuning knob (dk_debug_set_gemm_config kind 11)
+bool pw_deep_fwd_ok(int K, int C, int M, size_t xbytes);
+int pw_deep_fwd_rows(int M, int K, int C);
+int pw_deep_fwd_slices(int M, int K, int C);
+int pw_deep_fwd(const float* x, int N, int H, int W, int stride, int OH, int OW, const float* w, int K, int C,
+                const float* bias, float* y, const float* im, const float* iis, const float* ig, const float* ib,
+                int irelu, double* part, hipStream_t st, const struct FoldTail* ft = nullptr);
+bool pw_deep_dgrad_ok(int K, int C, int M);
+int pw_deep_dgrad_rows(int M, int K, int C);
+int pw_deep_dgrad_slices(int M, int K, int C);
+int pw_deep_dgrad_bnbwd(const float* g, const float* bn_x, int M, int K, int C, const float* om, const float* ois,
+                        const float* og, const float* ob, int orelu, const float* k12, float* dy_out, const float* w,
+                        float* dx, const float* res, const float* x, const float* im, const float* iis,
+                        const float* ig, const float* ib, int irelu, double* part, hipStream_t st,
+                        const struct FoldTail* ft = nullptr);
+
 // bf16 streaming pointwise kernels (pw_stream_bf16.hip, BASELINE config 5): K, C in {64, 128}.
 bool pw_stream_bf16_fwd_ok(int K, int C, int M);
 int pw_stream_bf16_fwd_rows(int M, int K, int C);

@@ -8,6 +8,11 @@ using namespace dk;
 DK_API int dk_pwconv_fwd_f32(const float* x, int N, int H, int W, int C, const float* w_kc, int K, int stride,
                              const float* bias, float* y, int OH, int OW, void* stream) {
   if (!fits((size_t)N * H * W * C * 4)) return DK_ERR_ARGS;
+  if (C % 4 == 0 && aligned16(x) && aligned16(w_kc) &&
+      pw_deep_fwd_ok(K, C, N * OH * OW, (size_t)N * H * W * C * 4))
+    // the deep streaming kernel (pw_deep.hip), bit-identical y (the strided skip projections)
+    return pw_deep_fwd(x, N, H, W, stride, OH, OW, w_kc, K, C, bias, y, nullptr, nullptr, nullptr, nullptr, 0,
+                       nullptr, as_stream(stream));
   MatDesc b = mat(w_kc, K, C, K);
   EpStore ep = ep_store(y, K, bias);
   if (C % 4 || !aligned16(x) || !aligned16(w_kc)) {
@@ -34,6 +39,7 @@ DK_API int dk_pwconv_fwd_bnx_f32(const float* x, int N, int H, int W, int C, con
 DK_API int dk_pwconv_fwd_stats_rows(int N, int OH, int OW, int K, int C) {
   const int M = N * OH * OW;
   // (the input extent does not change the choice for the shapes the network uses)
+  if (pw_deep_fwd_ok(K, C, M, 0)) return pw_deep_fwd_rows(M, K, C);
   if (pw_stream_fwd_ok(K, C, M, 0)) return pw_stream_fwd_rows(M, K);
   return stats_rows(M, K, C);
 }
@@ -43,6 +49,17 @@ DK_API int dk_pwconv_fwd_ex_f32(const float* x, int N, int H, int W, int C, cons
                                 const float* bn_invstd, const float* bn_gamma, const float* bn_beta, int bn_relu,
                                 double* stats, void* stream) {
   if (C % 4 || !aligned16(x) || !aligned16(w_kc) || !fits((size_t)N * H * W * C * 4)) return DK_ERR_ARGS;
+  if (pw_deep_fwd_ok(K, C, N * OH * OW, (size_t)N * H * W * C * 4)) {
+    // the deep streaming kernel (pw_deep.hip): bit-identical y, its own partial rows and slices
+    // (dk_pwconv_fwd_stats_rows sized the partials for it: no other path may take this call)
+    if (bn_mean && !bn_ok(bn_mean, bn_invstd, bn_gamma, bn_beta)) return DK_ERR_ARGS;
+    const int M = N * OH * OW;
+    FoldTail ft;
+    if (stats) fold_take(stats, pw_deep_fwd_rows(M, K, C), K, pw_deep_fwd_slices(M, K, C), &ft);
+    return fold_status(pw_deep_fwd(x, N, H, W, stride, OH, OW, w_kc, K, C, bias, y, bn_mean, bn_invstd, bn_gamma,
+                                   bn_beta, bn_relu, stats, as_stream(stream), stats ? &ft : nullptr),
+                       stats ? ft : FoldTail{});
+  }
   if (pw_stream_fwd_ok(K, C, N * OH * OW, (size_t)N * H * W * C * 4) && (!bn_mean || bn_ok(bn_mean, bn_invstd, bn_gamma, bn_beta)))
     // K = C = 64 / 128: the persistent streaming kernel (pw_stream.hip), bit-identical outputs
   {
@@ -79,6 +96,7 @@ DK_API int dk_pwconv_dgrad_f32(const float* dy, int N, int OH, int OW, int K, co
 DK_API int dk_pwconv_dgrad_stats_rows(int N, int OH, int OW, int K, int C) { return stats_rows(N * OH * OW, C, K); }
 DK_API int dk_pwconv_dgrad_bnbwd_stats_rows(int N, int OH, int OW, int K, int C) {
   const int M = N * OH * OW;
+  if (pw_deep_dgrad_ok(K, C, M)) return pw_deep_dgrad_rows(M, K, C);
   if (pw_stream_dgrad_ok(K, C, M)) return pw_stream_dgrad_rows(M);
   return stats_rows(M, C, K, kRowBnBwd);
 }
@@ -182,6 +200,17 @@ DK_API int dk_pwconv_dgrad_bnbwd_f32(const float* g, const float* bn_x, int N, i
   if (!vec_ok(b, 4, C) || K % 4 || !aligned16(g) || !aligned16(bn_x) || (dy_out && !aligned16(dy_out)) ||
       (size_t)K * 32 > 64 * 1024)
     return DK_ERR_ARGS;
+  if (pw_deep_dgrad_ok(K, C, M)) {
+    // the deep streaming kernel (pw_deep.hip): bit-identical dy and dx, its own partial rows
+    // (sized by dk_pwconv_dgrad_bnbwd_stats_rows: no other path may take this call)
+    if (part && !bn_ok(bn_mean, bn_invstd, bn_gamma, bn_beta)) return DK_ERR_ARGS;
+    FoldTail ft;
+    if (part) fold_take(part, pw_deep_dgrad_rows(M, K, C), C, pw_deep_dgrad_slices(M, K, C), &ft);
+    return fold_status(pw_deep_dgrad_bnbwd(g, bn_x, M, K, C, out_mean, out_invstd, out_gamma, out_beta, out_relu, k12,
+                                           dy_out, w_kc, dx, residual, part ? x : nullptr, bn_mean, bn_invstd,
+                                           bn_gamma, bn_beta, bn_relu, part, st, part ? &ft : nullptr),
+                       part ? ft : FoldTail{});
+  }
   if (pw_stream_dgrad_ok(K, C, M)) {
     // K = C = 64: the persistent streaming kernel (pw_stream.hip), bit-identical results
     if (part && !bn_ok(bn_mean, bn_invstd, bn_gamma, bn_beta)) return DK_ERR_ARGS;

@@ -1,0 +1,567 @@
+// fp32 kernels for the deep pointwise layers (layers/pointwise_convolution.py:46-75 at the 28 x 28 /
+// 14 x 14 / 7 x 7 units of ResNet-18-depsep: 128 / 256 / 512 channels on a side).  These GEMMs are
+// MFMA-bound (arithmetic intensity 32-256 flop/B against the fp32 ridge of ~20); the tiled engine
+// and pw_stream.hip's K = C = 128 forward reach 0.35-0.48 of the fp32 MFMA peak on them.
+//
+// What bounds them on gfx950 (profiles/r04_mfma_valu_overlap.txt, scripts/mfma_valu.hip): f32 VALU
+// work does not overlap v_mfma_f32_32x32x2_f32 on a SIMD -- 4 MFMAs alone run at 0.87-0.91 of the
+// peak, with one v_fma_f32 per MFMA 0.82-0.86, two 0.81-0.83, eight 0.67 -- while f64 VALU work
+// mostly does (one v_fma_f64 per MFMA: 0.88-0.90).  So the design goal is few f32 VALU instructions
+// per MFMA: the tiled engine's BN-on-load loaders and the first streaming kernels issued 5-8.
+//
+// Structure: weight-stationary waves over a block-shared pixel tile.
+//   * a block owns NB = 128 output columns (blockIdx.y) and walks 32-pixel row tiles (blockIdx.x,
+//     + gridDim.x, ...); its 4 waves own 32 columns each, with their B fragments -- the whole
+//     reduction of their columns, KR / 2 VGPRs per lane in the v_mfma_f32_32x32x2_f32 layout -- loaded
+//     into registers once;
+//   * the block stages each pixel tile (32 x KR) once: coalesced 16-byte row loads, the BatchNorm
+//     (+ReLU) applied on load (forward) or the following BatchNorm's backward formed on load (dgrad)
+//     once per element by the block -- not once per column slice -- into an LDS tile (double
+//     buffered; row stride KR + 4 floats, odd in float4s: conflict-free ds_read_b128);
+//   * per 4 MFMAs a wave reads one ds_read_b128 of A and no other operand; the next tile's global
+//     loads are in flight during the MFMAs; one barrier per tile;
+//   * the epilogue works in the MFMA C layout (lane = output column): BatchNorm partial sums stay in
+//     registers across the block's tiles, one partial row per block and column group.
+// MFMA k order 8q + 4h + e (h = lane half), as the tiled engine: outputs are bit-identical to it.
+#include <stdlib.h>
+
+#include <algorithm>
+
+#include "dk_common.h"
+#include "fold_tail.h"
+
+namespace dk {
+namespace pwd {
+
+constexpr int TR = 32;       // pixels per tile
+constexpr int NW = 4;        // waves per block (one 32-column MFMA block each)
+constexpr int NB = 32 * NW;  // output columns per block
+constexpr int NT = 64 * NW;  // threads per block
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// Waves per SIMD the registers are sized for: the B fragments take KR / 2 VGPRs per lane.
+template <int KR>
+constexpr int fwd_wps() {
+  return KR <= 64 ? 4 : KR <= 128 ? 3 : KR <= 256 ? 2 : 1;
+}
+template <int KR>
+constexpr int dgrad_wps() {
+  return KR <= 128 ? 2 : 1;
+}
+
+__device__ __forceinline__ uint32_t off4(int m, int ld, int c) { return ((uint32_t)m * ld + c) * 4u; }
+
+// A buffer resource over rows [tile * TR, nrows) of a [nrows][ld] tensor: the tile's row offset goes
+// into the (uniform) base address, so a lane's offset within the tile is the same for every tile (no
+// per-tile VALU address arithmetic), and the range check still drops rows past nrows.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t tile_rsrc(const float* p, int ld, int tile, int nrows) {
+  const int rows = nrows - tile * TR;
+  return make_rsrc_v(p + (size_t)tile * TR * ld, rows > 0 ? (uint32_t)rows * ld * 4u : 0u);
+}
+
+// acc = the 32 x 32 tile product of the LDS pixel tile (lane: row l32, k = 8q + 4h + e at ap + 8q) and the
+// lane's B fragments, k-pairs in ascending order (the tiled engine's).  The A reads run kAD float4s
+// ahead of their MFMAs (scheduling barriers keep each read D groups ahead): left to itself the
+// scheduler issued each read just before its MFMAs, exposing the LDS latency every 8 MFMAs -- a
+// quarter of the MFMA time at one wave per SIMD.
+constexpr int kAD = 4;
+template <int KQ>
+__device__ __forceinline__ void mfma_tile(const float* ap, const f32x4* bw, f32x16& acc) {
+  constexpr int D = KQ < kAD ? KQ : kAD;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  f32x4 ab[D];
+#pragma unroll
+  for (int i = 0; i < D; ++i) ab[i] = ld4(ap + 8 * i);
+#pragma unroll
+  for (int q = 0; q < KQ; ++q) {
+    const f32x4 av = ab[q % D];
+    if (q + D < KQ) ab[q % D] = ld4(ap + 8 * (q + D));
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[e], bw[q][e], acc, 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+struct FwdArgs {
+  const float* x;     // [input pixels][KR] (the preceding BN's raw input when BN)
+  const float* w;     // [N][KR]
+  const float* bias;  // [N] nullable
+  float* y;           // [M][N]
+  const float *im, *iis, *ig, *ib;  // input BN (BN on load)
+  int irelu;
+  double* part;       // [gridDim.x][2][N]: (sum y, sum y^2) per block
+  int M, N, H, W, OH, OW, sa;
+  uint32_t xbytes;
+  FoldTail ft;
+};
+
+// The block's partial row of column sums (fwd: sum y, sum y^2; dgrad: the BN-backward sums) from
+// each lane's per-column fp64 accumulators, then the in-launch fold when armed.
+__device__ __forceinline__ void partial_row(double ps, double pq, double* part, int N, int n0, const FoldTail& ft,
+                                            float* scratch) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l32 = lane & 31, h = lane >> 5;
+  double(*const red)[NB] = reinterpret_cast<double(*)[NB]>(scratch);  // [2][NB]
+  ps += __shfl_xor(ps, 32, 64);
+  pq += __shfl_xor(pq, 32, 64);
+  __syncthreads();  // the pixel tiles become scratch
+  if (h == 0) {
+    red[0][32 * wave + l32] = ps;
+    red[1][32 * wave + l32] = pq;
+  }
+  __syncthreads();
+  for (int i = tid; i < 2 * NB; i += NT) {
+    const int which = i / NB, c = i - which * NB;
+    pub_store(part + ((size_t)blockIdx.x * 2 + which) * N + n0 + c, red[which][c]);
+  }
+  if (ft.part) {
+    __syncthreads();  // red is read before the fold overwrites it
+    fold_tail<NT>(ft, blockIdx.x, n0, NB, blockIdx.y, reinterpret_cast<double2*>(scratch));
+  }
+}
+
+template <int KR, bool BN, bool STATS, bool STRIDED, bool HB>
+__global__ __launch_bounds__(NT, fwd_wps<KR>()) void fwd_kernel(FwdArgs a) {
+  constexpr int SK = KR + 4, KV = KR / 4, LV = TR * KV / NT, KQ = KR / 8;
+  static_assert(KR % 32 == 0 && (SK / 4) % 2 == 1 && NT % KV == 0, "pwd::fwd_kernel shape");
+  __shared__ __attribute__((aligned(16))) float As[2][TR * SK];
+  static_assert(sizeof(double) * 2 * NT <= sizeof(float) * 2 * TR * SK, "fold scratch fits in the tiles");
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int l32 = lane & 31, h = lane >> 5;
+  const int n0 = blockIdx.y * NB, N = a.N;
+  const int col = n0 + 32 * wave + l32;
+  // this lane's B fragments: W[col][8q + 4h + e] for every q, e (once; the weights are L2-resident)
+  f32x4 bw[KQ];
+#pragma unroll
+  for (int q = 0; q < KQ; ++q) bw[q] = ld4(a.w + (size_t)col * KR + 8 * q + 4 * h);
+  const float bias = HB ? a.bias[col] : 0.f;
+  const bool irelu = a.irelu != 0;
+  // staging: lane loads float4 kv = tid % KV of rows tid / KV + j * (NT / KV): fixed channels
+  const int kv = tid % KV, r0 = tid / KV;
+  f32x4 mu, is, ga, be;
+  if constexpr (BN) {
+    mu = ld4(a.im + 4 * kv);
+    is = ld4(a.iis + 4 * kv);
+    ga = ld4(a.ig + 4 * kv);
+    be = ld4(a.ib + 4 * kv);
+  }
+  const __amdgpu_buffer_rsrc_t rx = make_rsrc_v(a.x, a.xbytes);
+  const int ntiles = (a.M + TR - 1) / TR, G = gridDim.x;
+  // lane offsets within a tile (the tile's row offset is in the resource base: tile_rsrc)
+  uint32_t lofs[LV], eofs[16];
+#pragma unroll
+  for (int j = 0; j < LV; ++j) lofs[j] = off4(r0 + j * (NT / KV), KR, 4 * kv);
+#pragma unroll
+  for (int r = 0; r < 16; ++r) eofs[r] = off4(4 * h + (r & 3) + 8 * (r >> 2), N, col);
+
+  auto load_tile = [&](int tile, f32x4* st) {
+    const __amdgpu_buffer_rsrc_t rt = tile_rsrc(a.x, KR, tile, a.M);
+#pragma unroll
+    for (int j = 0; j < LV; ++j) {
+      if constexpr (STRIDED) {
+        // output pixel (n, oh, ow) reads input pixel (n, sa oh, sa ow); pixels past M map past the
+        // input (zeros)
+        const int m = tile * TR + r0 + j * (NT / KV);
+        const int ow = m % a.OW, q = m / a.OW, oh = q % a.OH, n = q / a.OH;
+        const int row = (n * a.H + oh * a.sa) * a.W + ow * a.sa;
+        st[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rx, (int)off4(row, KR, 4 * kv), 0, 0));
+      } else {
+        st[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rt, (int)lofs[j], 0, 0));
+      }
+    }
+  };
+  // the BatchNorm (+ReLU) on load; max(r, 0) is the reference's (r > 0) ? r : 0 (a NaN gives 0 both ways)
+  auto stage = [&](float* dst, const f32x4* st) {
+    if (BN && irelu) {
+#pragma unroll
+      for (int j = 0; j < LV; ++j) {
+        f32x4 v = st[j];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = __builtin_fmaxf(bn_out(v[e], mu[e], is[e], ga[e], be[e]), 0.f);
+        st4(dst + (r0 + j * (NT / KV)) * SK + 4 * kv, v);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < LV; ++j) {
+        f32x4 v = st[j];
+        if constexpr (BN) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = bn_out(v[e], mu[e], is[e], ga[e], be[e]);
+        }
+        st4(dst + (r0 + j * (NT / KV)) * SK + 4 * kv, v);
+      }
+    }
+  };
+
+  int t = blockIdx.x;
+  {
+    f32x4 st[LV];
+    load_tile(t, st);
+    stage(&As[0][0], st);
+  }
+  __syncthreads();
+  double ps = 0.0, pq = 0.0;
+  int buf = 0;
+  for (; t < ntiles; t += G) {
+    f32x4 nst[LV];
+    load_tile(t + G, nst);  // in flight during the MFMAs
+    const float* ap = &As[buf][0] + l32 * SK + 4 * h;
+    f32x16 acc;
+    mfma_tile<KQ>(ap, bw, acc);
+    // epilogue: rows (r & 3) + 8 (r >> 2) + 4h of the tile, column col
+    const int mb = t * TR + 4 * h;
+    const __amdgpu_buffer_rsrc_t ry = tile_rsrc(a.y, N, t, a.M);
+    if constexpr (HB) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[r] += bias;
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float v = acc[r];  // (not bit_cast(acc[r]): hipcc 7.2 stored element 0 for every r)
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), ry, (int)eofs[r], 0, 0);
+    }
+    if constexpr (STATS) {
+      if (t * TR + TR <= a.M) {  // a whole tile (uniform): no row masks
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const double d = (double)acc[r];
+          ps += d;
+          pq += d * d;
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int dm = (r & 3) + 8 * (r >> 2);
+          const double d = (mb + dm < a.M) ? (double)acc[r] : 0.0;
+          ps += d;
+          pq += d * d;
+        }
+      }
+    }
+    stage(&As[buf ^ 1][0], nst);
+    __syncthreads();
+    buf ^= 1;
+  }
+  if constexpr (STATS) partial_row(ps, pq, a.part, N, n0, a.ft, &As[0][0]);
+}
+
+// ---------------------------------------------------------------------------------------
+// BN-backward-on-load dgrad (layers/pointwise_convolution.py:57-75 + layers/batch_norm.py:125-174):
+// dx[M][N] = dy . W (+ residual), dy = the following BatchNorm's backward of (g, x_out) formed on
+// load (bn_bwd_elem, bit-identical to dk_bn_bwd_apply_f32) and written through by column group 0
+// for the weight gradient, and the input BatchNorm's backward partials of the stored dx.  KR = the
+// layer's output channels K (the reduction), N = its input channels C.
+// ---------------------------------------------------------------------------------------
+struct DgradArgs {
+  const float* g;     // [M][KR]
+  const float* xo;    // [M][KR] the following BN's raw input
+  float* dy_out;      // [M][KR] nullable
+  const float* w;     // [KR][N]
+  float* dx;          // [M][N]
+  const float* res;   // [M][N] nullable
+  const float* xi;    // [M][N] the input BN's raw input (partials), nullable
+  const float *om, *ois, *og, *ob, *k12;  // following BN
+  int orelu;
+  const float *im, *iis, *ig, *ib;  // input BN (partials)
+  int irelu;
+  double* part;       // [gridDim.x][2][N]
+  int M, N;
+  FoldTail ft;
+};
+
+template <int KR, bool RES, bool PART>
+__global__ __launch_bounds__(NT, dgrad_wps<KR>()) void dgrad_kernel(DgradArgs a) {
+  constexpr int SK = KR + 4, KV = KR / 4, LV = TR * KV / NT, KQ = KR / 8;
+  static_assert(KR % 32 == 0 && (SK / 4) % 2 == 1 && NT % KV == 0, "pwd::dgrad_kernel shape");
+  __shared__ __attribute__((aligned(16))) float As[2][TR * SK];
+  static_assert(sizeof(double) * 2 * NT <= sizeof(float) * 2 * TR * SK, "fold scratch fits in the tiles");
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int l32 = lane & 31, h = lane >> 5;
+  const int n0 = blockIdx.y * NB, N = a.N;
+  const int col = n0 + 32 * wave + l32;
+  // B fragments: W[8q + 4h + e][col]
+  f32x4 bw[KQ];
+#pragma unroll
+  for (int q = 0; q < KQ; ++q)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) bw[q][e] = a.w[(size_t)(8 * q + 4 * h + e) * N + col];
+  const int kv = tid % KV, r0 = tid / KV;
+  const f32x4 mu = ld4(a.om + 4 * kv), is = ld4(a.ois + 4 * kv), ga = ld4(a.og + 4 * kv), be = ld4(a.ob + 4 * kv);
+  const f32x4 k1 = ld4(a.k12 + 4 * kv), k2 = ld4(a.k12 + KR + 4 * kv);
+  f32x4 f;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) f[e] = ga[e] * is[e];
+  const float pm = PART ? a.im[col] : 0.f, pis = PART ? a.iis[col] : 0.f, pga = PART ? a.ig[col] : 0.f,
+              pbe = PART ? a.ib[col] : 0.f;
+  const bool orelu = a.orelu != 0, irelu = a.irelu != 0;
+
+  // dy written through by column group 0 only (the others' stores go to a zero-size resource)
+  const bool writer = a.dy_out != nullptr && blockIdx.y == 0;
+  const int ntiles = (a.M + TR - 1) / TR, G = gridDim.x;
+  // lane offsets within a tile (the tile's row offset is in the resource base: tile_rsrc)
+  uint32_t lofs[LV], eofs[16];
+#pragma unroll
+  for (int j = 0; j < LV; ++j) lofs[j] = off4(r0 + j * (NT / KV), KR, 4 * kv);
+#pragma unroll
+  for (int r = 0; r < 16; ++r) eofs[r] = off4(4 * h + (r & 3) + 8 * (r >> 2), N, col);
+
+  auto load_tile = [&](int tile, f32x4* sg, f32x4* sx) {
+    const __amdgpu_buffer_rsrc_t rg = tile_rsrc(a.g, KR, tile, a.M), rx = tile_rsrc(a.xo, KR, tile, a.M);
+#pragma unroll
+    for (int j = 0; j < LV; ++j) {
+      sg[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rg, (int)lofs[j], 0, 0));
+      sx[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rx, (int)lofs[j], 0, 0));
+    }
+  };
+  auto stage = [&](int tile, float* dst, const f32x4* sg, const f32x4* sx) {
+    const __amdgpu_buffer_rsrc_t rdy = tile_rsrc(writer ? a.dy_out : a.g, KR, tile, writer ? a.M : 0);
+#pragma unroll
+    for (int j = 0; j < LV; ++j) {
+      const int r = r0 + j * (NT / KV);
+      f32x4 v;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float xe = sx[j][e];
+        float ge = sg[j][e];
+        const bool kill = (!(bn_out(xe, mu[e], is[e], ga[e], be[e]) > 0.f)) & orelu;
+        ge = kill ? 0.f : ge;
+        v[e] = bn_bwd_elem(xe, ge, mu[e], is[e], f[e], k1[e], k2[e]);
+      }
+      st4(dst + r * SK + 4 * kv, v);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rdy, (int)lofs[j], 0, 0);
+    }
+  };
+
+  int t = blockIdx.x;
+  {
+    f32x4 sg[LV], sx[LV];
+    load_tile(t, sg, sx);
+    stage(t, &As[0][0], sg, sx);
+  }
+  __syncthreads();
+  double ps = 0.0, pq = 0.0;
+  int buf = 0;
+  for (; t < ntiles; t += G) {
+    f32x4 ng[LV], nx[LV];
+    load_tile(t + G, ng, nx);
+    // the epilogue's C-layout operands of this tile, in flight during the MFMAs
+    const int mb = t * TR + 4 * h;
+    const __amdgpu_buffer_rsrc_t rxi = tile_rsrc(PART ? a.xi : a.g, N, t, PART ? a.M : 0);
+    const __amdgpu_buffer_rsrc_t rr = tile_rsrc(RES ? a.res : a.g, N, t, RES ? a.M : 0);
+    const __amdgpu_buffer_rsrc_t rdx = tile_rsrc(a.dx, N, t, a.M);
+    float exi[16], ers[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      if constexpr (PART)
+        exi[r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rxi, (int)eofs[r], 0, 0));
+      if constexpr (RES)
+        ers[r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rr, (int)eofs[r], 0, 0));
+    }
+    const float* ap = &As[buf][0] + l32 * SK + 4 * h;
+    f32x16 acc;
+    mfma_tile<KQ>(ap, bw, acc);
+    if constexpr (RES) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[r] += ers[r];
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float v = acc[r];  // (not bit_cast(acc[r]): hipcc 7.2 stored element 0 for every r)
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), rdx, (int)eofs[r], 0, 0);
+    }
+    if constexpr (PART) {
+      const bool full = t * TR + TR <= a.M;  // a whole tile (uniform): no row masks
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int dm = (r & 3) + 8 * (r >> 2);
+        const float x = exi[r];
+        const float xh = (x - pm) * pis;
+        const bool kill = ((!(pga * xh + pbe > 0.f)) & irelu) | (!full && mb + dm >= a.M);
+        const float gv = kill ? 0.f : acc[r];
+        ps += (double)gv;
+        pq += (double)gv * (double)xh;
+      }
+    }
+    stage(t + G, &As[buf ^ 1][0], ng, nx);
+    __syncthreads();
+    buf ^= 1;
+  }
+  if constexpr (PART) partial_row(ps, pq, a.part, N, n0, a.ft, &As[0][0]);
+}
+
+// ---------------------------------------------------------------------------------------
+// Host side: the instantiated reductions and the grid.
+// ---------------------------------------------------------------------------------------
+#define DK_PWD_KR(X) X(64) X(128) X(256) X(512)
+
+static int occupancy(const void* fn) {
+  int v = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, fn, NT, 0) != hipSuccess || v < 1) v = 1;
+  return v;
+}
+
+template <int KR>
+static int fwd_occ() {
+  static const int occ = [] {
+#define DK_F(B_, S_, T_) reinterpret_cast<const void*>(&fwd_kernel<KR, B_, S_, T_, false>), \
+                         reinterpret_cast<const void*>(&fwd_kernel<KR, B_, S_, T_, true>)
+    const void* fs[] = {DK_F(true, true, false), DK_F(true, false, false), DK_F(false, true, false),
+                        DK_F(false, false, false), DK_F(true, true, true), DK_F(true, false, true),
+                        DK_F(false, true, true), DK_F(false, false, true)};
+#undef DK_F
+    int o = 1 << 20;
+    for (const void* f : fs) o = std::min(o, occupancy(f));
+    return o;
+  }();
+  return occ;
+}
+template <int KR>
+static int dgrad_occ() {
+  static const int occ = [] {
+    const void* fs[] = {reinterpret_cast<const void*>(&dgrad_kernel<KR, true, true>),
+                        reinterpret_cast<const void*>(&dgrad_kernel<KR, true, false>),
+                        reinterpret_cast<const void*>(&dgrad_kernel<KR, false, true>),
+                        reinterpret_cast<const void*>(&dgrad_kernel<KR, false, false>)};
+    int o = 1 << 20;
+    for (const void* f : fs) o = std::min(o, occupancy(f));
+    return o;
+  }();
+  return occ;
+}
+
+// Row-tile walkers per column group: every resident slot once (all blocks of a CU run at the same
+// time, so each CU gets the same number of blocks and each block within one tile of the same share),
+// at most one walker per tile; a multiple of the 8 XCDs when that costs no extra tile per walker, so
+// that walker x of every column group runs on one XCD (block id x + gx * y) and the groups of a row
+// tile share that XCD's L2 copy of its pixels.  A function of (M, N, occupancy) only: callers
+// allocate exactly the partial rows the launch writes.
+static int grid_x(int M, int N, int occ) {
+  const int ntiles = (M + TR - 1) / TR;
+  const int groups = N / NB;
+  int slots = occ * 256 / groups;
+  if (slots < 1) slots = 1;
+  int gx = std::min(ntiles, slots);
+  const int g8 = gx / 8 * 8;
+  if (g8 >= 8 && (ntiles + g8 - 1) / g8 == (ntiles + gx - 1) / gx) gx = g8;
+  return gx;
+}
+
+}  // namespace pwd
+
+// DORKNET_PW_DEEP=0 (or the streaming switch DORKNET_PW_STREAM=0) keeps the earlier paths; knob 11.
+static int g_pwd = -1;
+static bool pwd_enabled() {
+  if (g_pwd < 0) {
+    const char* e = getenv("DORKNET_PW_DEEP");
+    g_pwd = (e && e[0] == '0') ? 0 : 1;
+  }
+  return g_pwd == 1 && pw_stream_enabled();
+}
+void pw_deep_set(int v) { g_pwd = v < 0 ? -1 : v; }
+
+static bool pwd_kr(int KR) { return KR == 64 || KR == 128 || KR == 256 || KR == 512; }
+
+// The shapes the deep kernels take: reduction KR in {64, 128, 256, 512} with at least 128 channels
+// on one side (K = C = 64 stays on pw_stream.hip), outputs a multiple of the block's 128 columns.
+bool pw_deep_fwd_ok(int K, int C, int M, size_t xbytes) {
+  if (!pwd_enabled() || M <= 0 || (K < 128 && C < 128) || !pwd_kr(C) || K % pwd::NB) return false;
+  return xbytes < ((size_t)1 << 31) && (size_t)M * K * 4 < ((size_t)1 << 31);
+}
+bool pw_deep_dgrad_ok(int K, int C, int M) {
+  if (!pwd_enabled() || M <= 0 || (K < 128 && C < 128) || !pwd_kr(K) || C % pwd::NB) return false;
+  return (size_t)M * (K > C ? K : C) * 4 < ((size_t)1 << 31);
+}
+
+int pw_deep_fwd_rows(int M, int K, int C) {
+#define DK_ROWS(kr) \
+  if (C == kr) return pwd::grid_x(M, K, pwd::fwd_occ<kr>());
+  DK_PWD_KR(DK_ROWS)
+#undef DK_ROWS
+  return 0;
+}
+int pw_deep_fwd_slices(int M, int K, int C) { return K / pwd::NB; }
+int pw_deep_dgrad_rows(int M, int K, int C) {
+#define DK_ROWS(kr) \
+  if (K == kr) return pwd::grid_x(M, C, pwd::dgrad_occ<kr>());
+  DK_PWD_KR(DK_ROWS)
+#undef DK_ROWS
+  return 0;
+}
+int pw_deep_dgrad_slices(int M, int K, int C) { return C / pwd::NB; }
+
+int pw_deep_fwd(const float* x, int N, int H, int W, int stride, int OH, int OW, const float* w, int K, int C,
+                const float* bias, float* y, const float* im, const float* iis, const float* ig, const float* ib,
+                int irelu, double* part, hipStream_t st, const FoldTail* ft) {
+  const int M = N * OH * OW;
+  const bool strided = stride != 1 || H != OH || W != OW;
+  pwd::FwdArgs a{x, w, bias, y, im, iis, ig, ib, irelu, part, M, K, H, W, OH, OW, stride,
+                 (uint32_t)((size_t)N * H * W * C * 4)};
+  if (ft && part) a.ft = *ft;
+  const dim3 grid(pw_deep_fwd_rows(M, K, C), K / pwd::NB);
+  if (grid.x == 0) return DK_ERR_ARGS;
+#define DK_L(kr, B_, S_, T_)                                                                          \
+  do {                                                                                                \
+    if (bias)                                                                                         \
+      hipLaunchKernelGGL((pwd::fwd_kernel<kr, B_, S_, T_, true>), grid, dim3(pwd::NT), 0, st, a);     \
+    else                                                                                              \
+      hipLaunchKernelGGL((pwd::fwd_kernel<kr, B_, S_, T_, false>), grid, dim3(pwd::NT), 0, st, a);    \
+  } while (0)
+#define DK_FWD(kr)                    \
+  if (C == kr) {                      \
+    if (strided) {                    \
+      if (im && part)                 \
+        DK_L(kr, true, true, true);   \
+      else if (im)                    \
+        DK_L(kr, true, false, true);  \
+      else if (part)                  \
+        DK_L(kr, false, true, true);  \
+      else                            \
+        DK_L(kr, false, false, true); \
+    } else if (im && part)            \
+      DK_L(kr, true, true, false);    \
+    else if (im)                      \
+      DK_L(kr, true, false, false);   \
+    else if (part)                    \
+      DK_L(kr, false, true, false);   \
+    else                              \
+      DK_L(kr, false, false, false);  \
+    return launch_status();           \
+  }
+  DK_PWD_KR(DK_FWD)
+#undef DK_FWD
+#undef DK_L
+  return DK_ERR_ARGS;
+}
+
+int pw_deep_dgrad_bnbwd(const float* g, const float* bn_x, int M, int K, int C, const float* om, const float* ois,
+                        const float* og, const float* ob, int orelu, const float* k12, float* dy_out, const float* w,
+                        float* dx, const float* res, const float* x, const float* im, const float* iis,
+                        const float* ig, const float* ib, int irelu, double* part, hipStream_t st,
+                        const FoldTail* ft) {
+  pwd::DgradArgs a{g, bn_x, dy_out, w, dx, res, x, om, ois, og, ob, k12, orelu, im, iis, ig, ib, irelu, part, M, C};
+  if (ft && part) a.ft = *ft;
+  const dim3 grid(pw_deep_dgrad_rows(M, K, C), C / pwd::NB);
+  if (grid.x == 0) return DK_ERR_ARGS;
+#define DK_L(kr, R_, P_) hipLaunchKernelGGL((pwd::dgrad_kernel<kr, R_, P_>), grid, dim3(pwd::NT), 0, st, a)
+#define DK_DG(kr)             \
+  if (K == kr) {              \
+    if (res && x)             \
+      DK_L(kr, true, true);   \
+    else if (res)             \
+      DK_L(kr, true, false);  \
+    else if (x)               \
+      DK_L(kr, false, true);  \
+    else                      \
+      DK_L(kr, false, false); \
+    return launch_status();   \
+  }
+  DK_PWD_KR(DK_DG)
+#undef DK_DG
+#undef DK_L
+  return DK_ERR_ARGS;
+}
+
+}  // namespace dk

@@ -1,0 +1,167 @@
+"""The deep pointwise kernels (csrc/pw_deep.hip: reduction 64-512 with 128+ channels on a side)
+against the tiled engine they replace (knob 11 off and the streaming kernels off):
+dk_pwconv_fwd_ex_f32 y, dk_pwconv_fwd_f32 (the strided skip projections) y, and
+dk_pwconv_dgrad_bnbwd_f32 dy / dx bitwise (the same MFMA k order), the output statistics and the
+input BatchNorm's partial sums to fp64 rounding (one partial row per block and column group
+instead of one per tile); ragged pixel counts, every epilogue option, a large grid (several tiles
+per block), and nothing written past the outputs."""
+import numpy as np
+import pytest
+import torch
+
+from dorknet_amd._hip import lib, stream_handle
+
+pytestmark = pytest.mark.gpu
+
+STREAM_KNOB, DEEP_KNOB = 3, 11
+
+
+def nhwc(a):
+    return torch.as_tensor(np.ascontiguousarray(a, dtype=np.float32), device="cuda").contiguous(
+        memory_format=torch.channels_last)
+
+
+def bn_params(C, rng):
+    return [torch.as_tensor(v.astype(np.float32), device="cuda") for v in
+            (rng.randn(C) * 0.3, rng.rand(C) + 0.5, 1 + 0.3 * rng.randn(C), 0.2 * rng.randn(C))]
+
+
+def _modes(fn):
+    """fn() under the tiled engine (streaming kernels off) and under the deep kernels."""
+    out = []
+    for knobs in (((STREAM_KNOB, 0),), ((DEEP_KNOB, 1),)):
+        for k, v in knobs:
+            lib.dk_debug_set_gemm_config(k, v)
+        try:
+            out.append(fn())
+        finally:
+            for k, _ in knobs:
+                lib.dk_debug_set_gemm_config(k, -1)
+    return out
+
+
+def _close_sums(p0, p1):
+    s0, s1 = p0.sum(0), p1.sum(0)
+    return float((s1 - s0).norm() / max(float(s0.norm()), 1e-300)) < 1e-12
+
+
+SHAPES = [(128, 64), (128, 128), (256, 128), (256, 256), (512, 256), (512, 512), (128, 512)]  # (K, C)
+
+
+@pytest.mark.parametrize("K,C", SHAPES)
+@pytest.mark.parametrize("bn,relu,stats,stride,bias,N,H,W", [(True, 1, True, 1, False, 3, 13, 11),
+                                                           (True, 0, True, 2, False, 2, 13, 9),
+                                                           (False, 0, True, 1, True, 2, 8, 8),
+                                                           (True, 1, False, 1, False, 1, 1, 5),
+                                                           (False, 0, False, 2, True, 3, 6, 7),
+                                                           (True, 1, True, 1, False, 16, 14, 14)])
+def test_deep_fwd_matches_tiled_engine(K, C, bn, relu, stats, stride, bias, N, H, W):
+    rng = np.random.RandomState(K + C + int(bn) + 2 * relu + 4 * stats + 8 * stride + N)
+    x = nhwc(rng.randn(N, C, H, W) * 2 + 0.3)
+    w = torch.as_tensor((rng.randn(K, C) / np.sqrt(C)).astype(np.float32), device="cuda")
+    b = torch.as_tensor(rng.randn(K).astype(np.float32), device="cuda") if bias else None
+    pi = bn_params(C, rng)
+    OH, OW = -(-H // stride), -(-W // stride)
+    st = stream_handle()
+    bn_args = (*(t.data_ptr() for t in pi), relu) if bn else (0, 0, 0, 0, 0)
+
+    def run():
+        rows = lib.dk_pwconv_fwd_stats_rows(N, OH, OW, K, C)
+        part = torch.full((rows, 2, K), float("nan"), dtype=torch.float64, device="cuda") if stats else None
+        y = torch.full((N, K, OH, OW), float("nan"), device="cuda").contiguous(memory_format=torch.channels_last)
+        lib.dk_pwconv_fwd_ex_f32(x.data_ptr(), N, H, W, C, w.data_ptr(), K, stride, b.data_ptr() if bias else 0,
+                                 y.data_ptr(), OH, OW, *bn_args, part.data_ptr() if stats else 0, st)
+        torch.cuda.synchronize()
+        return y, part
+    (y0, p0), (y1, p1) = _modes(run)
+    assert torch.equal(y0, y1)
+    if stats:
+        assert _close_sums(p0, p1)
+
+
+@pytest.mark.parametrize("K,C,H", [(128, 64, 56), (256, 128, 28), (512, 256, 14), (128, 128, 9)])
+def test_deep_strided_skip_projection(K, C, H):
+    """dk_pwconv_fwd_f32 at stride 2 (the downsampling blocks' skip projections, no BN on load)."""
+    N = 3
+    rng = np.random.RandomState(K + H)
+    x = nhwc(rng.randn(N, C, H, H))
+    w = torch.as_tensor(rng.randn(K, C).astype(np.float32), device="cuda")
+    OH = -(-H // 2)
+    st = stream_handle()
+
+    def run():
+        y = torch.full((N, K, OH, OH), float("nan"), device="cuda").contiguous(memory_format=torch.channels_last)
+        lib.dk_pwconv_fwd_f32(x.data_ptr(), N, H, H, C, w.data_ptr(), K, 2, 0, y.data_ptr(), OH, OH, st)
+        torch.cuda.synchronize()
+        return y
+    y0, y1 = _modes(run)
+    assert torch.equal(y0, y1)
+
+
+@pytest.mark.parametrize("K,C", SHAPES)
+@pytest.mark.parametrize("relu,bn_in,resid,N,H,W", [(1, True, False, 3, 13, 11), (0, True, False, 2, 8, 8),
+                                                    (1, False, True, 3, 13, 11), (1, True, True, 5, 7, 9),
+                                                    (0, False, False, 1, 1, 3), (1, True, False, 16, 14, 14)])
+def test_deep_dgrad_bnbwd_matches_tiled_engine(K, C, relu, bn_in, resid, N, H, W):
+    rng = np.random.RandomState(K + C + relu + 2 * bn_in + 4 * resid + N)
+    xo = nhwc(rng.randn(N, K, H, W))
+    g = nhwc(rng.randn(N, K, H, W))
+    po = bn_params(K, rng)
+    k12 = torch.as_tensor(rng.randn(2 * K).astype(np.float32) * 0.1, device="cuda")
+    w = torch.as_tensor((rng.randn(K, C) / np.sqrt(K)).astype(np.float32), device="cuda")
+    xin = nhwc(rng.randn(N, C, H, W))
+    pi = bn_params(C, rng)
+    res = nhwc(rng.randn(N, C, H, W)) if resid else None
+    st = stream_handle()
+
+    def run():
+        rows = lib.dk_pwconv_dgrad_bnbwd_stats_rows(N, H, W, K, C)
+        dy = torch.full_like(g, float("nan"))
+        dx = torch.full_like(xin, float("nan"))
+        part = torch.full((rows, 2, C), float("nan"), dtype=torch.float64, device="cuda")
+        bn_args = (xin.data_ptr(), *(t.data_ptr() for t in pi), 1, part.data_ptr()) if bn_in else (0,) * 7
+        lib.dk_pwconv_dgrad_bnbwd_f32(g.data_ptr(), xo.data_ptr(), N, H, W, K, *(t.data_ptr() for t in po), relu,
+                                      k12.data_ptr(), dy.data_ptr(), w.data_ptr(), C, dx.data_ptr(),
+                                      res.data_ptr() if resid else 0, *bn_args, st)
+        torch.cuda.synchronize()
+        return dy, dx, part
+    (dy0, dx0, p0), (dy1, dx1, p1) = _modes(run)
+    assert torch.equal(dy0, dy1)
+    assert torch.equal(dx0, dx1)
+    if bn_in:
+        assert _close_sums(p0, p1)
+
+
+def test_deep_outputs_stay_in_bounds():
+    """A ragged pixel count (M % 32 != 0) at a deep shape: nothing is written past y, dy or dx (their
+    buffers are followed by a sentinel), and the deep path is the one taken."""
+    from dorknet_amd._hip import lib as L
+    N, H, W, K, C = 3, 7, 5, 256, 128
+    M = N * H * W
+    assert M % 32 and L.dk_pwconv_dgrad_bnbwd_stats_rows(N, H, W, K, C) > 0
+    rng = np.random.RandomState(9)
+    st = stream_handle()
+    x = nhwc(rng.randn(N, C, H, W))
+    w = torch.as_tensor(rng.randn(K, C).astype(np.float32), device="cuda")
+    pi = bn_params(C, rng)
+    ybuf = torch.full((M * K + 4096,), 12345.0, device="cuda")
+    rows = L.dk_pwconv_fwd_stats_rows(N, H, W, K, C)
+    part = torch.zeros((rows, 2, K), dtype=torch.float64, device="cuda")
+    L.dk_pwconv_fwd_ex_f32(x.data_ptr(), N, H, W, C, w.data_ptr(), K, 1, 0, ybuf.data_ptr(), H, W,
+                           *(t.data_ptr() for t in pi), 1, part.data_ptr(), st)
+    g = nhwc(rng.randn(N, K, H, W))
+    xo = nhwc(rng.randn(N, K, H, W))
+    po = bn_params(K, rng)
+    k12 = torch.as_tensor(rng.randn(2 * K).astype(np.float32) * 0.1, device="cuda")
+    dybuf = torch.full((M * K + 4096,), 12345.0, device="cuda")
+    dxbuf = torch.full((M * C + 4096,), 12345.0, device="cuda")
+    rows = L.dk_pwconv_dgrad_bnbwd_stats_rows(N, H, W, K, C)
+    partd = torch.zeros((rows, 2, C), dtype=torch.float64, device="cuda")
+    L.dk_pwconv_dgrad_bnbwd_f32(g.data_ptr(), xo.data_ptr(), N, H, W, K, *(t.data_ptr() for t in po), 1,
+                                k12.data_ptr(), dybuf.data_ptr(), w.data_ptr(), C, dxbuf.data_ptr(), 0, x.data_ptr(),
+                                *(t.data_ptr() for t in pi), 1, partd.data_ptr(), st)
+    torch.cuda.synchronize()
+    for buf, n in ((ybuf, M * K), (dybuf, M * K), (dxbuf, M * C)):
+        assert bool((buf[n:] == 12345.0).all())
+        assert bool(torch.isfinite(buf[:n]).all())
+    assert bool(torch.isfinite(part).all()) and bool(torch.isfinite(partd).all())
