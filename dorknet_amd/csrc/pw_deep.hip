@@ -30,6 +30,12 @@
 #include "dk_common.h"
 #include "fold_tail.h"
 
+// Timing experiments only (scripts/pwd_exp.sh builds variant libraries; 0 in the product build):
+// bit 0 drops the epilogue stores, bit 1 the on-load transforms, bit 3 the weight loads.
+#ifndef DK_PWD_EXP
+#define DK_PWD_EXP 0
+#endif
+
 namespace dk {
 namespace pwd {
 
@@ -135,7 +141,8 @@ __global__ __launch_bounds__(NT, fwd_wps<KR>()) void fwd_kernel(FwdArgs a) {
   // this lane's B fragments: W[col][8q + 4h + e] for every q, e (once; the weights are L2-resident)
   f32x4 bw[KQ];
 #pragma unroll
-  for (int q = 0; q < KQ; ++q) bw[q] = ld4(a.w + (size_t)col * KR + 8 * q + 4 * h);
+  for (int q = 0; q < KQ; ++q)
+    bw[q] = (DK_PWD_EXP & 8) ? f32x4{0.01f * q, 0.02f, 0.03f, (float)col} : ld4(a.w + (size_t)col * KR + 8 * q + 4 * h);
   const float bias = HB ? a.bias[col] : 0.f;
   const bool irelu = a.irelu != 0;
   // staging: lane loads float4 kv = tid % KV of rows tid / KV + j * (NT / KV): fixed channels
@@ -179,7 +186,8 @@ __global__ __launch_bounds__(NT, fwd_wps<KR>()) void fwd_kernel(FwdArgs a) {
       for (int j = 0; j < LV; ++j) {
         f32x4 v = st[j];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = __builtin_fmaxf(bn_out(v[e], mu[e], is[e], ga[e], be[e]), 0.f);
+        for (int e = 0; e < 4; ++e)
+          v[e] = (DK_PWD_EXP & 2) ? v[e] : __builtin_fmaxf(bn_out(v[e], mu[e], is[e], ga[e], be[e]), 0.f);
         st4(dst + (r0 + j * (NT / KV)) * SK + 4 * kv, v);
       }
     } else {
@@ -220,7 +228,8 @@ __global__ __launch_bounds__(NT, fwd_wps<KR>()) void fwd_kernel(FwdArgs a) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const float v = acc[r];  // (not bit_cast(acc[r]): hipcc 7.2 stored element 0 for every r)
-      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), ry, (int)eofs[r], 0, 0);
+      if (!(DK_PWD_EXP & 1))
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), ry, (int)eofs[r], 0, 0);
     }
     if constexpr (STATS) {
       if (t * TR + TR <= a.M) {  // a whole tile (uniform): no row masks
@@ -287,7 +296,7 @@ __global__ __launch_bounds__(NT, dgrad_wps<KR>()) void dgrad_kernel(DgradArgs a)
 #pragma unroll
   for (int q = 0; q < KQ; ++q)
 #pragma unroll
-    for (int e = 0; e < 4; ++e) bw[q][e] = a.w[(size_t)(8 * q + 4 * h + e) * N + col];
+    for (int e = 0; e < 4; ++e) bw[q][e] = (DK_PWD_EXP & 8) ? 0.01f * q + e : a.w[(size_t)(8 * q + 4 * h + e) * N + col];
   const int kv = tid % KV, r0 = tid / KV;
   const f32x4 mu = ld4(a.om + 4 * kv), is = ld4(a.ois + 4 * kv), ga = ld4(a.og + 4 * kv), be = ld4(a.ob + 4 * kv);
   const f32x4 k1 = ld4(a.k12 + 4 * kv), k2 = ld4(a.k12 + KR + 4 * kv);
@@ -328,7 +337,7 @@ __global__ __launch_bounds__(NT, dgrad_wps<KR>()) void dgrad_kernel(DgradArgs a)
         float ge = sg[j][e];
         const bool kill = (!(bn_out(xe, mu[e], is[e], ga[e], be[e]) > 0.f)) & orelu;
         ge = kill ? 0.f : ge;
-        v[e] = bn_bwd_elem(xe, ge, mu[e], is[e], f[e], k1[e], k2[e]);
+        v[e] = (DK_PWD_EXP & 2) ? ge + xe : bn_bwd_elem(xe, ge, mu[e], is[e], f[e], k1[e], k2[e]);
       }
       st4(dst + r * SK + 4 * kv, v);
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rdy, (int)lofs[j], 0, 0);
@@ -370,7 +379,8 @@ __global__ __launch_bounds__(NT, dgrad_wps<KR>()) void dgrad_kernel(DgradArgs a)
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const float v = acc[r];  // (not bit_cast(acc[r]): hipcc 7.2 stored element 0 for every r)
-      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), rdx, (int)eofs[r], 0, 0);
+      if (!(DK_PWD_EXP & 1))
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), rdx, (int)eofs[r], 0, 0);
     }
     if constexpr (PART) {
       const bool full = t * TR + TR <= a.M;  // a whole tile (uniform): no row masks
