@@ -18,6 +18,7 @@
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 namespace dk {
 
@@ -245,6 +246,11 @@ int pw_deep_fwd(const float* x, int N, int H, int W, int stride, int OH, int OW,
 bool pw_deep_dgrad_ok(int K, int C, int M);
 int pw_deep_dgrad_rows(int M, int K, int C);
 int pw_deep_dgrad_slices(int M, int K, int C);
+bool pw_deep_wgrad_ok(int K, int C, int M);
+int pw_deep_wgrad_chunks(int M, int K, int C);
+size_t pw_deep_wgrad_ws_bytes(int M, int K, int C);
+int pw_deep_wgrad(const float* dy, const float* x, int M, int K, int C, const float* im, const float* iis,
+                  const float* ig, const float* ib, int irelu, float* part, hipStream_t st);
 int pw_deep_dgrad_bnbwd(const float* g, const float* bn_x, int M, int K, int C, const float* om, const float* ois,
                         const float* og, const float* ob, int orelu, const float* k12, float* dy_out, const float* w,
                         float* dx, const float* res, const float* x, const float* im, const float* iis,

@@ -236,8 +236,11 @@ DK_API int dk_pwconv_dgrad_bnbwd_f32(const float* g, const float* bn_x, int N, i
 
 DK_API size_t dk_pwconv_wgrad_workspace_bytes(int N, int OH, int OW, int K, int C) {
   // (the bf16 twin's tiles can differ: the larger of the two)
-  const size_t a = splitk_ws_bytes(K, C, N * OH * OW), b = splitk_ws_bytes(K, C, N * OH * OW, kMfBf16);
-  return a > b ? a : b;
+  const int M = N * OH * OW;
+  size_t a = splitk_ws_bytes(K, C, M), b = splitk_ws_bytes(K, C, M, kMfBf16);
+  if (a < b) a = b;
+  if (pw_deep_wgrad_ok(K, C, M) && pw_deep_wgrad_ws_bytes(M, K, C) > a) a = pw_deep_wgrad_ws_bytes(M, K, C);
+  return a;
 }
 
 // dw[k][c] = sum_{n,oh,ow} dy[n,oh,ow,k] * x[n, oh*s, ow*s, c]  (+ l2 * w)   (pointwise_convolution.py:61-64)
@@ -245,7 +248,17 @@ DK_API int dk_pwconv_wgrad_f32(const float* dy, const float* x, int N, int H, in
                                int OH, int OW, const float* w_kc, float l2, float* dw_kc, void* ws, size_t ws_bytes,
                                void* stream) {
   if (C % 4 || !aligned16(x) || !fits((size_t)N * H * W * C * 4)) return DK_ERR_ARGS;
-  return wgrad(dy, img(x, N, H, W, C, OH, OW, 1, 1, stride, 1, 0, N * OH * OW), K, C, w_kc, l2, dw_kc, 0, C, C, 1, 1,
+  const int M = N * OH * OW;
+  if (stride == 1 && H == OH && W == OW && pw_deep_wgrad_ok(K, C, M) && aligned16(dy)) {
+    // the output-stationary deep kernel (pw_deep.hip): partial rows + the same fixed-order reduce
+    if (ws_bytes < pw_deep_wgrad_ws_bytes(M, K, C)) return DK_ERR_WORKSPACE;
+    float* part = static_cast<float*>(ws);
+    const hipStream_t st = as_stream(stream);
+    const int rc = pw_deep_wgrad(dy, x, M, K, C, nullptr, nullptr, nullptr, nullptr, 0, part, st);
+    if (rc) return rc;
+    return splitk_reduce(part, pw_deep_wgrad_chunks(M, K, C), K, C, dw_kc, w_kc, l2, 0, C, C, 1, 1, st);
+  }
+  return wgrad(dy, img(x, N, H, W, C, OH, OW, 1, 1, stride, 1, 0, M), K, C, w_kc, l2, dw_kc, 0, C, C, 1, 1,
                ws, ws_bytes, stream);
 }
 
@@ -255,6 +268,15 @@ DK_API int dk_pwconv_wgrad_bnx_f32(const float* dy, const float* x, int N, int H
                                    const float* bn_gamma, const float* bn_beta, int bn_relu, void* stream) {
   if (C % 4 || !aligned16(x) || !fits((size_t)N * H * W * C * 4)) return DK_ERR_ARGS;
   if (!bn_ok(bn_mean, bn_invstd, bn_gamma, bn_beta)) return DK_ERR_ARGS;
+  const int M = N * OH * OW;
+  if (stride == 1 && H == OH && W == OW && pw_deep_wgrad_ok(K, C, M) && aligned16(dy)) {
+    if (ws_bytes < pw_deep_wgrad_ws_bytes(M, K, C)) return DK_ERR_WORKSPACE;
+    float* part = static_cast<float*>(ws);
+    const hipStream_t st = as_stream(stream);
+    const int rc = pw_deep_wgrad(dy, x, M, K, C, bn_mean, bn_invstd, bn_gamma, bn_beta, bn_relu, part, st);
+    if (rc) return rc;
+    return splitk_reduce(part, pw_deep_wgrad_chunks(M, K, C), K, C, dw_kc, w_kc, l2, 0, C, C, 1, 1, st);
+  }
   return wgrad(dy,
                with_bn(img(x, N, H, W, C, OH, OW, 1, 1, stride, 1, 0, N * OH * OW), bn_mean, bn_invstd, bn_gamma,
                        bn_beta, bn_relu),

@@ -44,6 +44,7 @@ constexpr int NW = 4;        // waves per block (one 32-column MFMA block each)
 constexpr int NB = 32 * NW;  // output columns per block
 constexpr int NT = 64 * NW;  // threads per block
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
 // Waves per SIMD the registers are sized for: the B fragments take KR / 2 VGPRs per lane.
 template <int KR>
@@ -71,6 +72,15 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t tile_rsrc(const float* p, int 
 // scheduler issued each read just before its MFMAs, exposing the LDS latency every 8 MFMAs -- a
 // quarter of the MFMA time at one wave per SIMD.
 constexpr int kAD = 4;
+
+// The first row tile of walker blockIdx.x in column group blockIdx.y.  With ntiles = q G + r, the r
+// walkers that take an extra tile are rotated by a multiple of 8 per column group so that a CU's
+// blocks of different groups (ids x and x + G y) do not all take one, and walker x of every group
+// still stays on one XCD (ids congruent mod 8 when G is a multiple of 8).
+__device__ __forceinline__ int first_tile(int ntiles) {
+  const int G = gridDim.x, r = ntiles % G, s = (r + 7) & ~7;
+  return (int)((blockIdx.x + (unsigned)blockIdx.y * (unsigned)s) % (unsigned)G);
+}
 template <int KQ>
 __device__ __forceinline__ void mfma_tile(const float* ap, const f32x4* bw, f32x16& acc) {
   constexpr int D = KQ < kAD ? KQ : kAD;
@@ -138,11 +148,6 @@ __global__ __launch_bounds__(NT, fwd_wps<KR>()) void fwd_kernel(FwdArgs a) {
   const int l32 = lane & 31, h = lane >> 5;
   const int n0 = blockIdx.y * NB, N = a.N;
   const int col = n0 + 32 * wave + l32;
-  // this lane's B fragments: W[col][8q + 4h + e] for every q, e (once; the weights are L2-resident)
-  f32x4 bw[KQ];
-#pragma unroll
-  for (int q = 0; q < KQ; ++q)
-    bw[q] = (DK_PWD_EXP & 8) ? f32x4{0.01f * q, 0.02f, 0.03f, (float)col} : ld4(a.w + (size_t)col * KR + 8 * q + 4 * h);
   const float bias = HB ? a.bias[col] : 0.f;
   const bool irelu = a.irelu != 0;
   // staging: lane loads float4 kv = tid % KV of rows tid / KV + j * (NT / KV): fixed channels
@@ -203,10 +208,17 @@ __global__ __launch_bounds__(NT, fwd_wps<KR>()) void fwd_kernel(FwdArgs a) {
     }
   };
 
-  int t = blockIdx.x;
+  int t = first_tile(ntiles);
+  f32x4 bw[KQ];
   {
     f32x4 st[LV];
     load_tile(t, st);
+    // this lane's B fragments, W[col][8q + 4h + e] for every q, e, loaded once after the first tile's
+    // pixels: staging waits only for those, and the first tile's MFMAs for each fragment in turn, so
+    // the weight loads (L2-resident; 32-128 KB per block) overlap the first tile's work
+#pragma unroll
+    for (int q = 0; q < KQ; ++q)
+      bw[q] = (DK_PWD_EXP & 8) ? f32x4{0.01f * q, 0.02f, 0.03f, (float)col} : ld4(a.w + (size_t)col * KR + 8 * q + 4 * h);
     stage(&As[0][0], st);
   }
   __syncthreads();
@@ -291,12 +303,6 @@ __global__ __launch_bounds__(NT, dgrad_wps<KR>()) void dgrad_kernel(DgradArgs a)
   const int l32 = lane & 31, h = lane >> 5;
   const int n0 = blockIdx.y * NB, N = a.N;
   const int col = n0 + 32 * wave + l32;
-  // B fragments: W[8q + 4h + e][col]
-  f32x4 bw[KQ];
-#pragma unroll
-  for (int q = 0; q < KQ; ++q)
-#pragma unroll
-    for (int e = 0; e < 4; ++e) bw[q][e] = (DK_PWD_EXP & 8) ? 0.01f * q + e : a.w[(size_t)(8 * q + 4 * h + e) * N + col];
   const int kv = tid % KV, r0 = tid / KV;
   const f32x4 mu = ld4(a.om + 4 * kv), is = ld4(a.ois + 4 * kv), ga = ld4(a.og + 4 * kv), be = ld4(a.ob + 4 * kv);
   const f32x4 k1 = ld4(a.k12 + 4 * kv), k2 = ld4(a.k12 + KR + 4 * kv);
@@ -344,10 +350,16 @@ __global__ __launch_bounds__(NT, dgrad_wps<KR>()) void dgrad_kernel(DgradArgs a)
     }
   };
 
-  int t = blockIdx.x;
+  int t = first_tile(ntiles);
+  f32x4 bw[KQ];
   {
     f32x4 sg[LV], sx[LV];
     load_tile(t, sg, sx);
+    // B fragments W[8q + 4h + e][col], after the first tile's loads (as the forward)
+#pragma unroll
+    for (int q = 0; q < KQ; ++q)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) bw[q][e] = (DK_PWD_EXP & 8) ? 0.01f * q + e : a.w[(size_t)(8 * q + 4 * h + e) * N + col];
     stage(t, &As[0][0], sg, sx);
   }
   __syncthreads();
@@ -400,6 +412,195 @@ __global__ __launch_bounds__(NT, dgrad_wps<KR>()) void dgrad_kernel(DgradArgs a)
     buf ^= 1;
   }
   if constexpr (PART) partial_row(ps, pq, a.part, N, n0, a.ft, &As[0][0]);
+}
+
+// ---------------------------------------------------------------------------------------
+// Weight gradient (layers/pointwise_convolution.py:61-64): dW[k][c] = sum_m dy[m][k] xh[m][c] with
+// xh = the input BatchNorm (+ReLU) applied on load (bn_out, as the forward).  Output-stationary
+// waves: a wave owns a TK x TC block of dW -- (TK / 32) x (TC / 32) accumulator tiles, up to 256
+// AGPRs at one wave per SIMD -- and streams its own contiguous run of pixel pairs, each pair one
+// v_mfma_f32_32x32x2_f32 k-step.  The tiles are interleaved so that both operands come straight
+// from global memory in one 16-byte (or 8-byte) load per lane: lane (i, h) loads dy[2p + h][k0 +
+// TKQ i .. + TKQ) and x[2p + h][c0 + TCQ i .. + TCQ), and element a (b) of those is row i of k-tile
+// a (column i of c-tile b): k = k0 + TKQ i + a, c = c0 + TCQ j + b.  Every operand element is
+// loaded and transformed by exactly one lane (no LDS staging, no barriers in the loop), loads run
+// kWD pairs ahead in a register ring; the BN on load is packed fp32 arithmetic (v_pk_*), bitwise
+// bn_out.  The block's 4 waves split one dW block's pixel run four ways and add their tiles in
+// LDS (fixed order) into one partial row; the partial rows go through splitk_reduce (fp64, + l2 w).
+// ---------------------------------------------------------------------------------------
+constexpr int kWD = 8;  // pixel pairs in flight per wave
+
+struct WgradArgs {
+  const float* dy;  // [M][K]
+  const float* x;   // [M][C] (the input BN's raw input when BN)
+  const float *im, *iis, *ig, *ib;
+  int irelu;
+  float* part;      // [chunks][K][C]
+  int M, K, C, chunks;
+};
+
+template <int Q>
+struct VecOf;
+template <>
+struct VecOf<2> {
+  typedef f32x2 T;
+  static __device__ __forceinline__ T load(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b64(r, (int)off, 0, 0));
+  }
+};
+template <>
+struct VecOf<4> {
+  typedef f32x4 T;
+  static __device__ __forceinline__ T load(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0));
+  }
+};
+
+template <int TKQ, int TCQ>
+constexpr int wgrad_lds_floats() {
+  return 2 * (32 * TKQ) * (32 * TCQ + 4);
+}
+
+template <int TKQ, int TCQ, bool BN, bool RELU>
+__global__ __launch_bounds__(NT, 1) void wgrad_kernel(WgradArgs a) {
+  constexpr int TK = 32 * TKQ, TC = 32 * TCQ, SR = TC + 4;  // LDS row stride (floats)
+  typedef typename VecOf<TKQ>::T AV;
+  typedef typename VecOf<TCQ>::T BV;
+  extern __shared__ __attribute__((aligned(16))) float red[];  // [2][TK][SR]
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int l32 = lane & 31, h = lane >> 5;
+  const int K = a.K, C = a.C, tiles_c = C / TC, ntiles = (K / TK) * tiles_c;
+  // block -> (dW block, pixel chunk): chunk % 8 follows blockIdx % 8, so every dW block of one
+  // pixel chunk runs on one XCD and shares its L2 copy of the chunk's dy and x
+  const int id = blockIdx.x, rest = id >> 3;
+  const int tile = rest % ntiles, chunk = (id & 7) + 8 * (rest / ntiles);
+  const int k0 = (tile / tiles_c) * TK, c0 = (tile % tiles_c) * TC;
+  // this wave's pixel pairs [pb, pe)
+  const int npairs = (a.M + 1) >> 1, nsub = a.chunks * 4, sub = chunk * 4 + wave;
+  const int pb = (int)((long long)npairs * sub / nsub), pe = (int)((long long)npairs * (sub + 1) / nsub);
+  const uint32_t aoff = (uint32_t)(h * K + k0 + TKQ * l32) * 4u, boff = (uint32_t)(h * C + c0 + TCQ * l32) * 4u;
+  BV mu, is, ga, be;
+  if constexpr (BN) {
+#pragma unroll
+    for (int e = 0; e < TCQ; ++e) {
+      const int c = c0 + TCQ * l32 + e;
+      mu[e] = a.im[c];
+      is[e] = a.iis[c];
+      ga[e] = a.ig[c];
+      be[e] = a.ib[c];
+    }
+  }
+  // pair p's operands: one resource per tensor (range-checked: a ragged last pixel reads zeros),
+  // the pair's row offset added to the lane offset; pairs past pe read zeros (offset past any
+  // tensor), so they add nothing
+  const __amdgpu_buffer_rsrc_t rdy = make_rsrc_v(a.dy, (uint32_t)a.M * K * 4u);
+  const __amdgpu_buffer_rsrc_t rx = make_rsrc_v(a.x, (uint32_t)a.M * C * 4u);
+  auto load_pair = [&](int p, AV& av, BV& bv) __attribute__((always_inline)) {
+    const bool ok = p < pe;
+    const uint32_t oa = ok ? (uint32_t)p * (uint32_t)(2 * K * 4) : kOOBBytes;
+    const uint32_t ob = ok ? (uint32_t)p * (uint32_t)(2 * C * 4) : kOOBBytes;
+    av = VecOf<TKQ>::load(rdy, aoff + oa);
+    bv = VecOf<TCQ>::load(rx, boff + ob);
+  };
+  f32x16 acc[TKQ][TCQ];
+#pragma unroll
+  for (int i = 0; i < TKQ; ++i)
+#pragma unroll
+    for (int j = 0; j < TCQ; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  AV ra[kWD];
+  BV rb[kWD];
+  // (issued in ring order: the waitcnt pass merges this order with the loop's at the loop head,
+  // and a reordered prologue made it wait for every load there, every iteration)
+#pragma unroll
+  for (int s = 0; s < kWD; ++s) {
+    load_pair(pb + s, ra[s], rb[s]);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  for (int p = pb; p < pe; p += kWD) {
+#pragma unroll
+    for (int s = 0; s < kWD; ++s) {
+      const AV av = ra[s];
+      BV bv = rb[s];
+      if constexpr (BN) {
+        // bn_out elementwise in packed pairs: ((x - mean) * invstd) then fma(gamma, xh, beta)
+#pragma unroll
+        for (int e = 0; e < TCQ; e += 2) {
+          const f32x2 xv = {bv[e], bv[e + 1]}, m2 = {mu[e], mu[e + 1]}, i2 = {is[e], is[e + 1]};
+          const f32x2 g2 = {ga[e], ga[e + 1]}, b2 = {be[e], be[e + 1]};
+          const f32x2 xh = (xv - m2) * i2;
+          const f32x2 o = __builtin_elementwise_fma(g2, xh, b2);
+          bv[e] = o[0];
+          bv[e + 1] = o[1];
+        }
+        if constexpr (RELU) {
+#pragma unroll
+          for (int e = 0; e < TCQ; ++e) bv[e] = __builtin_fmaxf(bv[e], 0.f);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = 0; i < TKQ; ++i)
+#pragma unroll
+        for (int j = 0; j < TCQ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i], bv[j], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      // refill the ring slot once its operands are consumed (in place: loading it before the
+      // MFMAs made the compiler rotate the ring through copies that waited for every load)
+      load_pair(p + s + kWD, ra[s], rb[s]);
+    }
+  }
+  // the block's 4 partial tiles added in LDS: (w0 + w2) + (w1 + w3); element (i, j, r) of a lane
+  // is dW[k0 + TKQ (8 (r >> 2) + 4h + (r & 3)) + i][c0 + TCQ l32 + j].  The lane's base offsets are
+  // pinned here (asm barrier) so the per-element addresses stay base + constant: hoisted above the
+  // loop they took ~100 VGPRs and the 4 x 4 variant spilled.
+  int lb = TKQ * 4 * h * SR + TCQ * l32;
+  uint32_t gofs = (uint32_t)((k0 + TKQ * 4 * h) * C + c0 + TCQ * l32) * 4u;
+  asm volatile("" : "+v"(lb), "+v"(gofs));
+  auto tile_io = [&](float* base, bool add, bool store) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < TKQ; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        float* q = base + lb + (TKQ * (8 * (r >> 2) + (r & 3)) + i) * SR;
+        if (store) {
+          BV v;
+#pragma unroll
+          for (int j = 0; j < TCQ; ++j) v[j] = acc[i][j][r];
+          *reinterpret_cast<BV*>(q) = v;
+        } else {
+          const BV v = *reinterpret_cast<const BV*>(q);
+#pragma unroll
+          for (int j = 0; j < TCQ; ++j) acc[i][j][r] = add ? acc[i][j][r] + v[j] : v[j];
+        }
+        __builtin_amdgcn_sched_barrier(0);  // one row at a time
+      }
+  };
+  if (wave >= 2) tile_io(red + (wave - 2) * TK * SR, false, true);
+  __syncthreads();
+  if (wave < 2) tile_io(red + wave * TK * SR, true, false);
+  __syncthreads();
+  if (wave == 1) tile_io(red, false, true);
+  __syncthreads();
+  if (wave == 0) {
+    tile_io(red, true, false);
+    const __amdgpu_buffer_rsrc_t rp = make_rsrc_v(a.part + (size_t)chunk * K * C, (uint32_t)K * C * 4u);
+#pragma unroll
+    for (int i = 0; i < TKQ; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int dk = TKQ * (8 * (r >> 2) + (r & 3)) + i;
+        BV v;
+#pragma unroll
+        for (int j = 0; j < TCQ; ++j) v[j] = acc[i][j][r];
+        if constexpr (TCQ == 4)
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rp, (int)gofs, dk * C * 4, 0);
+        else
+          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), rp, (int)gofs, dk * C * 4, 0);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+  }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -501,6 +702,60 @@ int pw_deep_dgrad_rows(int M, int K, int C) {
   return 0;
 }
 int pw_deep_dgrad_slices(int M, int K, int C) { return C / pwd::NB; }
+
+// Weight gradient: K, C multiples of the dW block (TK = 128 when K >= 128, else 64; TC likewise),
+// stride 1, at least 128 channels on one side; chunks = pixel chunks per dW block (a multiple of
+// 8, about one wave per SIMD in all).
+static int wg_q(int n) { return n >= 128 ? 4 : 2; }
+bool pw_deep_wgrad_ok(int K, int C, int M) {
+  if (!pwd_enabled() || M <= 1 || (K < 128 && C < 128) || K % 64 || C % 64 || K > 1024 || C > 1024) return false;
+  if (K % (32 * wg_q(K)) || C % (32 * wg_q(C))) return false;
+  return (size_t)M * (K > C ? K : C) * 4 < ((size_t)1 << 31);
+}
+int pw_deep_wgrad_chunks(int M, int K, int C) {
+  const int ntiles = (K / (32 * wg_q(K))) * (C / (32 * wg_q(C)));
+  int ch = 256 / ntiles;
+  ch = ch < 8 ? 8 : ch / 8 * 8;
+  // at least a few pixel pairs per wave
+  while (ch > 8 && (long long)ch * 4 * 16 > (M + 1) / 2) ch -= 8;
+  return ch;
+}
+size_t pw_deep_wgrad_ws_bytes(int M, int K, int C) {
+  return (size_t)pw_deep_wgrad_chunks(M, K, C) * K * C * sizeof(float);
+}
+
+int pw_deep_wgrad(const float* dy, const float* x, int M, int K, int C, const float* im, const float* iis,
+                  const float* ig, const float* ib, int irelu, float* part, hipStream_t st) {
+  const int chunks = pw_deep_wgrad_chunks(M, K, C);
+  pwd::WgradArgs a{dy, x, im, iis, ig, ib, irelu, part, M, K, C, chunks};
+  const int tkq = wg_q(K), tcq = wg_q(C);
+  const int ntiles = (K / (32 * tkq)) * (C / (32 * tcq));
+  const dim3 grid((unsigned)(ntiles * chunks));
+#define DK_WG(TKQ_, TCQ_)                                                                                         \
+  if (tkq == TKQ_ && tcq == TCQ_) {                                                                               \
+    const size_t lds = sizeof(float) * pwd::wgrad_lds_floats<TKQ_, TCQ_>();                                        \
+    const void* fs[3] = {reinterpret_cast<const void*>(&pwd::wgrad_kernel<TKQ_, TCQ_, false, false>),              \
+                         reinterpret_cast<const void*>(&pwd::wgrad_kernel<TKQ_, TCQ_, true, false>),               \
+                         reinterpret_cast<const void*>(&pwd::wgrad_kernel<TKQ_, TCQ_, true, true>)};               \
+    static const bool attr = [&] {                                                                                \
+      for (const void* f : fs) (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); \
+      return true;                                                                                                \
+    }();                                                                                                          \
+    (void)attr;                                                                                                   \
+    if (im && irelu)                                                                                              \
+      hipLaunchKernelGGL((pwd::wgrad_kernel<TKQ_, TCQ_, true, true>), grid, dim3(pwd::NT), lds, st, a);           \
+    else if (im)                                                                                                  \
+      hipLaunchKernelGGL((pwd::wgrad_kernel<TKQ_, TCQ_, true, false>), grid, dim3(pwd::NT), lds, st, a);          \
+    else                                                                                                          \
+      hipLaunchKernelGGL((pwd::wgrad_kernel<TKQ_, TCQ_, false, false>), grid, dim3(pwd::NT), lds, st, a);         \
+    return launch_status();                                                                                       \
+  }
+  DK_WG(4, 4)
+  DK_WG(4, 2)
+  DK_WG(2, 4)
+#undef DK_WG
+  return DK_ERR_ARGS;
+}
 
 int pw_deep_fwd(const float* x, int N, int H, int W, int stride, int OH, int OW, const float* w, int K, int C,
                 const float* bias, float* y, const float* im, const float* iis, const float* ig, const float* ib,

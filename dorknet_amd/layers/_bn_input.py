@@ -10,6 +10,11 @@ results are bit-identical to running the layers one by one -- the normalised act
 just never exists in HBM (forward and weight-gradient passes recompute it on load).
 
 Anything that cannot consume it calls ``materialize()`` (one dk_bn_apply_f32 pass).
+
+Aliasing: ``mean`` / ``invstd`` are the owning BatchNormLayer's per-layer buffers (and, in test
+mode, its running statistics), which that layer's next forward rewrites in place.  A BNOut is
+therefore valid until its owner's next forward: ``bn_args()`` and ``materialize()`` raise on a
+stale one (a per-layer generation counter) instead of silently reading the newer statistics.
 """
 from __future__ import annotations
 
@@ -20,7 +25,7 @@ from .._tensor import empty_nhwc, is_nhwc, to_nhwc
 
 
 class BNOut:
-    __slots__ = ("x", "mean", "invstd", "gamma", "beta", "relu", "owner", "_y")
+    __slots__ = ("x", "mean", "invstd", "gamma", "beta", "relu", "owner", "_y", "gen")
 
     def __init__(self, x, mean, invstd, gamma, beta, relu, owner=None):
         self.x = x            # raw input of the BatchNormLayer (NHWC storage, logical NCHW)
@@ -31,6 +36,12 @@ class BNOut:
         self.relu = bool(relu)
         self.owner = owner    # the BatchNormLayer (its backward can take partial sums, see below)
         self._y = None
+        self.gen = getattr(owner, "_dk_gen", 0)  # the owner's forward this record belongs to
+
+    def _check_current(self):
+        if self.owner is not None and getattr(self.owner, "_dk_gen", 0) != self.gen:
+            raise RuntimeError("BNOut of {} used after that layer's next forward: its mean / invstd buffers "
+                               "now hold the newer batch's statistics".format(self.owner.layer_name))
 
     @property
     def shape(self):
@@ -49,6 +60,7 @@ class BNOut:
 
     def bn_args(self):
         """(mean, invstd, gamma, beta, relu) for a dk_*_bnx_f32 call."""
+        self._check_current()
         return (self.mean.data_ptr(), self.invstd.data_ptr(), self.gamma.data_ptr(), self.beta.data_ptr(),
                 int(self.relu))
 
@@ -76,6 +88,7 @@ class BNOut:
     def materialize(self):
         """The normalised tensor itself (computed once)."""
         if self._y is None:
+            self._check_current()
             x = self.x
             y = empty_nhwc(*x.shape, dtype=x.dtype) if x.dim() == 4 else torch.empty_like(x)
             apply = lib.dk_bn_apply_bf16 if x.dtype == torch.bfloat16 else lib.dk_bn_apply_f32

@@ -205,6 +205,11 @@ class BatchNormLayer(Layer):
         self.input_shape = tuple(x.shape)
         self._pending_bwd = None
         if not test_mode:
+            # mean / std / invstd are this layer's persistent buffers (_persist), and the running
+            # statistics are updated in place, by every training forward: self.std, and the BNOut /
+            # BNGrad records of an earlier forward, alias them.  The generation counter lets BNOut
+            # detect a stale use (layers/_bn_input.py); a test-mode forward rewrites neither.
+            self._dk_gen = getattr(self, "_dk_gen", 0) + 1
             mean, std, invstd = self._stats(x, P, C, st, stats)
             self.X = x
             self._mean, self._invstd = mean, invstd

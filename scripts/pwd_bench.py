@@ -1,9 +1,10 @@
 """fp32 deep pointwise layers of config 3 (batch 256): the deep streaming kernels (pw_deep.hip,
 knob 11 on) against the previous path (knob 11 off: the tiled engine, or pw_stream.hip's K = C = 128
-forward), forward with BN on load + statistics, the strided skip projections, and the
-BN-backward-on-load dgrad with dy write-through and the input BN's partials.  Median of 15 calls,
+forward), forward with BN on load + statistics, the strided skip projections, the
+BN-backward-on-load dgrad with dy write-through and the input BN's partials, and the BN-on-load
+weight gradient (with its split reduce).  Median of 15 calls,
 fraction of the fp32 MFMA peak (157.3 TF/s); outputs of the two paths compared bitwise.
-    python scripts/pwd_bench.py [--only fwd|skip|dgrad] [--shape HW,C,K] [--deep 0|1]
+    python scripts/pwd_bench.py [--only fwd|skip|dgrad|wgrad] [--shape HW,C,K] [--deep 0|1]
 """
 import os
 import sys
@@ -55,7 +56,7 @@ def main():
         po = [rnd(K), rnd(K).abs() + 0.5, rnd(K), rnd(K)]
         k12 = rnd(2 * K) * 0.1
         flops = 2.0 * M * K * C
-        res, outs = [], {}
+        res, outs, wout = [], {}, {}
         for deep in modes:
             lib.dk_debug_set_gemm_config(11, deep)
             y = torch.full((M * K,), float("nan"), device="cuda")
@@ -77,12 +78,25 @@ def main():
                       1, partd.data_ptr(), st)
                 td = timeit(lambda: lib.dk_pwconv_dgrad_bnbwd_f32(*da))
                 line.append(f"dgrad {td:6.1f} us {flops / td / 1e6 / PEAK:4.2f}")
+            if only in (None, "wgrad"):
+                nb = lib.dk_pwconv_wgrad_workspace_bytes(B, HW, HW, K, C)
+                ws = torch.empty(nb // 4 + 1, device="cuda")
+                dw = torch.empty(K * C, device="cuda")
+                wa = (g.data_ptr(), x.data_ptr(), B, HW, HW, C, K, 1, HW, HW, w.data_ptr(), 1e-4, dw.data_ptr(),
+                      ws.data_ptr(), nb, *(t.data_ptr() for t in pi), 1, st)
+                tw = timeit(lambda: lib.dk_pwconv_wgrad_bnx_f32(*wa))
+                line.append(f"wgrad {tw:6.1f} us {flops / tw / 1e6 / PEAK:4.2f}")
+                torch.cuda.synchronize()
+                wout[deep] = dw.clone()
             torch.cuda.synchronize()
             outs[deep] = (y.clone(), dy.clone(), dx.clone())
             res.append(("deep " if deep else "old  ") + ", ".join(line))
         lib.dk_debug_set_gemm_config(11, -1)
         same = ["bitwise" if torch.equal(a, b) else "DIFF(max %.2e)" % float((a - b).abs().nan_to_num(1e30).max())
                 for a, b in zip(outs[0], outs[1])] if len(outs) == 2 else []
+        if len(wout) == 2:
+            a, b = wout[0].double(), wout[1].double()
+            same.append("dW rel %.1e" % float((a - b).norm() / a.norm()))
         print(f"{B}x{HW}x{HW} C={C:3d} K={K:3d} | " + " | ".join(res) + " | y/dy/dx " + " ".join(same), flush=True)
     if only in (None, "skip") and "--shape" not in sys.argv:
         for H, C, K in SKIPS:

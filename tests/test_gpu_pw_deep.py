@@ -165,3 +165,60 @@ def test_deep_outputs_stay_in_bounds():
         assert bool((buf[n:] == 12345.0).all())
         assert bool(torch.isfinite(buf[:n]).all())
     assert bool(torch.isfinite(part).all()) and bool(torch.isfinite(partd).all())
+
+
+WGRAD_SHAPES = [(128, 64), (128, 128), (256, 128), (128, 256), (256, 256), (512, 512)]  # (K, C)
+
+
+@pytest.mark.parametrize("K,C", WGRAD_SHAPES)
+@pytest.mark.parametrize("bn,relu,N,H,W", [(True, 1, 3, 13, 11), (True, 0, 2, 8, 8), (False, 0, 1, 1, 5),
+                                           (True, 1, 16, 14, 14)])
+def test_deep_wgrad_matches_fp64(K, C, bn, relu, N, H, W):
+    """dk_pwconv_wgrad_bnx_f32 / dk_pwconv_wgrad_f32 on the deep output-stationary kernel (knob 11 on)
+    against an fp64 dW = dy^T relu(bn(x)) + l2 w, elementwise within 3e-5 of sum |dy| |xh| (fp32
+    partial sums of a few hundred products each, then the fp64 reduce), and against the tiled engine
+    (knob 11 off) within the same bound."""
+    rng = np.random.RandomState(K + 3 * C + N + int(bn) + 2 * relu)
+    M = N * H * W
+    dy = nhwc(rng.randn(N, K, H, W))
+    x = nhwc(rng.randn(N, C, H, W) * 1.5 + 0.2)
+    w = torch.as_tensor(rng.randn(K, C).astype(np.float32), device="cuda")
+    pi = bn_params(C, rng)
+    l2 = 1e-3
+    st = stream_handle()
+    nb = lib.dk_pwconv_wgrad_workspace_bytes(N, H, W, K, C)
+    ws = torch.empty(max(nb, 4) // 4 + 1, dtype=torch.float32, device="cuda")
+
+    def run():
+        dw = torch.full((K, C), float("nan"), device="cuda")
+        if bn:
+            rc = lib.dk_pwconv_wgrad_bnx_f32(dy.data_ptr(), x.data_ptr(), N, H, W, C, K, 1, H, W, w.data_ptr(), l2,
+                                             dw.data_ptr(), ws.data_ptr(), nb, *(t.data_ptr() for t in pi), relu, st)
+        else:
+            rc = lib.dk_pwconv_wgrad_f32(dy.data_ptr(), x.data_ptr(), N, H, W, C, K, 1, H, W, w.data_ptr(), l2,
+                                         dw.data_ptr(), ws.data_ptr(), nb, st)
+        assert rc == 0
+        torch.cuda.synchronize()
+        return dw
+    outs = []
+    for knob in (0, 1):
+        lib.dk_debug_set_gemm_config(DEEP_KNOB, knob)
+        try:
+            outs.append(run())
+        finally:
+            lib.dk_debug_set_gemm_config(DEEP_KNOB, -1)
+    dy64 = dy.permute(0, 2, 3, 1).reshape(M, K).double()
+    x64 = x.permute(0, 2, 3, 1).reshape(M, C).double()
+    if bn:
+        # the kernels' fp32 bn_out (up to the fma's last bit), then exact products
+        xf = x.permute(0, 2, 3, 1).reshape(M, C)
+        xh = (pi[2] * ((xf - pi[0]) * pi[1]) + pi[3]).double()
+        if relu:
+            xh = xh.clamp_min(0.0)
+    else:
+        xh = x64
+    ref = dy64.t() @ xh + l2 * w.double()
+    bound = 3e-5 * (dy64.abs().t() @ xh.abs()) + 1e-6
+    for dw in outs:
+        assert bool(torch.isfinite(dw).all())
+        assert bool(((dw.double() - ref).abs() <= bound).all()), float(((dw.double() - ref).abs() / bound).max())
