@@ -190,11 +190,20 @@ ENTRY_KERNEL = {
     # (prefix, regex): the GEMM instantiations whose A operand is the K-contiguous matrix
     # loader applying a BN backward (dgrad); the stem's weight gradient applies one on its
     # row-contiguous loader (LdMatICT) and is a different entry point
-    "dk_pwconv_dgrad_bnbwd_f32": ("dk::igemm_f32", r"dk::LdMatKCT<[^>]*>, dk::MatBwdDesc"),
+    # (and the deep kernel, pw_deep.hip)
+    "dk_pwconv_dgrad_bnbwd_f32": [("dk::igemm_f32", r"dk::LdMatKCT<[^>]*>, dk::MatBwdDesc"),
+                                  ("dk::pwd::dgrad_kernel", "")],
     # the pointwise forward with output statistics: the tiled engine's instantiations (1x1 image
-    # view, statistics epilogue) and the streaming K = C = 64 kernel
+    # view, statistics epilogue), the streaming K = C = 64 kernel and the deep kernels with
+    # statistics (STATS = true; the strided skip projections are dk_pwconv_fwd_f32)
     "dk_pwconv_fwd_ex_f32": [("dk::igemm_f32", r"Img(Bn)?DescE<float, true>.*EpStoreStatsT<float>"),
-                             ("dk::pws::fwd_kernel", "")],
+                             ("dk::pws::fwd_kernel", ""), ("dk::pwd::fwd_kernel", r"^dk::pwd::fwd_kernel<\d+, \w+, true")],
+    # config 5 (bf16 storage): the BN-backward-on-load pointwise dgrad (streaming K = C = 64 and deep
+    # kernels, the tiled engine elsewhere), the fused depthwise backward and the depthwise forward
+    "dk_pwconv_dgrad_bnbwd_bf16": [("dk::pwsh::dgrad_bnbwd_kernel", ""), ("dk::pwsh::dgrad_deep_kernel", ""),
+                                   ("dk::igemm_f32", r"dk::LdMatKCT<[^>]*>, dk::MatBwdDescE<unsigned short>")],
+    "dk_dwconv_bwd_bnbwd_bf16": ("dk::dw_bwd_fused_kernel", r"unsigned short>"),
+    "dk_dwconv_fwd_ex_bf16": ("dk::dw_fwd_kernel", r"unsigned short>"),
     "dk_conv2d_fwd_narrow_f32": ("dk::nar::fwd_kernel", ""),
     "dk_conv2d_wgrad_bnbwd_narrow_f32": ("dk::nar::wgrad_kernel", ""),
 }
@@ -238,26 +247,27 @@ def stream_ceiling(entry):
 
 
 def pmc_traffic(entry, path):
-    """Average HBM bytes per dispatch of `entry`'s kernel from a committed PMC summary, or
-    (None, None) when there is none for it."""
+    """Average HBM bytes per dispatch of `entry`'s kernel from a committed PMC summary (`path`, or
+    the newest profiles/*_pmc.json that has the kernel), or (None, None) when there is none."""
     import glob
-    if path is None:
-        cands = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")))
-        path = cands[-1] if cands else None
     kern = ENTRY_KERNEL.get(entry)
-    if not path or not kern or not os.path.exists(path):
+    if not kern:
         return None, None
-    with open(path) as f:
-        d = json.load(f)
-    n = t = 0
+    cands = [path] if path else sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")), reverse=True)
     pats = kern if isinstance(kern, list) else [kern if isinstance(kern, tuple) else (kern, "")]
-    for name, v in d.get("kernels", {}).items():
-        if any((name.startswith(pre + "<") or name == pre) and re.search(sub, name) for pre, sub in pats):
-            n += v["dispatches"]
-            t += v["traffic_bytes"] * v["dispatches"]
-    if n == 0:
-        return None, None
-    return t / n, os.path.relpath(path, ROOT)
+    for p in cands:
+        if not p or not os.path.exists(p):
+            continue
+        with open(p) as f:
+            d = json.load(f)
+        n = t = 0
+        for name, v in d.get("kernels", {}).items():
+            if any((name.startswith(pre + "<") or name == pre) and re.search(sub, name) for pre, sub in pats):
+                n += v["dispatches"]
+                t += v["traffic_bytes"] * v["dispatches"]
+        if n:
+            return t / n, os.path.relpath(p, ROOT)
+    return None, None
 
 
 def cpu_info():

@@ -41,6 +41,12 @@ __device__ __forceinline__ f32x4 mfma16(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
+// ih mod R for input rows ih >= -R (the padding rows above the image)
+template <int R>
+__device__ __forceinline__ int ring_slot(int ih) {
+  return (ih + R * 4) % R;
+}
+
 // The R x C input rows an output row (n, oh) reads: thread = staged column (Wp <= 256), one
 // register per (c, r) -- loaded for the next row while the current row's MFMAs run, stored
 // to LDS row (c * R + r) after the row's barrier.  Zero outside the image.
@@ -72,6 +78,38 @@ struct RowStage {
     for (int c = 0; c < C; ++c)
 #pragma unroll
       for (int r = 0; r < R; ++r) xin[(c * R + r) * g.CS + threadIdx.x] = v[c][r];
+  }
+  // Ring variant (the weight gradient): channel c's input row ih sits in LDS row c * R + (ih mod R),
+  // so an output row of the same image stages only its ST new rows (window rows R - ST .. R - 1)
+  // instead of all R; a block's first row, or the first row of a new image, stages all R.  Rows
+  // left out read nothing (offset past the buffer) and are not stored.  The window wraps in the
+  // ring: the per-k offsets are rebuilt per output row.
+  __device__ __forceinline__ void load_ring(const float* __restrict__ x, const Geo& g, int n, int oh, bool full) {
+    const __amdgpu_buffer_rsrc_t rsx = make_rsrc_v(x, (uint32_t)((size_t)g.N * C * g.H * g.W * 4));
+    const int iw = (int)threadIdx.x - g.pad;
+    const bool wok = (int)threadIdx.x < g.Wp && (unsigned)iw < (unsigned)g.W;
+    const int voff = wok ? iw * 4 : (int)kOOBBytes;
+    const int ih0 = ST * oh - g.pad;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const bool rok = (full || r >= R - ST) && (unsigned)(ih0 + r) < (unsigned)g.H;  // uniform
+      const int vo = rok ? voff : (int)kOOBBytes;
+#pragma unroll
+      for (int c = 0; c < C; ++c)
+        v[c][r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                rsx, vo, rok ? (((n * C + c) * g.H + ih0 + r) * g.W) * 4 : 0, 0));
+    }
+  }
+  __device__ __forceinline__ void store_ring(float* xin, const Geo& g, int oh, bool full) const {
+    if ((int)threadIdx.x >= g.Wp) return;
+    const int sb = ring_slot<R>(ST * oh - g.pad);
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      if (!full && r < R - ST) continue;  // (uniform)
+      const int slot = sb + r >= R ? sb + r - R : sb + r;
+#pragma unroll
+      for (int c = 0; c < C; ++c) xin[(c * R + slot) * g.CS + threadIdx.x] = v[c][r];
+    }
   }
 };
 
@@ -107,6 +145,9 @@ __global__ __launch_bounds__(NT, 2) void fwd_kernel(const float* __restrict__ x,
   const int blk = xcd_block(blockIdx.x, gridDim.x);  // consecutive row runs share an XCD's L2
   const int r0 = blk * g.rpb, r1 = min(g.rows, r0 + g.rpb);
   RowStage<C, R, ST> rs;
+  // (all R rows restaged per output row: a ring of the rows, as the weight gradient's, measured
+  // 3-6 % slower here -- profiles/r04p_stem_ab.txt -- the per-row offset shift costs more than the
+  // loads it saves)
   if (r0 < r1) rs.load(x, g, r0 / g.OH, r0 % g.OH);
   const float* const xl = xin + ST * li;
   for (int row = r0; row < r1; ++row) {
@@ -225,18 +266,26 @@ __global__ __launch_bounds__(NT, 3) void wgrad_kernel(DyIn d, const float* __res
                                                       float* __restrict__ ws) {
   constexpr int KRED = C * R * S, NTN = (KRED + 15) / 16;
   extern __shared__ float smem[];
-  float* const xin = smem;  // (C*R + 1) rows x CS
+  float* const xin = smem;  // (C + 1) * R rows x CS: the ring, then R zero rows
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  float* const at = smem + (C * R + 1) * g.CS + wave * QC * 64 + lane;  // A table: [wave][q][lane]
+  float* const at = smem + (C + 1) * R * g.CS + wave * QC * 64 + lane;  // A table: [wave][q][lane]
   const int li = lane & 15, lg = lane >> 4;
   const int filt = 16 * wave + li;  // this lane's filter (A row)
   const int voff = filt < g.K ? (lg * g.K + filt) * 4 : (int)kOOBBytes;
   // lattice g: lanes of odd pixels (lg odd) read nothing; even ones the compact pixel lg / 2
   const int voffg = d.lat == 1 ? voff : ((filt < g.K && !(lg & 1)) ? ((lg >> 1) * g.K + filt) * 4 : (int)kOOBBytes);
-  int offn[NTN];
+  // B column n = 16 nt + li is k = (c, r, s): staged row c * R + ((ih0 + r) mod R) (single ring,
+  // RowStage::store_ring<false>): offset = lo + sb * CS, less R rows once sb >= R - r; padded k
+  // read the R zero rows after the ring (no wrap)
+  int offlo[NTN], thr[NTN];
 #pragma unroll
-  for (int nt = 0; nt < NTN; ++nt) offn[nt] = koff<C, R, S>(16 * nt + li, g.CS) + ST * lg;
-  for (int e = tid; e < g.CS; e += NT) xin[C * R * g.CS + e] = 0.f;
+  for (int nt = 0; nt < NTN; ++nt) {
+    const int k = 16 * nt + li;
+    const int rw = k / S, c = rw / R, r = rw - c * R;
+    offlo[nt] = k < KRED ? rw * g.CS + (k - rw * S) + ST * lg : C * R * g.CS + ST * lg;
+    thr[nt] = k < KRED ? R - r : R;
+  }
+  for (int e = tid; e < R * g.CS; e += NT) xin[C * R * g.CS + e] = 0.f;
   float mu = 0.f, is = 0.f, ga = 0.f, be = 0.f, k1 = 0.f, k2 = 0.f, f = 0.f;
   if (BNDEF && filt < g.K) {
     mu = d.mean[filt];
@@ -255,12 +304,20 @@ __global__ __launch_bounds__(NT, 3) void wgrad_kernel(DyIn d, const float* __res
   RowStage<C, R, ST> rs;
   DyRow<BNDEF, QC> dr;
   if (r0 < r1) {
-    rs.load(x, g, r0 / g.OH, r0 % g.OH);
+    rs.load_ring(x, g, r0 / g.OH, r0 % g.OH, true);
     dr.load(d, g, r0, voff, voffg);
   }
   for (int row = r0; row < r1; ++row) {
+    const int oh = row % g.OH;
+    const bool full = row == r0 || oh == 0;
     __syncthreads();  // the previous row's LDS reads are done
-    rs.store(xin, g);
+    rs.store_ring(xin, g, oh, full);
+    int offn[NTN];
+    {
+      const int sb = ring_slot<R>(ST * oh - g.pad);
+#pragma unroll
+      for (int nt = 0; nt < NTN; ++nt) offn[nt] = offlo[nt] + (sb >= thr[nt] ? (sb - R) * g.CS : sb * g.CS);
+    }
 #pragma unroll
     for (int q = 0; q < QC; ++q) {  // dy -> this lane's slot of the wave's A table
       float ge = dr.gq[q];
@@ -274,7 +331,7 @@ __global__ __launch_bounds__(NT, 3) void wgrad_kernel(DyIn d, const float* __res
     }
     __syncthreads();
     if (row + 1 < r1) {  // in flight under this row's MFMAs
-      rs.load(x, g, (row + 1) / g.OH, (row + 1) % g.OH);
+      rs.load_ring(x, g, (row + 1) / g.OH, (row + 1) % g.OH, (row + 1) % g.OH == 0);
       dr.load(d, g, row + 1, voff, voffg);
     }
 #pragma unroll
@@ -345,8 +402,9 @@ static Geo geo(int N, int C, int H, int W, int K, int R, int S, int st, int pad,
   return g;
 }
 
-static size_t rows_lds(const Geo& g) { return (size_t)(g.C * g.R + 1) * g.CS * sizeof(float); }
-static size_t fwd_lds(const Geo& g) { return rows_lds(g); }
+// staged rows: forward C * R + 1 zero row; weight gradient the C * R ring + R zero rows
+static size_t rows_lds(const Geo& g) { return (size_t)(g.C + 1) * g.R * g.CS * sizeof(float); }
+static size_t fwd_lds(const Geo& g) { return (size_t)(g.C * g.R + 1) * g.CS * sizeof(float); }
 static size_t wgrad_lds(const Geo& g) { return rows_lds(g) + (size_t)4 * quads(g.OW) * 64 * sizeof(float); }
 
 using FwdFn = void (*)(const float*, const float*, const float*, float*, Geo, double*, FoldTail);

@@ -100,6 +100,22 @@ __device__ __forceinline__ void mfma_tile(const float* ap, const f32x4* bw, f32x
   }
 }
 
+// bn_out in packed fp32 (v_pk_mul / v_pk_fma: two lanes of the same IEEE operations per
+// instruction, bit-identical to the scalar form): the forward's staging transform is its main VALU
+// work, and f32 VALU does not overlap the MFMAs (the dgrad's per-element form packs as well left to
+// the compiler; written this way it took more registers).
+__device__ __forceinline__ f32x2 lo2(f32x4 v) { return f32x2{v[0], v[1]}; }
+__device__ __forceinline__ f32x2 hi2(f32x4 v) { return f32x2{v[2], v[3]}; }
+__device__ __forceinline__ f32x4 cat4(f32x2 a, f32x2 b) { return f32x4{a[0], a[1], b[0], b[1]}; }
+// (x - mean) * invstd
+__device__ __forceinline__ f32x4 xhat4(f32x4 x, f32x4 m, f32x4 i) {
+  return cat4((lo2(x) - lo2(m)) * lo2(i), (hi2(x) - hi2(m)) * hi2(i));
+}
+// gamma * xh + beta (fma)
+__device__ __forceinline__ f32x4 affine4(f32x4 xh, f32x4 g, f32x4 b) {
+  return cat4(__builtin_elementwise_fma(lo2(g), lo2(xh), lo2(b)), __builtin_elementwise_fma(hi2(g), hi2(xh), hi2(b)));
+}
+
 struct FwdArgs {
   const float* x;     // [input pixels][KR] (the preceding BN's raw input when BN)
   const float* w;     // [N][KR]
@@ -190,19 +206,18 @@ __global__ __launch_bounds__(NT, fwd_wps<KR>()) void fwd_kernel(FwdArgs a) {
 #pragma unroll
       for (int j = 0; j < LV; ++j) {
         f32x4 v = st[j];
+        if (!(DK_PWD_EXP & 2)) {
+          v = affine4(xhat4(v, mu, is), ga, be);
 #pragma unroll
-        for (int e = 0; e < 4; ++e)
-          v[e] = (DK_PWD_EXP & 2) ? v[e] : __builtin_fmaxf(bn_out(v[e], mu[e], is[e], ga[e], be[e]), 0.f);
+          for (int e = 0; e < 4; ++e) v[e] = __builtin_fmaxf(v[e], 0.f);
+        }
         st4(dst + (r0 + j * (NT / KV)) * SK + 4 * kv, v);
       }
     } else {
 #pragma unroll
       for (int j = 0; j < LV; ++j) {
         f32x4 v = st[j];
-        if constexpr (BN) {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = bn_out(v[e], mu[e], is[e], ga[e], be[e]);
-        }
+        if constexpr (BN) v = affine4(xhat4(v, mu, is), ga, be);
         st4(dst + (r0 + j * (NT / KV)) * SK + 4 * kv, v);
       }
     }
@@ -428,7 +443,7 @@ __global__ __launch_bounds__(NT, dgrad_wps<KR>()) void dgrad_kernel(DgradArgs a)
 // bn_out.  The block's 4 waves split one dW block's pixel run four ways and add their tiles in
 // LDS (fixed order) into one partial row; the partial rows go through splitk_reduce (fp64, + l2 w).
 // ---------------------------------------------------------------------------------------
-constexpr int kWD = 8;  // pixel pairs in flight per wave
+constexpr int kWD = 8;  // pixel pairs in flight per wave (16: 4-14 % slower, profiles/r04q_pwd_bench_kwd16.txt)
 
 struct WgradArgs {
   const float* dy;  // [M][K]
@@ -708,6 +723,10 @@ int pw_deep_dgrad_slices(int M, int K, int C) { return C / pwd::NB; }
 // 8, about one wave per SIMD in all).
 static int wg_q(int n) { return n >= 128 ? 4 : 2; }
 bool pw_deep_wgrad_ok(int K, int C, int M) {
+  // square layers only: at K = 2C (the widening layers) the tiled engine measured as fast or faster
+  // (profiles/r04n_pwd_bench.txt: 28x28 64->128 52.6 vs 52.9 us, 14x14 128->256 50.6 vs 50.5,
+  // 7x7 256->512 48.8 vs 46.2)
+  if (K != C) return false;
   if (!pwd_enabled() || M <= 1 || (K < 128 && C < 128) || K % 64 || C % 64 || K > 1024 || C > 1024) return false;
   if (K % (32 * wg_q(K)) || C % (32 * wg_q(C))) return false;
   return (size_t)M * (K > C ? K : C) * 4 < ((size_t)1 << 31);

@@ -4,7 +4,8 @@ forward), forward with BN on load + statistics, the strided skip projections, th
 BN-backward-on-load dgrad with dy write-through and the input BN's partials, and the BN-on-load
 weight gradient (with its split reduce).  Median of 15 calls,
 fraction of the fp32 MFMA peak (157.3 TF/s); outputs of the two paths compared bitwise.
-    python scripts/pwd_bench.py [--only fwd|skip|dgrad|wgrad] [--shape HW,C,K] [--deep 0|1]
+    python scripts/pwd_bench.py [--only fwd|skip|dgrad|wgrad] [--shape HW,C,K] [--deep 0|1] [--fold]
+(--fold: the forward also timed with the in-launch BatchNorm statistics fold armed, as in the network)
 """
 import os
 import sys
@@ -13,7 +14,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 import torch  # noqa: E402
 
-from dorknet_amd._hip import lib, stream_handle  # noqa: E402
+from dorknet_amd._hip import fold_resources, lib, stream_handle  # noqa: E402
 
 B = 256
 PEAK = 157.3
@@ -44,6 +45,7 @@ def main():
     shapes = SHAPES
     if "--shape" in sys.argv:
         shapes = [tuple(int(v) for v in sys.argv[sys.argv.index("--shape") + 1].split(","))]
+    fold = "--fold" in sys.argv
     modes = (0, 1)
     if "--deep" in sys.argv:
         modes = (int(sys.argv[sys.argv.index("--deep") + 1]),)
@@ -70,6 +72,17 @@ def main():
                       *(t.data_ptr() for t in pi), 1, part.data_ptr(), st)
                 tf = timeit(lambda: lib.dk_pwconv_fwd_ex_f32(*fa))
                 line.append(f"fwd {tf:6.1f} us {flops / tf / 1e6 / PEAK:4.2f}")
+                if fold:
+                    # the network's call: the following BatchNorm's statistics folded in-launch
+                    stats = [torch.empty(K, device="cuda") for _ in range(5)]
+                    fr = fold_resources.get()
+
+                    def armed():
+                        lib.dk_bn_fold_arm_stats(part.data_ptr(), rows, K, float(M), 1e-5, 0.95, 0,
+                                                 *(t.data_ptr() for t in stats), *fr)
+                        lib.dk_pwconv_fwd_ex_f32(*fa)
+                    tff = timeit(armed)
+                    line.append(f"fwd+fold {tff:6.1f} us {flops / tff / 1e6 / PEAK:4.2f}")
             if only in (None, "dgrad"):
                 rows = lib.dk_pwconv_dgrad_bnbwd_stats_rows(B, HW, HW, K, C)
                 partd = torch.empty(rows * 2 * C, dtype=torch.float64, device="cuda")

@@ -167,7 +167,7 @@ def test_deep_outputs_stay_in_bounds():
     assert bool(torch.isfinite(part).all()) and bool(torch.isfinite(partd).all())
 
 
-WGRAD_SHAPES = [(128, 64), (128, 128), (256, 128), (128, 256), (256, 256), (512, 512)]  # (K, C)
+WGRAD_SHAPES = [(128, 64), (128, 128), (256, 128), (256, 256), (512, 512)]  # (K, C); K != C: the tiled engine
 
 
 @pytest.mark.parametrize("K,C", WGRAD_SHAPES)
