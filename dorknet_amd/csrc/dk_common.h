@@ -246,6 +246,7 @@ int pw_deep_fwd(const float* x, int N, int H, int W, int stride, int OH, int OW,
 bool pw_deep_dgrad_ok(int K, int C, int M);
 int pw_deep_dgrad_rows(int M, int K, int C);
 int pw_deep_dgrad_slices(int M, int K, int C);
+void pw_deep_wgrad_set(int v);  // tuning knob (kind 12): the deep weight gradient alone
 bool pw_deep_wgrad_ok(int K, int C, int M);
 int pw_deep_wgrad_chunks(int M, int K, int C);
 size_t pw_deep_wgrad_ws_bytes(int M, int K, int C);

@@ -722,7 +722,21 @@ int pw_deep_dgrad_slices(int M, int K, int C) { return C / pwd::NB; }
 // stride 1, at least 128 channels on one side; chunks = pixel chunks per dW block (a multiple of
 // 8, about one wave per SIMD in all).
 static int wg_q(int n) { return n >= 128 ? 4 : 2; }
+// Off by default (DORKNET_PW_DEEP_WGRAD=1 or knob 12 = 1 turn it on): faster alone (square layers,
+// profiles/r04n_pwd_bench.txt) but a slower step (profiles/r04s_ab_deep.txt: 8.664 vs 8.593 ms per
+// step) -- a block takes a whole CU (one wave per SIMD, 512 registers, 135 KB of LDS), so on the
+// side stream it shuts the main stream's kernels out of the CUs it holds instead of sharing them.
+static int g_pwd_wg = -1;
+void pw_deep_wgrad_set(int v) { g_pwd_wg = v < 0 ? -1 : v; }
+static bool pwd_wgrad_enabled() {
+  if (g_pwd_wg < 0) {
+    const char* e = getenv("DORKNET_PW_DEEP_WGRAD");
+    g_pwd_wg = (e && e[0] == '1') ? 1 : 0;
+  }
+  return g_pwd_wg == 1;
+}
 bool pw_deep_wgrad_ok(int K, int C, int M) {
+  if (!pwd_wgrad_enabled()) return false;
   // square layers only: at K = 2C (the widening layers) the tiled engine measured as fast or faster
   // (profiles/r04n_pwd_bench.txt: 28x28 64->128 52.6 vs 52.9 us, 14x14 128->256 50.6 vs 50.5,
   // 7x7 256->512 48.8 vs 46.2)

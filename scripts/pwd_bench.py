@@ -61,6 +61,7 @@ def main():
         res, outs, wout = [], {}, {}
         for deep in modes:
             lib.dk_debug_set_gemm_config(11, deep)
+            lib.dk_debug_set_gemm_config(12, deep)
             y = torch.full((M * K,), float("nan"), device="cuda")
             dy = torch.full((M * K,), float("nan"), device="cuda")
             dx = torch.full((M * C,), float("nan"), device="cuda")
@@ -105,6 +106,7 @@ def main():
             outs[deep] = (y.clone(), dy.clone(), dx.clone())
             res.append(("deep " if deep else "old  ") + ", ".join(line))
         lib.dk_debug_set_gemm_config(11, -1)
+        lib.dk_debug_set_gemm_config(12, -1)
         same = ["bitwise" if torch.equal(a, b) else "DIFF(max %.2e)" % float((a - b).abs().nan_to_num(1e30).max())
                 for a, b in zip(outs[0], outs[1])] if len(outs) == 2 else []
         if len(wout) == 2:

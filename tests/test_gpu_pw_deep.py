@@ -13,7 +13,7 @@ from dorknet_amd._hip import lib, stream_handle
 
 pytestmark = pytest.mark.gpu
 
-STREAM_KNOB, DEEP_KNOB = 3, 11
+STREAM_KNOB, DEEP_KNOB, DEEP_WGRAD_KNOB = 3, 11, 12
 
 
 def nhwc(a):
@@ -174,7 +174,8 @@ WGRAD_SHAPES = [(128, 64), (128, 128), (256, 128), (256, 256), (512, 512)]  # (K
 @pytest.mark.parametrize("bn,relu,N,H,W", [(True, 1, 3, 13, 11), (True, 0, 2, 8, 8), (False, 0, 1, 1, 5),
                                            (True, 1, 16, 14, 14)])
 def test_deep_wgrad_matches_fp64(K, C, bn, relu, N, H, W):
-    """dk_pwconv_wgrad_bnx_f32 / dk_pwconv_wgrad_f32 on the deep output-stationary kernel (knob 11 on)
+    """dk_pwconv_wgrad_bnx_f32 / dk_pwconv_wgrad_f32 on the deep output-stationary kernel (knobs 11 and 12
+    on; off by default in the network)
     against an fp64 dW = dy^T relu(bn(x)) + l2 w, elementwise within 3e-5 of sum |dy| |xh| (fp32
     partial sums of a few hundred products each, then the fp64 reduce), and against the tiled engine
     (knob 11 off) within the same bound."""
@@ -203,10 +204,12 @@ def test_deep_wgrad_matches_fp64(K, C, bn, relu, N, H, W):
     outs = []
     for knob in (0, 1):
         lib.dk_debug_set_gemm_config(DEEP_KNOB, knob)
+        lib.dk_debug_set_gemm_config(DEEP_WGRAD_KNOB, knob)
         try:
             outs.append(run())
         finally:
             lib.dk_debug_set_gemm_config(DEEP_KNOB, -1)
+            lib.dk_debug_set_gemm_config(DEEP_WGRAD_KNOB, -1)
     dy64 = dy.permute(0, 2, 3, 1).reshape(M, K).double()
     x64 = x.permute(0, 2, 3, 1).reshape(M, C).double()
     if bn:
