@@ -208,3 +208,22 @@ def test_env_switches_follow_runtime_changes(monkeypatch):
     assert enabled("DORKNET_TEST_SWITCH")
     monkeypatch.delenv("DORKNET_TEST_SWITCH")
     assert getenv("DORKNET_TEST_SWITCH") is None
+
+
+def test_bnout_refuses_stale_statistics():
+    """A BNOut aliases its BatchNormLayer's per-layer mean / invstd buffers: after that layer's next
+    training forward (generation counter) using it raises instead of reading the newer batch's
+    statistics (layers/_bn_input.py); a test-mode forward rewrites neither and keeps it valid."""
+    import torch
+    from dorknet_amd.layers._bn_input import BNOut
+    bn = BatchNormLayer("bn_t", incoming_chans=4)
+    bn._dk_gen = 3
+    t = [torch.zeros(4) for _ in range(5)]
+    out = BNOut(t[0], t[1], t[2], t[3], t[4], True, owner=bn)
+    assert len(out.bn_args()) == 5
+    bn._dk_gen += 1  # what _normalisation does on a training forward
+    with pytest.raises(RuntimeError, match="bn_t"):
+        out.bn_args()
+    with pytest.raises(RuntimeError):
+        out.materialize()
+    assert BNOut(t[0], t[1], t[2], t[3], t[4], False, owner=None).bn_args()[-1] == 0
