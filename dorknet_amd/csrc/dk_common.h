@@ -246,6 +246,20 @@ int pw_deep_fwd(const float* x, int N, int H, int W, int stride, int OH, int OW,
 bool pw_deep_dgrad_ok(int K, int C, int M);
 int pw_deep_dgrad_rows(int M, int K, int C);
 int pw_deep_dgrad_slices(int M, int K, int C);
+// bf16 weight-stationary deep pointwise kernels (pw_deep_bf16.hip), used by the pw_stream_bf16 entries.
+void pw_deep16_set(int v);  // tuning knob (kind 13)
+bool pw_deep16_fwd_ok(int K, int C, int M);
+bool pw_deep16_dgrad_ok(int K, int C, int M);
+int pw_deep16_fwd_rows(int M, int K, int C);
+int pw_deep16_dgrad_rows(int M, int K, int C);
+int pw_deep16_fwd(const bf16_t* x, int M, const float* w, int K, int C, const float* bias, bf16_t* y, const float* im,
+                  const float* iis, const float* ig, const float* ib, int irelu, double* part, hipStream_t st,
+                  const struct FoldTail* ft);
+int pw_deep16_dgrad_bnbwd(const bf16_t* g, const bf16_t* bn_x, int M, int K, int C, const float* om, const float* ois,
+                          const float* og, const float* ob, int orelu, const float* k12, bf16_t* dy_out, const float* w,
+                          bf16_t* dx, const bf16_t* res, const bf16_t* x, const float* im, const float* iis,
+                          const float* ig, const float* ib, int irelu, double* part, hipStream_t st,
+                          const struct FoldTail* ft);
 void pw_deep_wgrad_set(int v);  // tuning knob (kind 12): the deep weight gradient alone
 bool pw_deep_wgrad_ok(int K, int C, int M);
 int pw_deep_wgrad_chunks(int M, int K, int C);

@@ -92,6 +92,10 @@ DK_API int dk_debug_set_gemm_config(int kind, int cfg) {
     pw_stream_bf16_deep_set(cfg);
     return 0;
   }
+  if (kind == 13) {  // the bf16 weight-stationary deep kernels (pw_deep_bf16.hip) on / off
+    pw_deep16_set(cfg);
+    return 0;
+  }
   if (kind == 12) {  // the deep output-stationary weight gradient alone (pw_deep.hip) on / off
     pw_deep_wgrad_set(cfg);
     return 0;

@@ -899,6 +899,7 @@ bool pw_stream_bf16_fwd_ok(int K, int C, int M) {
          (size_t)M * (K > C ? K : C) * 2 < ((size_t)1 << 31);
 }
 int pw_stream_bf16_fwd_rows(int M, int K, int C) {
+  if (!pwsh_shape(C, K) && pw_deep16_fwd_ok(K, C, M)) return pw_deep16_fwd_rows(M, K, C);
 #define DK_ROWS(kr, no) \
   if (C == kr && K == no) return pwsh::grid_blocks(M, pwsh::fwd_occ<kr, no>());
   DK_PWSH_SHAPES(DK_ROWS)
@@ -915,6 +916,7 @@ bool pw_stream_bf16_dgrad_ok(int K, int C, int M) {
          (size_t)M * (K > C ? K : C) * 2 < ((size_t)1 << 31);
 }
 int pw_stream_bf16_dgrad_rows(int M, int K, int C) {
+  if (!pwsh_shape(K, C) && pw_deep16_dgrad_ok(K, C, M)) return pw_deep16_dgrad_rows(M, K, C);
 #define DK_ROWS(kr, no) \
   if (K == kr && C == no) return pwsh::grid_blocks(M, pwsh::dgrad_occ<kr, no>());
   DK_PWSH_SHAPES(DK_ROWS)
@@ -930,6 +932,8 @@ int pw_stream_bf16_dgrad_slices(int K, int C) { return pwsh_shape(K, C) ? 1 : C 
 int pw_stream_bf16_fwd(const bf16_t* x, int M, const float* w, int K, int C, const float* bias, bf16_t* y,
                        const float* im, const float* iis, const float* ig, const float* ib, int irelu, double* part,
                        hipStream_t st, const FoldTail* ft) {
+  if (!pwsh_shape(C, K) && pw_deep16_fwd_ok(K, C, M))  // the weight-stationary kernels (pw_deep_bf16.hip)
+    return pw_deep16_fwd(x, M, w, K, C, bias, y, im, iis, ig, ib, irelu, part, st, ft);
   if (!pwsh_shape(C, K)) {
     pwsh::DeepArgs d{x, nullptr, nullptr, w, bias, y, nullptr, nullptr, im, iis, ig, ib, nullptr, irelu,
                      nullptr, nullptr, nullptr, nullptr, 0, part, M, K};
@@ -979,6 +983,9 @@ int pw_stream_bf16_dgrad_bnbwd(const bf16_t* g, const bf16_t* bn_x, int M, int K
                                bf16_t* dy_out, const float* w, bf16_t* dx, const bf16_t* res, const bf16_t* x,
                                const float* im, const float* iis, const float* ig, const float* ib, int irelu,
                                double* part, hipStream_t st, const FoldTail* ft) {
+  if (!pwsh_shape(K, C) && pw_deep16_dgrad_ok(K, C, M))
+    return pw_deep16_dgrad_bnbwd(g, bn_x, M, K, C, om, ois, og, ob, orelu, k12, dy_out, w, dx, res, x, im, iis, ig, ib,
+                                 irelu, part, st, ft);
   if (!pwsh_shape(K, C)) {
     pwsh::DeepArgs d{g, bn_x, dy_out, w, nullptr, dx, res, x, om, ois, og, ob, k12, orelu,
                      im, iis, ig, ib, irelu, part, M, C};

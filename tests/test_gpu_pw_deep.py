@@ -187,10 +187,11 @@ def test_deep_wgrad_matches_fp64(K, C, bn, relu, N, H, W):
     pi = bn_params(C, rng)
     l2 = 1e-3
     st = stream_handle()
-    nb = lib.dk_pwconv_wgrad_workspace_bytes(N, H, W, K, C)
-    ws = torch.empty(max(nb, 4) // 4 + 1, dtype=torch.float32, device="cuda")
 
     def run():
+        # (the workspace size depends on the path the knobs select)
+        nb = lib.dk_pwconv_wgrad_workspace_bytes(N, H, W, K, C)
+        ws = torch.empty(max(nb, 4) // 4 + 1, dtype=torch.float32, device="cuda")
         dw = torch.full((K, C), float("nan"), device="cuda")
         if bn:
             rc = lib.dk_pwconv_wgrad_bnx_f32(dy.data_ptr(), x.data_ptr(), N, H, W, C, K, 1, H, W, w.data_ptr(), l2,
