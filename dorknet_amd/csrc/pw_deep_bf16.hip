@@ -10,8 +10,10 @@
 //   * weight-stationary waves: a wave owns 32 output columns with their B fragments -- the whole
 //     reduction, bf16x8 per k-step of 16, KR / 4 VGPRs -- in registers (RNE from the fp32 weights);
 //   * a block (4 waves, 128 columns) stages each 32-pixel tile once: 16-byte row loads, the
-//     transform in fp32 with the lane's channels' BN terms in registers, RNE to bf16, into an LDS
-//     tile (row stride KR + 8 bf16: an odd number of 16-byte units, conflict-free ds_read_b128);
+//     transform in fp32 with the lane's 8 channels' BN terms read from an LDS table once per tile
+//     (kept in registers they held the forward at KR = 512 and the dgrad at 256 to one wave per
+//     SIMD), RNE to bf16, into an LDS tile (row stride KR + 8 bf16: an odd number of 16-byte units,
+//     conflict-free ds_read_b128);
 //   * per MFMA a wave reads one ds_read_b128 of A; one barrier per tile; the next tile's loads are
 //     in flight during the MFMAs; the epilogue works in the MFMA C layout.
 // Bit-identical to the kernels above and to the tiled engine's bf16 mode: the same operand
@@ -43,11 +45,11 @@ __device__ __forceinline__ float bf16_val(uint32_t bits) { return __builtin_bit_
 
 template <int KR>
 constexpr int fwd_wps() {
-  return KR <= 256 ? 2 : 1;
+  return 2;
 }
 template <int KR>
 constexpr int dgrad_wps() {
-  return KR <= 128 ? 2 : 1;
+  return KR <= 256 ? 2 : 1;
 }
 
 // A buffer resource over rows [tile * TR, nrows) of a [nrows][ld] bf16 tensor (see pw_deep.hip).
@@ -125,6 +127,9 @@ __global__ __launch_bounds__(NT, fwd_wps<KR>()) void fwd_kernel(FwdArgs a) {
   constexpr int SK = KR + 8, KV = KR / 8, LV = TR * KV / NT, KS = KR / 16;
   static_assert(KR % 64 == 0 && NT % KV == 0 && LV >= 1, "pwd16::fwd_kernel shape");
   __shared__ __attribute__((aligned(16))) bf16_t As[2][TR * SK];
+  // the input BN's terms [4][KR], read by each thread for its 8 channels once per tile (held in
+  // registers for the whole launch they cost 32 VGPRs: one wave per SIMD at KR = 512 instead of two)
+  __shared__ __attribute__((aligned(16))) float tab[BN ? 4 * KR : 4];
   static_assert(sizeof(double) * 2 * NT <= sizeof(bf16_t) * 2 * TR * SK, "fold scratch fits in the tiles");
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l32 = lane & 31, h = lane >> 5;
   const int n0 = blockIdx.y * NB, N = a.N, col = n0 + 32 * wave + l32;
@@ -132,31 +137,38 @@ __global__ __launch_bounds__(NT, fwd_wps<KR>()) void fwd_kernel(FwdArgs a) {
   const bool irelu = a.irelu != 0;
   // staging: lane loads 8 channels kv of rows tid / KV + j * (NT / KV)
   const int kv = tid % KV, r0 = tid / KV;
-  f32x4 mu[2], is[2], ga[2], be[2];
   if constexpr (BN) {
-#pragma unroll
-    for (int p = 0; p < 2; ++p) {
-      mu[p] = ld4(a.im + 8 * kv + 4 * p);
-      is[p] = ld4(a.iis + 8 * kv + 4 * p);
-      ga[p] = ld4(a.ig + 8 * kv + 4 * p);
-      be[p] = ld4(a.ib + 8 * kv + 4 * p);
+    for (int c = tid; c < KR; c += NT) {
+      tab[c] = a.im[c];
+      tab[KR + c] = a.iis[c];
+      tab[2 * KR + c] = a.ig[c];
+      tab[3 * KR + c] = a.ib[c];
     }
+    __syncthreads();
   }
   const int ntiles = (a.M + TR - 1) / TR, G = gridDim.x;
-  uint32_t lofs[LV], eofs[16];
-#pragma unroll
-  for (int j = 0; j < LV; ++j) lofs[j] = ((uint32_t)(r0 + j * (NT / KV)) * KR + 8 * kv) * 2u;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) eofs[r] = ((uint32_t)(4 * h + (r & 3) + 8 * (r >> 2)) * N + col) * 2u;
+  // lane offsets within a tile (bytes), rebuilt per use from one base (an array of them was 24 VGPRs)
+  const uint32_t lofs0 = ((uint32_t)r0 * KR + 8 * kv) * 2u, eofs0 = ((uint32_t)(4 * h) * N + col) * 2u;
+  constexpr uint32_t kLStep = (uint32_t)(NT / KV) * KR * 2u;
 
   auto load_tile = [&](int tile, u32x4* st) {
     const __amdgpu_buffer_rsrc_t rt = tile_rsrc(a.x, KR, tile, a.M);
 #pragma unroll
     for (int j = 0; j < LV; ++j)
-      st[j] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rt, (int)lofs[j], 0, 0));
+      st[j] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rt, (int)(lofs0 + j * kLStep), 0, 0));
   };
   // the BatchNorm (+ReLU) on load in fp32, RNE to bf16 (the reference's (r > 0) ? r : 0)
   auto stage = [&](bf16_t* dst, const u32x4* st) {
+    f32x4 mu[2], is[2], ga[2], be[2];
+    if constexpr (BN) {
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        mu[p] = *reinterpret_cast<const f32x4*>(tab + 8 * kv + 4 * p);
+        is[p] = *reinterpret_cast<const f32x4*>(tab + KR + 8 * kv + 4 * p);
+        ga[p] = *reinterpret_cast<const f32x4*>(tab + 2 * KR + 8 * kv + 4 * p);
+        be[p] = *reinterpret_cast<const f32x4*>(tab + 3 * KR + 8 * kv + 4 * p);
+      }
+    }
 #pragma unroll
     for (int j = 0; j < LV; ++j) {
       u32x4 q = st[j];
@@ -206,7 +218,7 @@ __global__ __launch_bounds__(NT, fwd_wps<KR>()) void fwd_kernel(FwdArgs a) {
       float v = acc[r];
       if constexpr (HB) v += bias;
       const uint16_t bits = bf16_bits(v);
-      __builtin_amdgcn_raw_buffer_store_b16(bits, ry, (int)eofs[r], 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b16(bits, ry, (int)(eofs0 + (uint32_t)(((r & 3) + 8 * (r >> 2)) * N) * 2u), 0, 0);
       if constexpr (STATS) {
         const int dm = (r & 3) + 8 * (r >> 2);
         const double d = (full || mb + dm < a.M) ? (double)bf16_val(bits) : 0.0;
@@ -250,40 +262,51 @@ __global__ __launch_bounds__(NT, dgrad_wps<KR>()) void dgrad_kernel(DgradArgs a)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l32 = lane & 31, h = lane >> 5;
   const int n0 = blockIdx.y * NB, N = a.N, col = n0 + 32 * wave + l32;
   const int kv = tid % KV, r0 = tid / KV;
-  f32x4 mu[2], is[2], ga[2], be[2], k1[2], k2[2], f[2];
-#pragma unroll
-  for (int p = 0; p < 2; ++p) {
-    const int c = 8 * kv + 4 * p;
-    mu[p] = ld4(a.om + c);
-    is[p] = ld4(a.ois + c);
-    ga[p] = ld4(a.og + c);
-    be[p] = ld4(a.ob + c);
-    k1[p] = ld4(a.k12 + c);
-    k2[p] = ld4(a.k12 + KR + c);
-#pragma unroll
-    for (int e = 0; e < 4; ++e) f[p][e] = ga[p][e] * is[p][e];
+  // the following BN's terms [7][KR] (mean, invstd, gamma, beta, k1, k2, gamma * invstd), read by
+  // each thread for its 8 channels once per tile
+  __shared__ __attribute__((aligned(16))) float tab[7 * KR];
+  for (int c = tid; c < KR; c += NT) {
+    const float is = a.ois[c], ga = a.og[c];
+    tab[c] = a.om[c];
+    tab[KR + c] = is;
+    tab[2 * KR + c] = ga;
+    tab[3 * KR + c] = a.ob[c];
+    tab[4 * KR + c] = a.k12[c];
+    tab[5 * KR + c] = a.k12[KR + c];
+    tab[6 * KR + c] = ga * is;
   }
+  __syncthreads();
   const float pm = PART ? a.im[col] : 0.f, pis = PART ? a.iis[col] : 0.f, pga = PART ? a.ig[col] : 0.f,
               pbe = PART ? a.ib[col] : 0.f;
   const bool orelu = a.orelu != 0, irelu = a.irelu != 0;
   const bool writer = a.dy_out != nullptr && blockIdx.y == 0;
   const int ntiles = (a.M + TR - 1) / TR, G = gridDim.x;
-  uint32_t lofs[LV], eofs[16];
-#pragma unroll
-  for (int j = 0; j < LV; ++j) lofs[j] = ((uint32_t)(r0 + j * (NT / KV)) * KR + 8 * kv) * 2u;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) eofs[r] = ((uint32_t)(4 * h + (r & 3) + 8 * (r >> 2)) * N + col) * 2u;
+  const uint32_t lofs0 = ((uint32_t)r0 * KR + 8 * kv) * 2u, eofs0 = ((uint32_t)(4 * h) * N + col) * 2u;
+  constexpr uint32_t kLStep = (uint32_t)(NT / KV) * KR * 2u;
+  auto eofs = [&](int r) { return (int)(eofs0 + (uint32_t)(((r & 3) + 8 * (r >> 2)) * N) * 2u); };
 
   auto load_tile = [&](int tile, u32x4* sg, u32x4* sx) {
     const __amdgpu_buffer_rsrc_t rg = tile_rsrc(a.g, KR, tile, a.M), rx = tile_rsrc(a.xo, KR, tile, a.M);
 #pragma unroll
     for (int j = 0; j < LV; ++j) {
-      sg[j] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rg, (int)lofs[j], 0, 0));
-      sx[j] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rx, (int)lofs[j], 0, 0));
+      sg[j] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rg, (int)(lofs0 + j * kLStep), 0, 0));
+      sx[j] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rx, (int)(lofs0 + j * kLStep), 0, 0));
     }
   };
   auto stage = [&](int tile, bf16_t* dst, const u32x4* sg, const u32x4* sx) {
     const __amdgpu_buffer_rsrc_t rdy = tile_rsrc(writer ? a.dy_out : a.g, KR, tile, writer ? a.M : 0);
+    f32x4 mu[2], is[2], ga[2], be[2], k1[2], k2[2], f[2];
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const float* tp = tab + 8 * kv + 4 * p;
+      mu[p] = *reinterpret_cast<const f32x4*>(tp);
+      is[p] = *reinterpret_cast<const f32x4*>(tp + KR);
+      ga[p] = *reinterpret_cast<const f32x4*>(tp + 2 * KR);
+      be[p] = *reinterpret_cast<const f32x4*>(tp + 3 * KR);
+      k1[p] = *reinterpret_cast<const f32x4*>(tp + 4 * KR);
+      k2[p] = *reinterpret_cast<const f32x4*>(tp + 5 * KR);
+      f[p] = *reinterpret_cast<const f32x4*>(tp + 6 * KR);
+    }
 #pragma unroll
     for (int j = 0; j < LV; ++j) {
       f32x4 gv[2], xv[2];
@@ -301,7 +324,7 @@ __global__ __launch_bounds__(NT, dgrad_wps<KR>()) void dgrad_kernel(DgradArgs a)
         }
       const u32x4 q = pack8(gv[0], gv[1]);
       *reinterpret_cast<u32x4*>(dst + (r0 + j * (NT / KV)) * SK + 8 * kv) = q;
-      __builtin_amdgcn_raw_buffer_store_b128(q, rdy, (int)lofs[j], 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b128(q, rdy, (int)(lofs0 + j * kLStep), 0, 0);
     }
   };
 
@@ -338,8 +361,8 @@ __global__ __launch_bounds__(NT, dgrad_wps<KR>()) void dgrad_kernel(DgradArgs a)
     uint32_t exi[16], ers[16];
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      if constexpr (PART) exi[r] = __builtin_amdgcn_raw_buffer_load_b16(rxi, (int)eofs[r], 0, 0);
-      if constexpr (RES) ers[r] = __builtin_amdgcn_raw_buffer_load_b16(rr, (int)eofs[r], 0, 0);
+      if constexpr (PART) exi[r] = __builtin_amdgcn_raw_buffer_load_b16(rxi, eofs(r), 0, 0);
+      if constexpr (RES) ers[r] = __builtin_amdgcn_raw_buffer_load_b16(rr, eofs(r), 0, 0);
     }
     f32x16 acc;
     mfma_tile<KS>(&As[buf][0] + l32 * SK + 8 * h, bw, acc);
@@ -349,7 +372,7 @@ __global__ __launch_bounds__(NT, dgrad_wps<KR>()) void dgrad_kernel(DgradArgs a)
       float v = acc[r];
       if constexpr (RES) v += bf16_val(ers[r]);
       const uint16_t bits = bf16_bits(v);
-      __builtin_amdgcn_raw_buffer_store_b16(bits, rdx, (int)eofs[r], 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b16(bits, rdx, eofs(r), 0, 0);
       if constexpr (PART) {
         const int dm = (r & 3) + 8 * (r >> 2);
         const float gs = bf16_val(bits), x = bf16_val(exi[r]);
