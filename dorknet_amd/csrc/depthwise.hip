@@ -12,6 +12,9 @@
 //   * stride-1 dgrad is the forward kernel run on dy with the taps flipped;
 //   * wgrad reduces per-block partials in a fixed order (reduce.hip) -- the reference
 //     issues N*OH*OW atomicAdds on each of the C*R*S weight addresses.
+#include <numeric>
+#include <type_traits>
+
 #include "dk_common.h"
 #include "fold_tail.h"
 
@@ -65,7 +68,42 @@ __device__ __forceinline__ void load_dw_weights(f32x4 (&wv)[R][S], const float* 
   }
 }
 
+// bn_relu_out on 4 channels in packed fp32 (v_pk_add / v_pk_mul / v_pk_fma: the same IEEE
+// operations two lanes per instruction, bit-identical to bn_out), the ReLU as a compile-time
+// v_max_f32 (max(r, 0) is the reference's (r > 0) ? r : 0; a NaN gives 0 both ways) instead of a
+// compare and select on the run-time flag.
+template <bool RELU>
+__device__ __forceinline__ f32x4 bn_in4p(f32x4 v, f32x4 m, f32x4 is, f32x4 g, f32x4 b) {
+  // x + (-mean) is x - mean exactly; written as an add it packs (v_pk_add_f32)
+  const f32x2 h0 = (f32x2{v[0], v[1]} + f32x2{-m[0], -m[1]}) * f32x2{is[0], is[1]};
+  const f32x2 h1 = (f32x2{v[2], v[3]} + f32x2{-m[2], -m[3]}) * f32x2{is[2], is[3]};
+  const f32x2 o0 = __builtin_elementwise_fma(f32x2{g[0], g[1]}, h0, f32x2{b[0], b[1]});
+  const f32x2 o1 = __builtin_elementwise_fma(f32x2{g[2], g[3]}, h1, f32x2{b[2], b[3]});
+  f32x4 o = {o0[0], o0[1], o1[0], o1[1]};
+  if constexpr (RELU) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = __builtin_fmaxf(o[e], 0.f);
+  }
+  return o;
+}
+
 // One input row of a strip: NC float4s at (ih, iw0 ..), BN-on-load applied, padding 0.
+template <int NC, bool BN, bool RELU, class T = float>
+__device__ __forceinline__ void load_row(f32x4 (&row)[NC], __amdgpu_buffer_rsrc_t rs, int n, int ih, int iw0, int H,
+                                         int W, int C, int c, f32x4 bm, f32x4 bi, f32x4 bg, f32x4 bb) {
+  const bool rv = (unsigned)ih < (unsigned)H;
+#pragma unroll
+  for (int q = 0; q < NC; ++q) {
+    const int iw = iw0 + q;
+    const bool ok = rv && (unsigned)iw < (unsigned)W;
+    row[q] = bload4e<T>(rs, ok, (uint32_t)(((n * H + ih) * W + iw) * C + c));
+    if constexpr (BN) {
+      const f32x4 t = bn_in4p<RELU>(row[q], bm, bi, bg, bb);
+      row[q] = ok ? t : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  }
+}
+// The same with the ReLU flag read at run time (the weight-gradient kernel).
 template <int NC, bool BN, class T = float>
 __device__ __forceinline__ void load_row(f32x4 (&row)[NC], __amdgpu_buffer_rsrc_t rs, int n, int ih, int iw0, int H,
                                          int W, int C, int c, const BnIn& bn, f32x4 bm, f32x4 bi, f32x4 bg,
@@ -95,7 +133,13 @@ struct DwTile {
 // extra blocks do not pay for it).
 static int g_dw_seg = -1;  // tuning knob dk_debug_set_gemm_config(8, rows); -1 = the default
 void dw_seg_set(int v) { g_dw_seg = v; }
-static inline int dw_fwd_seg() { return g_dw_seg > 0 ? g_dw_seg : 8; }
+// The default: segments of at most 8 rows, balanced (OH = 28 -> 4 x 7, OH = 14 -> 2 x 7 instead of
+// 8 + 8 + 8 + 4 / 8 + 6: the short last segments left threads idle; profiles/r04dw2_dwseg.txt).
+static inline int dw_fwd_seg(int OH) {
+  if (g_dw_seg > 0) return g_dw_seg;
+  const int nseg = (OH + 7) / 8;
+  return (OH + nseg - 1) / nseg;
+}
 
 // y[n,oh,ow,c] = sum_{r,s} w[r][s][c] * x[n, oh*ST + r - pad, ow*ST + s - pad, c] (+ bias[c])
 // Thread = (n, oh, TW-wide chunk of ow, 4 channels); consecutive threads take consecutive
@@ -110,7 +154,7 @@ static inline int dw_fwd_seg() { return g_dw_seg > 0 ? g_dw_seg : 8; }
 // fused ReLU (batch_norm.py:125-174, dk_bn_bwd_partial_f64); xo is that BN's raw input.
 // T: activation storage (float, or bf16_t for BASELINE config 5); compute is fp32, and the
 // statistics see the stored (rounded) outputs.
-template <int R, int S, int ST, bool BN, int STATS, int WL, class T = float>
+template <int R, int S, int ST, bool BN, bool RELU, int STATS, int WL, class T = float>
 __global__ __launch_bounds__(256) void dw_fwd_kernel(const T* __restrict__ x, uint32_t xbytes,
                                                      const float* __restrict__ wt, const float* __restrict__ bias,
                                                      T* __restrict__ y, int N, int H, int W, int C, int OH, int OW,
@@ -157,10 +201,18 @@ __global__ __launch_bounds__(256) void dw_fwd_kernel(const T* __restrict__ x, ui
       og = ld4(obn.gamma + c);
       ob = ld4(obn.beta + c);
     }
+    // The input window as a ring: logical row r of output row oh0 + P (P mod PER) is held in slot
+    // (P ST + r) % R, so sliding the window down one output row moves no registers -- the row loop
+    // is unrolled PER times, one copy per ring phase (the register moves of a shifted window were a
+    // seventh of this VALU-bound kernel's instructions)
+    // (stride 2 keeps the shifted window: two of its three rows are new each output row, and the
+    // unrolled ring took it past 256 registers)
+    constexpr bool RING = ST == 1;
+    constexpr int PER = RING ? R / std::gcd(R, ST) : 1;
     f32x4 win[R][NC];
 #pragma unroll
     for (int r = 0; r < R; ++r)
-      load_row<NC, BN, T>(win[r], rs, n, oh0 * ST - pad + r, iw0, H, W, C, c, bn, bm, bi, bg, bb);
+      load_row<NC, BN, RELU, T>(win[r], rs, n, oh0 * ST - pad + r, iw0, H, W, C, c, bm, bi, bg, bb);
     // stride 1: the next output row's new input row is loaded one row ahead (bf16 kept packed, 2
     // registers per 4 channels) and widened / normalised when it enters the window; stride 2 loads
     // it in the row that uses it (its window leaves no registers for a prefetch)
@@ -184,7 +236,10 @@ __global__ __launch_bounds__(256) void dw_fwd_kernel(const T* __restrict__ x, ui
       }
     };
     if (oh0 + 1 < oh1) load_pre((oh0 + 1) * ST - pad + R - 1);
-    for (int oh = oh0; oh < oh1; ++oh) {
+    // one output row at ring phase P; false once the segment is done
+    auto row = [&](int oh, auto PC) __attribute__((always_inline)) -> bool {
+      constexpr int P = decltype(PC)::value;
+      if (oh >= oh1) return false;
       // this row's residual / BN-input operands (dgrad only), issued ahead of the window
       // loads and FMAs
       const size_t pix0 = (size_t)(n * OH + oh) * OW + ow0;
@@ -198,12 +253,18 @@ __global__ __launch_bounds__(256) void dw_fwd_kernel(const T* __restrict__ x, ui
         }
       }
       if (oh > oh0) {
+        if constexpr (!RING) {
 #pragma unroll
-        for (int r = 0; r < R; ++r) {
-          if (r + ST < R) {
+          for (int r = 0; r + ST < R; ++r)
 #pragma unroll
             for (int q = 0; q < NC; ++q) win[r][q] = win[r + ST][q];
-          } else if constexpr (PFR) {
+        }
+        // the ST rows that enter the window: logical rows R - ST .. R - 1
+#pragma unroll
+        for (int r = R - ST; r < R; ++r) {
+          if (r < 0) continue;
+          const int slot = RING ? (P * ST + r) % R : r;
+          if constexpr (PFR) {
             // the prefetched row: widened, BN applied on the in-image elements (as load_row)
             const int ih = oh * ST - pad + r;
             const bool rv = (unsigned)ih < (unsigned)H;
@@ -216,14 +277,14 @@ __global__ __launch_bounds__(256) void dw_fwd_kernel(const T* __restrict__ x, ui
                 v = pre[q];
               if constexpr (BN) {
                 const bool ok = rv && (unsigned)(iw0 + q) < (unsigned)W;
-                const f32x4 t = bn_in4(v, bm, bi, bg, bb, bn.relu);
+                const f32x4 t = bn_in4p<RELU>(v, bm, bi, bg, bb);
                 v = ok ? t : f32x4{0.f, 0.f, 0.f, 0.f};
               }
-              win[r][q] = v;
+              win[slot][q] = v;
             }
             if (oh + 1 < oh1) load_pre((oh + 1) * ST - pad + R - 1);
           } else {
-            load_row<NC, BN, T>(win[r], rs, n, oh * ST - pad + r, iw0, H, W, C, c, bn, bm, bi, bg, bb);
+            load_row<NC, BN, RELU, T>(win[slot], rs, n, oh * ST - pad + r, iw0, H, W, C, c, bm, bi, bg, bb);
           }
         }
       }
@@ -235,20 +296,18 @@ __global__ __launch_bounds__(256) void dw_fwd_kernel(const T* __restrict__ x, ui
       f32x4 r1 = {0.f, 0.f, 0.f, 0.f}, r2 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int j = 0; j < TW; ++j) {
-        f32x4 acc = b0;
+        // (the first tap's fma takes the bias as its addend: no copy of b0 per output)
+        f32x4 acc = win[RING ? (P * ST) % R : 0][j * ST] * wv[0][0] + b0;
 #pragma unroll
         for (int r = 0; r < R; ++r)
 #pragma unroll
-          for (int s = 0; s < S; ++s) acc += win[r][j * ST + s] * wv[r][s];
+          for (int s = 0; s < S; ++s)
+            if (r + s > 0) acc += win[RING ? (P * ST + r) % R : r][j * ST + s] * wv[r][s];
         if (ow0 + j < OW) {
           if constexpr (WL == 2) {
             if (res) acc += rv[j];  // residual addend
           }
-          acc = rnd4<T>(acc);  // what the store keeps (identity for fp32)
-          if (nt)
-            st4nt(yrow + (size_t)(ow0 + j) * C, acc);
-          else
-            st4(yrow + (size_t)(ow0 + j) * C, acc);
+          acc = st4_kept(yrow + (size_t)(ow0 + j) * C, acc, nt);  // acc = what the store keeps
           if constexpr (RS) {
             r1 += acc;
 #pragma unroll
@@ -279,6 +338,24 @@ __global__ __launch_bounds__(256) void dw_fwd_kernel(const T* __restrict__ x, ui
           s2[e] += (double)r2[e];
         }
       }
+      return true;
+    };
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, 1>;
+    using I2 = std::integral_constant<int, 2>;
+    using I3 = std::integral_constant<int, 3>;
+    using I4 = std::integral_constant<int, 4>;
+    static_assert(PER >= 1 && PER <= 5, "ring period");
+    for (int oh = oh0;; oh += PER) {
+      if (!row(oh, I0{})) break;
+      if constexpr (PER > 1)
+        if (!row(oh + 1, I1{})) break;
+      if constexpr (PER > 2)
+        if (!row(oh + 2, I2{})) break;
+      if constexpr (PER > 3)
+        if (!row(oh + 3, I3{})) break;
+      if constexpr (PER > 4)
+        if (!row(oh + 4, I4{})) break;
     }
   }
   if constexpr (STATS != 0) {
@@ -862,8 +939,25 @@ __global__ __launch_bounds__(256) void dw_bwd_fused_kernel(const T* __restrict__
     load_x_row(xq[PF - 1], xn, xhh);
     if (++xhh == H) xhh = 0, ++xn;
     T* dxcol = dx ? dx + (size_t)pix(nn, 0, w) : nullptr;
+    // the input BN's output (+ReLU) for the weight gradient (bn_relu_out), and its ReLU mask (BN
+    // output > 0) kept as 4 bits for the backward partials (recomputing bn_out there re-read the
+    // BN terms from LDS once per element)
     f32x4 xb = xh;
-    if constexpr (BNX) xb = win_ok ? bn_in4(xh, bm, bi, bg, bb, bn.relu) : f32x4{0.f, 0.f, 0.f, 0.f};
+    uint32_t rmask = 0xfu;
+    if constexpr (BNX) {
+      const f32x4 vbm = bm, vbi = bi, vbg = bg, vbb = bb;
+      f32x4 xr;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        xr[e] = bn_out(xh[e], vbm[e], vbi[e], vbg[e], vbb[e]);
+        if (!(xr[e] > 0.f)) {
+          rmask &= ~(1u << e);
+          if (bn.relu) xr[e] = 0.f;
+        }
+      }
+      if (!bn.relu) rmask = 0xfu;
+      xb = win_ok ? xr : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int r = 0; r < R; ++r)
@@ -874,8 +968,8 @@ __global__ __launch_bounds__(256) void dw_bwd_fused_kernel(const T* __restrict__
       }
     if (win_ok) {
       if (res) acc += rh;
-      acc = rnd4<T>(acc);  // what the store keeps (identity for fp32)
       if constexpr (JOIN) {
+        acc = rnd4<T>(acc);
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           // dy * mask (activations.py:46); no mask given: this layer's input is the join's output
@@ -887,18 +981,24 @@ __global__ __launch_bounds__(256) void dw_bwd_fused_kernel(const T* __restrict__
           s2[e] += (double)acc[e] * (double)xn;
         }
       }
-      if (dxcol) {
-        if (nt)
-          st4nt(dxcol + (size_t)h * W * C, acc);
-        else
-          st4(dxcol + (size_t)h * W * C, acc);
+      if constexpr (JOIN) {
+        if (dxcol) {
+          if (nt)
+            st4nt(dxcol + (size_t)h * W * C, acc);
+          else
+            st4(dxcol + (size_t)h * W * C, acc);
+        }
+      } else if (dxcol) {
+        acc = st4_kept(dxcol + (size_t)h * W * C, acc, nt);  // acc = what the store keeps
+      } else {
+        acc = rnd4<T>(acc);
       }
       if constexpr (STATS) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           float ge = acc[e];
           const float xn = (xh[e] - bm[e]) * bi[e];
-          if (bn.relu && !(bn_out(xh[e], bm[e], bi[e], bg[e], bb[e]) > 0.f)) ge = 0.f;
+          if (!((rmask >> e) & 1u)) ge = 0.f;
           s1[e] += (double)ge;
           s2[e] += (double)ge * (double)xn;
         }
@@ -1009,7 +1109,7 @@ static inline bool bn_ok(const BnIn& bn) {
 template <int ST>
 static long long dw_fwd_threads(int N, int OH, int OW, int C) {
   constexpr int TW = DwTile<ST>::TW;
-  const int SEG = dw_fwd_seg();
+  const int SEG = dw_fwd_seg(OH);
   return (long long)N * ((OH + SEG - 1) / SEG) * ((OW + TW - 1) / TW) * (C / 4);
 }
 
@@ -1023,9 +1123,16 @@ static int launch_dw_fwd(const T* x, const float* wt, const float* bias, T* y, i
   const dim3 grid((unsigned)cdivll(dw_fwd_threads<ST>(N, OH, OW, C), 256));
   FoldTail ft;  // an armed in-launch fold of the partial rows (fold_tail.h)
   if (!part || !fold_take(part, (int)grid.x, C, 1, &ft)) ft.part = nullptr;
-#define DW_LAUNCH(B, ST_, WL_)                                                                                        \
-  hipLaunchKernelGGL((dw_fwd_kernel<R, S, ST, B, ST_, WL_, T>), grid, dim3(256), 0, st, x, xb, wt, bias, y, N, H, W, \
-                     C, OH, OW, pad, bn, part, xo, obn, res, ft, nt_stores(kNtDwFwd), dw_fwd_seg())
+#define DW_LAUNCH1(B, RL, ST_, WL_)                                                                                  \
+  hipLaunchKernelGGL((dw_fwd_kernel<R, S, ST, B, RL, ST_, WL_, T>), grid, dim3(256), 0, st, x, xb, wt, bias, y, N, H, \
+                     W, C, OH, OW, pad, bn, part, xo, obn, res, ft, nt_stores(kNtDwFwd), dw_fwd_seg(OH))
+#define DW_LAUNCH(B, ST_, WL_)            \
+  do {                                    \
+    if (B && bn.relu)                     \
+      DW_LAUNCH1(B, B, ST_, WL_);         \
+    else                                  \
+      DW_LAUNCH1(B, false, ST_, WL_);     \
+  } while (0)
   const int mode = part ? (xo ? 2 : 1) : 0;
   if (wl == 0 && !bn.mean && mode == 0)
     DW_LAUNCH(false, 0, 0);
@@ -1046,6 +1153,7 @@ static int launch_dw_fwd(const T* x, const float* wt, const float* bias, T* y, i
   else
     return DK_ERR_ARGS;
 #undef DW_LAUNCH
+#undef DW_LAUNCH1
   return fold_status(launch_status(), ft);
 }
 

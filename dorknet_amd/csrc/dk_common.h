@@ -65,6 +65,27 @@ __device__ __forceinline__ f32x4 rnd4(f32x4 v) {
   else
     return v;
 }
+// Store v (optionally nontemporal) and return what the store kept: one conversion for bf16
+// (rnd4 followed by st4 converted twice).
+__device__ __forceinline__ f32x4 st4_kept(float* p, f32x4 v, int nt) {
+  if (nt)
+    st4nt(p, v);
+  else
+    st4(p, v);
+  return v;
+}
+__device__ __forceinline__ f32x4 st4_kept(bf16_t* p, f32x4 v, int nt) {
+  uint2 u = f32_to_bf16x4(v);
+  // opaque to the optimiser: it otherwise re-derives each kept value with its own conversion
+  // (v_cvt_pk_bf16_f32 v, 0 + shift) instead of widening the two packed words
+  asm volatile("" : "+v"(u.x), "+v"(u.y));
+  typedef uint32_t u32x2_ __attribute__((ext_vector_type(2)));
+  if (nt)
+    __builtin_nontemporal_store(__builtin_bit_cast(u32x2_, u), reinterpret_cast<u32x2_*>(p));
+  else
+    *reinterpret_cast<uint2*>(p) = u;
+  return bf16x4_to_f32(u);
+}
 template <class T>
 __device__ __forceinline__ float rnd1(float v) {
   if constexpr (sizeof(T) == 2)
