@@ -125,6 +125,22 @@ __device__ __forceinline__ void bstore4e(__amdgpu_buffer_rsrc_t r, bool ok, uint
   }
 }
 
+// Buffer stores with the nontemporal bit (cache policy 2: streamed past the caches) chosen at run
+// time; the policy operand must be an immediate.
+template <class V>
+__device__ __forceinline__ void bstore_nt(V v, __amdgpu_buffer_rsrc_t r, int off, int soff, int nt) {
+  if constexpr (sizeof(V) == 2) {
+    if (nt) __builtin_amdgcn_raw_buffer_store_b16(v, r, off, soff, 2);
+    else __builtin_amdgcn_raw_buffer_store_b16(v, r, off, soff, 0);
+  } else if constexpr (sizeof(V) == 4) {
+    if (nt) __builtin_amdgcn_raw_buffer_store_b32(v, r, off, soff, 2);
+    else __builtin_amdgcn_raw_buffer_store_b32(v, r, off, soff, 0);
+  } else {
+    if (nt) __builtin_amdgcn_raw_buffer_store_b128(v, r, off, soff, 2);
+    else __builtin_amdgcn_raw_buffer_store_b128(v, r, off, soff, 0);
+  }
+}
+
 // Wave-level (64 lanes) sum.
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
@@ -213,8 +229,8 @@ enum : int { DK_FOLDED = 10100 };
 // nontemporally when set (A/B runs only; default from DORKNET_NT_STORES, else 0).
 // Nontemporal output stores per kernel family (tuning knob dk_debug_set_gemm_config(4, mask), env
 // DORKNET_NT_STORES=mask): bit kNt* set = that family's main output stores are nontemporal.
-enum NtFam : int { kNtDwFwd = 0, kNtDwBwd = 1, kNtBnAdd = 2, kNtPwsBwd = 3, kNtPwsFwd = 4, kNtPwsDgrad = 5, kNtGemm = 6, kNtStem = 7 };
-constexpr int kNtDefault = 127;  // families 0-6: config 3 8.868 -> 8.819 ms, config 5 7.596 -> 7.566 (profiles/r03q_ntfam_config*.txt)
+enum NtFam : int { kNtDwFwd = 0, kNtDwBwd = 1, kNtBnAdd = 2, kNtPwsBwd = 3, kNtPwsFwd = 4, kNtPwsDgrad = 5, kNtGemm = 6, kNtStem = 7, kNtPwd = 8, kNtPwd16 = 9 };
+constexpr int kNtDefault = 383;  // families 0-6: config 3 8.868 -> 8.819 ms, config 5 7.596 -> 7.566 (profiles/r03q_ntfam_config*.txt); family 8 (fp32 deep pointwise): config 3 8.697 -> 8.650 ms, 3 of 3 (profiles/r04nt_ab.txt); 9 (their bf16 twins) neutral, off
 int nt_stores(int fam);
 
 // Split-K second stage (reduce.hip): out = sum_s ws[s][M][N] (+ l2 * w), fixed order.

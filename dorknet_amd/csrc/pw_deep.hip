@@ -127,6 +127,7 @@ struct FwdArgs {
   int M, N, H, W, OH, OW, sa;
   uint32_t xbytes;
   FoldTail ft;
+  int nt;             // nontemporal y stores (nt_stores(kNtPwd))
 };
 
 // The block's partial row of column sums (fwd: sum y, sum y^2; dgrad: the BN-backward sums) from
@@ -256,7 +257,7 @@ __global__ __launch_bounds__(NT, fwd_wps<KR>()) void fwd_kernel(FwdArgs a) {
     for (int r = 0; r < 16; ++r) {
       const float v = acc[r];  // (not bit_cast(acc[r]): hipcc 7.2 stored element 0 for every r)
       if (!(DK_PWD_EXP & 1))
-        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), ry, (int)eofs[r], 0, 0);
+        bstore_nt(__builtin_bit_cast(uint32_t, v), ry, (int)eofs[r], 0, a.nt);
     }
     if constexpr (STATS) {
       if (t * TR + TR <= a.M) {  // a whole tile (uniform): no row masks
@@ -305,6 +306,7 @@ struct DgradArgs {
   double* part;       // [gridDim.x][2][N]
   int M, N;
   FoldTail ft;
+  int nt;             // nontemporal dy / dx stores (nt_stores(kNtPwd))
 };
 
 template <int KR, bool RES, bool PART>
@@ -361,7 +363,7 @@ __global__ __launch_bounds__(NT, dgrad_wps<KR>()) void dgrad_kernel(DgradArgs a)
         v[e] = (DK_PWD_EXP & 2) ? ge + xe : bn_bwd_elem(xe, ge, mu[e], is[e], f[e], k1[e], k2[e]);
       }
       st4(dst + r * SK + 4 * kv, v);
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rdy, (int)lofs[j], 0, 0);
+      bstore_nt(__builtin_bit_cast(u32x4, v), rdy, (int)lofs[j], 0, a.nt);
     }
   };
 
@@ -407,7 +409,7 @@ __global__ __launch_bounds__(NT, dgrad_wps<KR>()) void dgrad_kernel(DgradArgs a)
     for (int r = 0; r < 16; ++r) {
       const float v = acc[r];  // (not bit_cast(acc[r]): hipcc 7.2 stored element 0 for every r)
       if (!(DK_PWD_EXP & 1))
-        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), rdx, (int)eofs[r], 0, 0);
+        bstore_nt(__builtin_bit_cast(uint32_t, v), rdx, (int)eofs[r], 0, a.nt);
     }
     if constexpr (PART) {
       const bool full = t * TR + TR <= a.M;  // a whole tile (uniform): no row masks
@@ -798,6 +800,7 @@ int pw_deep_fwd(const float* x, int N, int H, int W, int stride, int OH, int OW,
   pwd::FwdArgs a{x, w, bias, y, im, iis, ig, ib, irelu, part, M, K, H, W, OH, OW, stride,
                  (uint32_t)((size_t)N * H * W * C * 4)};
   if (ft && part) a.ft = *ft;
+  a.nt = nt_stores(kNtPwd);
   const dim3 grid(pw_deep_fwd_rows(M, K, C), K / pwd::NB);
   if (grid.x == 0) return DK_ERR_ARGS;
 #define DK_L(kr, B_, S_, T_)                                                                          \
@@ -841,6 +844,7 @@ int pw_deep_dgrad_bnbwd(const float* g, const float* bn_x, int M, int K, int C, 
                         const FoldTail* ft) {
   pwd::DgradArgs a{g, bn_x, dy_out, w, dx, res, x, om, ois, og, ob, k12, orelu, im, iis, ig, ib, irelu, part, M, C};
   if (ft && part) a.ft = *ft;
+  a.nt = nt_stores(kNtPwd);
   const dim3 grid(pw_deep_dgrad_rows(M, K, C), C / pwd::NB);
   if (grid.x == 0) return DK_ERR_ARGS;
 #define DK_L(kr, R_, P_) hipLaunchKernelGGL((pwd::dgrad_kernel<kr, R_, P_>), grid, dim3(pwd::NT), 0, st, a)

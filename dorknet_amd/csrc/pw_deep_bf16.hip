@@ -120,6 +120,7 @@ struct FwdArgs {
   double* part;       // [gridDim.x][2][N]
   int M, N;
   FoldTail ft;
+  int nt;             // nontemporal output stores (nt_stores(kNtPwd16))
 };
 
 template <int KR, bool BN, bool STATS, bool HB>
@@ -218,7 +219,7 @@ __global__ __launch_bounds__(NT, fwd_wps<KR>()) void fwd_kernel(FwdArgs a) {
       float v = acc[r];
       if constexpr (HB) v += bias;
       const uint16_t bits = bf16_bits(v);
-      __builtin_amdgcn_raw_buffer_store_b16(bits, ry, (int)(eofs0 + (uint32_t)(((r & 3) + 8 * (r >> 2)) * N) * 2u), 0, 0);
+      bstore_nt(bits, ry, (int)(eofs0 + (uint32_t)(((r & 3) + 8 * (r >> 2)) * N) * 2u), 0, a.nt);
       if constexpr (STATS) {
         const int dm = (r & 3) + 8 * (r >> 2);
         const double d = (full || mb + dm < a.M) ? (double)bf16_val(bits) : 0.0;
@@ -251,6 +252,7 @@ struct DgradArgs {
   double* part;
   int M, N;
   FoldTail ft;
+  int nt;             // nontemporal output stores (nt_stores(kNtPwd16))
 };
 
 template <int KR, bool RES, bool PART>
@@ -324,7 +326,7 @@ __global__ __launch_bounds__(NT, dgrad_wps<KR>()) void dgrad_kernel(DgradArgs a)
         }
       const u32x4 q = pack8(gv[0], gv[1]);
       *reinterpret_cast<u32x4*>(dst + (r0 + j * (NT / KV)) * SK + 8 * kv) = q;
-      __builtin_amdgcn_raw_buffer_store_b128(q, rdy, (int)(lofs0 + j * kLStep), 0, 0);
+      bstore_nt(q, rdy, (int)(lofs0 + j * kLStep), 0, a.nt);
     }
   };
 
@@ -372,7 +374,7 @@ __global__ __launch_bounds__(NT, dgrad_wps<KR>()) void dgrad_kernel(DgradArgs a)
       float v = acc[r];
       if constexpr (RES) v += bf16_val(ers[r]);
       const uint16_t bits = bf16_bits(v);
-      __builtin_amdgcn_raw_buffer_store_b16(bits, rdx, eofs(r), 0, 0);
+      bstore_nt(bits, rdx, eofs(r), 0, a.nt);
       if constexpr (PART) {
         const int dm = (r & 3) + 8 * (r >> 2);
         const float gs = bf16_val(bits), x = bf16_val(exi[r]);
@@ -482,6 +484,7 @@ int pw_deep16_fwd(const bf16_t* x, int M, const float* w, int K, int C, const fl
                   const FoldTail* ft) {
   pwd16::FwdArgs a{x, w, bias, y, im, iis, ig, ib, irelu, part, M, K};
   if (ft && part) a.ft = *ft;
+  a.nt = nt_stores(kNtPwd16);
   const dim3 grid(pw_deep16_fwd_rows(M, K, C), K / pwd16::NB);
   if (grid.x == 0) return DK_ERR_ARGS;
 #define DK_L(kr, B_, S_)                                                                          \
@@ -516,6 +519,7 @@ int pw_deep16_dgrad_bnbwd(const bf16_t* g, const bf16_t* bn_x, int M, int K, int
                           const FoldTail* ft) {
   pwd16::DgradArgs a{g, bn_x, dy_out, w, dx, res, x, om, ois, og, ob, k12, orelu, im, iis, ig, ib, irelu, part, M, C};
   if (ft && part) a.ft = *ft;
+  a.nt = nt_stores(kNtPwd16);
   const dim3 grid(pw_deep16_dgrad_rows(M, K, C), C / pwd16::NB);
   if (grid.x == 0) return DK_ERR_ARGS;
 #define DK_L(kr, R_, P_) hipLaunchKernelGGL((pwd16::dgrad_kernel<kr, R_, P_>), grid, dim3(pwd16::NT), 0, st, a)
