@@ -954,7 +954,10 @@ static int bn_bwd_apply_t(const E* x, const E* dy, long long numel, int C, const
       default: BBA(8, true); break;
     }
 #undef BBA
-  } else if (vec)
+  } else if (vec && nt_stores(kNtBnBwd))
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<4, 4, true, E>), grid, dim3(256), 0, as_stream(stream), x, dy, P, C, ppb,
+                       mean, invstd, gamma, beta, relu, k12, dx);
+  else if (vec)
     hipLaunchKernelGGL((bn_bwd_apply_kernel<4, 4, false, E>), grid, dim3(256), 0, as_stream(stream), x, dy, P, C, ppb,
                        mean, invstd, gamma, beta, relu, k12, dx);
   else

@@ -406,7 +406,7 @@ __global__ __launch_bounds__(256) void dw_dgrad_subpixel_kernel(const T* __restr
                                                                 const float* __restrict__ wt, T* __restrict__ dx,
                                                                 int N, int H, int W, int C, int OH, int OW,
                                                                 const T* __restrict__ res, JoinBwd jn,
-                                                                double* __restrict__ part, FoldTail ft) {
+                                                                double* __restrict__ part, FoldTail ft, int nt) {
   using RP = SubPix<R, ST, PAD>;
   using SP = SubPix<S, ST, PAD>;
   constexpr int DR0 = RP::dmin(), NR = RP::dmax() - RP::dmin() + 1;
@@ -540,7 +540,7 @@ __global__ __launch_bounds__(256) void dw_dgrad_subpixel_kernel(const T* __restr
               }
             }
           }
-          bstore4e<T>(rdx, ok, off, o);
+          bstore4e_nt<T>(rdx, ok, off, o, nt);
         }
       }
     }
@@ -1268,11 +1268,11 @@ static int dw_dgrad(const T* dy, int N, int OH, int OW, int C, const float* w_cr
       FoldTail ft;                                                                                                   \
       if (!fold_take(part, (int)grid.x, C, 1, &ft)) ft.part = nullptr;                                              \
       hipLaunchKernelGGL((dw_dgrad_subpixel_kernel<RR, SS, STR, PD, T, true>), grid, dim3(256), 0, st, dy, gb,      \
-                         w_crs, dx, N, H, W, C, OH, OW, res, *jn, part, ft);                                         \
+                         w_crs, dx, N, H, W, C, OH, OW, res, *jn, part, ft, nt_stores(kNtDwDgrad));                  \
       return fold_status(launch_status(), ft);                                                                       \
     }                                                                                                                \
     hipLaunchKernelGGL((dw_dgrad_subpixel_kernel<RR, SS, STR, PD, T>), grid, dim3(256), 0, st, dy, gb, w_crs, dx, N, \
-                       H, W, C, OH, OW, res, JoinBwd{}, nullptr, FoldTail{});                                        \
+                       H, W, C, OH, OW, res, JoinBwd{}, nullptr, FoldTail{}, nt_stores(kNtDwDgrad));                 \
     return launch_status();                                                                                          \
   }
   DW_SUBPIX(3, 3, 2, 1)

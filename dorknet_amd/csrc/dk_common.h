@@ -141,6 +141,22 @@ __device__ __forceinline__ void bstore_nt(V v, __amdgpu_buffer_rsrc_t r, int off
   }
 }
 
+// bstore4e with the nontemporal bit chosen at run time
+template <class T>
+__device__ __forceinline__ void bstore4e_nt(__amdgpu_buffer_rsrc_t r, bool ok, uint32_t e, f32x4 v, int nt) {
+  if constexpr (sizeof(T) == 2) {
+    const uint32_t off = ok ? e * 2u : kOOBBytes;
+    typedef uint32_t u32x2_ __attribute__((ext_vector_type(2)));
+    const u32x2_ u = __builtin_bit_cast(u32x2_, f32_to_bf16x4(v));
+    if (nt) __builtin_amdgcn_raw_buffer_store_b64(u, r, (int)off, 0, 2);
+    else __builtin_amdgcn_raw_buffer_store_b64(u, r, (int)off, 0, 0);
+  } else {
+    typedef uint32_t u32x4_ __attribute__((ext_vector_type(4)));
+    const uint32_t off = ok ? e * 4u : kOOBBytes;
+    bstore_nt(__builtin_bit_cast(u32x4_, v), r, (int)off, 0, nt);
+  }
+}
+
 // Wave-level (64 lanes) sum.
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
@@ -229,7 +245,7 @@ enum : int { DK_FOLDED = 10100 };
 // nontemporally when set (A/B runs only; default from DORKNET_NT_STORES, else 0).
 // Nontemporal output stores per kernel family (tuning knob dk_debug_set_gemm_config(4, mask), env
 // DORKNET_NT_STORES=mask): bit kNt* set = that family's main output stores are nontemporal.
-enum NtFam : int { kNtDwFwd = 0, kNtDwBwd = 1, kNtBnAdd = 2, kNtPwsBwd = 3, kNtPwsFwd = 4, kNtPwsDgrad = 5, kNtGemm = 6, kNtStem = 7, kNtPwd = 8, kNtPwd16 = 9 };
+enum NtFam : int { kNtDwFwd = 0, kNtDwBwd = 1, kNtBnAdd = 2, kNtPwsBwd = 3, kNtPwsFwd = 4, kNtPwsDgrad = 5, kNtGemm = 6, kNtStem = 7, kNtPwd = 8, kNtPwd16 = 9, kNtDwDgrad = 10, kNtBnBwd = 11 };
 constexpr int kNtDefault = 383;  // families 0-6: config 3 8.868 -> 8.819 ms, config 5 7.596 -> 7.566 (profiles/r03q_ntfam_config*.txt); family 8 (fp32 deep pointwise): config 3 8.697 -> 8.650 ms, 3 of 3 (profiles/r04nt_ab.txt); 9 (their bf16 twins) neutral, off
 int nt_stores(int fam);
 
