@@ -246,7 +246,7 @@ enum : int { DK_FOLDED = 10100 };
 // Nontemporal output stores per kernel family (tuning knob dk_debug_set_gemm_config(4, mask), env
 // DORKNET_NT_STORES=mask): bit kNt* set = that family's main output stores are nontemporal.
 enum NtFam : int { kNtDwFwd = 0, kNtDwBwd = 1, kNtBnAdd = 2, kNtPwsBwd = 3, kNtPwsFwd = 4, kNtPwsDgrad = 5, kNtGemm = 6, kNtStem = 7, kNtPwd = 8, kNtPwd16 = 9, kNtDwDgrad = 10, kNtBnBwd = 11 };
-constexpr int kNtDefault = 383;  // families 0-6: config 3 8.868 -> 8.819 ms, config 5 7.596 -> 7.566 (profiles/r03q_ntfam_config*.txt); family 8 (fp32 deep pointwise): config 3 8.697 -> 8.650 ms, 3 of 3 (profiles/r04nt_ab.txt); 9 (their bf16 twins) neutral, off
+constexpr int kNtDefault = 2431;  // families 0-6: config 3 8.868 -> 8.819 ms, config 5 7.596 -> 7.566 (profiles/r03q_ntfam_config*.txt); 8 (fp32 deep pointwise): config 3 8.697 -> 8.650 ms, 3 of 3 (profiles/r04nt_ab.txt); 11 (BN backward apply): config 3 8.719 -> 8.700 ms (profiles/r04nt2_ab.txt); off: 9 (bf16 deep pointwise, neutral), 10 (strided depthwise dgrad, fp32 neutral or slower)
 int nt_stores(int fam);
 
 // Split-K second stage (reduce.hip): out = sum_s ws[s][M][N] (+ l2 * w), fixed order.
