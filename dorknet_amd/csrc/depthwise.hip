@@ -154,7 +154,7 @@ static inline int dw_fwd_seg(int OH) {
 // fused ReLU (batch_norm.py:125-174, dk_bn_bwd_partial_f64); xo is that BN's raw input.
 // T: activation storage (float, or bf16_t for BASELINE config 5); compute is fp32, and the
 // statistics see the stored (rounded) outputs.
-template <int R, int S, int ST, bool BN, bool RELU, int STATS, int WL, class T = float, bool NORING = false>
+template <int R, int S, int ST, bool BN, bool RELU, int STATS, int WL, class T = float>
 __global__ __launch_bounds__(256) void dw_fwd_kernel(const T* __restrict__ x, uint32_t xbytes,
                                                      const float* __restrict__ wt, const float* __restrict__ bias,
                                                      T* __restrict__ y, int N, int H, int W, int C, int OH, int OW,
@@ -207,7 +207,7 @@ __global__ __launch_bounds__(256) void dw_fwd_kernel(const T* __restrict__ x, ui
     // seventh of this VALU-bound kernel's instructions)
     // (stride 2 keeps the shifted window: two of its three rows are new each output row, and the
     // unrolled ring took it past 256 registers)
-    constexpr bool RING = ST == 1 && !NORING;
+    constexpr bool RING = ST == 1;
     constexpr int PER = RING ? R / std::gcd(R, ST) : 1;
     f32x4 win[R][NC];
 #pragma unroll
@@ -1138,24 +1138,8 @@ static int launch_dw_fwd(const T* x, const float* wt, const float* bias, T* y, i
     DW_LAUNCH(false, 0, 0);
   else if (wl == 0 && bn.mean && mode == 0)
     DW_LAUNCH(true, 0, 0);
-  else if (wl == 1 && bn.mean && mode == 1) {
-    // bf16 at 56 x 56: the shifted window measured 8 % faster than the ring (108 vs 117 us at batch
-    // 512, profiles/r04dw1_dwfwd.txt, r04dw2_dwseg.txt); the ring everywhere else
-    if constexpr (sizeof(T) == 2 && ST == 1) {
-      if (OW >= 48) {
-        if (bn.relu)
-          hipLaunchKernelGGL((dw_fwd_kernel<R, S, ST, true, true, 1, 1, T, true>), grid, dim3(256), 0, st, x, xb, wt,
-                             bias, y, N, H, W, C, OH, OW, pad, bn, part, xo, obn, res, ft, nt_stores(kNtDwFwd),
-                             dw_fwd_seg(OH));
-        else
-          hipLaunchKernelGGL((dw_fwd_kernel<R, S, ST, true, false, 1, 1, T, true>), grid, dim3(256), 0, st, x, xb, wt,
-                             bias, y, N, H, W, C, OH, OW, pad, bn, part, xo, obn, res, ft, nt_stores(kNtDwFwd),
-                             dw_fwd_seg(OH));
-        return fold_status(launch_status(), ft);
-      }
-    }
+  else if (wl == 1 && bn.mean && mode == 1)
     DW_LAUNCH(true, 1, 1);
-  }
   else if (wl == 1 && bn.mean && mode == 0)
     DW_LAUNCH(true, 0, 1);
   else if (wl == 1 && !bn.mean && mode == 1)
