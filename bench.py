@@ -7,7 +7,8 @@ Multi-GPU: one process per GPU (torchrun), data parallel over RCCL, per-rank bat
 
 Prints ONE JSON line (rank 0).  Besides the driver's contract fields it carries
   roofline      -- the dominant kernel (largest share of the step, measured with HIP events
-                   around every call of that C-ABI entry point during the timed region):
+                   around every call of that C-ABI entry point during a second run of the K
+                   timed steps; `value` comes from the first, uninstrumented run):
                    algorithmic work per call / average call duration vs the MI355X peak;
   cpu_baseline  -- the reference's CPU path restated (oracle/cpu_path.py: C/OpenMP versions
                    of its Cython kernels + numpy BLAS), timed on this host at N=1 on a small
@@ -48,7 +49,8 @@ def parse():
                          "5 = bf16 depthwise-separable stack (secondary lines, not the headline metric)")
     ap.add_argument("--pmc", default=None,
                     help="per-kernel HBM traffic from rocprofv3 FETCH_SIZE/WRITE_SIZE passes of this same command "
-                         "(scripts/pmc_summary.py output; default: the newest profiles/*_pmc.json)")
+                         "(scripts/pmc_summary.py output; default: the newest summary of this config in "
+                         "profiles/pmc_index.json)")
     a = ap.parse_args()
     # enough warmup for the clocks to settle (the first timed steps after 3 warmups ran up to 5 %
     # slow, profiles/r03s_cfg2_rows.txt round 1), and more steps for config 2's 1.6 ms pass
@@ -200,8 +202,9 @@ ENTRY_KERNEL = {
                              ("dk::pws::fwd_kernel", ""), ("dk::pwd::fwd_kernel", r"^dk::pwd::fwd_kernel<\d+, \w+, true")],
     # config 5 (bf16 storage): the BN-backward-on-load pointwise dgrad (streaming K = C = 64 and deep
     # kernels, the tiled engine elsewhere), the fused depthwise backward and the depthwise forward
-    "dk_pwconv_dgrad_bnbwd_bf16": [("dk::pwsh::dgrad_bnbwd_kernel", ""), ("dk::pwsh::dgrad_deep_kernel", ""),
+    "dk_pwconv_dgrad_bnbwd_bf16": [("dk::pwsh::dgrad_bnbwd_kernel", ""), ("dk::pwd16::dgrad_kernel", ""),
                                    ("dk::igemm_f32", r"dk::LdMatKCT<[^>]*>, dk::MatBwdDescE<unsigned short>")],
+    "dk_pwconv_fwd_ex_bf16": [("dk::pwsh::fwd_kernel", ""), ("dk::pwd16::fwd_kernel", "")],
     "dk_dwconv_bwd_bnbwd_bf16": ("dk::dw_bwd_fused_kernel", r"unsigned short>"),
     "dk_dwconv_fwd_ex_bf16": ("dk::dw_fwd_kernel", r"unsigned short>"),
     "dk_conv2d_fwd_narrow_f32": ("dk::nar::fwd_kernel", ""),
@@ -246,14 +249,24 @@ def stream_ceiling(entry):
             "probe": "dk_debug_stream_mix: float4 streams of 205 MB, median of 10"}
 
 
-def pmc_traffic(entry, path):
-    """Average HBM bytes per dispatch of `entry`'s kernel from a committed PMC summary (`path`, or
-    the newest profiles/*_pmc.json that has the kernel), or (None, None) when there is none."""
-    import glob
+def pmc_candidates(config):
+    """The committed PMC summaries of bench config `config`, newest first, in the order they were
+    added to profiles/pmc_index.json (scripts/pmc_summary.py --add): commit order, not file names."""
+    path = os.path.join(ROOT, "profiles", "pmc_index.json")
+    if not os.path.exists(path):
+        return []
+    with open(path) as f:
+        idx = json.load(f)
+    return [os.path.join(ROOT, e["file"]) for e in reversed(idx.get("entries", [])) if e.get("config") == config]
+
+
+def pmc_traffic(entry, path, config=3):
+    """Average HBM bytes per dispatch of `entry`'s kernels from a committed PMC summary (`path`, or
+    the newest summary of this config in profiles/pmc_index.json that has them), or (None, None)."""
     kern = ENTRY_KERNEL.get(entry)
     if not kern:
         return None, None
-    cands = [path] if path else sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")), reverse=True)
+    cands = [path] if path else pmc_candidates(config)
     pats = kern if isinstance(kern, list) else [kern if isinstance(kern, tuple) else (kern, "")]
     for p in cands:
         if not p or not os.path.exists(p):
@@ -268,6 +281,14 @@ def pmc_traffic(entry, path):
         if n:
             return t / n, os.path.relpath(p, ROOT)
     return None, None
+
+
+def attach_traffic(roof, entry, path, config):
+    traffic, src = pmc_traffic(entry, path, config)
+    if traffic is not None:
+        roof["traffic"] = round(traffic / 1e6, 2)
+        roof["traffic_unit"] = "MB per launch (HBM, rocprofv3 2*FETCH_SIZE + WRITE_SIZE)"
+        roof["traffic_source"] = src
 
 
 def cpu_info():
@@ -517,6 +538,7 @@ def other_config(args):
             torch.cuda.synchronize()
         roof = roofline_entry(dominant, ins.summary()[dominant], args.steps)
         roof["timing"] = "dominant entry timed with HIP events over a second run of the same K steps"
+        attach_traffic(roof, dominant, args.pmc, args.config)
     out = {"metric": metric, "value": round((1.0 if args.config == 2 else args.batch) / per, 2), "unit": unit,
            "n_gpus": 1, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * per, 3),
            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": dtype,
@@ -637,38 +659,37 @@ def main():
         breakdown["_step_roofline_bound_ms"] = round(step_bound, 3)
         barrier()
 
-    ins = Instrument([dominant], reserve=(breakdown[dominant]["calls"] * args.steps + 8)) if dominant else None
+    # value: K uninstrumented steps between barriers (max over ranks)
     barrier()
     t0 = time.perf_counter()
-    if ins:
-        ins.__enter__()
-    try:
-        for _ in range(args.steps):
-            step()
-        barrier()
-    finally:
-        if ins:
-            ins.__exit__(None, None, None)
+    for _ in range(args.steps):
+        step()
+    barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
+    # roofline: the dominant entry's live call durations from a second run of the same K steps with
+    # its calls bracketed by HIP events on the launch stream (the event records cost ~1 % of the
+    # step, so they stay out of the run that gives `value`: VERDICT r4, profiles/r04g_*)
     roof = None
-    if ins:
+    if dominant:
+        ins = Instrument([dominant], reserve=(breakdown[dominant]["calls"] * args.steps + 8))
+        with ins:
+            for _ in range(args.steps):
+                step()
+            barrier()
         s = ins.summary()[dominant]
         roof = roofline_entry(dominant, s, args.steps)
+        roof["timing"] = "dominant entry timed with HIP events over a second run of the same K steps"
         if roof["bound"] == "hbm":
             ceil = stream_ceiling(dominant)
             if ceil is not None:
                 ceil["frac"] = round(roof["achieved"] / ceil["value"], 4)
                 roof["practical_peak"] = ceil
-        traffic, src = pmc_traffic(dominant, args.pmc)
-        if traffic is not None:
-            roof["traffic"] = round(traffic / 1e6, 2)
-            roof["traffic_unit"] = "MB per launch (HBM, rocprofv3 2*FETCH_SIZE + WRITE_SIZE)"
-            roof["traffic_source"] = src
+        attach_traffic(roof, dominant, args.pmc, 3)
     value = world * args.batch * args.steps / elapsed
     ms_per_step = 1e3 * elapsed / args.steps
     cpu = None

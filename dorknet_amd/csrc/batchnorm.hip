@@ -553,7 +553,6 @@ static int bn_blocks(int P, int C) {
 // flight 4, nontemporal dx stores, 8 rows per pixel lane, up to 16384 blocks: measured
 // best or within 1 % of best on every ResNet BatchNorm shape (scripts/ew_tune.py; -10 % on
 // res1/res3 vs the row-loop defaults of the other BN passes).
-static int g_ew_variant = 22;
 
 static int bn_apply_blocks(int P, int C, int V) {
   const RowGeom g = row_geom(C, V);
@@ -656,7 +655,7 @@ DK_API size_t dk_bn_partials_workspace_bytes(int nblk, int C) {
 
 // Tuning knob (not thread-safe): launch variant of dk_bn_bwd_apply_f32 (-1 = built-in).
 DK_API int dk_debug_set_ew_variant(int v) {
-  g_ew_variant = v < 0 ? 22 : v;
+  knob_set(kKnobEwVariant, v);
   return 32;
 }
 
@@ -932,7 +931,7 @@ static int bn_bwd_apply_t(const E* x, const E* dy, long long numel, int C, const
   if (!vec && sizeof(E) != 4) return DK_ERR_ARGS;
   const int V = vec ? 4 : 1;
   const RowGeom g = row_geom(C, V);
-  const int var = g_ew_variant;
+  const int var = knob(kKnobEwVariant);
   int nblk = bn_apply_blocks(P, C, V);
   if (var >= 0) {  // tuning knob: rows per pixel lane 16 / 8 / 32 / 64, cap 4096 / 16384
     const int rpl[4] = {16, 8, 32, 64};

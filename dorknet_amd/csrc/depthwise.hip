@@ -131,12 +131,11 @@ struct DwTile {
 // within noise of best on every training shape of configs 3 and 5 (scripts/dw_fwd_seg.py,
 // profiles/r03q_dw_seg_{f32,bf16}.txt: fewer rows per thread re-load the window more often and the
 // extra blocks do not pay for it).
-static int g_dw_seg = -1;  // tuning knob dk_debug_set_gemm_config(8, rows); -1 = the default
-void dw_seg_set(int v) { g_dw_seg = v; }
 // The default: segments of at most 8 rows, balanced (OH = 28 -> 4 x 7, OH = 14 -> 2 x 7 instead of
 // 8 + 8 + 8 + 4 / 8 + 6: the short last segments left threads idle; profiles/r04dw2_dwseg.txt).
 static inline int dw_fwd_seg(int OH) {
-  if (g_dw_seg > 0) return g_dw_seg;
+  const int seg = knob(kKnobDwSeg);  // tuning knob (kind 8): rows per thread; -1 = this rule
+  if (seg > 0) return seg;
   const int nseg = (OH + 7) / 8;
   return (OH + nseg - 1) / nseg;
 }
@@ -1071,15 +1070,7 @@ static inline int dwb_cl(int W, int C) {
 // registers allow three); above that the batch is dealt into runs so the grid is one round (a
 // second, partial round of blocks cost small images up to twice the time: 7 x 7 x 512 ran 1024
 // one-image blocks).  0 = one image per block always.
-static int g_dwb_blocks = -1;  // tuning knob dk_debug_set_gemm_config(7, v)
-void dwb_blocks_set(int v) { g_dwb_blocks = v; }
-static inline int dwb_target_blocks() {
-  if (g_dwb_blocks < 0) {
-    const char* e = getenv("DORKNET_DWB_BLOCKS");
-    g_dwb_blocks = e ? atoi(e) : 768;
-  }
-  return g_dwb_blocks;
-}
+static inline int dwb_target_blocks() { return knob(kKnobDwbBlocks); }  // kind 7
 static inline int dwb_nranges(int N, int W, int C, int cl) {
   const int per_image = ((W + cl - 1) / cl) * ((C / 4) / (256 / cl));
   const int t = dwb_target_blocks();

@@ -249,6 +249,17 @@ enum NtFam : int { kNtDwFwd = 0, kNtDwBwd = 1, kNtBnAdd = 2, kNtPwsBwd = 3, kNtP
 constexpr int kNtDefault = 2431;  // families 0-6: config 3 8.868 -> 8.819 ms, config 5 7.596 -> 7.566 (profiles/r03q_ntfam_config*.txt); 8 (fp32 deep pointwise): config 3 8.697 -> 8.650 ms, 3 of 3 (profiles/r04nt_ab.txt); 11 (BN backward apply): config 3 8.719 -> 8.700 ms (profiles/r04nt2_ab.txt); off: 9 (bf16 deep pointwise, neutral), 10 (strided depthwise dgrad, fp32 neutral or slower)
 int nt_stores(int fam);
 
+// Run-time switches and tuning knobs (knobs.hip): one registry of atomics, defaults from the DORKNET_*
+// environment read once; dk_debug_set_gemm_config(kind = KnobId, v) overrides (-1 = default).
+enum KnobId : int {
+  kKnobRowCfg = 0, kKnobSplitCfg = 1, kKnobFillSplits = 2, kKnobPwStream = 3, kKnobNtStores = 4, kKnobPwsBwdPf = 5,
+  kKnobDwbBlocks = 7, kKnobDwSeg = 8, kKnobPwsh = 9, kKnobPwDeep = 11, kKnobPwDeep16 = 13, kKnobPwDeepBwd = 14,
+  kKnobPwStream128 = 15, kKnobPwfPrefetch = 16, kKnobPwfBlocksPerCu = 17, kKnobWgradBlocks = 18, kKnobEwVariant = 19,
+  kNumKnobs = 20
+};
+int knob(int id);
+void knob_set(int id, int v);
+
 // Split-K second stage (reduce.hip): out = sum_s ws[s][M][N] (+ l2 * w), fixed order.
 //   mode 0: out[m][n];  mode 1: columns (r, s, c) with c padded to Cp -> out KCRS.
 int splitk_reduce(const float* ws, int splits, int M, int N, float* out, const float* w, float l2, int mode, int C,
@@ -258,14 +269,9 @@ int splitk_reduce(const float* ws, int splits, int M, int N, float* out, const f
 // to launch on another stream (the weight-gradient side stream).
 int wgrad_reduce(const float* ws, int splits, int M, int N, float* out, const float* w, float l2, hipStream_t st);
 
-// Blocks the fused stride-1 depthwise backward aims for (depthwise.hip; knob kind 7, -1 = default).
-void dwb_blocks_set(int v);
-void dw_seg_set(int v);
 
 // Streaming pointwise kernels (pw_stream.hip) for the K = C = 64 shapes.
-bool pw_stream_enabled();  // DORKNET_PW_STREAM (default 1; 0 = the tiled engine everywhere, for A/B runs)
-void pw_stream_set(int v);  // tuning knob (dk_debug_set_gemm_config kind 3)
-void pw_stream_bwd_pf_set(int v);  // tuning knob (kind 5): the fused backward's operand prefetch
+bool pw_stream_enabled();  // knob kKnobPwStream (default 1; 0 = the tiled engine everywhere, for A/B runs)
 bool pw_stream_dgrad_ok(int K, int C, int M);
 int pw_stream_dgrad_rows(int M);
 bool pw_stream_bwd_ok(int K, int C, int M);
@@ -289,7 +295,6 @@ int pw_stream_dgrad_bnbwd(const float* g, const float* bn_x, int M, const float*
                           hipStream_t st, const struct FoldTail* ft = nullptr);
 
 // fp32 deep streaming pointwise kernels (pw_deep.hip): reduction 64-512 with 128+ channels on a side.
-void pw_deep_set(int v);  // tuning knob (dk_debug_set_gemm_config kind 11)
 bool pw_deep_fwd_ok(int K, int C, int M, size_t xbytes);
 int pw_deep_fwd_rows(int M, int K, int C);
 int pw_deep_fwd_slices(int M, int K, int C);
@@ -299,8 +304,16 @@ int pw_deep_fwd(const float* x, int N, int H, int W, int stride, int OH, int OW,
 bool pw_deep_dgrad_ok(int K, int C, int M);
 int pw_deep_dgrad_rows(int M, int K, int C);
 int pw_deep_dgrad_slices(int M, int K, int C);
+// The fused deep backward (dgrad + weight gradient in one pass, dy never stored): K in {128, 256}.
+bool pw_deep_bwd_ok(int K, int C, int M);
+int pw_deep_bwd_rows(int M, int K, int C);
+int pw_deep_bwd_slices(int M, int K, int C);
+int pw_deep_bwd_bnbwd(const float* g, const float* bn_x, int M, int K, int C, const float* om, const float* ois,
+                      const float* og, const float* ob, int orelu, const float* k12, const float* w, float* dx,
+                      const float* res, const float* x, const float* im, const float* iis, const float* ig,
+                      const float* ib, int irelu, double* part, float* wpart, hipStream_t st,
+                      const struct FoldTail* ft = nullptr);
 // bf16 weight-stationary deep pointwise kernels (pw_deep_bf16.hip), used by the pw_stream_bf16 entries.
-void pw_deep16_set(int v);  // tuning knob (kind 13)
 bool pw_deep16_fwd_ok(int K, int C, int M);
 bool pw_deep16_dgrad_ok(int K, int C, int M);
 int pw_deep16_fwd_rows(int M, int K, int C);
@@ -313,12 +326,6 @@ int pw_deep16_dgrad_bnbwd(const bf16_t* g, const bf16_t* bn_x, int M, int K, int
                           bf16_t* dx, const bf16_t* res, const bf16_t* x, const float* im, const float* iis,
                           const float* ig, const float* ib, int irelu, double* part, hipStream_t st,
                           const struct FoldTail* ft);
-void pw_deep_wgrad_set(int v);  // tuning knob (kind 12): the deep weight gradient alone
-bool pw_deep_wgrad_ok(int K, int C, int M);
-int pw_deep_wgrad_chunks(int M, int K, int C);
-size_t pw_deep_wgrad_ws_bytes(int M, int K, int C);
-int pw_deep_wgrad(const float* dy, const float* x, int M, int K, int C, const float* im, const float* iis,
-                  const float* ig, const float* ib, int irelu, float* part, hipStream_t st);
 int pw_deep_dgrad_bnbwd(const float* g, const float* bn_x, int M, int K, int C, const float* om, const float* ois,
                         const float* og, const float* ob, int orelu, const float* k12, float* dy_out, const float* w,
                         float* dx, const float* res, const float* x, const float* im, const float* iis,
@@ -340,7 +347,5 @@ int pw_stream_bf16_dgrad_bnbwd(const bf16_t* g, const bf16_t* bn_x, int M, int K
                                double* part, hipStream_t st, const struct FoldTail* ft = nullptr);
 int pw_stream_bf16_fwd_slices(int K, int C);    // channel slices of the partial rows (fold_take)
 int pw_stream_bf16_dgrad_slices(int K, int C);
-void pw_stream_bf16_deep_set(int v);  // tuning knob (dk_debug_set_gemm_config kind 10)
-void pw_stream_bf16_set(int v);  // tuning knob (dk_debug_set_gemm_config kind 9)
 
 }  // namespace dk

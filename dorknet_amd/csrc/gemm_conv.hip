@@ -5,16 +5,6 @@
 using namespace dk;
 
 namespace dk {
-int g_cfg_override[2] = {-1, -1};
-int g_fill_splits = 1;
-static int g_nt_stores = -1;
-int nt_stores(int fam) {
-  if (g_nt_stores < 0) {
-    const char* e = getenv("DORKNET_NT_STORES");  // a bitmask of NtFam families
-    g_nt_stores = e ? atoi(e) : kNtDefault;
-  }
-  return (g_nt_stores >> fam) & 1;
-}
 
 // Weight re-layouts (tiny; run once per call on the caller's stream).
 __global__ void w_kcrs_to_krsc_kernel(const float* __restrict__ w, int K, int C, int R, int S, int Cp,
@@ -67,54 +57,11 @@ __global__ void w_phase_kernel(const float* __restrict__ w, int K, int C, int R,
 
 }  // namespace dk
 
+// Tuning knobs (knobs.hip): kind = the KnobId; cfg = -1 restores the default.
 DK_API int dk_debug_set_gemm_config(int kind, int cfg) {
-  if (kind == 2) {
-    g_fill_splits = cfg < 0 ? 1 : cfg;
-    return 0;
-  }
-  if (kind == 3) {  // streaming pointwise kernels (pw_stream.hip) on / off
-    pw_stream_set(cfg < 0 ? 1 : cfg);
-    return 0;
-  }
-  if (kind == 5) {  // the streaming fused pointwise backward's operand prefetch (pw_stream.hip)
-    pw_stream_bwd_pf_set(cfg < 0 ? 0 : cfg);
-    return 0;
-  }
-  if (kind == 7) {  // blocks the fused stride-1 depthwise backward aims for (0: one image per block)
-    dwb_blocks_set(cfg < 0 ? 768 : cfg);
-    return 0;
-  }
-  if (kind == 8) {  // output rows per thread of the depthwise forward (depthwise.hip dw_fwd_seg; -1 = rule)
-    dw_seg_set(cfg);
-    return 0;
-  }
-  if (kind == 10) {  // the bf16 deep (column-sliced) streaming pointwise kernels on / off
-    pw_stream_bf16_deep_set(cfg);
-    return 0;
-  }
-  if (kind == 13) {  // the bf16 weight-stationary deep kernels (pw_deep_bf16.hip) on / off
-    pw_deep16_set(cfg);
-    return 0;
-  }
-  if (kind == 12) {  // the deep output-stationary weight gradient alone (pw_deep.hip) on / off
-    pw_deep_wgrad_set(cfg);
-    return 0;
-  }
-  if (kind == 11) {  // the fp32 deep streaming pointwise kernels (pw_deep.hip) on / off
-    pw_deep_set(cfg);
-    return 0;
-  }
-  if (kind == 9) {  // the bf16 streaming pointwise kernels (pw_stream_bf16.hip) on / off
-    pw_stream_bf16_set(cfg);
-    return 0;
-  }
-  if (kind == 4) {  // nontemporal output stores (kernels that support them)
-    g_nt_stores = cfg < 0 ? kNtDefault : cfg;
-    return 0;
-  }
-  if (kind < 0 || kind > 1) return -1;
-  g_cfg_override[kind] = cfg;
-  return kind == 0 ? kNumRowCfg : kNumSplitCfg;
+  if (kind < 0 || kind >= kNumKnobs || kind == 6 || kind == 10 || kind == 12 || kind == kKnobEwVariant) return -1;
+  knob_set(kind, cfg);
+  return kind == kKnobRowCfg ? kNumRowCfg : kind == kKnobSplitCfg ? kNumSplitCfg : 0;
 }
 
 DK_API int dk_conv_weight_krsc_f32(const float* w_kcrs, int K, int C, int R, int S, int Cp, float* w_krsc,

@@ -1092,12 +1092,10 @@ static const TileCfg kSplitCfg[] = {DK_SPLITK_CONFIGS(DK_CFG_ENTRY)};
 static const int kNumRowCfg = sizeof(kRowCfg) / sizeof(kRowCfg[0]);
 static const int kNumSplitCfg = sizeof(kSplitCfg) / sizeof(kSplitCfg[0]);
 
-extern int g_cfg_override[2];  // tuning knobs only (dk_debug_set_gemm_config, gemm_conv.hip)
 // Split-K grids fill the resident block slots once (g_fill_splits; tuning knob
 // dk_debug_set_gemm_config(2, 0/1)).  A persistent tile loop for the row problems was measured
 // and dropped (scripts/ab_step.py: 11.77 ms/step with one block per tile, 11.89 / 11.98 with
 // 1 / 2 resident waves of persistent blocks, and the loop slowed the one-tile case too).
-extern int g_fill_splits;
 constexpr int kNumCUs = 256;  // MI355X
 
 // Epilogues with an `nt` member take the nontemporal-store knob (nt_stores()).
@@ -1170,7 +1168,7 @@ static int launch_igemm(const DA& da, const DB& db, const EP& ep, int M, int N, 
                                    NT, dyn);
   if (occ < 0) return DK_ERR_ARGS;
   const int slots = occ * kNumCUs;
-  if (g_fill_splits && splits_used && splits > 1 && tiles * splits > slots && tiles <= slots) {
+  if (knob(kKnobFillSplits) && splits_used && splits > 1 && tiles * splits > slots && tiles <= slots) {
     // split-K: no second, partly filled round of blocks (the stem's 64x128 weight-gradient
     // tiles fit 3 per CU: 1024 splits ran as 768 + 256 blocks)
     splits = slots / tiles;
@@ -1202,7 +1200,7 @@ static int launch_igemm(const DA& da, const DB& db, const EP& ep, int M, int N, 
 enum : int { kRowPlain = 0, kRowBnBwd = 1, kRowConv = 2, kRowFwdH = 3 };
 
 static inline int row_config(int M, int N, int K, int kind = kRowPlain, int mf = kMfF32) {
-  if (g_cfg_override[0] >= 0) return g_cfg_override[0];
+  if (knob(kKnobRowCfg) >= 0) return knob(kKnobRowCfg);
   (void)M;
   if (mf == kMfBf16) {
     // bf16 MFMA (config 5's 14 x 14 and 7 x 7 units at batch 512; scripts/gemm_tune_deep.py --bf16,
@@ -1245,7 +1243,7 @@ static int igemm_rows(const DA& da, const DB& db, const EP& ep, int M, int N, in
 
 // Reduction-heavy problems (wgrad): split K over enough blocks to fill the chip.
 static inline int splitk_config(int M, int N, int Kred, int mf = kMfF32) {
-  if (g_cfg_override[1] >= 0) return g_cfg_override[1];
+  if (knob(kKnobSplitCfg) >= 0) return knob(kKnobSplitCfg);
   (void)Kred;
   // bf16 MFMA: 128 x 128 tiles for the 14 x 14 / 7 x 7 weight gradients (profiles/r03k_bf16_gemm_tune.txt)
   if (mf == kMfBf16 && M >= 128 && N >= 128) return 4;
@@ -1256,14 +1254,10 @@ static inline int splitk_config(int M, int N, int Kred, int mf = kMfF32) {
   return 1;  // 64x64x32: best or within 3% of best on every other measured wgrad shape
 }
 
-// Blocks a split-K weight gradient aims for (tuning knob DORKNET_WGRAD_BLOCKS, read once).
+// Blocks a split-K weight gradient aims for (knob kKnobWgradBlocks, DORKNET_WGRAD_BLOCKS; default 1024).
 static inline int wgrad_target_blocks() {
-  static int v = -1;
-  if (v < 0) {
-    const char* s = getenv("DORKNET_WGRAD_BLOCKS");
-    v = (s && atoi(s) > 0) ? atoi(s) : 1024;
-  }
-  return v;
+  const int v = knob(kKnobWgradBlocks);
+  return v > 0 ? v : 1024;
 }
 
 static inline int wgrad_splits(int M, int N, int Kred, const TileCfg& c) {

@@ -239,7 +239,6 @@ DK_API size_t dk_pwconv_wgrad_workspace_bytes(int N, int OH, int OW, int K, int 
   const int M = N * OH * OW;
   size_t a = splitk_ws_bytes(K, C, M), b = splitk_ws_bytes(K, C, M, kMfBf16);
   if (a < b) a = b;
-  if (pw_deep_wgrad_ok(K, C, M) && pw_deep_wgrad_ws_bytes(M, K, C) > a) a = pw_deep_wgrad_ws_bytes(M, K, C);
   return a;
 }
 
@@ -249,15 +248,6 @@ DK_API int dk_pwconv_wgrad_f32(const float* dy, const float* x, int N, int H, in
                                void* stream) {
   if (C % 4 || !aligned16(x) || !fits((size_t)N * H * W * C * 4)) return DK_ERR_ARGS;
   const int M = N * OH * OW;
-  if (stride == 1 && H == OH && W == OW && pw_deep_wgrad_ok(K, C, M) && aligned16(dy)) {
-    // the output-stationary deep kernel (pw_deep.hip): partial rows + the same fixed-order reduce
-    if (ws_bytes < pw_deep_wgrad_ws_bytes(M, K, C)) return DK_ERR_WORKSPACE;
-    float* part = static_cast<float*>(ws);
-    const hipStream_t st = as_stream(stream);
-    const int rc = pw_deep_wgrad(dy, x, M, K, C, nullptr, nullptr, nullptr, nullptr, 0, part, st);
-    if (rc) return rc;
-    return splitk_reduce(part, pw_deep_wgrad_chunks(M, K, C), K, C, dw_kc, w_kc, l2, 0, C, C, 1, 1, st);
-  }
   return wgrad(dy, img(x, N, H, W, C, OH, OW, 1, 1, stride, 1, 0, M), K, C, w_kc, l2, dw_kc, 0, C, C, 1, 1,
                ws, ws_bytes, stream);
 }
@@ -269,14 +259,6 @@ DK_API int dk_pwconv_wgrad_bnx_f32(const float* dy, const float* x, int N, int H
   if (C % 4 || !aligned16(x) || !fits((size_t)N * H * W * C * 4)) return DK_ERR_ARGS;
   if (!bn_ok(bn_mean, bn_invstd, bn_gamma, bn_beta)) return DK_ERR_ARGS;
   const int M = N * OH * OW;
-  if (stride == 1 && H == OH && W == OW && pw_deep_wgrad_ok(K, C, M) && aligned16(dy)) {
-    if (ws_bytes < pw_deep_wgrad_ws_bytes(M, K, C)) return DK_ERR_WORKSPACE;
-    float* part = static_cast<float*>(ws);
-    const hipStream_t st = as_stream(stream);
-    const int rc = pw_deep_wgrad(dy, x, M, K, C, bn_mean, bn_invstd, bn_gamma, bn_beta, bn_relu, part, st);
-    if (rc) return rc;
-    return splitk_reduce(part, pw_deep_wgrad_chunks(M, K, C), K, C, dw_kc, w_kc, l2, 0, C, C, 1, 1, st);
-  }
   return wgrad(dy,
                with_bn(img(x, N, H, W, C, OH, OW, 1, 1, stride, 1, 0, N * OH * OW), bn_mean, bn_invstd, bn_gamma,
                        bn_beta, bn_relu),

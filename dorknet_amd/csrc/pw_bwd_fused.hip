@@ -274,12 +274,8 @@ __global__ __launch_bounds__(256, 2) void pw_bwd_fused_kernel(const float* __res
 // Prefetch variant per shape (measured, scripts/pwf_bench.py); DORKNET_PWF_PREFETCH=0/1
 // overrides (tuning knob).
 static bool pwf_prefetch(int K, int C) {
-  static int env = -2;
-  if (env == -2) {
-    const char* s = getenv("DORKNET_PWF_PREFETCH");
-    env = s ? atoi(s) : -1;
-  }
-  if (env >= 0) return env != 0;
+  const int v = knob(kKnobPwfPrefetch);
+  if (v >= 0) return v != 0;
   return K * C <= 8192;
 }
 
@@ -304,13 +300,12 @@ static int pwf_blocks(long long P, int K, int C, int* tpb_out) {
                             : (C == 64 ? pwf_kernel<128, 64, true>(pf) : pwf_kernel<128, 128, true>(pf));
     int v = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, f, 256, 0) != hipSuccess || v < 1) v = 1;
-    const char* s = getenv("DORKNET_PWF_BLOCKS_PER_CU");  // tuning knob
-    if (s && atoi(s) > 0) v = atoi(s);
     o = v;
     oc.store(v, std::memory_order_relaxed);
   }
   const long long ntiles = (P + 63) / 64;
-  long long nblk = (long long)o * 256;
+  const int bpc = knob(kKnobPwfBlocksPerCu);  // tuning knob (DORKNET_PWF_BLOCKS_PER_CU)
+  long long nblk = (long long)(bpc > 0 ? bpc : o) * 256;
   if (nblk > ntiles) nblk = ntiles;
   if (nblk < 1) nblk = 1;
   const int tpb = (int)((ntiles + nblk - 1) / nblk);
@@ -326,15 +321,22 @@ int splitk_reduce(const float* ws, int splits, int M, int N, float* out, const f
 using namespace dk;
 
 DK_API int dk_pwconv_bwd_fused_rows(int N, int OH, int OW, int K, int C) {
-  if (!pwf_supported(K, C) || N < 1 || OH < 1 || OW < 1) return 0;
-  if (pw_stream_bwd_ok(K, C, N * OH * OW)) return pw_stream_bwd_rows(N * OH * OW);
-  return pwf_blocks((long long)N * OH * OW, K, C, nullptr);
+  if (N < 1 || OH < 1 || OW < 1) return 0;
+  const long long P = (long long)N * OH * OW;
+  if (P >= (1ll << 31)) return 0;
+  if (pw_stream_bwd_ok(K, C, (int)P)) return pw_stream_bwd_rows((int)P);
+  if (pw_deep_bwd_ok(K, C, (int)P)) return pw_deep_bwd_rows((int)P, K, C);
+  if (!pwf_supported(K, C)) return 0;
+  return pwf_blocks(P, K, C, nullptr);
 }
 
 // 1 when the fused backward is the faster path for this shape (the streaming kernel of
-// pw_stream.hip, K = C = 64); the layers use it by default there.
+// pw_stream.hip, K = C = 64; the weight-stationary deep kernel of pw_deep.hip, K in {128, 256});
+// the layers use it by default there.
 DK_API int dk_pwconv_bwd_fused_preferred(int N, int OH, int OW, int K, int C) {
-  return (N > 0 && OH > 0 && OW > 0 && pw_stream_bwd_ok(K, C, N * OH * OW)) ? 1 : 0;
+  if (N < 1 || OH < 1 || OW < 1 || (long long)N * OH * OW >= (1ll << 31)) return 0;
+  const int P = N * OH * OW;
+  return (pw_stream_bwd_ok(K, C, P) || pw_deep_bwd_ok(K, C, P)) ? 1 : 0;
 }
 
 DK_API size_t dk_pwconv_bwd_fused_workspace_bytes(int N, int OH, int OW, int K, int C) {
@@ -349,7 +351,9 @@ DK_API int dk_pwconv_bwd_bnbwd_f32(const float* g, const float* bn_x, int N, int
                                    const float* bn_beta, int bn_relu, double* part, void* ws, size_t ws_bytes,
                                    void* stream) {
   const hipStream_t st = as_stream(stream);
-  if (!pwf_supported(K, C) || N < 1 || OH < 1 || OW < 1) return DK_ERR_ARGS;
+  if (N < 1 || OH < 1 || OW < 1 || (long long)N * OH * OW >= (1ll << 31)) return DK_ERR_ARGS;
+  const bool deep = pw_deep_bwd_ok(K, C, N * OH * OW) && (bn_mean != nullptr) == (part != nullptr);
+  if (!pwf_supported(K, C) && !deep) return DK_ERR_ARGS;
   if (!g || !bn_x || !x || !w_kc || !dw_kc || !dx || !out_mean || !out_invstd || !out_gamma || !out_beta || !k12)
     return DK_ERR_ARGS;
   if (part && !bn_mean) return DK_ERR_ARGS;  // the input BN's partials need the input BN
@@ -370,6 +374,20 @@ DK_API int dk_pwconv_bwd_bnbwd_f32(const float* g, const float* bn_x, int N, int
     int rc = pw_stream_bwd_fused(g, bn_x, (int)P, out_mean, out_invstd, out_gamma, out_beta, out_relu, k12, w_kc, dx,
                                  residual, x, bn_mean, bn_invstd, bn_gamma, bn_beta, bn_relu, part, bn_mean,
                                  bn_invstd, bn_gamma, bn_beta, bn_relu, wp, st, part ? &ft : nullptr);
+    if (rc) return rc;
+    return fold_status(wgrad_reduce(wp, nb, K, C, dw_kc, l2 != 0.f ? w_kc : nullptr, l2, st),
+                       part ? ft : FoldTail{});
+  }
+  if (deep) {
+    // K in {128, 256}: the weight-stationary fused kernel (pw_deep.hip)
+    const int nb = pw_deep_bwd_rows((int)P, K, C);
+    if (ws_bytes < (size_t)nb * K * C * sizeof(float)) return DK_ERR_WORKSPACE;
+    float* wp = static_cast<float*>(ws);
+    FoldTail ft;
+    if (part) fold_take(part, nb, C, pw_deep_bwd_slices((int)P, K, C), &ft);
+    int rc = pw_deep_bwd_bnbwd(g, bn_x, (int)P, K, C, out_mean, out_invstd, out_gamma, out_beta, out_relu, k12, w_kc,
+                               dx, residual, x, bn_mean, bn_invstd, bn_gamma, bn_beta, bn_relu, part, wp, st,
+                               part ? &ft : nullptr);
     if (rc) return rc;
     return fold_status(wgrad_reduce(wp, nb, K, C, dw_kc, l2 != 0.f ? w_kc : nullptr, l2, st),
                        part ? ft : FoldTail{});

@@ -26,6 +26,7 @@
 #include <stdlib.h>
 
 #include <algorithm>
+#include <atomic>
 
 #include "dk_common.h"
 #include "fold_tail.h"
@@ -432,192 +433,228 @@ __global__ __launch_bounds__(NT, dgrad_wps<KR>()) void dgrad_kernel(DgradArgs a)
 }
 
 // ---------------------------------------------------------------------------------------
-// Weight gradient (layers/pointwise_convolution.py:61-64): dW[k][c] = sum_m dy[m][k] xh[m][c] with
-// xh = the input BatchNorm (+ReLU) applied on load (bn_out, as the forward).  Output-stationary
-// waves: a wave owns a TK x TC block of dW -- (TK / 32) x (TC / 32) accumulator tiles, up to 256
-// AGPRs at one wave per SIMD -- and streams its own contiguous run of pixel pairs, each pair one
-// v_mfma_f32_32x32x2_f32 k-step.  The tiles are interleaved so that both operands come straight
-// from global memory in one 16-byte (or 8-byte) load per lane: lane (i, h) loads dy[2p + h][k0 +
-// TKQ i .. + TKQ) and x[2p + h][c0 + TCQ i .. + TCQ), and element a (b) of those is row i of k-tile
-// a (column i of c-tile b): k = k0 + TKQ i + a, c = c0 + TCQ j + b.  Every operand element is
-// loaded and transformed by exactly one lane (no LDS staging, no barriers in the loop), loads run
-// kWD pairs ahead in a register ring; the BN on load is packed fp32 arithmetic (v_pk_*), bitwise
-// bn_out.  The block's 4 waves split one dW block's pixel run four ways and add their tiles in
-// LDS (fixed order) into one partial row; the partial rows go through splitk_reduce (fp64, + l2 w).
+// Fused backward (layers/pointwise_convolution.py:57-75 with the following BatchNorm's backward,
+// batch_norm.py:125-174, formed on load): the dgrad above plus the weight gradient
+//   dW[k][c] = sum_m dy[m][k] * bn_relu(x)[m][c]
+// in the same pass, so dy is never stored and the layer input is read once (the dgrad's epilogue
+// loads it for the input BatchNorm's partials anyway).  Per 32-pixel tile a wave
+//   1. runs the dgrad MFMAs of its 32 columns (B fragments W resident, A = the LDS dy tile);
+//   2. stores dx and reduces the input BN's partials from its C-layout x loads;
+//   3. applies the input BN (+ReLU) to those same x values in registers -- lane (l32, h) holds
+//      x[4h + (s & 3) + 8 (s >> 2)][col] for s = 0..15, which is exactly the A operand of k-step s
+//      of v_mfma_f32_32x32x2_f32 with rows = its column and the k pair = pixels (s, h) -- and runs
+//      dW^T[col][k] += bn_relu(x)^T . dy with B = the LDS dy tile read as one ds_read_b128 per 4
+//      MFMAs (k-tile kt covers channels 4 l32 + (kt & 3) + 128 (kt >> 2)).
+// The wave's dW block (its 32 columns x all KR channels, KR / 2 accumulator registers) lives in
+// registers for the block's life; at the end it goes through LDS into a coalesced partial row
+// wpart[blockIdx.x][KR][N], which splitk_reduce sums in a fixed order (+ l2 W).  dx and the BN
+// partials are bit-identical to dgrad_kernel's; dW regroups the fp32 sum over pixels.
 // ---------------------------------------------------------------------------------------
-constexpr int kWD = 8;  // pixel pairs in flight per wave (16: 4-14 % slower, profiles/r04q_pwd_bench_kwd16.txt)
-
-struct WgradArgs {
-  const float* dy;  // [M][K]
-  const float* x;   // [M][C] (the input BN's raw input when BN)
-  const float *im, *iis, *ig, *ib;
+struct BwdArgs {
+  const float* g;     // [M][KR]
+  const float* xo;    // [M][KR] the following BN's raw input
+  const float* w;     // [KR][N]
+  float* dx;          // [M][N]
+  const float* res;   // [M][N] nullable
+  const float* xi;    // [M][N] the layer input (the input BN's raw input when BNIN)
+  const float *om, *ois, *og, *ob, *k12;  // following BN
+  int orelu;
+  const float *im, *iis, *ig, *ib;  // input BN
   int irelu;
-  float* part;      // [chunks][K][C]
-  int M, K, C, chunks;
+  double* part;       // [gridDim.x][2][N] (BNIN)
+  float* wpart;       // [gridDim.x][KR][N]
+  int M, N;
+  FoldTail ft;
+  int nt;             // nontemporal dx stores (nt_stores(kNtPwd))
 };
 
-template <int Q>
-struct VecOf;
-template <>
-struct VecOf<2> {
-  typedef f32x2 T;
-  static __device__ __forceinline__ T load(__amdgpu_buffer_rsrc_t r, uint32_t off) {
-    return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b64(r, (int)off, 0, 0));
-  }
-};
-template <>
-struct VecOf<4> {
-  typedef f32x4 T;
-  static __device__ __forceinline__ T load(__amdgpu_buffer_rsrc_t r, uint32_t off) {
-    return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0));
-  }
-};
-
-template <int TKQ, int TCQ>
-constexpr int wgrad_lds_floats() {
-  return 2 * (32 * TKQ) * (32 * TCQ + 4);
+template <int KR>
+constexpr int bwd_wps() {
+  return KR <= 128 ? 2 : 1;
 }
 
-template <int TKQ, int TCQ, bool BN, bool RELU>
-__global__ __launch_bounds__(NT, 1) void wgrad_kernel(WgradArgs a) {
-  constexpr int TK = 32 * TKQ, TC = 32 * TCQ, SR = TC + 4;  // LDS row stride (floats)
-  typedef typename VecOf<TKQ>::T AV;
-  typedef typename VecOf<TCQ>::T BV;
-  extern __shared__ __attribute__((aligned(16))) float red[];  // [2][TK][SR]
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+template <int KR, bool RES, bool BNIN>
+__global__ __launch_bounds__(NT, bwd_wps<KR>()) void bwd_kernel(BwdArgs a) {
+  constexpr int SK = KR + 4, KV = KR / 4, LV = TR * KV / NT, KQ = KR / 8, NKT = KR / 32, NU = KR / 128;
+  static_assert(KR % 128 == 0 && (SK / 4) % 2 == 1 && NT % KV == 0, "pwd::bwd_kernel shape");
+  __shared__ __attribute__((aligned(16))) float As[2][TR * SK];
+  // the following BN's per-channel terms (mean, invstd, gamma, beta, k1, k2, gamma * invstd): read
+  // from LDS by the staging transform, so they hold no registers through the MFMA phases
+  __shared__ __attribute__((aligned(16))) f32x4 bnt[7][KV];
+  static_assert(sizeof(double) * 2 * NT <= sizeof(float) * 2 * TR * SK, "fold scratch fits in the tiles");
+  static_assert(32 * (NB + 4) <= 2 * TR * SK, "dW transpose tile fits in the tiles");
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int l32 = lane & 31, h = lane >> 5;
-  const int K = a.K, C = a.C, tiles_c = C / TC, ntiles = (K / TK) * tiles_c;
-  // block -> (dW block, pixel chunk): chunk % 8 follows blockIdx % 8, so every dW block of one
-  // pixel chunk runs on one XCD and shares its L2 copy of the chunk's dy and x
-  const int id = blockIdx.x, rest = id >> 3;
-  const int tile = rest % ntiles, chunk = (id & 7) + 8 * (rest / ntiles);
-  const int k0 = (tile / tiles_c) * TK, c0 = (tile % tiles_c) * TC;
-  // this wave's pixel pairs [pb, pe)
-  const int npairs = (a.M + 1) >> 1, nsub = a.chunks * 4, sub = chunk * 4 + wave;
-  const int pb = (int)((long long)npairs * sub / nsub), pe = (int)((long long)npairs * (sub + 1) / nsub);
-  const uint32_t aoff = (uint32_t)(h * K + k0 + TKQ * l32) * 4u, boff = (uint32_t)(h * C + c0 + TCQ * l32) * 4u;
-  BV mu, is, ga, be;
-  if constexpr (BN) {
+  const int n0 = blockIdx.y * NB, N = a.N;
+  const int col = n0 + 32 * wave + l32;
+  const int kv = tid % KV, r0 = tid / KV;
+  if (tid < KV) {
+    const f32x4 ga = ld4(a.og + 4 * tid), is = ld4(a.ois + 4 * tid);
+    bnt[0][tid] = ld4(a.om + 4 * tid);
+    bnt[1][tid] = is;
+    bnt[2][tid] = ga;
+    bnt[3][tid] = ld4(a.ob + 4 * tid);
+    bnt[4][tid] = ld4(a.k12 + 4 * tid);
+    bnt[5][tid] = ld4(a.k12 + KR + 4 * tid);
+    f32x4 f;
 #pragma unroll
-    for (int e = 0; e < TCQ; ++e) {
-      const int c = c0 + TCQ * l32 + e;
-      mu[e] = a.im[c];
-      is[e] = a.iis[c];
-      ga[e] = a.ig[c];
-      be[e] = a.ib[c];
+    for (int e = 0; e < 4; ++e) f[e] = ga[e] * is[e];
+    bnt[6][tid] = f;
+  }
+  __syncthreads();
+  const float pm = BNIN ? a.im[col] : 0.f, pis = BNIN ? a.iis[col] : 0.f, pga = BNIN ? a.ig[col] : 0.f,
+              pbe = BNIN ? a.ib[col] : 0.f;
+  const bool orelu = a.orelu != 0, irelu = a.irelu != 0;
+
+  const int ntiles = (a.M + TR - 1) / TR, G = gridDim.x;
+  uint32_t lofs[LV];
+#pragma unroll
+  for (int j = 0; j < LV; ++j) lofs[j] = off4(r0 + j * (NT / KV), KR, 4 * kv);
+  // C-layout element offsets within a tile: a lane base + a uniform row offset
+  const uint32_t cbase = off4(4 * h, N, col);
+
+  auto load_tile = [&](int tile, f32x4* sg, f32x4* sx) {
+    const __amdgpu_buffer_rsrc_t rg = tile_rsrc(a.g, KR, tile, a.M), rx = tile_rsrc(a.xo, KR, tile, a.M);
+#pragma unroll
+    for (int j = 0; j < LV; ++j) {
+      sg[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rg, (int)lofs[j], 0, 0));
+      sx[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rx, (int)lofs[j], 0, 0));
     }
-  }
-  // pair p's operands: one resource per tensor (range-checked: a ragged last pixel reads zeros),
-  // the pair's row offset added to the lane offset; pairs past pe read zeros (offset past any
-  // tensor), so they add nothing
-  const __amdgpu_buffer_rsrc_t rdy = make_rsrc_v(a.dy, (uint32_t)a.M * K * 4u);
-  const __amdgpu_buffer_rsrc_t rx = make_rsrc_v(a.x, (uint32_t)a.M * C * 4u);
-  auto load_pair = [&](int p, AV& av, BV& bv) __attribute__((always_inline)) {
-    const bool ok = p < pe;
-    const uint32_t oa = ok ? (uint32_t)p * (uint32_t)(2 * K * 4) : kOOBBytes;
-    const uint32_t ob = ok ? (uint32_t)p * (uint32_t)(2 * C * 4) : kOOBBytes;
-    av = VecOf<TKQ>::load(rdy, aoff + oa);
-    bv = VecOf<TCQ>::load(rx, boff + ob);
   };
-  f32x16 acc[TKQ][TCQ];
+  auto stage = [&](float* dst, const f32x4* sg, const f32x4* sx) {
+    const f32x4 mu = bnt[0][kv], is = bnt[1][kv], ga = bnt[2][kv], be = bnt[3][kv], k1 = bnt[4][kv], k2 = bnt[5][kv],
+                f = bnt[6][kv];
 #pragma unroll
-  for (int i = 0; i < TKQ; ++i)
+    for (int j = 0; j < LV; ++j) {
+      const int r = r0 + j * (NT / KV);
+      f32x4 v;
 #pragma unroll
-    for (int j = 0; j < TCQ; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-  AV ra[kWD];
-  BV rb[kWD];
-  // (issued in ring order: the waitcnt pass merges this order with the loop's at the loop head,
-  // and a reordered prologue made it wait for every load there, every iteration)
-#pragma unroll
-  for (int s = 0; s < kWD; ++s) {
-    load_pair(pb + s, ra[s], rb[s]);
-    __builtin_amdgcn_sched_barrier(0);
-  }
-  for (int p = pb; p < pe; p += kWD) {
-#pragma unroll
-    for (int s = 0; s < kWD; ++s) {
-      const AV av = ra[s];
-      BV bv = rb[s];
-      if constexpr (BN) {
-        // bn_out elementwise in packed pairs: ((x - mean) * invstd) then fma(gamma, xh, beta)
-#pragma unroll
-        for (int e = 0; e < TCQ; e += 2) {
-          const f32x2 xv = {bv[e], bv[e + 1]}, m2 = {mu[e], mu[e + 1]}, i2 = {is[e], is[e + 1]};
-          const f32x2 g2 = {ga[e], ga[e + 1]}, b2 = {be[e], be[e + 1]};
-          const f32x2 xh = (xv - m2) * i2;
-          const f32x2 o = __builtin_elementwise_fma(g2, xh, b2);
-          bv[e] = o[0];
-          bv[e + 1] = o[1];
-        }
-        if constexpr (RELU) {
-#pragma unroll
-          for (int e = 0; e < TCQ; ++e) bv[e] = __builtin_fmaxf(bv[e], 0.f);
-        }
+      for (int e = 0; e < 4; ++e) {
+        const float xe = sx[j][e];
+        float ge = sg[j][e];
+        const bool kill = (!(bn_out(xe, mu[e], is[e], ga[e], be[e]) > 0.f)) & orelu;
+        ge = kill ? 0.f : ge;
+        v[e] = bn_bwd_elem(xe, ge, mu[e], is[e], f[e], k1[e], k2[e]);
       }
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int i = 0; i < TKQ; ++i)
-#pragma unroll
-        for (int j = 0; j < TCQ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i], bv[j], acc[i][j], 0, 0, 0);
-      __builtin_amdgcn_sched_barrier(0);
-      // refill the ring slot once its operands are consumed (in place: loading it before the
-      // MFMAs made the compiler rotate the ring through copies that waited for every load)
-      load_pair(p + s + kWD, ra[s], rb[s]);
+      st4(dst + r * SK + 4 * kv, v);
     }
-  }
-  // the block's 4 partial tiles added in LDS: (w0 + w2) + (w1 + w3); element (i, j, r) of a lane
-  // is dW[k0 + TKQ (8 (r >> 2) + 4h + (r & 3)) + i][c0 + TCQ l32 + j].  The lane's base offsets are
-  // pinned here (asm barrier) so the per-element addresses stay base + constant: hoisted above the
-  // loop they took ~100 VGPRs and the 4 x 4 variant spilled.
-  int lb = TKQ * 4 * h * SR + TCQ * l32;
-  uint32_t gofs = (uint32_t)((k0 + TKQ * 4 * h) * C + c0 + TCQ * l32) * 4u;
-  asm volatile("" : "+v"(lb), "+v"(gofs));
-  auto tile_io = [&](float* base, bool add, bool store) __attribute__((always_inline)) {
-#pragma unroll
-    for (int i = 0; i < TKQ; ++i)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        float* q = base + lb + (TKQ * (8 * (r >> 2) + (r & 3)) + i) * SR;
-        if (store) {
-          BV v;
-#pragma unroll
-          for (int j = 0; j < TCQ; ++j) v[j] = acc[i][j][r];
-          *reinterpret_cast<BV*>(q) = v;
-        } else {
-          const BV v = *reinterpret_cast<const BV*>(q);
-#pragma unroll
-          for (int j = 0; j < TCQ; ++j) acc[i][j][r] = add ? acc[i][j][r] + v[j] : v[j];
-        }
-        __builtin_amdgcn_sched_barrier(0);  // one row at a time
-      }
   };
-  if (wave >= 2) tile_io(red + (wave - 2) * TK * SR, false, true);
-  __syncthreads();
-  if (wave < 2) tile_io(red + wave * TK * SR, true, false);
-  __syncthreads();
-  if (wave == 1) tile_io(red, false, true);
-  __syncthreads();
-  if (wave == 0) {
-    tile_io(red, true, false);
-    const __amdgpu_buffer_rsrc_t rp = make_rsrc_v(a.part + (size_t)chunk * K * C, (uint32_t)K * C * 4u);
+
+  int t = first_tile(ntiles);
+  f32x4 bw[KQ];
+  {
+    f32x4 sg[LV], sx[LV];
+    load_tile(t, sg, sx);
 #pragma unroll
-    for (int i = 0; i < TKQ; ++i)
+    for (int q = 0; q < KQ; ++q)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int dk = TKQ * (8 * (r >> 2) + (r & 3)) + i;
-        BV v;
+      for (int e = 0; e < 4; ++e) bw[q][e] = a.w[(size_t)(8 * q + 4 * h + e) * N + col];
+    stage(&As[0][0], sg, sx);
+  }
+  __syncthreads();
+  f32x16 dw[NKT];
 #pragma unroll
-        for (int j = 0; j < TCQ; ++j) v[j] = acc[i][j][r];
-        if constexpr (TCQ == 4)
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rp, (int)gofs, dk * C * 4, 0);
-        else
-          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), rp, (int)gofs, dk * C * 4, 0);
+  for (int i = 0; i < NKT; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) dw[i][r] = 0.f;
+  double ps = 0.0, pq = 0.0;
+  int buf = 0;
+  for (; t < ntiles; t += G) {
+    f32x4 ng[LV], nx[LV];
+    load_tile(t + G, ng, nx);
+    // the tile's C-layout operands (layer input, residual), in flight during the dgrad MFMAs
+    const int mb = t * TR + 4 * h;
+    const __amdgpu_buffer_rsrc_t rxi = tile_rsrc(a.xi, N, t, a.M);
+    const __amdgpu_buffer_rsrc_t rr = tile_rsrc(RES ? a.res : a.xi, N, t, RES ? a.M : 0);
+    const __amdgpu_buffer_rsrc_t rdx = tile_rsrc(a.dx, N, t, a.M);
+    float ex[16], ers[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int ro = ((r & 3) + 8 * (r >> 2)) * N * 4;
+      ex[r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rxi, (int)cbase, ro, 0));
+      if constexpr (RES) ers[r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rr, (int)cbase, ro, 0));
+    }
+    const float* tile = &As[buf][0];
+    f32x16 acc;
+    mfma_tile<KQ>(tile + l32 * SK + 4 * h, bw, acc);
+    if constexpr (RES) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[r] += ers[r];
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float v = acc[r];
+      bstore_nt(__builtin_bit_cast(uint32_t, v), rdx, (int)cbase, ((r & 3) + 8 * (r >> 2)) * N * 4, a.nt);
+    }
+    // the input BN's partials of dx, and the weight gradient's operand bn_relu(x)
+    const bool full = t * TR + TR <= a.M;  // a whole tile (uniform): no row masks
+    float yb[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int dm = (r & 3) + 8 * (r >> 2);
+      const bool out = !full && mb + dm >= a.M;
+      const float x = ex[r];
+      if constexpr (BNIN) {
+        const float xh = (x - pm) * pis;
+        const float v = __builtin_fmaf(pga, xh, pbe);  // bn_out
+        const bool dead = !(v > 0.f) & irelu;
+        const float gv = (dead | out) ? 0.f : acc[r];
+        ps += (double)gv;
+        pq += (double)gv * (double)xh;
+        yb[r] = (dead | out) ? 0.f : v;
+      } else {
+        yb[r] = out ? 0.f : x;
+      }
+    }
+    // dW^T[col][k] += bn_relu(x)^T . dy over the tile's 32 pixels (rows past M are zero in yb)
+    {
+      const float* bp = tile + (4 * h) * SK + 4 * l32;
+      f32x4 bv[NU], nb[NU];
+#pragma unroll
+      for (int u = 0; u < NU; ++u) bv[u] = ld4(bp + 128 * u);
+#pragma unroll
+      for (int s = 0; s < 16; ++s) {
+        if (s + 1 < 16) {
+          const int pn = ((s + 1) & 3) + 8 * ((s + 1) >> 2);
+#pragma unroll
+          for (int u = 0; u < NU; ++u) nb[u] = ld4(bp + pn * SK + 128 * u);
+        }
         __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int u = 0; u < NU; ++u)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) dw[4 * u + e] = __builtin_amdgcn_mfma_f32_32x32x2f32(yb[s], bv[u][e], dw[4 * u + e], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int u = 0; u < NU; ++u) bv[u] = nb[u];
       }
+    }
+    stage(&As[buf ^ 1][0], ng, nx);
+    __syncthreads();
+    buf ^= 1;
   }
+  // the weight-gradient partial row: per k-tile, the 4 waves' 32 x 32 blocks through an LDS tile
+  // [32 k][NB + 4] into coalesced row stores (k-tile kt holds channels 4 i + (kt & 3) + 128 (kt >> 2))
+  {
+    constexpr int ST = NB + 4;
+    float* T = &As[0][0];
+    float* wp = a.wpart + (size_t)blockIdx.x * KR * N + n0;
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt) {
+      __syncthreads();
+#pragma unroll
+      for (int r = 0; r < 16; ++r) T[l32 * ST + 32 * wave + 4 * h + (r & 3) + 8 * (r >> 2)] = dw[kt][r];
+      __syncthreads();
+#pragma unroll
+      for (int j = 0; j < 32 * NB / 4 / NT; ++j) {
+        const int idx = tid + NT * j, i = idx / (NB / 4), c4 = idx % (NB / 4);
+        const int k = 4 * i + (kt & 3) + 128 * (kt >> 2);
+        st4(wp + (size_t)k * N + 4 * c4, ld4(T + i * ST + 4 * c4));
+      }
+    }
+  }
+  if constexpr (BNIN) partial_row(ps, pq, a.part, N, n0, a.ft, &As[0][0]);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -660,6 +697,20 @@ static int dgrad_occ() {
   return occ;
 }
 
+template <int KR>
+static int bwd_occ() {
+  static const int occ = [] {
+    const void* fs[] = {reinterpret_cast<const void*>(&bwd_kernel<KR, true, true>),
+                        reinterpret_cast<const void*>(&bwd_kernel<KR, true, false>),
+                        reinterpret_cast<const void*>(&bwd_kernel<KR, false, true>),
+                        reinterpret_cast<const void*>(&bwd_kernel<KR, false, false>)};
+    int o = 1 << 20;
+    for (const void* f : fs) o = std::min(o, occupancy(f));
+    return o;
+  }();
+  return occ;
+}
+
 // Row-tile walkers per column group: every resident slot once (all blocks of a CU run at the same
 // time, so each CU gets the same number of blocks and each block within one tile of the same share),
 // at most one walker per tile; a multiple of the 8 XCDs when that costs no extra tile per walker, so
@@ -680,15 +731,7 @@ static int grid_x(int M, int N, int occ) {
 }  // namespace pwd
 
 // DORKNET_PW_DEEP=0 (or the streaming switch DORKNET_PW_STREAM=0) keeps the earlier paths; knob 11.
-static int g_pwd = -1;
-static bool pwd_enabled() {
-  if (g_pwd < 0) {
-    const char* e = getenv("DORKNET_PW_DEEP");
-    g_pwd = (e && e[0] == '0') ? 0 : 1;
-  }
-  return g_pwd == 1 && pw_stream_enabled();
-}
-void pw_deep_set(int v) { g_pwd = v < 0 ? -1 : v; }
+static bool pwd_enabled() { return knob(kKnobPwDeep) == 1 && pw_stream_enabled(); }
 
 static bool pwd_kr(int KR) { return KR == 64 || KR == 128 || KR == 256 || KR == 512; }
 
@@ -719,78 +762,6 @@ int pw_deep_dgrad_rows(int M, int K, int C) {
   return 0;
 }
 int pw_deep_dgrad_slices(int M, int K, int C) { return C / pwd::NB; }
-
-// Weight gradient: K, C multiples of the dW block (TK = 128 when K >= 128, else 64; TC likewise),
-// stride 1, at least 128 channels on one side; chunks = pixel chunks per dW block (a multiple of
-// 8, about one wave per SIMD in all).
-static int wg_q(int n) { return n >= 128 ? 4 : 2; }
-// Off by default (DORKNET_PW_DEEP_WGRAD=1 or knob 12 = 1 turn it on): faster alone (square layers,
-// profiles/r04n_pwd_bench.txt) but a slower step (profiles/r04s_ab_deep.txt: 8.664 vs 8.593 ms per
-// step) -- a block takes a whole CU (one wave per SIMD, 512 registers, 135 KB of LDS), so on the
-// side stream it shuts the main stream's kernels out of the CUs it holds instead of sharing them.
-static int g_pwd_wg = -1;
-void pw_deep_wgrad_set(int v) { g_pwd_wg = v < 0 ? -1 : v; }
-static bool pwd_wgrad_enabled() {
-  if (g_pwd_wg < 0) {
-    const char* e = getenv("DORKNET_PW_DEEP_WGRAD");
-    g_pwd_wg = (e && e[0] == '1') ? 1 : 0;
-  }
-  return g_pwd_wg == 1;
-}
-bool pw_deep_wgrad_ok(int K, int C, int M) {
-  if (!pwd_wgrad_enabled()) return false;
-  // square layers only: at K = 2C (the widening layers) the tiled engine measured as fast or faster
-  // (profiles/r04n_pwd_bench.txt: 28x28 64->128 52.6 vs 52.9 us, 14x14 128->256 50.6 vs 50.5,
-  // 7x7 256->512 48.8 vs 46.2)
-  if (K != C) return false;
-  if (!pwd_enabled() || M <= 1 || (K < 128 && C < 128) || K % 64 || C % 64 || K > 1024 || C > 1024) return false;
-  if (K % (32 * wg_q(K)) || C % (32 * wg_q(C))) return false;
-  return (size_t)M * (K > C ? K : C) * 4 < ((size_t)1 << 31);
-}
-int pw_deep_wgrad_chunks(int M, int K, int C) {
-  const int ntiles = (K / (32 * wg_q(K))) * (C / (32 * wg_q(C)));
-  int ch = 256 / ntiles;
-  ch = ch < 8 ? 8 : ch / 8 * 8;
-  // at least a few pixel pairs per wave
-  while (ch > 8 && (long long)ch * 4 * 16 > (M + 1) / 2) ch -= 8;
-  return ch;
-}
-size_t pw_deep_wgrad_ws_bytes(int M, int K, int C) {
-  return (size_t)pw_deep_wgrad_chunks(M, K, C) * K * C * sizeof(float);
-}
-
-int pw_deep_wgrad(const float* dy, const float* x, int M, int K, int C, const float* im, const float* iis,
-                  const float* ig, const float* ib, int irelu, float* part, hipStream_t st) {
-  const int chunks = pw_deep_wgrad_chunks(M, K, C);
-  pwd::WgradArgs a{dy, x, im, iis, ig, ib, irelu, part, M, K, C, chunks};
-  const int tkq = wg_q(K), tcq = wg_q(C);
-  const int ntiles = (K / (32 * tkq)) * (C / (32 * tcq));
-  const dim3 grid((unsigned)(ntiles * chunks));
-#define DK_WG(TKQ_, TCQ_)                                                                                         \
-  if (tkq == TKQ_ && tcq == TCQ_) {                                                                               \
-    const size_t lds = sizeof(float) * pwd::wgrad_lds_floats<TKQ_, TCQ_>();                                        \
-    const void* fs[3] = {reinterpret_cast<const void*>(&pwd::wgrad_kernel<TKQ_, TCQ_, false, false>),              \
-                         reinterpret_cast<const void*>(&pwd::wgrad_kernel<TKQ_, TCQ_, true, false>),               \
-                         reinterpret_cast<const void*>(&pwd::wgrad_kernel<TKQ_, TCQ_, true, true>)};               \
-    static const bool attr = [&] {                                                                                \
-      for (const void* f : fs) (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); \
-      return true;                                                                                                \
-    }();                                                                                                          \
-    (void)attr;                                                                                                   \
-    if (im && irelu)                                                                                              \
-      hipLaunchKernelGGL((pwd::wgrad_kernel<TKQ_, TCQ_, true, true>), grid, dim3(pwd::NT), lds, st, a);           \
-    else if (im)                                                                                                  \
-      hipLaunchKernelGGL((pwd::wgrad_kernel<TKQ_, TCQ_, true, false>), grid, dim3(pwd::NT), lds, st, a);          \
-    else                                                                                                          \
-      hipLaunchKernelGGL((pwd::wgrad_kernel<TKQ_, TCQ_, false, false>), grid, dim3(pwd::NT), lds, st, a);         \
-    return launch_status();                                                                                       \
-  }
-  DK_WG(4, 4)
-  DK_WG(4, 2)
-  DK_WG(2, 4)
-#undef DK_WG
-  return DK_ERR_ARGS;
-}
 
 int pw_deep_fwd(const float* x, int N, int H, int W, int stride, int OH, int OW, const float* w, int K, int C,
                 const float* bias, float* y, const float* im, const float* iis, const float* ig, const float* ib,
@@ -862,6 +833,50 @@ int pw_deep_dgrad_bnbwd(const float* g, const float* bn_x, int M, int K, int C, 
   }
   DK_PWD_KR(DK_DG)
 #undef DK_DG
+#undef DK_L
+  return DK_ERR_ARGS;
+}
+
+// Fused deep backward (bwd_kernel): reduction K in {128, 256}, C a multiple of the block's 128 columns.
+// Default on; DORKNET_PW_DEEP_BWD=0 (knob 14) keeps the dgrad + side-stream weight gradient pair.
+static bool pwd_bwd_enabled() { return knob(kKnobPwDeepBwd) == 1 && pwd_enabled(); }
+bool pw_deep_bwd_ok(int K, int C, int M) {
+  if (!pwd_bwd_enabled() || M <= 0 || (K != 128 && K != 256) || C % pwd::NB) return false;
+  return (size_t)M * (K > C ? K : C) * 4 < ((size_t)1 << 31);
+}
+int pw_deep_bwd_rows(int M, int K, int C) {
+  if (K == 128) return pwd::grid_x(M, C, pwd::bwd_occ<128>());
+  if (K == 256) return pwd::grid_x(M, C, pwd::bwd_occ<256>());
+  return 0;
+}
+int pw_deep_bwd_slices(int M, int K, int C) { return C / pwd::NB; }
+
+int pw_deep_bwd_bnbwd(const float* g, const float* bn_x, int M, int K, int C, const float* om, const float* ois,
+                      const float* og, const float* ob, int orelu, const float* k12, const float* w, float* dx,
+                      const float* res, const float* x, const float* im, const float* iis, const float* ig,
+                      const float* ib, int irelu, double* part, float* wpart, hipStream_t st, const FoldTail* ft) {
+  if ((im != nullptr) != (part != nullptr)) return DK_ERR_ARGS;
+  pwd::BwdArgs a{g, bn_x, w, dx, res, x, om, ois, og, ob, k12, orelu, im, iis, ig, ib, irelu, part, wpart, M, C};
+  if (ft && part) a.ft = *ft;
+  a.nt = nt_stores(kNtPwd);
+  const dim3 grid(pw_deep_bwd_rows(M, K, C), C / pwd::NB);
+  if (grid.x == 0) return DK_ERR_ARGS;
+#define DK_L(kr, R_, B_) hipLaunchKernelGGL((pwd::bwd_kernel<kr, R_, B_>), grid, dim3(pwd::NT), 0, st, a)
+#define DK_BW(kr)             \
+  if (K == kr) {              \
+    if (res && im)            \
+      DK_L(kr, true, true);   \
+    else if (res)             \
+      DK_L(kr, true, false);  \
+    else if (im)              \
+      DK_L(kr, false, true);  \
+    else                      \
+      DK_L(kr, false, false); \
+    return launch_status();   \
+  }
+  DK_BW(128)
+  DK_BW(256)
+#undef DK_BW
 #undef DK_L
   return DK_ERR_ARGS;
 }

@@ -2,8 +2,7 @@
 // 14 x 14 / 7 x 7 units with 128 / 256 / 512 channels, batch 512; layers/pointwise_convolution.py
 // :46-75), on v_mfma_f32_32x32x16_bf16.
 //
-// The column-sliced kernels they replace (pw_stream_bf16.hip, fwd_deep_kernel / dgrad_deep_kernel)
-// give every wave its own pixel tile: each wave forms the BatchNorm transform of its tile for every
+// The round-3 column-sliced kernels they replaced (since deleted) gave every wave its own pixel tile: each wave forms the BatchNorm transform of its tile for every
 // 128-column slice, reads the per-channel BN terms from an LDS table per 4 elements and the weight
 // fragments from LDS per MFMA -- 20+ VALU and 4-5 LDS reads per bf16 MFMA (r03z_sq_ratios_config5:
 // MFMA busy 0.05-0.06, VALU / MFMA 30-35), 0.16-0.26 of HBM.  Here, as in pw_deep.hip:
@@ -442,20 +441,12 @@ static int grid_x(int M, int N, int occ) {
 
 }  // namespace pwd16
 
-// DORKNET_PW_DEEP_BF16=0 keeps the column-sliced kernels (pw_stream_bf16.hip); knob 13.
-static int g_pwd16 = -1;
-void pw_deep16_set(int v) { g_pwd16 = v < 0 ? -1 : v; }
-static bool pwd16_enabled() {
-  if (g_pwd16 < 0) {
-    const char* e = getenv("DORKNET_PW_DEEP_BF16");
-    g_pwd16 = (e && e[0] == '0') ? 0 : 1;
-  }
-  return g_pwd16 == 1;
-}
+// DORKNET_PW_DEEP_BF16=0 (knob 13) keeps the tiled engine's bf16 mode for the deep shapes.
+static bool pwd16_enabled() { return knob(kKnobPwDeep16) == 1; }
 static bool pwd16_kr(int KR) { return KR == 128 || KR == 256 || KR == 512; }
 
-// The shapes the column-sliced kernels took (pw_stream_bf16.hip deep_shape): reduction 128 / 256 /
-// 512, outputs a multiple of 128 columns, 256+ channels on one side when the reduction is 128.
+// The deep shapes: reduction 128 / 256 / 512, outputs a multiple of 128 columns, 256+ channels on
+// one side when the reduction is 128.
 bool pw_deep16_fwd_ok(int K, int C, int M) {
   if (!pwd16_enabled() || M <= 0 || !pwd16_kr(C) || K % pwd16::NB || K > 4096 || (C < 256 && K < 256)) return false;
   return (size_t)M * (K > C ? K : C) * 2 < ((size_t)1 << 31);

@@ -828,17 +828,9 @@ __global__ __launch_bounds__(256, PF ? 1 : 2) void bwd_fused_kernel(BwdArgs ba) 
   }
 }
 
-// The backward's A-operand prefetch (tuning knob DORKNET_PWS_BWD_PF, dk_debug_set_gemm_config(5, v)).
-static int g_bwd_pf = -1;
-void bwd_pf_set(int v) { g_bwd_pf = v; }
-static bool bwd_pf() {
-  if (g_bwd_pf < 0) {
-    // default: no prefetch, 2 waves per SIMD (whole step 9.12 -> 9.02 ms, scripts/ab_step.py, r03)
-    const char* e = getenv("DORKNET_PWS_BWD_PF");
-    g_bwd_pf = (e && e[0] == '1') ? 1 : 0;
-  }
-  return g_bwd_pf == 1;
-}
+// The backward's A-operand prefetch (knob kKnobPwsBwdPf, DORKNET_PWS_BWD_PF, kind 5).  Default: no
+// prefetch, 2 waves per SIMD (whole step 9.12 -> 9.02 ms, scripts/ab_step.py, r03).
+static bool bwd_pf() { return knob(kKnobPwsBwdPf) == 1; }
 
 template <bool PF>
 static int bwd_fused_occ() {
@@ -857,17 +849,8 @@ int bwd_fused_blocks(int M) { return grid_blocks(M, bwd_pf() ? bwd_fused_occ<tru
 // above its occupancy only adds a second partial round of blocks, never changes the results' order)
 }  // namespace pws
 
-void pw_stream_bwd_pf_set(int v) { pws::bwd_pf_set(v); }
-
-static int g_pw_stream = -1;  // -1: from DORKNET_PW_STREAM (default on); dk_debug_set_gemm_config(3, v)
-void pw_stream_set(int v) { g_pw_stream = v; }
-bool pw_stream_enabled() {
-  if (g_pw_stream < 0) {
-    const char* e = getenv("DORKNET_PW_STREAM");
-    g_pw_stream = (e && e[0] == '0') ? 0 : 1;
-  }
-  return g_pw_stream == 1;
-}
+// knob kKnobPwStream (DORKNET_PW_STREAM, default on; kind 3)
+bool pw_stream_enabled() { return knob(kKnobPwStream) == 1; }
 
 // Shapes the streaming dgrad takes (the rest go to the tiled engine).
 bool pw_stream_dgrad_ok(int K, int C, int M) {
@@ -877,15 +860,8 @@ bool pw_stream_dgrad_ok(int K, int C, int M) {
 
 int pw_stream_dgrad_rows(int M) { return pws::dgrad_blocks(M); }
 
-// K = C = 128 on the streaming forward (tuning knob DORKNET_PW_STREAM128=0: the tiled engine)
-static bool pw_stream128() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("DORKNET_PW_STREAM128");
-    v = (e && e[0] == '0') ? 0 : 1;
-  }
-  return v == 1;
-}
+// K = C = 128 on the streaming forward (knob kKnobPwStream128, DORKNET_PW_STREAM128=0: the tiled engine)
+static bool pw_stream128() { return knob(kKnobPwStream128) == 1; }
 
 bool pw_stream_fwd_ok(int K, int C, int M, size_t xbytes) {
   if (!pw_stream_enabled()) return false;

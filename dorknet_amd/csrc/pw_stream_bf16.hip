@@ -418,377 +418,6 @@ __global__ __launch_bounds__(256, 2) void dgrad_bnbwd_kernel(DgradArgs a) {
   if (a.ft.part) fold_tail<256>(a.ft, blockIdx.x, 0, NO, 0);
 }
 
-// ---------------------------------------------------------------------------------------
-// Deep layers (the 14 x 14 and 7 x 7 units: K or C of 256 / 512).  The tiled engine's bf16 mode runs
-// these at 0.1-0.3 of their roofline (a 32-deep k-tile of bf16 MFMAs is too short to cover its
-// operand round trip, and every block pays a table fill, a prologue and an epilogue); here the
-// streaming structure above, with
-//   * column slices: block (x, y) owns output columns n0 = 128 y .. n0 + 127 (its weight slice,
-//     128 x (K + 8) bf16, in LDS), x = the persistent row-tile walker of that slice;
-//   * k-chunks: a wave tile's pixel operand streams in chunks of CK channels with the next chunk
-//     (the next tile's first at the end) in flight, so 256 / 512 channels need no more registers
-//     than a chunk pair;
-//   * NW = 8 waves per block when the weight slice needs most of the LDS (K = 512): one block per
-//     CU, still 2 waves per SIMD.
-// Bit-identical to the tiled engine (the same operand rounding, k-steps of 16 ascending, epilogue);
-// the slices repeat the operand transform (N / 128 times, as the engine's column tiles do).
-// ---------------------------------------------------------------------------------------
-constexpr int NOD = 128;  // columns per slice
-
-struct DeepArgs {
-  const bf16_t* a0;   // fwd: x [M][KR];  dgrad: g [M][KR]
-  const bf16_t* a1;   // dgrad: xo [M][KR] (the following BN's raw input)
-  bf16_t* dy_out;     // dgrad: [M][KR] nullable (written by slice 0)
-  const float* w;     // fwd: [N][KR];  dgrad: [KR][N]
-  const float* bias;  // fwd: [N] nullable
-  bf16_t* out;        // [M][N]
-  const bf16_t* res;  // dgrad: [M][N] nullable
-  const bf16_t* xi;   // dgrad: [M][N] the input BN's raw input (partials)
-  const float *m0, *is0, *g0, *b0, *k12;  // fwd: the input BN (m0 == nullptr: none); dgrad: the following BN
-  int relu0;
-  const float *m1, *is1, *g1, *b1;        // dgrad: the input BN (partials)
-  int relu1;
-  double* part;       // [gridDim.x][2][N] nullable
-  int M, N;
-  FoldTail ft;
-};
-
-template <int KR, int NW, int CK0, bool BN, bool STATS>
-__global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void fwd_deep_kernel(DeepArgs a) {
-  constexpr int CK = CK0 < KR ? CK0 : KR;
-  constexpr int NO = NOD, SKB = KR + 8, NU = NO / 32, CS = CK / 16, NCH = KR / CK, NT = 64 * NW;
-  static_assert(KR % CK == 0 && CK % 16 == 0, "chunks");
-  __shared__ __attribute__((aligned(16))) bf16_t Bs[NO * SKB];
-  __shared__ __attribute__((aligned(16))) float tab[4][KR];
-  static_assert(sizeof(bf16_t) * NO * SKB + sizeof(float) * 4 * KR <= 159 * 1024, "LDS of one CU");
-  // the statistics' block reduction reuses the weight slice once every wave has left the loop
-  double(*const red)[2][NO] = reinterpret_cast<double(*)[2][NO]>(Bs);
-  static_assert(sizeof(double) * NW * 2 * NO <= sizeof(bf16_t) * NO * SKB, "red fits in Bs");
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int l32 = lane & 31, h = lane >> 5;
-  const int n0 = blockIdx.y * NO, N = a.N;
-  // the weight slice, 4 k at a time (16-byte loads, 8-byte LDS stores)
-  for (int i = tid; i < KR * NO / 4; i += NT) {
-    const int n = i / (KR / 4), k = 4 * (i - n * (KR / 4));
-    const f32x4 v = ld4(a.w + (size_t)(n0 + n) * KR + k);
-    *reinterpret_cast<uint2*>(Bs + n * SKB + k) = f32_to_bf16x4(v);
-  }
-  if constexpr (BN) {
-    for (int c = tid; c < KR; c += NT) {
-      tab[0][c] = a.m0[c];
-      tab[1][c] = a.is0[c];
-      tab[2][c] = a.g0[c];
-      tab[3][c] = a.b0[c];
-    }
-  }
-  float bias[NU];
-#pragma unroll
-  for (int u = 0; u < NU; ++u) bias[u] = a.bias ? a.bias[n0 + 32 * u + l32] : 0.f;
-  const bool irelu = a.relu0 != 0;
-  __syncthreads();
-
-  const __amdgpu_buffer_rsrc_t rx = make_rsrc_v(a.a0, (uint32_t)a.M * KR * 2u);
-  const __amdgpu_buffer_rsrc_t ry = make_rsrc_v(a.out, (uint32_t)a.M * N * 2u);
-  const int ntiles = (a.M + TR - 1) / TR;
-  const int W = gridDim.x * NW;
-  int t = blockIdx.x * NW + wave;
-  double ps[NU], pq[NU];
-#pragma unroll
-  for (int u = 0; u < NU; ++u) ps[u] = pq[u] = 0.0;
-
-  auto load_chunk = [&](int tile, int c, u32x4* lx) {
-    const uint32_t base = ((uint32_t)(tile * TR + l32) * KR + c * CK + 8 * h) * 2u;
-#pragma unroll
-    for (int s = 0; s < CS; ++s)
-      lx[s] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rx, (int)(base + 32u * s), 0, 0));
-  };
-  u32x4 cx[CS];
-  load_chunk(t, 0, cx);
-  drain_vmem_loads();
-  for (; t < ntiles; t += W) {
-    const int m0 = t * TR;
-    int z = 0;
-    asm volatile("" : "+s"(z));
-    const float* tb = &tab[0][0] + z;
-    const bf16_t* bs = Bs + z;
-    f32x16 acc[NU];
-#pragma unroll
-    for (int u = 0; u < NU; ++u)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[u][r] = 0.f;
-#pragma unroll
-    for (int c = 0; c < NCH; ++c) {
-      u32x4 nx[CS];
-      if (c + 1 < NCH)
-        load_chunk(t, c + 1, nx);
-      else
-        load_chunk(t + W, 0, nx);
-      __builtin_amdgcn_sched_barrier(0);
-      bf16x8 af[CS];
-#pragma unroll
-      for (int s = 0; s < CS; ++s) {
-        if constexpr (BN) {
-          f32x4 v[2];
-          unpack8(cx[s], v[0], v[1]);
-#pragma unroll
-          for (int p = 0; p < 2; ++p) {
-            const int c0 = c * CK + 16 * s + 8 * h + 4 * p;
-            const f32x4 mu = ld4(tb + 0 * KR + c0), is = ld4(tb + 1 * KR + c0), ga = ld4(tb + 2 * KR + c0),
-                        be = ld4(tb + 3 * KR + c0);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              const float r = bn_out(v[p][e], mu[e], is[e], ga[e], be[e]);
-              v[p][e] = (irelu & !(r > 0.f)) ? 0.f : r;
-            }
-          }
-          af[s] = frag(pack8(v[0], v[1]));
-        } else {
-          af[s] = frag(cx[s]);
-        }
-      }
-#pragma unroll
-      for (int s = 0; s < CS; ++s) {
-#pragma unroll
-        for (int u = 0; u < NU; ++u) {
-          const bf16x8 bf = *reinterpret_cast<const bf16x8*>(bs + (32 * u + l32) * SKB + c * CK + 16 * s + 8 * h);
-          acc[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[s], bf, acc[u], 0, 0, 0);
-        }
-      }
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int s = 0; s < CS; ++s) cx[s] = nx[s];
-    }
-
-    const int mb = m0 + 4 * h;
-    const uint32_t eb = ((uint32_t)mb * N + n0 + l32) * 2u;
-#pragma unroll
-    for (int u = 0; u < NU; ++u) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int dm = (r & 3) + 8 * (r >> 2);
-        float v = acc[u][r];
-        if (a.bias) v += bias[u];
-        const uint16_t bits = bf16_bits(v);
-        __builtin_amdgcn_raw_buffer_store_b16(bits, ry, (int)(eb + (uint32_t)(dm * N + 32 * u) * 2u), 0, 0);
-        if constexpr (STATS) {
-          const double d = (mb + dm < a.M) ? (double)__builtin_bit_cast(float, (uint32_t)bits << 16) : 0.0;
-          ps[u] += d;
-          pq[u] += d * d;
-        }
-      }
-    }
-  }
-  if constexpr (!STATS) return;
-  __syncthreads();  // Bs becomes red
-#pragma unroll
-  for (int u = 0; u < NU; ++u) {
-    ps[u] += __shfl_xor(ps[u], 32, 64);
-    pq[u] += __shfl_xor(pq[u], 32, 64);
-    if (h == 0) {
-      red[wave][0][32 * u + l32] = ps[u];
-      red[wave][1][32 * u + l32] = pq[u];
-    }
-  }
-  __syncthreads();
-  for (int i = tid; i < 2 * NO; i += NT) {
-    const int which = i / NO, c = i - which * NO;
-    double s = 0.0;
-#pragma unroll
-    for (int w = 0; w < NW; ++w) s += red[w][which][c];
-    pub_store(a.part + ((size_t)blockIdx.x * 2 + which) * N + n0 + c, s);
-  }
-  if (a.ft.part) fold_tail<NT>(a.ft, blockIdx.x, n0, NO, blockIdx.y);
-}
-
-template <int KR, int NW, int CK0, bool RES, bool PART>
-__global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void dgrad_deep_kernel(DeepArgs a) {
-  constexpr int CK = CK0 < KR ? CK0 : KR;
-  constexpr int NO = NOD, SKB = KR + 8, NU = NO / 32, CS = CK / 16, NCH = KR / CK, NT = 64 * NW;
-  static_assert(KR % CK == 0 && CK % 16 == 0, "chunks");
-  __shared__ __attribute__((aligned(16))) bf16_t Bs[NO * SKB];  // Bs[c][k] = W[k][n0 + c]
-  __shared__ __attribute__((aligned(16))) float tab[7][KR];
-  static_assert(sizeof(bf16_t) * NO * SKB + sizeof(float) * 7 * KR <= 159 * 1024, "LDS of one CU");
-  double(*const red)[2][NO] = reinterpret_cast<double(*)[2][NO]>(Bs);
-  static_assert(sizeof(double) * NW * 2 * NO <= sizeof(bf16_t) * NO * SKB, "red fits in Bs");
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int l32 = lane & 31, h = lane >> 5;
-  const int n0 = blockIdx.y * NO, N = a.N;
-  // the weight slice transposed, a 4 x 4 block (4 k x 4 c) per step: 16-byte loads along c,
-  // 8-byte LDS stores along k
-  for (int i = tid; i < KR * NO / 16; i += NT) {
-    const int kq = i / (NO / 4), c = 4 * (i - kq * (NO / 4)), k = 4 * kq;
-    f32x4 r[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) r[j] = ld4(a.w + (size_t)(k + j) * N + n0 + c);
-#pragma unroll
-    for (int e = 0; e < 4; ++e)
-      *reinterpret_cast<uint2*>(Bs + (c + e) * SKB + k) = f32_to_bf16x4(f32x4{r[0][e], r[1][e], r[2][e], r[3][e]});
-  }
-  for (int k = tid; k < KR; k += NT) {
-    const float is = a.is0[k], ga = a.g0[k];
-    tab[0][k] = a.m0[k];
-    tab[1][k] = is;
-    tab[2][k] = ga;
-    tab[3][k] = a.b0[k];
-    tab[4][k] = a.k12[k];
-    tab[5][k] = a.k12[KR + k];
-    tab[6][k] = ga * is;
-  }
-  float pm[NU], pis[NU], pga[NU], pbe[NU];
-#pragma unroll
-  for (int u = 0; u < NU; ++u) {
-    const int c = n0 + 32 * u + l32;
-    pm[u] = PART ? a.m1[c] : 0.f;
-    pis[u] = PART ? a.is1[c] : 0.f;
-    pga[u] = PART ? a.g1[c] : 0.f;
-    pbe[u] = PART ? a.b1[c] : 0.f;
-  }
-  const bool orelu = a.relu0 != 0, irelu = a.relu1 != 0;
-  __syncthreads();
-
-  const uint32_t kbytes = (uint32_t)a.M * KR * 2u, nbytes = (uint32_t)a.M * N * 2u;
-  const __amdgpu_buffer_rsrc_t rg = make_rsrc_v(a.a0, kbytes), rx = make_rsrc_v(a.a1, kbytes);
-  const __amdgpu_buffer_rsrc_t rxi = make_rsrc_v(PART ? a.xi : a.a0, PART ? nbytes : 0u);
-  const __amdgpu_buffer_rsrc_t rr = make_rsrc_v(RES ? a.res : a.a0, RES ? nbytes : 0u);
-  const __amdgpu_buffer_rsrc_t rdx = make_rsrc_v(a.out, nbytes);
-  // dy written through by slice 0 only (the others' stores fall outside a zero-size resource)
-  const bool writer = a.dy_out != nullptr && blockIdx.y == 0;
-  const __amdgpu_buffer_rsrc_t rdy = make_rsrc_v(writer ? a.dy_out : a.out, writer ? kbytes : 0u);
-  const int ntiles = (a.M + TR - 1) / TR;
-  const int W = gridDim.x * NW;
-  int t = blockIdx.x * NW + wave;
-  double ps[NU], pq[NU];
-#pragma unroll
-  for (int u = 0; u < NU; ++u) ps[u] = pq[u] = 0.0;
-
-  auto load_chunk = [&](int tile, int c, u32x4* lg, u32x4* lx) {
-    const uint32_t base = ((uint32_t)(tile * TR + l32) * KR + c * CK + 8 * h) * 2u;
-#pragma unroll
-    for (int s = 0; s < CS; ++s) {
-      lg[s] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rg, (int)(base + 32u * s), 0, 0));
-      lx[s] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rx, (int)(base + 32u * s), 0, 0));
-    }
-  };
-  u32x4 cg[CS], cx[CS];
-  load_chunk(t, 0, cg, cx);
-  drain_vmem_loads();
-  for (; t < ntiles; t += W) {
-    const int m0 = t * TR;
-    int z = 0;
-    asm volatile("" : "+s"(z));
-    const float* tb = &tab[0][0] + z;
-    const bf16_t* bs = Bs + z;
-
-    const int mb = m0 + 4 * h;
-    const uint32_t eb = ((uint32_t)mb * N + n0 + l32) * 2u;
-    f32x16 acc[NU];
-#pragma unroll
-    for (int u = 0; u < NU; ++u)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[u][r] = 0.f;
-    const uint32_t dbase = ((uint32_t)(m0 + l32) * KR + 8 * h) * 2u;
-#pragma unroll
-    for (int c = 0; c < NCH; ++c) {
-      u32x4 ng[CS], nx[CS];
-      if (c + 1 < NCH)
-        load_chunk(t, c + 1, ng, nx);
-      else
-        load_chunk(t + W, 0, ng, nx);
-      __builtin_amdgcn_sched_barrier(0);
-      bf16x8 af[CS];
-#pragma unroll
-      for (int s = 0; s < CS; ++s) {
-        f32x4 gv[2], xv[2];
-        unpack8(cg[s], gv[0], gv[1]);
-        unpack8(cx[s], xv[0], xv[1]);
-#pragma unroll
-        for (int p = 0; p < 2; ++p) {
-          const int k0 = c * CK + 16 * s + 8 * h + 4 * p;
-          const f32x4 mu = ld4(tb + 0 * KR + k0), is = ld4(tb + 1 * KR + k0), ga = ld4(tb + 2 * KR + k0),
-                      be = ld4(tb + 3 * KR + k0);
-          const f32x4 k1 = ld4(tb + 4 * KR + k0), k2 = ld4(tb + 5 * KR + k0), f = ld4(tb + 6 * KR + k0);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const float xe = xv[p][e];
-            float ge = gv[p][e];
-            const bool kill = (!(bn_out(xe, mu[e], is[e], ga[e], be[e]) > 0.f)) & orelu;
-            ge = kill ? 0.f : ge;
-            gv[p][e] = bn_bwd_elem(xe, ge, mu[e], is[e], f[e], k1[e], k2[e]);
-          }
-        }
-        const u32x4 dyq = pack8(gv[0], gv[1]);
-        af[s] = frag(dyq);
-        __builtin_amdgcn_raw_buffer_store_b128(dyq, rdy, (int)(dbase + (uint32_t)(c * CK + 16 * s) * 2u), 0, 0);
-      }
-#pragma unroll
-      for (int s = 0; s < CS; ++s) {
-#pragma unroll
-        for (int u = 0; u < NU; ++u) {
-          const bf16x8 bf = *reinterpret_cast<const bf16x8*>(bs + (32 * u + l32) * SKB + c * CK + 16 * s + 8 * h);
-          acc[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[s], bf, acc[u], 0, 0, 0);
-        }
-      }
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int s = 0; s < CS; ++s) {
-        cg[s] = ng[s];
-        cx[s] = nx[s];
-      }
-    }
-
-    // the epilogue operands (C layout) of one column block at a time: 4 x 32 of them would not fit
-    // beside the chunk pipeline; the other wave of the SIMD covers their round trip
-#pragma unroll
-    for (int u = 0; u < NU; ++u) {
-      uint32_t exi[16], ers[16];
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int dm = (r & 3) + 8 * (r >> 2);
-        const int off = (int)(eb + (uint32_t)(dm * N + 32 * u) * 2u);
-        if constexpr (PART) exi[r] = __builtin_amdgcn_raw_buffer_load_b16(rxi, off, 0, 0);
-        if constexpr (RES) ers[r] = __builtin_amdgcn_raw_buffer_load_b16(rr, off, 0, 0);
-      }
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int dm = (r & 3) + 8 * (r >> 2);
-        float v = acc[u][r];
-        if constexpr (RES) v += __builtin_bit_cast(float, ers[r] << 16);
-        const uint16_t bits = bf16_bits(v);
-        __builtin_amdgcn_raw_buffer_store_b16(bits, rdx, (int)(eb + (uint32_t)(dm * N + 32 * u) * 2u), 0, 0);
-        if constexpr (PART) {
-          const float gs = __builtin_bit_cast(float, (uint32_t)bits << 16);
-          const float x = __builtin_bit_cast(float, exi[r] << 16);
-          const float xh = (x - pm[u]) * pis[u];
-          const bool kill = ((!(bn_out(x, pm[u], pis[u], pga[u], pbe[u]) > 0.f)) & irelu) | (mb + dm >= a.M);
-          const float g2 = kill ? 0.f : gs;
-          ps[u] += (double)g2;
-          pq[u] += (double)g2 * (double)xh;
-        }
-      }
-    }
-  }
-  if constexpr (!PART) return;
-  __syncthreads();  // Bs becomes red
-#pragma unroll
-  for (int u = 0; u < NU; ++u) {
-    ps[u] += __shfl_xor(ps[u], 32, 64);
-    pq[u] += __shfl_xor(pq[u], 32, 64);
-    if (h == 0) {
-      red[wave][0][32 * u + l32] = ps[u];
-      red[wave][1][32 * u + l32] = pq[u];
-    }
-  }
-  __syncthreads();
-  for (int i = tid; i < 2 * NO; i += NT) {
-    const int which = i / NO, c = i - which * NO;
-    double s = 0.0;
-#pragma unroll
-    for (int w = 0; w < NW; ++w) s += red[w][which][c];
-    pub_store(a.part + ((size_t)blockIdx.x * 2 + which) * N + n0 + c, s);
-  }
-  if (a.ft.part) fold_tail<NT>(a.ft, blockIdx.x, n0, NO, blockIdx.y);
-}
-
 template <int KR, int NO>
 static int fwd_occ() {
   // thread-safe one-time query (a function-local static initialised once)
@@ -814,88 +443,22 @@ static int dgrad_occ() {
   return occ;
 }
 
+
 // The (reduction, output) channel pairs instantiated.
 #define DK_PWSH_SHAPES(X) X(64, 64) X(64, 128) X(128, 64) X(128, 128)
-
-// Deep kernels: reductions instantiated, waves per block, chunk lengths.
-#define DK_PWSH_DEEP(X) X(128) X(256) X(512)
-template <int KR>
-constexpr int deep_nw() {
-  return KR >= 512 ? 8 : 4;
-}
-constexpr int kFwdCK = 64, kDgradCK = 64;
-static bool deep_shape(int KR, int N) {
-  return (KR == 128 || KR == 256 || KR == 512) && N % NOD == 0 && N >= NOD && N <= 4096 && (KR >= 256 || N >= 256);
-}
-template <int KR>
-static int fwd_deep_occ() {
-  // thread-safe one-time query (a function-local static initialised once)
-  static const int occ = [] {
-    constexpr int NW = deep_nw<KR>();
-    const void* fs[] = {reinterpret_cast<const void*>(&fwd_deep_kernel<KR, NW, kFwdCK, true, true>),
-                        reinterpret_cast<const void*>(&fwd_deep_kernel<KR, NW, kFwdCK, true, false>),
-                        reinterpret_cast<const void*>(&fwd_deep_kernel<KR, NW, kFwdCK, false, true>),
-                        reinterpret_cast<const void*>(&fwd_deep_kernel<KR, NW, kFwdCK, false, false>)};
-    return min_occupancy(fs, 4, 64 * NW);
-  }();
-  return occ;
-}
-template <int KR>
-static int dgrad_deep_occ() {
-  // thread-safe one-time query (a function-local static initialised once)
-  static const int occ = [] {
-    constexpr int NW = deep_nw<KR>();
-    const void* fs[] = {reinterpret_cast<const void*>(&dgrad_deep_kernel<KR, NW, kDgradCK, true, true>),
-                        reinterpret_cast<const void*>(&dgrad_deep_kernel<KR, NW, kDgradCK, true, false>),
-                        reinterpret_cast<const void*>(&dgrad_deep_kernel<KR, NW, kDgradCK, false, true>),
-                        reinterpret_cast<const void*>(&dgrad_deep_kernel<KR, NW, kDgradCK, false, false>)};
-    return min_occupancy(fs, 4, 64 * NW);
-  }();
-  return occ;
-}
-// Row walkers per slice: the slices share the resident slots; when the tiles need more than one
-// round, as few walkers as give the same number of rounds.  A function of (M, N, occupancy) only.
-static int deep_grid_x(int M, int N, int occ, int nw) {
-  const int ntiles = (M + TR - 1) / TR;
-  const int slices = N / NOD;
-  int slots = occ * 256 / slices;
-  if (slots < 1) slots = 1;
-  const int want = (ntiles + nw - 1) / nw;
-  if (want <= slots) return want > 0 ? want : 1;
-  const int rounds = (ntiles + slots * nw - 1) / (slots * nw);
-  return (ntiles + rounds * nw - 1) / (rounds * nw);
-}
 
 }  // namespace pwsh
 
 // DORKNET_PW_STREAM_BF16=0 (or the fp32 switch DORKNET_PW_STREAM=0) keeps the tiled engine.
-static int g_pwsh = -1;
-static bool pwsh_enabled() {
-  if (g_pwsh < 0) {
-    const char* e = getenv("DORKNET_PW_STREAM_BF16");
-    g_pwsh = (e && e[0] == '0') ? 0 : 1;
-  }
-  return g_pwsh == 1 && pw_stream_enabled();
-}
-void pw_stream_bf16_set(int v) { g_pwsh = v < 0 ? -1 : v; }
+// (knob kKnobPwsh, kind 9)
+static bool pwsh_enabled() { return knob(kKnobPwsh) == 1 && pw_stream_enabled(); }
 
 static bool pwsh_shape(int KR, int NO) { return (KR == 64 || KR == 128) && (NO == 64 || NO == 128); }
-// the deep (column-sliced) kernels: off with DORKNET_PW_STREAM_BF16_DEEP=0 or knob 10
-static int g_pwsh_deep = -1;
-static bool pwsh_deep_enabled() {
-  if (g_pwsh_deep < 0) {
-    const char* e = getenv("DORKNET_PW_STREAM_BF16_DEEP");
-    g_pwsh_deep = (e && e[0] == '0') ? 0 : 1;
-  }
-  return g_pwsh_deep == 1;
-}
-void pw_stream_bf16_deep_set(int v) { g_pwsh_deep = v < 0 ? -1 : v; }
-static bool deep_ok(int KR, int N, int M) {
-  return !pwsh_shape(KR, N) && pwsh_deep_enabled() && pwsh::deep_shape(KR, N);
-}
-
+constexpr int kDeepCols = 128;  // output columns per block of the deep kernels (pw_deep_bf16.hip)
+// The deep shapes (reduction or outputs of 256+) go to the weight-stationary kernels of
+// pw_deep_bf16.hip (knob 13); with those off they stay on the tiled engine.
 bool pw_stream_bf16_fwd_ok(int K, int C, int M) {
-  return pwsh_enabled() && (pwsh_shape(C, K) || deep_ok(C, K, M)) && M > 0 &&
+  return pwsh_enabled() && (pwsh_shape(C, K) || pw_deep16_fwd_ok(K, C, M)) && M > 0 &&
          (size_t)M * (K > C ? K : C) * 2 < ((size_t)1 << 31);
 }
 int pw_stream_bf16_fwd_rows(int M, int K, int C) {
@@ -904,15 +467,11 @@ int pw_stream_bf16_fwd_rows(int M, int K, int C) {
   if (C == kr && K == no) return pwsh::grid_blocks(M, pwsh::fwd_occ<kr, no>());
   DK_PWSH_SHAPES(DK_ROWS)
 #undef DK_ROWS
-#define DK_ROWS(kr) \
-  if (C == kr) return pwsh::deep_grid_x(M, K, pwsh::fwd_deep_occ<kr>(), pwsh::deep_nw<kr>());
-  DK_PWSH_DEEP(DK_ROWS)
-#undef DK_ROWS
   return 0;
 }
-int pw_stream_bf16_fwd_slices(int K, int C) { return pwsh_shape(C, K) ? 1 : K / pwsh::NOD; }
+int pw_stream_bf16_fwd_slices(int K, int C) { return pwsh_shape(C, K) ? 1 : K / kDeepCols; }
 bool pw_stream_bf16_dgrad_ok(int K, int C, int M) {
-  return pwsh_enabled() && (pwsh_shape(K, C) || deep_ok(K, C, M)) && M > 0 &&
+  return pwsh_enabled() && (pwsh_shape(K, C) || pw_deep16_dgrad_ok(K, C, M)) && M > 0 &&
          (size_t)M * (K > C ? K : C) * 2 < ((size_t)1 << 31);
 }
 int pw_stream_bf16_dgrad_rows(int M, int K, int C) {
@@ -921,42 +480,16 @@ int pw_stream_bf16_dgrad_rows(int M, int K, int C) {
   if (K == kr && C == no) return pwsh::grid_blocks(M, pwsh::dgrad_occ<kr, no>());
   DK_PWSH_SHAPES(DK_ROWS)
 #undef DK_ROWS
-#define DK_ROWS(kr) \
-  if (K == kr) return pwsh::deep_grid_x(M, C, pwsh::dgrad_deep_occ<kr>(), pwsh::deep_nw<kr>());
-  DK_PWSH_DEEP(DK_ROWS)
-#undef DK_ROWS
   return 0;
 }
-int pw_stream_bf16_dgrad_slices(int K, int C) { return pwsh_shape(K, C) ? 1 : C / pwsh::NOD; }
+int pw_stream_bf16_dgrad_slices(int K, int C) { return pwsh_shape(K, C) ? 1 : C / kDeepCols; }
 
 int pw_stream_bf16_fwd(const bf16_t* x, int M, const float* w, int K, int C, const float* bias, bf16_t* y,
                        const float* im, const float* iis, const float* ig, const float* ib, int irelu, double* part,
                        hipStream_t st, const FoldTail* ft) {
   if (!pwsh_shape(C, K) && pw_deep16_fwd_ok(K, C, M))  // the weight-stationary kernels (pw_deep_bf16.hip)
     return pw_deep16_fwd(x, M, w, K, C, bias, y, im, iis, ig, ib, irelu, part, st, ft);
-  if (!pwsh_shape(C, K)) {
-    pwsh::DeepArgs d{x, nullptr, nullptr, w, bias, y, nullptr, nullptr, im, iis, ig, ib, nullptr, irelu,
-                     nullptr, nullptr, nullptr, nullptr, 0, part, M, K};
-    if (ft && part) d.ft = *ft;
-    const dim3 grid(pw_stream_bf16_fwd_rows(M, K, C), K / pwsh::NOD);
-    if (grid.x == 0 || !pwsh::deep_shape(C, K)) return DK_ERR_ARGS;
-#define DK_FWD(kr)                                                                                       \
-  if (C == kr) {                                                                                         \
-    constexpr int NW = pwsh::deep_nw<kr>(), CK = pwsh::kFwdCK;                                           \
-    if (im && part)                                                                                      \
-      hipLaunchKernelGGL((pwsh::fwd_deep_kernel<kr, NW, CK, true, true>), grid, dim3(64 * NW), 0, st, d);  \
-    else if (im)                                                                                         \
-      hipLaunchKernelGGL((pwsh::fwd_deep_kernel<kr, NW, CK, true, false>), grid, dim3(64 * NW), 0, st, d); \
-    else if (part)                                                                                       \
-      hipLaunchKernelGGL((pwsh::fwd_deep_kernel<kr, NW, CK, false, true>), grid, dim3(64 * NW), 0, st, d); \
-    else                                                                                                 \
-      hipLaunchKernelGGL((pwsh::fwd_deep_kernel<kr, NW, CK, false, false>), grid, dim3(64 * NW), 0, st, d); \
-    return launch_status();                                                                              \
-  }
-    DK_PWSH_DEEP(DK_FWD)
-#undef DK_FWD
-    return DK_ERR_ARGS;
-  }
+  if (!pwsh_shape(C, K)) return DK_ERR_ARGS;
   pwsh::FwdArgs a{x, w, bias, y, im, iis, ig, ib, irelu, part, M};
   if (ft && part) a.ft = *ft;
   const dim3 grid(pw_stream_bf16_fwd_rows(M, K, C));
@@ -986,29 +519,7 @@ int pw_stream_bf16_dgrad_bnbwd(const bf16_t* g, const bf16_t* bn_x, int M, int K
   if (!pwsh_shape(K, C) && pw_deep16_dgrad_ok(K, C, M))
     return pw_deep16_dgrad_bnbwd(g, bn_x, M, K, C, om, ois, og, ob, orelu, k12, dy_out, w, dx, res, x, im, iis, ig, ib,
                                  irelu, part, st, ft);
-  if (!pwsh_shape(K, C)) {
-    pwsh::DeepArgs d{g, bn_x, dy_out, w, nullptr, dx, res, x, om, ois, og, ob, k12, orelu,
-                     im, iis, ig, ib, irelu, part, M, C};
-    if (ft && part) d.ft = *ft;
-    const dim3 grid(pw_stream_bf16_dgrad_rows(M, K, C), C / pwsh::NOD);
-    if (grid.x == 0 || !pwsh::deep_shape(K, C)) return DK_ERR_ARGS;
-#define DK_DG(kr)                                                                                          \
-  if (K == kr) {                                                                                           \
-    constexpr int NW = pwsh::deep_nw<kr>(), CK = pwsh::kDgradCK;                                           \
-    if (res && x)                                                                                          \
-      hipLaunchKernelGGL((pwsh::dgrad_deep_kernel<kr, NW, CK, true, true>), grid, dim3(64 * NW), 0, st, d);  \
-    else if (res)                                                                                          \
-      hipLaunchKernelGGL((pwsh::dgrad_deep_kernel<kr, NW, CK, true, false>), grid, dim3(64 * NW), 0, st, d); \
-    else if (x)                                                                                            \
-      hipLaunchKernelGGL((pwsh::dgrad_deep_kernel<kr, NW, CK, false, true>), grid, dim3(64 * NW), 0, st, d); \
-    else                                                                                                   \
-      hipLaunchKernelGGL((pwsh::dgrad_deep_kernel<kr, NW, CK, false, false>), grid, dim3(64 * NW), 0, st, d); \
-    return launch_status();                                                                                \
-  }
-    DK_PWSH_DEEP(DK_DG)
-#undef DK_DG
-    return DK_ERR_ARGS;
-  }
+  if (!pwsh_shape(K, C)) return DK_ERR_ARGS;
   pwsh::DgradArgs a{g, bn_x, dy_out, w, dx, res, x, om, ois, og, ob, k12, orelu, im, iis, ig, ib, irelu, part, M};
   if (ft && part) a.ft = *ft;
   const dim3 grid(pw_stream_bf16_dgrad_rows(M, K, C));

@@ -47,22 +47,30 @@ int dk_resize_bilinear_u8(const uint8_t* src, int N, int H, int W, int C, int OH
 int dk_u8_nhwc_to_nchw_f32(const uint8_t* src, int N, int H, int W, int C, const int* crop_rc, int OH, int OW, float shift, float* dst, void* stream);
 int dk_mixup_f32(const float* a, const float* b, long long n, float p, float one_minus_p, float* ab, float* ba, void* stream);
 
-/* Tuning knob (not for production use; not thread-safe): force GEMM tile configuration
- * `cfg` for kind 0 = forward/dgrad problems or 1 = split-K weight-gradient problems;
- * cfg = -1 restores the built-in heuristic.  Returns the number of configurations.
- * kind 2: split-K grids sized to one round of resident blocks (1 = default, also for -1) or
- * the fixed ~1024-block split (0); returns 0.
- * kind 3: the streaming pointwise kernels for K = C = 64 (1 = default, also for -1; 0 = the
- * tiled engine for every shape, as DORKNET_PW_STREAM=0); returns 0.
- * kind 4: nontemporal output stores, a bitmask over kernel families (bit 0 depthwise forward, 1 fused
- * depthwise backward, 2 bn_add, 3 fused pointwise backward, 4 streaming pointwise forward, 5 streaming
- * BN-backward dgrad, 6 tiled GEMM epilogues, 7 the narrow stem forward; -1 = the default mask, bits
- * 0-6); kind 5: the streaming fused pointwise backward's operand
- * prefetch; kind 6: unused; kind 7: blocks the fused stride-1 depthwise backward aims for (its
- * batch is dealt into image runs above that; 0 = one image per block; -1 = default 768);
+/* Tuning knobs for A/B runs (dorknet_amd/csrc/knobs.hip: one registry of atomics whose defaults
+ * come from the DORKNET_* environment, read once; not for production use).  cfg = -1 restores the
+ * default.  Returns the number of configurations for kinds 0 / 1, 0 for the others, -1 for an
+ * unknown kind.
+ * kind 0 / 1: force GEMM tile configuration `cfg` for forward/dgrad problems / split-K
+ * weight-gradient problems (-1 = the built-in heuristic);
+ * kind 2: split-K grids sized to one round of resident blocks (1 = default) or the fixed ~1024-block
+ * split (0);
+ * kind 3: the streaming pointwise kernels for K = C = 64 (1 = default; 0 = the tiled engine for every
+ * shape, as DORKNET_PW_STREAM=0);
+ * kind 4: nontemporal output stores, a bitmask over kernel families (NtFam in csrc/dk_common.h;
+ * DORKNET_NT_STORES);
+ * kind 5: the streaming fused pointwise backward's operand prefetch (DORKNET_PWS_BWD_PF);
+ * kind 7: blocks the fused stride-1 depthwise backward aims for (its batch is dealt into image runs
+ * above that; 0 = one image per block; default 768, DORKNET_DWB_BLOCKS);
  * kind 8: output rows per thread of the depthwise forward / stride-1 dgrad (-1 = the shape rule);
- * kind 9: the bf16 streaming pointwise kernels (1 / -1 = on, the default; 0 = the tiled engine);
- * kind 10: their column-sliced variants for K or C of 256 / 512 (1 / -1 = on; 0 = the tiled engine). */
+ * kind 9: the bf16 streaming pointwise kernels (1 = default; 0 = the tiled engine);
+ * kind 11: the fp32 weight-stationary deep pointwise kernels (DORKNET_PW_DEEP);
+ * kind 13: the bf16 weight-stationary deep pointwise kernels (DORKNET_PW_DEEP_BF16);
+ * kind 14: the fused deep pointwise backward, dgrad + weight gradient in one pass (DORKNET_PW_DEEP_BWD);
+ * kind 15: the streaming forward at K = C = 128 (DORKNET_PW_STREAM128);
+ * kind 16 / 17: the tiled fused pointwise backward's prefetch (-1 = per shape) and resident blocks per
+ * CU (0 = occupancy) (DORKNET_PWF_PREFETCH / DORKNET_PWF_BLOCKS_PER_CU);
+ * kind 18: blocks a split-K weight gradient aims for (DORKNET_WGRAD_BLOCKS, default 1024). */
 int dk_debug_set_gemm_config(int kind, int cfg);
 
 /* Bandwidth ceiling probe (not on the training path; scripts/stream_ceiling.py): reads nin

@@ -61,7 +61,7 @@ def main():
         res, outs, wout = [], {}, {}
         for deep in modes:
             lib.dk_debug_set_gemm_config(11, deep)
-            lib.dk_debug_set_gemm_config(12, deep)
+            lib.dk_debug_set_gemm_config(14, deep)
             y = torch.full((M * K,), float("nan"), device="cuda")
             dy = torch.full((M * K,), float("nan"), device="cuda")
             dx = torch.full((M * C,), float("nan"), device="cuda")
@@ -102,11 +102,23 @@ def main():
                 line.append(f"wgrad {tw:6.1f} us {flops / tw / 1e6 / PEAK:4.2f}")
                 torch.cuda.synchronize()
                 wout[deep] = dw.clone()
+            if only in (None, "bwd") and deep and lib.dk_pwconv_bwd_fused_preferred(B, HW, HW, K, C):
+                # the fused deep backward (knob 14): dgrad + weight gradient in one pass, dy not stored
+                rows = lib.dk_pwconv_bwd_fused_rows(B, HW, HW, K, C)
+                partb = torch.empty(rows * 2 * C, dtype=torch.float64, device="cuda")
+                nbf = lib.dk_pwconv_bwd_fused_workspace_bytes(B, HW, HW, K, C)
+                wsf = torch.empty(nbf // 4 + 1, device="cuda")
+                dwf = torch.empty(K * C, device="cuda")
+                ba = (g.data_ptr(), xo.data_ptr(), B, HW, HW, K, *(t.data_ptr() for t in po), 1, k12.data_ptr(),
+                      w.data_ptr(), C, 1e-4, dwf.data_ptr(), dx.data_ptr(), 0, x.data_ptr(),
+                      *(t.data_ptr() for t in pi), 1, partb.data_ptr(), wsf.data_ptr(), nbf, st)
+                tb = timeit(lambda: lib.dk_pwconv_bwd_bnbwd_f32(*ba))
+                line.append(f"fused bwd {tb:6.1f} us {2 * flops / tb / 1e6 / PEAK:4.2f}")
             torch.cuda.synchronize()
             outs[deep] = (y.clone(), dy.clone(), dx.clone())
             res.append(("deep " if deep else "old  ") + ", ".join(line))
         lib.dk_debug_set_gemm_config(11, -1)
-        lib.dk_debug_set_gemm_config(12, -1)
+        lib.dk_debug_set_gemm_config(14, -1)
         same = ["bitwise" if torch.equal(a, b) else "DIFF(max %.2e)" % float((a - b).abs().nan_to_num(1e30).max())
                 for a, b in zip(outs[0], outs[1])] if len(outs) == 2 else []
         if len(wout) == 2:

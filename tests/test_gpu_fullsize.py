@@ -217,11 +217,16 @@ def test_stem_full_size(monkeypatch, narrow):
     _check(got, want, f32, twin, layers)
 
 
-def test_res4_res6_full_size(monkeypatch):
+@pytest.mark.parametrize("deep_bwd", [1, 0])
+def test_res4_res6_full_size(monkeypatch, deep_bwd):
     """res4 (28 x 28 x 128), res5 (the stride-2 128 -> 256 block: strided depthwise, 128 -> 256
     pointwise, stride-2 skip projection) and res6 (14 x 14 x 256) at batch 256 through the fused
-    network path (the middle blocks had no full-size check)."""
+    network path (the middle blocks had no full-size check); the pointwise backward both
+    as the fused deep pass (dgrad + weight gradient, dy never stored: dk_pwconv_bwd_bnbwd_f32 on
+    pw_deep.hip's bwd_kernel, knob 14) and as the dgrad / side-stream weight-gradient pair."""
+    from dorknet_amd._hip import lib
     from examples.resnet18_depsep import ResNet18
+    lib.dk_debug_set_gemm_config(14, deep_bwd)
     np.random.seed(41)
     layers = ResNet18("r18").layers[9:12]
     assert [l.layer_name for l in layers] == ["res4", "res5", "res6"]
@@ -230,9 +235,15 @@ def test_res4_res6_full_size(monkeypatch):
     X = np.abs(rng.standard_normal((256, 128, 28, 28), dtype=np.float32))   # res3's ReLU output
     dY = rng.standard_normal((256, 256, 14, 14), dtype=np.float32)
     calls = Calls(monkeypatch, FUSED + ["dk_dwconv_bwd_bnbwd_join_f32", "dk_dwconv_dgrad_join_f32"])
-    got, want, f32, twin, _ = _run(layers, X, dY, input_grad=True)
-    assert {"dk_pwconv_fwd_ex_f32", "dk_pwconv_dgrad_bnbwd_f32", "dk_pwconv_wgrad_bnx_f32", "dk_dwconv_fwd_ex_f32",
-            "dk_bn_add_f32", "dk_dwconv_bwd_bnbwd_join_f32", "dk_dwconv_dgrad_join_f32"} <= calls.seen, calls.seen
+    try:
+        got, want, f32, twin, _ = _run(layers, X, dY, input_grad=True)
+    finally:
+        lib.dk_debug_set_gemm_config(14, -1)
+    pw_bwd = {"dk_pwconv_bwd_bnbwd_f32"} if deep_bwd else {"dk_pwconv_dgrad_bnbwd_f32", "dk_pwconv_wgrad_bnx_f32"}
+    assert pw_bwd | {"dk_pwconv_fwd_ex_f32", "dk_dwconv_fwd_ex_f32", "dk_bn_add_f32", "dk_dwconv_bwd_bnbwd_join_f32",
+                     "dk_dwconv_dgrad_join_f32"} <= calls.seen, calls.seen
+    if deep_bwd:
+        assert "dk_pwconv_dgrad_bnbwd_f32" not in calls.seen, calls.seen
     _check(got, want, f32, twin, layers)
 
 

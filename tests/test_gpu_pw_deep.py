@@ -13,7 +13,7 @@ from dorknet_amd._hip import lib, stream_handle
 
 pytestmark = pytest.mark.gpu
 
-STREAM_KNOB, DEEP_KNOB, DEEP_WGRAD_KNOB = 3, 11, 12
+STREAM_KNOB, DEEP_KNOB = 3, 11
 
 
 def nhwc(a):
@@ -167,18 +167,17 @@ def test_deep_outputs_stay_in_bounds():
     assert bool(torch.isfinite(part).all()) and bool(torch.isfinite(partd).all())
 
 
-WGRAD_SHAPES = [(128, 64), (128, 128), (256, 128), (256, 256), (512, 512)]  # (K, C); K != C: the tiled engine
+WGRAD_SHAPES = [(128, 64), (128, 128), (256, 128), (256, 256), (512, 512)]  # (K, C)
 
 
 @pytest.mark.parametrize("K,C", WGRAD_SHAPES)
 @pytest.mark.parametrize("bn,relu,N,H,W", [(True, 1, 3, 13, 11), (True, 0, 2, 8, 8), (False, 0, 1, 1, 5),
                                            (True, 1, 16, 14, 14)])
 def test_deep_wgrad_matches_fp64(K, C, bn, relu, N, H, W):
-    """dk_pwconv_wgrad_bnx_f32 / dk_pwconv_wgrad_f32 on the deep output-stationary kernel (knobs 11 and 12
-    on; off by default in the network)
-    against an fp64 dW = dy^T relu(bn(x)) + l2 w, elementwise within 3e-5 of sum |dy| |xh| (fp32
-    partial sums of a few hundred products each, then the fp64 reduce), and against the tiled engine
-    (knob 11 off) within the same bound."""
+    """dk_pwconv_wgrad_bnx_f32 / dk_pwconv_wgrad_f32 (the tiled engine's split-K weight gradient, the
+    deep layers' path when the fused backward is off) against an fp64 dW = dy^T relu(bn(x)) + l2 w,
+    elementwise within 3e-5 of sum |dy| |xh| (fp32 partial sums of a few hundred products each, then
+    the fp64 reduce)."""
     rng = np.random.RandomState(K + 3 * C + N + int(bn) + 2 * relu)
     M = N * H * W
     dy = nhwc(rng.randn(N, K, H, W))
@@ -202,15 +201,7 @@ def test_deep_wgrad_matches_fp64(K, C, bn, relu, N, H, W):
         assert rc == 0
         torch.cuda.synchronize()
         return dw
-    outs = []
-    for knob in (0, 1):
-        lib.dk_debug_set_gemm_config(DEEP_KNOB, knob)
-        lib.dk_debug_set_gemm_config(DEEP_WGRAD_KNOB, knob)
-        try:
-            outs.append(run())
-        finally:
-            lib.dk_debug_set_gemm_config(DEEP_KNOB, -1)
-            lib.dk_debug_set_gemm_config(DEEP_WGRAD_KNOB, -1)
+    outs = [run()]
     dy64 = dy.permute(0, 2, 3, 1).reshape(M, K).double()
     x64 = x.permute(0, 2, 3, 1).reshape(M, C).double()
     if bn:
@@ -226,3 +217,104 @@ def test_deep_wgrad_matches_fp64(K, C, bn, relu, N, H, W):
     for dw in outs:
         assert bool(torch.isfinite(dw).all())
         assert bool(((dw.double() - ref).abs() <= bound).all()), float(((dw.double() - ref).abs() / bound).max())
+
+
+FUSED_KNOB = 14
+FUSED_SHAPES = [(128, 128), (256, 128), (256, 256), (128, 256), (256, 512)]  # (K, C)
+
+
+@pytest.mark.parametrize("K,C", FUSED_SHAPES)
+@pytest.mark.parametrize("relu,bn_in,resid,N,H,W", [(1, True, False, 3, 13, 11), (0, True, False, 2, 8, 8),
+                                                    (1, False, True, 3, 13, 11), (1, True, True, 5, 7, 9),
+                                                    (0, False, False, 1, 1, 3), (1, True, False, 16, 14, 14),
+                                                    (1, True, False, 64, 14, 14)])
+def test_deep_fused_bwd_matches_unfused(K, C, relu, bn_in, resid, N, H, W):
+    """dk_pwconv_bwd_bnbwd_f32 on the fused deep kernel (pw_deep.hip bwd_kernel: dgrad and weight
+    gradient in one pass, dy never stored) against the deep dgrad (dk_pwconv_dgrad_bnbwd_f32): dx bitwise,
+    the input BatchNorm's partial sums to fp64 rounding; and its weight gradient against fp64
+    dW = dy^T relu(bn(x)) + l2 w (dy = the dgrad's stored dy, the values the fused kernel forms on load),
+    elementwise within 3e-5 of sum |dy| |xh|.  Reference: pointwise_convolution.py:57-75."""
+    assert lib.dk_pwconv_bwd_fused_preferred(N, H, W, K, C) == 1
+    rng = np.random.RandomState(K + C + relu + 2 * bn_in + 4 * resid + N)
+    M = N * H * W
+    xo = nhwc(rng.randn(N, K, H, W))
+    g = nhwc(rng.randn(N, K, H, W))
+    po = bn_params(K, rng)
+    k12 = torch.as_tensor(rng.randn(2 * K).astype(np.float32) * 0.1, device="cuda")
+    w = torch.as_tensor((rng.randn(K, C) / np.sqrt(K)).astype(np.float32), device="cuda")
+    xin = nhwc(rng.randn(N, C, H, W) * 1.5 + 0.2)
+    pi = bn_params(C, rng)
+    res = nhwc(rng.randn(N, C, H, W)) if resid else None
+    l2 = 1e-3
+    st = stream_handle()
+    # the reference: deep dgrad (stores dy)
+    rows = lib.dk_pwconv_dgrad_bnbwd_stats_rows(N, H, W, K, C)
+    dy = torch.full_like(g, float("nan"))
+    dx0 = torch.full_like(xin, float("nan"))
+    p0 = torch.full((rows, 2, C), float("nan"), dtype=torch.float64, device="cuda")
+    bn_args = (xin.data_ptr(), *(t.data_ptr() for t in pi), relu, p0.data_ptr()) if bn_in else (0,) * 7
+    assert lib.dk_pwconv_dgrad_bnbwd_f32(g.data_ptr(), xo.data_ptr(), N, H, W, K, *(t.data_ptr() for t in po), relu,
+                                         k12.data_ptr(), dy.data_ptr(), w.data_ptr(), C, dx0.data_ptr(),
+                                         res.data_ptr() if resid else 0, *bn_args, st) in (0, 10100)
+    # the fused kernel
+    rows1 = lib.dk_pwconv_bwd_fused_rows(N, H, W, K, C)
+    assert rows1 > 0
+    nb = lib.dk_pwconv_bwd_fused_workspace_bytes(N, H, W, K, C)
+    ws = torch.empty(nb // 4 + 4, dtype=torch.float32, device="cuda")
+    dx1 = torch.full_like(xin, float("nan"))
+    dw = torch.full((K, C), float("nan"), device="cuda")
+    p1 = torch.full((rows1, 2, C), float("nan"), dtype=torch.float64, device="cuda")
+    bnb = (*(t.data_ptr() for t in pi), relu, p1.data_ptr()) if bn_in else (0,) * 6
+    rc = lib.dk_pwconv_bwd_bnbwd_f32(g.data_ptr(), xo.data_ptr(), N, H, W, K, *(t.data_ptr() for t in po), relu,
+                                     k12.data_ptr(), w.data_ptr(), C, l2, dw.data_ptr(), dx1.data_ptr(),
+                                     res.data_ptr() if resid else 0, xin.data_ptr(), *bnb, ws.data_ptr(), nb, st)
+    assert rc in (0, 10100)
+    torch.cuda.synchronize()
+    assert torch.equal(dx0, dx1)
+    if bn_in:
+        assert _close_sums(p0, p1)
+    dy64 = dy.permute(0, 2, 3, 1).reshape(M, K).double()
+    xf = xin.permute(0, 2, 3, 1).reshape(M, C)
+    if bn_in:
+        xh = (pi[2] * ((xf - pi[0]) * pi[1]) + pi[3]).double()
+        if relu:
+            xh = xh.clamp_min(0.0)
+    else:
+        xh = xf.double()
+    ref = dy64.t() @ xh + l2 * w.double()
+    bound = 3e-5 * (dy64.abs().t() @ xh.abs()) + 1e-6
+    assert bool(torch.isfinite(dw).all())
+    assert bool(((dw.double() - ref).abs() <= bound).all()), float(((dw.double() - ref).abs() / bound).max())
+
+
+def test_deep_fused_bwd_deterministic_and_in_bounds():
+    """The fused deep backward twice on the same inputs: dx and dW bitwise equal run to run (fixed-order
+    reductions, no atomics); a ragged pixel count writes nothing past dx (sentinel)."""
+    N, H, W, K, C = 3, 7, 5, 256, 256
+    M = N * H * W
+    rng = np.random.RandomState(5)
+    st = stream_handle()
+    xo, g = nhwc(rng.randn(N, K, H, W)), nhwc(rng.randn(N, K, H, W))
+    po = bn_params(K, rng)
+    k12 = torch.as_tensor(rng.randn(2 * K).astype(np.float32) * 0.1, device="cuda")
+    w = torch.as_tensor(rng.randn(K, C).astype(np.float32), device="cuda")
+    xin = nhwc(rng.randn(N, C, H, W))
+    pi = bn_params(C, rng)
+    nb = lib.dk_pwconv_bwd_fused_workspace_bytes(N, H, W, K, C)
+    rows = lib.dk_pwconv_bwd_fused_rows(N, H, W, K, C)
+    outs = []
+    for _ in range(2):
+        ws = torch.empty(nb // 4 + 4, dtype=torch.float32, device="cuda")
+        dxbuf = torch.full((M * C + 4096,), 12345.0, device="cuda")
+        dw = torch.empty((K, C), device="cuda")
+        part = torch.zeros((rows, 2, C), dtype=torch.float64, device="cuda")
+        rc = lib.dk_pwconv_bwd_bnbwd_f32(g.data_ptr(), xo.data_ptr(), N, H, W, K, *(t.data_ptr() for t in po), 1,
+                                         k12.data_ptr(), w.data_ptr(), C, 1e-4, dw.data_ptr(), dxbuf.data_ptr(), 0,
+                                         xin.data_ptr(), *(t.data_ptr() for t in pi), 1, part.data_ptr(),
+                                         ws.data_ptr(), nb, st)
+        assert rc in (0, 10100)
+        torch.cuda.synchronize()
+        assert bool((dxbuf[M * C:] == 12345.0).all()) and bool(torch.isfinite(dxbuf[:M * C]).all())
+        outs.append((dxbuf.clone(), dw.clone(), part.clone()))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    assert torch.equal(outs[0][2], outs[1][2])

@@ -126,14 +126,15 @@ def test_bf16_stream_dgrad_bnbwd_matches_tiled_engine(K, C, relu, bn_in, resid, 
         assert float((s1 - s0).norm() / s0.norm()) < 1e-12
 
 
-# The deep (column-sliced, k-chunked) kernels: K or C of 256 / 512 (config 5's 14 x 14 and 7 x 7 units).
+# The deep shapes: K or C of 256 / 512 (config 5's 14 x 14 and 7 x 7 units), on the weight-stationary
+# kernels of pw_deep_bf16.hip (the round-3 column-sliced kernels they superseded are deleted).
 DEEP = [(256, 128), (256, 256), (512, 256), (512, 512), (128, 256)]
 
 
-DEEP16_KNOB = 13  # 1: the weight-stationary kernels (pw_deep_bf16.hip, default); 0: the column-sliced ones
+DEEP16_KNOB = 13  # 1: the weight-stationary kernels (pw_deep_bf16.hip, default); 0: the tiled engine
 
 
-@pytest.fixture(params=[1, 0], ids=["weight_stationary", "column_sliced"])
+@pytest.fixture(params=[1], ids=["weight_stationary"])
 def deep16(request):
     lib.dk_debug_set_gemm_config(DEEP16_KNOB, request.param)
     yield request.param
