@@ -153,13 +153,29 @@ static inline int dw_fwd_seg(int OH) {
 // fused ReLU (batch_norm.py:125-174, dk_bn_bwd_partial_f64); xo is that BN's raw input.
 // T: activation storage (float, or bf16_t for BASELINE config 5); compute is fp32, and the
 // statistics see the stored (rounded) outputs.
-template <int R, int S, int ST, bool BN, bool RELU, int STATS, int WL, class T = float>
-__global__ __launch_bounds__(256) void dw_fwd_kernel(const T* __restrict__ x, uint32_t xbytes,
+// JOIN: the layer's input is a residual block's output y = ReLU(bnA(a) + bnB(b)) (residual_block.py:75,
+// the join dk_bn_add_f32 computes), formed here as the window rows are loaded -- x is a (the chain's
+// last BatchNorm's raw input), jf.b the skip operand -- and stored once (jf.y, and the ReLU mask
+// jf.mask): each thread stores the rows and columns of its window that no other thread's window
+// owns (its output columns' input columns, its segment's input rows), so the separate join pass and
+// this layer's re-read of y disappear.  Bit-identical to dk_bn_add_f32 (the same per-element
+// operations: bn_relu_out of each operand, one add, the (v > 0) ? v : 0 ReLU).  3 x 3, pad 1, fp32.
+struct JoinFwd {
+  const float* b;  // the skip operand (raw; a BatchNorm input when bb.mean)
+  BnIn ba, bb;     // the BatchNorms applied to a and b (mean == nullptr: none)
+  float* y;        // the join output, NHWC like a
+  uint8_t* mask;   // its ReLU mask (nullable)
+};
+
+template <int R, int S, int ST, bool BN, bool RELU, int STATS, int WL, class T = float, bool JOIN = false>
+__global__ __launch_bounds__(256, JOIN ? 2 : 1) void dw_fwd_kernel(const T* __restrict__ x, uint32_t xbytes,
                                                      const float* __restrict__ wt, const float* __restrict__ bias,
                                                      T* __restrict__ y, int N, int H, int W, int C, int OH, int OW,
                                                      int pad, BnIn bn, double* __restrict__ part,
                                                      const T* __restrict__ xo, BnIn obn,
-                                                     const T* __restrict__ res, FoldTail ft, int nt, int SEG) {
+                                                     const T* __restrict__ res, FoldTail ft, int nt, int SEG,
+                                                     JoinFwd jf) {
+  static_assert(!JOIN || (R == 3 && S == 3 && !BN && sizeof(T) == 4), "the join is formed for 3 x 3 fp32 layers");
   constexpr int TW = DwTile<ST>::TW;
   constexpr int NC = (TW - 1) * ST + S;
   const int C4 = C >> 2;
@@ -169,6 +185,20 @@ __global__ __launch_bounds__(256) void dw_fwd_kernel(const T* __restrict__ x, ui
   const long long idx = (long long)xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
   const long long total = (long long)N * nseg * nwc * C4;
   const bool live = idx < total;
+  // the join's BatchNorm terms per channel group, in LDS (in registers they cost the kernel its second
+  // wave per SIMD)
+  __shared__ f32x4 jtab[JOIN ? 8 : 1][JOIN ? 128 : 1];
+  if constexpr (JOIN) {
+    for (int i = threadIdx.x; i < 8 * (C >> 2); i += 256) {
+      const int t = i / (C >> 2), q = i - t * (C >> 2);
+      const BnIn& b = t < 4 ? jf.ba : jf.bb;
+      f32x4 v = {0.f, 0.f, 0.f, 0.f};
+      if (b.mean) v = ld4((t & 3) == 0 ? b.mean + 4 * q : (t & 3) == 1 ? b.invstd + 4 * q : (t & 3) == 2 ? b.gamma + 4 * q
+                                                                                                         : b.beta + 4 * q);
+      jtab[t][q] = v;
+    }
+    __syncthreads();
+  }
   if (STATS == 0 && !live) return;
   const int cq = (int)(idx % C4);
   const int c = cq * 4;
@@ -209,15 +239,63 @@ __global__ __launch_bounds__(256) void dw_fwd_kernel(const T* __restrict__ x, ui
     constexpr bool RING = ST == 1;
     constexpr int PER = RING ? R / std::gcd(R, ST) : 1;
     f32x4 win[R][NC];
+    // the join (JOIN): operand b's resource, both operands' BatchNorm terms, and the rows / columns
+    // of the window this thread stores y for (input rows oh0 ST .. oh1 ST - 1, columns q = 1 .. 4 ST)
+    const __amdgpu_buffer_rsrc_t rjb = make_rsrc_v(JOIN ? jf.b : nullptr, JOIN ? xbytes : 0u);
+    const int own_r0 = oh0 * ST, own_r1 = oh1 * ST;
+    // y = ReLU(bnA(a) + bnB(b)) for one window row from its raw operands; stored where this thread owns it
+    auto join_row = [&](f32x4 (&dst)[NC], const f32x4* ra, const f32x4* rb, int ih) __attribute__((always_inline)) {
+      const bool rv = (unsigned)ih < (unsigned)H;
+      const bool own = rv && ih >= own_r0 && ih < own_r1;
 #pragma unroll
-    for (int r = 0; r < R; ++r)
-      load_row<NC, BN, RELU, T>(win[r], rs, n, oh0 * ST - pad + r, iw0, H, W, C, c, bm, bi, bg, bb);
+      for (int q = 0; q < NC; ++q) {
+        const int iw = iw0 + q;
+        const bool ok = rv && (unsigned)iw < (unsigned)W;
+        f32x4 va = ra[q], vb = rb[q];
+        if (jf.ba.mean) va = bn_in4(va, jtab[0][cq], jtab[1][cq], jtab[2][cq], jtab[3][cq], jf.ba.relu);
+        if (jf.bb.mean) vb = bn_in4(vb, jtab[4][cq], jtab[5][cq], jtab[6][cq], jtab[7][cq], jf.bb.relu);
+        f32x4 v = va + vb;
+        uint32_t m = 0;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const bool pos = v[e] > 0.f;
+          v[e] = pos ? v[e] : 0.f;
+          m |= (uint32_t)pos << (8 * e);
+        }
+        dst[q] = ok ? v : f32x4{0.f, 0.f, 0.f, 0.f};
+        if (q >= 1 && q <= TW * ST && own && ok) {
+          const size_t e0 = ((size_t)(n * H + ih) * W + iw) * C + c;
+          st4(jf.y + e0, v);
+          if (jf.mask) *reinterpret_cast<uint32_t*>(jf.mask + e0) = m;
+        }
+      }
+    };
+    auto join_load = [&](f32x4 (&dst)[NC], int ih) __attribute__((always_inline)) {
+      f32x4 ra[NC], rb[NC];
+      const bool rv = (unsigned)ih < (unsigned)H;
+#pragma unroll
+      for (int q = 0; q < NC; ++q) {
+        const bool ok = rv && (unsigned)(iw0 + q) < (unsigned)W;
+        const uint32_t e = (uint32_t)(((n * H + ih) * W + iw0 + q) * C + c);
+        ra[q] = bload4e<float>(rs, ok, e);
+        rb[q] = bload4e<float>(rjb, ok, e);
+      }
+      join_row(dst, ra, rb, ih);
+    };
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      if constexpr (JOIN)
+        join_load(win[r], oh0 * ST - pad + r);
+      else
+        load_row<NC, BN, RELU, T>(win[r], rs, n, oh0 * ST - pad + r, iw0, H, W, C, c, bm, bi, bg, bb);
+    }
     // stride 1: the next output row's new input row is loaded one row ahead (bf16 kept packed, 2
     // registers per 4 channels) and widened / normalised when it enters the window; stride 2 loads
     // it in the row that uses it (its window leaves no registers for a prefetch)
     constexpr bool PFR = ST == 1 && R == 3;
     using PT = typename std::conditional<sizeof(T) == 2, uint2, f32x4>::type;
     PT pre[PFR ? NC : 1];
+    f32x4 preb[(PFR && JOIN) ? NC : 1];
     auto load_pre = [&](int ih) {
       if constexpr (PFR) {
         const bool rv = (unsigned)ih < (unsigned)H;
@@ -225,6 +303,7 @@ __global__ __launch_bounds__(256) void dw_fwd_kernel(const T* __restrict__ x, ui
         for (int q = 0; q < NC; ++q) {
           const bool ok = rv && (unsigned)(iw0 + q) < (unsigned)W;
           const uint32_t e = (uint32_t)(((n * H + ih) * W + iw0 + q) * C + c);
+          if constexpr (JOIN) preb[q] = bload4e<float>(rjb, ok, e);
           if constexpr (sizeof(T) == 2)
             pre[q] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rs, (int)(ok ? e * 2u : kOOBBytes),
                                                                                     0, 0));
@@ -263,7 +342,10 @@ __global__ __launch_bounds__(256) void dw_fwd_kernel(const T* __restrict__ x, ui
         for (int r = R - ST; r < R; ++r) {
           if (r < 0) continue;
           const int slot = RING ? (P * ST + r) % R : r;
-          if constexpr (PFR) {
+          if constexpr (PFR && JOIN) {
+            join_row(win[slot], pre, preb, oh * ST - pad + r);
+            if (oh + 1 < oh1) load_pre((oh + 1) * ST - pad + R - 1);
+          } else if constexpr (PFR) {
             // the prefetched row: widened, BN applied on the in-image elements (as load_row)
             const int ih = oh * ST - pad + r;
             const bool rv = (unsigned)ih < (unsigned)H;
@@ -282,6 +364,8 @@ __global__ __launch_bounds__(256) void dw_fwd_kernel(const T* __restrict__ x, ui
               win[slot][q] = v;
             }
             if (oh + 1 < oh1) load_pre((oh + 1) * ST - pad + R - 1);
+          } else if constexpr (JOIN) {
+            join_load(win[slot], oh * ST - pad + r);
           } else {
             load_row<NC, BN, RELU, T>(win[slot], rs, n, oh * ST - pad + r, iw0, H, W, C, c, bm, bi, bg, bb);
           }
@@ -1109,14 +1193,31 @@ static long long dw_fwd_threads(int N, int OH, int OW, int C) {
 template <int R, int S, int ST, class T>
 static int launch_dw_fwd(const T* x, const float* wt, const float* bias, T* y, int N, int H, int W, int C, int OH,
                          int OW, int pad, const BnIn& bn, double* part, const T* xo, const BnIn& obn, int wl,
-                         const T* res, hipStream_t st) {
+                         const T* res, hipStream_t st, const JoinFwd* jn = nullptr) {
   const uint32_t xb = (uint32_t)((size_t)N * H * W * C * sizeof(T));
   const dim3 grid((unsigned)cdivll(dw_fwd_threads<ST>(N, OH, OW, C), 256));
   FoldTail ft;  // an armed in-launch fold of the partial rows (fold_tail.h)
   if (!part || !fold_take(part, (int)grid.x, C, 1, &ft)) ft.part = nullptr;
+  const JoinFwd jf = jn ? *jn : JoinFwd{};
+  if constexpr (R == 3 && S == 3 && sizeof(T) == 4) {
+    if (jn) {
+      // the residual join formed on load (JOIN): reference-layout filters, no input BN
+      if (wl != 1 || bn.mean || xo || pad != 1) return DK_ERR_ARGS;
+      if (part)
+        hipLaunchKernelGGL((dw_fwd_kernel<R, S, ST, false, false, 1, 1, T, true>), grid, dim3(256), 0, st, x, xb, wt,
+                           bias, y, N, H, W, C, OH, OW, pad, bn, part, xo, obn, res, ft, nt_stores(kNtDwFwd),
+                           dw_fwd_seg(OH), jf);
+      else
+        hipLaunchKernelGGL((dw_fwd_kernel<R, S, ST, false, false, 0, 1, T, true>), grid, dim3(256), 0, st, x, xb, wt,
+                           bias, y, N, H, W, C, OH, OW, pad, bn, part, xo, obn, res, ft, nt_stores(kNtDwFwd),
+                           dw_fwd_seg(OH), jf);
+      return fold_status(launch_status(), ft);
+    }
+  }
+  if (jn) return DK_ERR_ARGS;
 #define DW_LAUNCH1(B, RL, ST_, WL_)                                                                                  \
   hipLaunchKernelGGL((dw_fwd_kernel<R, S, ST, B, RL, ST_, WL_, T>), grid, dim3(256), 0, st, x, xb, wt, bias, y, N, H, \
-                     W, C, OH, OW, pad, bn, part, xo, obn, res, ft, nt_stores(kNtDwFwd), dw_fwd_seg(OH))
+                     W, C, OH, OW, pad, bn, part, xo, obn, res, ft, nt_stores(kNtDwFwd), dw_fwd_seg(OH), jf)
 #define DW_LAUNCH(B, ST_, WL_)            \
   do {                                    \
     if (B && bn.relu)                     \
@@ -1152,14 +1253,14 @@ template <class T>
 static int dw_fwd_dispatch(const T* x, const float* wt, const float* bias, T* y, int N, int H, int W, int C, int R,
                            int S, int stride, int OH, int OW, int pad, const BnIn& bn, hipStream_t st,
                            double* part = nullptr, const T* xo = nullptr, const BnIn& obn = BnIn{}, int wl = 0,
-                           const T* res = nullptr) {
+                           const T* res = nullptr, const JoinFwd* jn = nullptr) {
   if (res && (!aligned16(res) || wl != 2)) return DK_ERR_ARGS;  // residual addend: dgrad only
   if (C % 4 || !aligned16(x) || !aligned16(wt) || !fits((size_t)N * H * W * C * 4) || !bn_ok(bn)) return DK_ERR_ARGS;
   if (part && (C / 4 > 256 || 256 % (C / 4))) return DK_ERR_ARGS;
   if (xo && (bn.mean || !obn.mean || !aligned16(xo) || !bn_ok(obn))) return DK_ERR_ARGS;
 #define DW_CASE(RR, SS, STR)                                                                     \
   if (R == RR && S == SS && stride == STR)                                                           \
-    return launch_dw_fwd<RR, SS, STR, T>(x, wt, bias, y, N, H, W, C, OH, OW, pad, bn, part, xo, obn, wl, res, st);
+    return launch_dw_fwd<RR, SS, STR, T>(x, wt, bias, y, N, H, W, C, OH, OW, pad, bn, part, xo, obn, wl, res, st, jn);
   DW_CASE(3, 3, 1)
   DW_CASE(3, 3, 2)
   DW_CASE(5, 5, 1)
@@ -1217,6 +1318,24 @@ DK_API int dk_dwconv_fwd_ex_f32(const float* x, int N, int H, int W, int C, cons
   return dw_fwd_dispatch<float>(x, w_crs, bias, y, N, H, W, C, R, S, stride, OH, OW, pad,
                          BnIn{bn_mean, bn_invstd, bn_gamma, bn_beta, bn_relu}, as_stream(stream), stats, nullptr,
                          BnIn{}, 1);
+}
+
+// The layer's input is the residual join y = ReLU(bnA(a) + bnB(b)) (dk_bn_add_f32's operands), formed
+// as the window is loaded and stored once into y_join (+ its ReLU mask, nullable); the rest as
+// dk_dwconv_fwd_ex_f32 without an input BatchNorm.  3 x 3 filters, pad 1, stride 1 or 2.
+DK_API int dk_dwconv_fwd_join_f32(const float* a, const float* a_mean, const float* a_invstd, const float* a_gamma,
+                                  const float* a_beta, int a_relu, const float* b, const float* b_mean,
+                                  const float* b_invstd, const float* b_gamma, const float* b_beta, int b_relu,
+                                  float* y_join, uint8_t* mask, int N, int H, int W, int C, const float* w_crs,
+                                  int stride, const float* bias, float* y, int OH, int OW, double* stats,
+                                  void* stream) {
+  if (stride != 1 && stride != 2) return DK_ERR_ARGS;
+  const JoinFwd jf{b, BnIn{a_mean, a_invstd, a_gamma, a_beta, a_relu}, BnIn{b_mean, b_invstd, b_gamma, b_beta, b_relu},
+                   y_join, mask};
+  if (!b || !y_join || !aligned16(b) || !aligned16(y_join) || !bn_ok(jf.ba) || !bn_ok(jf.bb) || C > 512) return DK_ERR_ARGS;
+  if (mask && (reinterpret_cast<uintptr_t>(mask) & 3)) return DK_ERR_ARGS;
+  return dw_fwd_dispatch<float>(a, w_crs, bias, y, N, H, W, C, 3, 3, stride, OH, OW, 1, BnIn{}, as_stream(stream),
+                                stats, nullptr, BnIn{}, 1, nullptr, &jf);
 }
 
 // w_rsc is the (unflipped) [R][S][C] copy; stride-1 dgrad flips it internally into ws.

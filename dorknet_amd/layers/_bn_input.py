@@ -98,6 +98,74 @@ class BNOut:
         return self._y
 
 
+class JoinOut:
+    """A residual block's output y = ReLU(bnA(a) + bnB(b)) (residual_block.py:75) not yet written.
+
+    The join pass (dk_bn_add_f32) writes y and the next block's first depthwise layer reads it back
+    at once.  When that layer can take it (DepthwiseConvLayer.takes_join_input), the block hands over
+    this record instead: the layer forms y as it loads its input window and stores it once
+    (dk_dwconv_fwd_join_f32, bit-identical to the join pass), so y is written but not re-read.  `y`
+    and `mask` are allocated here; ``materialize()`` runs the join pass for any other consumer.
+    The closing ReLu's backward state is set when y is written (ReLu._join_written), the same state
+    the join pass leaves."""
+    __slots__ = ("A", "B", "relu_layer", "test_mode", "y", "mask", "written")
+
+    def __init__(self, A, B, relu_layer, test_mode, need_mask=True):
+        """need_mask: also store the join's ReLU mask (uint8).  A stride-1 consumer's fused backward
+        takes the mask as y > 0 (DepthwiseConvLayer._join_ok, from_y) and does not need it."""
+        self.A = A            # BNOut or NHWC tensor (the chain's output)
+        self.B = B            # BNOut or NHWC tensor (the skip operand)
+        self.relu_layer = relu_layer
+        self.test_mode = test_mode
+        x = A.x if isinstance(A, BNOut) else A
+        self.y = empty_nhwc(*x.shape)
+        self.mask = None if (test_mode or not need_mask) else torch.empty(
+            x.shape, dtype=torch.uint8, device=x.device, memory_format=torch.channels_last)
+        self.written = False
+
+    @property
+    def shape(self):
+        return self.y.shape
+
+    def dim(self):
+        return self.y.dim()
+
+    @property
+    def device(self):
+        return self.y.device
+
+    @property
+    def dtype(self):
+        return self.y.dtype
+
+    @staticmethod
+    def _operand(T):
+        if isinstance(T, BNOut):
+            return (T.x.data_ptr(), *T.bn_args())
+        return (T.data_ptr(), 0, 0, 0, 0, 0)
+
+    def join_args(self):
+        """(a, a_mean, a_invstd, a_gamma, a_beta, a_relu, b, b_mean, ..., b_relu, y, mask) for
+        dk_dwconv_fwd_join_f32 / dk_bn_add_f32."""
+        return (*self._operand(self.A), *self._operand(self.B), self.y.data_ptr(),
+                0 if self.mask is None else self.mask.data_ptr())
+
+    def mark_written(self):
+        self.written = True
+        self.relu_layer._join_written(self)
+
+    def materialize(self):
+        """y itself: the join pass (dk_bn_add_f32) unless a consumer already wrote it."""
+        if not self.written:
+            a = self._operand(self.A)
+            b = self._operand(self.B)
+            y = self.y
+            lib.dk_bn_add_f32(*a, *b, y.numel(), y.shape[1], 1, y.data_ptr(),
+                              0 if self.mask is None else self.mask.data_ptr(), stream_handle())
+            self.mark_written()
+        return self.y
+
+
 class BNGrad:
     """The gradient w.r.t. a BatchNormLayer's input with its last stage (the per-element
     apply, dk_bn_bwd_apply_f32) left to the producer of that input.
@@ -199,7 +267,7 @@ def accepts_bn_grad(layer, bn_layer) -> bool:
 
 
 def materialize(X):
-    return X.materialize() if isinstance(X, (BNOut, BNGrad)) else X
+    return X.materialize() if isinstance(X, (BNOut, BNGrad, JoinOut)) else X
 
 
 def accepts_bn_input(layer) -> bool:

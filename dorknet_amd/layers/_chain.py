@@ -124,7 +124,9 @@ class StatsRequest:
             self.armed = None
 
 
-def run_group(group, mode, X, test_mode=False, stats_req=None, bn_stats=None):
+def run_group(group, mode, X, test_mode=False, stats_req=None, bn_stats=None, join_out=False):
+    if join_out:
+        return group[0].forward(X, test_mode=test_mode, join_out=True)
     if mode == "defer":
         return group[0].forward_deferred(X, group[1] if len(group) == 2 else None, test_mode=test_mode,
                                          stats=bn_stats)
@@ -153,8 +155,13 @@ def execute(layers, X, test_mode=False, out_accepts=False, keep=(), visit=None):
         if (fuse and not test_mode and mode == "single" and getattr(group[0], "produces_bn_stats", False)
                 and nxt < len(layers) and type(layers[nxt]) is BatchNormLayer):
             req = StatsRequest(layers[nxt])
+        # a residual block whose output the next block forms on load (JoinOut, layers/_bn_input.py)
+        join_out = (fuse and mode == "single" and req is None and pending is None
+                    and getattr(group[0], "produces_join", False) and nxt < len(layers)
+                    and group[0].layer_name not in keep
+                    and getattr(layers[nxt], "takes_join_input", None) is not None and layers[nxt].takes_join_input())
         try:
-            X = run_group(group, mode, X, test_mode, stats_req=req, bn_stats=pending)
+            X = run_group(group, mode, X, test_mode, stats_req=req, bn_stats=pending, join_out=join_out)
         except BaseException:
             disarm_folds()  # an arming the failed group left behind must not outlive it
             raise
@@ -179,7 +186,9 @@ def _join_of(step):
     if len(step) != 1 or not enabled("DORKNET_FUSE_JOIN"):
         return None
     act = getattr(step[0], "post_skip_activation", None)
-    if act is None or getattr(act, "_join_bn", None) is None or getattr(act, "_mask", None) is None:
+    if act is None or getattr(act, "_join_bn", None) is None:
+        return None
+    if getattr(act, "_mask", None) is None and getattr(act, "_join_y", None) is None:
         return None
     return act
 

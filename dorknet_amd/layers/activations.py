@@ -12,7 +12,7 @@ import torch
 
 from .._hip import lib, stream_handle
 from .._tensor import act_dtype, as_device, empty_nhwc, is_nhwc as is_nhwc_t, rows, to_nhwc
-from ._bn_input import BNOut
+from ._bn_input import BNOut, JoinOut
 from .layer import Layer
 
 
@@ -30,6 +30,7 @@ class ReLu(Layer):
         self._join_bn = None
         self._join_done = False
         self._join_y_ptr = None  # data_ptr of the fused join's output (_bn_add)
+        self._join_y = None      # that output, when the join left no mask (JoinOut without one)
 
     def join_backward_done(self):
         """The consumer of this residual join's output applied this ReLU's backward (and stage 1
@@ -57,13 +58,22 @@ class ReLu(Layer):
         if not test_mode:
             self._mask, self._fused_out, self._join_bn = mask, None, None
             self._join_done = False
+            self._join_y = None
         return y
 
-    def forward_add(self, A, B, test_mode=False):
+    def forward_add(self, A, B, test_mode=False, defer=False, need_mask=True):
         """ReLU(A + B) in one pass -- the residual join (residual_block.py:75).  A and/or B may
-        be a BatchNorm output not yet written (BNOut): the normalisation is applied on load."""
+        be a BatchNorm output not yet written (BNOut): the normalisation is applied on load.
+        defer: the consumer of the result can form it on load (ResidualBlock.takes_join_input):
+        return a JoinOut (layers/_bn_input.py) instead of running the join pass."""
         self._require_on_gpu()
         st = stream_handle()
+        if isinstance(A, JoinOut):
+            A = A.materialize()
+        if isinstance(B, JoinOut):
+            B = B.materialize()
+        if defer and (isinstance(A, BNOut) or isinstance(B, BNOut)) and self._join_parts_ok(A, B):
+            return JoinOut(A, B, self, test_mode, need_mask)
         if isinstance(A, BNOut) or isinstance(B, BNOut):
             y = self._bn_add(A, B, test_mode, st)
             if y is not None:
@@ -80,7 +90,25 @@ class ReLu(Layer):
                        0 if mask is None else mask.data_ptr(), st)
         if not test_mode:
             self._mask, self._fused_out, self._join_bn = mask, None, None
+            self._join_y = None
         return y
+
+    @staticmethod
+    def _join_parts_ok(A, B):
+        if A.dim() != 4 or tuple(A.shape) != tuple(B.shape) or A.shape[1] % 4 or A.dtype != torch.float32:
+            return False
+        xs = [T.x if isinstance(T, BNOut) else T for T in (A, B)]
+        return all(isinstance(x, torch.Tensor) and x.dtype == torch.float32 and is_nhwc_t(x) for x in xs)
+
+    def _join_written(self, jo):
+        """The join output of a JoinOut was written (by its consumer, or by its materialize):
+        the backward state the join pass leaves (_bn_add)."""
+        if not jo.test_mode:
+            self._mask, self._fused_out = jo.mask, None
+            self._join_bn = jo.A if isinstance(jo.A, BNOut) else None
+            self._join_done = False
+            self._join_y_ptr = jo.y.data_ptr()
+            self._join_y = jo.y if jo.mask is None else None
 
     def _bn_add(self, A, B, test_mode, st):
         def parts(T):
@@ -103,15 +131,29 @@ class ReLu(Layer):
             self._join_bn = A if isinstance(A, BNOut) else None
             self._join_done = False
             self._join_y_ptr = y.data_ptr()  # a consumer holding y itself may take the mask as y > 0
+            self._join_y = None
         return y
 
     def _attach_fused(self, y, test_mode):
         if not test_mode:
             self._mask, self._fused_out, self._join_bn = None, y, None
+            self._join_y = None
+
+    def _mask_from_join(self):
+        """The join's ReLU mask from its stored output (y > 0), for a backward that needs the mask
+        when the join left none (a JoinOut whose consumer takes it as y > 0)."""
+        y = self._join_y
+        mask = torch.empty(y.shape, dtype=torch.uint8, device=y.device, memory_format=torch.channels_last)
+        tmp = self._empty_like(y)
+        lib.dk_relu_fwd_f32(y.data_ptr(), y.numel(), tmp.data_ptr(), mask.data_ptr(), stream_handle())
+        self._mask, self._join_y = mask, None
+        return mask
 
     @property
     def positive_locs(self):
         """fp32 mask (out > 0), as the reference's attribute (activations.py:42)."""
+        if self._mask is None and self._join_y is not None:
+            self._mask_from_join()
         if self._mask is not None:
             out = torch.empty(self._mask.shape, dtype=torch.float32, device=self._mask.device,
                               memory_format=torch.channels_last if self._mask.dim() == 4 else torch.contiguous_format)
@@ -133,6 +175,8 @@ class ReLu(Layer):
         if self._join_done:
             self._join_done = False
             return upstream_dx
+        if self._mask is None and self._join_y is not None:
+            self._mask_from_join()
         if self._mask is None:
             raise RuntimeError("ReLu {}: backward without a training-mode forward (or the layer ran fused with "
                                "the preceding BatchNormLayer; its backward is BatchNormLayer.backward_bn_relu)"

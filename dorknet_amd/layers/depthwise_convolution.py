@@ -17,7 +17,7 @@ import torch
 from .._env import getenv
 from .._hip import HipError, deferred_wgrad_reduce, lib, stream_handle, weight_grad_stream, workspace
 from .._tensor import BF16, empty_nhwc, ptr, to_nhwc
-from ._bn_input import BNGrad, BNOut, add_residual, dense_residual, lattice_operand, residual_operand
+from ._bn_input import BNGrad, BNOut, JoinOut, add_residual, dense_residual, lattice_operand, residual_operand
 from ._common import add_regulariser_grad, grad_buffer, init_weights, l2_strength
 from .layer import Layer
 
@@ -67,9 +67,23 @@ class DepthwiseConvLayer(Layer):
     accepts_bn_input = True   # forward(BNOut): the preceding BatchNorm is applied on load
     produces_bn_stats = True  # forward(..., bn_stats=StatsRequest): emits the next BN's statistics
 
+    def join_geometry_ok(self):
+        """forward(JoinOut) can form the residual join on load (dk_dwconv_fwd_join_f32): 3 x 3, pad
+        1, stride 1 or 2, no bias (the shapes and dtype are checked at the call)."""
+        return (self.num_filters is not None and self.f_rows == 3 and self.f_cols == 3 and self.padding == 1
+                and self.stride in (1, 2) and not self.with_bias)
+
+    def _takes_join(self, X):
+        return (self.join_geometry_ok() and X.dim() == 4 and X.dtype == torch.float32
+                and X.shape[1] == self.num_filters and X.shape[1] % 4 == 0 and X.shape[1] <= 512)
+
     def forward(self, X, test_mode=False, bn_stats=None):
         self._require_on_gpu()
         st = stream_handle()
+        if isinstance(X, JoinOut):
+            if not X.written and self._takes_join(X):
+                return self._forward_join(X, test_mode, bn_stats, st)
+            X = X.materialize()
         bn = X if isinstance(X, BNOut) and X.dim() == 4 and X.shape[1] % 4 == 0 else None
         x = bn.x if bn is not None else to_nhwc(X)
         N, C, H, W = x.shape
@@ -101,6 +115,33 @@ class DepthwiseConvLayer(Layer):
             self._bn_in = bn
         return y
 
+    def _forward_join(self, J, test_mode, bn_stats, st):
+        """forward on a residual block's output not yet written (JoinOut): the join is formed as the
+        input window is loaded and stored once (dk_dwconv_fwd_join_f32); the layer then holds y as
+        its input, exactly as after the join pass."""
+        N, C, H, W = J.shape
+        R, S = self.f_rows, self.f_cols
+        self.num_row_patches = ((H + 2 * self.padding - R) / self.stride) + 1
+        self.num_col_patches = ((W + 2 * self.padding - S) / self.stride) + 1
+        OH, OW = int(self.num_row_patches), int(self.num_col_patches)
+        y = empty_nhwc(N, C, OH, OW)
+        stats = None
+        if bn_stats is not None and not test_mode:
+            rows = lib.dk_dwconv_fwd_stats_rows(N, OH, OW, C, self.stride)
+            if rows:
+                stats = torch.empty((rows, 2, C), dtype=torch.float64, device=J.device)
+        if stats is not None:
+            bn_stats.arm(stats, N * OH * OW)
+        r = lib.dk_dwconv_fwd_join_f32(*J.join_args(), N, H, W, C, self.learned_params["weights"].data_ptr(),
+                                       self.stride, 0, y.data_ptr(), OH, OW, ptr(stats), st)
+        if stats is not None:
+            bn_stats.launched(stats, r)
+        J.mark_written()
+        if not test_mode:
+            self.X = J.y
+            self._bn_in = None
+        return y
+
     accepts_residual = True  # backward(dy, residual=R) returns dx + R (the residual join, fused)
 
     skips_input_grad = True  # backward(dy, need_dx=False): parameter gradients only (chain_backward)
@@ -129,10 +170,14 @@ class DepthwiseConvLayer(Layer):
         x = self.X
         jb = getattr(join, "_join_bn", None)
         mask = getattr(join, "_mask", None)
-        return (need_dx and self._bn_in is None and jb is not None and mask is not None
-                and tuple(mask.shape) == tuple(x.shape) and tuple(jb.x.shape) == tuple(x.shape)
-                and jb.x.dtype == torch.float32 and mask.is_contiguous(memory_format=torch.channels_last)
-                and jb.x.is_contiguous(memory_format=torch.channels_last))
+        if not (need_dx and self._bn_in is None and jb is not None and tuple(jb.x.shape) == tuple(x.shape)
+                and jb.x.dtype == torch.float32 and jb.x.is_contiguous(memory_format=torch.channels_last)):
+            return False
+        if mask is None:
+            # a join that left no mask (JoinOut): only the stride-1 form, which takes it as x > 0
+            return (self.stride == 1 and getattr(join, "_join_y", None) is not None
+                    and getattr(join, "_join_y_ptr", None) == x.data_ptr())
+        return tuple(mask.shape) == tuple(x.shape) and mask.is_contiguous(memory_format=torch.channels_last)
 
     def takes_lattice_residual(self, join, s):
         """backward(dy, residual=R, join=relu) adds R given as the compact stride-s lattice (a
@@ -174,6 +219,8 @@ class DepthwiseConvLayer(Layer):
             # x IS the join's output: the kernel takes the mask as x > 0 instead of reading it
             # (DORKNET_JOIN_MASK=1 reads the stored mask)
             from_y = getattr(join, "_join_y_ptr", None) == x.data_ptr() and getenv("DORKNET_JOIN_MASK") != "1"
+            if not from_y and join._mask is None:
+                join._mask_from_join()
             tok = jb.arm_partials(part)
             # the weight-gradient reduce on the side stream (not with a non-l2 regulariser, whose
             # term is added to gw on this stream right after)

@@ -11,10 +11,10 @@ gets the l2 term in its own backward; and SGDMomentum never updates the skip pro
 from __future__ import annotations
 
 
-from .._env import getenv
+from .._env import enabled, getenv
 from .._hip import branch_stream_enabled, lib, on_branch, resolve, stream_handle
 from .._tensor import empty_nhwc, to_nhwc
-from ._bn_input import accepts_bn_input, materialize
+from ._bn_input import JoinOut, accepts_bn_input, materialize
 from ._chain import chain_backward, chain_forward, fusion_enabled, notify_backward_done
 from .activations import ReLu
 from .batch_norm import BatchNormLayer
@@ -70,10 +70,24 @@ class ResidualBlock(Layer):
     # the skip projection and the join); the chain's last BatchNorm is applied by the join.
     accepts_bn_input = True
 
-    def forward(self, X, test_mode=False):
+    produces_join = True  # forward(..., join_out=True) may return its output as a JoinOut
+
+    def takes_join_input(self):
+        """forward(JoinOut): the previous block's join is formed by this block's first layer as it
+        loads its input (DepthwiseConvLayer._forward_join) -- an identity skip (the skip operand is
+        then that written y), a depthwise first layer of the right geometry, fusion on."""
+        first = self.layer_list[0] if self.layer_list else None
+        return (self.skip_projection is None and isinstance(first, DepthwiseConvLayer) and first.join_geometry_ok()
+                and fusion_enabled() and getenv("DORKNET_FUSE_JOIN_FWD") != "0")
+
+    def forward(self, X, test_mode=False, join_out=False):
+        """join_out: the next layer takes its input as a JoinOut (takes_join_input): the join is
+        handed over unwritten instead of running the join pass."""
         post = self.post_skip_activation
         join_fused = type(post) is ReLu
         skip = self.skip_projection
+        if isinstance(X, JoinOut) and not self.takes_join_input():
+            X = X.materialize()
         branch = skip is not None and branch_stream_enabled()
         if branch:
             # the skip projection on the branch stream, beside the chain; joined at the join
@@ -88,7 +102,10 @@ class ResidualBlock(Layer):
         else:
             skippee = X
         if join_fused:
-            return post.forward_add(X_tmp, skippee, test_mode=test_mode)
+            # a JoinOut consumer (takes_join_input: a stride-1 depthwise layer) takes the join's mask
+            # in its fused backward as y > 0; the mask is stored only when that fusion is off
+            need_mask = not (enabled("DORKNET_FUSE_JOIN") and getenv("DORKNET_JOIN_MASK") != "1")
+            return post.forward_add(X_tmp, skippee, test_mode=test_mode, defer=join_out, need_mask=need_mask)
         return post.forward(_add(materialize(X_tmp), materialize(skippee)), test_mode=test_mode)
 
     def regulariser_forward(self):

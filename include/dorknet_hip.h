@@ -177,6 +177,13 @@ int dk_pwconv_fwd_stats_rows(int N, int OH, int OW, int K, int C);
 int dk_pwconv_fwd_ex_f32(const float* x, int N, int H, int W, int C, const float* w_kc, int K, int stride, const float* bias, float* y, int OH, int OW, const float* bn_mean, const float* bn_invstd, const float* bn_gamma, const float* bn_beta, int bn_relu, double* stats, void* stream);
 int dk_dwconv_fwd_stats_rows(int N, int OH, int OW, int C, int stride);
 int dk_dwconv_fwd_ex_f32(const float* x, int N, int H, int W, int C, const float* w_crs, int R, int S, int stride, int pad, const float* bias, float* y, int OH, int OW, const float* bn_mean, const float* bn_invstd, const float* bn_gamma, const float* bn_beta, int bn_relu, double* stats, void* stream);
+/* Depthwise forward whose input is a residual block's output y = ReLU(bnA(a) + bnB(b))
+ * (residual_block.py:75; the operands of dk_bn_add_f32, bnX = identity when its mean is NULL): the
+ * join is formed as the window rows are loaded and stored once into y_join (+ its ReLU mask, uint8,
+ * nullable) -- bit-identical to dk_bn_add_f32 -- and the depthwise output / statistics are those of
+ * dk_dwconv_fwd_ex_f32 on y_join.  3 x 3, pad 1, stride 1 or 2, fp32, C % 4 == 0.  Replaces the
+ * separate join pass + this layer's re-read of its output. */
+int dk_dwconv_fwd_join_f32(const float* a, const float* a_mean, const float* a_invstd, const float* a_gamma, const float* a_beta, int a_relu, const float* b, const float* b_mean, const float* b_invstd, const float* b_gamma, const float* b_beta, int b_relu, float* y_join, uint8_t* mask, int N, int H, int W, int C, const float* w_crs, int stride, const float* bias, float* y, int OH, int OW, double* stats, void* stream);
 /* Backward side: *_dgrad_ex_f32 = the input gradient plus stage 1 of the backward of the
  * BatchNorm whose output this layer consumed (the BN-on-load input of its forward): with
  * g = dx masked by that BN's fused ReLU (recomputed from bn_x, the BN's raw input, laid out

@@ -104,5 +104,9 @@ def test_network_step_with_fused_pw_backward(monkeypatch):
 
 
 def test_pointwise_bwd_fused_rejects_other_shapes():
-    assert lib.dk_pwconv_bwd_fused_rows(2, 7, 7, 256, 256) == 0
+    # K = 512 (beyond the fused deep kernel's K in {128, 256}) and channel counts no kernel takes
+    assert lib.dk_pwconv_bwd_fused_rows(2, 7, 7, 512, 512) == 0
     assert lib.dk_pwconv_bwd_fused_rows(2, 7, 7, 64, 48) == 0
+    assert lib.dk_pwconv_bwd_fused_rows(2, 7, 7, 256, 64) == 0
+    # K = C = 256: the fused deep kernel (pw_deep.hip bwd_kernel)
+    assert lib.dk_pwconv_bwd_fused_rows(2, 7, 7, 256, 256) > 0
