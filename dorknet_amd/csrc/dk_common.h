@@ -255,7 +255,7 @@ enum KnobId : int {
   kKnobRowCfg = 0, kKnobSplitCfg = 1, kKnobFillSplits = 2, kKnobPwStream = 3, kKnobNtStores = 4, kKnobPwsBwdPf = 5,
   kKnobDwbBlocks = 7, kKnobDwSeg = 8, kKnobPwsh = 9, kKnobPwDeep = 11, kKnobPwDeep16 = 13, kKnobPwDeepBwd = 14,
   kKnobPwStream128 = 15, kKnobPwfPrefetch = 16, kKnobPwfBlocksPerCu = 17, kKnobWgradBlocks = 18, kKnobEwVariant = 19,
-  kNumKnobs = 20
+  kKnobPwsh16Bwd = 20, kNumKnobs = 21
 };
 int knob(int id);
 void knob_set(int id, int v);
@@ -346,6 +346,14 @@ int pw_stream_bf16_dgrad_bnbwd(const bf16_t* g, const bf16_t* bn_x, int M, int K
                                const float* im, const float* iis, const float* ig, const float* ib, int irelu,
                                double* part, hipStream_t st, const struct FoldTail* ft = nullptr);
 int pw_stream_bf16_fwd_slices(int K, int C);    // channel slices of the partial rows (fold_take)
+// the fused bf16 backward (dgrad + weight gradient, dy never stored) for K = C = 64
+bool pw_stream_bf16_bwd_ok(int K, int C, int M);
+int pw_stream_bf16_bwd_rows(int M);
+int pw_stream_bf16_bwd_fused(const bf16_t* g, const bf16_t* bn_x, int M, const float* om, const float* ois,
+                             const float* og, const float* ob, int orelu, const float* k12, const float* w, bf16_t* dx,
+                             const bf16_t* res, const bf16_t* x, const float* im, const float* iis, const float* ig,
+                             const float* ib, int irelu, double* part, float* wpart, hipStream_t st,
+                             const struct FoldTail* ft = nullptr);
 int pw_stream_bf16_dgrad_slices(int K, int C);
 
 }  // namespace dk

@@ -185,3 +185,47 @@ DK_API int dk_pwconv_dgrad_bnbwd_bf16(const bf16_t* g, const bf16_t* bn_x, int N
   return igemm_rows<LdMatKC, MatBwdDescE<bf16_t>, LdMatIC, MatDesc, EpStoreBnBwdT<bf16_t>, kRowBnBwd, kMfBf16>(
       a, b, ep, M, C, K, st);
 }
+
+// Fused pointwise backward for bf16 storage (dk_pwconv_bwd_bnbwd_f32's bf16 twin): the dgrad of
+// dk_pwconv_dgrad_bnbwd_bf16 (dy formed on load from (g, bn_x), rounded to bf16 as the MFMA operand,
+// dx bit-identical) and the weight gradient dW = dy^T bn_relu(x) (+ l2 w) in one pass, dy never
+// stored.  K = C = 64, stride 1 (pw_stream_bf16.hip bwd_fused_kernel); rows = partial rows of part,
+// the workspace holds rows fp32 [K][C] weight-gradient partial rows.
+DK_API int dk_pwconv_bwd_fused_bf16_rows(int N, int OH, int OW, int K, int C) {
+  if (N < 1 || OH < 1 || OW < 1 || (long long)N * OH * OW >= (1ll << 31)) return 0;
+  const int M = N * OH * OW;
+  return pw_stream_bf16_bwd_ok(K, C, M) ? pw_stream_bf16_bwd_rows(M) : 0;
+}
+
+DK_API size_t dk_pwconv_bwd_fused_bf16_workspace_bytes(int N, int OH, int OW, int K, int C) {
+  return (size_t)dk_pwconv_bwd_fused_bf16_rows(N, OH, OW, K, C) * K * C * sizeof(float);
+}
+
+DK_API int dk_pwconv_bwd_bnbwd_bf16(const bf16_t* g, const bf16_t* bn_x, int N, int OH, int OW, int K,
+                                    const float* out_mean, const float* out_invstd, const float* out_gamma,
+                                    const float* out_beta, int out_relu, const float* k12, const float* w_kc, int C,
+                                    float l2, float* dw_kc, bf16_t* dx, const bf16_t* residual, const bf16_t* x,
+                                    const float* bn_mean, const float* bn_invstd, const float* bn_gamma,
+                                    const float* bn_beta, int bn_relu, double* part, void* ws, size_t ws_bytes,
+                                    void* stream) {
+  const hipStream_t st = as_stream(stream);
+  const int rows = dk_pwconv_bwd_fused_bf16_rows(N, OH, OW, K, C);
+  if (rows <= 0) return DK_ERR_ARGS;
+  if (!g || !bn_x || !x || !w_kc || !dw_kc || !dx || !out_mean || !out_invstd || !out_gamma || !out_beta || !k12)
+    return DK_ERR_ARGS;
+  if (part && !bn_mean) return DK_ERR_ARGS;
+  if (bn_mean && !bn_ok(bn_mean, bn_invstd, bn_gamma, bn_beta)) return DK_ERR_ARGS;
+  if (!aligned16(g) || !aligned16(bn_x) || !aligned16(w_kc) || !aligned16(ws) || !al8(x) || !al8(dx) ||
+      (residual && !al8(residual)))
+    return DK_ERR_ARGS;
+  if (ws_bytes < (size_t)rows * K * C * sizeof(float)) return DK_ERR_WORKSPACE;
+  const int M = N * OH * OW;
+  float* wp = static_cast<float*>(ws);
+  FoldTail ft;
+  if (part) fold_take(part, rows, C, 1, &ft);
+  int rc = pw_stream_bf16_bwd_fused(g, bn_x, M, out_mean, out_invstd, out_gamma, out_beta, out_relu, k12, w_kc, dx,
+                                    residual, x, bn_mean, bn_invstd, bn_gamma, bn_beta, bn_relu, part, wp, st,
+                                    part ? &ft : nullptr);
+  if (rc) return rc;
+  return fold_status(wgrad_reduce(wp, rows, K, C, dw_kc, l2 != 0.f ? w_kc : nullptr, l2, st), part ? ft : FoldTail{});
+}

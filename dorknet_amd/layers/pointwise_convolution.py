@@ -240,24 +240,32 @@ class PointwiseConvLayer(Layer):
         return dx
 
     def _fused_bwd_ok(self, bg, residual):
-        """dk_pwconv_bwd_bnbwd_f32 applies: fp32, stride 1, no bias, K and C in {64, 128}, a
-        residual (if any) that fuses; taken by default where the library prefers it (K = C = 64:
-        the streaming kernel of pw_stream.hip, which never stores dy), DORKNET_PW_FUSED_BWD=1 / 0
-        forces it on / off.  The round-1 tiled fused kernel (K or C = 128) was measured 0.75 %
-        slower on the step than the unfused pair, so it is not the default."""
+        """dk_pwconv_bwd_bnbwd_f32 / _bf16 applies: stride 1, no bias, a residual (if any) that
+        fuses, and a shape a fused kernel takes -- fp32: K = C = 64 (the streaming kernel of
+        pw_stream.hip, which never stores dy) and K in {128, 256} (the weight-stationary kernel of
+        pw_deep.hip), taken by default where the library prefers it; bf16 (config 5): K = C = 64
+        (pw_stream_bf16.hip).  DORKNET_PW_FUSED_BWD=1 / 0 forces the fp32 path on / off (its round-1
+        tiled kernel for K or C = 128 measured 0.75 % slower than the unfused pair, DESIGN.md
+        section 5)."""
         x = self.X
-        if self.with_bias or x.dtype != torch.float32 or not self._takes_bn_grad(bg.x):
+        if self.with_bias or not self._takes_bn_grad(bg.x):
             return False
         N, C, H, W = x.shape
         OH, OW = self.out_hw
-        if lib.dk_pwconv_bwd_fused_rows(N, OH, OW, self.num_filters, C) <= 0:
-            return False
-        env = getenv("DORKNET_PW_FUSED_BWD")
-        if env is not None:
-            if env != "1":
+        if x.dtype == BF16:
+            if lib.dk_pwconv_bwd_fused_bf16_rows(N, OH, OW, self.num_filters, C) <= 0:
                 return False
-        elif not lib.dk_pwconv_bwd_fused_preferred(N, OH, OW, self.num_filters, C):
+        elif x.dtype != torch.float32:
             return False
+        else:
+            if lib.dk_pwconv_bwd_fused_rows(N, OH, OW, self.num_filters, C) <= 0:
+                return False
+            env = getenv("DORKNET_PW_FUSED_BWD")
+            if env is not None:
+                if env != "1":
+                    return False
+            elif not lib.dk_pwconv_bwd_fused_preferred(N, OH, OW, self.num_filters, C):
+                return False
         if residual is not None and residual_operand(residual, x) is None:
             return False
         return True
@@ -268,27 +276,29 @@ class PointwiseConvLayer(Layer):
         K = self.num_filters
         OH, OW = self.out_hw
         w = self.learned_params["weights"]
-        dx = empty_nhwc(N, C, OH, OW)
+        bf = x.dtype == BF16
+        dx = empty_nhwc(N, C, OH, OW, x.dtype)
         bn = self._bn_in
         res = residual_operand(residual, dx)
         g = to_nhwc(bg.g)
         part = None
+        rows_fn = lib.dk_pwconv_bwd_fused_bf16_rows if bf else lib.dk_pwconv_bwd_fused_rows
         if bn is not None:
-            rows = lib.dk_pwconv_bwd_fused_rows(N, OH, OW, K, C)
+            rows = rows_fn(N, OH, OW, K, C)
             part = torch.empty((rows, 2, C), dtype=torch.float64, device=dx.device)
         gw = grad_buffer(self, "weights", (K, C))
         l2s = l2_strength(self.weight_regulariser)
-        nb = lib.dk_pwconv_bwd_fused_workspace_bytes(N, OH, OW, K, C)
+        nb = (lib.dk_pwconv_bwd_fused_bf16_workspace_bytes if bf else lib.dk_pwconv_bwd_fused_workspace_bytes)(
+            N, OH, OW, K, C)
         tok = bn.arm_partials(part) if bn is not None else None
         # the weight-gradient reduce on the side stream (not with a non-l2 regulariser, whose term
         # is added to gw on this stream right after)
         red = deferred_wgrad_reduce(self, nb, l2s is not None)
         with red:
-            r = lib.dk_pwconv_bwd_bnbwd_f32(g.data_ptr(), bg.x.data_ptr(), N, OH, OW, K, *bg.bnbwd_args(),
-                                            w.data_ptr(), C, l2s or 0.0, gw.data_ptr(), dx.data_ptr(), ptr(res),
-                                            x.data_ptr(),
-                                            *((*bn.bn_args(), part.data_ptr()) if bn is not None else (0,) * 6),
-                                            red.ws, nb, st)
+            r = (lib.dk_pwconv_bwd_bnbwd_bf16 if bf else lib.dk_pwconv_bwd_bnbwd_f32)(
+                g.data_ptr(), bg.x.data_ptr(), N, OH, OW, K, *bg.bnbwd_args(), w.data_ptr(), C, l2s or 0.0,
+                gw.data_ptr(), dx.data_ptr(), ptr(res), x.data_ptr(),
+                *((*bn.bn_args(), part.data_ptr()) if bn is not None else (0,) * 6), red.ws, nb, st)
         red.flush()
         if l2s is None:
             add_regulariser_grad(gw, w, self.weight_regulariser)

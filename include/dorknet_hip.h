@@ -261,6 +261,15 @@ int dk_dwconv_dgrad_ex_bf16(const uint16_t* dy, int N, int OH, int OW, int C, co
  * MFMA operand and as written to dy_out; the depthwise backward keeps it fp32. */
 int dk_pwconv_dgrad_bnbwd_bf16_stats_rows(int N, int OH, int OW, int K, int C);
 int dk_pwconv_dgrad_bnbwd_bf16(const uint16_t* g, const uint16_t* bn_x, int N, int OH, int OW, int K, const float* out_mean, const float* out_invstd, const float* out_gamma, const float* out_beta, int out_relu, const float* k12, uint16_t* dy_out, const float* w_kc, int C, uint16_t* dx, const uint16_t* residual, const uint16_t* x, const float* bn_mean, const float* bn_invstd, const float* bn_gamma, const float* bn_beta, int bn_relu, double* part, void* stream);
+/* Fused pointwise backward for bf16 storage (the twin of dk_pwconv_bwd_bnbwd_f32; BASELINE config 5's
+ * 56 x 56 units, K = C = 64, stride 1): dx as dk_pwconv_dgrad_bnbwd_bf16 (bit-identical) plus the
+ * weight gradient dW = dy^T bn_relu(x) + l2 w (fp32, bf16 MFMA operands: dy as the dgrad rounds it,
+ * bn_relu(x) rounded to bf16) in one pass; dy is never stored.  Replaces the dgrad + the separate
+ * weight gradient (layers/pointwise_convolution.py:57-75).  *_rows: the partial rows of part (0 = shape
+ * not taken); the workspace holds that many fp32 [K][C] weight-gradient partial rows. */
+int dk_pwconv_bwd_fused_bf16_rows(int N, int OH, int OW, int K, int C);
+size_t dk_pwconv_bwd_fused_bf16_workspace_bytes(int N, int OH, int OW, int K, int C);
+int dk_pwconv_bwd_bnbwd_bf16(const uint16_t* g, const uint16_t* bn_x, int N, int OH, int OW, int K, const float* out_mean, const float* out_invstd, const float* out_gamma, const float* out_beta, int out_relu, const float* k12, const float* w_kc, int C, float l2, float* dw_kc, uint16_t* dx, const uint16_t* residual, const uint16_t* x, const float* bn_mean, const float* bn_invstd, const float* bn_gamma, const float* bn_beta, int bn_relu, double* part, void* ws, size_t ws_bytes, void* stream);
 int dk_dwconv_bwd_bnbwd_bf16(const uint16_t* g, const uint16_t* bn_x, int N, int H, int W, int C, const float* out_mean, const float* out_invstd, const float* out_gamma, const float* out_beta, int out_relu, const float* k12, const uint16_t* x, const float* w_crs, int R, int S, int pad, float l2, float* dw_crs, uint16_t* dx, const uint16_t* residual, const float* bn_mean, const float* bn_invstd, const float* bn_gamma, const float* bn_beta, int bn_relu, double* part, void* ws, size_t ws_bytes, void* stream);int dk_dwconv_wgrad_bnx_bf16(const uint16_t* dy, const uint16_t* x, int N, int H, int W, int C, int R, int S, int stride, int pad, int OH, int OW, const float* w_crs, float l2, float* dw_crs, void* ws, size_t ws_bytes, const float* bn_mean, const float* bn_invstd, const float* bn_gamma, const float* bn_beta, int bn_relu, void* stream);
 
 /* ---------------------------------------------------------------------------------------

@@ -170,3 +170,68 @@ def test_bf16_deep_kernels_dispatch():
         lib.dk_debug_set_gemm_config(9, -1)
     streamed = lib.dk_pwconv_fwd_bf16_stats_rows(512, 7, 7, 512, 512)
     assert streamed != tiled and streamed <= 256 and tiled >= M // 256
+
+
+@pytest.mark.parametrize("relu,bn_in,resid,N,H,W", [(1, True, False, 3, 13, 11), (0, True, False, 2, 8, 8),
+                                                    (1, False, True, 3, 13, 11), (1, True, True, 5, 7, 9),
+                                                    (0, False, False, 1, 1, 3), (1, True, False, 16, 56, 56)])
+def test_bf16_fused_bwd_matches_dgrad_and_fp64(relu, bn_in, resid, N, H, W):
+    """dk_pwconv_bwd_bnbwd_bf16 (pw_stream_bf16.hip bwd_fused_kernel, K = C = 64: dgrad and weight
+    gradient in one pass, dy never stored) against the streaming dgrad: dx bitwise, the input
+    BatchNorm's partial sums to fp64 rounding; and its weight gradient against fp64
+    dW = dy^T bf16(bn_relu(x)) + l2 w with dy the dgrad's stored bf16 dy (the MFMA operands the fused
+    kernel forms), elementwise within 3e-5 of sum |dy| |xh|.  Reference: pointwise_convolution.py:57-75."""
+    K = C = 64
+    assert lib.dk_pwconv_bwd_fused_bf16_rows(N, H, W, K, C) > 0
+    rng = np.random.RandomState(5 + relu + 2 * bn_in + 4 * resid + N)
+    M = N * H * W
+    xo, _ = padded(M, K, rng)
+    g, _ = padded(M, K, rng)
+    po = bn_params(K, rng)
+    k12 = torch.as_tensor(rng.randn(2 * K).astype(np.float32) * 0.1, device="cuda")
+    w = torch.as_tensor(rng.randn(K, C).astype(np.float32) * 0.2, device="cuda")
+    xin, _ = padded(M, C, rng)
+    pi = bn_params(C, rng)
+    res = padded(M, C, rng)[0] if resid else None
+    l2 = 1e-3
+    st = stream_handle()
+    # reference dgrad (stores dy)
+    dy, _ = padded(M, K)
+    dx0, _ = padded(M, C)
+    rows0 = lib.dk_pwconv_dgrad_bnbwd_bf16_stats_rows(N, H, W, K, C)
+    p0 = torch.zeros((rows0, 2, C), dtype=torch.float64, device="cuda")
+    bn_args = (xin.data_ptr(), *(t.data_ptr() for t in pi), relu, p0.data_ptr()) if bn_in else (0,) * 7
+    assert lib.dk_pwconv_dgrad_bnbwd_bf16(g.data_ptr(), xo.data_ptr(), N, H, W, K, *(t.data_ptr() for t in po), relu,
+                                          k12.data_ptr(), dy.data_ptr(), w.data_ptr(), C, dx0.data_ptr(),
+                                          res.data_ptr() if resid else 0, *bn_args, st) == 0
+    # fused
+    rows1 = lib.dk_pwconv_bwd_fused_bf16_rows(N, H, W, K, C)
+    nb = lib.dk_pwconv_bwd_fused_bf16_workspace_bytes(N, H, W, K, C)
+    ws = torch.empty(nb // 4 + 4, dtype=torch.float32, device="cuda")
+    dx1, dx1buf = padded(M, C)
+    dw = torch.full((K, C), float("nan"), device="cuda")
+    p1 = torch.zeros((rows1, 2, C), dtype=torch.float64, device="cuda")
+    bnb = (*(t.data_ptr() for t in pi), relu, p1.data_ptr()) if bn_in else (0,) * 6
+    rc = lib.dk_pwconv_bwd_bnbwd_bf16(g.data_ptr(), xo.data_ptr(), N, H, W, K, *(t.data_ptr() for t in po), relu,
+                                      k12.data_ptr(), w.data_ptr(), C, l2, dw.data_ptr(), dx1.data_ptr(),
+                                      res.data_ptr() if resid else 0, xin.data_ptr(), *bnb, ws.data_ptr(), nb, st)
+    assert rc in (0, 10100)
+    torch.cuda.synchronize()
+    assert torch.equal(dx0, dx1)
+    assert tail_is_nan(dx1buf, M, C)
+    if bn_in:
+        s0, s1 = p0.sum(0), p1.sum(0)
+        assert float((s1 - s0).norm() / s0.norm()) < 1e-12
+    dy64 = dy.view(M, K).double()
+    xf = xin.view(M, C).float()
+    if bn_in:
+        xh = pi[2] * ((xf - pi[0]) * pi[1]) + pi[3]
+        if relu:
+            xh = torch.where(xh > 0, xh, torch.zeros_like(xh))
+    else:
+        xh = xf
+    xh = xh.to(BF16).double()  # the bf16 MFMA operand
+    ref = dy64.t() @ xh + l2 * w.double()
+    bound = 3e-5 * (dy64.abs().t() @ xh.abs()) + 1e-6
+    assert bool(torch.isfinite(dw).all())
+    assert bool(((dw.double() - ref).abs() <= bound).all()), float(((dw.double() - ref).abs() / bound).max())
