@@ -332,6 +332,15 @@ int pw_deep_dgrad_bnbwd(const float* g, const float* bn_x, int M, int K, int C, 
                         const float* ig, const float* ib, int irelu, double* part, hipStream_t st,
                         const struct FoldTail* ft = nullptr);
 
+// the fused bf16 deep backward (pw_deep_bf16.hip bwd_kernel): K in {128, 256}
+bool pw_deep16_bwd_ok(int K, int C, int M);
+int pw_deep16_bwd_rows(int M, int K, int C);
+int pw_deep16_bwd_slices(int M, int K, int C);
+int pw_deep16_bwd_fused(const bf16_t* g, const bf16_t* bn_x, int M, int K, int C, const float* om, const float* ois,
+                        const float* og, const float* ob, int orelu, const float* k12, const float* w, bf16_t* dx,
+                        const bf16_t* res, const bf16_t* x, const float* im, const float* iis, const float* ig,
+                        const float* ib, int irelu, double* part, float* wpart, hipStream_t st,
+                        const struct FoldTail* ft = nullptr);
 // bf16 streaming pointwise kernels (pw_stream_bf16.hip, BASELINE config 5): K, C in {64, 128}.
 bool pw_stream_bf16_fwd_ok(int K, int C, int M);
 int pw_stream_bf16_fwd_rows(int M, int K, int C);

@@ -194,7 +194,9 @@ DK_API int dk_pwconv_dgrad_bnbwd_bf16(const bf16_t* g, const bf16_t* bn_x, int N
 DK_API int dk_pwconv_bwd_fused_bf16_rows(int N, int OH, int OW, int K, int C) {
   if (N < 1 || OH < 1 || OW < 1 || (long long)N * OH * OW >= (1ll << 31)) return 0;
   const int M = N * OH * OW;
-  return pw_stream_bf16_bwd_ok(K, C, M) ? pw_stream_bf16_bwd_rows(M) : 0;
+  if (pw_stream_bf16_bwd_ok(K, C, M)) return pw_stream_bf16_bwd_rows(M);
+  if (pw_deep16_bwd_ok(K, C, M)) return pw_deep16_bwd_rows(M, K, C);
+  return 0;
 }
 
 DK_API size_t dk_pwconv_bwd_fused_bf16_workspace_bytes(int N, int OH, int OW, int K, int C) {
@@ -222,6 +224,18 @@ DK_API int dk_pwconv_bwd_bnbwd_bf16(const bf16_t* g, const bf16_t* bn_x, int N, 
   const int M = N * OH * OW;
   float* wp = static_cast<float*>(ws);
   FoldTail ft;
+  if (!pw_stream_bf16_bwd_ok(K, C, M)) {
+    // K in {128, 256}: the weight-stationary kernel (pw_deep_bf16.hip); it needs the input BN's
+    // partials whenever there is an input BN
+    if ((bn_mean != nullptr) != (part != nullptr)) return DK_ERR_ARGS;
+    if (part) fold_take(part, rows, C, pw_deep16_bwd_slices(M, K, C), &ft);
+    int rc = pw_deep16_bwd_fused(g, bn_x, M, K, C, out_mean, out_invstd, out_gamma, out_beta, out_relu, k12, w_kc,
+                                 dx, residual, x, bn_mean, bn_invstd, bn_gamma, bn_beta, bn_relu, part, wp, st,
+                                 part ? &ft : nullptr);
+    if (rc) return rc;
+    return fold_status(wgrad_reduce(wp, rows, K, C, dw_kc, l2 != 0.f ? w_kc : nullptr, l2, st),
+                       part ? ft : FoldTail{});
+  }
   if (part) fold_take(part, rows, C, 1, &ft);
   int rc = pw_stream_bf16_bwd_fused(g, bn_x, M, out_mean, out_invstd, out_gamma, out_beta, out_relu, k12, w_kc, dx,
                                     residual, x, bn_mean, bn_invstd, bn_gamma, bn_beta, bn_relu, part, wp, st,

@@ -42,7 +42,8 @@ constexpr KnobDef kDefs[kNumKnobs] = {
     {"DORKNET_PWF_BLOCKS_PER_CU", 0},    // kKnobPwfBlocksPerCu: its resident blocks per CU (0 = occupancy)
     {"DORKNET_WGRAD_BLOCKS", 1024},      // kKnobWgradBlocks: blocks a split-K weight gradient aims for
     {nullptr, 22},                       // kKnobEwVariant: launch variant of dk_bn_bwd_apply_f32
-    {"DORKNET_PW_BF16_BWD", 1},          // kKnobPwsh16Bwd: fused bf16 pointwise backward at K = C = 64
+    {"DORKNET_PW_BF16_BWD", 1},          // kKnobPwsh16Bwd: fused bf16 pointwise backward (1: K = C = 64 and
+                                          // K in {128, 256}; 2: K = C = 64 only; 0: off)
 };
 
 struct Table {

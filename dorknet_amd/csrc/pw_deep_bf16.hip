@@ -391,6 +391,195 @@ __global__ __launch_bounds__(NT, dgrad_wps<KR>()) void dgrad_kernel(DgradArgs a)
   if constexpr (PART) partial_row(ps, pq, a.part, N, n0, a.ft, &As[0][0]);
 }
 
+
+// ---------------------------------------------------------------------------------------
+// Fused backward (bf16 storage, K in {128, 256}): the dgrad above plus the weight gradient
+//   dW[k][c] = sum_m dy[m][k] * bn_relu(x)[m][c]   (layers/pointwise_convolution.py:61-64)
+// in the same pass, dy never stored (pw_deep.hip's bwd_kernel on v_mfma_f32_32x32x16_bf16).  Per
+// 32-pixel tile a wave, after its dgrad MFMAs and dx stores:
+//   * forms the B operand bn_relu(x) of its 32 columns from the epilogue's C-layout x loads
+//     (registers 8s .. 8s + 7 of lane half h = pixels 16s + 8(j >> 2) + 4h + (j & 3)), rounded to
+//     bf16 as the tiled engine's BN-on-load loader does, zero past M;
+//   * reads the A operand dy^T (rows = channels, k-step = those 16 pixels) from the block's LDS dy
+//     tile with ds_read_b64_tr_b16 and accumulates its [KR][32] block of dW in registers.
+// dx and the input BN's partials are bit-identical to dgrad_kernel's; dW regroups the sum over
+// pixels.  Each wave stores its dW block into the partial row wpart[blockIdx.x][KR][N] at the end.
+// ---------------------------------------------------------------------------------------
+template <int KR>
+constexpr int bwd_wps() {
+  return KR <= 128 ? 2 : 1;
+}
+
+template <int KR, bool RES, bool BNIN>
+__global__ __launch_bounds__(NT, bwd_wps<KR>()) void bwd_kernel(DgradArgs a, float* wpart) {
+  constexpr int SK = KR + 8, KV = KR / 8, LV = TR * KV / NT, KS = KR / 16, KT = KR / 32;
+  static_assert(KR % 64 == 0 && NT % KV == 0 && LV >= 1, "pwd16::bwd_kernel shape");
+  __shared__ __attribute__((aligned(16))) bf16_t As[2][TR * SK];
+  static_assert(sizeof(double) * 2 * NT <= sizeof(bf16_t) * 2 * TR * SK, "fold scratch fits in the tiles");
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l32 = lane & 31, h = lane >> 5;
+  const int n0 = blockIdx.y * NB, N = a.N, col = n0 + 32 * wave + l32;
+  const int kv = tid % KV, r0 = tid / KV;
+  __shared__ __attribute__((aligned(16))) float tab[7 * KR];
+  for (int c = tid; c < KR; c += NT) {
+    const float is = a.ois[c], ga = a.og[c];
+    tab[c] = a.om[c];
+    tab[KR + c] = is;
+    tab[2 * KR + c] = ga;
+    tab[3 * KR + c] = a.ob[c];
+    tab[4 * KR + c] = a.k12[c];
+    tab[5 * KR + c] = a.k12[KR + c];
+    tab[6 * KR + c] = ga * is;
+  }
+  __syncthreads();
+  const float pm = BNIN ? a.im[col] : 0.f, pis = BNIN ? a.iis[col] : 0.f, pga = BNIN ? a.ig[col] : 0.f,
+              pbe = BNIN ? a.ib[col] : 0.f;
+  const bool orelu = a.orelu != 0, irelu = a.irelu != 0;
+  const int ntiles = (a.M + TR - 1) / TR, G = gridDim.x;
+  const uint32_t lofs0 = ((uint32_t)r0 * KR + 8 * kv) * 2u, eofs0 = ((uint32_t)(4 * h) * N + col) * 2u;
+  constexpr uint32_t kLStep = (uint32_t)(NT / KV) * KR * 2u;
+  auto eofs = [&](int r) { return (int)(eofs0 + (uint32_t)(((r & 3) + 8 * (r >> 2)) * N) * 2u); };
+
+  auto load_tile = [&](int tile, u32x4* sg, u32x4* sx) {
+    const __amdgpu_buffer_rsrc_t rg = tile_rsrc(a.g, KR, tile, a.M), rx = tile_rsrc(a.xo, KR, tile, a.M);
+#pragma unroll
+    for (int j = 0; j < LV; ++j) {
+      sg[j] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rg, (int)(lofs0 + j * kLStep), 0, 0));
+      sx[j] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rx, (int)(lofs0 + j * kLStep), 0, 0));
+    }
+  };
+  auto stage = [&](bf16_t* dst, const u32x4* sg, const u32x4* sx) {
+    f32x4 mu[2], is[2], ga[2], be[2], k1[2], k2[2], f[2];
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const float* tp = tab + 8 * kv + 4 * p;
+      mu[p] = *reinterpret_cast<const f32x4*>(tp);
+      is[p] = *reinterpret_cast<const f32x4*>(tp + KR);
+      ga[p] = *reinterpret_cast<const f32x4*>(tp + 2 * KR);
+      be[p] = *reinterpret_cast<const f32x4*>(tp + 3 * KR);
+      k1[p] = *reinterpret_cast<const f32x4*>(tp + 4 * KR);
+      k2[p] = *reinterpret_cast<const f32x4*>(tp + 5 * KR);
+      f[p] = *reinterpret_cast<const f32x4*>(tp + 6 * KR);
+    }
+#pragma unroll
+    for (int j = 0; j < LV; ++j) {
+      f32x4 gv[2], xv[2];
+      unpack8(sg[j], gv[0], gv[1]);
+      unpack8(sx[j], xv[0], xv[1]);
+#pragma unroll
+      for (int p = 0; p < 2; ++p)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float xe = xv[p][e];
+          float ge = gv[p][e];
+          const bool kill = (!(bn_out(xe, mu[p][e], is[p][e], ga[p][e], be[p][e]) > 0.f)) & orelu;
+          ge = kill ? 0.f : ge;
+          gv[p][e] = bn_bwd_elem(xe, ge, mu[p][e], is[p][e], f[p][e], k1[p][e], k2[p][e]);
+        }
+      *reinterpret_cast<u32x4*>(dst + (r0 + j * (NT / KV)) * SK + 8 * kv) = pack8(gv[0], gv[1]);
+    }
+  };
+
+  int t = first_tile(ntiles);
+  bf16x8 bw[KS];
+  {
+    u32x4 sg[LV], sx[LV];
+    load_tile(t, sg, sx);
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      f32x4 lo, hi;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        lo[e] = a.w[(size_t)(16 * s + 8 * h + e) * N + col];
+        hi[e] = a.w[(size_t)(16 * s + 8 * h + 4 + e) * N + col];
+      }
+      bw[s] = __builtin_bit_cast(bf16x8, pack8(lo, hi));
+    }
+    stage(&As[0][0], sg, sx);
+  }
+  __syncthreads();
+  f32x16 dwa[KT];
+#pragma unroll
+  for (int i = 0; i < KT; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) dwa[i][r] = 0.f;
+  double ps = 0.0, pq = 0.0;
+  int buf = 0;
+  typedef short s16x4 __attribute__((ext_vector_type(4)));
+  typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+  for (; t < ntiles; t += G) {
+    u32x4 ng[LV], nx[LV];
+    load_tile(t + G, ng, nx);
+    const int mb = t * TR + 4 * h;
+    const int rows = a.M - t * TR;
+    const uint32_t nb = rows > 0 ? (uint32_t)rows * N * 2u : 0u;
+    const __amdgpu_buffer_rsrc_t rxi = make_rsrc_v(a.xi + (size_t)t * TR * N, nb);
+    const __amdgpu_buffer_rsrc_t rr = make_rsrc_v(RES ? a.res + (size_t)t * TR * N : a.g, RES ? nb : 0u);
+    const __amdgpu_buffer_rsrc_t rdx = make_rsrc_v(a.dx + (size_t)t * TR * N, nb);
+    uint32_t exi[16], ers[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      exi[r] = __builtin_amdgcn_raw_buffer_load_b16(rxi, eofs(r), 0, 0);
+      if constexpr (RES) ers[r] = __builtin_amdgcn_raw_buffer_load_b16(rr, eofs(r), 0, 0);
+    }
+    const bf16_t* tile = &As[buf][0];
+    f32x16 acc;
+    mfma_tile<KS>(tile + l32 * SK + 8 * h, bw, acc);
+    const bool full = t * TR + TR <= a.M;
+    float xb[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int dm = (r & 3) + 8 * (r >> 2);
+      float v = acc[r];
+      if constexpr (RES) v += bf16_val(ers[r]);
+      const uint16_t bits = bf16_bits(v);
+      bstore_nt(bits, rdx, eofs(r), 0, a.nt);
+      const bool out = !full && mb + dm >= a.M;
+      const float x = bf16_val(exi[r]);
+      if constexpr (BNIN) {
+        const float xh = (x - pm) * pis;
+        const float bo = bn_out(x, pm, pis, pga, pbe);
+        const bool dead = (!(bo > 0.f)) & irelu;
+        const float g2 = (dead | out) ? 0.f : bf16_val(bits);
+        ps += (double)g2;
+        pq += (double)g2 * (double)xh;
+        xb[r] = (dead | out) ? 0.f : bo;
+      } else {
+        xb[r] = out ? 0.f : x;
+      }
+    }
+    // dW[k][col] += dy^T . bf16(bn_relu(x)) over the tile's 32 pixels, two k-steps of 16
+    {
+      const int i = lane & 15, g = (lane >> 4) & 1;
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const bf16x8 bx = __builtin_bit_cast(
+            bf16x8, pack8(f32x4{xb[8 * s2], xb[8 * s2 + 1], xb[8 * s2 + 2], xb[8 * s2 + 3]},
+                          f32x4{xb[8 * s2 + 4], xb[8 * s2 + 5], xb[8 * s2 + 6], xb[8 * s2 + 7]}));
+#pragma unroll
+        for (int kt = 0; kt < KT; ++kt) {
+          const bf16_t* p = tile + (16 * s2 + 4 * h + (i >> 2)) * SK + 32 * kt + 16 * g + 4 * (i & 3);
+          const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p));
+          const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p + 8 * SK));
+          const bf16x8 dyt = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+          dwa[kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(dyt, bx, dwa[kt], 0, 0, 0);
+        }
+      }
+    }
+    stage(&As[buf ^ 1][0], ng, nx);
+    __syncthreads();
+    buf ^= 1;
+  }
+  // this wave's dW block: element (kt, r) = dW[32 kt + (r & 3) + 8 (r >> 2) + 4h][col]
+  {
+    float* wp = wpart + (size_t)blockIdx.x * KR * N + col;
+#pragma unroll
+    for (int kt = 0; kt < KT; ++kt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) wp[(size_t)(32 * kt + (r & 3) + 8 * (r >> 2) + 4 * h) * N] = dwa[kt][r];
+  }
+  if constexpr (BNIN) partial_row(ps, pq, a.part, N, n0, a.ft, &As[0][0]);
+}
+
 // ---------------------------------------------------------------------------------------
 // Host side
 // ---------------------------------------------------------------------------------------
@@ -528,6 +717,62 @@ int pw_deep16_dgrad_bnbwd(const bf16_t* g, const bf16_t* bn_x, int M, int K, int
   }
   DK_PWD16_KR(DK_DG)
 #undef DK_DG
+#undef DK_L
+  return DK_ERR_ARGS;
+}
+
+template <int KR>
+static int bwd_occ16() {
+  static const int occ = [] {
+    const void* fs[] = {reinterpret_cast<const void*>(&pwd16::bwd_kernel<KR, true, true>),
+                        reinterpret_cast<const void*>(&pwd16::bwd_kernel<KR, true, false>),
+                        reinterpret_cast<const void*>(&pwd16::bwd_kernel<KR, false, true>),
+                        reinterpret_cast<const void*>(&pwd16::bwd_kernel<KR, false, false>)};
+    int o = 1 << 20;
+    for (const void* f : fs) o = std::min(o, pwd16::occupancy(f));
+    return o;
+  }();
+  return occ;
+}
+// The fused bf16 backward: K in {128, 256}, C a multiple of the block's 128 columns (knob 20 with the
+// K = C = 64 streaming form; 2 keeps only that one).
+bool pw_deep16_bwd_ok(int K, int C, int M) {
+  if (!pwd16_enabled() || knob(kKnobPwsh16Bwd) != 1 || M <= 0 || (K != 128 && K != 256) || C % pwd16::NB || C > 4096)
+    return false;
+  return (size_t)M * (K > C ? K : C) * 2 < ((size_t)1 << 31);
+}
+int pw_deep16_bwd_rows(int M, int K, int C) {
+  if (K == 128) return pwd16::grid_x(M, C, bwd_occ16<128>());
+  if (K == 256) return pwd16::grid_x(M, C, bwd_occ16<256>());
+  return 0;
+}
+int pw_deep16_bwd_slices(int M, int K, int C) { return C / pwd16::NB; }
+int pw_deep16_bwd_fused(const bf16_t* g, const bf16_t* bn_x, int M, int K, int C, const float* om, const float* ois,
+                        const float* og, const float* ob, int orelu, const float* k12, const float* w, bf16_t* dx,
+                        const bf16_t* res, const bf16_t* x, const float* im, const float* iis, const float* ig,
+                        const float* ib, int irelu, double* part, float* wpart, hipStream_t st, const FoldTail* ft) {
+  if (!x || (im != nullptr) != (part != nullptr)) return DK_ERR_ARGS;
+  pwd16::DgradArgs a{g, bn_x, nullptr, w, dx, res, x, om, ois, og, ob, k12, orelu, im, iis, ig, ib, irelu, part, M, C};
+  if (ft && part) a.ft = *ft;
+  a.nt = nt_stores(kNtPwd16);
+  const dim3 grid(pw_deep16_bwd_rows(M, K, C), C / pwd16::NB);
+  if (grid.x == 0) return DK_ERR_ARGS;
+#define DK_L(kr, R_, B_) hipLaunchKernelGGL((pwd16::bwd_kernel<kr, R_, B_>), grid, dim3(pwd16::NT), 0, st, a, wpart)
+#define DK_BW(kr)             \
+  if (K == kr) {              \
+    if (res && im)            \
+      DK_L(kr, true, true);   \
+    else if (res)             \
+      DK_L(kr, true, false);  \
+    else if (im)              \
+      DK_L(kr, false, true);  \
+    else                      \
+      DK_L(kr, false, false); \
+    return launch_status();   \
+  }
+  DK_BW(128)
+  DK_BW(256)
+#undef DK_BW
 #undef DK_L
   return DK_ERR_ARGS;
 }

@@ -837,7 +837,7 @@ static int pwsh_bwd_occ() {
   return occ;
 }
 bool pw_stream_bf16_bwd_ok(int K, int C, int M) {
-  return pwsh_enabled() && knob(kKnobPwsh16Bwd) == 1 && K == 64 && C == 64 && M > 0 &&
+  return pwsh_enabled() && knob(kKnobPwsh16Bwd) >= 1 && K == 64 && C == 64 && M > 0 &&
          (size_t)M * 64 * 2 < ((size_t)1 << 31);
 }
 int pw_stream_bf16_bwd_rows(int M) { return pwsh::grid_blocks(M, pwsh_bwd_occ()); }

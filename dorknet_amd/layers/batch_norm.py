@@ -122,6 +122,9 @@ class BatchNormLayer(Layer):
             return None
         mean, std, invstd, rm, rs, first = self._stats_outputs(C, part.device)
         self._first_pending = bool(first)
+        # the producer's launch rewrites mean / std / invstd before this layer's forward runs: records
+        # of the previous forward (BNOut, layers/_bn_input.py) are stale from here on
+        self._dk_gen = getattr(self, "_dk_gen", 0) + 1
         t, nt, sc, nsc = fold_resources.get()
         lib.dk_bn_fold_arm_stats(part.data_ptr(), part.shape[0], C, float(P), float(self.eps),
                                  float(self.run_momentum), int(first), mean.data_ptr(), std.data_ptr(),

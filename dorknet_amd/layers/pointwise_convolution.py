@@ -244,7 +244,7 @@ class PointwiseConvLayer(Layer):
         fuses, and a shape a fused kernel takes -- fp32: K = C = 64 (the streaming kernel of
         pw_stream.hip, which never stores dy) and K in {128, 256} (the weight-stationary kernel of
         pw_deep.hip), taken by default where the library prefers it; bf16 (config 5): K = C = 64
-        (pw_stream_bf16.hip).  DORKNET_PW_FUSED_BWD=1 / 0 forces the fp32 path on / off (its round-1
+        (pw_stream_bf16.hip) and K in {128, 256} with C a multiple of 128 (pw_deep_bf16.hip).  DORKNET_PW_FUSED_BWD=1 / 0 forces the fp32 path on / off (its round-1
         tiled kernel for K or C = 128 measured 0.75 % slower than the unfused pair, DESIGN.md
         section 5)."""
         x = self.X

@@ -70,7 +70,9 @@ int dk_mixup_f32(const float* a, const float* b, long long n, float p, float one
  * kind 15: the streaming forward at K = C = 128 (DORKNET_PW_STREAM128);
  * kind 16 / 17: the tiled fused pointwise backward's prefetch (-1 = per shape) and resident blocks per
  * CU (0 = occupancy) (DORKNET_PWF_PREFETCH / DORKNET_PWF_BLOCKS_PER_CU);
- * kind 18: blocks a split-K weight gradient aims for (DORKNET_WGRAD_BLOCKS, default 1024). */
+ * kind 18: blocks a split-K weight gradient aims for (DORKNET_WGRAD_BLOCKS, default 1024);
+ * kind 20: the fused bf16 pointwise backward (DORKNET_PW_BF16_BWD: 1 = K = C = 64 and K in {128, 256},
+ * 2 = K = C = 64 only, 0 = off). */
 int dk_debug_set_gemm_config(int kind, int cfg);
 
 /* Bandwidth ceiling probe (not on the training path; scripts/stream_ceiling.py): reads nin

@@ -110,3 +110,11 @@ def test_pointwise_bwd_fused_rejects_other_shapes():
     assert lib.dk_pwconv_bwd_fused_rows(2, 7, 7, 256, 64) == 0
     # K = C = 256: the fused deep kernel (pw_deep.hip bwd_kernel)
     assert lib.dk_pwconv_bwd_fused_rows(2, 7, 7, 256, 256) > 0
+
+
+def test_bf16_pointwise_bwd_fused_shapes():
+    # bf16: K = C = 64 (streaming form) and K in {128, 256} with C a multiple of 128 (deep form)
+    for K, C in [(64, 64), (128, 128), (256, 128), (256, 256), (128, 512)]:
+        assert lib.dk_pwconv_bwd_fused_bf16_rows(2, 7, 7, K, C) > 0, (K, C)
+    for K, C in [(512, 512), (128, 64), (64, 128), (256, 192)]:
+        assert lib.dk_pwconv_bwd_fused_bf16_rows(2, 7, 7, K, C) == 0, (K, C)

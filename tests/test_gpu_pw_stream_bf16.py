@@ -172,16 +172,17 @@ def test_bf16_deep_kernels_dispatch():
     assert streamed != tiled and streamed <= 256 and tiled >= M // 256
 
 
+@pytest.mark.parametrize("K,C", [(64, 64), (128, 128), (256, 128), (256, 256), (128, 256)])
 @pytest.mark.parametrize("relu,bn_in,resid,N,H,W", [(1, True, False, 3, 13, 11), (0, True, False, 2, 8, 8),
                                                     (1, False, True, 3, 13, 11), (1, True, True, 5, 7, 9),
                                                     (0, False, False, 1, 1, 3), (1, True, False, 16, 56, 56)])
-def test_bf16_fused_bwd_matches_dgrad_and_fp64(relu, bn_in, resid, N, H, W):
-    """dk_pwconv_bwd_bnbwd_bf16 (pw_stream_bf16.hip bwd_fused_kernel, K = C = 64: dgrad and weight
-    gradient in one pass, dy never stored) against the streaming dgrad: dx bitwise, the input
-    BatchNorm's partial sums to fp64 rounding; and its weight gradient against fp64
-    dW = dy^T bf16(bn_relu(x)) + l2 w with dy the dgrad's stored bf16 dy (the MFMA operands the fused
-    kernel forms), elementwise within 3e-5 of sum |dy| |xh|.  Reference: pointwise_convolution.py:57-75."""
-    K = C = 64
+def test_bf16_fused_bwd_matches_dgrad_and_fp64(K, C, relu, bn_in, resid, N, H, W):
+    """dk_pwconv_bwd_bnbwd_bf16 (dgrad and weight gradient in one pass, dy never stored: K = C = 64 on
+    pw_stream_bf16.hip bwd_fused_kernel, K in {128, 256} on pw_deep_bf16.hip bwd_kernel) against the
+    dgrad that stores dy: dx bitwise, the input BatchNorm's partial sums to fp64 rounding; and its
+    weight gradient against fp64 dW = dy^T bf16(bn_relu(x)) + l2 w with dy the dgrad's stored bf16 dy
+    (the MFMA operands the fused kernel forms), elementwise within 3e-5 of sum |dy| |xh|.
+    Reference: pointwise_convolution.py:57-75."""
     assert lib.dk_pwconv_bwd_fused_bf16_rows(N, H, W, K, C) > 0
     rng = np.random.RandomState(5 + relu + 2 * bn_in + 4 * resid + N)
     M = N * H * W

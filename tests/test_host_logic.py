@@ -227,3 +227,26 @@ def test_bnout_refuses_stale_statistics():
     with pytest.raises(RuntimeError):
         out.materialize()
     assert BNOut(t[0], t[1], t[2], t[3], t[4], False, owner=None).bn_args()[-1] == 0
+
+
+def test_stats_fold_arming_marks_records_stale(monkeypatch):
+    """Arming a producer's in-launch statistics fold (batch_norm.py arm_stats_fold) means that launch
+    rewrites the layer's mean / invstd before its forward runs: records of the previous forward go
+    stale at the arming, not only at the forward."""
+    import torch
+    from dorknet_amd.layers import batch_norm
+    from dorknet_amd.layers._bn_input import BNOut
+    bn = BatchNormLayer("bn_f", incoming_chans=4)
+    bn._dk_gen = 7
+    t = [torch.zeros(4) for _ in range(5)]
+    out = BNOut(t[0], t[1], t[2], t[3], t[4], True, owner=bn)
+    monkeypatch.setattr(bn, "_stats_outputs", lambda C, dev: (t[0], t[1], t[2], t[3], t[4], False))
+    monkeypatch.setattr(batch_norm.fold_resources, "get", lambda: (0, 0, 0, 0))
+
+    class _Lib:
+        def dk_bn_fold_arm_stats(self, *a):
+            return 0
+    monkeypatch.setattr(batch_norm, "lib", _Lib())
+    assert bn.arm_stats_fold(torch.zeros((3, 2, 4), dtype=torch.float64), 12) is not None
+    with pytest.raises(RuntimeError, match="bn_f"):
+        out.bn_args()
