@@ -820,8 +820,11 @@ struct BnBwdOut {  // the BatchNorm after this layer: dy = bn_bwd_elem(x1, g)
 
 // T: activation storage (float, or bf16_t for BASELINE config 5): g, x1, x, dx and res are T,
 // dy stays fp32 (LDS ring), and the input BN's partials see dx as stored (rounded).
-template <bool BNX, bool STATS, bool RELU1, bool JOIN = false, class T = float>
-__global__ __launch_bounds__(256) void dw_bwd_fused_kernel(const T* __restrict__ g, const T* __restrict__ x1,
+// CPT: adjacent output columns per thread (CL / CPT threads per channel group).  With 2 a thread's
+// 3 x 4 window and its per-channel terms (LDS ptab, one read per row) serve two pixels: per element
+// half the LDS reads, the bound of the one-column form on bf16 (twice the elements per byte).
+template <bool BNX, bool STATS, bool RELU1, bool JOIN = false, class T = float, int CPT = 1, int NT = 256>
+__global__ __launch_bounds__(NT, NT == 64 ? 2 : 1) void dw_bwd_fused_kernel(const T* __restrict__ g, const T* __restrict__ x1,
                                                            uint32_t bytes, BnBwdOut ob, const T* __restrict__ x,
                                                            BnIn bn, const float* __restrict__ w_crs,
                                                            T* __restrict__ dx, const T* __restrict__ res,
@@ -829,12 +832,14 @@ __global__ __launch_bounds__(256) void dw_bwd_fused_kernel(const T* __restrict__
                                                            int N, int H, int W, int C, int CL, FoldTail ft,
                                                            JoinBwd jn = JoinBwd{}, int nt = 0, int nranges = 0) {
   static_assert(!(JOIN && sizeof(T) != 4), "the join fusion is fp32 only");
+  static_assert(CPT == 1 || CPT == 2, "columns per thread");
   static_assert(!STATS || BNX, "input-BN partials need the input BN");
   static_assert(!(JOIN && (STATS || BNX)), "the join's partials replace the input BN's");
   constexpr bool PART = STATS || JOIN;
-  const int CG = 256 / CL;              // channel groups per block
+  const int CP = CL / CPT;               // threads per channel group
+  const int CG = NT / CP;                // channel groups per block
   const int NI = (CL + 2) * CG;         // dy float4s per LDS row (with the 1-column halos)
-  constexpr int R = 3, S = 3, RS = 9;
+  constexpr int R = 3, S = 3, RS = 9, WC = CPT + 2;  // window columns
   extern __shared__ f32x4 ring[];       // [2][NI]; reused by the final reductions
   const int tid = threadIdx.x;
   const int cg = tid % CG, cl = tid / CG;
@@ -846,13 +851,19 @@ __global__ __launch_bounds__(256) void dw_bwd_fused_kernel(const T* __restrict__
   const int n0 = nranges ? (int)((long long)nr * N / nranges) : nr;
   const int n1 = nranges ? (int)((long long)(nr + 1) * N / nranges) : nr + 1;
   const int c = (cht * CG + cg) * 4;
-  const int w = ct * CL + cl;
-  const bool win_ok = w < W;
+  const int w = ct * CL + CPT * cl;  // this thread's first output column
+  bool win_ok[CPT];
+#pragma unroll
+  for (int j = 0; j < CPT; ++j) win_ok[j] = w + j < W;
   const int wl = ct * CL - 1;  // LDS column 0
-  // this thread's dy items: columns wl + tid / CG and (tid < 2 CG) wl + CL + tid / CG, channel c
+  // this thread's dy items: columns wl + CPT cl + j (LDS columns CPT cl + j) and, for tid < 2 CG
+  // (wave 0), the halo column wl + CL + cl, channel c
   const bool two = tid < 2 * CG;
-  const int col0 = wl + cl, col1 = wl + CL + cl;
-  const bool cok0 = (unsigned)col0 < (unsigned)W, cok1 = two && (unsigned)col1 < (unsigned)W;
+  const int col0 = wl + CPT * cl, col1 = wl + CL + cl;
+  bool cok0[CPT];
+#pragma unroll
+  for (int j = 0; j < CPT; ++j) cok0[j] = (unsigned)(col0 + j) < (unsigned)W;
+  const bool cok1 = two && (unsigned)col1 < (unsigned)W;
   const __amdgpu_buffer_rsrc_t rg = make_rsrc_v(g, bytes), r1 = make_rsrc_v(x1, bytes), rx = make_rsrc_v(x, bytes);
   // the optional operands as buffers too (an absent one covers 0 bytes: its loads return 0), so
   // every load of the row loop is an unconditional buffer load and the waitcnt pass keeps the
@@ -863,8 +874,8 @@ __global__ __launch_bounds__(256) void dw_bwd_fused_kernel(const T* __restrict__
   const __amdgpu_buffer_rsrc_t rjm = make_rsrc_v(JOIN ? jn.mask : nullptr, (JOIN && jn.mask) ? bytes / 4u : 0u);
   // the per-channel BatchNorm terms and the (flipped) filters live in LDS, read where used:
   // held in registers they kept the kernel at 2 waves per SIMD, too few to hide a row's loads
-  __shared__ f32x4 ptab[13 + RS][32];  // [term][channel group]; CG <= 32 (dwb_cl)
-  for (int i = tid; i < 13 * CG; i += 256) {
+  __shared__ f32x4 ptab[13 + RS][NT == 64 ? 16 : 32];  // [term][channel group]; CG <= 32 (16: dwb_geom)
+  for (int i = tid; i < 13 * CG; i += NT) {
     const int t = i / CG, q = i - t * CG;
     const int cc = (cht * CG + q) * 4;
     f32x4 v = {0.f, 0.f, 0.f, 0.f};
@@ -928,12 +939,12 @@ __global__ __launch_bounds__(256) void dw_bwd_fused_kernel(const T* __restrict__
   using Raw = typename std::conditional<sizeof(T) == 2, uint2, f32x4>::type;
   constexpr int PF = sizeof(T) == 2 ? 2 : 1;
   struct DyQ {
-    Raw g0, x0, g1, x1;
+    Raw g0[CPT], x0[CPT], g1, x1;
   };
   struct XQ {
-    Raw xr, rv;
-    f32x4 jxin;    // (the kernel's #defines take jm / ji)
-    uint32_t jmask;
+    Raw xr[CPT], rv[CPT];
+    f32x4 jxin[CPT];    // (the kernel's #defines take jm / ji)
+    uint32_t jmask[CPT];
   };
   DyQ dq[PF];
   XQ xq[PF];
@@ -953,30 +964,36 @@ __global__ __launch_bounds__(256) void dw_bwd_fused_kernel(const T* __restrict__
   // load, so the waitcnt pass counts them instead of draining every memory operation
   auto load_dy_row = [&](DyQ& q, int nn, int hh) {
     const bool rok = (unsigned)hh < (unsigned)H && nn < n1;
-    q.g0 = raw_load(rg, rok && cok0, pix(nn, hh, col0));
-    q.x0 = raw_load(r1, rok && cok0, pix(nn, hh, col0));
+#pragma unroll
+    for (int j = 0; j < CPT; ++j) {
+      q.g0[j] = raw_load(rg, rok && cok0[j], pix(nn, hh, col0 + j));
+      q.x0[j] = raw_load(r1, rok && cok0[j], pix(nn, hh, col0 + j));
+    }
     q.g1 = raw_load(rg, rok && cok1, pix(nn, hh, col1));
     q.x1 = raw_load(r1, rok && cok1, pix(nn, hh, col1));
   };
   auto load_x_row = [&](XQ& q, int nn, int hh) {
-    const bool ok = win_ok && hh < H && nn < n1;
-    q.xr = raw_load(rx, ok, pix(nn, hh, w));
-    q.rv = raw_load(rres, ok, pix(nn, hh, w));
-    if constexpr (JOIN) {
-      q.jmask = __builtin_amdgcn_raw_buffer_load_b32(rjm, (int)(ok ? pix(nn, hh, w) : kOOBBytes), 0, 0);  // 4 mask bytes
-      q.jxin = bload4e<float>(rjx, ok, pix(nn, hh, w));
+#pragma unroll
+    for (int j = 0; j < CPT; ++j) {
+      const bool okj = win_ok[j] && hh < H && nn < n1;
+      q.xr[j] = raw_load(rx, okj, pix(nn, hh, w + j));
+      q.rv[j] = raw_load(rres, okj, pix(nn, hh, w + j));
+      if constexpr (JOIN) {
+        q.jmask[j] = __builtin_amdgcn_raw_buffer_load_b32(rjm, (int)(okj ? pix(nn, hh, w + j) : kOOBBytes), 0, 0);  // 4 mask bytes
+        q.jxin[j] = bload4e<float>(rjx, okj, pix(nn, hh, w + j));
+      }
     }
   };
   double s1[4] = {0.0, 0.0, 0.0, 0.0}, s2[4] = {0.0, 0.0, 0.0, 0.0};
   f32x4 wacc[R][S];
-  f32x4 d[R][S];
+  f32x4 d[R][WC];
 #pragma unroll
-  for (int r = 0; r < R; ++r)
+  for (int r = 0; r < R; ++r) {
 #pragma unroll
-    for (int s = 0; s < S; ++s) {
-      wacc[r][s] = f32x4{0.f, 0.f, 0.f, 0.f};
-      d[r][s] = f32x4{0.f, 0.f, 0.f, 0.f};
-    }
+    for (int s = 0; s < S; ++s) wacc[r][s] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < WC; ++s) d[r][s] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
   // load cursors: the (image, row) of the dy row PF steps ahead (row H = the zero row) and of the
   // next x row (rows 0 .. H-1 of each image of the run)
   int pn = n0, prr = 0, xn = n0, xhh = 0;
@@ -992,21 +1009,26 @@ __global__ __launch_bounds__(256) void dw_bwd_fused_kernel(const T* __restrict__
   int n = n0, rr = 0;
   for (int it = 0; it < iters; ++it) {
     const int rowok = rr < H;
-    const f32x4 d0 = xform(widen(dq[0].g0), widen(dq[0].x0), rowok && cok0);
-    const f32x4 d1 = xform(widen(dq[0].g1), widen(dq[0].x1), rowok && cok1);
+    f32x4 d0[CPT];
+#pragma unroll
+    for (int j = 0; j < CPT; ++j) d0[j] = xform(widen(dq[0].g0[j]), widen(dq[0].x0[j]), rowok && cok0[j]);
+    // the halo columns: wave 0 only (2 CG <= 64) -- a wave-uniform branch with two columns per thread
+    f32x4 d1 = {0.f, 0.f, 0.f, 0.f};
+    if (CPT == 1 || tid < 64) d1 = xform(widen(dq[0].g1), widen(dq[0].x1), rowok && cok1);
 #pragma unroll
     for (int k = 0; k + 1 < PF; ++k) dq[k] = dq[k + 1];
     load_dy_row(dq[PF - 1], pn, prr);
     if (++prr > H) prr = 0, ++pn;
     f32x4* slot = ring + (it & 1) * NI;
-    slot[tid] = d0;
-    if (two) slot[tid + 256] = d1;
+#pragma unroll
+    for (int j = 0; j < CPT; ++j) slot[(CPT * cl + j) * CG + cg] = d0[j];  // = slot[tid] for CPT 1
+    if (two) slot[CL * CG + tid] = d1;
     __syncthreads();
 #pragma unroll
-    for (int s = 0; s < S; ++s) {
+    for (int s = 0; s < WC; ++s) {
       d[0][s] = d[1][s];
       d[1][s] = d[2][s];
-      d[2][s] = slot[(cl + s) * CG + cg];
+      d[2][s] = slot[(CPT * cl + s) * CG + cg];
     }
     const int nn = n;
     if (++rr > H) {
@@ -1015,8 +1037,19 @@ __global__ __launch_bounds__(256) void dw_bwd_fused_kernel(const T* __restrict__
     }
     if (rr == 1) continue;  // just published row 0 of an image: no dx row to finish yet
     const int h = (rr == 0 ? H + 1 : rr) - 2;  // the dx row of image nn finished now
-    const f32x4 xh = widen(xq[0].xr), rh = widen(xq[0].rv), jh = xq[0].jxin;
-    const uint32_t jmh = xq[0].jmask;
+    f32x4 xh[CPT], rh[CPT];
+#pragma unroll
+    for (int q = 0; q < CPT; ++q) {
+      xh[q] = widen(xq[0].xr[q]);
+      rh[q] = widen(xq[0].rv[q]);
+    }
+    f32x4 jh[CPT];
+    uint32_t jmh[CPT];
+#pragma unroll
+    for (int q = 0; q < CPT; ++q) {
+      jh[q] = xq[0].jxin[q];
+      jmh[q] = xq[0].jmask[q];
+    }
 #pragma unroll
     for (int k = 0; k + 1 < PF; ++k) xq[k] = xq[k + 1];
     load_x_row(xq[PF - 1], xn, xhh);
@@ -1025,70 +1058,85 @@ __global__ __launch_bounds__(256) void dw_bwd_fused_kernel(const T* __restrict__
     // the input BN's output (+ReLU) for the weight gradient (bn_relu_out), and its ReLU mask (BN
     // output > 0) kept as 4 bits for the backward partials (recomputing bn_out there re-read the
     // BN terms from LDS once per element)
-    f32x4 xb = xh;
-    uint32_t rmask = 0xfu;
+    f32x4 xb[CPT];
+    uint32_t rmask[CPT];
+#pragma unroll
+    for (int q = 0; q < CPT; ++q) {
+      xb[q] = xh[q];
+      rmask[q] = 0xfu;
+    }
     if constexpr (BNX) {
       const f32x4 vbm = bm, vbi = bi, vbg = bg, vbb = bb;
-      f32x4 xr;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        xr[e] = bn_out(xh[e], vbm[e], vbi[e], vbg[e], vbb[e]);
-        if (!(xr[e] > 0.f)) {
-          rmask &= ~(1u << e);
-          if (bn.relu) xr[e] = 0.f;
+      for (int q = 0; q < CPT; ++q) {
+        f32x4 xr;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          xr[e] = bn_out(xh[q][e], vbm[e], vbi[e], vbg[e], vbb[e]);
+          if (!(xr[e] > 0.f)) {
+            rmask[q] &= ~(1u << e);
+            if (bn.relu) xr[e] = 0.f;
+          }
         }
+        if (!bn.relu) rmask[q] = 0xfu;
+        xb[q] = win_ok[q] ? xr : f32x4{0.f, 0.f, 0.f, 0.f};
       }
-      if (!bn.relu) rmask = 0xfu;
-      xb = win_ok ? xr : f32x4{0.f, 0.f, 0.f, 0.f};
     }
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    f32x4 acc[CPT];
+#pragma unroll
+    for (int q = 0; q < CPT; ++q) acc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int r = 0; r < R; ++r)
 #pragma unroll
       for (int s = 0; s < S; ++s) {
-        acc += d[r][s] * WV(r, s);
-        wacc[r][s] += d[r][s] * xb;
+        const f32x4 wv = WV(r, s);
+#pragma unroll
+        for (int q = 0; q < CPT; ++q) {
+          acc[q] += d[r][q + s] * wv;
+          wacc[r][s] += d[r][q + s] * xb[q];
+        }
       }
-    if (win_ok) {
-      if (res) acc += rh;
+#pragma unroll
+    for (int q = 0; q < CPT; ++q) {
+      if (!win_ok[q]) continue;
+      if (res) acc[q] += rh[q];
+      T* dxp = dxcol ? dxcol + (size_t)h * W * C + (size_t)q * C : nullptr;
       if constexpr (JOIN) {
-        acc = rnd4<T>(acc);
+        acc[q] = rnd4<T>(acc[q]);
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           // dy * mask (activations.py:46); no mask given: this layer's input is the join's output
           // y = max(v, 0), and y > 0 is exactly the stored mask (v > 0)
-          const bool keep = jn.mask ? ((jmh >> (8 * e)) & 0xffu) != 0u : xh[e] > 0.f;
-          if (!keep) acc[e] = 0.f;
-          const float xn = (jh[e] - jm[e]) * ji[e];
-          s1[e] += (double)acc[e];
-          s2[e] += (double)acc[e] * (double)xn;
+          const bool keep = jn.mask ? ((jmh[q] >> (8 * e)) & 0xffu) != 0u : xh[q][e] > 0.f;
+          if (!keep) acc[q][e] = 0.f;
+          const float xn = (jh[q][e] - jm[e]) * ji[e];
+          s1[e] += (double)acc[q][e];
+          s2[e] += (double)acc[q][e] * (double)xn;
         }
-      }
-      if constexpr (JOIN) {
-        if (dxcol) {
+        if (dxp) {
           if (nt)
-            st4nt(dxcol + (size_t)h * W * C, acc);
+            st4nt(dxp, acc[q]);
           else
-            st4(dxcol + (size_t)h * W * C, acc);
+            st4(dxp, acc[q]);
         }
-      } else if (dxcol) {
-        acc = st4_kept(dxcol + (size_t)h * W * C, acc, nt);  // acc = what the store keeps
+      } else if (dxp) {
+        acc[q] = st4_kept(dxp, acc[q], nt);  // acc = what the store keeps
       } else {
-        acc = rnd4<T>(acc);
+        acc[q] = rnd4<T>(acc[q]);
       }
       if constexpr (STATS) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          float ge = acc[e];
-          const float xn = (xh[e] - bm[e]) * bi[e];
-          if (!((rmask >> e) & 1u)) ge = 0.f;
+          float ge = acc[q][e];
+          const float xn = (xh[q][e] - bm[e]) * bi[e];
+          if (!((rmask[q] >> e) & 1u)) ge = 0.f;
           s1[e] += (double)ge;
           s2[e] += (double)ge * (double)xn;
         }
       }
     }
   }
-  // fixed-order block reductions over the CL column lanes of each channel group
+  // fixed-order block reductions over the CP column lanes of each channel group
   __syncthreads();
   if constexpr (PART) {
     double(*red)[8] = reinterpret_cast<double(*)[8]>(ring);
@@ -1098,32 +1146,32 @@ __global__ __launch_bounds__(256) void dw_bwd_fused_kernel(const T* __restrict__
       red[tid][4 + e] = s2[e];
     }
     __syncthreads();
-    for (int i = tid; i < CG * 8; i += 256) {
+    for (int i = tid; i < CG * 8; i += NT) {
       const int gq = i >> 3, e = i & 7;
       double a = 0.0;
-      for (int k = 0; k < CL; ++k) a += red[k * CG + gq][e];
+      for (int k = 0; k < CP; ++k) a += red[k * CG + gq][e];
       pub_store(spart + ((size_t)strip * 2 + (e >> 2)) * C + (cht * CG + gq) * 4 + (e & 3), a);
     }
     __syncthreads();
   }
-  float* wred = reinterpret_cast<float*>(ring);  // [256][RS][4]
+  float* wred = reinterpret_cast<float*>(ring);  // [NT][RS][4]
 #pragma unroll
   for (int r = 0; r < R; ++r)
 #pragma unroll
     for (int s = 0; s < S; ++s) st4(wred + (tid * RS + r * S + s) * 4, wacc[r][s]);
   __syncthreads();
   // wpart[strip][c][a][b], (a, b) = (2-r, 2-s)
-  for (int i = tid; i < CG * 4 * RS; i += 256) {
+  for (int i = tid; i < CG * 4 * RS; i += NT) {
     const int cc = i / RS, tap = i - cc * RS;
     const int a = tap / S, b = tap - a * S;
     const int gq = cc >> 2, e = cc & 3;
     const int fl = (R - 1 - a) * S + (S - 1 - b);
     float sum = 0.f;
-    for (int k = 0; k < CL; ++k) sum += wred[((k * CG + gq) * RS + fl) * 4 + e];
+    for (int k = 0; k < CP; ++k) sum += wred[((k * CG + gq) * RS + fl) * 4 + e];
     wpart[((size_t)strip * C + cht * CG * 4) * RS + i] = sum;
   }
   if constexpr (PART) {
-    if (ft.part) fold_tail<256>(ft, strip, cht * CG * 4, CG * 4, cht);
+    if (ft.part) fold_tail<NT>(ft, strip, cht * CG * 4, CG * 4, cht);
   }
 #undef om
 #undef oi
@@ -1141,28 +1189,251 @@ __global__ __launch_bounds__(256) void dw_bwd_fused_kernel(const T* __restrict__
 #undef WV
 }
 
-// Column-strip width CL (CG = 256 / CL channel groups per block): 16 columns x 64 channels, or
-// 8 x 128 for narrow images; fewer channel groups (wider strips) when C / 4 has no such factor.
-static inline int dwb_cl(int W, int C) {
+// The whole stride-2 depthwise backward in one pass (3x3, pad 1; the strided twin of
+// dw_bwd_fused_kernel): the layer's gradient dy = BN backward(g, x1) (the following BatchNorm,
+// batch_norm.py:125-174 stage 3) is formed as its window is loaded and never stored, and per
+// sub-pixel quad (the ST x ST dx pixels of dw_dgrad_subpixel_kernel) the same dy taps give
+//   dx[2i + a][2j + b] = sum over the taps of phase (a, b) of W[r][s] dy[i + nb(r)][j + nb(s)]
+//   dW[r][s]         += xb[2i + phase(r)][2j + phase(s)] dy[i + nb(r)][j + nb(s)]
+// (depthwise_convolution.py:198-221 reindexed by input pixel), xb = the layer's input as the
+// forward saw it (BNX: the input BatchNorm (+ReLU) applied on load).  dx is bit-identical to
+// dk_bn_bwd_apply -> dk_dwconv_dgrad_ex (same dy values in fp32, same tap order); the input BN's
+// backward partials (STATS: stage 1 over the stored dx, its ReLU mask recomputed from x) and the
+// weight gradient are per-block fixed-order sums.  A thread keeps one channel quad and walks items
+// (image, quad row, TWQ-quad column segment) with the grid's stride, so the partial rows are one per
+// block, not one per item.
+// JOIN (fp32; config 3's downsampling blocks): the layer's input x is a residual block's output
+// y = ReLU(bn_j(x_j) + skip) (residual_block.py:75): dx = (dgrad + residual) * (y > 0) -- the join's
+// ReLU backward, its mask read off y, which the weight gradient loads anyway -- and the partials are
+// stage 1 of bn_j's backward over that dx (jn.x = x_j, jn.mean / invstd); jn.res_lat: the residual
+// is the stride-2 lattice only (a strided skip projection's input gradient, compact).
+template <bool BNX, bool STATS, bool RELU1, class T, bool JOIN = false>
+__global__ __launch_bounds__(256, 2) void dw_bwd_s2_kernel(const T* __restrict__ g, const T* __restrict__ x1,
+                                                          uint32_t ybytes, BnBwdOut ob, const T* __restrict__ x,
+                                                          uint32_t xbytes, BnIn bn, const float* __restrict__ w_crs,
+                                                          T* __restrict__ dx, const T* __restrict__ res,
+                                                          double* __restrict__ spart, float* __restrict__ wpart,
+                                                          int N, int H, int W, int C, int OH, int OW, FoldTail ft,
+                                                          int nt, JoinBwd jn = JoinBwd{}) {
+  static_assert(!STATS || BNX, "input-BN partials need the input BN");
+  static_assert(!JOIN || (!BNX && sizeof(T) == 4), "the join form: fp32, no input BN");
+  constexpr bool PART = STATS || JOIN;
+  constexpr int R = 3, S = 3, ST = 2, PAD = 1, RS = 9, TWQ = 2;
+  using SP = SubPix<R, ST, PAD>;
+  constexpr int D0 = SP::dmin(), ND = SP::dmax() - SP::dmin() + 1, NCOL = TWQ + ND - 1;
+  extern __shared__ f32x4 scratch[];  // the final reductions
+  const int tid = threadIdx.x;
+  const int C4 = C >> 2, IPB = 256 / C4;  // items a block works on at once (C4 divides 256)
+  const int cq = tid % C4, il = tid / C4, c = 4 * cq;
+  const int QH = (H + 1) / 2, QW = (W + 1) / 2, nqc = (QW + TWQ - 1) / TWQ;
+  const int items = N * QH * nqc;
+  const __amdgpu_buffer_rsrc_t rg = make_rsrc_v(g, ybytes), r1 = make_rsrc_v(x1, ybytes), rx = make_rsrc_v(x, xbytes);
+  const int QHW = (JOIN && jn.res_lat) ? QH * QW : H * W;  // residual pixels per image
+  const __amdgpu_buffer_rsrc_t rres = make_rsrc_v(res, res ? (uint32_t)((size_t)N * QHW * C * sizeof(T)) : 0u);
+  const __amdgpu_buffer_rsrc_t rdx = make_rsrc_v(dx, dx ? xbytes : 0u);
+  const __amdgpu_buffer_rsrc_t rjx = make_rsrc_v(JOIN ? jn.x : nullptr, JOIN ? xbytes : 0u);
+  f32x4 jm = {0.f, 0.f, 0.f, 0.f}, ji = jm;
+  if constexpr (JOIN) {
+    jm = ld4(jn.mean + c);
+    ji = ld4(jn.invstd + c);
+  }
+  // this thread's channel terms: the following BN (dy), the filters W[c][r][s], the input BN
+  const f32x4 om = ld4(ob.mean + c), oi = ld4(ob.invstd + c), ok1 = ld4(ob.k12 + c), ok2 = ld4(ob.k12 + C + c);
+  const f32x4 of = ld4(ob.gamma + c) * oi;
+  f32x4 og = {0.f, 0.f, 0.f, 0.f}, obt = og;
+  if constexpr (RELU1) {
+    og = ld4(ob.gamma + c);
+    obt = ld4(ob.beta + c);
+  }
+  f32x4 bm = {0.f, 0.f, 0.f, 0.f}, bi = bm, bg = bm, bb = bm;
+  if constexpr (BNX) {
+    bm = ld4(bn.mean + c);
+    bi = ld4(bn.invstd + c);
+    bg = ld4(bn.gamma + c);
+    bb = ld4(bn.beta + c);
+  }
+  f32x4 wv[R][S];
+  load_dw_weights<R, S, 1>(wv, w_crs, c, C);
+  f32x4 wacc[R][S];
+#pragma unroll
+  for (int r = 0; r < R; ++r)
+#pragma unroll
+    for (int s = 0; s < S; ++s) wacc[r][s] = f32x4{0.f, 0.f, 0.f, 0.f};
+  double s1[4] = {0.0, 0.0, 0.0, 0.0}, s2[4] = {0.0, 0.0, 0.0, 0.0};
+  for (int item = blockIdx.x * IPB + il; item < items; item += gridDim.x * IPB) {
+    const int qc = item % nqc;
+    const int t = item / nqc;
+    const int qi = t % QH, n = t / QH;
+    const int j0 = qc * TWQ;
+    // the dy window: rows qi + D0 .., columns j0 + D0 .., formed from (g, x1) on load
+    f32x4 d[ND][NCOL];
+#pragma unroll
+    for (int a = 0; a < ND; ++a) {
+      const int oh = qi + D0 + a;
+#pragma unroll
+      for (int b = 0; b < NCOL; ++b) {
+        const int ow = j0 + D0 + b;
+        const bool ok = (unsigned)oh < (unsigned)OH && (unsigned)ow < (unsigned)OW;
+        const uint32_t e = (uint32_t)(((n * OH + oh) * OW + ow) * C + c);
+        const f32x4 gv = bload4e<T>(rg, ok, e), xv = bload4e<T>(r1, ok, e);
+        f32x4 o;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          float ge = gv[k];
+          if constexpr (RELU1) {
+            if (!(bn_out(xv[k], om[k], oi[k], og[k], obt[k]) > 0.f)) ge = 0.f;
+          }
+          o[k] = bn_bwd_elem(xv[k], ge, om[k], oi[k], of[k], ok1[k], ok2[k]);
+        }
+        d[a][b] = ok ? o : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < TWQ; ++q) {
+      const int j = j0 + q;
+      f32x4 xb[ST][ST], xr[ST][ST], acc[ST][ST], jxv[ST][ST];
+      bool okp[ST][ST];
+#pragma unroll
+      for (int a = 0; a < ST; ++a)
+#pragma unroll
+        for (int b = 0; b < ST; ++b) {
+          const int h = qi * ST + a, w = j * ST + b;
+          okp[a][b] = j < QW && h < H && w < W;
+          const uint32_t e = (uint32_t)(((n * H + h) * W + w) * C + c);
+          xr[a][b] = bload4e<T>(rx, okp[a][b], e);
+          if (JOIN && jn.res_lat)  // compact lattice residual: phase (0, 0) only, at quad (qi, j)
+            acc[a][b] = bload4e<T>(rres, okp[a][b] && a == 0 && b == 0, (uint32_t)(((n * QH + qi) * QW + j) * C + c));
+          else
+            acc[a][b] = res ? bload4e<T>(rres, okp[a][b], e) : f32x4{0.f, 0.f, 0.f, 0.f};
+          if constexpr (JOIN) jxv[a][b] = bload4e<float>(rjx, okp[a][b], e);
+          f32x4 v = xr[a][b];
+          if constexpr (BNX) v = bn_in4(v, bm, bi, bg, bb, bn.relu);
+          xb[a][b] = okp[a][b] ? v : f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+      // dgrad in dw_dgrad_subpixel_kernel's tap order (the residual added after, as there)
+      f32x4 dg[ST][ST];
+#pragma unroll
+      for (int a = 0; a < ST; ++a)
+#pragma unroll
+        for (int b = 0; b < ST; ++b) dg[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int s = 0; s < S; ++s) {
+          const f32x4 dv = d[SP::nb(r) - D0][q + SP::nb(s) - D0];
+          dg[SP::phase(r)][SP::phase(s)] += dv * wv[r][s];
+          wacc[r][s] += dv * xb[SP::phase(r)][SP::phase(s)];
+        }
+#pragma unroll
+      for (int a = 0; a < ST; ++a)
+#pragma unroll
+        for (int b = 0; b < ST; ++b) {
+          const int h = qi * ST + a, w = j * ST + b;
+          const uint32_t e = (uint32_t)(((n * H + h) * W + w) * C + c);
+          f32x4 o = res ? dg[a][b] + acc[a][b] : dg[a][b];
+          o = rnd4<T>(o);  // the partials see dx as stored
+          if constexpr (JOIN) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+              if (!(xr[a][b][k] > 0.f)) o[k] = 0.f;  // dy * mask (activations.py:46), mask = y > 0
+              const float xn = (jxv[a][b][k] - jm[k]) * ji[k];
+              const float gk = okp[a][b] ? o[k] : 0.f;
+              s1[k] += (double)gk;
+              s2[k] += (double)gk * (double)xn;
+            }
+          }
+          bstore4e_nt<T>(rdx, okp[a][b], e, o, nt);
+          if constexpr (STATS) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+              const float xv = xr[a][b][k];
+              const float xn = (xv - bm[k]) * bi[k];
+              const bool kill = !okp[a][b] || (bn.relu && !(bn_out(xv, bm[k], bi[k], bg[k], bb[k]) > 0.f));
+              const float gk = kill ? 0.f : o[k];
+              s1[k] += (double)gk;
+              s2[k] += (double)gk * (double)xn;
+            }
+          }
+        }
+    }
+  }
+  // fixed-order block reductions over the IPB item lanes of each channel quad
+  if constexpr (PART) {
+    double(*red)[8] = reinterpret_cast<double(*)[8]>(scratch);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      red[tid][k] = s1[k];
+      red[tid][4 + k] = s2[k];
+    }
+    __syncthreads();
+    for (int i = tid; i < C * 2; i += 256) {  // i = (which, channel)
+      const int which = i / C, ch = i - which * C;
+      const int q4 = ch >> 2, k = ch & 3;
+      double a = 0.0;
+      for (int l = q4; l < 256; l += C4) a += red[l][4 * which + k];
+      pub_store(spart + ((size_t)blockIdx.x * 2 + which) * C + ch, a);
+    }
+    __syncthreads();
+  }
+  float* wred = reinterpret_cast<float*>(scratch);  // [256][RS][4]
+#pragma unroll
+  for (int r = 0; r < R; ++r)
+#pragma unroll
+    for (int s = 0; s < S; ++s) st4(wred + (tid * RS + r * S + s) * 4, wacc[r][s]);
+  __syncthreads();
+  // wpart[block][c][r][s]
+  for (int i = tid; i < C * RS; i += 256) {
+    const int ch = i / RS, tap = i - ch * RS;
+    const int q4 = ch >> 2, k = ch & 3;
+    float a = 0.f;
+    for (int l = q4; l < 256; l += C4) a += wred[(l * RS + tap) * 4 + k];
+    wpart[(size_t)blockIdx.x * C * RS + i] = a;
+  }
+  if constexpr (PART) {
+    if (ft.part) fold_tail<256>(ft, blockIdx.x, 0, C, 0);
+  }
+}
+
+// Block geometry of the fused stride-1 backward: CG channel groups of 4 x CL / CPT column lanes
+// (CG * CL / CPT = 256 threads), a CL-column strip.  One column per thread: 16 columns x 64
+// channels, or 8 x 128 for narrow images; fewer channel groups (wider strips) when C / 4 has no
+// such factor.  Two columns per thread (DORKNET_DWB_COLS, kind 21; W >= 12): CG in {16, 32}
+// with the strip width (32 or 16 columns) that pads the row least, ties to the wider.  fp32 and bf16
+// alike: 512 x 56 x 56 x 64 bf16 328 -> 284 us, 256 x 56 x 56 x 64 fp32 205 -> 182 us (dwb_bench.py).
+struct DwbGeom {
+  int cpt, cl, cg, nt;
+};
+static inline DwbGeom dwb_geom(int W, int C, int cpt, int nt = 256) {
   const int C4 = C / 4;
+  if (cpt == 2 && W >= 12 && C4 % 16 == 0) {
+    const int pad32 = (W + 31) / 32 * 32 - W, pad16 = (W + 15) / 16 * 16 - W;
+    if (C4 % 32 == 0 && pad16 < pad32) return DwbGeom{2, 16, 32, 256};
+    return DwbGeom{2, 32, 16, 256};
+  }
   int cg = W > 8 ? 16 : 32;
   while (cg > 1 && C4 % cg) cg >>= 1;
-  return 256 / cg;
+  return DwbGeom{1, 256 / cg, cg, 256};
 }
+static inline int dwb_cpt(size_t) { return knob(kKnobDwbCols) == 2 ? 2 : 1; }
+static inline int dwb_nt(size_t) { return 256; }
 // Image runs of the fused stride-1 backward: one image per block while N * column strips * channel
 // tiles blocks fit DORKNET_DWB_BLOCKS (default 768 = three resident blocks per CU: its LDS and
 // registers allow three); above that the batch is dealt into runs so the grid is one round (a
 // second, partial round of blocks cost small images up to twice the time: 7 x 7 x 512 ran 1024
 // one-image blocks).  0 = one image per block always.
 static inline int dwb_target_blocks() { return knob(kKnobDwbBlocks); }  // kind 7
-static inline int dwb_nranges(int N, int W, int C, int cl) {
-  const int per_image = ((W + cl - 1) / cl) * ((C / 4) / (256 / cl));
-  const int t = dwb_target_blocks();
+static inline int dwb_nranges(int N, int W, int C, const DwbGeom& g) {
+  const int per_image = ((W + g.cl - 1) / g.cl) * ((C / 4) / g.cg);
+  // the two-column form holds two blocks per CU (its registers; eight one-wave blocks), the
+  // one-column form three
+  const int t = g.cpt == 2 ? dwb_target_blocks() * 2 / 3 * (256 / g.nt) : dwb_target_blocks();
   if (t <= 0 || (long long)N * per_image <= t) return N;
   const int r = t / per_image;
   return r < 1 ? 1 : (r > N ? N : r);
 }
-static inline int dwb_strips(int N, int W, int C, int cl) { return dwb_nranges(N, W, C, cl) * ((W + cl - 1) / cl); }
+static inline int dwb_strips(int N, int W, int C, const DwbGeom& g) {
+  return dwb_nranges(N, W, C, g) * ((W + g.cl - 1) / g.cl);
+}
 
 static int dw_wgrad_blocks(int N, int OH, int OW, int C) {
   const int C4 = C / 4;
@@ -1496,11 +1767,22 @@ DK_API int dk_dwconv_wgrad_f32(const float* dy, const float* x, int N, int H, in
 // Fused stride-1 backward (dw_bwd_fused_kernel).  Workspace: the weight-gradient partials.
 DK_API int dk_dwconv_bwd_bnbwd_stats_rows(int N, int H, int W, int C) {
   (void)H;
-  return (C < 4 || C % 4) ? 0 : dwb_strips(N, W, C, dwb_cl(W, C));
+  return (C < 4 || C % 4) ? 0 : dwb_strips(N, W, C, dwb_geom(W, C, dwb_cpt(4)));
 }
+// (the join entry dk_dwconv_bwd_bnbwd_join_f32 has the fp32 geometry: these rows)
 
 DK_API size_t dk_dwconv_bwd_bnbwd_workspace_bytes(int N, int H, int W, int C, int R, int S) {
   return (size_t)dk_dwconv_bwd_bnbwd_stats_rows(N, H, W, C) * C * R * S * sizeof(float);
+}
+
+// bf16 storage: its block geometry may differ (two columns per thread, dwb_geom)
+DK_API int dk_dwconv_bwd_bnbwd_bf16_stats_rows(int N, int H, int W, int C) {
+  (void)H;
+  return (C < 4 || C % 4) ? 0 : dwb_strips(N, W, C, dwb_geom(W, C, dwb_cpt(2), dwb_nt(2)));
+}
+
+DK_API size_t dk_dwconv_bwd_bnbwd_bf16_workspace_bytes(int N, int H, int W, int C, int R, int S) {
+  return (size_t)dk_dwconv_bwd_bnbwd_bf16_stats_rows(N, H, W, C) * C * R * S * sizeof(float);
 }
 
 namespace dk {
@@ -1513,7 +1795,8 @@ static int dw_bwd_fused(const T* g, const T* bn_x, int N, int H, int W, int C, c
                         size_t ws_bytes, void* stream) {
   const hipStream_t st = as_stream(stream);
   if (R != 3 || S != 3 || pad != 1 || C % 4 || N < 1 || H < 1 || W < 1) return DK_ERR_ARGS;
-  const int cl = dwb_cl(W, C);
+  const DwbGeom geo = dwb_geom(W, C, dwb_cpt(sizeof(T)), dwb_nt(sizeof(T)));
+  const int cl = geo.cl;
   if (!g || !bn_x || !x || !w_crs || !dw_crs || !out_mean || !out_invstd || !out_gamma || !out_beta || !k12)
     return DK_ERR_ARGS;
   const BnIn bn{bn_mean, bn_invstd, bn_gamma, bn_beta, bn_relu};
@@ -1524,25 +1807,30 @@ static int dw_bwd_fused(const T* g, const T* bn_x, int N, int H, int W, int C, c
     return DK_ERR_ARGS;
   const size_t bytes = (size_t)N * H * W * C * sizeof(T);
   if (!fits(bytes)) return DK_ERR_ARGS;
-  if (ws_bytes < dk_dwconv_bwd_bnbwd_workspace_bytes(N, H, W, C, R, S)) return DK_ERR_WORKSPACE;
-  const int strips = dwb_strips(N, W, C, cl);
-  const int nranges = dwb_nranges(N, W, C, cl);
-  const int ncht = (C / 4) / (256 / cl);
+  const size_t need = sizeof(T) == 2 ? dk_dwconv_bwd_bnbwd_bf16_workspace_bytes(N, H, W, C, R, S)
+                                      : dk_dwconv_bwd_bnbwd_workspace_bytes(N, H, W, C, R, S);
+  if (ws_bytes < need) return DK_ERR_WORKSPACE;
+  const int strips = dwb_strips(N, W, C, geo);
+  const int nranges = dwb_nranges(N, W, C, geo);
+  const int ncht = (C / 4) / geo.cg;
   float* wpart = static_cast<float*>(ws);
   const BnBwdOut ob{out_mean, out_invstd, out_gamma, out_beta, k12, out_relu};
   const dim3 grid((unsigned)(strips * ncht));
   FoldTail ft;  // an armed in-launch fold of the input BN's partial rows (fold_tail.h)
   if (!part || !fold_take(part, strips, C, ncht, &ft)) ft.part = nullptr;
-  size_t shm = (size_t)256 * 9 * 4 * sizeof(float);  // the weight-gradient reduction
-  const size_t ring = (size_t)2 * (cl + 2) * (256 / cl) * sizeof(f32x4);
+  size_t shm = (size_t)geo.nt * 9 * 4 * sizeof(float);  // the weight-gradient reduction
+  const size_t ring = (size_t)2 * (cl + 2) * geo.cg * sizeof(f32x4);
   if (ring > shm) shm = ring;
+  // two columns per thread (knob 21)
+  constexpr int CPT2 = 2;
 #define DWB_LAUNCH(BNX_, STATS_, RELU1_)                                                                             \
   {                                                                                                                  \
-    auto k = dw_bwd_fused_kernel<BNX_, STATS_, RELU1_, false, T>;                                                    \
+    auto k = geo.cpt == 2 ? dw_bwd_fused_kernel<BNX_, STATS_, RELU1_, false, T, CPT2>                              \
+                          : dw_bwd_fused_kernel<BNX_, STATS_, RELU1_, false, T>;                                   \
     if (shm > 65536)                                                                                                 \
       (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,       \
                                 (int)shm);                                                                           \
-    hipLaunchKernelGGL(k, grid, dim3(256), shm, st, g, bn_x, (uint32_t)bytes, ob, x, bn, w_crs, dx, residual, part,  \
+    hipLaunchKernelGGL(k, grid, dim3(geo.nt), shm, st, g, bn_x, (uint32_t)bytes, ob, x, bn, w_crs, dx, residual, part,  \
                        wpart, N, H, W, C, cl, ft, JoinBwd{}, nt_stores(kNtDwBwd), nranges);                                                        \
   }
   if (out_relu) {
@@ -1615,6 +1903,151 @@ DK_API int dk_dwconv_dgrad_join_f32(const float* dy, int N, int OH, int OW, int 
                          BnIn{}, part, as_stream(stream), &jn);
 }
 
+// ---- fused stride-2 depthwise backward (dw_bwd_s2_kernel) ----
+namespace dk {
+static int dws2_blocks(int N, int H, int W, int C) {
+  const int C4 = C / 4, IPB = 256 / C4;
+  const long long items = (long long)N * ((H + 1) / 2) * ((((W + 1) / 2) + 1) / 2);
+  long long b = (items + IPB - 1) / IPB;
+  const int target = knob(kKnobDwbBlocks) * 2 / 3;  // two resident blocks per CU
+  if (target > 0 && b > target) b = target;
+  return b < 1 ? 1 : (int)b;
+}
+static bool dws2_ok(int N, int H, int W, int C, int OH, int OW) {
+  return N >= 1 && H >= 1 && W >= 1 && C >= 4 && C % 4 == 0 && 256 % (C / 4) == 0 && OH == (H + 1) / 2 &&
+         OW == (W + 1) / 2;
+}
+}  // namespace dk
+
+DK_API int dk_dwconv_bwd_s2_stats_rows(int N, int H, int W, int C) {
+  return dk::dws2_ok(N, H, W, C, (H + 1) / 2, (W + 1) / 2) ? dk::dws2_blocks(N, H, W, C) : 0;
+}
+
+DK_API size_t dk_dwconv_bwd_s2_workspace_bytes(int N, int H, int W, int C) {
+  return (size_t)dk_dwconv_bwd_s2_stats_rows(N, H, W, C) * C * 9 * sizeof(float);
+}
+
+namespace dk {
+template <class T>
+static int dw_bwd_s2(const T* g, const T* bn_x, int N, int H, int W, int C, int OH, int OW, const float* out_mean,
+                     const float* out_invstd, const float* out_gamma, const float* out_beta, int out_relu,
+                     const float* k12, const T* x, const float* w_crs, float l2, float* dw_crs, T* dx,
+                     const T* residual, const float* bn_mean, const float* bn_invstd, const float* bn_gamma,
+                     const float* bn_beta, int bn_relu, double* part, void* ws, size_t ws_bytes, void* stream) {
+  const hipStream_t st = as_stream(stream);
+  if (!dws2_ok(N, H, W, C, OH, OW)) return DK_ERR_ARGS;
+  if (!g || !bn_x || !x || !w_crs || !dw_crs || !out_mean || !out_invstd || !out_gamma || !out_beta || !k12)
+    return DK_ERR_ARGS;
+  const BnIn bn{bn_mean, bn_invstd, bn_gamma, bn_beta, bn_relu};
+  if (part && !bn_mean) return DK_ERR_ARGS;
+  if (!aligned16(out_mean) || !aligned16(out_invstd) || !aligned16(out_gamma) || !aligned16(out_beta) ||
+      !aligned16(k12) || !bn_ok(bn) || ((reinterpret_cast<uintptr_t>(g) | reinterpret_cast<uintptr_t>(bn_x) |
+                                          reinterpret_cast<uintptr_t>(x)) & (4 * sizeof(T) - 1)))
+    return DK_ERR_ARGS;
+  const size_t xb = (size_t)N * H * W * C * sizeof(T), yb = (size_t)N * OH * OW * C * sizeof(T);
+  if (!fits(xb)) return DK_ERR_ARGS;
+  if (ws_bytes < dk_dwconv_bwd_s2_workspace_bytes(N, H, W, C)) return DK_ERR_WORKSPACE;
+  const int blocks = dws2_blocks(N, H, W, C);
+  float* wpart = static_cast<float*>(ws);
+  const BnBwdOut ob{out_mean, out_invstd, out_gamma, out_beta, k12, out_relu};
+  FoldTail ft;
+  if (!part || !fold_take(part, blocks, C, 1, &ft)) ft.part = nullptr;
+  const size_t shm = (size_t)256 * 9 * 4 * sizeof(float);
+#define DWS2_LAUNCH(BNX_, STATS_, RELU1_)                                                                           \
+  hipLaunchKernelGGL((dw_bwd_s2_kernel<BNX_, STATS_, RELU1_, T>), dim3(blocks), dim3(256), shm, st, g, bn_x,       \
+                     (uint32_t)yb, ob, x, (uint32_t)xb, bn, w_crs, dx, residual, part, wpart, N, H, W, C, OH, OW, ft, \
+                     nt_stores(kNtDwDgrad))
+  if (out_relu) {
+    if (part) DWS2_LAUNCH(true, true, true); else if (bn_mean) DWS2_LAUNCH(true, false, true);
+    else DWS2_LAUNCH(false, false, true);
+  } else {
+    if (part) DWS2_LAUNCH(true, true, false); else if (bn_mean) DWS2_LAUNCH(true, false, false);
+    else DWS2_LAUNCH(false, false, false);
+  }
+#undef DWS2_LAUNCH
+  int rc = launch_status();
+  if (rc) return rc;
+  return fold_status(wgrad_reduce(wpart, blocks, 1, C * 9, dw_crs, l2 != 0.f ? w_crs : nullptr, l2, st), ft);
+}
+}  // namespace dk
+
+// Fused stride-2 depthwise backward (3x3, pad 1): as dk_dwconv_bwd_bnbwd_f32 for a stride-2 layer.
+// g / bn_x: the following BatchNorm's output gradient and raw input (N x OH x OW x C); x: this
+// layer's input (N x H x W x C) with the input BN bn_* applied on load (bn_mean NULL: none); dx
+// (NULL: weight gradient only) gets dgrad (+ residual); part: the input BN's stage-1 partials,
+// dk_dwconv_bwd_s2_stats_rows rows.  OH = ceil(H / 2), OW = ceil(W / 2); C / 4 divides 256.
+DK_API int dk_dwconv_bwd_s2_bnbwd_f32(const float* g, const float* bn_x, int N, int H, int W, int C, int OH, int OW,
+                                      const float* out_mean, const float* out_invstd, const float* out_gamma,
+                                      const float* out_beta, int out_relu, const float* k12, const float* x,
+                                      const float* w_crs, float l2, float* dw_crs, float* dx, const float* residual,
+                                      const float* bn_mean, const float* bn_invstd, const float* bn_gamma,
+                                      const float* bn_beta, int bn_relu, double* part, void* ws, size_t ws_bytes,
+                                      void* stream) {
+  return dk::dw_bwd_s2(g, bn_x, N, H, W, C, OH, OW, out_mean, out_invstd, out_gamma, out_beta, out_relu, k12, x,
+                       w_crs, l2, dw_crs, dx, residual, bn_mean, bn_invstd, bn_gamma, bn_beta, bn_relu, part, ws,
+                       ws_bytes, stream);
+}
+
+// The join form (fp32): x is a residual block's output y = ReLU(bn_j(join_x) + skip), no input BN;
+// dx = (dgrad + residual) * (y > 0) and part (dk_dwconv_bwd_s2_stats_rows x 2 x C, required) gets
+// stage 1 of bn_j's backward (dk_dwconv_dgrad_join_f32's work on the stride-2 path).
+// residual_lattice = 2: the residual is the compact stride-2 lattice [N][OH][OW][C] (0: dense).
+DK_API int dk_dwconv_bwd_s2_bnbwd_join_f32(const float* g, const float* bn_x, int N, int H, int W, int C, int OH,
+                                           int OW, const float* out_mean, const float* out_invstd,
+                                           const float* out_gamma, const float* out_beta, int out_relu,
+                                           const float* k12, const float* x, const float* w_crs, float l2,
+                                           float* dw_crs, float* dx, const float* residual, int residual_lattice,
+                                           const float* join_x, const float* join_mean, const float* join_invstd,
+                                           double* part, void* ws, size_t ws_bytes, void* stream) {
+  using namespace dk;
+  const hipStream_t st = as_stream(stream);
+  if (!dws2_ok(N, H, W, C, OH, OW) || (residual_lattice != 0 && residual_lattice != 2)) return DK_ERR_ARGS;
+  if (!g || !bn_x || !x || !w_crs || !dw_crs || !dx || !out_mean || !out_invstd || !out_gamma || !out_beta || !k12 ||
+      !join_x || !join_mean || !join_invstd || !part)
+    return DK_ERR_ARGS;
+  if (!aligned16(out_mean) || !aligned16(out_invstd) || !aligned16(out_gamma) || !aligned16(out_beta) ||
+      !aligned16(k12) || !aligned16(g) || !aligned16(bn_x) || !aligned16(x) || !aligned16(dx) ||
+      !aligned16(join_x) || !aligned16(join_mean) || !aligned16(join_invstd) || (residual && !aligned16(residual)))
+    return DK_ERR_ARGS;
+  const size_t xb = (size_t)N * H * W * C * sizeof(float), yb = (size_t)N * OH * OW * C * sizeof(float);
+  if (!fits(xb)) return DK_ERR_ARGS;
+  if (ws_bytes < dk_dwconv_bwd_s2_workspace_bytes(N, H, W, C)) return DK_ERR_WORKSPACE;
+  const int blocks = dws2_blocks(N, H, W, C);
+  float* wpart = static_cast<float*>(ws);
+  const BnBwdOut ob{out_mean, out_invstd, out_gamma, out_beta, k12, out_relu};
+  JoinBwd jn{};
+  jn.x = join_x;
+  jn.mean = join_mean;
+  jn.invstd = join_invstd;
+  jn.res_lat = residual && residual_lattice == 2;
+  FoldTail ft;
+  if (!fold_take(part, blocks, C, 1, &ft)) ft.part = nullptr;
+  const size_t shm = (size_t)256 * 9 * 4 * sizeof(float);
+  if (out_relu)
+    hipLaunchKernelGGL((dw_bwd_s2_kernel<false, false, true, float, true>), dim3(blocks), dim3(256), shm, st, g, bn_x,
+                       (uint32_t)yb, ob, x, (uint32_t)xb, BnIn{}, w_crs, dx, residual, part, wpart, N, H, W, C, OH, OW,
+                       ft, nt_stores(kNtDwDgrad), jn);
+  else
+    hipLaunchKernelGGL((dw_bwd_s2_kernel<false, false, false, float, true>), dim3(blocks), dim3(256), shm, st, g,
+                       bn_x, (uint32_t)yb, ob, x, (uint32_t)xb, BnIn{}, w_crs, dx, residual, part, wpart, N, H, W, C,
+                       OH, OW, ft, nt_stores(kNtDwDgrad), jn);
+  int rc = launch_status();
+  if (rc) return rc;
+  return fold_status(wgrad_reduce(wpart, blocks, 1, C * 9, dw_crs, l2 != 0.f ? w_crs : nullptr, l2, st), ft);
+}
+
+DK_API int dk_dwconv_bwd_s2_bnbwd_bf16(const bf16_t* g, const bf16_t* bn_x, int N, int H, int W, int C, int OH,
+                                       int OW, const float* out_mean, const float* out_invstd, const float* out_gamma,
+                                       const float* out_beta, int out_relu, const float* k12, const bf16_t* x,
+                                       const float* w_crs, float l2, float* dw_crs, bf16_t* dx,
+                                       const bf16_t* residual, const float* bn_mean, const float* bn_invstd,
+                                       const float* bn_gamma, const float* bn_beta, int bn_relu, double* part,
+                                       void* ws, size_t ws_bytes, void* stream) {
+  return dk::dw_bwd_s2(g, bn_x, N, H, W, C, OH, OW, out_mean, out_invstd, out_gamma, out_beta, out_relu, k12, x,
+                       w_crs, l2, dw_crs, dx, residual, bn_mean, bn_invstd, bn_gamma, bn_beta, bn_relu, part, ws,
+                       ws_bytes, stream);
+}
+
 // dk_dwconv_bwd_bnbwd_f32 for a layer whose input is a residual join's output (no input BN): dx
 // is the gradient w.r.t. the join's pre-ReLU sum, dx = (dgrad + residual) * join_mask, and part
 // (stats_rows x 2 x C) gets stage 1 of the backward of the join's BatchNorm (join_x: its raw
@@ -1629,7 +2062,8 @@ DK_API int dk_dwconv_bwd_bnbwd_join_f32(const float* g, const float* bn_x, int N
                                         size_t ws_bytes, void* stream) {
   const hipStream_t st = as_stream(stream);
   if (R != 3 || S != 3 || pad != 1 || C % 4 || N < 1 || H < 1 || W < 1) return DK_ERR_ARGS;
-  const int cl = dwb_cl(W, C);
+  const DwbGeom geo = dwb_geom(W, C, dwb_cpt(4));
+  const int cl = geo.cl;
   if (!g || !bn_x || !x || !w_crs || !dw_crs || !dx || !out_mean || !out_invstd || !out_gamma || !out_beta ||
       !k12 || !join_x || !join_mean || !join_invstd || !part)
     return DK_ERR_ARGS;
@@ -1641,9 +2075,9 @@ DK_API int dk_dwconv_bwd_bnbwd_join_f32(const float* g, const float* bn_x, int N
   const size_t bytes = (size_t)N * H * W * C * sizeof(float);
   if (!fits(bytes)) return DK_ERR_ARGS;
   if (ws_bytes < dk_dwconv_bwd_bnbwd_workspace_bytes(N, H, W, C, R, S)) return DK_ERR_WORKSPACE;
-  const int strips = dwb_strips(N, W, C, cl);
-  const int nranges = dwb_nranges(N, W, C, cl);
-  const int ncht = (C / 4) / (256 / cl);
+  const int strips = dwb_strips(N, W, C, geo);
+  const int nranges = dwb_nranges(N, W, C, geo);
+  const int ncht = (C / 4) / geo.cg;
   float* wpart = static_cast<float*>(ws);
   const BnBwdOut ob{out_mean, out_invstd, out_gamma, out_beta, k12, out_relu};
   const JoinBwd jn{join_mask, join_x, join_mean, join_invstd};
@@ -1651,11 +2085,12 @@ DK_API int dk_dwconv_bwd_bnbwd_join_f32(const float* g, const float* bn_x, int N
   FoldTail ft;  // an armed in-launch fold of the join BN's partial rows (fold_tail.h)
   if (!fold_take(part, strips, C, ncht, &ft)) ft.part = nullptr;
   size_t shm = (size_t)256 * 9 * 4 * sizeof(float);
-  const size_t ring = (size_t)2 * (cl + 2) * (256 / cl) * sizeof(f32x4);
+  const size_t ring = (size_t)2 * (cl + 2) * geo.cg * sizeof(f32x4);
   if (ring > shm) shm = ring;
 #define DWJ_LAUNCH(RELU1_)                                                                                           \
   {                                                                                                                  \
-    auto k = dw_bwd_fused_kernel<false, false, RELU1_, true>;                                                        \
+    auto k = geo.cpt == 2 ? dw_bwd_fused_kernel<false, false, RELU1_, true, float, 2>                               \
+                          : dw_bwd_fused_kernel<false, false, RELU1_, true>;                                        \
     if (shm > 65536)                                                                                                 \
       (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,       \
                                 (int)shm);                                                                           \

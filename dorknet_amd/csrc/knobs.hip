@@ -44,6 +44,7 @@ constexpr KnobDef kDefs[kNumKnobs] = {
     {nullptr, 22},                       // kKnobEwVariant: launch variant of dk_bn_bwd_apply_f32
     {"DORKNET_PW_BF16_BWD", 1},          // kKnobPwsh16Bwd: fused bf16 pointwise backward (1: K = C = 64 and
                                           // K in {128, 256}; 2: K = C = 64 only; 0: off)
+    {"DORKNET_DWB_COLS", 2},             // kKnobDwbCols: columns per thread of the fused depthwise backward
 };
 
 struct Table {

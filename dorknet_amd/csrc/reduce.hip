@@ -193,7 +193,8 @@ int wgrad_reduce(const float* ws, int splits, int M, int N, float* out, const fl
 }  // namespace dk
 
 // Deferred weight-gradient reduce.  mode 1: the fused backward entry points called next on this
-// host thread (dk_dwconv_bwd_bnbwd_f32 / _bf16 / _join_f32, dk_pwconv_bwd_bnbwd_f32) leave their
+// host thread (dk_dwconv_bwd_bnbwd_f32 / _bf16 / _join_f32, dk_dwconv_bwd_s2_bnbwd_*,
+// dk_pwconv_bwd_bnbwd_f32 / _bf16) leave their
 // weight-gradient partial slab unreduced and record the reduce; mode 0: back to reducing in the
 // entry point (a recorded reduce stays for dk_wgrad_reduce_flush); mode -1: as 0 and drop it.
 DK_API int dk_wgrad_reduce_defer(int mode) {

@@ -148,8 +148,9 @@ class DepthwiseConvLayer(Layer):
 
     def accepts_bn_grad(self, bn_layer):
         """backward(BNGrad): the following BatchNorm's apply, this layer's dgrad and its weight
-        gradient run as one pass (dk_dwconv_bwd_bnbwd_f32) -- fp32, stride 1, 3x3 'same'
-        padding, no bias, C % 4 == 0."""
+        gradient run as one pass -- 3x3, padding 1, no bias, C % 4 == 0: stride 1
+        (dk_dwconv_bwd_bnbwd_f32 / _bf16) and stride 2 (dk_dwconv_bwd_s2_bnbwd_f32 / _bf16, C / 4
+        dividing 256; DORKNET_DW_S2_FUSED=0 turns it off)."""
         bx = getattr(bn_layer, "X", None)
         return getattr(self, "X", None) is not None and bx is not None and self._takes_bn_grad(bx)
 
@@ -157,9 +158,13 @@ class DepthwiseConvLayer(Layer):
         x = self.X
         if x.dim() != 4 or bx.dim() != 4 or x.dtype not in (torch.float32, BF16) or bx.dtype != x.dtype:
             return False
-        C = x.shape[1]
-        return (self.stride == 1 and self.f_rows == 3 and self.f_cols == 3 and self.padding == 1
-                and not self.with_bias and C % 4 == 0 and tuple(bx.shape) == tuple(x.shape))
+        N, C, H, W = x.shape
+        if not (self.f_rows == 3 and self.f_cols == 3 and self.padding == 1 and not self.with_bias and C % 4 == 0):
+            return False
+        if self.stride == 2:
+            return (getenv("DORKNET_DW_S2_FUSED", "1") != "0" and 256 % (C // 4) == 0
+                    and tuple(bx.shape) == (N, C, (H + 1) // 2, (W + 1) // 2))
+        return self.stride == 1 and tuple(bx.shape) == tuple(x.shape)
 
     accepts_join = True  # backward(BNGrad, residual=R, join=relu): the input's residual join rides on dx
 
@@ -210,6 +215,8 @@ class DepthwiseConvLayer(Layer):
         res = residual_operand(residual, dx) if need_dx else None
         if need_dx and residual is not None and res is None:
             res = residual_operand(to_nhwc(residual), dx)
+        if self.stride == 2:
+            return self._backward_bn_grad_s2(G, res, residual, need_dx, dx, gw, s, w)
         if join is not None and self._join_ok(join, need_dx):
             jb = join._join_bn
             rows = lib.dk_dwconv_bwd_bnbwd_stats_rows(N, H, W, C)
@@ -242,12 +249,13 @@ class DepthwiseConvLayer(Layer):
                     self.layer_name))
             return dx
         part = None
+        bf = x.dtype == BF16
         if need_dx and bn is not None:
-            rows = lib.dk_dwconv_bwd_bnbwd_stats_rows(N, H, W, C)
+            rows = (lib.dk_dwconv_bwd_bnbwd_bf16_stats_rows if bf else lib.dk_dwconv_bwd_bnbwd_stats_rows)(N, H, W, C)
             part = torch.empty((rows, 2, C), dtype=torch.float64, device=x.device)
         g = to_nhwc(G.g)
-        nb = lib.dk_dwconv_bwd_bnbwd_workspace_bytes(N, H, W, C, R, S)
-        bf = x.dtype == BF16
+        nb = (lib.dk_dwconv_bwd_bnbwd_bf16_workspace_bytes if bf else lib.dk_dwconv_bwd_bnbwd_workspace_bytes)(
+            N, H, W, C, R, S)
         tok = bn.arm_partials(part) if part is not None else None
         red = deferred_wgrad_reduce(self, nb, s is not None)
         with red:
@@ -266,10 +274,44 @@ class DepthwiseConvLayer(Layer):
             dx = add_residual(dx, residual)  # (a new tensor: the BN then recomputes its sums)
         return dx
 
+    def _backward_bn_grad_s2(self, G, res, residual, need_dx, dx, gw, s, w):
+        """The stride-2 form of _backward_bn_grad (dk_dwconv_bwd_s2_bnbwd_*): dx (+ the residual,
+        + the input BatchNorm's backward partial sums) and the weight gradient, dy never written."""
+        st = stream_handle()
+        x = self.X
+        N, C, H, W = x.shape
+        OH, OW = (H + 1) // 2, (W + 1) // 2
+        bn = self._bn_in
+        bf = x.dtype == BF16
+        if need_dx and residual is not None and res is None:
+            raise NotImplementedError("{}: the fused stride-2 backward needs an NHWC residual".format(self.layer_name))
+        part = None
+        if need_dx and bn is not None:
+            part = torch.empty((lib.dk_dwconv_bwd_s2_stats_rows(N, H, W, C), 2, C), dtype=torch.float64,
+                               device=x.device)
+        g = to_nhwc(G.g)
+        nb = lib.dk_dwconv_bwd_s2_workspace_bytes(N, H, W, C)
+        tok = bn.arm_partials(part) if part is not None else None
+        red = deferred_wgrad_reduce(self, nb, s is not None)
+        with red:
+            r = (lib.dk_dwconv_bwd_s2_bnbwd_bf16 if bf else lib.dk_dwconv_bwd_s2_bnbwd_f32)(
+                g.data_ptr(), G.x.data_ptr(), N, H, W, C, OH, OW, *G.bnbwd_args(), x.data_ptr(), w.data_ptr(),
+                s or 0.0, gw.data_ptr(), ptr(dx), ptr(res),
+                *(bn.bn_args() if bn is not None else (0, 0, 0, 0, 0)), ptr(part), red.ws, nb, st)
+        red.flush()
+        if s is None:
+            add_regulariser_grad(gw, w, self.weight_regulariser)
+        if not need_dx:
+            return None
+        if part is not None:
+            bn.hand_backward_partials(dx, part, r, tok)
+        return dx
+
     def backward(self, upstream_dx, residual=None, need_dx=True, join=None):
         self._require_on_gpu()
         if isinstance(upstream_dx, BNGrad):
-            if self._takes_bn_grad(upstream_dx.x):
+            # (the stride-2 form has no join operand: a join's backward stays with the join dgrad)
+            if self._takes_bn_grad(upstream_dx.x) and not (self.stride == 2 and join is not None):
                 return self._backward_bn_grad(upstream_dx, residual, need_dx, join)
             upstream_dx = upstream_dx.materialize()
         st = stream_handle()

@@ -72,7 +72,9 @@ int dk_mixup_f32(const float* a, const float* b, long long n, float p, float one
  * CU (0 = occupancy) (DORKNET_PWF_PREFETCH / DORKNET_PWF_BLOCKS_PER_CU);
  * kind 18: blocks a split-K weight gradient aims for (DORKNET_WGRAD_BLOCKS, default 1024);
  * kind 20: the fused bf16 pointwise backward (DORKNET_PW_BF16_BWD: 1 = K = C = 64 and K in {128, 256},
- * 2 = K = C = 64 only, 0 = off). */
+ * 2 = K = C = 64 only, 0 = off);
+ * kind 21: output columns per thread of the fused stride-1 depthwise backward (DORKNET_DWB_COLS: 2 =
+ * default where the width allows, 1 = one); the dk_dwconv_bwd_bnbwd*_stats_rows / _workspace_bytes follow it. */
 int dk_debug_set_gemm_config(int kind, int cfg);
 
 /* Bandwidth ceiling probe (not on the training path; scripts/stream_ceiling.py): reads nin
@@ -272,7 +274,12 @@ int dk_pwconv_dgrad_bnbwd_bf16(const uint16_t* g, const uint16_t* bn_x, int N, i
 int dk_pwconv_bwd_fused_bf16_rows(int N, int OH, int OW, int K, int C);
 size_t dk_pwconv_bwd_fused_bf16_workspace_bytes(int N, int OH, int OW, int K, int C);
 int dk_pwconv_bwd_bnbwd_bf16(const uint16_t* g, const uint16_t* bn_x, int N, int OH, int OW, int K, const float* out_mean, const float* out_invstd, const float* out_gamma, const float* out_beta, int out_relu, const float* k12, const float* w_kc, int C, float l2, float* dw_kc, uint16_t* dx, const uint16_t* residual, const uint16_t* x, const float* bn_mean, const float* bn_invstd, const float* bn_gamma, const float* bn_beta, int bn_relu, double* part, void* ws, size_t ws_bytes, void* stream);
-int dk_dwconv_bwd_bnbwd_bf16(const uint16_t* g, const uint16_t* bn_x, int N, int H, int W, int C, const float* out_mean, const float* out_invstd, const float* out_gamma, const float* out_beta, int out_relu, const float* k12, const uint16_t* x, const float* w_crs, int R, int S, int pad, float l2, float* dw_crs, uint16_t* dx, const uint16_t* residual, const float* bn_mean, const float* bn_invstd, const float* bn_gamma, const float* bn_beta, int bn_relu, double* part, void* ws, size_t ws_bytes, void* stream);int dk_dwconv_wgrad_bnx_bf16(const uint16_t* dy, const uint16_t* x, int N, int H, int W, int C, int R, int S, int stride, int pad, int OH, int OW, const float* w_crs, float l2, float* dw_crs, void* ws, size_t ws_bytes, const float* bn_mean, const float* bn_invstd, const float* bn_gamma, const float* bn_beta, int bn_relu, void* stream);
+int dk_dwconv_bwd_bnbwd_bf16(const uint16_t* g, const uint16_t* bn_x, int N, int H, int W, int C, const float* out_mean, const float* out_invstd, const float* out_gamma, const float* out_beta, int out_relu, const float* k12, const uint16_t* x, const float* w_crs, int R, int S, int pad, float l2, float* dw_crs, uint16_t* dx, const uint16_t* residual, const float* bn_mean, const float* bn_invstd, const float* bn_gamma, const float* bn_beta, int bn_relu, double* part, void* ws, size_t ws_bytes, void* stream);
+/* rows / workspace of dk_dwconv_bwd_bnbwd_bf16 (its block geometry: two output columns per thread
+ * where the width allows, knob 21) */
+int dk_dwconv_bwd_bnbwd_bf16_stats_rows(int N, int H, int W, int C);
+size_t dk_dwconv_bwd_bnbwd_bf16_workspace_bytes(int N, int H, int W, int C, int R, int S);
+int dk_dwconv_wgrad_bnx_bf16(const uint16_t* dy, const uint16_t* x, int N, int H, int W, int C, int R, int S, int stride, int pad, int OH, int OW, const float* w_crs, float l2, float* dw_crs, void* ws, size_t ws_bytes, const float* bn_mean, const float* bn_invstd, const float* bn_gamma, const float* bn_beta, int bn_relu, void* stream);
 
 /* ---------------------------------------------------------------------------------------
  * Depthwise convolution, direct (no MFMA).
@@ -317,6 +324,21 @@ int dk_dwconv_bwd_bnbwd_join_f32(const float* g, const float* bn_x, int N, int H
  * residual_lattice = stride: the residual is the skip projection's un-widened gradient, compact on the
  * stride lattice ([N][ceil(H/s)][ceil(W/s)][C], zero elsewhere); 0: dense [N][H][W][C]. */
 int dk_dwconv_dgrad_join_rows(int N, int H, int W, int C, int R, int S, int stride, int pad);
+/* Fused stride-2 depthwise backward (3x3, pad 1): dk_dwconv_bwd_bnbwd_f32's one pass for a stride-2
+ * layer (replaces dk_bn_bwd_apply -> dk_dwconv_dgrad_ex + dk_dwconv_wgrad_bnx; batch_norm.py:125-174
+ * stage 3, depthwise_convolution.py:198-221).  g / bn_x: the following BN's output gradient and raw
+ * input, N x OH x OW x C (OH = ceil(H / 2), OW = ceil(W / 2)); x: this layer's input N x H x W x C
+ * with bn_* applied on load (bn_mean NULL: none); dx (NULL: weight gradient only) = dgrad
+ * (+ residual); part (needs bn_*): that input BN's backward partials, dk_dwconv_bwd_s2_stats_rows
+ * rows [rows][2][C].  C / 4 must divide 256.  dx is bit-identical to the unfused sequence (fp32). */
+int dk_dwconv_bwd_s2_stats_rows(int N, int H, int W, int C);
+size_t dk_dwconv_bwd_s2_workspace_bytes(int N, int H, int W, int C);
+int dk_dwconv_bwd_s2_bnbwd_f32(const float* g, const float* bn_x, int N, int H, int W, int C, int OH, int OW, const float* out_mean, const float* out_invstd, const float* out_gamma, const float* out_beta, int out_relu, const float* k12, const float* x, const float* w_crs, float l2, float* dw_crs, float* dx, const float* residual, const float* bn_mean, const float* bn_invstd, const float* bn_gamma, const float* bn_beta, int bn_relu, double* part, void* ws, size_t ws_bytes, void* stream);
+/* The join form (fp32): x = a residual block's output y = ReLU(bn_j(join_x) + skip) (no input BN):
+ * dx = (dgrad + residual) * (y > 0), part (required) = stage 1 of bn_j's backward over dx;
+ * residual_lattice 2: the residual is the compact stride-2 lattice N x OH x OW x C (0: dense). */
+int dk_dwconv_bwd_s2_bnbwd_join_f32(const float* g, const float* bn_x, int N, int H, int W, int C, int OH, int OW, const float* out_mean, const float* out_invstd, const float* out_gamma, const float* out_beta, int out_relu, const float* k12, const float* x, const float* w_crs, float l2, float* dw_crs, float* dx, const float* residual, int residual_lattice, const float* join_x, const float* join_mean, const float* join_invstd, double* part, void* ws, size_t ws_bytes, void* stream);
+int dk_dwconv_bwd_s2_bnbwd_bf16(const uint16_t* g, const uint16_t* bn_x, int N, int H, int W, int C, int OH, int OW, const float* out_mean, const float* out_invstd, const float* out_gamma, const float* out_beta, int out_relu, const float* k12, const uint16_t* x, const float* w_crs, float l2, float* dw_crs, uint16_t* dx, const uint16_t* residual, const float* bn_mean, const float* bn_invstd, const float* bn_gamma, const float* bn_beta, int bn_relu, double* part, void* ws, size_t ws_bytes, void* stream);
 int dk_dwconv_dgrad_join_f32(const float* dy, int N, int OH, int OW, int C, const float* w_crs, int R, int S, int stride, int pad, float* dx, int H, int W, void* ws, size_t ws_bytes, const float* residual, int residual_lattice, const uint8_t* join_mask, const float* join_x, const float* join_mean, const float* join_invstd, double* part, void* stream);
 
 /* ---------------------------------------------------------------------------------------

@@ -106,7 +106,7 @@ def _stack_layers(units, seed):
     return layers, rng
 
 
-def _run_segment(units, in_shape, seed, monkeypatch):
+def _run_segment(units, in_shape, seed, monkeypatch, expect=()):
     from dorknet_amd.network.feed_forward_network import FeedForwardNetwork
     from tests.test_gpu_fullsize import Calls
     layers, rng = _stack_layers(units, seed)
@@ -117,7 +117,8 @@ def _run_segment(units, in_shape, seed, monkeypatch):
         net.add_layer(l)
     net.to_gpu()
     calls = Calls(monkeypatch, ["dk_pwconv_fwd_ex_bf16", "dk_pwconv_dgrad_ex_bf16", "dk_pwconv_wgrad_bnx_bf16",
-                                "dk_dwconv_fwd_ex_bf16", "dk_dwconv_dgrad_ex_bf16", "dk_dwconv_wgrad_bnx_bf16"])
+                                "dk_dwconv_fwd_ex_bf16", "dk_dwconv_dgrad_ex_bf16", "dk_dwconv_wgrad_bnx_bf16",
+                                "dk_dwconv_bwd_s2_bnbwd_bf16"])
     X = torch.randn(in_shape, generator=torch.Generator().manual_seed(seed)).to(BF16)
     Xd = X.to("cuda").contiguous(memory_format=torch.channels_last)
     _, Y = net.forward(Xd, None)
@@ -125,7 +126,7 @@ def _run_segment(units, in_shape, seed, monkeypatch):
     dY = torch.randn(tuple(Y.shape), generator=torch.Generator().manual_seed(seed + 2)).to(BF16)
     net.backward(dY.to("cuda").contiguous(memory_format=torch.channels_last))
     torch.cuda.synchronize()
-    assert {"dk_pwconv_fwd_ex_bf16", "dk_pwconv_dgrad_ex_bf16", "dk_pwconv_wgrad_bnx_bf16"} <= calls.seen, calls.seen
+    assert {"dk_pwconv_fwd_ex_bf16"} | set(expect) <= calls.seen, calls.seen
     Yg = Y.float().cpu().numpy().astype(np.float64)
     grads = {(l.layer_name, k): l.grads[k].float().cpu().numpy().astype(np.float64)
              for l in layers for k in sorted(l.grads or {})}
@@ -155,7 +156,8 @@ def test_config5_first_unit_bs512(monkeypatch):
 
 
 def test_config5_strided_unit_bs512(monkeypatch):
-    _run_segment((4, 5), (512, 64, 56, 56), 53, monkeypatch)
+    # the stride-2 depthwise backward runs fused (dk_dwconv_bwd_s2_bnbwd_bf16: dy never stored)
+    _run_segment((4, 5), (512, 64, 56, 56), 53, monkeypatch, expect=["dk_dwconv_bwd_s2_bnbwd_bf16"])
 
 
 def test_config5_last_two_units_bs512(monkeypatch):
