@@ -1218,7 +1218,7 @@ __global__ __launch_bounds__(256, 2) void dw_bwd_s2_kernel(const T* __restrict__
   static_assert(!STATS || BNX, "input-BN partials need the input BN");
   static_assert(!JOIN || (!BNX && sizeof(T) == 4), "the join form: fp32, no input BN");
   constexpr bool PART = STATS || JOIN;
-  constexpr int R = 3, S = 3, ST = 2, PAD = 1, RS = 9, TWQ = 2;
+  constexpr int R = 3, S = 3, ST = 2, PAD = 1, RS = 9, TWQ = JOIN ? 1 : 2;  // (the join form's operands need the registers)
   using SP = SubPix<R, ST, PAD>;
   constexpr int D0 = SP::dmin(), ND = SP::dmax() - SP::dmin() + 1, NCOL = TWQ + ND - 1;
   extern __shared__ f32x4 scratch[];  // the final reductions

@@ -210,13 +210,13 @@ class DepthwiseConvLayer(Layer):
         s = l2_strength(self.weight_regulariser)
         bn = self._bn_in
         dx = empty_nhwc(N, C, H, W, x.dtype) if need_dx else None
+        if self.stride == 2:
+            return self._backward_bn_grad_s2(G, residual, need_dx, dx, gw, s, w, join)
         if residual is not None:
             residual = dense_residual(residual, (N, C, H, W))
         res = residual_operand(residual, dx) if need_dx else None
         if need_dx and residual is not None and res is None:
             res = residual_operand(to_nhwc(residual), dx)
-        if self.stride == 2:
-            return self._backward_bn_grad_s2(G, res, residual, need_dx, dx, gw, s, w)
         if join is not None and self._join_ok(join, need_dx):
             jb = join._join_bn
             rows = lib.dk_dwconv_bwd_bnbwd_stats_rows(N, H, W, C)
@@ -274,15 +274,25 @@ class DepthwiseConvLayer(Layer):
             dx = add_residual(dx, residual)  # (a new tensor: the BN then recomputes its sums)
         return dx
 
-    def _backward_bn_grad_s2(self, G, res, residual, need_dx, dx, gw, s, w):
+    def _backward_bn_grad_s2(self, G, residual, need_dx, dx, gw, s, w, join=None):
         """The stride-2 form of _backward_bn_grad (dk_dwconv_bwd_s2_bnbwd_*): dx (+ the residual,
-        + the input BatchNorm's backward partial sums) and the weight gradient, dy never written."""
+        + the input BatchNorm's backward partial sums) and the weight gradient, dy never written.
+        With the input's residual join (fp32, _join_ok): dk_dwconv_bwd_s2_bnbwd_join_f32 -- dx
+        masked by y > 0 (y = this layer's input, the join's output), stage 1 of the join's
+        BatchNorm on the store, a strided skip's compact lattice residual added as such."""
         st = stream_handle()
         x = self.X
         N, C, H, W = x.shape
         OH, OW = (H + 1) // 2, (W + 1) // 2
         bn = self._bn_in
         bf = x.dtype == BF16
+        if join is not None and need_dx and not bf and self._join_ok(join, True):
+            return self._backward_bn_grad_s2_join(G, residual, dx, gw, s, w, join)
+        if residual is not None:
+            residual = dense_residual(residual, (N, C, H, W))
+        res = residual_operand(residual, dx) if need_dx else None
+        if need_dx and residual is not None and res is None:
+            res = residual_operand(to_nhwc(residual), dx)
         if need_dx and residual is not None and res is None:
             raise NotImplementedError("{}: the fused stride-2 backward needs an NHWC residual".format(self.layer_name))
         part = None
@@ -307,11 +317,39 @@ class DepthwiseConvLayer(Layer):
             bn.hand_backward_partials(dx, part, r, tok)
         return dx
 
+    def _backward_bn_grad_s2_join(self, G, residual, dx, gw, s, w, join):
+        st = stream_handle()
+        x = self.X
+        N, C, H, W = x.shape
+        OH, OW = (H + 1) // 2, (W + 1) // 2
+        jb = join._join_bn
+        lat = lattice_operand(residual, dx, 2)
+        if lat is None and residual is not None:
+            residual = dense_residual(residual, (N, C, H, W))
+        res = lat if lat is not None else residual_operand(residual, dx)
+        if residual is not None and res is None:
+            res = residual_operand(to_nhwc(residual), dx)
+        part = torch.empty((lib.dk_dwconv_bwd_s2_stats_rows(N, H, W, C), 2, C), dtype=torch.float64, device=x.device)
+        g = to_nhwc(G.g)
+        nb = lib.dk_dwconv_bwd_s2_workspace_bytes(N, H, W, C)
+        tok = jb.arm_partials(part)
+        red = deferred_wgrad_reduce(self, nb, s is not None)
+        with red:
+            r = lib.dk_dwconv_bwd_s2_bnbwd_join_f32(
+                g.data_ptr(), G.x.data_ptr(), N, H, W, C, OH, OW, *G.bnbwd_args(), x.data_ptr(), w.data_ptr(),
+                s or 0.0, gw.data_ptr(), dx.data_ptr(), ptr(res), 2 if lat is not None else 0, jb.x.data_ptr(),
+                jb.mean.data_ptr(), jb.invstd.data_ptr(), part.data_ptr(), red.ws, nb, st)
+        red.flush()
+        if s is None:
+            add_regulariser_grad(gw, w, self.weight_regulariser)
+        jb.hand_backward_partials(dx, part, r, tok)
+        join.join_backward_done()
+        return dx
+
     def backward(self, upstream_dx, residual=None, need_dx=True, join=None):
         self._require_on_gpu()
         if isinstance(upstream_dx, BNGrad):
-            # (the stride-2 form has no join operand: a join's backward stays with the join dgrad)
-            if self._takes_bn_grad(upstream_dx.x) and not (self.stride == 2 and join is not None):
+            if self._takes_bn_grad(upstream_dx.x):
                 return self._backward_bn_grad(upstream_dx, residual, need_dx, join)
             upstream_dx = upstream_dx.materialize()
         st = stream_handle()

@@ -159,11 +159,15 @@ def test_res1_full_size(monkeypatch, pw_fused_bwd):
     _check(got, want, f32, twin, layers)
 
 
-def test_joins_full_size(monkeypatch):
+@pytest.mark.parametrize("s2_fused", ["1", "0"])
+def test_joins_full_size(monkeypatch, s2_fused):
     """res1 -> res2 -> res3 at batch 256: both residual-join fusions at full size -- res1's join
-    backward in res2's fused stride-1 depthwise backward and res2's in res3's strided sub-pixel
-    dgrad (dk_dwconv_bwd_bnbwd_join_f32 / dk_dwconv_dgrad_join_f32: the join ReLU mask and the
-    join BatchNorm's stage-1 partials on the dgrad store)."""
+    backward in res2's fused stride-1 depthwise backward and res2's in res3's strided depthwise
+    backward (dk_dwconv_bwd_bnbwd_join_f32; stride 2: the fused one-pass backward
+    dk_dwconv_bwd_s2_bnbwd_join_f32, or with DORKNET_DW_S2_FUSED=0 the sub-pixel dgrad
+    dk_dwconv_dgrad_join_f32: the join ReLU mask and the join BatchNorm's stage-1 partials on the
+    dgrad store)."""
+    monkeypatch.setenv("DORKNET_DW_S2_FUSED", s2_fused)
     from examples.resnet18_depsep import ResNet18
     np.random.seed(37)
     layers = ResNet18("r18").layers[6:9]
@@ -171,9 +175,11 @@ def test_joins_full_size(monkeypatch):
     _perturb_bn(layers, rng)
     X = np.abs(rng.standard_normal((256, 64, 56, 56), dtype=np.float32))   # a ReLU output
     dY = rng.standard_normal((256, 128, 28, 28), dtype=np.float32)
-    calls = Calls(monkeypatch, FUSED + ["dk_dwconv_bwd_bnbwd_join_f32", "dk_dwconv_dgrad_join_f32"])
+    calls = Calls(monkeypatch, FUSED + ["dk_dwconv_bwd_bnbwd_join_f32", "dk_dwconv_dgrad_join_f32",
+                                        "dk_dwconv_bwd_s2_bnbwd_join_f32"])
     got, want, f32, twin, _ = _run(layers, X, dY, input_grad=True)
-    assert {"dk_dwconv_bwd_bnbwd_join_f32", "dk_dwconv_dgrad_join_f32"} <= calls.seen, calls.seen
+    s2 = "dk_dwconv_bwd_s2_bnbwd_join_f32" if s2_fused == "1" else "dk_dwconv_dgrad_join_f32"
+    assert {"dk_dwconv_bwd_bnbwd_join_f32", s2} <= calls.seen, calls.seen
     _check(got, want, f32, twin, layers)
 
 
@@ -234,14 +240,15 @@ def test_res4_res6_full_size(monkeypatch, deep_bwd):
     _perturb_bn(layers, rng)
     X = np.abs(rng.standard_normal((256, 128, 28, 28), dtype=np.float32))   # res3's ReLU output
     dY = rng.standard_normal((256, 256, 14, 14), dtype=np.float32)
-    calls = Calls(monkeypatch, FUSED + ["dk_dwconv_bwd_bnbwd_join_f32", "dk_dwconv_dgrad_join_f32"])
+    calls = Calls(monkeypatch, FUSED + ["dk_dwconv_bwd_bnbwd_join_f32", "dk_dwconv_dgrad_join_f32",
+                                        "dk_dwconv_bwd_s2_bnbwd_join_f32"])
     try:
         got, want, f32, twin, _ = _run(layers, X, dY, input_grad=True)
     finally:
         lib.dk_debug_set_gemm_config(14, -1)
     pw_bwd = {"dk_pwconv_bwd_bnbwd_f32"} if deep_bwd else {"dk_pwconv_dgrad_bnbwd_f32", "dk_pwconv_wgrad_bnx_f32"}
     assert pw_bwd | {"dk_pwconv_fwd_ex_f32", "dk_dwconv_fwd_ex_f32", "dk_bn_add_f32", "dk_dwconv_bwd_bnbwd_join_f32",
-                     "dk_dwconv_dgrad_join_f32"} <= calls.seen, calls.seen
+                     "dk_dwconv_bwd_s2_bnbwd_join_f32"} <= calls.seen, calls.seen
     if deep_bwd:
         assert "dk_pwconv_dgrad_bnbwd_f32" not in calls.seen, calls.seen
     _check(got, want, f32, twin, layers)

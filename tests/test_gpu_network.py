@@ -283,19 +283,23 @@ def test_join_fusion_agrees(monkeypatch):
 @pytest.mark.gpu
 def test_lattice_skip_agrees(monkeypatch):
     """A downsampling block's strided skip projection hands its input gradient over as the
-    compact stride-2 lattice and the next dgrad (dk_dwconv_dgrad_join_f32, residual_lattice = 2)
-    adds it there, vs the widened gradient (DORKNET_LATTICE=0, which also turns off the stem's
-    lattice hand-over): every gradient agrees to fp32 rounding (the lattice values are the
-    widened ones bit for bit; the BN partial sums regroup)."""
+    compact stride-2 lattice and the next strided depthwise backward (the fused one-pass
+    dk_dwconv_bwd_s2_bnbwd_join_f32, or dk_dwconv_dgrad_join_f32; residual_lattice = 2) adds it
+    there, vs the widened gradient (DORKNET_LATTICE=0, which also turns off the stem's lattice
+    hand-over): every gradient agrees to fp32 rounding (the lattice values are the widened ones
+    bit for bit; the BN partial sums regroup)."""
     from examples.resnet18_depsep import ResNet18, synthetic_batch
     from dorknet_amd import _hip
     X, _, onehot = synthetic_batch(2, seed=2)
     grads = {}
     orig = _hip.lib.dk_dwconv_dgrad_join_f32
+    orig2 = _hip.lib.dk_dwconv_bwd_s2_bnbwd_join_f32
     for lat in ("1", "0"):
         monkeypatch.setenv("DORKNET_LATTICE", lat)
         seen = []
         monkeypatch.setattr(_hip.lib, "dk_dwconv_dgrad_join_f32", lambda *a, seen=seen: seen.append(a[16]) or orig(*a))
+        monkeypatch.setattr(_hip.lib, "dk_dwconv_bwd_s2_bnbwd_join_f32",
+                            lambda *a, seen=seen: seen.append(a[20]) or orig2(*a))
         np.random.seed(0)
         net = ResNet18("r18")
         net.to_gpu()
