@@ -15,7 +15,7 @@ import re
 
 import torch  # noqa: F401  -- loads torch's HIP runtime first; our .so binds to the same one
 
-from ._env import enabled
+from ._env import enabled, getenv
 
 _PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 # DORKNET_HIP_LIB: another build of the same library (A/B runs of two builds on one box)
@@ -105,7 +105,8 @@ class _Lib:
             fn = getattr(lib, name)
             fn.restype = ctypes.c_size_t if ret == "size_t" else ctypes.c_int
             fn.argtypes = [_argtype(t) for t, _ in params]
-            counts = name.endswith(("_blocks", "_version", "_rows", "_count", "_preferred")) or name.startswith("dk_debug")
+            counts = (name.endswith(("_blocks", "_version", "_rows", "_count", "_preferred", "_pending"))
+                      or name.startswith("dk_debug"))
             if ret == "int" and not counts:
                 fn.errcheck = _errcheck
         self._decls = decls
@@ -331,6 +332,8 @@ class async_weight_grads:
         return self
 
     def __exit__(self, *exc):
+        if _ASYNC_DEPTH[0] == 1:
+            flush_wgrad_reduces()  # (on the side stream, while it is still the weight-gradient stream)
         _ASYNC_DEPTH[0] -= 1
         if _ASYNC_DEPTH[0] == 0:
             join_weight_grads()
@@ -384,9 +387,31 @@ class deferred_wgrad_reduce:
         return False
 
     def flush(self):
-        if self.on:
-            with weight_grad_stream():
-                lib.dk_wgrad_reduce_flush(stream_handle())
+        """Launch the recorded reduces once DORKNET_WGRAD_FLUSH_EVERY (default 60, i.e. at the end
+        of the backward) have collected: each flush makes the side stream wait for the main stream,
+        and every such wait put a ~7 us gap between two main-stream kernels (an event marker); the
+        slabs are per layer, so a recorded reduce can wait, and a flush runs all of them as one
+        multi-task kernel.  flush_wgrad_reduces() launches the rest (the end of the backward, a
+        data-parallel bucket's all-reduce).  Config 3 8.374 -> 8.339 ms, config 5 6.232 -> 6.147 ms
+        (profiles/r05u_ab_flush_every_multi_*.txt)."""
+        if self.on and lib.dk_wgrad_reduce_pending() >= _flush_every():
+            flush_wgrad_reduces()
+
+
+def _flush_every() -> int:
+    try:
+        return min(60, max(1, int(getenv("DORKNET_WGRAD_FLUSH_EVERY", "60"))))  # (the C queue holds 64)
+    except ValueError:
+        return 60
+
+
+def flush_wgrad_reduces() -> None:
+    """Launch every recorded weight-gradient reduce (deferred_wgrad_reduce) on the side stream,
+    ordered after the main stream."""
+    if lib._lib is None or lib.dk_wgrad_reduce_pending() == 0:
+        return
+    with weight_grad_stream():
+        lib.dk_wgrad_reduce_flush(stream_handle())
 
 
 def join_weight_grads() -> None:

@@ -255,7 +255,7 @@ enum KnobId : int {
   kKnobRowCfg = 0, kKnobSplitCfg = 1, kKnobFillSplits = 2, kKnobPwStream = 3, kKnobNtStores = 4, kKnobPwsBwdPf = 5,
   kKnobDwbBlocks = 7, kKnobDwSeg = 8, kKnobPwsh = 9, kKnobPwDeep = 11, kKnobPwDeep16 = 13, kKnobPwDeepBwd = 14,
   kKnobPwStream128 = 15, kKnobPwfPrefetch = 16, kKnobPwfBlocksPerCu = 17, kKnobWgradBlocks = 18, kKnobEwVariant = 19,
-  kKnobPwsh16Bwd = 20, kKnobDwbCols = 21, kNumKnobs = 22
+  kKnobPwsh16Bwd = 20, kKnobDwbCols = 21, kKnobMultiReduce = 22, kNumKnobs = 23
 };
 int knob(int id);
 void knob_set(int id, int v);

@@ -45,6 +45,7 @@ constexpr KnobDef kDefs[kNumKnobs] = {
     {"DORKNET_PW_BF16_BWD", 1},          // kKnobPwsh16Bwd: fused bf16 pointwise backward (1: K = C = 64 and
                                           // K in {128, 256}; 2: K = C = 64 only; 0: off)
     {"DORKNET_DWB_COLS", 2},             // kKnobDwbCols: columns per thread of the fused depthwise backward
+    {"DORKNET_MULTI_REDUCE", 1},         // kKnobMultiReduce: a flush's reduces in one launch (0: one each)
 };
 
 struct Table {

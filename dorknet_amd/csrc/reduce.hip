@@ -122,6 +122,79 @@ __global__ __launch_bounds__(CG* TPO) void splitk_reduce4_kernel(const float* __
   }
 }
 
+// Several float4-column reduces (mode 0) in one launch: the deferred weight-gradient reduces a flush
+// batches (dk_wgrad_reduce_flush).  Task t owns blocks [block0, block0 + nblk) and sums its slab with
+// splitk_reduce4_kernel's thread layout for its TPO (64 / 16 / 4 by the same split-count rule, so
+// every column's sum is in the same order: bit-identical to the per-task launch); one launch instead
+// of one per layer, each of which paid a launch and a serial tail of its own.
+constexpr int kMultiMax = 32;
+struct MultiTask {
+  const float* ws;
+  float* out;
+  const float* w;
+  float l2;
+  int splits, total, tpo, block0;
+};
+struct MultiTasks {
+  MultiTask t[kMultiMax];
+  int n;
+};
+__device__ __forceinline__ void multi_reduce_task(const MultiTask& k, int blk, int tid, double* red) {
+  const int TPO = k.tpo, CG = 256 / TPO;
+  const int j = tid % CG, q = tid / CG;
+  const long long total = k.total;
+  const long long idx = ((long long)blk * CG + j) * 4;
+  double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+  if (idx < total) {
+    const float* p = k.ws + idx;
+    int s = q;
+    for (; s + 3 * TPO < k.splits; s += 4 * TPO) {
+      f32x4 v[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = ld4(p + (size_t)(s + e * TPO) * total);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        a0 += (double)v[e].x;
+        a1 += (double)v[e].y;
+        a2 += (double)v[e].z;
+        a3 += (double)v[e].w;
+      }
+    }
+    for (; s < k.splits; s += TPO) {
+      const f32x4 v = ld4(p + (size_t)s * total);
+      a0 += (double)v.x;
+      a1 += (double)v.y;
+      a2 += (double)v.z;
+      a3 += (double)v.w;
+    }
+  }
+  // red[q][j][4] (TPO x CG x 4 doubles = 8 KB)
+  double* r = red + ((size_t)q * CG + j) * 4;
+  r[0] = a0;
+  r[1] = a1;
+  r[2] = a2;
+  r[3] = a3;
+  __syncthreads();
+  for (int t = tid; t < 4 * CG; t += 256) {
+    const int jj = t >> 2, e = t & 3;
+    const long long o = ((long long)blk * CG + jj) * 4 + e;
+    if (o >= total) break;
+    double sum = 0.0;
+    for (int l = 0; l < TPO; ++l) sum += red[((size_t)l * CG + jj) * 4 + e];
+    float v = (float)sum;
+    if (k.w) v = v + k.l2 * k.w[o];
+    k.out[o] = v;
+  }
+}
+__global__ __launch_bounds__(256) void splitk_multi_kernel(MultiTasks tasks) {
+  __shared__ double red[256 * 4];
+  int ti = 0;
+  while (ti + 1 < tasks.n && (int)blockIdx.x >= tasks.t[ti + 1].block0) ++ti;  // uniform
+  const MultiTask& k = tasks.t[ti];
+  multi_reduce_task(k, (int)blockIdx.x - k.block0, threadIdx.x, red);
+}
+static int multi_tpo(int splits) { return splits >= 256 ? 64 : splits >= 32 ? 16 : 4; }
+
 int splitk_reduce(const float* ws, int splits, int M, int N, float* out, const float* w, float l2, int mode, int C,
                   int Cp, int R, int S, hipStream_t st) {
   const long long total = (long long)M * N;
@@ -177,16 +250,19 @@ struct PendingReduce {
   float* out;
   const float* w;
   float l2;
-  bool set;
 };
+// Recorded reduces, launched in order by the next flush (the caller batches several layers' reduces
+// behind one cross-stream wait: each wait costs the main stream a ~7 us gap between kernels).
+constexpr int kMaxPending = 64;
 thread_local int t_defer = 0;
-thread_local PendingReduce t_pending{};
+thread_local int t_npending = 0;
+thread_local PendingReduce t_pending[kMaxPending];
 }  // namespace
 
 int wgrad_reduce(const float* ws, int splits, int M, int N, float* out, const float* w, float l2, hipStream_t st) {
   if (!t_defer) return splitk_reduce(ws, splits, M, N, out, w, l2, 0, N, N, 1, 1, st);
-  if (t_pending.set) return DK_ERR_ARGS;  // the previous deferred reduce was never flushed
-  t_pending = PendingReduce{ws, splits, M, N, out, w, l2, true};
+  if (t_npending == kMaxPending) return DK_ERR_ARGS;  // never flushed
+  t_pending[t_npending++] = PendingReduce{ws, splits, M, N, out, w, l2};
   return 0;
 }
 
@@ -194,21 +270,56 @@ int wgrad_reduce(const float* ws, int splits, int M, int N, float* out, const fl
 
 // Deferred weight-gradient reduce.  mode 1: the fused backward entry points called next on this
 // host thread (dk_dwconv_bwd_bnbwd_f32 / _bf16 / _join_f32, dk_dwconv_bwd_s2_bnbwd_*,
-// dk_pwconv_bwd_bnbwd_f32 / _bf16) leave their
-// weight-gradient partial slab unreduced and record the reduce; mode 0: back to reducing in the
-// entry point (a recorded reduce stays for dk_wgrad_reduce_flush); mode -1: as 0 and drop it.
+// dk_pwconv_bwd_bnbwd_f32 / _bf16) leave their weight-gradient partial slab unreduced and record
+// the reduce; mode 0: back to reducing in the entry point (recorded reduces stay for
+// dk_wgrad_reduce_flush); mode -1: as 0 and drop the recorded ones.
 DK_API int dk_wgrad_reduce_defer(int mode) {
   if (mode < -1 || mode > 1) return dk::DK_ERR_ARGS;
   dk::t_defer = mode == 1;
-  if (mode == -1) dk::t_pending.set = false;
+  if (mode == -1) dk::t_npending = 0;
   return 0;
 }
 
-// Launch the recorded reduce on `stream` (fixed order, the same result as in the entry point).
-// The slab must stay untouched until it has run; DK_ERR_ARGS if none is recorded.
+// Reduces recorded and not yet flushed on this host thread.
+DK_API int dk_wgrad_reduce_pending(void) { return dk::t_npending; }
+
+// Launch the recorded reduces on `stream`, in the order recorded (fixed order each, the same result
+// as in the entry point).  The slabs must stay untouched until they have run; DK_ERR_ARGS if none is
+// recorded.
 DK_API int dk_wgrad_reduce_flush(void* stream) {
-  if (!dk::t_pending.set) return dk::DK_ERR_ARGS;
-  const dk::PendingReduce p = dk::t_pending;
-  dk::t_pending.set = false;
-  return dk::splitk_reduce(p.ws, p.splits, p.M, p.N, p.out, p.w, p.l2, 0, p.N, p.N, 1, 1, dk::as_stream(stream));
+  using namespace dk;
+  if (t_npending == 0) return DK_ERR_ARGS;
+  const int n = t_npending;
+  t_npending = 0;
+  const hipStream_t st = as_stream(stream);
+  // float4-column slabs go into multi-task launches (same per-column order as splitk_reduce4_kernel),
+  // the rest one launch each
+  MultiTasks mt{};
+  int blocks = 0;
+  auto launch = [&]() -> int {
+    if (mt.n == 0) return 0;
+    hipLaunchKernelGGL(splitk_multi_kernel, dim3((unsigned)blocks), dim3(256), 0, st, mt);
+    mt.n = 0;
+    blocks = 0;
+    return launch_status();
+  };
+  for (int i = 0; i < n; ++i) {
+    const PendingReduce& p = t_pending[i];
+    const long long total = (long long)p.M * p.N;
+    if (knob(kKnobMultiReduce) == 1 && (total & 3) == 0 && (reinterpret_cast<uintptr_t>(p.ws) & 15) == 0 &&
+        total < (1ll << 31)) {
+      const int tpo = multi_tpo(p.splits), cg = 256 / tpo;
+      const int nb = (int)cdivll(total, 4ll * cg);
+      mt.t[mt.n++] = MultiTask{p.ws, p.out, p.w, p.l2, p.splits, (int)total, tpo, blocks};
+      blocks += nb;
+      if (mt.n == kMultiMax) {
+        const int rc = launch();
+        if (rc) return rc;
+      }
+    } else {
+      const int rc = splitk_reduce(p.ws, p.splits, p.M, p.N, p.out, p.w, p.l2, 0, p.N, p.N, 1, 1, st);
+      if (rc) return rc;
+    }
+  }
+  return launch();
 }

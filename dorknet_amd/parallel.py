@@ -34,7 +34,7 @@ from __future__ import annotations
 import torch
 import torch.distributed as dist
 
-from ._hip import async_weight_grads, branch_stream, branch_stream_enabled, side_stream_context
+from ._hip import async_weight_grads, branch_stream, branch_stream_enabled, flush_wgrad_reduces, side_stream_context
 from .layers._chain import backward_progress, chain_backward
 
 
@@ -136,6 +136,7 @@ class DataParallel:
         self._works = []
 
     def _launch(self, lo, hi):
+        flush_wgrad_reduces()  # reduces still recorded (batched) must land before the collective
         view = self.flat[lo:hi]
         op = dist.ReduceOp.AVG if self.native_avg else dist.ReduceOp.SUM
         if view.is_cuda:

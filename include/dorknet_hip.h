@@ -74,7 +74,9 @@ int dk_mixup_f32(const float* a, const float* b, long long n, float p, float one
  * kind 20: the fused bf16 pointwise backward (DORKNET_PW_BF16_BWD: 1 = K = C = 64 and K in {128, 256},
  * 2 = K = C = 64 only, 0 = off);
  * kind 21: output columns per thread of the fused stride-1 depthwise backward (DORKNET_DWB_COLS: 2 =
- * default where the width allows, 1 = one); the dk_dwconv_bwd_bnbwd*_stats_rows / _workspace_bytes follow it. */
+ * default where the width allows, 1 = one); the dk_dwconv_bwd_bnbwd*_stats_rows / _workspace_bytes follow it;
+ * kind 22: dk_wgrad_reduce_flush launches its reduces as one multi-task kernel (DORKNET_MULTI_REDUCE: 1 =
+ * default, 0 = one launch each; bit-identical either way). */
 int dk_debug_set_gemm_config(int kind, int cfg);
 
 /* Bandwidth ceiling probe (not on the training path; scripts/stream_ceiling.py): reads nin
@@ -401,12 +403,14 @@ int dk_bn_fold_arm_bwd(const void* part, int nrows, int C, double count, float* 
 int dk_bn_fold_disarm(void);
 /* Deferred weight-gradient reduce.  dk_wgrad_reduce_defer(1): the fused backward entry points
  * called next on this host thread (dk_dwconv_bwd_bnbwd_f32 / _bf16, dk_dwconv_bwd_bnbwd_join_f32,
- * dk_pwconv_bwd_bnbwd_f32) leave the weight-gradient partial slab in their workspace and record its
- * fixed-order reduce instead of launching it; dk_wgrad_reduce_flush(stream) launches it on `stream`
- * (the caller orders that stream after the entry point's and keeps the workspace untouched until
- * the reduce has run).  (0): reduce in the entry point again; (-1): as 0, dropping a recorded
- * reduce.  One recorded reduce per host thread (a second one is DK_ERR_ARGS until flushed). */
+ * dk_dwconv_bwd_s2_bnbwd_*, dk_pwconv_bwd_bnbwd_f32 / _bf16) leave the weight-gradient partial slab in their workspace and record its
+ * fixed-order reduce instead of launching it; dk_wgrad_reduce_flush(stream) launches the recorded
+ * ones, in order, on `stream` (the caller orders that stream after the entry points' and keeps the
+ * workspaces untouched until the reduces have run).  (0): reduce in the entry point again; (-1):
+ * as 0, dropping the recorded reduces.  Up to 64 recorded per host thread (then DK_ERR_ARGS until
+ * flushed); dk_wgrad_reduce_pending() = how many. */
 int dk_wgrad_reduce_defer(int mode);
+int dk_wgrad_reduce_pending(void);
 int dk_wgrad_reduce_flush(void* stream);
 size_t dk_bn_fold_scratch_bytes(int nrows, int C);
 int dk_bn_fold_tickets_needed_count(int nrows, int nslices);

@@ -97,15 +97,36 @@ def test_stream_helpers_match_torch():
 
 
 def test_wgrad_reduce_defer_protocol():
-    """A second deferred reduce before a flush is refused, a flush with none recorded is refused,
-    and mode -1 drops a recorded one."""
+    """A flush with none recorded is refused, an unknown mode is refused, and mode -1 drops the
+    recorded ones."""
     from dorknet_amd._hip import HipError, lib
     lib.dk_wgrad_reduce_defer(-1)
+    assert lib.dk_wgrad_reduce_pending() == 0
     with pytest.raises(HipError):
         lib.dk_wgrad_reduce_flush(0)
     with pytest.raises(HipError):
         lib.dk_wgrad_reduce_defer(2)
     lib.dk_wgrad_reduce_defer(0)
+
+
+@pytest.mark.parametrize("every", ["1", "4", "64"])
+def test_wgrad_reduce_batched_flush_bitwise(monkeypatch, every):
+    """Recorded reduces launched in batches (DORKNET_WGRAD_FLUSH_EVERY: one cross-stream wait per
+    batch) give the same gradients bit for bit as one flush per layer."""
+    from examples.resnet18_depsep import ResNet18, synthetic_batch
+    from dorknet_amd._hip import lib
+    X, _, onehot = synthetic_batch(8, seed=15)
+    np.random.seed(16)
+    net = ResNet18("r18")
+    net.to_gpu()
+    monkeypatch.setenv("DORKNET_WGRAD_FLUSH_EVERY", "1")
+    ref = _step(net, X, onehot)
+    monkeypatch.setenv("DORKNET_WGRAD_FLUSH_EVERY", every)
+    got = _step(net, X, onehot)
+    torch.cuda.synchronize()
+    assert lib.dk_wgrad_reduce_pending() == 0
+    for a, b in zip(ref, got):
+        assert torch.equal(a, b)
 
 
 def test_data_parallel_rccl_world1():

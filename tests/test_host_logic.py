@@ -250,3 +250,14 @@ def test_stats_fold_arming_marks_records_stale(monkeypatch):
     assert bn.arm_stats_fold(torch.zeros((3, 2, 4), dtype=torch.float64), 12) is not None
     with pytest.raises(RuntimeError, match="bn_f"):
         out.bn_args()
+
+
+def test_wgrad_flush_batch_setting(monkeypatch):
+    """DORKNET_WGRAD_FLUSH_EVERY: recorded weight-gradient reduces per cross-stream flush, clamped to
+    [1, 60] (the C queue holds 64), 60 (= at the end of the backward) by default or when unparsable."""
+    from dorknet_amd._hip import _flush_every
+    monkeypatch.delenv("DORKNET_WGRAD_FLUSH_EVERY", raising=False)
+    assert _flush_every() == 60
+    for v, want in (("1", 1), ("0", 1), ("8", 8), ("500", 60), ("x", 60)):
+        monkeypatch.setenv("DORKNET_WGRAD_FLUSH_EVERY", v)
+        assert _flush_every() == want
