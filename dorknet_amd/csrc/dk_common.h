@@ -282,7 +282,7 @@ int pw_stream_bwd_fused(const float* g, const float* bn_x, int M, const float* o
                         const float* res, const float* x, const float* im, const float* iis, const float* ig,
                         const float* ib, int irelu, double* part, const float* bm, const float* bis,
                         const float* bgm, const float* bbt, int brelu, float* wpart, hipStream_t st,
-                        const struct FoldTail* ft = nullptr);
+                        const struct FoldTail* ft = nullptr, const int* lattice = nullptr);
 bool pw_stream_fwd_ok(int K, int C, int M, size_t xbytes);
 int pw_stream_fwd_rows(int M, int K);
 int pw_stream_fwd(const float* x, int N, int H, int W, int stride, int OH, int OW, const float* w, int KC,

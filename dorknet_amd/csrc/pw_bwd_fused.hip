@@ -343,6 +343,42 @@ DK_API size_t dk_pwconv_bwd_fused_workspace_bytes(int N, int OH, int OW, int K, 
   return (size_t)dk_pwconv_bwd_fused_rows(N, OH, OW, K, C) * K * C * sizeof(float);
 }
 
+// The stride-s form for a layer whose input gradient the consumer takes as the compact lattice
+// (dk_pwconv_dgrad_lattice_f32's output; pointwise_convolution.py:57-75 with the widen's zeros never
+// stored): dk_pwconv_bwd_bnbwd_f32's one pass over the OH x OW output pixels, x (N x H x W x C, the
+// layer input, with its BatchNorm applied on load) read at the stride-s lattice, dx the compact
+// N x OH x OW x C.  K = C = 64 (the streaming kernel: the ResNet stem's pw0).  Rows: as
+// dk_pwconv_bwd_fused_rows(N, OH, OW, K, C).
+DK_API int dk_pwconv_bwd_bnbwd_lattice_f32(const float* g, const float* bn_x, int N, int OH, int OW, int K,
+                                           const float* out_mean, const float* out_invstd, const float* out_gamma,
+                                           const float* out_beta, int out_relu, const float* k12, const float* w_kc,
+                                           int C, float l2, float* dw_kc, float* dx, const float* x, int H, int W,
+                                           int stride, const float* bn_mean, const float* bn_invstd,
+                                           const float* bn_gamma, const float* bn_beta, int bn_relu, double* part,
+                                           void* ws, size_t ws_bytes, void* stream) {
+  const hipStream_t st = as_stream(stream);
+  if (N < 1 || OH < 1 || OW < 1 || stride < 2 || H < (OH - 1) * stride + 1 || W < (OW - 1) * stride + 1)
+    return DK_ERR_ARGS;
+  const long long P = (long long)N * OH * OW;
+  if (!pw_stream_bwd_ok(K, C, (int)P) || (long long)N * H * W * C * 4 >= (1ll << 31)) return DK_ERR_ARGS;
+  if (!g || !bn_x || !x || !w_kc || !dw_kc || !dx || !out_mean || !out_invstd || !out_gamma || !out_beta || !k12 ||
+      !bn_mean || !bn_invstd || !bn_gamma || !bn_beta)
+    return DK_ERR_ARGS;
+  auto al = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+  if (!al(g) || !al(bn_x) || !al(x) || !al(dx) || !al(ws)) return DK_ERR_ARGS;
+  const int nb = pw_stream_bwd_rows((int)P);
+  if (ws_bytes < (size_t)nb * K * C * sizeof(float)) return DK_ERR_WORKSPACE;
+  float* wp = static_cast<float*>(ws);
+  FoldTail ft;
+  if (part) fold_take(part, nb, C, 1, &ft);
+  const int lat[5] = {stride, H, W, OH, OW};
+  int rc = pw_stream_bwd_fused(g, bn_x, (int)P, out_mean, out_invstd, out_gamma, out_beta, out_relu, k12, w_kc, dx,
+                               nullptr, x, part ? bn_mean : nullptr, bn_invstd, bn_gamma, bn_beta, bn_relu, part,
+                               bn_mean, bn_invstd, bn_gamma, bn_beta, bn_relu, wp, st, part ? &ft : nullptr, lat);
+  if (rc) return rc;
+  return fold_status(wgrad_reduce(wp, nb, K, C, dw_kc, l2 != 0.f ? w_kc : nullptr, l2, st), part ? ft : FoldTail{});
+}
+
 DK_API int dk_pwconv_bwd_bnbwd_f32(const float* g, const float* bn_x, int N, int OH, int OW, int K,
                                    const float* out_mean, const float* out_invstd, const float* out_gamma,
                                    const float* out_beta, int out_relu, const float* k12, const float* w_kc, int C,

@@ -578,6 +578,10 @@ struct BwdArgs {
   const float* bb;
   int brelu;
   float* wpart;      // [gridDim.x][KR][NO]
+  // lattice (ls > 1): a stride-ls pointwise layer whose input gradient stays the compact lattice
+  // (pointwise_convolution.py:68-72 without the zeros): pixel m of g / dx is output pixel (n, oh, ow)
+  // of an lOH x lOW grid, and x (the layer input, lH x lW) is read at (n, ls oh, ls ow)
+  int ls, lH, lW, lOH, lOW;
 };
 
 constexpr int SKD = KR + 4;  // row stride of the wave's dy image
@@ -585,13 +589,15 @@ constexpr int SKD = KR + 4;  // row stride of the wave's dy image
 // PF: prefetch the next tile's A operands (g, x of the following BN) into registers during this
 // tile (one wave per SIMD: 256 VGPRs + 88 AGPRs); !PF: load them at the top of each tile and let a
 // second wave on the SIMD cover the latency (2 waves per SIMD).
-template <bool RES, bool PART, bool BNIN, bool PF = true>
+template <bool RES, bool PART, bool BNIN, bool PF = true, bool LAT = false>
 __global__ __launch_bounds__(256, PF ? 1 : 2) void bwd_fused_kernel(BwdArgs ba) {
+  static_assert(!LAT || (!RES && BNIN), "the lattice form: no residual, the input BN on load");
   const DgradArgs& a = ba.d;
   __shared__ float Bs[NO * SKB];
   __shared__ float tab[7][KR];
   __shared__ double red[WAVES][2][NO];
   __shared__ float Td[WAVES][TR * SKD];  // per-wave dy tile image (also the dW combine buffer)
+  __shared__ uint32_t rowoff[WAVES][TR];  // lattice: byte offset of each tile pixel's input row in x
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int l32 = lane & 31, h = lane >> 5;
@@ -628,7 +634,9 @@ __global__ __launch_bounds__(256, PF ? 1 : 2) void bwd_fused_kernel(BwdArgs ba) 
 
   const uint32_t kbytes = (uint32_t)a.M * KR * 4u, nbytes = (uint32_t)a.M * NO * 4u;
   const __amdgpu_buffer_rsrc_t rg = make_rsrc_v(a.g, kbytes), rx = make_rsrc_v(a.xo, kbytes);
-  const __amdgpu_buffer_rsrc_t rxi = make_rsrc_v(a.xi, nbytes);
+  constexpr bool lat = LAT;
+  const uint32_t xibytes = lat ? (uint32_t)(a.M / (ba.lOH * ba.lOW)) * ba.lH * ba.lW * NO * 4u : nbytes;
+  const __amdgpu_buffer_rsrc_t rxi = make_rsrc_v(a.xi, xibytes);
   const __amdgpu_buffer_rsrc_t rr = make_rsrc_v(RES ? a.res : a.g, RES ? nbytes : 0u);
   const __amdgpu_buffer_rsrc_t rdx = make_rsrc_v(a.dx, nbytes);
   const int ntiles = (a.M + TR - 1) / TR;
@@ -673,13 +681,27 @@ __global__ __launch_bounds__(256, PF ? 1 : 2) void bwd_fused_kernel(BwdArgs ba) 
     float exi[2][16], ers[2][16];
     const int mb = m0 + 4 * h;
     const uint32_t eb0 = row_off_bytes(mb, NO, l32), eb1 = eb0 + 16u * NO * 4u;
+    if constexpr (lat) {  // this tile's input rows, one per lane of the low half; LDS is in order per wave
+      if (h == 0) {
+        const int m = m0 + l32;
+        uint32_t off = kOOBBytes;
+        if (m < a.M) {
+          const int ow = m % ba.lOW, q = m / ba.lOW, oh = q % ba.lOH, n = q / ba.lOH;
+          off = (uint32_t)((n * ba.lH + ba.ls * oh) * ba.lW + ba.ls * ow) * (uint32_t)(NO * 4);
+        }
+        rowoff[wave][l32] = off;
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
 #pragma unroll
     for (int u = 0; u < 2; ++u)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const uint32_t imm = (uint32_t)(((r & 3) + 8 * ((r >> 2) & 1)) * NO + 32 * u) * 4u;
         const uint32_t eb = r < 8 ? eb0 : eb1;
-        exi[u][r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rxi, (int)(eb + imm), 0, 0));
+        const uint32_t xoff =
+            lat ? rowoff[wave][4 * h + (r & 3) + 8 * (r >> 2)] + (uint32_t)(32 * u + l32) * 4u : eb + imm;
+        exi[u][r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rxi, (int)xoff, 0, 0));
         if constexpr (RES)
           ers[u][r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rr, (int)(eb + imm), 0, 0));
       }
@@ -878,14 +900,29 @@ int pw_stream_bwd_fused(const float* g, const float* bn_x, int M, const float* o
                         const float* res, const float* x, const float* im, const float* iis, const float* ig,
                         const float* ib, int irelu, double* part, const float* bm, const float* bis,
                         const float* bgm, const float* bbt, int brelu, float* wpart, hipStream_t st,
-                        const FoldTail* ft) {
+                        const FoldTail* ft, const int* lattice) {
   pws::BwdArgs a{{g, bn_x, nullptr, w, dx, res, x, om, ois, og, ob, k12, orelu, im, iis, ig, ib, irelu, part, M},
-                 bm, bis, bgm, bbt, brelu, wpart};
+                 bm, bis, bgm, bbt, brelu, wpart, 0, 0, 0, 0, 0};
+  if (lattice) {  // {stride, H, W, OH, OW}
+    if (res || !bm || lattice[0] < 2) return DK_ERR_ARGS;
+    a.ls = lattice[0];
+    a.lH = lattice[1];
+    a.lW = lattice[2];
+    a.lOH = lattice[3];
+    a.lOW = lattice[4];
+  }
   if (ft && part) a.d.ft = *ft;
   a.d.nt = nt_stores(kNtPwsBwd);
   const dim3 grid(pws::bwd_fused_blocks(M));
   const bool r = res != nullptr, pt = part != nullptr, bn = bm != nullptr;
   if (pt && !bn) return DK_ERR_ARGS;
+  if (lattice) {  // (the lattice form keeps the prefetch: without it it spills at 2 waves per SIMD)
+    if (pt)
+      hipLaunchKernelGGL((pws::bwd_fused_kernel<false, true, true, true, true>), grid, dim3(256), 0, st, a);
+    else
+      hipLaunchKernelGGL((pws::bwd_fused_kernel<false, false, true, true, true>), grid, dim3(256), 0, st, a);
+    return launch_status();
+  }
   // (the residual variants keep the prefetch: without it they spill at 2 waves per SIMD)
 #define DK_BWD(R_, P_, B_)                                                                    \
   if (R_ || pws::bwd_pf())                                                                    \

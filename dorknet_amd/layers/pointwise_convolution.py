@@ -124,8 +124,25 @@ class PointwiseConvLayer(Layer):
         the 16-byte loads and the LDS coefficient table take."""
         x = getattr(self, "X", None)
         bx = getattr(bn_layer, "X", None)
+        if x is not None and bx is not None and self._lattice_fused_ok(bx):
+            return True  # (the strided stem layer: dk_pwconv_bwd_bnbwd_lattice_f32 when the lattice is asked for)
         return (x is not None and bx is not None and x.dtype in (torch.float32, BF16) and self.stride == 1
                 and x.dim() == 4 and x.shape[1] == self.num_channels and self._takes_bn_grad(bx))
+
+    def _lattice_fused_ok(self, bx, residual=None):
+        """backward(BNGrad, lattice_out=True) as one pass (dk_pwconv_bwd_bnbwd_lattice_f32: the
+        following BatchNorm's apply, the dgrad into the compact lattice, the weight gradient and the
+        input BatchNorm's partials; dy never stored): fp32, lattice_ok(), K = C = 64, the input
+        consumed as a BNOut, no residual (DORKNET_PW_LATTICE_FUSED=0: off)."""
+        x = self.X
+        if (residual is not None or self._bn_in is None or not self.lattice_ok() or bx.dtype != torch.float32
+                or bx.dim() != 4 or getenv("DORKNET_PW_LATTICE_FUSED", "1") == "0"):
+            return False
+        N = x.shape[0]
+        OH, OW = self.out_hw
+        return (tuple(bx.shape) == (N, self.num_filters, OH, OW)
+                and lib.dk_pwconv_bwd_fused_rows(N, OH, OW, self.num_filters, self.num_channels) > 0
+                and self.num_filters == 64 and self.num_channels == 64)
 
     def _takes_bn_grad(self, bx):
         bf = self.X.dtype == BF16
@@ -159,6 +176,8 @@ class PointwiseConvLayer(Layer):
         P = N * OH * OW
         w = self.learned_params["weights"]
         if isinstance(upstream_dx, BNGrad):
+            if need_dx and lattice_out and self._lattice_fused_ok(upstream_dx.x, residual):
+                return self._bwd_fused_lattice(upstream_dx, st)
             if need_dx and self._fused_bwd_ok(upstream_dx, residual):
                 # input gradient, weight gradient and the input BN's partials in one pass; dy
                 # is formed from the BatchNorm's gradient as it is loaded and never stored
@@ -309,6 +328,36 @@ class PointwiseConvLayer(Layer):
                 pass
         if bn is not None:
             bn.hand_backward_partials(dx, part, r, tok)
+        return dx
+
+    def _bwd_fused_lattice(self, bg, st):
+        x = self.X
+        N, C, H, W = x.shape
+        K, s = self.num_filters, self.stride
+        OH, OW = self.out_hw
+        w = self.learned_params["weights"]
+        dx = empty_nhwc(N, C, OH, OW)
+        bn = self._bn_in
+        rows = lib.dk_pwconv_bwd_fused_rows(N, OH, OW, K, C)
+        part = torch.empty((rows, 2, C), dtype=torch.float64, device=dx.device)
+        gw = grad_buffer(self, "weights", (K, C))
+        l2s = l2_strength(self.weight_regulariser)
+        nb = lib.dk_pwconv_bwd_fused_workspace_bytes(N, OH, OW, K, C)
+        tok = bn.arm_partials(part)
+        red = deferred_wgrad_reduce(self, nb, l2s is not None)
+        with red:
+            r = lib.dk_pwconv_bwd_bnbwd_lattice_f32(
+                to_nhwc(bg.g).data_ptr(), bg.x.data_ptr(), N, OH, OW, K, *bg.bnbwd_args(), w.data_ptr(), C,
+                l2s or 0.0, gw.data_ptr(), dx.data_ptr(), x.data_ptr(), H, W, s, *bn.bn_args(), part.data_ptr(),
+                red.ws, nb, st)
+        red.flush()
+        if l2s is None:
+            add_regulariser_grad(gw, w, self.weight_regulariser)
+        if not red.on:
+            with weight_grad_stream():
+                pass
+        dx._dk_lattice = s
+        bn.hand_backward_partials(dx, part, r, tok)
         return dx
 
     def _dgrad_bnbwd(self, bg, dy_out, residual, st):

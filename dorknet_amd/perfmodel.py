@@ -215,6 +215,11 @@ MODEL = {
     i, ga, b, r, part, ws, nb, st: (
         2 * 2 * N * OH * OW * K * C + 6 * N * OH * OW * K,
         E * (2 * N * OH * OW * K + N * OH * OW * C * (2 + (res != 0)) + 2 * K * C)),
+    # the same for a strided layer with dx kept as its lattice: x read at the lattice points only
+    "dk_pwconv_bwd_bnbwd_lattice_f32": lambda g, ox, N, OH, OW, K, om, oi, og, ob, orl, k12, w, C, l2, dw, dx, x, H,
+    W, s, m, i, ga, b, r, part, ws, nb, st: (
+        2 * 2 * N * OH * OW * K * C + 6 * N * OH * OW * K,
+        E * (2 * N * OH * OW * K + 2 * N * OH * OW * C + 2 * K * C)),
     # fused depthwise backward: reads g and the following BN's input (to form dy), the layer's
     # input (weight gradient; the input BN's partials), the residual addend; writes dx
     "dk_dwconv_bwd_bnbwd_f32": lambda g, ox, N, H, W, C, om, oi, og, ob, orl, k12, x, w, R, S, pad, l2, dw, dx, res,

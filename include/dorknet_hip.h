@@ -233,6 +233,12 @@ int dk_pwconv_bwd_fused_rows(int N, int OH, int OW, int K, int C);
  * the layers then take it by default), else 0. */
 int dk_pwconv_bwd_fused_preferred(int N, int OH, int OW, int K, int C);
 size_t dk_pwconv_bwd_fused_workspace_bytes(int N, int OH, int OW, int K, int C);
+/* The stride-s form for the compact-lattice input gradient (pointwise_convolution.py:57-75 with
+ * the widen's zeros never stored; dk_pwconv_dgrad_lattice_f32's output): one pass over the N x OH x OW
+ * output pixels, x = the layer input N x H x W x C read at the stride-s lattice with its BatchNorm
+ * (bn_*, required) applied on load, dx compact N x OH x OW x C, part (optional) that BN's partials,
+ * dk_pwconv_bwd_fused_rows(N, OH, OW, K, C) rows.  K = C = 64. */
+int dk_pwconv_bwd_bnbwd_lattice_f32(const float* g, const float* bn_x, int N, int OH, int OW, int K, const float* out_mean, const float* out_invstd, const float* out_gamma, const float* out_beta, int out_relu, const float* k12, const float* w_kc, int C, float l2, float* dw_kc, float* dx, const float* x, int H, int W, int stride, const float* bn_mean, const float* bn_invstd, const float* bn_gamma, const float* bn_beta, int bn_relu, double* part, void* ws, size_t ws_bytes, void* stream);
 int dk_pwconv_bwd_bnbwd_f32(const float* g, const float* bn_x, int N, int OH, int OW, int K, const float* out_mean, const float* out_invstd, const float* out_gamma, const float* out_beta, int out_relu, const float* k12, const float* w_kc, int C, float l2, float* dw_kc, float* dx, const float* residual, const float* x, const float* bn_mean, const float* bn_invstd, const float* bn_gamma, const float* bn_beta, int bn_relu, double* part, void* ws, size_t ws_bytes, void* stream);
 
 /* ---------------------------------------------------------------------------------------

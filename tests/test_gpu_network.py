@@ -316,6 +316,36 @@ def test_lattice_skip_agrees(monkeypatch):
 
 
 @pytest.mark.gpu
+def test_stem_lattice_fused_agrees(monkeypatch):
+    """The stem's strided pointwise layer takes its following BatchNorm's gradient and hands its
+    input gradient over as the lattice in one pass (dk_pwconv_bwd_bnbwd_lattice_f32) vs the
+    BatchNorm's apply + dk_pwconv_dgrad_lattice_f32 + the side-stream weight gradient
+    (DORKNET_PW_LATTICE_FUSED=0): every gradient agrees to fp32 rounding."""
+    from examples.resnet18_depsep import ResNet18, synthetic_batch
+    from dorknet_amd import _hip
+    X, _, onehot = synthetic_batch(2, seed=3)
+    grads = {}
+    orig = _hip.lib.dk_pwconv_bwd_bnbwd_lattice_f32
+    for fused in ("1", "0"):
+        monkeypatch.setenv("DORKNET_PW_LATTICE_FUSED", fused)
+        seen = []
+        monkeypatch.setattr(_hip.lib, "dk_pwconv_bwd_bnbwd_lattice_f32",
+                            lambda *a, seen=seen: seen.append(a[20]) or orig(*a))
+        np.random.seed(0)
+        net = ResNet18("r18")
+        net.to_gpu()
+        net.forward(dev(X), dev(onehot))
+        net.backward()
+        torch.cuda.synchronize()
+        assert (seen == [2]) == (fused == "1"), seen
+        grads[fused] = {(l.layer_name, k): host(v) for l in all_layers(net.layers) for k, v in (l.grads or {}).items()}
+    for key, a in grads["1"].items():
+        b = grads["0"][key]
+        err = np.linalg.norm((a - b).ravel()) / max(np.linalg.norm(b.ravel()), 1e-30)
+        assert err <= 1e-5 or np.linalg.norm(b.ravel()) < 1e-6, (key, err)
+
+
+@pytest.mark.gpu
 def test_join_mask_from_output_bitwise(monkeypatch):
     """The fused join backward takes the join's ReLU mask as (its output > 0) from the layer input
     it already reads, instead of the stored mask bytes (DORKNET_JOIN_MASK=1): every gradient is
