@@ -365,7 +365,8 @@ class deferred_wgrad_reduce:
     __slots__ = ("on", "slab", "ws")
 
     def __init__(self, layer, nbytes, defer=True):
-        self.on = bool(defer) and async_wgrad_enabled() and enabled("DORKNET_WGRAD_REDUCE_SIDE")
+        self.on = (bool(defer) and async_wgrad_enabled() and not _INLINE_REDUCE[0]
+                   and enabled("DORKNET_WGRAD_REDUCE_SIDE"))
         if self.on:
             slab = layer.__dict__.get("_dk_wgrad_slab")
             if slab is None or slab.numel() < nbytes:
@@ -403,6 +404,37 @@ def _flush_every() -> int:
         return min(60, max(1, int(getenv("DORKNET_WGRAD_FLUSH_EVERY", "60"))))  # (the C queue holds 64)
     except ValueError:
         return 60
+
+
+_INLINE_REDUCE = [False]
+
+
+class inline_wgrad_reduces:
+    """with inline_wgrad_reduces(): fused entry points keep their weight-gradient reduce on the
+    main stream (deferred_wgrad_reduce off).  The network's last step: nothing follows it on the
+    main stream to overlap, and a reduce sent to the side stream there costs two cross-stream hops
+    (~12 us each) before the update can start."""
+
+    def __enter__(self):
+        self.prev = _INLINE_REDUCE[0]
+        _INLINE_REDUCE[0] = True
+        return self
+
+    def __exit__(self, *exc):
+        _INLINE_REDUCE[0] = self.prev
+        return False
+
+
+def early_flush_steps() -> int:
+    """DORKNET_WGRAD_FLUSH_LAST (default 1): the network's backward flushes the recorded reduces
+    before each of its last this-many steps (0: only at the end of the backward).  With the reduces
+    batched until the end, the multi-task reduce ran after the last layer's kernels: ~90 us of tail
+    before the update (profiles/r05x_tail_timelines.txt); flushed before the last step it overlaps that
+    step's kernels (the stem's conv weight gradient, config 5's first depthwise backward)."""
+    try:
+        return max(0, int(getenv("DORKNET_WGRAD_FLUSH_LAST", "1")))
+    except ValueError:
+        return 1
 
 
 def flush_wgrad_reduces() -> None:

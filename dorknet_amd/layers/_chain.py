@@ -18,7 +18,8 @@ the per-layer parity tests; results are bit-identical either way).
 from __future__ import annotations
 
 from .._env import enabled
-from .._hip import DK_FOLDED, disarm_folds, inlaunch_folds_enabled, lib, resolve
+from .._hip import (DK_FOLDED, disarm_folds, early_flush_steps, flush_wgrad_reduces, inlaunch_folds_enabled,
+                    inline_wgrad_reduces, lib, resolve)
 from ._bn_input import accepts_bn_grad, accepts_bn_input, add_residual
 
 # BatchNormLayer / ReLu (their modules import this one): bound on first use
@@ -216,42 +217,55 @@ def _backward_steps(steps, dy, residual, after_step, need_input_grad, join):
     BatchNormLayer = _bn_relu()[0]
     last = len(steps) - 1
     fuse = fusion_enabled()
+    # the network's own chain (its image gradient is dropped): the weight-gradient reduces recorded
+    # so far go to the side stream before the last steps, where they run beside those steps'
+    # kernels instead of after the last one (_hip.early_flush_steps)
+    early = early_flush_steps() if not need_input_grad else 0
     for i in range(last, -1, -1):
-        step = steps[i]
-        # a BatchNorm whose producer can apply its backward while loading the gradient
-        # (layers/_bn_input.py BNGrad) hands over a deferred gradient instead of writing it
-        defer = (fuse and type(step[0]) is BatchNormLayer and i > 0 and len(steps[i - 1]) == 1
-                 and accepts_bn_grad(steps[i - 1][0], step[0]))
-        if len(step) == 2:
-            dy = step[0].backward_bn_relu(dy, step[1], defer=defer)
-        elif defer:
-            dy = step[0].backward(dy, defer=True)
-        elif i == 0 and not need_input_grad and residual is None and getattr(step[0], "skips_input_grad", False):
-            dy = step[0].backward(dy, need_dx=False)
-        elif i == 0 and residual is not None and getattr(step[0], "accepts_residual", False):
-            residual = resolve(residual)  # a skip gradient from the branch stream: wait for it here
-            if join is not None and getattr(step[0], "accepts_join", False):
-                dy = step[0].backward(dy, residual=residual, join=join)
-            else:
-                dy = step[0].backward(dy, residual=residual)
-            residual = None
-        elif (fuse and i >= 2 and len(step) == 1 and getattr(step[0], "lattice_ok", None) is not None
-              and step[0].lattice_ok() and type(steps[i - 1][0]) is BatchNormLayer and len(steps[i - 2]) == 1
-              and getattr(steps[i - 2][0], "accepts_lattice_grad", False)
-              and accepts_bn_grad(steps[i - 2][0], steps[i - 1][0])
-              and enabled("DORKNET_LATTICE")):
-            # a stride-2 pointwise layer whose input gradient goes (through a deferred BatchNorm) to a
-            # consumer that takes the lattice form: the widen's zeros are never written
-            dy = step[0].backward(dy, lattice_out=True)
-        elif fuse and i > 0 and len(step) == 1 and getattr(step[0], "accepts_join", False) and \
-                _join_of(steps[i - 1]) is not None:
-            dy = step[0].backward(dy, join=_join_of(steps[i - 1]))
+        if i < early:
+            flush_wgrad_reduces()
+        if i == 0 and early and enabled("DORKNET_WGRAD_INLINE_LAST"):
+            with inline_wgrad_reduces():
+                dy, residual = _backward_step(steps, i, dy, residual, need_input_grad, join, fuse, BatchNormLayer)
         else:
-            dy = step[0].backward(dy)
+            dy, residual = _backward_step(steps, i, dy, residual, need_input_grad, join, fuse, BatchNormLayer)
         if _progress:
-            notify_backward_done(step)
+            notify_backward_done(steps[i])
         if after_step is not None:
             after_step(i)
     if residual is not None:
         dy = add_residual(dy, resolve(residual))
     return dy
+
+
+def _backward_step(steps, i, dy, residual, need_input_grad, join, fuse, BatchNormLayer):
+    """Step i of _backward_steps: (its input gradient, the residual still to add -- None once
+    step 0 has added it in its dgrad epilogue)."""
+    step = steps[i]
+    # a BatchNorm whose producer can apply its backward while loading the gradient
+    # (layers/_bn_input.py BNGrad) hands over a deferred gradient instead of writing it
+    defer = (fuse and type(step[0]) is BatchNormLayer and i > 0 and len(steps[i - 1]) == 1
+             and accepts_bn_grad(steps[i - 1][0], step[0]))
+    if len(step) == 2:
+        return step[0].backward_bn_relu(dy, step[1], defer=defer), residual
+    if defer:
+        return step[0].backward(dy, defer=True), residual
+    if i == 0 and not need_input_grad and residual is None and getattr(step[0], "skips_input_grad", False):
+        return step[0].backward(dy, need_dx=False), residual
+    if i == 0 and residual is not None and getattr(step[0], "accepts_residual", False):
+        residual = resolve(residual)  # a skip gradient from the branch stream: wait for it here
+        if join is not None and getattr(step[0], "accepts_join", False):
+            return step[0].backward(dy, residual=residual, join=join), None
+        return step[0].backward(dy, residual=residual), None
+    if (fuse and i >= 2 and len(step) == 1 and getattr(step[0], "lattice_ok", None) is not None
+            and step[0].lattice_ok() and type(steps[i - 1][0]) is BatchNormLayer and len(steps[i - 2]) == 1
+            and getattr(steps[i - 2][0], "accepts_lattice_grad", False)
+            and accepts_bn_grad(steps[i - 2][0], steps[i - 1][0])
+            and enabled("DORKNET_LATTICE")):
+        # a stride-2 pointwise layer whose input gradient goes (through a deferred BatchNorm) to a
+        # consumer that takes the lattice form: the widen's zeros are never written
+        return step[0].backward(dy, lattice_out=True), residual
+    if fuse and i > 0 and len(step) == 1 and getattr(step[0], "accepts_join", False) and \
+            _join_of(steps[i - 1]) is not None:
+        return step[0].backward(dy, join=_join_of(steps[i - 1])), residual
+    return step[0].backward(dy), residual

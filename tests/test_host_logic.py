@@ -261,3 +261,14 @@ def test_wgrad_flush_batch_setting(monkeypatch):
     for v, want in (("1", 1), ("0", 1), ("8", 8), ("500", 60), ("x", 60)):
         monkeypatch.setenv("DORKNET_WGRAD_FLUSH_EVERY", v)
         assert _flush_every() == want
+
+
+def test_wgrad_flush_last_setting(monkeypatch):
+    """DORKNET_WGRAD_FLUSH_LAST: the network's backward flushes the recorded reduces before each of
+    its last this-many steps; 1 by default or when unparsable, never negative."""
+    from dorknet_amd._hip import early_flush_steps
+    monkeypatch.delenv("DORKNET_WGRAD_FLUSH_LAST", raising=False)
+    assert early_flush_steps() == 1
+    for v, want in (("0", 0), ("3", 3), ("-2", 0), ("x", 1)):
+        monkeypatch.setenv("DORKNET_WGRAD_FLUSH_LAST", v)
+        assert early_flush_steps() == want
