@@ -996,142 +996,331 @@ __global__ __launch_bounds__(NT, NT == 64 ? 2 : 1) void dw_bwd_fused_kernel(cons
   }
   // load cursors: the (image, row) of the dy row PF steps ahead (row H = the zero row) and of the
   // next x row (rows 0 .. H-1 of each image of the run)
+  constexpr bool ROT = sizeof(T) == 2 && CPT == 2;
   int pn = n0, prr = 0, xn = n0, xhh = 0;
+  // the x queue: the next x row (rows 0 .. H-1 of each image of the run); ROT: one entry per
+  // iteration instead, the first of each image empty (the iteration that publishes an image's row
+  // 0 finishes no dx row), so that its slots rotate with the iterations (xhh = entry, row xhh - 1)
+  auto next_x = [&](XQ& q) {
+    if constexpr (ROT) {
+      load_x_row(q, xhh > 0 ? xn : n1, xhh - 1);
+      if (++xhh > H) xhh = 0, ++xn;
+    } else {
+      load_x_row(q, xn, xhh);
+      if (++xhh == H) xhh = 0, ++xn;
+    }
+  };
 #pragma unroll
   for (int k = 0; k < PF; ++k) {
     load_dy_row(dq[k], pn, prr);
     if (++prr > H) prr = 0, ++pn;
-    load_x_row(xq[k], xn, xhh);
-    if (++xhh == H) xhh = 0, ++xn;
+    next_x(xq[k]);
   }
-  // flattened (image, row) loop: publish dy row rr of image n, then finish dx row rr - 1
-  const int iters = (n1 - n0) * (H + 1);
-  int n = n0, rr = 0;
-  for (int it = 0; it < iters; ++it) {
-    const int rowok = rr < H;
-    f32x4 d0[CPT];
-#pragma unroll
-    for (int j = 0; j < CPT; ++j) d0[j] = xform(widen(dq[0].g0[j]), widen(dq[0].x0[j]), rowok && cok0[j]);
-    // the halo columns: wave 0 only (2 CG <= 64) -- a wave-uniform branch with two columns per thread
-    f32x4 d1 = {0.f, 0.f, 0.f, 0.f};
-    if (CPT == 1 || tid < 64) d1 = xform(widen(dq[0].g1), widen(dq[0].x1), rowok && cok1);
-#pragma unroll
-    for (int k = 0; k + 1 < PF; ++k) dq[k] = dq[k + 1];
-    load_dy_row(dq[PF - 1], pn, prr);
-    if (++prr > H) prr = 0, ++pn;
-    f32x4* slot = ring + (it & 1) * NI;
-#pragma unroll
-    for (int j = 0; j < CPT; ++j) slot[(CPT * cl + j) * CG + cg] = d0[j];  // = slot[tid] for CPT 1
-    if (two) slot[CL * CG + tid] = d1;
-    __syncthreads();
-#pragma unroll
-    for (int s = 0; s < WC; ++s) {
-      d[0][s] = d[1][s];
-      d[1][s] = d[2][s];
-      d[2][s] = slot[(CPT * cl + s) * CG + cg];
-    }
-    const int nn = n;
-    if (++rr > H) {
-      rr = 0;
-      ++n;
-    }
-    if (rr == 1) continue;  // just published row 0 of an image: no dx row to finish yet
-    const int h = (rr == 0 ? H + 1 : rr) - 2;  // the dx row of image nn finished now
-    f32x4 xh[CPT], rh[CPT];
-#pragma unroll
-    for (int q = 0; q < CPT; ++q) {
-      xh[q] = widen(xq[0].xr[q]);
-      rh[q] = widen(xq[0].rv[q]);
-    }
-    f32x4 jh[CPT];
-    uint32_t jmh[CPT];
-#pragma unroll
-    for (int q = 0; q < CPT; ++q) {
-      jh[q] = xq[0].jxin[q];
-      jmh[q] = xq[0].jmask[q];
-    }
-#pragma unroll
-    for (int k = 0; k + 1 < PF; ++k) xq[k] = xq[k + 1];
-    load_x_row(xq[PF - 1], xn, xhh);
-    if (++xhh == H) xhh = 0, ++xn;
-    T* dxcol = dx ? dx + (size_t)pix(nn, 0, w) : nullptr;
-    // the input BN's output (+ReLU) for the weight gradient (bn_relu_out), and its ReLU mask (BN
-    // output > 0) kept as 4 bits for the backward partials (recomputing bn_out there re-read the
-    // BN terms from LDS once per element)
-    f32x4 xb[CPT];
-    uint32_t rmask[CPT];
-#pragma unroll
-    for (int q = 0; q < CPT; ++q) {
-      xb[q] = xh[q];
-      rmask[q] = 0xfu;
-    }
-    if constexpr (BNX) {
-      const f32x4 vbm = bm, vbi = bi, vbg = bg, vbb = bb;
-#pragma unroll
+  // ROT (bf16, two columns per thread): the row loop is unrolled by 6 (a multiple of the 3 window
+  // rows, of PF and of the 2 LDS slots) and the window and the dy load queue rotate by name -- phase
+  // P publishes into d[P % 3] and consumes / refills slot P % PF of both queues -- instead of by
+  // register copies: the
+  // copy of a queue slot at the loop latch waited for the loads still in flight (s_waitcnt vmcnt near
+  // 0 on the back edge), so no load stayed in flight across iterations.  512 x 56 x 56 x 64:
+  // 284 -> 255 us (profiles/r05ac_dwb_bf16_rotated_queue.txt; config 5 6.16 -> 6.06 ms).  fp32 and one column per thread keep the copies:
+  // rotated, their loops measured slower (more registers: the one-column kernels lost their third wave per
+  // SIMD; profiles/r05aa_dwb_rotation_experiments.txt).
+  if constexpr (ROT) {
+    int n = n0, rr = 0, it = 0;
+    auto step = [&](auto ph) __attribute__((always_inline)) {
+      constexpr int P = decltype(ph)::value;
+      constexpr int QP = ROT ? P % PF : 0, WP = ROT ? P % 3 : 0;
+      const int rowok = rr < H;
+      f32x4 d0[CPT];
+  #pragma unroll
+      for (int j = 0; j < CPT; ++j) d0[j] = xform(widen(dq[QP].g0[j]), widen(dq[QP].x0[j]), rowok && cok0[j]);
+      // the halo columns: wave 0 only (2 CG <= 64) -- a wave-uniform branch with two columns per thread
+      f32x4 d1 = {0.f, 0.f, 0.f, 0.f};
+      if (CPT == 1 || tid < 64) d1 = xform(widen(dq[QP].g1), widen(dq[QP].x1), rowok && cok1);
+      if constexpr (ROT) {
+        load_dy_row(dq[QP], pn, prr);
+      } else {
+  #pragma unroll
+        for (int k = 0; k + 1 < PF; ++k) dq[k] = dq[k + 1];
+        load_dy_row(dq[PF - 1], pn, prr);
+      }
+      if (++prr > H) prr = 0, ++pn;
+      f32x4* slot = ring + (ROT ? (P & 1) : (it & 1)) * NI;
+      ++it;
+  #pragma unroll
+      for (int j = 0; j < CPT; ++j) slot[(CPT * cl + j) * CG + cg] = d0[j];  // = slot[tid] for CPT 1
+      if (two) slot[CL * CG + tid] = d1;
+      __syncthreads();
+  #pragma unroll
+      for (int s = 0; s < WC; ++s) {
+        if constexpr (ROT) {
+          d[WP][s] = slot[(CPT * cl + s) * CG + cg];  // window row r now in d[(WP + 1 + r) % 3]
+        } else {
+          d[0][s] = d[1][s];
+          d[1][s] = d[2][s];
+          d[2][s] = slot[(CPT * cl + s) * CG + cg];
+        }
+      }
+      const int nn = n;
+      if (++rr > H) {
+        rr = 0;
+        ++n;
+      }
+      if (rr == 1) {  // just published row 0 of an image: no dx row to finish yet
+        if constexpr (ROT) next_x(xq[QP]);  // (its empty entry)
+        return;
+      }
+      const int h = (rr == 0 ? H + 1 : rr) - 2;  // the dx row of image nn finished now
+      f32x4 xh[CPT], rh[CPT];
+  #pragma unroll
       for (int q = 0; q < CPT; ++q) {
-        f32x4 xr;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          xr[e] = bn_out(xh[q][e], vbm[e], vbi[e], vbg[e], vbb[e]);
-          if (!(xr[e] > 0.f)) {
-            rmask[q] &= ~(1u << e);
-            if (bn.relu) xr[e] = 0.f;
+        xh[q] = widen(xq[QP].xr[q]);
+        rh[q] = widen(xq[QP].rv[q]);
+      }
+      f32x4 jh[CPT];
+      uint32_t jmh[CPT];
+  #pragma unroll
+      for (int q = 0; q < CPT; ++q) {
+        jh[q] = xq[QP].jxin[q];
+        jmh[q] = xq[QP].jmask[q];
+      }
+      if constexpr (ROT) {
+        next_x(xq[QP]);
+      } else {
+  #pragma unroll
+        for (int k = 0; k + 1 < PF; ++k) xq[k] = xq[k + 1];
+        next_x(xq[PF - 1]);
+      }
+      T* dxcol = dx ? dx + (size_t)pix(nn, 0, w) : nullptr;
+      // the input BN's output (+ReLU) for the weight gradient (bn_relu_out), and its ReLU mask (BN
+      // output > 0) kept as 4 bits for the backward partials (recomputing bn_out there re-read the
+      // BN terms from LDS once per element)
+      f32x4 xb[CPT];
+      uint32_t rmask[CPT];
+  #pragma unroll
+      for (int q = 0; q < CPT; ++q) {
+        xb[q] = xh[q];
+        rmask[q] = 0xfu;
+      }
+      if constexpr (BNX) {
+        const f32x4 vbm = bm, vbi = bi, vbg = bg, vbb = bb;
+  #pragma unroll
+        for (int q = 0; q < CPT; ++q) {
+          f32x4 xr;
+  #pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            xr[e] = bn_out(xh[q][e], vbm[e], vbi[e], vbg[e], vbb[e]);
+            if (!(xr[e] > 0.f)) {
+              rmask[q] &= ~(1u << e);
+              if (bn.relu) xr[e] = 0.f;
+            }
+          }
+          if (!bn.relu) rmask[q] = 0xfu;
+          xb[q] = win_ok[q] ? xr : f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+      }
+      f32x4 acc[CPT];
+  #pragma unroll
+      for (int q = 0; q < CPT; ++q) acc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+  #pragma unroll
+      for (int r = 0; r < R; ++r)
+  #pragma unroll
+        for (int s = 0; s < S; ++s) {
+          const f32x4 wv = WV(r, s);
+  #pragma unroll
+          for (int q = 0; q < CPT; ++q) {
+            acc[q] += d[ROT ? (WP + 1 + r) % 3 : r][q + s] * wv;
+            wacc[r][s] += d[ROT ? (WP + 1 + r) % 3 : r][q + s] * xb[q];
           }
         }
-        if (!bn.relu) rmask[q] = 0xfu;
-        xb[q] = win_ok[q] ? xr : f32x4{0.f, 0.f, 0.f, 0.f};
+  #pragma unroll
+      for (int q = 0; q < CPT; ++q) {
+        if (!win_ok[q]) continue;
+        if (res) acc[q] += rh[q];
+        T* dxp = dxcol ? dxcol + (size_t)h * W * C + (size_t)q * C : nullptr;
+        if constexpr (JOIN) {
+          acc[q] = rnd4<T>(acc[q]);
+  #pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            // dy * mask (activations.py:46); no mask given: this layer's input is the join's output
+            // y = max(v, 0), and y > 0 is exactly the stored mask (v > 0)
+            const bool keep = jn.mask ? ((jmh[q] >> (8 * e)) & 0xffu) != 0u : xh[q][e] > 0.f;
+            if (!keep) acc[q][e] = 0.f;
+            const float xn = (jh[q][e] - jm[e]) * ji[e];
+            s1[e] += (double)acc[q][e];
+            s2[e] += (double)acc[q][e] * (double)xn;
+          }
+          if (dxp) {
+            if (nt)
+              st4nt(dxp, acc[q]);
+            else
+              st4(dxp, acc[q]);
+          }
+        } else if (dxp) {
+          acc[q] = st4_kept(dxp, acc[q], nt);  // acc = what the store keeps
+        } else {
+          acc[q] = rnd4<T>(acc[q]);
+        }
+        if constexpr (STATS) {
+  #pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            float ge = acc[q][e];
+            const float xn = (xh[q][e] - bm[e]) * bi[e];
+            if (!((rmask[q] >> e) & 1u)) ge = 0.f;
+            s1[e] += (double)ge;
+            s2[e] += (double)ge * (double)xn;
+          }
+        }
       }
+    };
+    // flattened (image, row) loop: publish dy row rr of image n, then finish dx row rr - 1
+    using std::integral_constant;
+    const int iters = (n1 - n0) * (H + 1);
+    while (it + 6 <= iters) {
+      step(integral_constant<int, 0>{});
+      step(integral_constant<int, 1>{});
+      step(integral_constant<int, 2>{});
+      step(integral_constant<int, 3>{});
+      step(integral_constant<int, 4>{});
+      step(integral_constant<int, 5>{});
     }
-    f32x4 acc[CPT];
-#pragma unroll
-    for (int q = 0; q < CPT; ++q) acc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int r = 0; r < R; ++r)
-#pragma unroll
-      for (int s = 0; s < S; ++s) {
-        const f32x4 wv = WV(r, s);
-#pragma unroll
+    // the last iters % 6 iterations, phases continuing from 0
+    const int left = iters - it;
+    if (left > 0) step(integral_constant<int, 0>{});
+    if (left > 1) step(integral_constant<int, 1>{});
+    if (left > 2) step(integral_constant<int, 2>{});
+    if (left > 3) step(integral_constant<int, 3>{});
+    if (left > 4) step(integral_constant<int, 4>{});
+  } else {
+    // flattened (image, row) loop: publish dy row rr of image n, then finish dx row rr - 1
+    const int iters = (n1 - n0) * (H + 1);
+    int n = n0, rr = 0;
+    for (int it = 0; it < iters; ++it) {
+      const int rowok = rr < H;
+      f32x4 d0[CPT];
+  #pragma unroll
+      for (int j = 0; j < CPT; ++j) d0[j] = xform(widen(dq[0].g0[j]), widen(dq[0].x0[j]), rowok && cok0[j]);
+      // the halo columns: wave 0 only (2 CG <= 64) -- a wave-uniform branch with two columns per thread
+      f32x4 d1 = {0.f, 0.f, 0.f, 0.f};
+      if (CPT == 1 || tid < 64) d1 = xform(widen(dq[0].g1), widen(dq[0].x1), rowok && cok1);
+  #pragma unroll
+      for (int k = 0; k + 1 < PF; ++k) dq[k] = dq[k + 1];
+      load_dy_row(dq[PF - 1], pn, prr);
+      if (++prr > H) prr = 0, ++pn;
+      f32x4* slot = ring + (it & 1) * NI;
+  #pragma unroll
+      for (int j = 0; j < CPT; ++j) slot[(CPT * cl + j) * CG + cg] = d0[j];  // = slot[tid] for CPT 1
+      if (two) slot[CL * CG + tid] = d1;
+      __syncthreads();
+  #pragma unroll
+      for (int s = 0; s < WC; ++s) {
+        d[0][s] = d[1][s];
+        d[1][s] = d[2][s];
+        d[2][s] = slot[(CPT * cl + s) * CG + cg];
+      }
+      const int nn = n;
+      if (++rr > H) {
+        rr = 0;
+        ++n;
+      }
+      if (rr == 1) continue;  // just published row 0 of an image: no dx row to finish yet
+      const int h = (rr == 0 ? H + 1 : rr) - 2;  // the dx row of image nn finished now
+      f32x4 xh[CPT], rh[CPT];
+  #pragma unroll
+      for (int q = 0; q < CPT; ++q) {
+        xh[q] = widen(xq[0].xr[q]);
+        rh[q] = widen(xq[0].rv[q]);
+      }
+      f32x4 jh[CPT];
+      uint32_t jmh[CPT];
+  #pragma unroll
+      for (int q = 0; q < CPT; ++q) {
+        jh[q] = xq[0].jxin[q];
+        jmh[q] = xq[0].jmask[q];
+      }
+  #pragma unroll
+      for (int k = 0; k + 1 < PF; ++k) xq[k] = xq[k + 1];
+      load_x_row(xq[PF - 1], xn, xhh);
+      if (++xhh == H) xhh = 0, ++xn;
+      T* dxcol = dx ? dx + (size_t)pix(nn, 0, w) : nullptr;
+      // the input BN's output (+ReLU) for the weight gradient (bn_relu_out), and its ReLU mask (BN
+      // output > 0) kept as 4 bits for the backward partials (recomputing bn_out there re-read the
+      // BN terms from LDS once per element)
+      f32x4 xb[CPT];
+      uint32_t rmask[CPT];
+  #pragma unroll
+      for (int q = 0; q < CPT; ++q) {
+        xb[q] = xh[q];
+        rmask[q] = 0xfu;
+      }
+      if constexpr (BNX) {
+        const f32x4 vbm = bm, vbi = bi, vbg = bg, vbb = bb;
+  #pragma unroll
         for (int q = 0; q < CPT; ++q) {
-          acc[q] += d[r][q + s] * wv;
-          wacc[r][s] += d[r][q + s] * xb[q];
+          f32x4 xr;
+  #pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            xr[e] = bn_out(xh[q][e], vbm[e], vbi[e], vbg[e], vbb[e]);
+            if (!(xr[e] > 0.f)) {
+              rmask[q] &= ~(1u << e);
+              if (bn.relu) xr[e] = 0.f;
+            }
+          }
+          if (!bn.relu) rmask[q] = 0xfu;
+          xb[q] = win_ok[q] ? xr : f32x4{0.f, 0.f, 0.f, 0.f};
         }
       }
-#pragma unroll
-    for (int q = 0; q < CPT; ++q) {
-      if (!win_ok[q]) continue;
-      if (res) acc[q] += rh[q];
-      T* dxp = dxcol ? dxcol + (size_t)h * W * C + (size_t)q * C : nullptr;
-      if constexpr (JOIN) {
-        acc[q] = rnd4<T>(acc[q]);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          // dy * mask (activations.py:46); no mask given: this layer's input is the join's output
-          // y = max(v, 0), and y > 0 is exactly the stored mask (v > 0)
-          const bool keep = jn.mask ? ((jmh[q] >> (8 * e)) & 0xffu) != 0u : xh[q][e] > 0.f;
-          if (!keep) acc[q][e] = 0.f;
-          const float xn = (jh[q][e] - jm[e]) * ji[e];
-          s1[e] += (double)acc[q][e];
-          s2[e] += (double)acc[q][e] * (double)xn;
+      f32x4 acc[CPT];
+  #pragma unroll
+      for (int q = 0; q < CPT; ++q) acc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+  #pragma unroll
+      for (int r = 0; r < R; ++r)
+  #pragma unroll
+        for (int s = 0; s < S; ++s) {
+          const f32x4 wv = WV(r, s);
+  #pragma unroll
+          for (int q = 0; q < CPT; ++q) {
+            acc[q] += d[r][q + s] * wv;
+            wacc[r][s] += d[r][q + s] * xb[q];
+          }
         }
-        if (dxp) {
-          if (nt)
-            st4nt(dxp, acc[q]);
-          else
-            st4(dxp, acc[q]);
+  #pragma unroll
+      for (int q = 0; q < CPT; ++q) {
+        if (!win_ok[q]) continue;
+        if (res) acc[q] += rh[q];
+        T* dxp = dxcol ? dxcol + (size_t)h * W * C + (size_t)q * C : nullptr;
+        if constexpr (JOIN) {
+          acc[q] = rnd4<T>(acc[q]);
+  #pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            // dy * mask (activations.py:46); no mask given: this layer's input is the join's output
+            // y = max(v, 0), and y > 0 is exactly the stored mask (v > 0)
+            const bool keep = jn.mask ? ((jmh[q] >> (8 * e)) & 0xffu) != 0u : xh[q][e] > 0.f;
+            if (!keep) acc[q][e] = 0.f;
+            const float xn = (jh[q][e] - jm[e]) * ji[e];
+            s1[e] += (double)acc[q][e];
+            s2[e] += (double)acc[q][e] * (double)xn;
+          }
+          if (dxp) {
+            if (nt)
+              st4nt(dxp, acc[q]);
+            else
+              st4(dxp, acc[q]);
+          }
+        } else if (dxp) {
+          acc[q] = st4_kept(dxp, acc[q], nt);  // acc = what the store keeps
+        } else {
+          acc[q] = rnd4<T>(acc[q]);
         }
-      } else if (dxp) {
-        acc[q] = st4_kept(dxp, acc[q], nt);  // acc = what the store keeps
-      } else {
-        acc[q] = rnd4<T>(acc[q]);
-      }
-      if constexpr (STATS) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          float ge = acc[q][e];
-          const float xn = (xh[q][e] - bm[e]) * bi[e];
-          if (!((rmask[q] >> e) & 1u)) ge = 0.f;
-          s1[e] += (double)ge;
-          s2[e] += (double)ge * (double)xn;
+        if constexpr (STATS) {
+  #pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            float ge = acc[q][e];
+            const float xn = (xh[q][e] - bm[e]) * bi[e];
+            if (!((rmask[q] >> e) & 1u)) ge = 0.f;
+            s1[e] += (double)ge;
+            s2[e] += (double)ge * (double)xn;
+          }
         }
       }
     }
