@@ -1017,14 +1017,14 @@ __global__ __launch_bounds__(NT, NT == 64 ? 2 : 1) void dw_bwd_fused_kernel(cons
     next_x(xq[k]);
   }
   // ROT (bf16, two columns per thread): the row loop is unrolled by 6 (a multiple of the 3 window
-  // rows, of PF and of the 2 LDS slots) and the window and the dy load queue rotate by name -- phase
-  // P publishes into d[P % 3] and consumes / refills slot P % PF of both queues -- instead of by
-  // register copies: the
-  // copy of a queue slot at the loop latch waited for the loads still in flight (s_waitcnt vmcnt near
-  // 0 on the back edge), so no load stayed in flight across iterations.  512 x 56 x 56 x 64:
-  // 284 -> 255 us (profiles/r05ac_dwb_bf16_rotated_queue.txt; config 5 6.16 -> 6.06 ms).  fp32 and one column per thread keep the copies:
-  // rotated, their loops measured slower (more registers: the one-column kernels lost their third wave per
-  // SIMD; profiles/r05aa_dwb_rotation_experiments.txt).
+  // rows, of PF and of the 2 LDS slots) and the window and both load queues rotate by name -- phase
+  // P publishes into d[P % 3] and consumes / refills slot P % PF -- instead of by register copies:
+  // the copy of a queue slot at the loop latch waited for the loads still in flight (s_waitcnt
+  // vmcnt near 0 on the back edge), so no load stayed in flight across iterations.
+  // 512 x 56 x 56 x 64: 282 -> 251-270 us; config 5 6.16 -> 6.06 ms
+  // (profiles/r05ac_dwb_bf16_rotated_queue.txt).  fp32 and one column per thread keep the original
+  // loop: rotated, they took more registers (the one-column kernels lost their third wave per SIMD;
+  // profiles/r05aa_dwb_rotation_experiments.txt).
   if constexpr (ROT) {
     int n = n0, rr = 0, it = 0;
     auto step = [&](auto ph) __attribute__((always_inline)) {
