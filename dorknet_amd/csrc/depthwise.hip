@@ -296,9 +296,12 @@ __global__ __launch_bounds__(256, JOIN ? 2 : 1) void dw_fwd_kernel(const T* __re
     using PT = typename std::conditional<sizeof(T) == 2, uint2, f32x4>::type;
     PT pre[PFR ? NC : 1];
     f32x4 preb[(PFR && JOIN) ? NC : 1];
-    auto load_pre = [&](int ih) {
+    // (unconditional: a row past the segment reads nothing.  Issued under a branch, the loads went
+    // to temporaries copied into pre at the branch's end, which waited for them right there -- the
+    // prefetch was never in flight under the row's FMAs)
+    auto load_pre = [&](int ih, bool live_row) {
       if constexpr (PFR) {
-        const bool rv = (unsigned)ih < (unsigned)H;
+        const bool rv = live_row && (unsigned)ih < (unsigned)H;
 #pragma unroll
         for (int q = 0; q < NC; ++q) {
           const bool ok = rv && (unsigned)(iw0 + q) < (unsigned)W;
@@ -313,7 +316,7 @@ __global__ __launch_bounds__(256, JOIN ? 2 : 1) void dw_fwd_kernel(const T* __re
         }
       }
     };
-    if (oh0 + 1 < oh1) load_pre((oh0 + 1) * ST - pad + R - 1);
+    load_pre((oh0 + 1) * ST - pad + R - 1, oh0 + 1 < oh1);
     // one output row at ring phase P; false once the segment is done
     auto row = [&](int oh, auto PC) __attribute__((always_inline)) -> bool {
       constexpr int P = decltype(PC)::value;
@@ -344,7 +347,7 @@ __global__ __launch_bounds__(256, JOIN ? 2 : 1) void dw_fwd_kernel(const T* __re
           const int slot = RING ? (P * ST + r) % R : r;
           if constexpr (PFR && JOIN) {
             join_row(win[slot], pre, preb, oh * ST - pad + r);
-            if (oh + 1 < oh1) load_pre((oh + 1) * ST - pad + R - 1);
+            load_pre((oh + 1) * ST - pad + R - 1, oh + 1 < oh1);
           } else if constexpr (PFR) {
             // the prefetched row: widened, BN applied on the in-image elements (as load_row)
             const int ih = oh * ST - pad + r;
@@ -363,7 +366,7 @@ __global__ __launch_bounds__(256, JOIN ? 2 : 1) void dw_fwd_kernel(const T* __re
               }
               win[slot][q] = v;
             }
-            if (oh + 1 < oh1) load_pre((oh + 1) * ST - pad + R - 1);
+            load_pre((oh + 1) * ST - pad + R - 1, oh + 1 < oh1);
           } else if constexpr (JOIN) {
             join_load(win[slot], oh * ST - pad + r);
           } else {
