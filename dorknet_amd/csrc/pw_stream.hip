@@ -26,6 +26,8 @@
 // input BatchNorm's backward partial sums (sum g', sum g' x_hat) of dx.
 #include <stdlib.h>
 
+#include <type_traits>
+
 #include "dk_common.h"
 #include "fold_tail.h"
 
@@ -372,17 +374,18 @@ __global__ __launch_bounds__(256, KR_ == 64 ? 3 : 2) void fwd_kernel(FwdArgs a) 
     for (int q = 0; q < KQ; ++q)
       lx[q] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rx, (int)(base + 32u * q), 0, 0));
   };
-  f32x4 cx[KQ];
-  load_a(t, cx);
+  // the tile loop is unrolled by two so that the current and the prefetched tile's registers swap
+  // roles by name: copying the prefetched registers at the loop latch waited for their loads
+  f32x4 xa[KQ], xb[KQ];
+  load_a(t, xa);
   drain_vmem_loads();
-  for (; t < ntiles; t += W) {
+  auto tile = [&](f32x4 (&cx)[KQ], f32x4 (&nx)[KQ]) __attribute__((always_inline)) {
     const int m0 = t * TR;
     int z = 0;
     asm volatile("" : "+s"(z));
     const float* tb = &tab[0][0] + z;
     const float* bs = Bs + z;
 
-    f32x4 nx[KQ];
     load_a(t + W, nx);
     __builtin_amdgcn_sched_barrier(0);
 
@@ -450,28 +453,46 @@ __global__ __launch_bounds__(256, KR_ == 64 ? 3 : 2) void fwd_kernel(FwdArgs a) 
     const int mb = m0 + 4 * h;
     const uint32_t eb0 = row_off_bytes(mb, NO, l32), eb1 = eb0 + 16u * NO * 4u;
 #pragma unroll
-    for (int u = 0; u < NU; ++u) {
+    for (int u = 0; u < NU; ++u)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int dm = (r & 3) + 8 * (r >> 2);
-        const uint32_t imm = (uint32_t)(((r & 3) + 8 * ((r >> 2) & 1)) * NO + 32 * u) * 4u;
-        float v = acc[u][r];
-        if (a.bias) v += bias[u];
-        if (a.nt)
-          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), ry, (int)((r < 8 ? eb0 : eb1) + imm), 0,
-                                                2);
-        else
-          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), ry, (int)((r < 8 ? eb0 : eb1) + imm), 0,
-                                                0);
-        if constexpr (STATS) {
-          const double d = (mb + dm < a.M) ? (double)v : 0.0;
+      for (int r = 0; r < 16; ++r)
+        if (a.bias) acc[u][r] += bias[u];
+    // one branch around all the stores (the cache policy is an immediate): chosen per store, the
+    // branches hid the number of stores in flight from the wait-count pass, and the next tile waited
+    // for all of them (vmcnt(0)) before its loads were used
+    auto store_tile = [&](auto pol) __attribute__((always_inline)) {
+#pragma unroll
+      for (int u = 0; u < NU; ++u)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const uint32_t imm = (uint32_t)(((r & 3) + 8 * ((r >> 2) & 1)) * NO + 32 * u) * 4u;
+          const float v = acc[u][r];  // (not bit_cast(acc[u][r]): hipcc 7.2 stores element 0 for every r)
+          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), ry, (int)((r < 8 ? eb0 : eb1) + imm),
+                                                0, decltype(pol)::value);
+        }
+    };
+    if (a.nt)
+      store_tile(std::integral_constant<int, 2>{});
+    else
+      store_tile(std::integral_constant<int, 0>{});
+    if constexpr (STATS) {
+#pragma unroll
+      for (int u = 0; u < NU; ++u)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int dm = (r & 3) + 8 * (r >> 2);
+          const double d = (mb + dm < a.M) ? (double)acc[u][r] : 0.0;
           ps[u] += d;
           pq[u] += d * d;
         }
-      }
     }
-#pragma unroll
-    for (int q = 0; q < KQ; ++q) cx[q] = nx[q];
+  };
+  while (t < ntiles) {
+    tile(xa, xb);
+    t += W;
+    if (t >= ntiles) break;
+    tile(xb, xa);
+    t += W;
   }
   if constexpr (!STATS) return;
   __syncthreads();  // Bs becomes red
@@ -664,12 +685,14 @@ __global__ __launch_bounds__(256, PF ? 1 : 2) void bwd_fused_kernel(BwdArgs ba) 
       lx[q] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rx, (int)(base + 1024u * q), 0, 0));
     }
   };
-  f32x4 cg[KQ], cx[KQ];
+  // PF: the tile loop is unrolled by two and the current / prefetched registers swap roles by name
+  // (copied at the loop latch, the copy waited for the prefetch's loads)
+  f32x4 ga_[KQ], xa_[KQ], gb_[KQ], xb_[KQ];
   if constexpr (PF) {
-    load_a(t, cg, cx);
+    load_a(t, ga_, xa_);
     drain_vmem_loads();
   }
-  for (; t < ntiles; t += W) {
+  auto tile = [&](f32x4 (&cg)[KQ], f32x4 (&cx)[KQ], f32x4 (&ng)[KQ], f32x4 (&nx)[KQ]) __attribute__((always_inline)) {
     const int m0 = t * TR;
     int z = 0;
     asm volatile("" : "+s"(z));
@@ -705,7 +728,6 @@ __global__ __launch_bounds__(256, PF ? 1 : 2) void bwd_fused_kernel(BwdArgs ba) 
         if constexpr (RES)
           ers[u][r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rr, (int)(eb + imm), 0, 0));
       }
-    f32x4 ng[KQ], nx[KQ];
     if constexpr (PF) load_a(t + W, ng, nx);
     __builtin_amdgcn_sched_barrier(0);
 
@@ -755,7 +777,10 @@ __global__ __launch_bounds__(256, PF ? 1 : 2) void bwd_fused_kernel(BwdArgs ba) 
 
     // (4) per pixel pair r: wgrad aw[t][u] += dy[pixels]^T . bn(x)[pixels] (pixels past M contribute
     //     nothing), then (5) the dx epilogue rows of register r (+ residual) and the input BN's
-    //     partials
+    //     partials.  PF: one branch on the stores' cache policy around all of it (chosen per store,
+    //     the branches hid the stores in flight from the wait-count pass: the next tile's loads
+    //     waited for every store of this one)
+    auto epi = [&](auto pol) __attribute__((always_inline)) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int dm = (r & 3) + 8 * (r >> 2);
@@ -781,7 +806,10 @@ __global__ __launch_bounds__(256, PF ? 1 : 2) void bwd_fused_kernel(BwdArgs ba) 
         const uint32_t imm = (uint32_t)(((r & 3) + 8 * ((r >> 2) & 1)) * NO + 32 * u) * 4u;
         float v = acc[u][r];
         if constexpr (RES) v += ers[u][r];
-        if (a.nt)
+        if constexpr (decltype(pol)::value >= 0)
+          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), rdx, (int)((r < 8 ? eb0 : eb1) + imm),
+                                                0, decltype(pol)::value);
+        else if (a.nt)
           __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), rdx, (int)((r < 8 ? eb0 : eb1) + imm),
                                                 0, 2);
         else
@@ -797,13 +825,24 @@ __global__ __launch_bounds__(256, PF ? 1 : 2) void bwd_fused_kernel(BwdArgs ba) 
         }
       }
     }
-    if constexpr (PF) {
-#pragma unroll
-      for (int q = 0; q < KQ; ++q) {
-        cg[q] = ng[q];
-        cx[q] = nx[q];
-      }
+    };
+    if constexpr (!PF)
+      epi(std::integral_constant<int, -1>{});  // (hoisted, the branch cost this variant 512 bytes of spills)
+    else if (a.nt)
+      epi(std::integral_constant<int, 2>{});
+    else
+      epi(std::integral_constant<int, 0>{});
+  };
+  if constexpr (PF) {
+    while (t < ntiles) {
+      tile(ga_, xa_, gb_, xb_);
+      t += W;
+      if (t >= ntiles) break;
+      tile(gb_, xb_, ga_, xa_);
+      t += W;
     }
+  } else {
+    for (; t < ntiles; t += W) tile(ga_, xa_, gb_, xb_);
   }
 
   // the block's weight-gradient partial: the 4 waves summed in order through LDS
