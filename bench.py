@@ -205,8 +205,13 @@ ENTRY_KERNEL = {
     "dk_pwconv_dgrad_bnbwd_bf16": [("dk::pwsh::dgrad_bnbwd_kernel", ""), ("dk::pwd16::dgrad_kernel", ""),
                                    ("dk::igemm_f32", r"dk::LdMatKCT<[^>]*>, dk::MatBwdDescE<unsigned short>")],
     "dk_pwconv_fwd_ex_bf16": [("dk::pwsh::fwd_kernel", ""), ("dk::pwd16::fwd_kernel", "")],
-    "dk_dwconv_bwd_bnbwd_bf16": ("dk::dw_bwd_fused_kernel", r"unsigned short>"),
-    "dk_dwconv_fwd_ex_bf16": ("dk::dw_fwd_kernel", r"unsigned short>"),
+    "dk_dwconv_bwd_bnbwd_bf16": ("dk::dw_bwd_fused_kernel", r"unsigned short"),
+    "dk_dwconv_fwd_ex_bf16": ("dk::dw_fwd_kernel", r"unsigned short"),
+    # the fused pointwise backward (round 5): the streaming K = C = 64 kernel (not its lattice form,
+    # a separate entry) and the fused deep kernel
+    "dk_pwconv_bwd_bnbwd_f32": [("dk::pws::bwd_fused_kernel", r", false>$"), ("dk::pwd::bwd_kernel", "")],
+    "dk_dwconv_bwd_bnbwd_f32": ("dk::dw_bwd_fused_kernel", r"^dk::dw_bwd_fused_kernel<\w+, \w+, \w+, false, float"),
+    "dk_dwconv_fwd_ex_f32": ("dk::dw_fwd_kernel", r"float, false>"),
     "dk_conv2d_fwd_narrow_f32": ("dk::nar::fwd_kernel", ""),
     "dk_conv2d_wgrad_bnbwd_narrow_f32": ("dk::nar::wgrad_kernel", ""),
 }
@@ -216,6 +221,7 @@ ENTRY_KERNEL = {
 # that mix, dk_debug_stream_mix): dk_pwconv_dgrad_bnbwd_f32 reads g, the following BN's input and
 # the input BN's raw input, and writes dy and dx.
 ENTRY_MIX = {"dk_pwconv_dgrad_bnbwd_f32": (3, 2), "dk_pwconv_fwd_ex_f32": (1, 1), "dk_pwconv_wgrad_bnx_f32": (2, 0),
+             "dk_pwconv_bwd_bnbwd_f32": (3, 1),
              "dk_dwconv_bwd_bnbwd_f32": (3, 1), "dk_dwconv_fwd_ex_f32": (1, 1), "dk_bn_add_f32": (2, 1)}
 
 
