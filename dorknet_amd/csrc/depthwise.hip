@@ -127,16 +127,20 @@ struct DwTile {
   static constexpr int TW = 4;    // outputs per thread along W
 };
 
-// Output rows per thread (the input window slides down a segment of them).  8 measured best or
-// within noise of best on every training shape of configs 3 and 5 (scripts/dw_fwd_seg.py,
+// Output rows per thread (the input window slides down a segment of them).  Round 3 measured 8
+// best or within noise of best on every training shape of configs 3 and 5 (scripts/dw_fwd_seg.py,
 // profiles/r03q_dw_seg_{f32,bf16}.txt: fewer rows per thread re-load the window more often and the
 // extra blocks do not pay for it).
-// The default: segments of at most 8 rows, balanced (OH = 28 -> 4 x 7, OH = 14 -> 2 x 7 instead of
-// 8 + 8 + 8 + 4 / 8 + 6: the short last segments left threads idle; profiles/r04dw2_dwseg.txt).
+// Balanced segments (OH = 28 -> 4 x 7 rather than 8 + 8 + 8 + 4: short last segments left threads
+// idle; profiles/r04dw2_dwseg.txt).  At most 14 rows since round 5: with the row prefetch really in
+// flight (the unconditional load below) a row costs less and the window's prologue more, and
+// 14 rows per thread measured config 5 5.93 -> 5.84 ms, config 3 8.146 -> 8.132 ms
+// (profiles/r05ai_ab_dw_fwd_rows_per_thread.txt; whole columns were faster still for bf16, slower
+// for fp32).
 static inline int dw_fwd_seg(int OH) {
   const int seg = knob(kKnobDwSeg);  // tuning knob (kind 8): rows per thread; -1 = this rule
   if (seg > 0) return seg;
-  const int nseg = (OH + 7) / 8;
+  const int nseg = (OH + 13) / 14;
   return (OH + nseg - 1) / nseg;
 }
 
