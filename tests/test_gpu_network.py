@@ -86,6 +86,26 @@ def test_resnet18_depsep_training_steps(narrow, monkeypatch):
     _compare_step(net, onet, o32, X, onehot, lr=0.05 * 2 / 200.0)
 
 
+@pytest.mark.parametrize("seed", [3, 7])
+def test_resnet18_depsep_training_steps_batch8(seed):
+    """The same two training steps at batch 8 (every fused path of the step as the bench runs it:
+    the stem's lattice backward, the batched end-of-backward reduces, the fused stride-2 depthwise
+    backward), vs the fp64 oracle with the fp32 oracle bounding what vanishes in exact arithmetic.
+    Ties as at batch 2: input seeds 2 and 4 put a few res8 BN outputs within fp32 rounding of the
+    ReLU's zero and fail by 2e-4 / 4e-3 -- with bitwise-identical gradients whether the layers run
+    fused or not (DORKNET_FUSE=0; profiles/r05ap_batch8_seed_sweep.txt), so the fused kernels are
+    not what moves them; seeds 3 and 7 have none.  The full-size segments (test_gpu_fullsize.py)
+    carry batch 256."""
+    from examples.resnet18_depsep import ResNet18, synthetic_batch
+    np.random.seed(0)
+    net = ResNet18("r18")
+    onet = network_to_oracle(net)
+    o32 = network_to_oracle(net, np.float32)
+    net.to_gpu()
+    X, _, onehot = synthetic_batch(8, seed=seed)
+    _compare_step(net, onet, o32, X, onehot, lr=0.05 * 8 / 200.0)
+
+
 def test_resnet18_update_skip_projections():
     """SGDMomentum(update_skip_projections=True): the skip projections move (they stay put by
     default, the reference's quirk) and every weight after the update matches the oracle run
