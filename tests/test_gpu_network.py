@@ -92,9 +92,9 @@ def test_resnet18_depsep_training_steps_batch8(seed):
     the stem's lattice backward, the batched end-of-backward reduces, the fused stride-2 depthwise
     backward), vs the fp64 oracle with the fp32 oracle bounding what vanishes in exact arithmetic.
     Ties as at batch 2: input seeds 2 and 4 put a few res8 BN outputs within fp32 rounding of the
-    ReLU's zero and fail by 2e-4 / 4e-3 -- with bitwise-identical gradients whether the layers run
-    fused or not (DORKNET_FUSE=0; profiles/r05ap_batch8_seed_sweep.txt), so the fused kernels are
-    not what moves them; seeds 3 and 7 have none.  The full-size segments (test_gpu_fullsize.py)
+    ReLU's zero and fail by 2e-4 / 4e-3 -- with the same errors, to every printed digit, whether the
+    layers run fused or not (DORKNET_FUSE=0; profiles/r05ap_batch8_seed_sweep.txt), so the fused
+    kernels are not what moves them; seeds 3 and 7 have none.  The full-size segments (test_gpu_fullsize.py)
     carry batch 256."""
     from examples.resnet18_depsep import ResNet18, synthetic_batch
     np.random.seed(0)
