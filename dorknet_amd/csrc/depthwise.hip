@@ -830,7 +830,9 @@ struct BnBwdOut {  // the BatchNorm after this layer: dy = bn_bwd_elem(x1, g)
 // CPT: adjacent output columns per thread (CL / CPT threads per channel group).  With 2 a thread's
 // 3 x 4 window and its per-channel terms (LDS ptab, one read per row) serve two pixels: per element
 // half the LDS reads, the bound of the one-column form on bf16 (twice the elements per byte).
-template <bool BNX, bool STATS, bool RELU1, bool JOIN = false, class T = float, int CPT = 1, int NT = 256>
+// RES: a residual addend may be given (false: none -- its loads and widening are compiled out).
+template <bool BNX, bool STATS, bool RELU1, bool JOIN = false, class T = float, int CPT = 1, int NT = 256,
+          bool RES = true>
 __global__ __launch_bounds__(NT, NT == 64 ? 2 : 1) void dw_bwd_fused_kernel(const T* __restrict__ g, const T* __restrict__ x1,
                                                            uint32_t bytes, BnBwdOut ob, const T* __restrict__ x,
                                                            BnIn bn, const float* __restrict__ w_crs,
@@ -984,7 +986,10 @@ __global__ __launch_bounds__(NT, NT == 64 ? 2 : 1) void dw_bwd_fused_kernel(cons
     for (int j = 0; j < CPT; ++j) {
       const bool okj = win_ok[j] && hh < H && nn < n1;
       q.xr[j] = raw_load(rx, okj, pix(nn, hh, w + j));
-      q.rv[j] = raw_load(rres, okj, pix(nn, hh, w + j));
+      if constexpr (RES)
+        q.rv[j] = raw_load(rres, okj, pix(nn, hh, w + j));
+      else
+        q.rv[j] = Raw{};
       if constexpr (JOIN) {
         q.jmask[j] = __builtin_amdgcn_raw_buffer_load_b32(rjm, (int)(okj ? pix(nn, hh, w + j) : kOOBBytes), 0, 0);  // 4 mask bytes
         q.jxin[j] = bload4e<float>(rjx, okj, pix(nn, hh, w + j));
@@ -1082,7 +1087,7 @@ __global__ __launch_bounds__(NT, NT == 64 ? 2 : 1) void dw_bwd_fused_kernel(cons
   #pragma unroll
       for (int q = 0; q < CPT; ++q) {
         xh[q] = widen(xq[QP].xr[q]);
-        rh[q] = widen(xq[QP].rv[q]);
+        rh[q] = RES ? widen(xq[QP].rv[q]) : f32x4{0.f, 0.f, 0.f, 0.f};
       }
       f32x4 jh[CPT];
       uint32_t jmh[CPT];
@@ -1143,7 +1148,7 @@ __global__ __launch_bounds__(NT, NT == 64 ? 2 : 1) void dw_bwd_fused_kernel(cons
   #pragma unroll
       for (int q = 0; q < CPT; ++q) {
         if (!win_ok[q]) continue;
-        if (res) acc[q] += rh[q];
+        if (RES && res) acc[q] += rh[q];
         T* dxp = dxcol ? dxcol + (size_t)h * W * C + (size_t)q * C : nullptr;
         if constexpr (JOIN) {
           acc[q] = rnd4<T>(acc[q]);
@@ -1236,7 +1241,7 @@ __global__ __launch_bounds__(NT, NT == 64 ? 2 : 1) void dw_bwd_fused_kernel(cons
   #pragma unroll
       for (int q = 0; q < CPT; ++q) {
         xh[q] = widen(xq[0].xr[q]);
-        rh[q] = widen(xq[0].rv[q]);
+        rh[q] = RES ? widen(xq[0].rv[q]) : f32x4{0.f, 0.f, 0.f, 0.f};
       }
       f32x4 jh[CPT];
       uint32_t jmh[CPT];
@@ -1294,7 +1299,7 @@ __global__ __launch_bounds__(NT, NT == 64 ? 2 : 1) void dw_bwd_fused_kernel(cons
   #pragma unroll
       for (int q = 0; q < CPT; ++q) {
         if (!win_ok[q]) continue;
-        if (res) acc[q] += rh[q];
+        if (RES && res) acc[q] += rh[q];
         T* dxp = dxcol ? dxcol + (size_t)h * W * C + (size_t)q * C : nullptr;
         if constexpr (JOIN) {
           acc[q] = rnd4<T>(acc[q]);
@@ -2021,8 +2026,10 @@ static int dw_bwd_fused(const T* g, const T* bn_x, int N, int H, int W, int C, c
   constexpr int CPT2 = 2;
 #define DWB_LAUNCH(BNX_, STATS_, RELU1_)                                                                             \
   {                                                                                                                  \
-    auto k = geo.cpt == 2 ? dw_bwd_fused_kernel<BNX_, STATS_, RELU1_, false, T, CPT2>                              \
-                          : dw_bwd_fused_kernel<BNX_, STATS_, RELU1_, false, T>;                                   \
+    auto k = geo.cpt == 2 ? (residual ? dw_bwd_fused_kernel<BNX_, STATS_, RELU1_, false, T, CPT2>                 \
+                                      : dw_bwd_fused_kernel<BNX_, STATS_, RELU1_, false, T, CPT2, 256, false>)    \
+                          : (residual ? dw_bwd_fused_kernel<BNX_, STATS_, RELU1_, false, T>                       \
+                                      : dw_bwd_fused_kernel<BNX_, STATS_, RELU1_, false, T, 1, 256, false>);      \
     if (shm > 65536)                                                                                                 \
       (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,       \
                                 (int)shm);                                                                           \
@@ -2285,8 +2292,10 @@ DK_API int dk_dwconv_bwd_bnbwd_join_f32(const float* g, const float* bn_x, int N
   if (ring > shm) shm = ring;
 #define DWJ_LAUNCH(RELU1_)                                                                                           \
   {                                                                                                                  \
-    auto k = geo.cpt == 2 ? dw_bwd_fused_kernel<false, false, RELU1_, true, float, 2>                               \
-                          : dw_bwd_fused_kernel<false, false, RELU1_, true>;                                        \
+    auto k = geo.cpt == 2 ? (residual ? dw_bwd_fused_kernel<false, false, RELU1_, true, float, 2>                  \
+                                      : dw_bwd_fused_kernel<false, false, RELU1_, true, float, 2, 256, false>)     \
+                          : (residual ? dw_bwd_fused_kernel<false, false, RELU1_, true>                            \
+                                      : dw_bwd_fused_kernel<false, false, RELU1_, true, float, 1, 256, false>);    \
     if (shm > 65536)                                                                                                 \
       (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,       \
                                 (int)shm);                                                                           \
