@@ -1408,7 +1408,8 @@ __global__ __launch_bounds__(NT, NT == 64 ? 2 : 1) void dw_bwd_fused_kernel(cons
 // ReLU backward, its mask read off y, which the weight gradient loads anyway -- and the partials are
 // stage 1 of bn_j's backward over that dx (jn.x = x_j, jn.mean / invstd); jn.res_lat: the residual
 // is the stride-2 lattice only (a strided skip projection's input gradient, compact).
-template <bool BNX, bool STATS, bool RELU1, class T, bool JOIN = false>
+// RES: a residual addend may be given (false: its loads and adds are compiled out).
+template <bool BNX, bool STATS, bool RELU1, class T, bool JOIN = false, bool RES = true>
 __global__ __launch_bounds__(256, 2) void dw_bwd_s2_kernel(const T* __restrict__ g, const T* __restrict__ x1,
                                                           uint32_t ybytes, BnBwdOut ob, const T* __restrict__ x,
                                                           uint32_t xbytes, BnIn bn, const float* __restrict__ w_crs,
@@ -1505,7 +1506,7 @@ __global__ __launch_bounds__(256, 2) void dw_bwd_s2_kernel(const T* __restrict__
           if (JOIN && jn.res_lat)  // compact lattice residual: phase (0, 0) only, at quad (qi, j)
             acc[a][b] = bload4e<T>(rres, okp[a][b] && a == 0 && b == 0, (uint32_t)(((n * QH + qi) * QW + j) * C + c));
           else
-            acc[a][b] = res ? bload4e<T>(rres, okp[a][b], e) : f32x4{0.f, 0.f, 0.f, 0.f};
+            acc[a][b] = (RES && res) ? bload4e<T>(rres, okp[a][b], e) : f32x4{0.f, 0.f, 0.f, 0.f};
           if constexpr (JOIN) jxv[a][b] = bload4e<float>(rjx, okp[a][b], e);
           f32x4 v = xr[a][b];
           if constexpr (BNX) v = bn_in4(v, bm, bi, bg, bb, bn.relu);
@@ -1531,7 +1532,7 @@ __global__ __launch_bounds__(256, 2) void dw_bwd_s2_kernel(const T* __restrict__
         for (int b = 0; b < ST; ++b) {
           const int h = qi * ST + a, w = j * ST + b;
           const uint32_t e = (uint32_t)(((n * H + h) * W + w) * C + c);
-          f32x4 o = res ? dg[a][b] + acc[a][b] : dg[a][b];
+          f32x4 o = (RES && res) ? dg[a][b] + acc[a][b] : dg[a][b];
           o = rnd4<T>(o);  // the partials see dx as stored
           if constexpr (JOIN) {
 #pragma unroll
@@ -2157,9 +2158,16 @@ static int dw_bwd_s2(const T* g, const T* bn_x, int N, int H, int W, int C, int 
   if (!part || !fold_take(part, blocks, C, 1, &ft)) ft.part = nullptr;
   const size_t shm = (size_t)256 * 9 * 4 * sizeof(float);
 #define DWS2_LAUNCH(BNX_, STATS_, RELU1_)                                                                           \
-  hipLaunchKernelGGL((dw_bwd_s2_kernel<BNX_, STATS_, RELU1_, T>), dim3(blocks), dim3(256), shm, st, g, bn_x,       \
-                     (uint32_t)yb, ob, x, (uint32_t)xb, bn, w_crs, dx, residual, part, wpart, N, H, W, C, OH, OW, ft, \
-                     nt_stores(kNtDwDgrad))
+  do {                                                                                                              \
+    if (residual)                                                                                                   \
+      hipLaunchKernelGGL((dw_bwd_s2_kernel<BNX_, STATS_, RELU1_, T>), dim3(blocks), dim3(256), shm, st, g, bn_x,   \
+                         (uint32_t)yb, ob, x, (uint32_t)xb, bn, w_crs, dx, residual, part, wpart, N, H, W, C, OH, OW, \
+                         ft, nt_stores(kNtDwDgrad));                                                                \
+    else                                                                                                            \
+      hipLaunchKernelGGL((dw_bwd_s2_kernel<BNX_, STATS_, RELU1_, T, false, false>), dim3(blocks), dim3(256), shm,  \
+                         st, g, bn_x, (uint32_t)yb, ob, x, (uint32_t)xb, bn, w_crs, dx, residual, part, wpart, N, H, \
+                         W, C, OH, OW, ft, nt_stores(kNtDwDgrad));                                                  \
+  } while (0)
   if (out_relu) {
     if (part) DWS2_LAUNCH(true, true, true); else if (bn_mean) DWS2_LAUNCH(true, false, true);
     else DWS2_LAUNCH(false, false, true);
