@@ -831,8 +831,9 @@ struct BnBwdOut {  // the BatchNorm after this layer: dy = bn_bwd_elem(x1, g)
 // 3 x 4 window and its per-channel terms (LDS ptab, one read per row) serve two pixels: per element
 // half the LDS reads, the bound of the one-column form on bf16 (twice the elements per byte).
 // RES: a residual addend may be given (false: none -- its loads and widening are compiled out).
+// JM (JOIN): the join's ReLU mask bytes may be given (false: the mask is y > 0, no mask loads).
 template <bool BNX, bool STATS, bool RELU1, bool JOIN = false, class T = float, int CPT = 1, int NT = 256,
-          bool RES = true>
+          bool RES = true, bool JM = true>
 __global__ __launch_bounds__(NT, NT == 64 ? 2 : 1) void dw_bwd_fused_kernel(const T* __restrict__ g, const T* __restrict__ x1,
                                                            uint32_t bytes, BnBwdOut ob, const T* __restrict__ x,
                                                            BnIn bn, const float* __restrict__ w_crs,
@@ -991,7 +992,10 @@ __global__ __launch_bounds__(NT, NT == 64 ? 2 : 1) void dw_bwd_fused_kernel(cons
       else
         q.rv[j] = Raw{};
       if constexpr (JOIN) {
-        q.jmask[j] = __builtin_amdgcn_raw_buffer_load_b32(rjm, (int)(okj ? pix(nn, hh, w + j) : kOOBBytes), 0, 0);  // 4 mask bytes
+        if constexpr (JM)
+          q.jmask[j] = __builtin_amdgcn_raw_buffer_load_b32(rjm, (int)(okj ? pix(nn, hh, w + j) : kOOBBytes), 0, 0);  // 4 mask bytes
+        else
+          q.jmask[j] = 0u;
         q.jxin[j] = bload4e<float>(rjx, okj, pix(nn, hh, w + j));
       }
     }
@@ -1156,7 +1160,7 @@ __global__ __launch_bounds__(NT, NT == 64 ? 2 : 1) void dw_bwd_fused_kernel(cons
           for (int e = 0; e < 4; ++e) {
             // dy * mask (activations.py:46); no mask given: this layer's input is the join's output
             // y = max(v, 0), and y > 0 is exactly the stored mask (v > 0)
-            const bool keep = jn.mask ? ((jmh[q] >> (8 * e)) & 0xffu) != 0u : xh[q][e] > 0.f;
+            const bool keep = (JM && jn.mask) ? ((jmh[q] >> (8 * e)) & 0xffu) != 0u : xh[q][e] > 0.f;
             if (!keep) acc[q][e] = 0.f;
             const float xn = (jh[q][e] - jm[e]) * ji[e];
             s1[e] += (double)acc[q][e];
@@ -1307,7 +1311,7 @@ __global__ __launch_bounds__(NT, NT == 64 ? 2 : 1) void dw_bwd_fused_kernel(cons
           for (int e = 0; e < 4; ++e) {
             // dy * mask (activations.py:46); no mask given: this layer's input is the join's output
             // y = max(v, 0), and y > 0 is exactly the stored mask (v > 0)
-            const bool keep = jn.mask ? ((jmh[q] >> (8 * e)) & 0xffu) != 0u : xh[q][e] > 0.f;
+            const bool keep = (JM && jn.mask) ? ((jmh[q] >> (8 * e)) & 0xffu) != 0u : xh[q][e] > 0.f;
             if (!keep) acc[q][e] = 0.f;
             const float xn = (jh[q][e] - jm[e]) * ji[e];
             s1[e] += (double)acc[q][e];
@@ -2300,10 +2304,13 @@ DK_API int dk_dwconv_bwd_bnbwd_join_f32(const float* g, const float* bn_x, int N
   if (ring > shm) shm = ring;
 #define DWJ_LAUNCH(RELU1_)                                                                                           \
   {                                                                                                                  \
-    auto k = geo.cpt == 2 ? (residual ? dw_bwd_fused_kernel<false, false, RELU1_, true, float, 2>                  \
-                                      : dw_bwd_fused_kernel<false, false, RELU1_, true, float, 2, 256, false>)     \
-                          : (residual ? dw_bwd_fused_kernel<false, false, RELU1_, true>                            \
-                                      : dw_bwd_fused_kernel<false, false, RELU1_, true, float, 1, 256, false>);    \
+    auto k = geo.cpt == 2                                                                                          \
+                 ? (join_mask ? (residual ? dw_bwd_fused_kernel<false, false, RELU1_, true, float, 2>                \
+                                          : dw_bwd_fused_kernel<false, false, RELU1_, true, float, 2, 256, false>)   \
+                              : (residual ? dw_bwd_fused_kernel<false, false, RELU1_, true, float, 2, 256, true, false> \
+                                          : dw_bwd_fused_kernel<false, false, RELU1_, true, float, 2, 256, false, false>)) \
+                 : (residual ? dw_bwd_fused_kernel<false, false, RELU1_, true>                                        \
+                             : dw_bwd_fused_kernel<false, false, RELU1_, true, float, 1, 256, false>);               \
     if (shm > 65536)                                                                                                 \
       (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,       \
                                 (int)shm);                                                                           \
