@@ -388,22 +388,21 @@ class deferred_wgrad_reduce:
         return False
 
     def flush(self):
-        """Launch the recorded reduces once DORKNET_WGRAD_FLUSH_EVERY (default 60, i.e. at the end
-        of the backward) have collected: each flush makes the side stream wait for the main stream,
+        """Launch the recorded reduces once FLUSH_EVERY (60, i.e. at the end of the backward) have
+        collected: each flush makes the side stream wait for the main stream,
         and every such wait put a ~7 us gap between two main-stream kernels (an event marker); the
         slabs are per layer, so a recorded reduce can wait, and a flush runs all of them as one
         multi-task kernel.  flush_wgrad_reduces() launches the rest (the end of the backward, a
         data-parallel bucket's all-reduce).  Config 3 8.374 -> 8.339 ms, config 5 6.232 -> 6.147 ms
         (profiles/r05u_ab_flush_every_multi_*.txt)."""
-        if self.on and lib.dk_wgrad_reduce_pending() >= _flush_every():
+        if self.on and lib.dk_wgrad_reduce_pending() >= FLUSH_EVERY:
             flush_wgrad_reduces()
 
 
-def _flush_every() -> int:
-    try:
-        return min(60, max(1, int(getenv("DORKNET_WGRAD_FLUSH_EVERY", "60"))))  # (the C queue holds 64)
-    except ValueError:
-        return 60
+# Recorded reduces per flush, at most 60 (the C queue holds 64): 60 = only before the network's last
+# steps and at the end of the backward.  (A module constant; tests/test_gpu_streams.py sets it to
+# check that batching leaves every gradient bit-identical.)
+FLUSH_EVERY = 60
 
 
 _INLINE_REDUCE = [False]

@@ -1603,7 +1603,7 @@ __global__ __launch_bounds__(256, 2) void dw_bwd_s2_kernel(const T* __restrict__
 // Block geometry of the fused stride-1 backward: CG channel groups of 4 x CL / CPT column lanes
 // (CG * CL / CPT = 256 threads), a CL-column strip.  One column per thread: 16 columns x 64
 // channels, or 8 x 128 for narrow images; fewer channel groups (wider strips) when C / 4 has no
-// such factor.  Two columns per thread (DORKNET_DWB_COLS, kind 21; W >= 12): CG in {16, 32}
+// such factor.  Two columns per thread (knob kind 21; W >= 12): CG in {16, 32}
 // with the strip width (32 or 16 columns) that pads the row least, ties to the wider.  fp32 and bf16
 // alike: 512 x 56 x 56 x 64 bf16 328 -> 284 us, 256 x 56 x 56 x 64 fp32 205 -> 182 us (dwb_bench.py).
 struct DwbGeom {
@@ -1623,7 +1623,7 @@ static inline DwbGeom dwb_geom(int W, int C, int cpt, int nt = 256) {
 static inline int dwb_cpt(size_t) { return knob(kKnobDwbCols) == 2 ? 2 : 1; }
 static inline int dwb_nt(size_t) { return 256; }
 // Image runs of the fused stride-1 backward: one image per block while N * column strips * channel
-// tiles blocks fit DORKNET_DWB_BLOCKS (default 768 = three resident blocks per CU: its LDS and
+// tiles blocks fit knob kind 7 (default 768 = three resident blocks per CU: its LDS and
 // registers allow three); above that the batch is dealt into runs so the grid is one round (a
 // second, partial round of blocks cost small images up to twice the time: 7 x 7 x 512 ran 1024
 // one-image blocks).  0 = one image per block always.
@@ -2149,9 +2149,10 @@ static int dw_bwd_s2(const T* g, const T* bn_x, int N, int H, int W, int C, int 
   const BnIn bn{bn_mean, bn_invstd, bn_gamma, bn_beta, bn_relu};
   if (part && !bn_mean) return DK_ERR_ARGS;
   if (!aligned16(out_mean) || !aligned16(out_invstd) || !aligned16(out_gamma) || !aligned16(out_beta) ||
-      !aligned16(k12) || !bn_ok(bn) || ((reinterpret_cast<uintptr_t>(g) | reinterpret_cast<uintptr_t>(bn_x) |
-                                          reinterpret_cast<uintptr_t>(x)) & (4 * sizeof(T) - 1)))
-    return DK_ERR_ARGS;
+      !aligned16(k12) || !bn_ok(bn) ||
+      ((reinterpret_cast<uintptr_t>(g) | reinterpret_cast<uintptr_t>(bn_x) | reinterpret_cast<uintptr_t>(x) |
+        reinterpret_cast<uintptr_t>(dx) | reinterpret_cast<uintptr_t>(residual)) & (4 * sizeof(T) - 1)))
+    return DK_ERR_ARGS;  // (dx and the residual take 4-channel vector stores / loads too; null passes)
   const size_t xb = (size_t)N * H * W * C * sizeof(T), yb = (size_t)N * OH * OW * C * sizeof(T);
   if (!fits(xb)) return DK_ERR_ARGS;
   if (ws_bytes < dk_dwconv_bwd_s2_workspace_bytes(N, H, W, C)) return DK_ERR_WORKSPACE;

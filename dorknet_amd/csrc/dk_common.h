@@ -241,21 +241,20 @@ struct SubPix {
 enum : int { DK_ERR_ARGS = 10001, DK_ERR_WORKSPACE = 10002 };
 // Success, and the launch also folded the BN partials armed for it (dk_bn_fold_arm_*).
 enum : int { DK_FOLDED = 10100 };
-// Tuning knob (dk_debug_set_gemm_config kind 4): kernels that support it store their main output
-// nontemporally when set (A/B runs only; default from DORKNET_NT_STORES, else 0).
-// Nontemporal output stores per kernel family (tuning knob dk_debug_set_gemm_config(4, mask), env
-// DORKNET_NT_STORES=mask): bit kNt* set = that family's main output stores are nontemporal.
+// Nontemporal output stores per kernel family (tuning knob dk_debug_set_gemm_config(4, mask)): bit kNt*
+// set = that family's main output stores are nontemporal.
 enum NtFam : int { kNtDwFwd = 0, kNtDwBwd = 1, kNtBnAdd = 2, kNtPwsBwd = 3, kNtPwsFwd = 4, kNtPwsDgrad = 5, kNtGemm = 6, kNtStem = 7, kNtPwd = 8, kNtPwd16 = 9, kNtDwDgrad = 10, kNtBnBwd = 11 };
 constexpr int kNtDefault = 2431;  // families 0-6: config 3 8.868 -> 8.819 ms, config 5 7.596 -> 7.566 (profiles/r03q_ntfam_config*.txt); 8 (fp32 deep pointwise): config 3 8.697 -> 8.650 ms, 3 of 3 (profiles/r04nt_ab.txt); 11 (BN backward apply): config 3 8.719 -> 8.700 ms (profiles/r04nt2_ab.txt); off: 9 (bf16 deep pointwise, neutral), 10 (strided depthwise dgrad, fp32 neutral or slower)
 int nt_stores(int fam);
 
-// Run-time switches and tuning knobs (knobs.hip): one registry of atomics, defaults from the DORKNET_*
-// environment read once; dk_debug_set_gemm_config(kind = KnobId, v) overrides (-1 = default).
+// Path selectors and tuning knobs for tests and A/B runs (knobs.hip): one registry of atomics holding
+// the built-in defaults; dk_debug_set_gemm_config(kind = KnobId, v) overrides (-1 = default).  No
+// environment variable reaches them.  Numbers of retired knobs stay unused (tests and scripts address
+// knobs by number).
 enum KnobId : int {
-  kKnobRowCfg = 0, kKnobSplitCfg = 1, kKnobFillSplits = 2, kKnobPwStream = 3, kKnobNtStores = 4, kKnobPwsBwdPf = 5,
+  kKnobRowCfg = 0, kKnobSplitCfg = 1, kKnobFillSplits = 2, kKnobPwStream = 3, kKnobNtStores = 4,
   kKnobDwbBlocks = 7, kKnobDwSeg = 8, kKnobPwsh = 9, kKnobPwDeep = 11, kKnobPwDeep16 = 13, kKnobPwDeepBwd = 14,
-  kKnobPwStream128 = 15, kKnobPwfPrefetch = 16, kKnobPwfBlocksPerCu = 17, kKnobWgradBlocks = 18, kKnobEwVariant = 19,
-  kKnobPwsh16Bwd = 20, kKnobDwbCols = 21, kKnobMultiReduce = 22, kNumKnobs = 23
+  kKnobWgradBlocks = 18, kKnobEwVariant = 19, kKnobDwbCols = 21, kNumKnobs = 23
 };
 int knob(int id);
 void knob_set(int id, int v);

@@ -26,13 +26,13 @@ __global__ __launch_bounds__(256) void relu_fwd_kernel(const E* __restrict__ x, 
       v[e] = pos ? v[e] : 0.f;
       m |= (uint32_t)pos << (8 * e);
     }
-    st4(y + 4 * i, v);
+    if (y) st4(y + 4 * i, v);  // (y == NULL: the mask only)
     if (mask) reinterpret_cast<uint32_t*>(mask)[i] = m;
   }
   for (long long i = 4 * nv + (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
     const float v = ld1(x + i);
     const bool pos = v > 0.f;
-    st1(y + i, pos ? v : 0.f);
+    if (y) st1(y + i, pos ? v : 0.f);
     if (mask) mask[i] = pos;
   }
 }

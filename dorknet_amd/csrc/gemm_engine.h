@@ -1254,7 +1254,7 @@ static inline int splitk_config(int M, int N, int Kred, int mf = kMfF32) {
   return 1;  // 64x64x32: best or within 3% of best on every other measured wgrad shape
 }
 
-// Blocks a split-K weight gradient aims for (knob kKnobWgradBlocks, DORKNET_WGRAD_BLOCKS; default 1024).
+// Blocks a split-K weight gradient aims for (knob kKnobWgradBlocks, kind 18; default 1024).
 static inline int wgrad_target_blocks() {
   const int v = knob(kKnobWgradBlocks);
   return v > 0 ? v : 1024;

@@ -271,13 +271,8 @@ __global__ __launch_bounds__(256, 2) void pw_bwd_fused_kernel(const float* __res
   }
 }
 
-// Prefetch variant per shape (measured, scripts/pwf_bench.py); DORKNET_PWF_PREFETCH=0/1
-// overrides (tuning knob).
-static bool pwf_prefetch(int K, int C) {
-  const int v = knob(kKnobPwfPrefetch);
-  if (v >= 0) return v != 0;
-  return K * C <= 8192;
-}
+// Prefetch variant per shape (measured, scripts/pwf_bench.py).
+static bool pwf_prefetch(int K, int C) { return K * C <= 8192; }
 
 template <int K, int C, bool BNIN>
 static const void* pwf_kernel(bool pf) {
@@ -304,8 +299,7 @@ static int pwf_blocks(long long P, int K, int C, int* tpb_out) {
     oc.store(v, std::memory_order_relaxed);
   }
   const long long ntiles = (P + 63) / 64;
-  const int bpc = knob(kKnobPwfBlocksPerCu);  // tuning knob (DORKNET_PWF_BLOCKS_PER_CU)
-  long long nblk = (long long)(bpc > 0 ? bpc : o) * 256;
+  long long nblk = (long long)o * 256;
   if (nblk > ntiles) nblk = ntiles;
   if (nblk < 1) nblk = 1;
   const int tpb = (int)((ntiles + nblk - 1) / nblk);
@@ -388,7 +382,10 @@ DK_API int dk_pwconv_bwd_bnbwd_f32(const float* g, const float* bn_x, int N, int
                                    void* stream) {
   const hipStream_t st = as_stream(stream);
   if (N < 1 || OH < 1 || OW < 1 || (long long)N * OH * OW >= (1ll << 31)) return DK_ERR_ARGS;
-  const bool deep = pw_deep_bwd_ok(K, C, N * OH * OW) && (bn_mean != nullptr) == (part != nullptr);
+  // the deep kernel takes an input BN only with its partials (the rows / workspace queries assume the
+  // deep kernel whenever its shape fits, so that combination is refused rather than re-routed)
+  const bool deep = pw_deep_bwd_ok(K, C, N * OH * OW);
+  if (deep && (bn_mean != nullptr) != (part != nullptr)) return DK_ERR_ARGS;
   if (!pwf_supported(K, C) && !deep) return DK_ERR_ARGS;
   if (!g || !bn_x || !x || !w_kc || !dw_kc || !dx || !out_mean || !out_invstd || !out_gamma || !out_beta || !k12)
     return DK_ERR_ARGS;

@@ -433,6 +433,218 @@ __global__ __launch_bounds__(NT, dgrad_wps<KR>()) void dgrad_kernel(DgradArgs a)
 }
 
 // ---------------------------------------------------------------------------------------
+// The K = 512 dgrad at two waves per SIMD (round 6).  dgrad_kernel<512> holds each wave's B fragments
+// for 32 columns x 512 k in 256 VGPRs, so it runs one wave per SIMD and one block per CU, with no
+// second wave to cover its staging and barriers (0.28 of the fp32 MFMA peak in the step).  Here a
+// block of 8 waves owns the same 128 columns, 16 per wave, on v_mfma_f32_16x16x4_f32: a wave's B
+// fragments are 16 columns x 512 k = 128 VGPRs, so two waves share each SIMD.
+//   * the same exact-fp32 k order as the 32 x 32 x 2 kernels (MFMA i consumes k(i, 0..3), below), so
+//     dx and dy are bit-identical to dgrad_kernel and the tiled engine;
+//   * 16-pixel tiles (one 16 x 16 MFMA block per wave and tile; the LDS tile is 34 KB, double
+//     buffered), staged once per block with the BatchNorm backward formed on load, the next tile's
+//     global loads in flight during the MFMAs, one barrier per tile;
+//   * the LDS row is stored k-permuted, in four regions (one per MFMA k group kg = lane >> 4) holding
+//     the values in the order the MFMAs consume them, so one ds_read_b128 feeds four MFMAs;
+//   * the following BN's per-channel terms live in an LDS table (no registers through the MFMAs).
+// k order: the 32 x 32 x 2 chain consumes k = 8q + e then 8q + 4 + e for e = 0..3, q = 0..K/8-1
+// (exact fp32, an fmaf chain in k order: MI355X_MICROARCH.md).  MFMA i of the 16 x 16 x 4 chain takes
+// four consecutive of those, k(i, kg) = 8 (i >> 1) + 2 (i & 1) + (kg >> 1) + 4 (kg & 1).
+// ---------------------------------------------------------------------------------------
+constexpr int TR16 = 16;          // pixels per tile
+constexpr int NW16 = 8;           // waves per block, 16 columns each (the block's NB = 128 columns)
+constexpr int NT16 = 64 * NW16;   // threads per block
+
+template <int KR>
+struct K16 {
+  static constexpr int RS = KR / 4 + 4;  // region stride (floats): KR / 4 values per k group, + 4
+  static constexpr int SK = 4 * RS + 4;  // row stride: odd in float4s (conflict-free row-strided b128 reads)
+  static constexpr int KV = KR / 4;      // float4s per pixel row
+  static constexpr int LV = TR16 * KV / NT16;
+  static constexpr int NQ = KR / 16;     // ds_read_b128 per row block (4 MFMAs each)
+};
+
+// acc = the 16 x 16 tile product: A from the lane's k-group region (row l & 15), four values per read
+template <int NQ>
+__device__ __forceinline__ void mfma16_tile(const float* ap, const f32x4* bw, f32x4& acc) {
+  constexpr int D = 4;
+  acc = f32x4{0.f, 0.f, 0.f, 0.f};
+  f32x4 ab[D];
+#pragma unroll
+  for (int i = 0; i < D; ++i) ab[i] = ld4(ap + 4 * i);
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    const f32x4 av = ab[q % D];
+    if (q + D < NQ) ab[q % D] = ld4(ap + 4 * (q + D));
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u], bw[q][u], acc, 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+template <int KR, bool RES, bool PART>
+__global__ __launch_bounds__(NT16, 1) void dgrad16_kernel(DgradArgs a) {
+  using L = K16<KR>;
+  constexpr int SK = L::SK, RS = L::RS, KV = L::KV, LV = L::LV, NQ = L::NQ;
+  static_assert(KR % 64 == 0 && (SK / 4) % 2 == 1 && NT16 % KV == 0 && LV >= 1, "pwd::dgrad16_kernel shape");
+  __shared__ __attribute__((aligned(16))) float As[2][TR16 * SK];
+  __shared__ __attribute__((aligned(16))) f32x4 bnt[7][KV];
+  static_assert(sizeof(double) * 2 * NT16 <= sizeof(float) * 2 * TR16 * SK, "fold scratch fits in the tiles");
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int c16 = lane & 15, kg = lane >> 4;
+  const int n0 = blockIdx.y * NB, N = a.N;
+  const int col = n0 + 16 * wave + c16;
+  const int kv = tid % KV, r0 = tid / KV;
+  if (tid < KV) {
+    const f32x4 ga = ld4(a.og + 4 * tid), is = ld4(a.ois + 4 * tid);
+    bnt[0][tid] = ld4(a.om + 4 * tid);
+    bnt[1][tid] = is;
+    bnt[2][tid] = ga;
+    bnt[3][tid] = ld4(a.ob + 4 * tid);
+    bnt[4][tid] = ld4(a.k12 + 4 * tid);
+    bnt[5][tid] = ld4(a.k12 + KR + 4 * tid);
+    f32x4 f;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) f[e] = ga[e] * is[e];
+    bnt[6][tid] = f;
+  }
+  const float pm = PART ? a.im[col] : 0.f, pis = PART ? a.iis[col] : 0.f, pga = PART ? a.ig[col] : 0.f,
+              pbe = PART ? a.ib[col] : 0.f;
+  const bool orelu = a.orelu != 0, irelu = a.irelu != 0;
+  const bool writer = a.dy_out != nullptr && blockIdx.y == 0;
+  const int ntiles = (a.M + TR16 - 1) / TR16, G = gridDim.x;
+  uint32_t lofs[LV];
+#pragma unroll
+  for (int j = 0; j < LV; ++j) lofs[j] = off4(r0 + j * (NT16 / KV), KR, 4 * kv);
+  // C layout of a 16 x 16 block: lane (c16, kg) holds rows 4 kg + r, column col
+  const uint32_t cbase = off4(4 * kg, N, col);
+  // staging destinations: float4 kv of a row (k = 4 kv .. + 3) goes to regions (kv & 1) and (kv & 1) + 2
+  // at position kv & ~1, as two float2 (see the k order above)
+  const int sreg = (kv & 1) * RS + (kv & ~1);
+
+  auto tile_rsrc16 = [&](const float* p, int ld, int tile, int nrows) {
+    const int rows = nrows - tile * TR16;
+    return make_rsrc_v(p + (size_t)tile * TR16 * ld, rows > 0 ? (uint32_t)rows * ld * 4u : 0u);
+  };
+  auto load_tile = [&](int tile, f32x4* sg, f32x4* sx) {
+    const __amdgpu_buffer_rsrc_t rg = tile_rsrc16(a.g, KR, tile, a.M), rx = tile_rsrc16(a.xo, KR, tile, a.M);
+#pragma unroll
+    for (int j = 0; j < LV; ++j) {
+      sg[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rg, (int)lofs[j], 0, 0));
+      sx[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rx, (int)lofs[j], 0, 0));
+    }
+  };
+  auto stage = [&](int tile, float* dst, const f32x4* sg, const f32x4* sx) {
+    const __amdgpu_buffer_rsrc_t rdy = tile_rsrc16(writer ? a.dy_out : a.g, KR, tile, writer ? a.M : 0);
+    const f32x4 mu = bnt[0][kv], is = bnt[1][kv], ga = bnt[2][kv], be = bnt[3][kv], k1 = bnt[4][kv], k2 = bnt[5][kv],
+                f = bnt[6][kv];
+#pragma unroll
+    for (int j = 0; j < LV; ++j) {
+      const int r = r0 + j * (NT16 / KV);
+      f32x4 v;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float xe = sx[j][e];
+        float ge = sg[j][e];
+        const bool kill = (!(bn_out(xe, mu[e], is[e], ga[e], be[e]) > 0.f)) & orelu;
+        ge = kill ? 0.f : ge;
+        v[e] = bn_bwd_elem(xe, ge, mu[e], is[e], f[e], k1[e], k2[e]);
+      }
+      float* d = dst + r * SK + sreg;
+      *reinterpret_cast<f32x2*>(d) = f32x2{v[0], v[2]};
+      *reinterpret_cast<f32x2*>(d + 2 * RS) = f32x2{v[1], v[3]};
+      bstore_nt(__builtin_bit_cast(u32x4, v), rdy, (int)lofs[j], 0, a.nt);
+    }
+  };
+
+  __syncthreads();  // the BN table
+  int t = first_tile(ntiles);
+  f32x4 bw[NQ];
+  {
+    f32x4 sg[LV], sx[LV];
+    load_tile(t, sg, sx);
+    // B fragments W[k(i, kg)][col], i = 4q + u, after the first tile's loads
+#pragma unroll
+    for (int q = 0; q < NQ; ++q)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int i = 4 * q + u;
+        const int k = 8 * (i >> 1) + 2 * (i & 1) + (kg >> 1) + 4 * (kg & 1);
+        bw[q][u] = a.w[(size_t)k * N + col];
+      }
+    stage(t, &As[0][0], sg, sx);
+  }
+  __syncthreads();
+  double ps = 0.0, pq = 0.0;
+  int buf = 0;
+  for (; t < ntiles; t += G) {
+    f32x4 ng[LV], nx[LV];
+    load_tile(t + G, ng, nx);
+    const int mb = t * TR16 + 4 * kg;
+    const __amdgpu_buffer_rsrc_t rxi = tile_rsrc16(PART ? a.xi : a.g, N, t, PART ? a.M : 0);
+    const __amdgpu_buffer_rsrc_t rr = tile_rsrc16(RES ? a.res : a.g, N, t, RES ? a.M : 0);
+    const __amdgpu_buffer_rsrc_t rdx = tile_rsrc16(a.dx, N, t, a.M);
+    float exi[4], ers[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      if constexpr (PART)
+        exi[r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rxi, (int)cbase, r * N * 4, 0));
+      if constexpr (RES)
+        ers[r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rr, (int)cbase, r * N * 4, 0));
+    }
+    f32x4 acc;
+    mfma16_tile<NQ>(&As[buf][0] + c16 * SK + kg * RS, bw, acc);
+    if constexpr (RES) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[r] += ers[r];
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float v = acc[r];
+      bstore_nt(__builtin_bit_cast(uint32_t, v), rdx, (int)cbase, r * N * 4, a.nt);
+    }
+    if constexpr (PART) {
+      const bool full = t * TR16 + TR16 <= a.M;  // a whole tile (uniform): no row masks
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float x = exi[r];
+        const float xh = (x - pm) * pis;
+        const bool kill = ((!(pga * xh + pbe > 0.f)) & irelu) | (!full && mb + r >= a.M);
+        const float gv = kill ? 0.f : acc[r];
+        ps += (double)gv;
+        pq += (double)gv * (double)xh;
+      }
+    }
+    stage(t + G, &As[buf ^ 1][0], ng, nx);
+    __syncthreads();
+    buf ^= 1;
+  }
+  if constexpr (PART) {
+    // the block's partial row: the four k-group lanes of a column, then the waves' columns
+    double(*const red)[NB] = reinterpret_cast<double(*)[NB]>(&As[0][0]);  // [2][NB]
+    ps += __shfl_xor(ps, 16, 64);
+    pq += __shfl_xor(pq, 16, 64);
+    ps += __shfl_xor(ps, 32, 64);
+    pq += __shfl_xor(pq, 32, 64);
+    __syncthreads();  // the pixel tiles become scratch
+    if (kg == 0) {
+      red[0][16 * wave + c16] = ps;
+      red[1][16 * wave + c16] = pq;
+    }
+    __syncthreads();
+    for (int i = tid; i < 2 * NB; i += NT16) {
+      const int which = i / NB, c = i - which * NB;
+      pub_store(a.part + ((size_t)blockIdx.x * 2 + which) * N + n0 + c, red[which][c]);
+    }
+    if (a.ft.part) {
+      __syncthreads();  // red is read before the fold overwrites it
+      fold_tail<NT16>(a.ft, blockIdx.x, n0, NB, blockIdx.y, reinterpret_cast<double2*>(&As[0][0]));
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------
 // Fused backward (layers/pointwise_convolution.py:57-75 with the following BatchNorm's backward,
 // batch_norm.py:125-174, formed on load): the dgrad above plus the weight gradient
 //   dW[k][c] = sum_m dy[m][k] * bn_relu(x)[m][c]
@@ -661,10 +873,11 @@ __global__ __launch_bounds__(NT, bwd_wps<KR>()) void bwd_kernel(BwdArgs a) {
 // Host side: the instantiated reductions and the grid.
 // ---------------------------------------------------------------------------------------
 #define DK_PWD_KR(X) X(64) X(128) X(256) X(512)
+#define DK_PWD_KR_DGRAD(X) X(64) X(128) X(256)  // (K = 512: dgrad16_kernel)
 
-static int occupancy(const void* fn) {
+static int occupancy(const void* fn, int nt = NT) {
   int v = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, fn, NT, 0) != hipSuccess || v < 1) v = 1;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, fn, nt, 0) != hipSuccess || v < 1) v = 1;
   return v;
 }
 
@@ -698,6 +911,20 @@ static int dgrad_occ() {
 }
 
 template <int KR>
+static int dgrad16_occ() {
+  static const int occ = [] {
+    const void* fs[] = {reinterpret_cast<const void*>(&dgrad16_kernel<KR, true, true>),
+                        reinterpret_cast<const void*>(&dgrad16_kernel<KR, true, false>),
+                        reinterpret_cast<const void*>(&dgrad16_kernel<KR, false, true>),
+                        reinterpret_cast<const void*>(&dgrad16_kernel<KR, false, false>)};
+    int o = 1 << 20;
+    for (const void* f : fs) o = std::min(o, occupancy(f, NT16));
+    return o;
+  }();
+  return occ;
+}
+
+template <int KR>
 static int bwd_occ() {
   static const int occ = [] {
     const void* fs[] = {reinterpret_cast<const void*>(&bwd_kernel<KR, true, true>),
@@ -717,8 +944,8 @@ static int bwd_occ() {
 // that walker x of every column group runs on one XCD (block id x + gx * y) and the groups of a row
 // tile share that XCD's L2 copy of its pixels.  A function of (M, N, occupancy) only: callers
 // allocate exactly the partial rows the launch writes.
-static int grid_x(int M, int N, int occ) {
-  const int ntiles = (M + TR - 1) / TR;
+static int grid_x(int M, int N, int occ, int tr = TR) {
+  const int ntiles = (M + tr - 1) / tr;
   const int groups = N / NB;
   int slots = occ * 256 / groups;
   if (slots < 1) slots = 1;
@@ -730,7 +957,7 @@ static int grid_x(int M, int N, int occ) {
 
 }  // namespace pwd
 
-// DORKNET_PW_DEEP=0 (or the streaming switch DORKNET_PW_STREAM=0) keeps the earlier paths; knob 11.
+// Knob 11 = 0 (or the streaming knob 3 = 0) keeps the earlier paths.
 static bool pwd_enabled() { return knob(kKnobPwDeep) == 1 && pw_stream_enabled(); }
 
 static bool pwd_kr(int KR) { return KR == 64 || KR == 128 || KR == 256 || KR == 512; }
@@ -754,10 +981,14 @@ int pw_deep_fwd_rows(int M, int K, int C) {
   return 0;
 }
 int pw_deep_fwd_slices(int M, int K, int C) { return K / pwd::NB; }
+// K = 512 runs the two-waves-per-SIMD 16 x 16 kernel (dgrad16_kernel), 16-pixel tiles.
+static bool pwd_dgrad16(int K) { return K == 512; }
+
 int pw_deep_dgrad_rows(int M, int K, int C) {
+  if (pwd_dgrad16(K)) return pwd::grid_x(M, C, pwd::dgrad16_occ<512>(), pwd::TR16);
 #define DK_ROWS(kr) \
   if (K == kr) return pwd::grid_x(M, C, pwd::dgrad_occ<kr>());
-  DK_PWD_KR(DK_ROWS)
+  DK_PWD_KR_DGRAD(DK_ROWS)
 #undef DK_ROWS
   return 0;
 }
@@ -818,6 +1049,19 @@ int pw_deep_dgrad_bnbwd(const float* g, const float* bn_x, int M, int K, int C, 
   a.nt = nt_stores(kNtPwd);
   const dim3 grid(pw_deep_dgrad_rows(M, K, C), C / pwd::NB);
   if (grid.x == 0) return DK_ERR_ARGS;
+  if (pwd_dgrad16(K)) {
+#define DK_L16(R_, P_) hipLaunchKernelGGL((pwd::dgrad16_kernel<512, R_, P_>), grid, dim3(pwd::NT16), 0, st, a)
+    if (res && x)
+      DK_L16(true, true);
+    else if (res)
+      DK_L16(true, false);
+    else if (x)
+      DK_L16(false, true);
+    else
+      DK_L16(false, false);
+#undef DK_L16
+    return launch_status();
+  }
 #define DK_L(kr, R_, P_) hipLaunchKernelGGL((pwd::dgrad_kernel<kr, R_, P_>), grid, dim3(pwd::NT), 0, st, a)
 #define DK_DG(kr)             \
   if (K == kr) {              \
@@ -831,14 +1075,14 @@ int pw_deep_dgrad_bnbwd(const float* g, const float* bn_x, int M, int K, int C, 
       DK_L(kr, false, false); \
     return launch_status();   \
   }
-  DK_PWD_KR(DK_DG)
+  DK_PWD_KR_DGRAD(DK_DG)
 #undef DK_DG
 #undef DK_L
   return DK_ERR_ARGS;
 }
 
 // Fused deep backward (bwd_kernel): reduction K in {128, 256}, C a multiple of the block's 128 columns.
-// Default on; DORKNET_PW_DEEP_BWD=0 (knob 14) keeps the dgrad + side-stream weight gradient pair.
+// Default on; knob 14 = 0 keeps the dgrad + side-stream weight gradient pair.
 static bool pwd_bwd_enabled() { return knob(kKnobPwDeepBwd) == 1 && pwd_enabled(); }
 bool pw_deep_bwd_ok(int K, int C, int M) {
   if (!pwd_bwd_enabled() || M <= 0 || (K != 128 && K != 256) || C % pwd::NB) return false;

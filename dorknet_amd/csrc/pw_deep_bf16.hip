@@ -630,7 +630,7 @@ static int grid_x(int M, int N, int occ) {
 
 }  // namespace pwd16
 
-// DORKNET_PW_DEEP_BF16=0 (knob 13) keeps the tiled engine's bf16 mode for the deep shapes.
+// Knob 13 = 0 keeps the tiled engine's bf16 mode for the deep shapes.
 static bool pwd16_enabled() { return knob(kKnobPwDeep16) == 1; }
 static bool pwd16_kr(int KR) { return KR == 128 || KR == 256 || KR == 512; }
 
@@ -737,7 +737,7 @@ static int bwd_occ16() {
 // The fused bf16 backward: K in {128, 256}, C a multiple of the block's 128 columns (knob 20 with the
 // K = C = 64 streaming form; 2 keeps only that one).
 bool pw_deep16_bwd_ok(int K, int C, int M) {
-  if (!pwd16_enabled() || knob(kKnobPwsh16Bwd) != 1 || M <= 0 || (K != 128 && K != 256) || C % pwd16::NB || C > 4096)
+  if (!pwd16_enabled() || M <= 0 || (K != 128 && K != 256) || C % pwd16::NB || C > 4096)
     return false;
   return (size_t)M * (K > C ? K : C) * 2 < ((size_t)1 << 31);
 }

@@ -889,28 +889,25 @@ __global__ __launch_bounds__(256, PF ? 1 : 2) void bwd_fused_kernel(BwdArgs ba) 
   }
 }
 
-// The backward's A-operand prefetch (knob kKnobPwsBwdPf, DORKNET_PWS_BWD_PF, kind 5).  Default: no
-// prefetch, 2 waves per SIMD (whole step 9.12 -> 9.02 ms, scripts/ab_step.py, r03).
-static bool bwd_pf() { return knob(kKnobPwsBwdPf) == 1; }
-
-template <bool PF>
+// The backward's A-operand prefetch: off (2 waves per SIMD; whole step 9.12 -> 9.02 ms,
+// scripts/ab_step.py, r03) except in the residual and lattice variants, which spill without it.
 static int bwd_fused_occ() {
   // thread-safe one-time query (a function-local static initialised once)
   static const int occ = [] {
-    const void* fs[] = {reinterpret_cast<const void*>(&bwd_fused_kernel<false, true, true, PF>),
-                        reinterpret_cast<const void*>(&bwd_fused_kernel<false, false, true, PF>),
-                        reinterpret_cast<const void*>(&bwd_fused_kernel<false, false, false, PF>)};
+    const void* fs[] = {reinterpret_cast<const void*>(&bwd_fused_kernel<false, true, true, false>),
+                        reinterpret_cast<const void*>(&bwd_fused_kernel<false, false, true, false>),
+                        reinterpret_cast<const void*>(&bwd_fused_kernel<false, false, false, false>)};
     return min_occupancy(fs, 3);
   }();
   return occ;
 }
 
-int bwd_fused_blocks(int M) { return grid_blocks(M, bwd_pf() ? bwd_fused_occ<true>() : bwd_fused_occ<false>()); }
+int bwd_fused_blocks(int M) { return grid_blocks(M, bwd_fused_occ()); }
 // (the grid of a residual variant, which always prefetches, follows the same count: a block count
 // above its occupancy only adds a second partial round of blocks, never changes the results' order)
 }  // namespace pws
 
-// knob kKnobPwStream (DORKNET_PW_STREAM, default on; kind 3)
+// knob kKnobPwStream (default on; kind 3)
 bool pw_stream_enabled() { return knob(kKnobPwStream) == 1; }
 
 // Shapes the streaming dgrad takes (the rest go to the tiled engine).
@@ -921,12 +918,9 @@ bool pw_stream_dgrad_ok(int K, int C, int M) {
 
 int pw_stream_dgrad_rows(int M) { return pws::dgrad_blocks(M); }
 
-// K = C = 128 on the streaming forward (knob kKnobPwStream128, DORKNET_PW_STREAM128=0: the tiled engine)
-static bool pw_stream128() { return knob(kKnobPwStream128) == 1; }
-
 bool pw_stream_fwd_ok(int K, int C, int M, size_t xbytes) {
   if (!pw_stream_enabled()) return false;
-  const bool shape = (K == 64 && C == 64) || (K == 128 && C == 128 && pw_stream128());
+  const bool shape = (K == 64 && C == 64) || (K == 128 && C == 128);
   return shape && M > 0 && xbytes < ((size_t)1 << 31) && (size_t)M * K * 4 < ((size_t)1 << 31);
 }
 int pw_stream_fwd_rows(int M, int K) { return pws::fwd_blocks(M, K); }
@@ -963,11 +957,7 @@ int pw_stream_bwd_fused(const float* g, const float* bn_x, int M, const float* o
     return launch_status();
   }
   // (the residual variants keep the prefetch: without it they spill at 2 waves per SIMD)
-#define DK_BWD(R_, P_, B_)                                                                    \
-  if (R_ || pws::bwd_pf())                                                                    \
-    hipLaunchKernelGGL((pws::bwd_fused_kernel<R_, P_, B_, true>), grid, dim3(256), 0, st, a); \
-  else                                                                                        \
-    hipLaunchKernelGGL((pws::bwd_fused_kernel<R_, P_, B_, false>), grid, dim3(256), 0, st, a)
+#define DK_BWD(R_, P_, B_) hipLaunchKernelGGL((pws::bwd_fused_kernel<R_, P_, B_, R_>), grid, dim3(256), 0, st, a)
   if (pt) {
     if (r) {
       DK_BWD(true, true, true);

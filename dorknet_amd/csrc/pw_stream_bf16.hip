@@ -733,7 +733,7 @@ static int dgrad_occ() {
 
 }  // namespace pwsh
 
-// DORKNET_PW_STREAM_BF16=0 (or the fp32 switch DORKNET_PW_STREAM=0) keeps the tiled engine.
+// Knob 9 = 0 (or the fp32 streaming knob 3 = 0) keeps the tiled engine.
 // (knob kKnobPwsh, kind 9)
 static bool pwsh_enabled() { return knob(kKnobPwsh) == 1 && pw_stream_enabled(); }
 
@@ -837,7 +837,7 @@ static int pwsh_bwd_occ() {
   return occ;
 }
 bool pw_stream_bf16_bwd_ok(int K, int C, int M) {
-  return pwsh_enabled() && knob(kKnobPwsh16Bwd) >= 1 && K == 64 && C == 64 && M > 0 &&
+  return pwsh_enabled() && K == 64 && C == 64 && M > 0 &&
          (size_t)M * 64 * 2 < ((size_t)1 << 31);
 }
 int pw_stream_bf16_bwd_rows(int M) { return pwsh::grid_blocks(M, pwsh_bwd_occ()); }

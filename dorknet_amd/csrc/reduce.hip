@@ -256,6 +256,7 @@ struct PendingReduce {
 constexpr int kMaxPending = 64;
 thread_local int t_defer = 0;
 thread_local int t_npending = 0;
+thread_local int t_mark = 0;  // queue depth when recording was last turned on (dk_wgrad_reduce_defer(1))
 thread_local PendingReduce t_pending[kMaxPending];
 }  // namespace
 
@@ -272,11 +273,13 @@ int wgrad_reduce(const float* ws, int splits, int M, int N, float* out, const fl
 // host thread (dk_dwconv_bwd_bnbwd_f32 / _bf16 / _join_f32, dk_dwconv_bwd_s2_bnbwd_*,
 // dk_pwconv_bwd_bnbwd_f32 / _bf16) leave their weight-gradient partial slab unreduced and record
 // the reduce; mode 0: back to reducing in the entry point (recorded reduces stay for
-// dk_wgrad_reduce_flush); mode -1: as 0 and drop the recorded ones.
+// dk_wgrad_reduce_flush); mode -1: as 0 and drop the ones recorded since the last mode 1 (an entry
+// point that failed inside it), keeping those of the layers before.
 DK_API int dk_wgrad_reduce_defer(int mode) {
   if (mode < -1 || mode > 1) return dk::DK_ERR_ARGS;
+  if (mode == 1 && !dk::t_defer) dk::t_mark = dk::t_npending;
+  if (mode == -1 && dk::t_npending > dk::t_mark) dk::t_npending = dk::t_mark;
   dk::t_defer = mode == 1;
-  if (mode == -1) dk::t_npending = 0;
   return 0;
 }
 
@@ -285,41 +288,52 @@ DK_API int dk_wgrad_reduce_pending(void) { return dk::t_npending; }
 
 // Launch the recorded reduces on `stream`, in the order recorded (fixed order each, the same result
 // as in the entry point).  The slabs must stay untouched until they have run; DK_ERR_ARGS if none is
-// recorded.
+// recorded.  If a launch fails, the reduces not launched stay recorded (in order) and the error is
+// returned.
 DK_API int dk_wgrad_reduce_flush(void* stream) {
   using namespace dk;
   if (t_npending == 0) return DK_ERR_ARGS;
   const int n = t_npending;
-  t_npending = 0;
   const hipStream_t st = as_stream(stream);
   // float4-column slabs go into multi-task launches (same per-column order as splitk_reduce4_kernel),
   // the rest one launch each
   MultiTasks mt{};
   int blocks = 0;
+  bool launched[kMaxPending] = {};
+  int batch[kMultiMax];
   auto launch = [&]() -> int {
     if (mt.n == 0) return 0;
     hipLaunchKernelGGL(splitk_multi_kernel, dim3((unsigned)blocks), dim3(256), 0, st, mt);
+    const int rc = launch_status();
+    if (rc == 0)
+      for (int j = 0; j < mt.n; ++j) launched[batch[j]] = true;
     mt.n = 0;
     blocks = 0;
-    return launch_status();
+    return rc;
   };
-  for (int i = 0; i < n; ++i) {
+  int rc = 0;
+  for (int i = 0; i < n && rc == 0; ++i) {
     const PendingReduce& p = t_pending[i];
     const long long total = (long long)p.M * p.N;
-    if (knob(kKnobMultiReduce) == 1 && (total & 3) == 0 && (reinterpret_cast<uintptr_t>(p.ws) & 15) == 0 &&
+    if ((total & 3) == 0 && (reinterpret_cast<uintptr_t>(p.ws) & 15) == 0 &&
         total < (1ll << 31)) {
       const int tpo = multi_tpo(p.splits), cg = 256 / tpo;
       const int nb = (int)cdivll(total, 4ll * cg);
+      batch[mt.n] = i;
       mt.t[mt.n++] = MultiTask{p.ws, p.out, p.w, p.l2, p.splits, (int)total, tpo, blocks};
       blocks += nb;
-      if (mt.n == kMultiMax) {
-        const int rc = launch();
-        if (rc) return rc;
-      }
+      if (mt.n == kMultiMax) rc = launch();
     } else {
-      const int rc = splitk_reduce(p.ws, p.splits, p.M, p.N, p.out, p.w, p.l2, 0, p.N, p.N, 1, 1, st);
-      if (rc) return rc;
+      rc = splitk_reduce(p.ws, p.splits, p.M, p.N, p.out, p.w, p.l2, 0, p.N, p.N, 1, 1, st);
+      launched[i] = rc == 0;
     }
   }
-  return launch();
+  if (rc == 0) rc = launch();
+  // keep what did not launch
+  int k = 0;
+  for (int i = 0; i < n; ++i)
+    if (!launched[i]) t_pending[k++] = t_pending[i];
+  t_npending = k;
+  if (t_mark > k) t_mark = k;
+  return rc;
 }

@@ -144,8 +144,7 @@ class ReLu(Layer):
         when the join left none (a JoinOut whose consumer takes it as y > 0)."""
         y = self._join_y
         mask = torch.empty(y.shape, dtype=torch.uint8, device=y.device, memory_format=torch.channels_last)
-        tmp = self._empty_like(y)
-        lib.dk_relu_fwd_f32(y.data_ptr(), y.numel(), tmp.data_ptr(), mask.data_ptr(), stream_handle())
+        lib.dk_relu_fwd_f32(y.data_ptr(), y.numel(), 0, mask.data_ptr(), stream_handle())  # mask-only pass
         self._mask, self._join_y = mask, None
         return mask
 
@@ -163,8 +162,7 @@ class ReLu(Layer):
             y = as_device(self._fused_out)  # a BNOut is materialised here
             mask = torch.empty(y.shape, dtype=torch.uint8, device=y.device,
                                memory_format=torch.channels_last if y.dim() == 4 else torch.contiguous_format)
-            tmp = self._empty_like(y)
-            lib.dk_relu_fwd_f32(y.data_ptr(), y.numel(), tmp.data_ptr(), mask.data_ptr(), stream_handle())
+            lib.dk_relu_fwd_f32(y.data_ptr(), y.numel(), 0, mask.data_ptr(), stream_handle())  # mask-only pass
             out = self._empty_like(y)
             lib.dk_mask_to_f32(mask.data_ptr(), mask.numel(), out.data_ptr(), stream_handle())
             return out

@@ -409,7 +409,7 @@ class DepthwiseConvLayer(Layer):
         if bn is not None and R == S:
             if self.stride == 1:
                 rows = lib.dk_dwconv_dgrad_stats_rows(N, H, W, C, 1)
-            elif getenv("DORKNET_DW_STRIDED_BN", "1") != "0":  # (0: the BN runs its own backward)
+            else:
                 rows = lib.dk_dwconv_dgrad_join_rows(N, H, W, C, R, S, self.stride, self.padding)
         if rows and self.padding <= R - 1 and (residual is None or res is not None):
             # + stage 1 of the input BatchNorm's backward, in the dgrad epilogue (+ the residual)

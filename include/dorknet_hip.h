@@ -47,36 +47,27 @@ int dk_resize_bilinear_u8(const uint8_t* src, int N, int H, int W, int C, int OH
 int dk_u8_nhwc_to_nchw_f32(const uint8_t* src, int N, int H, int W, int C, const int* crop_rc, int OH, int OW, float shift, float* dst, void* stream);
 int dk_mixup_f32(const float* a, const float* b, long long n, float p, float one_minus_p, float* ab, float* ba, void* stream);
 
-/* Tuning knobs for A/B runs (dorknet_amd/csrc/knobs.hip: one registry of atomics whose defaults
- * come from the DORKNET_* environment, read once; not for production use).  cfg = -1 restores the
- * default.  Returns the number of configurations for kinds 0 / 1, 0 for the others, -1 for an
- * unknown kind.
+/* Path selectors and tuning knobs for tests and A/B runs (dorknet_amd/csrc/knobs.hip: one registry
+ * of atomics holding built-in defaults; no environment variable reaches them; not for production
+ * use).  cfg = -1 restores the default.  Returns the number of configurations for kinds 0 / 1, 0 for
+ * the others, -1 for an unknown or retired kind (5, 15-17, 20, 22).
  * kind 0 / 1: force GEMM tile configuration `cfg` for forward/dgrad problems / split-K
  * weight-gradient problems (-1 = the built-in heuristic);
  * kind 2: split-K grids sized to one round of resident blocks (1 = default) or the fixed ~1024-block
  * split (0);
- * kind 3: the streaming pointwise kernels for K = C = 64 (1 = default; 0 = the tiled engine for every
- * shape, as DORKNET_PW_STREAM=0);
- * kind 4: nontemporal output stores, a bitmask over kernel families (NtFam in csrc/dk_common.h;
- * DORKNET_NT_STORES);
- * kind 5: the streaming fused pointwise backward's operand prefetch (DORKNET_PWS_BWD_PF);
+ * kind 3: the streaming pointwise kernels for K = C = 64 / 128 (1 = default; 0 = the tiled engine for
+ * every shape);
+ * kind 4: nontemporal output stores, a bitmask over kernel families (NtFam in csrc/dk_common.h);
  * kind 7: blocks the fused stride-1 depthwise backward aims for (its batch is dealt into image runs
- * above that; 0 = one image per block; default 768, DORKNET_DWB_BLOCKS);
+ * above that; 0 = one image per block; default 768);
  * kind 8: output rows per thread of the depthwise forward / stride-1 dgrad (-1 = the shape rule);
  * kind 9: the bf16 streaming pointwise kernels (1 = default; 0 = the tiled engine);
- * kind 11: the fp32 weight-stationary deep pointwise kernels (DORKNET_PW_DEEP);
- * kind 13: the bf16 weight-stationary deep pointwise kernels (DORKNET_PW_DEEP_BF16);
- * kind 14: the fused deep pointwise backward, dgrad + weight gradient in one pass (DORKNET_PW_DEEP_BWD);
- * kind 15: the streaming forward at K = C = 128 (DORKNET_PW_STREAM128);
- * kind 16 / 17: the tiled fused pointwise backward's prefetch (-1 = per shape) and resident blocks per
- * CU (0 = occupancy) (DORKNET_PWF_PREFETCH / DORKNET_PWF_BLOCKS_PER_CU);
- * kind 18: blocks a split-K weight gradient aims for (DORKNET_WGRAD_BLOCKS, default 1024);
- * kind 20: the fused bf16 pointwise backward (DORKNET_PW_BF16_BWD: 1 = K = C = 64 and K in {128, 256},
- * 2 = K = C = 64 only, 0 = off);
- * kind 21: output columns per thread of the fused stride-1 depthwise backward (DORKNET_DWB_COLS: 2 =
- * default where the width allows, 1 = one); the dk_dwconv_bwd_bnbwd*_stats_rows / _workspace_bytes follow it;
- * kind 22: dk_wgrad_reduce_flush launches its reduces as one multi-task kernel (DORKNET_MULTI_REDUCE: 1 =
- * default, 0 = one launch each; bit-identical either way). */
+ * kind 11: the fp32 weight-stationary deep pointwise kernels (1 = default);
+ * kind 13: the bf16 weight-stationary deep pointwise kernels (1 = default);
+ * kind 14: the fused deep pointwise backward, dgrad + weight gradient in one pass (1 = default);
+ * kind 18: blocks a split-K weight gradient aims for (default 1024);
+ * kind 21: output columns per thread of the fused stride-1 depthwise backward (2 = default where the
+ * width allows, 1 = one); the dk_dwconv_bwd_bnbwd*_stats_rows / _workspace_bytes follow it. */
 int dk_debug_set_gemm_config(int kind, int cfg);
 
 /* Bandwidth ceiling probe (not on the training path; scripts/stream_ceiling.py): reads nin
@@ -227,7 +218,9 @@ int dk_pwconv_dgrad_bnbwd_f32(const float* g, const float* bn_x, int N, int OH, 
  * (+ residual), the weight gradient dw_kc = dy^T . bn_in(x) + l2 * w_kc (fixed-order reduce of
  * per-block partials in ws) and, when part != NULL, the input BN's backward partials
  * part[rows][2][C], rows = dk_pwconv_bwd_fused_rows().  dy itself is never stored.
- * K, C in {64, 128} (dk_pwconv_bwd_fused_rows() returns 0 for other shapes); fp32 NHWC. */
+ * K, C in {64, 128}, or K in {128, 256} with C a multiple of 128 (the weight-stationary deep kernel;
+ * dk_pwconv_bwd_fused_rows() returns 0 for other shapes); fp32 NHWC.  At the deep kernel's shapes an
+ * input BN (bn_*) must come with its partials (part), else DK_ERR_ARGS. */
 int dk_pwconv_bwd_fused_rows(int N, int OH, int OW, int K, int C);
 /* 1 when the fused backward is the faster path for the shape (K = C = 64: the streaming kernel;
  * the layers then take it by default), else 0. */
@@ -434,6 +427,7 @@ int dk_bn_bwd_f32(const float* x, const float* dy, int P, int C, const float* me
  *   add (+ReLU): ResidualBlock.forward/backward joins (layers/residual_block.py:75, :94-97).
  *   GAP: layers/pooling.py:23-36.   softmax + CE: layers/losses.py:13-34.
  * ------------------------------------------------------------------------------------- */
+/* dk_relu_fwd_*: y = max(x, 0) and mask = (x > 0) as uint8; either output may be NULL (a mask-only pass). */
 int dk_relu_fwd_f32(const float* x, long long n, float* y, uint8_t* mask, void* stream);
 int dk_relu_bwd_f32(const float* dy, const uint8_t* mask, long long n, float* dx, void* stream);
 int dk_mask_to_f32(const uint8_t* mask, long long n, float* out, void* stream);

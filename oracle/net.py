@@ -138,10 +138,23 @@ class OBatchNorm(OLayer):
 
 
 class OReLU(OLayer):
+    """activations.py:37-47.  `replay`: a bool mask that decides the next training forward instead
+    of out > 0 (the tests hand in the GPU's own decisions, so that an fp32 tie -- an input within
+    rounding of zero -- takes the same side in both; tests/_ties.py).  The pre-activation of that
+    forward is kept in `pre` for the tie analysis."""
+    replay = None
+
     def forward(self, X, test_mode=False):
+        if self.replay is not None and not test_mode:
+            m = np.asarray(self.replay, dtype=bool)
+            if m.shape != X.shape:
+                raise ValueError("replayed mask shape {} != input {}".format(m.shape, X.shape))
+            self.replay, self.pre = None, X
+            self.mask = m.astype(X.dtype)
+            return X * self.mask
         Y, mask = ref.relu_forward(X)
         if not test_mode:
-            self.mask = mask
+            self.mask, self.pre = mask, X
         return Y
 
     def backward(self, dY):

@@ -111,17 +111,18 @@ def test_wgrad_reduce_defer_protocol():
 
 @pytest.mark.parametrize("every", ["1", "4", "64"])
 def test_wgrad_reduce_batched_flush_bitwise(monkeypatch, every):
-    """Recorded reduces launched in batches (DORKNET_WGRAD_FLUSH_EVERY: one cross-stream wait per
+    """Recorded reduces launched in batches (dorknet_amd._hip.FLUSH_EVERY: one cross-stream wait per
     batch) give the same gradients bit for bit as one flush per layer."""
+    from dorknet_amd import _hip
     from examples.resnet18_depsep import ResNet18, synthetic_batch
     from dorknet_amd._hip import lib
     X, _, onehot = synthetic_batch(8, seed=15)
     np.random.seed(16)
     net = ResNet18("r18")
     net.to_gpu()
-    monkeypatch.setenv("DORKNET_WGRAD_FLUSH_EVERY", "1")
+    monkeypatch.setattr(_hip, "FLUSH_EVERY", 1)
     ref = _step(net, X, onehot)
-    monkeypatch.setenv("DORKNET_WGRAD_FLUSH_EVERY", every)
+    monkeypatch.setattr(_hip, "FLUSH_EVERY", min(60, int(every)))
     got = _step(net, X, onehot)
     torch.cuda.synchronize()
     assert lib.dk_wgrad_reduce_pending() == 0

@@ -252,17 +252,6 @@ def test_stats_fold_arming_marks_records_stale(monkeypatch):
         out.bn_args()
 
 
-def test_wgrad_flush_batch_setting(monkeypatch):
-    """DORKNET_WGRAD_FLUSH_EVERY: recorded weight-gradient reduces per cross-stream flush, clamped to
-    [1, 60] (the C queue holds 64), 60 (= at the end of the backward) by default or when unparsable."""
-    from dorknet_amd._hip import _flush_every
-    monkeypatch.delenv("DORKNET_WGRAD_FLUSH_EVERY", raising=False)
-    assert _flush_every() == 60
-    for v, want in (("1", 1), ("0", 1), ("8", 8), ("500", 60), ("x", 60)):
-        monkeypatch.setenv("DORKNET_WGRAD_FLUSH_EVERY", v)
-        assert _flush_every() == want
-
-
 def test_wgrad_flush_last_setting(monkeypatch):
     """DORKNET_WGRAD_FLUSH_LAST: the network's backward flushes the recorded reduces before each of
     its last this-many steps; 1 by default or when unparsable, never negative."""

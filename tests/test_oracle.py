@@ -160,6 +160,27 @@ def test_softmax_xent_relu_gap_vs_torch():
     assert rel(ref.gap_backward(dG, (4, 5)), at.grad.numpy()) < TOL
 
 
+def test_relu_decision_replay():
+    """OReLU.replay (tests/_ties.py): the replayed mask decides one training forward and its
+    backward; the next forward decides on out > 0 again; test mode ignores it."""
+    from oracle.net import OReLU
+    rng = np.random.default_rng(6)
+    A = rng.standard_normal((2, 3, 4, 5))
+    m = A > 0
+    m[0, 1, 2, 3] = not m[0, 1, 2, 3]           # one flipped decision, as at a tie
+    r = OReLU("r")
+    r.replay = m
+    assert np.array_equal(r.forward(A, test_mode=True), np.maximum(A, 0)) and r.replay is not None
+    y = r.forward(A)
+    assert np.array_equal(y, A * m) and r.replay is None and r.pre is A
+    dY = rng.standard_normal(A.shape)
+    assert np.array_equal(r.backward(dY), dY * m)
+    assert np.array_equal(r.forward(A), np.maximum(A, 0))
+    r.replay = m[:1]
+    with pytest.raises(ValueError):
+        r.forward(A)
+
+
 # ------------------------------- known-answer tests -------------------------------------
 
 def test_kat_identity_and_delta_filters():
