@@ -870,6 +870,360 @@ __global__ __launch_bounds__(NT, bwd_wps<KR>()) void bwd_kernel(BwdArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------
+// The C = 512 forward at two waves per SIMD (round 6): fwd_kernel's work with dgrad16_kernel's layout
+// (8 waves of 16 output columns, 16-pixel tiles, the k-permuted LDS tile of the BN-on-load input,
+// v_mfma_f32_16x16x4_f32 in the same k order: y bit-identical to fwd_kernel and the tiled engine).
+// The BatchNorm's per-channel terms sit in an LDS table; the output statistics reduce the four
+// k-group lanes of a column, then the block's columns, into one partial row as before.
+// ---------------------------------------------------------------------------------------
+template <int KR, bool BN, bool STATS, bool STRIDED, bool HB>
+__global__ __launch_bounds__(NT16, 1) void fwd16_kernel(FwdArgs a) {
+  using L = K16<KR>;
+  constexpr int SK = L::SK, RS = L::RS, KV = L::KV, LV = L::LV, NQ = L::NQ;
+  static_assert(KR % 64 == 0 && (SK / 4) % 2 == 1 && NT16 % KV == 0 && LV >= 1, "pwd::fwd16_kernel shape");
+  __shared__ __attribute__((aligned(16))) float As[2][TR16 * SK];
+  __shared__ __attribute__((aligned(16))) f32x4 bnt[4][BN ? KV : 1];
+  static_assert(sizeof(double) * 2 * NT16 <= sizeof(float) * 2 * TR16 * SK, "fold scratch fits in the tiles");
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int c16 = lane & 15, kg = lane >> 4;
+  const int n0 = blockIdx.y * NB, N = a.N;
+  const int col = n0 + 16 * wave + c16;
+  const float bias = HB ? a.bias[col] : 0.f;
+  const bool irelu = a.irelu != 0;
+  const int kv = tid % KV, r0 = tid / KV;
+  if constexpr (BN) {
+    if (tid < KV) {
+      bnt[0][tid] = ld4(a.im + 4 * tid);
+      bnt[1][tid] = ld4(a.iis + 4 * tid);
+      bnt[2][tid] = ld4(a.ig + 4 * tid);
+      bnt[3][tid] = ld4(a.ib + 4 * tid);
+    }
+  }
+  const __amdgpu_buffer_rsrc_t rx = make_rsrc_v(a.x, a.xbytes);
+  const int ntiles = (a.M + TR16 - 1) / TR16, G = gridDim.x;
+  uint32_t lofs[LV];
+#pragma unroll
+  for (int j = 0; j < LV; ++j) lofs[j] = off4(r0 + j * (NT16 / KV), KR, 4 * kv);
+  const uint32_t cbase = off4(4 * kg, N, col);
+  const int sreg = (kv & 1) * RS + (kv & ~1);
+
+  auto tile_rsrc16 = [&](const float* p, int ld, int tile, int nrows) {
+    const int rows = nrows - tile * TR16;
+    return make_rsrc_v(p + (size_t)tile * TR16 * ld, rows > 0 ? (uint32_t)rows * ld * 4u : 0u);
+  };
+  auto load_tile = [&](int tile, f32x4* st) {
+    const __amdgpu_buffer_rsrc_t rt = tile_rsrc16(a.x, KR, tile, a.M);
+#pragma unroll
+    for (int j = 0; j < LV; ++j) {
+      if constexpr (STRIDED) {
+        const int m = tile * TR16 + r0 + j * (NT16 / KV);
+        const int ow = m % a.OW, q = m / a.OW, oh = q % a.OH, n = q / a.OH;
+        const int row = (n * a.H + oh * a.sa) * a.W + ow * a.sa;
+        st[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rx, (int)off4(row, KR, 4 * kv), 0, 0));
+      } else {
+        st[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rt, (int)lofs[j], 0, 0));
+      }
+    }
+  };
+  auto stage = [&](float* dst, const f32x4* st) {
+    f32x4 mu, is, ga, be;
+    if constexpr (BN) {
+      mu = bnt[0][kv];
+      is = bnt[1][kv];
+      ga = bnt[2][kv];
+      be = bnt[3][kv];
+    }
+#pragma unroll
+    for (int j = 0; j < LV; ++j) {
+      f32x4 v = st[j];
+      if constexpr (BN) {
+        v = affine4(xhat4(v, mu, is), ga, be);
+        if (irelu) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = __builtin_fmaxf(v[e], 0.f);
+        }
+      }
+      float* d = dst + (r0 + j * (NT16 / KV)) * SK + sreg;
+      *reinterpret_cast<f32x2*>(d) = f32x2{v[0], v[2]};
+      *reinterpret_cast<f32x2*>(d + 2 * RS) = f32x2{v[1], v[3]};
+    }
+  };
+
+  if constexpr (BN) __syncthreads();  // the BN table
+  int t = first_tile(ntiles);
+  f32x4 bw[NQ];
+  {
+    f32x4 st[LV];
+    load_tile(t, st);
+    // B fragments W[col][k(i, kg)], i = 4q + u, after the first tile's loads
+#pragma unroll
+    for (int q = 0; q < NQ; ++q)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int i = 4 * q + u;
+        bw[q][u] = a.w[(size_t)col * KR + 8 * (i >> 1) + 2 * (i & 1) + (kg >> 1) + 4 * (kg & 1)];
+      }
+    stage(&As[0][0], st);
+  }
+  __syncthreads();
+  double ps = 0.0, pq = 0.0;
+  int buf = 0;
+  for (; t < ntiles; t += G) {
+    f32x4 nst[LV];
+    load_tile(t + G, nst);
+    f32x4 acc;
+    mfma16_tile<NQ>(&As[buf][0] + c16 * SK + kg * RS, bw, acc);
+    const int mb = t * TR16 + 4 * kg;
+    const __amdgpu_buffer_rsrc_t ry = tile_rsrc16(a.y, N, t, a.M);
+    if constexpr (HB) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[r] += bias;
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float v = acc[r];
+      bstore_nt(__builtin_bit_cast(uint32_t, v), ry, (int)cbase, r * N * 4, a.nt);
+    }
+    if constexpr (STATS) {
+      const bool full = t * TR16 + TR16 <= a.M;  // a whole tile (uniform): no row masks
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const double d = (full || mb + r < a.M) ? (double)acc[r] : 0.0;
+        ps += d;
+        pq += d * d;
+      }
+    }
+    stage(&As[buf ^ 1][0], nst);
+    __syncthreads();
+    buf ^= 1;
+  }
+  if constexpr (STATS) {
+    double(*const red)[NB] = reinterpret_cast<double(*)[NB]>(&As[0][0]);  // [2][NB]
+    ps += __shfl_xor(ps, 16, 64);
+    pq += __shfl_xor(pq, 16, 64);
+    ps += __shfl_xor(ps, 32, 64);
+    pq += __shfl_xor(pq, 32, 64);
+    __syncthreads();  // the pixel tiles become scratch
+    if (kg == 0) {
+      red[0][16 * wave + c16] = ps;
+      red[1][16 * wave + c16] = pq;
+    }
+    __syncthreads();
+    for (int i = tid; i < 2 * NB; i += NT16) {
+      const int which = i / NB, c = i - which * NB;
+      pub_store(a.part + ((size_t)blockIdx.x * 2 + which) * N + n0 + c, red[which][c]);
+    }
+    if (a.ft.part) {
+      __syncthreads();
+      fold_tail<NT16>(a.ft, blockIdx.x, n0, NB, blockIdx.y, reinterpret_cast<double2*>(&As[0][0]));
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// The fused backward on v_mfma_f32_16x16x4_f32 (round 6): bwd_kernel's dgrad + weight gradient with
+// dgrad16_kernel's layout -- 8 waves of 16 columns, 16-pixel tiles, the k-permuted LDS dy tile -- so
+// that at K = 256 a wave holds 64 VGPRs of B fragments and 64 of weight-gradient accumulators and two
+// waves share each SIMD (bwd_kernel<256>: one).  Per tile a wave
+//   1. runs the dgrad MFMAs of its 16 columns (dx bit-identical to dgrad16_kernel / dgrad_kernel);
+//   2. stores dx and reduces the input BN's partials from its C-layout x loads;
+//   3. forms bn_relu(x) for its four C-layout pixels 4 kg + r -- exactly the A operand of
+//      v_mfma_f32_16x16x4_f32 with rows = its 16 columns and the 4-deep reduction = pixels
+//      (4 kg' + r for k-group kg') -- and accumulates dW^T[col][k] over the tile with B = dy read from
+//      the LDS tile (lane (c16, kg) reads dy[pixel 4 kg + r][k = 16 kt + c16], one ds_read_b32 per
+//      MFMA, conflict-free: the 16 k of a chunk fall on 16 distinct banks of the permuted row).
+// Lane (c16, kg) ends with dW[16 kt + c16][col0 + 4 kg + 0..3] (col0 = the wave's first column), written
+// as one 16-byte store per chunk into the partial row wpart[blockIdx.x][KR][N] (bwd_kernel's layout:
+// the same fixed-order reduce follows).
+// ---------------------------------------------------------------------------------------
+template <int KR, bool RES, bool BNIN>
+__global__ __launch_bounds__(NT16, 1) void bwd16_kernel(BwdArgs a) {
+  using L = K16<KR>;
+  constexpr int SK = L::SK, RS = L::RS, KV = L::KV, LV = L::LV, NQ = L::NQ, NKT = KR / 16;
+  static_assert(KR % 64 == 0 && (SK / 4) % 2 == 1 && NT16 % KV == 0 && LV >= 1, "pwd::bwd16_kernel shape");
+  __shared__ __attribute__((aligned(16))) float As[2][TR16 * SK];
+  __shared__ __attribute__((aligned(16))) f32x4 bnt[7][KV];
+  static_assert(sizeof(double) * 2 * NT16 <= sizeof(float) * 2 * TR16 * SK, "fold scratch fits in the tiles");
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int c16 = lane & 15, kg = lane >> 4;
+  const int n0 = blockIdx.y * NB, N = a.N;
+  const int col = n0 + 16 * wave + c16;
+  const int kv = tid % KV, r0 = tid / KV;
+  if (tid < KV) {
+    const f32x4 ga = ld4(a.og + 4 * tid), is = ld4(a.ois + 4 * tid);
+    bnt[0][tid] = ld4(a.om + 4 * tid);
+    bnt[1][tid] = is;
+    bnt[2][tid] = ga;
+    bnt[3][tid] = ld4(a.ob + 4 * tid);
+    bnt[4][tid] = ld4(a.k12 + 4 * tid);
+    bnt[5][tid] = ld4(a.k12 + KR + 4 * tid);
+    f32x4 f;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) f[e] = ga[e] * is[e];
+    bnt[6][tid] = f;
+  }
+  const float pm = BNIN ? a.im[col] : 0.f, pis = BNIN ? a.iis[col] : 0.f, pga = BNIN ? a.ig[col] : 0.f,
+              pbe = BNIN ? a.ib[col] : 0.f;
+  const bool orelu = a.orelu != 0, irelu = a.irelu != 0;
+  const int ntiles = (a.M + TR16 - 1) / TR16, G = gridDim.x;
+  uint32_t lofs[LV];
+#pragma unroll
+  for (int j = 0; j < LV; ++j) lofs[j] = off4(r0 + j * (NT16 / KV), KR, 4 * kv);
+  const uint32_t cbase = off4(4 * kg, N, col);
+  const int sreg = (kv & 1) * RS + (kv & ~1);
+  // the weight gradient's B operand: k = 16 kt + c16 sits in region ((r8 & 1) << 1) | ((r8 >> 2) & 1) at
+  // position 4 kt + 2 (c16 >> 3) + ((r8 >> 1) & 1) of a pixel row (r8 = c16 & 7)
+  const int r8 = c16 & 7;
+  const int doff = ((((r8 & 1) << 1) | ((r8 >> 2) & 1)) * RS) + 2 * (c16 >> 3) + ((r8 >> 1) & 1);
+
+  auto tile_rsrc16 = [&](const float* p, int ld, int tile, int nrows) {
+    const int rows = nrows - tile * TR16;
+    return make_rsrc_v(p + (size_t)tile * TR16 * ld, rows > 0 ? (uint32_t)rows * ld * 4u : 0u);
+  };
+  auto load_tile = [&](int tile, f32x4* sg, f32x4* sx) {
+    const __amdgpu_buffer_rsrc_t rg = tile_rsrc16(a.g, KR, tile, a.M), rx = tile_rsrc16(a.xo, KR, tile, a.M);
+#pragma unroll
+    for (int j = 0; j < LV; ++j) {
+      sg[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rg, (int)lofs[j], 0, 0));
+      sx[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rx, (int)lofs[j], 0, 0));
+    }
+  };
+  auto stage = [&](float* dst, const f32x4* sg, const f32x4* sx) {
+    const f32x4 mu = bnt[0][kv], is = bnt[1][kv], ga = bnt[2][kv], be = bnt[3][kv], k1 = bnt[4][kv], k2 = bnt[5][kv],
+                f = bnt[6][kv];
+#pragma unroll
+    for (int j = 0; j < LV; ++j) {
+      const int r = r0 + j * (NT16 / KV);
+      f32x4 v;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float xe = sx[j][e];
+        float ge = sg[j][e];
+        const bool kill = (!(bn_out(xe, mu[e], is[e], ga[e], be[e]) > 0.f)) & orelu;
+        ge = kill ? 0.f : ge;
+        v[e] = bn_bwd_elem(xe, ge, mu[e], is[e], f[e], k1[e], k2[e]);
+      }
+      float* d = dst + r * SK + sreg;
+      *reinterpret_cast<f32x2*>(d) = f32x2{v[0], v[2]};
+      *reinterpret_cast<f32x2*>(d + 2 * RS) = f32x2{v[1], v[3]};
+    }
+  };
+
+  __syncthreads();  // the BN table
+  int t = first_tile(ntiles);
+  f32x4 bw[NQ];
+  {
+    f32x4 sg[LV], sx[LV];
+    load_tile(t, sg, sx);
+#pragma unroll
+    for (int q = 0; q < NQ; ++q)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int i = 4 * q + u;
+        const int k = 8 * (i >> 1) + 2 * (i & 1) + (kg >> 1) + 4 * (kg & 1);
+        bw[q][u] = a.w[(size_t)k * N + col];
+      }
+    stage(&As[0][0], sg, sx);
+  }
+  __syncthreads();
+  f32x4 dw[NKT];
+#pragma unroll
+  for (int i = 0; i < NKT; ++i) dw[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  double ps = 0.0, pq = 0.0;
+  int buf = 0;
+  for (; t < ntiles; t += G) {
+    f32x4 ng[LV], nx[LV];
+    load_tile(t + G, ng, nx);
+    const int mb = t * TR16 + 4 * kg;
+    const __amdgpu_buffer_rsrc_t rxi = tile_rsrc16(a.xi, N, t, a.M);
+    const __amdgpu_buffer_rsrc_t rr = tile_rsrc16(RES ? a.res : a.xi, N, t, RES ? a.M : 0);
+    const __amdgpu_buffer_rsrc_t rdx = tile_rsrc16(a.dx, N, t, a.M);
+    float ex[4], ers[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      ex[r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rxi, (int)cbase, r * N * 4, 0));
+      if constexpr (RES)
+        ers[r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rr, (int)cbase, r * N * 4, 0));
+    }
+    const float* tile = &As[buf][0];
+    f32x4 acc;
+    mfma16_tile<NQ>(tile + c16 * SK + kg * RS, bw, acc);
+    if constexpr (RES) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[r] += ers[r];
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float v = acc[r];
+      bstore_nt(__builtin_bit_cast(uint32_t, v), rdx, (int)cbase, r * N * 4, a.nt);
+    }
+    // the input BN's partials of dx, and the weight gradient's operand bn_relu(x)
+    const bool full = t * TR16 + TR16 <= a.M;  // a whole tile (uniform): no row masks
+    float yb[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const bool out = !full && mb + r >= a.M;
+      const float x = ex[r];
+      if constexpr (BNIN) {
+        const float xh = (x - pm) * pis;
+        const float v = __builtin_fmaf(pga, xh, pbe);  // bn_out
+        const bool dead = !(v > 0.f) & irelu;
+        const float gv = (dead | out) ? 0.f : acc[r];
+        ps += (double)gv;
+        pq += (double)gv * (double)xh;
+        yb[r] = (dead | out) ? 0.f : v;
+      } else {
+        yb[r] = out ? 0.f : x;
+      }
+    }
+    // dW^T[col][k] += bn_relu(x)^T . dy over the tile's 16 pixels (rows past M are zero in yb)
+    {
+      const float* bp = tile + (4 * kg) * SK + doff;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float bv[NKT];
+#pragma unroll
+        for (int kt = 0; kt < NKT; ++kt) bv[kt] = bp[r * SK + 4 * kt];
+#pragma unroll
+        for (int kt = 0; kt < NKT; ++kt) dw[kt] = __builtin_amdgcn_mfma_f32_16x16x4f32(yb[r], bv[kt], dw[kt], 0, 0, 0);
+      }
+    }
+    stage(&As[buf ^ 1][0], ng, nx);
+    __syncthreads();
+    buf ^= 1;
+  }
+  // the weight-gradient partial row: lane (c16, kg) holds dW[16 kt + c16][col0 + 4 kg + 0..3]
+  {
+    float* wp = a.wpart + (size_t)blockIdx.x * KR * N + n0 + 16 * wave + 4 * kg;
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt) st4(wp + (size_t)(16 * kt + c16) * N, dw[kt]);
+  }
+  if constexpr (BNIN) {
+    double(*const red)[NB] = reinterpret_cast<double(*)[NB]>(&As[0][0]);  // [2][NB]
+    ps += __shfl_xor(ps, 16, 64);
+    pq += __shfl_xor(pq, 16, 64);
+    ps += __shfl_xor(ps, 32, 64);
+    pq += __shfl_xor(pq, 32, 64);
+    __syncthreads();  // the pixel tiles become scratch
+    if (kg == 0) {
+      red[0][16 * wave + c16] = ps;
+      red[1][16 * wave + c16] = pq;
+    }
+    __syncthreads();
+    for (int i = tid; i < 2 * NB; i += NT16) {
+      const int which = i / NB, c = i - which * NB;
+      pub_store(a.part + ((size_t)blockIdx.x * 2 + which) * N + n0 + c, red[which][c]);
+    }
+    if (a.ft.part) {
+      __syncthreads();
+      fold_tail<NT16>(a.ft, blockIdx.x, n0, NB, blockIdx.y, reinterpret_cast<double2*>(&As[0][0]));
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------
 // Host side: the instantiated reductions and the grid.
 // ---------------------------------------------------------------------------------------
 #define DK_PWD_KR(X) X(64) X(128) X(256) X(512)
@@ -911,12 +1265,42 @@ static int dgrad_occ() {
 }
 
 template <int KR>
+static int fwd16_occ() {
+  static const int occ = [] {
+#define DK_F(B_, S_, T_) reinterpret_cast<const void*>(&fwd16_kernel<KR, B_, S_, T_, false>), \
+                         reinterpret_cast<const void*>(&fwd16_kernel<KR, B_, S_, T_, true>)
+    const void* fs[] = {DK_F(true, true, false), DK_F(true, false, false), DK_F(false, true, false),
+                        DK_F(false, false, false), DK_F(true, true, true), DK_F(true, false, true),
+                        DK_F(false, true, true), DK_F(false, false, true)};
+#undef DK_F
+    int o = 1 << 20;
+    for (const void* f : fs) o = std::min(o, occupancy(f, NT16));
+    return o;
+  }();
+  return occ;
+}
+
+template <int KR>
 static int dgrad16_occ() {
   static const int occ = [] {
     const void* fs[] = {reinterpret_cast<const void*>(&dgrad16_kernel<KR, true, true>),
                         reinterpret_cast<const void*>(&dgrad16_kernel<KR, true, false>),
                         reinterpret_cast<const void*>(&dgrad16_kernel<KR, false, true>),
                         reinterpret_cast<const void*>(&dgrad16_kernel<KR, false, false>)};
+    int o = 1 << 20;
+    for (const void* f : fs) o = std::min(o, occupancy(f, NT16));
+    return o;
+  }();
+  return occ;
+}
+
+template <int KR>
+static int bwd16_occ() {
+  static const int occ = [] {
+    const void* fs[] = {reinterpret_cast<const void*>(&bwd16_kernel<KR, true, true>),
+                        reinterpret_cast<const void*>(&bwd16_kernel<KR, true, false>),
+                        reinterpret_cast<const void*>(&bwd16_kernel<KR, false, true>),
+                        reinterpret_cast<const void*>(&bwd16_kernel<KR, false, false>)};
     int o = 1 << 20;
     for (const void* f : fs) o = std::min(o, occupancy(f, NT16));
     return o;
@@ -973,10 +1357,14 @@ bool pw_deep_dgrad_ok(int K, int C, int M) {
   return (size_t)M * (K > C ? K : C) * 4 < ((size_t)1 << 31);
 }
 
+// C = 512 runs the two-waves-per-SIMD 16 x 16 kernel (fwd16_kernel), 16-pixel tiles.
+static bool pwd_fwd16(int C) { return C == 512; }
+
 int pw_deep_fwd_rows(int M, int K, int C) {
+  if (pwd_fwd16(C)) return pwd::grid_x(M, K, pwd::fwd16_occ<512>(), pwd::TR16);
 #define DK_ROWS(kr) \
   if (C == kr) return pwd::grid_x(M, K, pwd::fwd_occ<kr>());
-  DK_PWD_KR(DK_ROWS)
+  DK_PWD_KR_DGRAD(DK_ROWS)
 #undef DK_ROWS
   return 0;
 }
@@ -1005,12 +1393,18 @@ int pw_deep_fwd(const float* x, int N, int H, int W, int stride, int OH, int OW,
   a.nt = nt_stores(kNtPwd);
   const dim3 grid(pw_deep_fwd_rows(M, K, C), K / pwd::NB);
   if (grid.x == 0) return DK_ERR_ARGS;
-#define DK_L(kr, B_, S_, T_)                                                                          \
-  do {                                                                                                \
-    if (bias)                                                                                         \
-      hipLaunchKernelGGL((pwd::fwd_kernel<kr, B_, S_, T_, true>), grid, dim3(pwd::NT), 0, st, a);     \
-    else                                                                                              \
-      hipLaunchKernelGGL((pwd::fwd_kernel<kr, B_, S_, T_, false>), grid, dim3(pwd::NT), 0, st, a);    \
+  // (C = 512: fwd16_kernel, pwd_fwd16)
+#define DK_L(kr, B_, S_, T_)                                                                           \
+  do {                                                                                                 \
+    if constexpr (kr == 512) {                                                                         \
+      if (bias)                                                                                        \
+        hipLaunchKernelGGL((pwd::fwd16_kernel<kr, B_, S_, T_, true>), grid, dim3(pwd::NT16), 0, st, a);  \
+      else                                                                                             \
+        hipLaunchKernelGGL((pwd::fwd16_kernel<kr, B_, S_, T_, false>), grid, dim3(pwd::NT16), 0, st, a); \
+    } else if (bias)                                                                                   \
+      hipLaunchKernelGGL((pwd::fwd_kernel<kr, B_, S_, T_, true>), grid, dim3(pwd::NT), 0, st, a);      \
+    else                                                                                               \
+      hipLaunchKernelGGL((pwd::fwd_kernel<kr, B_, S_, T_, false>), grid, dim3(pwd::NT), 0, st, a);     \
   } while (0)
 #define DK_FWD(kr)                    \
   if (C == kr) {                      \
@@ -1088,9 +1482,12 @@ bool pw_deep_bwd_ok(int K, int C, int M) {
   if (!pwd_bwd_enabled() || M <= 0 || (K != 128 && K != 256) || C % pwd::NB) return false;
   return (size_t)M * (K > C ? K : C) * 4 < ((size_t)1 << 31);
 }
+// K = 256 runs the two-waves-per-SIMD 16 x 16 kernel (bwd16_kernel), 16-pixel tiles.
+static bool pwd_bwd16(int K) { return K == 256; }
+
 int pw_deep_bwd_rows(int M, int K, int C) {
   if (K == 128) return pwd::grid_x(M, C, pwd::bwd_occ<128>());
-  if (K == 256) return pwd::grid_x(M, C, pwd::bwd_occ<256>());
+  if (pwd_bwd16(K)) return pwd::grid_x(M, C, pwd::bwd16_occ<256>(), pwd::TR16);
   return 0;
 }
 int pw_deep_bwd_slices(int M, int K, int C) { return C / pwd::NB; }
@@ -1105,6 +1502,19 @@ int pw_deep_bwd_bnbwd(const float* g, const float* bn_x, int M, int K, int C, co
   a.nt = nt_stores(kNtPwd);
   const dim3 grid(pw_deep_bwd_rows(M, K, C), C / pwd::NB);
   if (grid.x == 0) return DK_ERR_ARGS;
+  if (pwd_bwd16(K)) {
+#define DK_L16(R_, B_) hipLaunchKernelGGL((pwd::bwd16_kernel<256, R_, B_>), grid, dim3(pwd::NT16), 0, st, a)
+    if (res && im)
+      DK_L16(true, true);
+    else if (res)
+      DK_L16(true, false);
+    else if (im)
+      DK_L16(false, true);
+    else
+      DK_L16(false, false);
+#undef DK_L16
+    return launch_status();
+  }
 #define DK_L(kr, R_, B_) hipLaunchKernelGGL((pwd::bwd_kernel<kr, R_, B_>), grid, dim3(pwd::NT), 0, st, a)
 #define DK_BW(kr)             \
   if (K == kr) {              \
@@ -1119,7 +1529,6 @@ int pw_deep_bwd_bnbwd(const float* g, const float* bn_x, int M, int K, int C, co
     return launch_status();   \
   }
   DK_BW(128)
-  DK_BW(256)
 #undef DK_BW
 #undef DK_L
   return DK_ERR_ARGS;
