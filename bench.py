@@ -51,6 +51,8 @@ def parse():
                     help="per-kernel HBM traffic from rocprofv3 FETCH_SIZE/WRITE_SIZE passes of this same command "
                          "(scripts/pmc_summary.py output; default: the newest summary of this config in "
                          "profiles/pmc_index.json)")
+    ap.add_argument("--knob", action="append", default=[], metavar="KIND=V",
+                    help="A/B runs: dk_debug_set_gemm_config(KIND, V) before the run (include/dorknet_hip.h)")
     a = ap.parse_args()
     # enough warmup for the clocks to settle (the first timed steps after 3 warmups ran up to 5 %
     # slow, profiles/r03s_cfg2_rows.txt round 1), and more steps for config 2's 1.6 ms pass
@@ -579,10 +581,22 @@ def spawn_ranks(args):
     return subprocess.call(cmd, env=env)
 
 
+def set_knobs(args):
+    """--knob KIND=V (A/B runs): library knobs set before the run."""
+    if not args.knob:
+        return
+    from dorknet_amd._hip import lib
+    for kv in args.knob:
+        k, v = (int(t) for t in kv.split("="))
+        if lib.dk_debug_set_gemm_config(k, v) < 0:
+            raise SystemExit("unknown knob {}".format(k))
+
+
 def main():
     args = parse()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(spawn_ranks(args))
+    set_knobs(args)
     if args.config != 3:
         if args.gpus != 1:
             raise SystemExit("--config {} is a one-GPU configuration".format(args.config))

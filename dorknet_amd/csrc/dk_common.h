@@ -253,7 +253,7 @@ int nt_stores(int fam);
 // knobs by number).
 enum KnobId : int {
   kKnobRowCfg = 0, kKnobSplitCfg = 1, kKnobFillSplits = 2, kKnobPwStream = 3, kKnobNtStores = 4,
-  kKnobDwbBlocks = 7, kKnobDwSeg = 8, kKnobPwsh = 9, kKnobPwDeep = 11, kKnobPwDeep16 = 13, kKnobPwDeepBwd = 14,
+  kKnobDwbBlocks = 7, kKnobDwSeg = 8, kKnobPwsh = 9, kKnobPwDeep = 11, kKnobPw16 = 12, kKnobPwDeep16 = 13, kKnobPwDeepBwd = 14,
   kKnobWgradBlocks = 18, kKnobEwVariant = 19, kKnobDwbCols = 21, kNumKnobs = 23
 };
 int knob(int id);

@@ -60,7 +60,7 @@ __global__ void w_phase_kernel(const float* __restrict__ w, int K, int C, int R,
 // Tuning knobs (knobs.hip): kind = the KnobId; cfg = -1 restores the default.
 DK_API int dk_debug_set_gemm_config(int kind, int cfg) {
   // unused / retired numbers (knobs.hip) and the internal launch variant are refused
-  if (kind < 0 || kind >= kNumKnobs || kind == 5 || kind == 6 || kind == 10 || kind == 12 || (kind >= 15 && kind <= 17) ||
+  if (kind < 0 || kind >= kNumKnobs || kind == 5 || kind == 6 || kind == 10 || (kind >= 15 && kind <= 17) ||
       kind == 20 || kind == 22 || kind == kKnobEwVariant)
     return -1;
   knob_set(kind, cfg);

@@ -483,7 +483,7 @@ __device__ __forceinline__ void mfma16_tile(const float* ap, const f32x4* bw, f3
 }
 
 template <int KR, bool RES, bool PART>
-__global__ __launch_bounds__(NT16, 1) void dgrad16_kernel(DgradArgs a) {
+__global__ __launch_bounds__(NT16, 2) void dgrad16_kernel(DgradArgs a) {
   using L = K16<KR>;
   constexpr int SK = L::SK, RS = L::RS, KV = L::KV, LV = L::LV, NQ = L::NQ;
   static_assert(KR % 64 == 0 && (SK / 4) % 2 == 1 && NT16 % KV == 0 && LV >= 1, "pwd::dgrad16_kernel shape");
@@ -877,7 +877,7 @@ __global__ __launch_bounds__(NT, bwd_wps<KR>()) void bwd_kernel(BwdArgs a) {
 // k-group lanes of a column, then the block's columns, into one partial row as before.
 // ---------------------------------------------------------------------------------------
 template <int KR, bool BN, bool STATS, bool STRIDED, bool HB>
-__global__ __launch_bounds__(NT16, 1) void fwd16_kernel(FwdArgs a) {
+__global__ __launch_bounds__(NT16, 2) void fwd16_kernel(FwdArgs a) {
   using L = K16<KR>;
   constexpr int SK = L::SK, RS = L::RS, KV = L::KV, LV = L::LV, NQ = L::NQ;
   static_assert(KR % 64 == 0 && (SK / 4) % 2 == 1 && NT16 % KV == 0 && LV >= 1, "pwd::fwd16_kernel shape");
@@ -956,14 +956,26 @@ __global__ __launch_bounds__(NT16, 1) void fwd16_kernel(FwdArgs a) {
   {
     f32x4 st[LV];
     load_tile(t, st);
-    // B fragments W[col][k(i, kg)], i = 4q + u, after the first tile's loads
+    // B fragments W[col][k(i, kg)], i = 4q + u, after the first tile's loads.  MFMAs 4q .. 4q + 3 take
+    // k = 16 q + c(kg) + {0, 2, 8, 10} (c(kg) = (kg >> 1) + 4 (kg & 1)): the four k-group lanes of a
+    // column load the 16-float chunk 16 q .. + 15 as one float4 each (coalesced: one 64-byte segment per
+    // column; one scalar load per value made 4x the cache-line requests) and exchange -- lane kg takes
+    // elements kg >> 1 and + 2 of lanes (kg & 1) and (kg & 1) + 2.
+    {
+      const float* wrow = a.w + (size_t)col * KR + 4 * kg;
+      const int e0 = kg >> 1, sa = c16 + 16 * (kg & 1), sb = sa + 32;
 #pragma unroll
-    for (int q = 0; q < NQ; ++q)
+      for (int q = 0; q < NQ; ++q) {
+        const f32x4 v = ld4(wrow + 16 * q);
+        float xa[4], xb[4];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int i = 4 * q + u;
-        bw[q][u] = a.w[(size_t)col * KR + 8 * (i >> 1) + 2 * (i & 1) + (kg >> 1) + 4 * (kg & 1)];
+        for (int e = 0; e < 4; ++e) {
+          xa[e] = __shfl(v[e], sa, 64);
+          xb[e] = __shfl(v[e], sb, 64);
+        }
+        bw[q] = e0 ? f32x4{xa[1], xa[3], xb[1], xb[3]} : f32x4{xa[0], xa[2], xb[0], xb[2]};
       }
+    }
     stage(&As[0][0], st);
   }
   __syncthreads();
@@ -1038,7 +1050,7 @@ __global__ __launch_bounds__(NT16, 1) void fwd16_kernel(FwdArgs a) {
 // the same fixed-order reduce follows).
 // ---------------------------------------------------------------------------------------
 template <int KR, bool RES, bool BNIN>
-__global__ __launch_bounds__(NT16, 1) void bwd16_kernel(BwdArgs a) {
+__global__ __launch_bounds__(NT16, 2) void bwd16_kernel(BwdArgs a) {
   using L = K16<KR>;
   constexpr int SK = L::SK, RS = L::RS, KV = L::KV, LV = L::LV, NQ = L::NQ, NKT = KR / 16;
   static_assert(KR % 64 == 0 && (SK / 4) % 2 == 1 && NT16 % KV == 0 && LV >= 1, "pwd::bwd16_kernel shape");
@@ -1229,6 +1241,24 @@ __global__ __launch_bounds__(NT16, 1) void bwd16_kernel(BwdArgs a) {
 #define DK_PWD_KR(X) X(64) X(128) X(256) X(512)
 #define DK_PWD_KR_DGRAD(X) X(64) X(128) X(256)  // (K = 512: dgrad16_kernel)
 
+// The forward's launch: the 16 x 16 kernel at C = 512 (w16), else fwd_kernel.
+template <int KR, bool B_, bool S_, bool T_>
+static void launch_fwd(bool w16, bool bias, dim3 grid, hipStream_t st, const FwdArgs& a) {
+  if constexpr (KR == 512) {
+    if (w16) {
+      if (bias)
+        hipLaunchKernelGGL((fwd16_kernel<KR, B_, S_, T_, true>), grid, dim3(NT16), 0, st, a);
+      else
+        hipLaunchKernelGGL((fwd16_kernel<KR, B_, S_, T_, false>), grid, dim3(NT16), 0, st, a);
+      return;
+    }
+  }
+  if (bias)
+    hipLaunchKernelGGL((fwd_kernel<KR, B_, S_, T_, true>), grid, dim3(NT), 0, st, a);
+  else
+    hipLaunchKernelGGL((fwd_kernel<KR, B_, S_, T_, false>), grid, dim3(NT), 0, st, a);
+}
+
 static int occupancy(const void* fn, int nt = NT) {
   int v = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, fn, nt, 0) != hipSuccess || v < 1) v = 1;
@@ -1357,14 +1387,17 @@ bool pw_deep_dgrad_ok(int K, int C, int M) {
   return (size_t)M * (K > C ? K : C) * 4 < ((size_t)1 << 31);
 }
 
-// C = 512 runs the two-waves-per-SIMD 16 x 16 kernel (fwd16_kernel), 16-pixel tiles.
-static bool pwd_fwd16(int C) { return C == 512; }
+// C = 512 runs the two-waves-per-SIMD 16 x 16 kernel (fwd16_kernel), 16-pixel tiles; knob 12 = 0: the
+// one-wave fwd_kernel<512> (A/B).  At C = 128 / 256 the 16 x 16 layout (four waves per SIMD) measured
+// slower than fwd_kernel (0.50-0.52 vs 0.62 of the fp32 peak standalone, config 3 8.00 -> 8.15 ms;
+// profiles/r06f_pwd16_fwd_ab.txt), so fwd16_kernel is instantiated at C = 512 only.
+static bool pwd_fwd16(int C) { return C == 512 && knob(kKnobPw16) == 1; }
 
 int pw_deep_fwd_rows(int M, int K, int C) {
   if (pwd_fwd16(C)) return pwd::grid_x(M, K, pwd::fwd16_occ<512>(), pwd::TR16);
 #define DK_ROWS(kr) \
   if (C == kr) return pwd::grid_x(M, K, pwd::fwd_occ<kr>());
-  DK_PWD_KR_DGRAD(DK_ROWS)
+  DK_PWD_KR(DK_ROWS)
 #undef DK_ROWS
   return 0;
 }
@@ -1393,19 +1426,8 @@ int pw_deep_fwd(const float* x, int N, int H, int W, int stride, int OH, int OW,
   a.nt = nt_stores(kNtPwd);
   const dim3 grid(pw_deep_fwd_rows(M, K, C), K / pwd::NB);
   if (grid.x == 0) return DK_ERR_ARGS;
-  // (C = 512: fwd16_kernel, pwd_fwd16)
-#define DK_L(kr, B_, S_, T_)                                                                           \
-  do {                                                                                                 \
-    if constexpr (kr == 512) {                                                                         \
-      if (bias)                                                                                        \
-        hipLaunchKernelGGL((pwd::fwd16_kernel<kr, B_, S_, T_, true>), grid, dim3(pwd::NT16), 0, st, a);  \
-      else                                                                                             \
-        hipLaunchKernelGGL((pwd::fwd16_kernel<kr, B_, S_, T_, false>), grid, dim3(pwd::NT16), 0, st, a); \
-    } else if (bias)                                                                                   \
-      hipLaunchKernelGGL((pwd::fwd_kernel<kr, B_, S_, T_, true>), grid, dim3(pwd::NT), 0, st, a);      \
-    else                                                                                               \
-      hipLaunchKernelGGL((pwd::fwd_kernel<kr, B_, S_, T_, false>), grid, dim3(pwd::NT), 0, st, a);     \
-  } while (0)
+  const bool w16 = pwd_fwd16(C);
+#define DK_L(kr, B_, S_, T_) pwd::launch_fwd<kr, B_, S_, T_>(w16, bias != nullptr, grid, st, a)
 #define DK_FWD(kr)                    \
   if (C == kr) {                      \
     if (strided) {                    \
@@ -1482,12 +1504,14 @@ bool pw_deep_bwd_ok(int K, int C, int M) {
   if (!pwd_bwd_enabled() || M <= 0 || (K != 128 && K != 256) || C % pwd::NB) return false;
   return (size_t)M * (K > C ? K : C) * 4 < ((size_t)1 << 31);
 }
-// K = 256 runs the two-waves-per-SIMD 16 x 16 kernel (bwd16_kernel), 16-pixel tiles.
+// K = 256 runs the two-waves-per-SIMD 16 x 16 kernel (bwd16_kernel), 16-pixel tiles.  At K = 128 the
+// 16 x 16 layout (four waves per SIMD) measured slower than bwd_kernel<128> (173.6 vs 163.0 us at
+// 28 x 28 x 128, profiles/r06f_pwd16_bwd_ab.txt), so bwd16_kernel is instantiated at K = 256 only.
 static bool pwd_bwd16(int K) { return K == 256; }
 
 int pw_deep_bwd_rows(int M, int K, int C) {
-  if (K == 128) return pwd::grid_x(M, C, pwd::bwd_occ<128>());
   if (pwd_bwd16(K)) return pwd::grid_x(M, C, pwd::bwd16_occ<256>(), pwd::TR16);
+  if (K == 128) return pwd::grid_x(M, C, pwd::bwd_occ<128>());
   return 0;
 }
 int pw_deep_bwd_slices(int M, int K, int C) { return C / pwd::NB; }
@@ -1503,17 +1527,22 @@ int pw_deep_bwd_bnbwd(const float* g, const float* bn_x, int M, int K, int C, co
   const dim3 grid(pw_deep_bwd_rows(M, K, C), C / pwd::NB);
   if (grid.x == 0) return DK_ERR_ARGS;
   if (pwd_bwd16(K)) {
-#define DK_L16(R_, B_) hipLaunchKernelGGL((pwd::bwd16_kernel<256, R_, B_>), grid, dim3(pwd::NT16), 0, st, a)
-    if (res && im)
-      DK_L16(true, true);
-    else if (res)
-      DK_L16(true, false);
-    else if (im)
-      DK_L16(false, true);
-    else
-      DK_L16(false, false);
+#define DK_L16(kr, R_, B_) hipLaunchKernelGGL((pwd::bwd16_kernel<kr, R_, B_>), grid, dim3(pwd::NT16), 0, st, a)
+#define DK_B16(kr)             \
+  if (K == kr) {               \
+    if (res && im)             \
+      DK_L16(kr, true, true);  \
+    else if (res)              \
+      DK_L16(kr, true, false); \
+    else if (im)               \
+      DK_L16(kr, false, true); \
+    else                       \
+      DK_L16(kr, false, false); \
+    return launch_status();    \
+  }
+    DK_B16(256)
+#undef DK_B16
 #undef DK_L16
-    return launch_status();
   }
 #define DK_L(kr, R_, B_) hipLaunchKernelGGL((pwd::bwd_kernel<kr, R_, B_>), grid, dim3(pwd::NT), 0, st, a)
 #define DK_BW(kr)             \

@@ -63,6 +63,8 @@ int dk_mixup_f32(const float* a, const float* b, long long n, float p, float one
  * kind 8: output rows per thread of the depthwise forward / stride-1 dgrad (-1 = the shape rule);
  * kind 9: the bf16 streaming pointwise kernels (1 = default; 0 = the tiled engine);
  * kind 11: the fp32 weight-stationary deep pointwise kernels (1 = default);
+ * kind 12: the C = 512 deep pointwise forward on the two-waves-per-SIMD 16 x 16 layout (1 = default; 0 = the
+ * one-wave 32 x 32 kernel);
  * kind 13: the bf16 weight-stationary deep pointwise kernels (1 = default);
  * kind 14: the fused deep pointwise backward, dgrad + weight gradient in one pass (1 = default);
  * kind 18: blocks a split-K weight gradient aims for (default 1024);

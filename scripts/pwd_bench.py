@@ -46,9 +46,11 @@ def main():
     if "--shape" in sys.argv:
         shapes = [tuple(int(v) for v in sys.argv[sys.argv.index("--shape") + 1].split(","))]
     fold = "--fold" in sys.argv
-    modes = (0, 1)
-    if "--deep" in sys.argv:
-        modes = (int(sys.argv[sys.argv.index("--deep") + 1]),)
+    # 0: the tiled engine; 1: the deep kernels; 2: the deep kernels with knob 12 (the 16 x 16 layout
+    # at the smaller reductions too)
+    modes = (0, 1, 2)
+    if "--modes" in sys.argv:
+        modes = tuple(int(v) for v in sys.argv[sys.argv.index("--modes") + 1].split(","))
     torch.manual_seed(0)
     for HW, C, K in shapes:
         M = B * HW * HW
@@ -60,8 +62,9 @@ def main():
         flops = 2.0 * M * K * C
         res, outs, wout = [], {}, {}
         for deep in modes:
-            lib.dk_debug_set_gemm_config(11, deep)
-            lib.dk_debug_set_gemm_config(14, deep)
+            lib.dk_debug_set_gemm_config(11, 1 if deep else 0)
+            lib.dk_debug_set_gemm_config(14, 1 if deep else 0)
+            lib.dk_debug_set_gemm_config(12, 1 if deep == 2 else 0)
             y = torch.full((M * K,), float("nan"), device="cuda")
             dy = torch.full((M * K,), float("nan"), device="cuda")
             dx = torch.full((M * C,), float("nan"), device="cuda")
@@ -116,14 +119,18 @@ def main():
                 line.append(f"fused bwd {tb:6.1f} us {2 * flops / tb / 1e6 / PEAK:4.2f}")
             torch.cuda.synchronize()
             outs[deep] = (y.clone(), dy.clone(), dx.clone())
-            res.append(("deep " if deep else "old  ") + ", ".join(line))
-        lib.dk_debug_set_gemm_config(11, -1)
-        lib.dk_debug_set_gemm_config(14, -1)
-        same = ["bitwise" if torch.equal(a, b) else "DIFF(max %.2e)" % float((a - b).abs().nan_to_num(1e30).max())
-                for a, b in zip(outs[0], outs[1])] if len(outs) == 2 else []
-        if len(wout) == 2:
-            a, b = wout[0].double(), wout[1].double()
-            same.append("dW rel %.1e" % float((a - b).norm() / a.norm()))
+            res.append(("old  ", "deep ", "d16  ")[deep] + ", ".join(line))
+        for k in (11, 12, 14):
+            lib.dk_debug_set_gemm_config(k, -1)
+        same = []
+        ms = sorted(outs)
+        for m0, m1 in zip(ms, ms[1:]):
+            same.append("%d~%d " % (m0, m1) + " ".join(
+                "bitwise" if torch.equal(a, b) else "DIFF(max %.2e)" % float((a - b).abs().nan_to_num(1e30).max())
+                for a, b in zip(outs[m0], outs[m1])))
+            if m0 in wout and m1 in wout:
+                a, b = wout[m0].double(), wout[m1].double()
+                same.append("dW rel %.1e" % float((a - b).norm() / a.norm()))
         print(f"{B}x{HW}x{HW} C={C:3d} K={K:3d} | " + " | ".join(res) + " | y/dy/dx " + " ".join(same), flush=True)
     if only in (None, "skip") and "--shape" not in sys.argv:
         for H, C, K in SKIPS:

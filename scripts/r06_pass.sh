@@ -6,7 +6,10 @@
 #   bench     config 3 bench line                  bench5 / bench2   the config 5 / 2 lines
 #   prof      rocprofv3 kernel stats of config 3   suite  the whole -m gpu suite
 #   sq        SQ counter passes of config 3 (scripts/sq_passes.sh)
+#   ab        config-3 bench lines alternating the knob settings in $AB (e.g. AB="12=1 12=0"), 2 rounds
+#   prof0     as prof with the knob settings in $KNOBS (e.g. KNOBS="--knob 12=0")
 set -u
+AB=${AB:-}; KNOBS=${KNOBS:-}
 TAG=$1; shift
 ROOT=$(pwd); OUT=$ROOT/gpurun_out; mkdir -p "$OUT"
 step() { echo "== $1 rc=$2"; if [ "$2" -ne 0 ]; then echo "stopping after rc=$2"; exit "$2"; fi; }
@@ -31,6 +34,14 @@ for s in "$@"; do
               python "$ROOT/bench.py" --steps 5 --warmup 2 --cpu-sample 0 --no-roofline > "$OUT/prof_bench_$TAG.json" 2> "$OUT/prof_$TAG.err")
           rc=$?; step prof $rc
           python scripts/prof_summary.py "$OUT/prof_$TAG" --steps 6 > "$OUT/kstats_$TAG.md"; head -24 "$OUT/kstats_$TAG.md";;
+    prof0) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/prof0_$TAG" -o bench -- \
+              python "$ROOT/bench.py" --steps 5 --warmup 2 --cpu-sample 0 --no-roofline $KNOBS > "$OUT/prof0_bench_$TAG.json" 2> "$OUT/prof0_$TAG.err")
+          rc=$?; step prof0 $rc
+          python scripts/prof_summary.py "$OUT/prof0_$TAG" --steps 6 > "$OUT/kstats0_$TAG.md"; head -24 "$OUT/kstats0_$TAG.md";;
+    ab) for round in 1 2; do for kv in $AB; do
+          timeout -k 10 300 python bench.py --cpu-sample 0 --no-roofline --knob $kv > "$OUT/ab_${TAG}_${kv}_$round.json" 2>/dev/null
+          rc=$?; echo "knob $kv: $(grep -o 'ms_per_step": [0-9.]*' "$OUT/ab_${TAG}_${kv}_$round.json")"; step ab $rc
+        done; done;;
     sq) bash scripts/sq_passes.sh "$TAG" > "$OUT/sq_$TAG.log" 2>&1; rc=$?; tail -3 "$OUT/sq_$TAG.log"; step sq $rc
           python scripts/sq_ratios.py "$OUT/pmc_$TAG" --top 30 > "$OUT/sq_ratios_$TAG.md"; head -32 "$OUT/sq_ratios_$TAG.md";;
     suite) timeout -k 10 900 $PYT tests -m gpu > "$OUT/tests_${TAG}.log" 2>&1
