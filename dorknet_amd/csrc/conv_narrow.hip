@@ -268,7 +268,9 @@ __global__ __launch_bounds__(NT, 3) void wgrad_kernel(DyIn d, const float* __res
   extern __shared__ float smem[];
   float* const xin = smem;  // (C + 1) * R rows x CS: the ring, then R zero rows
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  float* const at = smem + (C + 1) * R * g.CS + wave * QC * 64 + lane;  // A table: [wave][q][lane]
+  // A table: [wave][q / 2][lane][q & 1] -- the pair (q, q + 1) of a lane is one 8-byte store and load
+  static_assert(QC % 2 == 0, "pixel quads come in pairs");
+  float* const at = smem + (C + 1) * R * g.CS + wave * QC * 64 + 2 * lane;
   const int li = lane & 15, lg = lane >> 4;
   const int filt = 16 * wave + li;  // this lane's filter (A row)
   const int voff = filt < g.K ? (lg * g.K + filt) * 4 : (int)kOOBBytes;
@@ -318,16 +320,29 @@ __global__ __launch_bounds__(NT, 3) void wgrad_kernel(DyIn d, const float* __res
 #pragma unroll
       for (int nt = 0; nt < NTN; ++nt) offn[nt] = offlo[nt] + (sb >= thr[nt] ? (sb - R) * g.CS : sb * g.CS);
     }
+    // dy -> this lane's slots of the wave's A table, two pixel quads at a time in packed fp32 (v_pk_*:
+    // the same IEEE operations as bn_bwd_elem / bn_out per element, bit-identical; the per-element form
+    // made this the kernel's main VALU work, 4.2 VALU instructions per MFMA, profiles/r06g_sq_ratios_c3.md)
+    const bool edge = 4 * QC > g.OW || 16 * (wave + 1) > g.K;  // (uniform) ragged / padded quads or filters
 #pragma unroll
-    for (int q = 0; q < QC; ++q) {  // dy -> this lane's slot of the wave's A table
-      float ge = dr.gq[q];
+    for (int q = 0; q < QC; q += 2) {
+      f32x2 ge = {dr.gq[q], dr.gq[q + 1]};
       if constexpr (BNDEF) {
-        const float xe = dr.xq[q];
-        if (d.relu && !(bn_out(xe, mu, is, ga, be) > 0.f)) ge = 0.f;
-        ge = bn_bwd_elem(xe, ge, mu, is, f, k1, k2);
+        const f32x2 xe = {dr.xq[q], dr.xq[q + 1]};
+        const f32x2 xh = (xe - f32x2{mu, mu}) * f32x2{is, is};
+        if (d.relu) {
+          const f32x2 bo = __builtin_elementwise_fma(f32x2{ga, ga}, xh, f32x2{be, be});  // bn_out
+          ge[0] = bo[0] > 0.f ? ge[0] : 0.f;
+          ge[1] = bo[1] > 0.f ? ge[1] : 0.f;
+        }
+        ge = f32x2{f, f} * __builtin_elementwise_fma(-xh, f32x2{k2, k2}, ge - f32x2{k1, k1});  // bn_bwd_elem
       }
-      if (4 * q + lg >= g.OW || filt >= g.K) ge = 0.f;  // ragged / padded quad, filter past K
-      at[q * 64] = ge;
+      if (edge) {
+#pragma unroll
+        for (int e = 0; e < 2; ++e)
+          if (4 * (q + e) + lg >= g.OW || filt >= g.K) ge[e] = 0.f;  // ragged / padded quad, filter past K
+      }
+      *reinterpret_cast<f32x2*>(at + q * 64) = ge;
     }
     __syncthreads();
     if (row + 1 < r1) {  // in flight under this row's MFMAs
@@ -335,11 +350,14 @@ __global__ __launch_bounds__(NT, 3) void wgrad_kernel(DyIn d, const float* __res
       dr.load(d, g, row + 1, voff, voffg);
     }
 #pragma unroll
-    for (int q = 0; q < QC; ++q) {
-      const float a = at[q * 64];
-      const float* bq = xin + 4 * ST * q;
+    for (int q = 0; q < QC; q += 2) {
+      const f32x2 a2 = *reinterpret_cast<const f32x2*>(at + q * 64);
 #pragma unroll
-      for (int nt = 0; nt < NTN; ++nt) acc[nt] = mfma16(a, bq[offn[nt]], acc[nt]);
+      for (int e = 0; e < 2; ++e) {
+        const float* bq = xin + 4 * ST * (q + e);
+#pragma unroll
+        for (int nt = 0; nt < NTN; ++nt) acc[nt] = mfma16(a2[e], bq[offn[nt]], acc[nt]);
+      }
     }
   }
   // partial dw of this block: ws[blk][k][n] (C/D row = filter 16w + 4lg + v, column n)

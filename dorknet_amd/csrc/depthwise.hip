@@ -450,7 +450,7 @@ __global__ __launch_bounds__(256, JOIN ? 2 : 1) void dw_fwd_kernel(const T* __re
   }
   if constexpr (STATS != 0) {
     // fixed-order block reduction over the 256 / C4 threads of each channel group
-    __shared__ double red[256][8];
+    __shared__ double red[256][9];  // (padded: [256][8] put 16 lanes' writes on one bank pair)
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       red[threadIdx.x][e] = s1[e];
@@ -636,7 +636,7 @@ __global__ __launch_bounds__(256) void dw_dgrad_subpixel_kernel(const T* __restr
     }
   }
   if constexpr (JOIN) {
-    __shared__ double red[256][8];
+    __shared__ double red[256][9];  // (padded: [256][8] put 16 lanes' writes on one bank pair)
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       red[threadIdx.x][e] = s1[e];

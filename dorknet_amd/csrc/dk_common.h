@@ -253,7 +253,7 @@ int nt_stores(int fam);
 // knobs by number).
 enum KnobId : int {
   kKnobRowCfg = 0, kKnobSplitCfg = 1, kKnobFillSplits = 2, kKnobPwStream = 3, kKnobNtStores = 4,
-  kKnobDwbBlocks = 7, kKnobDwSeg = 8, kKnobPwsh = 9, kKnobPwDeep = 11, kKnobPw16 = 12, kKnobPwDeep16 = 13, kKnobPwDeepBwd = 14,
+  kKnobDwbBlocks = 7, kKnobDwSeg = 8, kKnobPwsh = 9, kKnobPwDeep = 11, kKnobPwDeep16 = 13, kKnobPwDeepBwd = 14,
   kKnobWgradBlocks = 18, kKnobEwVariant = 19, kKnobDwbCols = 21, kNumKnobs = 23
 };
 int knob(int id);
@@ -307,6 +307,7 @@ int pw_deep_dgrad_slices(int M, int K, int C);
 bool pw_deep_bwd_ok(int K, int C, int M);
 int pw_deep_bwd_rows(int M, int K, int C);
 int pw_deep_bwd_slices(int M, int K, int C);
+
 int pw_deep_bwd_bnbwd(const float* g, const float* bn_x, int M, int K, int C, const float* om, const float* ois,
                       const float* og, const float* ob, int orelu, const float* k12, const float* w, float* dx,
                       const float* res, const float* x, const float* im, const float* iis, const float* ig,

@@ -27,7 +27,8 @@ constexpr int kDefaults[kNumKnobs] = {
     1,           // kKnobPwsh: bf16 streaming pointwise kernels
     0,           // 10: unused
     1,           // kKnobPwDeep: fp32 weight-stationary deep pointwise kernels
-    1,           // kKnobPw16: the C = 512 pointwise forward on the 16 x 16 layout (0: fwd_kernel<512>)
+    0,           // 12: retired (round 6: 16 x 16 variants of the C = 512 forward and the deep weight gradient,
+                 //     measured slower in the step)
     1,           // kKnobPwDeep16: bf16 weight-stationary deep pointwise kernels
     1,           // kKnobPwDeepBwd: fused deep pointwise backward (dgrad + wgrad)
     0,           // 15-17: retired (K = C = 128 streaming-forward switch; tiled fused backward prefetch and

@@ -486,7 +486,7 @@ template <int KR, bool RES, bool PART>
 __global__ __launch_bounds__(NT16, 2) void dgrad16_kernel(DgradArgs a) {
   using L = K16<KR>;
   constexpr int SK = L::SK, RS = L::RS, KV = L::KV, LV = L::LV, NQ = L::NQ;
-  static_assert(KR % 64 == 0 && (SK / 4) % 2 == 1 && NT16 % KV == 0 && LV >= 1, "pwd::dgrad16_kernel shape");
+  static_assert(KR % 256 == 0 && (SK / 4) % 2 == 1 && NT16 % KV == 0 && LV >= 1, "pwd::dgrad16_kernel shape");
   __shared__ __attribute__((aligned(16))) float As[2][TR16 * SK];
   __shared__ __attribute__((aligned(16))) f32x4 bnt[7][KV];
   static_assert(sizeof(double) * 2 * NT16 <= sizeof(float) * 2 * TR16 * SK, "fold scratch fits in the tiles");
@@ -495,7 +495,13 @@ __global__ __launch_bounds__(NT16, 2) void dgrad16_kernel(DgradArgs a) {
   const int c16 = lane & 15, kg = lane >> 4;
   const int n0 = blockIdx.y * NB, N = a.N;
   const int col = n0 + 16 * wave + c16;
-  const int kv = tid % KV, r0 = tid / KV;
+  // staging lanes: lanes 0-31 of a wave take the even float4s of its 64-float4 stretch of a pixel row,
+  // lanes 32-63 the odd ones, so the 16 lanes of one LDS store all write one k-group region's 32
+  // contiguous floats (in stretch order, even and odd neighbours hit the regions 4 banks apart: 3.6
+  // conflict cycles per LDS instruction, profiles/r06g_sq_ratios_c3.md); the wave's global loads still
+  // cover the stretch's 1 KB
+  const int kvl = tid % KV, r0 = tid / KV;
+  const int kv = (kvl & ~63) | ((kvl & 31) << 1) | ((kvl >> 5) & 1);
   if (tid < KV) {
     const f32x4 ga = ld4(a.og + 4 * tid), is = ld4(a.ois + 4 * tid);
     bnt[0][tid] = ld4(a.om + 4 * tid);
@@ -870,170 +876,6 @@ __global__ __launch_bounds__(NT, bwd_wps<KR>()) void bwd_kernel(BwdArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------
-// The C = 512 forward at two waves per SIMD (round 6): fwd_kernel's work with dgrad16_kernel's layout
-// (8 waves of 16 output columns, 16-pixel tiles, the k-permuted LDS tile of the BN-on-load input,
-// v_mfma_f32_16x16x4_f32 in the same k order: y bit-identical to fwd_kernel and the tiled engine).
-// The BatchNorm's per-channel terms sit in an LDS table; the output statistics reduce the four
-// k-group lanes of a column, then the block's columns, into one partial row as before.
-// ---------------------------------------------------------------------------------------
-template <int KR, bool BN, bool STATS, bool STRIDED, bool HB>
-__global__ __launch_bounds__(NT16, 2) void fwd16_kernel(FwdArgs a) {
-  using L = K16<KR>;
-  constexpr int SK = L::SK, RS = L::RS, KV = L::KV, LV = L::LV, NQ = L::NQ;
-  static_assert(KR % 64 == 0 && (SK / 4) % 2 == 1 && NT16 % KV == 0 && LV >= 1, "pwd::fwd16_kernel shape");
-  __shared__ __attribute__((aligned(16))) float As[2][TR16 * SK];
-  __shared__ __attribute__((aligned(16))) f32x4 bnt[4][BN ? KV : 1];
-  static_assert(sizeof(double) * 2 * NT16 <= sizeof(float) * 2 * TR16 * SK, "fold scratch fits in the tiles");
-
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int c16 = lane & 15, kg = lane >> 4;
-  const int n0 = blockIdx.y * NB, N = a.N;
-  const int col = n0 + 16 * wave + c16;
-  const float bias = HB ? a.bias[col] : 0.f;
-  const bool irelu = a.irelu != 0;
-  const int kv = tid % KV, r0 = tid / KV;
-  if constexpr (BN) {
-    if (tid < KV) {
-      bnt[0][tid] = ld4(a.im + 4 * tid);
-      bnt[1][tid] = ld4(a.iis + 4 * tid);
-      bnt[2][tid] = ld4(a.ig + 4 * tid);
-      bnt[3][tid] = ld4(a.ib + 4 * tid);
-    }
-  }
-  const __amdgpu_buffer_rsrc_t rx = make_rsrc_v(a.x, a.xbytes);
-  const int ntiles = (a.M + TR16 - 1) / TR16, G = gridDim.x;
-  uint32_t lofs[LV];
-#pragma unroll
-  for (int j = 0; j < LV; ++j) lofs[j] = off4(r0 + j * (NT16 / KV), KR, 4 * kv);
-  const uint32_t cbase = off4(4 * kg, N, col);
-  const int sreg = (kv & 1) * RS + (kv & ~1);
-
-  auto tile_rsrc16 = [&](const float* p, int ld, int tile, int nrows) {
-    const int rows = nrows - tile * TR16;
-    return make_rsrc_v(p + (size_t)tile * TR16 * ld, rows > 0 ? (uint32_t)rows * ld * 4u : 0u);
-  };
-  auto load_tile = [&](int tile, f32x4* st) {
-    const __amdgpu_buffer_rsrc_t rt = tile_rsrc16(a.x, KR, tile, a.M);
-#pragma unroll
-    for (int j = 0; j < LV; ++j) {
-      if constexpr (STRIDED) {
-        const int m = tile * TR16 + r0 + j * (NT16 / KV);
-        const int ow = m % a.OW, q = m / a.OW, oh = q % a.OH, n = q / a.OH;
-        const int row = (n * a.H + oh * a.sa) * a.W + ow * a.sa;
-        st[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rx, (int)off4(row, KR, 4 * kv), 0, 0));
-      } else {
-        st[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rt, (int)lofs[j], 0, 0));
-      }
-    }
-  };
-  auto stage = [&](float* dst, const f32x4* st) {
-    f32x4 mu, is, ga, be;
-    if constexpr (BN) {
-      mu = bnt[0][kv];
-      is = bnt[1][kv];
-      ga = bnt[2][kv];
-      be = bnt[3][kv];
-    }
-#pragma unroll
-    for (int j = 0; j < LV; ++j) {
-      f32x4 v = st[j];
-      if constexpr (BN) {
-        v = affine4(xhat4(v, mu, is), ga, be);
-        if (irelu) {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = __builtin_fmaxf(v[e], 0.f);
-        }
-      }
-      float* d = dst + (r0 + j * (NT16 / KV)) * SK + sreg;
-      *reinterpret_cast<f32x2*>(d) = f32x2{v[0], v[2]};
-      *reinterpret_cast<f32x2*>(d + 2 * RS) = f32x2{v[1], v[3]};
-    }
-  };
-
-  if constexpr (BN) __syncthreads();  // the BN table
-  int t = first_tile(ntiles);
-  f32x4 bw[NQ];
-  {
-    f32x4 st[LV];
-    load_tile(t, st);
-    // B fragments W[col][k(i, kg)], i = 4q + u, after the first tile's loads.  MFMAs 4q .. 4q + 3 take
-    // k = 16 q + c(kg) + {0, 2, 8, 10} (c(kg) = (kg >> 1) + 4 (kg & 1)): the four k-group lanes of a
-    // column load the 16-float chunk 16 q .. + 15 as one float4 each (coalesced: one 64-byte segment per
-    // column; one scalar load per value made 4x the cache-line requests) and exchange -- lane kg takes
-    // elements kg >> 1 and + 2 of lanes (kg & 1) and (kg & 1) + 2.
-    {
-      const float* wrow = a.w + (size_t)col * KR + 4 * kg;
-      const int e0 = kg >> 1, sa = c16 + 16 * (kg & 1), sb = sa + 32;
-#pragma unroll
-      for (int q = 0; q < NQ; ++q) {
-        const f32x4 v = ld4(wrow + 16 * q);
-        float xa[4], xb[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          xa[e] = __shfl(v[e], sa, 64);
-          xb[e] = __shfl(v[e], sb, 64);
-        }
-        bw[q] = e0 ? f32x4{xa[1], xa[3], xb[1], xb[3]} : f32x4{xa[0], xa[2], xb[0], xb[2]};
-      }
-    }
-    stage(&As[0][0], st);
-  }
-  __syncthreads();
-  double ps = 0.0, pq = 0.0;
-  int buf = 0;
-  for (; t < ntiles; t += G) {
-    f32x4 nst[LV];
-    load_tile(t + G, nst);
-    f32x4 acc;
-    mfma16_tile<NQ>(&As[buf][0] + c16 * SK + kg * RS, bw, acc);
-    const int mb = t * TR16 + 4 * kg;
-    const __amdgpu_buffer_rsrc_t ry = tile_rsrc16(a.y, N, t, a.M);
-    if constexpr (HB) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) acc[r] += bias;
-    }
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const float v = acc[r];
-      bstore_nt(__builtin_bit_cast(uint32_t, v), ry, (int)cbase, r * N * 4, a.nt);
-    }
-    if constexpr (STATS) {
-      const bool full = t * TR16 + TR16 <= a.M;  // a whole tile (uniform): no row masks
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const double d = (full || mb + r < a.M) ? (double)acc[r] : 0.0;
-        ps += d;
-        pq += d * d;
-      }
-    }
-    stage(&As[buf ^ 1][0], nst);
-    __syncthreads();
-    buf ^= 1;
-  }
-  if constexpr (STATS) {
-    double(*const red)[NB] = reinterpret_cast<double(*)[NB]>(&As[0][0]);  // [2][NB]
-    ps += __shfl_xor(ps, 16, 64);
-    pq += __shfl_xor(pq, 16, 64);
-    ps += __shfl_xor(ps, 32, 64);
-    pq += __shfl_xor(pq, 32, 64);
-    __syncthreads();  // the pixel tiles become scratch
-    if (kg == 0) {
-      red[0][16 * wave + c16] = ps;
-      red[1][16 * wave + c16] = pq;
-    }
-    __syncthreads();
-    for (int i = tid; i < 2 * NB; i += NT16) {
-      const int which = i / NB, c = i - which * NB;
-      pub_store(a.part + ((size_t)blockIdx.x * 2 + which) * N + n0 + c, red[which][c]);
-    }
-    if (a.ft.part) {
-      __syncthreads();
-      fold_tail<NT16>(a.ft, blockIdx.x, n0, NB, blockIdx.y, reinterpret_cast<double2*>(&As[0][0]));
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------------------
 // The fused backward on v_mfma_f32_16x16x4_f32 (round 6): bwd_kernel's dgrad + weight gradient with
 // dgrad16_kernel's layout -- 8 waves of 16 columns, 16-pixel tiles, the k-permuted LDS dy tile -- so
 // that at K = 256 a wave holds 64 VGPRs of B fragments and 64 of weight-gradient accumulators and two
@@ -1053,7 +895,7 @@ template <int KR, bool RES, bool BNIN>
 __global__ __launch_bounds__(NT16, 2) void bwd16_kernel(BwdArgs a) {
   using L = K16<KR>;
   constexpr int SK = L::SK, RS = L::RS, KV = L::KV, LV = L::LV, NQ = L::NQ, NKT = KR / 16;
-  static_assert(KR % 64 == 0 && (SK / 4) % 2 == 1 && NT16 % KV == 0 && LV >= 1, "pwd::bwd16_kernel shape");
+  static_assert(KR % 256 == 0 && (SK / 4) % 2 == 1 && NT16 % KV == 0 && LV >= 1, "pwd::bwd16_kernel shape");
   __shared__ __attribute__((aligned(16))) float As[2][TR16 * SK];
   __shared__ __attribute__((aligned(16))) f32x4 bnt[7][KV];
   static_assert(sizeof(double) * 2 * NT16 <= sizeof(float) * 2 * TR16 * SK, "fold scratch fits in the tiles");
@@ -1062,7 +904,13 @@ __global__ __launch_bounds__(NT16, 2) void bwd16_kernel(BwdArgs a) {
   const int c16 = lane & 15, kg = lane >> 4;
   const int n0 = blockIdx.y * NB, N = a.N;
   const int col = n0 + 16 * wave + c16;
-  const int kv = tid % KV, r0 = tid / KV;
+  // staging lanes: lanes 0-31 of a wave take the even float4s of its 64-float4 stretch of a pixel row,
+  // lanes 32-63 the odd ones, so the 16 lanes of one LDS store all write one k-group region's 32
+  // contiguous floats (in stretch order, even and odd neighbours hit the regions 4 banks apart: 3.6
+  // conflict cycles per LDS instruction, profiles/r06g_sq_ratios_c3.md); the wave's global loads still
+  // cover the stretch's 1 KB
+  const int kvl = tid % KV, r0 = tid / KV;
+  const int kv = (kvl & ~63) | ((kvl & 31) << 1) | ((kvl >> 5) & 1);
   if (tid < KV) {
     const f32x4 ga = ld4(a.og + 4 * tid), is = ld4(a.ois + 4 * tid);
     bnt[0][tid] = ld4(a.om + 4 * tid);
@@ -1241,24 +1089,6 @@ __global__ __launch_bounds__(NT16, 2) void bwd16_kernel(BwdArgs a) {
 #define DK_PWD_KR(X) X(64) X(128) X(256) X(512)
 #define DK_PWD_KR_DGRAD(X) X(64) X(128) X(256)  // (K = 512: dgrad16_kernel)
 
-// The forward's launch: the 16 x 16 kernel at C = 512 (w16), else fwd_kernel.
-template <int KR, bool B_, bool S_, bool T_>
-static void launch_fwd(bool w16, bool bias, dim3 grid, hipStream_t st, const FwdArgs& a) {
-  if constexpr (KR == 512) {
-    if (w16) {
-      if (bias)
-        hipLaunchKernelGGL((fwd16_kernel<KR, B_, S_, T_, true>), grid, dim3(NT16), 0, st, a);
-      else
-        hipLaunchKernelGGL((fwd16_kernel<KR, B_, S_, T_, false>), grid, dim3(NT16), 0, st, a);
-      return;
-    }
-  }
-  if (bias)
-    hipLaunchKernelGGL((fwd_kernel<KR, B_, S_, T_, true>), grid, dim3(NT), 0, st, a);
-  else
-    hipLaunchKernelGGL((fwd_kernel<KR, B_, S_, T_, false>), grid, dim3(NT), 0, st, a);
-}
-
 static int occupancy(const void* fn, int nt = NT) {
   int v = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, fn, nt, 0) != hipSuccess || v < 1) v = 1;
@@ -1289,22 +1119,6 @@ static int dgrad_occ() {
                         reinterpret_cast<const void*>(&dgrad_kernel<KR, false, false>)};
     int o = 1 << 20;
     for (const void* f : fs) o = std::min(o, occupancy(f));
-    return o;
-  }();
-  return occ;
-}
-
-template <int KR>
-static int fwd16_occ() {
-  static const int occ = [] {
-#define DK_F(B_, S_, T_) reinterpret_cast<const void*>(&fwd16_kernel<KR, B_, S_, T_, false>), \
-                         reinterpret_cast<const void*>(&fwd16_kernel<KR, B_, S_, T_, true>)
-    const void* fs[] = {DK_F(true, true, false), DK_F(true, false, false), DK_F(false, true, false),
-                        DK_F(false, false, false), DK_F(true, true, true), DK_F(true, false, true),
-                        DK_F(false, true, true), DK_F(false, false, true)};
-#undef DK_F
-    int o = 1 << 20;
-    for (const void* f : fs) o = std::min(o, occupancy(f, NT16));
     return o;
   }();
   return occ;
@@ -1387,14 +1201,7 @@ bool pw_deep_dgrad_ok(int K, int C, int M) {
   return (size_t)M * (K > C ? K : C) * 4 < ((size_t)1 << 31);
 }
 
-// C = 512 runs the two-waves-per-SIMD 16 x 16 kernel (fwd16_kernel), 16-pixel tiles; knob 12 = 0: the
-// one-wave fwd_kernel<512> (A/B).  At C = 128 / 256 the 16 x 16 layout (four waves per SIMD) measured
-// slower than fwd_kernel (0.50-0.52 vs 0.62 of the fp32 peak standalone, config 3 8.00 -> 8.15 ms;
-// profiles/r06f_pwd16_fwd_ab.txt), so fwd16_kernel is instantiated at C = 512 only.
-static bool pwd_fwd16(int C) { return C == 512 && knob(kKnobPw16) == 1; }
-
 int pw_deep_fwd_rows(int M, int K, int C) {
-  if (pwd_fwd16(C)) return pwd::grid_x(M, K, pwd::fwd16_occ<512>(), pwd::TR16);
 #define DK_ROWS(kr) \
   if (C == kr) return pwd::grid_x(M, K, pwd::fwd_occ<kr>());
   DK_PWD_KR(DK_ROWS)
@@ -1426,8 +1233,13 @@ int pw_deep_fwd(const float* x, int N, int H, int W, int stride, int OH, int OW,
   a.nt = nt_stores(kNtPwd);
   const dim3 grid(pw_deep_fwd_rows(M, K, C), K / pwd::NB);
   if (grid.x == 0) return DK_ERR_ARGS;
-  const bool w16 = pwd_fwd16(C);
-#define DK_L(kr, B_, S_, T_) pwd::launch_fwd<kr, B_, S_, T_>(w16, bias != nullptr, grid, st, a)
+#define DK_L(kr, B_, S_, T_)                                                                          \
+  do {                                                                                                \
+    if (bias)                                                                                         \
+      hipLaunchKernelGGL((pwd::fwd_kernel<kr, B_, S_, T_, true>), grid, dim3(pwd::NT), 0, st, a);     \
+    else                                                                                              \
+      hipLaunchKernelGGL((pwd::fwd_kernel<kr, B_, S_, T_, false>), grid, dim3(pwd::NT), 0, st, a);    \
+  } while (0)
 #define DK_FWD(kr)                    \
   if (C == kr) {                      \
     if (strided) {                    \
@@ -1562,5 +1374,6 @@ int pw_deep_bwd_bnbwd(const float* g, const float* bn_x, int M, int K, int C, co
 #undef DK_L
   return DK_ERR_ARGS;
 }
+
 
 }  // namespace dk

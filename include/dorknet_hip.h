@@ -50,7 +50,7 @@ int dk_mixup_f32(const float* a, const float* b, long long n, float p, float one
 /* Path selectors and tuning knobs for tests and A/B runs (dorknet_amd/csrc/knobs.hip: one registry
  * of atomics holding built-in defaults; no environment variable reaches them; not for production
  * use).  cfg = -1 restores the default.  Returns the number of configurations for kinds 0 / 1, 0 for
- * the others, -1 for an unknown or retired kind (5, 15-17, 20, 22).
+ * the others, -1 for an unknown or retired kind (5, 12, 15-17, 20, 22).
  * kind 0 / 1: force GEMM tile configuration `cfg` for forward/dgrad problems / split-K
  * weight-gradient problems (-1 = the built-in heuristic);
  * kind 2: split-K grids sized to one round of resident blocks (1 = default) or the fixed ~1024-block
@@ -63,14 +63,17 @@ int dk_mixup_f32(const float* a, const float* b, long long n, float p, float one
  * kind 8: output rows per thread of the depthwise forward / stride-1 dgrad (-1 = the shape rule);
  * kind 9: the bf16 streaming pointwise kernels (1 = default; 0 = the tiled engine);
  * kind 11: the fp32 weight-stationary deep pointwise kernels (1 = default);
- * kind 12: the C = 512 deep pointwise forward on the two-waves-per-SIMD 16 x 16 layout (1 = default; 0 = the
- * one-wave 32 x 32 kernel);
  * kind 13: the bf16 weight-stationary deep pointwise kernels (1 = default);
  * kind 14: the fused deep pointwise backward, dgrad + weight gradient in one pass (1 = default);
  * kind 18: blocks a split-K weight gradient aims for (default 1024);
  * kind 21: output columns per thread of the fused stride-1 depthwise backward (2 = default where the
  * width allows, 1 = one); the dk_dwconv_bwd_bnbwd*_stats_rows / _workspace_bytes follow it. */
 int dk_debug_set_gemm_config(int kind, int cfg);
+/* A HIP stream confined to every `every`-th compute unit of the device (hipExtStreamCreateWithCUMask;
+ * every = 1: all of them), for background work beside the critical path; *stream receives the
+ * hipStream_t.  dk_stream_destroy releases it. */
+int dk_stream_create_cu_mask(int every, void** stream);
+int dk_stream_destroy(void* stream);
 
 /* Bandwidth ceiling probe (not on the training path; scripts/stream_ceiling.py): reads nin
  * (1..3) fp32 arrays a, b, c and writes nout (0..2) arrays o0, o1 of numel elements each, 16

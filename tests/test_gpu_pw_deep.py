@@ -167,7 +167,7 @@ def test_deep_outputs_stay_in_bounds():
     assert bool(torch.isfinite(part).all()) and bool(torch.isfinite(partd).all())
 
 
-WGRAD_SHAPES = [(128, 64), (128, 128), (256, 128), (256, 256), (512, 512)]  # (K, C)
+WGRAD_SHAPES = [(128, 64), (128, 128), (256, 128), (256, 256), (512, 256), (512, 512)]  # (K, C)
 
 
 @pytest.mark.parametrize("K,C", WGRAD_SHAPES)
@@ -175,7 +175,7 @@ WGRAD_SHAPES = [(128, 64), (128, 128), (256, 128), (256, 256), (512, 512)]  # (K
                                            (True, 1, 16, 14, 14)])
 def test_deep_wgrad_matches_fp64(K, C, bn, relu, N, H, W):
     """dk_pwconv_wgrad_bnx_f32 / dk_pwconv_wgrad_f32 (the tiled engine's split-K weight gradient, the
-    deep layers' path when the fused backward is off) against an fp64 dW = dy^T relu(bn(x)) + l2 w,
+    deep layers' path where no fused backward takes them) against an fp64 dW = dy^T relu(bn(x)) + l2 w,
     elementwise within 3e-5 of sum |dy| |xh| (fp32 partial sums of a few hundred products each, then
     the fp64 reduce)."""
     rng = np.random.RandomState(K + 3 * C + N + int(bn) + 2 * relu)
@@ -217,6 +217,33 @@ def test_deep_wgrad_matches_fp64(K, C, bn, relu, N, H, W):
     for dw in outs:
         assert bool(torch.isfinite(dw).all())
         assert bool(((dw.double() - ref).abs() <= bound).all()), float(((dw.double() - ref).abs() / bound).max())
+
+
+@pytest.mark.parametrize("K,C,H", [(256, 128, 28), (512, 256, 14), (128, 128, 9), (256, 256, 13)])
+def test_deep_wgrad_strided_skip(K, C, H):
+    """dk_pwconv_wgrad_f32 at stride 2 (the downsampling blocks' skip projections: x read at (n, 2 oh, 2 ow))
+    against fp64, the same elementwise bound as above."""
+    N = 3
+    rng = np.random.RandomState(K + C + H)
+    OH = -(-H // 2)
+    M = N * OH * OH
+    dy = nhwc(rng.randn(N, K, OH, OH))
+    x = nhwc(rng.randn(N, C, H, H))
+    w = torch.as_tensor(rng.randn(K, C).astype(np.float32), device="cuda")
+    l2 = 1e-3
+    st = stream_handle()
+    nb = lib.dk_pwconv_wgrad_workspace_bytes(N, OH, OH, K, C)
+    ws = torch.empty(max(nb, 4) // 4 + 1, dtype=torch.float32, device="cuda")
+    dw = torch.full((K, C), float("nan"), device="cuda")
+    assert lib.dk_pwconv_wgrad_f32(dy.data_ptr(), x.data_ptr(), N, H, H, C, K, 2, OH, OH, w.data_ptr(), l2,
+                                   dw.data_ptr(), ws.data_ptr(), nb, st) == 0
+    torch.cuda.synchronize()
+    dy64 = dy.permute(0, 2, 3, 1).reshape(M, K).double()
+    xs = x[:, :, ::2, ::2].permute(0, 2, 3, 1).reshape(M, C).double()
+    ref = dy64.t() @ xs + l2 * w.double()
+    bound = 3e-5 * (dy64.abs().t() @ xs.abs()) + 1e-6
+    assert bool(torch.isfinite(dw).all())
+    assert bool(((dw.double() - ref).abs() <= bound).all()), float(((dw.double() - ref).abs() / bound).max())
 
 
 FUSED_KNOB = 14
