@@ -283,23 +283,11 @@ def async_wgrad_enabled() -> bool:
     return _ASYNC_DEPTH[0] > 0 and enabled("DORKNET_ASYNC_WGRAD")
 
 
-def _background_stream(dev):
-    """A stream for the side / branch work: with DORKNET_SIDE_CU_EVERY=n (A/B runs), confined to every
-    n-th compute unit (dk_stream_create_cu_mask), else an ordinary stream."""
-    every = int(getenv("DORKNET_SIDE_CU_EVERY", "0") or 0)
-    if every > 1:
-        ptr = ctypes.c_void_p()
-        with torch.cuda.device(dev):
-            lib.dk_stream_create_cu_mask(every, ctypes.addressof(ptr))
-        return torch.cuda.ExternalStream(ptr.value, device=torch.device("cuda", dev))
-    return torch.cuda.Stream(device=dev)
-
-
 def side_stream():
     dev = _get_dev() if _get_dev is not None else torch.cuda.current_device()
     s = _SIDE.get(dev)
     if s is None:
-        s = _SIDE[dev] = _background_stream(dev)
+        s = _SIDE[dev] = torch.cuda.Stream(device=dev)
     return s
 
 
@@ -491,7 +479,7 @@ def branch_stream():
     dev = _get_dev() if _get_dev is not None else torch.cuda.current_device()
     s = _BRANCH.get(dev)
     if s is None:
-        s = _BRANCH[dev] = _background_stream(dev)
+        s = _BRANCH[dev] = torch.cuda.Stream(device=dev)
     return s
 
 

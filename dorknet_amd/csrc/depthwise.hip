@@ -450,7 +450,10 @@ __global__ __launch_bounds__(256, JOIN ? 2 : 1) void dw_fwd_kernel(const T* __re
   }
   if constexpr (STATS != 0) {
     // fixed-order block reduction over the 256 / C4 threads of each channel group
-    __shared__ double red[256][9];  // (padded: [256][8] put 16 lanes' writes on one bank pair)
+    // (not padded like the other kernels' tables: [256][9] here left the stride-2 join variant -- 256
+    // VGPRs with spills -- without some of its y stores, tests/test_gpu_join_fwd.py; its time did not
+    // change with the padding)
+    __shared__ double red[256][8];
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       red[threadIdx.x][e] = s1[e];

@@ -22,6 +22,11 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 namespace dk {
 
+// halves of a float4 for packed fp32 (v_pk_mul / v_pk_fma / v_pk_add: two lanes of the same IEEE
+// operations per instruction, bit-identical to the scalar form)
+__device__ __forceinline__ f32x2 lo2(f32x4 v) { return f32x2{v[0], v[1]}; }
+__device__ __forceinline__ f32x2 hi2(f32x4 v) { return f32x2{v[2], v[3]}; }
+
 static inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
 static inline int launch_status() { return static_cast<int>(hipGetLastError()); }
@@ -307,6 +312,7 @@ int pw_deep_dgrad_slices(int M, int K, int C);
 bool pw_deep_bwd_ok(int K, int C, int M);
 int pw_deep_bwd_rows(int M, int K, int C);
 int pw_deep_bwd_slices(int M, int K, int C);
+int pw_deep_dgrad_plain(const float* dy, int M, int K, int C, const float* w, float* dx, hipStream_t st);
 
 int pw_deep_bwd_bnbwd(const float* g, const float* bn_x, int M, int K, int C, const float* om, const float* ois,
                       const float* og, const float* ob, int orelu, const float* k12, const float* w, float* dx,

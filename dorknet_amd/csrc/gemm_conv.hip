@@ -58,23 +58,6 @@ __global__ void w_phase_kernel(const float* __restrict__ w, int K, int C, int R,
 }  // namespace dk
 
 // Tuning knobs (knobs.hip): kind = the KnobId; cfg = -1 restores the default.
-DK_API int dk_stream_create_cu_mask(int every, void** stream) {
-  if (every < 1 || !stream) return DK_ERR_ARGS;
-  int dev = 0, ncu = 0;
-  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) !=
-                                               hipSuccess || ncu < 1 || ncu > 1024)
-    return DK_ERR_ARGS;
-  uint32_t mask[32] = {};
-  for (int i = 0; i < ncu; i += every) mask[i >> 5] |= 1u << (i & 31);
-  hipStream_t s = nullptr;
-  const hipError_t rc = hipExtStreamCreateWithCUMask(&s, (uint32_t)((ncu + 31) / 32), mask);
-  if (rc != hipSuccess) return (int)rc;
-  *stream = reinterpret_cast<void*>(s);
-  return 0;
-}
-
-DK_API int dk_stream_destroy(void* stream) { return (int)hipStreamDestroy(reinterpret_cast<hipStream_t>(stream)); }
-
 DK_API int dk_debug_set_gemm_config(int kind, int cfg) {
   // unused / retired numbers (knobs.hip) and the internal launch variant are refused
   if (kind < 0 || kind >= kNumKnobs || kind == 5 || kind == 6 || kind == 10 || kind == 12 || (kind >= 15 && kind <= 17) ||

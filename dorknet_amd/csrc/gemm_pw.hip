@@ -83,6 +83,9 @@ DK_API int dk_pwconv_dgrad_f32(const float* dy, int N, int OH, int OW, int K, co
   MatDesc b = mat(w_kc, K, C, C);
   const hipStream_t st = as_stream(stream);
   const bool vec = vec_ok(a, K, 4) && vec_ok(b, 4, C);
+  if (stride == 1 && vec && aligned16(dy) && aligned16(w_kc) && aligned16(dx) && pw_deep_dgrad_ok(K, C, M))
+    // the deep dgrad kernel's plain form (pw_deep.hip): bit-identical dx (the skip projections)
+    return pw_deep_dgrad_plain(dy, M, K, C, w_kc, dx, st);
   if (stride == 1) {
     EpStore ep = ep_store(dx, C, nullptr);
     if (vec) return igemm_rows<LdMatKC, MatDesc, LdMatIC, MatDesc, EpStore>(a, b, ep, M, C, K, st);

@@ -27,8 +27,7 @@ constexpr int kDefaults[kNumKnobs] = {
     1,           // kKnobPwsh: bf16 streaming pointwise kernels
     0,           // 10: unused
     1,           // kKnobPwDeep: fp32 weight-stationary deep pointwise kernels
-    0,           // 12: retired (round 6: 16 x 16 variants of the C = 512 forward and the deep weight gradient,
-                 //     measured slower in the step)
+    0,           // 12: retired (deep pointwise walkers per resident slot: more than one round was slower)
     1,           // kKnobPwDeep16: bf16 weight-stationary deep pointwise kernels
     1,           // kKnobPwDeepBwd: fused deep pointwise backward (dgrad + wgrad)
     0,           // 15-17: retired (K = C = 128 streaming-forward switch; tiled fused backward prefetch and

@@ -105,8 +105,6 @@ __device__ __forceinline__ void mfma_tile(const float* ap, const f32x4* bw, f32x
 // instruction, bit-identical to the scalar form): the forward's staging transform is its main VALU
 // work, and f32 VALU does not overlap the MFMAs (the dgrad's per-element form packs as well left to
 // the compiler; written this way it took more registers).
-__device__ __forceinline__ f32x2 lo2(f32x4 v) { return f32x2{v[0], v[1]}; }
-__device__ __forceinline__ f32x2 hi2(f32x4 v) { return f32x2{v[2], v[3]}; }
 __device__ __forceinline__ f32x4 cat4(f32x2 a, f32x2 b) { return f32x4{a[0], a[1], b[0], b[1]}; }
 // (x - mean) * invstd
 __device__ __forceinline__ f32x4 xhat4(f32x4 x, f32x4 m, f32x4 i) {
@@ -310,7 +308,9 @@ struct DgradArgs {
   int nt;             // nontemporal dy / dx stores (nt_stores(kNtPwd))
 };
 
-template <int KR, bool RES, bool PART>
+// PLAIN: the gradient is given as is (g = dy; no following BatchNorm: the skip projections' dgrad,
+// dk_pwconv_dgrad_f32 at stride 1 into the compact lattice) -- no xo loads, no transform, no write-through.
+template <int KR, bool RES, bool PART, bool PLAIN = false>
 __global__ __launch_bounds__(NT, dgrad_wps<KR>()) void dgrad_kernel(DgradArgs a) {
   constexpr int SK = KR + 4, KV = KR / 4, LV = TR * KV / NT, KQ = KR / 8;
   static_assert(KR % 32 == 0 && (SK / 4) % 2 == 1 && NT % KV == 0, "pwd::dgrad_kernel shape");
@@ -322,11 +322,13 @@ __global__ __launch_bounds__(NT, dgrad_wps<KR>()) void dgrad_kernel(DgradArgs a)
   const int n0 = blockIdx.y * NB, N = a.N;
   const int col = n0 + 32 * wave + l32;
   const int kv = tid % KV, r0 = tid / KV;
-  const f32x4 mu = ld4(a.om + 4 * kv), is = ld4(a.ois + 4 * kv), ga = ld4(a.og + 4 * kv), be = ld4(a.ob + 4 * kv);
-  const f32x4 k1 = ld4(a.k12 + 4 * kv), k2 = ld4(a.k12 + KR + 4 * kv);
-  f32x4 f;
+  f32x4 mu = {}, is = {}, ga = {}, be = {}, k1 = {}, k2 = {}, f = {};
+  if constexpr (!PLAIN) {
+    mu = ld4(a.om + 4 * kv), is = ld4(a.ois + 4 * kv), ga = ld4(a.og + 4 * kv), be = ld4(a.ob + 4 * kv);
+    k1 = ld4(a.k12 + 4 * kv), k2 = ld4(a.k12 + KR + 4 * kv);
 #pragma unroll
-  for (int e = 0; e < 4; ++e) f[e] = ga[e] * is[e];
+    for (int e = 0; e < 4; ++e) f[e] = ga[e] * is[e];
+  }
   const float pm = PART ? a.im[col] : 0.f, pis = PART ? a.iis[col] : 0.f, pga = PART ? a.ig[col] : 0.f,
               pbe = PART ? a.ib[col] : 0.f;
   const bool orelu = a.orelu != 0, irelu = a.irelu != 0;
@@ -346,7 +348,8 @@ __global__ __launch_bounds__(NT, dgrad_wps<KR>()) void dgrad_kernel(DgradArgs a)
 #pragma unroll
     for (int j = 0; j < LV; ++j) {
       sg[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rg, (int)lofs[j], 0, 0));
-      sx[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rx, (int)lofs[j], 0, 0));
+      if constexpr (!PLAIN)
+        sx[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rx, (int)lofs[j], 0, 0));
     }
   };
   auto stage = [&](int tile, float* dst, const f32x4* sg, const f32x4* sx) {
@@ -354,7 +357,8 @@ __global__ __launch_bounds__(NT, dgrad_wps<KR>()) void dgrad_kernel(DgradArgs a)
 #pragma unroll
     for (int j = 0; j < LV; ++j) {
       const int r = r0 + j * (NT / KV);
-      f32x4 v;
+      f32x4 v = sg[j];
+      if constexpr (!PLAIN)
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const float xe = sx[j][e];
@@ -364,7 +368,7 @@ __global__ __launch_bounds__(NT, dgrad_wps<KR>()) void dgrad_kernel(DgradArgs a)
         v[e] = (DK_PWD_EXP & 2) ? ge + xe : bn_bwd_elem(xe, ge, mu[e], is[e], f[e], k1[e], k2[e]);
       }
       st4(dst + r * SK + 4 * kv, v);
-      bstore_nt(__builtin_bit_cast(u32x4, v), rdy, (int)lofs[j], 0, a.nt);
+      if constexpr (!PLAIN) bstore_nt(__builtin_bit_cast(u32x4, v), rdy, (int)lofs[j], 0, a.nt);
     }
   };
 
@@ -482,7 +486,7 @@ __device__ __forceinline__ void mfma16_tile(const float* ap, const f32x4* bw, f3
   }
 }
 
-template <int KR, bool RES, bool PART>
+template <int KR, bool RES, bool PART, bool PLAIN = false>
 __global__ __launch_bounds__(NT16, 2) void dgrad16_kernel(DgradArgs a) {
   using L = K16<KR>;
   constexpr int SK = L::SK, RS = L::RS, KV = L::KV, LV = L::LV, NQ = L::NQ;
@@ -502,7 +506,7 @@ __global__ __launch_bounds__(NT16, 2) void dgrad16_kernel(DgradArgs a) {
   // cover the stretch's 1 KB
   const int kvl = tid % KV, r0 = tid / KV;
   const int kv = (kvl & ~63) | ((kvl & 31) << 1) | ((kvl >> 5) & 1);
-  if (tid < KV) {
+  if (!PLAIN && tid < KV) {
     const f32x4 ga = ld4(a.og + 4 * tid), is = ld4(a.ois + 4 * tid);
     bnt[0][tid] = ld4(a.om + 4 * tid);
     bnt[1][tid] = is;
@@ -538,29 +542,32 @@ __global__ __launch_bounds__(NT16, 2) void dgrad16_kernel(DgradArgs a) {
 #pragma unroll
     for (int j = 0; j < LV; ++j) {
       sg[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rg, (int)lofs[j], 0, 0));
-      sx[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rx, (int)lofs[j], 0, 0));
+      if constexpr (!PLAIN)
+        sx[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rx, (int)lofs[j], 0, 0));
     }
   };
   auto stage = [&](int tile, float* dst, const f32x4* sg, const f32x4* sx) {
     const __amdgpu_buffer_rsrc_t rdy = tile_rsrc16(writer ? a.dy_out : a.g, KR, tile, writer ? a.M : 0);
-    const f32x4 mu = bnt[0][kv], is = bnt[1][kv], ga = bnt[2][kv], be = bnt[3][kv], k1 = bnt[4][kv], k2 = bnt[5][kv],
-                f = bnt[6][kv];
 #pragma unroll
     for (int j = 0; j < LV; ++j) {
       const int r = r0 + j * (NT16 / KV);
-      f32x4 v;
+      f32x4 v = sg[j];
+      if constexpr (!PLAIN) {
+        const f32x4 mu = bnt[0][kv], is = bnt[1][kv], ga = bnt[2][kv], be = bnt[3][kv], k1 = bnt[4][kv],
+                    k2 = bnt[5][kv], f = bnt[6][kv];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float xe = sx[j][e];
-        float ge = sg[j][e];
-        const bool kill = (!(bn_out(xe, mu[e], is[e], ga[e], be[e]) > 0.f)) & orelu;
-        ge = kill ? 0.f : ge;
-        v[e] = bn_bwd_elem(xe, ge, mu[e], is[e], f[e], k1[e], k2[e]);
+        for (int e = 0; e < 4; ++e) {
+          const float xe = sx[j][e];
+          float ge = sg[j][e];
+          const bool kill = (!(bn_out(xe, mu[e], is[e], ga[e], be[e]) > 0.f)) & orelu;
+          ge = kill ? 0.f : ge;
+          v[e] = bn_bwd_elem(xe, ge, mu[e], is[e], f[e], k1[e], k2[e]);
+        }
       }
       float* d = dst + r * SK + sreg;
       *reinterpret_cast<f32x2*>(d) = f32x2{v[0], v[2]};
       *reinterpret_cast<f32x2*>(d + 2 * RS) = f32x2{v[1], v[3]};
-      bstore_nt(__builtin_bit_cast(u32x4, v), rdy, (int)lofs[j], 0, a.nt);
+      if constexpr (!PLAIN) bstore_nt(__builtin_bit_cast(u32x4, v), rdy, (int)lofs[j], 0, a.nt);
     }
   };
 
@@ -1306,6 +1313,29 @@ int pw_deep_dgrad_bnbwd(const float* g, const float* bn_x, int M, int K, int C, 
   DK_PWD_KR_DGRAD(DK_DG)
 #undef DK_DG
 #undef DK_L
+  return DK_ERR_ARGS;
+}
+
+// The plain deep dgrad (PLAIN: dy given, no BatchNorm around it): dx[M][C] = dy . W, bit-identical to the
+// tiled engine's (same MFMA k order).  The downsampling blocks' skip projections at stride 1 into the
+// compact lattice.
+int pw_deep_dgrad_plain(const float* dy, int M, int K, int C, const float* w, float* dx, hipStream_t st) {
+  pwd::DgradArgs a{dy, nullptr, nullptr, w, dx, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0,
+                   nullptr, nullptr, nullptr, nullptr, 0, nullptr, M, C};
+  a.nt = nt_stores(kNtPwd);
+  const dim3 grid(pw_deep_dgrad_rows(M, K, C), C / pwd::NB);
+  if (grid.x == 0) return DK_ERR_ARGS;
+  if (pwd_dgrad16(K)) {
+    hipLaunchKernelGGL((pwd::dgrad16_kernel<512, false, false, true>), grid, dim3(pwd::NT16), 0, st, a);
+    return launch_status();
+  }
+#define DK_DG(kr)                                                                                           \
+  if (K == kr) {                                                                                            \
+    hipLaunchKernelGGL((pwd::dgrad_kernel<kr, false, false, true>), grid, dim3(pwd::NT), 0, st, a);         \
+    return launch_status();                                                                                 \
+  }
+  DK_PWD_KR_DGRAD(DK_DG)
+#undef DK_DG
   return DK_ERR_ARGS;
 }
 

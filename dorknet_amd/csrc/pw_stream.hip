@@ -738,18 +738,24 @@ __global__ __launch_bounds__(256, PF ? 1 : 2) void bwd_fused_kernel(BwdArgs ba) 
       const f32x4 mu = ld4(tb + 0 * KR + k0), is = ld4(tb + 1 * KR + k0), ga = ld4(tb + 2 * KR + k0),
                   be = ld4(tb + 3 * KR + k0);
       const f32x4 k1 = ld4(tb + 4 * KR + k0), k2 = ld4(tb + 5 * KR + k0), f = ld4(tb + 6 * KR + k0);
+      // in packed fp32 (v_pk_*: per element the IEEE operations of bn_out / bn_bwd_elem, bit-identical):
+      // this transform is a third of the kernel's VALU work, and f32 VALU does not overlap the MFMAs
 #pragma unroll
       for (int q = 0; q < KQ; ++q) {
-        f32x4 o;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const float xe = cx[q][e];
-          float ge = cg[q][e];
-          const bool kill = (!(bn_out(xe, mu[e], is[e], ga[e], be[e]) > 0.f)) & orelu;
-          ge = kill ? 0.f : ge;
-          o[e] = bn_bwd_elem(xe, ge, mu[e], is[e], f[e], k1[e], k2[e]);
+        const f32x4 xv = cx[q];
+        f32x4 gv = cg[q];
+        const f32x2 xh0 = (lo2(xv) - lo2(mu)) * lo2(is), xh1 = (hi2(xv) - hi2(mu)) * hi2(is);
+        if (orelu) {
+          const f32x2 b0 = __builtin_elementwise_fma(lo2(ga), xh0, lo2(be)),
+                      b1 = __builtin_elementwise_fma(hi2(ga), xh1, hi2(be));
+          gv[0] = b0[0] > 0.f ? gv[0] : 0.f;
+          gv[1] = b0[1] > 0.f ? gv[1] : 0.f;
+          gv[2] = b1[0] > 0.f ? gv[2] : 0.f;
+          gv[3] = b1[1] > 0.f ? gv[3] : 0.f;
         }
-        st4(td + (pr + 4 * q) * SKD + k0, o);
+        const f32x2 o0 = lo2(f) * __builtin_elementwise_fma(-xh0, lo2(k2), lo2(gv) - lo2(k1));
+        const f32x2 o1 = hi2(f) * __builtin_elementwise_fma(-xh1, hi2(k2), hi2(gv) - hi2(k1));
+        st4(td + (pr + 4 * q) * SKD + k0, f32x4{o0[0], o0[1], o1[0], o1[1]});
       }
     }
     f32x4 af[KQ];
@@ -785,13 +791,17 @@ __global__ __launch_bounds__(256, PF ? 1 : 2) void bwd_fused_kernel(BwdArgs ba) 
     for (int r = 0; r < 16; ++r) {
       const int dm = (r & 3) + 8 * (r >> 2);
       const bool in = mb + dm < a.M;
-      float bx[2];
+      // the input BN's x_hat and output of the pixel, computed once: the weight gradient's operand uses
+      // them and so do the partials (PART implies BNIN, and the entry points pass the one BatchNorm for
+      // both -- pw_stream_bwd_fused checks), in bn_out's exact form (bit-identical)
+      float bx[2], bxh[2], bo[2];
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
         float v = exi[u][r];
         if constexpr (BNIN) {
-          const float o = bn_out(v, qm[u], qis[u], qga[u], qbe[u]);
-          v = (brelu & !(o > 0.f)) ? 0.f : o;
+          bxh[u] = (v - qm[u]) * qis[u];
+          bo[u] = qga[u] * bxh[u] + qbe[u];  // = bn_out(v, qm, qis, qga, qbe)
+          v = (brelu & !(bo[u] > 0.f)) ? 0.f : bo[u];
         }
         bx[u] = in ? v : 0.f;
       }
@@ -816,9 +826,8 @@ __global__ __launch_bounds__(256, PF ? 1 : 2) void bwd_fused_kernel(BwdArgs ba) 
           __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), rdx, (int)((r < 8 ? eb0 : eb1) + imm),
                                                 0, 0);
         if constexpr (PART) {
-          const float x = exi[u][r];
-          const float xh = (x - pm[u]) * pis[u];
-          const bool kill = ((!(bn_out(x, pm[u], pis[u], pga[u], pbe[u]) > 0.f)) & irelu) | (mb + dm >= a.M);
+          const float xh = bxh[u];
+          const bool kill = ((!(bo[u] > 0.f)) & irelu) | (mb + dm >= a.M);
           const float gv = kill ? 0.f : v;
           ps[u] += (double)gv;
           pq[u] += (double)gv * (double)xh;
@@ -949,6 +958,8 @@ int pw_stream_bwd_fused(const float* g, const float* bn_x, int M, const float* o
   const dim3 grid(pws::bwd_fused_blocks(M));
   const bool r = res != nullptr, pt = part != nullptr, bn = bm != nullptr;
   if (pt && !bn) return DK_ERR_ARGS;
+  // the partials' BatchNorm is the weight-gradient operand's (the kernel computes its terms once)
+  if (pt && (im != bm || iis != bis || ig != bgm || ib != bbt || (irelu != 0) != (brelu != 0))) return DK_ERR_ARGS;
   if (lattice) {  // (the lattice form keeps the prefetch: without it it spills at 2 waves per SIMD)
     if (pt)
       hipLaunchKernelGGL((pws::bwd_fused_kernel<false, true, true, true, true>), grid, dim3(256), 0, st, a);

@@ -69,11 +69,6 @@ int dk_mixup_f32(const float* a, const float* b, long long n, float p, float one
  * kind 21: output columns per thread of the fused stride-1 depthwise backward (2 = default where the
  * width allows, 1 = one); the dk_dwconv_bwd_bnbwd*_stats_rows / _workspace_bytes follow it. */
 int dk_debug_set_gemm_config(int kind, int cfg);
-/* A HIP stream confined to every `every`-th compute unit of the device (hipExtStreamCreateWithCUMask;
- * every = 1: all of them), for background work beside the critical path; *stream receives the
- * hipStream_t.  dk_stream_destroy releases it. */
-int dk_stream_create_cu_mask(int every, void** stream);
-int dk_stream_destroy(void* stream);
 
 /* Bandwidth ceiling probe (not on the training path; scripts/stream_ceiling.py): reads nin
  * (1..3) fp32 arrays a, b, c and writes nout (0..2) arrays o0, o1 of numel elements each, 16

@@ -1,7 +1,8 @@
 """The fused stride-1 depthwise backward (dk_dwconv_bwd_bnbwd_bf16 / _f32) at the depthwise-separable
 stack's shapes: median of 15 calls (HIP events on the launch stream), HBM bytes per call (g, the BN
 input, x read; dx written) and TB/s, per columns-per-thread setting (knob 21) for bf16.
-    python scripts/dwb_bench.py [--batch 512] [--f32] [--hw 56]
+    python scripts/dwb_bench.py [--batch 512] [--f32] [--hw 56] [--blocks 768,256,1536]
+(--blocks: the fused backward's block target, knob 7, swept per shape)
 """
 import os
 import sys
@@ -47,8 +48,10 @@ def main():
         w = torch.randn(C * 9, device="cuda") * 0.3
         dw = torch.empty(C * 9, device="cuda")
         line = f"{B}x{HW}x{HW}x{C} {'f32' if f32 else 'bf16'}:"
-        for cols, nt in ([(1, 256), (2, 256)]):
+        blocks = [int(v) for v in sys.argv[sys.argv.index("--blocks") + 1].split(",")] if "--blocks" in sys.argv else [-1]
+        for cols, nt, bt in [(c, 256, b) for c in (1, 2) for b in blocks]:
             lib.dk_debug_set_gemm_config(21, cols)
+            lib.dk_debug_set_gemm_config(7, bt)
             rows_fn = lib.dk_dwconv_bwd_bnbwd_stats_rows if f32 else lib.dk_dwconv_bwd_bnbwd_bf16_stats_rows
             ws_fn = lib.dk_dwconv_bwd_bnbwd_workspace_bytes if f32 else lib.dk_dwconv_bwd_bnbwd_bf16_workspace_bytes
             rows = rows_fn(B, HW, HW, C)
@@ -63,8 +66,9 @@ def main():
                    *(t.data_ptr() for t in p), 1, part.data_ptr(), ws.data_ptr(), nb, stream_handle())
             t = timeit(call)
             byt = 4 * n * esz
-            line += f"  cols {cols}: {t:7.1f} us {byt / t / 1e6:5.2f} TB/s ({rows} strips)"
+            line += f"  cols {cols}{'' if bt < 0 else ' blk %d' % bt}: {t:7.1f} us {byt / t / 1e6:5.2f} TB/s ({rows} strips)"
         lib.dk_debug_set_gemm_config(21, -1)
+        lib.dk_debug_set_gemm_config(7, -1)
         print(line, flush=True)
 
 

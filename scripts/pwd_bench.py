@@ -46,9 +46,8 @@ def main():
     if "--shape" in sys.argv:
         shapes = [tuple(int(v) for v in sys.argv[sys.argv.index("--shape") + 1].split(","))]
     fold = "--fold" in sys.argv
-    # 0: the tiled engine; 1: the deep kernels; 2: the deep kernels with knob 12 (the 16 x 16 layout
-    # at the smaller reductions too)
-    modes = (0, 1, 2)
+    # 0: the tiled engine; 1: the deep kernels
+    modes = (0, 1)
     if "--modes" in sys.argv:
         modes = tuple(int(v) for v in sys.argv[sys.argv.index("--modes") + 1].split(","))
     torch.manual_seed(0)
@@ -64,7 +63,6 @@ def main():
         for deep in modes:
             lib.dk_debug_set_gemm_config(11, 1 if deep else 0)
             lib.dk_debug_set_gemm_config(14, 1 if deep else 0)
-            lib.dk_debug_set_gemm_config(12, 1 if deep == 2 else 0)
             y = torch.full((M * K,), float("nan"), device="cuda")
             dy = torch.full((M * K,), float("nan"), device="cuda")
             dx = torch.full((M * C,), float("nan"), device="cuda")
@@ -119,8 +117,8 @@ def main():
                 line.append(f"fused bwd {tb:6.1f} us {2 * flops / tb / 1e6 / PEAK:4.2f}")
             torch.cuda.synchronize()
             outs[deep] = (y.clone(), dy.clone(), dx.clone())
-            res.append(("old  ", "deep ", "d16  ")[deep] + ", ".join(line))
-        for k in (11, 12, 14):
+            res.append(("old  ", "deep ")[deep] + ", ".join(line))
+        for k in (11, 14):
             lib.dk_debug_set_gemm_config(k, -1)
         same = []
         ms = sorted(outs)

@@ -6,11 +6,12 @@
 #   bench     config 3 bench line                  bench5 / bench2   the config 5 / 2 lines
 #   prof      rocprofv3 kernel stats of config 3   suite  the whole -m gpu suite
 #   sq        SQ counter passes of config 3 (scripts/sq_passes.sh)
-#   ab        config-3 bench lines alternating the knob settings in $AB (e.g. AB="12=1 12=0"), 2 rounds
-#   prof0     as prof with the knob settings in $KNOBS (e.g. KNOBS="--knob 12=0")
+#   file      the test file(s) in $TESTFILE
+#   ab        config-3 bench lines alternating the knob settings in $AB (e.g. AB="21=2 21=1"), 2 rounds
+#   prof0     as prof with the knob settings in $KNOBS (e.g. KNOBS="--knob 21=1")
 #   abenv     config-3 bench lines alternating the environment settings in $ABENV (e.g. ABENV="A=0 A=1")
 set -u
-AB=${AB:-}; KNOBS=${KNOBS:-}; ABENV=${ABENV:-}
+AB=${AB:-}; KNOBS=${KNOBS:-}; ABENV=${ABENV:-}; TESTFILE=${TESTFILE:-}
 TAG=$1; shift
 ROOT=$(pwd); OUT=$ROOT/gpurun_out; mkdir -p "$OUT"
 step() { echo "== $1 rc=$2"; if [ "$2" -ne 0 ]; then echo "stopping after rc=$2"; exit "$2"; fi; }
@@ -21,7 +22,7 @@ for s in "$@"; do
           rc=$?; tail -2 "$OUT/tests_${TAG}_deep.log"; step deep $rc;;
     net) timeout -k 10 600 $PYT -v -s tests/test_gpu_network.py -k training_steps > "$OUT/tests_${TAG}_net.log" 2>&1
           rc=$?; tail -2 "$OUT/tests_${TAG}_net.log"; step net $rc;;
-    pwdbench) timeout -k 10 300 python -u scripts/pwd_bench.py --only ${PWD_ONLY:-dgrad} --modes ${PWD_MODES:-0,1,2} > "$OUT/pwd_bench_${TAG}.txt" 2>&1
+    pwdbench) timeout -k 10 300 python -u scripts/pwd_bench.py --only ${PWD_ONLY:-dgrad} --modes ${PWD_MODES:-0,1} > "$OUT/pwd_bench_${TAG}.txt" 2>&1
           rc=$?; cat "$OUT/pwd_bench_${TAG}.txt"; step pwdbench $rc;;
     smoke) timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke_${TAG}.log" 2>&1
           rc=$?; tail -1 "$OUT/smoke_${TAG}.log"; step smoke $rc;;
@@ -49,6 +50,8 @@ for s in "$@"; do
         done; done;;
     sq) bash scripts/sq_passes.sh "$TAG" > "$OUT/sq_$TAG.log" 2>&1; rc=$?; tail -3 "$OUT/sq_$TAG.log"; step sq $rc
           python scripts/sq_ratios.py "$OUT/pmc_$TAG" --top 30 > "$OUT/sq_ratios_$TAG.md"; head -32 "$OUT/sq_ratios_$TAG.md";;
+    file) timeout -k 10 300 $PYT $TESTFILE > "$OUT/tests_${TAG}_file.log" 2>&1
+          rc=$?; tail -2 "$OUT/tests_${TAG}_file.log"; step file $rc;;
     suite) timeout -k 10 900 $PYT tests -m gpu > "$OUT/tests_${TAG}.log" 2>&1
           rc=$?; tail -2 "$OUT/tests_${TAG}.log"; step suite $rc;;
     *) echo "unknown step $s"; exit 2;;

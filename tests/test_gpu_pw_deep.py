@@ -345,3 +345,27 @@ def test_deep_fused_bwd_deterministic_and_in_bounds():
         outs.append((dxbuf.clone(), dw.clone(), part.clone()))
     assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
     assert torch.equal(outs[0][2], outs[1][2])
+
+
+@pytest.mark.parametrize("K,C,N,H,W", [(256, 128, 3, 14, 14), (512, 256, 5, 7, 7), (128, 128, 2, 9, 13),
+                                       (512, 512, 1, 3, 5)])
+def test_deep_plain_dgrad_matches_tiled_engine(K, C, N, H, W):
+    """dk_pwconv_dgrad_f32 at stride 1 (the skip projections' input gradient into the compact lattice) on
+    the deep dgrad kernels' plain form (no BatchNorm around dy) against the tiled engine: dx bitwise (the
+    same MFMA k order), ragged pixel counts, nothing written past dx."""
+    rng = np.random.RandomState(K + C + N + H)
+    M = N * H * W
+    dy = nhwc(rng.randn(N, K, H, W))
+    w = torch.as_tensor((rng.randn(K, C) / np.sqrt(K)).astype(np.float32), device="cuda")
+    st = stream_handle()
+
+    def run():
+        buf = torch.full((M * C + 64,), 12345.0, device="cuda")
+        assert lib.dk_pwconv_dgrad_f32(dy.data_ptr(), N, H, W, K, w.data_ptr(), C, 1, buf.data_ptr(), st) == 0
+        torch.cuda.synchronize()
+        assert bool((buf[M * C:] == 12345.0).all())
+        return buf[:M * C].clone()
+    d0, d1 = _modes(run)
+    assert torch.equal(d0, d1)
+    ref = dy.permute(0, 2, 3, 1).reshape(M, K).double() @ w.double()
+    assert float((d1.double().reshape(M, C) - ref).norm() / ref.norm()) < 1e-5
