@@ -172,7 +172,10 @@ struct JoinFwd {
 };
 
 template <int R, int S, int ST, bool BN, bool RELU, int STATS, int WL, class T = float, bool JOIN = false>
-__global__ __launch_bounds__(256, JOIN ? 2 : 1) void dw_fwd_kernel(const T* __restrict__ x, uint32_t xbytes,
+// (the stride-2 join at 2 waves per SIMD spilled VGPRs to scratch, and one build of it -- the
+// statistics table laid out differently -- dropped y stores of partially out-of-image column chunks;
+// at 1 wave per SIMD it takes AGPRs instead and no scratch.  Config 3 does not run it.)
+__global__ __launch_bounds__(256, (JOIN && ST == 1) ? 2 : 1) void dw_fwd_kernel(const T* __restrict__ x, uint32_t xbytes,
                                                      const float* __restrict__ wt, const float* __restrict__ bias,
                                                      T* __restrict__ y, int N, int H, int W, int C, int OH, int OW,
                                                      int pad, BnIn bn, double* __restrict__ part,
@@ -450,9 +453,7 @@ __global__ __launch_bounds__(256, JOIN ? 2 : 1) void dw_fwd_kernel(const T* __re
   }
   if constexpr (STATS != 0) {
     // fixed-order block reduction over the 256 / C4 threads of each channel group
-    // (not padded like the other kernels' tables: [256][9] here left the stride-2 join variant -- 256
-    // VGPRs with spills -- without some of its y stores, tests/test_gpu_join_fwd.py; its time did not
-    // change with the padding)
+    // (not padded like the other kernels' tables: the padding did not change this kernel's time)
     __shared__ double red[256][8];
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
