@@ -452,11 +452,12 @@ __global__ __launch_bounds__(256, KR_ == 64 ? 3 : 2) void fwd_kernel(FwdArgs a) 
 
     const int mb = m0 + 4 * h;
     const uint32_t eb0 = row_off_bytes(mb, NO, l32), eb1 = eb0 + 16u * NO * 4u;
+    if (a.bias) {
 #pragma unroll
-    for (int u = 0; u < NU; ++u)
+      for (int u = 0; u < NU; ++u)
 #pragma unroll
-      for (int r = 0; r < 16; ++r)
-        if (a.bias) acc[u][r] += bias[u];
+        for (int r = 0; r < 16; ++r) acc[u][r] += bias[u];
+    }
     // one branch around all the stores (the cache policy is an immediate): chosen per store, the
     // branches hid the number of stores in flight from the wait-count pass, and the next tile waited
     // for all of them (vmcnt(0)) before its loads were used
@@ -481,7 +482,11 @@ __global__ __launch_bounds__(256, KR_ == 64 ? 3 : 2) void fwd_kernel(FwdArgs a) 
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int dm = (r & 3) + 8 * (r >> 2);
-          const double d = (mb + dm < a.M) ? (double)acc[u][r] : 0.0;
+          // (the past-M select in fp32, kept ahead of the widening: sunk past it, it became two
+          // selects on the fp64 halves)
+          float v = (mb + dm < a.M) ? acc[u][r] : 0.f;
+          asm volatile("" : "+v"(v));
+          const double d = (double)v;
           ps[u] += d;
           pq[u] += d * d;
         }
@@ -651,6 +656,7 @@ __global__ __launch_bounds__(256, PF ? 1 : 2) void bwd_fused_kernel(BwdArgs ba) 
     qga[u] = BNIN ? ba.bg[c] : 0.f;
     qbe[u] = BNIN ? ba.bb[c] : 0.f;
   }
+  const f32x2 qm2 = {qm[0], qm[1]}, qis2 = {qis[0], qis[1]}, qga2 = {qga[0], qga[1]}, qbe2 = {qbe[0], qbe[1]};
   __syncthreads();
 
   const uint32_t kbytes = (uint32_t)a.M * KR * 4u, nbytes = (uint32_t)a.M * NO * 4u;
@@ -793,16 +799,20 @@ __global__ __launch_bounds__(256, PF ? 1 : 2) void bwd_fused_kernel(BwdArgs ba) 
       const bool in = mb + dm < a.M;
       // the input BN's x_hat and output of the pixel, computed once: the weight gradient's operand uses
       // them and so do the partials (PART implies BNIN, and the entry points pass the one BatchNorm for
-      // both -- pw_stream_bwd_fused checks), in bn_out's exact form (bit-identical)
+      // both -- pw_stream_bwd_fused checks), in bn_out's exact form (bit-identical), the two columns
+      // in packed fp32
       float bx[2], bxh[2], bo[2];
+      f32x2 bxh2 = {0.f, 0.f}, bo2 = {0.f, 0.f};
+      if constexpr (BNIN) {
+        bxh2 = (f32x2{exi[0][r], exi[1][r]} - qm2) * qis2;
+        bo2 = __builtin_elementwise_fma(qga2, bxh2, qbe2);  // = bn_out(v, qm, qis, qga, qbe)
+      }
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
         float v = exi[u][r];
-        if constexpr (BNIN) {
-          bxh[u] = (v - qm[u]) * qis[u];
-          bo[u] = qga[u] * bxh[u] + qbe[u];  // = bn_out(v, qm, qis, qga, qbe)
-          v = (brelu & !(bo[u] > 0.f)) ? 0.f : bo[u];
-        }
+        bxh[u] = bxh2[u];
+        bo[u] = bo2[u];
+        if constexpr (BNIN) v = (brelu & !(bo[u] > 0.f)) ? 0.f : bo[u];
         bx[u] = in ? v : 0.f;
       }
       const float a0 = td[(dm + 4 * h) * SKD + l32], a1 = td[(dm + 4 * h) * SKD + 32 + l32];
@@ -827,8 +837,11 @@ __global__ __launch_bounds__(256, PF ? 1 : 2) void bwd_fused_kernel(BwdArgs ba) 
                                                 0, 0);
         if constexpr (PART) {
           const float xh = bxh[u];
-          const bool kill = ((!(bo[u] > 0.f)) & irelu) | (mb + dm >= a.M);
-          const float gv = kill ? 0.f : v;
+          // the ReLU / past-M kill as fp32 selects, kept ahead of the widening (the compiler sank the
+          // select past it: a 0/1 mask built in VGPRs, then two selects on the fp64 halves)
+          float gv = (irelu && !(bo[u] > 0.f)) ? 0.f : v;
+          gv = in ? gv : 0.f;
+          asm volatile("" : "+v"(gv));
           ps[u] += (double)gv;
           pq[u] += (double)gv * (double)xh;
         }
@@ -836,7 +849,10 @@ __global__ __launch_bounds__(256, PF ? 1 : 2) void bwd_fused_kernel(BwdArgs ba) 
     }
     };
     if constexpr (!PF)
-      epi(std::integral_constant<int, -1>{});  // (hoisted, the branch cost this variant 512 bytes of spills)
+      // nontemporal dx stores always (the default, kNtPwsBwd): a run-time choice per store put a branch
+      // around each of the tile's 32 stores, and hoisted around the epilogue it cost this variant 512
+      // bytes of spills
+      epi(std::integral_constant<int, 2>{});
     else if (a.nt)
       epi(std::integral_constant<int, 2>{});
     else
