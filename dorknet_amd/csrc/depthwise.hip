@@ -122,9 +122,11 @@ __device__ __forceinline__ void load_row(f32x4 (&row)[NC], __amdgpu_buffer_rsrc_
 }
 
 // Outputs per thread along W: the input strip R x ((TW-1)*ST + S) float4s is loaded at once.
+// Stride 2 takes two: its window (R x 5 float4s, two rows of it new each output row) then leaves
+// the join-forming variant two waves per SIMD (with four outputs, R x 9, it ran at one).
 template <int ST>
 struct DwTile {
-  static constexpr int TW = 4;    // outputs per thread along W
+  static constexpr int TW = ST == 2 ? 2 : 4;    // outputs per thread along W
 };
 
 // Output rows per thread (the input window slides down a segment of them).  Round 3 measured 8
@@ -172,10 +174,7 @@ struct JoinFwd {
 };
 
 template <int R, int S, int ST, bool BN, bool RELU, int STATS, int WL, class T = float, bool JOIN = false>
-// (the stride-2 join at 2 waves per SIMD spilled VGPRs to scratch, and one build of it -- the
-// statistics table laid out differently -- dropped y stores of partially out-of-image column chunks;
-// at 1 wave per SIMD it takes AGPRs instead and no scratch.  Config 3 does not run it.)
-__global__ __launch_bounds__(256, (JOIN && ST == 1) ? 2 : 1) void dw_fwd_kernel(const T* __restrict__ x, uint32_t xbytes,
+__global__ __launch_bounds__(256, JOIN ? 2 : 1) void dw_fwd_kernel(const T* __restrict__ x, uint32_t xbytes,
                                                      const float* __restrict__ wt, const float* __restrict__ bias,
                                                      T* __restrict__ y, int N, int H, int W, int C, int OH, int OW,
                                                      int pad, BnIn bn, double* __restrict__ part,
@@ -375,7 +374,24 @@ __global__ __launch_bounds__(256, (JOIN && ST == 1) ? 2 : 1) void dw_fwd_kernel(
             }
             load_pre((oh + 1) * ST - pad + R - 1, oh + 1 < oh1);
           } else if constexpr (JOIN) {
-            join_load(win[slot], oh * ST - pad + r);
+            // (stride 2: both entering rows' operands are loaded before either is joined, below)
+            if (r == R - ST) {
+              f32x4 ra[ST][NC], rb[ST][NC];
+#pragma unroll
+              for (int k = 0; k < ST; ++k) {
+                const int ih = oh * ST - pad + r + k;
+                const bool rv = (unsigned)ih < (unsigned)H;
+#pragma unroll
+                for (int q = 0; q < NC; ++q) {
+                  const bool ok = rv && (unsigned)(iw0 + q) < (unsigned)W;
+                  const uint32_t e = (uint32_t)(((n * H + ih) * W + iw0 + q) * C + c);
+                  ra[k][q] = bload4e<float>(rs, ok, e);
+                  rb[k][q] = bload4e<float>(rjb, ok, e);
+                }
+              }
+#pragma unroll
+              for (int k = 0; k < ST; ++k) join_row(win[r + k], ra[k], rb[k], oh * ST - pad + r + k);
+            }
           } else {
             load_row<NC, BN, RELU, T>(win[slot], rs, n, oh * ST - pad + r, iw0, H, W, C, c, bm, bi, bg, bb);
           }

@@ -179,8 +179,9 @@ class DepthwiseConvLayer(Layer):
                 and jb.x.dtype == torch.float32 and jb.x.is_contiguous(memory_format=torch.channels_last)):
             return False
         if mask is None:
-            # a join that left no mask (JoinOut): only the stride-1 form, which takes it as x > 0
-            return (self.stride == 1 and getattr(join, "_join_y", None) is not None
+            # a join that left no mask (JoinOut): the fused backwards take it as x > 0 (x is the
+            # join's output); the plain join dgrad rebuilds it (ReLu._mask_from_join)
+            return (getattr(join, "_join_y", None) is not None
                     and getattr(join, "_join_y_ptr", None) == x.data_ptr())
         return tuple(mask.shape) == tuple(x.shape) and mask.is_contiguous(memory_format=torch.channels_last)
 
@@ -422,6 +423,8 @@ class DepthwiseConvLayer(Layer):
         if jrows:
             # the input's residual join: its ReLU backward and its BatchNorm's stage 1 on the store
             jb = join._join_bn
+            if join._mask is None:
+                join._mask_from_join()
             part = torch.empty((jrows, 2, C), dtype=torch.float64, device=dx.device)
             tok = jb.arm_partials(part)
             r = lib.dk_dwconv_dgrad_join_f32(dy.data_ptr(), N, OH, OW, C, w.data_ptr(), R, S, self.stride,

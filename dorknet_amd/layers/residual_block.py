@@ -15,7 +15,7 @@ from .._env import enabled, getenv
 from .._hip import branch_stream_enabled, lib, on_branch, resolve, stream_handle
 from .._tensor import empty_nhwc, to_nhwc
 from ._bn_input import JoinOut, accepts_bn_input, materialize
-from ._chain import chain_backward, chain_forward, fusion_enabled, notify_backward_done
+from ._chain import chain_backward, chain_forward, execute, fusion_enabled, notify_backward_done
 from .activations import ReLu
 from .batch_norm import BatchNormLayer
 from .convolution import ConvLayer
@@ -74,11 +74,15 @@ class ResidualBlock(Layer):
 
     def takes_join_input(self):
         """forward(JoinOut): the previous block's join is formed by this block's first layer as it
-        loads its input (DepthwiseConvLayer._forward_join) -- an identity skip (the skip operand is
-        then that written y), a depthwise first layer of the right geometry, fusion on."""
+        loads its input (DepthwiseConvLayer._forward_join) -- a depthwise first layer of the right
+        geometry, fusion on.  The skip operand is then that written y: an identity skip reads it
+        at the join, a skip projection (a downsampling block, whose first layer is the stride-2
+        depthwise) reads it once the first layer has written it."""
         first = self.layer_list[0] if self.layer_list else None
-        return (self.skip_projection is None and isinstance(first, DepthwiseConvLayer) and first.join_geometry_ok()
-                and fusion_enabled() and getenv("DORKNET_FUSE_JOIN_FWD") != "0")
+        if not (isinstance(first, DepthwiseConvLayer) and first.join_geometry_ok() and fusion_enabled()
+                and getenv("DORKNET_FUSE_JOIN_FWD") != "0"):
+            return False
+        return self.skip_projection is None or first.stride == 2
 
     def forward(self, X, test_mode=False, join_out=False):
         """join_out: the next layer takes its input as a JoinOut (takes_join_input): the join is
@@ -89,24 +93,45 @@ class ResidualBlock(Layer):
         if isinstance(X, JoinOut) and not self.takes_join_input():
             X = X.materialize()
         branch = skip is not None and branch_stream_enabled()
-        if branch:
-            # the skip projection on the branch stream, beside the chain; joined at the join
-            Xs = X if accepts_bn_input(skip) else materialize(X)
-            with on_branch(Xs) as b:
-                skippee = b.done(skip.forward(Xs, test_mode=test_mode))
-        X_tmp, self._steps = chain_forward(self.layer_list, X, test_mode=test_mode, out_accepts=join_fused)
+        skip_late = skip is not None and isinstance(X, JoinOut)
+        if skip_late:
+            # the chain's first layer writes the join as it loads it; the skip projection starts
+            # once it has (on the branch stream, beside the rest of the chain)
+            J, launched = X, []
+
+            def after_first(group, out):
+                if not launched:
+                    launched.append(self._skip_forward(J.materialize(), test_mode, branch))
+                return False
+            X_tmp, self._steps, _ = execute(self.layer_list, X, test_mode=test_mode, out_accepts=join_fused,
+                                            visit=after_first)
+            skippee = launched[0]
+        else:
+            if branch:
+                # the skip projection on the branch stream, beside the chain; joined at the join
+                skippee = self._skip_forward(X, test_mode, True)
+            X_tmp, self._steps = chain_forward(self.layer_list, X, test_mode=test_mode, out_accepts=join_fused)
+            if skip is None:
+                skippee = X
+            elif not branch:
+                skippee = self._skip_forward(X, test_mode, False)
         if branch:
             skippee = skippee.resolve()
-        elif skip is not None:
-            skippee = skip.forward(X if accepts_bn_input(skip) else materialize(X), test_mode=test_mode)
-        else:
-            skippee = X
         if join_fused:
-            # a JoinOut consumer (takes_join_input: a stride-1 depthwise layer) takes the join's mask
-            # in its fused backward as y > 0; the mask is stored only when that fusion is off
+            # a JoinOut consumer (takes_join_input: a depthwise layer) takes the join's mask in its
+            # fused backward as y > 0; the mask is stored only when that fusion is off
             need_mask = not (enabled("DORKNET_FUSE_JOIN") and getenv("DORKNET_JOIN_MASK") != "1")
             return post.forward_add(X_tmp, skippee, test_mode=test_mode, defer=join_out, need_mask=need_mask)
         return post.forward(_add(materialize(X_tmp), materialize(skippee)), test_mode=test_mode)
+
+    def _skip_forward(self, X, test_mode, branch):
+        """skip_projection(X), on the branch stream when `branch` (a Branch to resolve())."""
+        skip = self.skip_projection
+        Xs = X if accepts_bn_input(skip) else materialize(X)
+        if not branch:
+            return skip.forward(Xs, test_mode=test_mode)
+        with on_branch(Xs) as b:
+            return b.done(skip.forward(Xs, test_mode=test_mode))
 
     def regulariser_forward(self):
         regularisation = 0

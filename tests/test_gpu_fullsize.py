@@ -176,10 +176,12 @@ def test_joins_full_size(monkeypatch, s2_fused):
     X = np.abs(rng.standard_normal((256, 64, 56, 56), dtype=np.float32))   # a ReLU output
     dY = rng.standard_normal((256, 128, 28, 28), dtype=np.float32)
     calls = Calls(monkeypatch, FUSED + ["dk_dwconv_bwd_bnbwd_join_f32", "dk_dwconv_dgrad_join_f32",
-                                        "dk_dwconv_bwd_s2_bnbwd_join_f32"])
+                                        "dk_dwconv_bwd_s2_bnbwd_join_f32", "dk_dwconv_fwd_join_f32"])
     got, want, f32, twin, _ = _run(layers, X, dY, input_grad=True)
     s2 = "dk_dwconv_bwd_s2_bnbwd_join_f32" if s2_fused == "1" else "dk_dwconv_dgrad_join_f32"
-    assert {"dk_dwconv_bwd_bnbwd_join_f32", s2} <= calls.seen, calls.seen
+    # both joins are formed by the next block's depthwise forward (res3's the stride-2 one, its skip
+    # projection reading the written y)
+    assert {"dk_dwconv_bwd_bnbwd_join_f32", s2, "dk_dwconv_fwd_join_f32"} <= calls.seen, calls.seen
     _check(got, want, f32, twin, layers)
 
 

@@ -70,8 +70,8 @@ def test_join_fwd_matches_bn_add_then_dw(stride, C, N, H, W, abn, brelu, bbn, st
 @pytest.mark.parametrize("fwd_fuse", ["1", "0"])
 @pytest.mark.parametrize("bwd_join", ["1", "0"])
 def test_network_join_fwd_bitwise(monkeypatch, fwd_fuse, bwd_join):
-    """ResNet-18-depsep training step (batch 4) with the identity blocks' joins formed by the next
-    block's depthwise forward vs the join pass: loss, probabilities and every gradient bitwise --
+    """ResNet-18-depsep training step (batch 4) with the blocks' joins formed by the next block's
+    depthwise forward (stride 1, or stride 2 into a downsampling block) vs the join pass: loss, probabilities and every gradient bitwise --
     with the join's backward fused into the next depthwise backward (which takes the ReLU mask as
     y > 0, so the fused forward stores none) and without (DORKNET_FUSE_JOIN=0: the mask is stored)."""
     monkeypatch.setenv("DORKNET_FUSE_JOIN", bwd_join)
@@ -91,7 +91,9 @@ def test_network_join_fwd_bitwise(monkeypatch, fwd_fuse, bwd_join):
         loss, P = net.forward(torch.as_tensor(X, device="cuda"), torch.as_tensor(onehot, device="cuda"))
         net.backward()
         torch.cuda.synchronize()
-        assert (len(seen) == 4) == (fuse == "1"), len(seen)  # res1 -> res2, res3 -> res4, res5 -> res6, res7 -> res8
+        # every block's join but the last: res1 -> res2 ... res7 -> res8 (into res3 / res5 / res7 through their
+        # stride-2 depthwise forward, the skip projection then reading the written y)
+        assert len(seen) == (7 if fuse == "1" else 0), len(seen)
         out[fuse] = (float(loss), P.cpu().clone(),
                      {(l.layer_name, k): v.cpu().clone() for l in all_layers(net.layers) for k, v in (l.grads or {}).items()})
     a, b = out["1"], out["0"]
