@@ -51,10 +51,10 @@ struct RowGeom {
   int PL;   // pixel lanes = 256 / cgt
 };
 
-__host__ __device__ inline RowGeom row_geom(int C, int V) {
+__host__ __device__ inline RowGeom row_geom(int C, int V, int cgt_cap = 256) {
   RowGeom g;
   g.CG = C / V;
-  g.cgt = g.CG < 256 ? g.CG : 256;
+  g.cgt = g.CG < cgt_cap ? g.CG : cgt_cap;
   g.PL = 256 / g.cgt;
   return g;
 }
@@ -355,10 +355,11 @@ __global__ __launch_bounds__(256) void bn_bwd_partial_kernel(const E* __restrict
                                                              const float* __restrict__ beta, int relu,
                                                              double* __restrict__ part,
                                                              const uint8_t* __restrict__ mask = nullptr,
-                                                             E* __restrict__ gout = nullptr, FoldTail ft = FoldTail{}) {
+                                                             E* __restrict__ gout = nullptr, FoldTail ft = FoldTail{},
+                                                             int cgt_cap = 256) {
   using VT = VecT<V, E>;
   __shared__ double red[2][256][V];
-  const RowGeom g = row_geom(C, V);
+  const RowGeom g = row_geom(C, V, cgt_cap);
   const int tid = threadIdx.x;
   const int cg = blockIdx.y * g.cgt + tid % g.cgt;
   const int pl = tid / g.cgt;
@@ -885,16 +886,20 @@ DK_API int dk_relu_bwd_bn_partial_f64(const float* dy, const uint8_t* mask, cons
   const int nblk = bn_blocks(P, C);
   const int ppb = cdiv(P, nblk);
   const bool vec = vec_ok(x, C) && vec_ok(dy, C) && vec_ok(dx, C) && (reinterpret_cast<uintptr_t>(mask) & 3) == 0;
-  const RowGeom g = row_geom(C, vec ? 4 : 1);
+  // the same partial rows (pixel ranges) as the other BN passes, but at most 32 channel groups per block:
+  // the head's 7 x 7 x 512 join (P = 12,544) otherwise ran 196 blocks of 2 pixel lanes, one per CU
+  // on 196 CUs, each lane walking 32 pixels
+  const int cap = 32;
+  const RowGeom g = row_geom(C, vec ? 4 : 1, cap);
   const dim3 grid(nblk, cdiv(g.CG, g.cgt));
   FoldTail ft;  // an armed in-launch fold of the partial rows (fold_tail.h)
   if (!fold_take(part, nblk, C, (int)grid.y, &ft) || ((g.cgt * (vec ? 4 : 1)) & 1)) ft.part = nullptr;
   if (vec)
     hipLaunchKernelGGL((bn_bwd_partial_kernel<4, true>), grid, dim3(256), 0, as_stream(stream), x, dy, P, C, ppb,
-                       mean, invstd, gamma, beta, relu, static_cast<double*>(part), mask, dx, ft);
+                       mean, invstd, gamma, beta, relu, static_cast<double*>(part), mask, dx, ft, cap);
   else
     hipLaunchKernelGGL((bn_bwd_partial_kernel<1, true>), grid, dim3(256), 0, as_stream(stream), x, dy, P, C, ppb,
-                       mean, invstd, gamma, beta, relu, static_cast<double*>(part), mask, dx, ft);
+                       mean, invstd, gamma, beta, relu, static_cast<double*>(part), mask, dx, ft, cap);
   return fold_status(launch_status(), ft);
 }
 

@@ -123,17 +123,27 @@ __global__ __launch_bounds__(256) void bn_add_kernel(const float* __restrict__ a
 }
 
 // out[n][c] = mean_{hw} x[n][hw][c]
+// (the HW loads of a channel are issued eight at a time and added in order: the sum, and so the
+// result, is the one-at-a-time loop's; issued one by one they left the kernel latency-bound)
 __global__ void gap_fwd_kernel(const float* __restrict__ x, int N, int HW, int C, float* __restrict__ out) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= N * C) return;
   const int n = i / C, c = i - n * C;
   const float* p = x + (size_t)n * HW * C + c;
   float s = 0.f;
-  for (int k = 0; k < HW; ++k) s += p[(size_t)k * C];
+  int k = 0;
+  for (; k + 8 <= HW; k += 8) {
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = p[(size_t)(k + u) * C];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s += v[u];
+  }
+  for (; k < HW; ++k) s += p[(size_t)k * C];
   out[i] = s / (float)HW;
 }
 
-// dx[n][hw][c] = (1/HW) * dy[n][c]
+// dx[n][hw][c] = (1/HW) * dy[n][c]; gap_bwd4_kernel: four channels per thread (C % 4 == 0, 16-byte aligned)
 __global__ void gap_bwd_kernel(const float* __restrict__ dy, int N, int HW, int C, float* __restrict__ dx) {
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const long long total = (long long)N * HW * C;
@@ -142,59 +152,104 @@ __global__ void gap_bwd_kernel(const float* __restrict__ dy, int N, int HW, int 
   const int n = (int)(i / ((long long)HW * C));
   dx[i] = (1.0f / (float)HW) * dy[(size_t)n * C + c];
 }
+__global__ void gap_bwd4_kernel(const float* __restrict__ dy, int N, int HW, int C, float* __restrict__ dx) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;  // float4 index; N * HW * C < 2^31 (checked)
+  const int C4 = C >> 2;
+  if (i >= N * HW * C4) return;
+  const int c4 = i % C4;
+  const int n = i / (HW * C4);
+  const f32x4 g = ld4(dy + (size_t)n * C + 4 * c4);
+  const float f = 1.0f / (float)HW;
+  st4(dx + (size_t)i * 4, f32x4{f * g[0], f * g[1], f * g[2], f * g[3]});
+}
 
 // p = e^x / sum e^x per row (no max subtraction, losses.py:15-16);
 // loss = mean_b -log(sum_j p[b][j] * y[b][j])  (losses.py:23-26).  One block.
+template <bool V4>
 __global__ __launch_bounds__(1024) void softmax_xent_fwd_kernel(const float* __restrict__ x,
                                                                 const float* __restrict__ y, int B, int K,
                                                                 float* __restrict__ p, float* __restrict__ loss) {
-  // one wave per row (rows w, w + 16, ...); per-wave fp64 loss sums combined in a fixed order.
-  // K <= 128 (every model here): a wave loads RB rows (x and y) before computing any, so the
-  // 16 rows a wave owns cost B / (16 RB) load latencies instead of B / 16.
-  constexpr int RB = 8;
+  // K <= 128 (every model here): four lanes per row, 256 rows per pass; a lane holds the row's columns
+  // part, part + 4, ... (all its loads issued at once), the four lane sums combined by two quad
+  // exchanges (the same value in every lane of the quad).  The row losses go through LDS and wave 0
+  // adds them in a fixed order (rows past B are 0).
+  // K > 128: one wave per row (rows w, w + 16, ...), per-wave fp64 sums combined in a fixed order.
   __shared__ double red[16];
+  __shared__ double rl[256];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   double acc = 0.0;
   if (K <= 128) {
-    for (int b0 = wv * RB; b0 < B; b0 += 16 * RB) {
-      float xv[RB][2], yv[RB][2];
+    // lane `part` of a row's quad holds the row's float4 columns part, part + 4, ... (K % 4 == 0 and
+    // 16-byte rows: V4, one load per 4 columns -- the block's memory requests, all through one CU,
+    // were this kernel's time), else its scalar columns part, part + 4, ...
+    constexpr int KPT = 32;
+    const int part = threadIdx.x & 3, r = threadIdx.x >> 2;
+    auto col = [&](int j) { return V4 ? 4 * (part + 4 * (j >> 2)) + (j & 3) : part + 4 * j; };
+    for (int b0 = 0; b0 < B; b0 += 256) {
+      const int b = b0 + r;
+      const bool live = b < B;
+      float e[KPT], yv[KPT];
+      if constexpr (V4) {
 #pragma unroll
-      for (int i = 0; i < RB; ++i) {
+        for (int i = 0; i < KPT / 4; ++i) {
+          const int k = 4 * (part + 4 * i);
+          const bool in = live && k < K;
+          const f32x4 xv = in ? ld4(x + (size_t)b * K + k) : f32x4{0.f, 0.f, 0.f, 0.f};
+          const f32x4 yq = in && y ? ld4(y + (size_t)b * K + k) : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const int j = lane + 64 * h;
-          const bool in = b0 + i < B && j < K;
-          xv[i][h] = in ? x[(size_t)(b0 + i) * K + j] : 0.f;
-          yv[i][h] = in && y ? y[(size_t)(b0 + i) * K + j] : 0.f;
-        }
-      }
-#pragma unroll
-      for (int i = 0; i < RB; ++i) {
-        if (b0 + i >= B) break;
-        const int b = b0 + i;
-        float e[2], s = 0.f;
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          e[h] = lane + 64 * h < K ? expf(xv[i][h]) : 0.f;
-          s += e[h];
-        }
-        s = wave_sum(s);
-        const float inv = 1.0f / s;
-        float dot = 0.f;
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const int j = lane + 64 * h;
-          if (j < K) {
-            const float v = inv * e[h];
-            p[(size_t)b * K + j] = v;
-            dot += v * yv[i][h];
+          for (int u = 0; u < 4; ++u) {
+            e[4 * i + u] = xv[u];
+            yv[4 * i + u] = yq[u];
           }
         }
-        if (y) {
-          dot = wave_sum(dot);
-          acc += (double)(-logf(dot));
+      } else {
+#pragma unroll
+        for (int j = 0; j < KPT; ++j) {
+          const int k = col(j);
+          const bool in = live && k < K;
+          e[j] = in ? x[(size_t)b * K + k] : 0.f;
+          yv[j] = in && y ? y[(size_t)b * K + k] : 0.f;
         }
       }
+      float s = 0.f;
+#pragma unroll
+      for (int j = 0; j < KPT; ++j) {
+        e[j] = col(j) < K ? expf(e[j]) : 0.f;
+        s += e[j];
+      }
+      s += __shfl_xor(s, 1, 64);
+      s += __shfl_xor(s, 2, 64);
+      const float inv = 1.0f / s;
+      float dot = 0.f;
+#pragma unroll
+      for (int j = 0; j < KPT; ++j) {
+        const float v = inv * e[j];
+        e[j] = v;
+        dot += v * yv[j];
+      }
+      if constexpr (V4) {
+#pragma unroll
+        for (int i = 0; i < KPT / 4; ++i) {
+          const int k = 4 * (part + 4 * i);
+          if (live && k < K) st4(p + (size_t)b * K + k, f32x4{e[4 * i], e[4 * i + 1], e[4 * i + 2], e[4 * i + 3]});
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < KPT; ++j)
+          if (live && col(j) < K) p[(size_t)b * K + col(j)] = e[j];
+      }
+      dot += __shfl_xor(dot, 1, 64);
+      dot += __shfl_xor(dot, 2, 64);
+      if (part == 0) rl[r] = live && y ? (double)(-logf(dot)) : 0.0;
+      __syncthreads();
+      if (wv == 0) {
+        // fixed order: lane l adds rows 4l .. 4l + 3, then a 64-lane tree (thread 0 alone, one LDS
+        // read and one dependent fp64 add per row, took ~10 us)
+        double t = ((rl[4 * lane] + rl[4 * lane + 1]) + rl[4 * lane + 2]) + rl[4 * lane + 3];
+        t = wave_sum(t);
+        if (lane == 0) acc += t;
+      }
+      __syncthreads();
     }
   } else {
     for (int b = wv; b < B; b += 16) {
@@ -509,13 +564,26 @@ DK_API int dk_gap_fwd_f32(const float* x, int N, int HW, int C, float* out, void
 }
 
 DK_API int dk_gap_bwd_f32(const float* dy, int N, int HW, int C, float* dx, void* stream) {
-  hipLaunchKernelGGL(gap_bwd_kernel, grid1((long long)N * HW * C), dim3(256), 0, as_stream(stream), dy, N, HW, C, dx);
+  if (C % 4 == 0 && (long long)N * HW * C < (1ll << 31) && (reinterpret_cast<uintptr_t>(dy) & 15) == 0 &&
+      (reinterpret_cast<uintptr_t>(dx) & 15) == 0)
+    hipLaunchKernelGGL(gap_bwd4_kernel, grid1((long long)N * HW * C / 4), dim3(256), 0, as_stream(stream), dy, N, HW,
+                       C, dx);
+  else
+    hipLaunchKernelGGL(gap_bwd_kernel, grid1((long long)N * HW * C), dim3(256), 0, as_stream(stream), dy, N, HW, C,
+                       dx);
   return launch_status();
 }
 
 DK_API int dk_softmax_xent_fwd_f32(const float* x, const float* y_onehot, int B, int K, float* p, float* loss,
                                    void* stream) {
-  hipLaunchKernelGGL(softmax_xent_fwd_kernel, dim3(1), dim3(1024), 0, as_stream(stream), x, y_onehot, B, K, p, loss);
+  const bool v4 = K % 4 == 0 && ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(p) |
+                                   reinterpret_cast<uintptr_t>(y_onehot)) & 15) == 0;
+  if (v4)
+    hipLaunchKernelGGL(softmax_xent_fwd_kernel<true>, dim3(1), dim3(1024), 0, as_stream(stream), x, y_onehot, B, K, p,
+                       loss);
+  else
+    hipLaunchKernelGGL(softmax_xent_fwd_kernel<false>, dim3(1), dim3(1024), 0, as_stream(stream), x, y_onehot, B, K,
+                       p, loss);
   return launch_status();
 }
 

@@ -6,7 +6,7 @@ dgrad and wgrad (+ l2) run on the same MFMA GEMM engine as the convolutions
 """
 from __future__ import annotations
 
-from .._hip import lib, stream_handle, workspace
+from .._hip import lib, stream_handle, weight_grad_stream, workspace
 from .._tensor import ptr, rows
 from ._common import add_regulariser_grad, grad_buffer, init_weights, l2_strength
 from .layer import Layer
@@ -63,17 +63,20 @@ class DenseLayer(Layer):
         B, IN = x.shape
         w = self.learned_params["weights"]
         OUT = w.shape[1]
-        if self.with_bias:
-            gb = grad_buffer(self, "bias", (OUT,))
-            nb = lib.dk_colsum_workspace_bytes(B, OUT)
-            lib.dk_colsum_f32(dy.data_ptr(), B, OUT, gb.data_ptr(), workspace.get(nb), nb, st)
-        gw = grad_buffer(self, "weights", (IN, OUT))
-        s = l2_strength(self.weight_regulariser)
-        nb = lib.dk_dense_wgrad_workspace_bytes(B, IN, OUT)
-        lib.dk_dense_wgrad_f32(x.data_ptr(), dy.data_ptr(), B, IN, OUT, w.data_ptr() if s else 0, s or 0.0,
-                               gw.data_ptr(), workspace.get(nb), nb, st)
-        if s is None:
-            add_regulariser_grad(gw, w, self.weight_regulariser)
+        # the parameter gradients on the side stream (_hip.weight_grad_stream), beside the dgrad
+        with weight_grad_stream(dy, x):
+            sst = stream_handle()
+            if self.with_bias:
+                gb = grad_buffer(self, "bias", (OUT,))
+                nb = lib.dk_colsum_workspace_bytes(B, OUT)
+                lib.dk_colsum_f32(dy.data_ptr(), B, OUT, gb.data_ptr(), workspace.get(nb), nb, sst)
+            gw = grad_buffer(self, "weights", (IN, OUT))
+            s = l2_strength(self.weight_regulariser)
+            nb = lib.dk_dense_wgrad_workspace_bytes(B, IN, OUT)
+            lib.dk_dense_wgrad_f32(x.data_ptr(), dy.data_ptr(), B, IN, OUT, w.data_ptr() if s else 0, s or 0.0,
+                                   gw.data_ptr(), workspace.get(nb), nb, sst)
+            if s is None:
+                add_regulariser_grad(gw, w, self.weight_regulariser)
         dx = torch.empty((B, IN), dtype=torch.float32, device=x.device)
         lib.dk_dense_dgrad_f32(dy.data_ptr(), B, OUT, w.data_ptr(), IN, dx.data_ptr(), st)
         return dx
