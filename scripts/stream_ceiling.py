@@ -20,7 +20,8 @@ def main():
     st = torch.cuda.current_stream().cuda_stream
     bufs = [torch.randn(n, device="cuda") for _ in range(5)]
     p = [b.data_ptr() for b in bufs]
-    for nin, nout in ((1, 0), (1, 1), (2, 1), (1, 2), (2, 2), (3, 1), (3, 2), (1, 11), (2, 11), (3, 12)):
+    for nin, nout in ((1, 0), (1, 1), (2, 1), (1, 2), (2, 2), (3, 1), (3, 2), (1, 11), (2, 11), (3, 11), (2, 12),
+                       (3, 12)):
         for blocks in (1024, 2048):
             f = lambda: lib.dk_debug_stream_mix(p[0], p[1], p[2], p[3], p[4], nin, nout, n, blocks, st)
             for _ in range(3):
