@@ -257,6 +257,37 @@ def test_relu_gap_softmax():
     check("softmax test-mode", Pt, Po)
 
 
+@pytest.mark.parametrize("B,K", [(6, 120), (300, 12), (257, 10), (3, 130), (256, 128), (1, 4)])
+def test_softmax_xent_shapes(B, K):
+    """The head's softmax + cross-entropy forward on each of its paths: float4 rows (K % 4 == 0,
+    K <= 128), scalar columns (K % 4 != 0), one wave per row (K > 128), and more than one 256-row
+    pass (B > 256), against the oracle (losses.py:13-34)."""
+    from dorknet_amd.layers.losses import SoftmaxWithCrossEntropy
+    rng = np.random.RandomState(B + K)
+    sm = SoftmaxWithCrossEntropy("s")
+    logits = (2.0 * rng.randn(B, K)).astype(np.float32)
+    y = np.eye(K, dtype=np.float32)[rng.randint(0, K, B)]
+    loss, P = sm.forward(dev(logits), dev(y))
+    lo, Po = ref.softmax_xent_forward(logits.astype(np.float64), y.astype(np.float64))
+    check("softmax P", P, Po)
+    assert abs(float(loss) - lo) <= 1e-5 * max(1.0, abs(lo)), (float(loss), lo)
+    check("softmax bwd", sm.backward(), ref.softmax_xent_backward(Po, y.astype(np.float64)))
+
+
+@pytest.mark.parametrize("N,C,H", [(2, 8, 5), (3, 6, 7), (4, 512, 7), (2, 64, 3)])
+def test_gap_shapes(N, C, H):
+    """Global average pooling forward (loads issued eight at a time, HW = 9 / 25 / 49 with a remainder)
+    and backward (float4 for C % 4 == 0, scalar otherwise) against the oracle (pooling.py:23-36)."""
+    from dorknet_amd.layers.pooling import GlobalAveragePoolingLayer
+    rng = np.random.RandomState(N * C + H)
+    X = rng.randn(N, C, H, H).astype(np.float32)
+    gap = GlobalAveragePoolingLayer("g")
+    gap.to_gpu()
+    check("gap fwd", gap.forward(dev(X)), ref.gap_forward(X.astype(np.float64)))
+    dG = rng.randn(N, C).astype(np.float32)
+    check("gap bwd", gap.backward(dev(dG)), ref.gap_backward(dG.astype(np.float64), (H, H)))
+
+
 def test_residual_block_and_sgd():
     """A downsampling depthwise-separable residual block + the optimiser, vs the oracle."""
     from dorknet_amd.layers.residual_block import ResidualBlock
