@@ -291,6 +291,36 @@ def side_stream():
     return s
 
 
+class _SyncEvents:
+    """Events for the cross-stream hand-overs (dk_sync_event_create: no system-scope fence, no timing),
+    handed out round-robin; an event is free again once the wait on it has been enqueued, and a
+    recorded branch completion is waited on within the same block, long before 64 more hand-overs."""
+    N = 64
+
+    def __init__(self):
+        self._ev = []
+        self._i = 0
+
+    def next(self) -> int:
+        if not self._ev:
+            for _ in range(self.N):
+                h = ctypes.c_void_p()
+                lib.dk_sync_event_create(ctypes.addressof(h))
+                self._ev.append(h.value)
+        e = self._ev[self._i]
+        self._i = (self._i + 1) % self.N
+        return e
+
+
+_sync_events = _SyncEvents()
+
+
+def stream_wait(waiter, src) -> None:
+    """waiter.wait_stream(src) through a fence-free event (dk_stream_wait_stream): the runtime's
+    default event record carries a system-scope release, ~7 us of idle main stream per hand-over."""
+    lib.dk_stream_wait_stream(waiter.cuda_stream, src.cuda_stream, _sync_events.next())
+
+
 class weight_grad_stream:
     """with weight_grad_stream(dy, x, ...): launches inside go to the side stream, after
     everything already queued on the current stream.  The listed tensors are marked as in
@@ -307,7 +337,7 @@ class weight_grad_stream:
         side = side_stream()
         if main == side:
             return self
-        side.wait_stream(main)
+        stream_wait(side, main)
         self.ctx = use_stream(side)
         self.ctx.__enter__()
         return self
@@ -453,7 +483,7 @@ def join_weight_grads() -> None:
     if s is not None:
         cur = cur_stream()
         if s != cur:
-            cur.wait_stream(s)
+            stream_wait(cur, s)
 
 
 # ---------------------------------------------------------------------------------------
@@ -508,7 +538,7 @@ class Branch:
 
     def resolve(self):
         cur = cur_stream()
-        cur.wait_event(self.event)
+        lib.dk_stream_wait_event(cur.cuda_stream, self.event)
         record_on(cur, self.value)
         return self.value
 
@@ -529,7 +559,7 @@ class on_branch:
     def __enter__(self):
         main = cur_stream()
         br = branch_stream()
-        br.wait_stream(main)
+        stream_wait(br, main)
         record_on(br, *self.inputs)
         self.ctx = use_stream(br)
         self.ctx.__enter__()
@@ -540,7 +570,7 @@ class on_branch:
         return False
 
     def done(self, value):
-        ev = torch.cuda.Event()
-        ev.record(branch_stream())
+        ev = _sync_events.next()
+        lib.dk_sync_event_record(ev, branch_stream().cuda_stream)
         return Branch(value, ev)
 

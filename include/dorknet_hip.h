@@ -411,6 +411,17 @@ int dk_bn_fold_disarm(void);
 int dk_wgrad_reduce_defer(int mode);
 int dk_wgrad_reduce_pending(void);
 int dk_wgrad_reduce_flush(void* stream);
+/* Cross-stream ordering between the host's HIP streams (main / weight-gradient side / skip branch)
+ * with events created without the system-scope fence and without timing (the hand-overs are
+ * device-internal).  dk_stream_wait_stream(waiter, src, event): work enqueued on `waiter` from now on
+ * starts after everything enqueued on `src` so far; `event` (from dk_sync_event_create) may be
+ * recorded again once the call has returned.  dk_sync_event_record + dk_stream_wait_event: the same
+ * split in two (a branch's completion recorded now, waited on later).  Return 0 or the hipError_t. */
+int dk_sync_event_create(void** event);
+int dk_sync_event_destroy(void* event);
+int dk_sync_event_record(void* event, void* stream);
+int dk_stream_wait_event(void* stream, void* event);
+int dk_stream_wait_stream(void* waiter, void* src, void* event);
 size_t dk_bn_fold_scratch_bytes(int nrows, int C);
 int dk_bn_fold_tickets_needed_count(int nrows, int nslices);
 int dk_relu_bwd_bn_partial_f64(const float* dy, const uint8_t* mask, const float* x, int P, int C, const float* mean, const float* invstd, const float* gamma, const float* beta, int relu, float* dx, void* part, size_t part_bytes, void* stream);
