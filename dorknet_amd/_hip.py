@@ -537,9 +537,11 @@ class Branch:
         self.event = event
 
     def resolve(self):
-        cur = cur_stream()
-        lib.dk_stream_wait_event(cur.cuda_stream, self.event)
-        record_on(cur, self.value)
+        # (the value is not marked as used by the current stream: freeing a block so marked records
+        # an event on that stream -- a marker, ~6 us of idle main stream.  It needs none: the block
+        # returns to the branch stream's pool, and every branch-stream use starts with on_branch's
+        # wait for the main stream, which orders it after the kernels that consumed this value)
+        lib.dk_stream_wait_event(cur_stream().cuda_stream, self.event)
         return self.value
 
 
