@@ -194,9 +194,10 @@ ENTRY_KERNEL = {
     # (prefix, regex): the GEMM instantiations whose A operand is the K-contiguous matrix
     # loader applying a BN backward (dgrad); the stem's weight gradient applies one on its
     # row-contiguous loader (LdMatICT) and is a different entry point
-    # (and the deep kernel, pw_deep.hip)
+    # (and the deep kernels, pw_deep.hip, in their BatchNorm form: PLAIN = false, the last
+    # template argument; the plain form is the skip projections' dk_pwconv_dgrad_f32)
     "dk_pwconv_dgrad_bnbwd_f32": [("dk::igemm_f32", r"dk::LdMatKCT<[^>]*>, dk::MatBwdDesc"),
-                                  ("dk::pwd::dgrad_kernel", "")],
+                                  ("dk::pwd::dgrad_kernel", r", false>$"), ("dk::pwd::dgrad16_kernel", r", false>$")],
     # the pointwise forward with output statistics: the tiled engine's instantiations (1x1 image
     # view, statistics epilogue), the streaming K = C = 64 kernel and the deep kernels with
     # statistics (STATS = true; the strided skip projections are dk_pwconv_fwd_f32)
@@ -210,8 +211,9 @@ ENTRY_KERNEL = {
     "dk_dwconv_bwd_bnbwd_bf16": ("dk::dw_bwd_fused_kernel", r"unsigned short"),
     "dk_dwconv_fwd_ex_bf16": ("dk::dw_fwd_kernel", r"unsigned short"),
     # the fused pointwise backward (round 5): the streaming K = C = 64 kernel (not its lattice form,
-    # a separate entry) and the fused deep kernel
-    "dk_pwconv_bwd_bnbwd_f32": [("dk::pws::bwd_fused_kernel", r", false>$"), ("dk::pwd::bwd_kernel", "")],
+    # a separate entry) and the fused deep kernels (32 x 32 at K = 128, 16 x 16 at K = 256)
+    "dk_pwconv_bwd_bnbwd_f32": [("dk::pws::bwd_fused_kernel", r", false>$"), ("dk::pwd::bwd_kernel", ""),
+                                ("dk::pwd::bwd16_kernel", "")],
     "dk_dwconv_bwd_bnbwd_f32": ("dk::dw_bwd_fused_kernel", r"^dk::dw_bwd_fused_kernel<\w+, \w+, \w+, false, float"),
     "dk_dwconv_fwd_ex_f32": ("dk::dw_fwd_kernel", r"float, false>"),
     "dk_conv2d_fwd_narrow_f32": ("dk::nar::fwd_kernel", ""),
