@@ -143,6 +143,48 @@ __global__ void gap_fwd_kernel(const float* __restrict__ x, int N, int HW, int C
   out[i] = s / (float)HW;
 }
 
+// The pooling of the network's last residual join (the head: y = ReLU(bnA(a) + bnB(b)),
+// residual_block.py:75, is read only by the global average pooling, pooling.py:23-30):
+// out[n][c] = mean_hw y, every y formed as bn_add_kernel forms it (bn_relu_out of each operand, one
+// add, the (v > 0) ? v : 0 ReLU) and summed in gap_fwd_kernel's order (loads eight at a time, added
+// one by one) -- bit-identical to the join pass followed by dk_gap_fwd_f32 -- with y never stored:
+// only its ReLU mask (the join's backward, activations.py:44-47), when given.
+__global__ __launch_bounds__(256) void gap_join_kernel(const float* __restrict__ a, BnIn ba, const float* __restrict__ b,
+                                                       BnIn bb, int N, int HW, int C, uint8_t* __restrict__ mask,
+                                                       float* __restrict__ out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= N * C) return;
+  const int n = i / C, c = i - n * C;
+  const float am = ba.mean ? ba.mean[c] : 0.f, ai = ba.mean ? ba.invstd[c] : 0.f;
+  const float ag = ba.mean ? ba.gamma[c] : 0.f, abt = ba.mean ? ba.beta[c] : 0.f;
+  const float bm = bb.mean ? bb.mean[c] : 0.f, bi = bb.mean ? bb.invstd[c] : 0.f;
+  const float bg = bb.mean ? bb.gamma[c] : 0.f, bbt = bb.mean ? bb.beta[c] : 0.f;
+  const size_t base = (size_t)n * HW * C + c;
+  auto join = [&](float av, float bv, int k) {
+    const float va = ba.mean ? bn_relu_out(av, am, ai, ag, abt, ba.relu) : av;
+    const float vb = bb.mean ? bn_relu_out(bv, bm, bi, bg, bbt, bb.relu) : bv;
+    float v = va + vb;
+    const bool pos = v > 0.f;
+    v = pos ? v : 0.f;
+    if (mask) mask[base + (size_t)k * C] = (uint8_t)pos;
+    return v;
+  };
+  float s = 0.f;
+  int k = 0;
+  for (; k + 8 <= HW; k += 8) {
+    float va[8], vb[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      va[u] = a[base + (size_t)(k + u) * C];
+      vb[u] = b[base + (size_t)(k + u) * C];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s += join(va[u], vb[u], k + u);
+  }
+  for (; k < HW; ++k) s += join(a[base + (size_t)k * C], b[base + (size_t)k * C], k);
+  out[i] = s / (float)HW;
+}
+
 // dx[n][hw][c] = (1/HW) * dy[n][c]; gap_bwd4_kernel: four channels per thread (C % 4 == 0, 16-byte aligned)
 __global__ void gap_bwd_kernel(const float* __restrict__ dy, int N, int HW, int C, float* __restrict__ dx) {
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -560,6 +602,20 @@ DK_API int dk_bn_add_f32(const float* a, const float* a_mean, const float* a_inv
 
 DK_API int dk_gap_fwd_f32(const float* x, int N, int HW, int C, float* out, void* stream) {
   hipLaunchKernelGGL(gap_fwd_kernel, grid1((long long)N * C), dim3(256), 0, as_stream(stream), x, N, HW, C, out);
+  return launch_status();
+}
+
+DK_API int dk_gap_join_fwd_f32(const float* a, const float* a_mean, const float* a_invstd, const float* a_gamma,
+                               const float* a_beta, int a_relu, const float* b, const float* b_mean,
+                               const float* b_invstd, const float* b_gamma, const float* b_beta, int b_relu, int N,
+                               int HW, int C, uint8_t* mask, float* out, void* stream) {
+  const BnIn ba{a_mean, a_invstd, a_gamma, a_beta, a_relu}, bb{b_mean, b_invstd, b_gamma, b_beta, b_relu};
+  auto params_ok = [](const BnIn& p) { return !p.mean || (p.invstd && p.gamma && p.beta); };
+  if (!a || !b || !out || N < 1 || HW < 1 || C < 1 || (long long)N * HW * C >= (1ll << 31) || !params_ok(ba) ||
+      !params_ok(bb))
+    return DK_ERR_ARGS;
+  hipLaunchKernelGGL(gap_join_kernel, grid1((long long)N * C), dim3(256), 0, as_stream(stream), a, ba, b, bb, N, HW, C,
+                     mask, out);
   return launch_status();
 }
 

@@ -123,20 +123,23 @@ class JoinOut:
             x.shape, dtype=torch.uint8, device=x.device, memory_format=torch.channels_last)
         self.written = False
 
+    def _like(self):
+        return self.A.x if isinstance(self.A, BNOut) else self.A
+
     @property
     def shape(self):
-        return self.y.shape
+        return self._like().shape
 
     def dim(self):
-        return self.y.dim()
+        return self._like().dim()
 
     @property
     def device(self):
-        return self.y.device
+        return self._like().device
 
     @property
     def dtype(self):
-        return self.y.dtype
+        return self._like().dtype
 
     @staticmethod
     def _operand(T):
@@ -154,8 +157,16 @@ class JoinOut:
         self.written = True
         self.relu_layer._join_written(self)
 
+    def mark_pooled(self):
+        """The consumer pooled the join as it formed it (dk_gap_join_fwd_f32): y was never stored
+        (only the mask), so it is dropped here and materialize() refuses."""
+        self.y = None
+        self.mark_written()
+
     def materialize(self):
         """y itself: the join pass (dk_bn_add_f32) unless a consumer already wrote it."""
+        if self.written and self.y is None:
+            raise RuntimeError("the residual join was pooled as it was formed (mark_pooled): y was never stored")
         if not self.written:
             a = self._operand(self.A)
             b = self._operand(self.B)

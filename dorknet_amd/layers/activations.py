@@ -107,7 +107,7 @@ class ReLu(Layer):
             self._mask, self._fused_out = jo.mask, None
             self._join_bn = jo.A if isinstance(jo.A, BNOut) else None
             self._join_done = False
-            self._join_y_ptr = jo.y.data_ptr()
+            self._join_y_ptr = None if jo.y is None else jo.y.data_ptr()  # (None: pooled, mark_pooled)
             self._join_y = jo.y if jo.mask is None else None
 
     def _bn_add(self, A, B, test_mode, st):

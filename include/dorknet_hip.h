@@ -448,6 +448,10 @@ int dk_add_f32(const float* a, const float* b, long long n, int relu, float* y, 
  * apply + ResidualBlock join + post-activation (residual_block.py:65-75). */
 int dk_bn_add_f32(const float* a, const float* a_mean, const float* a_invstd, const float* a_gamma, const float* a_beta, int a_relu, const float* b, const float* b_mean, const float* b_invstd, const float* b_gamma, const float* b_beta, int b_relu, long long n, int C, int relu, float* y, uint8_t* mask, void* stream);
 int dk_gap_fwd_f32(const float* x, int N, int HW, int C, float* out, void* stream);
+/* The global average pooling of a residual join y = ReLU(bnA(a) + bnB(b)) (dk_bn_add_f32's operands;
+ * residual_block.py:75 then pooling.py:23-30) without storing y: out[N][C] bit-identical to
+ * dk_bn_add_f32 followed by dk_gap_fwd_f32, y's ReLU mask (N*HW*C bytes, NHWC) written when non-NULL. */
+int dk_gap_join_fwd_f32(const float* a, const float* a_mean, const float* a_invstd, const float* a_gamma, const float* a_beta, int a_relu, const float* b, const float* b_mean, const float* b_invstd, const float* b_gamma, const float* b_beta, int b_relu, int N, int HW, int C, uint8_t* mask, float* out, void* stream);
 int dk_gap_bwd_f32(const float* dy, int N, int HW, int C, float* dx, void* stream);
 int dk_softmax_xent_fwd_f32(const float* x, const float* y_onehot, int B, int K, float* p, float* loss, void* stream);
 int dk_softmax_xent_bwd_f32(const float* p, const float* y_onehot, int B, int K, float* dx, void* stream);

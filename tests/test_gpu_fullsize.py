@@ -53,7 +53,7 @@ def _perturb_bn(layers, rng):
             l.learned_params["beta"] = (0.1 * rng.standard_normal((1, C, 1, 1))).astype(np.float32)
 
 
-def _run(layers, X, dY, input_grad, onehot=None):
+def _run(layers, X, dY, input_grad, onehot=None, nhwc_input=False):
     """The layers as a FeedForwardNetwork on the GPU and the fp64 / fp32 twins.  With `onehot`
     the network ends in the reference's loss layer (SoftmaxWithCrossEntropy): Y = the
     probabilities, backward from the loss, and the losses are returned as twin.loss / twin32.loss
@@ -68,6 +68,8 @@ def _run(layers, X, dY, input_grad, onehot=None):
         net.set_loss_layer(SoftmaxWithCrossEntropy("softmax1"))
     net.to_gpu()
     Xd = torch.as_tensor(X, device="cuda")
+    if nhwc_input:  # as a previous block hands it over (channels-last storage)
+        Xd = Xd.contiguous(memory_format=torch.channels_last)
     if onehot is None:
         dYd = torch.as_tensor(dY, device="cuda")
         _, Y = net.forward(Xd, None)
@@ -269,10 +271,12 @@ def test_res8_head_full_size(monkeypatch):
     _perturb_bn(layers, rng)
     X = np.abs(rng.standard_normal((256, 512, 7, 7), dtype=np.float32))     # res7's ReLU output
     onehot = np.eye(120, dtype=np.float32)[rng.integers(0, 120, 256)]
-    calls = Calls(monkeypatch, FUSED + ["dk_gap_fwd_f32", "dk_gap_bwd_f32", "dk_dense_fwd_f32", "dk_dense_dgrad_f32",
+    calls = Calls(monkeypatch, FUSED + ["dk_gap_join_fwd_f32", "dk_gap_bwd_f32", "dk_dense_fwd_f32", "dk_dense_dgrad_f32",
                                         "dk_dense_wgrad_f32", "dk_softmax_xent_fwd_f32", "dk_softmax_xent_bwd_f32"])
-    got, want, f32, twin, net = _run(layers, X, None, input_grad=True, onehot=onehot)
-    assert {"dk_pwconv_fwd_ex_f32", "dk_pwconv_dgrad_bnbwd_f32", "dk_gap_fwd_f32", "dk_gap_bwd_f32", "dk_dense_fwd_f32",
+    got, want, f32, twin, net = _run(layers, X, None, input_grad=True, onehot=onehot, nhwc_input=True)
+    # res8's join is pooled as it is formed (dk_gap_join_fwd_f32): no join pass, y never stored
+    assert "dk_bn_add_f32" not in calls.seen, calls.seen
+    assert {"dk_pwconv_fwd_ex_f32", "dk_pwconv_dgrad_bnbwd_f32", "dk_gap_join_fwd_f32", "dk_gap_bwd_f32", "dk_dense_fwd_f32",
             "dk_dense_dgrad_f32", "dk_dense_wgrad_f32", "dk_softmax_xent_fwd_f32",
             "dk_softmax_xent_bwd_f32"} <= calls.seen, calls.seen
     assert abs(net._dk_loss - twin.loss) <= max(TOL * abs(twin.loss), 3.0 * abs(twin.loss32 - twin.loss)), \

@@ -101,3 +101,45 @@ def test_network_join_fwd_bitwise(monkeypatch, fwd_fuse, bwd_join):
     assert torch.equal(a[1], b[1])
     for key, g in a[2].items():
         assert torch.equal(g, b[2][key]), key
+
+
+@pytest.mark.parametrize("C,N,H", [(512, 4, 7), (64, 3, 5), (6, 2, 9), (256, 2, 1)])
+@pytest.mark.parametrize("abn,brelu,bbn", [(True, 0, False), (True, 1, True), (False, 0, True)])
+@pytest.mark.parametrize("with_mask", [True, False])
+def test_gap_join_matches_bn_add_then_gap(C, N, H, abn, brelu, bbn, with_mask):
+    """The head's pooling of the last join (dk_gap_join_fwd_f32) against the join pass + the pooling
+    (dk_bn_add_f32 -> dk_gap_fwd_f32): the pooled output and the ReLU mask bitwise (HW = 49 / 25 / 81 / 1:
+    the eight-at-a-time loads with and without a remainder; C = 6: the C % 4 != 0 case the join pass
+    does not take, checked against an elementwise torch join)."""
+    rng = np.random.RandomState(C + N + H + 5 * abn + 7 * bbn + brelu)
+    a = nhwc(rng.randn(N, C, H, H) * 1.5)
+    b = nhwc(rng.randn(N, C, H, H))
+    pa, pb = bn_params(C, rng), bn_params(C, rng)
+    st = stream_handle()
+    aa = (*(t.data_ptr() for t in pa), 0) if abn else (0, 0, 0, 0, 0)
+    ba = (*(t.data_ptr() for t in pb), brelu) if bbn else (0, 0, 0, 0, 0)
+    out1 = torch.full((N, C), float("nan"), device="cuda")
+    m1 = torch.full((N, C, H, H), 7, dtype=torch.uint8, device="cuda").contiguous(memory_format=torch.channels_last)
+    assert lib.dk_gap_join_fwd_f32(a.data_ptr(), *aa, b.data_ptr(), *ba, N, H * H, C,
+                                   m1.data_ptr() if with_mask else 0, out1.data_ptr(), st) == 0
+    if C % 4 == 0:
+        y0 = nhwc(np.zeros((N, C, H, H)))
+        m0 = torch.zeros((N, C, H, H), dtype=torch.uint8, device="cuda").contiguous(memory_format=torch.channels_last)
+        lib.dk_bn_add_f32(a.data_ptr(), *aa, b.data_ptr(), *ba, a.numel(), C, 1, y0.data_ptr(), m0.data_ptr(), st)
+    else:
+        def bn(x, p, relu):
+            m, i, g, be = (t.view(1, C, 1, 1) for t in p)
+            r = g * ((x - m) * i) + be
+            return torch.where(r > 0, r, torch.zeros_like(r)) if relu else r
+        y0 = (bn(a, pa, 0) if abn else a) + (bn(b, pb, brelu) if bbn else b)
+        m0 = (y0 > 0).to(torch.uint8)
+        y0 = torch.where(y0 > 0, y0, torch.zeros_like(y0)).contiguous(memory_format=torch.channels_last)
+    out0 = torch.empty((N, C), device="cuda")
+    lib.dk_gap_fwd_f32(y0.data_ptr(), N, H * H, C, out0.data_ptr(), st)
+    torch.cuda.synchronize()
+    if C % 4 == 0:
+        assert torch.equal(out0, out1)
+    else:
+        torch.testing.assert_close(out1, out0, rtol=1e-6, atol=1e-6)
+    if with_mask:
+        assert torch.equal(m0.contiguous(memory_format=torch.channels_last), m1)
