@@ -143,13 +143,14 @@ __device__ __forceinline__ void partial_row(double ps, double pq, double* part, 
     red[1][32 * wave + l32] = pq;
   }
   __syncthreads();
+  const int nc = N - n0 < NB ? N - n0 : NB;  // (NB except the C = 64 fused backward's one column group)
   for (int i = tid; i < 2 * NB; i += NT) {
     const int which = i / NB, c = i - which * NB;
-    pub_store(part + ((size_t)blockIdx.x * 2 + which) * N + n0 + c, red[which][c]);
+    if (c < nc) pub_store(part + ((size_t)blockIdx.x * 2 + which) * N + n0 + c, red[which][c]);
   }
   if (ft.part) {
     __syncthreads();  // red is read before the fold overwrites it
-    fold_tail<NT>(ft, blockIdx.x, n0, NB, blockIdx.y, reinterpret_cast<double2*>(scratch));
+    fold_tail<NT>(ft, blockIdx.x, n0, nc, blockIdx.y, reinterpret_cast<double2*>(scratch));
   }
 }
 
@@ -713,6 +714,9 @@ __global__ __launch_bounds__(NT, bwd_wps<KR>()) void bwd_kernel(BwdArgs a) {
   const int l32 = lane & 31, h = lane >> 5;
   const int n0 = blockIdx.y * NB, N = a.N;
   const int col = n0 + 32 * wave + l32;
+  // C = 64 (the stride-2 block's first pointwise layer): one column group of 64, so waves 2 and 3 only
+  // stage the dy tiles (wave-uniform; N is a multiple of 32)
+  const bool wact = n0 + 32 * wave < N;
   const int kv = tid % KV, r0 = tid / KV;
   if (tid < KV) {
     const f32x4 ga = ld4(a.og + 4 * tid), is = ld4(a.ois + 4 * tid);
@@ -728,8 +732,8 @@ __global__ __launch_bounds__(NT, bwd_wps<KR>()) void bwd_kernel(BwdArgs a) {
     bnt[6][tid] = f;
   }
   __syncthreads();
-  const float pm = BNIN ? a.im[col] : 0.f, pis = BNIN ? a.iis[col] : 0.f, pga = BNIN ? a.ig[col] : 0.f,
-              pbe = BNIN ? a.ib[col] : 0.f;
+  const float pm = BNIN && wact ? a.im[col] : 0.f, pis = BNIN && wact ? a.iis[col] : 0.f,
+              pga = BNIN && wact ? a.ig[col] : 0.f, pbe = BNIN && wact ? a.ib[col] : 0.f;
   const bool orelu = a.orelu != 0, irelu = a.irelu != 0;
 
   const int ntiles = (a.M + TR - 1) / TR, G = gridDim.x;
@@ -774,7 +778,7 @@ __global__ __launch_bounds__(NT, bwd_wps<KR>()) void bwd_kernel(BwdArgs a) {
 #pragma unroll
     for (int q = 0; q < KQ; ++q)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) bw[q][e] = a.w[(size_t)(8 * q + 4 * h + e) * N + col];
+      for (int e = 0; e < 4; ++e) bw[q][e] = wact ? a.w[(size_t)(8 * q + 4 * h + e) * N + col] : 0.f;
     stage(&As[0][0], sg, sx);
   }
   __syncthreads();
@@ -788,6 +792,8 @@ __global__ __launch_bounds__(NT, bwd_wps<KR>()) void bwd_kernel(BwdArgs a) {
   for (; t < ntiles; t += G) {
     f32x4 ng[LV], nx[LV];
     load_tile(t + G, ng, nx);
+    const float* tile = &As[buf][0];
+    if (wact) {
     // the tile's C-layout operands (layer input, residual), in flight during the dgrad MFMAs
     const int mb = t * TR + 4 * h;
     const __amdgpu_buffer_rsrc_t rxi = tile_rsrc(a.xi, N, t, a.M);
@@ -800,7 +806,6 @@ __global__ __launch_bounds__(NT, bwd_wps<KR>()) void bwd_kernel(BwdArgs a) {
       ex[r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rxi, (int)cbase, ro, 0));
       if constexpr (RES) ers[r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rr, (int)cbase, ro, 0));
     }
-    const float* tile = &As[buf][0];
     f32x16 acc;
     mfma_tile<KQ>(tile + l32 * SK + 4 * h, bw, acc);
     if constexpr (RES) {
@@ -855,6 +860,7 @@ __global__ __launch_bounds__(NT, bwd_wps<KR>()) void bwd_kernel(BwdArgs a) {
         for (int u = 0; u < NU; ++u) bv[u] = nb[u];
       }
     }
+    }  // wact
     stage(&As[buf ^ 1][0], ng, nx);
     __syncthreads();
     buf ^= 1;
@@ -875,7 +881,7 @@ __global__ __launch_bounds__(NT, bwd_wps<KR>()) void bwd_kernel(BwdArgs a) {
       for (int j = 0; j < 32 * NB / 4 / NT; ++j) {
         const int idx = tid + NT * j, i = idx / (NB / 4), c4 = idx % (NB / 4);
         const int k = 4 * i + (kt & 3) + 128 * (kt >> 2);
-        st4(wp + (size_t)k * N + 4 * c4, ld4(T + i * ST + 4 * c4));
+        if (n0 + 4 * c4 < N) st4(wp + (size_t)k * N + 4 * c4, ld4(T + i * ST + 4 * c4));
       }
     }
   }
@@ -1181,7 +1187,7 @@ static int bwd_occ() {
 // allocate exactly the partial rows the launch writes.
 static int grid_x(int M, int N, int occ, int tr = TR) {
   const int ntiles = (M + tr - 1) / tr;
-  const int groups = N / NB;
+  const int groups = N < NB ? 1 : N / NB;  // (N < NB: the C = 64 fused backward, one column group)
   int slots = occ * 256 / groups;
   if (slots < 1) slots = 1;
   int gx = std::min(ntiles, slots);
@@ -1339,11 +1345,14 @@ int pw_deep_dgrad_plain(const float* dy, int M, int K, int C, const float* w, fl
   return DK_ERR_ARGS;
 }
 
-// Fused deep backward (bwd_kernel): reduction K in {128, 256}, C a multiple of the block's 128 columns.
+// Fused deep backward (bwd_kernel): reduction K in {128, 256}, C a multiple of the block's 128 columns,
+// or K = 128 with C = 64 (one column group, half its waves staging only: the downsampling blocks' first
+// pointwise layer at 28 x 28, whose unfused pair stored dy and re-read it on the side stream).
 // Default on; knob 14 = 0 keeps the dgrad + side-stream weight gradient pair.
 static bool pwd_bwd_enabled() { return knob(kKnobPwDeepBwd) == 1 && pwd_enabled(); }
 bool pw_deep_bwd_ok(int K, int C, int M) {
-  if (!pwd_bwd_enabled() || M <= 0 || (K != 128 && K != 256) || C % pwd::NB) return false;
+  if (!pwd_bwd_enabled() || M <= 0 || (K != 128 && K != 256) || (C % pwd::NB && !(K == 128 && C == 64)))
+    return false;
   return (size_t)M * (K > C ? K : C) * 4 < ((size_t)1 << 31);
 }
 // K = 256 runs the two-waves-per-SIMD 16 x 16 kernel (bwd16_kernel), 16-pixel tiles.  At K = 128 the
@@ -1356,7 +1365,7 @@ int pw_deep_bwd_rows(int M, int K, int C) {
   if (K == 128) return pwd::grid_x(M, C, pwd::bwd_occ<128>());
   return 0;
 }
-int pw_deep_bwd_slices(int M, int K, int C) { return C / pwd::NB; }
+int pw_deep_bwd_slices(int M, int K, int C) { return C < pwd::NB ? 1 : C / pwd::NB; }
 
 int pw_deep_bwd_bnbwd(const float* g, const float* bn_x, int M, int K, int C, const float* om, const float* ois,
                       const float* og, const float* ob, int orelu, const float* k12, const float* w, float* dx,
@@ -1366,7 +1375,7 @@ int pw_deep_bwd_bnbwd(const float* g, const float* bn_x, int M, int K, int C, co
   pwd::BwdArgs a{g, bn_x, w, dx, res, x, om, ois, og, ob, k12, orelu, im, iis, ig, ib, irelu, part, wpart, M, C};
   if (ft && part) a.ft = *ft;
   a.nt = nt_stores(kNtPwd);
-  const dim3 grid(pw_deep_bwd_rows(M, K, C), C / pwd::NB);
+  const dim3 grid(pw_deep_bwd_rows(M, K, C), pw_deep_bwd_slices(M, K, C));
   if (grid.x == 0) return DK_ERR_ARGS;
   if (pwd_bwd16(K)) {
 #define DK_L16(kr, R_, B_) hipLaunchKernelGGL((pwd::bwd16_kernel<kr, R_, B_>), grid, dim3(pwd::NT16), 0, st, a)

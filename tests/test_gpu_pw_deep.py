@@ -247,7 +247,7 @@ def test_deep_wgrad_strided_skip(K, C, H):
 
 
 FUSED_KNOB = 14
-FUSED_SHAPES = [(128, 128), (256, 128), (256, 256), (128, 256), (256, 512)]  # (K, C)
+FUSED_SHAPES = [(128, 128), (256, 128), (256, 256), (128, 256), (256, 512), (128, 64)]  # (K, C)
 
 
 @pytest.mark.parametrize("K,C", FUSED_SHAPES)
@@ -314,10 +314,12 @@ def test_deep_fused_bwd_matches_unfused(K, C, relu, bn_in, resid, N, H, W):
     assert bool(((dw.double() - ref).abs() <= bound).all()), float(((dw.double() - ref).abs() / bound).max())
 
 
-def test_deep_fused_bwd_deterministic_and_in_bounds():
+@pytest.mark.parametrize("K,C", [(256, 256), (128, 64)])
+def test_deep_fused_bwd_deterministic_and_in_bounds(K, C):
     """The fused deep backward twice on the same inputs: dx and dW bitwise equal run to run (fixed-order
-    reductions, no atomics); a ragged pixel count writes nothing past dx (sentinel)."""
-    N, H, W, K, C = 3, 7, 5, 256, 256
+    reductions, no atomics); a ragged pixel count writes nothing past dx, the weight-gradient partial rows
+    or the BatchNorm partial rows (sentinels; C = 64: the column group's idle half writes nothing)."""
+    N, H, W = 3, 7, 5
     M = N * H * W
     rng = np.random.RandomState(5)
     st = stream_handle()
@@ -331,10 +333,11 @@ def test_deep_fused_bwd_deterministic_and_in_bounds():
     rows = lib.dk_pwconv_bwd_fused_rows(N, H, W, K, C)
     outs = []
     for _ in range(2):
-        ws = torch.empty(nb // 4 + 4, dtype=torch.float32, device="cuda")
+        ws = torch.full((nb // 4 + 4096,), 54321.0, dtype=torch.float32, device="cuda")
         dxbuf = torch.full((M * C + 4096,), 12345.0, device="cuda")
         dw = torch.empty((K, C), device="cuda")
-        part = torch.zeros((rows, 2, C), dtype=torch.float64, device="cuda")
+        pbuf = torch.full((rows * 2 * C + 1024,), 777.0, dtype=torch.float64, device="cuda")
+        part = pbuf[:rows * 2 * C].view(rows, 2, C)
         rc = lib.dk_pwconv_bwd_bnbwd_f32(g.data_ptr(), xo.data_ptr(), N, H, W, K, *(t.data_ptr() for t in po), 1,
                                          k12.data_ptr(), w.data_ptr(), C, 1e-4, dw.data_ptr(), dxbuf.data_ptr(), 0,
                                          xin.data_ptr(), *(t.data_ptr() for t in pi), 1, part.data_ptr(),
@@ -342,6 +345,7 @@ def test_deep_fused_bwd_deterministic_and_in_bounds():
         assert rc in (0, 10100)
         torch.cuda.synchronize()
         assert bool((dxbuf[M * C:] == 12345.0).all()) and bool(torch.isfinite(dxbuf[:M * C]).all())
+        assert bool((ws[nb // 4:] == 54321.0).all()) and bool((pbuf[rows * 2 * C:] == 777.0).all())
         outs.append((dxbuf.clone(), dw.clone(), part.clone()))
     assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
     assert torch.equal(outs[0][2], outs[1][2])
