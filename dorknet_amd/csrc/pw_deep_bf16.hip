@@ -99,13 +99,14 @@ __device__ __forceinline__ void partial_row(double ps, double pq, double* part, 
     red[1][32 * wave + l32] = pq;
   }
   __syncthreads();
+  const int nc = N - n0 < NB ? N - n0 : NB;  // (NB except the C = 64 fused backward's one column group)
   for (int i = tid; i < 2 * NB; i += NT) {
     const int which = i / NB, c = i - which * NB;
-    pub_store(part + ((size_t)blockIdx.x * 2 + which) * N + n0 + c, red[which][c]);
+    if (c < nc) pub_store(part + ((size_t)blockIdx.x * 2 + which) * N + n0 + c, red[which][c]);
   }
   if (ft.part) {
     __syncthreads();
-    fold_tail<NT>(ft, blockIdx.x, n0, NB, blockIdx.y, reinterpret_cast<double2*>(scratch));
+    fold_tail<NT>(ft, blockIdx.x, n0, nc, blockIdx.y, reinterpret_cast<double2*>(scratch));
   }
 }
 
@@ -418,6 +419,8 @@ __global__ __launch_bounds__(NT, bwd_wps<KR>()) void bwd_kernel(DgradArgs a, flo
   static_assert(sizeof(double) * 2 * NT <= sizeof(bf16_t) * 2 * TR * SK, "fold scratch fits in the tiles");
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l32 = lane & 31, h = lane >> 5;
   const int n0 = blockIdx.y * NB, N = a.N, col = n0 + 32 * wave + l32;
+  // C = 64: one column group of 64, waves 2 and 3 only stage the dy tiles (wave-uniform)
+  const bool wact = n0 + 32 * wave < N;
   const int kv = tid % KV, r0 = tid / KV;
   __shared__ __attribute__((aligned(16))) float tab[7 * KR];
   for (int c = tid; c < KR; c += NT) {
@@ -431,8 +434,8 @@ __global__ __launch_bounds__(NT, bwd_wps<KR>()) void bwd_kernel(DgradArgs a, flo
     tab[6 * KR + c] = ga * is;
   }
   __syncthreads();
-  const float pm = BNIN ? a.im[col] : 0.f, pis = BNIN ? a.iis[col] : 0.f, pga = BNIN ? a.ig[col] : 0.f,
-              pbe = BNIN ? a.ib[col] : 0.f;
+  const float pm = BNIN && wact ? a.im[col] : 0.f, pis = BNIN && wact ? a.iis[col] : 0.f,
+              pga = BNIN && wact ? a.ig[col] : 0.f, pbe = BNIN && wact ? a.ib[col] : 0.f;
   const bool orelu = a.orelu != 0, irelu = a.irelu != 0;
   const int ntiles = (a.M + TR - 1) / TR, G = gridDim.x;
   const uint32_t lofs0 = ((uint32_t)r0 * KR + 8 * kv) * 2u, eofs0 = ((uint32_t)(4 * h) * N + col) * 2u;
@@ -489,8 +492,8 @@ __global__ __launch_bounds__(NT, bwd_wps<KR>()) void bwd_kernel(DgradArgs a, flo
       f32x4 lo, hi;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        lo[e] = a.w[(size_t)(16 * s + 8 * h + e) * N + col];
-        hi[e] = a.w[(size_t)(16 * s + 8 * h + 4 + e) * N + col];
+        lo[e] = wact ? a.w[(size_t)(16 * s + 8 * h + e) * N + col] : 0.f;
+        hi[e] = wact ? a.w[(size_t)(16 * s + 8 * h + 4 + e) * N + col] : 0.f;
       }
       bw[s] = __builtin_bit_cast(bf16x8, pack8(lo, hi));
     }
@@ -509,6 +512,7 @@ __global__ __launch_bounds__(NT, bwd_wps<KR>()) void bwd_kernel(DgradArgs a, flo
   for (; t < ntiles; t += G) {
     u32x4 ng[LV], nx[LV];
     load_tile(t + G, ng, nx);
+    if (wact) {
     const int mb = t * TR + 4 * h;
     const int rows = a.M - t * TR;
     const uint32_t nb = rows > 0 ? (uint32_t)rows * N * 2u : 0u;
@@ -565,12 +569,13 @@ __global__ __launch_bounds__(NT, bwd_wps<KR>()) void bwd_kernel(DgradArgs a, flo
         }
       }
     }
+    }  // wact
     stage(&As[buf ^ 1][0], ng, nx);
     __syncthreads();
     buf ^= 1;
   }
   // this wave's dW block: element (kt, r) = dW[32 kt + (r & 3) + 8 (r >> 2) + 4h][col]
-  {
+  if (wact) {
     float* wp = wpart + (size_t)blockIdx.x * KR * N + col;
 #pragma unroll
     for (int kt = 0; kt < KT; ++kt)
@@ -620,7 +625,7 @@ static int dgrad_occ() {
 // per tile, a multiple of 8 when that costs no extra tile per walker.
 static int grid_x(int M, int N, int occ) {
   const int ntiles = (M + TR - 1) / TR;
-  int slots = occ * 256 / (N / NB);
+  int slots = occ * 256 / (N < NB ? 1 : N / NB);  // (N < NB: the C = 64 fused backward, one column group)
   if (slots < 1) slots = 1;
   int gx = std::min(ntiles, slots);
   const int g8 = gx / 8 * 8;
@@ -734,10 +739,12 @@ static int bwd_occ16() {
   }();
   return occ;
 }
-// The fused bf16 backward: K in {128, 256}, C a multiple of the block's 128 columns (knob 20 with the
-// K = C = 64 streaming form; 2 keeps only that one).
+// The fused bf16 backward: K in {128, 256}, C a multiple of the block's 128 columns, or K = 128 with
+// C = 64 (one column group, half the block's waves staging only: config 5's 64 -> 128 unit, whose
+// unfused pair stored dy for a side-stream weight GEMM).
 bool pw_deep16_bwd_ok(int K, int C, int M) {
-  if (!pwd16_enabled() || M <= 0 || (K != 128 && K != 256) || C % pwd16::NB || C > 4096)
+  if (!pwd16_enabled() || M <= 0 || (K != 128 && K != 256) || (C % pwd16::NB && !(K == 128 && C == 64)) ||
+      C > 4096)
     return false;
   return (size_t)M * (K > C ? K : C) * 2 < ((size_t)1 << 31);
 }
@@ -746,7 +753,7 @@ int pw_deep16_bwd_rows(int M, int K, int C) {
   if (K == 256) return pwd16::grid_x(M, C, bwd_occ16<256>());
   return 0;
 }
-int pw_deep16_bwd_slices(int M, int K, int C) { return C / pwd16::NB; }
+int pw_deep16_bwd_slices(int M, int K, int C) { return C < pwd16::NB ? 1 : C / pwd16::NB; }
 int pw_deep16_bwd_fused(const bf16_t* g, const bf16_t* bn_x, int M, int K, int C, const float* om, const float* ois,
                         const float* og, const float* ob, int orelu, const float* k12, const float* w, bf16_t* dx,
                         const bf16_t* res, const bf16_t* x, const float* im, const float* iis, const float* ig,
@@ -755,7 +762,7 @@ int pw_deep16_bwd_fused(const bf16_t* g, const bf16_t* bn_x, int M, int K, int C
   pwd16::DgradArgs a{g, bn_x, nullptr, w, dx, res, x, om, ois, og, ob, k12, orelu, im, iis, ig, ib, irelu, part, M, C};
   if (ft && part) a.ft = *ft;
   a.nt = nt_stores(kNtPwd16);
-  const dim3 grid(pw_deep16_bwd_rows(M, K, C), C / pwd16::NB);
+  const dim3 grid(pw_deep16_bwd_rows(M, K, C), pw_deep16_bwd_slices(M, K, C));
   if (grid.x == 0) return DK_ERR_ARGS;
 #define DK_L(kr, R_, B_) hipLaunchKernelGGL((pwd16::bwd_kernel<kr, R_, B_>), grid, dim3(pwd16::NT), 0, st, a, wpart)
 #define DK_BW(kr)             \

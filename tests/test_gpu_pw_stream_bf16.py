@@ -172,13 +172,14 @@ def test_bf16_deep_kernels_dispatch():
     assert streamed != tiled and streamed <= 256 and tiled >= M // 256
 
 
-@pytest.mark.parametrize("K,C", [(64, 64), (128, 128), (256, 128), (256, 256), (128, 256)])
+@pytest.mark.parametrize("K,C", [(64, 64), (128, 128), (256, 128), (256, 256), (128, 256), (128, 64)])
 @pytest.mark.parametrize("relu,bn_in,resid,N,H,W", [(1, True, False, 3, 13, 11), (0, True, False, 2, 8, 8),
                                                     (1, False, True, 3, 13, 11), (1, True, True, 5, 7, 9),
                                                     (0, False, False, 1, 1, 3), (1, True, False, 16, 56, 56)])
 def test_bf16_fused_bwd_matches_dgrad_and_fp64(K, C, relu, bn_in, resid, N, H, W):
     """dk_pwconv_bwd_bnbwd_bf16 (dgrad and weight gradient in one pass, dy never stored: K = C = 64 on
-    pw_stream_bf16.hip bwd_fused_kernel, K in {128, 256} on pw_deep_bf16.hip bwd_kernel) against the
+    pw_stream_bf16.hip bwd_fused_kernel, K in {128, 256} on pw_deep_bf16.hip bwd_kernel, incl. K = 128 with
+    C = 64, one column group) against the
     dgrad that stores dy: dx bitwise, the input BatchNorm's partial sums to fp64 rounding; and its
     weight gradient against fp64 dW = dy^T bf16(bn_relu(x)) + l2 w with dy the dgrad's stored bf16 dy
     (the MFMA operands the fused kernel forms), elementwise within 3e-5 of sum |dy| |xh|.
