@@ -150,6 +150,8 @@ __global__ __launch_bounds__(NT, 2) void fwd_kernel(const float* __restrict__ x,
   // loads it saves)
   if (r0 < r1) rs.load(x, g, r0 / g.OH, r0 % g.OH);
   const float* const xl = xin + ST * li;
+  const uint32_t kb = (uint32_t)g.K * 4u;                                    // bytes per output pixel
+  const uint32_t vbase = cok ? (uint32_t)(4 * lg * g.K + col) * 4u : kOOBBytes;  // lane part of the store offset
   for (int row = r0; row < r1; ++row) {
     __syncthreads();  // the previous row's LDS reads are done
     rs.store(xin, g);
@@ -166,23 +168,28 @@ __global__ __launch_bounds__(NT, 2) void fwd_kernel(const float* __restrict__ x,
 #pragma unroll
       for (int t = 0; t < T; ++t) acc[t] = mfma16(a[t], b[kk], acc[t]);
     }
-    // C/D: row (output pixel) 16t + 4lg + v, column = filter col
-    float* yr = y + (size_t)row * g.OW * g.K + col;
+    // C/D: row (output pixel) 16t + 4lg + v, column = filter col.  Branch-free: buffer stores on the
+    // row's bytes (a filter past K reads kOOBBytes, a pixel past OW lands past the row's range: both
+    // dropped by the range check) and the statistics take 0 for them, in the same order.
+    const __amdgpu_buffer_rsrc_t ry = make_rsrc_v(y + (size_t)row * g.OW * g.K, (uint32_t)g.OW * g.K * 4u);
+    auto epilogue = [&](auto pol) {
 #pragma unroll
-    for (int t = 0; t < T; ++t)
+      for (int t = 0; t < T; ++t)
 #pragma unroll
-      for (int v = 0; v < 4; ++v) {
-        const int ow = 16 * t + 4 * lg + v;
-        if (cok && ow < g.OW) {
+        for (int v = 0; v < 4; ++v) {
+          const int ow = 16 * t + 4 * lg + v;
           const float o = acc[t][v] + bv;
-          if (g.nt)
-            __builtin_nontemporal_store(o, yr + (size_t)ow * g.K);
-          else
-            yr[(size_t)ow * g.K] = o;
-          sa += (double)o;
-          sb += (double)o * (double)o;
+          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, o), ry, (int)(vbase + (16 * t + v) * kb),
+                                                0, decltype(pol)::value);
+          const double od = cok && ow < g.OW ? (double)o : 0.0;
+          sa += od;
+          sb += od * od;
         }
-      }
+    };
+    if (g.nt)
+      epilogue(std::integral_constant<int, 2>{});
+    else
+      epilogue(std::integral_constant<int, 0>{});
   }
   if (!part) return;
   // per-filter totals of the block: lane groups lg = 0..3 added in a fixed order
