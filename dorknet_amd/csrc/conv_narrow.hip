@@ -160,13 +160,22 @@ __global__ __launch_bounds__(NT, 2) void fwd_kernel(const float* __restrict__ x,
     f32x4 acc[T];
 #pragma unroll
     for (int t = 0; t < T; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // A values one k-step ahead: k-step kk + 1's LDS reads are issued before k-step kk's T MFMAs
+    // (the scheduler otherwise waited out an LDS round trip every two MFMAs); the groups pin the
+    // order, the k order of every accumulator is unchanged.
+    float a[2][T];
+#pragma unroll
+    for (int t = 0; t < T; ++t) a[0][t] = xl[off[0] + 16 * ST * t];
 #pragma unroll
     for (int kk = 0; kk < KK; ++kk) {
-      float a[T];
+      if (kk + 1 < KK) {
 #pragma unroll
-      for (int t = 0; t < T; ++t) a[t] = xl[off[kk] + 16 * ST * t];
+        for (int t = 0; t < T; ++t) a[(kk + 1) & 1][t] = xl[off[kk + 1] + 16 * ST * t];
+      }
 #pragma unroll
-      for (int t = 0; t < T; ++t) acc[t] = mfma16(a[t], b[kk], acc[t]);
+      for (int t = 0; t < T; ++t) acc[t] = mfma16(a[kk & 1][t], b[kk], acc[t]);
+      if (kk + 1 < KK) __builtin_amdgcn_sched_group_barrier(0x100, T, 0);  // the next k-step's reads
+      __builtin_amdgcn_sched_group_barrier(0x008, T, 0);                  // this k-step's MFMAs
     }
     // C/D: row (output pixel) 16t + 4lg + v, column = filter col.  Branch-free: buffer stores on the
     // row's bytes (a filter past K reads kOOBBytes, a pixel past OW lands past the row's range: both
