@@ -113,8 +113,9 @@ def test_pointwise_bwd_fused_rejects_other_shapes():
 
 
 def test_bf16_pointwise_bwd_fused_shapes():
-    # bf16: K = C = 64 (streaming form) and K in {128, 256} with C a multiple of 128 (deep form)
-    for K, C in [(64, 64), (128, 128), (256, 128), (256, 256), (128, 512)]:
+    # bf16: K = C = 64 (streaming form) and K in {128, 256} with C a multiple of 128 or K = 128 with
+    # C = 64 (deep form, one column group)
+    for K, C in [(64, 64), (128, 128), (256, 128), (256, 256), (128, 512), (128, 64)]:
         assert lib.dk_pwconv_bwd_fused_bf16_rows(2, 7, 7, K, C) > 0, (K, C)
-    for K, C in [(512, 512), (128, 64), (64, 128), (256, 192)]:
+    for K, C in [(512, 512), (256, 64), (64, 128), (256, 192)]:
         assert lib.dk_pwconv_bwd_fused_bf16_rows(2, 7, 7, K, C) == 0, (K, C)
