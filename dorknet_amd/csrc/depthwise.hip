@@ -139,9 +139,12 @@ struct DwTile {
 // 14 rows per thread measured config 5 5.93 -> 5.84 ms, config 3 8.146 -> 8.132 ms
 // (profiles/r05ai_ab_dw_fwd_rows_per_thread.txt; whole columns were faster still for bf16, slower
 // for fp32).
-static inline int dw_fwd_seg(int OH) {
+// bf16 (whole): a thread slides down its whole output column -- config 5 5.776 -> 5.731 ms, while
+// fp32 measured slower that way (config 3 7.764 -> 7.786 ms; profiles/r06av_ab_dw_fwd_rows_bf16.txt).
+static inline int dw_fwd_seg(int OH, bool whole) {
   const int seg = knob(kKnobDwSeg);  // tuning knob (kind 8): rows per thread; -1 = this rule
   if (seg > 0) return seg;
+  if (whole) return OH;
   const int nseg = (OH + 13) / 14;
   return (OH + nseg - 1) / nseg;
 }
@@ -1679,9 +1682,9 @@ static inline bool bn_ok(const BnIn& bn) {
 }
 
 template <int ST>
-static long long dw_fwd_threads(int N, int OH, int OW, int C) {
+static long long dw_fwd_threads(int N, int OH, int OW, int C, bool whole) {
   constexpr int TW = DwTile<ST>::TW;
-  const int SEG = dw_fwd_seg(OH);
+  const int SEG = dw_fwd_seg(OH, whole);
   return (long long)N * ((OH + SEG - 1) / SEG) * ((OW + TW - 1) / TW) * (C / 4);
 }
 
@@ -1692,7 +1695,8 @@ static int launch_dw_fwd(const T* x, const float* wt, const float* bias, T* y, i
                          int OW, int pad, const BnIn& bn, double* part, const T* xo, const BnIn& obn, int wl,
                          const T* res, hipStream_t st, const JoinFwd* jn = nullptr) {
   const uint32_t xb = (uint32_t)((size_t)N * H * W * C * sizeof(T));
-  const dim3 grid((unsigned)cdivll(dw_fwd_threads<ST>(N, OH, OW, C), 256));
+  constexpr bool whole = sizeof(T) == 2;
+  const dim3 grid((unsigned)cdivll(dw_fwd_threads<ST>(N, OH, OW, C, whole), 256));
   FoldTail ft;  // an armed in-launch fold of the partial rows (fold_tail.h)
   if (!part || !fold_take(part, (int)grid.x, C, 1, &ft)) ft.part = nullptr;
   const JoinFwd jf = jn ? *jn : JoinFwd{};
@@ -1703,18 +1707,18 @@ static int launch_dw_fwd(const T* x, const float* wt, const float* bias, T* y, i
       if (part)
         hipLaunchKernelGGL((dw_fwd_kernel<R, S, ST, false, false, 1, 1, T, true>), grid, dim3(256), 0, st, x, xb, wt,
                            bias, y, N, H, W, C, OH, OW, pad, bn, part, xo, obn, res, ft, nt_stores(kNtDwFwd),
-                           dw_fwd_seg(OH), jf);
+                           dw_fwd_seg(OH, whole), jf);
       else
         hipLaunchKernelGGL((dw_fwd_kernel<R, S, ST, false, false, 0, 1, T, true>), grid, dim3(256), 0, st, x, xb, wt,
                            bias, y, N, H, W, C, OH, OW, pad, bn, part, xo, obn, res, ft, nt_stores(kNtDwFwd),
-                           dw_fwd_seg(OH), jf);
+                           dw_fwd_seg(OH, whole), jf);
       return fold_status(launch_status(), ft);
     }
   }
   if (jn) return DK_ERR_ARGS;
 #define DW_LAUNCH1(B, RL, ST_, WL_)                                                                                  \
   hipLaunchKernelGGL((dw_fwd_kernel<R, S, ST, B, RL, ST_, WL_, T>), grid, dim3(256), 0, st, x, xb, wt, bias, y, N, H, \
-                     W, C, OH, OW, pad, bn, part, xo, obn, res, ft, nt_stores(kNtDwFwd), dw_fwd_seg(OH), jf)
+                     W, C, OH, OW, pad, bn, part, xo, obn, res, ft, nt_stores(kNtDwFwd), dw_fwd_seg(OH, whole), jf)
 #define DW_LAUNCH(B, ST_, WL_)            \
   do {                                    \
     if (B && bn.relu)                     \
@@ -1800,10 +1804,18 @@ DK_API int dk_dwconv_fwd_bnx_f32(const float* x, int N, int H, int W, int C, con
 
 // Rows of BatchNorm partial statistics dk_dwconv_fwd_ex_f32 writes; 0 = statistics not
 // supported for this channel count (C/4 must divide 256).
-DK_API int dk_dwconv_fwd_stats_rows(int N, int OH, int OW, int C, int stride) {
+static int dw_fwd_stats_rows(int N, int OH, int OW, int C, int stride, bool whole) {
   if (C % 4 || C / 4 > 256 || 256 % (C / 4)) return 0;
-  const long long thr = stride == 1 ? dw_fwd_threads<1>(N, OH, OW, C) : dw_fwd_threads<2>(N, OH, OW, C);
+  const long long thr =
+      stride == 1 ? dw_fwd_threads<1>(N, OH, OW, C, whole) : dw_fwd_threads<2>(N, OH, OW, C, whole);
   return (int)cdivll(thr, 256);
+}
+DK_API int dk_dwconv_fwd_stats_rows(int N, int OH, int OW, int C, int stride) {
+  return dw_fwd_stats_rows(N, OH, OW, C, stride, false);
+}
+// The bf16 forward's rows (dk_dwconv_fwd_ex_bf16: whole output columns per thread, fewer blocks).
+DK_API int dk_dwconv_fwd_bf16_stats_rows(int N, int OH, int OW, int C, int stride) {
+  return dw_fwd_stats_rows(N, OH, OW, C, stride, true);
 }
 
 // Reads the filters in the reference layout W[C][R][S] (no re-layout copy).

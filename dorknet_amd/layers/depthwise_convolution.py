@@ -97,7 +97,7 @@ class DepthwiseConvLayer(Layer):
         bias = self.learned_params["bias"] if self.with_bias else None
         stats = None
         if bn_stats is not None and not test_mode and self.stride in (1, 2):
-            rows = lib.dk_dwconv_fwd_stats_rows(N, OH, OW, C, self.stride)
+            rows = (lib.dk_dwconv_fwd_bf16_stats_rows if bf else lib.dk_dwconv_fwd_stats_rows)(N, OH, OW, C, self.stride)
             if rows:
                 stats = torch.empty((rows, 2, C), dtype=torch.float64, device=x.device)
         w = self.learned_params["weights"]  # W[C][R][S], read in place by the _ex entry

@@ -173,6 +173,8 @@ int dk_conv2d_fwd_ex_f32(const float* x, int N, int H, int W, int C, const float
 int dk_pwconv_fwd_stats_rows(int N, int OH, int OW, int K, int C);
 int dk_pwconv_fwd_ex_f32(const float* x, int N, int H, int W, int C, const float* w_kc, int K, int stride, const float* bias, float* y, int OH, int OW, const float* bn_mean, const float* bn_invstd, const float* bn_gamma, const float* bn_beta, int bn_relu, double* stats, void* stream);
 int dk_dwconv_fwd_stats_rows(int N, int OH, int OW, int C, int stride);
+/* The same for dk_dwconv_fwd_ex_bf16 (whole output columns per thread: fewer blocks, fewer rows). */
+int dk_dwconv_fwd_bf16_stats_rows(int N, int OH, int OW, int C, int stride);
 int dk_dwconv_fwd_ex_f32(const float* x, int N, int H, int W, int C, const float* w_crs, int R, int S, int stride, int pad, const float* bias, float* y, int OH, int OW, const float* bn_mean, const float* bn_invstd, const float* bn_gamma, const float* bn_beta, int bn_relu, double* stats, void* stream);
 /* Depthwise forward whose input is a residual block's output y = ReLU(bnA(a) + bnB(b))
  * (residual_block.py:75; the operands of dk_bn_add_f32, bnX = identity when its mean is NULL): the

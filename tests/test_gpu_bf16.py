@@ -76,6 +76,32 @@ def test_depthwise_and_pointwise_bf16_match_fp32_twins(stride):
         assert float((ph != ref).float().mean()) < 0.02
 
 
+@pytest.mark.parametrize("stride", [1, 2])
+def test_depthwise_bf16_statistics_rows(stride):
+    """The bf16 depthwise forward runs whole output columns per thread (fewer blocks than the fp32
+    forward at OH > 14): dk_dwconv_fwd_bf16_stats_rows gives exactly the rows it writes (a row past
+    them stays untouched), and the rows sum to the fp64 statistics of the stored bf16 outputs."""
+    rng = np.random.RandomState(11 + stride)
+    N, C, H, W = 2, 32, 60, 60
+    st = stream_handle()
+    xh = nhwc(torch.as_tensor(rng.randn(N, C, H, W).astype(np.float32), device="cuda").to(BF16))
+    w = torch.as_tensor(rng.randn(C, 3, 3).astype(np.float32), device="cuda")
+    OH, OW = (H + 2 - 3) // stride + 1, (W + 2 - 3) // stride + 1
+    rows = lib.dk_dwconv_fwd_bf16_stats_rows(N, OH, OW, C, stride)
+    assert 0 < rows < lib.dk_dwconv_fwd_stats_rows(N, OH, OW, C, stride)
+    part = torch.full((rows + 1, 2, C), float("nan"), dtype=torch.float64, device="cuda")
+    yh = nhwc(torch.empty((N, C, OH, OW), device="cuda", dtype=BF16))
+    assert lib.dk_dwconv_fwd_ex_bf16(xh.data_ptr(), N, H, W, C, w.data_ptr(), 3, 3, stride, 1, 0, yh.data_ptr(),
+                                     OH, OW, 0, 0, 0, 0, 0, part.data_ptr(), st) == 0
+    torch.cuda.synchronize()
+    assert bool(torch.isnan(part[rows]).all())
+    s = part[:rows].sum(0)
+    y = yh.double()
+    ref = torch.stack([y.sum((0, 2, 3)), (y * y).sum((0, 2, 3))])
+    # (a thread's row of outputs is summed in fp32, the rows in fp64: the fp32 forward's rule)
+    assert float((s - ref).norm() / ref.norm()) < 1e-6
+
+
 def _stack(blocks=None, seed=0):
     from examples.mobilenet_stack import BLOCKS, MobileNetStack
     np.random.seed(seed)
