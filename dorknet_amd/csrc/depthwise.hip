@@ -124,6 +124,13 @@ __device__ __forceinline__ void load_row(f32x4 (&row)[NC], __amdgpu_buffer_rsrc_
 // Outputs per thread along W: the input strip R x ((TW-1)*ST + S) float4s is loaded at once.
 // Stride 2 takes two: its window (R x 5 float4s, two rows of it new each output row) then leaves
 // the join-forming variant two waves per SIMD (with four outputs, R x 9, it ran at one).
+// Nontemporal-store family of a strided depthwise dgrad: bf16 has its own (12, on: config 5 5.747 ->
+// 5.718 ms, profiles/r06ay_ab_nt_stem.txt), fp32 keeps family 10 (off: neutral or slower).
+template <class T>
+constexpr int dgrad_nt_fam() {
+  return sizeof(T) == 2 ? kNtDwDgrad16 : kNtDwDgrad;
+}
+
 template <int ST>
 struct DwTile {
   static constexpr int TW = ST == 2 ? 2 : 4;    // outputs per thread along W
@@ -1887,11 +1894,11 @@ static int dw_dgrad(const T* dy, int N, int OH, int OW, int C, const float* w_cr
       FoldTail ft;                                                                                                   \
       if (!fold_take(part, (int)grid.x, C, 1, &ft)) ft.part = nullptr;                                              \
       hipLaunchKernelGGL((dw_dgrad_subpixel_kernel<RR, SS, STR, PD, T, true>), grid, dim3(256), 0, st, dy, gb,      \
-                         w_crs, dx, N, H, W, C, OH, OW, res, *jn, part, ft, nt_stores(kNtDwDgrad));                  \
+                         w_crs, dx, N, H, W, C, OH, OW, res, *jn, part, ft, nt_stores(dgrad_nt_fam<T>()));                  \
       return fold_status(launch_status(), ft);                                                                       \
     }                                                                                                                \
     hipLaunchKernelGGL((dw_dgrad_subpixel_kernel<RR, SS, STR, PD, T>), grid, dim3(256), 0, st, dy, gb, w_crs, dx, N, \
-                       H, W, C, OH, OW, res, JoinBwd{}, nullptr, FoldTail{}, nt_stores(kNtDwDgrad));                 \
+                       H, W, C, OH, OW, res, JoinBwd{}, nullptr, FoldTail{}, nt_stores(dgrad_nt_fam<T>()));                 \
     return launch_status();                                                                                          \
   }
   DW_SUBPIX(3, 3, 2, 1)
@@ -2199,11 +2206,11 @@ static int dw_bwd_s2(const T* g, const T* bn_x, int N, int H, int W, int C, int 
     if (residual)                                                                                                   \
       hipLaunchKernelGGL((dw_bwd_s2_kernel<BNX_, STATS_, RELU1_, T>), dim3(blocks), dim3(256), shm, st, g, bn_x,   \
                          (uint32_t)yb, ob, x, (uint32_t)xb, bn, w_crs, dx, residual, part, wpart, N, H, W, C, OH, OW, \
-                         ft, nt_stores(kNtDwDgrad));                                                                \
+                         ft, nt_stores(dgrad_nt_fam<T>()));                                                                \
     else                                                                                                            \
       hipLaunchKernelGGL((dw_bwd_s2_kernel<BNX_, STATS_, RELU1_, T, false, false>), dim3(blocks), dim3(256), shm,  \
                          st, g, bn_x, (uint32_t)yb, ob, x, (uint32_t)xb, bn, w_crs, dx, residual, part, wpart, N, H, \
-                         W, C, OH, OW, ft, nt_stores(kNtDwDgrad));                                                  \
+                         W, C, OH, OW, ft, nt_stores(dgrad_nt_fam<T>()));                                                  \
   } while (0)
   if (out_relu) {
     if (part) DWS2_LAUNCH(true, true, true); else if (bn_mean) DWS2_LAUNCH(true, false, true);

@@ -248,8 +248,8 @@ enum : int { DK_ERR_ARGS = 10001, DK_ERR_WORKSPACE = 10002 };
 enum : int { DK_FOLDED = 10100 };
 // Nontemporal output stores per kernel family (tuning knob dk_debug_set_gemm_config(4, mask)): bit kNt*
 // set = that family's main output stores are nontemporal.
-enum NtFam : int { kNtDwFwd = 0, kNtDwBwd = 1, kNtBnAdd = 2, kNtPwsBwd = 3, kNtPwsFwd = 4, kNtPwsDgrad = 5, kNtGemm = 6, kNtStem = 7, kNtPwd = 8, kNtPwd16 = 9, kNtDwDgrad = 10, kNtBnBwd = 11 };
-constexpr int kNtDefault = 2431;  // families 0-6: config 3 8.868 -> 8.819 ms, config 5 7.596 -> 7.566 (profiles/r03q_ntfam_config*.txt); 8 (fp32 deep pointwise): config 3 8.697 -> 8.650 ms, 3 of 3 (profiles/r04nt_ab.txt); 11 (BN backward apply): config 3 8.719 -> 8.700 ms (profiles/r04nt2_ab.txt); off: 9 (bf16 deep pointwise, neutral), 10 (strided depthwise dgrad, fp32 neutral or slower)
+enum NtFam : int { kNtDwFwd = 0, kNtDwBwd = 1, kNtBnAdd = 2, kNtPwsBwd = 3, kNtPwsFwd = 4, kNtPwsDgrad = 5, kNtGemm = 6, kNtStem = 7, kNtPwd = 8, kNtPwd16 = 9, kNtDwDgrad = 10, kNtBnBwd = 11, kNtDwDgrad16 = 12 };
+constexpr int kNtDefault = 6655;  // families 0-6: config 3 8.868 -> 8.819 ms, config 5 7.596 -> 7.566 (profiles/r03q_ntfam_config*.txt); 7 (the stem's output): config 3 7.861 -> 7.835 ms, 5 of 6 rounds (profiles/r06ay_ab_nt_stem.txt); 8 (fp32 deep pointwise): config 3 8.697 -> 8.650 ms, 3 of 3 (profiles/r04nt_ab.txt); 11 (BN backward apply): config 3 8.719 -> 8.700 ms (profiles/r04nt2_ab.txt); 12 (bf16 strided depthwise dgrad): config 5 5.747 -> 5.718 ms, 4 of 5 rounds (profiles/r06ay_ab_nt_stem.txt); off: 9 (bf16 deep pointwise, neutral), 10 (fp32 strided depthwise dgrad, neutral or slower)
 int nt_stores(int fam);
 
 // Path selectors and tuning knobs for tests and A/B runs (knobs.hip): one registry of atomics holding
